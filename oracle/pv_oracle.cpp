@@ -1,0 +1,1307 @@
+// SPDX-License-Identifier: MPL-2.0
+//
+// oracle/pv_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// A single-threaded CPU restatement of pktvisor's per-packet hot path, written
+// from the reference source as a specification (not copied):
+//   * pcap record loop ............ src/inputs/pcap/PcapInputStream.cpp:471-527
+//   * L2/L3/L4 classify + dir ..... src/inputs/pcap/PcapInputStream.cpp:380-428,
+//                                   libs/visor_utils/utils.cpp:26-69,105-164
+//   * hash5Tuple flowkey .......... PcapPlusPlus 23.09 PacketUtils (not vendored;
+//                                   restated, parity unpinned)
+//   * Net v1 bucket ............... src/handlers/net/v1/NetStreamHandler.cpp:161-169,
+//                                   516-548,682-764
+//   * DNS wire decoder ............ libs/visor_dns/DnsLayer.cpp:119-209,
+//                                   libs/visor_dns/DnsResource.cpp:19-32,53-148
+//   * DNS v1 bucket + xacts ....... src/handlers/dns/v1/DnsStreamHandler.cpp:270-302,
+//                                   910-1049,1093-1138,1350-1370,
+//                                   libs/visor_transaction/TransactionManager.h:24-117
+//   * aggregateDomain ............. libs/visor_dns/dns.cpp:9-43
+//   * window / period shift ....... src/AbstractMetricsManager.h:177-206,276-333,423-437,601-647
+//   * sketches: CPC (HIP/ICON), exact top-N counts, exact quantiles with the
+//     KLL rank rule — 3rd/datasketches/cpc/include/cpc_sketch_impl.hpp:75-385,
+//     icon_estimator.hpp:225-270, common/include/quantiles_sorted_view_impl.hpp:76-84.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+// this code, and only as the checker / CPU baseline. The product path
+// (pktvisor_amd, libpvgpu.so) never links or calls it.
+//
+// Parity status: pinned against the reference's own known-answer tests on the
+// UDP fixtures (tests/golden/, see tests/test_oracle_kat.py) and, for the sketch
+// estimators, against the vendored datasketches library compiled by
+// oracle/Makefile into oracle/_ref/ (tests/test_ref_sketch.py).
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+#include <arpa/inet.h>
+
+namespace pvo {
+
+// ---------------------------------------------------------------- utilities
+static inline uint16_t rd16be(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+static inline uint32_t rd32le(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+
+struct TS {
+    int64_t sec = 0;
+    int64_t nsec = 0;
+};
+
+// ---------------------------------------------------------------- MurmurHash3_x64_128
+// Standard public-domain algorithm; datasketches uses it with seed 9001
+// (3rd/datasketches/common/include/common_defs.hpp:34).
+static inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t fmix64(uint64_t k)
+{
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+static void murmur3_128(const uint8_t *data, size_t len, uint64_t seed, uint64_t &o1, uint64_t &o2)
+{
+    const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    uint64_t h1 = seed, h2 = seed;
+    size_t nb = len / 16;
+    for (size_t i = 0; i < nb; i++) {
+        uint64_t k1, k2;
+        memcpy(&k1, data + 16 * i, 8);
+        memcpy(&k2, data + 16 * i + 8, 8);
+        k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+        h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+        k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+        h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+    }
+    const uint8_t *t = data + nb * 16;
+    uint64_t k1 = 0, k2 = 0;
+    size_t r = len & 15;
+    for (size_t i = r; i > 8; i--) k2 ^= (uint64_t)t[i - 1] << (8 * (i - 9));
+    if (r > 8) { k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2; }
+    for (size_t i = std::min<size_t>(r, 8); i > 0; i--) k1 ^= (uint64_t)t[i - 1] << (8 * (i - 1));
+    if (r > 0) { k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1; }
+    h1 ^= len; h2 ^= len;
+    h1 += h2; h2 += h1;
+    h1 = fmix64(h1); h2 = fmix64(h2);
+    h1 += h2; h2 += h1;
+    o1 = h1; o2 = h2;
+}
+
+// ---------------------------------------------------------------- CPC (lg_k = 11)
+// Restatement of the coupon/HIP/ICON logic of cpc_sketch_impl.hpp. The sketch
+// state is the set of coupons; HIP depends on the order in which coupons first
+// appear plus the periodic kxp refresh at window offsets that are multiples of 8.
+static const int CPC_LGK = 11;
+static const uint32_t CPC_K = 1u << CPC_LGK;
+
+// icon_estimator.hpp:98-102 (log K = 11 row) — the published polynomial.
+static const double ICON_COEF_LGK11[20] = {
+    0.9999186020796150265, 0.3333249054574359826, 0.126791713589799987, -0.06662487271699729652,
+    -0.07335552427910230211, 0.3316370184815959909, -1.434143797561290068, 4.180260309967409604,
+    -8.593906870708760692, 12.95088874800289958, -14.56876092520539956, 12.37074367531410068,
+    -7.969152075707960137, 3.888774396648960074, -1.424923326506990051, 0.385084561785229984,
+    -0.07435541911616409816, 0.009695363567476529554, -0.0007644375960047160388, 2.75156194717188011e-05};
+
+double icon_estimate(uint32_t c)
+{
+    if (c < 2) return c == 0 ? 0.0 : 1.0;
+    const double k = (double)CPC_K, dc = (double)c;
+    if (dc > 5.7 * k) return 0.7940236163830469 * k * pow(2.0, dc / k);
+    const double x = dc / (2.0 * k);
+    double total = ICON_COEF_LGK11[19];
+    for (int j = 18; j >= 0; j--) { total *= x; total += ICON_COEF_LGK11[j]; }
+    const double ratio = dc / k;
+    const double term = 1.0 + (ratio * ratio * ratio / 66.774757);
+    const double result = dc * total * term;
+    return result >= dc ? result : dc;
+}
+
+static double kxp_byte(uint8_t b)
+{
+    double s = 0;
+    for (int col = 0; col < 8; col++)
+        if (((b >> col) & 1) == 0) s += ldexp(1.0, -(col + 1));
+    return s;
+}
+
+struct Cpc {
+    std::vector<uint64_t> rows = std::vector<uint64_t>(CPC_K, 0);
+    uint32_t num_coupons = 0;
+    double kxp = (double)CPC_K;
+    double hip = 0;
+    int window_offset = 0;
+    bool windowed = false;
+    bool merged = false;
+
+    void refresh_kxp()
+    {
+        double byte_sums[8] = {0};
+        for (uint32_t i = 0; i < CPC_K; i++) {
+            uint64_t w = rows[i];
+            for (int j = 0; j < 8; j++) { byte_sums[j] += kxp_byte(w & 0xff); w >>= 8; }
+        }
+        double total = 0;
+        for (int j = 7; j >= 0; j--) total += ldexp(1.0, -8 * j) * byte_sums[j];
+        kxp = total;
+    }
+    void coupon(uint32_t row, uint32_t col)
+    {
+        if ((rows[row] >> col) & 1) return;
+        rows[row] |= 1ULL << col;
+        num_coupons++;
+        hip += (double)CPC_K / kxp;
+        kxp -= ldexp(1.0, -(int)(col + 1));
+        if (!windowed) {
+            if (((uint64_t)num_coupons << 5) >= 3ULL * CPC_K) windowed = true;
+        } else {
+            if (((uint64_t)num_coupons << 3) >= (27ULL + ((uint64_t)window_offset << 3)) * CPC_K) {
+                window_offset++;
+                if ((window_offset & 7) == 0) refresh_kxp();
+            }
+        }
+    }
+    void update_bytes(const void *p, size_t n)
+    {
+        uint64_t h1, h2;
+        murmur3_128((const uint8_t *)p, n, 9001, h1, h2);
+        uint32_t col = h2 ? (uint32_t)__builtin_clzll(h2) : 64;
+        if (col > 63) col = 63;
+        coupon((uint32_t)(h1 & (CPC_K - 1)), col);
+    }
+    // cpc_sketch_impl.hpp:124-132: uint32 -> int32 -> int64 (sign extension), 8 bytes
+    void update_u32(uint32_t v)
+    {
+        int64_t x = (int64_t)(int32_t)v;
+        update_bytes(&x, 8);
+    }
+    void update_str(const std::string &s)
+    {
+        if (s.empty()) return; // cpc_sketch_impl.hpp:109-112
+        update_bytes(s.data(), s.size());
+    }
+    void merge(const Cpc &o)
+    {
+        for (uint32_t i = 0; i < CPC_K; i++) rows[i] |= o.rows[i];
+        num_coupons = 0;
+        for (uint32_t i = 0; i < CPC_K; i++) num_coupons += __builtin_popcountll(rows[i]);
+        merged = true;
+    }
+    double estimate() const { return merged ? icon_estimate(num_coupons) : hip; }
+};
+
+// ---------------------------------------------------------------- exact quantiles
+// Same rank rule as the KLL sorted view in exact mode
+// (quantiles_sorted_view_impl.hpp:76-84, inclusive=true): item at ceil(rank*n)-1.
+template <typename T>
+struct ExactQuantile {
+    std::vector<T> v;
+    void update(T x) { v.push_back(x); }
+    void merge(const ExactQuantile &o) { v.insert(v.end(), o.v.begin(), o.v.end()); }
+    bool empty() const { return v.empty(); }
+    std::vector<T> quantiles() const
+    {
+        std::vector<T> s = v;
+        std::sort(s.begin(), s.end());
+        std::vector<T> out;
+        const double ranks[4] = {0.50, 0.90, 0.95, 0.99};
+        for (double r : ranks) {
+            uint64_t w = (uint64_t)std::ceil(r * (double)s.size());
+            size_t idx = w == 0 ? 0 : (size_t)(w - 1);
+            if (idx >= s.size()) idx = s.size() - 1;
+            out.push_back(s[idx]);
+        }
+        return out;
+    }
+    T p(double r) const
+    {
+        std::vector<T> s = v;
+        std::sort(s.begin(), s.end());
+        uint64_t w = (uint64_t)std::ceil(r * (double)s.size());
+        size_t idx = w == 0 ? 0 : (size_t)(w - 1);
+        if (idx >= s.size()) idx = s.size() - 1;
+        return s[idx];
+    }
+};
+
+// ---------------------------------------------------------------- exact top-N
+template <typename K>
+struct ExactTop {
+    std::map<K, uint64_t> m;
+    void update(const K &k, uint64_t w = 1) { m[k] += w; }
+    void merge(const ExactTop &o)
+    {
+        for (auto &kv : o.m) m[kv.first] += kv.second;
+    }
+};
+
+// ---------------------------------------------------------------- JSON writer
+struct J {
+    std::string s;
+    std::vector<bool> first{true};
+    void comma()
+    {
+        if (!first.back()) s += ',';
+        first.back() = false;
+    }
+    void key(const std::string &k)
+    {
+        comma();
+        str_(k);
+        s += ':';
+        first.back() = true; // value follows immediately
+        pending_value = true;
+    }
+    bool pending_value = false;
+    void pre_value()
+    {
+        if (pending_value) { pending_value = false; first.back() = false; return; }
+        comma();
+    }
+    void str_(const std::string &v)
+    {
+        s += '"';
+        for (unsigned char c : v) {
+            if (c == '"') s += "\\\"";
+            else if (c == '\\') s += "\\\\";
+            else if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); s += b; }
+            else s += (char)c;
+        }
+        s += '"';
+    }
+    void str(const std::string &v) { pre_value(); str_(v); }
+    void u64(uint64_t v) { pre_value(); s += std::to_string(v); }
+    void i64(int64_t v) { pre_value(); s += std::to_string(v); }
+    void dbl(double v)
+    {
+        pre_value();
+        char b[40];
+        snprintf(b, sizeof b, "%.17g", v);
+        s += b;
+        if (!strpbrk(b, ".eEn")) s += ".0";
+    }
+    void obj() { pre_value(); s += '{'; first.push_back(true); }
+    void end_obj() { s += '}'; first.pop_back(); }
+    void arr() { pre_value(); s += '['; first.push_back(true); }
+    void end_arr() { s += ']'; first.pop_back(); }
+};
+
+// ---------------------------------------------------------------- name tables
+// libs/visor_dns/dns.h:31-265 (QTypeNames / RCodeNames); restated for the
+// codes the decoder can emit names for.
+static const std::map<uint16_t, std::string> &qtype_names()
+{
+    static const std::map<uint16_t, std::string> m = {
+        {0, "Reserved (0)"}, {1, "A"}, {2, "NS"}, {3, "MD"}, {4, "MF"}, {5, "CNAME"}, {6, "SOA"}, {7, "MB"}, {8, "MG"}, {9, "MR"},
+        {10, "NULL"}, {11, "WKS"}, {12, "PTR"}, {13, "HINFO"}, {14, "MINFO"}, {15, "MX"}, {16, "TXT"},
+        {17, "RP"}, {18, "AFSDB"}, {19, "X25"}, {20, "ISDN"}, {21, "RT"}, {22, "NSAP"}, {23, "NSAP-PTR"},
+        {24, "SIG"}, {25, "KEY"}, {26, "PX"}, {27, "GPOS"}, {28, "AAAA"}, {29, "LOC"}, {30, "NXT"},
+        {31, "EID"}, {32, "NIMLOC"}, {33, "SRV"}, {34, "ATMA"}, {35, "NAPTR"}, {36, "KX"}, {37, "CERT"},
+        {38, "A6"}, {39, "DNAME"}, {40, "SINK"}, {41, "OPT"}, {42, "APL"}, {43, "DS"}, {44, "SSHFP"},
+        {45, "IPSECKEY"}, {46, "RRSIG"}, {47, "NSEC"}, {48, "DNSKEY"}, {49, "DHCID"}, {50, "NSEC3"},
+        {51, "NSEC3PARAM"}, {52, "TLSA"}, {53, "SMIMEA"}, {55, "HIP"}, {56, "NINFO"}, {57, "RKEY"},
+        {58, "TALINK"}, {59, "CDS"}, {60, "CDNSKEY"}, {61, "OPENPGPKEY"}, {62, "CSYNC"}, {63, "ZONEMD"},
+        {64, "SVCB"}, {65, "HTTPS"}, {99, "SPF"}, {100, "UINFO"}, {101, "UID"}, {102, "GID"}, {103, "UNSPEC"},
+        {104, "NID"}, {105, "L32"}, {106, "L64"}, {107, "LP"}, {108, "EUI48"}, {109, "EUI64"},
+        {249, "TKEY"}, {250, "TSIG"}, {251, "IXFR"}, {252, "AXFR"}, {253, "MAILB"}, {254, "MAILA"},
+        {255, "*"}, {256, "URI"}, {257, "CAA"}, {258, "AVC"}, {259, "DOA"}, {260, "AMTRELAY"},
+        {32768, "TA"}, {32769, "DLV"}, {65535, "Reserved (65535)"}};
+    return m;
+}
+static const std::map<uint16_t, std::string> &rcode_names()
+{
+    static const std::map<uint16_t, std::string> m = {
+        {0, "NOERROR"}, {1, "FORMERR"}, {2, "SRVFAIL"}, {3, "NXDOMAIN"}, {4, "NOTIMP"}, {5, "REFUSED"},
+        {6, "YXDOMAIN"}, {7, "YXRRSET"}, {8, "NXRRSET"}, {9, "NOTAUTH"}, {10, "NOTZONE"}, {11, "DSOTYPENI"},
+        {16, "BADVERS"}, {17, "BADKEY"}, {18, "BADTIME"}, {19, "BADMODE"}, {20, "BADNAME"}, {21, "BADALG"},
+        {22, "BADTRUNC"}, {23, "BADCOOKIE"}};
+    return m;
+}
+
+// ---------------------------------------------------------------- config
+struct V4Net { uint32_t addr; uint8_t cidr; };  // addr: network-order bytes as LE u32 (in_addr.s_addr)
+struct V6Net { uint8_t addr[16]; uint8_t cidr; };
+
+struct Config {
+    std::vector<V4Net> v4;
+    std::vector<V6Net> v6;
+    unsigned num_periods = 5;
+    unsigned window = 5; // output window: 1 => single bucket 0 ("1m"), N>=2 => merged N ("Nm")
+    size_t topn_count = 10;
+    uint32_t xact_ttl_ms = 5000;
+    bool dns_details = false; // enable top_qnames_details group
+    bool recorded_stream = true;
+};
+
+// libs/visor_utils/utils.cpp:128-164
+static bool parse_host_specs(const std::string &spec, Config &c, std::string &err)
+{
+    size_t pos = 0;
+    while (pos <= spec.size() && !spec.empty()) {
+        size_t e = spec.find(',', pos);
+        std::string host = spec.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
+        pos = e == std::string::npos ? spec.size() + 1 : e + 1;
+        if (host.empty()) continue;
+        size_t d = host.find('/');
+        if (d == std::string::npos) { err = "invalid CIDR: " + host; return false; }
+        std::string ip = host.substr(0, d), cs = host.substr(d + 1);
+        if (cs.empty() || !std::all_of(cs.begin(), cs.end(), ::isdigit)) { err = "invalid CIDR: " + host; return false; }
+        int cidr = atoi(cs.c_str());
+        if (ip.find(':') != std::string::npos) {
+            if (cidr < 0 || cidr > 128) { err = "invalid CIDR: " + host; return false; }
+            V6Net n;
+            if (inet_pton(AF_INET6, ip.c_str(), n.addr) != 1) { err = "invalid IPv6 address: " + ip; return false; }
+            n.cidr = (uint8_t)cidr;
+            c.v6.push_back(n);
+        } else {
+            if (cidr < 0 || cidr > 32) { err = "invalid CIDR: " + host; return false; }
+            in_addr a;
+            if (inet_pton(AF_INET, ip.c_str(), &a) != 1) { err = "invalid IPv4 address: " + ip; return false; }
+            c.v4.push_back({a.s_addr, (uint8_t)cidr});
+        }
+    }
+    return true;
+}
+
+// utils.cpp:26-43 — value 0 never matches; cidr 0 matches everything.
+static bool match_v4(const Config &c, uint32_t ip)
+{
+    if (!ip) return false;
+    for (auto &n : c.v4) {
+        if (n.cidr == 0) return true;
+        uint32_t mask = htonl(0xFFFFFFFFu << (32 - n.cidr));
+        if (((ip ^ n.addr) & mask) == 0) return true;
+    }
+    return false;
+}
+// utils.cpp:45-69 — byte compare then bit compare; prefix 0 never matches.
+static bool match_v6(const Config &c, const uint8_t *ip)
+{
+    for (auto &n : c.v6) {
+        uint8_t bytes = n.cidr / 8, bits = n.cidr % 8;
+        bool r = false;
+        if (bytes > 0) r = memcmp(n.addr, ip, bytes) == 0;
+        if ((r || n.cidr < 8) && bits > 0) r = (n.addr[bytes] >> (8 - bits)) == (ip[bytes] >> (8 - bits));
+        if (r) return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------- packet parse
+// PcapPlusPlus 23.09 `Packet(raw, TCP|UDP)` semantics restated.
+enum { L3_UNKNOWN = 0, L3_IPV4 = 4, L3_IPV6 = 6 };
+enum { L4_UNKNOWN = 0, L4_TCP = 6, L4_UDP = 17 };
+enum Dir { DIR_TO_HOST = 0, DIR_FROM_HOST = 1, DIR_UNKNOWN = 2 };
+
+struct Pkt {
+    const uint8_t *data = nullptr;
+    uint32_t caplen = 0;
+    TS ts;
+    int l3 = L3_UNKNOWN, l4 = L4_UNKNOWN;
+    bool has_v4 = false, has_v6 = false;
+    const uint8_t *v4hdr = nullptr; // first IPv4 layer header
+    const uint8_t *v6hdr = nullptr; // first IPv6 layer header
+    const uint8_t *l4hdr = nullptr;
+    uint32_t l4len = 0; // L4 layer data length (incl. L4 header), IP-length trimmed
+    bool syn = false;
+    Dir dir = DIR_UNKNOWN;
+};
+
+static void parse_ip(Pkt &p, const uint8_t *d, size_t len, int depth);
+
+static bool ipv4_valid(const uint8_t *d, size_t len) { return len >= 20 && (d[0] >> 4) == 4 && (d[0] & 0x0f) >= 5; }
+static bool ipv6_valid(const uint8_t *, size_t len) { return len >= 40; }
+
+static void parse_l4(Pkt &p, int proto, const uint8_t *d, size_t len)
+{
+    if (proto == 17) {
+        if (len >= 8) { p.l4 = L4_UDP; p.l4hdr = d; p.l4len = (uint32_t)len; }
+    } else if (proto == 6) {
+        if (len >= 20) {
+            p.l4 = L4_TCP; p.l4hdr = d; p.l4len = (uint32_t)len;
+            p.syn = (d[13] & 0x02) != 0;
+        }
+    }
+}
+
+static void parse_ipv4(Pkt &p, const uint8_t *d, size_t len, int depth)
+{
+    if (!p.has_v4) { p.has_v4 = true; p.v4hdr = d; }
+    size_t total = rd16be(d + 2);
+    if (total < len && total != 0) len = total; // IPv4Layer ctor trims to totalLength
+    size_t hl = (size_t)(d[0] & 0x0f) * 4;
+    if (len <= hl) return;
+    const uint8_t *pl = d + hl;
+    size_t pll = len - hl;
+    uint16_t frag = rd16be(d + 6);
+    if ((frag & 0x2000) || (frag & 0x1fff)) return; // fragment -> payload layer, no L4
+    uint8_t proto = d[9];
+    if (proto == 17 || proto == 6) parse_l4(p, proto, pl, pll);
+    else if (proto == 4 || proto == 41) parse_ip(p, pl, pll, depth + 1);
+}
+
+static void parse_ipv6(Pkt &p, const uint8_t *d, size_t len, int depth)
+{
+    if (!p.has_v6) { p.has_v6 = true; p.v6hdr = d; }
+    // IPv6Layer::parseExtensions
+    uint8_t next = d[6];
+    size_t off = 40;
+    bool frag = false;
+    while (len >= 2 && off <= len - 2) {
+        size_t elen;
+        if (next == 44) elen = 8;
+        else if (next == 0 || next == 60 || next == 43) elen = ((size_t)d[off + 1] + 1) * 8;
+        else if (next == 51) elen = ((size_t)d[off + 1] + 2) * 4;
+        else break;
+        frag = (next == 44);
+        next = d[off];
+        off += elen;
+    }
+    size_t hdrlen = off;
+    size_t total = (size_t)rd16be(d + 4) + hdrlen;
+    if (total < len) len = total;
+    if (len <= hdrlen) return;
+    const uint8_t *pl = d + hdrlen;
+    size_t pll = len - hdrlen;
+    if (frag) return;
+    if (next == 17 || next == 6) parse_l4(p, next, pl, pll);
+    else if (next == 4 || next == 41) parse_ip(p, pl, pll, depth + 1);
+}
+
+static void parse_ip(Pkt &p, const uint8_t *d, size_t len, int depth)
+{
+    if (depth > 4 || len < 1) return;
+    int v = d[0] >> 4;
+    if (v == 4 && ipv4_valid(d, len)) parse_ipv4(p, d, len, depth);
+    else if (v == 6 && ipv6_valid(d, len)) parse_ipv6(p, d, len, depth);
+}
+
+static void parse_ether_payload(Pkt &p, uint16_t et, const uint8_t *d, size_t len, int depth)
+{
+    if (et == 0x0800) { if (ipv4_valid(d, len)) parse_ipv4(p, d, len, 0); }
+    else if (et == 0x86DD) { if (ipv6_valid(d, len)) parse_ipv6(p, d, len, 0); }
+    else if ((et == 0x8100 || et == 0x88A8) && depth < 8) {
+        if (len <= 4) return;
+        parse_ether_payload(p, rd16be(d + 2), d + 4, len - 4, depth + 1);
+    }
+}
+
+static void parse_packet(Pkt &p, uint32_t linktype)
+{
+    const uint8_t *d = p.data;
+    size_t len = p.caplen;
+    if (linktype == 1) {
+        if (len < 14 || rd16be(d + 12) < 0x600) return;
+        if (len <= 14) return;
+        parse_ether_payload(p, rd16be(d + 12), d + 14, len - 14, 0);
+    } else if (linktype == 101 || linktype == 12 || linktype == 14 || linktype == 228 || linktype == 229) {
+        parse_ip(p, d, len, 0);
+    } else if (linktype == 113) {
+        if (len <= 16) return;
+        parse_ether_payload(p, rd16be(d + 14), d + 16, len - 16, 0);
+    }
+    if (p.has_v4) p.l3 = L3_IPV4;
+    else if (p.has_v6) p.l3 = L3_IPV6;
+}
+
+// PcapInputStream.cpp:401-416
+static void set_direction(Pkt &p, const Config &c)
+{
+    p.dir = DIR_UNKNOWN;
+    if (p.has_v4) {
+        if (match_v4(c, rd32le(p.v4hdr + 16))) p.dir = DIR_TO_HOST;
+        else if (match_v4(c, rd32le(p.v4hdr + 12))) p.dir = DIR_FROM_HOST;
+    } else if (p.has_v6) {
+        if (match_v6(c, p.v6hdr + 24)) p.dir = DIR_TO_HOST;
+        else if (match_v6(c, p.v6hdr + 8)) p.dir = DIR_FROM_HOST;
+    }
+}
+
+// PcapPlusPlus hash5Tuple (directionUnique=false), FNV-1 32-bit. Restated.
+static uint32_t hash5tuple(const Pkt &p)
+{
+    if (!p.has_v4 && !p.has_v6) return 0;
+    if (p.l4 != L4_TCP && p.l4 != L4_UDP) return 0;
+    uint16_t ps, pd;
+    memcpy(&ps, p.l4hdr, 2);
+    memcpy(&pd, p.l4hdr + 2, 2);
+    int sp = (pd < ps) ? 1 : 0;
+    const uint8_t *vec[5];
+    size_t vl[5];
+    vec[0 + sp] = (const uint8_t *)&ps; vl[0 + sp] = 2;
+    vec[1 - sp] = (const uint8_t *)&pd; vl[1 - sp] = 2;
+    if (p.has_v4) {
+        uint32_t s = rd32le(p.v4hdr + 12), dd = rd32le(p.v4hdr + 16);
+        if (ps == pd && dd < s) sp = 1;
+        vec[2 + sp] = p.v4hdr + 12; vl[2 + sp] = 4;
+        vec[3 - sp] = p.v4hdr + 16; vl[3 - sp] = 4;
+        vec[4] = p.v4hdr + 9; vl[4] = 1;
+    } else {
+        // the reference compares the two array addresses, never true
+        vec[2 + sp] = p.v6hdr + 8; vl[2 + sp] = 16;
+        vec[3 - sp] = p.v6hdr + 24; vl[3 - sp] = 16;
+        vec[4] = p.v6hdr + 6; vl[4] = 1;
+    }
+    uint32_t h = 0x811C9DC5u;
+    for (int i = 0; i < 5; i++)
+        for (size_t j = 0; j < vl[i]; j++) { h *= 0x01000193u; h ^= vec[i][j]; }
+    return h;
+}
+
+static std::string ipv4_str(uint32_t le)
+{
+    char b[20];
+    snprintf(b, sizeof b, "%u.%u.%u.%u", le & 0xff, (le >> 8) & 0xff, (le >> 16) & 0xff, le >> 24);
+    return b;
+}
+static std::string ipv6_str(const uint8_t *a)
+{
+    char b[64];
+    inet_ntop(AF_INET6, a, b, sizeof b);
+    return b;
+}
+
+// ---------------------------------------------------------------- DNS decoder
+// libs/visor_dns/DnsResource.cpp:53-148 decodeName, restated with identical
+// bounds/truncation/pointer rules. Returns the encoded length; `out` receives
+// the decoded bytes (not NUL-truncated here; callers truncate as std::string did).
+struct DnsMsg {
+    const uint8_t *d;
+    size_t len;
+    uint8_t byte(size_t off) const { return d[off]; }
+};
+
+static size_t decode_name(const DnsMsg &m, size_t off, std::string &out, int iteration)
+{
+    size_t enc = 0, dec = 0;
+    out.clear();
+    size_t cur = off;
+    if (cur + 1 > m.len) return enc;
+    if (iteration > 20) return enc;
+    uint8_t wl = m.byte(cur);
+    while (wl != 0) {
+        if ((wl & 0xc0) == 0xc0) {
+            if (cur + 2 > m.len || enc > 255) return enc;
+            uint16_t ptr = (uint16_t)((wl & 0x3f) * 256 + m.byte(cur + 1));
+            if (ptr < 12 || ptr >= m.len) { out.clear(); return 0; }
+            std::string tmp;
+            decode_name(m, ptr, tmp, iteration + 1);
+            // tempResult is a zero-filled buffer: copy stops at the first NUL
+            size_t i = 0;
+            while (i < tmp.size() && tmp[i] != 0 && dec < 255) { out.push_back(tmp[i++]); dec++; }
+            return enc + 2;
+        } else {
+            if (cur + wl + 1 > m.len || enc + wl > 255) {
+                if (enc == 256) { out.pop_back(); dec--; }
+                else enc++;
+                return enc;
+            }
+            out.append((const char *)m.d + cur + 1, wl);
+            out.push_back('.');
+            dec += wl + 1;
+            cur += wl + 1;
+            enc += wl + 1;
+            if (cur + 1 > m.len) {
+                if (enc == 256) { dec--; out.pop_back(); }
+                else enc++;
+                return enc;
+            }
+            wl = m.byte(cur);
+        }
+    }
+    if (!out.empty()) out.pop_back(); // remove the last '.'
+    enc++;
+    return enc;
+}
+
+struct DnsParse {
+    bool ok = false;        // parseResources(queryOnly=true) result
+    bool has_query = false;
+    std::string name;       // getName() (NUL-truncated like std::string(char*))
+    uint16_t qtype = 0;
+};
+
+// DnsLayer.cpp:119-209 with queryOnly=true.
+static DnsParse parse_resources(const DnsMsg &m)
+{
+    DnsParse r;
+    uint16_t qd = rd16be(m.d + 4), an = rd16be(m.d + 6), ns = rd16be(m.d + 8), ar = rd16be(m.d + 10);
+    uint32_t total = (uint32_t)qd + an + ns + ar;
+    if (total > 100) return r;
+    size_t off = 12;
+    for (uint32_t i = 0; i < total; i++) {
+        bool is_q = false;
+        if (qd > 0) { is_q = true; qd--; }
+        else if (an > 0) an--;
+        else if (ns > 0) ns--;
+        else ar--;
+        std::string nm;
+        size_t nl = decode_name(m, off, nm, 1);
+        size_t sz;
+        if (is_q) sz = nl + 4;
+        else {
+            size_t dl_off = off + nl + 8;
+            uint16_t dl = (dl_off + 2 <= m.len) ? rd16be(m.d + dl_off) : 0;
+            sz = nl + 10 + dl;
+        }
+        size_t start = off;
+        off += sz;
+        if (off > m.len) return r;
+        if (is_q) {
+            r.has_query = true;
+            if (nl > 0) {
+                size_t z = nm.find('\0');
+                r.name = z == std::string::npos ? nm : nm.substr(0, z);
+            }
+            r.qtype = rd16be(m.d + start + nl);
+            break;
+        }
+    }
+    r.ok = true;
+    return r;
+}
+
+static std::string lower(const std::string &s)
+{
+    std::string o = s;
+    for (auto &c : o) c = (char)tolower((unsigned char)c);
+    return o;
+}
+
+// libs/visor_dns/dns.cpp:9-43
+static void aggregate_domain(const std::string &domain, size_t suffix_size, std::string &q2, std::string &q3)
+{
+    q2 = domain;
+    q3 = domain;
+    if (domain.size() < 5) { q3 = ""; return; }
+    size_t endDot = std::string::npos;
+    if (suffix_size > 0 && domain.size() > suffix_size) endDot = domain.size() - suffix_size;
+    else if (domain.back() == '.') endDot = domain.size() - 2;
+    size_t first_dot = domain.rfind('.', endDot);
+    if (first_dot != std::string::npos && first_dot > 0) {
+        size_t second_dot = domain.rfind('.', first_dot - 1);
+        if (second_dot != std::string::npos) {
+            q2 = domain.substr(second_dot);
+            if (second_dot > 0) {
+                size_t third_dot = domain.rfind('.', second_dot - 1);
+                if (third_dot != std::string::npos) q3 = domain.substr(third_dot);
+            }
+        } else {
+            q3 = "";
+        }
+    }
+}
+
+// ---------------------------------------------------------------- buckets
+struct BaseBucket {
+    TS start, end;
+    unsigned period_length = 0;
+    bool read_only = false;
+    uint64_t num_events = 0, num_samples = 0;
+    void set_read_only(TS s)
+    {
+        end = s;
+        period_length = (unsigned)(end.sec - start.sec);
+        read_only = true;
+    }
+};
+
+struct NetBucket : BaseBucket {
+    uint64_t UDP = 0, TCP = 0, OtherL4 = 0, IPv4 = 0, IPv6 = 0, TCP_SYN = 0, in = 0, out = 0, unk = 0, total = 0,
+             filtered = 0;
+    ExactQuantile<uint64_t> payload;
+    Cpc src, dst;
+    ExactTop<uint32_t> top4;
+    ExactTop<std::string> top6;
+
+    void merge(const NetBucket &o)
+    {
+        UDP += o.UDP; TCP += o.TCP; OtherL4 += o.OtherL4; IPv4 += o.IPv4; IPv6 += o.IPv6; TCP_SYN += o.TCP_SYN;
+        in += o.in; out += o.out; unk += o.unk; total += o.total; filtered += o.filtered;
+        payload.merge(o.payload);
+        src.merge(o.src);
+        dst.merge(o.dst);
+        top4.merge(o.top4);
+        top6.merge(o.top6);
+    }
+};
+
+struct DnsBucket : BaseBucket {
+    uint64_t xacts_total = 0, xacts_in = 0, xacts_out = 0, xacts_timed_out = 0, queries = 0, replies = 0, UDP = 0,
+             TCP = 0, IPv4 = 0, IPv6 = 0, NX = 0, REFUSED = 0, SRVFAIL = 0, NOERROR = 0, NODATA = 0, total = 0,
+             filtered = 0;
+    ExactQuantile<uint64_t> xact_from, xact_to; // "out" / "in" quantiles_us
+    ExactQuantile<double> ratio;
+    Cpc qname;
+    ExactTop<std::string> qname2, qname3, nx, refused, srvfail, nodata, noerror, sized_resp, slow_in, slow_out;
+    ExactTop<uint16_t> udp_port, qtype, rcode;
+
+    void merge(const DnsBucket &o)
+    {
+        xacts_total += o.xacts_total; xacts_in += o.xacts_in; xacts_out += o.xacts_out;
+        xacts_timed_out += o.xacts_timed_out; queries += o.queries; replies += o.replies; UDP += o.UDP;
+        TCP += o.TCP; IPv4 += o.IPv4; IPv6 += o.IPv6; NX += o.NX; REFUSED += o.REFUSED; SRVFAIL += o.SRVFAIL;
+        NOERROR += o.NOERROR; NODATA += o.NODATA; total += o.total; filtered += o.filtered;
+        xact_from.merge(o.xact_from); xact_to.merge(o.xact_to); ratio.merge(o.ratio);
+        qname.merge(o.qname);
+        qname2.merge(o.qname2); qname3.merge(o.qname3); nx.merge(o.nx); refused.merge(o.refused);
+        srvfail.merge(o.srvfail); nodata.merge(o.nodata); noerror.merge(o.noerror); sized_resp.merge(o.sized_resp);
+        slow_in.merge(o.slow_in); slow_out.merge(o.slow_out);
+        udp_port.merge(o.udp_port); qtype.merge(o.qtype); rcode.merge(o.rcode);
+    }
+};
+
+// AbstractMetricsManager window/period engine (src/AbstractMetricsManager.h:276-333)
+template <typename B>
+struct Window {
+    std::deque<std::unique_ptr<B>> buckets;
+    unsigned num_periods;
+    int64_t next_shift_sec = 0;
+    explicit Window(unsigned np) : num_periods(std::max(1u, std::min(np, 10u))) { buckets.emplace_front(new B()); }
+    B &live() { return *buckets.front(); }
+    void set_start(TS ts)
+    {
+        next_shift_sec = ts.sec + 60;
+        buckets.front()->start = ts;
+    }
+    void set_end(TS ts) { buckets.front()->set_read_only(ts); }
+    // returns true if a period shift happened
+    bool maybe_shift(TS ts)
+    {
+        if (!(num_periods > 1 && ts.sec >= next_shift_sec)) return false;
+        buckets.emplace_front(new B());
+        buckets.front()->start = ts;
+        buckets[1]->set_read_only(ts);
+        if (buckets.size() > num_periods) buckets.pop_back();
+        next_shift_sec = ts.sec + 60;
+        return true;
+    }
+    void new_event(bool deep)
+    {
+        live().num_events++;
+        if (deep) live().num_samples++;
+    }
+};
+
+struct XactKey {
+    uint32_t flow;
+    uint16_t txid;
+    bool operator==(const XactKey &o) const { return flow == o.flow && txid == o.txid; }
+};
+struct XactKeyHash {
+    size_t operator()(const XactKey &k) const { return std::hash<uint64_t>()(((uint64_t)k.flow << 16) | k.txid); }
+};
+struct Xact {
+    TS start;
+    size_t query_size;
+};
+
+// ---------------------------------------------------------------- the engine
+struct Engine {
+    Config cfg;
+    uint32_t linktype = 1;
+    Window<NetBucket> net;
+    Window<DnsBucket> dns;
+    std::unordered_map<XactKey, Xact, XactKeyHash> xacts;
+    uint32_t ttl_s = 0, ttl_ms = 0;
+    float to90 = 0.0f, from90 = 0.0f;
+
+    explicit Engine(const Config &c) : cfg(c), net(c.num_periods), dns(c.num_periods)
+    {
+        // TransactionManager.h:60-68
+        if (c.xact_ttl_ms > 1000) { ttl_s = c.xact_ttl_ms / 1000; ttl_ms = c.xact_ttl_ms - ttl_s * 1000; }
+        else ttl_ms = c.xact_ttl_ms;
+    }
+
+    void start(TS ts)
+    {
+        net.set_start(ts);
+        dns.set_start(ts);
+    }
+    void end(TS ts)
+    {
+        net.set_end(ts);
+        dns.set_end(ts);
+    }
+
+    // NetworkMetricsManager::process_packet + bucket (net/v1 ...cpp:516-548,682-764)
+    void net_packet(const Pkt &p)
+    {
+        net.maybe_shift(p.ts);
+        net.new_event(true);
+        NetBucket &b = net.live();
+        b.total++;
+        if (p.dir == DIR_FROM_HOST) b.out++;
+        else if (p.dir == DIR_TO_HOST) b.in++;
+        else b.unk++;
+        if (p.l3 == L3_IPV6) b.IPv6++;
+        else if (p.l3 == L3_IPV4) b.IPv4++;
+        if (p.l4 == L4_UDP) b.UDP++;
+        else if (p.l4 == L4_TCP) { b.TCP++; if (p.syn) b.TCP_SYN++; }
+        else b.OtherL4++;
+        b.payload.update(p.caplen);
+        if (p.has_v4) {
+            uint32_t in = 0, out = 0;
+            if (p.dir == DIR_TO_HOST) in = rd32le(p.v4hdr + 12);
+            else if (p.dir == DIR_FROM_HOST) out = rd32le(p.v4hdr + 16);
+            if (p.l3 == L3_IPV4 && in) { b.src.update_u32(in); b.top4.update(in); }
+            if (p.l3 == L3_IPV4 && out) { b.dst.update_u32(out); b.top4.update(out); }
+        } else if (p.has_v6) {
+            static const uint8_t zero[16] = {0};
+            const uint8_t *in = nullptr, *out = nullptr;
+            if (p.dir == DIR_TO_HOST) in = p.v6hdr + 8;
+            else if (p.dir == DIR_FROM_HOST) out = p.v6hdr + 24;
+            if (p.l3 == L3_IPV6 && in && memcmp(in, zero, 16)) { b.src.update_bytes(in, 16); b.top6.update(ipv6_str(in)); }
+            if (p.l3 == L3_IPV6 && out && memcmp(out, zero, 16)) { b.dst.update_bytes(out, 16); b.top6.update(ipv6_str(out)); }
+        }
+    }
+
+    // DnsStreamHandler::process_udp_packet_cb (dns/v1 ...cpp:270-302) and the manager/bucket path
+    void dns_udp_packet(const Pkt &p, uint32_t flowkey)
+    {
+        uint16_t sport = rd16be(p.l4hdr), dport = rd16be(p.l4hdr + 2);
+        auto is_dns = [](uint16_t x) { return x == 53 || x == 5353 || x == 5355 || x == 53000; };
+        uint16_t metric_port = 0;
+        if (is_dns(dport)) metric_port = sport;
+        else if (is_dns(sport)) metric_port = dport;
+        if (!metric_port) return;
+        DnsMsg m{p.l4hdr + 8, p.l4len - 8};
+        // A DNS message shorter than the 12-byte header is read past its end by
+        // the reference (UB); we read the bytes that follow inside the capture, else 0.
+        uint8_t hdr_buf[12];
+        const uint8_t *cap_end = p.data + p.caplen;
+        for (int i = 0; i < 12; i++) hdr_buf[i] = (m.d + i < cap_end) ? m.d[i] : 0;
+        DnsMsg hm = m;
+        std::vector<uint8_t> tmp;
+        if (m.len < 12) {
+            tmp.assign(hdr_buf, hdr_buf + 12);
+            hm = DnsMsg{tmp.data(), m.len};
+        }
+        const uint8_t *h = hm.d;
+        uint16_t txid = rd16be(h);
+        bool qr = (h[2] & 0x80) != 0;
+        uint8_t rcode = h[3] & 0x0f;
+        uint16_t ancount = rd16be(h + 6);
+
+        // DnsMetricsManager::process_dns_layer (:1350-1370)
+        if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
+        dns.new_event(true);
+        DnsBucket &b = dns.live();
+        b.total++;
+        if (p.l3 == L3_IPV6) b.IPv6++;
+        else if (p.l3 == L3_IPV4) b.IPv4++;
+        b.UDP++;
+        if (qr) {
+            b.replies++;
+            if (rcode == 0) { b.NOERROR++; if (!ancount) b.NODATA++; }
+            else if (rcode == 2) b.SRVFAIL++;
+            else if (rcode == 3) b.NX++;
+            else if (rcode == 5) b.REFUSED++;
+        } else b.queries++;
+        b.udp_port.update(metric_port);
+        DnsParse r;
+        if (m.len >= 12) r = parse_resources(m);
+        else {
+            DnsMsg mm{hdr_buf, m.len};
+            r = parse_resources_short(mm);
+        }
+        std::string name_lower;
+        if (r.ok) {
+            if (qr) b.rcode.update(rcode);
+            if (r.has_query) {
+                name_lower = lower(r.name);
+                b.qname.update_str(name_lower);
+                b.qtype.update(r.qtype);
+                if (qr) {
+                    if (rcode == 2) b.srvfail.update(name_lower);
+                    else if (rcode == 3) b.nx.update(name_lower);
+                    else if (rcode == 5) b.refused.update(name_lower);
+                    else if (rcode == 0) {
+                        if (cfg.dns_details) b.noerror.update(name_lower);
+                        if (!ancount) b.nodata.update(name_lower);
+                    }
+                    if (cfg.dns_details) b.sized_resp.update(name_lower, m.len);
+                }
+                std::string q2, q3;
+                aggregate_domain(name_lower, 0, q2, q3);
+                b.qname2.update(q2);
+                if (!q3.empty()) b.qname3.update(q3);
+            }
+        }
+        // transactions
+        XactKey k{flowkey, txid};
+        if (qr) {
+            auto it = xacts.find(k);
+            if (it != xacts.end()) {
+                Xact x = it->second;
+                xacts.erase(it);
+                // timespec_diff (TransactionManager.h:24-37)
+                TS d;
+                d.sec = p.ts.sec > x.start.sec ? p.ts.sec - x.start.sec : x.start.sec - p.ts.sec;
+                d.nsec = p.ts.nsec - x.start.nsec;
+                if (d.nsec < 0) { d.sec--; d.nsec += 1000000000L; }
+                bool timed_out = false;
+                if (d.sec > (int64_t)ttl_s) timed_out = true;
+                else if (d.sec == (int64_t)ttl_s && (d.nsec / 1.0e6) >= ttl_ms) timed_out = true;
+                if (timed_out) b.xacts_timed_out++;
+                else new_xact(b, p, d, x, r);
+            }
+        } else {
+            xacts[k] = Xact{p.ts, m.len};
+        }
+    }
+
+    // header-only message (< 12 bytes): the counts come from the padded header copy
+    DnsParse parse_resources_short(const DnsMsg &m)
+    {
+        DnsParse r;
+        uint16_t qd = rd16be(m.d + 4), an = rd16be(m.d + 6), ns = rd16be(m.d + 8), ar = rd16be(m.d + 10);
+        uint32_t total = (uint32_t)qd + an + ns + ar;
+        if (total > 100) return r;
+        if (total == 0) { r.ok = true; return r; }
+        return r; // first resource starts at offset 12 > len: out of bounds
+    }
+
+    // DnsMetricsBucket::new_dns_transaction (:1093-1138)
+    void new_xact(DnsBucket &b, const Pkt &p, TS d, const Xact &x, const DnsParse &r)
+    {
+        uint64_t us = (uint64_t)((d.sec * 1000000000LL) + d.nsec) / 1000;
+        b.xacts_total++;
+        if (p.dir == DIR_TO_HOST) { b.xacts_out++; b.xact_from.update(us); }
+        else if (p.dir == DIR_FROM_HOST) { b.xacts_in++; b.xact_to.update(us); }
+        size_t resp_len = p.l4len - 8;
+        if (x.query_size) b.ratio.update((double)resp_len / (double)x.query_size);
+        if (r.ok && r.has_query) {
+            if (p.dir == DIR_TO_HOST && from90 > 0 && (float)us >= from90) b.slow_out.update(r.name);
+            else if (p.dir == DIR_FROM_HOST && to90 > 0 && (float)us >= to90) b.slow_in.update(r.name);
+        }
+    }
+
+    // DnsMetricsManager::on_period_shift (dns/v1/DnsStreamHandler.h:252-267)
+    void on_dns_period_shift(TS ts)
+    {
+        uint64_t timed_out = 0;
+        for (auto it = xacts.begin(); it != xacts.end();) {
+            if (ts.sec >= (int64_t)ttl_s + it->second.start.sec) { it = xacts.erase(it); timed_out++; }
+            else ++it;
+        }
+        if (timed_out) dns.live().xacts_timed_out += timed_out;
+        const DnsBucket &b1 = *dns.buckets.at(1);
+        if (!b1.xact_from.empty()) from90 = (float)b1.xact_from.p(0.90);
+        if (!b1.xact_to.empty()) to90 = (float)b1.xact_to.p(0.90);
+    }
+
+    void process(const Pkt &p0)
+    {
+        Pkt p = p0;
+        parse_packet(p, linktype);
+        set_direction(p, cfg);
+        net_packet(p);
+        if (p.l4 == L4_UDP) dns_udp_packet(p, hash5tuple(p));
+    }
+};
+
+// ---------------------------------------------------------------- JSON rendering
+template <typename K, typename F>
+static void top_json(J &j, const std::string &key, const ExactTop<K> &t, size_t n, F fmt)
+{
+    std::vector<std::pair<std::string, uint64_t>> v;
+    for (auto &kv : t.m) v.push_back({fmt(kv.first), kv.second});
+    std::sort(v.begin(), v.end(), [](const auto &a, const auto &b) {
+        if (a.second != b.second) return a.second > b.second;
+        return a.first < b.first;
+    });
+    j.key(key);
+    j.arr();
+    for (size_t i = 0; i < std::min(n, v.size()); i++) {
+        j.obj();
+        j.key("name"); j.str(v[i].first);
+        j.key("estimate"); j.u64(v[i].second);
+        j.end_obj();
+    }
+    j.end_arr();
+}
+
+template <typename T>
+static void quant_json(J &j, const std::string &key, const ExactQuantile<T> &q)
+{
+    if (q.empty()) return;
+    auto v = q.quantiles();
+    const char *names[4] = {"p50", "p90", "p95", "p99"};
+    j.key(key);
+    j.obj();
+    for (int i = 0; i < 4; i++) {
+        j.key(names[i]);
+        if constexpr (std::is_floating_point<T>::value) j.dbl(v[i]);
+        else j.u64((uint64_t)v[i]);
+    }
+    j.end_obj();
+}
+
+static std::string id_str(const std::string &s) { return s; }
+
+static void net_json(J &j, const NetBucket &b, size_t topn)
+{
+    j.key("period"); j.obj();
+    j.key("start_ts"); j.i64(b.start.sec);
+    j.key("length"); j.u64(b.period_length);
+    j.end_obj();
+    j.key("events"); j.u64(b.num_events);
+    j.key("deep_samples"); j.u64(b.num_samples);
+    j.key("udp"); j.u64(b.UDP);
+    j.key("tcp"); j.u64(b.TCP);
+    j.key("protocol"); j.obj(); j.key("tcp"); j.obj(); j.key("syn"); j.u64(b.TCP_SYN); j.end_obj(); j.end_obj();
+    j.key("other_l4"); j.u64(b.OtherL4);
+    j.key("ipv4"); j.u64(b.IPv4);
+    j.key("ipv6"); j.u64(b.IPv6);
+    j.key("in"); j.u64(b.in);
+    j.key("out"); j.u64(b.out);
+    j.key("unknown_dir"); j.u64(b.unk);
+    j.key("total"); j.u64(b.total);
+    j.key("filtered"); j.u64(b.filtered);
+    j.key("cardinality"); j.obj();
+    j.key("src_ips_in"); j.i64(lround(b.src.estimate()));
+    j.key("dst_ips_out"); j.i64(lround(b.dst.estimate()));
+    j.end_obj();
+    top_json(j, "top_ipv4", b.top4, topn, ipv4_str);
+    top_json(j, "top_ipv6", b.top6, topn, id_str);
+    j.key("top_geoLoc"); j.arr(); j.end_arr();
+    j.key("top_ASN"); j.arr(); j.end_arr();
+    quant_json(j, "payload_size", b.payload);
+}
+
+static void dns_json(J &j, const DnsBucket &b, size_t topn, bool details)
+{
+    auto u16s = [](const uint16_t &v) { return std::to_string(v); };
+    auto rc = [](const uint16_t &v) { auto &m = rcode_names(); auto it = m.find(v); return it != m.end() ? it->second : std::to_string(v); };
+    auto qt = [](const uint16_t &v) { auto &m = qtype_names(); auto it = m.find(v); return it != m.end() ? it->second : std::to_string(v); };
+    j.key("period"); j.obj();
+    j.key("start_ts"); j.i64(b.start.sec);
+    j.key("length"); j.u64(b.period_length);
+    j.end_obj();
+    j.key("wire_packets"); j.obj();
+    j.key("events"); j.u64(b.num_events);
+    j.key("deep_samples"); j.u64(b.num_samples);
+    j.key("queries"); j.u64(b.queries);
+    j.key("replies"); j.u64(b.replies);
+    j.key("tcp"); j.u64(b.TCP);
+    j.key("udp"); j.u64(b.UDP);
+    j.key("ipv4"); j.u64(b.IPv4);
+    j.key("ipv6"); j.u64(b.IPv6);
+    j.key("nxdomain"); j.u64(b.NX);
+    j.key("refused"); j.u64(b.REFUSED);
+    j.key("srvfail"); j.u64(b.SRVFAIL);
+    j.key("noerror"); j.u64(b.NOERROR);
+    j.key("nodata"); j.u64(b.NODATA);
+    j.key("total"); j.u64(b.total);
+    j.key("filtered"); j.u64(b.filtered);
+    j.end_obj();
+    j.key("cardinality"); j.obj(); j.key("qname"); j.i64(lround(b.qname.estimate())); j.end_obj();
+    j.key("xact"); j.obj();
+    j.key("counts"); j.obj(); j.key("total"); j.u64(b.xacts_total); j.key("timed_out"); j.u64(b.xacts_timed_out); j.end_obj();
+    j.key("in"); j.obj(); j.key("total"); j.u64(b.xacts_in);
+    top_json(j, "top_slow", b.slow_in, topn, id_str);
+    quant_json(j, "quantiles_us", b.xact_to);
+    j.end_obj();
+    j.key("out"); j.obj(); j.key("total"); j.u64(b.xacts_out);
+    top_json(j, "top_slow", b.slow_out, topn, id_str);
+    quant_json(j, "quantiles_us", b.xact_from);
+    j.end_obj();
+    if (!b.ratio.empty()) { j.key("ratio"); j.obj(); quant_json(j, "quantiles", b.ratio); j.end_obj(); }
+    j.end_obj();
+    top_json(j, "top_udp_ports", b.udp_port, topn, u16s);
+    top_json(j, "top_qname2", b.qname2, topn, id_str);
+    top_json(j, "top_qname3", b.qname3, topn, id_str);
+    top_json(j, "top_nxdomain", b.nx, topn, id_str);
+    top_json(j, "top_refused", b.refused, topn, id_str);
+    top_json(j, "top_srvfail", b.srvfail, topn, id_str);
+    top_json(j, "top_nodata", b.nodata, topn, id_str);
+    if (details) {
+        top_json(j, "top_qname_by_resp_bytes", b.sized_resp, topn, id_str);
+        top_json(j, "top_noerror", b.noerror, topn, id_str);
+    }
+    top_json(j, "top_rcode", b.rcode, topn, rc);
+    top_json(j, "top_qtype", b.qtype, topn, qt);
+}
+
+// merged window (AbstractMetricsManager::window_merged_json) or a single bucket
+template <typename B>
+static std::unique_ptr<B> window_bucket(const Window<B> &w, unsigned window)
+{
+    std::unique_ptr<B> out(new B());
+    if (window <= 1) {
+        *out = *w.buckets.at(0);
+        return out;
+    }
+    bool firstb = true;
+    unsigned p = window;
+    for (auto &m : w.buckets) {
+        if (p-- == 0) break;
+        out->num_events += m->num_events;
+        out->num_samples += m->num_samples;
+        out->period_length += m->period_length;
+        if (firstb || m->start.sec < out->start.sec) out->start.sec = m->start.sec;
+        if (firstb || m->end.sec > out->end.sec) out->end.sec = m->end.sec;
+        firstb = false;
+        out->merge(*m);
+        // a union of CPC sketches reports the ICON estimate even for one input
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------- pcap reader
+struct PcapFile {
+    bool swapped = false, nano = false;
+    uint32_t linktype = 1;
+    const uint8_t *p = nullptr;
+    size_t len = 0, pos = 24;
+    bool open(const uint8_t *d, size_t n, std::string &err)
+    {
+        p = d; len = n;
+        if (n < 24) { err = "Cannot open pcap/pcapng file"; return false; }
+        uint32_t magic = rd32le(d);
+        if (magic == 0xa1b2c3d4) {} else if (magic == 0xa1b23c4d) nano = true;
+        else if (magic == 0xd4c3b2a1) swapped = true;
+        else if (magic == 0x4d3cb2a1) { swapped = true; nano = true; }
+        else { err = "Cannot open pcap/pcapng file"; return false; }
+        linktype = u32(d + 20);
+        return true;
+    }
+    uint32_t u32(const uint8_t *q) const { uint32_t v = rd32le(q); return swapped ? __builtin_bswap32(v) : v; }
+    bool next(Pkt &pk)
+    {
+        if (pos + 16 > len) return false;
+        const uint8_t *h = p + pos;
+        uint32_t incl = u32(h + 8);
+        if (pos + 16 + incl > len) return false;
+        pk = Pkt();
+        pk.ts.sec = u32(h);
+        pk.ts.nsec = nano ? u32(h + 4) : (int64_t)u32(h + 4) * 1000;
+        pk.caplen = incl;
+        pk.data = h + 16;
+        pos += 16 + incl;
+        return true;
+    }
+};
+
+static bool parse_config(const char *s, Config &c, std::string &err)
+{
+    std::string str = s ? s : "";
+    size_t pos = 0;
+    while (pos < str.size()) {
+        size_t e = str.find(';', pos);
+        std::string kv = str.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
+        pos = e == std::string::npos ? str.size() : e + 1;
+        if (kv.empty()) continue;
+        size_t eq = kv.find('=');
+        std::string k = kv.substr(0, eq), v = eq == std::string::npos ? "" : kv.substr(eq + 1);
+        if (k == "host_spec") { if (!parse_host_specs(v, c, err)) return false; }
+        else if (k == "num_periods") c.num_periods = (unsigned)atoi(v.c_str());
+        else if (k == "window") c.window = (unsigned)atoi(v.c_str());
+        else if (k == "topn_count") c.topn_count = (size_t)atoll(v.c_str());
+        else if (k == "xact_ttl_ms") c.xact_ttl_ms = (uint32_t)atoll(v.c_str());
+        else if (k == "dns_details") c.dns_details = atoi(v.c_str()) != 0;
+        else { err = "unknown config key: " + k; return false; }
+    }
+    return true;
+}
+
+} // namespace pvo
+
+// ---------------------------------------------------------------- C ABI (tests / cpu_baseline only)
+extern "C" {
+
+// Runs the restated pktvisor-reader pipeline (net v1 + dns v1) on an in-memory
+// pcap file image. `cfg` is "key=value;..." (host_spec, num_periods, window,
+// topn_count, xact_ttl_ms, dns_details). On success returns 0 and *out holds a
+// malloc'd JSON document {"<W>m": {"packets": {...}, "dns": {...}}}.
+int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
+{
+    using namespace pvo;
+    Config c;
+    std::string err;
+    *out = nullptr;
+    if (!parse_config(cfg, c, err)) { *out = strdup(err.c_str()); return -1; }
+    PcapFile f;
+    if (!f.open(file, len, err)) { *out = strdup(err.c_str()); return -2; }
+    Engine e(c);
+    e.linktype = f.linktype;
+    Pkt pk;
+    TS last;
+    bool first = true;
+    while (f.next(pk)) {
+        if (first) { e.start(pk.ts); first = false; }
+        e.process(pk);
+        last = pk.ts;
+    }
+    if (!first) e.end(last);
+    J j;
+    j.obj();
+    unsigned w = c.window <= 1 ? 1 : c.window;
+    j.key(std::to_string(w) + "m");
+    j.obj();
+    auto nb = window_bucket(e.net, w);
+    j.key("packets"); j.obj(); net_json(j, *nb, c.topn_count); j.end_obj();
+    auto db = window_bucket(e.dns, w);
+    j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_details); j.end_obj();
+    j.end_obj();
+    j.end_obj();
+    *out = strdup(j.s.c_str());
+    return 0;
+}
+
+void pvo_free(char *p) { free(p); }
+
+// Exposed for the sketch pinning tests: estimate of a CPC sketch fed with the
+// given sequence of uint32 values (update(uint32_t)) or byte strings.
+double pvo_cpc_u32(const uint32_t *v, size_t n, int merged)
+{
+    pvo::Cpc c;
+    for (size_t i = 0; i < n; i++) c.update_u32(v[i]);
+    if (merged) { pvo::Cpc u; u.merge(c); return u.estimate(); }
+    return c.estimate();
+}
+
+void pvo_murmur3(const uint8_t *d, size_t n, uint64_t seed, uint64_t *out2)
+{
+    pvo::murmur3_128(d, n, seed, out2[0], out2[1]);
+}
+
+double pvo_icon(uint32_t c) { return pvo::icon_estimate(c); }
+
+} // extern "C"
+
+#ifdef PVO_MAIN
+// CLI mirroring cmd/pktvisor-reader/main.cpp:28-51 for the options the hot path
+// uses: pvo_reader [-H HOST_SPEC] [--periods N] FILE
+#include <fstream>
+#include <iterator>
+int main(int argc, char **argv)
+{
+    std::string host, file;
+    unsigned periods = 5;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        if (a == "-H" && i + 1 < argc) host = argv[++i];
+        else if (a == "--periods" && i + 1 < argc) periods = (unsigned)atoi(argv[++i]);
+        else file = a;
+    }
+    std::ifstream f(file, std::ios::binary);
+    std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    std::string cfg = "num_periods=" + std::to_string(periods) + ";window=" + std::to_string(periods);
+    if (!host.empty()) cfg += ";host_spec=" + host;
+    char *out = nullptr;
+    int rc = pvo_run(buf.data(), buf.size(), cfg.c_str(), &out);
+    printf("%s\n", out ? out : "");
+    pvo_free(out);
+    return rc ? 1 : 0;
+}
+#endif
