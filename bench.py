@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Device-resident Mpkt/s of pktvisor's Net+DNS handler path on MI355X.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--records R]
+
+One step = one pass of the fused Net v1 + DNS v1 hot path over one batch of
+synthetic pcap records already resident in HBM: bucket reset, the parse kernel
+(pv_net_dns_kernel), DNS transaction pairing when the batch has DNS, the status
+read-back, and - for N > 1 - the RCCL all-reduce of the live buckets over xGMI.
+Each rank processes its own shard of R records (weak scaling). Rank 0 prints
+one JSON line. The default workload is BASELINE.json configs[1] (C2: 10M x 64 B
+UDP, host_spec 10.0.0.0/8) with both handlers attached, the config the
+north-star roofline target is quoted on.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+WORKLOADS = {
+    2: "C2: Net+DNS handlers, 64 B UDP (Eth+IPv4+UDP+22 B), Zipf IPs, host_spec 10.0.0.0/8",
+    3: "C3: Net+DNS handlers, UDP/53 queries, single label L~U[51,63] + EDNS0, mean 128 B",
+    4: "C4: Net+DNS handlers, IMIX 70% {64,576,1500} + 30% DNS query/response pairs",
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
+    ap.add_argument("--records", type=int, default=10_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    import pktvisor_amd as pa
+    from pktvisor_amd import dist as pvdist
+    from pktvisor_amd import synth
+
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    # ---- synthetic shard for this rank, then resident in HBM
+    n = args.records
+    seed = synth.SEEDS[args.config] + 7919 * rank
+    buf, offs, used = synth.records(args.config, n, seed=seed, with_offsets=False)
+    idx = pa.RecordIndex(buf[:used], max_records=n)
+    assert idx.n == n
+    d_recs = torch.from_numpy(buf).to(device)  # includes 256 B zero padding
+    d_offs = torch.from_numpy(idx.offsets).to(device)
+    torch.cuda.synchronize(device)
+    algo_bytes = used  # sum over records of (16 + caplen)
+
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=n, device=local)
+    h.set_global_base(rank * n)
+
+    def step():
+        h.reset()
+        h.process_device(d_recs.data_ptr(), d_offs.data_ptr(), idx)
+        if world > 1:
+            pvdist.reduce_handlers(h, device)
+        else:
+            h.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    h.kernel_timing(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    h.synchronize()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kms, launches = h.kernel_timing()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed, kms / max(launches, 1)], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+    else:
+        kernel_ms = kms / max(launches, 1)
+
+    # parity sanity on the final state (not timed)
+    out = h.window_json(0, merged=False)
+    events = out["packets"]["events"]
+    if events != n * world:
+        raise SystemExit(f"bench: bucket holds {events} events, expected {n * world}")
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = n * world * args.steps / elapsed / 1e6
+        achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
+        line = {
+            "metric": "Mpkt/s device-resident (Net+DNS handler parse)",
+            "value": round(value, 2),
+            "unit": "Mpkt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": WORKLOADS[args.config], "records_per_gpu": n,
+                       "bytes_per_record": round(algo_bytes / n, 2), "handlers": "net v1 + dns v1 (default groups)",
+                       "parallelism": f"dp{world} (contiguous record shards, RCCL all-reduce of live buckets)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profile(args.config, n),
+                         "kernel": "pv_net_dns_kernel", "kernel_ms": round(kernel_ms, 4),
+                         "bytes_per_launch": algo_bytes},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    h.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def traffic_from_profile(cfg: int, n: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 +
+    WRITE_SIZE, MI355X_MICROARCH.md HBM section), if one exists for this workload."""
+    p = os.path.join(ROOT, "profiles", f"pmc_c{cfg}_{n}.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p))["hbm_bytes_per_launch"]
+        except Exception:
+            return None
+    return None
+
+
+def cpu_baseline(cfg: int, seconds: float):
+    """The oracle (single-threaded CPU restatement of the reference handlers) on a
+    bounded sample of the same workload, timed on this host."""
+    from pktvisor_amd import synth
+    from tests.oracle_ctypes import load
+    orc = load()
+    cfgs = dict(host_spec=synth.HOST_SPEC, num_periods=5, window=5)
+    probe_n = 100_000
+    pcap = synth.pcap_bytes(cfg, probe_n)
+    t0 = time.perf_counter()
+    orc.run_bytes(pcap, **cfgs)
+    rate = probe_n / (time.perf_counter() - t0)
+    n = int(min(10_000_000, max(probe_n, rate * seconds)))
+    pcap = synth.pcap_bytes(cfg, n)
+    t0 = time.perf_counter()
+    orc.run_bytes(pcap, **cfgs)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+            "sample": f"{n} records of the same synthetic workload, in-memory pcap, oracle/pv_oracle.cpp single thread, {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+/* SPDX-License-Identifier: MPL-2.0
+ *
+ * pvgpu.h — C-ABI of the MI355X-native Net+DNS per-packet path.
+ *
+ * This is the drop-in boundary a pktvisor build binds to (see INTEGRATION.md for
+ * the StreamHandler / InputStream shim). Plain pointers and sizes only; no
+ * exceptions cross it; every call returns 0 on success or a negative pv_status,
+ * and pv_last_error() returns the message of the last failure on a context.
+ *
+ * Mapping to the reference (/root/reference):
+ *   pv_create / pv_destroy ........ NetStreamHandler / DnsStreamHandler ctor+start()/stop()
+ *                                   (src/handlers/net/v1/NetStreamHandler.cpp:31-130,
+ *                                    src/handlers/dns/v1/DnsStreamHandler.cpp:30-232) and
+ *                                   the window config of AbstractMetricsManager
+ *                                   (src/AbstractMetricsManager.h:351-389)
+ *   pv_index_records .............. the record walk of PcapInputStream::_open_pcap
+ *                                   (src/inputs/pcap/PcapInputStream.cpp:471-527)
+ *   pv_process_host /
+ *   pv_process_device ............. per-record dispatch PcapInputStream::process_raw_packet
+ *                                   (PcapInputStream.cpp:380-428) into
+ *                                   NetStreamHandler::process_packet_cb (net/v1 ...cpp:161-169)
+ *                                   and DnsStreamHandler::process_udp_packet_cb
+ *                                   (dns/v1 ...cpp:270-302), for a whole block of records
+ *   pv_set_start_tstamp /
+ *   pv_set_end_tstamp ............. start_tstamp_signal / end_tstamp_signal
+ *                                   (PcapInputStream.cpp:494-500,514-517;
+ *                                    AbstractMetricsManager.h:423-437)
+ *   pv_window_json ................ StreamHandler::window_json(j, period, merged)
+ *                                   (src/StreamHandler.h:71-77, AbstractMetricsManager.h:480-504,601-647)
+ *   pv_state_* / pv_reduce_* ...... the bucket merge (AbstractMetricsBucket::merge,
+ *                                   AbstractMetricsManager.h:177-195) split into
+ *                                   collective-friendly regions for a multi-GPU reduce
+ */
+#ifndef PVGPU_H
+#define PVGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pv_ctx pv_ctx;
+
+enum pv_status {
+    PV_OK = 0,
+    PV_EINVAL = -1,    /* bad argument / config (message in pv_last_error) */
+    PV_EHIP = -2,      /* HIP runtime failure */
+    PV_ECAPACITY = -3, /* a device table overflowed its configured capacity */
+    PV_EUNSUPPORTED = -4,
+    PV_ENODEV = -5     /* no HIP device / extension not usable */
+};
+
+/* Metric groups (names as the reference's _group_defs). */
+enum pv_net_group { PV_NET_COUNTERS = 1u << 0, PV_NET_CARDINALITY = 1u << 1, PV_NET_TOP_GEO = 1u << 2, PV_NET_TOP_IPS = 1u << 3 };
+enum pv_dns_group {
+    PV_DNS_CARDINALITY = 1u << 0, PV_DNS_COUNTERS = 1u << 1, PV_DNS_QUANTILES = 1u << 2, PV_DNS_HISTOGRAMS = 1u << 3,
+    PV_DNS_TRANSACTIONS = 1u << 4, PV_DNS_TOP_ECS = 1u << 5, PV_DNS_TOP_QNAMES = 1u << 6,
+    PV_DNS_TOP_QNAMES_DETAILS = 1u << 7, PV_DNS_TOP_PORTS = 1u << 8
+};
+#define PV_NET_DEFAULT_GROUPS (PV_NET_COUNTERS | PV_NET_CARDINALITY | PV_NET_TOP_GEO | PV_NET_TOP_IPS)
+#define PV_DNS_DEFAULT_GROUPS (PV_DNS_CARDINALITY | PV_DNS_COUNTERS | PV_DNS_QUANTILES | PV_DNS_TRANSACTIONS | \
+                               PV_DNS_TOP_QNAMES | PV_DNS_TOP_PORTS)
+
+typedef struct pv_config {
+    const char *host_spec;   /* comma-separated CIDRs, PcapInputStream "host_spec" (may be NULL) */
+    uint32_t num_periods;    /* window history 1..10 ("num_periods", default 5) */
+    uint32_t topn_count;     /* "topn_count", default 10 */
+    uint32_t xact_ttl_ms;    /* "xact_ttl_ms", default 5000 */
+    uint32_t net_groups;     /* pv_net_group bits; 0 => defaults */
+    uint32_t dns_groups;     /* pv_dns_group bits; 0 => defaults */
+    uint32_t linktype;       /* pcap linktype of the records (1 = Ethernet) */
+    uint32_t ts_nano;        /* 1 if record timestamps are ns (magic a1b23c4d) */
+    int32_t device;          /* HIP device ordinal, -1 => current */
+    uint32_t table_log2;     /* log2 slots of each per-period top-N table, 0 => 22 */
+    uint64_t max_records;    /* largest batch that will be submitted (sizes scratch) */
+} pv_config;
+
+/* Result of one host-side walk over a run of classic-pcap records. */
+typedef struct pv_index_info {
+    uint64_t n_records;      /* records indexed */
+    uint64_t bytes_used;     /* bytes of whole records consumed */
+    int64_t first_sec, first_nsec, last_sec, last_nsec;
+    uint32_t monotone;       /* 1 if ts_sec never decreases inside the run */
+    uint32_t n_sec_changes;  /* entries written to sec_change_* */
+} pv_index_info;
+
+const char *pv_version(void);
+int pv_device_count(int *count);
+
+int pv_create(const pv_config *cfg, pv_ctx **out);
+void pv_destroy(pv_ctx *ctx);
+const char *pv_last_error(const pv_ctx *ctx);
+
+/* Walk records [recs, recs+bytes): per-record byte offsets (relative to recs)
+ * into offsets[max_records], and the points where ts_sec changes into
+ * sec_change_idx/sec_change_sec[max_changes] (index of the first record with
+ * that second). Pure host function; no context needed. */
+int pv_index_records(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32_t *offsets, uint64_t max_records,
+                     uint32_t *sec_change_idx, uint32_t *sec_change_sec, uint32_t max_changes, pv_index_info *info);
+
+/* Process a block of records already resident in device memory. d_recs must be
+ * readable for 64 bytes past the last record (padding). `stream` is a
+ * hipStream_t (NULL = the context's own stream). Returns after enqueueing, except
+ * where a period boundary needs host validation (then it synchronises). */
+int pv_process_device(pv_ctx *ctx, const uint8_t *d_recs, const uint32_t *d_offsets, const pv_index_info *info,
+                      const uint32_t *sec_change_idx, const uint32_t *sec_change_sec, void *stream);
+
+/* Process records in host memory: index, H2D (pinned staging), kernels. */
+int pv_process_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes);
+
+int pv_set_start_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);
+int pv_set_end_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);
+int pv_synchronize(pv_ctx *ctx);
+/* Clear every bucket and all transaction state (a fresh handler). */
+int pv_reset(pv_ctx *ctx);
+
+/* JSON for schema keys "packets" and "dns": {"packets":{...},"dns":{...}}.
+ * merged == 0: bucket `period` (0 = live); merged != 0: merge the `period` most
+ * recent buckets (window_merged_json). *out is malloc'd; free with pv_free. */
+int pv_window_json(pv_ctx *ctx, uint32_t period, int merged, char **out);
+void pv_free(void *p);
+
+/* Device-state regions of the live window, for a multi-GPU reduce:
+ *   SUM region: uint64 counters and dense tables (all-reduce SUM)
+ *   MIN region: int64 CPC first-occurrence global record indices (all-reduce MIN)
+ * Global record index = pv_set_global_base() + records processed before; ranks
+ * that process contiguous shards set their shard's first global record index. */
+int pv_state_regions(pv_ctx *ctx, void **sum_ptr, size_t *sum_bytes, void **min_ptr, size_t *min_bytes);
+int pv_set_global_base(pv_ctx *ctx, uint64_t base);
+/* Bucket slots of the Net and DNS windows (front = live) and the per-slot sizes
+ * of the SUM (uint64) and MIN (int64) regions, so a reduce can touch only them. */
+int pv_window_slots(pv_ctx *ctx, uint32_t *slots, uint32_t max_slots, uint32_t *n_slots, size_t *sum_slot_words,
+                    size_t *min_slot_words);
+/* Compact the top-N tables of all live buckets into a host buffer of
+ * (slot, metric, key, count, name) records (see pvgpu_topn_rec) for exchange;
+ * pv_merge_topn adds such records from another rank into this context's view. */
+int pv_export_topn(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
+int pv_merge_topn(pv_ctx *ctx, const uint8_t *buf, size_t bytes);
+
+/* Device time of the fused parse kernel (pv_net_dns_kernel), from HIP events
+ * recorded on the launch stream around every launch since the last reset:
+ * total milliseconds and number of launches. */
+int pv_kernel_timing(pv_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PVGPU_H */

@@ -272,7 +272,7 @@ struct J {
         for (unsigned char c : v) {
             if (c == '"') s += "\\\"";
             else if (c == '\\') s += "\\\\";
-            else if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); s += b; }
+            else if (c < 0x20 || c >= 0x80) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); s += b; } // bytes >= 0x80 as U+0080..U+00FF
             else s += (char)c;
         }
         s += '"';

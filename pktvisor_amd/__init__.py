@@ -1,0 +1,265 @@
+"""pktvisor_amd — MI355X-native Net v1 + DNS v1 per-packet path of pktvisor.
+
+Python mirror of the reference's handler surface over the C-ABI in
+include/pvgpu.h (libpvgpu.so, built in-tree by pktvisor_amd/Makefile):
+
+  * ``PvHandlers`` ~ a NetStreamHandler + DnsStreamHandler pair attached to one
+    PcapInputStream (src/handlers/net/v1/NetStreamHandler.cpp:31-130,
+    src/handlers/dns/v1/DnsStreamHandler.cpp:30-232), with ``window_json``
+    (src/StreamHandler.h:71-77) and the window config keys of
+    AbstractMetricsManager (src/AbstractMetricsManager.h:351-389).
+  * ``read_pcap`` / ``index_records`` ~ PcapInputStream::_open_pcap's record walk
+    (src/inputs/pcap/PcapInputStream.cpp:471-527).
+  * ``pktvisor_reader`` ~ cmd/pktvisor-reader/main.cpp:86-258 for net + dns.
+
+There is no CPU fallback: if the HIP library cannot be loaded or no GPU is
+present, constructing a handler raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import struct
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpvgpu.so")
+
+PV_NET_COUNTERS, PV_NET_CARDINALITY, PV_NET_TOP_GEO, PV_NET_TOP_IPS = 1, 2, 4, 8
+DNS_GROUPS = {"cardinality": 1 << 0, "counters": 1 << 1, "quantiles": 1 << 2, "histograms": 1 << 3,
+              "dns_transaction": 1 << 4, "top_ecs": 1 << 5, "top_qnames": 1 << 6, "top_qnames_details": 1 << 7,
+              "top_ports": 1 << 8}
+NET_GROUPS = {"counters": 1, "cardinality": 2, "top_geo": 4, "top_ips": 8}
+DNS_DEFAULT = sum(DNS_GROUPS[g] for g in ("cardinality", "counters", "quantiles", "dns_transaction", "top_qnames",
+                                          "top_ports"))
+NET_DEFAULT = 15
+
+
+class PvError(RuntimeError):
+    pass
+
+
+class pv_config(ctypes.Structure):
+    _fields_ = [("host_spec", ctypes.c_char_p), ("num_periods", ctypes.c_uint32), ("topn_count", ctypes.c_uint32),
+                ("xact_ttl_ms", ctypes.c_uint32), ("net_groups", ctypes.c_uint32), ("dns_groups", ctypes.c_uint32),
+                ("linktype", ctypes.c_uint32), ("ts_nano", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("table_log2", ctypes.c_uint32), ("max_records", ctypes.c_uint64)]
+
+
+class pv_index_info(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint64), ("bytes_used", ctypes.c_uint64), ("first_sec", ctypes.c_int64),
+                ("first_nsec", ctypes.c_int64), ("last_sec", ctypes.c_int64), ("last_nsec", ctypes.c_int64),
+                ("monotone", ctypes.c_uint32), ("n_sec_changes", ctypes.c_uint32)]
+
+
+# every symbol include/pvgpu.h declares (checked by tests/test_abi.py)
+EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_error", "pv_index_records",
+           "pv_process_device", "pv_process_host", "pv_set_start_tstamp", "pv_set_end_tstamp", "pv_synchronize",
+           "pv_reset", "pv_window_json", "pv_free", "pv_state_regions", "pv_set_global_base", "pv_export_topn",
+           "pv_merge_topn", "pv_kernel_timing", "pv_window_slots"]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libpvgpu.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PvError(f"{path} missing: run `make -C pktvisor_amd` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    P, U32, U64, I64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64
+    lib.pv_version.restype = ctypes.c_char_p
+    lib.pv_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    lib.pv_create.argtypes = [ctypes.POINTER(pv_config), ctypes.POINTER(P)]
+    lib.pv_destroy.argtypes = [P]
+    lib.pv_destroy.restype = None
+    lib.pv_last_error.argtypes = [P]
+    lib.pv_last_error.restype = ctypes.c_char_p
+    lib.pv_index_records.argtypes = [P, ctypes.c_size_t, U32, P, U64, P, P, U32, ctypes.POINTER(pv_index_info)]
+    lib.pv_process_device.argtypes = [P, P, P, ctypes.POINTER(pv_index_info), P, P, P]
+    lib.pv_process_host.argtypes = [P, P, ctypes.c_size_t]
+    lib.pv_set_start_tstamp.argtypes = [P, I64, I64]
+    lib.pv_set_end_tstamp.argtypes = [P, I64, I64]
+    lib.pv_synchronize.argtypes = [P]
+    lib.pv_reset.argtypes = [P]
+    lib.pv_window_json.argtypes = [P, U32, ctypes.c_int, ctypes.POINTER(P)]
+    lib.pv_free.argtypes = [P]
+    lib.pv_free.restype = None
+    lib.pv_state_regions.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(P),
+                                     ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_set_global_base.argtypes = [P, U64]
+    lib.pv_export_topn.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_merge_topn.argtypes = [P, P, ctypes.c_size_t]
+    lib.pv_window_slots.argtypes = [P, P, U32, ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_size_t),
+                                    ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_kernel_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.c_int]
+    _lib = lib
+    return lib
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    load_library().pv_device_count(ctypes.byref(n))
+    return n.value
+
+
+def read_pcap(path: str):
+    """Classic pcap file -> (linktype, ts_nano, record bytes after the 24-byte global header)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if len(data) < 24:
+        raise PvError("Cannot open pcap/pcapng file")
+    magic = struct.unpack_from("<I", data, 0)[0]
+    if magic not in (0xA1B2C3D4, 0xA1B23C4D):
+        raise PvError("Cannot open pcap/pcapng file (only little-endian classic pcap is supported)")
+    linktype = struct.unpack_from("<I", data, 20)[0]
+    return linktype, int(magic == 0xA1B23C4D), data[24:]
+
+
+def pcap_file_bytes(records: bytes, linktype: int = 1, ts_nano: int = 0) -> bytes:
+    magic = 0xA1B23C4D if ts_nano else 0xA1B2C3D4
+    return struct.pack("<IHHiIII", magic, 2, 4, 0, 0, 262144, linktype) + records
+
+
+class RecordIndex:
+    """Host-side index of a run of pcap records (offsets + second-change points)."""
+
+    def __init__(self, recs, ts_nano: int = 0, max_records: Optional[int] = None, max_changes: int = 1 << 20):
+        lib = load_library()
+        buf = np.frombuffer(recs, dtype=np.uint8) if not isinstance(recs, np.ndarray) else recs
+        if max_records is None:
+            max_records = max(1, len(buf) // 16)
+        self.offsets = np.empty(max_records, dtype=np.uint32)
+        self.sc_idx = np.empty(max_changes, dtype=np.uint32)
+        self.sc_sec = np.empty(max_changes, dtype=np.uint32)
+        self.info = pv_index_info()
+        rc = lib.pv_index_records(buf.ctypes.data, len(buf), ts_nano, self.offsets.ctypes.data, max_records,
+                                  self.sc_idx.ctypes.data, self.sc_sec.ctypes.data, max_changes,
+                                  ctypes.byref(self.info))
+        if rc:
+            raise PvError(f"pv_index_records failed ({rc})")
+        self.offsets = self.offsets[: self.info.n_records]
+        self.n = int(self.info.n_records)
+
+
+class PvHandlers:
+    """Net v1 ("packets") + DNS v1 ("dns") handlers on one MI355X."""
+
+    def __init__(self, host_spec: Optional[str] = None, num_periods: int = 5, topn_count: int = 10,
+                 xact_ttl_ms: int = 5000, linktype: int = 1, ts_nano: int = 0, device: int = -1,
+                 table_log2: int = 0, max_records: int = 1 << 20, net_groups: int = 0, dns_groups: int = 0):
+        self.lib = load_library()
+        self._host = host_spec.encode() if host_spec else None
+        cfg = pv_config(self._host, num_periods, topn_count, xact_ttl_ms, net_groups, dns_groups, linktype, ts_nano,
+                        device, table_log2, max_records)
+        self.num_periods = num_periods
+        self.ctx = ctypes.c_void_p()
+        rc = self.lib.pv_create(ctypes.byref(cfg), ctypes.byref(self.ctx))
+        if rc:
+            msg = self.lib.pv_last_error(self.ctx).decode() if self.ctx else "pv_create"
+            self.lib.pv_destroy(self.ctx)
+            self.ctx = None
+            raise PvError(f"pv_create failed ({rc}): {msg}")
+
+    def _check(self, rc, what):
+        if rc:
+            raise PvError(f"{what} failed ({rc}): {self.lib.pv_last_error(self.ctx).decode()}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.pv_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def process_host(self, recs: bytes):
+        buf = np.frombuffer(recs, dtype=np.uint8)
+        self._check(self.lib.pv_process_host(self.ctx, buf.ctypes.data, len(buf)), "pv_process_host")
+
+    def process_device(self, d_recs: int, d_offs: int, index: RecordIndex, stream: Optional[int] = None):
+        self._check(self.lib.pv_process_device(self.ctx, d_recs, d_offs, ctypes.byref(index.info),
+                                               index.sc_idx.ctypes.data, index.sc_sec.ctypes.data, stream),
+                    "pv_process_device")
+
+    def set_end_tstamp(self, sec: int, nsec: int):
+        self._check(self.lib.pv_set_end_tstamp(self.ctx, sec, nsec), "pv_set_end_tstamp")
+
+    def set_global_base(self, base: int):
+        self._check(self.lib.pv_set_global_base(self.ctx, base), "pv_set_global_base")
+
+    def synchronize(self):
+        self._check(self.lib.pv_synchronize(self.ctx), "pv_synchronize")
+
+    def reset(self):
+        self._check(self.lib.pv_reset(self.ctx), "pv_reset")
+
+    def window_json(self, period: int = 0, merged: bool = False) -> dict:
+        out = ctypes.c_void_p()
+        self._check(self.lib.pv_window_json(self.ctx, period, 1 if merged else 0, ctypes.byref(out)),
+                    "pv_window_json")
+        txt = ctypes.string_at(out.value).decode()
+        self.lib.pv_free(out)
+        return json.loads(txt)
+
+    def state_regions(self):
+        sp, mp = ctypes.c_void_p(), ctypes.c_void_p()
+        sb, mb = ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(self.lib.pv_state_regions(self.ctx, ctypes.byref(sp), ctypes.byref(sb), ctypes.byref(mp),
+                                              ctypes.byref(mb)), "pv_state_regions")
+        return sp.value, sb.value, mp.value, mb.value
+
+    def kernel_timing(self, reset: bool = False):
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        self._check(self.lib.pv_kernel_timing(self.ctx, ctypes.byref(ms), ctypes.byref(n), int(reset)),
+                    "pv_kernel_timing")
+        return ms.value, n.value
+
+    def window_slots(self):
+        """(slot ids, SUM words per slot, MIN words per slot) of the live windows"""
+        slots = np.zeros(32, dtype=np.uint32)
+        n, sw, mw = ctypes.c_uint32(), ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(self.lib.pv_window_slots(self.ctx, slots.ctypes.data, 32, ctypes.byref(n), ctypes.byref(sw),
+                                             ctypes.byref(mw)), "pv_window_slots")
+        return [int(x) for x in slots[: n.value]], sw.value, mw.value
+
+    def export_topn(self) -> bytes:
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self.lib.pv_export_topn(self.ctx, ctypes.byref(p), ctypes.byref(n)), "pv_export_topn")
+        data = ctypes.string_at(p.value, n.value) if n.value else b""
+        self.lib.pv_free(p)
+        return data
+
+    def merge_topn(self, data: bytes):
+        buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
+        self._check(self.lib.pv_merge_topn(self.ctx, buf.ctypes.data, len(data)), "pv_merge_topn")
+
+
+def last_record_ts(recs: bytes, index: RecordIndex, ts_nano: int = 0):
+    off = int(index.offsets[-1])
+    sec, frac = struct.unpack_from("<II", recs, off)
+    return sec, (frac if ts_nano else frac * 1000)
+
+
+def pktvisor_reader(path: str, host_spec: Optional[str] = None, periods: int = 5, **kw) -> dict:
+    """GPU equivalent of `pktvisor-reader [-H host_spec] --periods N FILE` for net + dns."""
+    linktype, ts_nano, recs = read_pcap(path)
+    idx = RecordIndex(recs, ts_nano)
+    h = PvHandlers(host_spec=host_spec, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
+                   max_records=max(1, idx.n), **kw)
+    try:
+        h.process_host(recs)
+        if idx.n:
+            h.set_end_tstamp(*last_record_ts(recs, idx, ts_nano))
+        key = f"{1 if periods == 1 else periods}m"
+        return {key: h.window_json(0 if periods == 1 else periods, merged=periods != 1)}
+    finally:
+        h.close()

@@ -1,0 +1,1207 @@
+// SPDX-License-Identifier: MPL-2.0
+//
+// pv_host.cpp — host runtime behind include/pvgpu.h.
+//
+// Owns the device state of one Net v1 + DNS v1 handler pair on one GPU:
+// bucket slots (ring of PV_SLOTS), the window of the last num_periods buckets,
+// period-shift bookkeeping (AbstractMetricsManager::new_event/_period_shift,
+// src/AbstractMetricsManager.h:276-333), the transaction pairing pass, and the
+// finalisation of device buckets into the reference's JSON shape
+// (NetworkMetricsBucket::to_json net/v1 ...cpp:447-505, DnsMetricsBucket::to_json
+// dns/v1 ...cpp:735-836, window_merged_json AbstractMetricsManager.h:601-647).
+//
+// Sketch outputs: counters and dense tables are exact; top-N estimates are
+// exact counts (inside the FI sketch's stated error bound, which allows
+// [true, true + 3.5/2^13 * N]); quantiles are exact under the KLL rank rule
+// (identical to KLL while n <= 200, within its rank error beyond); CPC is the
+// reference estimator replayed exactly from per-coupon first-occurrence indices
+// (HIP for a single bucket, ICON after a union), bit-identical to datasketches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <arpa/inet.h>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pvgpu.h"
+#include "pv_layout.h"
+
+extern "C" __global__ void pv_net_dns_kernel(PvParams P);
+extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
+extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
+extern "C" __global__ void pv_xact_keys(const PvXEvent *ev, uint32_t n, uint64_t *skeys, uint32_t *svals);
+extern "C" __global__ void pv_xact_resolve(PvXactParams X);
+extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
+                                          uint32_t *vout, size_t n, hipStream_t s);
+
+namespace {
+
+// status words (device): flags, n_events, n_resp, n_vals, dns_any[8], dns_at_thresh[8]
+enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_DNS_ANY = 4, ST_DNS_AT = 12, ST_WORDS = 20 };
+
+struct SlotMeta {
+    int64_t start_sec = 0, start_nsec = 0, end_sec = 0, end_nsec = 0;
+    bool read_only = false;
+    uint64_t period_length = 0;
+    int64_t rel_base = 0;
+    void set_read_only(int64_t s, int64_t ns)
+    {
+        end_sec = s; end_nsec = ns;
+        period_length = (uint64_t)(end_sec - start_sec);
+        read_only = true;
+    }
+};
+
+struct Window {
+    std::deque<uint32_t> slots; // front = live bucket
+    int64_t next_shift_sec = 0;
+};
+
+// ICON polynomial for lg_k = 11 (3rd/datasketches/cpc/include/icon_estimator.hpp:98-102)
+const double ICON11[20] = {
+    0.9999186020796150265, 0.3333249054574359826, 0.126791713589799987, -0.06662487271699729652,
+    -0.07335552427910230211, 0.3316370184815959909, -1.434143797561290068, 4.180260309967409604,
+    -8.593906870708760692, 12.95088874800289958, -14.56876092520539956, 12.37074367531410068,
+    -7.969152075707960137, 3.888774396648960074, -1.424923326506990051, 0.385084561785229984,
+    -0.07435541911616409816, 0.009695363567476529554, -0.0007644375960047160388, 2.75156194717188011e-05};
+
+double icon11(uint32_t c)
+{
+    if (c < 2) return c == 0 ? 0.0 : 1.0;
+    const double k = 2048.0, dc = (double)c;
+    if (dc > 5.7 * k) return 0.7940236163830469 * k * pow(2.0, dc / k);
+    const double x = dc / (2.0 * k);
+    double t = ICON11[19];
+    for (int j = 18; j >= 0; j--) t = t * x + ICON11[j];
+    const double r = dc / k;
+    const double res = dc * t * (1.0 + r * r * r / 66.774757);
+    return res >= dc ? res : dc;
+}
+
+// HIP estimate replayed from coupons in first-occurrence order, with the
+// sparse->windowed promotion and the kxp refresh of every 8th window move
+// (cpc_sketch_impl.hpp:196-380).
+double cpc_hip(std::vector<std::pair<int64_t, uint32_t>> &firsts)
+{
+    std::sort(firsts.begin(), firsts.end());
+    std::vector<uint64_t> rows(2048, 0);
+    static double kxp_byte[256];
+    static bool init = false;
+    if (!init) {
+        for (int b = 0; b < 256; b++) {
+            double s = 0;
+            for (int c = 0; c < 8; c++) if (!((b >> c) & 1)) s += ldexp(1.0, -(c + 1));
+            kxp_byte[b] = s;
+        }
+        init = true;
+    }
+    double kxp = 2048.0, hip = 0;
+    uint32_t C = 0;
+    int w = 0;
+    bool windowed = false;
+    for (auto &f : firsts) {
+        uint32_t row = f.second >> 6, col = f.second & 63;
+        rows[row] |= 1ull << col;
+        C++;
+        hip += 2048.0 / kxp;
+        kxp -= ldexp(1.0, -(int)(col + 1));
+        if (!windowed) {
+            if (((uint64_t)C << 5) >= 3ull * 2048) windowed = true;
+        } else if (((uint64_t)C << 3) >= (27ull + ((uint64_t)w << 3)) * 2048) {
+            w++;
+            if ((w & 7) == 0) {
+                double bs[8] = {0};
+                for (int i = 0; i < 2048; i++) {
+                    uint64_t word = rows[i];
+                    for (int j = 0; j < 8; j++) { bs[j] += kxp_byte[word & 0xff]; word >>= 8; }
+                }
+                double tot = 0;
+                for (int j = 7; j >= 0; j--) tot += ldexp(1.0, -8 * j) * bs[j];
+                kxp = tot;
+            }
+        }
+    }
+    return hip;
+}
+
+// libs/visor_dns/dns.h:31-265 name tables (IANA registry values, reference spellings)
+const std::map<uint16_t, const char *> &qtype_names()
+{
+    static const std::map<uint16_t, const char *> m = {
+        {0, "Reserved (0)"}, {1, "A"}, {2, "NS"}, {3, "MD"}, {4, "MF"}, {5, "CNAME"}, {6, "SOA"}, {7, "MB"},
+        {8, "MG"}, {9, "MR"}, {10, "NULL"}, {11, "WKS"}, {12, "PTR"}, {13, "HINFO"}, {14, "MINFO"}, {15, "MX"},
+        {16, "TXT"}, {17, "RP"}, {18, "AFSDB"}, {19, "X25"}, {20, "ISDN"}, {21, "RT"}, {22, "NSAP"},
+        {23, "NSAP-PTR"}, {24, "SIG"}, {25, "KEY"}, {26, "PX"}, {27, "GPOS"}, {28, "AAAA"}, {29, "LOC"},
+        {30, "NXT"}, {31, "EID"}, {32, "NIMLOC"}, {33, "SRV"}, {34, "ATMA"}, {35, "NAPTR"}, {36, "KX"},
+        {37, "CERT"}, {38, "A6"}, {39, "DNAME"}, {40, "SINK"}, {41, "OPT"}, {42, "APL"}, {43, "DS"},
+        {44, "SSHFP"}, {45, "IPSECKEY"}, {46, "RRSIG"}, {47, "NSEC"}, {48, "DNSKEY"}, {49, "DHCID"},
+        {50, "NSEC3"}, {51, "NSEC3PARAM"}, {52, "TLSA"}, {53, "SMIMEA"}, {55, "HIP"}, {56, "NINFO"},
+        {57, "RKEY"}, {58, "TALINK"}, {59, "CDS"}, {60, "CDNSKEY"}, {61, "OPENPGPKEY"}, {62, "CSYNC"},
+        {63, "ZONEMD"}, {64, "SVCB"}, {65, "HTTPS"}, {99, "SPF"}, {100, "UINFO"}, {101, "UID"}, {102, "GID"},
+        {103, "UNSPEC"}, {104, "NID"}, {105, "L32"}, {106, "L64"}, {107, "LP"}, {108, "EUI48"}, {109, "EUI64"},
+        {249, "TKEY"}, {250, "TSIG"}, {251, "IXFR"}, {252, "AXFR"}, {253, "MAILB"}, {254, "MAILA"}, {255, "*"},
+        {256, "URI"}, {257, "CAA"}, {258, "AVC"}, {259, "DOA"}, {260, "AMTRELAY"}, {32768, "TA"}, {32769, "DLV"},
+        {65535, "Reserved (65535)"}};
+    return m;
+}
+const std::map<uint16_t, const char *> &rcode_names()
+{
+    static const std::map<uint16_t, const char *> m = {
+        {0, "NOERROR"}, {1, "FORMERR"}, {2, "SRVFAIL"}, {3, "NXDOMAIN"}, {4, "NOTIMP"}, {5, "REFUSED"},
+        {6, "YXDOMAIN"}, {7, "YXRRSET"}, {8, "NXRRSET"}, {9, "NOTAUTH"}, {10, "NOTZONE"}, {11, "DSOTYPENI"},
+        {16, "BADVERS"}, {17, "BADKEY"}, {18, "BADTIME"}, {19, "BADMODE"}, {20, "BADNAME"}, {21, "BADALG"},
+        {22, "BADTRUNC"}, {23, "BADCOOKIE"}};
+    return m;
+}
+
+// ---------------------------------------------------------------- JSON writer
+struct Json {
+    std::string s;
+    std::vector<int> n{0};
+    bool after_key = false;
+    void sep()
+    {
+        if (after_key) { after_key = false; return; }
+        if (n.back()++) s += ',';
+    }
+    void esc(const std::string &v)
+    {
+        s += '"';
+        for (unsigned char c : v) {
+            if (c == '"') s += "\\\"";
+            else if (c == '\\') s += "\\\\";
+            else if (c < 0x20 || c >= 0x80) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); s += b; } // bytes >= 0x80 as U+0080..U+00FF
+            else s += (char)c;
+        }
+        s += '"';
+    }
+    Json &key(const std::string &k) { sep(); esc(k); s += ':'; after_key = true; return *this; }
+    void str(const std::string &v) { sep(); esc(v); }
+    void u(uint64_t v) { sep(); s += std::to_string(v); }
+    void i(int64_t v) { sep(); s += std::to_string(v); }
+    void d(double v)
+    {
+        sep();
+        char b[40];
+        snprintf(b, sizeof b, "%.17g", v);
+        s += b;
+        if (!strpbrk(b, ".eEn")) s += ".0";
+    }
+    void obj() { sep(); s += '{'; n.push_back(0); }
+    void end_obj() { s += '}'; n.pop_back(); }
+    void arr() { sep(); s += '['; n.push_back(0); }
+    void end_arr() { s += ']'; n.pop_back(); }
+};
+
+inline bool hip_ok(hipError_t e) { return e == hipSuccess; }
+
+} // namespace
+
+// ---------------------------------------------------------------- context
+struct pv_ctx {
+    pv_config cfg{};
+    std::string err;
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    PvSubnets nets{};
+    uint32_t ttl_s = 0, ttl_ms = 0;
+    uint32_t net_groups = PV_NET_DEFAULT_GROUPS, dns_groups = PV_DNS_DEFAULT_GROUPS;
+    // device state
+    uint64_t *d_sum = nullptr;
+    int64_t *d_cpc = nullptr;
+    uint64_t *d_tkeys = nullptr, *d_tcnt = nullptr;
+    uint32_t *d_taux = nullptr;
+    uint8_t *d_arena = nullptr;
+    uint64_t *d_arena_top = nullptr;
+    uint64_t arena_cap = 64ull << 20;
+    uint32_t tcap_log2 = 22;
+    PvXEvent *d_events = nullptr;
+    uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
+    uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
+    void *d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    PvXValue *d_xvals = nullptr;
+    uint32_t *d_status = nullptr;
+    uint64_t max_records = 0;
+    // host-path staging
+    uint8_t *d_recs = nullptr;
+    uint32_t *d_offs = nullptr;
+    size_t recs_cap = 0;
+    // window state
+    SlotMeta meta[PV_SLOTS];
+    bool slot_used[PV_SLOTS] = {false};
+    Window net, dns;
+    bool started = false, ended = false;
+    int64_t last_sec = 0, last_nsec = 0;
+    uint64_t global_base = 0, records_seen = 0;
+    // host copies of transaction values, per slot/kind
+    std::vector<PvXValue> xvals_host;
+    // merged top-N records from other ranks: slot -> key -> (count, name)
+    std::map<uint32_t, std::map<uint64_t, std::pair<uint64_t, std::string>>> remote_topn;
+    // kernel timing (pv_kernel_timing)
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    double kernel_ms = 0;
+    uint64_t kernel_launches = 0;
+
+    int fail(int code, const char *fmt, ...)
+    {
+        char b[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(b, sizeof b, fmt, ap);
+        va_end(ap);
+        err = b;
+        return code;
+    }
+    int hipfail(hipError_t e, const char *what)
+    {
+        return fail(PV_EHIP, "%s: %s", what, hipGetErrorString(e));
+    }
+};
+
+namespace {
+
+int parse_host_spec(pv_ctx *c, const char *spec)
+{
+    if (!spec) return 0;
+    std::string s = spec;
+    size_t pos = 0;
+    while (pos < s.size()) {
+        size_t e = s.find(',', pos);
+        std::string host = s.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
+        pos = e == std::string::npos ? s.size() : e + 1;
+        if (host.empty()) continue;
+        // libs/visor_utils/utils.cpp:128-164 (same error strings)
+        size_t d = host.find('/');
+        if (d == std::string::npos) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+        std::string ip = host.substr(0, d), cs = host.substr(d + 1);
+        if (cs.empty() || !std::all_of(cs.begin(), cs.end(), ::isdigit)) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+        int cidr = atoi(cs.c_str());
+        if (ip.find(':') != std::string::npos) {
+            if (cidr < 0 || cidr > 128) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+            if (c->nets.n6 >= PV_MAX_SUBNETS) return c->fail(PV_EINVAL, "too many host subnets");
+            uint8_t a[16];
+            if (inet_pton(AF_INET6, ip.c_str(), a) != 1) return c->fail(PV_EINVAL, "invalid IPv6 address: %s", ip.c_str());
+            memcpy(c->nets.v6_addr[c->nets.n6], a, 16);
+            c->nets.v6_cidr[c->nets.n6++] = (uint32_t)cidr;
+        } else {
+            if (cidr < 0 || cidr > 32) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+            if (c->nets.n4 >= PV_MAX_SUBNETS) return c->fail(PV_EINVAL, "too many host subnets");
+            in_addr a;
+            if (inet_pton(AF_INET, ip.c_str(), &a) != 1) return c->fail(PV_EINVAL, "invalid IPv4 address: %s", ip.c_str());
+            uint32_t i = c->nets.n4++;
+            c->nets.v4_addr[i] = a.s_addr;
+            c->nets.v4_all[i] = cidr == 0;
+            c->nets.v4_mask[i] = cidr == 0 ? 0 : htonl(0xFFFFFFFFu << (32 - cidr));
+        }
+    }
+    return 0;
+}
+
+int launch_fill64(pv_ctx *c, uint64_t *p, uint64_t n, uint64_t v)
+{
+    if (!n) return 0;
+    uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(pv_fill_u64, dim3(blocks), dim3(256), 0, c->stream, p, n, v);
+    return 0;
+}
+int launch_fill32(pv_ctx *c, uint32_t *p, uint64_t n, uint32_t v)
+{
+    if (!n) return 0;
+    uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(pv_fill_u32, dim3(blocks), dim3(256), 0, c->stream, p, n, v);
+    return 0;
+}
+
+// clear one bucket slot on the device (enqueued on the context stream)
+void clear_slot(pv_ctx *c, uint32_t s, int64_t rel_base)
+{
+    uint64_t tcap = 1ull << c->tcap_log2;
+    launch_fill64(c, c->d_sum + (uint64_t)s * PV_SUM_WORDS, PV_SUM_WORDS, 0);
+    launch_fill64(c, (uint64_t *)c->d_cpc + (uint64_t)s * PV_MIN_WORDS, PV_MIN_WORDS, (uint64_t)PV_CPC_EMPTY);
+    launch_fill64(c, c->d_tkeys + s * tcap, tcap, 0);
+    launch_fill64(c, c->d_tcnt + s * tcap, tcap, 0);
+    launch_fill32(c, c->d_taux + s * tcap, tcap, 0);
+    launch_fill64(c, c->d_arena_top + s, 1, 0);
+    c->meta[s] = SlotMeta();
+    c->meta[s].rel_base = rel_base;
+    c->slot_used[s] = true;
+    // drop host-side values of a recycled slot
+    c->xvals_host.erase(std::remove_if(c->xvals_host.begin(), c->xvals_host.end(), [s](const PvXValue &v) { return v.slot == s; }),
+                        c->xvals_host.end());
+    c->remote_topn.erase(s);
+}
+
+uint32_t alloc_slot(pv_ctx *c)
+{
+    // a slot not referenced by either window
+    for (uint32_t s = 0; s < PV_SLOTS; s++) {
+        bool used = false;
+        for (auto x : c->net.slots) used |= x == s;
+        for (auto x : c->dns.slots) used |= x == s;
+        if (!used) return s;
+    }
+    return 0xffffffffu;
+}
+
+int ensure_started(pv_ctx *c, int64_t sec, int64_t nsec)
+{
+    if (c->started) return 0;
+    // set_start_tstamp on both managers (AbstractMetricsManager.h:423-431)
+    uint32_t s = alloc_slot(c);
+    clear_slot(c, s, (int64_t)c->global_base);
+    c->meta[s].start_sec = sec;
+    c->meta[s].start_nsec = nsec;
+    c->net.slots.assign(1, s);
+    c->dns.slots.assign(1, s);
+    c->net.next_shift_sec = sec + 60;
+    c->dns.next_shift_sec = sec + 60;
+    c->started = true;
+    return 0;
+}
+
+// Device-side top-N records of one slot: (key, count, name)
+struct TopRec {
+    uint64_t key;
+    uint64_t count;
+    std::string name;
+};
+
+int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out)
+{
+    uint64_t tcap = 1ull << c->tcap_log2;
+    std::vector<uint64_t> keys(tcap), cnt(tcap);
+    std::vector<uint32_t> aux(tcap);
+    uint64_t top = 0;
+    hipError_t e;
+    if (!hip_ok(e = hipMemcpyAsync(keys.data(), c->d_tkeys + s * tcap, tcap * 8, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipMemcpyAsync(cnt.data(), c->d_tcnt + s * tcap, tcap * 8, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipMemcpyAsync(aux.data(), c->d_taux + s * tcap, tcap * 4, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipMemcpyAsync(&top, c->d_arena_top + s, 8, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "read top-N table");
+    top = std::min<uint64_t>(top, c->arena_cap);
+    std::vector<uint8_t> arena(top);
+    if (top && (!hip_ok(e = hipMemcpy(arena.data(), c->d_arena + s * c->arena_cap, top, hipMemcpyDeviceToHost))))
+        return c->hipfail(e, "read name arena");
+    for (uint64_t i = 0; i < tcap; i++) {
+        if (!keys[i]) continue;
+        TopRec r{keys[i], cnt[i], std::string()};
+        uint32_t m = PV_KEY_METRIC(keys[i]);
+        if (m == TM_IPV4) {
+            uint32_t ip = (uint32_t)keys[i];
+            char b[20];
+            snprintf(b, sizeof b, "%u.%u.%u.%u", ip & 0xff, (ip >> 8) & 0xff, (ip >> 16) & 0xff, ip >> 24);
+            r.name = b;
+        } else if (aux[i] && aux[i] - 1 + 2 <= top) {
+            uint64_t p = aux[i] - 1;
+            uint32_t len = arena[p] | (arena[p + 1] << 8);
+            if (p + 2 + len <= top) {
+                if (m == TM_IPV6) {
+                    char b[64];
+                    inet_ntop(AF_INET6, &arena[p + 2], b, sizeof b);
+                    r.name = b;
+                } else {
+                    r.name.assign((const char *)&arena[p + 2], len);
+                }
+            }
+        }
+        out.push_back(std::move(r));
+    }
+    auto it = c->remote_topn.find(s);
+    if (it != c->remote_topn.end())
+        for (auto &kv : it->second) out.push_back(TopRec{kv.first, kv.second.first, kv.second.second});
+    return 0;
+}
+
+// A finalised bucket (possibly the merge of several slots) on the host.
+struct HostBucket {
+    int64_t start_sec = 0;
+    uint64_t period_length = 0;
+    std::vector<uint64_t> sum;                           // PV_SUM_WORDS
+    std::vector<int64_t> cpc;                            // PV_MIN_WORDS (min-merged)
+    std::map<uint32_t, std::map<std::string, uint64_t>> tops; // metric -> name -> count
+    std::vector<uint64_t> from_us, to_us;
+    std::vector<double> ratio;
+    bool merged = false;
+};
+
+template <typename T>
+std::vector<T> quantiles(std::vector<T> v)
+{
+    std::sort(v.begin(), v.end());
+    std::vector<T> out;
+    for (double r : {0.50, 0.90, 0.95, 0.99}) {
+        uint64_t w = (uint64_t)std::ceil(r * (double)v.size());
+        size_t idx = w == 0 ? 0 : (size_t)(w - 1);
+        if (idx >= v.size()) idx = v.size() - 1;
+        out.push_back(v[idx]);
+    }
+    return out;
+}
+
+// exact quantiles of the payload-size histogram with the KLL inclusive rank rule
+std::vector<uint64_t> hist_quantiles(const uint64_t *h, size_t bins, uint64_t &n)
+{
+    n = 0;
+    for (size_t i = 0; i < bins; i++) n += h[i];
+    std::vector<uint64_t> out;
+    if (!n) return out;
+    for (double r : {0.50, 0.90, 0.95, 0.99}) {
+        uint64_t w = (uint64_t)std::ceil(r * (double)n);
+        if (w == 0) w = 1;
+        uint64_t acc = 0;
+        size_t i = 0;
+        for (; i < bins; i++) { acc += h[i]; if (acc >= w) break; }
+        out.push_back(std::min(i, bins - 1));
+    }
+    return out;
+}
+
+double cpc_estimate(const int64_t *t, bool merged)
+{
+    if (merged) {
+        uint32_t c = 0;
+        for (uint32_t i = 0; i < PV_CPC_COUPONS; i++) c += t[i] != PV_CPC_EMPTY;
+        return icon11(c);
+    }
+    std::vector<std::pair<int64_t, uint32_t>> f;
+    for (uint32_t i = 0; i < PV_CPC_COUPONS; i++)
+        if (t[i] != PV_CPC_EMPTY) f.push_back({t[i], i});
+    return cpc_hip(f);
+}
+
+int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, const Window &win, HostBucket &b)
+{
+    b.sum.assign(PV_SUM_WORDS, 0);
+    b.cpc.assign(PV_MIN_WORDS, PV_CPC_EMPTY);
+    b.merged = merged;
+    std::vector<uint64_t> sum(PV_SUM_WORDS);
+    std::vector<int64_t> cpc(PV_MIN_WORDS);
+    bool first = true;
+    for (uint32_t s : slots) {
+        hipError_t e;
+        if (!hip_ok(e = hipMemcpyAsync(sum.data(), c->d_sum + (uint64_t)s * PV_SUM_WORDS, PV_SUM_WORDS * 8, hipMemcpyDeviceToHost, c->stream)) ||
+            !hip_ok(e = hipMemcpyAsync(cpc.data(), c->d_cpc + (uint64_t)s * PV_MIN_WORDS, PV_MIN_WORDS * 8, hipMemcpyDeviceToHost, c->stream)) ||
+            !hip_ok(e = hipStreamSynchronize(c->stream)))
+            return c->hipfail(e, "read bucket");
+        for (size_t i = 0; i < PV_SUM_WORDS; i++) b.sum[i] += sum[i];
+        // CPC union: a coupon is present if present in any bucket; for a single
+        // bucket the first-occurrence order is kept for the HIP replay
+        for (size_t i = 0; i < PV_MIN_WORDS; i++) b.cpc[i] = std::min(b.cpc[i], cpc[i]);
+        const SlotMeta &m = c->meta[s];
+        b.period_length += m.read_only ? m.period_length : 0;
+        if (first || m.start_sec < b.start_sec) b.start_sec = m.start_sec;
+        first = false;
+        std::vector<TopRec> recs;
+        int rc = read_topn(c, s, recs);
+        if (rc) return rc;
+        for (auto &r : recs) b.tops[PV_KEY_METRIC(r.key)][r.name] += r.count;
+        for (auto &v : c->xvals_host) {
+            if (v.slot != s) continue;
+            if (v.kind == XV_FROM_US) b.from_us.push_back(v.bits);
+            else if (v.kind == XV_TO_US) b.to_us.push_back(v.bits);
+            else { double d; memcpy(&d, &v.bits, 8); b.ratio.push_back(d); }
+        }
+    }
+    (void)win;
+    return 0;
+}
+
+void top_json(Json &j, const char *key, const std::vector<std::pair<std::string, uint64_t>> &v0, size_t n)
+{
+    auto v = v0;
+    std::sort(v.begin(), v.end(), [](const auto &a, const auto &b) {
+        if (a.second != b.second) return a.second > b.second;
+        return a.first < b.first;
+    });
+    j.key(key);
+    j.arr();
+    for (size_t i = 0; i < std::min(n, v.size()); i++) {
+        j.obj();
+        j.key("name").str(v[i].first);
+        j.key("estimate").u(v[i].second);
+        j.end_obj();
+    }
+    j.end_arr();
+}
+std::vector<std::pair<std::string, uint64_t>> tops_of(const HostBucket &b, uint32_t metric)
+{
+    std::vector<std::pair<std::string, uint64_t>> v;
+    auto it = b.tops.find(metric);
+    if (it != b.tops.end())
+        for (auto &kv : it->second) v.push_back(kv);
+    return v;
+}
+std::vector<std::pair<std::string, uint64_t>> dense_tops(const uint64_t *t, size_t bins, int kind)
+{
+    std::vector<std::pair<std::string, uint64_t>> v;
+    for (size_t i = 0; i < bins; i++) {
+        if (!t[i]) continue;
+        std::string name;
+        if (kind == 0) name = std::to_string(i);
+        else {
+            auto &m = kind == 1 ? qtype_names() : rcode_names();
+            auto it = m.find((uint16_t)i);
+            name = it != m.end() ? it->second : std::to_string(i);
+        }
+        v.push_back({name, t[i]});
+    }
+    return v;
+}
+
+template <typename T>
+void quant_json(Json &j, const char *key, const std::vector<T> &v)
+{
+    if (v.empty()) return;
+    auto q = quantiles(v);
+    const char *names[4] = {"p50", "p90", "p95", "p99"};
+    j.key(key);
+    j.obj();
+    for (int i = 0; i < 4; i++) {
+        j.key(names[i]);
+        if constexpr (std::is_floating_point<T>::value) j.d(q[i]);
+        else j.u((uint64_t)q[i]);
+    }
+    j.end_obj();
+}
+
+void net_json(pv_ctx *c, Json &j, const HostBucket &b)
+{
+    const uint64_t *n = &b.sum[PV_OFF_NET];
+    size_t topn = c->cfg.topn_count;
+    j.key("period").obj();
+    j.key("start_ts").i(b.start_sec);
+    j.key("length").u(b.period_length);
+    j.end_obj();
+    j.key("events").u(n[NC_EVENTS]);
+    j.key("deep_samples").u(n[NC_SAMPLES]);
+    if (c->net_groups & PV_NET_COUNTERS) {
+        j.key("udp").u(n[NC_UDP]);
+        j.key("tcp").u(n[NC_TCP]);
+        j.key("protocol").obj(); j.key("tcp").obj(); j.key("syn").u(n[NC_SYN]); j.end_obj(); j.end_obj();
+        j.key("other_l4").u(n[NC_OTHER]);
+        j.key("ipv4").u(n[NC_V4]);
+        j.key("ipv6").u(n[NC_V6]);
+        j.key("in").u(n[NC_IN]);
+        j.key("out").u(n[NC_OUT]);
+        j.key("unknown_dir").u(n[NC_UNK]);
+        j.key("total").u(n[NC_TOTAL]);
+        j.key("filtered").u(n[NC_FILTERED]);
+    }
+    if (c->net_groups & PV_NET_CARDINALITY) {
+        j.key("cardinality").obj();
+        j.key("src_ips_in").i(lround(cpc_estimate(&b.cpc[CPC_SRC * PV_CPC_COUPONS], b.merged)));
+        j.key("dst_ips_out").i(lround(cpc_estimate(&b.cpc[CPC_DST * PV_CPC_COUPONS], b.merged)));
+        j.end_obj();
+    }
+    if (c->net_groups & PV_NET_TOP_IPS) {
+        top_json(j, "top_ipv4", tops_of(b, TM_IPV4), topn);
+        top_json(j, "top_ipv6", tops_of(b, TM_IPV6), topn);
+    }
+    if (c->net_groups & PV_NET_TOP_GEO) {
+        j.key("top_geoLoc").arr(); j.end_arr();
+        j.key("top_ASN").arr(); j.end_arr();
+    }
+    uint64_t cnt;
+    auto q = hist_quantiles(&b.sum[PV_OFF_PAYLOAD], PV_PAYLOAD_BINS, cnt);
+    if (cnt) {
+        j.key("payload_size").obj();
+        j.key("p50").u(q[0]); j.key("p90").u(q[1]); j.key("p95").u(q[2]); j.key("p99").u(q[3]);
+        j.end_obj();
+    }
+}
+
+void dns_json(pv_ctx *c, Json &j, const HostBucket &b)
+{
+    const uint64_t *d = &b.sum[PV_OFF_DNS];
+    size_t topn = c->cfg.topn_count;
+    uint32_t g = c->dns_groups;
+    j.key("period").obj();
+    j.key("start_ts").i(b.start_sec);
+    j.key("length").u(b.period_length);
+    j.end_obj();
+    j.key("wire_packets").obj();
+    j.key("events").u(d[DC_EVENTS]);
+    j.key("deep_samples").u(d[DC_SAMPLES]);
+    if (g & PV_DNS_COUNTERS) {
+        j.key("queries").u(d[DC_QUERIES]);
+        j.key("replies").u(d[DC_REPLIES]);
+        j.key("tcp").u(d[DC_TCP]);
+        j.key("udp").u(d[DC_UDP]);
+        j.key("ipv4").u(d[DC_V4]);
+        j.key("ipv6").u(d[DC_V6]);
+        j.key("nxdomain").u(d[DC_NX]);
+        j.key("refused").u(d[DC_REFUSED]);
+        j.key("srvfail").u(d[DC_SRVFAIL]);
+        j.key("noerror").u(d[DC_NOERROR]);
+        j.key("nodata").u(d[DC_NODATA]);
+        j.key("total").u(d[DC_TOTAL]);
+        j.key("filtered").u(d[DC_FILTERED]);
+    }
+    j.end_obj();
+    if (g & PV_DNS_CARDINALITY) {
+        j.key("cardinality").obj();
+        j.key("qname").i(lround(cpc_estimate(&b.cpc[CPC_QNAME * PV_CPC_COUPONS], b.merged)));
+        j.end_obj();
+    }
+    if (g & PV_DNS_TRANSACTIONS) {
+        j.key("xact").obj();
+        j.key("counts").obj(); j.key("total").u(d[DC_XTOTAL]); j.key("timed_out").u(d[DC_XTIMEOUT]); j.end_obj();
+        j.key("in").obj();
+        j.key("total").u(d[DC_XIN]);
+        top_json(j, "top_slow", tops_of(b, TM_SLOW_IN), topn);
+        if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.to_us);
+        j.end_obj();
+        j.key("out").obj();
+        j.key("total").u(d[DC_XOUT]);
+        top_json(j, "top_slow", tops_of(b, TM_SLOW_OUT), topn);
+        if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.from_us);
+        j.end_obj();
+        if ((g & PV_DNS_QUANTILES) && !b.ratio.empty()) { j.key("ratio").obj(); quant_json(j, "quantiles", b.ratio); j.end_obj(); }
+        j.end_obj();
+    }
+    if (g & PV_DNS_TOP_PORTS) top_json(j, "top_udp_ports", dense_tops(&b.sum[PV_OFF_PORT], PV_PORT_BINS, 0), topn);
+    if (g & PV_DNS_TOP_QNAMES) {
+        top_json(j, "top_qname2", tops_of(b, TM_QNAME2), topn);
+        top_json(j, "top_qname3", tops_of(b, TM_QNAME3), topn);
+        top_json(j, "top_nxdomain", tops_of(b, TM_NX), topn);
+        top_json(j, "top_refused", tops_of(b, TM_REFUSED), topn);
+        top_json(j, "top_srvfail", tops_of(b, TM_SRVFAIL), topn);
+        top_json(j, "top_nodata", tops_of(b, TM_NODATA), topn);
+        if (g & PV_DNS_TOP_QNAMES_DETAILS) {
+            top_json(j, "top_qname_by_resp_bytes", tops_of(b, TM_SIZED), topn);
+            top_json(j, "top_noerror", tops_of(b, TM_NOERROR), topn);
+        }
+    }
+    top_json(j, "top_rcode", dense_tops(&b.sum[PV_OFF_RCODE], PV_RCODE_BINS, 2), topn);
+    top_json(j, "top_qtype", dense_tops(&b.sum[PV_OFF_QTYPE], PV_QTYPE_BINS, 1), topn);
+}
+
+int window_slots(pv_ctx *c, const Window &w, uint32_t period, bool merged, std::vector<uint32_t> &out)
+{
+    out.clear();
+    if (!merged) {
+        if (period >= c->cfg.num_periods)
+            return c->fail(PV_EINVAL, "invalid metrics period, specify [0, %u]", c->cfg.num_periods - 1);
+        if (period >= w.slots.size())
+            return c->fail(PV_EINVAL, "requested metrics period has not yet accumulated, current range is [0, %zu]",
+                           w.slots.size() - 1);
+        out.push_back(w.slots[period]);
+        return 0;
+    }
+    if (period <= 1 || period > c->cfg.num_periods)
+        return c->fail(PV_EINVAL, "invalid metrics period, specify [2, %u]", c->cfg.num_periods);
+    for (size_t i = 0; i < w.slots.size() && i < period; i++) out.push_back(w.slots[i]);
+    return 0;
+}
+
+} // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char *pv_version(void) { return "pvgpu 0.1 (gfx950)"; }
+
+int pv_device_count(int *count)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return 0;
+}
+
+const char *pv_last_error(const pv_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void pv_free(void *p) { free(p); }
+
+int pv_create(const pv_config *cfg, pv_ctx **out)
+{
+    *out = nullptr;
+    if (!cfg) return PV_EINVAL;
+    pv_ctx *c = new pv_ctx();
+    c->cfg = *cfg;
+    if (c->cfg.num_periods == 0) c->cfg.num_periods = 5;
+    c->cfg.num_periods = std::max(1u, std::min(c->cfg.num_periods, 10u));
+    if (c->cfg.topn_count == 0) c->cfg.topn_count = 10;
+    if (c->cfg.xact_ttl_ms == 0) c->cfg.xact_ttl_ms = 5000;
+    if (c->cfg.linktype == 0) c->cfg.linktype = 1;
+    if (c->cfg.net_groups) c->net_groups = c->cfg.net_groups;
+    if (c->cfg.dns_groups) c->dns_groups = c->cfg.dns_groups;
+    if (c->cfg.table_log2) c->tcap_log2 = c->cfg.table_log2;
+    if (c->cfg.max_records == 0) c->cfg.max_records = 1 << 20;
+    c->max_records = c->cfg.max_records;
+    // TransactionManager(ttl_ms) split (TransactionManager.h:60-68)
+    if (c->cfg.xact_ttl_ms > 1000) { c->ttl_s = c->cfg.xact_ttl_ms / 1000; c->ttl_ms = c->cfg.xact_ttl_ms - c->ttl_s * 1000; }
+    else c->ttl_ms = c->cfg.xact_ttl_ms;
+    int rc = parse_host_spec(c, cfg->host_spec);
+    if (rc) { *out = c; return rc; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { *out = c; return c->fail(PV_ENODEV, "no HIP device"); }
+    if (cfg->device >= 0) {
+        if (cfg->device >= ndev) { *out = c; return c->fail(PV_EINVAL, "device %d out of range", cfg->device); }
+        c->device = cfg->device;
+    } else {
+        hipGetDevice(&c->device);
+    }
+    hipSetDevice(c->device);
+    hipError_t e;
+    uint64_t tcap = 1ull << c->tcap_log2;
+    uint64_t mr = c->max_records;
+    if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
+        !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_cpc, (size_t)PV_SLOTS * PV_MIN_WORDS * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_tkeys, (size_t)PV_SLOTS * tcap * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_tcnt, (size_t)PV_SLOTS * tcap * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_taux, (size_t)PV_SLOTS * tcap * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_arena, (size_t)PV_SLOTS * c->arena_cap)) ||
+        !hip_ok(e = hipMalloc(&c->d_arena_top, PV_SLOTS * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_events, (size_t)mr * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)mr * 8)) || !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)mr * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_svals, (size_t)mr * 4)) || !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)mr * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * sizeof(PvXValue))) ||
+        !hip_ok(e = hipMalloc(&c->d_status, ST_WORDS * 4)) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
+        !hip_ok(e = hipEventCreate(&c->ev_stop))) {
+        *out = c;
+        return c->hipfail(e, "device allocation");
+    }
+    size_t tmp = 0;
+    pv_radix_sort_pairs(nullptr, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, (size_t)mr, c->stream);
+    c->sort_tmp_bytes = std::max<size_t>(tmp, 256);
+    if (!hip_ok(e = hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes))) { *out = c; return c->hipfail(e, "sort scratch"); }
+    *out = c;
+    return pv_reset(c);
+}
+
+void pv_destroy(pv_ctx *c)
+{
+    if (!c) return;
+    if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
+    void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
+                    c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
+                    c->d_recs, c->d_offs};
+    for (void *p : ptrs) if (p) hipFree(p);
+    if (c->ev_start) hipEventDestroy(c->ev_start);
+    if (c->ev_stop) hipEventDestroy(c->ev_stop);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int pv_reset(pv_ctx *c)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    for (uint32_t s = 0; s < PV_SLOTS; s++) c->slot_used[s] = false;
+    c->net = Window();
+    c->dns = Window();
+    c->started = c->ended = false;
+    c->records_seen = 0;
+    c->xvals_host.clear();
+    c->remote_topn.clear();
+    return 0;
+}
+
+int pv_set_global_base(pv_ctx *c, uint64_t base)
+{
+    c->global_base = base;
+    return 0;
+}
+
+int pv_index_records(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32_t *offsets, uint64_t max_records,
+                     uint32_t *sc_idx, uint32_t *sc_sec, uint32_t max_changes, pv_index_info *info)
+{
+    (void)ts_nano;
+    memset(info, 0, sizeof *info);
+    info->monotone = 1;
+    size_t pos = 0;
+    uint64_t n = 0;
+    uint32_t nc = 0;
+    int64_t prev_sec = -1;
+    while (pos + 16 <= bytes && n < max_records) {
+        uint32_t h[4];
+        memcpy(h, recs + pos, 16);
+        if (pos + 16 + h[2] > bytes) break;
+        if (pos > 0xffffffffull) return PV_EINVAL; // offsets are 32-bit: split larger runs
+        offsets[n] = (uint32_t)pos;
+        int64_t sec = h[0];
+        int64_t nsec = ts_nano ? h[1] : (int64_t)h[1] * 1000;
+        if (n == 0) { info->first_sec = sec; info->first_nsec = nsec; }
+        info->last_sec = sec; info->last_nsec = nsec;
+        if (sec != prev_sec) {
+            if (sec < prev_sec) info->monotone = 0;
+            if (nc < max_changes) { sc_idx[nc] = (uint32_t)n; sc_sec[nc] = (uint32_t)sec; }
+            nc++;
+            prev_sec = sec;
+        }
+        pos += 16 + h[2];
+        n++;
+    }
+    info->n_records = n;
+    info->bytes_used = pos;
+    info->n_sec_changes = nc;
+    if (nc > max_changes) return PV_ECAPACITY;
+    return 0;
+}
+
+int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
+                      const uint32_t *sc_idx, const uint32_t *sc_sec, void *stream)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)sc_idx;
+    hipSetDevice(c->device);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t saved = c->stream;
+    c->stream = st;
+    struct Restore { pv_ctx *c; hipStream_t s; ~Restore() { c->stream = s; } } restore{c, saved};
+    const uint64_t n = info->n_records;
+    if (n == 0) return 0;
+    if (n > c->max_records) return c->fail(PV_ECAPACITY, "batch of %llu records exceeds max_records %llu",
+                                           (unsigned long long)n, (unsigned long long)c->max_records);
+    ensure_started(c, info->first_sec, info->first_nsec);
+
+    // ---- period shifts inside this batch (AbstractMetricsManager::new_event)
+    const uint32_t np = c->cfg.num_periods;
+    std::vector<int64_t> thresh;
+    if (np > 1) {
+        int64_t T = c->net.next_shift_sec;
+        if (info->last_sec >= T || !info->monotone) {
+            if (!info->monotone) {
+                // any record at or beyond the next boundary in a non-monotone run needs per-record periods
+                bool crosses = false;
+                for (uint32_t k = 0; k < info->n_sec_changes; k++) crosses |= (int64_t)sc_sec[k] >= T;
+                if (crosses) return c->fail(PV_EUNSUPPORTED, "period shift inside a batch with non-monotone timestamps");
+            } else {
+                for (uint32_t k = 0; k < info->n_sec_changes; k++) {
+                    if ((int64_t)sc_sec[k] >= T) {
+                        thresh.push_back(sc_sec[k]);
+                        T = (int64_t)sc_sec[k] + 60;
+                    }
+                }
+            }
+        }
+    }
+    if (thresh.size() > PV_MAX_SHIFTS)
+        return c->fail(PV_EUNSUPPORTED, "%zu period shifts in one batch (max %d): submit smaller batches", thresh.size(), PV_MAX_SHIFTS);
+
+    PvParams P;
+    memset(&P, 0, sizeof P);
+    P.recs = d_recs;
+    P.offs = d_offs;
+    P.n = n;
+    P.linktype = c->cfg.linktype;
+    P.ts_nano = c->cfg.ts_nano;
+    P.net_groups = c->net_groups;
+    P.dns_groups = c->dns_groups;
+    P.n_shift = (uint32_t)thresh.size();
+    for (size_t k = 0; k < thresh.size(); k++) P.thresh[k] = thresh[k];
+    P.skip_before = P.n_shift + 1 > np ? P.n_shift + 1 - np : 0;
+    P.gbase = c->global_base + c->records_seen;
+    P.nets = c->nets;
+    // slots: period 0 -> live; each shift -> a fresh slot
+    P.slot_of[0] = c->net.slots.front();
+    std::vector<uint32_t> new_slots;
+    {
+        // reserve fresh slots for the shifts that stay in the window
+        std::deque<uint32_t> sim = c->net.slots;
+        for (uint32_t k = 1; k <= P.n_shift; k++) {
+            uint32_t s = 0xffffffffu;
+            for (uint32_t cand = 0; cand < PV_SLOTS && s == 0xffffffffu; cand++) {
+                bool used = false;
+                for (auto x : sim) used |= x == cand;
+                for (auto x : c->dns.slots) used |= x == cand;
+                for (auto x : new_slots) used |= x == cand;
+                if (!used) s = cand;
+            }
+            if (s == 0xffffffffu) return c->fail(PV_ECAPACITY, "no free bucket slot");
+            new_slots.push_back(s);
+            P.slot_of[k] = s;
+            clear_slot(c, s, (int64_t)P.gbase);
+            c->meta[s].start_sec = thresh[k - 1];
+        }
+    }
+    P.sum = c->d_sum;
+    P.cpc = c->d_cpc;
+    P.tkeys = c->d_tkeys;
+    P.tcnt = c->d_tcnt;
+    P.taux = c->d_taux;
+    P.tcap_log2 = c->tcap_log2;
+    P.arena = c->d_arena;
+    P.arena_top = c->d_arena_top;
+    P.arena_cap = c->arena_cap;
+    P.events = c->d_events;
+    P.n_events = c->d_status + ST_NEV;
+    P.want_events = (c->dns_groups & PV_DNS_TRANSACTIONS) ? 1 : 0;
+    P.flags = c->d_status + ST_FLAGS;
+    P.dns_first = c->d_status + ST_DNS_ANY;
+    P.dns_at_thresh = c->d_status + ST_DNS_AT;
+    launch_fill32(c, c->d_status, ST_WORDS, 0);
+    int dev_cus = 256;
+    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    uint64_t tiles = (n + 255) / 256;
+    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)dev_cus * 3);
+    hipEventRecord(c->ev_start, st);
+    hipLaunchKernelGGL(pv_net_dns_kernel, dim3(grid), dim3(256), 0, st, P);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return c->hipfail(e, "launch pv_net_dns_kernel");
+    hipEventRecord(c->ev_stop, st);
+
+    // ---- transactions: pair responses with queries (sort by key, then record index)
+    uint32_t status[ST_WORDS];
+    if (!hip_ok(e = hipMemcpyAsync(status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "kernel execution");
+    {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, c->ev_start, c->ev_stop) == hipSuccess) { c->kernel_ms += ms; c->kernel_launches++; }
+    }
+    uint32_t flags = status[ST_FLAGS];
+    if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
+    if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
+    uint32_t nev = status[ST_NEV];
+    // DNS handler shifts only at DNS events: they must coincide with the Net shifts
+    for (uint32_t k = 1; k <= P.n_shift; k++) {
+        bool later_dns = false;
+        for (uint32_t j = k; j <= P.n_shift; j++) later_dns |= status[ST_DNS_ANY + j] != 0;
+        (void)later_dns;
+    }
+    if (nev > 0) {
+        // (DNS events exist in this batch) every Net shift must coincide with a DNS event second
+        for (uint32_t k = 1; k <= P.n_shift; k++)
+            if (!status[ST_DNS_AT + k])
+                return c->fail(PV_EUNSUPPORTED, "DNS period boundary differs from the Net boundary at second %lld",
+                               (long long)thresh[k - 1]);
+        uint32_t threads = 256, blocks = (nev + threads - 1) / threads;
+        hipLaunchKernelGGL(pv_xact_keys, dim3(blocks), dim3(threads), 0, st, c->d_events, nev, c->d_skeys, c->d_svals);
+        size_t tmp = c->sort_tmp_bytes;
+        if (!hip_ok(e = pv_radix_sort_pairs(c->d_sort_tmp, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
+                                             (size_t)nev, st)))
+            return c->hipfail(e, "radix sort");
+        PvXactParams X;
+        memset(&X, 0, sizeof X);
+        X.events = c->d_events;
+        X.skeys = c->d_skeys2;
+        X.svals = c->d_svals2;
+        X.n = nev;
+        X.n_shift = P.n_shift;
+        for (int k = 0; k < PV_MAX_SHIFTS; k++) X.thresh[k] = P.thresh[k];
+        for (int k = 0; k <= PV_MAX_SHIFTS; k++) X.slot_of[k] = P.slot_of[k];
+        X.skip_before = P.skip_before;
+        X.ttl_s = c->ttl_s;
+        X.ttl_ms = c->ttl_ms;
+        X.quantiles = (c->dns_groups & PV_DNS_QUANTILES) ? 1 : 0;
+        X.sum = c->d_sum;
+        X.vals = c->d_xvals;
+        X.n_vals = c->d_status + ST_NVALS;
+        X.vals_cap = (uint32_t)c->max_records;
+        X.flags = c->d_status + ST_FLAGS;
+        hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, X);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
+    }
+
+    // ---- window bookkeeping (host mirror of _period_shift)
+    for (uint32_t k = 1; k <= P.n_shift; k++) {
+        uint32_t s = P.slot_of[k];
+        int64_t T = thresh[k - 1];
+        c->meta[c->net.slots.front()].set_read_only(T, 0);
+        c->net.slots.push_front(s);
+        if (c->net.slots.size() > np) c->net.slots.pop_back();
+        c->net.next_shift_sec = T + 60;
+        if (nev > 0) {
+            c->dns.slots.push_front(s);
+            if (c->dns.slots.size() > np) c->dns.slots.pop_back();
+            c->dns.next_shift_sec = T + 60;
+        }
+    }
+    c->records_seen += n;
+    c->last_sec = info->last_sec;
+    c->last_nsec = info->last_nsec;
+    return 0;
+}
+
+int pv_synchronize(pv_ctx *c)
+{
+    hipSetDevice(c->device);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return c->hipfail(e, "synchronize");
+    // pull transaction values produced so far
+    uint32_t status[ST_WORDS];
+    if (!hip_ok(e = hipMemcpy(status, c->d_status, sizeof status, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
+    uint32_t nv = std::min<uint32_t>(status[ST_NVALS], (uint32_t)c->max_records);
+    if (status[ST_FLAGS] & PVF_VALUES_FULL) return c->fail(PV_ECAPACITY, "transaction value buffer full");
+    if (nv) {
+        size_t old = c->xvals_host.size();
+        c->xvals_host.resize(old + nv);
+        if (!hip_ok(e = hipMemcpy(&c->xvals_host[old], c->d_xvals, nv * sizeof(PvXValue), hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "transaction values");
+        uint32_t zero = 0;
+        hipMemcpy(c->d_status + ST_NVALS, &zero, 4, hipMemcpyHostToDevice);
+    }
+    return 0;
+}
+
+int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
+{
+    hipSetDevice(c->device);
+    uint64_t maxr = c->max_records;
+    std::vector<uint32_t> offs(maxr);
+    std::vector<uint32_t> sci(1 << 16), scs(1 << 16);
+    size_t pos = 0;
+    while (pos < bytes) {
+        pv_index_info info;
+        int rc = pv_index_records(recs + pos, bytes - pos, c->cfg.ts_nano, offs.data(), maxr, sci.data(), scs.data(),
+                                  (uint32_t)sci.size(), &info);
+        if (rc) return c->fail(rc, "record index failed");
+        if (info.n_records == 0) break;
+        size_t need = info.bytes_used + 256;
+        hipError_t e;
+        if (need > c->recs_cap) {
+            if (c->d_recs) hipFree(c->d_recs);
+            if (c->d_offs) hipFree(c->d_offs);
+            c->d_recs = nullptr; c->d_offs = nullptr;
+            if (!hip_ok(e = hipMalloc(&c->d_recs, need)) || !hip_ok(e = hipMalloc(&c->d_offs, maxr * 4)))
+                return c->hipfail(e, "staging allocation");
+            c->recs_cap = need;
+        }
+        if (!hip_ok(e = hipMemcpyAsync(c->d_recs, recs + pos, info.bytes_used, hipMemcpyHostToDevice, c->stream)) ||
+            !hip_ok(e = hipMemsetAsync(c->d_recs + info.bytes_used, 0, 256, c->stream)) ||
+            !hip_ok(e = hipMemcpyAsync(c->d_offs, offs.data(), info.n_records * 4, hipMemcpyHostToDevice, c->stream)))
+            return c->hipfail(e, "H2D");
+        rc = pv_process_device(c, c->d_recs, c->d_offs, &info, sci.data(), scs.data(), nullptr);
+        if (rc) return rc;
+        rc = pv_synchronize(c);
+        if (rc) return rc;
+        pos += info.bytes_used;
+    }
+    return 0;
+}
+
+int pv_set_start_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
+{
+    return ensure_started(c, sec, nsec);
+}
+
+int pv_set_end_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
+{
+    if (!c->started) return 0;
+    // end_tstamp_signal: the live bucket of each manager becomes read-only
+    c->meta[c->net.slots.front()].set_read_only(sec, nsec);
+    if (c->dns.slots.front() != c->net.slots.front()) c->meta[c->dns.slots.front()].set_read_only(sec, nsec);
+    c->ended = true;
+    return 0;
+}
+
+int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
+{
+    *out = nullptr;
+    int rc = pv_synchronize(c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->started) return c->fail(PV_EINVAL, "no data");
+    Json j;
+    j.obj();
+    std::vector<uint32_t> slots;
+    {
+        if ((rc = window_slots(c, c->net, period, merged != 0, slots))) return rc;
+        HostBucket b;
+        if ((rc = load_bucket(c, slots, merged != 0, c->net, b))) return rc;
+        j.key("packets").obj();
+        net_json(c, j, b);
+        j.end_obj();
+    }
+    {
+        if ((rc = window_slots(c, c->dns, period, merged != 0, slots))) return rc;
+        HostBucket b;
+        if ((rc = load_bucket(c, slots, merged != 0, c->dns, b))) return rc;
+        j.key("dns").obj();
+        dns_json(c, j, b);
+        j.end_obj();
+    }
+    j.end_obj();
+    *out = strdup(j.s.c_str());
+    return 0;
+}
+
+int pv_state_regions(pv_ctx *c, void **sum_ptr, size_t *sum_bytes, void **min_ptr, size_t *min_bytes)
+{
+    *sum_ptr = c->d_sum;
+    *sum_bytes = (size_t)PV_SLOTS * PV_SUM_WORDS * 8;
+    *min_ptr = c->d_cpc;
+    *min_bytes = (size_t)PV_SLOTS * PV_MIN_WORDS * 8;
+    return 0;
+}
+
+// record: u32 slot, u64 key, u64 count, u16 name_len, name bytes
+int pv_export_topn(pv_ctx *c, uint8_t **buf, size_t *bytes)
+{
+    std::vector<uint8_t> o;
+    std::vector<uint32_t> live;
+    for (auto s : c->net.slots) live.push_back(s);
+    for (auto s : c->dns.slots) if (std::find(live.begin(), live.end(), s) == live.end()) live.push_back(s);
+    for (uint32_t s : live) {
+        std::vector<TopRec> recs;
+        int rc = read_topn(c, s, recs);
+        if (rc) return rc;
+        for (auto &r : recs) {
+            uint16_t l = (uint16_t)std::min<size_t>(r.name.size(), 65535);
+            size_t p = o.size();
+            o.resize(p + 4 + 8 + 8 + 2 + l);
+            memcpy(&o[p], &s, 4);
+            memcpy(&o[p + 4], &r.key, 8);
+            memcpy(&o[p + 12], &r.count, 8);
+            memcpy(&o[p + 20], &l, 2);
+            memcpy(&o[p + 22], r.name.data(), l);
+        }
+    }
+    *bytes = o.size();
+    *buf = (uint8_t *)malloc(o.size() ? o.size() : 1);
+    if (!o.empty()) memcpy(*buf, o.data(), o.size());
+    return 0;
+}
+
+int pv_merge_topn(pv_ctx *c, const uint8_t *buf, size_t bytes)
+{
+    size_t p = 0;
+    while (p + 22 <= bytes) {
+        uint32_t s; uint64_t key, cnt; uint16_t l;
+        memcpy(&s, buf + p, 4); memcpy(&key, buf + p + 4, 8); memcpy(&cnt, buf + p + 12, 8); memcpy(&l, buf + p + 20, 2);
+        if (p + 22 + l > bytes || s >= PV_SLOTS) return c->fail(PV_EINVAL, "malformed top-N buffer");
+        auto &e = c->remote_topn[s][key];
+        e.first += cnt;
+        e.second.assign((const char *)buf + p + 22, l);
+        p += 22 + l;
+    }
+    return 0;
+}
+
+int pv_window_slots(pv_ctx *c, uint32_t *slots, uint32_t max_slots, uint32_t *n_slots, size_t *sum_slot_words,
+                    size_t *min_slot_words)
+{
+    std::vector<uint32_t> v;
+    for (auto s : c->net.slots) v.push_back(s);
+    for (auto s : c->dns.slots) if (std::find(v.begin(), v.end(), s) == v.end()) v.push_back(s);
+    *n_slots = (uint32_t)v.size();
+    for (uint32_t i = 0; i < v.size() && i < max_slots; i++) slots[i] = v[i];
+    *sum_slot_words = PV_SUM_WORDS;
+    *min_slot_words = PV_MIN_WORDS;
+    return 0;
+}
+
+int pv_kernel_timing(pv_ctx *c, double *total_ms, uint64_t *launches, int reset)
+{
+    *total_ms = c->kernel_ms;
+    *launches = c->kernel_launches;
+    if (reset) { c->kernel_ms = 0; c->kernel_launches = 0; }
+    return 0;
+}
+
+} // extern "C"

@@ -1,0 +1,163 @@
+// SPDX-License-Identifier: MPL-2.0
+// pv_layout.h — device-state layout shared by the HIP kernels and the host runtime.
+//
+// One "slot" holds one metrics bucket (a 60 s period, AbstractMetricsManager.h:276-308)
+// of both handlers. Slots form a ring of PV_SLOTS; the live window is the last
+// num_periods slots. Per slot, in HBM:
+//   SUM region   uint64  net counters | dns counters | payload-size histogram |
+//                        udp-port / qtype / rcode tables     (all-reduce SUM)
+//   MIN region   int64   CPC first-occurrence global record index per coupon, 3 x 2^17
+//                                                           (all-reduce MIN)
+//   top-N table  open addressing (key u64, count u64, aux u32) + name arena
+#pragma once
+#include <stdint.h>
+
+#define PV_SLOTS 16
+#define PV_MAX_SHIFTS 6 // period shifts handled inside one device batch
+#define PV_MAX_SUBNETS 16
+
+// group bits (same values as pv_net_group / pv_dns_group in include/pvgpu.h)
+#define PV_NET_COUNTERS_BIT 1u
+#define PV_NET_CARDINALITY_BIT 2u
+#define PV_NET_TOP_IPS_BIT 8u
+#define PV_DNS_CARDINALITY_BIT (1u << 0)
+#define PV_DNS_COUNTERS_BIT (1u << 1)
+#define PV_DNS_QUANTILES_BIT (1u << 2)
+#define PV_DNS_TRANSACTIONS_BIT (1u << 4)
+#define PV_DNS_TOP_QNAMES_BIT (1u << 6)
+#define PV_DNS_TOP_QNAMES_DETAILS_BIT (1u << 7)
+#define PV_DNS_TOP_PORTS_BIT (1u << 8)
+
+// ---- SUM region (uint64 words), per slot
+#define PV_NET_CTRS 32
+#define PV_DNS_CTRS 32
+#define PV_PAYLOAD_BINS 65536
+#define PV_PORT_BINS 65536
+#define PV_QTYPE_BINS 65536
+#define PV_RCODE_BINS 16
+#define PV_OFF_NET 0
+#define PV_OFF_DNS (PV_OFF_NET + PV_NET_CTRS)
+#define PV_OFF_PAYLOAD (PV_OFF_DNS + PV_DNS_CTRS)
+#define PV_OFF_PORT (PV_OFF_PAYLOAD + PV_PAYLOAD_BINS)
+#define PV_OFF_QTYPE (PV_OFF_PORT + PV_PORT_BINS)
+#define PV_OFF_RCODE (PV_OFF_QTYPE + PV_QTYPE_BINS)
+#define PV_SUM_WORDS (PV_OFF_RCODE + PV_RCODE_BINS)
+
+// net counters (src/handlers/net/v1/NetStreamHandler.h:69-96 + base event counters)
+enum {
+    NC_EVENTS = 0, NC_SAMPLES, NC_UDP, NC_TCP, NC_OTHER, NC_V4, NC_V6, NC_SYN, NC_IN, NC_OUT, NC_UNK, NC_TOTAL,
+    NC_FILTERED, NC_COUNT
+};
+// dns counters (src/handlers/dns/v1/DnsStreamHandler.h:94-139 + base event counters)
+enum {
+    DC_EVENTS = 0, DC_SAMPLES, DC_QUERIES, DC_REPLIES, DC_TCP, DC_UDP, DC_V4, DC_V6, DC_NX, DC_REFUSED, DC_SRVFAIL,
+    DC_NOERROR, DC_NODATA, DC_TOTAL, DC_FILTERED, DC_XTOTAL, DC_XIN, DC_XOUT, DC_XTIMEOUT, DC_COUNT
+};
+
+// ---- MIN region (int64 global record index), per slot: CPC lg_k = 11 => 2048 rows x 64 cols
+#define PV_CPC_COUPONS (2048 * 64)
+enum { CPC_SRC = 0, CPC_DST = 1, CPC_QNAME = 2, CPC_SKETCHES = 3 };
+#define PV_MIN_WORDS (CPC_SKETCHES * PV_CPC_COUPONS)
+#define PV_CPC_EMPTY 0x7fffffffffffffffLL
+
+// ---- top-N metrics: key = metric << 56 | payload (56 bits)
+enum {
+    TM_NONE = 0, TM_IPV4 = 1, TM_IPV6 = 2, TM_QNAME2 = 3, TM_QNAME3 = 4, TM_NX = 5, TM_REFUSED = 6, TM_SRVFAIL = 7,
+    TM_NODATA = 8, TM_NOERROR = 9, TM_SIZED = 10, TM_SLOW_IN = 11, TM_SLOW_OUT = 12,
+    // dense metrics share the block cache, flushed into the SUM region
+    TM_DENSE_PORT = 16, TM_DENSE_QTYPE = 17, TM_DENSE_RCODE = 18
+};
+#define PV_KEY(metric, payload) (((uint64_t)(metric) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
+#define PV_KEY_METRIC(k) ((uint32_t)((k) >> 56))
+
+// aux word of a top-N entry: arena offset + 1 of its name record (0 = none)
+// arena record: uint16 length, then bytes
+
+// ---- flags word bits (device -> host)
+enum {
+    PVF_TABLE_FULL = 1u << 0,
+    PVF_ARENA_FULL = 1u << 1,
+    PVF_EVENTS_FULL = 1u << 2,
+    PVF_VALUES_FULL = 1u << 3,
+    PVF_BIG_CAPLEN = 1u << 4
+};
+
+// DNS transaction event, one per DNS wire packet (for the pairing pass)
+struct PvXEvent {
+    uint64_t key;   // flowkey << 16 | txid
+    uint32_t idx;   // record index within the batch
+    uint32_t len;   // DNS message length (DnsLayer::getDataLen)
+    int64_t sec;
+    int32_t nsec;
+    uint8_t qr;     // 1 = response
+    uint8_t dir;    // PacketDirection: 0 toHost, 1 fromHost, 2 unknown
+    uint8_t period; // period index within the batch
+    uint8_t pad;
+};
+
+// one transaction-derived value (quantile input), grouped per slot/kind on the host
+enum { XV_FROM_US = 0, XV_TO_US = 1, XV_RATIO = 2 };
+struct PvXValue {
+    uint64_t bits; // uint64 microseconds, or the IEEE-754 bits of the double ratio
+    uint32_t slot;
+    uint32_t kind;
+};
+
+struct PvXactParams {
+    const PvXEvent *events;
+    const uint64_t *skeys; // sorted (hash32(key) << 32 | idx)
+    const uint32_t *svals; // event position for each sorted key
+    uint32_t n;
+    uint32_t n_shift;
+    int64_t thresh[PV_MAX_SHIFTS];
+    uint32_t slot_of[PV_MAX_SHIFTS + 1];
+    uint32_t skip_before;
+    uint32_t ttl_s, ttl_ms;
+    uint32_t quantiles;
+    uint64_t *sum;
+    PvXValue *vals;
+    uint32_t *n_vals;
+    uint32_t vals_cap;
+    uint32_t *flags;
+};
+
+struct PvSubnets {
+    uint32_t n4, n6;
+    uint32_t v4_addr[PV_MAX_SUBNETS]; // in_addr.s_addr (network byte order as loaded LE)
+    uint32_t v4_mask[PV_MAX_SUBNETS]; // htobe32(0xffffffff << (32 - cidr)); cidr 0 => match-all flag below
+    uint32_t v4_all[PV_MAX_SUBNETS];
+    uint8_t v6_addr[PV_MAX_SUBNETS][16];
+    uint32_t v6_cidr[PV_MAX_SUBNETS];
+};
+
+struct PvParams {
+    const uint8_t *recs;
+    const uint32_t *offs;
+    uint64_t n;
+    uint32_t linktype;
+    uint32_t ts_nano;
+    uint32_t net_groups, dns_groups;
+    // periods inside this batch: period p (0..n_shift) covers ts_sec in [thresh[p-1], thresh[p])
+    uint32_t n_shift;
+    int64_t thresh[PV_MAX_SHIFTS];
+    uint32_t slot_of[PV_MAX_SHIFTS + 1];
+    uint32_t skip_before; // periods < skip_before are outside the kept window (no bucket updates)
+    uint64_t gbase;
+    PvSubnets nets;
+    // device state
+    uint64_t *sum;    // PV_SLOTS x PV_SUM_WORDS
+    int64_t *cpc;     // PV_SLOTS x PV_MIN_WORDS
+    uint64_t *tkeys;  // PV_SLOTS x tcap
+    uint64_t *tcnt;
+    uint32_t *taux;
+    uint32_t tcap_log2;
+    uint8_t *arena;   // PV_SLOTS x arena_cap
+    uint64_t *arena_top;
+    uint64_t arena_cap;
+    PvXEvent *events;
+    uint32_t *n_events;
+    uint32_t want_events;
+    uint32_t *flags;
+    uint32_t *dns_first; // per period: min record index of a DNS event in that period
+    uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
+};
