@@ -591,7 +591,10 @@ static size_t decode_name(const DnsMsg &m, size_t off, std::string &out, int ite
         if ((wl & 0xc0) == 0xc0) {
             if (cur + 2 > m.len || enc > 255) return enc;
             uint16_t ptr = (uint16_t)((wl & 0x3f) * 256 + m.byte(cur + 1));
-            if (ptr < 12 || ptr >= m.len) { out.clear(); return 0; }
+            // illegal pointer: return 0. At the top level the caller discards the text
+            // (m_NameLength == 0); a nested caller copies what this level already wrote
+            // into its zero-filled tempResult (labels with their trailing '.').
+            if (ptr < 12 || ptr >= m.len) return 0;
             std::string tmp;
             decode_name(m, ptr, tmp, iteration + 1);
             // tempResult is a zero-filled buffer: copy stops at the first NUL
@@ -1276,6 +1279,34 @@ void pvo_murmur3(const uint8_t *d, size_t n, uint64_t seed, uint64_t *out2)
 }
 
 double pvo_icon(uint32_t c) { return pvo::icon_estimate(c); }
+
+// First query name as DnsQuery would hold it (NUL-truncated) and m_NameLength.
+uint32_t pvo_decode_qname(const uint8_t *msg, uint32_t len, char *out, uint32_t *outlen)
+{
+    pvo::DnsMsg m{msg, len};
+    std::string nm;
+    size_t nl = pvo::decode_name(m, 12, nm, 1);
+    std::string name;
+    if (nl > 0) { size_t z = nm.find('\0'); name = z == std::string::npos ? nm : nm.substr(0, z); }
+    memcpy(out, name.data(), name.size());
+    *outlen = (uint32_t)name.size();
+    return (uint32_t)nl;
+}
+
+void pvo_dns_parse(const uint8_t *msg, uint32_t len, int *ok, int *has_query, uint32_t *qtype)
+{
+    pvo::DnsMsg m{msg, len};
+    pvo::DnsParse r = pvo::parse_resources(m);
+    *ok = r.ok; *has_query = r.has_query; *qtype = r.qtype;
+}
+
+void pvo_aggregate_domain(const char *name, size_t n, size_t suffix, size_t *q2_start, long *q3_start)
+{
+    std::string d(name, n), q2, q3;
+    pvo::aggregate_domain(d, suffix, q2, q3);
+    *q2_start = d.size() - q2.size();
+    *q3_start = q3.empty() ? -1 : (long)(d.size() - q3.size());
+}
 
 } // extern "C"
 

@@ -37,481 +37,19 @@ namespace {
 // ------------------------------------------------------------------ byte access
 // recs is 256-B aligned and padded by >= 64 bytes: two aligned dword loads and
 // v_alignbyte give an unaligned little-endian u32 without byte loops.
-__device__ __forceinline__ uint32_t ld32(const uint8_t *base, uint64_t off)
+__device__ __forceinline__ uint32_t pv_ld32(const uint8_t *base, uint64_t off)
 {
     const uint32_t *p = reinterpret_cast<const uint32_t *>(base + (off & ~3ull));
     uint32_t lo = p[0], hi = p[1];
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
 }
-__device__ __forceinline__ uint32_t ld8(const uint8_t *base, uint64_t off) { return base[off]; }
-__device__ __forceinline__ uint32_t be16(const uint8_t *base, uint64_t off)
-{
-    uint32_t w = ld32(base, off);
-    return ((w & 0xff) << 8) | ((w >> 8) & 0xff);
-}
-
-// ------------------------------------------------------------------ hashing
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-__device__ __forceinline__ uint64_t fmix64(uint64_t k)
-{
-    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
-    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
-    k ^= k >> 33;
-    return k;
-}
-#define MM_C1 0x87c37b91114253d5ULL
-#define MM_C2 0x4cf5ad432745937fULL
-
-// Streaming MurmurHash3_x64_128 (seed 9001, datasketches DEFAULT_SEED).
-struct Murmur {
-    uint64_t h1, h2, k1, k2;
-    uint32_t n;
-    __device__ void init() { h1 = h2 = 9001; k1 = k2 = 0; n = 0; }
-    __device__ void block()
-    {
-        k1 *= MM_C1; k1 = rotl64(k1, 31); k1 *= MM_C2; h1 ^= k1;
-        h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
-        k2 *= MM_C2; k2 = rotl64(k2, 33); k2 *= MM_C1; h2 ^= k2;
-        h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
-        k1 = k2 = 0;
-    }
-    __device__ void put(uint32_t c)
-    {
-        uint32_t j = n & 15;
-        if (j < 8) k1 |= (uint64_t)c << (8 * j);
-        else k2 |= (uint64_t)c << (8 * (j - 8));
-        n++;
-        if ((n & 15) == 0) block();
-    }
-    __device__ void finish(uint64_t &o1, uint64_t &o2)
-    {
-        uint32_t r = n & 15;
-        if (r > 8) { k2 *= MM_C2; k2 = rotl64(k2, 33); k2 *= MM_C1; h2 ^= k2; }
-        if (r > 0) { k1 *= MM_C1; k1 = rotl64(k1, 31); k1 *= MM_C2; h1 ^= k1; }
-        h1 ^= n; h2 ^= n;
-        h1 += h2; h2 += h1;
-        h1 = fmix64(h1); h2 = fmix64(h2);
-        h1 += h2; h2 += h1;
-        o1 = h1; o2 = h2;
-    }
-};
-
-// Fixed-length murmur for 8 and 16 byte items (one/one-and-a-half blocks).
-__device__ __forceinline__ void murmur_8(uint64_t v, uint64_t &o1, uint64_t &o2)
-{
-    uint64_t h1 = 9001, h2 = 9001, k1 = v;
-    k1 *= MM_C1; k1 = rotl64(k1, 31); k1 *= MM_C2; h1 ^= k1;
-    h1 ^= 8; h2 ^= 8;
-    h1 += h2; h2 += h1;
-    h1 = fmix64(h1); h2 = fmix64(h2);
-    h1 += h2; h2 += h1;
-    o1 = h1; o2 = h2;
-}
-__device__ __forceinline__ void murmur_16(uint64_t a, uint64_t b, uint64_t &o1, uint64_t &o2)
-{
-    uint64_t h1 = 9001, h2 = 9001, k1 = a, k2 = b;
-    k1 *= MM_C1; k1 = rotl64(k1, 31); k1 *= MM_C2; h1 ^= k1;
-    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
-    k2 *= MM_C2; k2 = rotl64(k2, 33); k2 *= MM_C1; h2 ^= k2;
-    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
-    h1 ^= 16; h2 ^= 16;
-    h1 += h2; h2 += h1;
-    h1 = fmix64(h1); h2 = fmix64(h2);
-    h1 += h2; h2 += h1;
-    o1 = h1; o2 = h2;
-}
-
-// CPC coupon index from the two hash halves (cpc_sketch_impl.hpp:175-185), lg_k = 11.
-__device__ __forceinline__ uint32_t cpc_coupon(uint64_t h1, uint64_t h2)
-{
-    uint32_t col = h2 ? (uint32_t)__clzll((long long)h2) : 63;
-    if (col > 63) col = 63;
-    uint32_t row = (uint32_t)(h1 & 2047);
-    return (row << 6) | col;
-}
-
-// Polynomial string fingerprint modulo the Mersenne prime 2^61-1.
-#define MP61 ((1ULL << 61) - 1)
-#define PBASE 0x1f3d5b79a2c4e681ULL % MP61
-__device__ __forceinline__ uint64_t mulmod61(uint64_t a, uint64_t b)
-{
-    uint64_t lo = a * b, hi = __umul64hi(a, b);
-    uint64_t r = (lo & MP61) + ((lo >> 61) | (hi << 3));
-    r = (r & MP61) + (r >> 61);
-    return r >= MP61 ? r - MP61 : r;
-}
-__device__ __forceinline__ uint64_t addmod61(uint64_t a, uint64_t b)
-{
-    uint64_t r = a + b;
-    return r >= MP61 ? r - MP61 : r;
-}
-__device__ uint64_t powmod61(uint64_t b, uint32_t e)
-{
-    uint64_t r = 1;
-    while (e) { if (e & 1) r = mulmod61(r, b); b = mulmod61(b, b); e >>= 1; }
-    return r;
-}
-// 56-bit fingerprint of a byte string from its polynomial hash and length
-__device__ __forceinline__ uint64_t fp56(uint64_t poly, uint32_t len, uint32_t salt)
-{
-    return fmix64(poly ^ ((uint64_t)len << 48) ^ ((uint64_t)salt << 40) ^ 0x9e3779b97f4a7c15ULL) & 0x00ffffffffffffffULL;
-}
-__device__ __forceinline__ uint32_t hash32(uint64_t k) { return (uint32_t)(fmix64(k) >> 17); }
-
-// ------------------------------------------------------------------ packet parse
-struct Parsed {
-    uint32_t caplen;
-    int64_t sec;
-    int32_t nsec;
-    uint64_t frame;    // absolute offset of frame byte 0
-    uint8_t l3, l4;    // 0/4/6, 0/6/17
-    uint8_t has4, has6;
-    uint8_t syn, dir;
-    uint64_t v4;       // absolute offset of first IPv4 header
-    uint64_t v6;       // absolute offset of first IPv6 header
-    uint64_t l4off;    // absolute offset of the TCP/UDP header
-    uint32_t l4len;    // IP-length-trimmed L4 layer length
-};
-
-__device__ __forceinline__ bool match4(const PvSubnets &s, uint32_t ip)
-{
-    if (!ip) return false;
-    for (uint32_t i = 0; i < s.n4; i++) {
-        if (s.v4_all[i]) return true;
-        if (((ip ^ s.v4_addr[i]) & s.v4_mask[i]) == 0) return true;
-    }
-    return false;
-}
-__device__ bool match6(const PvSubnets &s, const uint8_t *recs, uint64_t a)
-{
-    for (uint32_t i = 0; i < s.n6; i++) {
-        uint32_t cidr = s.v6_cidr[i], bytes = cidr / 8, bits = cidr % 8;
-        bool r = false;
-        if (bytes > 0) {
-            r = true;
-            for (uint32_t b = 0; b < bytes; b++)
-                if (ld8(recs, a + b) != s.v6_addr[i][b]) { r = false; break; }
-        }
-        if ((r || cidr < 8) && bits > 0) r = (s.v6_addr[i][bytes] >> (8 - bits)) == (ld8(recs, a + bytes) >> (8 - bits));
-        if (r) return true;
-    }
-    return false;
-}
-
-__device__ void parse_record(const PvParams &P, uint64_t rec, Parsed &o)
-{
-    const uint8_t *R = P.recs;
-    uint32_t tsec = ld32(R, rec), tfrac = ld32(R, rec + 4);
-    o.caplen = ld32(R, rec + 8);
-    o.sec = tsec;
-    o.nsec = P.ts_nano ? (int32_t)tfrac : (int32_t)(tfrac * 1000u);
-    o.frame = rec + 16;
-    o.l3 = o.l4 = 0; o.has4 = o.has6 = 0; o.syn = 0; o.dir = 2;
-    o.v4 = o.v6 = o.l4off = 0; o.l4len = 0;
-    uint64_t cur = o.frame;
-    uint32_t len = o.caplen;
-    uint32_t kind = 0; // 4 or 6 once an IP header is located
-    uint32_t et = 0;
-    bool l2ok = false;
-    if (P.linktype == 1) {
-        if (len >= 14) {
-            et = be16(R, cur + 12);
-            if (et >= 0x600 && len > 14) { cur += 14; len -= 14; l2ok = true; }
-        }
-    } else if (P.linktype == 113) {
-        if (len > 16) { et = be16(R, cur + 14); cur += 16; len -= 16; l2ok = true; }
-    } else if (P.linktype == 101 || P.linktype == 12 || P.linktype == 14 || P.linktype == 228 || P.linktype == 229) {
-        if (len >= 1) { uint32_t v = ld8(R, cur) >> 4; kind = (v == 4 || v == 6) ? v : 0; }
-    }
-    if (l2ok) {
-        for (int d = 0; d < 8 && (et == 0x8100 || et == 0x88A8); d++) {
-            if (len <= 4) { et = 0; break; }
-            et = be16(R, cur + 2);
-            cur += 4; len -= 4;
-        }
-        kind = et == 0x0800 ? 4 : (et == 0x86DD ? 6 : 0);
-    }
-    for (int depth = 0; depth < 4 && kind; depth++) {
-        uint32_t proto, hl;
-        if (kind == 4) {
-            uint32_t b0 = ld8(R, cur);
-            if (!(len >= 20 && (b0 >> 4) == 4 && (b0 & 15) >= 5)) break;
-            if (!o.has4) { o.has4 = 1; o.v4 = cur; }
-            uint32_t total = be16(R, cur + 2);
-            if (total < len && total != 0) len = total;
-            hl = (b0 & 15) * 4;
-            if (len <= hl) break;
-            uint32_t frag = be16(R, cur + 6);
-            if ((frag & 0x2000) || (frag & 0x1fff)) break;
-            proto = ld8(R, cur + 9);
-        } else {
-            if (len < 40) break;
-            if (!o.has6) { o.has6 = 1; o.v6 = cur; }
-            uint32_t next = ld8(R, cur + 6);
-            uint32_t off = 40;
-            bool frag = false;
-            for (int e = 0; e < 8 && len >= 2 && off <= len - 2; e++) {
-                uint32_t elen;
-                if (next == 44) elen = 8;
-                else if (next == 0 || next == 60 || next == 43) elen = (ld8(R, cur + off + 1) + 1) * 8;
-                else if (next == 51) elen = (ld8(R, cur + off + 1) + 2) * 4;
-                else break;
-                frag = next == 44;
-                next = ld8(R, cur + off);
-                off += elen;
-            }
-            uint32_t total = be16(R, cur + 4) + off;
-            if (total < len) len = total;
-            hl = off;
-            if (len <= hl || frag) break;
-            proto = next;
-        }
-        uint64_t pl = cur + hl;
-        uint32_t pll = len - hl;
-        if (proto == 17) {
-            if (pll >= 8) { o.l4 = 17; o.l4off = pl; o.l4len = pll; }
-            break;
-        }
-        if (proto == 6) {
-            if (pll >= 20) { o.l4 = 6; o.l4off = pl; o.l4len = pll; o.syn = (ld8(R, pl + 13) & 2) ? 1 : 0; }
-            break;
-        }
-        if ((proto == 4 || proto == 41) && pll >= 1) {
-            uint32_t v = ld8(R, pl) >> 4;
-            kind = (v == 4 || v == 6) ? v : 0;
-            cur = pl; len = pll;
-            continue;
-        }
-        break;
-    }
-    o.l3 = o.has4 ? 4 : (o.has6 ? 6 : 0);
-    // direction (PcapInputStream.cpp:401-416)
-    if (o.has4) {
-        if (match4(P.nets, ld32(R, o.v4 + 16))) o.dir = 0;
-        else if (match4(P.nets, ld32(R, o.v4 + 12))) o.dir = 1;
-    } else if (o.has6) {
-        if (match6(P.nets, R, o.v6 + 24)) o.dir = 0;
-        else if (match6(P.nets, R, o.v6 + 8)) o.dir = 1;
-    }
-}
-
-// PcapPlusPlus hash5Tuple(packet, directionUnique=false): FNV-1 32-bit.
-__device__ __forceinline__ uint32_t fnv_bytes(uint32_t h, uint32_t v, int n)
-{
-    for (int i = 0; i < n; i++) { h *= 0x01000193u; h ^= (v >> (8 * i)) & 0xff; }
-    return h;
-}
-__device__ uint32_t flowkey(const PvParams &P, const Parsed &o)
-{
-    const uint8_t *R = P.recs;
-    uint32_t pw = ld32(R, o.l4off);
-    uint32_t ps = pw & 0xffff, pd = pw >> 16; // raw network-order u16 read little-endian
-    int sp = pd < ps ? 1 : 0;
-    uint32_t h = 0x811C9DC5u;
-    uint32_t p0 = sp ? pd : ps, p1 = sp ? ps : pd;
-    h = fnv_bytes(h, p0, 2);
-    h = fnv_bytes(h, p1, 2);
-    if (o.has4) {
-        uint32_t s = ld32(R, o.v4 + 12), d = ld32(R, o.v4 + 16);
-        if (ps == pd && d < s) sp = 1;
-        uint32_t a = sp ? d : s, b = sp ? s : d;
-        h = fnv_bytes(h, a, 4);
-        h = fnv_bytes(h, b, 4);
-        h = fnv_bytes(h, ld8(R, o.v4 + 9), 1);
-    } else {
-        uint64_t a = sp ? o.v6 + 24 : o.v6 + 8, b = sp ? o.v6 + 8 : o.v6 + 24;
-        for (int i = 0; i < 16; i += 4) h = fnv_bytes(h, ld32(R, a + i), 4);
-        for (int i = 0; i < 16; i += 4) h = fnv_bytes(h, ld32(R, b + i), 4);
-        h = fnv_bytes(h, ld8(R, o.v6 + 6), 1);
-    }
-    return h;
-}
-
-// ------------------------------------------------------------------ DNS name decode
-// Level-1 structural walk of decodeName: returns m_NameLength (encoded length)
-// and whether the name text is forced empty (illegal top-level pointer => 0).
-__device__ uint32_t name_len_l1(const uint8_t *R, uint64_t m, uint32_t len, uint32_t off)
-{
-    uint32_t enc = 0, cur = off;
-    if (cur + 1 > len) return 0;
-    uint32_t wl = ld8(R, m + cur);
-    while (wl != 0) {
-        if ((wl & 0xc0) == 0xc0) {
-            if (cur + 2 > len || enc > 255) return enc;
-            uint32_t ptr = ((wl & 0x3f) << 8) | ld8(R, m + cur + 1);
-            if (ptr < 12 || ptr >= len) return 0;
-            return enc + 2;
-        }
-        if (cur + wl + 1 > len || enc + wl > 255) return enc == 256 ? enc : enc + 1;
-        cur += wl + 1;
-        enc += wl + 1;
-        if (cur + 1 > len) return enc == 256 ? enc : enc + 1;
-        wl = ld8(R, m + cur);
-    }
-    return enc + 1;
-}
-
-// Iterative decodeName producing the characters of the final std::string
-// (NUL-truncated, per-level 255-char copy limits, trailing-dot rules).
-// E::put(c) receives each character; returns false when the name is empty.
-template <class E>
-__device__ void name_emit(const uint8_t *R, uint64_t m, uint32_t len, uint32_t off, E &e)
-{
-    uint32_t cur = off, enc = 0, dec = 0, level = 1;
-    int budget = 1 << 30; // chars that can still travel up to the top-level buffer
-    bool pending = false, stop = false;
-    auto emit = [&](uint32_t c) {
-        if (stop) return;
-        if (c == 0) { stop = true; return; }
-        if (level >= 2) {
-            if (budget <= 0) { stop = true; return; }
-            budget--;
-        }
-        e.put(c);
-    };
-    if (cur + 1 > len) return;
-    uint32_t wl = ld8(R, m + cur);
-    for (int guard = 0; guard < 4096 && !stop; guard++) {
-        if (wl == 0) return; // normal termination: trailing '.' dropped
-        if ((wl & 0xc0) == 0xc0) {
-            if (cur + 2 > len || enc > 255) { if (pending) emit('.'); return; }
-            uint32_t ptr = ((wl & 0x3f) << 8) | ld8(R, m + cur + 1);
-            if (ptr < 12 || ptr >= len) { if (level >= 2 && pending) emit('.'); return; }
-            if (pending) { emit('.'); pending = false; }
-            int cap = 255 - (int)dec;
-            if (level >= 2 && budget < cap) cap = budget;
-            budget = cap;
-            level++;
-            if (level > 21) return; // iteration > 20: nested call returns an empty string
-            cur = ptr; enc = 0; dec = 0;
-            wl = ld8(R, m + cur);
-            continue;
-        }
-        if (cur + wl + 1 > len || enc + wl > 255) { if (enc != 256 && pending) emit('.'); return; }
-        if (pending) emit('.');
-        for (uint32_t i = 0; i < wl && !stop; i++) emit(ld8(R, m + cur + 1 + i));
-        pending = true;
-        dec += wl + 1;
-        cur += wl + 1;
-        enc += wl + 1;
-        if (cur + 1 > len) { if (enc != 256 && pending) emit('.'); return; }
-        wl = ld8(R, m + cur);
-    }
-}
-
-__device__ __forceinline__ uint32_t lower(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
-
-// Per-packet name statistics: murmur for CPC, length, last dots with prefix hashes.
-struct NameStats {
-    Murmur mm;
-    uint64_t ph;         // polynomial prefix hash of the chars so far
-    uint32_t n;          // chars so far
-    uint32_t dot_pos[4]; // positions of the last 4 dots (ring, newest at [n_dots&3])
-    uint64_t dot_ph[4];  // prefix hash *before* that dot
-    uint32_t n_dots;
-    uint32_t last_c;
-    __device__ void init() { mm.init(); ph = 0; n = 0; n_dots = 0; last_c = 0; }
-    __device__ void put(uint32_t c)
-    {
-        c = lower(c);
-        if (c == '.') { dot_pos[n_dots & 3] = n; dot_ph[n_dots & 3] = ph; n_dots++; }
-        mm.put(c);
-        ph = addmod61(mulmod61(ph, PBASE), c + 1);
-        n++;
-        last_c = c;
-    }
-    // most recent dot at position <= lim (rfind semantics); returns -1 if none among the tracked ones
-    __device__ int rfind(int lim, uint64_t &pph) const
-    {
-        uint32_t cnt = n_dots < 4 ? n_dots : 4;
-        for (uint32_t i = 0; i < cnt; i++) {
-            uint32_t s = (n_dots - 1 - i) & 3;
-            if ((int)dot_pos[s] <= lim) { pph = dot_ph[s]; return (int)dot_pos[s]; }
-        }
-        return -1;
-    }
-};
-
-// aggregateDomain(name, 0): suffix start positions for qname2 / qname3 (-1 = empty)
-__device__ void agg_domain(const NameStats &s, int &q2, int &q3, uint64_t &ph2, uint64_t &ph3)
-{
-    int n = (int)s.n;
-    q2 = 0; q3 = 0; ph2 = 0; ph3 = 0;
-    if (n < 5) { q3 = -1; return; }
-    int endDot = 1 << 30;
-    if (s.last_c == '.') endDot = n - 2;
-    uint64_t h1;
-    int first = s.rfind(endDot, h1);
-    if (first > 0) {
-        uint64_t h2;
-        int second = s.rfind(first - 1, h2);
-        if (second >= 0) {
-            q2 = second; ph2 = h2;
-            if (second > 0) {
-                uint64_t h3;
-                int third = s.rfind(second - 1, h3);
-                if (third >= 0) { q3 = third; ph3 = h3; }
-            }
-        } else {
-            q3 = -1;
-        }
-    }
-}
-// polynomial hash of the suffix [start, n) given the prefix hash at start
-__device__ __forceinline__ uint64_t suffix_hash(const NameStats &s, int start, uint64_t ph_start)
-{
-    uint64_t sub = mulmod61(ph_start, powmod61(PBASE, s.n - (uint32_t)start));
-    return addmod61(s.ph, MP61 - sub);
-}
-
-struct CountEmit {
-    uint32_t n;
-    __device__ void put(uint32_t) { n++; }
-};
-struct CopyEmit {
-    uint8_t *dst;
-    uint32_t from, n;
-    __device__ void put(uint32_t c)
-    {
-        if (n >= from) dst[n - from] = (uint8_t)lower(c);
-        n++;
-    }
-};
-
-// ------------------------------------------------------------------ DNS message
-struct DnsInfo {
-    bool ok;          // parseResources(queryOnly) succeeded
-    bool has_query;
-    uint32_t name_off; // offset of the first query name in the message
-    uint32_t name_len_enc;
-    uint32_t qtype;
-};
-
-__device__ void dns_parse(const uint8_t *R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns,
-                          uint32_t ar, DnsInfo &d)
-{
-    d.ok = false; d.has_query = false; d.qtype = 0; d.name_off = 12; d.name_len_enc = 0;
-    uint32_t total = qd + an + ns + ar;
-    if (total > 100) return;
-    if (total == 0) { d.ok = true; return; }
-    if (len < 12) return;
-    if (qd > 0) {
-        uint32_t nl = name_len_l1(R, m, len, 12);
-        if (12 + nl + 4 > len) return;
-        d.ok = true; d.has_query = true; d.name_len_enc = nl;
-        d.qtype = be16(R, m + 12 + nl);
-        return;
-    }
-    uint32_t off = 12;
-    for (uint32_t i = 0; i < total; i++) {
-        uint32_t nl = name_len_l1(R, m, len, off);
-        uint32_t dl = 0;
-        if (off + nl + 10 <= len) dl = be16(R, m + off + nl + 8);
-        off += nl + 10 + dl;
-        if (off > len) return;
-    }
-    d.ok = true;
-}
+__device__ __forceinline__ uint32_t pv_ld8(const uint8_t *base, uint64_t off) { return base[off]; }
+__device__ __forceinline__ uint32_t pv_clz64(uint64_t x) { return (uint32_t)__clzll((long long)x); }
+__device__ __forceinline__ uint64_t pv_umulhi(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
+#define PV_FN __device__ __forceinline__
+} // namespace
+#include "pv_parse.h"
+namespace {
 
 // ------------------------------------------------------------------ LDS workgroup state
 struct BlockState {

@@ -1,0 +1,53 @@
+// tests/native/parse_harness.cpp — TEST ONLY: compiles the product's parse/decode
+// source (pktvisor_amd/csrc/pv_parse.h, the code the HIP kernel runs) for the CPU
+// so it can be fuzzed against the oracle without a GPU. Not a fallback: nothing in
+// the product loads this library.
+#include <cstring>
+#include <stdint.h>
+
+#define PV_FN inline
+inline uint32_t pv_ld32(const uint8_t *b, uint64_t off) { uint32_t v; memcpy(&v, b + off, 4); return v; }
+inline uint32_t pv_ld8(const uint8_t *b, uint64_t off) { return b[off]; }
+inline uint32_t pv_clz64(uint64_t x) { return (uint32_t)__builtin_clzll(x); }
+inline uint64_t pv_umulhi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+#include "../../pktvisor_amd/csrc/pv_parse.h"
+
+extern "C" {
+
+// first query name of a DNS message (buffer must be readable 8 bytes past len):
+// returns m_NameLength, writes the raw name bytes (as the final std::string) to out
+uint32_t h_decode_qname(const uint8_t *msg, uint32_t len, char *out, uint32_t *outlen)
+{
+    struct Coll {
+        char *o;
+        uint32_t n;
+        void put(uint32_t c) { o[n++] = (char)c; }
+    } col{out, 0};
+    uint32_t nl = name_len_l1(msg, 0, len, 12);
+    if (nl > 0) name_emit(msg, 0, len, 12, col);
+    *outlen = col.n;
+    return nl;
+}
+
+// parseResources(queryOnly) outcome: ok, has_query, qtype
+void h_dns_parse(const uint8_t *msg, uint32_t len, int *ok, int *has_query, uint32_t *qtype)
+{
+    DnsInfo d;
+    uint32_t qd = be16(msg, 4), an = be16(msg, 6), ns = be16(msg, 8), ar = be16(msg, 10);
+    dns_parse(msg, 0, len, qd, an, ns, ar, d);
+    *ok = d.ok; *has_query = d.has_query; *qtype = d.qtype;
+}
+
+// lower-case name stats: length, murmur (CPC) halves, aggregateDomain suffix starts
+void h_name_stats(const uint8_t *msg, uint32_t len, uint32_t *n, uint64_t *h1, uint64_t *h2, int *q2, int *q3)
+{
+    NameStats st;
+    st.init();
+    uint32_t nl = name_len_l1(msg, 0, len, 12);
+    if (nl > 0) name_emit(msg, 0, len, 12, st);
+    *n = st.n;
+    st.mm.finish(*h1, *h2);
+    uint64_t a, b;
+    if (st.n) agg_domain(st, *q2, *q3, a, b); else { *q2 = 0; *q3 = -1; }
+}
+}
