@@ -40,6 +40,7 @@ extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_xact_keys(const PvXEvent *ev, uint32_t n, uint64_t *skeys, uint32_t *svals);
 extern "C" __global__ void pv_xact_resolve(PvXactParams X);
+extern "C" __global__ void pv_xact_slow(PvXactParams X, uint32_t n_valid);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
                                           uint32_t *vout, size_t n, hipStream_t s);
 
@@ -231,6 +232,11 @@ struct pv_ctx {
     void *d_sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     PvXValue *d_xvals = nullptr;
+    PvXValid *d_valid = nullptr;
+    uint32_t *d_nvals = nullptr;  // [0] values appended since reset, [1] deferred slow candidates
+    uint32_t gen[PV_SLOTS] = {0}; // bumped when a slot is recycled; values carry slot | gen << 8
+    size_t xvals_synced = 0;
+    float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
     uint32_t *d_status = nullptr;
     uint64_t max_records = 0;
     // host-path staging
@@ -336,9 +342,7 @@ void clear_slot(pv_ctx *c, uint32_t s, int64_t rel_base)
     c->meta[s] = SlotMeta();
     c->meta[s].rel_base = rel_base;
     c->slot_used[s] = true;
-    // drop host-side values of a recycled slot
-    c->xvals_host.erase(std::remove_if(c->xvals_host.begin(), c->xvals_host.end(), [s](const PvXValue &v) { return v.slot == s; }),
-                        c->xvals_host.end());
+    c->gen[s] = (c->gen[s] + 1) & 0xffffff; // values of the previous use of this slot no longer match
     c->remote_topn.erase(s);
 }
 
@@ -507,8 +511,9 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, cons
         int rc = read_topn(c, s, recs);
         if (rc) return rc;
         for (auto &r : recs) b.tops[PV_KEY_METRIC(r.key)][r.name] += r.count;
+        const uint32_t sg = s | (c->gen[s] << 8);
         for (auto &v : c->xvals_host) {
-            if (v.slot != s) continue;
+            if (v.slot != sg) continue;
             if (v.kind == XV_FROM_US) b.from_us.push_back(v.bits);
             else if (v.kind == XV_TO_US) b.to_us.push_back(v.bits);
             else { double d; memcpy(&d, &v.bits, 8); b.ratio.push_back(d); }
@@ -688,6 +693,38 @@ void dns_json(pv_ctx *c, Json &j, const HostBucket &b)
     top_json(j, "top_qtype", dense_tops(&b.sum[PV_OFF_QTYPE], PV_QTYPE_BINS, 1), topn);
 }
 
+// KLL inclusive rank rule on exact data
+uint64_t quantile_at(std::vector<uint64_t> v, double r)
+{
+    std::sort(v.begin(), v.end());
+    uint64_t w = (uint64_t)std::ceil(r * (double)v.size());
+    size_t idx = w == 0 ? 0 : (size_t)(w - 1);
+    if (idx >= v.size()) idx = v.size() - 1;
+    return v[idx];
+}
+
+// copy the transaction values appended on the device since the last sync
+int sync_xvals(pv_ctx *c)
+{
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return c->hipfail(e, "synchronize");
+    uint32_t status[ST_WORDS], nv = 0;
+    if (!hip_ok(e = hipMemcpy(status, c->d_status, sizeof status, hipMemcpyDeviceToHost)) ||
+        !hip_ok(e = hipMemcpy(&nv, c->d_nvals, 4, hipMemcpyDeviceToHost)))
+        return c->hipfail(e, "status");
+    if (status[ST_FLAGS] & PVF_VALUES_FULL || nv > c->max_records * 2)
+        return c->fail(PV_ECAPACITY, "transaction value buffer full");
+    if (nv > c->xvals_synced) {
+        size_t old = c->xvals_host.size(), add = nv - c->xvals_synced;
+        c->xvals_host.resize(old + add);
+        if (!hip_ok(e = hipMemcpy(&c->xvals_host[old], c->d_xvals + c->xvals_synced, add * sizeof(PvXValue),
+                                  hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "transaction values");
+        c->xvals_synced = nv;
+    }
+    return 0;
+}
+
 int window_slots(pv_ctx *c, const Window &w, uint32_t period, bool merged, std::vector<uint32_t> &out)
 {
     out.clear();
@@ -769,7 +806,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_events, (size_t)mr * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)mr * 8)) || !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)mr * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_svals, (size_t)mr * 4)) || !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)mr * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * sizeof(PvXValue))) ||
+        !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
+        !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
+        !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
         !hip_ok(e = hipMalloc(&c->d_status, ST_WORDS * 4)) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
         !hip_ok(e = hipEventCreate(&c->ev_stop))) {
         *out = c;
@@ -789,6 +828,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
+                    c->d_valid, c->d_nvals,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -807,7 +847,11 @@ int pv_reset(pv_ctx *c)
     c->started = c->ended = false;
     c->records_seen = 0;
     c->xvals_host.clear();
+    c->xvals_synced = 0;
+    c->from90 = c->to90 = 0.0f;
     c->remote_topn.clear();
+    hipError_t e = hipMemsetAsync(c->d_nvals, 0, 16, c->stream);
+    if (e != hipSuccess) return c->hipfail(e, "reset");
     return 0;
 }
 
@@ -988,24 +1032,54 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
             return c->hipfail(e, "radix sort");
         PvXactParams X;
         memset(&X, 0, sizeof X);
+        X.P = P;
         X.events = c->d_events;
         X.skeys = c->d_skeys2;
         X.svals = c->d_svals2;
         X.n = nev;
-        X.n_shift = P.n_shift;
-        for (int k = 0; k < PV_MAX_SHIFTS; k++) X.thresh[k] = P.thresh[k];
-        for (int k = 0; k <= PV_MAX_SHIFTS; k++) X.slot_of[k] = P.slot_of[k];
-        X.skip_before = P.skip_before;
         X.ttl_s = c->ttl_s;
         X.ttl_ms = c->ttl_ms;
         X.quantiles = (c->dns_groups & PV_DNS_QUANTILES) ? 1 : 0;
-        X.sum = c->d_sum;
+        for (uint32_t k = 0; k <= P.n_shift; k++) {
+            X.slot_gen[k] = P.slot_of[k] | (c->gen[P.slot_of[k]] << 8);
+            X.thr_from[k] = k == 0 ? c->from90 : -1.0f;
+            X.thr_to[k] = k == 0 ? c->to90 : -1.0f;
+        }
         X.vals = c->d_xvals;
-        X.n_vals = c->d_status + ST_NVALS;
-        X.vals_cap = (uint32_t)c->max_records;
-        X.flags = c->d_status + ST_FLAGS;
+        X.n_vals = c->d_nvals;
+        X.vals_cap = (uint32_t)(c->max_records * 2);
+        X.valid = c->d_valid;
+        X.n_valid = c->d_nvals + 1;
         hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, X);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
+        if (P.n_shift > 0 && (c->dns_groups & PV_DNS_QUANTILES)) {
+            // on_period_shift: slow thresholds = p90 of the bucket that just closed
+            // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
+            int rc = sync_xvals(c);
+            if (rc) return rc;
+            for (uint32_t k = 1; k <= P.n_shift; k++) {
+                const uint32_t sg = P.slot_of[k - 1] | (c->gen[P.slot_of[k - 1]] << 8);
+                std::vector<uint64_t> fr, to;
+                for (auto &v : c->xvals_host) {
+                    if (v.slot != sg) continue;
+                    if (v.kind == XV_FROM_US) fr.push_back(v.bits);
+                    else if (v.kind == XV_TO_US) to.push_back(v.bits);
+                }
+                if (!fr.empty()) c->from90 = (float)quantile_at(fr, 0.90);
+                if (!to.empty()) c->to90 = (float)quantile_at(to, 0.90);
+                X.thr_from[k] = c->from90;
+                X.thr_to[k] = c->to90;
+            }
+            uint32_t nvalid = 0;
+            if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
+            if (nvalid) {
+                hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st, X, nvalid);
+                if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_slow");
+            }
+            uint32_t zero = 0;
+            hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st);
+            hipStreamSynchronize(st);
+        }
     }
 
     // ---- window bookkeeping (host mirror of _period_shift)
@@ -1033,19 +1107,6 @@ int pv_synchronize(pv_ctx *c)
     hipSetDevice(c->device);
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return c->hipfail(e, "synchronize");
-    // pull transaction values produced so far
-    uint32_t status[ST_WORDS];
-    if (!hip_ok(e = hipMemcpy(status, c->d_status, sizeof status, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
-    uint32_t nv = std::min<uint32_t>(status[ST_NVALS], (uint32_t)c->max_records);
-    if (status[ST_FLAGS] & PVF_VALUES_FULL) return c->fail(PV_ECAPACITY, "transaction value buffer full");
-    if (nv) {
-        size_t old = c->xvals_host.size();
-        c->xvals_host.resize(old + nv);
-        if (!hip_ok(e = hipMemcpy(&c->xvals_host[old], c->d_xvals, nv * sizeof(PvXValue), hipMemcpyDeviceToHost)))
-            return c->hipfail(e, "transaction values");
-        uint32_t zero = 0;
-        hipMemcpy(c->d_status + ST_NVALS, &zero, 4, hipMemcpyHostToDevice);
-    }
     return 0;
 }
 
@@ -1103,7 +1164,7 @@ int pv_set_end_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
 int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
 {
     *out = nullptr;
-    int rc = pv_synchronize(c);
+    int rc = sync_xvals(c);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->started) return c->fail(PV_EINVAL, "no data");

@@ -100,7 +100,7 @@ __device__ uint32_t write_name(const PvParams &P, uint32_t slot, uint32_t metric
     arena[pos] = (uint8_t)(slen & 0xff);
     arena[pos + 1] = (uint8_t)(slen >> 8);
     if (slen > 0 && nl > 0) {
-        CopyEmit ce{arena + pos + 2, (uint32_t)start, 0};
+        CopyEmit ce{arena + pos + 2, (uint32_t)start, 0, (metric == TM_SLOW_IN || metric == TM_SLOW_OUT) ? 1u : 0u};
         name_emit(R, m, len, 12, ce);
     }
     return (uint32_t)pos + 1;
@@ -421,21 +421,41 @@ extern "C" __global__ void pv_xact_keys(const PvXEvent *ev, uint32_t n, uint64_t
 namespace {
 // first shift k (1-based period index) after period `a` whose threshold purges a
 // query started at `sec`; returns 0 if none inside this batch
-__device__ __forceinline__ uint32_t purge_period(const PvXactParams &X, uint32_t a, int64_t sec)
+__device__ __forceinline__ uint32_t purge_period(const PvParams &P, uint32_t ttl_s, uint32_t a, int64_t sec)
 {
-    for (uint32_t k = a + 1; k <= X.n_shift; k++)
-        if (X.thresh[k - 1] >= (int64_t)X.ttl_s + sec) return k;
+    for (uint32_t k = a + 1; k <= P.n_shift; k++)
+        if (P.thresh[k - 1] >= (int64_t)ttl_s + sec) return k;
     return 0;
 }
-__device__ __forceinline__ void xctr(const PvXactParams &X, uint32_t slot, uint32_t c)
+__device__ __forceinline__ void xctr(const PvParams &P, uint32_t slot, uint32_t c)
 {
-    atomicAdd((unsigned long long *)&X.sum[(uint64_t)slot * PV_SUM_WORDS + PV_OFF_DNS + c], 1ull);
+    atomicAdd((unsigned long long *)&P.sum[(uint64_t)slot * PV_SUM_WORDS + PV_OFF_DNS + c], 1ull);
 }
-__device__ __forceinline__ void xval(const PvXactParams &X, uint32_t slot, uint32_t kind, uint64_t bits)
+__device__ __forceinline__ void xval(const PvXactParams &X, uint32_t period, uint32_t kind, uint64_t bits)
 {
     uint32_t p = atomicAdd(X.n_vals, 1u);
-    if (p >= X.vals_cap) { atomicOr(X.flags, PVF_VALUES_FULL); return; }
-    X.vals[p] = PvXValue{bits, slot, kind};
+    if (p >= X.vals_cap) { atomicOr(X.P.flags, PVF_VALUES_FULL); return; }
+    X.vals[p] = PvXValue{bits, X.slot_gen[period], kind};
+}
+// DnsMetricsBucket::new_dns_transaction slow branch (dns/v1 ...cpp:1126-1136): the
+// response's first query name (getName(), case kept) into top_slow
+__device__ void slow_check(const PvXactParams &X, uint32_t idx, uint32_t period, uint32_t dir, uint64_t us)
+{
+    const float thr = dir == 0 ? X.thr_from[period] : (dir == 1 ? X.thr_to[period] : 0.0f);
+    if (!(thr > 0.0f && (float)us >= thr)) return;
+    const PvParams &P = X.P;
+    Parsed o;
+    parse_record(P, P.offs[idx], o);
+    const uint8_t *R = P.recs;
+    uint64_t m = o.l4off + 8;
+    uint32_t len = o.l4len - 8;
+    DnsInfo d;
+    dns_parse(R, m, len, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8), be16(R, m + 10), d);
+    if (!(d.ok && d.has_query)) return;
+    RawName rn{0, 0};
+    if (d.name_len_enc > 0) name_emit(R, m, len, 12, rn);
+    const uint32_t metric = dir == 0 ? TM_SLOW_OUT : TM_SLOW_IN;
+    global_add(P, P.slot_of[period], PV_KEY(metric, fp56(rn.ph, rn.n, 1)), 1, idx);
 }
 } // namespace
 
@@ -443,6 +463,7 @@ extern "C" __global__ void pv_xact_resolve(PvXactParams X)
 {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= X.n) return;
+    const PvParams &P = X.P;
     const PvXEvent e = X.events[X.svals[p]];
     const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
     if (e.qr) {
@@ -453,36 +474,56 @@ extern "C" __global__ void pv_xact_resolve(PvXactParams X)
         if (q < 0 || (uint32_t)(X.skeys[q] >> 32) != h) return; // NotExist
         const PvXEvent qe = X.events[X.svals[q]];
         if (qe.qr) return; // previous event was a response: erased => NotExist
-        uint32_t kp = purge_period(X, qe.period, qe.sec);
+        uint32_t kp = purge_period(P, X.ttl_s, qe.period, qe.sec);
         if (kp && kp <= e.period) return; // purged at a period shift before this response
-        if (e.period < X.skip_before) return;
-        const uint32_t slot = X.slot_of[e.period];
+        const bool kept = e.period >= P.skip_before;
+        const uint32_t slot = P.slot_of[e.period];
         // timespec_diff(endTS, startTS) (TransactionManager.h:24-37)
         int64_t dsec = e.sec > qe.sec ? e.sec - qe.sec : qe.sec - e.sec;
         int64_t dnsec = (int64_t)e.nsec - (int64_t)qe.nsec;
         if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
         bool timed_out = dsec > (int64_t)X.ttl_s || (dsec == (int64_t)X.ttl_s && ((double)dnsec / 1.0e6) >= (double)X.ttl_ms);
-        if (timed_out) { xctr(X, slot, DC_XTIMEOUT); return; }
+        if (timed_out) { if (kept) xctr(P, slot, DC_XTIMEOUT); return; }
         // DnsMetricsBucket::new_dns_transaction (dns/v1 ...cpp:1093-1138)
         uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
-        xctr(X, slot, DC_XTOTAL);
-        if (e.dir == 0) { xctr(X, slot, DC_XOUT); if (X.quantiles) xval(X, slot, XV_FROM_US, us); }
-        else if (e.dir == 1) { xctr(X, slot, DC_XIN); if (X.quantiles) xval(X, slot, XV_TO_US, us); }
-        if (qe.len && X.quantiles) {
-            double r = (double)e.len / (double)qe.len;
-            xval(X, slot, XV_RATIO, (uint64_t)__double_as_longlong(r));
+        if (kept) {
+            xctr(P, slot, DC_XTOTAL);
+            if (e.dir == 0) xctr(P, slot, DC_XOUT);
+            else if (e.dir == 1) xctr(P, slot, DC_XIN);
+        }
+        // quantile inputs of every period (skipped ones still feed the next period's p90)
+        if (X.quantiles) {
+            if (e.dir == 0) xval(X, e.period, XV_FROM_US, us);
+            else if (e.dir == 1) xval(X, e.period, XV_TO_US, us);
+            if (qe.len && kept) xval(X, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
+        }
+        if (!kept || e.dir == 2) return;
+        if (X.thr_from[e.period] < 0.0f) {
+            uint32_t v = atomicAdd(X.n_valid, 1u);
+            X.valid[v] = PvXValid{e.idx, e.period, e.dir, 0, 0, us};
+        } else {
+            slow_check(X, e.idx, e.period, e.dir, us);
         }
     } else {
         // an open query purged at a later period shift counts as timed out there
-        uint32_t kp = purge_period(X, e.period, e.sec);
+        uint32_t kp = purge_period(P, X.ttl_s, e.period, e.sec);
         if (!kp) return;
         uint32_t q = p + 1;
         for (; q < X.n && (uint32_t)(X.skeys[q] >> 32) == h; q++)
             if (X.events[X.svals[q]].key == e.key) break;
         if (q < X.n && (uint32_t)(X.skeys[q] >> 32) == h && X.events[X.svals[q]].period < kp) return;
-        if (kp < X.skip_before) return;
-        xctr(X, X.slot_of[kp], DC_XTIMEOUT);
+        if (kp < P.skip_before) return;
+        xctr(P, P.slot_of[kp], DC_XTIMEOUT);
     }
+}
+
+// top_slow for transactions of periods whose threshold became known after the resolve
+extern "C" __global__ void pv_xact_slow(PvXactParams X, uint32_t n_valid)
+{
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_valid) return;
+    const PvXValid v = X.valid[i];
+    slow_check(X, v.idx, v.period, v.dir, v.us);
 }
 
 // Stable LSD radix sort of (key, value) pairs over all 64 key bits (rocPRIM onesweep).

@@ -99,27 +99,17 @@ struct PvXEvent {
 enum { XV_FROM_US = 0, XV_TO_US = 1, XV_RATIO = 2 };
 struct PvXValue {
     uint64_t bits; // uint64 microseconds, or the IEEE-754 bits of the double ratio
-    uint32_t slot;
+    uint32_t slot; // slot | generation << 8
     uint32_t kind;
 };
 
-struct PvXactParams {
-    const PvXEvent *events;
-    const uint64_t *skeys; // sorted (hash32(key) << 32 | idx)
-    const uint32_t *svals; // event position for each sorted key
-    uint32_t n;
-    uint32_t n_shift;
-    int64_t thresh[PV_MAX_SHIFTS];
-    uint32_t slot_of[PV_MAX_SHIFTS + 1];
-    uint32_t skip_before;
-    uint32_t ttl_s, ttl_ms;
-    uint32_t quantiles;
-    uint64_t *sum;
-    PvXValue *vals;
-    uint32_t *n_vals;
-    uint32_t vals_cap;
-    uint32_t *flags;
+// a valid transaction whose period's slow threshold is not known yet
+struct PvXValid {
+    uint32_t idx; // response record index within the batch
+    uint8_t period, dir, pad0, pad1;
+    uint64_t us;
 };
+
 
 struct PvSubnets {
     uint32_t n4, n6;
@@ -160,4 +150,22 @@ struct PvParams {
     uint32_t *flags;
     uint32_t *dns_first; // per period: min record index of a DNS event in that period
     uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
+};
+
+struct PvXactParams {
+    PvParams P;            // record access + top-N tables (slow transaction names)
+    const PvXEvent *events;
+    const uint64_t *skeys; // sorted (hash32(key) << 32 | idx)
+    const uint32_t *svals; // event position for each sorted key
+    uint32_t n;
+    uint32_t ttl_s, ttl_ms;
+    uint32_t quantiles;
+    uint32_t slot_gen[PV_MAX_SHIFTS + 1]; // slot | generation << 8 per period
+    float thr_from[PV_MAX_SHIFTS + 1];    // p90 slow thresholds per period, < 0 = not known yet
+    float thr_to[PV_MAX_SHIFTS + 1];
+    PvXValue *vals;
+    uint32_t *n_vals;
+    uint32_t vals_cap;
+    PvXValid *valid;
+    uint32_t *n_valid;
 };

@@ -443,9 +443,20 @@ struct CountEmit {
 struct CopyEmit {
     uint8_t *dst;
     uint32_t from, n;
+    uint32_t raw; // 1: keep case (DnsQuery::getName), 0: lower case (getNameLower)
     PV_FN void put(uint32_t c)
     {
-        if (n >= from) dst[n - from] = (uint8_t)lower(c);
+        if (n >= from) dst[n - from] = (uint8_t)(raw ? c : lower(c));
+        n++;
+    }
+};
+// case-preserving polynomial hash of a name (top_slow keys use getName())
+struct RawName {
+    uint64_t ph;
+    uint32_t n;
+    PV_FN void put(uint32_t c)
+    {
+        ph = addmod61(mulmod61(ph, PBASE), c + 1);
         n++;
     }
 };
