@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--records", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--net-groups", type=int, default=0, help="pv_net_group bits (0 = reference defaults)")
+    ap.add_argument("--dns-groups", type=int, default=0, help="pv_dns_group bits (0 = reference defaults)")
+    ap.add_argument("--read-ceiling", action="store_true", help="also time a plain read of the blob (HBM ceiling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -67,7 +70,8 @@ def main():
     torch.cuda.synchronize(device)
     algo_bytes = used  # sum over records of (16 + caplen)
 
-    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=n, device=local)
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=n, device=local,
+                      net_groups=args.net_groups, dns_groups=args.dns_groups)
     h.set_global_base(rank * n)
 
     def step():
@@ -132,12 +136,30 @@ def main():
                          "kernel": "pv_net_dns_kernel", "kernel_ms": round(kernel_ms, 4),
                          "bytes_per_launch": algo_bytes},
         }
+        if args.read_ceiling:
+            line["read_ceiling_gbs"] = read_ceiling(d_recs, used)
+        if args.net_groups or args.dns_groups:
+            line["groups"] = {"net": args.net_groups, "dns": args.dns_groups}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def read_ceiling(d_recs, used: int) -> float:
+    """GB/s of a plain full read of the same blob (torch reduction), for reference."""
+    import torch
+    v = d_recs[: used // 8 * 8].view(torch.int64)
+    for _ in range(3):
+        v.sum()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        v.sum()
+    torch.cuda.synchronize()
+    return round(used * 10 / (time.perf_counter() - t0) / 1e9, 1)
 
 
 def traffic_from_profile(cfg: int, n: int):
