@@ -35,12 +35,12 @@
 #include "../../include/pvgpu.h"
 #include "pv_layout.h"
 
-extern "C" __global__ void pv_net_dns_kernel(PvParams P);
+extern "C" __global__ void pv_net_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_xact_keys(const PvXEvent *ev, uint32_t n, uint64_t *skeys, uint32_t *svals);
-extern "C" __global__ void pv_xact_resolve(PvXactParams X);
-extern "C" __global__ void pv_xact_slow(PvXactParams X, uint32_t n_valid);
+extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
+extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
                                           uint32_t *vout, size_t n, hipStream_t s);
 
@@ -238,6 +238,8 @@ struct pv_ctx {
     size_t xvals_synced = 0;
     float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
     uint32_t *d_status = nullptr;
+    PvParams *d_params = nullptr;      // kernel parameter blocks (device memory)
+    PvXactParams *d_xparams = nullptr;
     uint64_t max_records = 0;
     // host-path staging
     uint8_t *d_recs = nullptr;
@@ -809,7 +811,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
-        !hip_ok(e = hipMalloc(&c->d_status, ST_WORDS * 4)) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
+        !hip_ok(e = hipMalloc(&c->d_status, ST_WORDS * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_params, sizeof(PvParams))) ||
+        !hip_ok(e = hipMalloc(&c->d_xparams, sizeof(PvXactParams))) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
         !hip_ok(e = hipEventCreate(&c->ev_stop))) {
         *out = c;
         return c->hipfail(e, "device allocation");
@@ -828,7 +832,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -901,7 +905,6 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
                       const uint32_t *sc_idx, const uint32_t *sc_sec, void *stream)
 {
     std::lock_guard<std::mutex> g(c->mu);
-    (void)sc_idx;
     hipSetDevice(c->device);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     hipStream_t saved = c->stream;
@@ -916,6 +919,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     // ---- period shifts inside this batch (AbstractMetricsManager::new_event)
     const uint32_t np = c->cfg.num_periods;
     std::vector<int64_t> thresh;
+    std::vector<uint64_t> pstart; // first record index of each new period (monotone runs)
     if (np > 1) {
         int64_t T = c->net.next_shift_sec;
         if (info->last_sec >= T || !info->monotone) {
@@ -928,6 +932,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
                 for (uint32_t k = 0; k < info->n_sec_changes; k++) {
                     if ((int64_t)sc_sec[k] >= T) {
                         thresh.push_back(sc_sec[k]);
+                        pstart.push_back(sc_idx[k]);
                         T = (int64_t)sc_sec[k] + 60;
                     }
                 }
@@ -947,7 +952,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.net_groups = c->net_groups;
     P.dns_groups = c->dns_groups;
     P.n_shift = (uint32_t)thresh.size();
-    for (size_t k = 0; k < thresh.size(); k++) P.thresh[k] = thresh[k];
+    for (size_t k = 0; k < thresh.size(); k++) { P.thresh[k] = thresh[k]; P.pstart[k] = pstart[k]; }
     P.skip_before = P.n_shift + 1 > np ? P.n_shift + 1 - np : 0;
     P.gbase = c->global_base + c->records_seen;
     P.nets = c->nets;
@@ -989,13 +994,16 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.dns_first = c->d_status + ST_DNS_ANY;
     P.dns_at_thresh = c->d_status + ST_DNS_AT;
     launch_fill32(c, c->d_status, ST_WORDS, 0);
+    hipError_t e;
     int dev_cus = 256;
     hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     uint64_t tiles = (n + 255) / 256;
     uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)dev_cus * 3);
+    if (!hip_ok(e = hipMemcpyAsync(c->d_params, &P, sizeof P, hipMemcpyHostToDevice, st)))
+        return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
-    hipLaunchKernelGGL(pv_net_dns_kernel, dim3(grid), dim3(256), 0, st, P);
-    hipError_t e = hipGetLastError();
+    hipLaunchKernelGGL(pv_net_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_dns_kernel");
     hipEventRecord(c->ev_stop, st);
 
@@ -1050,7 +1058,9 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         X.vals_cap = (uint32_t)(c->max_records * 2);
         X.valid = c->d_valid;
         X.n_valid = c->d_nvals + 1;
-        hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, X);
+        if (!hip_ok(e = hipMemcpyAsync(c->d_xparams, &X, sizeof X, hipMemcpyHostToDevice, st)))
+            return c->hipfail(e, "parameter upload");
+        hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
         if (P.n_shift > 0 && (c->dns_groups & PV_DNS_QUANTILES)) {
             // on_period_shift: slow thresholds = p90 of the bucket that just closed
@@ -1073,7 +1083,10 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
             uint32_t nvalid = 0;
             if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
             if (nvalid) {
-                hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st, X, nvalid);
+                if (!hip_ok(e = hipMemcpyAsync(c->d_xparams, &X, sizeof X, hipMemcpyHostToDevice, st)))
+                    return c->hipfail(e, "parameter upload");
+                hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st,
+                                   (const PvXactParams *)c->d_xparams, nvalid);
                 if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_slow");
             }
             uint32_t zero = 0;

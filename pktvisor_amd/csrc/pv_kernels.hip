@@ -29,54 +29,75 @@
 
 #define PV_BLOCK 256
 #define PV_CACHE_N 2048
-#define PV_HIST_N 4096
-#define PV_LDS_CTRS 64
-
-namespace {
+#define PV_HIST_N 2048
+#define PV_WIN 128              // bytes of each record staged into LDS (record header + frame start)
+#define PV_WINW (PV_WIN / 4)
 
 // ------------------------------------------------------------------ byte access
-// recs is 256-B aligned and padded by >= 64 bytes: two aligned dword loads and
-// v_alignbyte give an unaligned little-endian u32 without byte loops.
+// recs is 256-B aligned and padded by >= 256 bytes: two aligned dword loads and
+// v_alignbyte give an unaligned little-endian u32.
 __device__ __forceinline__ uint32_t pv_ld32(const uint8_t *base, uint64_t off)
 {
     const uint32_t *p = reinterpret_cast<const uint32_t *>(base + (off & ~3ull));
     uint32_t lo = p[0], hi = p[1];
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
 }
-__device__ __forceinline__ uint32_t pv_ld8(const uint8_t *base, uint64_t off) { return base[off]; }
 __device__ __forceinline__ uint32_t pv_clz64(uint64_t x) { return (uint32_t)__clzll((long long)x); }
-__device__ __forceinline__ uint64_t pv_umulhi(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
 #define PV_FN __device__ __forceinline__
-} // namespace
 #include "pv_parse.h"
+
 namespace {
 
-// ------------------------------------------------------------------ LDS workgroup state
-struct BlockState {
-    uint64_t ckey[PV_CACHE_N];
-    uint32_t ccnt[PV_CACHE_N];
-    uint32_t crep[PV_CACHE_N];
-    uint32_t hist[PV_HIST_N];
-    uint32_t ctr[PV_LDS_CTRS]; // [0,32) net, [32,64) dns
-    uint32_t slot;             // bucket slot the LDS state accumulates for
-    uint32_t tile_slot_lo, tile_slot_hi;
+// HBM accessor
+struct GAcc {
+    const uint8_t *R;
+    PV_FN uint32_t u32(uint64_t off) const { return pv_ld32(R, off); }
+    PV_FN uint32_t u8(uint64_t off) const { return R[off]; }
+};
+
+// Per-lane LDS window over the first PV_WIN bytes from the 16-B aligned start of
+// the lane's record, dword-major ([dword][lane]) so any per-lane offset reads
+// conflict-free; bytes past the window come from HBM.
+struct WAcc {
+    const uint8_t *R;
+    uint64_t wbase;
+    const uint32_t *win; // &win[0][lane]
+    PV_FN uint32_t u32(uint64_t off) const
+    {
+        uint64_t rel = off - wbase;
+        if (rel < PV_WIN - 4) {
+            uint32_t r = (uint32_t)rel;
+            uint32_t lo = win[(r >> 2) * PV_BLOCK], hi = win[((r >> 2) + 1) * PV_BLOCK];
+            return __builtin_amdgcn_alignbyte(hi, lo, r & 3);
+        }
+        return pv_ld32(R, off);
+    }
+    PV_FN uint32_t u8(uint64_t off) const
+    {
+        uint64_t rel = off - wbase;
+        if (rel < PV_WIN) {
+            uint32_t r = (uint32_t)rel;
+            return (win[(r >> 2) * PV_BLOCK] >> ((r & 3) * 8)) & 0xff;
+        }
+        return R[off];
+    }
 };
 
 __device__ __forceinline__ uint64_t *slot_sum(const PvParams &P, uint32_t slot) { return P.sum + (uint64_t)slot * PV_SUM_WORDS; }
 
 // Writes the name record for a newly created global top-N entry (arena: u16 len + bytes).
-__device__ uint32_t write_name(const PvParams &P, uint32_t slot, uint32_t metric, uint32_t rep)
+__device__ __noinline__ uint32_t write_name(const PvParams &P, uint32_t slot, uint32_t metric, uint32_t rep)
 {
     Parsed o;
-    parse_record(P, P.offs[rep], o);
-    const uint8_t *R = P.recs;
+    const GAcc R{P.recs};
+    parse_record(R, P, P.offs[rep], o);
     uint8_t *arena = P.arena + (uint64_t)slot * P.arena_cap;
     if (metric == TM_IPV6) {
         uint64_t a = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
         uint64_t pos = atomicAdd((unsigned long long *)&P.arena_top[slot], 18ull);
         if (pos + 18 > P.arena_cap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
         arena[pos] = 16; arena[pos + 1] = 0;
-        for (int i = 0; i < 16; i++) arena[pos + 2 + i] = (uint8_t)ld8(R, a + i);
+        for (int i = 0; i < 16; i++) arena[pos + 2 + i] = (uint8_t)R.u8(a + i);
         return (uint32_t)pos + 1;
     }
     // DNS names: re-derive the first query name of the record
@@ -106,33 +127,47 @@ __device__ uint32_t write_name(const PvParams &P, uint32_t slot, uint32_t metric
     return (uint32_t)pos + 1;
 }
 
-__device__ void global_add(const PvParams &P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
+__device__ __noinline__ void global_add(const PvParams &P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
 {
     uint32_t metric = PV_KEY_METRIC(key);
     uint64_t *sum = slot_sum(P, slot);
     if (metric == TM_DENSE_PORT) { atomicAdd((unsigned long long *)&sum[PV_OFF_PORT + (key & 0xffff)], (unsigned long long)w); return; }
     if (metric == TM_DENSE_QTYPE) { atomicAdd((unsigned long long *)&sum[PV_OFF_QTYPE + (key & 0xffff)], (unsigned long long)w); return; }
     if (metric == TM_DENSE_RCODE) { atomicAdd((unsigned long long *)&sum[PV_OFF_RCODE + (key & 0xf)], (unsigned long long)w); return; }
-    uint64_t cap = 1ull << P.tcap_log2;
-    uint64_t base = (uint64_t)slot << P.tcap_log2;
+    const uint64_t cap = 1ull << P.tcap_log2;
+    const uint64_t base = (uint64_t)slot << P.tcap_log2;
     uint64_t h = fmix64(key ^ 0x5bd1e995ULL) & (cap - 1);
-    for (int probe = 0; probe < 128; probe++) {
+    // the probe loop only claims / finds the entry; a new entry's name record is
+    // written once after it, so lanes never serialise on name decoding inside it
+    int64_t created = -1;
+    bool done = false;
+    for (int probe = 0; probe < 128 && !done; probe++) {
         uint64_t *kp = &P.tkeys[base + h];
         uint64_t k = __atomic_load_n(kp, __ATOMIC_RELAXED);
-        if (k == key) { atomicAdd((unsigned long long *)&P.tcnt[base + h], (unsigned long long)w); return; }
         if (k == 0) {
             uint64_t prev = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)key);
-            if (prev == 0) {
-                atomicAdd((unsigned long long *)&P.tcnt[base + h], (unsigned long long)w);
-                if (metric != TM_IPV4) P.taux[base + h] = write_name(P, slot, metric, rep);
-                return;
-            }
-            if (prev == key) { atomicAdd((unsigned long long *)&P.tcnt[base + h], (unsigned long long)w); return; }
+            if (prev == 0) created = (int64_t)h;
+            k = prev == 0 ? key : prev;
         }
-        h = (h + 1) & (cap - 1);
+        if (k == key) {
+            atomicAdd((unsigned long long *)&P.tcnt[base + h], (unsigned long long)w);
+            done = true;
+        } else {
+            h = (h + 1) & (cap - 1);
+        }
     }
-    atomicOr(P.flags, PVF_TABLE_FULL);
+    if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
+    if (created >= 0 && metric != TM_IPV4) P.taux[base + (uint64_t)created] = write_name(P, slot, metric, rep);
 }
+
+// ------------------------------------------------------------------ LDS workgroup state
+struct BlockState {
+    uint32_t win[PV_WINW][PV_BLOCK]; // record windows
+    uint64_t ckey[PV_CACHE_N];       // key -> count cache for top-N and dense tables
+    uint32_t ccnt[PV_CACHE_N];
+    uint32_t crep[PV_CACHE_N];
+    uint32_t hist[PV_HIST_N];        // payload-size histogram (caplen < PV_HIST_N)
+};
 
 // LDS key cache: returns false when the probe window is full (caller goes global)
 __device__ __forceinline__ bool cache_add(BlockState &S, uint64_t key, uint32_t w, uint32_t rep)
@@ -157,18 +192,64 @@ __device__ __forceinline__ void top_add(const PvParams &P, BlockState &S, bool c
     if (!(cached && cache_add(S, key, w, rep))) global_add(P, slot, key, w, rep);
 }
 
-__device__ void block_init(BlockState &S)
+__device__ __forceinline__ void cpc_add(const PvParams &P, uint32_t slot, uint32_t sketch, uint32_t coupon, int64_t gidx)
+{
+    int64_t *t = P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)sketch * PV_CPC_COUPONS + coupon;
+    if (__atomic_load_n(t, __ATOMIC_RELAXED) > gidx) atomicMin((long long *)t, (long long)gidx);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// per-lane counters of the current bucket slot, kept in registers
+struct Ctr {
+    uint32_t nev, nin, nout, nunk, n4, n6, nudp, ntcp, nsyn, noth;
+    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata;
+    PV_FN void zero()
+    {
+        nev = nin = nout = nunk = n4 = n6 = nudp = ntcp = nsyn = noth = 0;
+        dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = 0;
+    }
+};
+
+// wave-reduce the register counters and add them to the slot's SUM region
+__device__ void ctr_flush(const PvParams &P, uint32_t slot, Ctr &c)
+{
+    uint64_t *s = slot_sum(P, slot);
+    const bool lead = (threadIdx.x & 63) == 0;
+    const bool nc = P.net_groups & PV_NET_COUNTERS_BIT, dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
+#define PV_FL(field, word, on)                                                              \
+    {                                                                                       \
+        uint32_t v = wave_sum(c.field);                                                     \
+        if (lead && v && (on)) atomicAdd((unsigned long long *)&s[word], (unsigned long long)v); \
+    }
+    PV_FL(nev, PV_OFF_NET + NC_EVENTS, true) PV_FL(nev, PV_OFF_NET + NC_SAMPLES, true)
+    PV_FL(nev, PV_OFF_NET + NC_TOTAL, nc) PV_FL(nin, PV_OFF_NET + NC_IN, nc) PV_FL(nout, PV_OFF_NET + NC_OUT, nc)
+    PV_FL(nunk, PV_OFF_NET + NC_UNK, nc) PV_FL(n4, PV_OFF_NET + NC_V4, nc) PV_FL(n6, PV_OFF_NET + NC_V6, nc)
+    PV_FL(nudp, PV_OFF_NET + NC_UDP, nc) PV_FL(ntcp, PV_OFF_NET + NC_TCP, nc) PV_FL(nsyn, PV_OFF_NET + NC_SYN, nc)
+    PV_FL(noth, PV_OFF_NET + NC_OTHER, nc)
+    PV_FL(dev, PV_OFF_DNS + DC_EVENTS, true) PV_FL(dev, PV_OFF_DNS + DC_SAMPLES, true)
+    PV_FL(dev, PV_OFF_DNS + DC_TOTAL, dc) PV_FL(dev, PV_OFF_DNS + DC_UDP, dc) PV_FL(dq, PV_OFF_DNS + DC_QUERIES, dc)
+    PV_FL(dr, PV_OFF_DNS + DC_REPLIES, dc) PV_FL(d4, PV_OFF_DNS + DC_V4, dc) PV_FL(d6, PV_OFF_DNS + DC_V6, dc)
+    PV_FL(dnx, PV_OFF_DNS + DC_NX, dc) PV_FL(dref, PV_OFF_DNS + DC_REFUSED, dc) PV_FL(dsrv, PV_OFF_DNS + DC_SRVFAIL, dc)
+    PV_FL(dnoerr, PV_OFF_DNS + DC_NOERROR, dc) PV_FL(dnodata, PV_OFF_DNS + DC_NODATA, dc)
+#undef PV_FL
+    c.zero();
+}
+
+__device__ void block_clear(BlockState &S)
 {
     for (uint32_t i = threadIdx.x; i < PV_CACHE_N; i += PV_BLOCK) { S.ckey[i] = 0; S.ccnt[i] = 0; }
     for (uint32_t i = threadIdx.x; i < PV_HIST_N; i += PV_BLOCK) S.hist[i] = 0;
-    for (uint32_t i = threadIdx.x; i < PV_LDS_CTRS; i += PV_BLOCK) S.ctr[i] = 0;
 }
 
-// Flush the LDS partial bucket of S.slot to HBM and clear it (all threads).
-__device__ void block_flush(const PvParams &P, BlockState &S)
+// Flush the LDS partial bucket of `slot` to HBM and clear it (all threads, block-uniform).
+__device__ void block_flush(const PvParams &P, BlockState &S, uint32_t slot)
 {
     __syncthreads();
-    uint32_t slot = S.slot;
     if (slot < PV_SLOTS) {
         uint64_t *sum = slot_sum(P, slot);
         for (uint32_t i = threadIdx.x; i < PV_CACHE_N; i += PV_BLOCK) {
@@ -177,221 +258,273 @@ __device__ void block_flush(const PvParams &P, BlockState &S)
         }
         for (uint32_t i = threadIdx.x; i < PV_HIST_N; i += PV_BLOCK)
             if (S.hist[i]) atomicAdd((unsigned long long *)&sum[PV_OFF_PAYLOAD + i], (unsigned long long)S.hist[i]);
-        for (uint32_t i = threadIdx.x; i < PV_LDS_CTRS; i += PV_BLOCK)
-            if (S.ctr[i]) atomicAdd((unsigned long long *)&sum[(i < 32 ? PV_OFF_NET + i : PV_OFF_DNS + (i - 32))],
-                                    (unsigned long long)S.ctr[i]);
     }
     __syncthreads();
-    block_init(S);
+    block_clear(S);
     __syncthreads();
 }
 
-// wave-aggregated counter increment into LDS (lane-uniform slot) or HBM
-__device__ __forceinline__ void ctr_add(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint32_t idx,
-                                        bool flag)
+__device__ __forceinline__ uint32_t period_of(const PvParams &P, uint64_t i)
 {
-    if (cached) {
-        uint64_t b = __ballot(flag);
-        if (b && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)b) - 1)) atomicAdd(&S.ctr[idx], (uint32_t)__popcll(b));
-    } else if (flag) {
-        uint64_t *sum = slot_sum(P, slot);
-        atomicAdd((unsigned long long *)&sum[idx < 32 ? PV_OFF_NET + idx : PV_OFF_DNS + idx - 32], 1ull);
-    }
+    uint32_t p = 0;
+    while (p < P.n_shift && i >= P.pstart[p]) p++;
+    return p;
 }
 
-__device__ __forceinline__ void cpc_add(const PvParams &P, uint32_t slot, uint32_t sketch, uint32_t coupon, int64_t gidx)
+// payload-size histogram: a per-lane run cache in front of the LDS histogram
+__device__ __forceinline__ void hist_put(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint32_t v,
+                                         uint32_t n)
 {
-    int64_t *t = P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)sketch * PV_CPC_COUPONS + coupon;
-    if (__atomic_load_n(t, __ATOMIC_RELAXED) > gidx) atomicMin((long long *)t, (long long)gidx);
+    if (!n) return;
+    if (cached && v < PV_HIST_N) atomicAdd(&S.hist[v], n);
+    else atomicAdd((unsigned long long *)&slot_sum(P, slot)[PV_OFF_PAYLOAD + v], (unsigned long long)n);
+}
+
+// DNS v1 over UDP for one lane (DnsStreamHandler::process_udp_packet_cb, :270-302, and
+// DnsMetricsBucket::process_dns_layer, :910-1049)
+template <class A>
+__device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const A &R, const Parsed &o, bool cached,
+                                         bool upd, uint32_t slot, uint32_t period, uint64_t i, Ctr &c)
+{
+    uint32_t pw = R.u32(o.l4off);
+    uint32_t sport = ((pw & 0xff) << 8) | ((pw >> 8) & 0xff);
+    uint32_t dport = ((pw >> 8) & 0xff00) | (pw >> 24);
+    uint32_t metric_port = 0;
+    if (dport == 53 || dport == 5353 || dport == 5355 || dport == 53000) metric_port = sport;
+    else if (sport == 53 || sport == 5353 || sport == 5355 || sport == 53000) metric_port = dport;
+    if (!metric_port) return;
+    const uint64_t m = o.l4off + 8;
+    const uint32_t dlen = o.l4len - 8;
+    // header words; bytes past the capture read as 0 (the reference over-reads there)
+    const uint64_t cap_end = o.frame + o.caplen;
+    uint32_t w0, w1, w2;
+    if (m + 12 <= cap_end) { w0 = R.u32(m); w1 = R.u32(m + 4); w2 = R.u32(m + 8); }
+    else {
+        w0 = w1 = w2 = 0;
+        for (uint32_t b = 0; b < 12; b++) {
+            uint32_t v = (m + b < cap_end) ? R.u8(m + b) : 0;
+            if (b < 4) w0 |= v << (8 * b); else if (b < 8) w1 |= v << (8 * (b - 4)); else w2 |= v << (8 * (b - 8));
+        }
+    }
+    const uint32_t txid = ((w0 & 0xff) << 8) | ((w0 >> 8) & 0xff);
+    const uint32_t qr = (w0 >> 23) & 1;
+    const uint32_t rcode = (w0 >> 24) & 15;
+    const uint32_t qd = ((w1 & 0xff) << 8) | ((w1 >> 8) & 0xff);
+    const uint32_t ancount = ((w1 >> 8) & 0xff00) | (w1 >> 24);
+    const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
+    const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+    if (upd) {
+        c.dev++;
+        c.d4 += o.l3 == 4; c.d6 += o.l3 == 6;
+        c.dq += !qr; c.dr += qr;
+        c.dnoerr += qr && rcode == 0; c.dnodata += qr && rcode == 0 && ancount == 0;
+        c.dsrv += qr && rcode == 2; c.dnx += qr && rcode == 3; c.dref += qr && rcode == 5;
+        DnsInfo d;
+        dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
+        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_PORT, metric_port), 1, (uint32_t)i);
+        if (d.ok) {
+            if (qr) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_RCODE, rcode), 1, (uint32_t)i);
+            if (d.has_query) {
+                NameStats st;
+                st.init();
+                if (d.name_len_enc > 0) name_emit(R, m, dlen, 12, st);
+                uint64_t h1, h2;
+                st.mm.finish(h1, h2);
+                if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT))
+                    cpc_add(P, slot, CPC_QNAME, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
+                top_add(P, S, cached, slot, PV_KEY(TM_DENSE_QTYPE, d.qtype), 1, (uint32_t)i);
+                if (P.dns_groups & PV_DNS_TOP_QNAMES_BIT) {
+                    const uint64_t fp_full = fp56(st.ph, st.n, 0);
+                    if (qr) {
+                        if (rcode == 2) top_add(P, S, cached, slot, PV_KEY(TM_SRVFAIL, fp_full), 1, (uint32_t)i);
+                        else if (rcode == 3) top_add(P, S, cached, slot, PV_KEY(TM_NX, fp_full), 1, (uint32_t)i);
+                        else if (rcode == 5) top_add(P, S, cached, slot, PV_KEY(TM_REFUSED, fp_full), 1, (uint32_t)i);
+                        else if (rcode == 0) {
+                            if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
+                                top_add(P, S, cached, slot, PV_KEY(TM_NOERROR, fp_full), 1, (uint32_t)i);
+                            if (!ancount) top_add(P, S, cached, slot, PV_KEY(TM_NODATA, fp_full), 1, (uint32_t)i);
+                        }
+                        if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
+                            top_add(P, S, cached, slot, PV_KEY(TM_SIZED, fp_full), dlen, (uint32_t)i);
+                    }
+                    int q2, q3;
+                    uint64_t h2p, h3p;
+                    agg_domain(st, q2, q3, h2p, h3p);
+                    const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
+                    top_add(P, S, cached, slot, PV_KEY(TM_QNAME2, fp56(k2, st.n - q2, 0)), 1, (uint32_t)i);
+                    if (q3 >= 0 && (uint32_t)q3 < st.n) {
+                        const uint64_t k3 = q3 == 0 ? st.ph : suffix_hash(st, q3, h3p);
+                        top_add(P, S, cached, slot, PV_KEY(TM_QNAME3, fp56(k3, st.n - q3, 0)), 1, (uint32_t)i);
+                    }
+                }
+            }
+        }
+    }
+    if (P.want_events) {
+        uint32_t e = atomicAdd(P.n_events, 1u);
+        PvXEvent ev;
+        ev.key = ((uint64_t)flowkey(R, o) << 16) | txid;
+        ev.idx = (uint32_t)i;
+        ev.len = dlen;
+        ev.sec = o.sec;
+        ev.nsec = o.nsec;
+        ev.qr = (uint8_t)qr;
+        ev.dir = o.dir;
+        ev.period = (uint8_t)period;
+        ev.pad = 0;
+        P.events[e] = ev;
+    }
+    if (period > 0 && o.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
 }
 
 } // namespace
 
 // ------------------------------------------------------------------ the fused kernel
-extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(PvParams P)
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const PvParams *__restrict__ Pp)
 {
+    const PvParams &P = *Pp; // parameters live in device memory: scalar loads, no stack copy
     __shared__ BlockState S;
-    block_init(S);
-    if (threadIdx.x == 0) S.slot = 0xffffffffu;
+    block_clear(S);
     __syncthreads();
+    uint32_t cur_slot = 0xffffffffu; // block-uniform: slot the LDS state and counters belong to
+    Ctr c;
+    c.zero();
+    uint32_t run_v = 0, run_n = 0;   // payload-size run cache
 
     const uint64_t ntiles = (P.n + PV_BLOCK - 1) / PV_BLOCK;
-    const uint8_t *R = P.recs;
+    const uint32_t tid = threadIdx.x;
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const uint64_t i = tile * PV_BLOCK + threadIdx.x;
-        const bool active = i < P.n;
-        Parsed o;
-        uint32_t period = 0, slot = 0;
-        bool in_window = false;
-        if (active) {
-            parse_record(P, P.offs[i], o);
-            while (period < P.n_shift && o.sec >= P.thresh[period]) period++;
-            slot = P.slot_of[period];
-            in_window = period >= P.skip_before;
+        const uint64_t t0 = tile * PV_BLOCK;
+        const uint64_t t1 = (t0 + PV_BLOCK < P.n ? t0 + PV_BLOCK : P.n) - 1;
+        // periods are contiguous index ranges (host-provided start indices): a tile is
+        // uniform when its first and last record share a period
+        const uint32_t p_lo = period_of(P, t0), p_hi = period_of(P, t1);
+        const bool uniform = p_lo == p_hi && p_lo >= P.skip_before;
+        if (uniform && P.slot_of[p_lo] != cur_slot) {
+            if (cur_slot != 0xffffffffu) {
+                hist_put(P, S, true, cur_slot, run_v, run_n);
+                run_n = 0;
+                ctr_flush(P, cur_slot, c);
+                block_flush(P, S, cur_slot);
+            }
+            cur_slot = P.slot_of[p_lo];
         }
-        // tile slot uniformity (LDS reduce)
-        if (threadIdx.x == 0) { S.tile_slot_lo = 0xffffffffu; S.tile_slot_hi = 0; }
-        __syncthreads();
-        if (active && in_window) { atomicMin(&S.tile_slot_lo, slot); atomicMax(&S.tile_slot_hi, slot); }
-        __syncthreads();
-        const uint32_t lo = S.tile_slot_lo, hi = S.tile_slot_hi;
-        if (lo == hi && lo != S.slot) {
-            block_flush(P, S);
-            if (threadIdx.x == 0) S.slot = lo;
-            __syncthreads();
-        }
-        const bool cached = (lo == hi) && (lo == S.slot);
-        const bool upd = active && in_window;
-        const int64_t rel = (int64_t)(P.gbase + i); // global record index (CPC first occurrence)
-        uint64_t *sum = slot_sum(P, slot);
+        const bool cached = uniform && P.slot_of[p_lo] == cur_slot;
 
-        // ---------------- Net v1 (NetworkMetricsBucket::process_net_layer)
-        const bool net_ctr = upd && (P.net_groups & 1u);
-        ctr_add(P, S, cached, slot, NC_EVENTS, upd);
-        ctr_add(P, S, cached, slot, NC_SAMPLES, upd);
-        ctr_add(P, S, cached, slot, NC_TOTAL, net_ctr);
-        ctr_add(P, S, cached, slot, NC_IN, net_ctr && o.dir == 0);
-        ctr_add(P, S, cached, slot, NC_OUT, net_ctr && o.dir == 1);
-        ctr_add(P, S, cached, slot, NC_UNK, net_ctr && o.dir == 2);
-        ctr_add(P, S, cached, slot, NC_V4, net_ctr && o.l3 == 4);
-        ctr_add(P, S, cached, slot, NC_V6, net_ctr && o.l3 == 6);
-        ctr_add(P, S, cached, slot, NC_UDP, net_ctr && o.l4 == 17);
-        ctr_add(P, S, cached, slot, NC_TCP, net_ctr && o.l4 == 6);
-        ctr_add(P, S, cached, slot, NC_SYN, net_ctr && o.l4 == 6 && o.syn);
-        ctr_add(P, S, cached, slot, NC_OTHER, net_ctr && o.l4 == 0);
-        if (upd) {
-            uint32_t cl = o.caplen;
-            if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
-            if (cached && cl < PV_HIST_N) atomicAdd(&S.hist[cl], 1u);
-            else atomicAdd((unsigned long long *)&sum[PV_OFF_PAYLOAD + cl], 1ull);
-
-            const bool card = P.net_groups & 2u, tops = P.net_groups & 8u;
-            if (o.has4 && o.dir != 2) {
-                uint32_t ip = ld32(R, o.dir == 0 ? o.v4 + 12 : o.v4 + 16);
-                if (ip) {
-                    uint64_t h1, h2;
-                    if (card) {
-                        murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
-                        cpc_add(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), rel);
-                    }
-                    if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV4, ip), 1, (uint32_t)i);
-                }
-            } else if (!o.has4 && o.has6 && o.dir != 2) {
-                uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
-                uint64_t w0 = (uint64_t)ld32(R, a) | ((uint64_t)ld32(R, a + 4) << 32);
-                uint64_t w1 = (uint64_t)ld32(R, a + 8) | ((uint64_t)ld32(R, a + 12) << 32);
-                if (w0 | w1) {
-                    uint64_t h1, h2;
-                    murmur_16(w0, w1, h1, h2);
-                    if (card) cpc_add(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), rel);
-                    if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV6, h1 ^ (h2 << 1)), 1, (uint32_t)i);
-                }
+        const uint64_t i = t0 + tid;
+        const bool active = i <= t1;
+        const uint64_t off = active ? P.offs[i] : 0;
+        // stage this record's first PV_WIN bytes (16-B aligned) into the lane's LDS window
+        const uint64_t wbase = off & ~15ull;
+        {
+            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + wbase);
+#pragma unroll
+            for (int j = 0; j < PV_WIN / 16; j++) {
+                uint4 v = active ? src[j] : make_uint4(0, 0, 0, 0);
+                S.win[4 * j + 0][tid] = v.x;
+                S.win[4 * j + 1][tid] = v.y;
+                S.win[4 * j + 2][tid] = v.z;
+                S.win[4 * j + 3][tid] = v.w;
             }
         }
-
-        // ---------------- DNS v1 over UDP (DnsStreamHandler::process_udp_packet_cb)
-        bool dns = false;
-        uint32_t metric_port = 0, dlen = 0, qr = 0, rcode = 0, ancount = 0, txid = 0;
-        uint64_t m = 0;
-        if (active && o.l4 == 17) {
-            uint32_t pw = ld32(R, o.l4off);
-            uint32_t sport = ((pw & 0xff) << 8) | ((pw >> 8) & 0xff);
-            uint32_t dport = ((pw >> 8) & 0xff00) | (pw >> 24);
-            auto isdns = [](uint32_t p) { return p == 53 || p == 5353 || p == 5355 || p == 53000; };
-            if (isdns(dport)) metric_port = sport;
-            else if (isdns(sport)) metric_port = dport;
-            if (metric_port) {
-                dns = true;
-                m = o.l4off + 8;
-                dlen = o.l4len - 8;
-                // header bytes past the capture read as 0 (the reference over-reads)
-                uint64_t cap_end = o.frame + o.caplen;
-                uint32_t hb[12];
-                for (int b = 0; b < 12; b++) hb[b] = (m + b < cap_end) ? ld8(R, m + b) : 0;
-                txid = (hb[0] << 8) | hb[1];
-                qr = hb[2] >> 7;
-                rcode = hb[3] & 15;
-                ancount = (hb[6] << 8) | hb[7];
-                uint32_t qd = (hb[4] << 8) | hb[5], ns = (hb[8] << 8) | hb[9], ar = (hb[10] << 8) | hb[11];
-                DnsInfo d;
-                dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
-                if (upd) {
-                    // deep path (DnsMetricsBucket::process_dns_layer :968-1023)
-                    const bool qn = P.dns_groups & PV_DNS_TOP_QNAMES_BIT;
-                    if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_PORT, metric_port), 1, (uint32_t)i);
-                    if (d.ok) {
-                        if (qr) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_RCODE, rcode), 1, (uint32_t)i);
-                        if (d.has_query) {
-                            NameStats st;
-                            st.init();
-                            if (d.name_len_enc > 0) name_emit(R, m, dlen, 12, st);
-                            uint64_t fp_full = fp56(st.ph, st.n, 0);
-                            if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT)) {
-                                uint64_t h1, h2;
-                                st.mm.finish(h1, h2);
-                                cpc_add(P, slot, CPC_QNAME, cpc_coupon(h1, h2), rel);
-                            }
-                            top_add(P, S, cached, slot, PV_KEY(TM_DENSE_QTYPE, d.qtype), 1, (uint32_t)i);
-                            if (qn) {
-                                if (qr) {
-                                    if (rcode == 2) top_add(P, S, cached, slot, PV_KEY(TM_SRVFAIL, fp_full), 1, (uint32_t)i);
-                                    else if (rcode == 3) top_add(P, S, cached, slot, PV_KEY(TM_NX, fp_full), 1, (uint32_t)i);
-                                    else if (rcode == 5) top_add(P, S, cached, slot, PV_KEY(TM_REFUSED, fp_full), 1, (uint32_t)i);
-                                    else if (rcode == 0) {
-                                        if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                                            top_add(P, S, cached, slot, PV_KEY(TM_NOERROR, fp_full), 1, (uint32_t)i);
-                                        if (!ancount) top_add(P, S, cached, slot, PV_KEY(TM_NODATA, fp_full), 1, (uint32_t)i);
-                                    }
-                                    if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                                        top_add(P, S, cached, slot, PV_KEY(TM_SIZED, fp_full), dlen, (uint32_t)i);
-                                }
-                                int q2, q3;
-                                uint64_t h2p, h3p;
-                                agg_domain(st, q2, q3, h2p, h3p);
-                                uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
-                                top_add(P, S, cached, slot, PV_KEY(TM_QNAME2, fp56(k2, st.n - q2, 0)), 1, (uint32_t)i);
-                                if (q3 >= 0 && (uint32_t)q3 < st.n) {
-                                    uint64_t k3 = q3 == 0 ? st.ph : suffix_hash(st, q3, h3p);
-                                    top_add(P, S, cached, slot, PV_KEY(TM_QNAME3, fp56(k3, st.n - q3, 0)), 1, (uint32_t)i);
-                                }
-                            }
+        if (active) {
+            const WAcc R{P.recs, wbase, &S.win[0][tid]};
+            Parsed o;
+            parse_record(R, P, off, o);
+            const uint32_t period = uniform ? p_lo : period_of(P, i);
+            const uint32_t slot = P.slot_of[period];
+            const bool upd = period >= P.skip_before;
+            if (upd && !cached) {
+                // boundary tile: this lane's record goes straight to HBM
+                Ctr one;
+                one.zero();
+                one.nev = 1; one.nin = o.dir == 0; one.nout = o.dir == 1; one.nunk = o.dir == 2;
+                one.n4 = o.l3 == 4; one.n6 = o.l3 == 6; one.nudp = o.l4 == 17; one.ntcp = o.l4 == 6;
+                one.nsyn = o.l4 == 6 && o.syn; one.noth = o.l4 == 0;
+                uint64_t *s = slot_sum(P, slot);
+                const bool nc = P.net_groups & PV_NET_COUNTERS_BIT;
+                atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_EVENTS], 1ull);
+                atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SAMPLES], 1ull);
+                if (nc) {
+                    atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_TOTAL], 1ull);
+                    atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.dir == 0 ? NC_IN : (o.dir == 1 ? NC_OUT : NC_UNK))], 1ull);
+                    if (o.l3) atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l3 == 4 ? NC_V4 : NC_V6)], 1ull);
+                    atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l4 == 17 ? NC_UDP : (o.l4 == 6 ? NC_TCP : NC_OTHER))], 1ull);
+                    if (o.l4 == 6 && o.syn) atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SYN], 1ull);
+                }
+                uint32_t cl = o.caplen > 65535 ? 65535 : o.caplen;
+                if (o.caplen > 65535) atomicOr(P.flags, PVF_BIG_CAPLEN);
+                atomicAdd((unsigned long long *)&s[PV_OFF_PAYLOAD + cl], 1ull);
+            } else if (upd) {
+                // ---- Net v1 counters (NetworkMetricsBucket::process_net_layer)
+                c.nev++;
+                c.nin += o.dir == 0; c.nout += o.dir == 1; c.nunk += o.dir == 2;
+                c.n4 += o.l3 == 4; c.n6 += o.l3 == 6;
+                c.nudp += o.l4 == 17; c.ntcp += o.l4 == 6; c.nsyn += o.l4 == 6 && o.syn; c.noth += o.l4 == 0;
+                uint32_t cl = o.caplen;
+                if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
+                if (cl == run_v) run_n++;
+                else { hist_put(P, S, true, cur_slot, run_v, run_n); run_v = cl; run_n = 1; }
+            }
+            if (upd) {
+                // ---- cardinality + top IPs (process_net_layer :745-763)
+                const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
+                if (o.has4 && o.dir != 2) {
+                    uint32_t ip = R.u32(o.dir == 0 ? o.v4 + 12 : o.v4 + 16);
+                    if (ip) {
+                        if (card) {
+                            uint64_t h1, h2;
+                            murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+                            cpc_add(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
+                        }
+                        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV4, ip), 1, (uint32_t)i);
+                    }
+                } else if (!o.has4 && o.has6 && o.dir != 2) {
+                    uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
+                    uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
+                    uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
+                    if (w0 | w1) {
+                        uint64_t h1, h2;
+                        murmur_16(w0, w1, h1, h2);
+                        if (card) cpc_add(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
+                        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV6, h1 ^ (h2 << 1)), 1, (uint32_t)i);
+                    }
+                }
+            }
+            // ---- DNS v1 over UDP
+            if (o.l4 == 17) {
+                if (cached || !upd) dns_lane(P, S, R, o, cached, upd, slot, period, i, c);
+                else {
+                    Ctr one;
+                    one.zero();
+                    dns_lane(P, S, R, o, false, upd, slot, period, i, one);
+                    uint64_t *s = slot_sum(P, slot);
+                    if (one.dev) {
+                        const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
+                        atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_EVENTS], 1ull);
+                        atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SAMPLES], 1ull);
+                        if (dc) {
+                            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_TOTAL], 1ull);
+                            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_UDP], 1ull);
+                            if (one.d4) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V4], 1ull);
+                            if (one.d6) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V6], 1ull);
+                            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + (one.dq ? DC_QUERIES : DC_REPLIES)], 1ull);
+                            if (one.dnoerr) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NOERROR], 1ull);
+                            if (one.dnodata) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NODATA], 1ull);
+                            if (one.dsrv) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SRVFAIL], 1ull);
+                            if (one.dnx) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NX], 1ull);
+                            if (one.dref) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_REFUSED], 1ull);
                         }
                     }
                 }
-                if (P.want_events) {
-                    uint32_t e = atomicAdd(P.n_events, 1u);
-                    PvXEvent ev;
-                    ev.key = ((uint64_t)flowkey(P, o) << 16) | txid;
-                    ev.idx = (uint32_t)i;
-                    ev.len = dlen;
-                    ev.sec = o.sec;
-                    ev.nsec = o.nsec;
-                    ev.qr = (uint8_t)qr;
-                    ev.dir = o.dir;
-                    ev.period = (uint8_t)period;
-                    ev.pad = 0;
-                    P.events[e] = ev;
-                }
-                if (period > 0 && o.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
             }
         }
-        const bool dc = dns && upd && (P.dns_groups & PV_DNS_COUNTERS_BIT);
-        ctr_add(P, S, cached, slot, 32 + DC_EVENTS, dns && upd);
-        ctr_add(P, S, cached, slot, 32 + DC_SAMPLES, dns && upd);
-        ctr_add(P, S, cached, slot, 32 + DC_TOTAL, dc);
-        ctr_add(P, S, cached, slot, 32 + DC_UDP, dc);
-        ctr_add(P, S, cached, slot, 32 + DC_V4, dc && o.l3 == 4);
-        ctr_add(P, S, cached, slot, 32 + DC_V6, dc && o.l3 == 6);
-        ctr_add(P, S, cached, slot, 32 + DC_QUERIES, dc && !qr);
-        ctr_add(P, S, cached, slot, 32 + DC_REPLIES, dc && qr);
-        ctr_add(P, S, cached, slot, 32 + DC_NOERROR, dc && qr && rcode == 0);
-        ctr_add(P, S, cached, slot, 32 + DC_NODATA, dc && qr && rcode == 0 && ancount == 0);
-        ctr_add(P, S, cached, slot, 32 + DC_SRVFAIL, dc && qr && rcode == 2);
-        ctr_add(P, S, cached, slot, 32 + DC_NX, dc && qr && rcode == 3);
-        ctr_add(P, S, cached, slot, 32 + DC_REFUSED, dc && qr && rcode == 5);
-        __syncthreads();
     }
-    block_flush(P, S);
+    if (cur_slot != 0xffffffffu) {
+        hist_put(P, S, true, cur_slot, run_v, run_n);
+        ctr_flush(P, cur_slot, c);
+        block_flush(P, S, cur_slot);
+    }
 }
 
 // Zero a device region of 64-bit words (grid-stride).
@@ -445,8 +578,8 @@ __device__ void slow_check(const PvXactParams &X, uint32_t idx, uint32_t period,
     if (!(thr > 0.0f && (float)us >= thr)) return;
     const PvParams &P = X.P;
     Parsed o;
-    parse_record(P, P.offs[idx], o);
-    const uint8_t *R = P.recs;
+    const GAcc R{P.recs};
+    parse_record(R, P, P.offs[idx], o);
     uint64_t m = o.l4off + 8;
     uint32_t len = o.l4len - 8;
     DnsInfo d;
@@ -459,8 +592,9 @@ __device__ void slow_check(const PvXactParams &X, uint32_t idx, uint32_t period,
 }
 } // namespace
 
-extern "C" __global__ void pv_xact_resolve(PvXactParams X)
+extern "C" __global__ void pv_xact_resolve(const PvXactParams *__restrict__ Xp)
 {
+    const PvXactParams &X = *Xp;
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= X.n) return;
     const PvParams &P = X.P;
@@ -518,8 +652,9 @@ extern "C" __global__ void pv_xact_resolve(PvXactParams X)
 }
 
 // top_slow for transactions of periods whose threshold became known after the resolve
-extern "C" __global__ void pv_xact_slow(PvXactParams X, uint32_t n_valid)
+extern "C" __global__ void pv_xact_slow(const PvXactParams *__restrict__ Xp, uint32_t n_valid)
 {
+    const PvXactParams &X = *Xp;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_valid) return;
     const PvXValid v = X.valid[i];

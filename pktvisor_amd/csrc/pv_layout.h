@@ -132,6 +132,7 @@ struct PvParams {
     int64_t thresh[PV_MAX_SHIFTS];
     uint32_t slot_of[PV_MAX_SHIFTS + 1];
     uint32_t skip_before; // periods < skip_before are outside the kept window (no bucket updates)
+    uint64_t pstart[PV_MAX_SHIFTS]; // first record index (in this batch) of period p+1
     uint64_t gbase;
     PvSubnets nets;
     // device state

@@ -5,20 +5,21 @@
 // tests/native/parse_harness.cpp, which fuzzes this exact source against the
 // oracle. The includer defines:
 //   PV_FN                      function qualifiers (__device__ __forceinline__ / inline)
-//   pv_ld32(base, off)         little-endian u32 at any byte offset
-//   pv_ld8(base, off)          byte load
 //   pv_clz64(x)                count leading zeros of a non-zero u64
-//   pv_umulhi(a, b)            high 64 bits of a 64x64 product
+// Byte access goes through an accessor object A with
+//   A.u32(off)  little-endian u32 at any absolute byte offset of the record blob
+//   A.u8(off)   one byte
+// (the kernel uses an LDS window over each record's first bytes, falling back to
+// HBM; the CPU harness reads plain memory).
 #pragma once
 #include <stdint.h>
 
 #include "pv_layout.h"
 
-#define ld32 pv_ld32
-#define ld8 pv_ld8
-PV_FN uint32_t be16(const uint8_t *base, uint64_t off)
+template <class A>
+PV_FN uint32_t be16(const A &R, uint64_t off)
 {
-    uint32_t w = ld32(base, off);
+    uint32_t w = R.u32(off);
     return ((w & 0xff) << 8) | ((w >> 8) & 0xff);
 }
 
@@ -102,25 +103,13 @@ PV_FN uint32_t cpc_coupon(uint64_t h1, uint64_t h2)
     return (row << 6) | col;
 }
 
-// Polynomial string fingerprint modulo the Mersenne prime 2^61-1.
-#define MP61 ((1ULL << 61) - 1)
-#define PBASE 0x1f3d5b79a2c4e681ULL % MP61
-PV_FN uint64_t mulmod61(uint64_t a, uint64_t b)
+// Polynomial string hash over Z/2^64 (odd base): prefix hashes give suffix hashes
+// by H(s[i:n]) = H(s[:n]) - H(s[:i]) * B^(n-i). Names are <= 255 chars.
+#define PBASE 0x9e3779b97f4a7c15ULL
+PV_FN uint64_t powb(uint32_t e)
 {
-    uint64_t lo = a * b, hi = pv_umulhi(a, b);
-    uint64_t r = (lo & MP61) + ((lo >> 61) | (hi << 3));
-    r = (r & MP61) + (r >> 61);
-    return r >= MP61 ? r - MP61 : r;
-}
-PV_FN uint64_t addmod61(uint64_t a, uint64_t b)
-{
-    uint64_t r = a + b;
-    return r >= MP61 ? r - MP61 : r;
-}
-PV_FN uint64_t powmod61(uint64_t b, uint32_t e)
-{
-    uint64_t r = 1;
-    while (e) { if (e & 1) r = mulmod61(r, b); b = mulmod61(b, b); e >>= 1; }
+    uint64_t r = 1, b = PBASE;
+    while (e) { if (e & 1) r *= b; b *= b; e >>= 1; }
     return r;
 }
 // 56-bit fingerprint of a byte string from its polynomial hash and length
@@ -154,7 +143,8 @@ PV_FN bool match4(const PvSubnets &s, uint32_t ip)
     }
     return false;
 }
-PV_FN bool match6(const PvSubnets &s, const uint8_t *recs, uint64_t a)
+template <class A>
+PV_FN bool match6(const PvSubnets &s, const A &R, uint64_t a)
 {
     for (uint32_t i = 0; i < s.n6; i++) {
         uint32_t cidr = s.v6_cidr[i], bytes = cidr / 8, bits = cidr % 8;
@@ -162,19 +152,19 @@ PV_FN bool match6(const PvSubnets &s, const uint8_t *recs, uint64_t a)
         if (bytes > 0) {
             r = true;
             for (uint32_t b = 0; b < bytes; b++)
-                if (ld8(recs, a + b) != s.v6_addr[i][b]) { r = false; break; }
+                if (R.u8(a + b) != s.v6_addr[i][b]) { r = false; break; }
         }
-        if ((r || cidr < 8) && bits > 0) r = (s.v6_addr[i][bytes] >> (8 - bits)) == (ld8(recs, a + bytes) >> (8 - bits));
+        if ((r || cidr < 8) && bits > 0) r = (s.v6_addr[i][bytes] >> (8 - bits)) == (R.u8(a + bytes) >> (8 - bits));
         if (r) return true;
     }
     return false;
 }
 
-PV_FN void parse_record(const PvParams &P, uint64_t rec, Parsed &o)
+template <class A>
+PV_FN void parse_record(const A &R, const PvParams &P, uint64_t rec, Parsed &o)
 {
-    const uint8_t *R = P.recs;
-    uint32_t tsec = ld32(R, rec), tfrac = ld32(R, rec + 4);
-    o.caplen = ld32(R, rec + 8);
+    uint32_t tsec = R.u32(rec), tfrac = R.u32(rec + 4);
+    o.caplen = R.u32(rec + 8);
     o.sec = tsec;
     o.nsec = P.ts_nano ? (int32_t)tfrac : (int32_t)(tfrac * 1000u);
     o.frame = rec + 16;
@@ -193,7 +183,7 @@ PV_FN void parse_record(const PvParams &P, uint64_t rec, Parsed &o)
     } else if (P.linktype == 113) {
         if (len > 16) { et = be16(R, cur + 14); cur += 16; len -= 16; l2ok = true; }
     } else if (P.linktype == 101 || P.linktype == 12 || P.linktype == 14 || P.linktype == 228 || P.linktype == 229) {
-        if (len >= 1) { uint32_t v = ld8(R, cur) >> 4; kind = (v == 4 || v == 6) ? v : 0; }
+        if (len >= 1) { uint32_t v = R.u8(cur) >> 4; kind = (v == 4 || v == 6) ? v : 0; }
     }
     if (l2ok) {
         for (int d = 0; d < 8 && (et == 0x8100 || et == 0x88A8); d++) {
@@ -206,7 +196,7 @@ PV_FN void parse_record(const PvParams &P, uint64_t rec, Parsed &o)
     for (int depth = 0; depth < 4 && kind; depth++) {
         uint32_t proto, hl;
         if (kind == 4) {
-            uint32_t b0 = ld8(R, cur);
+            uint32_t b0 = R.u8(cur);
             if (!(len >= 20 && (b0 >> 4) == 4 && (b0 & 15) >= 5)) break;
             if (!o.has4) { o.has4 = 1; o.v4 = cur; }
             uint32_t total = be16(R, cur + 2);
@@ -215,21 +205,21 @@ PV_FN void parse_record(const PvParams &P, uint64_t rec, Parsed &o)
             if (len <= hl) break;
             uint32_t frag = be16(R, cur + 6);
             if ((frag & 0x2000) || (frag & 0x1fff)) break;
-            proto = ld8(R, cur + 9);
+            proto = R.u8(cur + 9);
         } else {
             if (len < 40) break;
             if (!o.has6) { o.has6 = 1; o.v6 = cur; }
-            uint32_t next = ld8(R, cur + 6);
+            uint32_t next = R.u8(cur + 6);
             uint32_t off = 40;
             bool frag = false;
             for (int e = 0; e < 8 && len >= 2 && off <= len - 2; e++) {
                 uint32_t elen;
                 if (next == 44) elen = 8;
-                else if (next == 0 || next == 60 || next == 43) elen = (ld8(R, cur + off + 1) + 1) * 8;
-                else if (next == 51) elen = (ld8(R, cur + off + 1) + 2) * 4;
+                else if (next == 0 || next == 60 || next == 43) elen = (R.u8(cur + off + 1) + 1) * 8;
+                else if (next == 51) elen = (R.u8(cur + off + 1) + 2) * 4;
                 else break;
                 frag = next == 44;
-                next = ld8(R, cur + off);
+                next = R.u8(cur + off);
                 off += elen;
             }
             uint32_t total = be16(R, cur + 4) + off;
@@ -245,11 +235,11 @@ PV_FN void parse_record(const PvParams &P, uint64_t rec, Parsed &o)
             break;
         }
         if (proto == 6) {
-            if (pll >= 20) { o.l4 = 6; o.l4off = pl; o.l4len = pll; o.syn = (ld8(R, pl + 13) & 2) ? 1 : 0; }
+            if (pll >= 20) { o.l4 = 6; o.l4off = pl; o.l4len = pll; o.syn = (R.u8(pl + 13) & 2) ? 1 : 0; }
             break;
         }
         if ((proto == 4 || proto == 41) && pll >= 1) {
-            uint32_t v = ld8(R, pl) >> 4;
+            uint32_t v = R.u8(pl) >> 4;
             kind = (v == 4 || v == 6) ? v : 0;
             cur = pl; len = pll;
             continue;
@@ -259,8 +249,8 @@ PV_FN void parse_record(const PvParams &P, uint64_t rec, Parsed &o)
     o.l3 = o.has4 ? 4 : (o.has6 ? 6 : 0);
     // direction (PcapInputStream.cpp:401-416)
     if (o.has4) {
-        if (match4(P.nets, ld32(R, o.v4 + 16))) o.dir = 0;
-        else if (match4(P.nets, ld32(R, o.v4 + 12))) o.dir = 1;
+        if (match4(P.nets, R.u32(o.v4 + 16))) o.dir = 0;
+        else if (match4(P.nets, R.u32(o.v4 + 12))) o.dir = 1;
     } else if (o.has6) {
         if (match6(P.nets, R, o.v6 + 24)) o.dir = 0;
         else if (match6(P.nets, R, o.v6 + 8)) o.dir = 1;
@@ -273,10 +263,10 @@ PV_FN uint32_t fnv_bytes(uint32_t h, uint32_t v, int n)
     for (int i = 0; i < n; i++) { h *= 0x01000193u; h ^= (v >> (8 * i)) & 0xff; }
     return h;
 }
-PV_FN uint32_t flowkey(const PvParams &P, const Parsed &o)
+template <class A>
+PV_FN uint32_t flowkey(const A &R, const Parsed &o)
 {
-    const uint8_t *R = P.recs;
-    uint32_t pw = ld32(R, o.l4off);
+    uint32_t pw = R.u32(o.l4off);
     uint32_t ps = pw & 0xffff, pd = pw >> 16; // raw network-order u16 read little-endian
     int sp = pd < ps ? 1 : 0;
     uint32_t h = 0x811C9DC5u;
@@ -284,17 +274,17 @@ PV_FN uint32_t flowkey(const PvParams &P, const Parsed &o)
     h = fnv_bytes(h, p0, 2);
     h = fnv_bytes(h, p1, 2);
     if (o.has4) {
-        uint32_t s = ld32(R, o.v4 + 12), d = ld32(R, o.v4 + 16);
+        uint32_t s = R.u32(o.v4 + 12), d = R.u32(o.v4 + 16);
         if (ps == pd && d < s) sp = 1;
         uint32_t a = sp ? d : s, b = sp ? s : d;
         h = fnv_bytes(h, a, 4);
         h = fnv_bytes(h, b, 4);
-        h = fnv_bytes(h, ld8(R, o.v4 + 9), 1);
+        h = fnv_bytes(h, R.u8(o.v4 + 9), 1);
     } else {
         uint64_t a = sp ? o.v6 + 24 : o.v6 + 8, b = sp ? o.v6 + 8 : o.v6 + 24;
-        for (int i = 0; i < 16; i += 4) h = fnv_bytes(h, ld32(R, a + i), 4);
-        for (int i = 0; i < 16; i += 4) h = fnv_bytes(h, ld32(R, b + i), 4);
-        h = fnv_bytes(h, ld8(R, o.v6 + 6), 1);
+        for (int i = 0; i < 16; i += 4) h = fnv_bytes(h, R.u32(a + i), 4);
+        for (int i = 0; i < 16; i += 4) h = fnv_bytes(h, R.u32(b + i), 4);
+        h = fnv_bytes(h, R.u8(o.v6 + 6), 1);
     }
     return h;
 }
@@ -302,15 +292,16 @@ PV_FN uint32_t flowkey(const PvParams &P, const Parsed &o)
 // ------------------------------------------------------------------ DNS name decode
 // Level-1 structural walk of decodeName: returns m_NameLength (encoded length)
 // and whether the name text is forced empty (illegal top-level pointer => 0).
-PV_FN uint32_t name_len_l1(const uint8_t *R, uint64_t m, uint32_t len, uint32_t off)
+template <class A>
+PV_FN uint32_t name_len_l1(const A &R, uint64_t m, uint32_t len, uint32_t off)
 {
     uint32_t enc = 0, cur = off;
     if (cur + 1 > len) return 0;
-    uint32_t wl = ld8(R, m + cur);
+    uint32_t wl = R.u8(m + cur);
     while (wl != 0) {
         if ((wl & 0xc0) == 0xc0) {
             if (cur + 2 > len || enc > 255) return enc;
-            uint32_t ptr = ((wl & 0x3f) << 8) | ld8(R, m + cur + 1);
+            uint32_t ptr = ((wl & 0x3f) << 8) | R.u8(m + cur + 1);
             if (ptr < 12 || ptr >= len) return 0;
             return enc + 2;
         }
@@ -318,7 +309,7 @@ PV_FN uint32_t name_len_l1(const uint8_t *R, uint64_t m, uint32_t len, uint32_t 
         cur += wl + 1;
         enc += wl + 1;
         if (cur + 1 > len) return enc == 256 ? enc : enc + 1;
-        wl = ld8(R, m + cur);
+        wl = R.u8(m + cur);
     }
     return enc + 1;
 }
@@ -326,8 +317,8 @@ PV_FN uint32_t name_len_l1(const uint8_t *R, uint64_t m, uint32_t len, uint32_t 
 // Iterative decodeName producing the characters of the final std::string
 // (NUL-truncated, per-level 255-char copy limits, trailing-dot rules).
 // E::put(c) receives each character; returns false when the name is empty.
-template <class E>
-PV_FN void name_emit(const uint8_t *R, uint64_t m, uint32_t len, uint32_t off, E &e)
+template <class A, class E>
+PV_FN void name_emit(const A &R, uint64_t m, uint32_t len, uint32_t off, E &e)
 {
     uint32_t cur = off, enc = 0, dec = 0, level = 1;
     int budget = 1 << 30; // chars that can still travel up to the top-level buffer
@@ -342,12 +333,12 @@ PV_FN void name_emit(const uint8_t *R, uint64_t m, uint32_t len, uint32_t off, E
         e.put(c);
     };
     if (cur + 1 > len) return;
-    uint32_t wl = ld8(R, m + cur);
+    uint32_t wl = R.u8(m + cur);
     for (int guard = 0; guard < 4096 && !stop; guard++) {
         if (wl == 0) return; // normal termination: trailing '.' dropped
         if ((wl & 0xc0) == 0xc0) {
             if (cur + 2 > len || enc > 255) { if (pending) emit('.'); return; }
-            uint32_t ptr = ((wl & 0x3f) << 8) | ld8(R, m + cur + 1);
+            uint32_t ptr = ((wl & 0x3f) << 8) | R.u8(m + cur + 1);
             if (ptr < 12 || ptr >= len) { if (level >= 2 && pending) emit('.'); return; }
             if (pending) { emit('.'); pending = false; }
             int cap = 255 - (int)dec;
@@ -356,50 +347,53 @@ PV_FN void name_emit(const uint8_t *R, uint64_t m, uint32_t len, uint32_t off, E
             level++;
             if (level > 20) return; // decodeName(iteration > 20) returns an empty string
             cur = ptr; enc = 0; dec = 0;
-            wl = ld8(R, m + cur);
+            wl = R.u8(m + cur);
             continue;
         }
         if (cur + wl + 1 > len || enc + wl > 255) { if (enc != 256 && pending) emit('.'); return; }
         if (pending) emit('.');
-        for (uint32_t i = 0; i < wl && !stop; i++) emit(ld8(R, m + cur + 1 + i));
+        for (uint32_t i = 0; i < wl && !stop; i++) emit(R.u8(m + cur + 1 + i));
         pending = true;
         dec += wl + 1;
         cur += wl + 1;
         enc += wl + 1;
         if (cur + 1 > len) { if (enc != 256 && pending) emit('.'); return; }
-        wl = ld8(R, m + cur);
+        wl = R.u8(m + cur);
     }
 }
 
 PV_FN uint32_t lower(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
-// Per-packet name statistics: murmur for CPC, length, last dots with prefix hashes.
+// Per-packet name statistics: murmur for CPC, length, the last four dots with the
+// prefix hash in front of each (newest first, registers only), full prefix hash.
 struct NameStats {
     Murmur mm;
-    uint64_t ph;         // polynomial prefix hash of the chars so far
-    uint32_t n;          // chars so far
-    uint32_t dot_pos[4]; // positions of the last 4 dots (ring, newest at [n_dots&3])
-    uint64_t dot_ph[4];  // prefix hash *before* that dot
-    uint32_t n_dots;
+    uint64_t ph;                     // polynomial prefix hash of the chars so far
+    uint32_t n;                      // chars so far
+    int32_t d0, d1, d2, d3;          // positions of the last dots, newest first (-1 = none)
+    uint64_t h0, h1, h2, h3;         // prefix hash before each of those dots
     uint32_t last_c;
-    PV_FN void init() { mm.init(); ph = 0; n = 0; n_dots = 0; last_c = 0; }
+    PV_FN void init()
+    {
+        mm.init(); ph = 0; n = 0; last_c = 0;
+        d0 = d1 = d2 = d3 = -1; h0 = h1 = h2 = h3 = 0;
+    }
     PV_FN void put(uint32_t c)
     {
         c = lower(c);
-        if (c == '.') { dot_pos[n_dots & 3] = n; dot_ph[n_dots & 3] = ph; n_dots++; }
+        if (c == '.') { d3 = d2; h3 = h2; d2 = d1; h2 = h1; d1 = d0; h1 = h0; d0 = (int32_t)n; h0 = ph; }
         mm.put(c);
-        ph = addmod61(mulmod61(ph, PBASE), c + 1);
+        ph = ph * PBASE + (c + 1);
         n++;
         last_c = c;
     }
-    // most recent dot at position <= lim (rfind semantics); returns -1 if none among the tracked ones
+    // last dot at position <= lim among the tracked ones (std::string::rfind), -1 if none
     PV_FN int rfind(int lim, uint64_t &pph) const
     {
-        uint32_t cnt = n_dots < 4 ? n_dots : 4;
-        for (uint32_t i = 0; i < cnt; i++) {
-            uint32_t s = (n_dots - 1 - i) & 3;
-            if ((int)dot_pos[s] <= lim) { pph = dot_ph[s]; return (int)dot_pos[s]; }
-        }
+        if (d0 >= 0 && d0 <= lim) { pph = h0; return d0; }
+        if (d1 >= 0 && d1 <= lim) { pph = h1; return d1; }
+        if (d2 >= 0 && d2 <= lim) { pph = h2; return d2; }
+        if (d3 >= 0 && d3 <= lim) { pph = h3; return d3; }
         return -1;
     }
 };
@@ -412,17 +406,17 @@ PV_FN void agg_domain(const NameStats &s, int &q2, int &q3, uint64_t &ph2, uint6
     if (n < 5) { q3 = -1; return; }
     int endDot = 1 << 30;
     if (s.last_c == '.') endDot = n - 2;
-    uint64_t h1;
-    int first = s.rfind(endDot, h1);
+    uint64_t x1;
+    int first = s.rfind(endDot, x1);
     if (first > 0) {
-        uint64_t h2;
-        int second = s.rfind(first - 1, h2);
+        uint64_t x2;
+        int second = s.rfind(first - 1, x2);
         if (second >= 0) {
-            q2 = second; ph2 = h2;
+            q2 = second; ph2 = x2;
             if (second > 0) {
-                uint64_t h3;
-                int third = s.rfind(second - 1, h3);
-                if (third >= 0) { q3 = third; ph3 = h3; }
+                uint64_t x3;
+                int third = s.rfind(second - 1, x3);
+                if (third >= 0) { q3 = third; ph3 = x3; }
             }
         } else {
             q3 = -1;
@@ -432,8 +426,7 @@ PV_FN void agg_domain(const NameStats &s, int &q2, int &q3, uint64_t &ph2, uint6
 // polynomial hash of the suffix [start, n) given the prefix hash at start
 PV_FN uint64_t suffix_hash(const NameStats &s, int start, uint64_t ph_start)
 {
-    uint64_t sub = mulmod61(ph_start, powmod61(PBASE, s.n - (uint32_t)start));
-    return addmod61(s.ph, MP61 - sub);
+    return s.ph - ph_start * powb(s.n - (uint32_t)start);
 }
 
 struct CountEmit {
@@ -456,7 +449,7 @@ struct RawName {
     uint32_t n;
     PV_FN void put(uint32_t c)
     {
-        ph = addmod61(mulmod61(ph, PBASE), c + 1);
+        ph = ph * PBASE + (c + 1);
         n++;
     }
 };
@@ -470,7 +463,8 @@ struct DnsInfo {
     uint32_t qtype;
 };
 
-PV_FN void dns_parse(const uint8_t *R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns,
+template <class A>
+PV_FN void dns_parse(const A &R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns,
                           uint32_t ar, DnsInfo &d)
 {
     d.ok = false; d.has_query = false; d.qtype = 0; d.name_off = 12; d.name_len_enc = 0;

@@ -6,11 +6,15 @@
 #include <stdint.h>
 
 #define PV_FN inline
-inline uint32_t pv_ld32(const uint8_t *b, uint64_t off) { uint32_t v; memcpy(&v, b + off, 4); return v; }
-inline uint32_t pv_ld8(const uint8_t *b, uint64_t off) { return b[off]; }
 inline uint32_t pv_clz64(uint64_t x) { return (uint32_t)__builtin_clzll(x); }
-inline uint64_t pv_umulhi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
 #include "../../pktvisor_amd/csrc/pv_parse.h"
+
+// plain-memory accessor (the kernel uses an LDS-window accessor with the same interface)
+struct HAcc {
+    const uint8_t *R;
+    uint32_t u32(uint64_t off) const { uint32_t v; memcpy(&v, R + off, 4); return v; }
+    uint32_t u8(uint64_t off) const { return R[off]; }
+};
 
 extern "C" {
 
@@ -23,8 +27,9 @@ uint32_t h_decode_qname(const uint8_t *msg, uint32_t len, char *out, uint32_t *o
         uint32_t n;
         void put(uint32_t c) { o[n++] = (char)c; }
     } col{out, 0};
-    uint32_t nl = name_len_l1(msg, 0, len, 12);
-    if (nl > 0) name_emit(msg, 0, len, 12, col);
+    const HAcc R{msg};
+    uint32_t nl = name_len_l1(R, 0, len, 12);
+    if (nl > 0) name_emit(R, 0, len, 12, col);
     *outlen = col.n;
     return nl;
 }
@@ -33,8 +38,9 @@ uint32_t h_decode_qname(const uint8_t *msg, uint32_t len, char *out, uint32_t *o
 void h_dns_parse(const uint8_t *msg, uint32_t len, int *ok, int *has_query, uint32_t *qtype)
 {
     DnsInfo d;
-    uint32_t qd = be16(msg, 4), an = be16(msg, 6), ns = be16(msg, 8), ar = be16(msg, 10);
-    dns_parse(msg, 0, len, qd, an, ns, ar, d);
+    const HAcc R{msg};
+    uint32_t qd = be16(R, 4), an = be16(R, 6), ns = be16(R, 8), ar = be16(R, 10);
+    dns_parse(R, 0, len, qd, an, ns, ar, d);
     *ok = d.ok; *has_query = d.has_query; *qtype = d.qtype;
 }
 
@@ -43,8 +49,9 @@ void h_name_stats(const uint8_t *msg, uint32_t len, uint32_t *n, uint64_t *h1, u
 {
     NameStats st;
     st.init();
-    uint32_t nl = name_len_l1(msg, 0, len, 12);
-    if (nl > 0) name_emit(msg, 0, len, 12, st);
+    const HAcc R{msg};
+    uint32_t nl = name_len_l1(R, 0, len, 12);
+    if (nl > 0) name_emit(R, 0, len, 12, st);
     *n = st.n;
     st.mm.finish(*h1, *h2);
     uint64_t a, b;
