@@ -38,7 +38,7 @@
 extern "C" __global__ void pv_net_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
-extern "C" __global__ void pv_xact_keys(const PvXEvent *ev, uint32_t n, uint64_t *skeys, uint32_t *svals);
+extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
@@ -227,6 +227,8 @@ struct pv_ctx {
     uint64_t arena_cap = 64ull << 20;
     uint32_t tcap_log2 = 22;
     PvXEvent *d_events = nullptr;
+    uint64_t *d_ekeys = nullptr;
+    uint32_t *d_blk_events = nullptr;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
     void *d_sort_tmp = nullptr;
@@ -805,7 +807,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_taux, (size_t)PV_SLOTS * tcap * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_arena, (size_t)PV_SLOTS * c->arena_cap)) ||
         !hip_ok(e = hipMalloc(&c->d_arena_top, PV_SLOTS * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_events, (size_t)mr * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_events, (size_t)(mr + 256) * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)(mr + 256) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)mr * 8)) || !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)mr * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_svals, (size_t)mr * 4)) || !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)mr * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
@@ -832,7 +836,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -988,7 +992,11 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.arena_top = c->d_arena_top;
     P.arena_cap = c->arena_cap;
     P.events = c->d_events;
-    P.n_events = c->d_status + ST_NEV;
+    P.ekeys = c->d_ekeys;
+    P.blk_events = c->d_blk_events;
+    P.skeys = c->d_skeys;
+    P.svals = c->d_svals;
+    P.n_events = c->d_status + ST_NEV; // [0] packed total, [1] responses (ST_NRESP)
     P.want_events = (c->dns_groups & PV_DNS_TRANSACTIONS) ? 1 : 0;
     P.flags = c->d_status + ST_FLAGS;
     P.dns_first = c->d_status + ST_DNS_ANY;
@@ -998,7 +1006,9 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     int dev_cus = 256;
     hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     uint64_t tiles = (n + 255) / 256;
-    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)dev_cus * 3);
+    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)dev_cus * 4);
+    P.tiles_per_block = (uint32_t)((tiles + grid - 1) / grid);
+    grid = (uint32_t)((tiles + P.tiles_per_block - 1) / P.tiles_per_block);
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, &P, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
@@ -1006,6 +1016,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_dns_kernel");
     hipEventRecord(c->ev_stop, st);
+    if (P.want_events) hipLaunchKernelGGL(pv_xact_compact, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params, grid);
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
     uint32_t status[ST_WORDS];
@@ -1020,6 +1031,8 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
     if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
     uint32_t nev = status[ST_NEV];
+    const uint32_t nresp = status[ST_NRESP];
+    if (nresp == 0 && P.n_shift == 0) nev = 0; // nothing to pair, nothing to purge in this batch
     // DNS handler shifts only at DNS events: they must coincide with the Net shifts
     for (uint32_t k = 1; k <= P.n_shift; k++) {
         bool later_dns = false;
@@ -1033,7 +1046,6 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
                 return c->fail(PV_EUNSUPPORTED, "DNS period boundary differs from the Net boundary at second %lld",
                                (long long)thresh[k - 1]);
         uint32_t threads = 256, blocks = (nev + threads - 1) / threads;
-        hipLaunchKernelGGL(pv_xact_keys, dim3(blocks), dim3(threads), 0, st, c->d_events, nev, c->d_skeys, c->d_svals);
         size_t tmp = c->sort_tmp_bytes;
         if (!hip_ok(e = pv_radix_sort_pairs(c->d_sort_tmp, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
                                              (size_t)nev, st)))

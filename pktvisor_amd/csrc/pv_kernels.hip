@@ -167,6 +167,8 @@ struct BlockState {
     uint32_t ccnt[PV_CACHE_N];
     uint32_t crep[PV_CACHE_N];
     uint32_t hist[PV_HIST_N];        // payload-size histogram (caplen < PV_HIST_N)
+    uint32_t nev;                    // DNS events appended to this block's region
+    uint32_t nresp;                  // of which responses
 };
 
 // LDS key cache: returns false when the probe window is full (caller goes global)
@@ -361,7 +363,10 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
         }
     }
     if (P.want_events) {
-        uint32_t e = atomicAdd(P.n_events, 1u);
+        // append to this workgroup's event region (records are contiguous per workgroup,
+        // so region order is record order); LDS counter, no global atomics
+        uint32_t e = (uint32_t)(blockIdx.x * P.tiles_per_block) * PV_BLOCK + atomicAdd(&S.nev, 1u);
+        if (qr) atomicAdd(&S.nresp, 1u);
         PvXEvent ev;
         ev.key = ((uint64_t)flowkey(R, o) << 16) | txid;
         ev.idx = (uint32_t)i;
@@ -373,6 +378,7 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
         ev.period = (uint8_t)period;
         ev.pad = 0;
         P.events[e] = ev;
+        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)i;
     }
     if (period > 0 && o.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
 }
@@ -385,6 +391,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const P
     const PvParams &P = *Pp; // parameters live in device memory: scalar loads, no stack copy
     __shared__ BlockState S;
     block_clear(S);
+    if (threadIdx.x == 0) { S.nev = 0; S.nresp = 0; }
     __syncthreads();
     uint32_t cur_slot = 0xffffffffu; // block-uniform: slot the LDS state and counters belong to
     Ctr c;
@@ -393,7 +400,10 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const P
 
     const uint64_t ntiles = (P.n + PV_BLOCK - 1) / PV_BLOCK;
     const uint32_t tid = threadIdx.x;
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // each workgroup owns a contiguous run of tiles (record order inside its event region)
+    const uint64_t tbeg = (uint64_t)blockIdx.x * P.tiles_per_block;
+    const uint64_t tend = tbeg + P.tiles_per_block < ntiles ? tbeg + P.tiles_per_block : ntiles;
+    for (uint64_t tile = tbeg; tile < tend; tile++) {
         const uint64_t t0 = tile * PV_BLOCK;
         const uint64_t t1 = (t0 + PV_BLOCK < P.n ? t0 + PV_BLOCK : P.n) - 1;
         // periods are contiguous index ranges (host-provided start indices): a tile is
@@ -525,6 +535,32 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const P
         ctr_flush(P, cur_slot, c);
         block_flush(P, S, cur_slot);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        P.blk_events[blockIdx.x] = S.nev;
+        if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
+    }
+}
+
+// Packs the per-workgroup event regions into one dense run (workgroup order = record
+// order) and writes the total to n_events[0].
+extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint32_t nblk)
+{
+    const PvParams &P = *Pp;
+    __shared__ uint32_t base;
+    if (threadIdx.x == 0) {
+        uint32_t b = 0;
+        for (uint32_t j = 0; j < blockIdx.x; j++) b += P.blk_events[j];
+        base = b;
+        if (blockIdx.x == nblk - 1) P.n_events[0] = b + P.blk_events[blockIdx.x];
+    }
+    __syncthreads();
+    const uint32_t cnt = P.blk_events[blockIdx.x];
+    const uint64_t src = (uint64_t)blockIdx.x * P.tiles_per_block * PV_BLOCK;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+        P.skeys[base + j] = P.ekeys[src + j];
+        P.svals[base + j] = (uint32_t)(src + j);
+    }
 }
 
 // Zero a device region of 64-bit words (grid-stride).
@@ -543,14 +579,6 @@ extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v)
 // response pairs with the immediately preceding event of the same key iff that
 // event is a query (start_transaction overwrites, maybe_end_transaction erases).
 // Period shifts purge queries older than the TTL (DnsStreamHandler.h:252-267).
-extern "C" __global__ void pv_xact_keys(const PvXEvent *ev, uint32_t n, uint64_t *skeys, uint32_t *svals)
-{
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    skeys[i] = ((uint64_t)hash32(ev[i].key) << 32) | ev[i].idx;
-    svals[i] = i;
-}
-
 namespace {
 // first shift k (1-based period index) after period `a` whose threshold purges a
 // query started at `sec`; returns 0 if none inside this batch

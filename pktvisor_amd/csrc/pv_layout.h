@@ -145,9 +145,14 @@ struct PvParams {
     uint8_t *arena;   // PV_SLOTS x arena_cap
     uint64_t *arena_top;
     uint64_t arena_cap;
-    PvXEvent *events;
-    uint32_t *n_events;
+    PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
+    uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
+    uint32_t *blk_events; // events appended by each workgroup
+    uint64_t *skeys;      // packed keys (sort input)
+    uint32_t *svals;      // packed event slot positions (sort input)
+    uint32_t *n_events;   // [0] packed total (pv_xact_compact), [1] responses
     uint32_t want_events;
+    uint32_t tiles_per_block;
     uint32_t *flags;
     uint32_t *dns_first; // per period: min record index of a DNS event in that period
     uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
