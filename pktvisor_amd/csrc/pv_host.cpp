@@ -224,7 +224,7 @@ struct pv_ctx {
     uint32_t *d_taux = nullptr;
     uint8_t *d_arena = nullptr;
     uint64_t *d_arena_top = nullptr;
-    uint64_t arena_cap = 64ull << 20;
+    uint64_t arena_cap = 128ull << 20; // per slot; PV_ARENA_PARTS partitions
     uint32_t tcap_log2 = 22;
     PvXEvent *d_events = nullptr;
     uint64_t *d_ekeys = nullptr;
@@ -342,7 +342,7 @@ void clear_slot(pv_ctx *c, uint32_t s, int64_t rel_base)
     launch_fill64(c, c->d_tkeys + s * tcap, tcap, 0);
     launch_fill64(c, c->d_tcnt + s * tcap, tcap, 0);
     launch_fill32(c, c->d_taux + s * tcap, tcap, 0);
-    launch_fill64(c, c->d_arena_top + s, 1, 0);
+    launch_fill64(c, c->d_arena_top + (uint64_t)s * PV_ARENA_PARTS, PV_ARENA_PARTS, 0);
     c->meta[s] = SlotMeta();
     c->meta[s].rel_base = rel_base;
     c->slot_used[s] = true;
@@ -390,18 +390,22 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out)
     uint64_t tcap = 1ull << c->tcap_log2;
     std::vector<uint64_t> keys(tcap), cnt(tcap);
     std::vector<uint32_t> aux(tcap);
-    uint64_t top = 0;
+    uint64_t tops[PV_ARENA_PARTS];
     hipError_t e;
     if (!hip_ok(e = hipMemcpyAsync(keys.data(), c->d_tkeys + s * tcap, tcap * 8, hipMemcpyDeviceToHost, c->stream)) ||
         !hip_ok(e = hipMemcpyAsync(cnt.data(), c->d_tcnt + s * tcap, tcap * 8, hipMemcpyDeviceToHost, c->stream)) ||
         !hip_ok(e = hipMemcpyAsync(aux.data(), c->d_taux + s * tcap, tcap * 4, hipMemcpyDeviceToHost, c->stream)) ||
-        !hip_ok(e = hipMemcpyAsync(&top, c->d_arena_top + s, 8, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipMemcpyAsync(tops, c->d_arena_top + (uint64_t)s * PV_ARENA_PARTS, sizeof tops, hipMemcpyDeviceToHost, c->stream)) ||
         !hip_ok(e = hipStreamSynchronize(c->stream)))
         return c->hipfail(e, "read top-N table");
-    top = std::min<uint64_t>(top, c->arena_cap);
-    std::vector<uint8_t> arena(top);
-    if (top && (!hip_ok(e = hipMemcpy(arena.data(), c->d_arena + s * c->arena_cap, top, hipMemcpyDeviceToHost))))
-        return c->hipfail(e, "read name arena");
+    const uint64_t pcap = c->arena_cap / PV_ARENA_PARTS;
+    std::vector<std::vector<uint8_t>> parts(PV_ARENA_PARTS);
+    for (uint32_t p = 0; p < PV_ARENA_PARTS; p++) {
+        uint64_t used = std::min<uint64_t>(tops[p], pcap);
+        parts[p].resize(used);
+        if (used && !hip_ok(e = hipMemcpy(parts[p].data(), c->d_arena + s * c->arena_cap + p * pcap, used, hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "read name arena");
+    }
     for (uint64_t i = 0; i < tcap; i++) {
         if (!keys[i]) continue;
         TopRec r{keys[i], cnt[i], std::string()};
@@ -411,8 +415,10 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out)
             char b[20];
             snprintf(b, sizeof b, "%u.%u.%u.%u", ip & 0xff, (ip >> 8) & 0xff, (ip >> 16) & 0xff, ip >> 24);
             r.name = b;
-        } else if (aux[i] && aux[i] - 1 + 2 <= top) {
-            uint64_t p = aux[i] - 1;
+        } else if (aux[i] && (aux[i] - 1) % pcap + 2 <= parts[(aux[i] - 1) / pcap].size()) {
+            const std::vector<uint8_t> &arena = parts[(aux[i] - 1) / pcap];
+            const uint64_t top = arena.size();
+            uint64_t p = (aux[i] - 1) % pcap;
             uint32_t len = arena[p] | (arena[p + 1] << 8);
             if (p + 2 + len <= top) {
                 if (m == TM_IPV6) {
@@ -806,7 +812,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_tcnt, (size_t)PV_SLOTS * tcap * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_taux, (size_t)PV_SLOTS * tcap * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_arena, (size_t)PV_SLOTS * c->arena_cap)) ||
-        !hip_ok(e = hipMalloc(&c->d_arena_top, PV_SLOTS * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_arena_top, PV_SLOTS * PV_ARENA_PARTS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_events, (size_t)(mr + 256) * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)(mr + 256) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||

@@ -91,11 +91,15 @@ __device__ __noinline__ uint32_t write_name(const PvParams &P, uint32_t slot, ui
     Parsed o;
     const GAcc R{P.recs};
     parse_record(R, P, P.offs[rep], o);
+    const uint32_t part = blockIdx.x & (PV_ARENA_PARTS - 1);
+    const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
+    unsigned long long *top = (unsigned long long *)&P.arena_top[slot * PV_ARENA_PARTS + part];
     uint8_t *arena = P.arena + (uint64_t)slot * P.arena_cap;
     if (metric == TM_IPV6) {
         uint64_t a = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
-        uint64_t pos = atomicAdd((unsigned long long *)&P.arena_top[slot], 18ull);
-        if (pos + 18 > P.arena_cap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+        uint64_t pos = atomicAdd(top, 18ull);
+        if (pos + 18 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+        pos += part * pcap;
         arena[pos] = 16; arena[pos + 1] = 0;
         for (int i = 0; i < 16; i++) arena[pos + 2 + i] = (uint8_t)R.u8(a + i);
         return (uint32_t)pos + 1;
@@ -116,8 +120,9 @@ __device__ __noinline__ uint32_t write_name(const PvParams &P, uint32_t slot, ui
         if (start < 0) start = (int)n;
     }
     uint32_t slen = n - (uint32_t)start;
-    uint64_t pos = atomicAdd((unsigned long long *)&P.arena_top[slot], (unsigned long long)(slen + 2));
-    if (pos + slen + 2 > P.arena_cap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+    uint64_t pos = atomicAdd(top, (unsigned long long)(slen + 2));
+    if (pos + slen + 2 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+    pos += part * pcap;
     arena[pos] = (uint8_t)(slen & 0xff);
     arena[pos + 1] = (uint8_t)(slen >> 8);
     if (slen > 0 && nl > 0) {
@@ -588,15 +593,20 @@ __device__ __forceinline__ uint32_t purge_period(const PvParams &P, uint32_t ttl
         if (P.thresh[k - 1] >= (int64_t)ttl_s + sec) return k;
     return 0;
 }
-__device__ __forceinline__ void xctr(const PvParams &P, uint32_t slot, uint32_t c)
+// Workgroup-local staging: transaction counters per period and the quantile / slow
+// lists are gathered in LDS and reserved in global memory once per workgroup, so no
+// global address sees more than one atomic per workgroup.
+enum { XC_TOTAL, XC_OUT, XC_IN, XC_TIMEOUT, XC_N };
+struct XState {
+    uint32_t ctr[PV_MAX_SHIFTS + 1][XC_N];
+    PvXValue val[PV_BLOCK * 3];
+    PvXValid valid[PV_BLOCK];
+    uint32_t nval, nvalid, vbase, dbase;
+};
+__device__ __forceinline__ void xctr(XState &T, uint32_t period, uint32_t c) { atomicAdd(&T.ctr[period][c], 1u); }
+__device__ __forceinline__ void xval(const PvXactParams &X, XState &T, uint32_t period, uint32_t kind, uint64_t bits)
 {
-    atomicAdd((unsigned long long *)&P.sum[(uint64_t)slot * PV_SUM_WORDS + PV_OFF_DNS + c], 1ull);
-}
-__device__ __forceinline__ void xval(const PvXactParams &X, uint32_t period, uint32_t kind, uint64_t bits)
-{
-    uint32_t p = atomicAdd(X.n_vals, 1u);
-    if (p >= X.vals_cap) { atomicOr(X.P.flags, PVF_VALUES_FULL); return; }
-    X.vals[p] = PvXValue{bits, X.slot_gen[period], kind};
+    T.val[atomicAdd(&T.nval, 1u)] = PvXValue{bits, X.slot_gen[period], kind};
 }
 // DnsMetricsBucket::new_dns_transaction slow branch (dns/v1 ...cpp:1126-1136): the
 // response's first query name (getName(), case kept) into top_slow
@@ -620,11 +630,8 @@ __device__ void slow_check(const PvXactParams &X, uint32_t idx, uint32_t period,
 }
 } // namespace
 
-extern "C" __global__ void pv_xact_resolve(const PvXactParams *__restrict__ Xp)
+__device__ void resolve_one(const PvXactParams &X, XState &T, uint32_t p)
 {
-    const PvXactParams &X = *Xp;
-    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= X.n) return;
     const PvParams &P = X.P;
     const PvXEvent e = X.events[X.svals[p]];
     const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
@@ -639,30 +646,28 @@ extern "C" __global__ void pv_xact_resolve(const PvXactParams *__restrict__ Xp)
         uint32_t kp = purge_period(P, X.ttl_s, qe.period, qe.sec);
         if (kp && kp <= e.period) return; // purged at a period shift before this response
         const bool kept = e.period >= P.skip_before;
-        const uint32_t slot = P.slot_of[e.period];
         // timespec_diff(endTS, startTS) (TransactionManager.h:24-37)
         int64_t dsec = e.sec > qe.sec ? e.sec - qe.sec : qe.sec - e.sec;
         int64_t dnsec = (int64_t)e.nsec - (int64_t)qe.nsec;
         if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
         bool timed_out = dsec > (int64_t)X.ttl_s || (dsec == (int64_t)X.ttl_s && ((double)dnsec / 1.0e6) >= (double)X.ttl_ms);
-        if (timed_out) { if (kept) xctr(P, slot, DC_XTIMEOUT); return; }
+        if (timed_out) { if (kept) xctr(T, e.period, XC_TIMEOUT); return; }
         // DnsMetricsBucket::new_dns_transaction (dns/v1 ...cpp:1093-1138)
         uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
         if (kept) {
-            xctr(P, slot, DC_XTOTAL);
-            if (e.dir == 0) xctr(P, slot, DC_XOUT);
-            else if (e.dir == 1) xctr(P, slot, DC_XIN);
+            xctr(T, e.period, XC_TOTAL);
+            if (e.dir == 0) xctr(T, e.period, XC_OUT);
+            else if (e.dir == 1) xctr(T, e.period, XC_IN);
         }
         // quantile inputs of every period (skipped ones still feed the next period's p90)
         if (X.quantiles) {
-            if (e.dir == 0) xval(X, e.period, XV_FROM_US, us);
-            else if (e.dir == 1) xval(X, e.period, XV_TO_US, us);
-            if (qe.len && kept) xval(X, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
+            if (e.dir == 0) xval(X, T, e.period, XV_FROM_US, us);
+            else if (e.dir == 1) xval(X, T, e.period, XV_TO_US, us);
+            if (qe.len && kept) xval(X, T, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
         }
         if (!kept || e.dir == 2) return;
         if (X.thr_from[e.period] < 0.0f) {
-            uint32_t v = atomicAdd(X.n_valid, 1u);
-            X.valid[v] = PvXValid{e.idx, e.period, e.dir, 0, 0, us};
+            T.valid[atomicAdd(&T.nvalid, 1u)] = PvXValid{e.idx, (uint8_t)e.period, (uint8_t)e.dir, 0, 0, us};
         } else {
             slow_check(X, e.idx, e.period, e.dir, us);
         }
@@ -675,8 +680,40 @@ extern "C" __global__ void pv_xact_resolve(const PvXactParams *__restrict__ Xp)
             if (X.events[X.svals[q]].key == e.key) break;
         if (q < X.n && (uint32_t)(X.skeys[q] >> 32) == h && X.events[X.svals[q]].period < kp) return;
         if (kp < P.skip_before) return;
-        xctr(P, P.slot_of[kp], DC_XTIMEOUT);
+        xctr(T, kp, XC_TIMEOUT);
     }
+}
+
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvXactParams *__restrict__ Xp)
+{
+    const PvXactParams &X = *Xp;
+    const PvParams &P = X.P;
+    __shared__ XState T;
+    for (uint32_t j = threadIdx.x; j < (PV_MAX_SHIFTS + 1) * XC_N; j += blockDim.x) (&T.ctr[0][0])[j] = 0;
+    if (threadIdx.x == 0) { T.nval = 0; T.nvalid = 0; }
+    __syncthreads();
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < X.n) resolve_one(X, T, p);
+    __syncthreads();
+    static const uint8_t dc[XC_N] = {DC_XTOTAL, DC_XOUT, DC_XIN, DC_XTIMEOUT};
+    if (threadIdx.x < (PV_MAX_SHIFTS + 1) * XC_N) {
+        const uint32_t per = threadIdx.x / XC_N, c = threadIdx.x % XC_N;
+        const uint32_t v = T.ctr[per][c];
+        if (v && per <= P.n_shift)
+            atomicAdd((unsigned long long *)&P.sum[(uint64_t)P.slot_of[per] * PV_SUM_WORDS + PV_OFF_DNS + dc[c]],
+                      (unsigned long long)v);
+    }
+    if (threadIdx.x == 0) {
+        T.vbase = T.nval ? atomicAdd(X.n_vals, T.nval) : 0;
+        T.dbase = T.nvalid ? atomicAdd(X.n_valid, T.nvalid) : 0;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < T.nval; j += blockDim.x) {
+        const uint32_t q = T.vbase + j;
+        if (q < X.vals_cap) X.vals[q] = T.val[j];
+        else atomicOr(X.P.flags, PVF_VALUES_FULL);
+    }
+    for (uint32_t j = threadIdx.x; j < T.nvalid; j += blockDim.x) X.valid[T.dbase + j] = T.valid[j];
 }
 
 // top_slow for transactions of periods whose threshold became known after the resolve

@@ -15,6 +15,9 @@
 #define PV_SLOTS 16
 #define PV_MAX_SHIFTS 6 // period shifts handled inside one device batch
 #define PV_MAX_SUBNETS 16
+// name arena partitions per slot: workgroup b allocates from partition b % PV_ARENA_PARTS,
+// so no bump pointer is shared by more than a few workgroups
+#define PV_ARENA_PARTS 64
 
 // group bits (same values as pv_net_group / pv_dns_group in include/pvgpu.h)
 #define PV_NET_COUNTERS_BIT 1u
@@ -142,9 +145,9 @@ struct PvParams {
     uint64_t *tcnt;
     uint32_t *taux;
     uint32_t tcap_log2;
-    uint8_t *arena;   // PV_SLOTS x arena_cap
-    uint64_t *arena_top;
-    uint64_t arena_cap;
+    uint8_t *arena;      // PV_SLOTS x arena_cap, each slot split in PV_ARENA_PARTS partitions
+    uint64_t *arena_top; // PV_SLOTS x PV_ARENA_PARTS bump pointers (bytes used in the partition)
+    uint64_t arena_cap;  // bytes per slot
     PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
     uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
     uint32_t *blk_events; // events appended by each workgroup
