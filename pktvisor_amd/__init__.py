@@ -65,10 +65,12 @@ _lib = None
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libpvgpu.so (raises if it was not built: there is no fallback)."""
+    """Load libpvgpu.so (raises if it was not built: there is no fallback).
+    PVGPU_LIB overrides the path (kernel tuning variants built in-tree)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("PVGPU_LIB", path)
     if not os.path.exists(path):
         raise PvError(f"{path} missing: run `make -C pktvisor_amd` (or __graft_entry__.build())")
     lib = ctypes.CDLL(path)

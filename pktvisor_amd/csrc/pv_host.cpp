@@ -39,6 +39,7 @@ extern "C" __global__ void pv_net_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
+extern "C" __global__ void pv_boundary_kernel(const PvParams *P);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
@@ -229,6 +230,8 @@ struct pv_ctx {
     PvXEvent *d_events = nullptr;
     uint64_t *d_ekeys = nullptr;
     uint32_t *d_blk_events = nullptr;
+    uint64_t *d_mq = nullptr; // per-workgroup top-N miss queues
+    int cus = 256;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
     void *d_sort_tmp = nullptr;
@@ -805,6 +808,10 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     hipError_t e;
     uint64_t tcap = 1ull << c->tcap_log2;
     uint64_t mr = c->max_records;
+    hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    // event regions: main workgroups own tiles_per_block * 256 slots each (the last may
+    // overhang the batch by < tiles_per_block tiles), boundary workgroups 256 each
+    const uint64_t ev_cap = mr + mr / (4 * (uint64_t)c->cus) + 16 * 256;
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
         !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_cpc, (size_t)PV_SLOTS * PV_MIN_WORDS * 8)) ||
@@ -813,8 +820,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_taux, (size_t)PV_SLOTS * tcap * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_arena, (size_t)PV_SLOTS * c->arena_cap)) ||
         !hip_ok(e = hipMalloc(&c->d_arena_top, PV_SLOTS * PV_ARENA_PARTS * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_events, (size_t)(mr + 256) * sizeof(PvXEvent))) ||
-        !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)(mr + 256) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_events, (size_t)ev_cap * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)ev_cap * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_mq, (size_t)c->cus * 4 * PV_MQ_CAP * 16)) ||
         !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)mr * 8)) || !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)mr * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_svals, (size_t)mr * 4)) || !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)mr * 4)) ||
@@ -842,7 +850,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -1009,20 +1017,41 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.dns_at_thresh = c->d_status + ST_DNS_AT;
     launch_fill32(c, c->d_status, ST_WORDS, 0);
     hipError_t e;
-    int dev_cus = 256;
-    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     uint64_t tiles = (n + 255) / 256;
-    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)dev_cus * 4);
+    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->cus * 4);
     P.tiles_per_block = (uint32_t)((tiles + grid - 1) / grid);
+    P.rec_bytes = info->bytes_used;
+    {
+        static const char *dbg = getenv("PV_DEBUG_STAGES");
+        P.dbg = dbg ? (uint32_t)atoi(dbg) : 0;
+    }
     grid = (uint32_t)((tiles + P.tiles_per_block - 1) / P.tiles_per_block);
+    P.grid_main = grid;
+    P.mq = c->d_mq;
+    // tiles that hold a period shift go to pv_boundary_kernel
+    P.n_btiles = 0;
+    for (uint32_t k = 0; k < P.n_shift; k++) {
+        const uint64_t ps = P.pstart[k];
+        if (ps % 256 == 0 || ps >= n) continue;
+        const uint32_t t = (uint32_t)(ps / 256);
+        bool seen = false;
+        for (uint32_t j = 0; j < P.n_btiles; j++) seen |= P.btile[j] == t;
+        if (!seen) P.btile[P.n_btiles++] = t;
+    }
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, &P, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
     hipLaunchKernelGGL(pv_net_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_dns_kernel");
+    if (P.n_btiles) {
+        hipLaunchKernelGGL(pv_boundary_kernel, dim3(P.n_btiles), dim3(256), 0, st, (const PvParams *)c->d_params);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_boundary_kernel");
+    }
     hipEventRecord(c->ev_stop, st);
-    if (P.want_events) hipLaunchKernelGGL(pv_xact_compact, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params, grid);
+    if (P.want_events)
+        hipLaunchKernelGGL(pv_xact_compact, dim3(grid + P.n_btiles), dim3(256), 0, st, (const PvParams *)c->d_params,
+                           grid + P.n_btiles);
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
     uint32_t status[ST_WORDS];

@@ -28,10 +28,18 @@
 #include "pv_layout.h"
 
 #define PV_BLOCK 256
+#ifndef PV_CACHE_N
 #define PV_CACHE_N 2048
+#endif
 #define PV_HIST_N 2048
-#define PV_WIN 128              // bytes of each record staged into LDS (record header + frame start)
+#ifndef PV_WIN
+#define PV_WIN 128 // bytes of each record staged into LDS (record header + frame start)
+#endif
+#ifndef PV_WPE
+#define PV_WPE 2 // waves per SIMD the main kernel is register-budgeted for
+#endif
 #define PV_WINW (PV_WIN / 4)
+#define PV_CPCF_N 512           // LDS filter of CPC coupons already submitted by this workgroup
 
 // ------------------------------------------------------------------ byte access
 // recs is 256-B aligned and padded by >= 256 bytes: two aligned dword loads and
@@ -55,29 +63,36 @@ struct GAcc {
     PV_FN uint32_t u8(uint64_t off) const { return R[off]; }
 };
 
-// Per-lane LDS window over the first PV_WIN bytes from the 16-B aligned start of
-// the lane's record, dword-major ([dword][lane]) so any per-lane offset reads
-// conflict-free; bytes past the window come from HBM.
-struct WAcc {
+// LDS staging accessor. A tile's bytes sit in LDS in one of two layouts, chosen per
+// tile (uniform):
+//   packed  - the tile's whole contiguous record span, loaded with fully coalesced
+//             16-B lane loads (small records): dword d of the span at stage[d];
+//   window  - each lane's first PV_WIN bytes from the 16-B aligned start of its own
+//             record (large records), dword-major: dword d of lane l at stage[d*256+l],
+//             so per-lane reads at any offset are bank-conflict free.
+// One multiply-add covers both (mul = 1/add = 0, or mul = 256/add = lane). Bytes
+// outside the staged range come from HBM.
+struct TAcc {
     const uint8_t *R;
-    uint64_t wbase;
-    const uint32_t *win; // &win[0][lane]
+    const uint32_t *L;
+    uint64_t gbase;
+    uint32_t lim, mul, add;
     PV_FN uint32_t u32(uint64_t off) const
     {
-        uint64_t rel = off - wbase;
-        if (rel < PV_WIN - 4) {
+        uint64_t rel = off - gbase;
+        if (rel < lim) {
             uint32_t r = (uint32_t)rel;
-            uint32_t lo = win[(r >> 2) * PV_BLOCK], hi = win[((r >> 2) + 1) * PV_BLOCK];
-            return __builtin_amdgcn_alignbyte(hi, lo, r & 3);
+            uint32_t d = (r >> 2) * mul + add;
+            return __builtin_amdgcn_alignbyte(L[d + mul], L[d], r & 3);
         }
         return pv_ld32(R, off);
     }
     PV_FN uint32_t u8(uint64_t off) const
     {
-        uint64_t rel = off - wbase;
-        if (rel < PV_WIN) {
+        uint64_t rel = off - gbase;
+        if (rel < lim) {
             uint32_t r = (uint32_t)rel;
-            return (win[(r >> 2) * PV_BLOCK] >> ((r & 3) * 8)) & 0xff;
+            return (L[(r >> 2) * mul + add] >> ((r & 3) * 8)) & 0xff;
         }
         return R[off];
     }
@@ -167,12 +182,15 @@ __device__ __noinline__ void global_add(const PvParams &P, uint32_t slot, uint64
 
 // ------------------------------------------------------------------ LDS workgroup state
 struct BlockState {
-    uint32_t win[PV_WINW][PV_BLOCK]; // record windows
+    uint32_t stage[PV_WINW * PV_BLOCK]; // tile bytes (TAcc layouts), 32 KiB
     uint64_t ckey[PV_CACHE_N];       // key -> count cache for top-N and dense tables
     uint32_t ccnt[PV_CACHE_N];
     uint32_t crep[PV_CACHE_N];
     uint32_t hist[PV_HIST_N];        // payload-size histogram (caplen < PV_HIST_N)
+    uint32_t cpcf[PV_CPCF_N];        // (sketch << 17 | coupon) + 1 submitted in an earlier tile
+    uint32_t mq_n[2];                // queued top-N misses of the current tile (tile parity)
     uint32_t nev;                    // DNS events appended to this block's region
+    uint64_t ebase;                  // first event slot of this block's region
     uint32_t nresp;                  // of which responses
 };
 
@@ -193,16 +211,52 @@ __device__ __forceinline__ bool cache_add(BlockState &S, uint64_t key, uint32_t 
     return false;
 }
 
+// Cached tiles: LDS cache first. A miss of a dense table is a fire-and-forget HBM
+// atomic; a miss of a hashed table is stored to the workgroup's HBM miss queue and
+// inserted after the tile, so no lane waits on an HBM round trip mid-tile (which would
+// also drain the next tile's in-flight prefetch). The queue cannot overflow: at most 6
+// hashed updates per record (PV_MQ_CAP).
 __device__ __forceinline__ void top_add(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint64_t key,
-                                        uint32_t w, uint32_t rep)
+                                        uint32_t w, uint32_t rep, uint32_t mqp = 0)
 {
-    if (!(cached && cache_add(S, key, w, rep))) global_add(P, slot, key, w, rep);
+    if (cached) {
+        if (cache_add(S, key, w, rep)) return;
+        const uint32_t metric = PV_KEY_METRIC(key);
+        if (metric < TM_DENSE_PORT) {
+            const uint32_t q = atomicAdd(&S.mq_n[mqp], 1u);
+            PV_G uint64_t *e = P.mq + ((uint64_t)blockIdx.x * PV_MQ_CAP + q) * 2;
+            e[0] = key;
+            e[1] = (uint64_t)w | ((uint64_t)rep << 32);
+            return;
+        }
+    }
+    global_add(P, slot, key, w, rep);
 }
 
-__device__ __forceinline__ void cpc_add(const PvParams &P, uint32_t slot, uint32_t sketch, uint32_t coupon, int64_t gidx)
+// CPC first occurrence: atomicMin of the global record index into the coupon's slot.
+// Records of a workgroup are visited in index order, so a coupon this workgroup already
+// submitted in an EARLIER tile cannot lower the minimum: the LDS filter skips it. Keys
+// seen in the current tile are inserted only after the tile's barrier (cpc_commit).
+__device__ __forceinline__ uint32_t cpcf_slot(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - 9); }
+__device__ __forceinline__ void cpc_add(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint32_t sketch,
+                                        uint32_t coupon, int64_t gidx, uint32_t &pending)
 {
+    const uint32_t key = ((sketch << 17) | coupon) + 1;
+    if (cached && S.cpcf[cpcf_slot(key)] == key) return;
     int64_t *t = P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)sketch * PV_CPC_COUPONS + coupon;
-    if (__atomic_load_n(t, __ATOMIC_RELAXED) > gidx) atomicMin((long long *)t, (long long)gidx);
+    atomicMin((long long *)t, (long long)gidx); // no return value: nothing waits on it
+    if (cached) pending = key;
+}
+__device__ __forceinline__ void cpc_commit(BlockState &S, uint32_t key)
+{
+    if (key) S.cpcf[cpcf_slot(key)] = key;
+}
+// workgroup barrier that orders LDS only (global loads in flight stay in flight)
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -251,6 +305,7 @@ __device__ void block_clear(BlockState &S)
 {
     for (uint32_t i = threadIdx.x; i < PV_CACHE_N; i += PV_BLOCK) { S.ckey[i] = 0; S.ccnt[i] = 0; }
     for (uint32_t i = threadIdx.x; i < PV_HIST_N; i += PV_BLOCK) S.hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < PV_CPCF_N; i += PV_BLOCK) S.cpcf[i] = 0;
 }
 
 // Flush the LDS partial bucket of `slot` to HBM and clear it (all threads, block-uniform).
@@ -291,7 +346,8 @@ __device__ __forceinline__ void hist_put(const PvParams &P, BlockState &S, bool 
 // DnsMetricsBucket::process_dns_layer, :910-1049)
 template <class A>
 __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const A &R, const Parsed &o, bool cached,
-                                         bool upd, uint32_t slot, uint32_t period, uint64_t i, Ctr &c)
+                                         bool upd, uint32_t slot, uint32_t period, uint64_t i, Ctr &c,
+                                         uint32_t &pend_q, uint32_t mqp)
 {
     uint32_t pw = R.u32(o.l4off);
     uint32_t sport = ((pw & 0xff) << 8) | ((pw >> 8) & 0xff);
@@ -328,9 +384,9 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
         c.dsrv += qr && rcode == 2; c.dnx += qr && rcode == 3; c.dref += qr && rcode == 5;
         DnsInfo d;
         dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
-        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_PORT, metric_port), 1, (uint32_t)i);
+        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_PORT, metric_port), 1, (uint32_t)i, mqp);
         if (d.ok) {
-            if (qr) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_RCODE, rcode), 1, (uint32_t)i);
+            if (qr) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_RCODE, rcode), 1, (uint32_t)i, mqp);
             if (d.has_query) {
                 NameStats st;
                 st.init();
@@ -338,30 +394,30 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
                 uint64_t h1, h2;
                 st.mm.finish(h1, h2);
                 if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT))
-                    cpc_add(P, slot, CPC_QNAME, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
-                top_add(P, S, cached, slot, PV_KEY(TM_DENSE_QTYPE, d.qtype), 1, (uint32_t)i);
+                    cpc_add(P, S, cached, slot, CPC_QNAME, cpc_coupon(h1, h2), (int64_t)(P.gbase + i), pend_q);
+                top_add(P, S, cached, slot, PV_KEY(TM_DENSE_QTYPE, d.qtype), 1, (uint32_t)i, mqp);
                 if (P.dns_groups & PV_DNS_TOP_QNAMES_BIT) {
                     const uint64_t fp_full = fp56(st.ph, st.n, 0);
                     if (qr) {
-                        if (rcode == 2) top_add(P, S, cached, slot, PV_KEY(TM_SRVFAIL, fp_full), 1, (uint32_t)i);
-                        else if (rcode == 3) top_add(P, S, cached, slot, PV_KEY(TM_NX, fp_full), 1, (uint32_t)i);
-                        else if (rcode == 5) top_add(P, S, cached, slot, PV_KEY(TM_REFUSED, fp_full), 1, (uint32_t)i);
+                        if (rcode == 2) top_add(P, S, cached, slot, PV_KEY(TM_SRVFAIL, fp_full), 1, (uint32_t)i, mqp);
+                        else if (rcode == 3) top_add(P, S, cached, slot, PV_KEY(TM_NX, fp_full), 1, (uint32_t)i, mqp);
+                        else if (rcode == 5) top_add(P, S, cached, slot, PV_KEY(TM_REFUSED, fp_full), 1, (uint32_t)i, mqp);
                         else if (rcode == 0) {
                             if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                                top_add(P, S, cached, slot, PV_KEY(TM_NOERROR, fp_full), 1, (uint32_t)i);
-                            if (!ancount) top_add(P, S, cached, slot, PV_KEY(TM_NODATA, fp_full), 1, (uint32_t)i);
+                                top_add(P, S, cached, slot, PV_KEY(TM_NOERROR, fp_full), 1, (uint32_t)i, mqp);
+                            if (!ancount) top_add(P, S, cached, slot, PV_KEY(TM_NODATA, fp_full), 1, (uint32_t)i, mqp);
                         }
                         if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                            top_add(P, S, cached, slot, PV_KEY(TM_SIZED, fp_full), dlen, (uint32_t)i);
+                            top_add(P, S, cached, slot, PV_KEY(TM_SIZED, fp_full), dlen, (uint32_t)i, mqp);
                     }
                     int q2, q3;
                     uint64_t h2p, h3p;
                     agg_domain(st, q2, q3, h2p, h3p);
                     const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
-                    top_add(P, S, cached, slot, PV_KEY(TM_QNAME2, fp56(k2, st.n - q2, 0)), 1, (uint32_t)i);
+                    top_add(P, S, cached, slot, PV_KEY(TM_QNAME2, fp56(k2, st.n - q2, 0)), 1, (uint32_t)i, mqp);
                     if (q3 >= 0 && (uint32_t)q3 < st.n) {
                         const uint64_t k3 = q3 == 0 ? st.ph : suffix_hash(st, q3, h3p);
-                        top_add(P, S, cached, slot, PV_KEY(TM_QNAME3, fp56(k3, st.n - q3, 0)), 1, (uint32_t)i);
+                        top_add(P, S, cached, slot, PV_KEY(TM_QNAME3, fp56(k3, st.n - q3, 0)), 1, (uint32_t)i, mqp);
                     }
                 }
             }
@@ -370,7 +426,7 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
     if (P.want_events) {
         // append to this workgroup's event region (records are contiguous per workgroup,
         // so region order is record order); LDS counter, no global atomics
-        uint32_t e = (uint32_t)(blockIdx.x * P.tiles_per_block) * PV_BLOCK + atomicAdd(&S.nev, 1u);
+        uint32_t e = (uint32_t)S.ebase + atomicAdd(&S.nev, 1u);
         if (qr) atomicAdd(&S.nresp, 1u);
         PvXEvent ev;
         ev.key = ((uint64_t)flowkey(R, o) << 16) | txid;
@@ -388,15 +444,119 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
     if (period > 0 && o.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
 }
 
+
+// cardinality + top IPs of one record (NetworkMetricsBucket::process_net_layer :745-763)
+template <class A>
+__device__ __forceinline__ void net_ips(const PvParams &P, BlockState &S, const A &R, const Parsed &o, uint64_t i,
+                                        bool cached, uint32_t slot, uint32_t mqp, uint32_t &pend_n)
+{
+    const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
+    if (o.dir == 2) return;
+    if (o.has4) {
+        const uint32_t ip = R.u32(o.dir == 0 ? o.v4 + 12 : o.v4 + 16);
+        if (!ip) return;
+        if (card) {
+            uint64_t h1, h2;
+            murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+            cpc_add(P, S, cached, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i),
+                    pend_n);
+        }
+        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV4, ip), 1, (uint32_t)i, mqp);
+    } else if (o.has6) {
+        const uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
+        const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
+        const uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
+        if (!(w0 | w1)) return;
+        uint64_t h1, h2;
+        murmur_16(w0, w1, h1, h2);
+        if (card)
+            cpc_add(P, S, cached, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i),
+                    pend_n);
+        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV6, h1 ^ (h2 << 1)), 1, (uint32_t)i, mqp);
+    }
+}
+
+// One record of a tile whose records all fall in period `period` -> bucket slot `slot`
+// (both workgroup-uniform): counters in registers, tables through the LDS cache.
+__device__ __forceinline__ void lane_hot(const PvParams &P, BlockState &S, const TAcc &R, const Parsed &o, uint64_t i,
+                                         uint32_t period, uint32_t slot, uint32_t mqp, Ctr &c, uint32_t &run_v,
+                                         uint32_t &run_n, uint32_t &pend_n, uint32_t &pend_q)
+{
+    // Net v1 counters (NetworkMetricsBucket::process_net_layer)
+    c.nev++;
+    c.nin += o.dir == 0; c.nout += o.dir == 1; c.nunk += o.dir == 2;
+    c.n4 += o.l3 == 4; c.n6 += o.l3 == 6;
+    c.nudp += o.l4 == 17; c.ntcp += o.l4 == 6; c.nsyn += o.l4 == 6 && o.syn; c.noth += o.l4 == 0;
+    uint32_t cl = o.caplen;
+    if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
+    if (cl == run_v) run_n++;
+    else { hist_put(P, S, true, slot, run_v, run_n); run_v = cl; run_n = 1; }
+    net_ips(P, S, R, o, i, true, slot, mqp, pend_n);
+    if (o.l4 == 17 && !(P.dbg & 4)) dns_lane(P, S, R, o, true, true, slot, period, i, c, pend_q, mqp);
+}
+
+// One record of a boundary tile (a period shift inside the tile, or periods outside the
+// kept window): the lane resolves its own period and updates HBM directly. Cold path.
+template <class A>
+__device__ __forceinline__ void lane_cold(const PvParams &P, BlockState &S, const A &R, const Parsed &o, uint64_t i)
+{
+    const uint32_t period = period_of(P, i);
+    const uint32_t slot = P.slot_of[period];
+    const bool upd = period >= P.skip_before;
+    uint64_t *s = slot_sum(P, slot);
+    uint32_t pend = 0;
+    if (upd) {
+        const bool nc = P.net_groups & PV_NET_COUNTERS_BIT;
+        atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_EVENTS], 1ull);
+        atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SAMPLES], 1ull);
+        if (nc) {
+            atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_TOTAL], 1ull);
+            atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.dir == 0 ? NC_IN : (o.dir == 1 ? NC_OUT : NC_UNK))], 1ull);
+            if (o.l3) atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l3 == 4 ? NC_V4 : NC_V6)], 1ull);
+            atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l4 == 17 ? NC_UDP : (o.l4 == 6 ? NC_TCP : NC_OTHER))], 1ull);
+            if (o.l4 == 6 && o.syn) atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SYN], 1ull);
+        }
+        const uint32_t cl = o.caplen > 65535 ? 65535 : o.caplen;
+        if (o.caplen > 65535) atomicOr(P.flags, PVF_BIG_CAPLEN);
+        atomicAdd((unsigned long long *)&s[PV_OFF_PAYLOAD + cl], 1ull);
+        net_ips(P, S, R, o, i, false, slot, 0, pend);
+    }
+    if (o.l4 == 17 && !(P.dbg & 4)) {
+        Ctr one;
+        one.zero();
+        dns_lane(P, S, R, o, false, upd, slot, period, i, one, pend, 0);
+        if (upd && one.dev) {
+            const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
+            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_EVENTS], 1ull);
+            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SAMPLES], 1ull);
+            if (dc) {
+                atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_TOTAL], 1ull);
+                atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_UDP], 1ull);
+                if (one.d4) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V4], 1ull);
+                if (one.d6) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V6], 1ull);
+                atomicAdd((unsigned long long *)&s[PV_OFF_DNS + (one.dq ? DC_QUERIES : DC_REPLIES)], 1ull);
+                if (one.dnoerr) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NOERROR], 1ull);
+                if (one.dnodata) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NODATA], 1ull);
+                if (one.dsrv) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SRVFAIL], 1ull);
+                if (one.dnx) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NX], 1ull);
+                if (one.dref) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_REFUSED], 1ull);
+            }
+        }
+    }
+}
+
 } // namespace
 
 // ------------------------------------------------------------------ the fused kernel
-extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const PvParams *__restrict__ Pp)
+extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel(const PvParams *__restrict__ Pp)
 {
     const PvParams &P = *Pp; // parameters live in device memory: scalar loads, no stack copy
     __shared__ BlockState S;
     block_clear(S);
-    if (threadIdx.x == 0) { S.nev = 0; S.nresp = 0; }
+    if (threadIdx.x == 0) {
+        S.nev = 0; S.nresp = 0; S.mq_n[0] = 0; S.mq_n[1] = 0;
+        S.ebase = (uint64_t)blockIdx.x * P.tiles_per_block * PV_BLOCK;
+    }
     __syncthreads();
     uint32_t cur_slot = 0xffffffffu; // block-uniform: slot the LDS state and counters belong to
     Ctr c;
@@ -408,13 +568,59 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const P
     // each workgroup owns a contiguous run of tiles (record order inside its event region)
     const uint64_t tbeg = (uint64_t)blockIdx.x * P.tiles_per_block;
     const uint64_t tend = tbeg + P.tiles_per_block < ntiles ? tbeg + P.tiles_per_block : ntiles;
+    // software pipeline: while tile t is parsed, the staged bytes of tile t+1 are in
+    // flight in registers, so HBM latency overlaps the parse instead of stalling each
+    // tile. Everything the next issue needs (tile span bounds, window-tile lane offsets)
+    // was loaded one tile earlier still, and cached lanes never wait on HBM mid-tile
+    // (table misses are queued), so no wait inside the tile drains the prefetch.
+    uint4 pf[PV_WIN / 16];
+    auto tile_off = [&](uint64_t t) -> uint64_t {
+        return t * PV_BLOCK < P.n ? (uint64_t)P.offs[t * PV_BLOCK] : P.rec_bytes;
+    };
+    auto lane_off = [&](uint64_t t) -> uint64_t {
+        const uint64_t r = t * PV_BLOCK + tid;
+        return (t < tend && r < P.n) ? (uint64_t)P.offs[r] : 0;
+    };
+    // issue the staging loads of tile t; b0/b1 = byte offsets of its first record and of
+    // the next tile's first record (uniform), loff = the lane's record offset
+    auto issue = [&](uint64_t t, uint64_t b0, uint64_t b1, uint64_t loff, uint32_t &chunks) {
+        const uint64_t base = b0 & ~15ull;
+        const uint64_t nch = (b1 - base + 15) >> 4;
+        if (nch <= PV_WINW * PV_BLOCK / 4) {
+            chunks = (uint32_t)nch;
+            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + base);
+#pragma unroll
+            for (int j = 0; j < PV_WIN / 16; j++) {
+                const uint32_t ch = j * PV_BLOCK + tid;
+                pf[j] = ch < chunks ? src[ch] : make_uint4(0, 0, 0, 0);
+            }
+        } else {
+            chunks = 0;
+            const bool act = t * PV_BLOCK + tid < P.n;
+            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + (loff & ~15ull));
+#pragma unroll
+            for (int j = 0; j < PV_WIN / 16; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    // ring: tile t's (b, lane offset) in use; t+1 and t+2 bounds, t+1 lane offsets loaded
+    uint64_t b_cur = 0, b_n1 = 0, b_n2 = 0, off_cur = 0, off_n1 = 0;
+    uint32_t chunks_cur = 0;
+    if (tbeg < tend) {
+        b_cur = tile_off(tbeg);
+        b_n1 = tile_off(tbeg + 1);
+        b_n2 = tile_off(tbeg + 2);
+        off_cur = lane_off(tbeg);
+        off_n1 = lane_off(tbeg + 1);
+        issue(tbeg, b_cur, b_n1, off_cur, chunks_cur);
+    }
     for (uint64_t tile = tbeg; tile < tend; tile++) {
         const uint64_t t0 = tile * PV_BLOCK;
         const uint64_t t1 = (t0 + PV_BLOCK < P.n ? t0 + PV_BLOCK : P.n) - 1;
         // periods are contiguous index ranges (host-provided start indices): a tile is
         // uniform when its first and last record share a period
         const uint32_t p_lo = period_of(P, t0), p_hi = period_of(P, t1);
-        const bool uniform = p_lo == p_hi && p_lo >= P.skip_before;
+        const bool straddle = p_lo != p_hi; // pv_boundary_kernel's tile
+        const bool uniform = !straddle && p_lo >= P.skip_before;
         if (uniform && P.slot_of[p_lo] != cur_slot) {
             if (cur_slot != 0xffffffffu) {
                 hist_put(P, S, true, cur_slot, run_v, run_n);
@@ -424,116 +630,69 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const P
             }
             cur_slot = P.slot_of[p_lo];
         }
-        const bool cached = uniform && P.slot_of[p_lo] == cur_slot;
+        const bool cached = uniform; // bucket slot cur_slot, period p_lo
 
         const uint64_t i = t0 + tid;
-        const bool active = i <= t1;
-        const uint64_t off = active ? P.offs[i] : 0;
-        // stage this record's first PV_WIN bytes (16-B aligned) into the lane's LDS window
-        const uint64_t wbase = off & ~15ull;
-        {
-            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + wbase);
+        const bool active = i <= t1 && !straddle;
+        const uint64_t off = off_cur;
+        const uint64_t base = __builtin_amdgcn_readfirstlane((uint32_t)b_cur) & ~15u;
+        const uint32_t chunks = __builtin_amdgcn_readfirstlane(chunks_cur);
+        // commit tile t's staged bytes to LDS
+        if (chunks) {
+            uint4 *st4 = reinterpret_cast<uint4 *>(S.stage);
+#pragma unroll
+            for (int j = 0; j < PV_WIN / 16; j++) st4[j * PV_BLOCK + tid] = pf[j];
+        } else {
 #pragma unroll
             for (int j = 0; j < PV_WIN / 16; j++) {
-                uint4 v = active ? src[j] : make_uint4(0, 0, 0, 0);
-                S.win[4 * j + 0][tid] = v.x;
-                S.win[4 * j + 1][tid] = v.y;
-                S.win[4 * j + 2][tid] = v.z;
-                S.win[4 * j + 3][tid] = v.w;
+                S.stage[(4 * j + 0) * PV_BLOCK + tid] = pf[j].x;
+                S.stage[(4 * j + 1) * PV_BLOCK + tid] = pf[j].y;
+                S.stage[(4 * j + 2) * PV_BLOCK + tid] = pf[j].z;
+                S.stage[(4 * j + 3) * PV_BLOCK + tid] = pf[j].w;
             }
         }
+        lds_barrier(); // packed tiles: lanes read bytes other lanes staged
+        // issue tile t+1's staging loads; load tile t+3's bound and tile t+2's lane offsets
+        if (tile + 1 < tend) {
+            const uint64_t b0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b_n1 >> 32)) << 32) |
+                                __builtin_amdgcn_readfirstlane((uint32_t)b_n1);
+            const uint64_t b1 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b_n2 >> 32)) << 32) |
+                                __builtin_amdgcn_readfirstlane((uint32_t)b_n2);
+            issue(tile + 1, b0, b1, off_n1, chunks_cur);
+            b_cur = b_n1;
+            b_n1 = b_n2;
+            b_n2 = tile_off(tile + 3);
+            off_cur = off_n1;
+            off_n1 = lane_off(tile + 2);
+        }
+        const uint32_t mqp = (uint32_t)(tile & 1);
+        uint32_t pend_n = 0, pend_q = 0; // CPC filter keys to commit after the tile barrier
+        if (P.dbg & 1) { c.nev += active && (S.stage[tid] | 1); continue; }
         if (active) {
-            const WAcc R{P.recs, wbase, &S.win[0][tid]};
+            const TAcc R = chunks ? TAcc{P.recs, S.stage, base, chunks * 16 - 4, 1u, 0u}
+                                  : TAcc{P.recs, S.stage, off & ~15ull, PV_WIN - 4, (uint32_t)PV_BLOCK, tid};
             Parsed o;
             parse_record(R, P, off, o);
-            const uint32_t period = uniform ? p_lo : period_of(P, i);
-            const uint32_t slot = P.slot_of[period];
-            const bool upd = period >= P.skip_before;
-            if (upd && !cached) {
-                // boundary tile: this lane's record goes straight to HBM
-                Ctr one;
-                one.zero();
-                one.nev = 1; one.nin = o.dir == 0; one.nout = o.dir == 1; one.nunk = o.dir == 2;
-                one.n4 = o.l3 == 4; one.n6 = o.l3 == 6; one.nudp = o.l4 == 17; one.ntcp = o.l4 == 6;
-                one.nsyn = o.l4 == 6 && o.syn; one.noth = o.l4 == 0;
-                uint64_t *s = slot_sum(P, slot);
-                const bool nc = P.net_groups & PV_NET_COUNTERS_BIT;
-                atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_EVENTS], 1ull);
-                atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SAMPLES], 1ull);
-                if (nc) {
-                    atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_TOTAL], 1ull);
-                    atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.dir == 0 ? NC_IN : (o.dir == 1 ? NC_OUT : NC_UNK))], 1ull);
-                    if (o.l3) atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l3 == 4 ? NC_V4 : NC_V6)], 1ull);
-                    atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l4 == 17 ? NC_UDP : (o.l4 == 6 ? NC_TCP : NC_OTHER))], 1ull);
-                    if (o.l4 == 6 && o.syn) atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SYN], 1ull);
-                }
-                uint32_t cl = o.caplen > 65535 ? 65535 : o.caplen;
-                if (o.caplen > 65535) atomicOr(P.flags, PVF_BIG_CAPLEN);
-                atomicAdd((unsigned long long *)&s[PV_OFF_PAYLOAD + cl], 1ull);
-            } else if (upd) {
-                // ---- Net v1 counters (NetworkMetricsBucket::process_net_layer)
-                c.nev++;
-                c.nin += o.dir == 0; c.nout += o.dir == 1; c.nunk += o.dir == 2;
-                c.n4 += o.l3 == 4; c.n6 += o.l3 == 6;
-                c.nudp += o.l4 == 17; c.ntcp += o.l4 == 6; c.nsyn += o.l4 == 6 && o.syn; c.noth += o.l4 == 0;
-                uint32_t cl = o.caplen;
-                if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
-                if (cl == run_v) run_n++;
-                else { hist_put(P, S, true, cur_slot, run_v, run_n); run_v = cl; run_n = 1; }
-            }
-            if (upd) {
-                // ---- cardinality + top IPs (process_net_layer :745-763)
-                const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
-                if (o.has4 && o.dir != 2) {
-                    uint32_t ip = R.u32(o.dir == 0 ? o.v4 + 12 : o.v4 + 16);
-                    if (ip) {
-                        if (card) {
-                            uint64_t h1, h2;
-                            murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
-                            cpc_add(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
-                        }
-                        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV4, ip), 1, (uint32_t)i);
-                    }
-                } else if (!o.has4 && o.has6 && o.dir != 2) {
-                    uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
-                    uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
-                    uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
-                    if (w0 | w1) {
-                        uint64_t h1, h2;
-                        murmur_16(w0, w1, h1, h2);
-                        if (card) cpc_add(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
-                        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV6, h1 ^ (h2 << 1)), 1, (uint32_t)i);
-                    }
-                }
-            }
-            // ---- DNS v1 over UDP
-            if (o.l4 == 17) {
-                if (cached || !upd) dns_lane(P, S, R, o, cached, upd, slot, period, i, c);
-                else {
-                    Ctr one;
-                    one.zero();
-                    dns_lane(P, S, R, o, false, upd, slot, period, i, one);
-                    uint64_t *s = slot_sum(P, slot);
-                    if (one.dev) {
-                        const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
-                        atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_EVENTS], 1ull);
-                        atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SAMPLES], 1ull);
-                        if (dc) {
-                            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_TOTAL], 1ull);
-                            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_UDP], 1ull);
-                            if (one.d4) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V4], 1ull);
-                            if (one.d6) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V6], 1ull);
-                            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + (one.dq ? DC_QUERIES : DC_REPLIES)], 1ull);
-                            if (one.dnoerr) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NOERROR], 1ull);
-                            if (one.dnodata) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NODATA], 1ull);
-                            if (one.dsrv) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SRVFAIL], 1ull);
-                            if (one.dnx) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NX], 1ull);
-                            if (one.dref) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_REFUSED], 1ull);
-                        }
-                    }
-                }
+            if (P.dbg & 2) { c.nev += 1; c.nin += o.dir == 0; c.nudp += o.l4 == 17; continue; }
+            if (cached) lane_hot(P, S, R, o, i, p_lo, cur_slot, mqp, c, run_v, run_n, pend_n, pend_q);
+            else if (o.l4 == 17) // a tile before the kept window: DNS transaction events only
+                dns_lane(P, S, R, o, false, false, 0, p_lo, i, c, pend_q, 0);
+        }
+        if (P.dbg & 3) continue; // (profiling stages skip lanes with `continue`: no barrier then)
+        // every lane's CPC filter probes and queued misses of this tile are in LDS
+        lds_barrier();
+        cpc_commit(S, pend_n);
+        cpc_commit(S, pend_q);
+        const uint32_t nq = S.mq_n[mqp];
+        if (nq) {
+            __syncthreads(); // the queued entries (global stores of other lanes) are visible
+            const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * PV_MQ_CAP * 2;
+            for (uint32_t j = tid; j < nq; j += PV_BLOCK) {
+                const uint64_t v = q[2 * j + 1];
+                global_add(P, cur_slot, q[2 * j], (uint32_t)v, (uint32_t)(v >> 32));
             }
         }
+        if (tid == 0) S.mq_n[mqp ^ 1] = 0; // next tile's queue (last drained before this tile's first barrier)
     }
     if (cur_slot != 0xffffffffu) {
         hist_put(P, S, true, cur_slot, run_v, run_n);
@@ -543,6 +702,33 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_net_dns_kernel(const P
     __syncthreads();
     if (threadIdx.x == 0) {
         P.blk_events[blockIdx.x] = S.nev;
+        if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
+    }
+}
+
+// Tiles that hold a period shift: one workgroup per tile, each lane resolves its own
+// period and updates HBM directly (no LDS bucket state). Runs after pv_net_dns_kernel
+// on the same stream; its DNS events go to regions after the main kernel's.
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_boundary_kernel(const PvParams *__restrict__ Pp)
+{
+    const PvParams &P = *Pp;
+    __shared__ BlockState S;
+    if (threadIdx.x == 0) {
+        S.nev = 0; S.nresp = 0;
+        S.ebase = ((uint64_t)P.grid_main * P.tiles_per_block + blockIdx.x) * PV_BLOCK;
+    }
+    __syncthreads();
+    const uint64_t i = (uint64_t)P.btile[blockIdx.x] * PV_BLOCK + threadIdx.x;
+    if (i < P.n) {
+        const GAcc R{P.recs};
+        Parsed o;
+        const uint64_t off = P.offs[i];
+        parse_record(R, P, off, o);
+        lane_cold(P, S, R, o, i);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        P.blk_events[P.grid_main + blockIdx.x] = S.nev;
         if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
     }
 }
@@ -561,7 +747,9 @@ extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint
     }
     __syncthreads();
     const uint32_t cnt = P.blk_events[blockIdx.x];
-    const uint64_t src = (uint64_t)blockIdx.x * P.tiles_per_block * PV_BLOCK;
+    const uint64_t src = (blockIdx.x < P.grid_main ? (uint64_t)blockIdx.x * P.tiles_per_block
+                                                   : (uint64_t)P.grid_main * P.tiles_per_block + (blockIdx.x - P.grid_main)) *
+                         PV_BLOCK;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         P.skeys[base + j] = P.ekeys[src + j];
         P.svals[base + j] = (uint32_t)(src + j);

@@ -18,6 +18,8 @@
 // name arena partitions per slot: workgroup b allocates from partition b % PV_ARENA_PARTS,
 // so no bump pointer is shared by more than a few workgroups
 #define PV_ARENA_PARTS 64
+// per-workgroup top-N miss queue: 256 lanes x at most 6 hashed top-N updates per record
+#define PV_MQ_CAP 2048
 
 // group bits (same values as pv_net_group / pv_dns_group in include/pvgpu.h)
 #define PV_NET_COUNTERS_BIT 1u
@@ -114,6 +116,15 @@ struct PvXValid {
 };
 
 
+// Device pointers carry the global address space in the device compile, so the kernels
+// emit global_* (not flat_*) memory instructions: flat accesses also count against
+// lgkmcnt, which would make every LDS wait drain the in-flight HBM prefetch.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PV_G __attribute__((address_space(1)))
+#else
+#define PV_G
+#endif
+
 struct PvSubnets {
     uint32_t n4, n6;
     uint32_t v4_addr[PV_MAX_SUBNETS]; // in_addr.s_addr (network byte order as loaded LE)
@@ -124,8 +135,8 @@ struct PvSubnets {
 };
 
 struct PvParams {
-    const uint8_t *recs;
-    const uint32_t *offs;
+    const PV_G uint8_t *recs;
+    const PV_G uint32_t *offs;
     uint64_t n;
     uint32_t linktype;
     uint32_t ts_nano;
@@ -139,42 +150,48 @@ struct PvParams {
     uint64_t gbase;
     PvSubnets nets;
     // device state
-    uint64_t *sum;    // PV_SLOTS x PV_SUM_WORDS
-    int64_t *cpc;     // PV_SLOTS x PV_MIN_WORDS
-    uint64_t *tkeys;  // PV_SLOTS x tcap
-    uint64_t *tcnt;
-    uint32_t *taux;
+    PV_G uint64_t *sum;    // PV_SLOTS x PV_SUM_WORDS
+    PV_G int64_t *cpc;     // PV_SLOTS x PV_MIN_WORDS
+    PV_G uint64_t *tkeys;  // PV_SLOTS x tcap
+    PV_G uint64_t *tcnt;
+    PV_G uint32_t *taux;
     uint32_t tcap_log2;
-    uint8_t *arena;      // PV_SLOTS x arena_cap, each slot split in PV_ARENA_PARTS partitions
-    uint64_t *arena_top; // PV_SLOTS x PV_ARENA_PARTS bump pointers (bytes used in the partition)
+    PV_G uint8_t *arena;      // PV_SLOTS x arena_cap, each slot split in PV_ARENA_PARTS partitions
+    PV_G uint64_t *arena_top; // PV_SLOTS x PV_ARENA_PARTS bump pointers (bytes used in the partition)
     uint64_t arena_cap;  // bytes per slot
-    PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
-    uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
-    uint32_t *blk_events; // events appended by each workgroup
-    uint64_t *skeys;      // packed keys (sort input)
-    uint32_t *svals;      // packed event slot positions (sort input)
-    uint32_t *n_events;   // [0] packed total (pv_xact_compact), [1] responses
+    PV_G PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
+    PV_G uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
+    PV_G uint32_t *blk_events; // events appended by each workgroup
+    PV_G uint64_t *skeys;      // packed keys (sort input)
+    PV_G uint32_t *svals;      // packed event slot positions (sort input)
+    PV_G uint32_t *n_events;   // [0] packed total (pv_xact_compact), [1] responses
     uint32_t want_events;
     uint32_t tiles_per_block;
-    uint32_t *flags;
-    uint32_t *dns_first; // per period: min record index of a DNS event in that period
-    uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
+    uint64_t rec_bytes; // bytes of the record run (end of the last record)
+    PV_G uint64_t *mq;    // per-workgroup queues of top-N cache misses: PV_MQ_CAP x {key, w | rep << 32}
+    uint32_t grid_main;   // workgroups of pv_net_dns_kernel
+    uint32_t n_btiles;    // tiles holding a period shift (handled by pv_boundary_kernel)
+    uint32_t btile[PV_MAX_SHIFTS];
+    uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane
+    PV_G uint32_t *flags;
+    PV_G uint32_t *dns_first; // per period: min record index of a DNS event in that period
+    PV_G uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
 };
 
 struct PvXactParams {
     PvParams P;            // record access + top-N tables (slow transaction names)
-    const PvXEvent *events;
-    const uint64_t *skeys; // sorted (hash32(key) << 32 | idx)
-    const uint32_t *svals; // event position for each sorted key
+    const PV_G PvXEvent *events;
+    const PV_G uint64_t *skeys; // sorted (hash32(key) << 32 | idx)
+    const PV_G uint32_t *svals; // event position for each sorted key
     uint32_t n;
     uint32_t ttl_s, ttl_ms;
     uint32_t quantiles;
     uint32_t slot_gen[PV_MAX_SHIFTS + 1]; // slot | generation << 8 per period
     float thr_from[PV_MAX_SHIFTS + 1];    // p90 slow thresholds per period, < 0 = not known yet
     float thr_to[PV_MAX_SHIFTS + 1];
-    PvXValue *vals;
-    uint32_t *n_vals;
+    PV_G PvXValue *vals;
+    PV_G uint32_t *n_vals;
     uint32_t vals_cap;
-    PvXValid *valid;
-    uint32_t *n_valid;
+    PV_G PvXValid *valid;
+    PV_G uint32_t *n_valid;
 };
