@@ -40,6 +40,7 @@ extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
 extern "C" __global__ void pv_boundary_kernel(const PvParams *P);
+extern "C" __global__ void pv_topn_insert(const PvParams *P);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
@@ -230,7 +231,10 @@ struct pv_ctx {
     PvXEvent *d_events = nullptr;
     uint64_t *d_ekeys = nullptr;
     uint32_t *d_blk_events = nullptr;
-    uint64_t *d_mq = nullptr; // per-workgroup top-N miss queues
+    uint64_t *d_mq = nullptr; // per-workgroup top-N update logs (grown on demand)
+    size_t mq_bytes = 0;
+    uint32_t *d_mq_cnt = nullptr;
+    uint64_t *d_stamps = nullptr; // diagnostic phase stamps (PV_STAMPS env + -DPV_STAMPS build)
     int cus = 256;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
@@ -822,7 +826,8 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_arena_top, PV_SLOTS * PV_ARENA_PARTS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_events, (size_t)ev_cap * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)ev_cap * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_mq, (size_t)c->cus * 4 * PV_MQ_CAP * 16)) ||
+        !hip_ok(e = hipMalloc(&c->d_mq_cnt, 65536 * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_stamps, 65536 * 4 * 8 * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)mr * 8)) || !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)mr * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_svals, (size_t)mr * 4)) || !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)mr * 4)) ||
@@ -850,7 +855,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_mq_cnt, c->d_stamps,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -1027,7 +1032,20 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     }
     grid = (uint32_t)((tiles + P.tiles_per_block - 1) / P.tiles_per_block);
     P.grid_main = grid;
+    P.mq_cap = P.tiles_per_block * 256u * PV_MQ_PER_REC + PV_CACHE_MAX * (P.n_shift + 1);
+    {
+        const size_t need = (size_t)grid * P.mq_cap * 16;
+        if (need > c->mq_bytes) {
+            if (c->d_mq) hipFree(c->d_mq);
+            c->d_mq = nullptr;
+            c->mq_bytes = 0;
+            if (!hip_ok(e = hipMalloc(&c->d_mq, need))) return c->hipfail(e, "top-N update log");
+            c->mq_bytes = need;
+        }
+    }
     P.mq = c->d_mq;
+    P.mq_cnt = c->d_mq_cnt;
+    P.stamps = c->d_stamps;
     // tiles that hold a period shift go to pv_boundary_kernel
     P.n_btiles = 0;
     for (uint32_t k = 0; k < P.n_shift; k++) {
@@ -1044,6 +1062,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     hipLaunchKernelGGL(pv_net_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_dns_kernel");
+    hipLaunchKernelGGL(pv_topn_insert, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (P.n_btiles) {
         hipLaunchKernelGGL(pv_boundary_kernel, dim3(P.n_btiles), dim3(256), 0, st, (const PvParams *)c->d_params);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_boundary_kernel");
@@ -1065,6 +1084,18 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     uint32_t flags = status[ST_FLAGS];
     if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
     if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
+    if (getenv("PV_STAMPS")) {
+        std::vector<uint64_t> st((size_t)grid * 4 * 8);
+        if (hip_ok(hipMemcpy(st.data(), c->d_stamps, st.size() * 8, hipMemcpyDeviceToHost))) {
+            double sum[8] = {0};
+            for (size_t w = 0; w < (size_t)grid * 4; w++)
+                for (int k = 0; k < 8; k++) sum[k] += (double)st[w * 8 + k];
+            fprintf(stderr, "pv_stamps (mean cycles per wave, %u tiles/wg):", P.tiles_per_block);
+            static const char *nm[8] = {"slot", "commit", "barA", "issue", "parse", "lane", "barB", "flush"};
+            for (int k = 0; k < 8; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (grid * 4.0));
+            fprintf(stderr, "\n");
+        }
+    }
     uint32_t nev = status[ST_NEV];
     const uint32_t nresp = status[ST_NRESP];
     if (nresp == 0 && P.n_shift == 0) nev = 0; // nothing to pair, nothing to purge in this batch

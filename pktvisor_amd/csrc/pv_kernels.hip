@@ -32,6 +32,26 @@
 #define PV_CACHE_N 2048
 #endif
 #define PV_HIST_N 2048
+// diagnostic build (-DPV_STAMPS): per-wave cycles spent in each phase of the tile loop
+#ifdef PV_STAMPS
+#define STAMP_DECL                                                                           \
+    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                          \
+    uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(k)                                                                             \
+    {                                                                                        \
+        const uint64_t now = __builtin_amdgcn_s_memtime();                                   \
+        st_acc[k] += now - st_prev;                                                          \
+        st_prev = now;                                                                       \
+    }
+#define STAMP_FLUSH                                                                          \
+    if ((threadIdx.x & 63) == 0)                                                             \
+        for (int k_ = 0; k_ < 8; k_++) P.stamps[((uint64_t)blockIdx.x * 4 + threadIdx.x / 64) * 8 + k_] = st_acc[k_];
+#else
+#define STAMP_DECL
+#define STAMP(k)
+#define STAMP_FLUSH
+#endif
+static_assert(PV_CACHE_N <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cache entries per flush");
 #ifndef PV_WIN
 #define PV_WIN 128 // bytes of each record staged into LDS (record header + frame start)
 #endif
@@ -188,7 +208,7 @@ struct BlockState {
     uint32_t crep[PV_CACHE_N];
     uint32_t hist[PV_HIST_N];        // payload-size histogram (caplen < PV_HIST_N)
     uint32_t cpcf[PV_CPCF_N];        // (sketch << 17 | coupon) + 1 submitted in an earlier tile
-    uint32_t mq_n[2];                // queued top-N misses of the current tile (tile parity)
+    uint32_t mq_n;                   // entries in this workgroup's top-N update log
     uint32_t nev;                    // DNS events appended to this block's region
     uint64_t ebase;                  // first event slot of this block's region
     uint32_t nresp;                  // of which responses
@@ -211,24 +231,37 @@ __device__ __forceinline__ bool cache_add(BlockState &S, uint64_t key, uint32_t 
     return false;
 }
 
-// Cached tiles: LDS cache first. A miss of a dense table is a fire-and-forget HBM
-// atomic; a miss of a hashed table is stored to the workgroup's HBM miss queue and
-// inserted after the tile, so no lane waits on an HBM round trip mid-tile (which would
-// also drain the next tile's in-flight prefetch). The queue cannot overflow: at most 6
-// hashed updates per record (PV_MQ_CAP).
+// Top-N updates that the LDS cache cannot absorb go to the workgroup's HBM update log
+// (fire-and-forget stores; slot in the top 4 key bits, which hashed metrics leave free);
+// pv_topn_insert applies the log to the global tables after the parse kernel, so no
+// lane of the parse kernel ever waits on an HBM round trip for a table update.
+__device__ __forceinline__ void log_put(const PvParams &P, BlockState &S, uint32_t slot, uint64_t key, uint32_t w,
+                                        uint32_t rep)
+{
+    const uint32_t q = atomicAdd(&S.mq_n, 1u);
+    PV_G uint64_t *e = P.mq + ((uint64_t)blockIdx.x * P.mq_cap + q) * 2;
+    e[0] = key | ((uint64_t)slot << 60);
+    e[1] = (uint64_t)w | ((uint64_t)rep << 32);
+}
+// dense tables (ports, qtypes, rcodes): plain HBM atomics, nothing waits on them
+__device__ __forceinline__ void dense_add(const PvParams &P, uint32_t slot, uint64_t key, uint32_t w)
+{
+    PV_G uint64_t *sum = P.sum + (uint64_t)slot * PV_SUM_WORDS;
+    const uint32_t metric = PV_KEY_METRIC(key);
+    const uint32_t off = metric == TM_DENSE_PORT ? PV_OFF_PORT + (uint32_t)(key & 0xffff)
+                       : metric == TM_DENSE_QTYPE ? PV_OFF_QTYPE + (uint32_t)(key & 0xffff)
+                                                  : PV_OFF_RCODE + (uint32_t)(key & 0xf);
+    __hip_atomic_fetch_add(sum + off, (uint64_t)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// cached: LDS cache, then the update log; uncached (boundary kernel): the global table
 __device__ __forceinline__ void top_add(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint64_t key,
-                                        uint32_t w, uint32_t rep, uint32_t mqp = 0)
+                                        uint32_t w, uint32_t rep)
 {
     if (cached) {
         if (cache_add(S, key, w, rep)) return;
-        const uint32_t metric = PV_KEY_METRIC(key);
-        if (metric < TM_DENSE_PORT) {
-            const uint32_t q = atomicAdd(&S.mq_n[mqp], 1u);
-            PV_G uint64_t *e = P.mq + ((uint64_t)blockIdx.x * PV_MQ_CAP + q) * 2;
-            e[0] = key;
-            e[1] = (uint64_t)w | ((uint64_t)rep << 32);
-            return;
-        }
+        if (PV_KEY_METRIC(key) >= TM_DENSE_PORT) dense_add(P, slot, key, w);
+        else log_put(P, S, slot, key, w, rep);
+        return;
     }
     global_add(P, slot, key, w, rep);
 }
@@ -315,8 +348,10 @@ __device__ void block_flush(const PvParams &P, BlockState &S, uint32_t slot)
     if (slot < PV_SLOTS) {
         uint64_t *sum = slot_sum(P, slot);
         for (uint32_t i = threadIdx.x; i < PV_CACHE_N; i += PV_BLOCK) {
-            uint64_t k = S.ckey[i];
-            if (k) global_add(P, slot, k, S.ccnt[i], S.crep[i]);
+            const uint64_t k = S.ckey[i];
+            if (!k) continue;
+            if (PV_KEY_METRIC(k) >= TM_DENSE_PORT) dense_add(P, slot, k, S.ccnt[i]);
+            else log_put(P, S, slot, k, S.ccnt[i], S.crep[i]);
         }
         for (uint32_t i = threadIdx.x; i < PV_HIST_N; i += PV_BLOCK)
             if (S.hist[i]) atomicAdd((unsigned long long *)&sum[PV_OFF_PAYLOAD + i], (unsigned long long)S.hist[i]);
@@ -347,7 +382,7 @@ __device__ __forceinline__ void hist_put(const PvParams &P, BlockState &S, bool 
 template <class A>
 __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const A &R, const Parsed &o, bool cached,
                                          bool upd, uint32_t slot, uint32_t period, uint64_t i, Ctr &c,
-                                         uint32_t &pend_q, uint32_t mqp)
+                                         uint32_t &pend_q)
 {
     uint32_t pw = R.u32(o.l4off);
     uint32_t sport = ((pw & 0xff) << 8) | ((pw >> 8) & 0xff);
@@ -384,9 +419,9 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
         c.dsrv += qr && rcode == 2; c.dnx += qr && rcode == 3; c.dref += qr && rcode == 5;
         DnsInfo d;
         dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
-        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_PORT, metric_port), 1, (uint32_t)i, mqp);
+        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_PORT, metric_port), 1, (uint32_t)i);
         if (d.ok) {
-            if (qr) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_RCODE, rcode), 1, (uint32_t)i, mqp);
+            if (qr) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_RCODE, rcode), 1, (uint32_t)i);
             if (d.has_query) {
                 NameStats st;
                 st.init();
@@ -395,29 +430,29 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
                 st.mm.finish(h1, h2);
                 if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT))
                     cpc_add(P, S, cached, slot, CPC_QNAME, cpc_coupon(h1, h2), (int64_t)(P.gbase + i), pend_q);
-                top_add(P, S, cached, slot, PV_KEY(TM_DENSE_QTYPE, d.qtype), 1, (uint32_t)i, mqp);
+                top_add(P, S, cached, slot, PV_KEY(TM_DENSE_QTYPE, d.qtype), 1, (uint32_t)i);
                 if (P.dns_groups & PV_DNS_TOP_QNAMES_BIT) {
                     const uint64_t fp_full = fp56(st.ph, st.n, 0);
                     if (qr) {
-                        if (rcode == 2) top_add(P, S, cached, slot, PV_KEY(TM_SRVFAIL, fp_full), 1, (uint32_t)i, mqp);
-                        else if (rcode == 3) top_add(P, S, cached, slot, PV_KEY(TM_NX, fp_full), 1, (uint32_t)i, mqp);
-                        else if (rcode == 5) top_add(P, S, cached, slot, PV_KEY(TM_REFUSED, fp_full), 1, (uint32_t)i, mqp);
+                        if (rcode == 2) top_add(P, S, cached, slot, PV_KEY(TM_SRVFAIL, fp_full), 1, (uint32_t)i);
+                        else if (rcode == 3) top_add(P, S, cached, slot, PV_KEY(TM_NX, fp_full), 1, (uint32_t)i);
+                        else if (rcode == 5) top_add(P, S, cached, slot, PV_KEY(TM_REFUSED, fp_full), 1, (uint32_t)i);
                         else if (rcode == 0) {
                             if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                                top_add(P, S, cached, slot, PV_KEY(TM_NOERROR, fp_full), 1, (uint32_t)i, mqp);
-                            if (!ancount) top_add(P, S, cached, slot, PV_KEY(TM_NODATA, fp_full), 1, (uint32_t)i, mqp);
+                                top_add(P, S, cached, slot, PV_KEY(TM_NOERROR, fp_full), 1, (uint32_t)i);
+                            if (!ancount) top_add(P, S, cached, slot, PV_KEY(TM_NODATA, fp_full), 1, (uint32_t)i);
                         }
                         if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                            top_add(P, S, cached, slot, PV_KEY(TM_SIZED, fp_full), dlen, (uint32_t)i, mqp);
+                            top_add(P, S, cached, slot, PV_KEY(TM_SIZED, fp_full), dlen, (uint32_t)i);
                     }
                     int q2, q3;
                     uint64_t h2p, h3p;
                     agg_domain(st, q2, q3, h2p, h3p);
                     const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
-                    top_add(P, S, cached, slot, PV_KEY(TM_QNAME2, fp56(k2, st.n - q2, 0)), 1, (uint32_t)i, mqp);
+                    top_add(P, S, cached, slot, PV_KEY(TM_QNAME2, fp56(k2, st.n - q2, 0)), 1, (uint32_t)i);
                     if (q3 >= 0 && (uint32_t)q3 < st.n) {
                         const uint64_t k3 = q3 == 0 ? st.ph : suffix_hash(st, q3, h3p);
-                        top_add(P, S, cached, slot, PV_KEY(TM_QNAME3, fp56(k3, st.n - q3, 0)), 1, (uint32_t)i, mqp);
+                        top_add(P, S, cached, slot, PV_KEY(TM_QNAME3, fp56(k3, st.n - q3, 0)), 1, (uint32_t)i);
                     }
                 }
             }
@@ -448,7 +483,7 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
 // cardinality + top IPs of one record (NetworkMetricsBucket::process_net_layer :745-763)
 template <class A>
 __device__ __forceinline__ void net_ips(const PvParams &P, BlockState &S, const A &R, const Parsed &o, uint64_t i,
-                                        bool cached, uint32_t slot, uint32_t mqp, uint32_t &pend_n)
+                                        bool cached, uint32_t slot, uint32_t &pend_n)
 {
     const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
     if (o.dir == 2) return;
@@ -461,7 +496,7 @@ __device__ __forceinline__ void net_ips(const PvParams &P, BlockState &S, const 
             cpc_add(P, S, cached, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i),
                     pend_n);
         }
-        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV4, ip), 1, (uint32_t)i, mqp);
+        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV4, ip), 1, (uint32_t)i);
     } else if (o.has6) {
         const uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
         const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
@@ -472,14 +507,14 @@ __device__ __forceinline__ void net_ips(const PvParams &P, BlockState &S, const 
         if (card)
             cpc_add(P, S, cached, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i),
                     pend_n);
-        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV6, h1 ^ (h2 << 1)), 1, (uint32_t)i, mqp);
+        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV6, h1 ^ (h2 << 1)), 1, (uint32_t)i);
     }
 }
 
 // One record of a tile whose records all fall in period `period` -> bucket slot `slot`
 // (both workgroup-uniform): counters in registers, tables through the LDS cache.
 __device__ __forceinline__ void lane_hot(const PvParams &P, BlockState &S, const TAcc &R, const Parsed &o, uint64_t i,
-                                         uint32_t period, uint32_t slot, uint32_t mqp, Ctr &c, uint32_t &run_v,
+                                         uint32_t period, uint32_t slot, Ctr &c, uint32_t &run_v,
                                          uint32_t &run_n, uint32_t &pend_n, uint32_t &pend_q)
 {
     // Net v1 counters (NetworkMetricsBucket::process_net_layer)
@@ -491,8 +526,8 @@ __device__ __forceinline__ void lane_hot(const PvParams &P, BlockState &S, const
     if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
     if (cl == run_v) run_n++;
     else { hist_put(P, S, true, slot, run_v, run_n); run_v = cl; run_n = 1; }
-    net_ips(P, S, R, o, i, true, slot, mqp, pend_n);
-    if (o.l4 == 17 && !(P.dbg & 4)) dns_lane(P, S, R, o, true, true, slot, period, i, c, pend_q, mqp);
+    net_ips(P, S, R, o, i, true, slot, pend_n);
+    if (o.l4 == 17 && !(P.dbg & 4)) dns_lane(P, S, R, o, true, true, slot, period, i, c, pend_q);
 }
 
 // One record of a boundary tile (a period shift inside the tile, or periods outside the
@@ -519,12 +554,12 @@ __device__ __forceinline__ void lane_cold(const PvParams &P, BlockState &S, cons
         const uint32_t cl = o.caplen > 65535 ? 65535 : o.caplen;
         if (o.caplen > 65535) atomicOr(P.flags, PVF_BIG_CAPLEN);
         atomicAdd((unsigned long long *)&s[PV_OFF_PAYLOAD + cl], 1ull);
-        net_ips(P, S, R, o, i, false, slot, 0, pend);
+        net_ips(P, S, R, o, i, false, slot, pend);
     }
     if (o.l4 == 17 && !(P.dbg & 4)) {
         Ctr one;
         one.zero();
-        dns_lane(P, S, R, o, false, upd, slot, period, i, one, pend, 0);
+        dns_lane(P, S, R, o, false, upd, slot, period, i, one, pend);
         if (upd && one.dev) {
             const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
             atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_EVENTS], 1ull);
@@ -554,7 +589,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
     __shared__ BlockState S;
     block_clear(S);
     if (threadIdx.x == 0) {
-        S.nev = 0; S.nresp = 0; S.mq_n[0] = 0; S.mq_n[1] = 0;
+        S.nev = 0; S.nresp = 0; S.mq_n = 0;
         S.ebase = (uint64_t)blockIdx.x * P.tiles_per_block * PV_BLOCK;
     }
     __syncthreads();
@@ -613,6 +648,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
         off_n1 = lane_off(tbeg + 1);
         issue(tbeg, b_cur, b_n1, off_cur, chunks_cur);
     }
+    STAMP_DECL
     for (uint64_t tile = tbeg; tile < tend; tile++) {
         const uint64_t t0 = tile * PV_BLOCK;
         const uint64_t t1 = (t0 + PV_BLOCK < P.n ? t0 + PV_BLOCK : P.n) - 1;
@@ -631,6 +667,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
             cur_slot = P.slot_of[p_lo];
         }
         const bool cached = uniform; // bucket slot cur_slot, period p_lo
+        STAMP(0)
 
         const uint64_t i = t0 + tid;
         const bool active = i <= t1 && !straddle;
@@ -651,7 +688,9 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
                 S.stage[(4 * j + 3) * PV_BLOCK + tid] = pf[j].w;
             }
         }
+        STAMP(1)
         lds_barrier(); // packed tiles: lanes read bytes other lanes staged
+        STAMP(2)
         // issue tile t+1's staging loads; load tile t+3's bound and tile t+2's lane offsets
         if (tile + 1 < tend) {
             const uint64_t b0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b_n1 >> 32)) << 32) |
@@ -665,7 +704,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
             off_cur = off_n1;
             off_n1 = lane_off(tile + 2);
         }
-        const uint32_t mqp = (uint32_t)(tile & 1);
+        STAMP(3)
         uint32_t pend_n = 0, pend_q = 0; // CPC filter keys to commit after the tile barrier
         if (P.dbg & 1) { c.nev += active && (S.stage[tid] | 1); continue; }
         if (active) {
@@ -673,36 +712,45 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
                                   : TAcc{P.recs, S.stage, off & ~15ull, PV_WIN - 4, (uint32_t)PV_BLOCK, tid};
             Parsed o;
             parse_record(R, P, off, o);
+            STAMP(4)
             if (P.dbg & 2) { c.nev += 1; c.nin += o.dir == 0; c.nudp += o.l4 == 17; continue; }
-            if (cached) lane_hot(P, S, R, o, i, p_lo, cur_slot, mqp, c, run_v, run_n, pend_n, pend_q);
+            if (cached) lane_hot(P, S, R, o, i, p_lo, cur_slot, c, run_v, run_n, pend_n, pend_q);
             else if (o.l4 == 17) // a tile before the kept window: DNS transaction events only
-                dns_lane(P, S, R, o, false, false, 0, p_lo, i, c, pend_q, 0);
+                dns_lane(P, S, R, o, false, false, 0, p_lo, i, c, pend_q);
         }
+        STAMP(5)
         if (P.dbg & 3) continue; // (profiling stages skip lanes with `continue`: no barrier then)
         // every lane's CPC filter probes and queued misses of this tile are in LDS
         lds_barrier();
         cpc_commit(S, pend_n);
         cpc_commit(S, pend_q);
-        const uint32_t nq = S.mq_n[mqp];
-        if (nq) {
-            __syncthreads(); // the queued entries (global stores of other lanes) are visible
-            const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * PV_MQ_CAP * 2;
-            for (uint32_t j = tid; j < nq; j += PV_BLOCK) {
-                const uint64_t v = q[2 * j + 1];
-                global_add(P, cur_slot, q[2 * j], (uint32_t)v, (uint32_t)(v >> 32));
-            }
-        }
-        if (tid == 0) S.mq_n[mqp ^ 1] = 0; // next tile's queue (last drained before this tile's first barrier)
+        STAMP(6)
     }
     if (cur_slot != 0xffffffffu) {
         hist_put(P, S, true, cur_slot, run_v, run_n);
         ctr_flush(P, cur_slot, c);
         block_flush(P, S, cur_slot);
     }
+    STAMP(7)
+    STAMP_FLUSH
     __syncthreads();
     if (threadIdx.x == 0) {
         P.blk_events[blockIdx.x] = S.nev;
+        P.mq_cnt[blockIdx.x] = S.mq_n;
         if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
+    }
+}
+
+// Applies each workgroup's top-N update log (pv_net_dns_kernel) to the global tables:
+// one entry per lane, so the insert round trips of many entries are in flight at once.
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_topn_insert(const PvParams *__restrict__ Pp)
+{
+    const PvParams &P = *Pp;
+    const uint32_t cnt = P.mq_cnt[blockIdx.x];
+    const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * P.mq_cap * 2;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+        const uint64_t e0 = q[2 * j], e1 = q[2 * j + 1];
+        global_add(P, (uint32_t)(e0 >> 60), e0 & ((1ull << 60) - 1), (uint32_t)e1, (uint32_t)(e1 >> 32));
     }
 }
 

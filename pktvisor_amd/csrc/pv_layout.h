@@ -18,8 +18,10 @@
 // name arena partitions per slot: workgroup b allocates from partition b % PV_ARENA_PARTS,
 // so no bump pointer is shared by more than a few workgroups
 #define PV_ARENA_PARTS 64
-// per-workgroup top-N miss queue: 256 lanes x at most 6 hashed top-N updates per record
-#define PV_MQ_CAP 2048
+// per-workgroup top-N update log: at most 6 hashed top-N updates per record, plus one
+// LDS cache flush (<= PV_CACHE_MAX entries) per bucket slot the workgroup touches
+#define PV_MQ_PER_REC 6
+#define PV_CACHE_MAX 4096
 
 // group bits (same values as pv_net_group / pv_dns_group in include/pvgpu.h)
 #define PV_NET_COUNTERS_BIT 1u
@@ -168,7 +170,10 @@ struct PvParams {
     uint32_t want_events;
     uint32_t tiles_per_block;
     uint64_t rec_bytes; // bytes of the record run (end of the last record)
-    PV_G uint64_t *mq;    // per-workgroup queues of top-N cache misses: PV_MQ_CAP x {key, w | rep << 32}
+    PV_G uint64_t *mq;    // per-workgroup top-N update logs: mq_cap x {key | slot << 60, w | rep << 32}
+    PV_G uint32_t *mq_cnt; // entries per workgroup log
+    PV_G uint64_t *stamps; // diagnostic builds (-DPV_STAMPS): 8 phase cycle sums per wave
+    uint32_t mq_cap;
     uint32_t grid_main;   // workgroups of pv_net_dns_kernel
     uint32_t n_btiles;    // tiles holding a period shift (handled by pv_boundary_kernel)
     uint32_t btile[PV_MAX_SHIFTS];
