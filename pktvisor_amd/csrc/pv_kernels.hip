@@ -28,6 +28,7 @@
 #include "pv_layout.h"
 
 #define PV_BLOCK 256
+#define PV_C __attribute__((address_space(4)))
 #ifndef PV_CACHE_N
 #define PV_CACHE_N 2048
 #endif
@@ -72,6 +73,8 @@ __device__ __forceinline__ uint32_t pv_ld32(const uint8_t *base, uint64_t off)
 }
 __device__ __forceinline__ uint32_t pv_clz64(uint64_t x) { return (uint32_t)__clzll((long long)x); }
 #define PV_FN __device__ __forceinline__
+// kernel parameters are read through the constant address space (scalar loads)
+#define PV_CREF(T) const PV_C T &
 #include "pv_parse.h"
 
 namespace {
@@ -118,10 +121,10 @@ struct TAcc {
     }
 };
 
-__device__ __forceinline__ uint64_t *slot_sum(const PvParams &P, uint32_t slot) { return P.sum + (uint64_t)slot * PV_SUM_WORDS; }
+__device__ __forceinline__ uint64_t *slot_sum(PV_CREF(PvParams) P, uint32_t slot) { return P.sum + (uint64_t)slot * PV_SUM_WORDS; }
 
 // Writes the name record for a newly created global top-N entry (arena: u16 len + bytes).
-__device__ __noinline__ uint32_t write_name(const PvParams &P, uint32_t slot, uint32_t metric, uint32_t rep)
+__device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, uint32_t metric, uint32_t rep)
 {
     Parsed o;
     const GAcc R{P.recs};
@@ -167,7 +170,7 @@ __device__ __noinline__ uint32_t write_name(const PvParams &P, uint32_t slot, ui
     return (uint32_t)pos + 1;
 }
 
-__device__ __noinline__ void global_add(const PvParams &P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
+__device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
 {
     uint32_t metric = PV_KEY_METRIC(key);
     uint64_t *sum = slot_sum(P, slot);
@@ -235,7 +238,7 @@ __device__ __forceinline__ bool cache_add(BlockState &S, uint64_t key, uint32_t 
 // (fire-and-forget stores; slot in the top 4 key bits, which hashed metrics leave free);
 // pv_topn_insert applies the log to the global tables after the parse kernel, so no
 // lane of the parse kernel ever waits on an HBM round trip for a table update.
-__device__ __forceinline__ void log_put(const PvParams &P, BlockState &S, uint32_t slot, uint64_t key, uint32_t w,
+__device__ __forceinline__ void log_put(PV_CREF(PvParams) P, BlockState &S, uint32_t slot, uint64_t key, uint32_t w,
                                         uint32_t rep)
 {
     const uint32_t q = atomicAdd(&S.mq_n, 1u);
@@ -244,7 +247,7 @@ __device__ __forceinline__ void log_put(const PvParams &P, BlockState &S, uint32
     e[1] = (uint64_t)w | ((uint64_t)rep << 32);
 }
 // dense tables (ports, qtypes, rcodes): plain HBM atomics, nothing waits on them
-__device__ __forceinline__ void dense_add(const PvParams &P, uint32_t slot, uint64_t key, uint32_t w)
+__device__ __forceinline__ void dense_add(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint32_t w)
 {
     PV_G uint64_t *sum = P.sum + (uint64_t)slot * PV_SUM_WORDS;
     const uint32_t metric = PV_KEY_METRIC(key);
@@ -254,7 +257,7 @@ __device__ __forceinline__ void dense_add(const PvParams &P, uint32_t slot, uint
     __hip_atomic_fetch_add(sum + off, (uint64_t)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // cached: LDS cache, then the update log; uncached (boundary kernel): the global table
-__device__ __forceinline__ void top_add(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint64_t key,
+__device__ __forceinline__ void top_add(PV_CREF(PvParams) P, BlockState &S, bool cached, uint32_t slot, uint64_t key,
                                         uint32_t w, uint32_t rep)
 {
     if (cached) {
@@ -271,7 +274,7 @@ __device__ __forceinline__ void top_add(const PvParams &P, BlockState &S, bool c
 // submitted in an EARLIER tile cannot lower the minimum: the LDS filter skips it. Keys
 // seen in the current tile are inserted only after the tile's barrier (cpc_commit).
 __device__ __forceinline__ uint32_t cpcf_slot(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - 9); }
-__device__ __forceinline__ void cpc_add(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint32_t sketch,
+__device__ __forceinline__ void cpc_add(PV_CREF(PvParams) P, BlockState &S, bool cached, uint32_t slot, uint32_t sketch,
                                         uint32_t coupon, int64_t gidx, uint32_t &pending)
 {
     const uint32_t key = ((sketch << 17) | coupon) + 1;
@@ -310,7 +313,7 @@ struct Ctr {
 };
 
 // wave-reduce the register counters and add them to the slot's SUM region
-__device__ void ctr_flush(const PvParams &P, uint32_t slot, Ctr &c)
+__device__ void ctr_flush(PV_CREF(PvParams) P, uint32_t slot, Ctr &c)
 {
     uint64_t *s = slot_sum(P, slot);
     const bool lead = (threadIdx.x & 63) == 0;
@@ -342,7 +345,7 @@ __device__ void block_clear(BlockState &S)
 }
 
 // Flush the LDS partial bucket of `slot` to HBM and clear it (all threads, block-uniform).
-__device__ void block_flush(const PvParams &P, BlockState &S, uint32_t slot)
+__device__ void block_flush(PV_CREF(PvParams) P, BlockState &S, uint32_t slot)
 {
     __syncthreads();
     if (slot < PV_SLOTS) {
@@ -361,7 +364,7 @@ __device__ void block_flush(const PvParams &P, BlockState &S, uint32_t slot)
     __syncthreads();
 }
 
-__device__ __forceinline__ uint32_t period_of(const PvParams &P, uint64_t i)
+__device__ __forceinline__ uint32_t period_of(PV_CREF(PvParams) P, uint64_t i)
 {
     uint32_t p = 0;
     while (p < P.n_shift && i >= P.pstart[p]) p++;
@@ -369,7 +372,7 @@ __device__ __forceinline__ uint32_t period_of(const PvParams &P, uint64_t i)
 }
 
 // payload-size histogram: a per-lane run cache in front of the LDS histogram
-__device__ __forceinline__ void hist_put(const PvParams &P, BlockState &S, bool cached, uint32_t slot, uint32_t v,
+__device__ __forceinline__ void hist_put(PV_CREF(PvParams) P, BlockState &S, bool cached, uint32_t slot, uint32_t v,
                                          uint32_t n)
 {
     if (!n) return;
@@ -380,7 +383,7 @@ __device__ __forceinline__ void hist_put(const PvParams &P, BlockState &S, bool 
 // DNS v1 over UDP for one lane (DnsStreamHandler::process_udp_packet_cb, :270-302, and
 // DnsMetricsBucket::process_dns_layer, :910-1049)
 template <class A>
-__device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const A &R, const Parsed &o, bool cached,
+__device__ __forceinline__ void dns_lane(PV_CREF(PvParams) P, BlockState &S, const A &R, const Parsed &o, bool cached,
                                          bool upd, uint32_t slot, uint32_t period, uint64_t i, Ctr &c,
                                          uint32_t &pend_q)
 {
@@ -482,7 +485,7 @@ __device__ __forceinline__ void dns_lane(const PvParams &P, BlockState &S, const
 
 // cardinality + top IPs of one record (NetworkMetricsBucket::process_net_layer :745-763)
 template <class A>
-__device__ __forceinline__ void net_ips(const PvParams &P, BlockState &S, const A &R, const Parsed &o, uint64_t i,
+__device__ __forceinline__ void net_ips(PV_CREF(PvParams) P, BlockState &S, const A &R, const Parsed &o, uint64_t i,
                                         bool cached, uint32_t slot, uint32_t &pend_n)
 {
     const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
@@ -513,7 +516,7 @@ __device__ __forceinline__ void net_ips(const PvParams &P, BlockState &S, const 
 
 // One record of a tile whose records all fall in period `period` -> bucket slot `slot`
 // (both workgroup-uniform): counters in registers, tables through the LDS cache.
-__device__ __forceinline__ void lane_hot(const PvParams &P, BlockState &S, const TAcc &R, const Parsed &o, uint64_t i,
+__device__ __forceinline__ void lane_hot(PV_CREF(PvParams) P, BlockState &S, const TAcc &R, const Parsed &o, uint64_t i,
                                          uint32_t period, uint32_t slot, Ctr &c, uint32_t &run_v,
                                          uint32_t &run_n, uint32_t &pend_n, uint32_t &pend_q)
 {
@@ -533,7 +536,7 @@ __device__ __forceinline__ void lane_hot(const PvParams &P, BlockState &S, const
 // One record of a boundary tile (a period shift inside the tile, or periods outside the
 // kept window): the lane resolves its own period and updates HBM directly. Cold path.
 template <class A>
-__device__ __forceinline__ void lane_cold(const PvParams &P, BlockState &S, const A &R, const Parsed &o, uint64_t i)
+__device__ __forceinline__ void lane_cold(PV_CREF(PvParams) P, BlockState &S, const A &R, const Parsed &o, uint64_t i)
 {
     const uint32_t period = period_of(P, i);
     const uint32_t slot = P.slot_of[period];
@@ -585,7 +588,9 @@ __device__ __forceinline__ void lane_cold(const PvParams &P, BlockState &S, cons
 // ------------------------------------------------------------------ the fused kernel
 extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel(const PvParams *__restrict__ Pp)
 {
-    const PvParams &P = *Pp; // parameters live in device memory: scalar loads, no stack copy
+    // parameters live in device memory and are read-only for the launch: reading them
+    // through the constant address space makes every uniform field a scalar load
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ BlockState S;
     block_clear(S);
     if (threadIdx.x == 0) {
@@ -649,7 +654,11 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
         issue(tbeg, b_cur, b_n1, off_cur, chunks_cur);
     }
     STAMP_DECL
-    for (uint64_t tile = tbeg; tile < tend; tile++) {
+    for (uint64_t tile_ = tbeg; tile_ < tend; tile_++) {
+        // the tile index is workgroup-uniform: say so, or divergence analysis may keep it
+        // (and every parameter load derived from it) in vector registers
+        const uint64_t tile = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tile_ >> 32)) << 32) |
+                              __builtin_amdgcn_readfirstlane((uint32_t)tile_);
         const uint64_t t0 = tile * PV_BLOCK;
         const uint64_t t1 = (t0 + PV_BLOCK < P.n ? t0 + PV_BLOCK : P.n) - 1;
         // periods are contiguous index ranges (host-provided start indices): a tile is
@@ -706,21 +715,22 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
         }
         STAMP(3)
         uint32_t pend_n = 0, pend_q = 0; // CPC filter keys to commit after the tile barrier
-        if (P.dbg & 1) { c.nev += active && (S.stage[tid] | 1); continue; }
-        if (active) {
+        // (no `continue` in this loop: a divergent latch would make the tile loop
+        // non-uniform and turn every uniform parameter load into a waiting vector load)
+        if (P.dbg & 1) c.nev += active && (S.stage[tid] | 1);
+        if (active && !(P.dbg & 1)) {
             const TAcc R = chunks ? TAcc{P.recs, S.stage, base, chunks * 16 - 4, 1u, 0u}
                                   : TAcc{P.recs, S.stage, off & ~15ull, PV_WIN - 4, (uint32_t)PV_BLOCK, tid};
             Parsed o;
             parse_record(R, P, off, o);
             STAMP(4)
-            if (P.dbg & 2) { c.nev += 1; c.nin += o.dir == 0; c.nudp += o.l4 == 17; continue; }
-            if (cached) lane_hot(P, S, R, o, i, p_lo, cur_slot, c, run_v, run_n, pend_n, pend_q);
+            if (P.dbg & 2) { c.nev += 1; c.nin += o.dir == 0; c.nudp += o.l4 == 17; }
+            else if (cached) lane_hot(P, S, R, o, i, p_lo, cur_slot, c, run_v, run_n, pend_n, pend_q);
             else if (o.l4 == 17) // a tile before the kept window: DNS transaction events only
                 dns_lane(P, S, R, o, false, false, 0, p_lo, i, c, pend_q);
         }
         STAMP(5)
-        if (P.dbg & 3) continue; // (profiling stages skip lanes with `continue`: no barrier then)
-        // every lane's CPC filter probes and queued misses of this tile are in LDS
+        // every lane's CPC filter probes of this tile precede the inserts
         lds_barrier();
         cpc_commit(S, pend_n);
         cpc_commit(S, pend_q);
@@ -745,7 +755,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel
 // one entry per lane, so the insert round trips of many entries are in flight at once.
 extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_topn_insert(const PvParams *__restrict__ Pp)
 {
-    const PvParams &P = *Pp;
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     const uint32_t cnt = P.mq_cnt[blockIdx.x];
     const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * P.mq_cap * 2;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
@@ -759,7 +769,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_topn_insert(const PvPa
 // on the same stream; its DNS events go to regions after the main kernel's.
 extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_boundary_kernel(const PvParams *__restrict__ Pp)
 {
-    const PvParams &P = *Pp;
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ BlockState S;
     if (threadIdx.x == 0) {
         S.nev = 0; S.nresp = 0;
@@ -785,7 +795,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_boundary_kernel(const 
 // order) and writes the total to n_events[0].
 extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint32_t nblk)
 {
-    const PvParams &P = *Pp;
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ uint32_t base;
     if (threadIdx.x == 0) {
         uint32_t b = 0;
@@ -823,7 +833,7 @@ extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v)
 namespace {
 // first shift k (1-based period index) after period `a` whose threshold purges a
 // query started at `sec`; returns 0 if none inside this batch
-__device__ __forceinline__ uint32_t purge_period(const PvParams &P, uint32_t ttl_s, uint32_t a, int64_t sec)
+__device__ __forceinline__ uint32_t purge_period(PV_CREF(PvParams) P, uint32_t ttl_s, uint32_t a, int64_t sec)
 {
     for (uint32_t k = a + 1; k <= P.n_shift; k++)
         if (P.thresh[k - 1] >= (int64_t)ttl_s + sec) return k;
@@ -840,17 +850,17 @@ struct XState {
     uint32_t nval, nvalid, vbase, dbase;
 };
 __device__ __forceinline__ void xctr(XState &T, uint32_t period, uint32_t c) { atomicAdd(&T.ctr[period][c], 1u); }
-__device__ __forceinline__ void xval(const PvXactParams &X, XState &T, uint32_t period, uint32_t kind, uint64_t bits)
+__device__ __forceinline__ void xval(PV_CREF(PvXactParams) X, XState &T, uint32_t period, uint32_t kind, uint64_t bits)
 {
     T.val[atomicAdd(&T.nval, 1u)] = PvXValue{bits, X.slot_gen[period], kind};
 }
 // DnsMetricsBucket::new_dns_transaction slow branch (dns/v1 ...cpp:1126-1136): the
 // response's first query name (getName(), case kept) into top_slow
-__device__ void slow_check(const PvXactParams &X, uint32_t idx, uint32_t period, uint32_t dir, uint64_t us)
+__device__ void slow_check(PV_CREF(PvXactParams) X, uint32_t idx, uint32_t period, uint32_t dir, uint64_t us)
 {
     const float thr = dir == 0 ? X.thr_from[period] : (dir == 1 ? X.thr_to[period] : 0.0f);
     if (!(thr > 0.0f && (float)us >= thr)) return;
-    const PvParams &P = X.P;
+    PV_CREF(PvParams) P = X.P;
     Parsed o;
     const GAcc R{P.recs};
     parse_record(R, P, P.offs[idx], o);
@@ -866,9 +876,9 @@ __device__ void slow_check(const PvXactParams &X, uint32_t idx, uint32_t period,
 }
 } // namespace
 
-__device__ void resolve_one(const PvXactParams &X, XState &T, uint32_t p)
+__device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
 {
-    const PvParams &P = X.P;
+    PV_CREF(PvParams) P = X.P;
     const PvXEvent e = X.events[X.svals[p]];
     const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
     if (e.qr) {
@@ -922,8 +932,8 @@ __device__ void resolve_one(const PvXactParams &X, XState &T, uint32_t p)
 
 extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvXactParams *__restrict__ Xp)
 {
-    const PvXactParams &X = *Xp;
-    const PvParams &P = X.P;
+    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
+    PV_CREF(PvParams) P = X.P;
     __shared__ XState T;
     for (uint32_t j = threadIdx.x; j < (PV_MAX_SHIFTS + 1) * XC_N; j += blockDim.x) (&T.ctr[0][0])[j] = 0;
     if (threadIdx.x == 0) { T.nval = 0; T.nvalid = 0; }
@@ -955,7 +965,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvX
 // top_slow for transactions of periods whose threshold became known after the resolve
 extern "C" __global__ void pv_xact_slow(const PvXactParams *__restrict__ Xp, uint32_t n_valid)
 {
-    const PvXactParams &X = *Xp;
+    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_valid) return;
     const PvXValid v = X.valid[i];

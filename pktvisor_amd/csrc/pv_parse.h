@@ -134,7 +134,7 @@ struct Parsed {
     uint32_t l4len;    // IP-length-trimmed L4 layer length
 };
 
-PV_FN bool match4(const PvSubnets &s, uint32_t ip)
+PV_FN bool match4(PV_CREF(PvSubnets) s, uint32_t ip)
 {
     if (!ip) return false;
     for (uint32_t i = 0; i < s.n4; i++) {
@@ -144,7 +144,7 @@ PV_FN bool match4(const PvSubnets &s, uint32_t ip)
     return false;
 }
 template <class A>
-PV_FN bool match6(const PvSubnets &s, const A &R, uint64_t a)
+PV_FN bool match6(PV_CREF(PvSubnets) s, const A &R, uint64_t a)
 {
     for (uint32_t i = 0; i < s.n6; i++) {
         uint32_t cidr = s.v6_cidr[i], bytes = cidr / 8, bits = cidr % 8;
@@ -161,7 +161,7 @@ PV_FN bool match6(const PvSubnets &s, const A &R, uint64_t a)
 }
 
 template <class A>
-PV_FN void parse_record(const A &R, const PvParams &P, uint64_t rec, Parsed &o)
+PV_FN void parse_record(const A &R, PV_CREF(PvParams) P, uint64_t rec, Parsed &o)
 {
     uint32_t tsec = R.u32(rec), tfrac = R.u32(rec + 4);
     o.caplen = R.u32(rec + 8);

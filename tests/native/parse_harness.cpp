@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #define PV_FN inline
+#define PV_CREF(T) const T &
 inline uint32_t pv_clz64(uint64_t x) { return (uint32_t)__builtin_clzll(x); }
 #include "../../pktvisor_amd/csrc/pv_parse.h"
 
