@@ -35,7 +35,8 @@
 #include "../../include/pvgpu.h"
 #include "pv_layout.h"
 
-extern "C" __global__ void pv_net_dns_kernel(const PvParams *P);
+extern "C" __global__ void pv_net_kernel(const PvParams *P);
+extern "C" __global__ void pv_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
@@ -236,7 +237,9 @@ struct pv_ctx {
     uint32_t *d_mq_cnt = nullptr;
     uint64_t *d_stamps = nullptr; // diagnostic phase stamps (PV_STAMPS env + -DPV_STAMPS build)
     int cus = 256;
-    int wg_per_cu = 2; // resident pv_net_dns_kernel workgroups per CU (occupancy API)
+    int wg_per_cu = 2; // resident pv_net_kernel workgroups per CU (occupancy API)
+    uint64_t *d_dq = nullptr; // DNS work lists (32-B messages)
+    uint32_t *d_dq_cnt = nullptr;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
     void *d_sort_tmp = nullptr;
@@ -816,12 +819,12 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
     {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_net_dns_kernel), 256, 0) ==
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_net_kernel), 256, 0) ==
                 hipSuccess && nb > 0)
             c->wg_per_cu = nb;
     }
-    // event regions: main workgroups own tiles_per_block * 256 slots each (the last may
-    // overhang the batch by < tiles_per_block tiles), boundary workgroups 256 each
+    // event / DNS work-list regions: main workgroups own wt_per_block * 64 slots each (the
+    // last may overhang the batch by < wt_per_block tiles), boundary workgroups 64 each
     const uint64_t ev_cap = mr + mr / ((uint64_t)c->wg_per_cu * c->cus) + 16 * 256;
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
         !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
@@ -834,6 +837,8 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_events, (size_t)ev_cap * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)ev_cap * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_mq_cnt, 65536 * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_dq, (size_t)ev_cap * 32)) ||
+        !hip_ok(e = hipMalloc(&c->d_dq_cnt, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_stamps, 65536 * 4 * 8 * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)mr * 8)) || !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)mr * 8)) ||
@@ -862,7 +867,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_mq_cnt, c->d_stamps,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -1029,19 +1034,20 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.dns_at_thresh = c->d_status + ST_DNS_AT;
     launch_fill32(c, c->d_status, ST_WORDS, 0);
     hipError_t e;
-    uint64_t tiles = (n + 255) / 256;
+    const uint64_t tiles = (n + 63) / 64; // 64-record wave tiles
     // persistent grid: exactly the workgroups that are resident at once (LDS/VGPR
-    // occupancy), each owning a contiguous run of tiles
-    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->cus * c->wg_per_cu);
-    P.tiles_per_block = (uint32_t)((tiles + grid - 1) / grid);
+    // occupancy), each owning a contiguous run of wave tiles
+    uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + 3) / 4, (uint64_t)c->cus * c->wg_per_cu);
+    P.wt_per_block = (uint32_t)((tiles + grid - 1) / grid);
     P.rec_bytes = info->bytes_used;
     {
         static const char *dbg = getenv("PV_DEBUG_STAGES");
         P.dbg = dbg ? (uint32_t)atoi(dbg) : 0;
     }
-    grid = (uint32_t)((tiles + P.tiles_per_block - 1) / P.tiles_per_block);
+    grid = (uint32_t)((tiles + P.wt_per_block - 1) / P.wt_per_block);
     P.grid_main = grid;
-    P.mq_cap = P.tiles_per_block * 256u * PV_MQ_PER_REC + PV_CACHE_MAX * (P.n_shift + 1);
+    // per workgroup: at most 6 hashed updates per record, plus one cache flush per pass
+    P.mq_cap = P.wt_per_block * 64u * PV_MQ_PER_REC + PV_CACHE_MAX * 2;
     {
         const size_t need = (size_t)grid * P.mq_cap * 16;
         if (need > c->mq_bytes) {
@@ -1055,12 +1061,14 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.mq = c->d_mq;
     P.mq_cnt = c->d_mq_cnt;
     P.stamps = c->d_stamps;
+    P.dq = c->d_dq;
+    P.dq_cnt = c->d_dq_cnt;
     // tiles that hold a period shift go to pv_boundary_kernel
     P.n_btiles = 0;
     for (uint32_t k = 0; k < P.n_shift; k++) {
         const uint64_t ps = P.pstart[k];
-        if (ps % 256 == 0 || ps >= n) continue;
-        const uint32_t t = (uint32_t)(ps / 256);
+        if (ps % 64 == 0 || ps >= n) continue;
+        const uint32_t t = (uint32_t)(ps / 64);
         bool seen = false;
         for (uint32_t j = 0; j < P.n_btiles; j++) seen |= P.btile[j] == t;
         if (!seen) P.btile[P.n_btiles++] = t;
@@ -1068,13 +1076,14 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, &P, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
-    hipLaunchKernelGGL(pv_net_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     e = hipGetLastError();
-    if (e != hipSuccess) return c->hipfail(e, "launch pv_net_dns_kernel");
-    hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the parse kernel alone (bench roofline)
+    if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
+    hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
+    hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_insert, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (P.n_btiles) {
-        hipLaunchKernelGGL(pv_boundary_kernel, dim3(P.n_btiles), dim3(256), 0, st, (const PvParams *)c->d_params);
+        hipLaunchKernelGGL(pv_boundary_kernel, dim3(P.n_btiles), dim3(64), 0, st, (const PvParams *)c->d_params);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_boundary_kernel");
     }
     if (P.want_events)
@@ -1099,7 +1108,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
             double sum[8] = {0};
             for (size_t w = 0; w < (size_t)grid * 4; w++)
                 for (int k = 0; k < 8; k++) sum[k] += (double)st[w * 8 + k];
-            fprintf(stderr, "pv_stamps (mean cycles per wave, %u tiles/wg):", P.tiles_per_block);
+            fprintf(stderr, "pv_stamps (mean cycles per wave, %u wave tiles/wg):", P.wt_per_block);
             static const char *nm[8] = {"slot", "commit", "barA", "issue", "parse", "lane", "barB", "flush"};
             for (int k = 0; k < 8; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (grid * 4.0));
             fprintf(stderr, "\n");

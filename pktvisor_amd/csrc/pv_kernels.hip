@@ -29,10 +29,6 @@
 
 #define PV_BLOCK 256
 #define PV_C __attribute__((address_space(4)))
-#ifndef PV_CACHE_N
-#define PV_CACHE_N 2048
-#endif
-#define PV_HIST_N 2048
 // diagnostic build (-DPV_STAMPS): per-wave cycles spent in each phase of the tile loop
 #ifdef PV_STAMPS
 #define STAMP_DECL                                                                           \
@@ -52,7 +48,6 @@
 #define STAMP(k)
 #define STAMP_FLUSH
 #endif
-static_assert(PV_CACHE_N <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cache entries per flush");
 #ifndef PV_WIN
 #define PV_WIN 128 // bytes of each record staged into LDS (record header + frame start)
 #endif
@@ -60,7 +55,6 @@ static_assert(PV_CACHE_N <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cac
 #define PV_WPE 2 // waves per SIMD the main kernel is register-budgeted for
 #endif
 #define PV_WINW (PV_WIN / 4)
-#define PV_CPCF_N 512           // LDS filter of CPC coupons already submitted by this workgroup
 
 // ------------------------------------------------------------------ byte access
 // recs is 256-B aligned and padded by >= 256 bytes: two aligned dword loads and
@@ -203,96 +197,77 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
     if (created >= 0 && metric != TM_IPV4) P.taux[base + (uint64_t)created] = write_name(P, slot, metric, rep);
 }
 
-// ------------------------------------------------------------------ LDS workgroup state
-struct BlockState {
-    uint32_t stage[PV_WINW * PV_BLOCK]; // tile bytes (TAcc layouts), 32 KiB
-    uint64_t ckey[PV_CACHE_N];       // key -> count cache for top-N and dense tables
-    uint32_t ccnt[PV_CACHE_N];
-    uint32_t crep[PV_CACHE_N];
-    uint32_t hist[PV_HIST_N];        // payload-size histogram (caplen < PV_HIST_N)
-    uint32_t cpcf[PV_CPCF_N];        // (sketch << 17 | coupon) + 1 submitted in an earlier tile
-    uint32_t mq_n;                   // entries in this workgroup's top-N update log
-    uint32_t nev;                    // DNS events appended to this block's region
-    uint64_t ebase;                  // first event slot of this block's region
-    uint32_t nresp;                  // of which responses
+// ------------------------------------------------------------------ LDS key cache
+// Open-addressed key -> (count, min record index) cache shared by a workgroup's
+// waves. Keys carry their bucket slot in bits 60..63 (local metric ids are < 16), so
+// one cache serves every slot a workgroup touches and is flushed once, at the end.
+// crep holds the smallest record index that touched the entry: a later record of the
+// same key knows its CPC coupon (same key => same coupon) was already submitted with a
+// smaller index, and the insert kernel uses it as the record a name is decoded from.
+#define PV_LKEY(slot, lm, payload) (((uint64_t)(slot) << 60) | ((uint64_t)(lm) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
+template <int N>
+struct KeyCache {
+    uint64_t key[N];
+    uint32_t cnt[N];
+    uint32_t rep[N];
+    __device__ __forceinline__ void clear()
+    {
+        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) { key[i] = 0; cnt[i] = 0; rep[i] = 0xffffffffu; }
+    }
+    // adds w to key's count; returns false if the probe window is full. first = the
+    // entry's smallest record index before this call (0xffffffff if new)
+    __device__ __forceinline__ bool add(uint64_t k, uint32_t w, uint32_t idx, uint32_t &first)
+    {
+        uint32_t h = (uint32_t)(fmix64(k) >> 32) & (N - 1);
+        for (int probe = 0; probe < 8; probe++) {
+            uint64_t cur = key[h];
+            if (cur == 0) {
+                const uint64_t prev = atomicCAS((unsigned long long *)&key[h], 0ull, (unsigned long long)k);
+                cur = prev == 0 ? k : prev;
+            }
+            if (cur == k) {
+                if (w) atomicAdd(&cnt[h], w);
+                first = atomicMin(&rep[h], idx);
+                return true;
+            }
+            h = (h + 1) & (N - 1);
+        }
+        return false;
+    }
 };
 
-// LDS key cache: returns false when the probe window is full (caller goes global)
-__device__ __forceinline__ bool cache_add(BlockState &S, uint64_t key, uint32_t w, uint32_t rep)
-{
-    uint32_t h = hash32(key) & (PV_CACHE_N - 1);
-    for (int probe = 0; probe < 8; probe++) {
-        uint64_t k = S.ckey[h];
-        if (k == key) { atomicAdd(&S.ccnt[h], w); return true; }
-        if (k == 0) {
-            uint64_t prev = atomicCAS((unsigned long long *)&S.ckey[h], 0ull, (unsigned long long)key);
-            if (prev == 0) { S.crep[h] = rep; atomicAdd(&S.ccnt[h], w); return true; }
-            if (prev == key) { atomicAdd(&S.ccnt[h], w); return true; }
-        }
-        h = (h + 1) & (PV_CACHE_N - 1);
-    }
-    return false;
-}
-
-// Top-N updates that the LDS cache cannot absorb go to the workgroup's HBM update log
-// (fire-and-forget stores; slot in the top 4 key bits, which hashed metrics leave free);
-// pv_topn_insert applies the log to the global tables after the parse kernel, so no
-// lane of the parse kernel ever waits on an HBM round trip for a table update.
-__device__ __forceinline__ void log_put(PV_CREF(PvParams) P, BlockState &S, uint32_t slot, uint64_t key, uint32_t w,
+// Top-N updates the LDS cache does not absorb go to the workgroup's HBM update log
+// (fire-and-forget stores, slot in key bits 60..63); pv_topn_insert applies the log to
+// the global tables after the parse kernels, so no lane waits on an HBM round trip for
+// a table update.
+__device__ __forceinline__ void log_put(PV_CREF(PvParams) P, uint32_t *mq_n, uint32_t slot, uint64_t key, uint32_t w,
                                         uint32_t rep)
 {
-    const uint32_t q = atomicAdd(&S.mq_n, 1u);
+    const uint32_t q = atomicAdd(mq_n, 1u);
     PV_G uint64_t *e = P.mq + ((uint64_t)blockIdx.x * P.mq_cap + q) * 2;
-    e[0] = key | ((uint64_t)slot << 60);
+    e[0] = (key & ((1ull << 60) - 1)) | ((uint64_t)slot << 60);
     e[1] = (uint64_t)w | ((uint64_t)rep << 32);
 }
-// dense tables (ports, qtypes, rcodes): plain HBM atomics, nothing waits on them
-__device__ __forceinline__ void dense_add(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint32_t w)
+// dense tables (payload sizes, ports, qtypes, rcodes): no-return HBM atomics
+__device__ __forceinline__ void sum_add(PV_CREF(PvParams) P, uint32_t slot, uint32_t word, uint64_t w)
 {
-    PV_G uint64_t *sum = P.sum + (uint64_t)slot * PV_SUM_WORDS;
-    const uint32_t metric = PV_KEY_METRIC(key);
-    const uint32_t off = metric == TM_DENSE_PORT ? PV_OFF_PORT + (uint32_t)(key & 0xffff)
-                       : metric == TM_DENSE_QTYPE ? PV_OFF_QTYPE + (uint32_t)(key & 0xffff)
-                                                  : PV_OFF_RCODE + (uint32_t)(key & 0xf);
-    __hip_atomic_fetch_add(sum + off, (uint64_t)w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(P.sum + (uint64_t)slot * PV_SUM_WORDS + word, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// cached: LDS cache, then the update log; uncached (boundary kernel): the global table
-__device__ __forceinline__ void top_add(PV_CREF(PvParams) P, BlockState &S, bool cached, uint32_t slot, uint64_t key,
-                                        uint32_t w, uint32_t rep)
+__device__ __forceinline__ uint32_t dense_word(uint32_t metric, uint64_t payload)
 {
-    if (cached) {
-        if (cache_add(S, key, w, rep)) return;
-        if (PV_KEY_METRIC(key) >= TM_DENSE_PORT) dense_add(P, slot, key, w);
-        else log_put(P, S, slot, key, w, rep);
-        return;
-    }
-    global_add(P, slot, key, w, rep);
+    return metric == TM_DENSE_PORT ? PV_OFF_PORT + (uint32_t)(payload & 0xffff)
+         : metric == TM_DENSE_QTYPE ? PV_OFF_QTYPE + (uint32_t)(payload & 0xffff)
+                                    : PV_OFF_RCODE + (uint32_t)(payload & 0xf);
 }
-
-// CPC first occurrence: atomicMin of the global record index into the coupon's slot.
-// Records of a workgroup are visited in index order, so a coupon this workgroup already
-// submitted in an EARLIER tile cannot lower the minimum: the LDS filter skips it. Keys
-// seen in the current tile are inserted only after the tile's barrier (cpc_commit).
-__device__ __forceinline__ uint32_t cpcf_slot(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - 9); }
-__device__ __forceinline__ void cpc_add(PV_CREF(PvParams) P, BlockState &S, bool cached, uint32_t slot, uint32_t sketch,
-                                        uint32_t coupon, int64_t gidx, uint32_t &pending)
+// cache-local metric ids (cache keys hold metric ids < 16; these two never reach the
+// global tables): payload-size histogram bins and CPC qname coupons
+#define LM_HIST TM_SLOW_OUT
+#define LM_CPCQ TM_SLOW_IN
+// CPC first occurrence: no-return atomicMin of the global record index
+__device__ __forceinline__ void cpc_min(PV_CREF(PvParams) P, uint32_t slot, uint32_t sketch, uint32_t coupon, int64_t gidx)
 {
-    const uint32_t key = ((sketch << 17) | coupon) + 1;
-    if (cached && S.cpcf[cpcf_slot(key)] == key) return;
-    int64_t *t = P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)sketch * PV_CPC_COUPONS + coupon;
-    atomicMin((long long *)t, (long long)gidx); // no return value: nothing waits on it
-    if (cached) pending = key;
-}
-__device__ __forceinline__ void cpc_commit(BlockState &S, uint32_t key)
-{
-    if (key) S.cpcf[cpcf_slot(key)] = key;
-}
-// workgroup barrier that orders LDS only (global loads in flight stay in flight)
-__device__ __forceinline__ void lds_barrier()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    __hip_atomic_fetch_min(P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)sketch * PV_CPC_COUPONS + coupon, gidx,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -300,68 +275,51 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+#define PV_FLUSH1(s, word, v, on)                                                       \
+    {                                                                                   \
+        const uint32_t t_ = wave_sum(v);                                                \
+        if ((threadIdx.x & 63) == 0 && t_ && (on)) sum_add(P, s, word, t_);             \
+    }
 
-// per-lane counters of the current bucket slot, kept in registers
-struct Ctr {
+// Net v1 counters of the wave's current slot, in registers
+struct NetCtr {
     uint32_t nev, nin, nout, nunk, n4, n6, nudp, ntcp, nsyn, noth;
-    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata;
-    PV_FN void zero()
+    __device__ __forceinline__ void zero() { nev = nin = nout = nunk = n4 = n6 = nudp = ntcp = nsyn = noth = 0; }
+    __device__ __forceinline__ void add(const Parsed &o)
     {
-        nev = nin = nout = nunk = n4 = n6 = nudp = ntcp = nsyn = noth = 0;
-        dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = 0;
+        nev++;
+        nin += o.dir == 0; nout += o.dir == 1; nunk += o.dir == 2;
+        n4 += o.l3 == 4; n6 += o.l3 == 6;
+        nudp += o.l4 == 17; ntcp += o.l4 == 6; nsyn += o.l4 == 6 && o.syn; noth += o.l4 == 0;
     }
 };
-
-// wave-reduce the register counters and add them to the slot's SUM region
-__device__ void ctr_flush(PV_CREF(PvParams) P, uint32_t slot, Ctr &c)
+__device__ void net_flush(PV_CREF(PvParams) P, uint32_t s, NetCtr &c)
 {
-    uint64_t *s = slot_sum(P, slot);
-    const bool lead = (threadIdx.x & 63) == 0;
-    const bool nc = P.net_groups & PV_NET_COUNTERS_BIT, dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
-#define PV_FL(field, word, on)                                                              \
-    {                                                                                       \
-        uint32_t v = wave_sum(c.field);                                                     \
-        if (lead && v && (on)) atomicAdd((unsigned long long *)&s[word], (unsigned long long)v); \
-    }
-    PV_FL(nev, PV_OFF_NET + NC_EVENTS, true) PV_FL(nev, PV_OFF_NET + NC_SAMPLES, true)
-    PV_FL(nev, PV_OFF_NET + NC_TOTAL, nc) PV_FL(nin, PV_OFF_NET + NC_IN, nc) PV_FL(nout, PV_OFF_NET + NC_OUT, nc)
-    PV_FL(nunk, PV_OFF_NET + NC_UNK, nc) PV_FL(n4, PV_OFF_NET + NC_V4, nc) PV_FL(n6, PV_OFF_NET + NC_V6, nc)
-    PV_FL(nudp, PV_OFF_NET + NC_UDP, nc) PV_FL(ntcp, PV_OFF_NET + NC_TCP, nc) PV_FL(nsyn, PV_OFF_NET + NC_SYN, nc)
-    PV_FL(noth, PV_OFF_NET + NC_OTHER, nc)
-    PV_FL(dev, PV_OFF_DNS + DC_EVENTS, true) PV_FL(dev, PV_OFF_DNS + DC_SAMPLES, true)
-    PV_FL(dev, PV_OFF_DNS + DC_TOTAL, dc) PV_FL(dev, PV_OFF_DNS + DC_UDP, dc) PV_FL(dq, PV_OFF_DNS + DC_QUERIES, dc)
-    PV_FL(dr, PV_OFF_DNS + DC_REPLIES, dc) PV_FL(d4, PV_OFF_DNS + DC_V4, dc) PV_FL(d6, PV_OFF_DNS + DC_V6, dc)
-    PV_FL(dnx, PV_OFF_DNS + DC_NX, dc) PV_FL(dref, PV_OFF_DNS + DC_REFUSED, dc) PV_FL(dsrv, PV_OFF_DNS + DC_SRVFAIL, dc)
-    PV_FL(dnoerr, PV_OFF_DNS + DC_NOERROR, dc) PV_FL(dnodata, PV_OFF_DNS + DC_NODATA, dc)
-#undef PV_FL
+    const bool nc = P.net_groups & PV_NET_COUNTERS_BIT;
+    PV_FLUSH1(s, PV_OFF_NET + NC_EVENTS, c.nev, true) PV_FLUSH1(s, PV_OFF_NET + NC_SAMPLES, c.nev, true)
+    PV_FLUSH1(s, PV_OFF_NET + NC_TOTAL, c.nev, nc) PV_FLUSH1(s, PV_OFF_NET + NC_IN, c.nin, nc)
+    PV_FLUSH1(s, PV_OFF_NET + NC_OUT, c.nout, nc) PV_FLUSH1(s, PV_OFF_NET + NC_UNK, c.nunk, nc)
+    PV_FLUSH1(s, PV_OFF_NET + NC_V4, c.n4, nc) PV_FLUSH1(s, PV_OFF_NET + NC_V6, c.n6, nc)
+    PV_FLUSH1(s, PV_OFF_NET + NC_UDP, c.nudp, nc) PV_FLUSH1(s, PV_OFF_NET + NC_TCP, c.ntcp, nc)
+    PV_FLUSH1(s, PV_OFF_NET + NC_SYN, c.nsyn, nc) PV_FLUSH1(s, PV_OFF_NET + NC_OTHER, c.noth, nc)
     c.zero();
 }
-
-__device__ void block_clear(BlockState &S)
+// DNS v1 counters of the wave's current slot
+struct DnsCtr {
+    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata;
+    __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = 0; }
+};
+__device__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
 {
-    for (uint32_t i = threadIdx.x; i < PV_CACHE_N; i += PV_BLOCK) { S.ckey[i] = 0; S.ccnt[i] = 0; }
-    for (uint32_t i = threadIdx.x; i < PV_HIST_N; i += PV_BLOCK) S.hist[i] = 0;
-    for (uint32_t i = threadIdx.x; i < PV_CPCF_N; i += PV_BLOCK) S.cpcf[i] = 0;
-}
-
-// Flush the LDS partial bucket of `slot` to HBM and clear it (all threads, block-uniform).
-__device__ void block_flush(PV_CREF(PvParams) P, BlockState &S, uint32_t slot)
-{
-    __syncthreads();
-    if (slot < PV_SLOTS) {
-        uint64_t *sum = slot_sum(P, slot);
-        for (uint32_t i = threadIdx.x; i < PV_CACHE_N; i += PV_BLOCK) {
-            const uint64_t k = S.ckey[i];
-            if (!k) continue;
-            if (PV_KEY_METRIC(k) >= TM_DENSE_PORT) dense_add(P, slot, k, S.ccnt[i]);
-            else log_put(P, S, slot, k, S.ccnt[i], S.crep[i]);
-        }
-        for (uint32_t i = threadIdx.x; i < PV_HIST_N; i += PV_BLOCK)
-            if (S.hist[i]) atomicAdd((unsigned long long *)&sum[PV_OFF_PAYLOAD + i], (unsigned long long)S.hist[i]);
-    }
-    __syncthreads();
-    block_clear(S);
-    __syncthreads();
+    const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
+    PV_FLUSH1(s, PV_OFF_DNS + DC_EVENTS, c.dev, true) PV_FLUSH1(s, PV_OFF_DNS + DC_SAMPLES, c.dev, true)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_TOTAL, c.dev, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_UDP, c.dev, dc)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_QUERIES, c.dq, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REPLIES, c.dr, dc)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_V4, c.d4, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_V6, c.d6, dc)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_NX, c.dnx, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REFUSED, c.dref, dc)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_SRVFAIL, c.dsrv, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_NOERROR, c.dnoerr, dc)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_NODATA, c.dnodata, dc)
+    c.zero();
 }
 
 __device__ __forceinline__ uint32_t period_of(PV_CREF(PvParams) P, uint64_t i)
@@ -370,40 +328,78 @@ __device__ __forceinline__ uint32_t period_of(PV_CREF(PvParams) P, uint64_t i)
     while (p < P.n_shift && i >= P.pstart[p]) p++;
     return p;
 }
-
-// payload-size histogram: a per-lane run cache in front of the LDS histogram
-__device__ __forceinline__ void hist_put(PV_CREF(PvParams) P, BlockState &S, bool cached, uint32_t slot, uint32_t v,
-                                         uint32_t n)
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
 {
-    if (!n) return;
-    if (cached && v < PV_HIST_N) atomicAdd(&S.hist[v], n);
-    else atomicAdd((unsigned long long *)&slot_sum(P, slot)[PV_OFF_PAYLOAD + v], (unsigned long long)n);
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
-// DNS v1 over UDP for one lane (DnsStreamHandler::process_udp_packet_cb, :270-302, and
-// DnsMetricsBucket::process_dns_layer, :910-1049)
-template <class A>
-__device__ __forceinline__ void dns_lane(PV_CREF(PvParams) P, BlockState &S, const A &R, const Parsed &o, bool cached,
-                                         bool upd, uint32_t slot, uint32_t period, uint64_t i, Ctr &c,
-                                         uint32_t &pend_q)
+// DNS over UDP: the message of one record, located by the Net pass
+// (DnsStreamHandler::process_udp_packet_cb, :270-302)
+struct DnsMsg {
+    uint32_t idx;     // record index in the batch
+    uint32_t moff;    // absolute byte offset of the DNS header in the record blob
+    uint16_t mlen;    // UDP payload length (IP-length trimmed)
+    uint16_t mcap;    // bytes of the message inside the capture
+    uint16_t port;    // metric port
+    uint8_t flags;    // bit0-1 dir, bit2 IPv6, bit3 update buckets (period inside the window)
+    uint8_t period;
+    uint32_t fkey;    // hash5Tuple
+    uint32_t sec;
+    uint32_t nsec;
+    uint32_t pad;
+};
+static_assert(sizeof(DnsMsg) == 32, "DnsMsg is two 16-B stores");
+
+// Metric port of a UDP datagram (0 = not DNS), from the raw port word
+__device__ __forceinline__ uint32_t dns_port(uint32_t pw)
 {
-    uint32_t pw = R.u32(o.l4off);
-    uint32_t sport = ((pw & 0xff) << 8) | ((pw >> 8) & 0xff);
-    uint32_t dport = ((pw >> 8) & 0xff00) | (pw >> 24);
-    uint32_t metric_port = 0;
-    if (dport == 53 || dport == 5353 || dport == 5355 || dport == 53000) metric_port = sport;
-    else if (sport == 53 || sport == 5353 || sport == 5355 || sport == 53000) metric_port = dport;
-    if (!metric_port) return;
-    const uint64_t m = o.l4off + 8;
-    const uint32_t dlen = o.l4len - 8;
-    // header words; bytes past the capture read as 0 (the reference over-reads there)
+    const uint32_t sport = ((pw & 0xff) << 8) | ((pw >> 8) & 0xff);
+    const uint32_t dport = ((pw >> 8) & 0xff00) | (pw >> 24);
+    if (dport == 53 || dport == 5353 || dport == 5355 || dport == 53000) return sport;
+    if (sport == 53 || sport == 5353 || sport == 5355 || sport == 53000) return dport;
+    return 0;
+}
+template <class A>
+__device__ __forceinline__ DnsMsg dns_msg_of(PV_CREF(PvParams) P, const A &R, const Parsed &o, uint64_t i, uint32_t port,
+                                             uint32_t period, bool upd)
+{
+    DnsMsg d;
+    d.idx = (uint32_t)i;
+    d.moff = (uint32_t)(o.l4off + 8);
+    d.mlen = (uint16_t)(o.l4len - 8);
     const uint64_t cap_end = o.frame + o.caplen;
+    d.mcap = (uint16_t)(cap_end > o.l4off + 8 ? min<uint64_t>(cap_end - (o.l4off + 8), 65535) : 0);
+    d.port = (uint16_t)port;
+    d.flags = (uint8_t)(o.dir | (o.l3 == 6 ? 4 : 0) | (upd ? 8 : 0));
+    d.period = (uint8_t)period;
+    d.fkey = flowkey(R, o);
+    d.sec = (uint32_t)o.sec;
+    d.nsec = (uint32_t)o.nsec;
+    d.pad = 0;
+    return d;
+}
+
+// DnsMetricsBucket::process_dns_layer (:910-1049) + the transaction event of one DNS
+// message. `cache` null = boundary path (direct HBM updates); counters go to `c` when
+// `own` (this lane's slot is the wave's register slot), else straight to HBM.
+template <class A, class Cache>
+__device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, uint32_t *nev,
+                                            uint32_t *nresp, uint64_t ebase, const A &R, const DnsMsg &dm, bool own,
+                                            DnsCtr &c)
+{
+    const bool upd = dm.flags & 8;
+    const uint32_t period = dm.period;
+    const uint32_t slot = P.slot_of[period];
+    const uint64_t m = dm.moff;
+    const uint32_t dlen = dm.mlen;
+    const uint32_t i = dm.idx;
+    // header words; bytes past the capture read as 0 (the reference over-reads there)
     uint32_t w0, w1, w2;
-    if (m + 12 <= cap_end) { w0 = R.u32(m); w1 = R.u32(m + 4); w2 = R.u32(m + 8); }
+    if (dm.mcap >= 12) { w0 = R.u32(m); w1 = R.u32(m + 4); w2 = R.u32(m + 8); }
     else {
         w0 = w1 = w2 = 0;
         for (uint32_t b = 0; b < 12; b++) {
-            uint32_t v = (m + b < cap_end) ? R.u8(m + b) : 0;
+            const uint32_t v = b < dm.mcap ? R.u8(m + b) : 0;
             if (b < 4) w0 |= v << (8 * b); else if (b < 8) w1 |= v << (8 * (b - 4)); else w2 |= v << (8 * (b - 8));
         }
     }
@@ -414,346 +410,428 @@ __device__ __forceinline__ void dns_lane(PV_CREF(PvParams) P, BlockState &S, con
     const uint32_t ancount = ((w1 >> 8) & 0xff00) | (w1 >> 24);
     const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
     const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+    // top-N / dense update: cache, else log (hashed) or HBM atomic (dense); boundary: global table
+    auto top = [&](uint32_t metric, uint64_t payload, uint32_t w) {
+        const uint64_t key = PV_KEY(metric, payload);
+        if (cache) {
+            uint32_t first;
+            if (cache->add(PV_LKEY(slot, metric, payload), w, i, first)) return;
+            if (metric >= TM_DENSE_PORT) sum_add(P, slot, dense_word(metric, payload), w);
+            else log_put(P, mq_n, slot, key, w, i);
+        } else {
+            global_add(P, slot, key, w, i);
+        }
+    };
     if (upd) {
-        c.dev++;
-        c.d4 += o.l3 == 4; c.d6 += o.l3 == 6;
-        c.dq += !qr; c.dr += qr;
-        c.dnoerr += qr && rcode == 0; c.dnodata += qr && rcode == 0 && ancount == 0;
-        c.dsrv += qr && rcode == 2; c.dnx += qr && rcode == 3; c.dref += qr && rcode == 5;
+        const uint32_t d4 = !(dm.flags & 4), d6 = (dm.flags & 4) ? 1 : 0;
+        if (own) {
+            c.dev++;
+            c.d4 += d4; c.d6 += d6;
+            c.dq += !qr; c.dr += qr;
+            c.dnoerr += qr && rcode == 0; c.dnodata += qr && rcode == 0 && ancount == 0;
+            c.dsrv += qr && rcode == 2; c.dnx += qr && rcode == 3; c.dref += qr && rcode == 5;
+        } else {
+            const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
+            sum_add(P, slot, PV_OFF_DNS + DC_EVENTS, 1);
+            sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
+            if (dc) {
+                sum_add(P, slot, PV_OFF_DNS + DC_TOTAL, 1);
+                sum_add(P, slot, PV_OFF_DNS + DC_UDP, 1);
+                sum_add(P, slot, PV_OFF_DNS + (d6 ? DC_V6 : DC_V4), 1);
+                sum_add(P, slot, PV_OFF_DNS + (qr ? DC_REPLIES : DC_QUERIES), 1);
+                if (qr && rcode == 0) sum_add(P, slot, PV_OFF_DNS + DC_NOERROR, 1);
+                if (qr && rcode == 0 && ancount == 0) sum_add(P, slot, PV_OFF_DNS + DC_NODATA, 1);
+                if (qr && rcode == 2) sum_add(P, slot, PV_OFF_DNS + DC_SRVFAIL, 1);
+                if (qr && rcode == 3) sum_add(P, slot, PV_OFF_DNS + DC_NX, 1);
+                if (qr && rcode == 5) sum_add(P, slot, PV_OFF_DNS + DC_REFUSED, 1);
+            }
+        }
         DnsInfo d;
         dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
-        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_PORT, metric_port), 1, (uint32_t)i);
+        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top(TM_DENSE_PORT, dm.port, 1);
         if (d.ok) {
-            if (qr) top_add(P, S, cached, slot, PV_KEY(TM_DENSE_RCODE, rcode), 1, (uint32_t)i);
+            if (qr) top(TM_DENSE_RCODE, rcode, 1);
             if (d.has_query) {
                 NameStats st;
                 st.init();
                 if (d.name_len_enc > 0) name_emit(R, m, dlen, 12, st);
                 uint64_t h1, h2;
                 st.mm.finish(h1, h2);
-                if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT))
-                    cpc_add(P, S, cached, slot, CPC_QNAME, cpc_coupon(h1, h2), (int64_t)(P.gbase + i), pend_q);
-                top_add(P, S, cached, slot, PV_KEY(TM_DENSE_QTYPE, d.qtype), 1, (uint32_t)i);
+                if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT)) {
+                    const uint32_t coupon = cpc_coupon(h1, h2);
+                    uint32_t first = 0xffffffffu;
+                    // same name => same coupon: skip when a smaller record index already submitted it
+                    if (!(cache && cache->add(PV_LKEY(slot, LM_CPCQ, coupon), 0, i, first) && first < i))
+                        cpc_min(P, slot, CPC_QNAME, coupon, (int64_t)(P.gbase + i));
+                }
+                top(TM_DENSE_QTYPE, d.qtype, 1);
                 if (P.dns_groups & PV_DNS_TOP_QNAMES_BIT) {
                     const uint64_t fp_full = fp56(st.ph, st.n, 0);
                     if (qr) {
-                        if (rcode == 2) top_add(P, S, cached, slot, PV_KEY(TM_SRVFAIL, fp_full), 1, (uint32_t)i);
-                        else if (rcode == 3) top_add(P, S, cached, slot, PV_KEY(TM_NX, fp_full), 1, (uint32_t)i);
-                        else if (rcode == 5) top_add(P, S, cached, slot, PV_KEY(TM_REFUSED, fp_full), 1, (uint32_t)i);
+                        if (rcode == 2) top(TM_SRVFAIL, fp_full, 1);
+                        else if (rcode == 3) top(TM_NX, fp_full, 1);
+                        else if (rcode == 5) top(TM_REFUSED, fp_full, 1);
                         else if (rcode == 0) {
-                            if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                                top_add(P, S, cached, slot, PV_KEY(TM_NOERROR, fp_full), 1, (uint32_t)i);
-                            if (!ancount) top_add(P, S, cached, slot, PV_KEY(TM_NODATA, fp_full), 1, (uint32_t)i);
+                            if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT) top(TM_NOERROR, fp_full, 1);
+                            if (!ancount) top(TM_NODATA, fp_full, 1);
                         }
-                        if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT)
-                            top_add(P, S, cached, slot, PV_KEY(TM_SIZED, fp_full), dlen, (uint32_t)i);
+                        if (P.dns_groups & PV_DNS_TOP_QNAMES_DETAILS_BIT) top(TM_SIZED, fp_full, dlen);
                     }
                     int q2, q3;
                     uint64_t h2p, h3p;
                     agg_domain(st, q2, q3, h2p, h3p);
                     const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
-                    top_add(P, S, cached, slot, PV_KEY(TM_QNAME2, fp56(k2, st.n - q2, 0)), 1, (uint32_t)i);
+                    top(TM_QNAME2, fp56(k2, st.n - q2, 0), 1);
                     if (q3 >= 0 && (uint32_t)q3 < st.n) {
                         const uint64_t k3 = q3 == 0 ? st.ph : suffix_hash(st, q3, h3p);
-                        top_add(P, S, cached, slot, PV_KEY(TM_QNAME3, fp56(k3, st.n - q3, 0)), 1, (uint32_t)i);
+                        top(TM_QNAME3, fp56(k3, st.n - q3, 0), 1);
                     }
                 }
             }
         }
     }
     if (P.want_events) {
-        // append to this workgroup's event region (records are contiguous per workgroup,
-        // so region order is record order); LDS counter, no global atomics
-        uint32_t e = (uint32_t)S.ebase + atomicAdd(&S.nev, 1u);
-        if (qr) atomicAdd(&S.nresp, 1u);
+        // the workgroup's event region; LDS counter, order irrelevant (sorted by key, index)
+        const uint64_t e = ebase + atomicAdd(nev, 1u);
+        if (qr) atomicAdd(nresp, 1u);
         PvXEvent ev;
-        ev.key = ((uint64_t)flowkey(R, o) << 16) | txid;
-        ev.idx = (uint32_t)i;
+        ev.key = ((uint64_t)dm.fkey << 16) | txid;
+        ev.idx = i;
         ev.len = dlen;
-        ev.sec = o.sec;
-        ev.nsec = o.nsec;
+        ev.sec = dm.sec;
+        ev.nsec = (int32_t)dm.nsec;
         ev.qr = (uint8_t)qr;
-        ev.dir = o.dir;
+        ev.dir = dm.flags & 3;
         ev.period = (uint8_t)period;
         ev.pad = 0;
         P.events[e] = ev;
-        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)i;
+        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | i;
     }
-    if (period > 0 && o.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
+    if (period > 0 && (int64_t)dm.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
 }
 
-
-// cardinality + top IPs of one record (NetworkMetricsBucket::process_net_layer :745-763)
-template <class A>
-__device__ __forceinline__ void net_ips(PV_CREF(PvParams) P, BlockState &S, const A &R, const Parsed &o, uint64_t i,
-                                        bool cached, uint32_t slot, uint32_t &pend_n)
+// cardinality + top IPs of one record (NetworkMetricsBucket::process_net_layer :745-763).
+// One cache entry per (direction, address) carries both the top-N count and the
+// smallest record index, which makes the CPC coupon update of a repeated address free.
+template <class A, class Cache>
+__device__ __forceinline__ void net_ips(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, const A &R, const Parsed &o,
+                                        uint64_t i, uint32_t slot)
 {
     const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
-    if (o.dir == 2) return;
+    if (o.dir == 2 || !(card || tops)) return;
+    uint64_t key, lpay;
+    uint32_t lm;
+    uint64_t h1, h2;
+    bool hashed = false;
     if (o.has4) {
         const uint32_t ip = R.u32(o.dir == 0 ? o.v4 + 12 : o.v4 + 16);
         if (!ip) return;
-        if (card) {
-            uint64_t h1, h2;
-            murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
-            cpc_add(P, S, cached, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i),
-                    pend_n);
-        }
-        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV4, ip), 1, (uint32_t)i);
+        key = PV_KEY(TM_IPV4, ip);
+        lm = TM_IPV4;
+        lpay = ((uint64_t)o.dir << 32) | ip;
     } else if (o.has6) {
         const uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
         const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
         const uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
         if (!(w0 | w1)) return;
-        uint64_t h1, h2;
         murmur_16(w0, w1, h1, h2);
-        if (card)
-            cpc_add(P, S, cached, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i),
-                    pend_n);
-        if (tops) top_add(P, S, cached, slot, PV_KEY(TM_IPV6, h1 ^ (h2 << 1)), 1, (uint32_t)i);
+        hashed = true;
+        const uint64_t hk = (h1 ^ (h2 << 1)) & ((1ull << 55) - 1);
+        key = PV_KEY(TM_IPV6, hk);
+        lm = TM_IPV6;
+        lpay = ((uint64_t)o.dir << 55) | hk;
+    } else {
+        return;
+    }
+    uint32_t first = 0xffffffffu;
+    bool in_cache = false;
+    if (cache) in_cache = cache->add(PV_LKEY(slot, lm, lpay), tops ? 1 : 0, (uint32_t)i, first);
+    if (card && !(in_cache && first < (uint32_t)i)) {
+        if (!hashed) murmur_8((uint64_t)(int64_t)(int32_t)(uint32_t)(key & 0xffffffffu), h1, h2);
+        cpc_min(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
+    }
+    if (tops && !in_cache) {
+        if (cache) log_put(P, mq_n, slot, key, 1, (uint32_t)i);
+        else global_add(P, slot, key, 1, (uint32_t)i);
     }
 }
 
-// One record of a tile whose records all fall in period `period` -> bucket slot `slot`
-// (both workgroup-uniform): counters in registers, tables through the LDS cache.
-__device__ __forceinline__ void lane_hot(PV_CREF(PvParams) P, BlockState &S, const TAcc &R, const Parsed &o, uint64_t i,
-                                         uint32_t period, uint32_t slot, Ctr &c, uint32_t &run_v,
-                                         uint32_t &run_n, uint32_t &pend_n, uint32_t &pend_q)
+// Flush a workgroup's key cache: hashed keys to the update log, dense keys to HBM.
+template <class Cache>
+__device__ void cache_flush(PV_CREF(PvParams) P, Cache &C, uint32_t n, uint32_t *mq_n)
 {
-    // Net v1 counters (NetworkMetricsBucket::process_net_layer)
-    c.nev++;
-    c.nin += o.dir == 0; c.nout += o.dir == 1; c.nunk += o.dir == 2;
-    c.n4 += o.l3 == 4; c.n6 += o.l3 == 6;
-    c.nudp += o.l4 == 17; c.ntcp += o.l4 == 6; c.nsyn += o.l4 == 6 && o.syn; c.noth += o.l4 == 0;
-    uint32_t cl = o.caplen;
-    if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
-    if (cl == run_v) run_n++;
-    else { hist_put(P, S, true, slot, run_v, run_n); run_v = cl; run_n = 1; }
-    net_ips(P, S, R, o, i, true, slot, pend_n);
-    if (o.l4 == 17 && !(P.dbg & 4)) dns_lane(P, S, R, o, true, true, slot, period, i, c, pend_q);
-}
-
-// One record of a boundary tile (a period shift inside the tile, or periods outside the
-// kept window): the lane resolves its own period and updates HBM directly. Cold path.
-template <class A>
-__device__ __forceinline__ void lane_cold(PV_CREF(PvParams) P, BlockState &S, const A &R, const Parsed &o, uint64_t i)
-{
-    const uint32_t period = period_of(P, i);
-    const uint32_t slot = P.slot_of[period];
-    const bool upd = period >= P.skip_before;
-    uint64_t *s = slot_sum(P, slot);
-    uint32_t pend = 0;
-    if (upd) {
-        const bool nc = P.net_groups & PV_NET_COUNTERS_BIT;
-        atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_EVENTS], 1ull);
-        atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SAMPLES], 1ull);
-        if (nc) {
-            atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_TOTAL], 1ull);
-            atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.dir == 0 ? NC_IN : (o.dir == 1 ? NC_OUT : NC_UNK))], 1ull);
-            if (o.l3) atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l3 == 4 ? NC_V4 : NC_V6)], 1ull);
-            atomicAdd((unsigned long long *)&s[PV_OFF_NET + (o.l4 == 17 ? NC_UDP : (o.l4 == 6 ? NC_TCP : NC_OTHER))], 1ull);
-            if (o.l4 == 6 && o.syn) atomicAdd((unsigned long long *)&s[PV_OFF_NET + NC_SYN], 1ull);
-        }
-        const uint32_t cl = o.caplen > 65535 ? 65535 : o.caplen;
-        if (o.caplen > 65535) atomicOr(P.flags, PVF_BIG_CAPLEN);
-        atomicAdd((unsigned long long *)&s[PV_OFF_PAYLOAD + cl], 1ull);
-        net_ips(P, S, R, o, i, false, slot, pend);
-    }
-    if (o.l4 == 17 && !(P.dbg & 4)) {
-        Ctr one;
-        one.zero();
-        dns_lane(P, S, R, o, false, upd, slot, period, i, one, pend);
-        if (upd && one.dev) {
-            const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
-            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_EVENTS], 1ull);
-            atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SAMPLES], 1ull);
-            if (dc) {
-                atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_TOTAL], 1ull);
-                atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_UDP], 1ull);
-                if (one.d4) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V4], 1ull);
-                if (one.d6) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_V6], 1ull);
-                atomicAdd((unsigned long long *)&s[PV_OFF_DNS + (one.dq ? DC_QUERIES : DC_REPLIES)], 1ull);
-                if (one.dnoerr) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NOERROR], 1ull);
-                if (one.dnodata) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NODATA], 1ull);
-                if (one.dsrv) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_SRVFAIL], 1ull);
-                if (one.dnx) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_NX], 1ull);
-                if (one.dref) atomicAdd((unsigned long long *)&s[PV_OFF_DNS + DC_REFUSED], 1ull);
-            }
-        }
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+        const uint64_t k = C.key[j];
+        if (!k || !C.cnt[j]) continue;
+        const uint32_t slot = (uint32_t)(k >> 60), lm = (uint32_t)(k >> 56) & 15;
+        const uint64_t pay = k & 0x00ffffffffffffffULL;
+        if (lm >= TM_DENSE_PORT) sum_add(P, slot, dense_word(lm, pay), C.cnt[j]);
+        else if (lm == LM_HIST) sum_add(P, slot, PV_OFF_PAYLOAD + (uint32_t)(pay & 0xffff), C.cnt[j]);
+        else if (lm == TM_IPV4) log_put(P, mq_n, slot, PV_KEY(TM_IPV4, pay & 0xffffffffu), C.cnt[j], C.rep[j]);
+        else if (lm == TM_IPV6) log_put(P, mq_n, slot, PV_KEY(TM_IPV6, pay & ((1ull << 55) - 1)), C.cnt[j], C.rep[j]);
+        else if (lm != LM_CPCQ) log_put(P, mq_n, slot, PV_KEY(lm, pay), C.cnt[j], C.rep[j]);
     }
 }
 
-} // namespace
+// LDS staging accessor over one wave's 8 KiB area (see TAcc): packed (the wave tile's
+// contiguous record span, coalesced loads) or per-lane 128-B windows (dword-major).
+#define PV_WT 64      // records per wave tile
+#define PV_WSTAGE 8192 // LDS staging bytes per wave
+#ifndef PV_NCACHE
+#define PV_NCACHE 1024
+#endif
+static_assert(PV_NCACHE <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cache entries per flush");
 
-// ------------------------------------------------------------------ the fused kernel
-extern "C" __global__ void __launch_bounds__(PV_BLOCK, PV_WPE) pv_net_dns_kernel(const PvParams *__restrict__ Pp)
-{
-    // parameters live in device memory and are read-only for the launch: reading them
-    // through the constant address space makes every uniform field a scalar load
-    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ BlockState S;
-    block_clear(S);
-    if (threadIdx.x == 0) {
-        S.nev = 0; S.nresp = 0; S.mq_n = 0;
-        S.ebase = (uint64_t)blockIdx.x * P.tiles_per_block * PV_BLOCK;
-    }
-    __syncthreads();
-    uint32_t cur_slot = 0xffffffffu; // block-uniform: slot the LDS state and counters belong to
-    Ctr c;
-    c.zero();
-    uint32_t run_v = 0, run_n = 0;   // payload-size run cache
-
-    const uint64_t ntiles = (P.n + PV_BLOCK - 1) / PV_BLOCK;
-    const uint32_t tid = threadIdx.x;
-    // each workgroup owns a contiguous run of tiles (record order inside its event region)
-    const uint64_t tbeg = (uint64_t)blockIdx.x * P.tiles_per_block;
-    const uint64_t tend = tbeg + P.tiles_per_block < ntiles ? tbeg + P.tiles_per_block : ntiles;
-    // software pipeline: while tile t is parsed, the staged bytes of tile t+1 are in
-    // flight in registers, so HBM latency overlaps the parse instead of stalling each
-    // tile. Everything the next issue needs (tile span bounds, window-tile lane offsets)
-    // was loaded one tile earlier still, and cached lanes never wait on HBM mid-tile
-    // (table misses are queued), so no wait inside the tile drains the prefetch.
-    uint4 pf[PV_WIN / 16];
-    auto tile_off = [&](uint64_t t) -> uint64_t {
-        return t * PV_BLOCK < P.n ? (uint64_t)P.offs[t * PV_BLOCK] : P.rec_bytes;
-    };
-    auto lane_off = [&](uint64_t t) -> uint64_t {
-        const uint64_t r = t * PV_BLOCK + tid;
-        return (t < tend && r < P.n) ? (uint64_t)P.offs[r] : 0;
-    };
-    // issue the staging loads of tile t; b0/b1 = byte offsets of its first record and of
-    // the next tile's first record (uniform), loff = the lane's record offset
-    auto issue = [&](uint64_t t, uint64_t b0, uint64_t b1, uint64_t loff, uint32_t &chunks) {
-        const uint64_t base = b0 & ~15ull;
+struct WaveStage {
+    uint4 pf[PV_WSTAGE / 16 / PV_WT]; // 8 x 16 B per lane in flight
+    uint32_t chunks;                  // packed: 16-B chunks of the span (0 = window layout)
+    uint64_t base;                    // packed: span start (16-B aligned)
+    // issue the loads of a wave tile: [b0, b1) = its record span, loff = lane's record offset
+    __device__ __forceinline__ void issue(const uint8_t *recs, uint64_t b0, uint64_t b1, uint64_t loff, bool act,
+                                          uint32_t lane)
+    {
+        base = b0 & ~15ull;
         const uint64_t nch = (b1 - base + 15) >> 4;
-        if (nch <= PV_WINW * PV_BLOCK / 4) {
+        if (nch <= PV_WSTAGE / 16) {
             chunks = (uint32_t)nch;
-            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + base);
+            const uint4 *src = reinterpret_cast<const uint4 *>(recs + base);
 #pragma unroll
-            for (int j = 0; j < PV_WIN / 16; j++) {
-                const uint32_t ch = j * PV_BLOCK + tid;
+            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) {
+                const uint32_t ch = j * PV_WT + lane;
                 pf[j] = ch < chunks ? src[ch] : make_uint4(0, 0, 0, 0);
             }
         } else {
             chunks = 0;
-            const bool act = t * PV_BLOCK + tid < P.n;
-            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + (loff & ~15ull));
+            const uint4 *src = reinterpret_cast<const uint4 *>(recs + (loff & ~15ull));
 #pragma unroll
-            for (int j = 0; j < PV_WIN / 16; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
+            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
         }
-    };
-    // ring: tile t's (b, lane offset) in use; t+1 and t+2 bounds, t+1 lane offsets loaded
-    uint64_t b_cur = 0, b_n1 = 0, b_n2 = 0, off_cur = 0, off_n1 = 0;
-    uint32_t chunks_cur = 0;
-    if (tbeg < tend) {
-        b_cur = tile_off(tbeg);
-        b_n1 = tile_off(tbeg + 1);
-        b_n2 = tile_off(tbeg + 2);
-        off_cur = lane_off(tbeg);
-        off_n1 = lane_off(tbeg + 1);
-        issue(tbeg, b_cur, b_n1, off_cur, chunks_cur);
     }
-    STAMP_DECL
-    for (uint64_t tile_ = tbeg; tile_ < tend; tile_++) {
-        // the tile index is workgroup-uniform: say so, or divergence analysis may keep it
-        // (and every parameter load derived from it) in vector registers
-        const uint64_t tile = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tile_ >> 32)) << 32) |
-                              __builtin_amdgcn_readfirstlane((uint32_t)tile_);
-        const uint64_t t0 = tile * PV_BLOCK;
-        const uint64_t t1 = (t0 + PV_BLOCK < P.n ? t0 + PV_BLOCK : P.n) - 1;
-        // periods are contiguous index ranges (host-provided start indices): a tile is
-        // uniform when its first and last record share a period
-        const uint32_t p_lo = period_of(P, t0), p_hi = period_of(P, t1);
-        const bool straddle = p_lo != p_hi; // pv_boundary_kernel's tile
-        const bool uniform = !straddle && p_lo >= P.skip_before;
-        if (uniform && P.slot_of[p_lo] != cur_slot) {
-            if (cur_slot != 0xffffffffu) {
-                hist_put(P, S, true, cur_slot, run_v, run_n);
-                run_n = 0;
-                ctr_flush(P, cur_slot, c);
-                block_flush(P, S, cur_slot);
-            }
-            cur_slot = P.slot_of[p_lo];
-        }
-        const bool cached = uniform; // bucket slot cur_slot, period p_lo
-        STAMP(0)
-
-        const uint64_t i = t0 + tid;
-        const bool active = i <= t1 && !straddle;
-        const uint64_t off = off_cur;
-        const uint64_t base = __builtin_amdgcn_readfirstlane((uint32_t)b_cur) & ~15u;
-        const uint32_t chunks = __builtin_amdgcn_readfirstlane(chunks_cur);
-        // commit tile t's staged bytes to LDS
+    // write the landed bytes to the wave's LDS area (same-wave readers: no barrier)
+    __device__ __forceinline__ void commit(uint32_t *L, uint32_t lane) const
+    {
         if (chunks) {
-            uint4 *st4 = reinterpret_cast<uint4 *>(S.stage);
+            uint4 *L4 = reinterpret_cast<uint4 *>(L);
 #pragma unroll
-            for (int j = 0; j < PV_WIN / 16; j++) st4[j * PV_BLOCK + tid] = pf[j];
+            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) L4[j * PV_WT + lane] = pf[j];
         } else {
 #pragma unroll
-            for (int j = 0; j < PV_WIN / 16; j++) {
-                S.stage[(4 * j + 0) * PV_BLOCK + tid] = pf[j].x;
-                S.stage[(4 * j + 1) * PV_BLOCK + tid] = pf[j].y;
-                S.stage[(4 * j + 2) * PV_BLOCK + tid] = pf[j].z;
-                S.stage[(4 * j + 3) * PV_BLOCK + tid] = pf[j].w;
+            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) {
+                L[(4 * j + 0) * PV_WT + lane] = pf[j].x;
+                L[(4 * j + 1) * PV_WT + lane] = pf[j].y;
+                L[(4 * j + 2) * PV_WT + lane] = pf[j].z;
+                L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
             }
         }
+    }
+};
+
+struct NetState {
+    uint32_t stage[4][PV_WSTAGE / 4];
+    KeyCache<PV_NCACHE> C;
+    uint32_t mq_n; // update-log entries
+    uint32_t nd;   // DNS messages found
+};
+struct DnsState {
+    uint32_t stage[4][PV_WSTAGE / 4];
+    KeyCache<PV_NCACHE> C;
+    uint32_t mq_n;
+    uint32_t nev, nresp;
+};
+
+} // namespace
+
+// ------------------------------------------------------------------ the Net pass
+// One lane per record. Each wave owns 64-record tiles of its workgroup's contiguous
+// record range (tiles w, w+4, ...), stages a tile in its own LDS area and parses it
+// while the next tile's loads are in flight; waves never wait on each other. DNS
+// messages are appended to the workgroup's DNS work list for the DNS pass.
+extern "C" __global__ void __launch_bounds__(256, PV_WPE) pv_net_kernel(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ NetState S;
+    S.C.clear();
+    if (threadIdx.x == 0) { S.mq_n = 0; S.nd = 0; }
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t *L = S.stage[wave];
+    const uint64_t nwt = (P.n + PV_WT - 1) / PV_WT;
+    const uint64_t wbeg = (uint64_t)blockIdx.x * P.wt_per_block;
+    const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+    const uint64_t dq_base = wbeg * PV_WT; // this workgroup's DNS work-list region
+    auto tile_off = [&](uint64_t t) -> uint64_t { return t * PV_WT < P.n ? (uint64_t)P.offs[t * PV_WT] : P.rec_bytes; };
+    auto lane_off = [&](uint64_t t) -> uint64_t {
+        const uint64_t r = t * PV_WT + lane;
+        return (t < wend && r < P.n) ? (uint64_t)P.offs[r] : 0;
+    };
+    NetCtr c;
+    c.zero();
+    uint32_t wslot = 0xffffffffu;
+    WaveStage W;
+    // ring: this tile's lane offset; next tile's bounds and lane offsets
+    uint64_t t = wbeg + wave;
+    uint64_t off_cur = 0, off_n = 0, b_n0 = 0, b_n1 = 0;
+    if (t < wend) {
+        off_cur = lane_off(t);
+        W.issue(P.recs, tile_off(t), tile_off(t + 1), off_cur, t * PV_WT + lane < P.n, lane);
+        b_n0 = tile_off(t + 4);
+        b_n1 = tile_off(t + 5);
+        off_n = lane_off(t + 4);
+    }
+    STAMP_DECL
+    for (; t < wend; t += 4) {
+        t = uni64(t);
+        const uint64_t r0 = t * PV_WT;
+        const uint64_t r1 = min<uint64_t>(r0 + PV_WT, P.n) - 1;
+        const uint32_t p_lo = period_of(P, r0), p_hi = period_of(P, r1);
+        const bool straddle = p_lo != p_hi; // pv_boundary_kernel's tile
+        const bool upd = !straddle && p_lo >= P.skip_before;
+        const uint32_t slot = P.slot_of[p_lo];
+        if (upd && slot != wslot) {
+            if (wslot != 0xffffffffu) net_flush(P, wslot, c);
+            wslot = slot;
+        }
+        STAMP(0)
+        const uint64_t i = r0 + lane;
+        const bool active = i <= r1 && !straddle;
+        const uint64_t off = off_cur;
+        const uint32_t chunks = __builtin_amdgcn_readfirstlane(W.chunks);
+        const uint64_t base = uni64(W.base);
+        W.commit(L, lane);
         STAMP(1)
-        lds_barrier(); // packed tiles: lanes read bytes other lanes staged
-        STAMP(2)
-        // issue tile t+1's staging loads; load tile t+3's bound and tile t+2's lane offsets
-        if (tile + 1 < tend) {
-            const uint64_t b0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b_n1 >> 32)) << 32) |
-                                __builtin_amdgcn_readfirstlane((uint32_t)b_n1);
-            const uint64_t b1 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b_n2 >> 32)) << 32) |
-                                __builtin_amdgcn_readfirstlane((uint32_t)b_n2);
-            issue(tile + 1, b0, b1, off_n1, chunks_cur);
-            b_cur = b_n1;
-            b_n1 = b_n2;
-            b_n2 = tile_off(tile + 3);
-            off_cur = off_n1;
-            off_n1 = lane_off(tile + 2);
+        if (t + 4 < wend) {
+            W.issue(P.recs, uni64(b_n0), uni64(b_n1), off_n, t * PV_WT + 4 * PV_WT + lane < P.n, lane);
+            off_cur = off_n;
+            b_n0 = tile_off(t + 8);
+            b_n1 = tile_off(t + 9);
+            off_n = lane_off(t + 8);
         }
         STAMP(3)
-        uint32_t pend_n = 0, pend_q = 0; // CPC filter keys to commit after the tile barrier
-        // (no `continue` in this loop: a divergent latch would make the tile loop
-        // non-uniform and turn every uniform parameter load into a waiting vector load)
-        if (P.dbg & 1) c.nev += active && (S.stage[tid] | 1);
         if (active && !(P.dbg & 1)) {
-            const TAcc R = chunks ? TAcc{P.recs, S.stage, base, chunks * 16 - 4, 1u, 0u}
-                                  : TAcc{P.recs, S.stage, off & ~15ull, PV_WIN - 4, (uint32_t)PV_BLOCK, tid};
+            const TAcc R = chunks ? TAcc{P.recs, L, base, chunks * 16 - 4, 1u, 0u}
+                                  : TAcc{P.recs, L, off & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
             Parsed o;
             parse_record(R, P, off, o);
             STAMP(4)
-            if (P.dbg & 2) { c.nev += 1; c.nin += o.dir == 0; c.nudp += o.l4 == 17; }
-            else if (cached) lane_hot(P, S, R, o, i, p_lo, cur_slot, c, run_v, run_n, pend_n, pend_q);
-            else if (o.l4 == 17) // a tile before the kept window: DNS transaction events only
-                dns_lane(P, S, R, o, false, false, 0, p_lo, i, c, pend_q);
+            if (P.dbg & 2) {
+                c.add(o);
+            } else {
+                if (upd) {
+                    c.add(o);
+                    uint32_t cl = o.caplen;
+                    if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
+                    uint32_t first;
+                    if (!S.C.add(PV_LKEY(slot, LM_HIST, cl), 1, (uint32_t)i, first)) sum_add(P, slot, PV_OFF_PAYLOAD + cl, 1);
+                    net_ips(P, &S.C, &S.mq_n, R, o, i, slot);
+                }
+                if (o.l4 == 17 && !(P.dbg & 4)) {
+                    const uint32_t port = dns_port(R.u32(o.l4off));
+                    if (port) {
+                        const DnsMsg d = dns_msg_of(P, R, o, i, port, p_lo, upd);
+                        const uint32_t q = atomicAdd(&S.nd, 1u);
+                        reinterpret_cast<PV_G DnsMsg *>(P.dq)[dq_base + q] = d;
+                    }
+                }
+            }
+        } else if (P.dbg & 1) {
+            c.nev += active;
         }
         STAMP(5)
-        // every lane's CPC filter probes of this tile precede the inserts
-        lds_barrier();
-        cpc_commit(S, pend_n);
-        cpc_commit(S, pend_q);
-        STAMP(6)
     }
-    if (cur_slot != 0xffffffffu) {
-        hist_put(P, S, true, cur_slot, run_v, run_n);
-        ctr_flush(P, cur_slot, c);
-        block_flush(P, S, cur_slot);
-    }
+    if (wslot != 0xffffffffu) net_flush(P, wslot, c);
+    __syncthreads();
+    cache_flush(P, S.C, PV_NCACHE, &S.mq_n);
+    __syncthreads();
     STAMP(7)
     STAMP_FLUSH
+    if (threadIdx.x == 0) {
+        P.mq_cnt[blockIdx.x] = S.mq_n;
+        P.dq_cnt[blockIdx.x] = S.nd;
+    }
+}
+
+// ------------------------------------------------------------------ the DNS pass
+// One lane per DNS message of the Net pass's work list (same workgroup mapping).
+// Each wave stages 128-B windows of its 64 messages in LDS (names past the window
+// come from HBM) while the next messages' windows are in flight.
+extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ DnsState S;
+    S.C.clear();
+    if (threadIdx.x == 0) { S.mq_n = P.mq_cnt[blockIdx.x]; S.nev = 0; S.nresp = 0; }
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t *L = S.stage[wave];
+    const uint32_t nd = P.dq_cnt[blockIdx.x];
+    const uint64_t region = (uint64_t)blockIdx.x * P.wt_per_block * PV_WT;
+    const PV_G DnsMsg *Q = reinterpret_cast<const PV_G DnsMsg *>(P.dq) + region;
+    const uint32_t ntl = (nd + PV_WT - 1) / PV_WT;
+    DnsCtr c;
+    c.zero();
+    uint32_t wslot = 0xffffffffu;
+    auto msg = [&](uint32_t t) -> DnsMsg {
+        const uint32_t j = t * PV_WT + lane;
+        DnsMsg d;
+        if (t < ntl && j < nd) d = Q[j];
+        else { d = DnsMsg{}; d.flags = 0; }
+        return d;
+    };
+    uint32_t t = wave;
+    DnsMsg m_cur{}, m_n{};
+    uint4 pf[8];
+    auto issue = [&](const DnsMsg &d, bool act) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + ((uint64_t)d.moff & ~15ull));
+#pragma unroll
+        for (int j = 0; j < 8; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
+    };
+    if (t < ntl) {
+        m_cur = msg(t);
+        issue(m_cur, t * PV_WT + lane < nd);
+        m_n = msg(t + 4);
+    }
+    for (; t < ntl; t += 4) {
+        t = __builtin_amdgcn_readfirstlane(t);
+        const bool active = t * PV_WT + lane < nd;
+        const DnsMsg dm = m_cur;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            L[(4 * j + 0) * PV_WT + lane] = pf[j].x;
+            L[(4 * j + 1) * PV_WT + lane] = pf[j].y;
+            L[(4 * j + 2) * PV_WT + lane] = pf[j].z;
+            L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
+        }
+        if (t + 4 < ntl) {
+            issue(m_n, (t + 4) * PV_WT + lane < nd);
+            m_cur = m_n;
+            m_n = msg(t + 8);
+        }
+        // the wave's register counters follow the slot of its first message
+        const uint32_t s0 = P.slot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
+        if (s0 != wslot) {
+            if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
+            wslot = s0;
+        }
+        if (active) {
+            const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
+            const bool own = P.slot_of[dm.period] == wslot;
+            dns_process(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
+        }
+    }
+    if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
+    __syncthreads();
+    cache_flush(P, S.C, PV_NCACHE, &S.mq_n);
     __syncthreads();
     if (threadIdx.x == 0) {
-        P.blk_events[blockIdx.x] = S.nev;
         P.mq_cnt[blockIdx.x] = S.mq_n;
+        P.blk_events[blockIdx.x] = S.nev;
         if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
     }
 }
 
-// Applies each workgroup's top-N update log (pv_net_dns_kernel) to the global tables:
-// one entry per lane, so the insert round trips of many entries are in flight at once.
-extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_topn_insert(const PvParams *__restrict__ Pp)
+// Applies each workgroup's top-N update log to the global tables: one entry per
+// lane, so the insert round trips of many entries are in flight at once.
+extern "C" __global__ void __launch_bounds__(256) pv_topn_insert(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     const uint32_t cnt = P.mq_cnt[blockIdx.x];
@@ -764,35 +842,58 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_topn_insert(const PvPa
     }
 }
 
-// Tiles that hold a period shift: one workgroup per tile, each lane resolves its own
-// period and updates HBM directly (no LDS bucket state). Runs after pv_net_dns_kernel
-// on the same stream; its DNS events go to regions after the main kernel's.
-extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_boundary_kernel(const PvParams *__restrict__ Pp)
+// 64-record tiles that hold a period shift: one wave per tile, each lane resolves its
+// own period and updates HBM directly. Runs after the DNS pass on the same stream;
+// its DNS events go to regions after the DNS pass's.
+extern "C" __global__ void __launch_bounds__(64) pv_boundary_kernel(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ BlockState S;
-    if (threadIdx.x == 0) {
-        S.nev = 0; S.nresp = 0;
-        S.ebase = ((uint64_t)P.grid_main * P.tiles_per_block + blockIdx.x) * PV_BLOCK;
-    }
+    __shared__ uint32_t nev, nresp;
+    if (threadIdx.x == 0) { nev = 0; nresp = 0; }
     __syncthreads();
-    const uint64_t i = (uint64_t)P.btile[blockIdx.x] * PV_BLOCK + threadIdx.x;
+    const uint64_t ebase = ((uint64_t)P.grid_main * P.wt_per_block + blockIdx.x) * PV_WT;
+    const uint64_t i = (uint64_t)P.btile[blockIdx.x] * PV_WT + threadIdx.x;
     if (i < P.n) {
         const GAcc R{P.recs};
         Parsed o;
-        const uint64_t off = P.offs[i];
-        parse_record(R, P, off, o);
-        lane_cold(P, S, R, o, i);
+        parse_record(R, P, P.offs[i], o);
+        const uint32_t period = period_of(P, i);
+        const uint32_t slot = P.slot_of[period];
+        const bool upd = period >= P.skip_before;
+        if (upd) {
+            const bool nc = P.net_groups & PV_NET_COUNTERS_BIT;
+            sum_add(P, slot, PV_OFF_NET + NC_EVENTS, 1);
+            sum_add(P, slot, PV_OFF_NET + NC_SAMPLES, 1);
+            if (nc) {
+                sum_add(P, slot, PV_OFF_NET + NC_TOTAL, 1);
+                sum_add(P, slot, PV_OFF_NET + (o.dir == 0 ? NC_IN : (o.dir == 1 ? NC_OUT : NC_UNK)), 1);
+                if (o.l3) sum_add(P, slot, PV_OFF_NET + (o.l3 == 4 ? NC_V4 : NC_V6), 1);
+                sum_add(P, slot, PV_OFF_NET + (o.l4 == 17 ? NC_UDP : (o.l4 == 6 ? NC_TCP : NC_OTHER)), 1);
+                if (o.l4 == 6 && o.syn) sum_add(P, slot, PV_OFF_NET + NC_SYN, 1);
+            }
+            if (o.caplen > 65535) atomicOr(P.flags, PVF_BIG_CAPLEN);
+            sum_add(P, slot, PV_OFF_PAYLOAD + (o.caplen > 65535 ? 65535 : o.caplen), 1);
+            net_ips(P, (KeyCache<2> *)nullptr, nullptr, R, o, i, slot);
+        }
+        if (o.l4 == 17) {
+            const uint32_t port = dns_port(R.u32(o.l4off));
+            if (port) {
+                const DnsMsg dm = dns_msg_of(P, R, o, i, port, period, upd);
+                DnsCtr c;
+                c.zero();
+                dns_process(P, (KeyCache<2> *)nullptr, nullptr, &nev, &nresp, ebase, R, dm, false, c);
+            }
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        P.blk_events[P.grid_main + blockIdx.x] = S.nev;
-        if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
+        P.blk_events[P.grid_main + blockIdx.x] = nev;
+        if (nresp) atomicAdd(P.n_events + 1, nresp);
     }
 }
 
-// Packs the per-workgroup event regions into one dense run (workgroup order = record
-// order) and writes the total to n_events[0].
+// Packs the per-workgroup event regions into one dense run and writes the total to
+// n_events[0] (region order is irrelevant: events are sorted by (key, index)).
 extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint32_t nblk)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
@@ -805,9 +906,9 @@ extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint
     }
     __syncthreads();
     const uint32_t cnt = P.blk_events[blockIdx.x];
-    const uint64_t src = (blockIdx.x < P.grid_main ? (uint64_t)blockIdx.x * P.tiles_per_block
-                                                   : (uint64_t)P.grid_main * P.tiles_per_block + (blockIdx.x - P.grid_main)) *
-                         PV_BLOCK;
+    const uint64_t region = (uint64_t)P.wt_per_block * PV_WT;
+    const uint64_t src = blockIdx.x < P.grid_main ? (uint64_t)blockIdx.x * region
+                                                  : (uint64_t)P.grid_main * region + (uint64_t)(blockIdx.x - P.grid_main) * PV_WT;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         P.skeys[base + j] = P.ekeys[src + j];
         P.svals[base + j] = (uint32_t)(src + j);

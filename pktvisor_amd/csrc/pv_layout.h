@@ -72,7 +72,7 @@ enum {
     TM_NONE = 0, TM_IPV4 = 1, TM_IPV6 = 2, TM_QNAME2 = 3, TM_QNAME3 = 4, TM_NX = 5, TM_REFUSED = 6, TM_SRVFAIL = 7,
     TM_NODATA = 8, TM_NOERROR = 9, TM_SIZED = 10, TM_SLOW_IN = 11, TM_SLOW_OUT = 12,
     // dense metrics share the block cache, flushed into the SUM region
-    TM_DENSE_PORT = 16, TM_DENSE_QTYPE = 17, TM_DENSE_RCODE = 18
+    TM_DENSE_PORT = 13, TM_DENSE_QTYPE = 14, TM_DENSE_RCODE = 15
 };
 #define PV_KEY(metric, payload) (((uint64_t)(metric) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
 #define PV_KEY_METRIC(k) ((uint32_t)((k) >> 56))
@@ -168,14 +168,16 @@ struct PvParams {
     PV_G uint32_t *svals;      // packed event slot positions (sort input)
     PV_G uint32_t *n_events;   // [0] packed total (pv_xact_compact), [1] responses
     uint32_t want_events;
-    uint32_t tiles_per_block;
+    uint32_t wt_per_block; // 64-record wave tiles per workgroup (contiguous record range)
     uint64_t rec_bytes; // bytes of the record run (end of the last record)
     PV_G uint64_t *mq;    // per-workgroup top-N update logs: mq_cap x {key | slot << 60, w | rep << 32}
     PV_G uint32_t *mq_cnt; // entries per workgroup log
     PV_G uint64_t *stamps; // diagnostic builds (-DPV_STAMPS): 8 phase cycle sums per wave
     uint32_t mq_cap;
     uint32_t grid_main;   // workgroups of pv_net_dns_kernel
-    uint32_t n_btiles;    // tiles holding a period shift (handled by pv_boundary_kernel)
+    uint32_t n_btiles;    // 64-record tiles holding a period shift (pv_boundary_kernel)
+    PV_G uint64_t *dq;    // per-workgroup DNS work lists (32-B DnsMsg), region = wt_per_block * 64
+    PV_G uint32_t *dq_cnt;
     uint32_t btile[PV_MAX_SHIFTS];
     uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane
     PV_G uint32_t *flags;
