@@ -41,7 +41,11 @@ extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
 extern "C" __global__ void pv_boundary_kernel(const PvParams *P);
-extern "C" __global__ void pv_topn_insert(const PvParams *P);
+extern "C" __global__ void pv_topn_count(const PvParams *P);
+extern "C" __global__ void pv_topn_scan(const PvParams *P);
+extern "C" __global__ void pv_topn_scatter(const PvParams *P);
+extern "C" __global__ void pv_topn_merge(const PvParams *P);
+extern "C" __global__ void pv_topn_names(const PvParams *P);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
@@ -50,7 +54,13 @@ extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t
 namespace {
 
 // status words (device): flags, n_events, n_resp, n_vals, dns_any[8], dns_at_thresh[8]
-enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_DNS_ANY = 4, ST_DNS_AT = 12, ST_WORDS = 20 };
+enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_DNS_ANY = 4, ST_DNS_AT = 12, ST_NNEW = 20, ST_WORDS = 21 };
+// after the status words (one allocation, zeroed per batch up to the live region count):
+// per-region update counts, then offsets and fill pointers
+#define ST_TP_CNT 32
+#define ST_TP_OFF (ST_TP_CNT + (1 << PV_MAX_REGIONS_LOG2))
+#define ST_TP_FILL (ST_TP_OFF + (1 << PV_MAX_REGIONS_LOG2))
+#define ST_ALLOC (ST_TP_FILL + (1 << PV_MAX_REGIONS_LOG2))
 
 struct SlotMeta {
     int64_t start_sec = 0, start_nsec = 0, end_sec = 0, end_nsec = 0;
@@ -233,6 +243,10 @@ struct pv_ctx {
     uint64_t *d_ekeys = nullptr;
     uint32_t *d_blk_events = nullptr;
     uint64_t *d_mq = nullptr; // per-workgroup top-N update logs (grown on demand)
+    uint64_t *d_tpbuf = nullptr; // the logs bucketed by table region (same size)
+    PvNewName *d_nn = nullptr;   // entries created by pv_topn_merge (names pending)
+    uint32_t nn_cap = 0;
+    uint32_t reg_log2 = 0;
     size_t mq_bytes = 0;
     uint32_t *d_mq_cnt = nullptr;
     uint64_t *d_stamps = nullptr; // diagnostic phase stamps (PV_STAMPS env + -DPV_STAMPS build)
@@ -797,6 +811,12 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     if (c->cfg.net_groups) c->net_groups = c->cfg.net_groups;
     if (c->cfg.dns_groups) c->dns_groups = c->cfg.dns_groups;
     if (c->cfg.table_log2) c->tcap_log2 = c->cfg.table_log2;
+    if (c->tcap_log2 < 8 || c->tcap_log2 > PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2) {
+        *out = c;
+        return c->fail(PV_EINVAL, "table_log2 %u out of range [8, %d]", c->tcap_log2, PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2);
+    }
+    c->reg_log2 = c->tcap_log2 > PV_REGION_LOG2 ? c->tcap_log2 - PV_REGION_LOG2 : 0;
+    c->nn_cap = (uint32_t)std::min<uint64_t>(1ull << c->tcap_log2, 1ull << 22);
     if (c->cfg.max_records == 0) c->cfg.max_records = 1 << 20;
     c->max_records = c->cfg.max_records;
     // TransactionManager(ttl_ms) split (TransactionManager.h:60-68)
@@ -846,7 +866,8 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
-        !hip_ok(e = hipMalloc(&c->d_status, ST_WORDS * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_status, ST_ALLOC * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
         !hip_ok(e = hipMalloc(&c->d_params, sizeof(PvParams))) ||
         !hip_ok(e = hipMalloc(&c->d_xparams, sizeof(PvXactParams))) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
         !hip_ok(e = hipEventCreate(&c->ev_stop))) {
@@ -867,7 +888,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_nn, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -1032,7 +1053,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.flags = c->d_status + ST_FLAGS;
     P.dns_first = c->d_status + ST_DNS_ANY;
     P.dns_at_thresh = c->d_status + ST_DNS_AT;
-    launch_fill32(c, c->d_status, ST_WORDS, 0);
+    launch_fill32(c, c->d_status, ST_TP_CNT + (1u << c->reg_log2), 0);
     hipError_t e;
     const uint64_t tiles = (n + 63) / 64; // 64-record wave tiles
     // persistent grid: exactly the workgroups that are resident at once (LDS/VGPR
@@ -1052,14 +1073,24 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         const size_t need = (size_t)grid * P.mq_cap * 16;
         if (need > c->mq_bytes) {
             if (c->d_mq) hipFree(c->d_mq);
-            c->d_mq = nullptr;
+            if (c->d_tpbuf) hipFree(c->d_tpbuf);
+            c->d_mq = c->d_tpbuf = nullptr;
             c->mq_bytes = 0;
-            if (!hip_ok(e = hipMalloc(&c->d_mq, need))) return c->hipfail(e, "top-N update log");
+            if (!hip_ok(e = hipMalloc(&c->d_mq, need)) || !hip_ok(e = hipMalloc(&c->d_tpbuf, need)))
+                return c->hipfail(e, "top-N update log");
             c->mq_bytes = need;
         }
     }
     P.mq = c->d_mq;
     P.mq_cnt = c->d_mq_cnt;
+    P.reg_log2 = c->reg_log2;
+    P.tp_cnt = c->d_status + ST_TP_CNT;
+    P.tp_off = c->d_status + ST_TP_OFF;
+    P.tp_fill = c->d_status + ST_TP_FILL;
+    P.tp_buf = c->d_tpbuf;
+    P.nn_cnt = c->d_status + ST_NNEW;
+    P.nn = c->d_nn;
+    P.nn_cap = c->nn_cap;
     P.stamps = c->d_stamps;
     P.dq = c->d_dq;
     P.dq_cnt = c->d_dq_cnt;
@@ -1081,7 +1112,12 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
     hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
     hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
-    hipLaunchKernelGGL(pv_topn_insert, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    // top-N: bucket the update logs by table region, merge each region in LDS, names
+    hipLaunchKernelGGL(pv_topn_count, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_topn_scan, dim3(1), dim3(1024), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_topn_scatter, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_topn_merge, dim3(1u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 8), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (P.n_btiles) {
         hipLaunchKernelGGL(pv_boundary_kernel, dim3(P.n_btiles), dim3(64), 0, st, (const PvParams *)c->d_params);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_boundary_kernel");

@@ -164,6 +164,29 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     return (uint32_t)pos + 1;
 }
 
+// Table position of a key: its region base (slot included) and start index in the region.
+struct TPos {
+    uint64_t rbase;
+    uint32_t pos, rmask;
+};
+__device__ __forceinline__ uint64_t tkey_hash(uint64_t key) { return fmix64(key ^ 0x5bd1e995ULL); }
+__device__ __forceinline__ uint32_t tregion(PV_CREF(PvParams) P, uint64_t h)
+{
+    return (uint32_t)(h >> 40) & ((1u << P.reg_log2) - 1);
+}
+__device__ __forceinline__ TPos tpos(PV_CREF(PvParams) P, uint32_t slot, uint64_t key)
+{
+    const uint32_t rsl = P.tcap_log2 - P.reg_log2;
+    const uint64_t h = tkey_hash(key);
+    TPos t;
+    t.rmask = (1u << rsl) - 1;
+    t.rbase = ((uint64_t)slot << P.tcap_log2) + ((uint64_t)tregion(P, h) << rsl);
+    t.pos = (uint32_t)h & t.rmask;
+    return t;
+}
+
+// Direct insert into the global table (boundary tiles, slow transactions, regions with
+// few updates in a batch): device-scope CAS / add, probing inside the key's region.
 __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
 {
     uint32_t metric = PV_KEY_METRIC(key);
@@ -171,30 +194,28 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
     if (metric == TM_DENSE_PORT) { atomicAdd((unsigned long long *)&sum[PV_OFF_PORT + (key & 0xffff)], (unsigned long long)w); return; }
     if (metric == TM_DENSE_QTYPE) { atomicAdd((unsigned long long *)&sum[PV_OFF_QTYPE + (key & 0xffff)], (unsigned long long)w); return; }
     if (metric == TM_DENSE_RCODE) { atomicAdd((unsigned long long *)&sum[PV_OFF_RCODE + (key & 0xf)], (unsigned long long)w); return; }
-    const uint64_t cap = 1ull << P.tcap_log2;
-    const uint64_t base = (uint64_t)slot << P.tcap_log2;
-    uint64_t h = fmix64(key ^ 0x5bd1e995ULL) & (cap - 1);
+    TPos t = tpos(P, slot, key);
     // the probe loop only claims / finds the entry; a new entry's name record is
     // written once after it, so lanes never serialise on name decoding inside it
     int64_t created = -1;
     bool done = false;
-    for (int probe = 0; probe < 128 && !done; probe++) {
-        uint64_t *kp = &P.tkeys[base + h];
+    for (int probe = 0; probe < PV_PROBES && !done; probe++) {
+        uint64_t *kp = &P.tkeys[t.rbase + t.pos];
         uint64_t k = __atomic_load_n(kp, __ATOMIC_RELAXED);
         if (k == 0) {
             uint64_t prev = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)key);
-            if (prev == 0) created = (int64_t)h;
+            if (prev == 0) created = (int64_t)(t.rbase + t.pos);
             k = prev == 0 ? key : prev;
         }
         if (k == key) {
-            atomicAdd((unsigned long long *)&P.tcnt[base + h], (unsigned long long)w);
+            atomicAdd((unsigned long long *)&P.tcnt[t.rbase + t.pos], (unsigned long long)w);
             done = true;
         } else {
-            h = (h + 1) & (cap - 1);
+            t.pos = (t.pos + 1) & t.rmask;
         }
     }
     if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
-    if (created >= 0 && metric != TM_IPV4) P.taux[base + (uint64_t)created] = write_name(P, slot, metric, rep);
+    if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep);
 }
 
 // ------------------------------------------------------------------ LDS key cache
@@ -237,8 +258,8 @@ struct KeyCache {
 };
 
 // Top-N updates the LDS cache does not absorb go to the workgroup's HBM update log
-// (fire-and-forget stores, slot in key bits 60..63); pv_topn_insert applies the log to
-// the global tables after the parse kernels, so no lane waits on an HBM round trip for
+// (fire-and-forget stores, slot in key bits 60..63); the top-N merge kernels apply the
+// logs to the global tables after the parse kernels, so no lane waits on an HBM round trip for
 // a table update.
 __device__ __forceinline__ void log_put(PV_CREF(PvParams) P, uint32_t *mq_n, uint32_t slot, uint64_t key, uint32_t w,
                                         uint32_t rep)
@@ -829,16 +850,272 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *
     }
 }
 
-// Applies each workgroup's top-N update log to the global tables: one entry per
-// lane, so the insert round trips of many entries are in flight at once.
-extern "C" __global__ void __launch_bounds__(256) pv_topn_insert(const PvParams *__restrict__ Pp)
+// ------------------------------------------------------------------ top-N merge
+// The parse passes leave per-workgroup update logs. They are bucketed by table region
+// (count -> scan -> scatter); then one workgroup per region merges the region's updates:
+// it loads the region (keys, counts) into LDS, applies every update with LDS atomics,
+// writes the region back with coalesced stores and lists the entries it created, whose
+// names pv_topn_names decodes. No update waits on an HBM round trip and no update
+// issues an HBM atomic (regions with only a few updates take the direct path).
+#define PV_RS (1u << PV_REGION_LOG2)
+#define PV_MERGE_DIRECT 64 // regions with at most this many updates use global_add
+
+__device__ __forceinline__ uint32_t log_region(PV_CREF(PvParams) P, uint64_t e0)
+{
+    return tregion(P, tkey_hash(e0 & ((1ull << 60) - 1)));
+}
+
+extern "C" __global__ void __launch_bounds__(256) pv_topn_count(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t h[1u << PV_MAX_REGIONS_LOG2];
+    const uint32_t nreg = 1u << P.reg_log2;
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) h[r] = 0;
+    __syncthreads();
     const uint32_t cnt = P.mq_cnt[blockIdx.x];
     const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * P.mq_cap * 2;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) atomicAdd(&h[log_region(P, q[2 * j])], 1u);
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
+        if (h[r]) atomicAdd(&P.tp_cnt[r], h[r]);
+}
+
+// exclusive scan of the region counts (one workgroup)
+extern "C" __global__ void __launch_bounds__(1024) pv_topn_scan(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t part[1024];
+    const uint32_t nreg = 1u << P.reg_log2;
+    const uint32_t per = (nreg + 1023) / 1024;
+    const uint32_t r0 = threadIdx.x * per;
+    uint32_t s = 0;
+    for (uint32_t r = r0; r < r0 + per && r < nreg; r++) s += P.tp_cnt[r];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - s;
+    for (uint32_t r = r0; r < r0 + per && r < nreg; r++) {
+        P.tp_off[r] = run;
+        P.tp_fill[r] = run;
+        run += P.tp_cnt[r];
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(256) pv_topn_scatter(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t h[1u << PV_MAX_REGIONS_LOG2];
+    const uint32_t nreg = 1u << P.reg_log2;
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) h[r] = 0;
+    __syncthreads();
+    const uint32_t cnt = P.mq_cnt[blockIdx.x];
+    const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * P.mq_cap * 2;
+    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) atomicAdd(&h[log_region(P, q[2 * j])], 1u);
+    __syncthreads();
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
+        if (h[r]) h[r] = atomicAdd(&P.tp_fill[r], h[r]);
+    __syncthreads();
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         const uint64_t e0 = q[2 * j], e1 = q[2 * j + 1];
-        global_add(P, (uint32_t)(e0 >> 60), e0 & ((1ull << 60) - 1), (uint32_t)e1, (uint32_t)(e1 >> 32));
+        const uint32_t pos = atomicAdd(&h[log_region(P, e0)], 1u);
+        P.tp_buf[2 * (uint64_t)pos] = e0;
+        P.tp_buf[2 * (uint64_t)pos + 1] = e1;
+    }
+}
+
+struct MergeState {
+    uint64_t key[PV_RS];
+    uint64_t cnt[PV_RS];
+    uint32_t nidx[PV_RS]; // entries created in this batch: region index, source record
+    uint32_t nrep[PV_RS];
+    uint32_t nnew, slots, nbase;
+};
+
+extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t r = blockIdx.x;
+    const uint32_t n = P.tp_cnt[r];
+    if (n == 0) return;
+    const PV_G uint64_t *q = P.tp_buf + 2 * (uint64_t)P.tp_off[r];
+    if (n <= PV_MERGE_DIRECT) {
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            const uint64_t e0 = q[2 * j], e1 = q[2 * j + 1];
+            global_add(P, (uint32_t)(e0 >> 60), e0 & ((1ull << 60) - 1), (uint32_t)e1, (uint32_t)(e1 >> 32));
+        }
+        return;
+    }
+    __shared__ MergeState S;
+    const uint32_t rsl = P.tcap_log2 - P.reg_log2;
+    const uint32_t rs = 1u << rsl;
+    if (threadIdx.x == 0) S.slots = 0;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) atomicOr(&S.slots, 1u << (uint32_t)(q[2 * j] >> 60));
+    __syncthreads();
+    uint32_t slots = S.slots;
+    while (slots) {
+        const uint32_t s = __builtin_ctz(slots);
+        slots &= slots - 1;
+        const uint64_t rbase = ((uint64_t)s << P.tcap_log2) + ((uint64_t)r << rsl);
+        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+            S.key[i] = P.tkeys[rbase + i];
+            S.cnt[i] = P.tcnt[rbase + i];
+        }
+        if (threadIdx.x == 0) S.nnew = 0;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            const uint64_t e0 = q[2 * j];
+            if ((uint32_t)(e0 >> 60) != s) continue;
+            const uint64_t e1 = q[2 * j + 1];
+            const uint64_t key = e0 & ((1ull << 60) - 1);
+            uint32_t pos = (uint32_t)tkey_hash(key) & (rs - 1);
+            bool done = false;
+            for (int probe = 0; probe < PV_PROBES && !done; probe++) {
+                uint64_t cur = S.key[pos];
+                bool created = false;
+                if (cur == 0) {
+                    const uint64_t prev = atomicCAS((unsigned long long *)&S.key[pos], 0ull, (unsigned long long)key);
+                    created = prev == 0;
+                    cur = created ? key : prev;
+                }
+                if (cur == key) {
+                    atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)(uint32_t)e1);
+                    if (created && PV_KEY_METRIC(key) != TM_IPV4) {
+                        const uint32_t k = atomicAdd(&S.nnew, 1u);
+                        S.nidx[k] = pos;
+                        S.nrep[k] = (uint32_t)(e1 >> 32);
+                    }
+                    done = true;
+                } else {
+                    pos = (pos + 1) & (rs - 1);
+                }
+            }
+            if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+            P.tkeys[rbase + i] = S.key[i];
+            P.tcnt[rbase + i] = S.cnt[i];
+        }
+        const uint32_t nnew = S.nnew;
+        if (threadIdx.x == 0 && nnew) S.nbase = atomicAdd(P.nn_cnt, nnew);
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nnew; k += blockDim.x) {
+            const uint32_t g = S.nbase + k;
+            const uint64_t pos = rbase + S.nidx[k];
+            if (g < P.nn_cap) P.nn[g] = PvNewName{s, S.nrep[k], pos};
+            else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k]);
+        }
+        __syncthreads();
+    }
+}
+
+// Name records of the entries pv_topn_merge created, one lane per entry: the record
+// is parsed again, the first PV_WIN bytes of its DNS message are staged into the lane's
+// LDS window with independent 16-B loads, and the name is decoded from there (bytes past
+// the window come from HBM). Each wave reserves its lanes' arena bytes with one atomic.
+extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t stage[4][PV_WINW * 64];
+    const uint32_t n = min(*P.nn_cnt, P.nn_cap);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t *L = stage[threadIdx.x >> 6];
+    const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
+    const GAcc G{P.recs};
+    for (uint32_t b = blockIdx.x * blockDim.x; b < n; b += gridDim.x * blockDim.x) {
+        const uint32_t i = b + threadIdx.x;
+        const bool act = i < n;
+        PvNewName e{0, 0, 0};
+        uint32_t metric = 0, size = 0, start = 0, nl = 0, mlen = 0;
+        uint64_t m = 0, a6 = 0;
+        Parsed o;
+        if (act) {
+            e = P.nn[i];
+            metric = PV_KEY_METRIC(P.tkeys[e.pos]);
+            parse_record(G, P, P.offs[e.rep], o);
+            m = o.l4off + 8;
+            mlen = o.l4len - 8;
+        }
+        const uint64_t wbase = m & ~15ull;
+        {
+            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + wbase);
+            uint4 pf[PV_WIN / 16];
+#pragma unroll
+            for (int j = 0; j < PV_WIN / 16; j++) pf[j] = (act && metric != TM_IPV6) ? src[j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < PV_WIN / 16; j++) {
+                L[(4 * j + 0) * 64 + lane] = pf[j].x;
+                L[(4 * j + 1) * 64 + lane] = pf[j].y;
+                L[(4 * j + 2) * 64 + lane] = pf[j].z;
+                L[(4 * j + 3) * 64 + lane] = pf[j].w;
+            }
+        }
+        const TAcc R{P.recs, L, wbase, PV_WIN - 4, 64u, lane};
+        if (act) {
+            if (metric == TM_IPV6) {
+                a6 = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
+                size = 18;
+            } else {
+                NameStats st;
+                st.init();
+                nl = name_len_l1(R, m, mlen, 12);
+                if (nl > 0) name_emit(R, m, mlen, 12, st);
+                const uint32_t nch = nl > 0 ? st.n : 0;
+                if (metric == TM_QNAME2 || metric == TM_QNAME3) {
+                    int q2, q3;
+                    uint64_t h2, h3;
+                    if (nl > 0) agg_domain(st, q2, q3, h2, h3);
+                    else { q2 = 0; q3 = -1; }
+                    const int st0 = metric == TM_QNAME2 ? q2 : q3;
+                    start = st0 < 0 ? nch : (uint32_t)st0;
+                }
+                size = nch - start + 2;
+            }
+        }
+        // wave prefix sum of the sizes; one arena reservation per wave when its lanes
+        // share a slot (the common case), else one per lane
+        uint32_t incl = size;
+        for (int o2 = 1; o2 < 64; o2 <<= 1) {
+            const uint32_t v = __shfl_up(incl, o2, 64);
+            if (lane >= (uint32_t)o2) incl += v;
+        }
+        const uint32_t tot = __shfl(incl, 63, 64);
+        const uint32_t part = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (PV_ARENA_PARTS - 1);
+        const uint32_t s0 = __shfl(e.slot, 0, 64);
+        const bool uniform = __all(!act || e.slot == s0);
+        uint64_t pos = 0;
+        if (uniform) {
+            unsigned long long wb = 0;
+            if (lane == 0 && tot) wb = atomicAdd((unsigned long long *)&P.arena_top[s0 * PV_ARENA_PARTS + part], (unsigned long long)tot);
+            wb = __shfl(wb, 0, 64);
+            pos = wb + incl - size;
+        } else if (act) {
+            pos = atomicAdd((unsigned long long *)&P.arena_top[e.slot * PV_ARENA_PARTS + part], (unsigned long long)size);
+        }
+        if (act) {
+            if (pos + size > pcap) {
+                atomicOr(P.flags, PVF_ARENA_FULL);
+            } else {
+                pos += part * pcap;
+                uint8_t *arena = P.arena + (uint64_t)e.slot * P.arena_cap;
+                const uint32_t slen = size - 2;
+                arena[pos] = (uint8_t)(slen & 0xff);
+                arena[pos + 1] = (uint8_t)(slen >> 8);
+                if (metric == TM_IPV6) {
+                    for (int k = 0; k < 16; k++) arena[pos + 2 + k] = (uint8_t)G.u8(a6 + k);
+                } else if (slen > 0 && nl > 0) {
+                    CopyEmit ce{arena + pos + 2, start, 0, (metric == TM_SLOW_IN || metric == TM_SLOW_OUT) ? 1u : 0u};
+                    name_emit(R, m, mlen, 12, ce);
+                }
+                P.taux[e.pos] = (uint32_t)pos + 1;
+            }
+        }
     }
 }
 

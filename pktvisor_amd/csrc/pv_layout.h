@@ -77,6 +77,20 @@ enum {
 #define PV_KEY(metric, payload) (((uint64_t)(metric) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
 #define PV_KEY_METRIC(k) ((uint32_t)((k) >> 56))
 
+// Each slot's table is cut into regions of 2^PV_REGION_LOG2 entries (fewer when the table
+// is smaller). A key lives in region (hash >> 40) & (regions - 1), at hash & (region - 1)
+// plus linear probing that wraps inside the region, so one workgroup of pv_topn_merge
+// can own a region outright and merge a batch's updates into it in LDS.
+#define PV_REGION_LOG2 12
+#define PV_MAX_REGIONS_LOG2 12 // table_log2 <= PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2
+#define PV_PROBES 256
+// entry of the new-name list (pv_topn_merge -> pv_topn_names)
+struct PvNewName {
+    uint32_t slot;
+    uint32_t rep;  // record index in the batch the name is decoded from
+    uint64_t pos;  // table index (slot-relative offset included)
+};
+
 // aux word of a top-N entry: arena offset + 1 of its name record (0 = none)
 // arena record: uint16 length, then bytes
 
@@ -179,6 +193,16 @@ struct PvParams {
     PV_G uint64_t *dq;    // per-workgroup DNS work lists (32-B DnsMsg), region = wt_per_block * 64
     PV_G uint32_t *dq_cnt;
     uint32_t btile[PV_MAX_SHIFTS];
+    // top-N merge: regions per slot table (log2), per-region update counts / offsets /
+    // fill pointers into the region-sorted update buffer, and the new-name list
+    uint32_t reg_log2;
+    PV_G uint32_t *tp_cnt;
+    PV_G uint32_t *tp_off;
+    PV_G uint32_t *tp_fill;
+    PV_G uint64_t *tp_buf;
+    PV_G uint32_t *nn_cnt;
+    PV_G PvNewName *nn;
+    uint32_t nn_cap;
     uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane
     PV_G uint32_t *flags;
     PV_G uint32_t *dns_first; // per period: min record index of a DNS event in that period

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Iteration check: GPU parity tests, then kernel-trace stats of C2 / C3 / C4 benches.
+# usage: gpu_iter.sh TAG  -> gpurun_out/it_TAG/
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+T=${1:-x}
+O=gpurun_out/it_$T
+mkdir -p $O
+export TMPDIR=/tmp
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+R="rocprofv3 --kernel-trace --stats --output-format csv"
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 &&
+timeout -k 10 300 $R -d $O/c2 -o k -- $B > $O/c2.log 2>&1 &&
+timeout -k 10 300 $R -d $O/c3 -o k -- $B --config 3 > $O/c3.log 2>&1 &&
+timeout -k 10 300 $R -d $O/c4 -o k -- $B --config 4 --records 4000000 > $O/c4.log 2>&1
+rc=$?
+echo "chain exit $rc"
+exit $rc
