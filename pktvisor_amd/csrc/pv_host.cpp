@@ -41,7 +41,7 @@ extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
 extern "C" __global__ void pv_boundary_kernel(const PvParams *P);
-extern "C" __global__ void pv_topn_count(const PvParams *P);
+extern "C" __global__ void pv_topn_combine(const PvParams *P);
 extern "C" __global__ void pv_topn_scan(const PvParams *P);
 extern "C" __global__ void pv_topn_scatter(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
@@ -57,6 +57,8 @@ namespace {
 enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_DNS_ANY = 4, ST_DNS_AT = 12, ST_NNEW = 20, ST_WORDS = 21 };
 // after the status words (one allocation, zeroed per batch up to the live region count):
 // per-region update counts, then offsets and fill pointers
+#define PV_NET_THREADS 256    // pv_net_kernel: four waves
+#define PV_TRASH_WAVES 16384 // Net-pass waves with a 2-KiB trash area (grid <= 4096)
 #define ST_TP_CNT 32
 #define ST_TP_OFF (ST_TP_CNT + (1 << PV_MAX_REGIONS_LOG2))
 #define ST_TP_FILL (ST_TP_OFF + (1 << PV_MAX_REGIONS_LOG2))
@@ -244,7 +246,11 @@ struct pv_ctx {
     uint32_t *d_blk_events = nullptr;
     uint64_t *d_mq = nullptr; // per-workgroup top-N update logs (grown on demand)
     uint64_t *d_tpbuf = nullptr; // the logs bucketed by table region (same size)
+    uint64_t *d_cb = nullptr;    // combined update lists (same size)
+    uint32_t *d_cb_cnt = nullptr;
     PvNewName *d_nn = nullptr;   // entries created by pv_topn_merge (names pending)
+    uint64_t *d_iplog = nullptr; // dense IP log, one u64 per record (max_records + one tile)
+    uint64_t *d_trash = nullptr; // 64 B per Net-pass wave
     uint32_t nn_cap = 0;
     uint32_t reg_log2 = 0;
     size_t mq_bytes = 0;
@@ -839,13 +845,14 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
     {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_net_kernel), 256, 0) ==
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_net_kernel), PV_NET_THREADS, 0) ==
                 hipSuccess && nb > 0)
             c->wg_per_cu = nb;
     }
     // event / DNS work-list regions: main workgroups own wt_per_block * 64 slots each (the
     // last may overhang the batch by < wt_per_block tiles), boundary workgroups 64 each
-    const uint64_t ev_cap = mr + mr / ((uint64_t)c->wg_per_cu * c->cus) + 16 * 256;
+    // (the last workgroup's region may overhang the batch by < wt_per_block tiles)
+    const uint64_t ev_cap = mr + mr / ((uint64_t)c->wg_per_cu * c->cus) + 64 * 64 + 16 * 256;
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
         !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_cpc, (size_t)PV_SLOTS * PV_MIN_WORDS * 8)) ||
@@ -868,6 +875,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
         !hip_ok(e = hipMalloc(&c->d_status, ST_ALLOC * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
+        !hip_ok(e = hipMalloc(&c->d_iplog, (size_t)(mr + 64) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_trash, (size_t)PV_TRASH_WAVES * 2048)) ||
+        !hip_ok(e = hipMalloc(&c->d_cb_cnt, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_params, sizeof(PvParams))) ||
         !hip_ok(e = hipMalloc(&c->d_xparams, sizeof(PvXactParams))) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
         !hip_ok(e = hipEventCreate(&c->ev_stop))) {
@@ -888,7 +898,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_nn, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->d_recs, c->d_offs};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->ev_start) hipEventDestroy(c->ev_start);
@@ -1058,7 +1068,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     const uint64_t tiles = (n + 63) / 64; // 64-record wave tiles
     // persistent grid: exactly the workgroups that are resident at once (LDS/VGPR
     // occupancy), each owning a contiguous run of wave tiles
-    uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + 3) / 4, (uint64_t)c->cus * c->wg_per_cu);
+    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->cus * c->wg_per_cu);
     P.wt_per_block = (uint32_t)((tiles + grid - 1) / grid);
     P.rec_bytes = info->bytes_used;
     {
@@ -1074,9 +1084,11 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         if (need > c->mq_bytes) {
             if (c->d_mq) hipFree(c->d_mq);
             if (c->d_tpbuf) hipFree(c->d_tpbuf);
-            c->d_mq = c->d_tpbuf = nullptr;
+            if (c->d_cb) hipFree(c->d_cb);
+            c->d_mq = c->d_tpbuf = c->d_cb = nullptr;
             c->mq_bytes = 0;
-            if (!hip_ok(e = hipMalloc(&c->d_mq, need)) || !hip_ok(e = hipMalloc(&c->d_tpbuf, need)))
+            if (!hip_ok(e = hipMalloc(&c->d_mq, need)) || !hip_ok(e = hipMalloc(&c->d_tpbuf, need)) ||
+                !hip_ok(e = hipMalloc(&c->d_cb, need)))
                 return c->hipfail(e, "top-N update log");
             c->mq_bytes = need;
         }
@@ -1091,6 +1103,11 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.nn_cnt = c->d_status + ST_NNEW;
     P.nn = c->d_nn;
     P.nn_cap = c->nn_cap;
+    P.iplog = c->d_iplog;
+    P.trash = c->d_trash;
+    if ((uint64_t)grid * 4 > PV_TRASH_WAVES) return c->fail(PV_ECAPACITY, "grid of %u workgroups exceeds the trash area", grid);
+    P.cb = c->d_cb;
+    P.cb_cnt = c->d_cb_cnt;
     P.stamps = c->d_stamps;
     P.dq = c->d_dq;
     P.dq_cnt = c->d_dq_cnt;
@@ -1107,13 +1124,14 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, &P, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
-    hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
     hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
     hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
-    // top-N: bucket the update logs by table region, merge each region in LDS, names
-    hipLaunchKernelGGL(pv_topn_count, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    // top-N: combine each workgroup's updates, bucket them by table region, merge each
+    // region in LDS, decode the names of new entries
+    hipLaunchKernelGGL(pv_topn_combine, dim3(grid), dim3(512), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_scan, dim3(1), dim3(1024), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_scatter, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_merge, dim3(1u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);

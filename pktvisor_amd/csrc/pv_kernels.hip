@@ -42,7 +42,7 @@
     }
 #define STAMP_FLUSH                                                                          \
     if ((threadIdx.x & 63) == 0)                                                             \
-        for (int k_ = 0; k_ < 8; k_++) P.stamps[((uint64_t)blockIdx.x * 4 + threadIdx.x / 64) * 8 + k_] = st_acc[k_];
+        for (int k_ = 0; k_ < 8; k_++) P.stamps[((uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 8 + k_] = st_acc[k_];
 #else
 #define STAMP_DECL
 #define STAMP(k)
@@ -52,7 +52,7 @@
 #define PV_WIN 128 // bytes of each record staged into LDS (record header + frame start)
 #endif
 #ifndef PV_WPE
-#define PV_WPE 2 // waves per SIMD the main kernel is register-budgeted for
+#define PV_WPE 4 // waves per SIMD the Net pass is register-budgeted for
 #endif
 #define PV_WINW (PV_WIN / 4)
 
@@ -356,7 +356,7 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v)
 
 // DNS over UDP: the message of one record, located by the Net pass
 // (DnsStreamHandler::process_udp_packet_cb, :270-302)
-struct DnsMsg {
+struct alignas(16) DnsMsg {
     uint32_t idx;     // record index in the batch
     uint32_t moff;    // absolute byte offset of the DNS header in the record blob
     uint16_t mlen;    // UDP payload length (IP-length trimmed)
@@ -370,6 +370,25 @@ struct DnsMsg {
     uint32_t pad;
 };
 static_assert(sizeof(DnsMsg) == 32, "DnsMsg is two 16-B stores");
+// a DnsMsg as its two 16-B words, composed dword by dword (field-wise stores of the
+// struct would split into sub-dword stores)
+struct DnsMsgW {
+    uint4 a, b;
+};
+__device__ __forceinline__ DnsMsgW msg_words(const DnsMsg &d)
+{
+    DnsMsgW w;
+    w.a = make_uint4(d.idx, d.moff, (uint32_t)d.mlen | ((uint32_t)d.mcap << 16),
+                     (uint32_t)d.port | ((uint32_t)d.flags << 16) | ((uint32_t)d.period << 24));
+    w.b = make_uint4(d.fkey, d.sec, d.nsec, 0u);
+    return w;
+}
+__device__ __forceinline__ void put_msg(PV_G DnsMsg *dst, const DnsMsgW &w)
+{
+    PV_G uint4 *p = reinterpret_cast<PV_G uint4 *>(dst);
+    p[0] = w.a;
+    p[1] = w.b;
+}
 
 // Metric port of a UDP datagram (0 = not DNS), from the raw port word
 __device__ __forceinline__ uint32_t dns_port(uint32_t pw)
@@ -382,7 +401,7 @@ __device__ __forceinline__ uint32_t dns_port(uint32_t pw)
 }
 template <class A>
 __device__ __forceinline__ DnsMsg dns_msg_of(PV_CREF(PvParams) P, const A &R, const Parsed &o, uint64_t i, uint32_t port,
-                                             uint32_t period, bool upd)
+                                             uint32_t period, bool upd, bool with_key = true)
 {
     DnsMsg d;
     d.idx = (uint32_t)i;
@@ -393,7 +412,7 @@ __device__ __forceinline__ DnsMsg dns_msg_of(PV_CREF(PvParams) P, const A &R, co
     d.port = (uint16_t)port;
     d.flags = (uint8_t)(o.dir | (o.l3 == 6 ? 4 : 0) | (upd ? 8 : 0));
     d.period = (uint8_t)period;
-    d.fkey = flowkey(R, o);
+    d.fkey = with_key ? flowkey(R, o) : 0u;
     d.sec = (uint32_t)o.sec;
     d.nsec = (uint32_t)o.nsec;
     d.pad = 0;
@@ -594,65 +613,15 @@ __device__ void cache_flush(PV_CREF(PvParams) P, Cache &C, uint32_t n, uint32_t 
     }
 }
 
-// LDS staging accessor over one wave's 8 KiB area (see TAcc): packed (the wave tile's
-// contiguous record span, coalesced loads) or per-lane 128-B windows (dword-major).
 #define PV_WT 64      // records per wave tile
-#define PV_WSTAGE 8192 // LDS staging bytes per wave
+#define PV_WSTAGE 8192 // DNS pass: LDS staging bytes per wave (128-B message windows)
 #ifndef PV_NCACHE
 #define PV_NCACHE 1024
 #endif
 static_assert(PV_NCACHE <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cache entries per flush");
 
-struct WaveStage {
-    uint4 pf[PV_WSTAGE / 16 / PV_WT]; // 8 x 16 B per lane in flight
-    uint32_t chunks;                  // packed: 16-B chunks of the span (0 = window layout)
-    uint64_t base;                    // packed: span start (16-B aligned)
-    // issue the loads of a wave tile: [b0, b1) = its record span, loff = lane's record offset
-    __device__ __forceinline__ void issue(const uint8_t *recs, uint64_t b0, uint64_t b1, uint64_t loff, bool act,
-                                          uint32_t lane)
-    {
-        base = b0 & ~15ull;
-        const uint64_t nch = (b1 - base + 15) >> 4;
-        if (nch <= PV_WSTAGE / 16) {
-            chunks = (uint32_t)nch;
-            const uint4 *src = reinterpret_cast<const uint4 *>(recs + base);
-#pragma unroll
-            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) {
-                const uint32_t ch = j * PV_WT + lane;
-                pf[j] = ch < chunks ? src[ch] : make_uint4(0, 0, 0, 0);
-            }
-        } else {
-            chunks = 0;
-            const uint4 *src = reinterpret_cast<const uint4 *>(recs + (loff & ~15ull));
-#pragma unroll
-            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
-        }
-    }
-    // write the landed bytes to the wave's LDS area (same-wave readers: no barrier)
-    __device__ __forceinline__ void commit(uint32_t *L, uint32_t lane) const
-    {
-        if (chunks) {
-            uint4 *L4 = reinterpret_cast<uint4 *>(L);
-#pragma unroll
-            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) L4[j * PV_WT + lane] = pf[j];
-        } else {
-#pragma unroll
-            for (int j = 0; j < PV_WSTAGE / 16 / PV_WT; j++) {
-                L[(4 * j + 0) * PV_WT + lane] = pf[j].x;
-                L[(4 * j + 1) * PV_WT + lane] = pf[j].y;
-                L[(4 * j + 2) * PV_WT + lane] = pf[j].z;
-                L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
-            }
-        }
-    }
-};
-
-struct NetState {
-    uint32_t stage[4][PV_WSTAGE / 4];
-    KeyCache<PV_NCACHE> C;
-    uint32_t mq_n; // update-log entries
-    uint32_t nd;   // DNS messages found
-};
+#define PV_HBINS 2048 // payload-size bins the Net pass keeps in LDS (larger sizes: HBM atomics)
+#define PV_NOH 0xffffffffu
 struct DnsState {
     uint32_t stage[4][PV_WSTAGE / 4];
     KeyCache<PV_NCACHE> C;
@@ -660,113 +629,436 @@ struct DnsState {
     uint32_t nev, nresp;
 };
 
+// Adds one to H[v] for every lane with v != PV_NOH. The two most common values of the
+// wave are added once each by a leader lane (packet sizes repeat: a whole wave often
+// shares one), the rest per lane.
+__device__ __forceinline__ void hist_add(uint32_t *H, uint32_t v, uint32_t lane)
+{
+    uint64_t m = __ballot(v != PV_NOH);
+    for (int it = 0; it < 2 && m; it++) {
+        const uint32_t ld = (uint32_t)__builtin_ctzll(m);
+        const uint32_t lv = __builtin_amdgcn_readlane(v, ld);
+        const uint64_t eq = __ballot(v == lv);
+        if (lane == ld) atomicAdd(&H[lv], (uint32_t)__popcll(eq));
+        if (v == lv) v = PV_NOH;
+        m &= ~eq;
+    }
+    if (v != PV_NOH) atomicAdd(&H[v], 1u);
+}
+
+// Loop-invariant values of the Net pass, read from the parameter block once: inside the
+// record loop nothing waits on a scalar load (a scalar-load wait also drains the wave's
+// LDS operations).
+struct NetK {
+    const PV_G uint8_t *recs;
+    const PV_G uint32_t *offs;
+    uint64_t n, rec_bytes, gbase;
+    PV_G uint64_t *sum;
+    PV_G int64_t *cpc;
+    PV_G uint64_t *iplog;
+    PV_G uint64_t *dq;
+    PV_G uint32_t *flags;
+    uint32_t n_shift, skip_before, slot0, net_groups, dbg;
+};
+__device__ __forceinline__ void ksum_add(const NetK &K, uint32_t slot, uint32_t word, uint64_t w)
+{
+    __hip_atomic_fetch_add(K.sum + (uint64_t)slot * PV_SUM_WORDS + word, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void kcpc_min(const NetK &K, uint32_t slot, uint32_t sketch, uint32_t coupon, uint64_t i)
+{
+    __hip_atomic_fetch_min(K.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)sketch * PV_CPC_COUPONS + coupon,
+                           (int64_t)(K.gbase + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#define PV_KFLUSH1(s, word, v, on)                                                      \
+    {                                                                                   \
+        const uint32_t t_ = wave_sum(v);                                                \
+        if ((threadIdx.x & 63) == 0 && t_ && (on)) ksum_add(K, s, word, t_);            \
+    }
+__device__ void knet_flush(const NetK &K, uint32_t s, NetCtr &c)
+{
+    const bool nc = K.net_groups & PV_NET_COUNTERS_BIT;
+    PV_KFLUSH1(s, PV_OFF_NET + NC_EVENTS, c.nev, true) PV_KFLUSH1(s, PV_OFF_NET + NC_SAMPLES, c.nev, true)
+    PV_KFLUSH1(s, PV_OFF_NET + NC_TOTAL, c.nev, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_IN, c.nin, nc)
+    PV_KFLUSH1(s, PV_OFF_NET + NC_OUT, c.nout, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_UNK, c.nunk, nc)
+    PV_KFLUSH1(s, PV_OFF_NET + NC_V4, c.n4, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_V6, c.n6, nc)
+    PV_KFLUSH1(s, PV_OFF_NET + NC_UDP, c.nudp, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_TCP, c.ntcp, nc)
+    PV_KFLUSH1(s, PV_OFF_NET + NC_SYN, c.nsyn, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_OTHER, c.noth, nc)
+    c.zero();
+}
+
+// Dense IP log entry of one record for the top-N merge (0 = none):
+//   IPv4  slot<<60 | TM_IPV4<<56 | card<<33 | dir<<32 | address
+//   IPv6  slot<<60 | TM_IPV6<<56 | 55-bit address hash
+// IPv4 cardinality is applied by pv_topn_merge, once per distinct address and batch,
+// with the smallest record index; IPv6 cardinality (and cardinality without top IPs)
+// goes straight to the first-occurrence table here.
+// (NetworkMetricsBucket::process_net_layer :745-763)
+template <class A>
+__device__ __forceinline__ uint64_t net_ip_entry(const NetK &K, const A &R, const Parsed &o, uint64_t i, uint32_t slot)
+{
+    const bool card = K.net_groups & PV_NET_CARDINALITY_BIT, tops = K.net_groups & PV_NET_TOP_IPS_BIT;
+    if (o.dir == 2 || !(card || tops)) return 0;
+    uint64_t h1, h2;
+    if (o.has4) {
+        const uint32_t ip = R.u32(o.dir == 0 ? o.v4 + 12 : o.v4 + 16);
+        if (!ip) return 0;
+        if (tops)
+            return ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) | ((uint64_t)o.dir << 32) | ip;
+        murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+        kcpc_min(K, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), i);
+        return 0;
+    }
+    if (o.has6) {
+        const uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
+        const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
+        const uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
+        if (!(w0 | w1)) return 0;
+        murmur_16(w0, w1, h1, h2);
+        if (card) kcpc_min(K, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), i);
+        if (tops) return ((uint64_t)slot << 60) | PV_KEY(TM_IPV6, (h1 ^ (h2 << 1)) & ((1ull << 55) - 1));
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ Net pass staging
+// Every wave streams its own tiles into a private LDS ring with LDS-DMA
+// (global_load_lds: no VGPR holds data in flight) and keeps PV_NL_Q - 1 tiles in flight
+// while it parses one. Per tile it issues, in this order, two row loads of record offsets
+// (each lane's start and end) for the tile PV_NL_Q ahead and the tile's own DMA pieces;
+// every tile slot of the sequence is issued even past the range's end (a clamped copy),
+// so the count of DMA operations younger than any tile is fixed and the wave waits for it
+// with an exact vmcnt. The wave's other memory operations (stores, rare HBM reads) only
+// make such a wait wait for a little more.
+#ifndef PV_NL_Q
+#define PV_NL_Q 3 // ring slots per wave
+#endif
+#ifndef PV_NL_SLOT
+#define PV_NL_SLOT 5120 // bytes per slot: the packed span of a tile, or 80-B windows
+#endif
+#define PV_NL_NJ (PV_NL_SLOT / 1024)     // 1-KiB DMA pieces per tile
+#define PV_NL_OPS (PV_NL_NJ + 2)         // DMA operations per tile
+#define PV_NL_OROWS (PV_NL_Q + 1)        // offset-row pairs per wave
+static_assert(PV_NL_SLOT % 1024 == 0, "whole DMA pieces");
+static_assert(PV_NL_SLOT / PV_WT >= 80, "window must cover Eth + IPv4 + UDP from a 16-B aligned start");
+
+struct NetWave {
+    uint32_t slot[PV_NL_Q][PV_NL_SLOT / 4];
+    uint32_t lo[PV_NL_OROWS][PV_WT]; // each lane's record start
+    uint32_t hi[PV_NL_OROWS][PV_WT]; // each lane's record end (the next start)
+};
+struct NetState {
+    NetWave w[4];
+    uint32_t hist[PV_HBINS];
+    uint32_t nd; // DNS messages found
+};
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
+{
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const lds_u8 *)p);
+}
+// 64 lanes x 16 B from per-lane global addresses into LDS [m0 + lane * 16] (one 1-KiB piece)
+__device__ __forceinline__ void dma16(const void *gsrc, uint32_t lds)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+// 64 lanes x 4 B into LDS [m0 + lane * 4]
+__device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+#define PV_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
+
+// Slot accessor: packed (dword d of the span at L[d]) or the lane's window as the DMA
+// wrote it in 16-B pieces (dword d of lane l at L[(d >> 2) * 256 + l * 4 + (d & 3)]).
+// Bytes outside the staged range come from HBM.
+struct SAcc {
+    const uint8_t *R;
+    const uint32_t *L;
+    uint64_t gbase;
+    uint32_t lim, lane4, packed;
+    PV_FN uint32_t idx(uint32_t d) const { return packed ? d : ((d >> 2) << 8) + lane4 + (d & 3); }
+    PV_FN uint32_t u32(uint64_t off) const
+    {
+        const uint64_t rel = off - gbase;
+        if (rel < lim) {
+            const uint32_t r = (uint32_t)rel, d = r >> 2;
+            return __builtin_amdgcn_alignbyte(L[idx(d + 1)], L[idx(d)], r & 3);
+        }
+        return pv_ld32(R, off);
+    }
+    PV_FN uint32_t u8(uint64_t off) const
+    {
+        const uint64_t rel = off - gbase;
+        if (rel < lim) {
+            const uint32_t r = (uint32_t)rel;
+            return (L[idx(r >> 2)] >> ((r & 3) * 8)) & 0xff;
+        }
+        return R[off];
+    }
+};
+
+// Fast path of the per-record work: Ethernet II + IPv4 without options (and not
+// IP-in-IP), the frame shape parse_record's own fast path takes. The record's first 64
+// bytes are read from the slot into registers with independent LDS reads (one wait),
+// and every field the Net pass needs is taken from them at a fixed offset; the results
+// equal parse_record's, flowkey's and the accessor reads' on the same bytes.
+struct RecW {
+    uint32_t w[16]; // dwords at record offsets 0, 4, ..., 60
+    PV_FN uint32_t at(int off) const // little-endian u32 at a constant record offset
+    {
+        return (off & 3) ? __builtin_amdgcn_alignbyte(w[(off >> 2) + 1], w[off >> 2], off & 3) : w[off >> 2];
+    }
+};
+__device__ __forceinline__ void recw_load(const uint32_t *L, uint32_t d0, uint32_t sh, bool packed, uint32_t lane4, RecW &r)
+{
+    uint32_t x[17];
+#pragma unroll
+    for (int j = 0; j < 17; j++) {
+        const uint32_t d = d0 + j;
+        x[j] = L[packed ? d : ((d >> 2) << 8) + lane4 + (d & 3)];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+}
+// parse_record's fast path from the words (o as parse_record sets it); false: not this shape
+__device__ __forceinline__ bool fast_parse(const RecW &r, const ParseCfg &C, PV_CREF(PvParams) P, uint64_t rec, Parsed &o)
+{
+    o.caplen = r.w[2];
+    o.sec = r.w[0];
+    o.nsec = C.ts_nano ? (int32_t)r.w[1] : (int32_t)(r.w[1] * 1000u);
+    o.frame = rec + 16;
+    o.l3 = o.l4 = 0; o.has4 = o.has6 = 0; o.syn = 0; o.dir = 2;
+    o.v4 = o.v6 = o.l4off = 0; o.l4len = 0;
+    const uint32_t w3 = r.w[7], w4 = r.w[8], w5 = r.w[9];
+    const uint32_t proto = w5 >> 24;
+    if (!(C.linktype == 1 && o.caplen >= 34 && (w3 & 0xffffffu) == 0x450008u && proto != 4 && proto != 41)) return false;
+    const uint32_t total = ((w4 & 0xff) << 8) | ((w4 >> 8) & 0xff);
+    const uint32_t frag = ((w5 & 0xff) << 8) | ((w5 >> 8) & 0xff);
+    uint32_t len = o.caplen - 14;
+    if (total < len && total != 0) len = total;
+    o.has4 = 1; o.l3 = 4; o.v4 = o.frame + 14;
+    if (len > 20 && !(frag & 0x3fff)) {
+        const uint64_t pl = o.frame + 34;
+        const uint32_t pll = len - 20;
+        if (proto == 17 && pll >= 8) { o.l4 = 17; o.l4off = pl; o.l4len = pll; }
+        else if (proto == 6 && pll >= 20) {
+            o.l4 = 6; o.l4off = pl; o.l4len = pll;
+            o.syn = ((r.w[15] >> 24) & 2) ? 1 : 0; // TCP flags at record offset 63
+        }
+    }
+    if (match4(C, P.nets, r.at(46))) o.dir = 0;
+    else if (match4(C, P.nets, r.at(42))) o.dir = 1;
+    return true;
+}
+// hash5Tuple of a fast-path record (flowkey on the same bytes)
+__device__ __forceinline__ uint32_t fast_flowkey(const RecW &r)
+{
+    const uint32_t pw = r.at(50);
+    const uint32_t ps = pw & 0xffff, pd = pw >> 16;
+    int sp = pd < ps ? 1 : 0;
+    uint32_t h = 0x811C9DC5u;
+    const uint32_t p0 = sp ? pd : ps, p1 = sp ? ps : pd;
+    h = fnv_bytes(h, p0, 2);
+    h = fnv_bytes(h, p1, 2);
+    const uint32_t sa = r.at(42), da = r.at(46);
+    if (ps == pd && da < sa) sp = 1;
+    h = fnv_bytes(h, sp ? da : sa, 4);
+    h = fnv_bytes(h, sp ? sa : da, 4);
+    return fnv_bytes(h, r.w[9] >> 24, 1);
+}
+
 } // namespace
 
 // ------------------------------------------------------------------ the Net pass
-// One lane per record. Each wave owns 64-record tiles of its workgroup's contiguous
-// record range (tiles w, w+4, ...), stages a tile in its own LDS area and parses it
-// while the next tile's loads are in flight; waves never wait on each other. DNS
-// messages are appended to the workgroup's DNS work list for the DNS pass.
-extern "C" __global__ void __launch_bounds__(256, PV_WPE) pv_net_kernel(const PvParams *__restrict__ Pp)
+// One lane per record; workgroup b owns the contiguous tile range [b*T, (b+1)*T) and its
+// wave w takes the range's tiles w, w+4, ... (staging above). Counters stay in registers,
+// payload sizes go to an LDS histogram, the IP of each record to the dense IP log
+// (coalesced stores) and DNS messages to the workgroup's DNS work list. No table lookups
+// and no atomics with a return on the per-record path.
+extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ NetState S;
-    S.C.clear();
-    if (threadIdx.x == 0) { S.mq_n = 0; S.nd = 0; }
-    __syncthreads();
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t *L = S.stage[wave];
-    const uint64_t nwt = (P.n + PV_WT - 1) / PV_WT;
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
+    if (threadIdx.x == 0) S.nd = 0;
+    __syncthreads();
+    NetK K;
+    K.recs = P.recs; K.offs = P.offs; K.n = P.n; K.rec_bytes = P.rec_bytes; K.gbase = P.gbase;
+    K.sum = P.sum; K.cpc = P.cpc; K.iplog = P.iplog; K.dq = P.dq; K.flags = P.flags;
+    K.n_shift = P.n_shift; K.skip_before = P.skip_before; K.slot0 = P.slot_of[0];
+    K.net_groups = P.net_groups; K.dbg = P.dbg;
+    const ParseCfg C = parse_cfg(P);
+    const uint64_t n = K.n, last = n - 1;
+    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
     const uint64_t wbeg = (uint64_t)blockIdx.x * P.wt_per_block;
     const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+    // this wave's tiles: t(k) = wbeg + wave + 4k, k < ntl
+    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + 3) / 4) : 0u;
     const uint64_t dq_base = wbeg * PV_WT; // this workgroup's DNS work-list region
-    auto tile_off = [&](uint64_t t) -> uint64_t { return t * PV_WT < P.n ? (uint64_t)P.offs[t * PV_WT] : P.rec_bytes; };
-    auto lane_off = [&](uint64_t t) -> uint64_t {
-        const uint64_t r = t * PV_WT + lane;
-        return (t < wend && r < P.n) ? (uint64_t)P.offs[r] : 0;
+    NetWave &NW = S.w[wave];
+    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + 4ull * min(k, ntl - 1); };
+    // offset rows of tile k (clamped), then its DMA pieces into slot k % Q
+    auto issue_rows = [&](uint32_t k) {
+        const uint64_t r = tile_of(k) * PV_WT + lane;
+        const uint32_t row = k % PV_NL_OROWS;
+        dma4(K.offs + min<uint64_t>(r, last), lds_addr(&NW.lo[row][0]));
+        dma4(K.offs + min<uint64_t>(r + 1, last), lds_addr(&NW.hi[row][0]));
     };
+    auto issue_tile = [&](uint32_t k) {
+        const uint32_t row = k % PV_NL_OROWS;
+        const uint64_t t = tile_of(k);
+        const uint32_t o = NW.lo[row][lane];
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
+        const uint32_t b1 = t * PV_WT + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row][63]);
+        const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
+        const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
+        const uint32_t dst = lds_addr(&NW.slot[k % PV_NL_Q][0]);
+#pragma unroll
+        for (int j = 0; j < PV_NL_NJ; j++) {
+            const uint32_t ch = (uint32_t)(j * 64) + lane;
+            const uint32_t src = packed ? base + min(ch, nch - 1) * 16 : (o & ~15u) + 16u * j;
+            dma16(K.recs + src, dst + j * 1024);
+        }
+    };
+    auto period = [&](uint64_t r) -> uint32_t { return K.n_shift ? period_of(P, r) : 0u; };
+    auto slot_of = [&](uint32_t p) -> uint32_t { return K.n_shift ? P.slot_of[p] : K.slot0; };
+    // the LDS histogram belongs to the slot of the workgroup's first record
+    const uint32_t hslot = slot_of(period(min<uint64_t>(wbeg * PV_WT, last)));
+    const bool tops = K.net_groups & PV_NET_TOP_IPS_BIT;
     NetCtr c;
     c.zero();
     uint32_t wslot = 0xffffffffu;
-    WaveStage W;
-    // ring: this tile's lane offset; next tile's bounds and lane offsets
-    uint64_t t = wbeg + wave;
-    uint64_t off_cur = 0, off_n = 0, b_n0 = 0, b_n1 = 0;
-    if (t < wend) {
-        off_cur = lane_off(t);
-        W.issue(P.recs, tile_off(t), tile_off(t + 1), off_cur, t * PV_WT + lane < P.n, lane);
-        b_n0 = tile_off(t + 4);
-        b_n1 = tile_off(t + 5);
-        off_n = lane_off(t + 4);
+    if (ntl) {
+        // prologue: the sequence's first Q - 1 steps ([rows k + 1][tile k])
+        issue_rows(0);
+        PV_VMCNT(0);
+        for (uint32_t k = 0; k + 1 < PV_NL_Q; k++) {
+            issue_rows(k + 1);
+            if (k) PV_VMCNT(PV_NL_NJ + 2); // rows k landed (behind tile k - 1 and rows k + 1)
+            issue_tile(k);
+        }
     }
     STAMP_DECL
-    for (; t < wend; t += 4) {
-        t = uni64(t);
+    for (uint32_t k = 0; k < ntl; k++) {
+        // step: rows k + Q, then tile k + Q - 1 (its rows came one step earlier)
+        issue_rows(k + PV_NL_Q);
+        PV_VMCNT(PV_NL_NJ + 2);
+        issue_tile(k + PV_NL_Q - 1);
+        PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed
+        STAMP(1)
+        const uint32_t sl = k % PV_NL_Q, row = k % PV_NL_OROWS;
+        const uint64_t t = tile_of(k);
         const uint64_t r0 = t * PV_WT;
-        const uint64_t r1 = min<uint64_t>(r0 + PV_WT, P.n) - 1;
-        const uint32_t p_lo = period_of(P, r0), p_hi = period_of(P, r1);
+        const uint64_t r1 = min<uint64_t>(r0 + PV_WT, n) - 1;
+        const uint32_t p_lo = period(r0), p_hi = period(r1);
         const bool straddle = p_lo != p_hi; // pv_boundary_kernel's tile
-        const bool upd = !straddle && p_lo >= P.skip_before;
-        const uint32_t slot = P.slot_of[p_lo];
+        const bool upd = !straddle && p_lo >= K.skip_before;
+        const uint32_t slot = slot_of(p_lo);
         if (upd && slot != wslot) {
-            if (wslot != 0xffffffffu) net_flush(P, wslot, c);
+            if (wslot != 0xffffffffu) knet_flush(K, wslot, c);
             wslot = slot;
         }
-        STAMP(0)
         const uint64_t i = r0 + lane;
         const bool active = i <= r1 && !straddle;
-        const uint64_t off = off_cur;
-        const uint32_t chunks = __builtin_amdgcn_readfirstlane(W.chunks);
-        const uint64_t base = uni64(W.base);
-        W.commit(L, lane);
-        STAMP(1)
-        if (t + 4 < wend) {
-            W.issue(P.recs, uni64(b_n0), uni64(b_n1), off_n, t * PV_WT + 4 * PV_WT + lane < P.n, lane);
-            off_cur = off_n;
-            b_n0 = tile_off(t + 8);
-            b_n1 = tile_off(t + 9);
-            off_n = lane_off(t + 8);
-        }
-        STAMP(3)
-        if (active && !(P.dbg & 1)) {
-            const TAcc R = chunks ? TAcc{P.recs, L, base, chunks * 16 - 4, 1u, 0u}
-                                  : TAcc{P.recs, L, off & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
+        const uint64_t off = NW.lo[row][lane];
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
+        const uint32_t b1 = r0 + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row][63]);
+        const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
+        const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
+        uint32_t hv = PV_NOH;
+        uint64_t ek = 0;
+        DnsMsgW dm{};
+        bool isdns = false;
+        if (active && !(K.dbg & 1)) {
+            const SAcc R = packed ? SAcc{K.recs, NW.slot[sl], base, nch * 16 - 4, 0u, 1u}
+                                  : SAcc{K.recs, NW.slot[sl], off & ~15ull, PV_NL_SLOT / PV_WT - 4, lane * 4, 0u};
+            // fast path: the record's first 68 bytes are inside the staged range
+            const uint32_t rel = (uint32_t)(off - R.gbase);
+            RecW rw;
+            bool fast = rel + 68 <= R.lim + 4;
             Parsed o;
-            parse_record(R, P, off, o);
+            if (fast) {
+                recw_load(R.L, rel >> 2, rel & 3, packed, lane * 4, rw);
+                fast = fast_parse(rw, C, P, off, o);
+            }
+            if (!fast) parse_record(R, C, P, off, o);
             STAMP(4)
-            if (P.dbg & 2) {
+            if (K.dbg & 2) {
                 c.add(o);
             } else {
                 if (upd) {
                     c.add(o);
                     uint32_t cl = o.caplen;
-                    if (cl > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); cl = 65535; }
-                    uint32_t first;
-                    if (!S.C.add(PV_LKEY(slot, LM_HIST, cl), 1, (uint32_t)i, first)) sum_add(P, slot, PV_OFF_PAYLOAD + cl, 1);
-                    net_ips(P, &S.C, &S.mq_n, R, o, i, slot);
+                    if (cl > 65535) { atomicOr(K.flags, PVF_BIG_CAPLEN); cl = 65535; }
+                    if (slot == hslot && cl < PV_HBINS) hv = cl;
+                    else ksum_add(K, slot, PV_OFF_PAYLOAD + cl, 1);
+                    if (fast) {
+                        // net_ip_entry on the words (IPv4 only)
+                        const bool card = K.net_groups & PV_NET_CARDINALITY_BIT;
+                        const uint32_t ip = o.dir == 0 ? rw.at(42) : rw.at(46);
+                        if (o.dir != 2 && ip && (card || tops)) {
+                            if (tops)
+                                ek = ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
+                                     ((uint64_t)o.dir << 32) | ip;
+                            else {
+                                uint64_t h1, h2;
+                                murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+                                kcpc_min(K, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), i);
+                            }
+                        }
+                    } else {
+                        ek = net_ip_entry(K, R, o, i, slot);
+                    }
                 }
-                if (o.l4 == 17 && !(P.dbg & 4)) {
-                    const uint32_t port = dns_port(R.u32(o.l4off));
+                if (o.l4 == 17 && !(K.dbg & 4)) {
+                    const uint32_t port = dns_port(fast ? rw.at(50) : R.u32(o.l4off));
                     if (port) {
-                        const DnsMsg d = dns_msg_of(P, R, o, i, port, p_lo, upd);
-                        const uint32_t q = atomicAdd(&S.nd, 1u);
-                        reinterpret_cast<PV_G DnsMsg *>(P.dq)[dq_base + q] = d;
+                        DnsMsg d = dns_msg_of(P, R, o, i, port, p_lo, upd, !fast);
+                        if (fast) d.fkey = fast_flowkey(rw);
+                        dm = msg_words(d);
+                        isdns = true;
                     }
                 }
             }
-        } else if (P.dbg & 1) {
+        } else if (K.dbg & 1) {
             c.nev += active;
         }
+        // all reads of slot sl are issued before the next step's DMA may overwrite it
+        asm volatile("" ::: "memory");
         STAMP(5)
+        if (!(K.dbg & 1)) {
+            hist_add(S.hist, hv, lane);
+            // DNS messages: wave-compacted into the workgroup's work list
+            const uint64_t m = __ballot(isdns);
+            if (m) {
+                uint32_t q = 0;
+                if (lane == 0) q = atomicAdd(&S.nd, (uint32_t)__popcll(m));
+                q = __builtin_amdgcn_readlane(q, 0);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (isdns) {
+                    PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(K.dq) + 2 * (dq_base + q + below);
+                    dd[0] = dm.a;
+                    dd[1] = dm.b;
+                }
+            }
+            if (tops && i <= r1) K.iplog[i] = ek;
+        }
+        STAMP(6)
     }
-    if (wslot != 0xffffffffu) net_flush(P, wslot, c);
+    PV_VMCNT(0); // the sequence's trailing copies land before the workgroup ends
+    if (wslot != 0xffffffffu) knet_flush(K, wslot, c);
     __syncthreads();
-    cache_flush(P, S.C, PV_NCACHE, &S.mq_n);
-    __syncthreads();
-    STAMP(7)
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
+        if (S.hist[b]) ksum_add(K, hslot, PV_OFF_PAYLOAD + b, S.hist[b]);
     STAMP_FLUSH
     if (threadIdx.x == 0) {
-        P.mq_cnt[blockIdx.x] = S.mq_n;
+        P.mq_cnt[blockIdx.x] = 0;
         P.dq_cnt[blockIdx.x] = S.nd;
     }
 }
@@ -858,26 +1150,131 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *
 // names pv_topn_names decodes. No update waits on an HBM round trip and no update
 // issues an HBM atomic (regions with only a few updates take the direct path).
 #define PV_RS (1u << PV_REGION_LOG2)
+// Visits j in [0, n) with this thread's stride-blockDim.x share, U loads in flight per
+// thread: the loops below are bound by load latency, not by their LDS work.
+template <int U, class Ld, class Body>
+__device__ __forceinline__ void batched(uint64_t n, Ld ld, Body body)
+{
+    for (uint64_t j0 = threadIdx.x; j0 < n; j0 += (uint64_t)U * blockDim.x) {
+        decltype(ld(0)) v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * blockDim.x;
+            if (j < n) v[u] = ld(j);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t j = j0 + (uint64_t)u * blockDim.x;
+            if (j < n) body(j, v[u]);
+        }
+    }
+}
+#define PV_E16(q) reinterpret_cast<const PV_G ulonglong2 *>(q)
 #define PV_MERGE_DIRECT 64 // regions with at most this many updates use global_add
+#define PV_W_IP4 (1u << 31)  // weight word of a combined IPv4 entry: flag | dir << 30 | card << 29 | count
+
+// CPC coupon of an IPv4 address (cpc_sketch update of the int32 address)
+__device__ __forceinline__ uint32_t ip4_coupon(uint32_t ip)
+{
+    uint64_t h1, h2;
+    murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+    return cpc_coupon(h1, h2);
+}
 
 __device__ __forceinline__ uint32_t log_region(PV_CREF(PvParams) P, uint64_t e0)
 {
     return tregion(P, tkey_hash(e0 & ((1ull << 60) - 1)));
 }
+// table key (slot bits kept) of a dense IP log entry: IPv4 drops the card / dir bits
+__device__ __forceinline__ uint64_t ip_tkey(uint64_t e)
+{
+    return PV_KEY_METRIC(e & ((1ull << 60) - 1)) == TM_IPV4 ? (e & (0xffull << 56)) | (e & 0xffffffffull) : e;
+}
+// record range of workgroup b (the Net pass mapping), clipped to the batch
+__device__ __forceinline__ void wg_records(PV_CREF(PvParams) P, uint32_t b, uint64_t &r0, uint64_t &r1)
+{
+    r0 = min<uint64_t>((uint64_t)b * P.wt_per_block * PV_WT, P.n);
+    r1 = min<uint64_t>(r0 + (uint64_t)P.wt_per_block * PV_WT, P.n);
+}
 
-extern "C" __global__ void __launch_bounds__(256) pv_topn_count(const PvParams *__restrict__ Pp)
+// Combine: one workgroup per Net/DNS workgroup range aggregates its update log and its
+// records' dense IP entries in an LDS table (key -> weight, smallest record index), so a
+// heavy hitter leaves one entry per range instead of one per packet; entries the table
+// cannot take pass through unchanged. The combined list goes to the workgroup's cb
+// region and its entries are counted per table region.
+#define PV_CB_N 4096
+#define PV_W_CNT ((1u << 29) - 1) // weight bits of a dense IPv4 entry
+struct CombState {
+    uint64_t key[PV_CB_N];
+    uint32_t cnt[PV_CB_N];
+    uint32_t rep[PV_CB_N];
+    uint32_t h[1u << PV_MAX_REGIONS_LOG2];
+    uint32_t nout;
+};
+// combined entry (e0 = slot | table key, e1 = weight word | rep << 32) of a cache key;
+// IPv4 cache keys are dense entries (card << 33 | dir << 32 | address)
+__device__ __forceinline__ void comb_out(PV_CREF(PvParams) P, CombState &S, uint64_t *out, uint64_t ck, uint32_t w,
+                                         uint32_t rep)
+{
+    uint64_t e0 = ck;
+    if (PV_KEY_METRIC(ck & ((1ull << 60) - 1)) == TM_IPV4) {
+        e0 = ip_tkey(ck);
+        w = PV_W_IP4 | ((uint32_t)(ck >> 32) & 1u) << 30 | ((uint32_t)(ck >> 33) & 1u) << 29 | (w & PV_W_CNT);
+    }
+    const uint32_t k = atomicAdd(&S.nout, 1u);
+    out[2 * (uint64_t)k] = e0;
+    out[2 * (uint64_t)k + 1] = (uint64_t)w | ((uint64_t)rep << 32);
+    atomicAdd(&S.h[log_region(P, e0)], 1u);
+}
+__device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, CombState &S, uint64_t *out, uint64_t ck, uint32_t w,
+                                         uint32_t rep)
+{
+    uint32_t pos = (uint32_t)(fmix64(ck) >> 20) & (PV_CB_N - 1);
+    for (int probe = 0; probe < 16; probe++) {
+        uint64_t cur = S.key[pos];
+        if (cur == 0) {
+            const uint64_t prev = atomicCAS((unsigned long long *)&S.key[pos], 0ull, (unsigned long long)ck);
+            cur = prev == 0 ? ck : prev;
+        }
+        if (cur == ck) {
+            atomicAdd(&S.cnt[pos], w);
+            atomicMin(&S.rep[pos], rep);
+            return;
+        }
+        pos = (pos + 1) & (PV_CB_N - 1);
+    }
+    comb_out(P, S, out, ck, w, rep);
+}
+
+extern "C" __global__ void __launch_bounds__(512) pv_topn_combine(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ uint32_t h[1u << PV_MAX_REGIONS_LOG2];
+    __shared__ CombState S;
     const uint32_t nreg = 1u << P.reg_log2;
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) h[r] = 0;
+    for (uint32_t j = threadIdx.x; j < PV_CB_N; j += blockDim.x) { S.key[j] = 0; S.cnt[j] = 0; S.rep[j] = 0xffffffffu; }
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) S.h[r] = 0;
+    if (threadIdx.x == 0) S.nout = 0;
     __syncthreads();
+    uint64_t *out = P.cb + (uint64_t)blockIdx.x * P.mq_cap * 2;
     const uint32_t cnt = P.mq_cnt[blockIdx.x];
     const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * P.mq_cap * 2;
-    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) atomicAdd(&h[log_region(P, q[2 * j])], 1u);
+    batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; },
+               [&](uint64_t, ulonglong2 e) { comb_add(P, S, out, e.x, (uint32_t)e.y, (uint32_t)(e.y >> 32)); });
+    if (P.net_groups & PV_NET_TOP_IPS_BIT) {
+        uint64_t a, z;
+        wg_records(P, blockIdx.x, a, z);
+        const PV_G uint64_t *ipl = P.iplog + a;
+        batched<8>(z - a, [&](uint64_t j) { return ipl[j]; }, [&](uint64_t j, uint64_t e) {
+            if (e) comb_add(P, S, out, e, 1u, (uint32_t)(a + j));
+        });
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < PV_CB_N; j += blockDim.x)
+        if (S.key[j]) comb_out(P, S, out, S.key[j], S.cnt[j], S.rep[j]);
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
-        if (h[r]) atomicAdd(&P.tp_cnt[r], h[r]);
+        if (S.h[r]) atomicAdd(&P.tp_cnt[r], S.h[r]);
+    if (threadIdx.x == 0) P.cb_cnt[blockIdx.x] = S.nout;
 }
 
 // exclusive scan of the region counts (one workgroup)
@@ -913,24 +1310,23 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_scatter(const PvParams
     const uint32_t nreg = 1u << P.reg_log2;
     for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) h[r] = 0;
     __syncthreads();
-    const uint32_t cnt = P.mq_cnt[blockIdx.x];
-    const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * P.mq_cap * 2;
-    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) atomicAdd(&h[log_region(P, q[2 * j])], 1u);
+    const uint32_t cnt = P.cb_cnt[blockIdx.x];
+    const PV_G uint64_t *q = P.cb + (uint64_t)blockIdx.x * P.mq_cap * 2;
+    batched<8>(cnt, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) { atomicAdd(&h[log_region(P, e0)], 1u); });
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
         if (h[r]) h[r] = atomicAdd(&P.tp_fill[r], h[r]);
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-        const uint64_t e0 = q[2 * j], e1 = q[2 * j + 1];
-        const uint32_t pos = atomicAdd(&h[log_region(P, e0)], 1u);
-        P.tp_buf[2 * (uint64_t)pos] = e0;
-        P.tp_buf[2 * (uint64_t)pos + 1] = e1;
-    }
+    batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
+        const uint32_t pos = atomicAdd(&h[log_region(P, e.x)], 1u);
+        reinterpret_cast<PV_G ulonglong2 *>(P.tp_buf)[pos] = e;
+    });
 }
 
 struct MergeState {
     uint64_t key[PV_RS];
     uint64_t cnt[PV_RS];
+    uint32_t mn[2][PV_RS]; // smallest record index of an IPv4 key per direction (CPC)
     uint32_t nidx[PV_RS]; // entries created in this batch: region index, source record
     uint32_t nrep[PV_RS];
     uint32_t nnew, slots, nbase;
@@ -945,8 +1341,17 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
     const PV_G uint64_t *q = P.tp_buf + 2 * (uint64_t)P.tp_off[r];
     if (n <= PV_MERGE_DIRECT) {
         for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            const uint64_t e0 = q[2 * j], e1 = q[2 * j + 1];
-            global_add(P, (uint32_t)(e0 >> 60), e0 & ((1ull << 60) - 1), (uint32_t)e1, (uint32_t)(e1 >> 32));
+            const ulonglong2 e = PV_E16(q)[j];
+            const uint64_t e0 = e.x, e1 = e.y;
+            const uint32_t s = (uint32_t)(e0 >> 60), w = (uint32_t)e1, rep = (uint32_t)(e1 >> 32);
+            const uint64_t key = e0 & ((1ull << 60) - 1);
+            if (w & PV_W_IP4) {
+                global_add(P, s, key, w & PV_W_CNT, rep);
+                if ((w >> 29) & 1)
+                    cpc_min(P, s, ((w >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
+            } else {
+                global_add(P, s, key, w, rep);
+            }
         }
         return;
     }
@@ -955,7 +1360,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
     const uint32_t rs = 1u << rsl;
     if (threadIdx.x == 0) S.slots = 0;
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) atomicOr(&S.slots, 1u << (uint32_t)(q[2 * j] >> 60));
+    batched<8>(n, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) { atomicOr(&S.slots, 1u << (uint32_t)(e0 >> 60)); });
     __syncthreads();
     uint32_t slots = S.slots;
     while (slots) {
@@ -965,13 +1370,15 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
             S.key[i] = P.tkeys[rbase + i];
             S.cnt[i] = P.tcnt[rbase + i];
+            S.mn[0][i] = 0xffffffffu;
+            S.mn[1][i] = 0xffffffffu;
         }
         if (threadIdx.x == 0) S.nnew = 0;
         __syncthreads();
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            const uint64_t e0 = q[2 * j];
-            if ((uint32_t)(e0 >> 60) != s) continue;
-            const uint64_t e1 = q[2 * j + 1];
+        batched<4>(n, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
+            const uint64_t e0 = e.x;
+            if ((uint32_t)(e0 >> 60) != s) return;
+            const uint64_t e1 = e.y;
             const uint64_t key = e0 & ((1ull << 60) - 1);
             uint32_t pos = (uint32_t)tkey_hash(key) & (rs - 1);
             bool done = false;
@@ -984,7 +1391,13 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                     cur = created ? key : prev;
                 }
                 if (cur == key) {
-                    atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)(uint32_t)e1);
+                    const uint32_t w = (uint32_t)e1;
+                    if (w & PV_W_IP4) {
+                        atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)(w & PV_W_CNT));
+                        if ((w >> 29) & 1) atomicMin(&S.mn[(w >> 30) & 1][pos], (uint32_t)(e1 >> 32));
+                    } else {
+                        atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)w);
+                    }
                     if (created && PV_KEY_METRIC(key) != TM_IPV4) {
                         const uint32_t k = atomicAdd(&S.nnew, 1u);
                         S.nidx[k] = pos;
@@ -996,11 +1409,15 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                 }
             }
             if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
-        }
+        });
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
             P.tkeys[rbase + i] = S.key[i];
             P.tcnt[rbase + i] = S.cnt[i];
+            // IPv4 cardinality: one first-occurrence update per address and direction
+            for (uint32_t d = 0; d < 2; d++)
+                if (S.mn[d][i] != 0xffffffffu)
+                    cpc_min(P, s, d ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)S.key[i]), (int64_t)(P.gbase + S.mn[d][i]));
         }
         const uint32_t nnew = S.nnew;
         if (threadIdx.x == 0 && nnew) S.nbase = atomicAdd(P.nn_cnt, nnew);

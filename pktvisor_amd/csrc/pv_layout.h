@@ -18,9 +18,10 @@
 // name arena partitions per slot: workgroup b allocates from partition b % PV_ARENA_PARTS,
 // so no bump pointer is shared by more than a few workgroups
 #define PV_ARENA_PARTS 64
-// per-workgroup top-N update log: at most 6 hashed top-N updates per record, plus one
+// per-workgroup top-N update log (and its region-sorted copy, which also holds the dense
+// IP entries): at most 7 top-N updates per record, plus one
 // LDS cache flush (<= PV_CACHE_MAX entries) per bucket slot the workgroup touches
-#define PV_MQ_PER_REC 6
+#define PV_MQ_PER_REC 7
 #define PV_CACHE_MAX 4096
 
 // group bits (same values as pv_net_group / pv_dns_group in include/pvgpu.h)
@@ -203,6 +204,10 @@ struct PvParams {
     PV_G uint32_t *nn_cnt;
     PV_G PvNewName *nn;
     uint32_t nn_cap;
+    PV_G uint64_t *iplog; // dense IP log: one entry per record of the batch (Net pass)
+    PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
+    PV_G uint64_t *cb;    // combined update lists, one region of mq_cap entries per workgroup
+    PV_G uint32_t *cb_cnt;
     uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane
     PV_G uint32_t *flags;
     PV_G uint32_t *dns_first; // per period: min record index of a DNS event in that period

@@ -134,13 +134,31 @@ struct Parsed {
     uint32_t l4len;    // IP-length-trimmed L4 layer length
 };
 
-PV_FN bool match4(PV_CREF(PvSubnets) s, uint32_t ip)
+// Parse configuration: the link type and the first two IPv4 host subnets held in
+// registers (the kernels build it once per thread); further subnets and IPv6 subnets
+// are read from the parameter block. A /0 subnet has mask 0, so the mask test alone
+// reproduces the reference's match-all rule.
+struct ParseCfg {
+    uint32_t linktype, ts_nano, n4;
+    uint32_t a0, m0, a1, m1;
+};
+PV_FN ParseCfg parse_cfg(PV_CREF(PvParams) P)
+{
+    ParseCfg c;
+    c.linktype = P.linktype;
+    c.ts_nano = P.ts_nano;
+    c.n4 = P.nets.n4;
+    c.a0 = P.nets.v4_addr[0]; c.m0 = c.n4 > 0 ? P.nets.v4_mask[0] : 0xffffffffu;
+    c.a1 = P.nets.v4_addr[1]; c.m1 = c.n4 > 1 ? P.nets.v4_mask[1] : 0xffffffffu;
+    return c;
+}
+PV_FN bool match4(const ParseCfg &c, PV_CREF(PvSubnets) s, uint32_t ip)
 {
     if (!ip) return false;
-    for (uint32_t i = 0; i < s.n4; i++) {
-        if (s.v4_all[i]) return true;
-        if (((ip ^ s.v4_addr[i]) & s.v4_mask[i]) == 0) return true;
-    }
+    if (c.n4 > 0 && ((ip ^ c.a0) & c.m0) == 0) return true;
+    if (c.n4 > 1 && ((ip ^ c.a1) & c.m1) == 0) return true;
+    for (uint32_t i = 2; i < c.n4; i++)
+        if (s.v4_all[i] || ((ip ^ s.v4_addr[i]) & s.v4_mask[i]) == 0) return true;
     return false;
 }
 template <class A>
@@ -161,18 +179,21 @@ PV_FN bool match6(PV_CREF(PvSubnets) s, const A &R, uint64_t a)
 }
 
 template <class A>
-PV_FN void parse_record(const A &R, PV_CREF(PvParams) P, uint64_t rec, Parsed &o)
+PV_FN void parse_dir(const A &R, const ParseCfg &C, PV_CREF(PvParams) P, Parsed &o);
+
+template <class A>
+PV_FN void parse_record(const A &R, const ParseCfg &C, PV_CREF(PvParams) P, uint64_t rec, Parsed &o)
 {
     uint32_t tsec = R.u32(rec), tfrac = R.u32(rec + 4);
     o.caplen = R.u32(rec + 8);
     o.sec = tsec;
-    o.nsec = P.ts_nano ? (int32_t)tfrac : (int32_t)(tfrac * 1000u);
+    o.nsec = C.ts_nano ? (int32_t)tfrac : (int32_t)(tfrac * 1000u);
     o.frame = rec + 16;
     o.l3 = o.l4 = 0; o.has4 = o.has6 = 0; o.syn = 0; o.dir = 2;
     o.v4 = o.v6 = o.l4off = 0; o.l4len = 0;
     // fast path: Ethernet II + IPv4 without options (the overwhelmingly common frame);
     // identical results to the general walk below, which handles everything else
-    if (P.linktype == 1 && o.caplen >= 34) {
+    if (C.linktype == 1 && o.caplen >= 34) {
         const uint32_t w3 = R.u32(o.frame + 12); // ethertype, version/IHL
         if ((w3 & 0xffffffu) == 0x450008u) {
             const uint32_t w4 = R.u32(o.frame + 16), w5 = R.u32(o.frame + 20);
@@ -192,8 +213,8 @@ PV_FN void parse_record(const A &R, PV_CREF(PvParams) P, uint64_t rec, Parsed &o
                         o.syn = (R.u8(pl + 13) & 2) ? 1 : 0;
                     }
                 }
-                if (match4(P.nets, R.u32(o.frame + 30))) o.dir = 0;
-                else if (match4(P.nets, R.u32(o.frame + 26))) o.dir = 1;
+                if (match4(C, P.nets, R.u32(o.frame + 30))) o.dir = 0;
+                else if (match4(C, P.nets, R.u32(o.frame + 26))) o.dir = 1;
                 return;
             }
         }
@@ -203,14 +224,14 @@ PV_FN void parse_record(const A &R, PV_CREF(PvParams) P, uint64_t rec, Parsed &o
     uint32_t kind = 0; // 4 or 6 once an IP header is located
     uint32_t et = 0;
     bool l2ok = false;
-    if (P.linktype == 1) {
+    if (C.linktype == 1) {
         if (len >= 14) {
             et = be16(R, cur + 12);
             if (et >= 0x600 && len > 14) { cur += 14; len -= 14; l2ok = true; }
         }
-    } else if (P.linktype == 113) {
+    } else if (C.linktype == 113) {
         if (len > 16) { et = be16(R, cur + 14); cur += 16; len -= 16; l2ok = true; }
-    } else if (P.linktype == 101 || P.linktype == 12 || P.linktype == 14 || P.linktype == 228 || P.linktype == 229) {
+    } else if (C.linktype == 101 || C.linktype == 12 || C.linktype == 14 || C.linktype == 228 || C.linktype == 229) {
         if (len >= 1) { uint32_t v = R.u8(cur) >> 4; kind = (v == 4 || v == 6) ? v : 0; }
     }
     if (l2ok) {
@@ -275,14 +296,25 @@ PV_FN void parse_record(const A &R, PV_CREF(PvParams) P, uint64_t rec, Parsed &o
         break;
     }
     o.l3 = o.has4 ? 4 : (o.has6 ? 6 : 0);
-    // direction (PcapInputStream.cpp:401-416)
+    parse_dir(R, C, P, o);
+}
+// direction (PcapInputStream.cpp:401-416) for the general walk
+template <class A>
+PV_FN void parse_dir(const A &R, const ParseCfg &C, PV_CREF(PvParams) P, Parsed &o)
+{
     if (o.has4) {
-        if (match4(P.nets, R.u32(o.v4 + 16))) o.dir = 0;
-        else if (match4(P.nets, R.u32(o.v4 + 12))) o.dir = 1;
+        if (match4(C, P.nets, R.u32(o.v4 + 16))) o.dir = 0;
+        else if (match4(C, P.nets, R.u32(o.v4 + 12))) o.dir = 1;
     } else if (o.has6) {
         if (match6(P.nets, R, o.v6 + 24)) o.dir = 0;
         else if (match6(P.nets, R, o.v6 + 8)) o.dir = 1;
     }
+}
+
+template <class A>
+PV_FN void parse_record(const A &R, PV_CREF(PvParams) P, uint64_t rec, Parsed &o)
+{
+    parse_record(R, parse_cfg(P), P, rec, o);
 }
 
 // PcapPlusPlus hash5Tuple(packet, directionUnique=false): FNV-1 32-bit.

@@ -14,4 +14,6 @@ timeout -k 10 300 $R -d $O/c3 -o k -- $B --config 3 > $O/c3.log 2>&1 &&
 timeout -k 10 300 $R -d $O/c4 -o k -- $B --config 4 --records 4000000 > $O/c4.log 2>&1
 rc=$?
 echo "chain exit $rc"
+# staging floor and parse floor of the Net pass (kernel_ms in the bench line)
+[ $rc -eq 0 ] && [ -n "$STAGES" ] && (export PV_DEBUG_STAGES=1; timeout -k 10 200 $B > $O/c2_stage.log 2>&1) && (export PV_DEBUG_STAGES=2; timeout -k 10 200 $B > $O/c2_parse.log 2>&1)
 exit $rc
