@@ -123,7 +123,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     Parsed o;
     const GAcc R{P.recs};
     parse_record(R, P, P.offs[rep], o);
-    const uint32_t part = blockIdx.x & (PV_ARENA_PARTS - 1);
+    const uint32_t part = (blockIdx.x * 7 + threadIdx.x / 64) & (PV_ARENA_PARTS - 1);
     const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
     unsigned long long *top = (unsigned long long *)&P.arena_top[slot * PV_ARENA_PARTS + part];
     uint8_t *arena = P.arena + (uint64_t)slot * P.arena_cap;
@@ -1367,15 +1367,16 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         const uint32_t s = __builtin_ctz(slots);
         slots &= slots - 1;
         const uint64_t rbase = ((uint64_t)s << P.tcap_log2) + ((uint64_t)r << rsl);
-        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
-            S.key[i] = P.tkeys[rbase + i];
-            S.cnt[i] = P.tcnt[rbase + i];
-            S.mn[0][i] = 0xffffffffu;
-            S.mn[1][i] = 0xffffffffu;
-        }
+        batched<4>(rs, [&](uint64_t i) { return make_ulonglong2(P.tkeys[rbase + i], P.tcnt[rbase + i]); },
+                   [&](uint64_t i, ulonglong2 kc) {
+                       S.key[i] = kc.x;
+                       S.cnt[i] = kc.y;
+                       S.mn[0][i] = 0xffffffffu;
+                       S.mn[1][i] = 0xffffffffu;
+                   });
         if (threadIdx.x == 0) S.nnew = 0;
         __syncthreads();
-        batched<4>(n, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
+        batched<8>(n, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
             const uint64_t e0 = e.x;
             if ((uint32_t)(e0 >> 60) != s) return;
             const uint64_t e1 = e.y;
