@@ -39,6 +39,7 @@ extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
+extern "C" __global__ void pv_fill_multi(PvFillList L);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
 extern "C" __global__ void pv_boundary_kernel(const PvParams *P);
 extern "C" __global__ void pv_topn_combine(const PvParams *P);
@@ -289,6 +290,9 @@ struct pv_ctx {
     std::vector<PvXValue> xvals_host;
     // merged top-N records from other ranks: slot -> key -> (count, name)
     std::map<uint32_t, std::map<uint64_t, std::pair<uint64_t, std::string>>> remote_topn;
+    // device fills not launched yet (launch_fill*; one pv_fill_multi per flush_fills)
+    PvFillList fills{};
+    uint64_t fills_max = 0;
     // kernel timing (pv_kernel_timing)
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     double kernel_ms = 0;
@@ -349,18 +353,32 @@ int parse_host_spec(pv_ctx *c, const char *spec)
     return 0;
 }
 
+// Device fills are queued and launched together by flush_fills (one kernel instead of
+// one per region); every path that launches kernels or reads device state flushes first.
+void flush_fills(pv_ctx *c)
+{
+    if (!c->fills.n) return;
+    hipSetDevice(c->device);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((c->fills_max + 255) / 256, 4096);
+    hipLaunchKernelGGL(pv_fill_multi, dim3(blocks), dim3(256), 0, c->stream, c->fills);
+    c->fills.n = 0;
+    c->fills_max = 0;
+}
+void queue_fill(pv_ctx *c, void *p, uint64_t n, uint64_t v, uint32_t w32)
+{
+    if (!n) return;
+    if (c->fills.n == PV_FILL_SEGS) flush_fills(c);
+    c->fills.s[c->fills.n++] = PvFillSeg{p, n, v, w32, 0};
+    c->fills_max = std::max(c->fills_max, n);
+}
 int launch_fill64(pv_ctx *c, uint64_t *p, uint64_t n, uint64_t v)
 {
-    if (!n) return 0;
-    uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(pv_fill_u64, dim3(blocks), dim3(256), 0, c->stream, p, n, v);
+    queue_fill(c, p, n, v, 0);
     return 0;
 }
 int launch_fill32(pv_ctx *c, uint32_t *p, uint64_t n, uint32_t v)
 {
-    if (!n) return 0;
-    uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(pv_fill_u32, dim3(blocks), dim3(256), 0, c->stream, p, n, v);
+    queue_fill(c, p, n, v, 1);
     return 0;
 }
 
@@ -418,6 +436,7 @@ struct TopRec {
 
 int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out)
 {
+    flush_fills(c);
     uint64_t tcap = 1ull << c->tcap_log2;
     std::vector<uint64_t> keys(tcap), cnt(tcap);
     std::vector<uint32_t> aux(tcap);
@@ -528,6 +547,7 @@ double cpc_estimate(const int64_t *t, bool merged)
 
 int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, const Window &win, HostBucket &b)
 {
+    flush_fills(c);
     b.sum.assign(PV_SUM_WORDS, 0);
     b.cpc.assign(PV_MIN_WORDS, PV_CPC_EMPTY);
     b.merged = merged;
@@ -1121,6 +1141,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         for (uint32_t j = 0; j < P.n_btiles; j++) seen |= P.btile[j] == t;
         if (!seen) P.btile[P.n_btiles++] = t;
     }
+    flush_fills(c);
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, &P, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
@@ -1267,6 +1288,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
 
 int pv_synchronize(pv_ctx *c)
 {
+    flush_fills(c);
     hipSetDevice(c->device);
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return c->hipfail(e, "synchronize");
@@ -1330,6 +1352,7 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
     int rc = sync_xvals(c);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(c->mu);
+    flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
     Json j;
     j.obj();
@@ -1357,6 +1380,7 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
 
 int pv_state_regions(pv_ctx *c, void **sum_ptr, size_t *sum_bytes, void **min_ptr, size_t *min_bytes)
 {
+    flush_fills(c);
     *sum_ptr = c->d_sum;
     *sum_bytes = (size_t)PV_SLOTS * PV_SUM_WORDS * 8;
     *min_ptr = c->d_cpc;
@@ -1367,6 +1391,7 @@ int pv_state_regions(pv_ctx *c, void **sum_ptr, size_t *sum_bytes, void **min_pt
 // record: u32 slot, u64 key, u64 count, u16 name_len, name bytes
 int pv_export_topn(pv_ctx *c, uint8_t **buf, size_t *bytes)
 {
+    flush_fills(c);
     std::vector<uint8_t> o;
     std::vector<uint32_t> live;
     for (auto s : c->net.slots) live.push_back(s);

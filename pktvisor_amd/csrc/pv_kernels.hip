@@ -1592,21 +1592,39 @@ extern "C" __global__ void __launch_bounds__(64) pv_boundary_kernel(const PvPara
 extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint32_t nblk)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ uint32_t base;
-    if (threadIdx.x == 0) {
-        uint32_t b = 0;
-        for (uint32_t j = 0; j < blockIdx.x; j++) b += P.blk_events[j];
-        base = b;
-        if (blockIdx.x == nblk - 1) P.n_events[0] = b + P.blk_events[blockIdx.x];
-    }
+    __shared__ uint32_t part[4];
+    // this block's base: the events of all earlier blocks, summed by the whole block
+    uint32_t b = 0;
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += blockDim.x) b += P.blk_events[j];
+    b = wave_sum(b);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = b;
     __syncthreads();
+    const uint32_t base = part[0] + part[1] + part[2] + part[3];
     const uint32_t cnt = P.blk_events[blockIdx.x];
+    if (threadIdx.x == 0 && blockIdx.x == nblk - 1) P.n_events[0] = base + cnt;
     const uint64_t region = (uint64_t)P.wt_per_block * PV_WT;
     const uint64_t src = blockIdx.x < P.grid_main ? (uint64_t)blockIdx.x * region
                                                   : (uint64_t)P.grid_main * region + (uint64_t)(blockIdx.x - P.grid_main) * PV_WT;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         P.skeys[base + j] = P.ekeys[src + j];
         P.svals[base + j] = (uint32_t)(src + j);
+    }
+}
+
+// Fills a list of device regions in one launch (bucket-slot clears and the per-batch
+// status reset), grid-stride over every segment.
+extern "C" __global__ void pv_fill_multi(PvFillList L)
+{
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint32_t k = 0; k < L.n; k++) {
+        const PvFillSeg &f = L.s[k];
+        if (f.w32) {
+            uint32_t *p = reinterpret_cast<uint32_t *>(f.p);
+            for (uint64_t i = g; i < f.n; i += gs) p[i] = (uint32_t)f.v;
+        } else {
+            uint64_t *p = reinterpret_cast<uint64_t *>(f.p);
+            for (uint64_t i = g; i < f.n; i += gs) p[i] = f.v;
+        }
     }
 }
 

@@ -214,6 +214,20 @@ struct PvParams {
     PV_G uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
 };
 
+// pv_fill_multi's segment list (kernel argument)
+#define PV_FILL_SEGS 24
+struct PvFillSeg {
+    void *p;
+    uint64_t n;
+    uint64_t v;
+    uint32_t w32; // 1: 32-bit words
+    uint32_t pad;
+};
+struct PvFillList {
+    PvFillSeg s[PV_FILL_SEGS];
+    uint32_t n;
+};
+
 struct PvXactParams {
     PvParams P;            // record access + top-N tables (slow transaction names)
     const PV_G PvXEvent *events;
