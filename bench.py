@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--net-groups", type=int, default=0, help="pv_net_group bits (0 = reference defaults)")
     ap.add_argument("--dns-groups", type=int, default=0, help="pv_dns_group bits (0 = reference defaults)")
     ap.add_argument("--read-ceiling", action="store_true", help="also time a plain read of the blob (HBM ceiling)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the host-memory path (record blob in host RAM -> index -> H2D -> kernels)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,11 +135,13 @@ def main():
                        "parallelism": f"dp{world} (contiguous record shards, RCCL all-reduce of live buckets)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profile(args.config, n),
-                         "kernel": "pv_net_dns_kernel", "kernel_ms": round(kernel_ms, 4),
+                         "kernel": "pv_net_kernel", "kernel_ms": round(kernel_ms, 4),
                          "bytes_per_launch": algo_bytes},
         }
         if args.read_ceiling:
             line["read_ceiling_gbs"] = read_ceiling(d_recs, used)
+        if args.e2e and world == 1:
+            line["e2e"] = end_to_end(h, buf[:used].tobytes(), n, max(2, args.steps // 4))
         if args.net_groups or args.dns_groups:
             line["groups"] = {"net": args.net_groups, "dns": args.dns_groups}
         if world == 1 and not args.no_cpu_baseline:
@@ -160,6 +164,22 @@ def read_ceiling(d_recs, used: int) -> float:
         v.sum()
     torch.cuda.synchronize()
     return round(used * 10 / (time.perf_counter() - t0) / 1e9, 1)
+
+
+def end_to_end(h, blob: bytes, n: int, steps: int) -> dict:
+    """Mpkt/s of the path that starts in host memory: pv_process_host on the record blob
+    (host indexing, H2D copy of records and offsets, the kernels, status read-back)."""
+    h.reset()
+    h.process_host(blob)
+    h.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        h.reset()
+        h.process_host(blob)
+        h.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(n / dt / 1e6, 2), "unit": "Mpkt/s", "ms_per_step": round(dt * 1e3, 3), "steps": steps,
+            "path": "record blob in pageable host RAM -> pv_index_records (host) -> H2D records+offsets -> kernels -> status D2H"}
 
 
 def traffic_from_profile(cfg: int, n: int):
