@@ -66,6 +66,7 @@ __device__ __forceinline__ uint32_t pv_ld32(const uint8_t *base, uint64_t off)
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
 }
 __device__ __forceinline__ uint32_t pv_clz64(uint64_t x) { return (uint32_t)__clzll((long long)x); }
+__device__ __forceinline__ uint32_t pv_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
 #define PV_FN __device__ __forceinline__
 // kernel parameters are read through the constant address space (scalar loads)
 #define PV_CREF(T) const PV_C T &
@@ -77,6 +78,7 @@ namespace {
 struct GAcc {
     const uint8_t *R;
     PV_FN uint32_t u32(uint64_t off) const { return pv_ld32(R, off); }
+    PV_FN uint32_t u32a(uint64_t off) const { return *reinterpret_cast<const uint32_t *>(R + off); }
     PV_FN uint32_t u8(uint64_t off) const { return R[off]; }
 };
 
@@ -103,6 +105,12 @@ struct TAcc {
             return __builtin_amdgcn_alignbyte(L[d + mul], L[d], r & 3);
         }
         return pv_ld32(R, off);
+    }
+    PV_FN uint32_t u32a(uint64_t off) const // off 4-aligned
+    {
+        uint64_t rel = off - gbase;
+        if (rel < lim) return L[(uint32_t)(rel >> 2) * mul + add];
+        return *reinterpret_cast<const uint32_t *>(R + off);
     }
     PV_FN uint32_t u8(uint64_t off) const
     {
@@ -142,7 +150,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     NameStats st;
     st.init();
     uint32_t nl = name_len_l1(R, m, len, 12);
-    if (nl > 0) name_emit(R, m, len, 12, st);
+    if (nl > 0) name_stats(R, m, len, 12, st);
     int start = 0;
     uint32_t n = nl > 0 ? st.n : 0;
     if (metric == TM_QNAME2 || metric == TM_QNAME3) {
@@ -453,6 +461,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     // top-N / dense update: cache, else log (hashed) or HBM atomic (dense); boundary: global table
     auto top = [&](uint32_t metric, uint64_t payload, uint32_t w) {
         const uint64_t key = PV_KEY(metric, payload);
+        if (P.dbg & 32) return; // profiling knob: no table updates
         if (cache) {
             uint32_t first;
             if (cache->add(PV_LKEY(slot, metric, payload), w, i, first)) return;
@@ -494,7 +503,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             if (d.has_query) {
                 NameStats st;
                 st.init();
-                if (d.name_len_enc > 0) name_emit(R, m, dlen, 12, st);
+                if (d.name_len_enc > 0 && !(P.dbg & 16)) name_stats(R, m, dlen, 12, st);
                 uint64_t h1, h2;
                 st.mm.finish(h1, h2);
                 if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT)) {
@@ -790,6 +799,12 @@ struct SAcc {
             return __builtin_amdgcn_alignbyte(L[idx(d + 1)], L[idx(d)], r & 3);
         }
         return pv_ld32(R, off);
+    }
+    PV_FN uint32_t u32a(uint64_t off) const // off 4-aligned
+    {
+        const uint64_t rel = off - gbase;
+        if (rel < lim) return L[idx((uint32_t)rel >> 2)];
+        return *reinterpret_cast<const uint32_t *>(R + off);
     }
     PV_FN uint32_t u8(uint64_t off) const
     {
@@ -1483,7 +1498,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 NameStats st;
                 st.init();
                 nl = name_len_l1(R, m, mlen, 12);
-                if (nl > 0) name_emit(R, m, mlen, 12, st);
+                if (nl > 0) name_stats(R, m, mlen, 12, st);
                 const uint32_t nch = nl > 0 ? st.n : 0;
                 if (metric == TM_QNAME2 || metric == TM_QNAME3) {
                     int q2, q3;

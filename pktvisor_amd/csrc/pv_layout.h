@@ -208,7 +208,8 @@ struct PvParams {
     PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
     PV_G uint64_t *cb;    // combined update lists, one region of mq_cap entries per workgroup
     PV_G uint32_t *cb_cnt;
-    uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane
+    uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane,
+                  // 16 no DNS name decode, 32 no DNS table updates
     PV_G uint32_t *flags;
     PV_G uint32_t *dns_first; // per period: min record index of a DNS event in that period
     PV_G uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]

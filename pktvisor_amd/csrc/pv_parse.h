@@ -6,8 +6,10 @@
 // oracle. The includer defines:
 //   PV_FN                      function qualifiers (__device__ __forceinline__ / inline)
 //   pv_clz64(x)                count leading zeros of a non-zero u64
+//   pv_alignbyte(hi, lo, s)    bytes s..s+3 of the little-endian pair (lo, hi), s < 4
 // Byte access goes through an accessor object A with
 //   A.u32(off)  little-endian u32 at any absolute byte offset of the record blob
+//   A.u32a(off) the same at a 4-aligned offset (one LDS / memory word)
 //   A.u8(off)   one byte
 // (the kernel uses an LDS window over each record's first bytes, falling back to
 // HBM; the CPU harness reads plain memory).
@@ -487,6 +489,115 @@ PV_FN void agg_domain(const NameStats &s, int &q2, int &q3, uint64_t &ph2, uint6
 PV_FN uint64_t suffix_hash(const NameStats &s, int start, uint64_t ph_start)
 {
     return s.ph - ph_start * powb(s.n - (uint32_t)start);
+}
+
+// ------------------------------------------------------------------ name fast path
+// A level-1 name made of plain labels (lengths 1..63, no pointer, no NUL and no '.'
+// byte inside a label, at most 8 inner dots, terminated inside the message within the
+// 255-byte limit) decodes, under name_emit's rules, to the wire bytes
+// [off + 1, off + 1 + n) with each inner length byte read as '.'. name_stats_fast
+// computes NameStats of that text four bytes at a time (SWAR lower-casing, dot
+// substitution from the label walk, murmur over 16-byte blocks, prefix hashes at the
+// last four dots taken from the running Horner values); it returns false, st untouched,
+// for every other name.
+PV_FN uint32_t lower4(uint32_t w)
+{
+    const uint32_t t = w & 0x7f7f7f7fu;
+    const uint32_t up = (t + 0x3f3f3f3fu) & ~(t + 0x25252525u) & ~w & 0x80808080u; // 'A' <= byte <= 'Z'
+    return w | (up >> 2);
+}
+PV_FN uint32_t nonzero4(uint32_t w) { return (((w & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w) & 0x80808080u; }
+PV_FN uint32_t nibble_bytes(uint32_t x) { return ((x * 0x00204081u) & 0x01010101u) * 0xffu; }
+
+template <class A>
+PV_FN bool name_stats_fast(const A &R, uint64_t m, uint32_t len, uint32_t off, NameStats &st)
+{
+    // label walk: inner dot positions of the decoded text, newest in the low byte (0xff = none)
+    uint32_t cur = off, enc = 0, nb = 0;
+    uint64_t bp = ~0ull;
+    if (cur + 1 > len) return false;
+    uint32_t wl = R.u8(m + cur);
+    while (wl != 0) {
+        if (wl > 63 || cur + wl + 1 > len || enc + wl > 255) return false;
+        if (enc) {
+            if (nb == 8) return false;
+            bp = (bp << 8) | (enc - 1);
+            nb++;
+        }
+        cur += wl + 1;
+        enc += wl + 1;
+        if (cur + 1 > len) return false;
+        wl = R.u8(m + cur);
+    }
+    const uint32_t n = enc ? enc - 1 : 0;
+    uint32_t t[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t b = (uint32_t)(bp >> (8 * k)) & 0xff;
+        t[k] = b == 0xff ? 0xffffffffu : b;
+    }
+    Murmur mm;
+    mm.init();
+    uint64_t ph = 0, hk[4] = {0, 0, 0, 0};
+    const uint64_t src = m + off + 1;
+    const uint64_t abase = src & ~3ull;
+    const uint32_t sh = (uint32_t)(src & 3);
+    uint32_t prev = R.u32a(abase);
+    bool bad = false;
+    for (uint32_t j = 0; j * 16 < n; j++) {
+        // inner dots inside this 16-byte block
+        uint32_t bm = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t rel = ((uint32_t)(bp >> (8 * k)) & 0xff) - 16 * j;
+            bm |= rel < 16 ? 1u << rel : 0u;
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t p = 16 * j + 4 * q;
+            const uint32_t nv = n > p + 4 ? 4u : n > p ? n - p : 0u;
+            const uint32_t vm = nv >= 4 ? 0xffffffffu : (1u << (8 * nv)) - 1u;
+            const uint32_t dm = nibble_bytes((bm >> (4 * q)) & 15);
+            const uint32_t nxt = R.u32a(abase + p + 4);
+            uint32_t x = lower4(pv_alignbyte(nxt, prev, sh));
+            prev = nxt;
+            const uint32_t ok = nonzero4(x) & nonzero4(x ^ 0x2e2e2e2eu);
+            bad |= ((~ok & 0x80808080u) & vm & ~dm) != 0;
+            x = ((x & ~dm) | (0x2e2e2e2eu & dm)) & vm;
+            w[q] = x;
+            // Horner over the valid bytes; a tracked dot takes the hash before its byte
+            uint64_t hv[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                hv[r] = ph;
+                if ((uint32_t)r < nv) ph = ph * PBASE + (((x >> (8 * r)) & 0xff) + 1);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t rel = t[k] - p;
+                if (rel < 4) hk[k] = rel == 0 ? hv[0] : rel == 1 ? hv[1] : rel == 2 ? hv[2] : hv[3];
+            }
+        }
+        mm.k1 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        mm.k2 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+        if (16 * j + 16 <= n) mm.block();
+    }
+    if (bad) return false;
+    mm.n = n;
+    st.mm = mm;
+    st.ph = ph;
+    st.n = n;
+    st.d0 = (int32_t)t[0]; st.d1 = (int32_t)t[1]; st.d2 = (int32_t)t[2]; st.d3 = (int32_t)t[3];
+    st.h0 = hk[0]; st.h1 = hk[1]; st.h2 = hk[2]; st.h3 = hk[3];
+    st.last_c = n ? lower(R.u8(src + n - 1)) : 0;
+    return true;
+}
+// NameStats of the first query name (name_emit's result, by the fast path where it applies)
+template <class A>
+PV_FN void name_stats(const A &R, uint64_t m, uint32_t len, uint32_t off, NameStats &st)
+{
+    if (!name_stats_fast(R, m, len, off, st)) name_emit(R, m, len, off, st);
 }
 
 struct CountEmit {
