@@ -43,8 +43,8 @@ def main():
     ap.add_argument("--net-groups", type=int, default=0, help="pv_net_group bits (0 = reference defaults)")
     ap.add_argument("--dns-groups", type=int, default=0, help="pv_dns_group bits (0 = reference defaults)")
     ap.add_argument("--read-ceiling", action="store_true", help="also time a plain read of the blob (HBM ceiling)")
-    ap.add_argument("--e2e", action="store_true",
-                    help="also time the host-memory path (record blob in host RAM -> index -> H2D -> kernels)")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false",
+                    help="skip timing the host-memory path (record blob in host RAM -> index -> H2D -> kernels)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,7 +141,7 @@ def main():
         if args.read_ceiling:
             line["read_ceiling_gbs"] = read_ceiling(d_recs, used)
         if args.e2e and world == 1:
-            line["e2e"] = end_to_end(h, buf[:used].tobytes(), n, max(2, args.steps // 4))
+            line["e2e"] = end_to_end(h, buf[:used], n, max(3, args.steps // 4))
         if args.net_groups or args.dns_groups:
             line["groups"] = {"net": args.net_groups, "dns": args.dns_groups}
         if world == 1 and not args.no_cpu_baseline:
@@ -166,20 +166,40 @@ def read_ceiling(d_recs, used: int) -> float:
     return round(used * 10 / (time.perf_counter() - t0) / 1e9, 1)
 
 
-def end_to_end(h, blob: bytes, n: int, steps: int) -> dict:
-    """Mpkt/s of the path that starts in host memory: pv_process_host on the record blob
-    (host indexing, H2D copy of records and offsets, the kernels, status read-back)."""
-    h.reset()
-    h.process_host(blob)
-    h.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        h.reset()
-        h.process_host(blob)
-        h.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    return {"value": round(n / dt / 1e6, 2), "unit": "Mpkt/s", "ms_per_step": round(dt * 1e3, 3), "steps": steps,
-            "path": "record blob in pageable host RAM -> pv_index_records (host) -> H2D records+offsets -> kernels -> status D2H"}
+def end_to_end(h, blob, n: int, steps: int) -> dict:
+    """Mpkt/s of the path that starts in host memory (pv_process_host: parallel copy into
+    pinned staging, parallel record index, H2D on a copy stream overlapping the previous
+    chunk's kernels, status read-back), from pageable memory and from a page-locked
+    (pv_host_register) buffer, with the host-side time split."""
+    import numpy as np
+    import pktvisor_amd as pa
+    lib = pa.load_library()
+    buf = np.frombuffer(blob, dtype=np.uint8).copy()
+    out = {"unit": "Mpkt/s", "steps": steps, "chunk_mb": int(os.environ.get("PV_INGEST_CHUNK_MB", "64")),
+           "path": "record blob in host RAM -> parallel index + (pageable only) copy to pinned -> H2D -> kernels"}
+    for mode in ("pageable", "registered"):
+        if mode == "registered" and lib.pv_host_register(buf.ctypes.data, buf.nbytes) != 0:
+            out[mode] = None
+            continue
+        try:
+            h.reset()
+            h.process_host(buf)
+            h.synchronize()
+            h.ingest_timing(reset=True)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                h.reset()
+                h.process_host(buf)
+                h.synchronize()
+            dt = (time.perf_counter() - t0) / steps
+            t = [round(x / steps, 3) for x in h.ingest_timing(reset=True)]
+            out[mode] = {"value": round(n / dt / 1e6, 2), "ms_per_step": round(dt * 1e3, 3),
+                         "copy_index_ms": t[0], "index_ms": t[1], "h2d_enqueue_ms": t[2], "device_ms": t[3]}
+        finally:
+            if mode == "registered":
+                lib.pv_host_unregister(buf.ctypes.data)
+    out["value"] = out["pageable"]["value"]
+    return out
 
 
 def traffic_from_profile(cfg: int, n: int):

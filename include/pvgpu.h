@@ -107,8 +107,24 @@ int pv_index_records(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32
 int pv_process_device(pv_ctx *ctx, const uint8_t *d_recs, const uint32_t *d_offsets, const pv_index_info *info,
                       const uint32_t *sec_change_idx, const uint32_t *sec_change_sec, void *stream);
 
-/* Process records in host memory: index, H2D (pinned staging), kernels. */
+/* pv_index_records with the walk split over nthreads host threads (0 = default:
+ * PV_HOST_THREADS, else the online CPUs up to 16); identical results. */
+int pv_index_records_mt(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32_t *offsets, uint64_t max_records,
+                        uint32_t *sec_change_idx, uint32_t *sec_change_sec, uint32_t max_changes, pv_index_info *info,
+                        uint32_t nthreads);
+
+/* Process records in host memory, pipelined over 64 MiB chunks (PV_INGEST_CHUNK_MB):
+ * parallel copy into pinned staging (skipped when recs is pinned, e.g. registered
+ * with pv_host_register), parallel record index, H2D on a copy stream overlapping
+ * the previous chunk's kernels. Returns when every record has been processed. */
 int pv_process_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes);
+/* Page-lock a host range so pv_process_host DMAs from it directly (hipHostRegister). */
+int pv_host_register(void *ptr, size_t bytes);
+int pv_host_unregister(void *ptr);
+/* Accumulated ms of the host-memory path: [0] copy into pinned staging + record index
+ * (pageable source), [1] record index (pinned source),
+ * [2] H2D enqueue, [3] device processing as seen by the calling thread. */
+int pv_ingest_timing(pv_ctx *ctx, double *ms4, int reset);
 
 int pv_set_start_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);
 int pv_set_end_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);

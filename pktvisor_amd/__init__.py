@@ -59,7 +59,8 @@ class pv_index_info(ctypes.Structure):
 EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_error", "pv_index_records",
            "pv_process_device", "pv_process_host", "pv_set_start_tstamp", "pv_set_end_tstamp", "pv_synchronize",
            "pv_reset", "pv_window_json", "pv_free", "pv_state_regions", "pv_set_global_base", "pv_export_topn",
-           "pv_merge_topn", "pv_kernel_timing", "pv_window_slots"]
+           "pv_merge_topn", "pv_kernel_timing", "pv_window_slots", "pv_index_records_mt", "pv_host_register",
+           "pv_host_unregister", "pv_ingest_timing"]
 
 _lib = None
 
@@ -84,7 +85,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_last_error.restype = ctypes.c_char_p
     lib.pv_index_records.argtypes = [P, ctypes.c_size_t, U32, P, U64, P, P, U32, ctypes.POINTER(pv_index_info)]
     lib.pv_process_device.argtypes = [P, P, P, ctypes.POINTER(pv_index_info), P, P, P]
+    lib.pv_index_records_mt.argtypes = [P, ctypes.c_size_t, U32, P, U64, P, P, U32, ctypes.POINTER(pv_index_info),
+                                        U32]
     lib.pv_process_host.argtypes = [P, P, ctypes.c_size_t]
+    lib.pv_host_register.argtypes = [P, ctypes.c_size_t]
+    lib.pv_host_unregister.argtypes = [P]
+    lib.pv_ingest_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
     lib.pv_set_start_tstamp.argtypes = [P, I64, I64]
     lib.pv_set_end_tstamp.argtypes = [P, I64, I64]
     lib.pv_synchronize.argtypes = [P]
@@ -131,7 +137,9 @@ def pcap_file_bytes(records: bytes, linktype: int = 1, ts_nano: int = 0) -> byte
 class RecordIndex:
     """Host-side index of a run of pcap records (offsets + second-change points)."""
 
-    def __init__(self, recs, ts_nano: int = 0, max_records: Optional[int] = None, max_changes: int = 1 << 20):
+    def __init__(self, recs, ts_nano: int = 0, max_records: Optional[int] = None, max_changes: int = 1 << 20,
+                 threads: int = 1):
+        """threads > 1: the parallel walk (pv_index_records_mt), identical results."""
         lib = load_library()
         buf = np.frombuffer(recs, dtype=np.uint8) if not isinstance(recs, np.ndarray) else recs
         if max_records is None:
@@ -140,9 +148,10 @@ class RecordIndex:
         self.sc_idx = np.empty(max_changes, dtype=np.uint32)
         self.sc_sec = np.empty(max_changes, dtype=np.uint32)
         self.info = pv_index_info()
-        rc = lib.pv_index_records(buf.ctypes.data, len(buf), ts_nano, self.offsets.ctypes.data, max_records,
-                                  self.sc_idx.ctypes.data, self.sc_sec.ctypes.data, max_changes,
-                                  ctypes.byref(self.info))
+        args = (buf.ctypes.data, len(buf), ts_nano, self.offsets.ctypes.data, max_records, self.sc_idx.ctypes.data,
+                self.sc_sec.ctypes.data, max_changes, ctypes.byref(self.info))
+        rc = lib.pv_index_records_mt(*args, threads) if threads != 1 else lib.pv_index_records(*args)
+        self.rc = rc
         if rc:
             raise PvError(f"pv_index_records failed ({rc})")
         self.offsets = self.offsets[: self.info.n_records]
@@ -183,9 +192,15 @@ class PvHandlers:
         except Exception:
             pass
 
-    def process_host(self, recs: bytes):
-        buf = np.frombuffer(recs, dtype=np.uint8)
-        self._check(self.lib.pv_process_host(self.ctx, buf.ctypes.data, len(buf)), "pv_process_host")
+    def process_host(self, recs):
+        buf = recs if isinstance(recs, np.ndarray) else np.frombuffer(recs, dtype=np.uint8)
+        self._check(self.lib.pv_process_host(self.ctx, buf.ctypes.data, buf.nbytes), "pv_process_host")
+
+    def ingest_timing(self, reset: bool = False):
+        """ms spent by pv_process_host: copy + index (pageable), index (pinned), H2D enqueue, device."""
+        v = (ctypes.c_double * 4)()
+        self.lib.pv_ingest_timing(self.ctx, v, int(reset))
+        return list(v)
 
     def process_device(self, d_recs: int, d_offs: int, index: RecordIndex, stream: Optional[int] = None):
         self._check(self.lib.pv_process_device(self.ctx, d_recs, d_offs, ctypes.byref(index.info),

@@ -32,7 +32,13 @@
 #include <unordered_map>
 #include <vector>
 
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <thread>
+
 #include "../../include/pvgpu.h"
+#include "pv_ingest.h"
 #include "pv_layout.h"
 
 extern "C" __global__ void pv_net_kernel(const PvParams *P);
@@ -49,6 +55,11 @@ extern "C" __global__ void pv_topn_merge(const PvParams *P);
 extern "C" __global__ void pv_topn_names(const PvParams *P);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
+extern "C" __global__ void pv_xact_carry(const PvXactParams *X);
+extern "C" __global__ void pv_xact_defer(const uint64_t *skeys, const uint32_t *svals, const PvXEvent *events, uint32_t n,
+                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at);
+extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, uint32_t n_pend,
+                                           uint32_t at);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
                                           uint32_t *vout, size_t n, hipStream_t s);
 
@@ -267,7 +278,14 @@ struct pv_ctx {
     size_t sort_tmp_bytes = 0;
     PvXValue *d_xvals = nullptr;
     PvXValid *d_valid = nullptr;
-    uint32_t *d_nvals = nullptr;  // [0] values appended since reset, [1] deferred slow candidates
+    uint32_t *d_nvals = nullptr;  // [0] values appended since reset, [1] deferred slow candidates, [2] carried queries
+    // DNS queries still open at the end of the last batch (double-buffered), in sort-key
+    // rank order; ranks of later records count from pend_base
+    PvXEvent *d_pend[2] = {nullptr, nullptr};
+    uint64_t *d_pkeys[2] = {nullptr, nullptr};
+    uint32_t pend_cur = 0;
+    uint64_t n_pend = 0, pend_cap = 0;
+    int64_t pend_base = -1;
     uint32_t gen[PV_SLOTS] = {0}; // bumped when a slot is recycled; values carry slot | gen << 8
     size_t xvals_synced = 0;
     float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
@@ -275,10 +293,21 @@ struct pv_ctx {
     PvParams *d_params = nullptr;      // kernel parameter blocks (device memory)
     PvXactParams *d_xparams = nullptr;
     uint64_t max_records = 0;
-    // host-path staging
-    uint8_t *d_recs = nullptr;
-    uint32_t *d_offs = nullptr;
-    size_t recs_cap = 0;
+    // host-memory ingest (pv_process_host): worker pool, copy stream and two staging
+    // slots (pinned host chunk + offsets, device chunk + offsets)
+    struct Stage {
+        uint8_t *h_recs = nullptr, *d_recs = nullptr;
+        uint32_t *h_offs = nullptr, *d_offs = nullptr;
+        hipEvent_t copied = nullptr;
+        std::vector<uint32_t> sci, scs;
+        pv_index_info info{};
+    };
+    std::unique_ptr<pvi::Pool> pool;
+    Stage stage[2];
+    size_t stage_bytes = 0;   // record bytes per chunk
+    uint64_t stage_recs = 0;  // records per chunk
+    hipStream_t copy_stream = nullptr;
+    double ingest_ms[4] = {0, 0, 0, 0}; // host copy, index, H2D issue, device processing (pv_ingest_timing)
     // window state
     SlotMeta meta[PV_SLOTS];
     bool slot_used[PV_SLOTS] = {false};
@@ -873,6 +902,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     // last may overhang the batch by < wt_per_block tiles), boundary workgroups 64 each
     // (the last workgroup's region may overhang the batch by < wt_per_block tiles)
     const uint64_t ev_cap = mr + mr / ((uint64_t)c->wg_per_cu * c->cus) + 64 * 64 + 16 * 256;
+    c->pend_cap = 2 * mr; // open queries carried between batches
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
         !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_cpc, (size_t)PV_SLOTS * PV_MIN_WORDS * 8)) ||
@@ -888,8 +918,14 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_dq_cnt, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_stamps, 65536 * 4 * 8 * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)mr * 8)) || !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)mr * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_svals, (size_t)mr * 4)) || !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)mr * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_pend[0], (size_t)(c->pend_cap + mr) * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_pend[1], (size_t)(c->pend_cap + mr) * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_pkeys[0], (size_t)(c->pend_cap + mr) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_pkeys[1], (size_t)(c->pend_cap + mr) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)(mr + c->pend_cap) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)(mr + c->pend_cap) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_svals, (size_t)(mr + c->pend_cap) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)(mr + c->pend_cap) * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
@@ -905,7 +941,8 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         return c->hipfail(e, "device allocation");
     }
     size_t tmp = 0;
-    pv_radix_sort_pairs(nullptr, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, (size_t)mr, c->stream);
+    pv_radix_sort_pairs(nullptr, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, (size_t)(mr + c->pend_cap),
+                        c->stream);
     c->sort_tmp_bytes = std::max<size_t>(tmp, 256);
     if (!hip_ok(e = hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes))) { *out = c; return c->hipfail(e, "sort scratch"); }
     *out = c;
@@ -919,8 +956,16 @@ void pv_destroy(pv_ctx *c)
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
                     c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
-                    c->d_recs, c->d_offs};
+                    c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
+                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1]};
     for (void *p : ptrs) if (p) hipFree(p);
+    for (auto &st : c->stage) {
+        if (st.h_recs) hipHostFree(st.h_recs);
+        if (st.h_offs) hipHostFree(st.h_offs);
+        if (st.copied) hipEventDestroy(st.copied);
+    }
+    if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+    c->pool.reset();
     if (c->ev_start) hipEventDestroy(c->ev_start);
     if (c->ev_stop) hipEventDestroy(c->ev_stop);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -940,6 +985,8 @@ int pv_reset(pv_ctx *c)
     c->xvals_synced = 0;
     c->from90 = c->to90 = 0.0f;
     c->remote_topn.clear();
+    c->n_pend = 0;
+    c->pend_base = -1;
     hipError_t e = hipMemsetAsync(c->d_nvals, 0, 16, c->stream);
     if (e != hipSuccess) return c->hipfail(e, "reset");
     return 0;
@@ -1080,6 +1127,11 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.svals = c->d_svals;
     P.n_events = c->d_status + ST_NEV; // [0] packed total, [1] responses (ST_NRESP)
     P.want_events = (c->dns_groups & PV_DNS_TRANSACTIONS) ? 1 : 0;
+    // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
+    if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
+    if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0xffffffffull)
+        return c->fail(PV_ECAPACITY, "open DNS queries carried over more than 2^32 records without a response");
+    P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
     P.flags = c->d_status + ST_FLAGS;
     P.dns_first = c->d_status + ST_DNS_ANY;
     P.dns_at_thresh = c->d_status + ST_DNS_AT;
@@ -1189,21 +1241,33 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
             fprintf(stderr, "\n");
         }
     }
-    uint32_t nev = status[ST_NEV];
+    const uint32_t nev_b = status[ST_NEV];
     const uint32_t nresp = status[ST_NRESP];
-    if (nresp == 0 && P.n_shift == 0) nev = 0; // nothing to pair, nothing to purge in this batch
-    // DNS handler shifts only at DNS events: they must coincide with the Net shifts
-    for (uint32_t k = 1; k <= P.n_shift; k++) {
-        bool later_dns = false;
-        for (uint32_t j = k; j <= P.n_shift; j++) later_dns |= status[ST_DNS_ANY + j] != 0;
-        (void)later_dns;
+    // TransactionManager state across batches: a batch with responses or a period shift
+    // pairs (sort + resolve) its events together with the queries carried in; a batch of
+    // queries only just appends them to the carried list
+    const bool dns_here = nev_b > 0;
+    bool pair = dns_here && (nresp > 0 || P.n_shift > 0);
+    if (dns_here && !pair && c->n_pend + nev_b > c->pend_cap) pair = true; // compact the carried list
+    if (dns_here && !pair) {
+        hipLaunchKernelGGL(pv_xact_defer, dim3((nev_b + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
+                           c->d_events, nev_b, c->d_pend[c->pend_cur], c->d_pkeys[c->pend_cur], (uint32_t)c->n_pend);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_defer");
+        c->n_pend += nev_b;
     }
-    if (nev > 0) {
+    if (pair) {
         // (DNS events exist in this batch) every Net shift must coincide with a DNS event second
         for (uint32_t k = 1; k <= P.n_shift; k++)
             if (!status[ST_DNS_AT + k])
                 return c->fail(PV_EUNSUPPORTED, "DNS period boundary differs from the Net boundary at second %lld",
                                (long long)thresh[k - 1]);
+        const uint32_t np_in = (uint32_t)c->n_pend;
+        if (np_in) {
+            hipLaunchKernelGGL(pv_xact_pend_in, dim3((np_in + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
+                               c->d_pkeys[c->pend_cur], np_in, nev_b);
+            if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_pend_in");
+        }
+        const uint32_t nev = nev_b + np_in;
         uint32_t threads = 256, blocks = (nev + threads - 1) / threads;
         size_t tmp = c->sort_tmp_bytes;
         if (!hip_ok(e = pv_radix_sort_pairs(c->d_sort_tmp, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
@@ -1229,10 +1293,17 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         X.vals_cap = (uint32_t)(c->max_records * 2);
         X.valid = c->d_valid;
         X.n_valid = c->d_nvals + 1;
-        if (!hip_ok(e = hipMemcpyAsync(c->d_xparams, &X, sizeof X, hipMemcpyHostToDevice, st)))
+        X.pend = c->d_pend[c->pend_cur];
+        X.pend_out = c->d_pend[c->pend_cur ^ 1];
+        X.pkeys_out = c->d_pkeys[c->pend_cur ^ 1];
+        X.n_pend_out = c->d_nvals + 2;
+        if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
+            !hip_ok(e = hipMemcpyAsync(c->d_xparams, &X, sizeof X, hipMemcpyHostToDevice, st)))
             return c->hipfail(e, "parameter upload");
         hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
+        hipLaunchKernelGGL(pv_xact_carry, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_carry");
         if (P.n_shift > 0 && (c->dns_groups & PV_DNS_QUANTILES)) {
             // on_period_shift: slow thresholds = p90 of the bucket that just closed
             // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
@@ -1264,6 +1335,22 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
             hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st);
             hipStreamSynchronize(st);
         }
+        uint32_t nv3[3] = {0, 0, 0};
+        if (!hip_ok(e = hipMemcpyAsync(nv3, c->d_nvals, 12, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "carried queries");
+        const uint32_t npo = nv3[2];
+        if (nv3[0] > c->max_records) {
+            // drain the device value buffer to the host copy: every batch then has the
+            // whole 2 x max_records capacity (at most two values per response)
+            if (int rc = sync_xvals(c)) return rc;
+            c->xvals_synced = 0;
+            if (!hip_ok(e = hipMemsetAsync(c->d_nvals, 0, 4, st))) return c->hipfail(e, "value buffer drain");
+        }
+        if (npo > c->pend_cap) return c->fail(PV_ECAPACITY, "%u open DNS queries exceed the carried-list capacity", npo);
+        c->n_pend = npo;
+        c->pend_cur ^= 1;
+        c->pend_base = (int64_t)(c->records_seen + n) - 1;
     }
 
     // ---- window bookkeeping (host mirror of _period_shift)
@@ -1274,7 +1361,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         c->net.slots.push_front(s);
         if (c->net.slots.size() > np) c->net.slots.pop_back();
         c->net.next_shift_sec = T + 60;
-        if (nev > 0) {
+        if (dns_here) {
             c->dns.slots.push_front(s);
             if (c->dns.slots.size() > np) c->dns.slots.pop_back();
             c->dns.next_shift_sec = T + 60;
@@ -1295,40 +1382,180 @@ int pv_synchronize(pv_ctx *c)
     return 0;
 }
 
+namespace {
+
+int ingest_setup(pv_ctx *c)
+{
+    if (c->copy_stream) return 0;
+    hipError_t e;
+    size_t chunk = 64ull << 20;
+    if (const char *v = getenv("PV_INGEST_CHUNK_MB")) chunk = std::max<size_t>(1, strtoull(v, nullptr, 10)) << 20;
+    c->stage_recs = std::min<uint64_t>(c->max_records, chunk / 16 + 1);
+    c->stage_bytes = chunk;
+    c->pool.reset(new pvi::Pool(pvi::default_threads()));
+    if (!hip_ok(e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) return c->hipfail(e, "copy stream");
+    for (auto &st : c->stage) {
+        if (!hip_ok(e = hipHostMalloc((void **)&st.h_recs, chunk + 256, hipHostMallocDefault)) ||
+            !hip_ok(e = hipHostMalloc((void **)&st.h_offs, c->stage_recs * 4, hipHostMallocDefault)) ||
+            !hip_ok(e = hipMalloc(&st.d_recs, chunk + 256)) || !hip_ok(e = hipMalloc(&st.d_offs, c->stage_recs * 4)) ||
+            !hip_ok(e = hipEventCreateWithFlags(&st.copied, hipEventDisableTiming)))
+            return c->hipfail(e, "ingest staging");
+        st.sci.resize(1 << 16);
+        st.scs.resize(1 << 16);
+    }
+    return 0;
+}
+
+bool host_pinned(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+} // namespace
+
+// Host-memory path, pipelined over chunks of the record blob: a producer thread stages
+// chunk k + 1 (parallel copy into pinned memory unless the caller's buffer is already
+// pinned, parallel record index, H2D on the copy stream) while the calling thread runs
+// chunk k's kernels. Results equal one pv_process_device per chunk, in order.
 int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
 {
     hipSetDevice(c->device);
-    uint64_t maxr = c->max_records;
-    std::vector<uint32_t> offs(maxr);
-    std::vector<uint32_t> sci(1 << 16), scs(1 << 16);
-    size_t pos = 0;
-    while (pos < bytes) {
-        pv_index_info info;
-        int rc = pv_index_records(recs + pos, bytes - pos, c->cfg.ts_nano, offs.data(), maxr, sci.data(), scs.data(),
-                                  (uint32_t)sci.size(), &info);
-        if (rc) return c->fail(rc, "record index failed");
-        if (info.n_records == 0) break;
-        size_t need = info.bytes_used + 256;
-        hipError_t e;
-        if (need > c->recs_cap) {
-            if (c->d_recs) hipFree(c->d_recs);
-            if (c->d_offs) hipFree(c->d_offs);
-            c->d_recs = nullptr; c->d_offs = nullptr;
-            if (!hip_ok(e = hipMalloc(&c->d_recs, need)) || !hip_ok(e = hipMalloc(&c->d_offs, maxr * 4)))
-                return c->hipfail(e, "staging allocation");
-            c->recs_cap = need;
+    if (int rc = ingest_setup(c)) return rc;
+    const bool pinned = host_pinned(recs);
+    std::mutex mu;
+    std::condition_variable cv;
+    int state[2] = {0, 0};        // 0 free, 1 ready
+    bool prod_done = false, abort = false;
+    uint64_t nchunks = 0;
+    int prod_rc = 0;
+    std::string prod_err;
+    auto producer = [&] {
+        size_t pos = 0;
+        uint64_t k = 0;
+        int rc = 0;
+        while (pos < bytes) {
+            pv_ctx::Stage &st = c->stage[k & 1];
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return state[k & 1] == 0 || abort; });
+                if (abort) break;
+            }
+            const size_t L = std::min(c->stage_bytes, bytes - pos);
+            const uint8_t *src = recs + pos;
+            auto t1 = std::chrono::steady_clock::now();
+            // pageable source: copied into pinned staging by the threads that index it
+            rc = pvi::index_records_parallel(*c->pool, src, L, c->cfg.ts_nano, st.h_offs, c->stage_recs, st.sci.data(),
+                                             st.scs.data(), (uint32_t)st.sci.size(), &st.info,
+                                             pinned ? nullptr : st.h_recs);
+            const uint8_t *base = pinned ? src : st.h_recs;
+            c->ingest_ms[pinned ? 1 : 0] += ms_since(t1);
+            if (rc) { prod_err = "record index failed"; break; }
+            if (st.info.n_records == 0) {
+                if (L == c->stage_bytes && pos + L < bytes) { rc = PV_ECAPACITY; prod_err = "record larger than the ingest chunk"; }
+                break;
+            }
+            // a chunk that is not the last ends at a ts_sec boundary when it spans more than
+            // one second, so a period shift and the DNS records of its first second reach
+            // the device in the same batch
+            if (pos + st.info.bytes_used < bytes && st.info.n_sec_changes > 1 &&
+                st.info.n_sec_changes <= st.sci.size()) {
+                const uint32_t last = st.sci[st.info.n_sec_changes - 1];
+                st.info.n_records = last;
+                st.info.bytes_used = st.h_offs[last];
+                st.info.n_sec_changes -= 1;
+                const uint32_t prev = st.h_offs[last - 1];
+                uint32_t h[2];
+                memcpy(h, base + prev, 8);
+                st.info.last_sec = h[0];
+                st.info.last_nsec = c->cfg.ts_nano ? (int64_t)h[1] : (int64_t)h[1] * 1000;
+            }
+            auto t2 = std::chrono::steady_clock::now();
+            const size_t used = st.info.bytes_used;
+            hipError_t e;
+            if (!hip_ok(e = hipMemcpyAsync(st.d_recs, base, used, hipMemcpyHostToDevice, c->copy_stream)) ||
+                !hip_ok(e = hipMemsetAsync(st.d_recs + used, 0, 256, c->copy_stream)) ||
+                !hip_ok(e = hipMemcpyAsync(st.d_offs, st.h_offs, st.info.n_records * 4, hipMemcpyHostToDevice,
+                                           c->copy_stream)) ||
+                !hip_ok(e = hipEventRecord(st.copied, c->copy_stream))) {
+                rc = PV_EHIP;
+                prod_err = std::string("H2D: ") + hipGetErrorString(e);
+                break;
+            }
+            c->ingest_ms[2] += ms_since(t2);
+            pos += used;
+            std::lock_guard<std::mutex> g(mu);
+            state[k & 1] = 1;
+            k++;
+            cv.notify_all();
         }
-        if (!hip_ok(e = hipMemcpyAsync(c->d_recs, recs + pos, info.bytes_used, hipMemcpyHostToDevice, c->stream)) ||
-            !hip_ok(e = hipMemsetAsync(c->d_recs + info.bytes_used, 0, 256, c->stream)) ||
-            !hip_ok(e = hipMemcpyAsync(c->d_offs, offs.data(), info.n_records * 4, hipMemcpyHostToDevice, c->stream)))
-            return c->hipfail(e, "H2D");
-        rc = pv_process_device(c, c->d_recs, c->d_offs, &info, sci.data(), scs.data(), nullptr);
-        if (rc) return rc;
-        rc = pv_synchronize(c);
-        if (rc) return rc;
-        pos += info.bytes_used;
+        std::lock_guard<std::mutex> g(mu);
+        prod_rc = rc;
+        prod_done = true;
+        nchunks = k;
+        cv.notify_all();
+    };
+    std::thread th(producer);
+    int rc = 0;
+    for (uint64_t k = 0;; k++) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return state[k & 1] == 1 || (prod_done && k >= nchunks); });
+            if (state[k & 1] != 1) break;
+        }
+        pv_ctx::Stage &st = c->stage[k & 1];
+        auto t0 = std::chrono::steady_clock::now();
+        hipError_t e = hipStreamWaitEvent(c->stream, st.copied, 0);
+        if (!hip_ok(e)) rc = c->hipfail(e, "stream wait");
+        if (!rc) rc = pv_process_device(c, st.d_recs, st.d_offs, &st.info, st.sci.data(), st.scs.data(), nullptr);
+        if (!rc) rc = pv_synchronize(c);
+        c->ingest_ms[3] += ms_since(t0);
+        std::lock_guard<std::mutex> g(mu);
+        state[k & 1] = 0;
+        if (rc) abort = true;
+        cv.notify_all();
+        if (rc) break;
     }
+    th.join();
+    hipStreamSynchronize(c->copy_stream);
+    if (rc) return rc;
+    if (prod_rc) return c->fail(prod_rc, "%s", prod_err.c_str());
     return 0;
+}
+
+int pv_ingest_timing(pv_ctx *c, double *ms4, int reset)
+{
+    for (int i = 0; i < 4; i++) ms4[i] = c->ingest_ms[i];
+    if (reset) for (double &v : c->ingest_ms) v = 0;
+    return 0;
+}
+
+int pv_host_register(void *p, size_t bytes)
+{
+    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? 0 : PV_EHIP;
+}
+
+int pv_host_unregister(void *p)
+{
+    return hipHostUnregister(p) == hipSuccess ? 0 : PV_EHIP;
+}
+
+int pv_index_records_mt(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32_t *offsets, uint64_t max_records,
+                        uint32_t *sc_idx, uint32_t *sc_sec, uint32_t max_changes, pv_index_info *info,
+                        uint32_t nthreads)
+{
+    pvi::Pool pool(nthreads ? nthreads : pvi::default_threads());
+    return pvi::index_records_parallel(pool, recs, bytes, ts_nano, offsets, max_records, sc_idx, sc_sec, max_changes,
+                                       info);
 }
 
 int pv_set_start_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)

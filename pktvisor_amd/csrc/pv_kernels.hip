@@ -554,7 +554,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         ev.period = (uint8_t)period;
         ev.pad = 0;
         P.events[e] = ev;
-        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | i;
+        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)(P.ekey_base + i);
     }
     if (period > 0 && (int64_t)dm.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
 }
@@ -1705,18 +1705,25 @@ __device__ void slow_check(PV_CREF(PvXactParams) X, uint32_t idx, uint32_t perio
 }
 } // namespace
 
+// event of a sorted position: this batch's events, or a query carried in from an earlier batch
+__device__ __forceinline__ PvXEvent xev(PV_CREF(PvXactParams) X, uint32_t p)
+{
+    const uint32_t v = X.svals[p];
+    return (v & PV_PEND_FLAG) ? X.pend[v & ~PV_PEND_FLAG] : X.events[v];
+}
+
 __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
 {
     PV_CREF(PvParams) P = X.P;
-    const PvXEvent e = X.events[X.svals[p]];
+    const PvXEvent e = xev(X, p);
     const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
     if (e.qr) {
         // predecessor on the same (flow, txid)
         int q = (int)p - 1;
         for (; q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h; q--)
-            if (X.events[X.svals[q]].key == e.key) break;
+            if (xev(X, q).key == e.key) break;
         if (q < 0 || (uint32_t)(X.skeys[q] >> 32) != h) return; // NotExist
-        const PvXEvent qe = X.events[X.svals[q]];
+        const PvXEvent qe = xev(X, q);
         if (qe.qr) return; // previous event was a response: erased => NotExist
         uint32_t kp = purge_period(P, X.ttl_s, qe.period, qe.sec);
         if (kp && kp <= e.period) return; // purged at a period shift before this response
@@ -1752,8 +1759,8 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         if (!kp) return;
         uint32_t q = p + 1;
         for (; q < X.n && (uint32_t)(X.skeys[q] >> 32) == h; q++)
-            if (X.events[X.svals[q]].key == e.key) break;
-        if (q < X.n && (uint32_t)(X.skeys[q] >> 32) == h && X.events[X.svals[q]].period < kp) return;
+            if (xev(X, q).key == e.key) break;
+        if (q < X.n && (uint32_t)(X.skeys[q] >> 32) == h && xev(X, q).period < kp) return;
         if (kp < P.skip_before) return;
         xctr(T, kp, XC_TIMEOUT);
     }
@@ -1789,6 +1796,44 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvX
         else atomicOr(X.P.flags, PVF_VALUES_FULL);
     }
     for (uint32_t j = threadIdx.x; j < T.nvalid; j += blockDim.x) X.valid[T.dbase + j] = T.valid[j];
+}
+
+// Queries still open after this batch (the latest event of their (flow, txid) is a query
+// not purged by a period shift here) move to the carried list for the next batch, as
+// period 0 with sort rank 0: TransactionManager's map surviving the batch edge.
+extern "C" __global__ void pv_xact_carry(const PvXactParams *__restrict__ Xp)
+{
+    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= X.n) return;
+    PvXEvent e = xev(X, p);
+    if (e.qr || purge_period(X.P, X.ttl_s, e.period, e.sec)) return;
+    const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
+    for (uint32_t q = p + 1; q < X.n && (uint32_t)(X.skeys[q] >> 32) == h; q++)
+        if (xev(X, q).key == e.key) return;
+    e.period = 0;
+    const uint32_t k = atomicAdd(X.n_pend_out, 1u);
+    X.pend_out[k] = e;
+    X.pkeys_out[k] = (uint64_t)h << 32;
+}
+// A batch with queries only and no period shift pairs nothing: its events join the
+// carried list unresolved, in rank order behind the earlier ones.
+extern "C" __global__ void pv_xact_defer(const uint64_t *skeys, const uint32_t *svals, const PvXEvent *events, uint32_t n,
+                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    pend[at + j] = events[svals[j]];
+    pkeys[at + j] = skeys[j];
+}
+// the carried list's keys behind this batch's compacted keys, values flagged
+extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, uint32_t n_pend,
+                                           uint32_t at)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_pend) return;
+    skeys[at + j] = pkeys[j];
+    svals[at + j] = PV_PEND_FLAG | j;
 }
 
 // top_slow for transactions of periods whose threshold became known after the resolve

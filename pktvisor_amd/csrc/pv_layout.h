@@ -183,6 +183,7 @@ struct PvParams {
     PV_G uint32_t *svals;      // packed event slot positions (sort input)
     PV_G uint32_t *n_events;   // [0] packed total (pv_xact_compact), [1] responses
     uint32_t want_events;
+    uint32_t ekey_base;        // sort rank of the batch's first record (open queries carried in have rank 0)
     uint32_t wt_per_block; // 64-record wave tiles per workgroup (contiguous record range)
     uint64_t rec_bytes; // bytes of the record run (end of the last record)
     PV_G uint64_t *mq;    // per-workgroup top-N update logs: mq_cap x {key | slot << 60, w | rep << 32}
@@ -245,4 +246,12 @@ struct PvXactParams {
     uint32_t vals_cap;
     PV_G PvXValid *valid;
     PV_G uint32_t *n_valid;
+    // DNS queries still open from earlier batches (TransactionManager's map carried across
+    // batches): sorted-key values with PV_PEND_FLAG index `pend`; pv_xact_carry writes the
+    // queries still open after this batch to pend_out / pkeys_out, counting n_pend_out
+    const PV_G PvXEvent *pend;
+    PV_G PvXEvent *pend_out;
+    PV_G uint64_t *pkeys_out;
+    PV_G uint32_t *n_pend_out;
 };
+#define PV_PEND_FLAG 0x80000000u

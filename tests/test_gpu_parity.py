@@ -83,3 +83,76 @@ def test_edge_mix_many_seeds(oracle, tmp_path):
 def test_large_c4_against_oracle(oracle, tmp_path):
     gpu, ref = run_both(oracle, synth.pcap_bytes(4, 1_000_000), synth.HOST_SPEC, 5, tmp_path)
     assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("periods", [1, 5])
+def test_chunked_ingest_parity(oracle, tmp_path, monkeypatch, periods):
+    """pv_process_host's pipeline over 1 MiB chunks (many chunks, a period shift and DNS
+    transactions straddling chunk edges) against the oracle's single pass."""
+    monkeypatch.setenv("PV_INGEST_CHUNK_MB", "1")
+    monkeypatch.setenv("PV_HOST_THREADS", "7")
+    gpu, ref = run_both(oracle, synth.pcap_bytes(4, 60000, ts_step_us=1500), synth.HOST_SPEC, periods, tmp_path)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_registered_host_buffer_same_result(tmp_path, monkeypatch):
+    """A page-locked source (pv_host_register: H2D straight from the caller's buffer)
+    gives the same windows as pageable staging."""
+    import numpy as np
+    monkeypatch.setenv("PV_INGEST_CHUNK_MB", "2")
+    recs = np.frombuffer(synth.pcap_bytes(4, 40000)[24:], dtype=np.uint8).copy()
+    out = []
+    for reg in (False, True):
+        h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=1, max_records=len(recs) // 16)
+        lib = pa.load_library()
+        if reg:
+            assert lib.pv_host_register(recs.ctypes.data, recs.nbytes) == 0
+        try:
+            h.process_host(recs)
+            out.append(h.window_json(0, merged=False))
+        finally:
+            if reg:
+                lib.pv_host_unregister(recs.ctypes.data)
+            h.close()
+    assert diff(out[1], out[0]) is None, diff(out[1], out[0])
+
+
+@pytest.mark.parametrize("cfg,n,step_us", [(1, 1000, 1), (4, 20000, 9000)])
+def test_many_small_batches_parity(oracle, cfg, n, step_us):
+    """The same capture submitted as many small batches (1..60 records each): DNS queries
+    carried across batch edges (query-only batches defer pairing, later batches pair them;
+    with 9 ms steps also TTL purges at period shifts) must give the single-pass result."""
+    import numpy as np
+    pcap = synth.pcap_bytes(cfg, n, ts_step_us=step_us)
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    offs = list(idx.offsets) + [len(recs)]
+    rng = np.random.default_rng(cfg)
+    # batch edges anywhere, except inside a second at which a period shifts (a window
+    # shift at S0 + 60 k; pv_process_host's chunks end at second boundaries for this)
+    o = np.asarray(idx.offsets, dtype=np.int64)
+    secs = np.frombuffer(recs, dtype=np.uint8)[o[:, None] + np.arange(4)].copy().view("<u4")[:, 0].astype(np.int64)
+
+    def bad(j):
+        return 0 < j < idx.n and secs[j] == secs[j - 1] and secs[j] != secs[0] and (secs[j] - secs[0]) % 60 == 0
+
+    for periods in (1, 5):
+        h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=periods, max_records=256)
+        try:
+            i = 0
+            while i < idx.n:
+                j = min(idx.n, i + int(rng.integers(1, 61)))
+                while bad(j) and j > i + 1:
+                    j -= 1
+                while bad(j):
+                    j += 1
+                assert j - i <= 256
+                h.process_host(recs[offs[i]:offs[j]])
+                i = j
+            h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+            key = f"{1 if periods == 1 else periods}m"
+            gpu = {key: h.window_json(0 if periods == 1 else periods, merged=periods != 1)}
+        finally:
+            h.close()
+        ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=periods, window=periods)
+        assert diff(gpu, ref) is None, (periods, diff(gpu, ref))
