@@ -125,6 +125,24 @@ int pv_host_unregister(void *ptr);
  * (pageable source), [1] record index (pinned source),
  * [2] H2D enqueue, [3] device processing as seen by the calling thread. */
 int pv_ingest_timing(pv_ctx *ctx, double *ms4, int reset);
+/* Multi-GPU shard edges (one context per rank, contiguous shards in rank order).
+ * pv_edge_export: this shard's DNS transaction stubs (queries open at its end, responses
+ * that are the first event of their (flow, txid) in it, its DNS period shifts).
+ * pv_edge_merge: given every rank's export (bufs[0..nranks)), pair this shard's stub
+ * responses with the queries the earlier shards leave open and count the timeouts of
+ * those queries at this shard's shifts, into this rank's buckets; call before the
+ * bucket all-reduce. Replaces the single-stream TransactionManager continuity
+ * (libs/visor_transaction/TransactionManager.h:51-106) across shard boundaries. */
+int pv_edge_export(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
+int pv_edge_merge(pv_ctx *ctx, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks, uint32_t my_rank);
+/* Quantile inputs of the live window, (slot, kind, value) records, for the merge of the
+ * dns_xact_* quantiles across ranks (DnsMetricsBucket::specialized_merge of the KLL
+ * sketches, src/handlers/dns/v1/DnsStreamHandler.cpp:692). */
+int pv_values_export(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
+int pv_values_merge(pv_ctx *ctx, const uint8_t *buf, size_t bytes);
+/* Live slots with their bucket start seconds, newest first (merge alignment check). */
+int pv_window_periods(pv_ctx *ctx, uint32_t *slots, int64_t *start_sec, uint32_t max_n, uint32_t *n);
+
 
 int pv_set_start_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);
 int pv_set_end_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);

@@ -60,7 +60,8 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_process_device", "pv_process_host", "pv_set_start_tstamp", "pv_set_end_tstamp", "pv_synchronize",
            "pv_reset", "pv_window_json", "pv_free", "pv_state_regions", "pv_set_global_base", "pv_export_topn",
            "pv_merge_topn", "pv_kernel_timing", "pv_window_slots", "pv_index_records_mt", "pv_host_register",
-           "pv_host_unregister", "pv_ingest_timing"]
+           "pv_host_unregister", "pv_ingest_timing", "pv_edge_export", "pv_edge_merge", "pv_values_export",
+           "pv_values_merge", "pv_window_periods"]
 
 _lib = None
 
@@ -106,6 +107,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_window_slots.argtypes = [P, P, U32, ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_size_t),
                                     ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_kernel_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.c_int]
+    lib.pv_edge_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_edge_merge.argtypes = [P, P, P, U32, U32]
+    lib.pv_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_values_merge.argtypes = [P, P, ctypes.c_size_t]
+    lib.pv_window_periods.argtypes = [P, P, P, U32, ctypes.POINTER(U32)]
     _lib = lib
     return lib
 
@@ -258,6 +264,43 @@ class PvHandlers:
     def merge_topn(self, data: bytes):
         buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
         self._check(self.lib.pv_merge_topn(self.ctx, buf.ctypes.data, len(data)), "pv_merge_topn")
+
+    def _export(self, fn, what) -> bytes:
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(fn(self.ctx, ctypes.byref(p), ctypes.byref(n)), what)
+        data = ctypes.string_at(p.value, n.value) if n.value else b""
+        self.lib.pv_free(p)
+        return data
+
+    def edge_export(self) -> bytes:
+        """shard-edge DNS transaction stubs of this shard (pv_edge_export)"""
+        return self._export(self.lib.pv_edge_export, "pv_edge_export")
+
+    def edge_merge(self, exports, rank: int):
+        """pair this shard's stub responses with queries the earlier shards leave open"""
+        bufs = [np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, dtype=np.uint8) for b in exports]
+        ptrs = (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+        sizes = (ctypes.c_size_t * len(bufs))(*[len(b) for b in exports])
+        self._check(self.lib.pv_edge_merge(self.ctx, ptrs, sizes, len(bufs), rank), "pv_edge_merge")
+
+    def values_export(self) -> bytes:
+        return self._export(self.lib.pv_values_export, "pv_values_export")
+
+    def values_merge(self, data: bytes):
+        buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
+        self._check(self.lib.pv_values_merge(self.ctx, buf.ctypes.data, len(data)), "pv_values_merge")
+
+    def window_periods(self):
+        """[(slot, bucket start second)] of the live windows, newest first"""
+        slots = np.zeros(32, dtype=np.uint32)
+        starts = np.zeros(32, dtype=np.int64)
+        n = ctypes.c_uint32()
+        self._check(self.lib.pv_window_periods(self.ctx, slots.ctypes.data, starts.ctypes.data, 32, ctypes.byref(n)),
+                    "pv_window_periods")
+        return [(int(a), int(b)) for a, b in zip(slots[: n.value], starts[: n.value])]
+
+    def set_start_tstamp(self, sec: int, nsec: int = 0):
+        self._check(self.lib.pv_set_start_tstamp(self.ctx, sec, nsec), "pv_set_start_tstamp")
 
 
 def last_record_ts(recs: bytes, index: RecordIndex, ts_nano: int = 0):

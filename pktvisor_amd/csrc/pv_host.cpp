@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <arpa/inet.h>
 #include <cmath>
 #include <cstdarg>
@@ -286,6 +287,10 @@ struct pv_ctx {
     uint32_t pend_cur = 0;
     uint64_t n_pend = 0, pend_cap = 0;
     int64_t pend_base = -1;
+    // shard-edge stubs (orphan responses) accumulated since reset, device counter in d_nvals[3]
+    PvXEvent *d_orph = nullptr;
+    uint32_t orph_cap = 0;
+    std::vector<std::pair<int64_t, uint32_t>> dns_shifts; // (threshold second, new slot) since reset
     uint32_t gen[PV_SLOTS] = {0}; // bumped when a slot is recycled; values carry slot | gen << 8
     size_t xvals_synced = 0;
     float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
@@ -903,6 +908,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     // (the last workgroup's region may overhang the batch by < wt_per_block tiles)
     const uint64_t ev_cap = mr + mr / ((uint64_t)c->wg_per_cu * c->cus) + 64 * 64 + 16 * 256;
     c->pend_cap = 2 * mr; // open queries carried between batches
+    c->orph_cap = (uint32_t)std::min<uint64_t>(2 * mr, 1u << 30);
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
         !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_cpc, (size_t)PV_SLOTS * PV_MIN_WORDS * 8)) ||
@@ -918,6 +924,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_dq_cnt, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_stamps, 65536 * 4 * 8 * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_orph, (size_t)c->orph_cap * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_pend[0], (size_t)(c->pend_cap + mr) * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_pend[1], (size_t)(c->pend_cap + mr) * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_pkeys[0], (size_t)(c->pend_cap + mr) * 8)) ||
@@ -957,7 +964,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
                     c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
-                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1]};
+                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph};
     for (void *p : ptrs) if (p) hipFree(p);
     for (auto &st : c->stage) {
         if (st.h_recs) hipHostFree(st.h_recs);
@@ -987,6 +994,7 @@ int pv_reset(pv_ctx *c)
     c->remote_topn.clear();
     c->n_pend = 0;
     c->pend_base = -1;
+    c->dns_shifts.clear();
     hipError_t e = hipMemsetAsync(c->d_nvals, 0, 16, c->stream);
     if (e != hipSuccess) return c->hipfail(e, "reset");
     return 0;
@@ -1297,6 +1305,9 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         X.pend_out = c->d_pend[c->pend_cur ^ 1];
         X.pkeys_out = c->d_pkeys[c->pend_cur ^ 1];
         X.n_pend_out = c->d_nvals + 2;
+        X.orph = c->d_orph;
+        X.n_orph = c->d_nvals + 3;
+        X.orph_cap = c->orph_cap;
         if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
             !hip_ok(e = hipMemcpyAsync(c->d_xparams, &X, sizeof X, hipMemcpyHostToDevice, st)))
             return c->hipfail(e, "parameter upload");
@@ -1362,6 +1373,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         if (c->net.slots.size() > np) c->net.slots.pop_back();
         c->net.next_shift_sec = T + 60;
         if (dns_here) {
+            c->dns_shifts.emplace_back(T, s);
             c->dns.slots.push_front(s);
             if (c->dns.slots.size() > np) c->dns.slots.pop_back();
             c->dns.next_shift_sec = T + 60;
@@ -1677,6 +1689,244 @@ int pv_kernel_timing(pv_ctx *c, double *total_ms, uint64_t *launches, int reset)
     *total_ms = c->kernel_ms;
     *launches = c->kernel_launches;
     if (reset) { c->kernel_ms = 0; c->kernel_launches = 0; }
+    return 0;
+}
+
+// ---- multi-GPU shard edges: DNS transactions across contiguous shards.
+// Each rank exports its shard-edge stubs: the queries still open at the end of its
+// stream (latest per (flow, txid)), its orphan responses (first event of their key in
+// its stream) and its DNS period shifts. Every rank then replays the ranks before it:
+// the open queries of shard j that shards j+1 .. r-1 neither answered nor purged reach
+// shard r, where they pair with r's orphan responses (TransactionManager::
+// maybe_end_transaction, libs/visor_transaction/TransactionManager.h:51-106) or time out
+// at r's period shifts (DnsStreamHandler.h:252-267). Each rank counts only what happens
+// in its own shard, into its own buckets, before the bucket all-reduce.
+namespace {
+struct EdgeHdr {
+    uint32_t magic, n_open, n_orph, n_shift;
+};
+const uint32_t EDGE_MAGIC = 0x31455650u; // "PVE1"
+struct EdgeView {
+    std::vector<PvXEvent> open, orph;
+    std::vector<std::pair<int64_t, uint32_t>> shifts;
+};
+bool edge_parse(const uint8_t *b, size_t n, EdgeView &v)
+{
+    EdgeHdr h;
+    if (n < sizeof h) return false;
+    memcpy(&h, b, sizeof h);
+    const size_t need = sizeof h + ((size_t)h.n_open + h.n_orph) * sizeof(PvXEvent) + (size_t)h.n_shift * 12;
+    if (h.magic != EDGE_MAGIC || n != need) return false;
+    const uint8_t *p = b + sizeof h;
+    v.open.resize(h.n_open);
+    v.orph.resize(h.n_orph);
+    if (h.n_open) memcpy(v.open.data(), p, h.n_open * sizeof(PvXEvent));
+    p += h.n_open * sizeof(PvXEvent);
+    if (h.n_orph) memcpy(v.orph.data(), p, h.n_orph * sizeof(PvXEvent));
+    p += h.n_orph * sizeof(PvXEvent);
+    v.shifts.resize(h.n_shift);
+    for (uint32_t i = 0; i < h.n_shift; i++) {
+        memcpy(&v.shifts[i].first, p + 12 * i, 8);
+        memcpy(&v.shifts[i].second, p + 12 * i + 8, 4);
+    }
+    return true;
+}
+// first shift of `sh` at or after ttl + sec (the purge of a query started at sec), or -1
+int purge_shift(const std::vector<std::pair<int64_t, uint32_t>> &sh, uint32_t ttl_s, int64_t sec)
+{
+    for (size_t i = 0; i < sh.size(); i++)
+        if (sh[i].first >= (int64_t)ttl_s + sec) return (int)i;
+    return -1;
+}
+int add_dns_words(pv_ctx *c, uint32_t slot, const uint64_t add[4])
+{
+    static const int w[4] = {DC_XTOTAL, DC_XOUT, DC_XIN, DC_XTIMEOUT};
+    for (int k = 0; k < 4; k++) {
+        if (!add[k]) continue;
+        uint64_t *dp = c->d_sum + (size_t)slot * PV_SUM_WORDS + PV_OFF_DNS + w[k];
+        uint64_t v = 0;
+        hipError_t e;
+        if (!hip_ok(e = hipMemcpy(&v, dp, 8, hipMemcpyDeviceToHost))) return c->hipfail(e, "edge counters");
+        v += add[k];
+        if (!hip_ok(e = hipMemcpy(dp, &v, 8, hipMemcpyHostToDevice))) return c->hipfail(e, "edge counters");
+    }
+    return 0;
+}
+bool in_dns_window(pv_ctx *c, uint32_t slot)
+{
+    return std::find(c->dns.slots.begin(), c->dns.slots.end(), slot) != c->dns.slots.end();
+}
+} // namespace
+
+int pv_edge_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return c->hipfail(e, "synchronize");
+    uint32_t nv[4];
+    if (!hip_ok(e = hipMemcpy(nv, c->d_nvals, 16, hipMemcpyDeviceToHost))) return c->hipfail(e, "edge counts");
+    if (nv[3] > c->orph_cap) return c->fail(PV_ECAPACITY, "%u shard-edge responses exceed the stub capacity", nv[3]);
+    // open queries: the carried list, latest event per key (rank order in the sort keys)
+    std::vector<PvXEvent> pend(c->n_pend), open;
+    std::vector<uint64_t> pk(c->n_pend);
+    if (c->n_pend) {
+        if (!hip_ok(e = hipMemcpy(pend.data(), c->d_pend[c->pend_cur], c->n_pend * sizeof(PvXEvent), hipMemcpyDeviceToHost)) ||
+            !hip_ok(e = hipMemcpy(pk.data(), c->d_pkeys[c->pend_cur], c->n_pend * 8, hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "open queries");
+        std::unordered_map<uint64_t, size_t> last;
+        last.reserve(pend.size() * 2);
+        for (size_t i = 0; i < pend.size(); i++) {
+            auto it = last.find(pend[i].key);
+            if (it == last.end() || (uint32_t)pk[i] >= (uint32_t)pk[it->second]) last[pend[i].key] = i;
+        }
+        open.reserve(last.size());
+        for (auto &kv : last) open.push_back(pend[kv.second]);
+    }
+    std::vector<PvXEvent> orph(nv[3]);
+    if (nv[3] && !hip_ok(e = hipMemcpy(orph.data(), c->d_orph, nv[3] * sizeof(PvXEvent), hipMemcpyDeviceToHost)))
+        return c->hipfail(e, "edge responses");
+    EdgeHdr h{EDGE_MAGIC, (uint32_t)open.size(), (uint32_t)orph.size(), (uint32_t)c->dns_shifts.size()};
+    const size_t n = sizeof h + (open.size() + orph.size()) * sizeof(PvXEvent) + c->dns_shifts.size() * 12;
+    uint8_t *o = (uint8_t *)malloc(n);
+    if (!o) return c->fail(PV_ECAPACITY, "out of host memory");
+    memcpy(o, &h, sizeof h);
+    uint8_t *p = o + sizeof h;
+    if (!open.empty()) memcpy(p, open.data(), open.size() * sizeof(PvXEvent));
+    p += open.size() * sizeof(PvXEvent);
+    if (!orph.empty()) memcpy(p, orph.data(), orph.size() * sizeof(PvXEvent));
+    p += orph.size() * sizeof(PvXEvent);
+    for (auto &sh : c->dns_shifts) {
+        memcpy(p, &sh.first, 8);
+        memcpy(p + 8, &sh.second, 4);
+        p += 12;
+    }
+    *buf = o;
+    *bytes = n;
+    return 0;
+}
+
+int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks, uint32_t me)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (me >= nranks) return c->fail(PV_EINVAL, "rank %u of %u", me, nranks);
+    std::vector<EdgeView> v(nranks);
+    for (uint32_t j = 0; j <= me; j++)
+        if (!edge_parse(bufs[j], sizes[j], v[j])) return c->fail(PV_EINVAL, "malformed shard-edge buffer of rank %u", j);
+    // queries open at the start of shard me, as the ranks before it leave them
+    std::unordered_map<uint64_t, PvXEvent> M;
+    for (uint32_t j = 0; j < me; j++) {
+        for (auto &o : v[j].orph) M.erase(o.key); // answered (or found purged) in shard j
+        for (auto it = M.begin(); it != M.end();)
+            it = purge_shift(v[j].shifts, c->ttl_s, it->second.sec) >= 0 ? M.erase(it) : std::next(it);
+        for (auto &q : v[j].open) M[q.key] = q;
+    }
+    if (M.empty()) return 0;
+    std::unordered_map<uint64_t, const PvXEvent *> orph;
+    for (auto &o : v[me].orph) orph[o.key] = &o;
+    std::map<uint32_t, std::array<uint64_t, 4>> add; // slot -> total, out, in, timeout
+    const bool quant = c->dns_groups & PV_DNS_QUANTILES;
+    for (auto &kv : M) {
+        const PvXEvent &qe = kv.second;
+        const int ps = purge_shift(c->dns_shifts, c->ttl_s, qe.sec);
+        auto it = orph.find(kv.first);
+        if (it != orph.end() && (ps < 0 || it->second->sec < c->dns_shifts[ps].first)) {
+            const PvXEvent &r = *it->second;
+            const uint32_t slot = r.pad & 0x7f;
+            const bool kept = (r.pad & 0x80) && in_dns_window(c, slot);
+            // pv_xact_resolve's pairing arithmetic (timespec_diff, TransactionManager.h:24-37)
+            int64_t dsec = r.sec > qe.sec ? r.sec - qe.sec : qe.sec - r.sec;
+            int64_t dnsec = (int64_t)r.nsec - (int64_t)qe.nsec;
+            if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
+            const bool timed_out = dsec > (int64_t)c->ttl_s ||
+                                   (dsec == (int64_t)c->ttl_s && ((double)dnsec / 1.0e6) >= (double)c->ttl_ms);
+            auto &a = add[slot];
+            if (timed_out) {
+                if (kept) a[3]++;
+                continue;
+            }
+            const uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
+            if (kept) {
+                a[0]++;
+                if (r.dir == 0) a[1]++;
+                else if (r.dir == 1) a[2]++;
+            }
+            if (quant && in_dns_window(c, slot)) {
+                const uint32_t sg = slot | (c->gen[slot] << 8);
+                if (r.dir == 0) c->xvals_host.push_back(PvXValue{us, sg, XV_FROM_US});
+                else if (r.dir == 1) c->xvals_host.push_back(PvXValue{us, sg, XV_TO_US});
+                if (qe.len && kept) {
+                    const double ratio = (double)r.len / (double)qe.len;
+                    uint64_t bits;
+                    memcpy(&bits, &ratio, 8);
+                    c->xvals_host.push_back(PvXValue{bits, sg, XV_RATIO});
+                }
+            }
+        } else if (ps >= 0) {
+            const uint32_t slot = c->dns_shifts[ps].second;
+            if (in_dns_window(c, slot)) add[slot][3]++;
+        }
+    }
+    for (auto &kv : add) {
+        const uint64_t a4[4] = {kv.second[0], kv.second[1], kv.second[2], kv.second[3]};
+        if (int rc = add_dns_words(c, kv.first, a4)) return rc;
+    }
+    return 0;
+}
+
+// Quantile inputs (transaction values) of the live window, exchanged so every rank's
+// quantiles cover the whole stream: (slot, kind, bits) records.
+int pv_values_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (int rc = sync_xvals(c)) return rc;
+    std::vector<uint8_t> o;
+    for (auto &v : c->xvals_host) {
+        const uint32_t slot = v.slot & 0xff;
+        if (slot >= PV_SLOTS || (v.slot >> 8) != c->gen[slot] || !in_dns_window(c, slot)) continue;
+        const size_t p = o.size();
+        o.resize(p + 16);
+        memcpy(&o[p], &v.bits, 8);
+        memcpy(&o[p + 8], &slot, 4);
+        memcpy(&o[p + 12], &v.kind, 4);
+    }
+    *bytes = o.size();
+    *buf = (uint8_t *)malloc(o.size() ? o.size() : 1);
+    if (!o.empty()) memcpy(*buf, o.data(), o.size());
+    return 0;
+}
+
+int pv_values_merge(pv_ctx *c, const uint8_t *buf, size_t bytes)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    if (bytes % 16) return c->fail(PV_EINVAL, "malformed value buffer");
+    if (int rc = sync_xvals(c)) return rc;
+    for (size_t p = 0; p < bytes; p += 16) {
+        PvXValue v;
+        uint32_t slot;
+        memcpy(&v.bits, buf + p, 8);
+        memcpy(&slot, buf + p + 8, 4);
+        memcpy(&v.kind, buf + p + 12, 4);
+        if (slot >= PV_SLOTS) return c->fail(PV_EINVAL, "malformed value buffer");
+        v.slot = slot | (c->gen[slot] << 8);
+        c->xvals_host.push_back(v);
+    }
+    return 0;
+}
+
+// Window identity for the merge: (slot, start second) of every live slot, newest first.
+int pv_window_periods(pv_ctx *c, uint32_t *slots, int64_t *start_sec, uint32_t max_n, uint32_t *n)
+{
+    std::vector<uint32_t> v;
+    for (auto s : c->net.slots) v.push_back(s);
+    for (auto s : c->dns.slots) if (std::find(v.begin(), v.end(), s) == v.end()) v.push_back(s);
+    *n = (uint32_t)v.size();
+    for (uint32_t i = 0; i < v.size() && i < max_n; i++) {
+        slots[i] = v[i];
+        start_sec[i] = c->meta[v[i]].start_sec;
+    }
     return 0;
 }
 

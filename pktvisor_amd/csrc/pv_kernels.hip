@@ -629,7 +629,9 @@ __device__ void cache_flush(PV_CREF(PvParams) P, Cache &C, uint32_t n, uint32_t 
 #endif
 static_assert(PV_NCACHE <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cache entries per flush");
 
+#ifndef PV_HBINS
 #define PV_HBINS 2048 // payload-size bins the Net pass keeps in LDS (larger sizes: HBM atomics)
+#endif
 #define PV_NOH 0xffffffffu
 struct DnsState {
     uint32_t stage[4][PV_WSTAGE / 4];
@@ -1722,7 +1724,16 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         int q = (int)p - 1;
         for (; q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h; q--)
             if (xev(X, q).key == e.key) break;
-        if (q < 0 || (uint32_t)(X.skeys[q] >> 32) != h) return; // NotExist
+        if (q < 0 || (uint32_t)(X.skeys[q] >> 32) != h) {
+            // NotExist here; a shard-edge stub for the multi-GPU merge
+            const uint32_t k = atomicAdd(X.n_orph, 1u);
+            if (k < X.orph_cap) {
+                PvXEvent o = e;
+                o.pad = (uint8_t)(P.slot_of[e.period] | (e.period >= P.skip_before ? 0x80u : 0u));
+                X.orph[k] = o;
+            }
+            return;
+        }
         const PvXEvent qe = xev(X, q);
         if (qe.qr) return; // previous event was a response: erased => NotExist
         uint32_t kp = purge_period(P, X.ttl_s, qe.period, qe.sec);

@@ -253,5 +253,11 @@ struct PvXactParams {
     PV_G PvXEvent *pend_out;
     PV_G uint64_t *pkeys_out;
     PV_G uint32_t *n_pend_out;
+    // shard-edge stubs: responses that are the first event of their (flow, txid) in this
+    // context's whole stream ("orphans"; they may answer a query open at the end of the
+    // previous shard), appended with pad = slot | kept << 7
+    PV_G PvXEvent *orph;
+    PV_G uint32_t *n_orph;
+    uint32_t orph_cap;
 };
 #define PV_PEND_FLAG 0x80000000u

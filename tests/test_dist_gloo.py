@@ -1,0 +1,17 @@
+"""CPU, world_size 2 over gloo: the collective helpers of the multi-GPU merge
+(pktvisor_amd/dist.py): SUM of u64 counters carried as int64 (two's-complement wrap, as
+RCCL's int64 sum), MIN of CPC first-occurrence indices, contiguous shard ranges,
+object all-gather of per-rank export buffers."""
+import json
+
+from tests.dist_launch import run_ranks
+
+
+def test_gloo_two_ranks(tmp_path):
+    out = str(tmp_path / "r")
+    run_ranks(2, ["cpu", out], timeout=180)
+    r0, r1 = (json.load(open(f"{out}.{r}")) for r in (0, 1))
+    assert r0["sum"] == r1["sum"] == [3, -(1 << 63) + 5, 14]  # (2^63 - 5) + 10 wraps
+    assert r0["min"] == r1["min"] == [100, 4, 3]
+    assert r0["ranges"] == [[0, 5], [5, 10]]
+    assert r0["gathered"] == r1["gathered"] == [[0, "00"], [1, "0101"]]
