@@ -359,7 +359,8 @@ __device__ __forceinline__ uint32_t period_of(PV_CREF(PvParams) P, uint64_t i)
 }
 __device__ __forceinline__ uint64_t uni64(uint64_t v)
 {
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
 // DNS over UDP: the message of one record, located by the Net pass
@@ -735,7 +736,10 @@ __device__ __forceinline__ uint64_t net_ip_entry(const NetK &K, const A &R, cons
 // Every wave streams its own tiles into a private LDS ring with LDS-DMA
 // (global_load_lds: no VGPR holds data in flight) and keeps PV_NL_Q - 1 tiles in flight
 // while it parses one. Per tile it issues, in this order, two row loads of record offsets
-// (each lane's start and end) for the tile PV_NL_Q ahead and the tile's own DMA pieces;
+// (each lane's start and end) for the tile PV_NL_Q + 1 ahead and the tile's own DMA pieces.
+// A tile's rows are thus issued two steps before its DMA needs them: loads retire in
+// issue order, so rows issued only one step ahead would make every step wait one full
+// memory latency and defeat the tile ring;
 // every tile slot of the sequence is issued even past the range's end (a clamped copy),
 // so the count of DMA operations younger than any tile is fixed and the wave waits for it
 // with an exact vmcnt. The wave's other memory operations (stores, rare HBM reads) only
@@ -748,7 +752,7 @@ __device__ __forceinline__ uint64_t net_ip_entry(const NetK &K, const A &R, cons
 #endif
 #define PV_NL_NJ (PV_NL_SLOT / 1024)     // 1-KiB DMA pieces per tile
 #define PV_NL_OPS (PV_NL_NJ + 2)         // DMA operations per tile
-#define PV_NL_OROWS (PV_NL_Q + 1)        // offset-row pairs per wave
+#define PV_NL_OROWS (PV_NL_Q + 2)        // offset-row pairs per wave (tiles k .. k + Q + 1)
 static_assert(PV_NL_SLOT % 1024 == 0, "whole DMA pieces");
 static_assert(PV_NL_SLOT / PV_WT >= 80, "window must cover Eth + IPv4 + UDP from a 16-B aligned start");
 
@@ -952,20 +956,25 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
     c.zero();
     uint32_t wslot = 0xffffffffu;
     if (ntl) {
-        // prologue: the sequence's first Q - 1 steps ([rows k + 1][tile k])
+        // prologue: rows 0 and 1, then the sequence's first Q - 1 steps, each
+        // [rows t + 2][tile t] for t = 0 .. Q - 2 (the steady state's pattern, so the
+        // vmcnt counts below hold from the first loop step on)
         issue_rows(0);
+        issue_rows(1);
         PV_VMCNT(0);
-        for (uint32_t k = 0; k + 1 < PV_NL_Q; k++) {
-            issue_rows(k + 1);
-            if (k) PV_VMCNT(PV_NL_NJ + 2); // rows k landed (behind tile k - 1 and rows k + 1)
-            issue_tile(k);
+        for (uint32_t t = 0; t + 1 < PV_NL_Q; t++) {
+            issue_rows(t + 2);
+            if (t >= 2) PV_VMCNT(2 * PV_NL_OPS); // rows t landed (issued two steps earlier)
+            issue_tile(t);
         }
     }
     STAMP_DECL
     for (uint32_t k = 0; k < ntl; k++) {
-        // step: rows k + Q, then tile k + Q - 1 (its rows came one step earlier)
-        issue_rows(k + PV_NL_Q);
-        PV_VMCNT(PV_NL_NJ + 2);
+        // step: rows k + Q + 1, then tile k + Q - 1, whose rows came two steps earlier:
+        // younger than them are that step's tile, the last step's rows and tile, and this
+        // step's rows
+        issue_rows(k + PV_NL_Q + 1);
+        PV_VMCNT(2 * PV_NL_OPS);
         issue_tile(k + PV_NL_Q - 1);
         PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed
         STAMP(1)

@@ -6,7 +6,7 @@ T=${1:-x}
 O=gpurun_out/it_$T
 mkdir -p $O
 export TMPDIR=/tmp
-B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e"
 R="rocprofv3 --kernel-trace --stats --output-format csv"
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 &&
 timeout -k 10 300 $R -d $O/c2 -o k -- $B > $O/c2.log 2>&1 &&
