@@ -5,7 +5,7 @@ python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--records 
 
 One step = one pass of the fused Net v1 + DNS v1 hot path over one batch of
 synthetic pcap records already resident in HBM: bucket reset, the parse kernel
-(pv_net_dns_kernel), DNS transaction pairing when the batch has DNS, the status
+(pv_net_kernel, pv_dns_kernel, the top-N merge kernels), DNS transaction pairing when the batch has DNS, the status
 read-back, and - for N > 1 - the RCCL all-reduce of the live buckets over xGMI.
 Each rank processes its own shard of R records (weak scaling). Rank 0 prints
 one JSON line. The default workload is BASELINE.json configs[1] (C2: 10M x 64 B

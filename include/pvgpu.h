@@ -173,7 +173,7 @@ int pv_window_slots(pv_ctx *ctx, uint32_t *slots, uint32_t max_slots, uint32_t *
 int pv_export_topn(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
 int pv_merge_topn(pv_ctx *ctx, const uint8_t *buf, size_t bytes);
 
-/* Device time of the fused parse kernel (pv_net_dns_kernel), from HIP events
+/* Device time of the Net-pass kernel (pv_net_kernel), from HIP events
  * recorded on the launch stream around every launch since the last reset:
  * total milliseconds and number of launches. */
 int pv_kernel_timing(pv_ctx *ctx, double *total_ms, uint64_t *launches, int reset);

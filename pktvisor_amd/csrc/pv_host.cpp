@@ -270,7 +270,7 @@ struct pv_ctx {
     uint32_t *d_mq_cnt = nullptr;
     uint64_t *d_stamps = nullptr; // diagnostic phase stamps (PV_STAMPS env + -DPV_STAMPS build)
     int cus = 256;
-    int wg_per_cu = 2; // resident pv_net_kernel workgroups per CU (occupancy API)
+    int wg_per_cu = 2; // resident Net-pass workgroups per CU (occupancy API)
     uint64_t *d_dq = nullptr; // DNS work lists (32-B messages)
     uint32_t *d_dq_cnt = nullptr;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;

@@ -787,6 +787,9 @@ __device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds)
                  : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
 #define PV_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
+// s_waitcnt vmcnt(0) as the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15), which
+// the compiler's wait insertion sees, unlike inline asm
+#define PV_WAIT_VMCNT0 0x0F70
 
 // Slot accessor: packed (dword d of the span at L[d]) or the lane's window as the DMA
 // wrote it in 16-B pieces (dword d of lane l at L[(d >> 2) * 256 + l * 4 + (d & 3)]).
@@ -895,6 +898,40 @@ __device__ __forceinline__ uint32_t fast_flowkey(const RecW &r)
 
 } // namespace
 
+// The general per-record path (every frame the fast path does not take: VLAN, IPv6,
+// options, tunnels, other link types), out of line. A call returns with its reads done, so
+// the Net pass's loop never carries a register load pending across its edge; otherwise
+// the compiler's vmcnt(0) before that register's next write, on the fast path too, would
+// drain every tile in flight on every step. Fills what the caller's counters need and
+// the record's dense IP log entry and DNS message.
+struct SlowOut {
+    uint64_t ek;
+    DnsMsgW dm;
+    uint32_t caplen, isdns;
+    uint8_t dir, l3, l4, syn;
+};
+__device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF(PvParams) P, const NetK K, uint64_t off,
+                                         uint64_t i, uint32_t slot, uint32_t p_lo, bool upd)
+{
+    SlowOut so;
+    so.ek = 0;
+    so.dm = DnsMsgW{};
+    so.isdns = 0;
+    Parsed o;
+    parse_record(R, C, P, off, o);
+    so.caplen = o.caplen; so.dir = o.dir; so.l3 = o.l3; so.l4 = o.l4; so.syn = o.syn;
+    if (K.dbg & 2) return so;
+    if (upd) so.ek = net_ip_entry(K, R, o, i, slot);
+    if (o.l4 == 17 && !(K.dbg & 4)) {
+        const uint32_t port = dns_port(R.u32(o.l4off));
+        if (port) {
+            so.dm = msg_words(dns_msg_of(P, R, o, i, port, p_lo, upd, true));
+            so.isdns = 1;
+        }
+    }
+    return so;
+}
+
 // ------------------------------------------------------------------ the Net pass
 // One lane per record; workgroup b owns the contiguous tile range [b*T, (b+1)*T) and its
 // wave w takes the range's tiles w, w+4, ... (staging above). Counters stay in registers,
@@ -905,7 +942,9 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ NetState S;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave index as a scalar: tile and period arithmetic stays uniform (no vector loads
+    // whose vmcnt wait would also drain the tiles in flight)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x == 0) S.nd = 0;
     __syncthreads();
@@ -982,7 +1021,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         const uint64_t t = tile_of(k);
         const uint64_t r0 = t * PV_WT;
         const uint64_t r1 = min<uint64_t>(r0 + PV_WT, n) - 1;
-        const uint32_t p_lo = period(r0), p_hi = period(r1);
+        const uint32_t p_lo = __builtin_amdgcn_readfirstlane(period(r0)), p_hi = __builtin_amdgcn_readfirstlane(period(r1));
         const bool straddle = p_lo != p_hi; // pv_boundary_kernel's tile
         const bool upd = !straddle && p_lo >= K.skip_before;
         const uint32_t slot = slot_of(p_lo);
@@ -1004,16 +1043,24 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         if (active && !(K.dbg & 1)) {
             const SAcc R = packed ? SAcc{K.recs, NW.slot[sl], base, nch * 16 - 4, 0u, 1u}
                                   : SAcc{K.recs, NW.slot[sl], off & ~15ull, PV_NL_SLOT / PV_WT - 4, lane * 4, 0u};
-            // fast path: the record's first 68 bytes are inside the staged range
+            // fast path: the 17 staged dwords recw_load reads (the record's first 64 bytes
+            // plus the alignment spill) are inside the staged range; in window mode that
+            // holds for every record (start within 15 bytes of the 16-B aligned window)
             const uint32_t rel = (uint32_t)(off - R.gbase);
             RecW rw;
-            bool fast = rel + 68 <= R.lim + 4;
+            bool fast = (rel >> 2) + 17 <= (R.lim + 4) >> 2;
             Parsed o;
             if (fast) {
                 recw_load(R.L, rel >> 2, rel & 3, packed, lane * 4, rw);
                 fast = fast_parse(rw, C, P, off, o);
             }
-            if (!fast) parse_record(R, C, P, off, o);
+            if (!fast) {
+                const SlowOut so = net_slow(R, C, P, K, off, i, slot, p_lo, upd);
+                o.caplen = so.caplen; o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
+                ek = so.ek;
+                dm = so.dm;
+                isdns = so.isdns;
+            }
             STAMP(4)
             if (K.dbg & 2) {
                 c.add(o);
@@ -1038,15 +1085,13 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                                 kcpc_min(K, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), i);
                             }
                         }
-                    } else {
-                        ek = net_ip_entry(K, R, o, i, slot);
                     }
                 }
-                if (o.l4 == 17 && !(K.dbg & 4)) {
-                    const uint32_t port = dns_port(fast ? rw.at(50) : R.u32(o.l4off));
+                if (fast && o.l4 == 17 && !(K.dbg & 4)) {
+                    const uint32_t port = dns_port(rw.at(50));
                     if (port) {
-                        DnsMsg d = dns_msg_of(P, R, o, i, port, p_lo, upd, !fast);
-                        if (fast) d.fkey = fast_flowkey(rw);
+                        DnsMsg d = dns_msg_of(P, R, o, i, port, p_lo, upd, false);
+                        d.fkey = fast_flowkey(rw);
                         dm = msg_words(d);
                         isdns = true;
                     }

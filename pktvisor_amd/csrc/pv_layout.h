@@ -190,7 +190,7 @@ struct PvParams {
     PV_G uint32_t *mq_cnt; // entries per workgroup log
     PV_G uint64_t *stamps; // diagnostic builds (-DPV_STAMPS): 8 phase cycle sums per wave
     uint32_t mq_cap;
-    uint32_t grid_main;   // workgroups of pv_net_dns_kernel
+    uint32_t grid_main;   // workgroups of pv_net_kernel / pv_dns_kernel
     uint32_t n_btiles;    // 64-record tiles holding a period shift (pv_boundary_kernel)
     PV_G uint64_t *dq;    // per-workgroup DNS work lists (32-B DnsMsg), region = wt_per_block * 64
     PV_G uint32_t *dq_cnt;
