@@ -1154,20 +1154,17 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *
     DnsCtr c;
     c.zero();
     uint32_t wslot = 0xffffffffu;
-    auto msg = [&](uint32_t t) -> DnsMsg {
-        const uint32_t j = t * PV_WT + lane;
-        DnsMsg d;
-        if (t < ntl && j < nd) d = Q[j];
-        else { d = DnsMsg{}; d.flags = 0; }
-        return d;
-    };
+    // message and window loads are unconditional (clamped index; an inactive lane's copy is
+    // never read), so every iteration issues the same number of loads in the same order and
+    // the compiler's vmcnt waits stay exact instead of falling back to vmcnt(0)
+    auto msg = [&](uint32_t t) -> DnsMsg { return Q[min(t * PV_WT + lane, nd - 1)]; };
     uint32_t t = wave;
     DnsMsg m_cur{}, m_n{};
     uint4 pf[8];
-    auto issue = [&](const DnsMsg &d, bool act) {
+    auto issue = [&](const DnsMsg &d, bool) {
         const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + ((uint64_t)d.moff & ~15ull));
 #pragma unroll
-        for (int j = 0; j < 8; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
+        for (int j = 0; j < 8; j++) pf[j] = src[j];
     };
     if (t < ntl) {
         m_cur = msg(t);
@@ -1186,9 +1183,13 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *
             L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
         }
         if (t + 4 < ntl) {
+            // the message after next is loaded before the next windows: loads retire in
+            // issue order, so the register moves of the message rotation then wait for
+            // the message alone, never for the windows still in flight
+            const DnsMsg m_nn = msg(t + 8);
             issue(m_n, (t + 4) * PV_WT + lane < nd);
             m_cur = m_n;
-            m_n = msg(t + 8);
+            m_n = m_nn;
         }
         // the wave's register counters follow the slot of its first message
         const uint32_t s0 = P.slot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
