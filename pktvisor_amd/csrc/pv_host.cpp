@@ -1212,7 +1212,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates, bucket them by table region, merge each
     // region in LDS, decode the names of new entries
-    hipLaunchKernelGGL(pv_topn_combine, dim3(grid), dim3(512), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_topn_combine, dim3(grid), dim3(PV_CB_THREADS), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_scan, dim3(1), dim3(1024), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_scatter, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_merge, dim3(1u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);

@@ -1274,7 +1274,9 @@ __device__ __forceinline__ void wg_records(PV_CREF(PvParams) P, uint32_t b, uint
 // heavy hitter leaves one entry per range instead of one per packet; entries the table
 // cannot take pass through unchanged. The combined list goes to the workgroup's cb
 // region and its entries are counted per table region.
-#define PV_CB_N 4096
+#ifndef PV_CB_N
+#define PV_CB_N 8192 // combine: LDS table entries per workgroup (128 KiB: one workgroup per CU)
+#endif
 #define PV_W_CNT ((1u << 29) - 1) // weight bits of a dense IPv4 entry
 struct CombState {
     uint64_t key[PV_CB_N];
@@ -1318,7 +1320,7 @@ __device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, CombState &S, uint
     comb_out(P, S, out, ck, w, rep);
 }
 
-extern "C" __global__ void __launch_bounds__(512) pv_topn_combine(const PvParams *__restrict__ Pp)
+extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ CombState S;

@@ -83,6 +83,7 @@ enum {
 // plus linear probing that wraps inside the region, so one workgroup of pv_topn_merge
 // can own a region outright and merge a batch's updates into it in LDS.
 #define PV_REGION_LOG2 12
+#define PV_CB_THREADS 1024 // pv_topn_combine workgroup size
 #define PV_MAX_REGIONS_LOG2 12 // table_log2 <= PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2
 #define PV_PROBES 256
 // entry of the new-name list (pv_topn_merge -> pv_topn_names)
