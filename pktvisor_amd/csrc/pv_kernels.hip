@@ -233,6 +233,9 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
 // crep holds the smallest record index that touched the entry: a later record of the
 // same key knows its CPC coupon (same key => same coupon) was already submitted with a
 // smaller index, and the insert kernel uses it as the record a name is decoded from.
+#ifndef PV_CACHE_PROBES
+#define PV_CACHE_PROBES 4 // slots a key may probe before it goes to the update log
+#endif
 #define PV_LKEY(slot, lm, payload) (((uint64_t)(slot) << 60) | ((uint64_t)(lm) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
 template <int N>
 struct KeyCache {
@@ -248,7 +251,7 @@ struct KeyCache {
     __device__ __forceinline__ bool add(uint64_t k, uint32_t w, uint32_t idx, uint32_t &first)
     {
         uint32_t h = (uint32_t)(fmix64(k) >> 32) & (N - 1);
-        for (int probe = 0; probe < 8; probe++) {
+        for (int probe = 0; probe < PV_CACHE_PROBES; probe++) {
             uint64_t cur = key[h];
             if (cur == 0) {
                 const uint64_t prev = atomicCAS((unsigned long long *)&key[h], 0ull, (unsigned long long)k);
@@ -498,7 +501,12 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         }
         DnsInfo d;
         dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
-        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) top(TM_DENSE_PORT, dm.port, 1);
+        // client ports spread over 64 K values and rarely repeat inside a workgroup: a
+        // no-return HBM atomic on the dense table, not an LDS cache probe (boundary: as before)
+        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) {
+            if (cache && !(P.dbg & 32)) sum_add(P, slot, PV_OFF_PORT + (dm.port & 0xffff), 1);
+            else top(TM_DENSE_PORT, dm.port, 1);
+        }
         if (d.ok) {
             if (qr) top(TM_DENSE_RCODE, rcode, 1);
             if (d.has_query) {
