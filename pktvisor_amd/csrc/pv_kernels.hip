@@ -55,6 +55,7 @@
 #define PV_WPE 4 // waves per SIMD the Net pass is register-budgeted for
 #endif
 #define PV_WINW (PV_WIN / 4)
+#define PV_NWIN 192 // bytes of each record staged by pv_topn_names
 
 // ------------------------------------------------------------------ byte access
 // recs is 256-B aligned and padded by >= 256 bytes: two aligned dword loads and
@@ -1522,7 +1523,10 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
 extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ uint32_t stage[4][PV_WINW * 64];
+    // each lane stages PV_NWIN bytes from its record's 16-B aligned start: the frame
+    // headers and, for a plain DNS message, the whole first question, so the record is
+    // parsed and its name decoded from LDS after one round of loads
+    __shared__ uint32_t stage[4][PV_NWIN / 4 * 64];
     const uint32_t n = min(*P.nn_cnt, P.nn_cap);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t *L = stage[threadIdx.x >> 6];
@@ -1535,28 +1539,32 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
         uint32_t metric = 0, size = 0, start = 0, nl = 0, mlen = 0;
         uint64_t m = 0, a6 = 0;
         Parsed o;
+        uint64_t roff = 0;
         if (act) {
             e = P.nn[i];
             metric = PV_KEY_METRIC(P.tkeys[e.pos]);
-            parse_record(G, P, P.offs[e.rep], o);
-            m = o.l4off + 8;
-            mlen = o.l4len - 8;
+            roff = P.offs[e.rep];
         }
-        const uint64_t wbase = m & ~15ull;
+        const uint64_t wbase = roff & ~15ull;
         {
             const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + wbase);
-            uint4 pf[PV_WIN / 16];
+            uint4 pf[PV_NWIN / 16];
 #pragma unroll
-            for (int j = 0; j < PV_WIN / 16; j++) pf[j] = (act && metric != TM_IPV6) ? src[j] : make_uint4(0, 0, 0, 0);
+            for (int j = 0; j < PV_NWIN / 16; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
 #pragma unroll
-            for (int j = 0; j < PV_WIN / 16; j++) {
+            for (int j = 0; j < PV_NWIN / 16; j++) {
                 L[(4 * j + 0) * 64 + lane] = pf[j].x;
                 L[(4 * j + 1) * 64 + lane] = pf[j].y;
                 L[(4 * j + 2) * 64 + lane] = pf[j].z;
                 L[(4 * j + 3) * 64 + lane] = pf[j].w;
             }
         }
-        const TAcc R{P.recs, L, wbase, PV_WIN - 4, 64u, lane};
+        const TAcc R{P.recs, L, wbase, PV_NWIN - 4, 64u, lane};
+        if (act) {
+            parse_record(R, P, roff, o);
+            m = o.l4off + 8;
+            mlen = o.l4len - 8;
+        }
         if (act) {
             if (metric == TM_IPV6) {
                 a6 = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
