@@ -296,6 +296,11 @@ struct pv_ctx {
     float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
     uint32_t *d_status = nullptr;
     PvParams *d_params = nullptr;      // kernel parameter blocks (device memory)
+    // pinned host mirrors of the per-batch uploads and the status read-back (direct DMA,
+    // no pageable staging copy on the stream)
+    PvParams *h_params = nullptr;
+    PvXactParams *h_xparams = nullptr;
+    uint32_t *h_status = nullptr;
     PvXactParams *d_xparams = nullptr;
     uint64_t max_records = 0;
     // host-memory ingest (pv_process_host): worker pool, copy stream and two staging
@@ -801,6 +806,7 @@ uint64_t quantile_at(std::vector<uint64_t> v, double r)
 // copy the transaction values appended on the device since the last sync
 int sync_xvals(pv_ctx *c)
 {
+    flush_fills(c);
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return c->hipfail(e, "synchronize");
     uint32_t status[ST_WORDS], nv = 0;
@@ -942,6 +948,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_trash, (size_t)PV_TRASH_WAVES * 2048)) ||
         !hip_ok(e = hipMalloc(&c->d_cb_cnt, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_params, sizeof(PvParams))) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_params, sizeof(PvParams), hipHostMallocDefault)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_xparams, sizeof(PvXactParams), hipHostMallocDefault)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_status, ST_ALLOC * 4, hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_xparams, sizeof(PvXactParams))) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
         !hip_ok(e = hipEventCreate(&c->ev_stop))) {
         *out = c;
@@ -966,6 +975,8 @@ void pv_destroy(pv_ctx *c)
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
                     c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph};
     for (void *p : ptrs) if (p) hipFree(p);
+    for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status})
+        if (hp) hipHostFree(hp);
     for (auto &st : c->stage) {
         if (st.h_recs) hipHostFree(st.h_recs);
         if (st.h_offs) hipHostFree(st.h_offs);
@@ -995,8 +1006,7 @@ int pv_reset(pv_ctx *c)
     c->n_pend = 0;
     c->pend_base = -1;
     c->dns_shifts.clear();
-    hipError_t e = hipMemsetAsync(c->d_nvals, 0, 16, c->stream);
-    if (e != hipSuccess) return c->hipfail(e, "reset");
+    launch_fill32(c, c->d_nvals, 4, 0); // with the next batch's slot clears
     return 0;
 }
 
@@ -1202,7 +1212,8 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         if (!seen) P.btile[P.n_btiles++] = t;
     }
     flush_fills(c);
-    if (!hip_ok(e = hipMemcpyAsync(c->d_params, &P, sizeof P, hipMemcpyHostToDevice, st)))
+    *c->h_params = P;
+    if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
     hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -1227,9 +1238,10 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
     uint32_t status[ST_WORDS];
-    if (!hip_ok(e = hipMemcpyAsync(status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
+    if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "kernel execution");
+    memcpy(status, c->h_status, sizeof status);
     {
         float ms = 0;
         if (hipEventElapsedTime(&ms, c->ev_start, c->ev_stop) == hipSuccess) { c->kernel_ms += ms; c->kernel_launches++; }
@@ -1309,7 +1321,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         X.n_orph = c->d_nvals + 3;
         X.orph_cap = c->orph_cap;
         if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
-            !hip_ok(e = hipMemcpyAsync(c->d_xparams, &X, sizeof X, hipMemcpyHostToDevice, st)))
+            !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
             return c->hipfail(e, "parameter upload");
         hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
@@ -1336,7 +1348,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
             uint32_t nvalid = 0;
             if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
             if (nvalid) {
-                if (!hip_ok(e = hipMemcpyAsync(c->d_xparams, &X, sizeof X, hipMemcpyHostToDevice, st)))
+                if (!hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
                     return c->hipfail(e, "parameter upload");
                 hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st,
                                    (const PvXactParams *)c->d_xparams, nvalid);
