@@ -105,14 +105,33 @@ PV_FN uint32_t cpc_coupon(uint64_t h1, uint64_t h2)
     return (row << 6) | col;
 }
 
-// Polynomial string hash over Z/2^64 (odd base): prefix hashes give suffix hashes
-// by H(s[i:n]) = H(s[:n]) - H(s[:i]) * B^(n-i). Names are <= 255 chars.
-#define PBASE 0x9e3779b97f4a7c15ULL
-PV_FN uint64_t powb(uint32_t e)
+// Name fingerprint state: two polynomial string hashes over Z/2^32 with odd bases, packed
+// as lo | hi << 32. Prefix hashes give suffix hashes by H(s[i:n]) = H(s[:n]) - H(s[:i]) *
+// B^(n-i) in each lane. Two 32-bit lanes cost a GPU two quarter-rate multiplies per
+// character where one 64-bit lane costs four. Names are <= 255 chars.
+#define PB1 0x9e3779b1u
+#define PB2 0x85ebca77u
+PV_FN uint64_t ph_step(uint64_t h, uint32_t c)
 {
-    uint64_t r = 1, b = PBASE;
-    while (e) { if (e & 1) r *= b; b *= b; e >>= 1; }
-    return r;
+    const uint32_t lo = (uint32_t)h * PB1 + (c + 1), hi = (uint32_t)(h >> 32) * PB2 + (c + 1);
+    return ((uint64_t)hi << 32) | lo;
+}
+PV_FN uint64_t powb(uint32_t e) // (PB1^e, PB2^e)
+{
+    uint32_t r1 = 1, r2 = 1, b1 = PB1, b2 = PB2;
+    while (e) {
+        if (e & 1) { r1 *= b1; r2 *= b2; }
+        b1 *= b1; b2 *= b2;
+        e >>= 1;
+    }
+    return ((uint64_t)r2 << 32) | r1;
+}
+// a - b * p, lane by lane
+PV_FN uint64_t ph_submul(uint64_t a, uint64_t b, uint64_t p)
+{
+    const uint32_t lo = (uint32_t)a - (uint32_t)b * (uint32_t)p;
+    const uint32_t hi = (uint32_t)(a >> 32) - (uint32_t)(b >> 32) * (uint32_t)(p >> 32);
+    return ((uint64_t)hi << 32) | lo;
 }
 // 56-bit fingerprint of a byte string from its polynomial hash and length
 PV_FN uint64_t fp56(uint64_t poly, uint32_t len, uint32_t salt)
@@ -445,7 +464,7 @@ struct NameStats {
         c = lower(c);
         if (c == '.') { d3 = d2; h3 = h2; d2 = d1; h2 = h1; d1 = d0; h1 = h0; d0 = (int32_t)n; h0 = ph; }
         mm.put(c);
-        ph = ph * PBASE + (c + 1);
+        ph = ph_step(ph, c);
         n++;
         last_c = c;
     }
@@ -488,7 +507,7 @@ PV_FN void agg_domain(const NameStats &s, int &q2, int &q3, uint64_t &ph2, uint6
 // polynomial hash of the suffix [start, n) given the prefix hash at start
 PV_FN uint64_t suffix_hash(const NameStats &s, int start, uint64_t ph_start)
 {
-    return s.ph - ph_start * powb(s.n - (uint32_t)start);
+    return ph_submul(s.ph, ph_start, powb(s.n - (uint32_t)start));
 }
 
 // ------------------------------------------------------------------ name fast path
@@ -571,7 +590,7 @@ PV_FN bool name_stats_fast(const A &R, uint64_t m, uint32_t len, uint32_t off, N
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 hv[r] = ph;
-                if ((uint32_t)r < nv) ph = ph * PBASE + (((x >> (8 * r)) & 0xff) + 1);
+                if ((uint32_t)r < nv) ph = ph_step(ph, (x >> (8 * r)) & 0xff);
             }
 #pragma unroll
             for (int k = 0; k < 4; k++) {
@@ -620,7 +639,7 @@ struct RawName {
     uint32_t n;
     PV_FN void put(uint32_t c)
     {
-        ph = ph * PBASE + (c + 1);
+        ph = ph_step(ph, c);
         n++;
     }
 };
