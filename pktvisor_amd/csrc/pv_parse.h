@@ -564,12 +564,14 @@ PV_FN bool name_stats_fast(const A &R, uint64_t m, uint32_t len, uint32_t off, N
     uint32_t prev = R.u32a(abase);
     bool bad = false;
     for (uint32_t j = 0; j * 16 < n; j++) {
-        // inner dots inside this 16-byte block
+        // inner dots inside this 16-byte block (none for a single-label name)
         uint32_t bm = 0;
+        if (nb) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t rel = ((uint32_t)(bp >> (8 * k)) & 0xff) - 16 * j;
-            bm |= rel < 16 ? 1u << rel : 0u;
+            for (int k = 0; k < 8; k++) {
+                const uint32_t rel = ((uint32_t)(bp >> (8 * k)) & 0xff) - 16 * j;
+                bm |= rel < 16 ? 1u << rel : 0u;
+            }
         }
         uint32_t w[4];
 #pragma unroll
@@ -592,10 +594,13 @@ PV_FN bool name_stats_fast(const A &R, uint64_t m, uint32_t len, uint32_t off, N
                 hv[r] = ph;
                 if ((uint32_t)r < nv) ph = ph_step(ph, (x >> (8 * r)) & 0xff);
             }
+            // a tracked dot in this dword is rare: test all four at once, select only then
+            if (((t[0] - p) < 4) | ((t[1] - p) < 4) | ((t[2] - p) < 4) | ((t[3] - p) < 4)) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t rel = t[k] - p;
-                if (rel < 4) hk[k] = rel == 0 ? hv[0] : rel == 1 ? hv[1] : rel == 2 ? hv[2] : hv[3];
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t rel = t[k] - p;
+                    if (rel < 4) hk[k] = rel == 0 ? hv[0] : rel == 1 ? hv[1] : rel == 2 ? hv[2] : hv[3];
+                }
             }
         }
         mm.k1 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
