@@ -77,6 +77,31 @@ typedef struct pv_config {
     uint64_t max_records;    /* largest batch that will be submitted (sizes scratch) */
 } pv_config;
 
+/* DNS v1 filters, the typed form of the "exclude_noerror", "only_rcode", "answer_count",
+ * "only_queries", "only_responses" and "only_qtype" handler config keys
+ * (DnsStreamHandler::start, src/handlers/dns/v1/DnsStreamHandler.cpp:60-150; applied as
+ * _filtering :538-648). A filtered DNS packet is an event plus the `filtered` counter and
+ * nothing else (process_filtered, :1341-1347). only_rcode is the input-proxy predicate
+ * (:485-508): packets it rejects (queries, other rcodes) are not events at all.
+ * only_qname / only_qname_suffix / only_dnssec_response / geoloc / asn are not built. */
+typedef struct pv_dns_filters {
+    uint32_t exclude_noerror;   /* nonzero: filter rcode 0 (queries too); wins over only_rcode */
+    uint32_t only_rcode_mask;   /* bit r: rcode r wanted (r <= 15, a known RCodeNames value) */
+    int32_t answer_count;       /* ANCOUNT wanted, -1 = off */
+    uint32_t only_queries;      /* nonzero: filter responses */
+    uint32_t only_responses;    /* nonzero: filter queries */
+    uint32_t n_qtypes;          /* entries used in qtypes (<= 16), 0 = off */
+    uint16_t qtypes[16];        /* first-query qtype wanted (QTypeNames values) */
+} pv_dns_filters;
+
+/* Replaces DnsStreamHandler::start's filter setup (dns/v1/DnsStreamHandler.cpp:60-150). Call
+ * before the first batch; NULL clears. PV_EINVAL with the reference's ConfigException text
+ * for an unknown rcode/qtype. */
+int pv_set_dns_filters(pv_ctx *ctx, const pv_dns_filters *f);
+/* Name or decimal -> code for kind 0 = rcode (RCodeNumbers) or 1 = qtype (QTypeNumbers),
+ * case-insensitive, libs/visor_dns/dns.h:31-265; PV_EINVAL if unknown. Pure host function. */
+int pv_dns_code(int kind, const char *name, uint32_t *value);
+
 /* Result of one host-side walk over a run of classic-pcap records. */
 typedef struct pv_index_info {
     uint64_t n_records;      /* records indexed */

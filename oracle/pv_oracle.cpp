@@ -339,6 +339,13 @@ struct Config {
     uint32_t xact_ttl_ms = 5000;
     bool dns_details = false; // enable top_qnames_details group
     bool recorded_stream = true;
+    // DNS v1 filters (DnsStreamHandler::start, dns/v1/DnsStreamHandler.cpp:60-160)
+    bool exclude_noerror = false;   // "exclude_noerror" (:61-63)
+    uint32_t only_rcode_mask = 0;   // "only_rcode": bit r set = rcode r wanted (:64-113); predicate mode
+    bool has_answer_count = false;  // "answer_count" (:123-130)
+    uint32_t answer_count = 0;
+    bool only_queries = false, only_responses = false; // (:114-119)
+    std::vector<uint16_t> only_qtype;                   // "only_qtype" (:131-150)
 };
 
 // libs/visor_utils/utils.cpp:128-164
@@ -894,6 +901,28 @@ struct Engine {
         uint8_t rcode = h[3] & 0x0f;
         uint16_t ancount = rd16be(h + 6);
 
+        // only_rcode installs a UDP predicate in the input proxy (dns/v1 ...cpp:485-508): a
+        // non-response or a response whose rcode is not listed never reaches the handler
+        if (cfg.only_rcode_mask && !cfg.exclude_noerror && (!qr || !((cfg.only_rcode_mask >> rcode) & 1))) return;
+        // DnsStreamHandler::_filtering (:538-648) in its order; a filtered packet is
+        // process_filtered: an event without a sample of its own and the `filtered` counter
+        bool filt = false;
+        if (cfg.exclude_noerror && rcode == 0) filt = true;
+        else if (cfg.has_answer_count && ancount != cfg.answer_count) filt = true;
+        else if (cfg.only_queries && qr) filt = true;
+        else if (cfg.only_responses && !qr) filt = true;
+        else if (!cfg.only_qtype.empty()) {
+            DnsParse fr = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{hdr_buf, m.len});
+            if (!fr.ok || !fr.has_query) filt = true;
+            else if (std::find(cfg.only_qtype.begin(), cfg.only_qtype.end(), fr.qtype) == cfg.only_qtype.end()) filt = true;
+        }
+        if (filt) {
+            if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
+            dns.new_event(true);
+            dns.live().filtered++;
+            return;
+        }
+
         // DnsMetricsManager::process_dns_layer (:1350-1370)
         if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
         dns.new_event(true);
@@ -1212,6 +1241,20 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "topn_count") c.topn_count = (size_t)atoll(v.c_str());
         else if (k == "xact_ttl_ms") c.xact_ttl_ms = (uint32_t)atoll(v.c_str());
         else if (k == "dns_details") c.dns_details = atoi(v.c_str()) != 0;
+        else if (k == "exclude_noerror") c.exclude_noerror = atoi(v.c_str()) != 0;
+        else if (k == "only_rcode_mask") c.only_rcode_mask = (uint32_t)strtoul(v.c_str(), nullptr, 0);
+        else if (k == "answer_count") { c.has_answer_count = true; c.answer_count = (uint32_t)atoll(v.c_str()); }
+        else if (k == "only_queries") c.only_queries = atoi(v.c_str()) != 0;
+        else if (k == "only_responses") c.only_responses = atoi(v.c_str()) != 0;
+        else if (k == "only_qtype") {
+            size_t q = 0;
+            while (q < v.size()) {
+                size_t e2 = v.find(',', q);
+                std::string t = v.substr(q, e2 == std::string::npos ? std::string::npos : e2 - q);
+                if (!t.empty()) c.only_qtype.push_back((uint16_t)atoi(t.c_str()));
+                q = e2 == std::string::npos ? v.size() : e2 + 1;
+            }
+        }
         else { err = "unknown config key: " + k; return false; }
     }
     return true;

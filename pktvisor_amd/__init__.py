@@ -49,6 +49,76 @@ class pv_config(ctypes.Structure):
                 ("table_log2", ctypes.c_uint32), ("max_records", ctypes.c_uint64)]
 
 
+class pv_dns_filters(ctypes.Structure):
+    _fields_ = [("exclude_noerror", ctypes.c_uint32), ("only_rcode_mask", ctypes.c_uint32),
+                ("answer_count", ctypes.c_int32), ("only_queries", ctypes.c_uint32), ("only_responses", ctypes.c_uint32),
+                ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16)]
+
+
+class ConfigError(PvError):
+    """The reference's ConfigException (src/Configurable.h), same messages."""
+
+
+DNS_FILTER_KEYS = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype")
+DNS_FILTER_NOT_BUILT = ("only_dnssec_response", "only_qname", "only_qname_suffix", "geoloc_notfound", "asn_notfound",
+                        "dnstap_msg_type", "public_suffix_list")
+
+
+def _dns_code(kind: int, name: str):
+    v = ctypes.c_uint32()
+    return int(v.value) if load_library().pv_dns_code(kind, str(name).encode(), ctypes.byref(v)) == 0 else None
+
+
+def dns_filter_config(cfg: dict) -> dict:
+    """DnsStreamHandler::start's filter setup (src/handlers/dns/v1/DnsStreamHandler.cpp:60-150):
+    typed values in, the pv_dns_filters fields out; ConfigError with the reference's text."""
+    out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[])
+    for k in cfg:
+        if k in DNS_FILTER_NOT_BUILT:
+            raise ConfigError(f"DnsStreamHandler: filter {k} is not supported by the GPU handler")
+        if k not in DNS_FILTER_KEYS:
+            raise ConfigError(f"{k} is an invalid/unsupported config or filter. The valid configs/filters are: "
+                              + ", ".join(DNS_FILTER_KEYS))
+    if cfg.get("exclude_noerror"):
+        out["exclude_noerror"] = 1
+    elif "only_rcode" in cfg:
+        v = cfg["only_rcode"]
+        if isinstance(v, bool) or not isinstance(v, (int, list, tuple)):
+            raise ConfigError("DnsStreamHandler: wrong value type for only_rcode filter. It should be an integer or an array")
+        if isinstance(v, int):
+            if _dns_code(0, str(v)) is None:
+                raise ConfigError("DnsStreamHandler: only_rcode filter contained an invalid/unsupported rcode")
+            codes = [v]
+        else:
+            codes = []
+            for r in v:
+                c = _dns_code(0, r)
+                if c is None:
+                    raise ConfigError(f"DnsStreamHandler: only_rcode filter contained an invalid/unsupported rcode: {r}")
+                codes.append(c)
+        for c in codes:
+            if c > 15:  # a DNS header carries a 4-bit rcode; the reference accepts these but never matches them
+                raise ConfigError("DnsStreamHandler: only_rcode filter contained an invalid/unsupported rcode")
+            out["only_rcode_mask"] |= 1 << c
+    if cfg.get("only_queries"):
+        out["only_queries"] = 1
+    if cfg.get("only_responses"):
+        out["only_responses"] = 1
+    if "answer_count" in cfg:
+        v = cfg["answer_count"]
+        if isinstance(v, bool) or not isinstance(v, int):
+            raise ConfigError("DnsStreamHandler: wrong value type for answer_count filter. It should be an integer")
+        out["answer_count"] = v
+    for q in cfg.get("only_qtype", []):
+        c = _dns_code(1, q)
+        if c is None:
+            raise ConfigError(f"DnsStreamHandler: only_qtype filter contained an invalid/unsupported qtype: {q}")
+        out["only_qtype"].append(c)
+    if len(out["only_qtype"]) > 16:
+        raise ConfigError("DnsStreamHandler: only_qtype: at most 16 qtypes")
+    return out
+
+
 class pv_index_info(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint64), ("bytes_used", ctypes.c_uint64), ("first_sec", ctypes.c_int64),
                 ("first_nsec", ctypes.c_int64), ("last_sec", ctypes.c_int64), ("last_nsec", ctypes.c_int64),
@@ -61,7 +131,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_reset", "pv_window_json", "pv_free", "pv_state_regions", "pv_set_global_base", "pv_export_topn",
            "pv_merge_topn", "pv_kernel_timing", "pv_window_slots", "pv_index_records_mt", "pv_host_register",
            "pv_host_unregister", "pv_ingest_timing", "pv_edge_export", "pv_edge_merge", "pv_values_export",
-           "pv_values_merge", "pv_window_periods"]
+           "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code"]
 
 _lib = None
 
@@ -112,6 +182,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_values_merge.argtypes = [P, P, ctypes.c_size_t]
     lib.pv_window_periods.argtypes = [P, P, P, U32, ctypes.POINTER(U32)]
+    lib.pv_set_dns_filters.argtypes = [P, ctypes.POINTER(pv_dns_filters)]
+    lib.pv_dns_code.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(U32)]
     _lib = lib
     return lib
 
@@ -169,8 +241,10 @@ class PvHandlers:
 
     def __init__(self, host_spec: Optional[str] = None, num_periods: int = 5, topn_count: int = 10,
                  xact_ttl_ms: int = 5000, linktype: int = 1, ts_nano: int = 0, device: int = -1,
-                 table_log2: int = 0, max_records: int = 1 << 20, net_groups: int = 0, dns_groups: int = 0):
+                 table_log2: int = 0, max_records: int = 1 << 20, net_groups: int = 0, dns_groups: int = 0,
+                 dns_filters: Optional[dict] = None):
         self.lib = load_library()
+        filt = dns_filter_config(dns_filters) if dns_filters else None
         self._host = host_spec.encode() if host_spec else None
         cfg = pv_config(self._host, num_periods, topn_count, xact_ttl_ms, net_groups, dns_groups, linktype, ts_nano,
                         device, table_log2, max_records)
@@ -182,6 +256,12 @@ class PvHandlers:
             self.lib.pv_destroy(self.ctx)
             self.ctx = None
             raise PvError(f"pv_create failed ({rc}): {msg}")
+        if filt:
+            f = pv_dns_filters(filt["exclude_noerror"], filt["only_rcode_mask"], filt["answer_count"],
+                               filt["only_queries"], filt["only_responses"], len(filt["only_qtype"]))
+            for k, q in enumerate(filt["only_qtype"]):
+                f.qtypes[k] = q
+            self._check(self.lib.pv_set_dns_filters(self.ctx, ctypes.byref(f)), "pv_set_dns_filters")
 
     def _check(self, rc, what):
         if rc:

@@ -25,6 +25,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -295,6 +296,9 @@ struct pv_ctx {
     size_t xvals_synced = 0;
     float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
     uint32_t *d_status = nullptr;
+    // DNS v1 filters (pv_set_dns_filters): PVF_* bits, only_rcode mask, answer_count, only_qtype
+    uint32_t f_flags = 0, f_rcode_mask = 0, f_ancount = 0, f_nq = 0;
+    uint16_t f_qt[PV_MAX_QTYPES] = {};
     PvParams *d_params = nullptr;      // kernel parameter blocks (device memory)
     // pinned host mirrors of the per-batch uploads and the status read-back (direct DMA,
     // no pageable staging copy on the stream)
@@ -863,6 +867,56 @@ const char *pv_last_error(const pv_ctx *ctx) { return ctx ? ctx->err.c_str() : "
 
 void pv_free(void *p) { free(p); }
 
+int pv_dns_code(int kind, const char *name, uint32_t *value)
+{
+    if (!name || !value || (kind != 0 && kind != 1)) return PV_EINVAL;
+    const auto &m = kind == 0 ? rcode_names() : qtype_names();
+    std::string n(name);
+    if (n.empty()) return PV_EINVAL;
+    if (std::all_of(n.begin(), n.end(), [](unsigned char ch) { return std::isdigit(ch); })) {
+        if (n.size() > 6) return PV_EINVAL;
+        const unsigned long v = std::stoul(n);
+        if (!m.count((uint16_t)v) || v > 65535) return PV_EINVAL;
+        *value = (uint32_t)v;
+        return 0;
+    }
+    std::transform(n.begin(), n.end(), n.begin(), [](unsigned char ch) { return (char)std::toupper(ch); });
+    for (const auto &kv : m)
+        if (n == kv.second) { *value = kv.first; return 0; }
+    return PV_EINVAL;
+}
+
+int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
+{
+    if (!c) return PV_EINVAL;
+    if (c->records_seen) return c->fail(PV_EINVAL, "DNS filters must be set before the first batch");
+    if (!f) { c->f_flags = c->f_rcode_mask = c->f_ancount = c->f_nq = 0; return 0; }
+    uint32_t fl = 0;
+    if (f->exclude_noerror) fl |= PVDF_EXCLUDE_NOERROR;
+    else if (f->only_rcode_mask) {
+        for (uint32_t r = 0; r < 32; r++)
+            if ((f->only_rcode_mask >> r) & 1 && (r > 15 || !rcode_names().count((uint16_t)r)))
+                // a DNS header carries a 4-bit rcode: extended rcodes can never match
+                return c->fail(PV_EINVAL, "DnsStreamHandler: only_rcode filter contained an invalid/unsupported rcode");
+        fl |= PVDF_ONLY_RCODE;
+    }
+    if (f->answer_count >= 0) fl |= PVDF_ANSWER_COUNT;
+    if (f->only_queries) fl |= PVDF_ONLY_QUERIES;
+    if (f->only_responses) fl |= PVDF_ONLY_RESPONSES;
+    if (f->n_qtypes > PV_MAX_QTYPES) return c->fail(PV_EINVAL, "only_qtype: at most %d qtypes", PV_MAX_QTYPES);
+    for (uint32_t k = 0; k < f->n_qtypes; k++)
+        if (!qtype_names().count(f->qtypes[k]))
+            return c->fail(PV_EINVAL, "DnsStreamHandler: only_qtype filter contained an invalid/unsupported qtype: %u",
+                           (unsigned)f->qtypes[k]);
+    if (f->n_qtypes) fl |= PVDF_ONLY_QTYPE;
+    c->f_flags = fl;
+    c->f_rcode_mask = (fl & PVDF_ONLY_RCODE) ? f->only_rcode_mask : 0;
+    c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
+    c->f_nq = f->n_qtypes;
+    for (uint32_t k = 0; k < f->n_qtypes; k++) c->f_qt[k] = f->qtypes[k];
+    return 0;
+}
+
 int pv_create(const pv_config *cfg, pv_ctx **out)
 {
     *out = nullptr;
@@ -1145,6 +1199,11 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.svals = c->d_svals;
     P.n_events = c->d_status + ST_NEV; // [0] packed total, [1] responses (ST_NRESP)
     P.want_events = (c->dns_groups & PV_DNS_TRANSACTIONS) ? 1 : 0;
+    P.f_flags = c->f_flags;
+    P.f_rcode_mask = c->f_rcode_mask;
+    P.f_ancount = c->f_ancount;
+    P.f_nq = c->f_nq;
+    for (uint32_t k = 0; k < c->f_nq; k++) P.f_qt[k] = c->f_qt[k];
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
     if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0xffffffffull)
@@ -1267,6 +1326,14 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     // pairs (sort + resolve) its events together with the queries carried in; a batch of
     // queries only just appends them to the carried list
     const bool dns_here = nev_b > 0;
+    // DNS events of any kind (a filtered event or, with transactions off, any event leaves no
+    // transaction record but still drives the DNS window: AbstractMetricsManager::new_event)
+    const bool dns_evt = dns_here || status[ST_DNS_ANY];
+    if (dns_evt)
+        for (uint32_t k = 1; k <= P.n_shift; k++)
+            if (!status[ST_DNS_AT + k])
+                return c->fail(PV_EUNSUPPORTED, "DNS period boundary differs from the Net boundary at second %lld",
+                               (long long)thresh[k - 1]);
     bool pair = dns_here && (nresp > 0 || P.n_shift > 0);
     if (dns_here && !pair && c->n_pend + nev_b > c->pend_cap) pair = true; // compact the carried list
     if (dns_here && !pair) {
@@ -1276,11 +1343,6 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         c->n_pend += nev_b;
     }
     if (pair) {
-        // (DNS events exist in this batch) every Net shift must coincide with a DNS event second
-        for (uint32_t k = 1; k <= P.n_shift; k++)
-            if (!status[ST_DNS_AT + k])
-                return c->fail(PV_EUNSUPPORTED, "DNS period boundary differs from the Net boundary at second %lld",
-                               (long long)thresh[k - 1]);
         const uint32_t np_in = (uint32_t)c->n_pend;
         if (np_in) {
             hipLaunchKernelGGL(pv_xact_pend_in, dim3((np_in + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
@@ -1384,7 +1446,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         c->net.slots.push_front(s);
         if (c->net.slots.size() > np) c->net.slots.pop_back();
         c->net.next_shift_sec = T + 60;
-        if (dns_here) {
+        if (dns_evt) {
             c->dns_shifts.emplace_back(T, s);
             c->dns.slots.push_front(s);
             if (c->dns.slots.size() > np) c->dns.slots.pop_back();

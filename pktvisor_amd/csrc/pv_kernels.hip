@@ -339,14 +339,15 @@ __device__ void net_flush(PV_CREF(PvParams) P, uint32_t s, NetCtr &c)
 }
 // DNS v1 counters of the wave's current slot
 struct DnsCtr {
-    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata;
-    __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = 0; }
+    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata, dfilt;
+    __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = dfilt = 0; }
 };
 __device__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
 {
     const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
-    PV_FLUSH1(s, PV_OFF_DNS + DC_EVENTS, c.dev, true) PV_FLUSH1(s, PV_OFF_DNS + DC_SAMPLES, c.dev, true)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_EVENTS, c.dev + c.dfilt, true) PV_FLUSH1(s, PV_OFF_DNS + DC_SAMPLES, c.dev + c.dfilt, true)
     PV_FLUSH1(s, PV_OFF_DNS + DC_TOTAL, c.dev, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_UDP, c.dev, dc)
+    if (P.f_flags) PV_FLUSH1(s, PV_OFF_DNS + DC_FILTERED, c.dfilt, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_QUERIES, c.dq, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REPLIES, c.dr, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_V4, c.d4, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_V6, c.d6, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_NX, c.dnx, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REFUSED, c.dref, dc)
@@ -463,6 +464,37 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     const uint32_t ancount = ((w1 >> 8) & 0xff00) | (w1 >> 24);
     const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
     const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+    if (P.f_flags) {
+        // only_rcode is the input proxy's UDP predicate (dns/v1/DnsStreamHandler.cpp:485-508):
+        // a query, or a response with an unlisted rcode, never reaches the handler (no event)
+        if ((P.f_flags & PVDF_ONLY_RCODE) && (!qr || !((P.f_rcode_mask >> rcode) & 1))) return;
+        // DnsStreamHandler::_filtering (:538-648), in its order
+        bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
+                    ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
+                    ((P.f_flags & PVDF_ONLY_QUERIES) && qr) || ((P.f_flags & PVDF_ONLY_RESPONSES) && !qr);
+        if (!filt && (P.f_flags & PVDF_ONLY_QTYPE)) {
+            DnsInfo fd;
+            dns_parse(R, m, dlen, qd, ancount, ns, ar, fd);
+            bool hit = false;
+            for (uint32_t k = 0; k < P.f_nq; k++) hit |= fd.qtype == P.f_qt[k];
+            filt = !fd.ok || !fd.has_query || !hit;
+        }
+        if (filt) {
+            // process_filtered (:1341-1347): an event (sampled at rate 100) and `filtered`
+            if (upd) {
+                if (own) c.dfilt++;
+                else {
+                    sum_add(P, slot, PV_OFF_DNS + DC_EVENTS, 1);
+                    sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
+                    if (P.dns_groups & PV_DNS_COUNTERS_BIT) sum_add(P, slot, PV_OFF_DNS + DC_FILTERED, 1);
+                }
+            }
+            P.dns_first[0] = 1; // a DNS event without a transaction record: the DNS window moves
+            if (period > 0 && (int64_t)dm.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
+            return;
+        }
+    }
+    if (!P.want_events) P.dns_first[0] = 1;
     // top-N / dense update: cache, else log (hashed) or HBM atomic (dense); boundary: global table
     auto top = [&](uint32_t metric, uint64_t payload, uint32_t w) {
         const uint64_t key = PV_KEY(metric, payload);

@@ -152,6 +152,10 @@ struct PvSubnets {
     uint32_t v6_cidr[PV_MAX_SUBNETS];
 };
 
+// DNS filter bits (PvParams::f_flags)
+#define PV_MAX_QTYPES 16
+enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
+       PVDF_ONLY_QTYPE = 32 };
 struct PvParams {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
@@ -215,6 +219,9 @@ struct PvParams {
     PV_G uint32_t *flags;
     PV_G uint32_t *dns_first; // per period: min record index of a DNS event in that period
     PV_G uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
+    // DNS v1 filters (DnsStreamHandler::_filtering, dns/v1/DnsStreamHandler.cpp:538-648)
+    uint32_t f_flags, f_rcode_mask, f_ancount, f_nq;
+    uint16_t f_qt[PV_MAX_QTYPES];
 };
 
 // pv_fill_multi's segment list (kernel argument)

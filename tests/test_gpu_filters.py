@@ -1,0 +1,104 @@
+"""DNS v1 filters on the GPU path (pv_set_dns_filters through the C-ABI) against the oracle,
+bit-exact, and against the reference's filter known-answer tests
+(src/handlers/dns/v1/tests/test_dns_layer.cpp:271-366,524-705)."""
+import os
+
+import pytest
+
+import pktvisor_amd as pa
+from pktvisor_amd import synth
+from tests.test_gpu_parity import diff
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+# handler config (reference key names / typed values) for each case
+FILTERS = [
+    {"exclude_noerror": True},
+    {"only_rcode": 3},
+    {"only_rcode": ["nxdomain", "5"]},
+    {"only_rcode": 0, "answer_count": 0},
+    {"only_queries": True},
+    {"only_responses": True},
+    {"only_qtype": ["AAAA", "TxT"]},
+    {"only_qtype": ["A", "MX"], "only_responses": True},
+    {"answer_count": 2},
+]
+IDS = ["exclude_noerror", "rcode_nx", "rcode_nx_refused", "rcode_noerror_an0", "only_queries", "only_responses",
+       "qtype_aaaa_txt", "qtype_a_mx_resp", "an2"]
+
+
+def oracle_kw(f):
+    """the oracle's typed filter keys (oracle/pv_oracle.cpp parse_config)"""
+    t = pa.dns_filter_config(f)
+    kw = {}
+    if t["exclude_noerror"]:
+        kw["exclude_noerror"] = 1
+    if t["only_rcode_mask"]:
+        kw["only_rcode_mask"] = t["only_rcode_mask"]
+    if t["answer_count"] >= 0:
+        kw["answer_count"] = t["answer_count"]
+    if t["only_queries"]:
+        kw["only_queries"] = 1
+    if t["only_responses"]:
+        kw["only_responses"] = 1
+    if t["only_qtype"]:
+        kw["only_qtype"] = ",".join(map(str, t["only_qtype"]))
+    return kw
+
+
+def run_both(oracle, pcap: bytes, host: str, periods: int, tmp_path, f):
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec=host or None, periods=periods, dns_filters=f)
+    ref = oracle.run_bytes(pcap, host_spec=host, num_periods=periods, window=periods, **oracle_kw(f))
+    return gpu, ref
+
+
+@pytest.mark.parametrize("f", FILTERS, ids=IDS)
+@pytest.mark.parametrize("fixture,host", [("dns_udp_mixed_rcode.pcap", "192.168.0.0/24"),
+                                          ("dns_udp_tcp_random.pcap", "192.168.0.0/24"), ("dns_ipv6_udp.pcap", "")],
+                         ids=["mixed_rcode", "udp_tcp_random", "ipv6_udp"])
+def test_filter_fixture_parity(oracle, tmp_path, fixture, host, f):
+    pcap = open(os.path.join(GOLD, fixture), "rb").read()
+    for periods in (1, 5):
+        gpu, ref = run_both(oracle, pcap, host, periods, tmp_path, f)
+        assert diff(gpu, ref) is None, (periods, diff(gpu, ref))
+
+
+@pytest.mark.parametrize("f", FILTERS, ids=IDS)
+def test_filter_synthetic_parity(oracle, tmp_path, f):
+    gpu, ref = run_both(oracle, synth.pcap_bytes(4, 60000), synth.HOST_SPEC, 1, tmp_path, f)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+    gpu, ref = run_both(oracle, synth.pcap_bytes(1, 1000), synth.HOST_SPEC, 5, tmp_path, f)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("f", [{"exclude_noerror": True}, {"only_queries": True}, {"only_qtype": ["AAAA"]}],
+                         ids=["exclude_noerror", "only_queries", "qtype_aaaa"])
+def test_filter_multi_period_parity(oracle, tmp_path, f):
+    # 120k records x 1.5 ms = 180 s: period shifts inside one batch, filtered events shift too
+    gpu, ref = run_both(oracle, synth.pcap_bytes(4, 120000, ts_step_us=1500), synth.HOST_SPEC, 5, tmp_path, f)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_filter_reference_kats(tmp_path):
+    """the reference's own numbers, straight from the GPU path"""
+    path = os.path.join(GOLD, "dns_udp_mixed_rcode.pcap")
+
+    def wp(f):
+        return pa.pktvisor_reader(path, host_spec="192.168.0.0/24", periods=1, dns_filters=f)["1m"]["dns"]
+
+    d = wp({"exclude_noerror": True})["wire_packets"]
+    assert (d["noerror"], d["srvfail"], d["refused"], d["nxdomain"], d["nodata"], d["filtered"]) == (0, 0, 1, 1, 0, 22)
+    d = wp({"only_rcode": 3})["wire_packets"]
+    assert (d["noerror"], d["refused"], d["nxdomain"], d["filtered"]) == (0, 0, 1, 0)
+    d = wp({"only_rcode": ["nxdomain", "5"]})["wire_packets"]
+    assert (d["refused"], d["nxdomain"], d["filtered"]) == (1, 1, 0)
+    d = wp({"only_rcode": 0, "answer_count": 0})["wire_packets"]
+    assert (d["udp"], d["noerror"], d["nodata"], d["filtered"]) == (4, 4, 4, 6)
+    j = wp({"only_queries": True})
+    assert (j["wire_packets"]["udp"], j["wire_packets"]["filtered"]) == (12, 12)
+    assert j["top_qname2"][0]["name"] == ".mwbsys.com" and j["top_qname3"][0]["name"] == "sirius.mwbsys.com"
+    d = wp({"only_responses": True})["wire_packets"]
+    assert (d["udp"], d["noerror"], d["refused"], d["nxdomain"], d["filtered"]) == (12, 10, 1, 1, 12)
