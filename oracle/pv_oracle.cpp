@@ -346,6 +346,7 @@ struct Config {
     uint32_t answer_count = 0;
     bool only_queries = false, only_responses = false; // (:114-119)
     std::vector<uint16_t> only_qtype;                   // "only_qtype" (:131-150)
+    std::vector<std::string> only_qname;                // "only_qname" (:151-160), lower-case; predicate mode
 };
 
 // libs/visor_utils/utils.cpp:128-164
@@ -904,6 +905,12 @@ struct Engine {
         // only_rcode installs a UDP predicate in the input proxy (dns/v1 ...cpp:485-508): a
         // non-response or a response whose rcode is not listed never reaches the handler
         if (cfg.only_rcode_mask && !cfg.exclude_noerror && (!qr || !((cfg.only_rcode_mask >> rcode) & 1))) return;
+        // only_qname's predicate (:509-524): parse failure or no query never matches a listed name
+        if (!cfg.only_qname.empty()) {
+            DnsParse qp = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{hdr_buf, m.len});
+            if (!qp.ok || !qp.has_query) return;
+            if (std::find(cfg.only_qname.begin(), cfg.only_qname.end(), lower(qp.name)) == cfg.only_qname.end()) return;
+        }
         // DnsStreamHandler::_filtering (:538-648) in its order; a filtered packet is
         // process_filtered: an event without a sample of its own and the `filtered` counter
         bool filt = false;
@@ -1246,6 +1253,15 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "answer_count") { c.has_answer_count = true; c.answer_count = (uint32_t)atoll(v.c_str()); }
         else if (k == "only_queries") c.only_queries = atoi(v.c_str()) != 0;
         else if (k == "only_responses") c.only_responses = atoi(v.c_str()) != 0;
+        else if (k == "only_qname") {
+            size_t q = 0;
+            while (q < v.size()) {
+                size_t e2 = v.find(',', q);
+                std::string t = v.substr(q, e2 == std::string::npos ? std::string::npos : e2 - q);
+                if (!t.empty()) c.only_qname.push_back(lower(t));
+                q = e2 == std::string::npos ? v.size() : e2 + 1;
+            }
+        }
         else if (k == "only_qtype") {
             size_t q = 0;
             while (q < v.size()) {

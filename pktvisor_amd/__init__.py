@@ -52,15 +52,17 @@ class pv_config(ctypes.Structure):
 class pv_dns_filters(ctypes.Structure):
     _fields_ = [("exclude_noerror", ctypes.c_uint32), ("only_rcode_mask", ctypes.c_uint32),
                 ("answer_count", ctypes.c_int32), ("only_queries", ctypes.c_uint32), ("only_responses", ctypes.c_uint32),
-                ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16)]
+                ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16), ("n_qnames", ctypes.c_uint32),
+                ("qnames", ctypes.POINTER(ctypes.c_char_p))]
 
 
 class ConfigError(PvError):
     """The reference's ConfigException (src/Configurable.h), same messages."""
 
 
-DNS_FILTER_KEYS = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype")
-DNS_FILTER_NOT_BUILT = ("only_dnssec_response", "only_qname", "only_qname_suffix", "geoloc_notfound", "asn_notfound",
+DNS_FILTER_KEYS = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype",
+                   "only_qname")
+DNS_FILTER_NOT_BUILT = ("only_dnssec_response", "only_qname_suffix", "geoloc_notfound", "asn_notfound",
                         "dnstap_msg_type", "public_suffix_list")
 
 
@@ -72,7 +74,8 @@ def _dns_code(kind: int, name: str):
 def dns_filter_config(cfg: dict) -> dict:
     """DnsStreamHandler::start's filter setup (src/handlers/dns/v1/DnsStreamHandler.cpp:60-150):
     typed values in, the pv_dns_filters fields out; ConfigError with the reference's text."""
-    out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[])
+    out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[],
+               only_qname=[])
     for k in cfg:
         if k in DNS_FILTER_NOT_BUILT:
             raise ConfigError(f"DnsStreamHandler: filter {k} is not supported by the GPU handler")
@@ -114,6 +117,12 @@ def dns_filter_config(cfg: dict) -> dict:
         if c is None:
             raise ConfigError(f"DnsStreamHandler: only_qtype filter contained an invalid/unsupported qtype: {q}")
         out["only_qtype"].append(c)
+    # only_qname (:151-160): lower-cased; an input predicate, as only_rcode is
+    out["only_qname"] = [str(q).lower() for q in cfg.get("only_qname", [])]
+    if out["only_qname"] and out["only_rcode_mask"]:
+        raise ConfigError("DnsStreamHandler: only_qname and only_rcode both install an input predicate: use one")
+    if len(out["only_qname"]) > 8 or any(not q or len(q) > 255 for q in out["only_qname"]):
+        raise ConfigError("DnsStreamHandler: only_qname: 1..8 names of 1..255 characters")
     if len(out["only_qtype"]) > 16:
         raise ConfigError("DnsStreamHandler: only_qtype: at most 16 qtypes")
     return out
@@ -261,6 +270,10 @@ class PvHandlers:
                                filt["only_queries"], filt["only_responses"], len(filt["only_qtype"]))
             for k, q in enumerate(filt["only_qtype"]):
                 f.qtypes[k] = q
+            if filt["only_qname"]:
+                self._qnames = (ctypes.c_char_p * len(filt["only_qname"]))(*[q.encode() for q in filt["only_qname"]])
+                f.n_qnames = len(filt["only_qname"])
+                f.qnames = ctypes.cast(self._qnames, ctypes.POINTER(ctypes.c_char_p))
             self._check(self.lib.pv_set_dns_filters(self.ctx, ctypes.byref(f)), "pv_set_dns_filters")
 
     def _check(self, rc, what):

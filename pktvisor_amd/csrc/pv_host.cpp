@@ -43,6 +43,25 @@
 #include "pv_ingest.h"
 #include "pv_layout.h"
 
+// The kernel's name fingerprint (pv_parse.h NameStats + fp56), compiled for the host so
+// pv_set_dns_filters can key "only_qname" names exactly as the DNS pass keys first-query names.
+namespace pvname {
+#define PV_FN inline
+#define PV_CREF(T) const T &
+inline uint32_t pv_clz64(uint64_t x) { return (uint32_t)__builtin_clzll(x); }
+inline uint32_t pv_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) { return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh)); }
+#include "pv_parse.h"
+#undef PV_FN
+#undef PV_CREF
+inline uint64_t name_fp(const char *s, size_t n)
+{
+    NameStats st;
+    st.init();
+    for (size_t k = 0; k < n; k++) st.put((uint8_t)s[k]);
+    return fp56(st.ph, st.n, 0);
+}
+} // namespace pvname
+
 extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
@@ -299,6 +318,8 @@ struct pv_ctx {
     // DNS v1 filters (pv_set_dns_filters): PVF_* bits, only_rcode mask, answer_count, only_qtype
     uint32_t f_flags = 0, f_rcode_mask = 0, f_ancount = 0, f_nq = 0;
     uint16_t f_qt[PV_MAX_QTYPES] = {};
+    uint32_t f_nqn = 0;
+    uint64_t f_qn[PV_MAX_QNAMES] = {};
     PvParams *d_params = nullptr;      // kernel parameter blocks (device memory)
     // pinned host mirrors of the per-batch uploads and the status read-back (direct DMA,
     // no pageable staging copy on the stream)
@@ -890,7 +911,7 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
 {
     if (!c) return PV_EINVAL;
     if (c->records_seen) return c->fail(PV_EINVAL, "DNS filters must be set before the first batch");
-    if (!f) { c->f_flags = c->f_rcode_mask = c->f_ancount = c->f_nq = 0; return 0; }
+    if (!f) { c->f_flags = c->f_rcode_mask = c->f_ancount = c->f_nq = c->f_nqn = 0; return 0; }
     uint32_t fl = 0;
     if (f->exclude_noerror) fl |= PVDF_EXCLUDE_NOERROR;
     else if (f->only_rcode_mask) {
@@ -909,6 +930,16 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
             return c->fail(PV_EINVAL, "DnsStreamHandler: only_qtype filter contained an invalid/unsupported qtype: %u",
                            (unsigned)f->qtypes[k]);
     if (f->n_qtypes) fl |= PVDF_ONLY_QTYPE;
+    if (f->n_qnames > PV_MAX_QNAMES) return c->fail(PV_EINVAL, "only_qname: at most %d names", PV_MAX_QNAMES);
+    if (f->n_qnames && (fl & PVDF_ONLY_RCODE))
+        return c->fail(PV_EINVAL, "only_qname and only_rcode both install an input predicate: use one");
+    for (uint32_t k = 0; k < f->n_qnames; k++) {
+        const char *q = f->qnames ? f->qnames[k] : nullptr;
+        if (!q || !*q || strlen(q) > 255) return c->fail(PV_EINVAL, "only_qname: empty or over-long name");
+        c->f_qn[k] = pvname::name_fp(q, strlen(q)); // NameStats lower-cases, as only_qname's qname_ci (:151-160)
+    }
+    c->f_nqn = f->n_qnames;
+    if (f->n_qnames) fl |= PVDF_ONLY_QNAME;
     c->f_flags = fl;
     c->f_rcode_mask = (fl & PVDF_ONLY_RCODE) ? f->only_rcode_mask : 0;
     c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
@@ -1204,6 +1235,8 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.f_ancount = c->f_ancount;
     P.f_nq = c->f_nq;
     for (uint32_t k = 0; k < c->f_nq; k++) P.f_qt[k] = c->f_qt[k];
+    P.f_nqn = c->f_nqn;
+    for (uint32_t k = 0; k < c->f_nqn; k++) P.f_qn[k] = c->f_qn[k];
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
     if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0xffffffffull)

@@ -468,6 +468,20 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         // only_rcode is the input proxy's UDP predicate (dns/v1/DnsStreamHandler.cpp:485-508):
         // a query, or a response with an unlisted rcode, never reaches the handler (no event)
         if ((P.f_flags & PVDF_ONLY_RCODE) && (!qr || !((P.f_rcode_mask >> rcode) & 1))) return;
+        // only_qname's predicate (:509-524): the lower-case first-query name must be listed
+        if (P.f_flags & PVDF_ONLY_QNAME) {
+            DnsInfo qi;
+            dns_parse(R, m, dlen, qd, ancount, ns, ar, qi);
+            bool hit = false;
+            if (qi.ok && qi.has_query && qi.name_len_enc > 0) {
+                NameStats st;
+                st.init();
+                name_stats(R, m, dlen, 12, st);
+                const uint64_t fp = fp56(st.ph, st.n, 0);
+                for (uint32_t k = 0; k < P.f_nqn; k++) hit |= st.n > 0 && fp == P.f_qn[k];
+            }
+            if (!hit) return;
+        }
         // DnsStreamHandler::_filtering (:538-648), in its order
         bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
                     ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||

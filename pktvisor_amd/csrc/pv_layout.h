@@ -154,8 +154,9 @@ struct PvSubnets {
 
 // DNS filter bits (PvParams::f_flags)
 #define PV_MAX_QTYPES 16
+#define PV_MAX_QNAMES 8
 enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
-       PVDF_ONLY_QTYPE = 32 };
+       PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64 };
 struct PvParams {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
@@ -222,6 +223,8 @@ struct PvParams {
     // DNS v1 filters (DnsStreamHandler::_filtering, dns/v1/DnsStreamHandler.cpp:538-648)
     uint32_t f_flags, f_rcode_mask, f_ancount, f_nq;
     uint16_t f_qt[PV_MAX_QTYPES];
+    uint32_t f_nqn;
+    uint64_t f_qn[PV_MAX_QNAMES]; // only_qname: name fingerprints (fp56 of the lower-case name)
 };
 
 // pv_fill_multi's segment list (kernel argument)

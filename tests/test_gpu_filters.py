@@ -23,9 +23,11 @@ FILTERS = [
     {"only_qtype": ["AAAA", "TxT"]},
     {"only_qtype": ["A", "MX"], "only_responses": True},
     {"answer_count": 2},
+    {"only_qname": ["play.GooGle.com", "nonexistent.google.com"]},
+    {"only_qname": ["play.google.com"], "only_responses": True},
 ]
 IDS = ["exclude_noerror", "rcode_nx", "rcode_nx_refused", "rcode_noerror_an0", "only_queries", "only_responses",
-       "qtype_aaaa_txt", "qtype_a_mx_resp", "an2"]
+       "qtype_aaaa_txt", "qtype_a_mx_resp", "an2", "qname", "qname_resp"]
 
 
 def oracle_kw(f):
@@ -44,6 +46,8 @@ def oracle_kw(f):
         kw["only_responses"] = 1
     if t["only_qtype"]:
         kw["only_qtype"] = ",".join(map(str, t["only_qtype"]))
+    if t["only_qname"]:
+        kw["only_qname"] = ",".join(t["only_qname"])
     return kw
 
 
@@ -82,6 +86,19 @@ def test_filter_multi_period_parity(oracle, tmp_path, f):
     assert diff(gpu, ref) is None, diff(gpu, ref)
 
 
+def test_only_qname_synthetic(oracle, tmp_path):
+    """only_qname over names the synthetic stream holds (taken from the unfiltered oracle run's
+    full-name tops), mixed case in the config"""
+    pcap = synth.pcap_bytes(4, 60000)
+    full = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=1, window=1)["1m"]["dns"]
+    names = [e["name"] for e in full["top_nxdomain"][:2] + full["top_refused"][:2]]
+    assert names
+    f = {"only_qname": [n.upper() for n in names] + ["absent.example"]}
+    gpu, ref = run_both(oracle, pcap, synth.HOST_SPEC, 1, tmp_path, f)
+    assert ref["1m"]["dns"]["wire_packets"]["total"] > 0
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
 def test_filter_reference_kats(tmp_path):
     """the reference's own numbers, straight from the GPU path"""
     path = os.path.join(GOLD, "dns_udp_mixed_rcode.pcap")
@@ -100,5 +117,9 @@ def test_filter_reference_kats(tmp_path):
     j = wp({"only_queries": True})
     assert (j["wire_packets"]["udp"], j["wire_packets"]["filtered"]) == (12, 12)
     assert j["top_qname2"][0]["name"] == ".mwbsys.com" and j["top_qname3"][0]["name"] == "sirius.mwbsys.com"
+    j = wp({"only_qname": ["play.GooGle.com", "nonexistent.google.com"]})
+    d = j["wire_packets"]
+    assert (d["udp"], d["noerror"], d["nxdomain"], d["nodata"], d["total"], d["filtered"]) == (6, 2, 1, 2, 6, 0)
+    assert j["top_qname2"][0]["name"] == ".google.com" and j["top_qname3"][0]["name"] == "play.google.com"
     d = wp({"only_responses": True})["wire_packets"]
     assert (d["udp"], d["noerror"], d["refused"], d["nxdomain"], d["filtered"]) == (12, 10, 1, 1, 12)

@@ -10,6 +10,9 @@ MIXED = os.path.join(GOLD, "dns_udp_mixed_rcode.pcap")
 
 # (cite, oracle filter config, expected wire_packets counters, expected top names)
 KAT = [
+    ("test_dns_layer.cpp:446-483 only_qname (predicate)", dict(only_qname="play.GooGle.com,nonexistent.google.com"),
+     dict(udp=6, noerror=2, srvfail=0, refused=0, nxdomain=1, nodata=2, total=6, filtered=0),
+     dict(top_qname2=".google.com", top_qname3="play.google.com")),
     ("test_dns_layer.cpp:271-302 exclude_noerror", dict(exclude_noerror=1),
      dict(noerror=0, srvfail=0, refused=1, nxdomain=1, nodata=0, filtered=22), {}),
     ("test_dns_layer.cpp:304-334 only_rcode nx (predicate)", dict(only_rcode_mask=1 << 3),
@@ -59,5 +62,6 @@ def test_filter_config_parsing():
         with pytest.raises(ConfigError) as e:
             dns_filter_config(cfg)
         assert str(e.value) == msg
+    assert dns_filter_config({"only_qname": ["play.GooGle.com"]})["only_qname"] == ["play.google.com"]
     with pytest.raises(ConfigError):
-        dns_filter_config({"only_qname": ["example.com"]})  # not built on the GPU path: refused loudly
+        dns_filter_config({"only_qname_suffix": ["google.com"]})  # not built on the GPU path: refused loudly
