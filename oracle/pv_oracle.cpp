@@ -347,6 +347,7 @@ struct Config {
     bool only_queries = false, only_responses = false; // (:114-119)
     std::vector<uint16_t> only_qtype;                   // "only_qtype" (:131-150)
     std::vector<std::string> only_qname;                // "only_qname" (:151-160), lower-case; predicate mode
+    std::vector<std::string> only_qname_suffix;         // "only_qname_suffix" (:161-169), lower-case
 };
 
 // libs/visor_utils/utils.cpp:128-164
@@ -923,6 +924,22 @@ struct Engine {
             if (!fr.ok || !fr.has_query) filt = true;
             else if (std::find(cfg.only_qtype.begin(), cfg.only_qtype.end(), fr.qtype) == cfg.only_qtype.end()) filt = true;
         }
+        // only_qname_suffix (:615-630): the first listed suffix the name ends with sets suffix_size
+        size_t suffix_size = 0;
+        if (!filt && !cfg.only_qname_suffix.empty()) {
+            DnsParse sp = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{hdr_buf, m.len});
+            bool hit = false;
+            if (sp.ok && sp.has_query) {
+                const std::string nl = lower(sp.name);
+                for (const auto &sfx : cfg.only_qname_suffix)
+                    if (nl.size() >= sfx.size() && nl.compare(nl.size() - sfx.size(), sfx.size(), sfx) == 0) {
+                        suffix_size = sfx.size();
+                        hit = true;
+                        break;
+                    }
+            }
+            filt = !hit;
+        }
         if (filt) {
             if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
             dns.new_event(true);
@@ -970,7 +987,7 @@ struct Engine {
                     if (cfg.dns_details) b.sized_resp.update(name_lower, m.len);
                 }
                 std::string q2, q3;
-                aggregate_domain(name_lower, 0, q2, q3);
+                aggregate_domain(name_lower, suffix_size, q2, q3);
                 b.qname2.update(q2);
                 if (!q3.empty()) b.qname3.update(q3);
             }
@@ -1253,6 +1270,14 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "answer_count") { c.has_answer_count = true; c.answer_count = (uint32_t)atoll(v.c_str()); }
         else if (k == "only_queries") c.only_queries = atoi(v.c_str()) != 0;
         else if (k == "only_responses") c.only_responses = atoi(v.c_str()) != 0;
+        else if (k == "only_qname_suffix") {
+            size_t q = 0;
+            while (q < v.size()) {
+                size_t e2 = v.find(',', q);
+                c.only_qname_suffix.push_back(lower(v.substr(q, e2 == std::string::npos ? std::string::npos : e2 - q)));
+                q = e2 == std::string::npos ? v.size() : e2 + 1;
+            }
+        }
         else if (k == "only_qname") {
             size_t q = 0;
             while (q < v.size()) {

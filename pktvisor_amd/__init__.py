@@ -53,7 +53,8 @@ class pv_dns_filters(ctypes.Structure):
     _fields_ = [("exclude_noerror", ctypes.c_uint32), ("only_rcode_mask", ctypes.c_uint32),
                 ("answer_count", ctypes.c_int32), ("only_queries", ctypes.c_uint32), ("only_responses", ctypes.c_uint32),
                 ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16), ("n_qnames", ctypes.c_uint32),
-                ("qnames", ctypes.POINTER(ctypes.c_char_p))]
+                ("qnames", ctypes.POINTER(ctypes.c_char_p)), ("n_qname_suffixes", ctypes.c_uint32),
+                ("qname_suffixes", ctypes.POINTER(ctypes.c_char_p))]
 
 
 class ConfigError(PvError):
@@ -61,8 +62,8 @@ class ConfigError(PvError):
 
 
 DNS_FILTER_KEYS = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype",
-                   "only_qname")
-DNS_FILTER_NOT_BUILT = ("only_dnssec_response", "only_qname_suffix", "geoloc_notfound", "asn_notfound",
+                   "only_qname", "only_qname_suffix")
+DNS_FILTER_NOT_BUILT = ("only_dnssec_response", "geoloc_notfound", "asn_notfound",
                         "dnstap_msg_type", "public_suffix_list")
 
 
@@ -75,7 +76,7 @@ def dns_filter_config(cfg: dict) -> dict:
     """DnsStreamHandler::start's filter setup (src/handlers/dns/v1/DnsStreamHandler.cpp:60-150):
     typed values in, the pv_dns_filters fields out; ConfigError with the reference's text."""
     out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[],
-               only_qname=[])
+               only_qname=[], only_qname_suffix=[])
     for k in cfg:
         if k in DNS_FILTER_NOT_BUILT:
             raise ConfigError(f"DnsStreamHandler: filter {k} is not supported by the GPU handler")
@@ -123,6 +124,10 @@ def dns_filter_config(cfg: dict) -> dict:
         raise ConfigError("DnsStreamHandler: only_qname and only_rcode both install an input predicate: use one")
     if len(out["only_qname"]) > 8 or any(not q or len(q) > 255 for q in out["only_qname"]):
         raise ConfigError("DnsStreamHandler: only_qname: 1..8 names of 1..255 characters")
+    # only_qname_suffix (:161-169): lower-cased, first match wins
+    out["only_qname_suffix"] = [str(q).lower() for q in cfg.get("only_qname_suffix", [])]
+    if len(out["only_qname_suffix"]) > 4:
+        raise ConfigError("DnsStreamHandler: only_qname_suffix: at most 4 suffixes")
     if len(out["only_qtype"]) > 16:
         raise ConfigError("DnsStreamHandler: only_qtype: at most 16 qtypes")
     return out
@@ -274,6 +279,11 @@ class PvHandlers:
                 self._qnames = (ctypes.c_char_p * len(filt["only_qname"]))(*[q.encode() for q in filt["only_qname"]])
                 f.n_qnames = len(filt["only_qname"])
                 f.qnames = ctypes.cast(self._qnames, ctypes.POINTER(ctypes.c_char_p))
+            if filt["only_qname_suffix"]:
+                sx = filt["only_qname_suffix"]
+                self._qsfx = (ctypes.c_char_p * len(sx))(*[q.encode() for q in sx])
+                f.n_qname_suffixes = len(sx)
+                f.qname_suffixes = ctypes.cast(self._qsfx, ctypes.POINTER(ctypes.c_char_p))
             self._check(self.lib.pv_set_dns_filters(self.ctx, ctypes.byref(f)), "pv_set_dns_filters")
 
     def _check(self, rc, what):

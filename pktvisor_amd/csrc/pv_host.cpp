@@ -53,6 +53,12 @@ inline uint32_t pv_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) { return (ui
 #include "pv_parse.h"
 #undef PV_FN
 #undef PV_CREF
+inline uint64_t name_ph(const char *s, size_t n) // polynomial hash of the lower-case string
+{
+    uint64_t ph = 0;
+    for (size_t k = 0; k < n; k++) ph = ph_step(ph, lower((uint8_t)s[k]));
+    return ph;
+}
 inline uint64_t name_fp(const char *s, size_t n)
 {
     NameStats st;
@@ -64,6 +70,7 @@ inline uint64_t name_fp(const char *s, size_t n)
 
 extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
+extern "C" __global__ void pv_dns_suffix(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_fill_multi(PvFillList L);
@@ -320,6 +327,9 @@ struct pv_ctx {
     uint16_t f_qt[PV_MAX_QTYPES] = {};
     uint32_t f_nqn = 0;
     uint64_t f_qn[PV_MAX_QNAMES] = {};
+    uint8_t *d_sfx = nullptr; // only_qname_suffix: suffix_size per record of the batch (names kernels)
+    uint32_t f_nsx = 0, f_sxl[PV_MAX_SUFFIXES] = {};
+    uint64_t f_sxh[PV_MAX_SUFFIXES] = {};
     PvParams *d_params = nullptr;      // kernel parameter blocks (device memory)
     // pinned host mirrors of the per-batch uploads and the status read-back (direct DMA,
     // no pageable staging copy on the stream)
@@ -911,7 +921,7 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
 {
     if (!c) return PV_EINVAL;
     if (c->records_seen) return c->fail(PV_EINVAL, "DNS filters must be set before the first batch");
-    if (!f) { c->f_flags = c->f_rcode_mask = c->f_ancount = c->f_nq = c->f_nqn = 0; return 0; }
+    if (!f) { c->f_flags = c->f_rcode_mask = c->f_ancount = c->f_nq = c->f_nqn = c->f_nsx = 0; return 0; }
     uint32_t fl = 0;
     if (f->exclude_noerror) fl |= PVDF_EXCLUDE_NOERROR;
     else if (f->only_rcode_mask) {
@@ -940,6 +950,27 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
     }
     c->f_nqn = f->n_qnames;
     if (f->n_qnames) fl |= PVDF_ONLY_QNAME;
+    if (f->n_qname_suffixes > PV_MAX_SUFFIXES)
+        return c->fail(PV_EINVAL, "only_qname_suffix: at most %d suffixes", PV_MAX_SUFFIXES);
+    for (uint32_t k = 0; k < f->n_qname_suffixes; k++) {
+        const char *q = f->qname_suffixes ? f->qname_suffixes[k] : nullptr;
+        if (!q || strlen(q) > 254) return c->fail(PV_EINVAL, "only_qname_suffix: missing or over-long suffix");
+        // aggregateDomain(name, suffix_size) looks for three dots at or before the suffix start;
+        // the DNS pass tracks a name's last four dots, so the suffix may hold one more
+        uint32_t dots = 0;
+        for (const char *x = q + (*q ? 1 : 0); *x; x++) dots += *x == '.';
+        if (dots > 1)
+            return c->fail(PV_EUNSUPPORTED, "only_qname_suffix: '%s' has more than one dot after its first character", q);
+        c->f_sxl[k] = (uint32_t)strlen(q);
+        c->f_sxh[k] = pvname::name_ph(q, strlen(q));
+    }
+    c->f_nsx = f->n_qname_suffixes;
+    if (f->n_qname_suffixes) {
+        fl |= PVDF_ONLY_QSUFFIX;
+        hipError_t e;
+        if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
+            return c->hipfail(e, "only_qname_suffix record buffer");
+    }
     c->f_flags = fl;
     c->f_rcode_mask = (fl & PVDF_ONLY_RCODE) ? f->only_rcode_mask : 0;
     c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
@@ -1058,7 +1089,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
                     c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
-                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph};
+                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx};
     for (void *p : ptrs) if (p) hipFree(p);
     for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status})
         if (hp) hipHostFree(hp);
@@ -1237,6 +1268,9 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     for (uint32_t k = 0; k < c->f_nq; k++) P.f_qt[k] = c->f_qt[k];
     P.f_nqn = c->f_nqn;
     for (uint32_t k = 0; k < c->f_nqn; k++) P.f_qn[k] = c->f_qn[k];
+    P.f_nsx = c->f_nsx;
+    P.sfx_of = c->d_sfx;
+    for (uint32_t k = 0; k < c->f_nsx; k++) { P.f_sxl[k] = c->f_sxl[k]; P.f_sxh[k] = c->f_sxh[k]; }
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
     if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0xffffffffull)
@@ -1312,6 +1346,8 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
     hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
+    if (P.f_flags & PVDF_ONLY_QSUFFIX)
+        hipLaunchKernelGGL(pv_dns_suffix, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates, bucket them by table region, merge each
     // region in LDS, decode the names of new entries

@@ -72,6 +72,7 @@ __device__ __forceinline__ uint32_t pv_alignbyte(uint32_t hi, uint32_t lo, uint3
 // kernel parameters are read through the constant address space (scalar loads)
 #define PV_CREF(T) const PV_C T &
 #include "pv_parse.h"
+#include <type_traits>
 
 namespace {
 
@@ -126,6 +127,44 @@ struct TAcc {
 
 __device__ __forceinline__ uint64_t *slot_sum(PV_CREF(PvParams) P, uint32_t slot) { return P.sum + (uint64_t)slot * PV_SUM_WORDS; }
 
+// DnsStreamHandler::_filtering's only_qname_suffix (dns/v1/DnsStreamHandler.cpp:615-630): the
+// length of the first listed suffix the lower-case first-query name ends with (the
+// suffix_size aggregateDomain then uses), -1 if none. n / ph: the name's NameStats length
+// and prefix hash, nl its encoded length. Out of line with by-value arguments, so the DNS
+// pass keeps no stack frame and no extra registers for this filter-only path.
+template <class A>
+__device__ __noinline__ int qname_suffix(PV_CREF(PvParams) P, A R, uint64_t m, uint32_t len, uint32_t n, uint64_t ph,
+                                         uint32_t nl)
+{
+    // one decode per listed suffix, a single capture each; the DNS pass records the result
+    // per record (sfx_of) for the name writers, which never re-derive it
+    for (uint32_t k = 0; k < P.f_nsx; k++) {
+        const uint32_t L = P.f_sxl[k];
+        if (L > n) continue;
+        if (L == 0) return 0;
+        SuffixCap sc{0, 0, 0, n - L};
+        if (nl > 0) name_emit(R, m, len, 12, sc);
+        if (ph_submul(ph, sc.cap, powb(L)) == P.f_sxh[k]) return (int)L;
+    }
+    return -1;
+}
+
+// only_qname_suffix result of one DNS message: the matched suffix size, 0xff if the
+// message has no first query or no listed suffix matches
+template <class A>
+__device__ __forceinline__ uint32_t dns_suffix_of(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen,
+                                                  uint32_t qd, uint32_t an, uint32_t ns, uint32_t ar)
+{
+    DnsInfo si;
+    dns_parse(R, m, dlen, qd, an, ns, ar, si);
+    if (!si.ok || !si.has_query) return 0xffu;
+    NameStats st;
+    st.init();
+    if (si.name_len_enc > 0) name_stats(R, m, dlen, 12, st);
+    const int r = qname_suffix(P, R, m, dlen, st.n, st.ph, si.name_len_enc);
+    return r < 0 ? 0xffu : (uint32_t)r;
+}
+
 // Writes the name record for a newly created global top-N entry (arena: u16 len + bytes).
 __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, uint32_t metric, uint32_t rep)
 {
@@ -156,7 +195,8 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     uint32_t n = nl > 0 ? st.n : 0;
     if (metric == TM_QNAME2 || metric == TM_QNAME3) {
         int q2, q3; uint64_t h2, h3;
-        if (nl > 0) agg_domain(st, q2, q3, h2, h3); else { q2 = 0; q3 = -1; }
+        const uint32_t sfx = (P.f_flags & PVDF_ONLY_QSUFFIX) ? P.sfx_of[rep] : 0u;
+        if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx); else { q2 = 0; q3 = -1; }
         start = metric == TM_QNAME2 ? q2 : q3;
         if (start < 0) start = (int)n;
     }
@@ -464,6 +504,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     const uint32_t ancount = ((w1 >> 8) & 0xff00) | (w1 >> 24);
     const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
     const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+    uint32_t sfx = 0; // only_qname_suffix's suffix_size for aggregateDomain
     if (P.f_flags) {
         // only_rcode is the input proxy's UDP predicate (dns/v1/DnsStreamHandler.cpp:485-508):
         // a query, or a response with an unlisted rcode, never reaches the handler (no event)
@@ -492,6 +533,16 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             bool hit = false;
             for (uint32_t k = 0; k < P.f_nq; k++) hit |= fd.qtype == P.f_qt[k];
             filt = !fd.ok || !fd.has_query || !hit;
+        }
+        if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) {
+            // matched by pv_dns_suffix before this pass (0xff: no listed suffix); the
+            // boundary path, whose records that kernel does not see, matches here
+            uint32_t r;
+            if constexpr (!std::is_same<Cache, KeyCache<2>>::value) r = P.sfx_of[i];
+            else r = dns_suffix_of(P, R, m, dlen, qd, ancount, ns, ar);
+            filt = r == 0xffu;
+            sfx = filt ? 0u : r;
+            if constexpr (std::is_same<Cache, KeyCache<2>>::value) P.sfx_of[i] = (uint8_t)r;
         }
         if (filt) {
             // process_filtered (:1341-1347): an event (sampled at rate 100) and `filtered`
@@ -584,7 +635,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                     }
                     int q2, q3;
                     uint64_t h2p, h3p;
-                    agg_domain(st, q2, q3, h2p, h3p);
+                    agg_domain(st, q2, q3, h2p, h3p, sfx);
                     const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
                     top(TM_QNAME2, fp56(k2, st.n - q2, 0), 1);
                     if (q3 >= 0 && (uint32_t)q3 < st.n) {
@@ -1193,6 +1244,36 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
 // One lane per DNS message of the Net pass's work list (same workgroup mapping).
 // Each wave stages 128-B windows of its 64 messages in LDS (names past the window
 // come from HBM) while the next messages' windows are in flight.
+// only_qname_suffix (filter-enabled runs only): the suffix match of every message on the
+// DNS work lists, one lane per message, into sfx_of[record], so the DNS pass itself carries
+// no suffix code (it cost that pass 11% on C3 when inlined)
+extern "C" __global__ void __launch_bounds__(256) pv_dns_suffix(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t nd = P.dq_cnt[blockIdx.x];
+    const uint64_t region = (uint64_t)blockIdx.x * P.wt_per_block * PV_WT;
+    const PV_G DnsMsg *Q = reinterpret_cast<const PV_G DnsMsg *>(P.dq) + region;
+    const GAcc R{P.recs};
+    for (uint32_t t = threadIdx.x; t < nd; t += blockDim.x) {
+        const DnsMsg dm = Q[t];
+        const uint64_t m = dm.moff;
+        // header words as dns_process reads them (bytes past the capture read as 0)
+        uint32_t w1 = 0, w2 = 0;
+        if (dm.mcap >= 12) { w1 = R.u32(m + 4); w2 = R.u32(m + 8); }
+        else {
+            for (uint32_t b = 4; b < 12; b++) {
+                const uint32_t v = b < dm.mcap ? R.u8(m + b) : 0;
+                if (b < 8) w1 |= v << (8 * (b - 4)); else w2 |= v << (8 * (b - 8));
+            }
+        }
+        const uint32_t qd = ((w1 & 0xff) << 8) | ((w1 >> 8) & 0xff);
+        const uint32_t an = ((w1 >> 8) & 0xff00) | (w1 >> 24);
+        const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
+        const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+        P.sfx_of[dm.idx] = (uint8_t)dns_suffix_of(P, R, m, dm.mlen, qd, an, ns, ar);
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
@@ -1624,7 +1705,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 if (metric == TM_QNAME2 || metric == TM_QNAME3) {
                     int q2, q3;
                     uint64_t h2, h3;
-                    if (nl > 0) agg_domain(st, q2, q3, h2, h3);
+                    const uint32_t sfx = (P.f_flags & PVDF_ONLY_QSUFFIX) ? P.sfx_of[e.rep] : 0u;
+                    if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx);
                     else { q2 = 0; q3 = -1; }
                     const int st0 = metric == TM_QNAME2 ? q2 : q3;
                     start = st0 < 0 ? nch : (uint32_t)st0;

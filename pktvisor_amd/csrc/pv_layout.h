@@ -155,8 +155,9 @@ struct PvSubnets {
 // DNS filter bits (PvParams::f_flags)
 #define PV_MAX_QTYPES 16
 #define PV_MAX_QNAMES 8
+#define PV_MAX_SUFFIXES 4
 enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
-       PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64 };
+       PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64, PVDF_ONLY_QSUFFIX = 128 };
 struct PvParams {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
@@ -225,6 +226,10 @@ struct PvParams {
     uint16_t f_qt[PV_MAX_QTYPES];
     uint32_t f_nqn;
     uint64_t f_qn[PV_MAX_QNAMES]; // only_qname: name fingerprints (fp56 of the lower-case name)
+    uint32_t f_nsx;                    // only_qname_suffix: list length, then per suffix
+    uint32_t f_sxl[PV_MAX_SUFFIXES];   // its length and
+    uint64_t f_sxh[PV_MAX_SUFFIXES];   // its polynomial hash (ph_step over the lower-case chars)
+    PV_G uint8_t *sfx_of;              // per record of the batch: the matched suffix size (DNS pass writes)
 };
 
 // pv_fill_multi's segment list (kernel argument)

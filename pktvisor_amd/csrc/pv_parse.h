@@ -480,13 +480,15 @@ struct NameStats {
 };
 
 // aggregateDomain(name, 0): suffix start positions for qname2 / qname3 (-1 = empty)
-PV_FN void agg_domain(const NameStats &s, int &q2, int &q3, uint64_t &ph2, uint64_t &ph3)
+// (suffix_size > 0: aggregateDomain(name, suffix_size), libs/visor_dns/dns.cpp:19-23)
+PV_FN void agg_domain(const NameStats &s, int &q2, int &q3, uint64_t &ph2, uint64_t &ph3, uint32_t suffix_size = 0)
 {
     int n = (int)s.n;
     q2 = 0; q3 = 0; ph2 = 0; ph3 = 0;
     if (n < 5) { q3 = -1; return; }
     int endDot = 1 << 30;
-    if (s.last_c == '.') endDot = n - 2;
+    if (suffix_size > 0 && (uint32_t)n > suffix_size) endDot = n - (int)suffix_size;
+    else if (s.last_c == '.') endDot = n - 2;
     uint64_t x1;
     int first = s.rfind(endDot, x1);
     if (first > 0) {
@@ -645,6 +647,19 @@ struct RawName {
     PV_FN void put(uint32_t c)
     {
         ph = ph_step(ph, c);
+        n++;
+    }
+};
+
+// prefix hash of the lower-case name at position tgt (only_qname_suffix: the hash of the
+// last L chars is H(name) - H(name[:n-L]) * B^L)
+struct SuffixCap {
+    uint64_t ph, cap;
+    uint32_t n, tgt;
+    PV_FN void put(uint32_t c)
+    {
+        if (n == tgt) cap = ph;
+        ph = ph_step(ph, lower(c));
         n++;
     }
 };

@@ -25,9 +25,13 @@ FILTERS = [
     {"answer_count": 2},
     {"only_qname": ["play.GooGle.com", "nonexistent.google.com"]},
     {"only_qname": ["play.google.com"], "only_responses": True},
+    {"only_qname_suffix": ["GooGle.com"]},
+    {"only_qname_suffix": ["t", "e.com", ".NET", "io"]},
+    {"only_qname_suffix": ["le.com", "s.com"], "only_responses": True},
 ]
 IDS = ["exclude_noerror", "rcode_nx", "rcode_nx_refused", "rcode_noerror_an0", "only_queries", "only_responses",
-       "qtype_aaaa_txt", "qtype_a_mx_resp", "an2", "qname", "qname_resp"]
+       "qtype_aaaa_txt", "qtype_a_mx_resp", "an2", "qname", "qname_resp", "suffix", "suffix_multi",
+       "suffix_resp"]
 
 
 def oracle_kw(f):
@@ -48,6 +52,8 @@ def oracle_kw(f):
         kw["only_qtype"] = ",".join(map(str, t["only_qtype"]))
     if t["only_qname"]:
         kw["only_qname"] = ",".join(t["only_qname"])
+    if t["only_qname_suffix"]:
+        kw["only_qname_suffix"] = ",".join(t["only_qname_suffix"])
     return kw
 
 
@@ -78,8 +84,9 @@ def test_filter_synthetic_parity(oracle, tmp_path, f):
     assert diff(gpu, ref) is None, diff(gpu, ref)
 
 
-@pytest.mark.parametrize("f", [{"exclude_noerror": True}, {"only_queries": True}, {"only_qtype": ["AAAA"]}],
-                         ids=["exclude_noerror", "only_queries", "qtype_aaaa"])
+@pytest.mark.parametrize("f", [{"exclude_noerror": True}, {"only_queries": True}, {"only_qtype": ["AAAA"]},
+                               {"only_qname_suffix": ["t", ".com"]}],
+                         ids=["exclude_noerror", "only_queries", "qtype_aaaa", "suffix"])
 def test_filter_multi_period_parity(oracle, tmp_path, f):
     # 120k records x 1.5 ms = 180 s: period shifts inside one batch, filtered events shift too
     gpu, ref = run_both(oracle, synth.pcap_bytes(4, 120000, ts_step_us=1500), synth.HOST_SPEC, 5, tmp_path, f)
@@ -121,5 +128,9 @@ def test_filter_reference_kats(tmp_path):
     d = j["wire_packets"]
     assert (d["udp"], d["noerror"], d["nxdomain"], d["nodata"], d["total"], d["filtered"]) == (6, 2, 1, 2, 6, 0)
     assert j["top_qname2"][0]["name"] == ".google.com" and j["top_qname3"][0]["name"] == "play.google.com"
+    j = wp({"only_qname_suffix": ["GooGle.com"]})
+    d = j["wire_packets"]
+    assert (d["udp"], d["noerror"], d["nxdomain"], d["nodata"], d["total"], d["filtered"]) == (10, 4, 1, 2, 10, 14)
+    assert "google.com" in j["top_qname2"][0]["name"] and j["top_qname3"] == []
     d = wp({"only_responses": True})["wire_packets"]
     assert (d["udp"], d["noerror"], d["refused"], d["nxdomain"], d["filtered"]) == (12, 10, 1, 1, 12)

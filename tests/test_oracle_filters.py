@@ -10,6 +10,8 @@ MIXED = os.path.join(GOLD, "dns_udp_mixed_rcode.pcap")
 
 # (cite, oracle filter config, expected wire_packets counters, expected top names)
 KAT = [
+    ("test_dns_layer.cpp:485-522 only_qname_suffix", dict(only_qname_suffix="GooGle.com"),
+     dict(udp=10, noerror=4, srvfail=0, refused=0, nxdomain=1, nodata=2, total=10, filtered=14), {}),
     ("test_dns_layer.cpp:446-483 only_qname (predicate)", dict(only_qname="play.GooGle.com,nonexistent.google.com"),
      dict(udp=6, noerror=2, srvfail=0, refused=0, nxdomain=1, nodata=2, total=6, filtered=0),
      dict(top_qname2=".google.com", top_qname3="play.google.com")),
@@ -36,6 +38,8 @@ def test_oracle_filter_kats(oracle, cite, cfg, want, tops):
         assert d["wire_packets"][k] == v, (cite, k)
     for k, v in tops.items():
         assert d[k][0]["name"] == v, (cite, k)
+    if "only_qname_suffix" in cfg:  # :520-521
+        assert "google.com" in d["top_qname2"][0]["name"] and d["top_qname3"] == []
 
 
 def test_filter_config_parsing():
@@ -63,5 +67,6 @@ def test_filter_config_parsing():
             dns_filter_config(cfg)
         assert str(e.value) == msg
     assert dns_filter_config({"only_qname": ["play.GooGle.com"]})["only_qname"] == ["play.google.com"]
+    assert dns_filter_config({"only_qname_suffix": ["GooGle.com"]})["only_qname_suffix"] == ["google.com"]
     with pytest.raises(ConfigError):
-        dns_filter_config({"only_qname_suffix": ["google.com"]})  # not built on the GPU path: refused loudly
+        dns_filter_config({"only_dnssec_response": True})  # not built on the GPU path: refused loudly
