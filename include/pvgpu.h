@@ -83,7 +83,7 @@ typedef struct pv_config {
  * _filtering :538-648). A filtered DNS packet is an event plus the `filtered` counter and
  * nothing else (process_filtered, :1341-1347). only_rcode is the input-proxy predicate
  * (:485-508): packets it rejects (queries, other rcodes) are not events at all.
- * only_dnssec_response / geoloc / asn are not built. only_qname is matched by the DNS
+ * geoloc / asn / public_suffix_list are not built. only_qname is matched by the DNS
  * pass's 56-bit name fingerprint (the key its top-N tables use), only_qname_suffix by the
  * 64-bit polynomial hash of the name's last L characters. */
 typedef struct pv_dns_filters {
@@ -99,6 +99,7 @@ typedef struct pv_dns_filters {
     uint32_t n_qname_suffixes;  /* "only_qname_suffix" entries (<= 4), 0 = off */
     const char *const *qname_suffixes; /* lower-cased; the first one the name ends with sets the
                                           aggregateDomain suffix size (at most one dot after its first char) */
+    uint32_t only_dnssec_response; /* nonzero: filter all but responses with an RRSIG answer */
 } pv_dns_filters;
 
 /* Replaces DnsStreamHandler::start's filter setup (dns/v1/DnsStreamHandler.cpp:60-150). Call

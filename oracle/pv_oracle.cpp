@@ -345,6 +345,7 @@ struct Config {
     bool has_answer_count = false;  // "answer_count" (:123-130)
     uint32_t answer_count = 0;
     bool only_queries = false, only_responses = false; // (:114-119)
+    bool only_dnssec = false;                           // "only_dnssec_response" (:120-122)
     std::vector<uint16_t> only_qtype;                   // "only_qtype" (:131-150)
     std::vector<std::string> only_qname;                // "only_qname" (:151-160), lower-case; predicate mode
     std::vector<std::string> only_qname_suffix;         // "only_qname_suffix" (:161-169), lower-case
@@ -642,6 +643,40 @@ struct DnsParse {
 };
 
 // DnsLayer.cpp:119-209 with queryOnly=true.
+// only_dnssec_response (dns/v1/DnsStreamHandler.cpp:573-595): parseResources(false, true, true)
+// walks questions, answers, authorities and the first additional (DnsLayer.cpp:119-209); the
+// packet passes if that walk stays in bounds and an answer has type RRSIG (46)
+static bool dnssec_answer(const DnsMsg &m)
+{
+    uint16_t qd = rd16be(m.d + 4), an = rd16be(m.d + 6), ns = rd16be(m.d + 8), ar = rd16be(m.d + 10);
+    uint32_t total = (uint32_t)qd + an + ns + ar;
+    if (total > 100 || m.len < 12) return false;
+    size_t off = 12;
+    bool sig = false;
+    for (uint32_t i = 0; i < total; i++) {
+        int kind = 0; // 0 query, 1 answer, 2 authority, 3 additional
+        if (qd > 0) qd--;
+        else if (an > 0) { an--; kind = 1; }
+        else if (ns > 0) { ns--; kind = 2; }
+        else { ar--; kind = 3; }
+        std::string nm;
+        size_t nl = decode_name(m, off, nm, 1);
+        size_t sz;
+        if (kind == 0) sz = nl + 4;
+        else {
+            size_t dl_off = off + nl + 8;
+            uint16_t dl = (dl_off + 2 <= m.len) ? rd16be(m.d + dl_off) : 0;
+            sz = nl + 10 + dl;
+        }
+        const size_t start = off;
+        off += sz;
+        if (off > m.len) return false;
+        if (kind == 1 && rd16be(m.d + start + nl) == 46) sig = true;
+        if (kind == 3) break;
+    }
+    return sig;
+}
+
 static DnsParse parse_resources(const DnsMsg &m)
 {
     DnsParse r;
@@ -919,6 +954,7 @@ struct Engine {
         else if (cfg.has_answer_count && ancount != cfg.answer_count) filt = true;
         else if (cfg.only_queries && qr) filt = true;
         else if (cfg.only_responses && !qr) filt = true;
+        else if (cfg.only_dnssec && (!qr || !ancount || !dnssec_answer(m))) filt = true;
         else if (!cfg.only_qtype.empty()) {
             DnsParse fr = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{hdr_buf, m.len});
             if (!fr.ok || !fr.has_query) filt = true;
@@ -1270,6 +1306,7 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "answer_count") { c.has_answer_count = true; c.answer_count = (uint32_t)atoll(v.c_str()); }
         else if (k == "only_queries") c.only_queries = atoi(v.c_str()) != 0;
         else if (k == "only_responses") c.only_responses = atoi(v.c_str()) != 0;
+        else if (k == "only_dnssec_response") c.only_dnssec = atoi(v.c_str()) != 0;
         else if (k == "only_qname_suffix") {
             size_t q = 0;
             while (q < v.size()) {

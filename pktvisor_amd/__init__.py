@@ -54,7 +54,7 @@ class pv_dns_filters(ctypes.Structure):
                 ("answer_count", ctypes.c_int32), ("only_queries", ctypes.c_uint32), ("only_responses", ctypes.c_uint32),
                 ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16), ("n_qnames", ctypes.c_uint32),
                 ("qnames", ctypes.POINTER(ctypes.c_char_p)), ("n_qname_suffixes", ctypes.c_uint32),
-                ("qname_suffixes", ctypes.POINTER(ctypes.c_char_p))]
+                ("qname_suffixes", ctypes.POINTER(ctypes.c_char_p)), ("only_dnssec_response", ctypes.c_uint32)]
 
 
 class ConfigError(PvError):
@@ -62,8 +62,8 @@ class ConfigError(PvError):
 
 
 DNS_FILTER_KEYS = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype",
-                   "only_qname", "only_qname_suffix")
-DNS_FILTER_NOT_BUILT = ("only_dnssec_response", "geoloc_notfound", "asn_notfound",
+                   "only_qname", "only_qname_suffix", "only_dnssec_response")
+DNS_FILTER_NOT_BUILT = ( "geoloc_notfound", "asn_notfound",
                         "dnstap_msg_type", "public_suffix_list")
 
 
@@ -76,7 +76,7 @@ def dns_filter_config(cfg: dict) -> dict:
     """DnsStreamHandler::start's filter setup (src/handlers/dns/v1/DnsStreamHandler.cpp:60-150):
     typed values in, the pv_dns_filters fields out; ConfigError with the reference's text."""
     out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[],
-               only_qname=[], only_qname_suffix=[])
+               only_qname=[], only_qname_suffix=[], only_dnssec_response=0)
     for k in cfg:
         if k in DNS_FILTER_NOT_BUILT:
             raise ConfigError(f"DnsStreamHandler: filter {k} is not supported by the GPU handler")
@@ -108,6 +108,8 @@ def dns_filter_config(cfg: dict) -> dict:
         out["only_queries"] = 1
     if cfg.get("only_responses"):
         out["only_responses"] = 1
+    if cfg.get("only_dnssec_response"):
+        out["only_dnssec_response"] = 1
     if "answer_count" in cfg:
         v = cfg["answer_count"]
         if isinstance(v, bool) or not isinstance(v, int):
@@ -275,6 +277,7 @@ class PvHandlers:
                                filt["only_queries"], filt["only_responses"], len(filt["only_qtype"]))
             for k, q in enumerate(filt["only_qtype"]):
                 f.qtypes[k] = q
+            f.only_dnssec_response = filt["only_dnssec_response"]
             if filt["only_qname"]:
                 self._qnames = (ctypes.c_char_p * len(filt["only_qname"]))(*[q.encode() for q in filt["only_qname"]])
                 f.n_qnames = len(filt["only_qname"])

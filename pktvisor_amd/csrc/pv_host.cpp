@@ -934,6 +934,7 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
     if (f->answer_count >= 0) fl |= PVDF_ANSWER_COUNT;
     if (f->only_queries) fl |= PVDF_ONLY_QUERIES;
     if (f->only_responses) fl |= PVDF_ONLY_RESPONSES;
+    if (f->only_dnssec_response) fl |= PVDF_ONLY_DNSSEC;
     if (f->n_qtypes > PV_MAX_QTYPES) return c->fail(PV_EINVAL, "only_qtype: at most %d qtypes", PV_MAX_QTYPES);
     for (uint32_t k = 0; k < f->n_qtypes; k++)
         if (!qtype_names().count(f->qtypes[k]))

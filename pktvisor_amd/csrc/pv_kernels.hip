@@ -526,7 +526,8 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         // DnsStreamHandler::_filtering (:538-648), in its order
         bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
                     ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
-                    ((P.f_flags & PVDF_ONLY_QUERIES) && qr) || ((P.f_flags & PVDF_ONLY_RESPONSES) && !qr);
+                    ((P.f_flags & PVDF_ONLY_QUERIES) && qr) || ((P.f_flags & PVDF_ONLY_RESPONSES) && !qr) ||
+                    ((P.f_flags & PVDF_ONLY_DNSSEC) && (!qr || !ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar)));
         if (!filt && (P.f_flags & PVDF_ONLY_QTYPE)) {
             DnsInfo fd;
             dns_parse(R, m, dlen, qd, ancount, ns, ar, fd);

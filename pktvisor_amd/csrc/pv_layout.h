@@ -157,7 +157,8 @@ struct PvSubnets {
 #define PV_MAX_QNAMES 8
 #define PV_MAX_SUFFIXES 4
 enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
-       PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64, PVDF_ONLY_QSUFFIX = 128 };
+       PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64, PVDF_ONLY_QSUFFIX = 128,
+       PVDF_ONLY_DNSSEC = 256 };
 struct PvParams {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;

@@ -673,6 +673,31 @@ struct DnsInfo {
     uint32_t qtype;
 };
 
+// only_dnssec_response (dns/v1/DnsStreamHandler.cpp:573-595): parseResources(false, true,
+// true) walks questions, answers, authorities and the first additional (DnsLayer.cpp:119-209);
+// true if that walk stays in bounds and an answer has type RRSIG (46)
+template <class A>
+PV_FN bool dns_dnssec(const A &R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns, uint32_t ar)
+{
+    const uint32_t total = qd + an + ns + ar;
+    if (total > 100 || len < 12) return false;
+    uint32_t off = 12;
+    bool sig = false;
+    for (uint32_t i = 0; i < total; i++) {
+        const uint32_t nl = name_len_l1(R, m, len, off);
+        const uint32_t start = off;
+        if (i < qd) off += nl + 4;
+        else {
+            const uint32_t dl = (off + nl + 10 <= len) ? be16(R, m + off + nl + 8) : 0u;
+            off += nl + 10 + dl;
+        }
+        if (off > len) return false;
+        if (i >= qd && i < qd + an && be16(R, m + start + nl) == 46) sig = true;
+        if (i >= qd + an + ns) break; // the first additional record ends the walk
+    }
+    return sig;
+}
+
 template <class A>
 PV_FN void dns_parse(const A &R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns,
                           uint32_t ar, DnsInfo &d)

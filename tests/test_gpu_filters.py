@@ -28,10 +28,11 @@ FILTERS = [
     {"only_qname_suffix": ["GooGle.com"]},
     {"only_qname_suffix": ["t", "e.com", ".NET", "io"]},
     {"only_qname_suffix": ["le.com", "s.com"], "only_responses": True},
+    {"only_dnssec_response": True},
 ]
 IDS = ["exclude_noerror", "rcode_nx", "rcode_nx_refused", "rcode_noerror_an0", "only_queries", "only_responses",
        "qtype_aaaa_txt", "qtype_a_mx_resp", "an2", "qname", "qname_resp", "suffix", "suffix_multi",
-       "suffix_resp"]
+       "suffix_resp", "dnssec"]
 
 
 def oracle_kw(f):
@@ -52,6 +53,8 @@ def oracle_kw(f):
         kw["only_qtype"] = ",".join(map(str, t["only_qtype"]))
     if t["only_qname"]:
         kw["only_qname"] = ",".join(t["only_qname"])
+    if t["only_dnssec_response"]:
+        kw["only_dnssec_response"] = 1
     if t["only_qname_suffix"]:
         kw["only_qname_suffix"] = ",".join(t["only_qname_suffix"])
     return kw
@@ -67,8 +70,9 @@ def run_both(oracle, pcap: bytes, host: str, periods: int, tmp_path, f):
 
 @pytest.mark.parametrize("f", FILTERS, ids=IDS)
 @pytest.mark.parametrize("fixture,host", [("dns_udp_mixed_rcode.pcap", "192.168.0.0/24"),
-                                          ("dns_udp_tcp_random.pcap", "192.168.0.0/24"), ("dns_ipv6_udp.pcap", "")],
-                         ids=["mixed_rcode", "udp_tcp_random", "ipv6_udp"])
+                                          ("dns_udp_tcp_random.pcap", "192.168.0.0/24"), ("dns_ipv6_udp.pcap", ""),
+                                          ("dnssec.pcap", "192.168.0.0/24")],
+                         ids=["mixed_rcode", "udp_tcp_random", "ipv6_udp", "dnssec"])
 def test_filter_fixture_parity(oracle, tmp_path, fixture, host, f):
     pcap = open(os.path.join(GOLD, fixture), "rb").read()
     for periods in (1, 5):
@@ -134,3 +138,13 @@ def test_filter_reference_kats(tmp_path):
     assert "google.com" in j["top_qname2"][0]["name"] and j["top_qname3"] == []
     d = wp({"only_responses": True})["wire_packets"]
     assert (d["udp"], d["noerror"], d["refused"], d["nxdomain"], d["filtered"]) == (12, 10, 1, 1, 12)
+
+
+def test_dnssec_reference_kat():
+    """test_dns_layer.cpp:558-596, straight from the GPU path"""
+    d = pa.pktvisor_reader(os.path.join(GOLD, "dnssec.pcap"), host_spec="192.168.0.0/24", periods=1,
+                           dns_filters={"only_dnssec_response": True})["1m"]["dns"]
+    w = d["wire_packets"]
+    assert (w["events"], w["udp"], w["replies"], w["noerror"], w["queries"]) == (14, 6, 6, 6, 0)
+    assert d["cardinality"]["qname"] == 3
+    assert [(e["name"], e["estimate"]) for e in d["top_qtype"][:3]] == [("DNSKEY", 3), ("DS", 2), ("A", 1)]

@@ -69,4 +69,15 @@ def test_filter_config_parsing():
     assert dns_filter_config({"only_qname": ["play.GooGle.com"]})["only_qname"] == ["play.google.com"]
     assert dns_filter_config({"only_qname_suffix": ["GooGle.com"]})["only_qname_suffix"] == ["google.com"]
     with pytest.raises(ConfigError):
-        dns_filter_config({"only_dnssec_response": True})  # not built on the GPU path: refused loudly
+        dns_filter_config({"public_suffix_list": True})  # not built on the GPU path: refused loudly
+
+
+def test_oracle_dnssec_kat(oracle):
+    """test_dns_layer.cpp:558-596 only_dnssec_response on dnssec.pcap"""
+    d = oracle.run_file(os.path.join(GOLD, "dnssec.pcap"), host_spec="192.168.0.0/24", num_periods=1, window=1,
+                        only_dnssec_response=1)["1m"]["dns"]
+    w = d["wire_packets"]
+    assert (w["events"], w["deep_samples"], w["tcp"], w["udp"], w["ipv4"], w["ipv6"]) == (14, 14, 0, 6, 6, 0)
+    assert (w["queries"], w["replies"], w["noerror"]) == (0, 6, 6)
+    assert d["cardinality"]["qname"] == 3
+    assert [(e["name"], e["estimate"]) for e in d["top_qtype"][:3]] == [("DNSKEY", 3), ("DS", 2), ("A", 1)]
