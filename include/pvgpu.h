@@ -133,10 +133,18 @@ const char *pv_last_error(const pv_ctx *ctx);
 int pv_index_records(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32_t *offsets, uint64_t max_records,
                      uint32_t *sec_change_idx, uint32_t *sec_change_sec, uint32_t max_changes, pv_index_info *info);
 
+/* Bytes of device memory past the end of the last record that the kernels may read (the
+ * LDS windows of pv_topn_names and the DNS pass load whole 16-B aligned windows of up to
+ * 192 bytes from a record's start). Every d_recs buffer must be readable this far. */
+#define PV_RECS_PAD 256
+
 /* Process a block of records already resident in device memory. d_recs must be
- * readable for 64 bytes past the last record (padding). `stream` is a
- * hipStream_t (NULL = the context's own stream). Returns after enqueueing, except
- * where a period boundary needs host validation (then it synchronises). */
+ * readable for PV_RECS_PAD bytes past the last record. `stream` is a hipStream_t
+ * (NULL = the context's own stream). Each manager (Net, DNS) shifts its own window on the
+ * first of its own events at or after its next shift (AbstractMetricsManager::new_event,
+ * src/AbstractMetricsManager.h:318-333); a batch that may hold a DNS shift is prescanned
+ * for its DNS events first, and a batch with more than PV_MAX_SHIFTS (6) shifts of one
+ * manager is processed as several device spans. Returns once the batch's status is read. */
 int pv_process_device(pv_ctx *ctx, const uint8_t *d_recs, const uint32_t *d_offsets, const pv_index_info *info,
                       const uint32_t *sec_change_idx, const uint32_t *sec_change_sec, void *stream);
 
@@ -173,8 +181,22 @@ int pv_edge_merge(pv_ctx *ctx, const uint8_t *const *bufs, const size_t *sizes, 
  * sketches, src/handlers/dns/v1/DnsStreamHandler.cpp:692). */
 int pv_values_export(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
 int pv_values_merge(pv_ctx *ctx, const uint8_t *buf, size_t bytes);
-/* Live slots with their bucket start seconds, newest first (merge alignment check). */
-int pv_window_periods(pv_ctx *ctx, uint32_t *slots, int64_t *start_sec, uint32_t max_n, uint32_t *n);
+/* Live slots of one manager (part 0 = Net "packets", 1 = DNS) with their bucket start
+ * seconds, newest first. */
+int pv_window_periods(pv_ctx *ctx, int part, uint32_t *slots, int64_t *start_sec, uint32_t max_n, uint32_t *n);
+/* Sharded runs (one context per rank, contiguous shards): shifts of one manager whose shifting
+ * event lies in another rank's shard, applied in order as window operations only (an empty
+ * bucket opens at each threshold second). Call with the earlier ranks' shifts before the first
+ * batch and with the later ranks' shifts after the last, so every rank's window holds the same
+ * periods in the same slots (the global period table). */
+int pv_advance_windows(pv_ctx *ctx, int part, const int64_t *thresh, uint32_t n);
+/* The seconds (stream order, each once) in which a device batch holds a DNS event (a UDP
+ * datagram on a DNS port that the input predicates pass): what the ranks exchange to compute
+ * the DNS manager's global shifts. Does not touch the buckets. */
+int pv_dns_event_seconds(pv_ctx *ctx, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
+                         const uint32_t *sc_idx, const uint32_t *sc_sec, int64_t *secs, uint32_t max, uint32_t *n);
+/* The same over records in host memory (staged through the ingest chunks). */
+int pv_dns_event_seconds_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes, int64_t *secs, uint32_t max, uint32_t *n);
 
 
 int pv_set_start_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);
@@ -196,10 +218,18 @@ void pv_free(void *p);
  * that process contiguous shards set their shard's first global record index. */
 int pv_state_regions(pv_ctx *ctx, void **sum_ptr, size_t *sum_bytes, void **min_ptr, size_t *min_bytes);
 int pv_set_global_base(pv_ctx *ctx, uint64_t base);
-/* Bucket slots of the Net and DNS windows (front = live) and the per-slot sizes
- * of the SUM (uint64) and MIN (int64) regions, so a reduce can touch only them. */
-int pv_window_slots(pv_ctx *ctx, uint32_t *slots, uint32_t max_slots, uint32_t *n_slots, size_t *sum_slot_words,
-                    size_t *min_slot_words);
+/* The device regions of both live windows a multi-GPU reduce combines, in a fixed order
+ * (identical on every rank whose windows hold the same periods): per Net slot its net part,
+ * per DNS slot its dns part, of the SUM words (uint64, all-reduce SUM) and of the MIN words
+ * (int64 CPC first-occurrence indices, all-reduce MIN). */
+enum pv_reduce_op { PV_REDUCE_SUM = 0, PV_REDUCE_MIN = 1 };
+typedef struct pv_region {
+    void *ptr;      /* device pointer */
+    uint64_t words; /* 64-bit words */
+    uint32_t op;    /* pv_reduce_op */
+    uint32_t pad;
+} pv_region;
+int pv_window_regions(pv_ctx *ctx, pv_region *regions, uint32_t max, uint32_t *n);
 /* Compact the top-N tables of all live buckets into a host buffer of
  * (slot, metric, key, count, name) records (see pvgpu_topn_rec) for exchange;
  * pv_merge_topn adds such records from another rank into this context's view. */

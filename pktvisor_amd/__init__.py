@@ -145,9 +145,16 @@ class pv_index_info(ctypes.Structure):
 EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_error", "pv_index_records",
            "pv_process_device", "pv_process_host", "pv_set_start_tstamp", "pv_set_end_tstamp", "pv_synchronize",
            "pv_reset", "pv_window_json", "pv_free", "pv_state_regions", "pv_set_global_base", "pv_export_topn",
-           "pv_merge_topn", "pv_kernel_timing", "pv_window_slots", "pv_index_records_mt", "pv_host_register",
+           "pv_merge_topn", "pv_kernel_timing", "pv_window_regions", "pv_index_records_mt", "pv_host_register",
            "pv_host_unregister", "pv_ingest_timing", "pv_edge_export", "pv_edge_merge", "pv_values_export",
-           "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code"]
+           "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code", "pv_advance_windows",
+           "pv_dns_event_seconds", "pv_dns_event_seconds_host"]
+PART_NET, PART_DNS = 0, 1
+PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
+
+
+class pv_region(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("words", ctypes.c_uint64), ("op", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 _lib = None
 
@@ -190,14 +197,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_set_global_base.argtypes = [P, U64]
     lib.pv_export_topn.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_merge_topn.argtypes = [P, P, ctypes.c_size_t]
-    lib.pv_window_slots.argtypes = [P, P, U32, ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_size_t),
-                                    ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_window_regions.argtypes = [P, P, U32, ctypes.POINTER(U32)]
+    lib.pv_advance_windows.argtypes = [P, ctypes.c_int, P, U32]
+    lib.pv_dns_event_seconds.argtypes = [P, P, P, ctypes.POINTER(pv_index_info), P, P, P, U32, ctypes.POINTER(U32)]
+    lib.pv_dns_event_seconds_host.argtypes = [P, P, ctypes.c_size_t, P, U32, ctypes.POINTER(U32)]
     lib.pv_kernel_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.c_int]
     lib.pv_edge_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_edge_merge.argtypes = [P, P, P, U32, U32]
     lib.pv_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_values_merge.argtypes = [P, P, ctypes.c_size_t]
-    lib.pv_window_periods.argtypes = [P, P, P, U32, ctypes.POINTER(U32)]
+    lib.pv_window_periods.argtypes = [P, ctypes.c_int, P, P, U32, ctypes.POINTER(U32)]
     lib.pv_set_dns_filters.argtypes = [P, ctypes.POINTER(pv_dns_filters)]
     lib.pv_dns_code.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(U32)]
     _lib = lib
@@ -352,13 +361,36 @@ class PvHandlers:
                     "pv_kernel_timing")
         return ms.value, n.value
 
-    def window_slots(self):
-        """(slot ids, SUM words per slot, MIN words per slot) of the live windows"""
-        slots = np.zeros(32, dtype=np.uint32)
-        n, sw, mw = ctypes.c_uint32(), ctypes.c_size_t(), ctypes.c_size_t()
-        self._check(self.lib.pv_window_slots(self.ctx, slots.ctypes.data, 32, ctypes.byref(n), ctypes.byref(sw),
-                                             ctypes.byref(mw)), "pv_window_slots")
-        return [int(x) for x in slots[: n.value]], sw.value, mw.value
+    def window_regions(self):
+        """[(device ptr, 64-bit words, PV_REDUCE_SUM | PV_REDUCE_MIN)] of both live windows, in the
+        order every rank with the same windows lists them (pv_window_regions)"""
+        regs = (pv_region * 64)()
+        n = ctypes.c_uint32()
+        self._check(self.lib.pv_window_regions(self.ctx, regs, 64, ctypes.byref(n)), "pv_window_regions")
+        return [(int(r.ptr), int(r.words), int(r.op)) for r in regs[: n.value]]
+
+    def advance_windows(self, part: int, thresholds):
+        """apply shifts whose shifting event lies in another shard (pv_advance_windows)"""
+        t = np.asarray(list(thresholds), dtype=np.int64)
+        if len(t):
+            self._check(self.lib.pv_advance_windows(self.ctx, part, t.ctypes.data, len(t)), "pv_advance_windows")
+
+    def dns_event_seconds_host(self, recs, max_n: int = 1 << 22):
+        """seconds (stream order) in which the records hold a DNS event (pv_dns_event_seconds_host)"""
+        buf = recs if isinstance(recs, np.ndarray) else np.frombuffer(recs, dtype=np.uint8)
+        out = np.zeros(max_n, dtype=np.int64)
+        n = ctypes.c_uint32()
+        self._check(self.lib.pv_dns_event_seconds_host(self.ctx, buf.ctypes.data, buf.nbytes, out.ctypes.data, max_n,
+                                                       ctypes.byref(n)), "pv_dns_event_seconds_host")
+        return [int(x) for x in out[: n.value]]
+
+    def dns_event_seconds(self, d_recs: int, d_offs: int, index: "RecordIndex", max_n: int = 1 << 22):
+        out = np.zeros(max_n, dtype=np.int64)
+        n = ctypes.c_uint32()
+        self._check(self.lib.pv_dns_event_seconds(self.ctx, d_recs, d_offs, ctypes.byref(index.info),
+                                                  index.sc_idx.ctypes.data, index.sc_sec.ctypes.data, out.ctypes.data,
+                                                  max_n, ctypes.byref(n)), "pv_dns_event_seconds")
+        return [int(x) for x in out[: n.value]]
 
     def export_topn(self) -> bytes:
         p, n = ctypes.c_void_p(), ctypes.c_size_t()
@@ -396,13 +428,13 @@ class PvHandlers:
         buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
         self._check(self.lib.pv_values_merge(self.ctx, buf.ctypes.data, len(data)), "pv_values_merge")
 
-    def window_periods(self):
-        """[(slot, bucket start second)] of the live windows, newest first"""
+    def window_periods(self, part: int = PART_NET):
+        """[(slot, bucket start second)] of one manager's live window, newest first"""
         slots = np.zeros(32, dtype=np.uint32)
         starts = np.zeros(32, dtype=np.int64)
         n = ctypes.c_uint32()
-        self._check(self.lib.pv_window_periods(self.ctx, slots.ctypes.data, starts.ctypes.data, 32, ctypes.byref(n)),
-                    "pv_window_periods")
+        self._check(self.lib.pv_window_periods(self.ctx, part, slots.ctypes.data, starts.ctypes.data, 32,
+                                               ctypes.byref(n)), "pv_window_periods")
         return [(int(a), int(b)) for a, b in zip(slots[: n.value], starts[: n.value])]
 
     def set_start_tstamp(self, sec: int, nsec: int = 0):

@@ -75,7 +75,7 @@ extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_fill_multi(PvFillList L);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
-extern "C" __global__ void pv_boundary_kernel(const PvParams *P);
+extern "C" __global__ void pv_dns_prescan(const PvParams *P);
 extern "C" __global__ void pv_topn_combine(const PvParams *P);
 extern "C" __global__ void pv_topn_scan(const PvParams *P);
 extern "C" __global__ void pv_topn_scatter(const PvParams *P);
@@ -93,8 +93,8 @@ extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t
 
 namespace {
 
-// status words (device): flags, n_events, n_resp, n_vals, dns_any[8], dns_at_thresh[8]
-enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_DNS_ANY = 4, ST_DNS_AT = 12, ST_NNEW = 20, ST_WORDS = 21 };
+// status words (device): flags, n_events, n_resp, n_vals, DNS messages, new top-N names
+enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNEW = 5, ST_WORDS = 6 };
 // after the status words (one allocation, zeroed per batch up to the live region count):
 // per-region update counts, then offsets and fill pointers
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
@@ -117,9 +117,17 @@ struct SlotMeta {
     }
 };
 
+// One handler's window (AbstractMetricsManager::_metric_buckets + _next_shift_tstamp,
+// src/AbstractMetricsManager.h:233,264-305). The bucket of period ordinal k lives in slot
+// k % PV_SLOTS of this handler's part of the device state.
+enum { PART_NET = 0, PART_DNS = 1 };
 struct Window {
     std::deque<uint32_t> slots; // front = live bucket
     int64_t next_shift_sec = 0;
+    uint64_t ordinal = 0;       // period ordinal of the live bucket
+    SlotMeta meta[PV_SLOTS];
+    bool clean[PV_SLOTS] = {};  // slot part cleared and not written since
+    uint32_t slot_at(uint64_t k) const { return (uint32_t)((ordinal + k) % PV_SLOTS); }
 };
 
 // ICON polynomial for lg_k = 11 (3rd/datasketches/cpc/include/icon_estimator.hpp:98-102)
@@ -279,7 +287,7 @@ struct pv_ctx {
     uint32_t *d_taux = nullptr;
     uint8_t *d_arena = nullptr;
     uint64_t *d_arena_top = nullptr;
-    uint64_t arena_cap = 128ull << 20; // per slot; PV_ARENA_PARTS partitions
+    uint64_t arena_cap = 128ull << 20; // per table; PV_ARENA_PARTS partitions
     uint32_t tcap_log2 = 22;
     PvXEvent *d_events = nullptr;
     uint64_t *d_ekeys = nullptr;
@@ -317,8 +325,10 @@ struct pv_ctx {
     // shard-edge stubs (orphan responses) accumulated since reset, device counter in d_nvals[3]
     PvXEvent *d_orph = nullptr;
     uint32_t orph_cap = 0;
-    std::vector<std::pair<int64_t, uint32_t>> dns_shifts; // (threshold second, new slot) since reset
-    uint32_t gen[PV_SLOTS] = {0}; // bumped when a slot is recycled; values carry slot | gen << 8
+    std::vector<std::pair<int64_t, uint32_t>> dns_shifts; // (threshold second, new DNS slot) since reset
+    uint32_t gen[PV_SLOTS] = {0}; // bumped when a DNS slot is recycled; values carry slot | gen << 8
+    uint64_t *d_dbits = nullptr;  // pv_dns_prescan output (one bit per record)
+    uint64_t *h_dbits = nullptr;  // pinned host copy
     size_t xvals_synced = 0;
     float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
     uint32_t *d_status = nullptr;
@@ -353,16 +363,14 @@ struct pv_ctx {
     uint64_t stage_recs = 0;  // records per chunk
     hipStream_t copy_stream = nullptr;
     double ingest_ms[4] = {0, 0, 0, 0}; // host copy, index, H2D issue, device processing (pv_ingest_timing)
-    // window state
-    SlotMeta meta[PV_SLOTS];
-    bool slot_used[PV_SLOTS] = {false};
+    // window state: the Net and DNS managers shift independently
     Window net, dns;
     bool started = false, ended = false;
     int64_t last_sec = 0, last_nsec = 0;
     uint64_t global_base = 0, records_seen = 0;
     // host copies of transaction values, per slot/kind
     std::vector<PvXValue> xvals_host;
-    // merged top-N records from other ranks: slot -> key -> (count, name)
+    // merged top-N records from other ranks: table -> key -> (count, name)
     std::map<uint32_t, std::map<uint64_t, std::pair<uint64_t, std::string>>> remote_topn;
     // device fills not launched yet (launch_fill*; one pv_fill_multi per flush_fills)
     PvFillList fills{};
@@ -456,59 +464,79 @@ int launch_fill32(pv_ctx *c, uint32_t *p, uint64_t n, uint32_t v)
     return 0;
 }
 
-// clear one bucket slot on the device (enqueued on the context stream)
-void clear_slot(pv_ctx *c, uint32_t s, int64_t rel_base)
+// Clear one handler's part of a slot on the device (enqueued on the context stream):
+// its SUM and MIN words and its top-N table. A part that is still clean is skipped.
+void clear_part(pv_ctx *c, int part, uint32_t s)
 {
-    uint64_t tcap = 1ull << c->tcap_log2;
-    launch_fill64(c, c->d_sum + (uint64_t)s * PV_SUM_WORDS, PV_SUM_WORDS, 0);
-    launch_fill64(c, (uint64_t *)c->d_cpc + (uint64_t)s * PV_MIN_WORDS, PV_MIN_WORDS, (uint64_t)PV_CPC_EMPTY);
-    launch_fill64(c, c->d_tkeys + s * tcap, tcap, 0);
-    launch_fill64(c, c->d_tcnt + s * tcap, tcap, 0);
-    launch_fill32(c, c->d_taux + s * tcap, tcap, 0);
-    launch_fill64(c, c->d_arena_top + (uint64_t)s * PV_ARENA_PARTS, PV_ARENA_PARTS, 0);
-    c->meta[s] = SlotMeta();
-    c->meta[s].rel_base = rel_base;
-    c->slot_used[s] = true;
-    c->gen[s] = (c->gen[s] + 1) & 0xffffff; // values of the previous use of this slot no longer match
-    c->remote_topn.erase(s);
+    Window &w = part == PART_NET ? c->net : c->dns;
+    if (part == PART_DNS) {
+        // quantile inputs of the slot's previous bucket no longer match (bounded host memory)
+        c->gen[s] = (c->gen[s] + 1) & 0xffffff;
+        c->xvals_host.erase(std::remove_if(c->xvals_host.begin(), c->xvals_host.end(),
+                                           [s](const PvXValue &v) { return (v.slot & 0xff) == s; }),
+                            c->xvals_host.end());
+    }
+    const uint32_t t = s + (part == PART_DNS ? PV_SLOTS : 0);
+    c->remote_topn.erase(t);
+    w.meta[s] = SlotMeta();
+    if (w.clean[s]) return;
+    const uint64_t tcap = 1ull << c->tcap_log2;
+    uint64_t *sum = c->d_sum + (uint64_t)s * PV_SUM_WORDS;
+    uint64_t *cpc = (uint64_t *)c->d_cpc + (uint64_t)s * PV_MIN_WORDS;
+    if (part == PART_NET) {
+        launch_fill64(c, sum, PV_SUM_NET_WORDS, 0);
+        launch_fill64(c, cpc, PV_MIN_NET_WORDS, (uint64_t)PV_CPC_EMPTY);
+    } else {
+        launch_fill64(c, sum + PV_OFF_DNS, PV_SUM_WORDS - PV_OFF_DNS, 0);
+        launch_fill64(c, cpc + PV_MIN_NET_WORDS, PV_MIN_WORDS - PV_MIN_NET_WORDS, (uint64_t)PV_CPC_EMPTY);
+    }
+    launch_fill64(c, c->d_tkeys + t * tcap, tcap, 0);
+    launch_fill64(c, c->d_tcnt + t * tcap, tcap, 0);
+    launch_fill32(c, c->d_taux + t * tcap, tcap, 0);
+    launch_fill64(c, c->d_arena_top + (uint64_t)t * PV_ARENA_PARTS, PV_ARENA_PARTS, 0);
+    w.clean[s] = true;
 }
 
-uint32_t alloc_slot(pv_ctx *c)
+// _period_shift (src/AbstractMetricsManager.h:276-305) on the host mirror of one window: the
+// live bucket becomes read-only at T, the next ordinal's slot (reserved and cleared before
+// the batch that shifts) becomes live, the oldest beyond num_periods drops out.
+void win_shift(pv_ctx *c, Window &w, int64_t T)
 {
-    // a slot not referenced by either window
-    for (uint32_t s = 0; s < PV_SLOTS; s++) {
-        bool used = false;
-        for (auto x : c->net.slots) used |= x == s;
-        for (auto x : c->dns.slots) used |= x == s;
-        if (!used) return s;
-    }
-    return 0xffffffffu;
+    w.meta[w.slots.front()].set_read_only(T, 0);
+    w.ordinal++;
+    const uint32_t s = w.slot_at(0);
+    w.meta[s] = SlotMeta();
+    w.meta[s].start_sec = T;
+    w.slots.push_front(s);
+    if (w.slots.size() > c->cfg.num_periods) w.slots.pop_back();
+    w.next_shift_sec = T + 60;
 }
 
 int ensure_started(pv_ctx *c, int64_t sec, int64_t nsec)
 {
     if (c->started) return 0;
     // set_start_tstamp on both managers (AbstractMetricsManager.h:423-431)
-    uint32_t s = alloc_slot(c);
-    clear_slot(c, s, (int64_t)c->global_base);
-    c->meta[s].start_sec = sec;
-    c->meta[s].start_nsec = nsec;
-    c->net.slots.assign(1, s);
-    c->dns.slots.assign(1, s);
-    c->net.next_shift_sec = sec + 60;
-    c->dns.next_shift_sec = sec + 60;
+    for (int part : {PART_NET, PART_DNS}) {
+        Window &w = part == PART_NET ? c->net : c->dns;
+        w.ordinal = 0;
+        clear_part(c, part, 0);
+        w.meta[0].start_sec = sec;
+        w.meta[0].start_nsec = nsec;
+        w.slots.assign(1, 0);
+        w.next_shift_sec = sec + 60;
+    }
     c->started = true;
     return 0;
 }
 
-// Device-side top-N records of one slot: (key, count, name)
+// Device-side top-N records of one table: (key, count, name)
 struct TopRec {
     uint64_t key;
     uint64_t count;
     std::string name;
 };
 
-int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out)
+int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out) // s: table (PV_TSLOT)
 {
     flush_fills(c);
     uint64_t tcap = 1ull << c->tcap_log2;
@@ -619,33 +647,41 @@ double cpc_estimate(const int64_t *t, bool merged)
     return cpc_hip(f);
 }
 
-int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, const Window &win, HostBucket &b)
+// One handler's bucket over `slots` (merged: window_merged_json's fold, AbstractMetricsManager.h:601-647)
+int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int part, HostBucket &b)
 {
     flush_fills(c);
+    const Window &win = part == PART_NET ? c->net : c->dns;
     b.sum.assign(PV_SUM_WORDS, 0);
     b.cpc.assign(PV_MIN_WORDS, PV_CPC_EMPTY);
     b.merged = merged;
+    // this handler's part of the slot's SUM and MIN words
+    const size_t s0 = part == PART_NET ? 0 : PV_OFF_DNS, s1 = part == PART_NET ? PV_SUM_NET_WORDS : PV_SUM_WORDS;
+    const size_t m0 = part == PART_NET ? 0 : PV_MIN_NET_WORDS, m1 = part == PART_NET ? PV_MIN_NET_WORDS : PV_MIN_WORDS;
     std::vector<uint64_t> sum(PV_SUM_WORDS);
     std::vector<int64_t> cpc(PV_MIN_WORDS);
     bool first = true;
     for (uint32_t s : slots) {
         hipError_t e;
-        if (!hip_ok(e = hipMemcpyAsync(sum.data(), c->d_sum + (uint64_t)s * PV_SUM_WORDS, PV_SUM_WORDS * 8, hipMemcpyDeviceToHost, c->stream)) ||
-            !hip_ok(e = hipMemcpyAsync(cpc.data(), c->d_cpc + (uint64_t)s * PV_MIN_WORDS, PV_MIN_WORDS * 8, hipMemcpyDeviceToHost, c->stream)) ||
+        if (!hip_ok(e = hipMemcpyAsync(sum.data() + s0, c->d_sum + (uint64_t)s * PV_SUM_WORDS + s0, (s1 - s0) * 8,
+                                       hipMemcpyDeviceToHost, c->stream)) ||
+            !hip_ok(e = hipMemcpyAsync(cpc.data() + m0, c->d_cpc + (uint64_t)s * PV_MIN_WORDS + m0, (m1 - m0) * 8,
+                                       hipMemcpyDeviceToHost, c->stream)) ||
             !hip_ok(e = hipStreamSynchronize(c->stream)))
             return c->hipfail(e, "read bucket");
-        for (size_t i = 0; i < PV_SUM_WORDS; i++) b.sum[i] += sum[i];
+        for (size_t i = s0; i < s1; i++) b.sum[i] += sum[i];
         // CPC union: a coupon is present if present in any bucket; for a single
         // bucket the first-occurrence order is kept for the HIP replay
-        for (size_t i = 0; i < PV_MIN_WORDS; i++) b.cpc[i] = std::min(b.cpc[i], cpc[i]);
-        const SlotMeta &m = c->meta[s];
+        for (size_t i = m0; i < m1; i++) b.cpc[i] = std::min(b.cpc[i], cpc[i]);
+        const SlotMeta &m = win.meta[s];
         b.period_length += m.read_only ? m.period_length : 0;
         if (first || m.start_sec < b.start_sec) b.start_sec = m.start_sec;
         first = false;
         std::vector<TopRec> recs;
-        int rc = read_topn(c, s, recs);
+        int rc = read_topn(c, s + (part == PART_DNS ? PV_SLOTS : 0), recs);
         if (rc) return rc;
         for (auto &r : recs) b.tops[PV_KEY_METRIC(r.key)][r.name] += r.count;
+        if (part != PART_DNS) continue;
         const uint32_t sg = s | (c->gen[s] << 8);
         for (auto &v : c->xvals_host) {
             if (v.slot != sg) continue;
@@ -654,7 +690,6 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, cons
             else { double d; memcpy(&d, &v.bits, 8); b.ratio.push_back(d); }
         }
     }
-    (void)win;
     return 0;
 }
 
@@ -1035,11 +1070,13 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
         !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_cpc, (size_t)PV_SLOTS * PV_MIN_WORDS * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_tkeys, (size_t)PV_SLOTS * tcap * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_tcnt, (size_t)PV_SLOTS * tcap * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_taux, (size_t)PV_SLOTS * tcap * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_arena, (size_t)PV_SLOTS * c->arena_cap)) ||
-        !hip_ok(e = hipMalloc(&c->d_arena_top, PV_SLOTS * PV_ARENA_PARTS * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_tkeys, (size_t)PV_TABLES * tcap * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_tcnt, (size_t)PV_TABLES * tcap * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_taux, (size_t)PV_TABLES * tcap * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_arena, (size_t)PV_TABLES * c->arena_cap)) ||
+        !hip_ok(e = hipMalloc(&c->d_arena_top, PV_TABLES * PV_ARENA_PARTS * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_dbits, (size_t)(mr / 64 + 2) * 8)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_dbits, (size_t)(mr / 64 + 2) * 8, hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_events, (size_t)ev_cap * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)ev_cap * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_mq_cnt, 65536 * 4)) ||
@@ -1092,7 +1129,8 @@ void pv_destroy(pv_ctx *c)
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
                     c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx};
     for (void *p : ptrs) if (p) hipFree(p);
-    for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status})
+    if (c->d_dbits) hipFree(c->d_dbits);
+    for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits})
         if (hp) hipHostFree(hp);
     for (auto &st : c->stage) {
         if (st.h_recs) hipHostFree(st.h_recs);
@@ -1111,9 +1149,13 @@ int pv_reset(pv_ctx *c)
 {
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
-    for (uint32_t s = 0; s < PV_SLOTS; s++) c->slot_used[s] = false;
-    c->net = Window();
-    c->dns = Window();
+    // device state stays as it is: which slot parts are clean carries over
+    for (Window *w : {&c->net, &c->dns}) {
+        bool cl[PV_SLOTS];
+        memcpy(cl, w->clean, sizeof cl);
+        *w = Window();
+        memcpy(w->clean, cl, sizeof cl);
+    }
     c->started = c->ended = false;
     c->records_seen = 0;
     c->xvals_host.clear();
@@ -1169,48 +1211,61 @@ int pv_index_records(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32
     return 0;
 }
 
-int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
-                      const uint32_t *sc_idx, const uint32_t *sc_sec, void *stream)
-{
-    std::lock_guard<std::mutex> g(c->mu);
-    hipSetDevice(c->device);
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    hipStream_t saved = c->stream;
-    c->stream = st;
-    struct Restore { pv_ctx *c; hipStream_t s; ~Restore() { c->stream = s; } } restore{c, saved};
-    const uint64_t n = info->n_records;
-    if (n == 0) return 0;
-    if (n > c->max_records) return c->fail(PV_ECAPACITY, "batch of %llu records exceeds max_records %llu",
-                                           (unsigned long long)n, (unsigned long long)c->max_records);
-    ensure_started(c, info->first_sec, info->first_nsec);
+namespace {
 
-    // ---- period shifts inside this batch (AbstractMetricsManager::new_event)
-    const uint32_t np = c->cfg.num_periods;
-    std::vector<int64_t> thresh;
-    std::vector<uint64_t> pstart; // first record index of each new period (monotone runs)
-    if (np > 1) {
-        int64_t T = c->net.next_shift_sec;
-        if (info->last_sec >= T || !info->monotone) {
-            if (!info->monotone) {
-                // any record at or beyond the next boundary in a non-monotone run needs per-record periods
-                bool crosses = false;
-                for (uint32_t k = 0; k < info->n_sec_changes; k++) crosses |= (int64_t)sc_sec[k] >= T;
-                if (crosses) return c->fail(PV_EUNSUPPORTED, "period shift inside a batch with non-monotone timestamps");
-            } else {
-                for (uint32_t k = 0; k < info->n_sec_changes; k++) {
-                    if ((int64_t)sc_sec[k] >= T) {
-                        thresh.push_back(sc_sec[k]);
-                        pstart.push_back(sc_idx[k]);
-                        T = (int64_t)sc_sec[k] + 60;
-                    }
-                }
-            }
+// A period shift inside a batch: its threshold second (the shifting event's ts_sec) and the
+// batch record index of that event (AbstractMetricsManager::new_event, src/AbstractMetricsManager.h:318-333)
+struct Shift {
+    int64_t sec;
+    uint64_t idx;
+};
+
+// The Net manager's shifts: every packet is a Net event, so the first record with
+// ts_sec >= next_shift shifts, then next_shift = its second + 60, repeatedly.
+void net_shifts_of(int64_t T, const pv_index_info *info, const uint32_t *sc_idx, const uint32_t *sc_sec,
+                   std::vector<Shift> &out)
+{
+    for (uint32_t k = 0; k < info->n_sec_changes; k++)
+        if ((int64_t)sc_sec[k] >= T) {
+            out.push_back({(int64_t)sc_sec[k], sc_idx[k]});
+            T = (int64_t)sc_sec[k] + 60;
+        }
+}
+
+uint64_t next_bit(const uint64_t *bits, uint64_t from, uint64_t n)
+{
+    for (uint64_t w = from >> 6; (w << 6) < n; w++) {
+        uint64_t v = bits[w];
+        if (w == (from >> 6)) v &= ~0ull << (from & 63);
+        if (v) {
+            const uint64_t i = (w << 6) + (uint64_t)__builtin_ctzll(v);
+            return i < n ? i : n;
         }
     }
-    if (thresh.size() > PV_MAX_SHIFTS)
-        return c->fail(PV_EUNSUPPORTED, "%zu period shifts in one batch (max %d): submit smaller batches", thresh.size(), PV_MAX_SHIFTS);
+    return n;
+}
 
-    PvParams P;
+// The DNS manager's shifts: the first DNS event (pv_dns_prescan's bits) with ts_sec >=
+// next_shift, then next_shift = its second + 60, repeatedly (monotone batch).
+void dns_shifts_of(int64_t T, const uint64_t *bits, uint64_t n, const pv_index_info *info, const uint32_t *sc_idx,
+                   const uint32_t *sc_sec, std::vector<Shift> &out)
+{
+    const uint32_t nsc = info->n_sec_changes;
+    uint32_t k = 0;
+    for (;;) {
+        while (k < nsc && (int64_t)sc_sec[k] < T) k++;
+        if (k == nsc) return;
+        const uint64_t i = next_bit(bits, sc_idx[k], n);
+        if (i >= n) return;
+        while (k + 1 < nsc && sc_idx[k + 1] <= i) k++;
+        out.push_back({(int64_t)sc_sec[k], i});
+        T = (int64_t)sc_sec[k] + 60;
+    }
+}
+
+// parameter fields every kernel reads: record access, parse configuration, DNS filters
+void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n)
+{
     memset(&P, 0, sizeof P);
     P.recs = d_recs;
     P.offs = d_offs;
@@ -1219,32 +1274,64 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.ts_nano = c->cfg.ts_nano;
     P.net_groups = c->net_groups;
     P.dns_groups = c->dns_groups;
-    P.n_shift = (uint32_t)thresh.size();
-    for (size_t k = 0; k < thresh.size(); k++) { P.thresh[k] = thresh[k]; P.pstart[k] = pstart[k]; }
-    P.skip_before = P.n_shift + 1 > np ? P.n_shift + 1 - np : 0;
-    P.gbase = c->global_base + c->records_seen;
     P.nets = c->nets;
-    // slots: period 0 -> live; each shift -> a fresh slot
-    P.slot_of[0] = c->net.slots.front();
-    std::vector<uint32_t> new_slots;
-    {
-        // reserve fresh slots for the shifts that stay in the window
-        std::deque<uint32_t> sim = c->net.slots;
-        for (uint32_t k = 1; k <= P.n_shift; k++) {
-            uint32_t s = 0xffffffffu;
-            for (uint32_t cand = 0; cand < PV_SLOTS && s == 0xffffffffu; cand++) {
-                bool used = false;
-                for (auto x : sim) used |= x == cand;
-                for (auto x : c->dns.slots) used |= x == cand;
-                for (auto x : new_slots) used |= x == cand;
-                if (!used) s = cand;
-            }
-            if (s == 0xffffffffu) return c->fail(PV_ECAPACITY, "no free bucket slot");
-            new_slots.push_back(s);
-            P.slot_of[k] = s;
-            clear_slot(c, s, (int64_t)P.gbase);
-            c->meta[s].start_sec = thresh[k - 1];
-        }
+    P.f_flags = c->f_flags;
+    P.f_rcode_mask = c->f_rcode_mask;
+    P.f_ancount = c->f_ancount;
+    P.f_nq = c->f_nq;
+    for (uint32_t k = 0; k < c->f_nq; k++) P.f_qt[k] = c->f_qt[k];
+    P.f_nqn = c->f_nqn;
+    for (uint32_t k = 0; k < c->f_nqn; k++) P.f_qn[k] = c->f_qn[k];
+    P.f_nsx = c->f_nsx;
+    P.sfx_of = c->d_sfx;
+    for (uint32_t k = 0; k < c->f_nsx; k++) { P.f_sxl[k] = c->f_sxl[k]; P.f_sxh[k] = c->f_sxh[k]; }
+    P.dbits = c->d_dbits;
+}
+
+// pv_dns_prescan over a batch, its bits copied to c->h_dbits (synchronises)
+int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, hipStream_t st)
+{
+    flush_fills(c);
+    PvParams P;
+    params_common(c, P, d_recs, d_offs, n);
+    hipError_t e;
+    *c->h_params = P;
+    if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
+        return c->hipfail(e, "parameter upload");
+    const uint64_t tiles = (n + 63) / 64;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + 3) / 4, (uint64_t)c->cus * 8);
+    hipLaunchKernelGGL(pv_dns_prescan, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_dns_prescan");
+    if (!hip_ok(e = hipMemcpyAsync(c->h_dbits, c->d_dbits, tiles * 8, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "DNS prescan");
+    return 0;
+}
+
+// One device batch with at most PV_MAX_SHIFTS shifts of each manager. nsh / dsh: the Net and
+// DNS shifts inside it (record indices relative to d_offs).
+int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, uint64_t rec_bytes,
+                 const std::vector<Shift> &nsh, const std::vector<Shift> &dsh, hipStream_t st)
+{
+    const uint32_t np = c->cfg.num_periods;
+    PvParams P;
+    params_common(c, P, d_recs, d_offs, n);
+    P.gbase = c->global_base + c->records_seen;
+    // Net periods and slots: period 0 -> the live bucket, each shift -> the next ordinal's slot
+    P.n_shift = (uint32_t)nsh.size();
+    for (size_t k = 0; k < nsh.size(); k++) { P.thresh[k] = nsh[k].sec; P.pstart[k] = nsh[k].idx; }
+    P.skip_before = P.n_shift + 1 > np ? P.n_shift + 1 - np : 0;
+    for (uint32_t k = 0; k <= P.n_shift; k++) {
+        P.slot_of[k] = c->net.slot_at(k);
+        if (k) clear_part(c, PART_NET, P.slot_of[k]);
+    }
+    // DNS periods and slots, from the DNS manager's own shifts
+    P.n_dshift = (uint32_t)dsh.size();
+    for (size_t k = 0; k < dsh.size(); k++) P.dthresh[k] = dsh[k].sec;
+    P.dskip_before = P.n_dshift + 1 > np ? P.n_dshift + 1 - np : 0;
+    for (uint32_t k = 0; k <= P.n_dshift; k++) {
+        P.dslot_of[k] = c->dns.slot_at(k);
+        if (k) clear_part(c, PART_DNS, P.dslot_of[k]);
     }
     P.sum = c->d_sum;
     P.cpc = c->d_cpc;
@@ -1261,25 +1348,14 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.skeys = c->d_skeys;
     P.svals = c->d_svals;
     P.n_events = c->d_status + ST_NEV; // [0] packed total, [1] responses (ST_NRESP)
+    P.n_dns = c->d_status + ST_NDNS;
     P.want_events = (c->dns_groups & PV_DNS_TRANSACTIONS) ? 1 : 0;
-    P.f_flags = c->f_flags;
-    P.f_rcode_mask = c->f_rcode_mask;
-    P.f_ancount = c->f_ancount;
-    P.f_nq = c->f_nq;
-    for (uint32_t k = 0; k < c->f_nq; k++) P.f_qt[k] = c->f_qt[k];
-    P.f_nqn = c->f_nqn;
-    for (uint32_t k = 0; k < c->f_nqn; k++) P.f_qn[k] = c->f_qn[k];
-    P.f_nsx = c->f_nsx;
-    P.sfx_of = c->d_sfx;
-    for (uint32_t k = 0; k < c->f_nsx; k++) { P.f_sxl[k] = c->f_sxl[k]; P.f_sxh[k] = c->f_sxh[k]; }
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
     if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0xffffffffull)
         return c->fail(PV_ECAPACITY, "open DNS queries carried over more than 2^32 records without a response");
     P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
     P.flags = c->d_status + ST_FLAGS;
-    P.dns_first = c->d_status + ST_DNS_ANY;
-    P.dns_at_thresh = c->d_status + ST_DNS_AT;
     launch_fill32(c, c->d_status, ST_TP_CNT + (1u << c->reg_log2), 0);
     hipError_t e;
     const uint64_t tiles = (n + 63) / 64; // 64-record wave tiles
@@ -1287,7 +1363,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     // occupancy), each owning a contiguous run of wave tiles
     uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->cus * c->wg_per_cu);
     P.wt_per_block = (uint32_t)((tiles + grid - 1) / grid);
-    P.rec_bytes = info->bytes_used;
+    P.rec_bytes = rec_bytes;
     {
         static const char *dbg = getenv("PV_DEBUG_STAGES");
         P.dbg = dbg ? (uint32_t)atoi(dbg) : 0;
@@ -1328,16 +1404,6 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     P.stamps = c->d_stamps;
     P.dq = c->d_dq;
     P.dq_cnt = c->d_dq_cnt;
-    // tiles that hold a period shift go to pv_boundary_kernel
-    P.n_btiles = 0;
-    for (uint32_t k = 0; k < P.n_shift; k++) {
-        const uint64_t ps = P.pstart[k];
-        if (ps % 64 == 0 || ps >= n) continue;
-        const uint32_t t = (uint32_t)(ps / 64);
-        bool seen = false;
-        for (uint32_t j = 0; j < P.n_btiles; j++) seen |= P.btile[j] == t;
-        if (!seen) P.btile[P.n_btiles++] = t;
-    }
     flush_fills(c);
     *c->h_params = P;
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
@@ -1357,13 +1423,9 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     hipLaunchKernelGGL(pv_topn_scatter, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_merge, dim3(1u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 8), dim3(256), 0, st, (const PvParams *)c->d_params);
-    if (P.n_btiles) {
-        hipLaunchKernelGGL(pv_boundary_kernel, dim3(P.n_btiles), dim3(64), 0, st, (const PvParams *)c->d_params);
-        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_boundary_kernel");
-    }
     if (P.want_events)
-        hipLaunchKernelGGL(pv_xact_compact, dim3(grid + P.n_btiles), dim3(256), 0, st, (const PvParams *)c->d_params,
-                           grid + P.n_btiles);
+        hipLaunchKernelGGL(pv_xact_compact, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params, grid);
+    if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch");
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
     uint32_t status[ST_WORDS];
@@ -1375,15 +1437,19 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         float ms = 0;
         if (hipEventElapsedTime(&ms, c->ev_start, c->ev_stop) == hipSuccess) { c->kernel_ms += ms; c->kernel_launches++; }
     }
+    // the parts this batch wrote are no longer clean
+    for (uint32_t k = 0; k <= P.n_shift; k++) c->net.clean[P.slot_of[k]] = false;
+    if (status[ST_NDNS])
+        for (uint32_t k = 0; k <= P.n_dshift; k++) c->dns.clean[P.dslot_of[k]] = false;
     uint32_t flags = status[ST_FLAGS];
     if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
     if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
     if (getenv("PV_STAMPS")) {
-        std::vector<uint64_t> st((size_t)grid * 4 * 8);
-        if (hip_ok(hipMemcpy(st.data(), c->d_stamps, st.size() * 8, hipMemcpyDeviceToHost))) {
+        std::vector<uint64_t> stv((size_t)grid * 4 * 8);
+        if (hip_ok(hipMemcpy(stv.data(), c->d_stamps, stv.size() * 8, hipMemcpyDeviceToHost))) {
             double sum[8] = {0};
             for (size_t w = 0; w < (size_t)grid * 4; w++)
-                for (int k = 0; k < 8; k++) sum[k] += (double)st[w * 8 + k];
+                for (int k = 0; k < 8; k++) sum[k] += (double)stv[w * 8 + k];
             fprintf(stderr, "pv_stamps (mean cycles per wave, %u wave tiles/wg):", P.wt_per_block);
             static const char *nm[8] = {"slot", "commit", "barA", "issue", "parse", "lane", "barB", "flush"};
             for (int k = 0; k < 8; k++) fprintf(stderr, " %s=%.0f", nm[k], sum[k] / (grid * 4.0));
@@ -1392,19 +1458,11 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     }
     const uint32_t nev_b = status[ST_NEV];
     const uint32_t nresp = status[ST_NRESP];
-    // TransactionManager state across batches: a batch with responses or a period shift
+    // TransactionManager state across batches: a batch with responses or a DNS period shift
     // pairs (sort + resolve) its events together with the queries carried in; a batch of
     // queries only just appends them to the carried list
     const bool dns_here = nev_b > 0;
-    // DNS events of any kind (a filtered event or, with transactions off, any event leaves no
-    // transaction record but still drives the DNS window: AbstractMetricsManager::new_event)
-    const bool dns_evt = dns_here || status[ST_DNS_ANY];
-    if (dns_evt)
-        for (uint32_t k = 1; k <= P.n_shift; k++)
-            if (!status[ST_DNS_AT + k])
-                return c->fail(PV_EUNSUPPORTED, "DNS period boundary differs from the Net boundary at second %lld",
-                               (long long)thresh[k - 1]);
-    bool pair = dns_here && (nresp > 0 || P.n_shift > 0);
+    bool pair = dns_here && (nresp > 0 || P.n_dshift > 0);
     if (dns_here && !pair && c->n_pend + nev_b > c->pend_cap) pair = true; // compact the carried list
     if (dns_here && !pair) {
         hipLaunchKernelGGL(pv_xact_defer, dim3((nev_b + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
@@ -1435,8 +1493,8 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         X.ttl_s = c->ttl_s;
         X.ttl_ms = c->ttl_ms;
         X.quantiles = (c->dns_groups & PV_DNS_QUANTILES) ? 1 : 0;
-        for (uint32_t k = 0; k <= P.n_shift; k++) {
-            X.slot_gen[k] = P.slot_of[k] | (c->gen[P.slot_of[k]] << 8);
+        for (uint32_t k = 0; k <= P.n_dshift; k++) {
+            X.slot_gen[k] = P.dslot_of[k] | (c->gen[P.dslot_of[k]] << 8);
             X.thr_from[k] = k == 0 ? c->from90 : -1.0f;
             X.thr_to[k] = k == 0 ? c->to90 : -1.0f;
         }
@@ -1459,13 +1517,13 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
         hipLaunchKernelGGL(pv_xact_carry, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_carry");
-        if (P.n_shift > 0 && (c->dns_groups & PV_DNS_QUANTILES)) {
+        if (P.n_dshift > 0 && (c->dns_groups & PV_DNS_QUANTILES)) {
             // on_period_shift: slow thresholds = p90 of the bucket that just closed
             // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
             int rc = sync_xvals(c);
             if (rc) return rc;
-            for (uint32_t k = 1; k <= P.n_shift; k++) {
-                const uint32_t sg = P.slot_of[k - 1] | (c->gen[P.slot_of[k - 1]] << 8);
+            for (uint32_t k = 1; k <= P.n_dshift; k++) {
+                const uint32_t sg = P.dslot_of[k - 1] | (c->gen[P.dslot_of[k - 1]] << 8);
                 std::vector<uint64_t> fr, to;
                 for (auto &v : c->xvals_host) {
                     if (v.slot != sg) continue;
@@ -1508,22 +1566,78 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         c->pend_base = (int64_t)(c->records_seen + n) - 1;
     }
 
-    // ---- window bookkeeping (host mirror of _period_shift)
-    for (uint32_t k = 1; k <= P.n_shift; k++) {
-        uint32_t s = P.slot_of[k];
-        int64_t T = thresh[k - 1];
-        c->meta[c->net.slots.front()].set_read_only(T, 0);
-        c->net.slots.push_front(s);
-        if (c->net.slots.size() > np) c->net.slots.pop_back();
-        c->net.next_shift_sec = T + 60;
-        if (dns_evt) {
-            c->dns_shifts.emplace_back(T, s);
-            c->dns.slots.push_front(s);
-            if (c->dns.slots.size() > np) c->dns.slots.pop_back();
-            c->dns.next_shift_sec = T + 60;
-        }
+    // ---- window bookkeeping (host mirror of each manager's _period_shift)
+    for (const Shift &sh : nsh) win_shift(c, c->net, sh.sec);
+    for (const Shift &sh : dsh) {
+        win_shift(c, c->dns, sh.sec);
+        c->dns_shifts.emplace_back(sh.sec, c->dns.slot_at(0));
     }
     c->records_seen += n;
+    return 0;
+}
+
+// Both managers' shifts of a batch (Net from the record seconds, DNS from the prescan bits)
+int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
+                 const uint32_t *sc_idx, const uint32_t *sc_sec, hipStream_t st, std::vector<Shift> &nsh,
+                 std::vector<Shift> &dsh)
+{
+    if (c->cfg.num_periods <= 1) return 0;
+    const bool net_may = info->last_sec >= c->net.next_shift_sec, dns_may = info->last_sec >= c->dns.next_shift_sec;
+    if (!net_may && !dns_may) return 0;
+    if (!info->monotone) {
+        // a shift decided per event needs event order = time order
+        for (uint32_t k = 0; k < info->n_sec_changes; k++)
+            if ((int64_t)sc_sec[k] >= std::min(c->net.next_shift_sec, c->dns.next_shift_sec))
+                return c->fail(PV_EUNSUPPORTED, "period shift inside a batch with non-monotone timestamps");
+        return 0;
+    }
+    if (net_may) net_shifts_of(c->net.next_shift_sec, info, sc_idx, sc_sec, nsh);
+    if (dns_may) {
+        if (int rc = dns_prescan(c, d_recs, d_offs, info->n_records, st)) return rc;
+        dns_shifts_of(c->dns.next_shift_sec, c->h_dbits, info->n_records, info, sc_idx, sc_sec, dsh);
+    }
+    return 0;
+}
+
+} // namespace
+
+int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
+                      const uint32_t *sc_idx, const uint32_t *sc_sec, void *stream)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t saved = c->stream;
+    c->stream = st;
+    struct Restore { pv_ctx *c; hipStream_t s; ~Restore() { c->stream = s; } } restore{c, saved};
+    const uint64_t n = info->n_records;
+    if (n == 0) return 0;
+    if (n > c->max_records) return c->fail(PV_ECAPACITY, "batch of %llu records exceeds max_records %llu",
+                                           (unsigned long long)n, (unsigned long long)c->max_records);
+    ensure_started(c, info->first_sec, info->first_nsec);
+    std::vector<Shift> nsh, dsh;
+    if (int rc = batch_shifts(c, d_recs, d_offs, info, sc_idx, sc_sec, st, nsh, dsh)) return rc;
+    // spans of at most PV_MAX_SHIFTS shifts of each manager, cut at the shifting record
+    uint64_t a = 0;
+    size_t ni = 0, di = 0;
+    while (a < n) {
+        uint64_t b = n;
+        if (nsh.size() - ni > PV_MAX_SHIFTS) b = std::min<uint64_t>(b, nsh[ni + PV_MAX_SHIFTS].idx);
+        if (dsh.size() - di > PV_MAX_SHIFTS) b = std::min<uint64_t>(b, dsh[di + PV_MAX_SHIFTS].idx);
+        std::vector<Shift> ns, ds;
+        for (; ni < nsh.size() && nsh[ni].idx < b; ni++) ns.push_back({nsh[ni].sec, nsh[ni].idx - a});
+        for (; di < dsh.size() && dsh[di].idx < b; di++) ds.push_back({dsh[di].sec, dsh[di].idx - a});
+        uint64_t rec_bytes = info->bytes_used;
+        if (b < n) {
+            uint32_t ob = 0;
+            hipError_t e;
+            if (!hip_ok(e = hipMemcpyAsync(&ob, d_offs + b, 4, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)))
+                return c->hipfail(e, "span end");
+            rec_bytes = ob;
+        }
+        if (int rc = process_span(c, d_recs, d_offs + a, b - a, rec_bytes, ns, ds, st)) return rc;
+        a = b;
+    }
     c->last_sec = info->last_sec;
     c->last_nsec = info->last_nsec;
     return 0;
@@ -1551,9 +1665,9 @@ int ingest_setup(pv_ctx *c)
     c->pool.reset(new pvi::Pool(pvi::default_threads()));
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) return c->hipfail(e, "copy stream");
     for (auto &st : c->stage) {
-        if (!hip_ok(e = hipHostMalloc((void **)&st.h_recs, chunk + 256, hipHostMallocDefault)) ||
+        if (!hip_ok(e = hipHostMalloc((void **)&st.h_recs, chunk + PV_RECS_PAD, hipHostMallocDefault)) ||
             !hip_ok(e = hipHostMalloc((void **)&st.h_offs, c->stage_recs * 4, hipHostMallocDefault)) ||
-            !hip_ok(e = hipMalloc(&st.d_recs, chunk + 256)) || !hip_ok(e = hipMalloc(&st.d_offs, c->stage_recs * 4)) ||
+            !hip_ok(e = hipMalloc(&st.d_recs, chunk + PV_RECS_PAD)) || !hip_ok(e = hipMalloc(&st.d_offs, c->stage_recs * 4)) ||
             !hip_ok(e = hipEventCreateWithFlags(&st.copied, hipEventDisableTiming)))
             return c->hipfail(e, "ingest staging");
         st.sci.resize(1 << 16);
@@ -1578,6 +1692,43 @@ double ms_since(std::chrono::steady_clock::time_point t0)
 }
 
 } // namespace
+
+// pv_dns_event_seconds over records in host memory, through the ingest staging (chunked).
+int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int64_t *secs, uint32_t max, uint32_t *n)
+{
+    hipSetDevice(c->device);
+    *n = 0;
+    if (int rc = ingest_setup(c)) return rc;
+    pv_ctx::Stage &st = c->stage[0];
+    size_t pos = 0;
+    uint32_t k = 0;
+    while (pos < bytes) {
+        const size_t L = std::min(c->stage_bytes, bytes - pos);
+        int rc = pvi::index_records_parallel(*c->pool, recs + pos, L, c->cfg.ts_nano, st.h_offs, c->stage_recs,
+                                             st.sci.data(), st.scs.data(), (uint32_t)st.sci.size(), &st.info, st.h_recs);
+        if (rc) return c->fail(rc, "record index failed");
+        if (st.info.n_records == 0) return c->fail(PV_ECAPACITY, "record larger than the ingest chunk");
+        const size_t used = st.info.bytes_used;
+        hipError_t e;
+        if (!hip_ok(e = hipMemcpyAsync(st.d_recs, st.h_recs, used, hipMemcpyHostToDevice, c->stream)) ||
+            !hip_ok(e = hipMemsetAsync(st.d_recs + used, 0, PV_RECS_PAD, c->stream)) ||
+            !hip_ok(e = hipMemcpyAsync(st.d_offs, st.h_offs, st.info.n_records * 4, hipMemcpyHostToDevice, c->stream)))
+            return c->hipfail(e, "H2D");
+        std::vector<int64_t> part(st.info.n_sec_changes);
+        uint32_t m = 0;
+        if ((rc = pv_dns_event_seconds(c, st.d_recs, st.d_offs, &st.info, st.sci.data(), st.scs.data(), part.data(),
+                                       (uint32_t)part.size(), &m)))
+            return rc;
+        for (uint32_t j = 0; j < m; j++) {
+            if (k && secs[k - 1] == part[j]) continue; // a second split across chunks
+            if (k >= max) return c->fail(PV_ECAPACITY, "more than %u DNS seconds", max);
+            secs[k++] = part[j];
+        }
+        pos += used;
+    }
+    *n = k;
+    return 0;
+}
 
 // Host-memory path, pipelined over chunks of the record blob: a producer thread stages
 // chunk k + 1 (parallel copy into pinned memory unless the caller's buffer is already
@@ -1639,7 +1790,7 @@ int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
             const size_t used = st.info.bytes_used;
             hipError_t e;
             if (!hip_ok(e = hipMemcpyAsync(st.d_recs, base, used, hipMemcpyHostToDevice, c->copy_stream)) ||
-                !hip_ok(e = hipMemsetAsync(st.d_recs + used, 0, 256, c->copy_stream)) ||
+                !hip_ok(e = hipMemsetAsync(st.d_recs + used, 0, PV_RECS_PAD, c->copy_stream)) ||
                 !hip_ok(e = hipMemcpyAsync(st.d_offs, st.h_offs, st.info.n_records * 4, hipMemcpyHostToDevice,
                                            c->copy_stream)) ||
                 !hip_ok(e = hipEventRecord(st.copied, c->copy_stream))) {
@@ -1723,8 +1874,8 @@ int pv_set_end_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
 {
     if (!c->started) return 0;
     // end_tstamp_signal: the live bucket of each manager becomes read-only
-    c->meta[c->net.slots.front()].set_read_only(sec, nsec);
-    if (c->dns.slots.front() != c->net.slots.front()) c->meta[c->dns.slots.front()].set_read_only(sec, nsec);
+    c->net.meta[c->net.slots.front()].set_read_only(sec, nsec);
+    c->dns.meta[c->dns.slots.front()].set_read_only(sec, nsec);
     c->ended = true;
     return 0;
 }
@@ -1743,7 +1894,7 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
     {
         if ((rc = window_slots(c, c->net, period, merged != 0, slots))) return rc;
         HostBucket b;
-        if ((rc = load_bucket(c, slots, merged != 0, c->net, b))) return rc;
+        if ((rc = load_bucket(c, slots, merged != 0, PART_NET, b))) return rc;
         j.key("packets").obj();
         net_json(c, j, b);
         j.end_obj();
@@ -1751,7 +1902,7 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
     {
         if ((rc = window_slots(c, c->dns, period, merged != 0, slots))) return rc;
         HostBucket b;
-        if ((rc = load_bucket(c, slots, merged != 0, c->dns, b))) return rc;
+        if ((rc = load_bucket(c, slots, merged != 0, PART_DNS, b))) return rc;
         j.key("dns").obj();
         dns_json(c, j, b);
         j.end_obj();
@@ -1771,14 +1922,14 @@ int pv_state_regions(pv_ctx *c, void **sum_ptr, size_t *sum_bytes, void **min_pt
     return 0;
 }
 
-// record: u32 slot, u64 key, u64 count, u16 name_len, name bytes
+// record: u32 table, u64 key, u64 count, u16 name_len, name bytes
 int pv_export_topn(pv_ctx *c, uint8_t **buf, size_t *bytes)
 {
     flush_fills(c);
     std::vector<uint8_t> o;
-    std::vector<uint32_t> live;
+    std::vector<uint32_t> live; // the tables of both windows
     for (auto s : c->net.slots) live.push_back(s);
-    for (auto s : c->dns.slots) if (std::find(live.begin(), live.end(), s) == live.end()) live.push_back(s);
+    for (auto s : c->dns.slots) live.push_back(s + PV_SLOTS);
     for (uint32_t s : live) {
         std::vector<TopRec> recs;
         int rc = read_topn(c, s, recs);
@@ -1806,7 +1957,7 @@ int pv_merge_topn(pv_ctx *c, const uint8_t *buf, size_t bytes)
     while (p + 22 <= bytes) {
         uint32_t s; uint64_t key, cnt; uint16_t l;
         memcpy(&s, buf + p, 4); memcpy(&key, buf + p + 4, 8); memcpy(&cnt, buf + p + 12, 8); memcpy(&l, buf + p + 20, 2);
-        if (p + 22 + l > bytes || s >= PV_SLOTS) return c->fail(PV_EINVAL, "malformed top-N buffer");
+        if (p + 22 + l > bytes || s >= PV_TABLES) return c->fail(PV_EINVAL, "malformed top-N buffer");
         auto &e = c->remote_topn[s][key];
         e.first += cnt;
         e.second.assign((const char *)buf + p + 22, l);
@@ -1815,16 +1966,27 @@ int pv_merge_topn(pv_ctx *c, const uint8_t *buf, size_t bytes)
     return 0;
 }
 
-int pv_window_slots(pv_ctx *c, uint32_t *slots, uint32_t max_slots, uint32_t *n_slots, size_t *sum_slot_words,
-                    size_t *min_slot_words)
+// The device regions of both live windows a multi-GPU reduce combines: each Net slot's
+// net part and each DNS slot's dns part of the SUM (all-reduce SUM) and MIN (all-reduce MIN)
+// words. The caller writes them, so they stop being clean.
+int pv_window_regions(pv_ctx *c, pv_region *r, uint32_t max, uint32_t *n)
 {
-    std::vector<uint32_t> v;
-    for (auto s : c->net.slots) v.push_back(s);
-    for (auto s : c->dns.slots) if (std::find(v.begin(), v.end(), s) == v.end()) v.push_back(s);
-    *n_slots = (uint32_t)v.size();
-    for (uint32_t i = 0; i < v.size() && i < max_slots; i++) slots[i] = v[i];
-    *sum_slot_words = PV_SUM_WORDS;
-    *min_slot_words = PV_MIN_WORDS;
+    std::lock_guard<std::mutex> g(c->mu);
+    flush_fills(c);
+    std::vector<pv_region> v;
+    for (uint32_t s : c->net.slots) {
+        v.push_back(pv_region{c->d_sum + (size_t)s * PV_SUM_WORDS, PV_SUM_NET_WORDS, PV_REDUCE_SUM, 0});
+        v.push_back(pv_region{c->d_cpc + (size_t)s * PV_MIN_WORDS, PV_MIN_NET_WORDS, PV_REDUCE_MIN, 0});
+        c->net.clean[s] = false;
+    }
+    for (uint32_t s : c->dns.slots) {
+        v.push_back(pv_region{c->d_sum + (size_t)s * PV_SUM_WORDS + PV_OFF_DNS, PV_SUM_WORDS - PV_OFF_DNS, PV_REDUCE_SUM, 0});
+        v.push_back(pv_region{c->d_cpc + (size_t)s * PV_MIN_WORDS + PV_MIN_NET_WORDS, PV_MIN_WORDS - PV_MIN_NET_WORDS,
+                              PV_REDUCE_MIN, 0});
+        c->dns.clean[s] = false;
+    }
+    *n = (uint32_t)v.size();
+    for (uint32_t i = 0; i < v.size() && i < max; i++) r[i] = v[i];
     return 0;
 }
 
@@ -1885,6 +2047,7 @@ int purge_shift(const std::vector<std::pair<int64_t, uint32_t>> &sh, uint32_t tt
 int add_dns_words(pv_ctx *c, uint32_t slot, const uint64_t add[4])
 {
     static const int w[4] = {DC_XTOTAL, DC_XOUT, DC_XIN, DC_XTIMEOUT};
+    c->dns.clean[slot] = false;
     for (int k = 0; k < 4; k++) {
         if (!add[k]) continue;
         uint64_t *dp = c->d_sum + (size_t)slot * PV_SUM_WORDS + PV_OFF_DNS + w[k];
@@ -2060,17 +2223,62 @@ int pv_values_merge(pv_ctx *c, const uint8_t *buf, size_t bytes)
     return 0;
 }
 
-// Window identity for the merge: (slot, start second) of every live slot, newest first.
-int pv_window_periods(pv_ctx *c, uint32_t *slots, int64_t *start_sec, uint32_t max_n, uint32_t *n)
+// Window identity for the merge: (slot, start second) of every live bucket of one manager
+// (part 0 = Net, 1 = DNS), newest first.
+int pv_window_periods(pv_ctx *c, int part, uint32_t *slots, int64_t *start_sec, uint32_t max_n, uint32_t *n)
 {
-    std::vector<uint32_t> v;
-    for (auto s : c->net.slots) v.push_back(s);
-    for (auto s : c->dns.slots) if (std::find(v.begin(), v.end(), s) == v.end()) v.push_back(s);
-    *n = (uint32_t)v.size();
-    for (uint32_t i = 0; i < v.size() && i < max_n; i++) {
-        slots[i] = v[i];
-        start_sec[i] = c->meta[v[i]].start_sec;
+    std::lock_guard<std::mutex> g(c->mu);
+    const Window &w = part == PART_NET ? c->net : c->dns;
+    *n = (uint32_t)w.slots.size();
+    for (uint32_t i = 0; i < w.slots.size() && i < max_n; i++) {
+        slots[i] = w.slots[i];
+        start_sec[i] = w.meta[w.slots[i]].start_sec;
     }
+    return 0;
+}
+
+// Shifts of one manager that happen outside this context's stream (a sharded run: those
+// whose shifting event lies in another rank's shard), applied in order as window operations
+// only: a bucket opens at each threshold second (empty here), the oldest drops out, and
+// next_shift moves on. No transaction purge is counted for them here (the shard that holds
+// the shifting event counts its purges through pv_edge_merge).
+int pv_advance_windows(pv_ctx *c, int part, const int64_t *thresh, uint32_t n)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    if (part != PART_NET && part != PART_DNS) return c->fail(PV_EINVAL, "part %d", part);
+    if (!c->started) return c->fail(PV_EINVAL, "pv_advance_windows before the start timestamp");
+    if (c->cfg.num_periods <= 1) return 0;
+    Window &w = part == PART_NET ? c->net : c->dns;
+    for (uint32_t k = 0; k < n; k++) {
+        if (thresh[k] < w.next_shift_sec)
+            return c->fail(PV_EINVAL, "shift at %lld precedes the window's next shift %lld", (long long)thresh[k],
+                           (long long)w.next_shift_sec);
+        clear_part(c, part, w.slot_at(1));
+        win_shift(c, w, thresh[k]);
+    }
+    return 0;
+}
+
+// The seconds (stream order, each once) in which a batch holds a DNS event, by pv_dns_prescan.
+// A sharded run's ranks exchange these to compute the DNS manager's global shifts.
+int pv_dns_event_seconds(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
+                         const uint32_t *sc_idx, const uint32_t *sc_sec, int64_t *secs, uint32_t max, uint32_t *n)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    *n = 0;
+    const uint64_t nr = info->n_records;
+    if (!nr) return 0;
+    if (nr > c->max_records) return c->fail(PV_ECAPACITY, "batch exceeds max_records");
+    if (int rc = dns_prescan(c, d_recs, d_offs, nr, c->stream)) return rc;
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < info->n_sec_changes; j++) {
+        const uint64_t lo = sc_idx[j], hi = j + 1 < info->n_sec_changes ? sc_idx[j + 1] : nr;
+        if (next_bit(c->h_dbits, lo, nr) >= hi) continue;
+        if (k >= max) return c->fail(PV_ECAPACITY, "more than %u DNS seconds", max);
+        secs[k++] = sc_sec[j];
+    }
+    *n = k;
     return 0;
 }
 

@@ -173,8 +173,9 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     parse_record(R, P, P.offs[rep], o);
     const uint32_t part = (blockIdx.x * 7 + threadIdx.x / 64) & (PV_ARENA_PARTS - 1);
     const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
-    unsigned long long *top = (unsigned long long *)&P.arena_top[slot * PV_ARENA_PARTS + part];
-    uint8_t *arena = P.arena + (uint64_t)slot * P.arena_cap;
+    const uint32_t tab = PV_TSLOT(slot, metric);
+    unsigned long long *top = (unsigned long long *)&P.arena_top[tab * PV_ARENA_PARTS + part];
+    uint8_t *arena = P.arena + (uint64_t)tab * P.arena_cap;
     if (metric == TM_IPV6) {
         uint64_t a = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
         uint64_t pos = atomicAdd(top, 18ull);
@@ -196,7 +197,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     if (metric == TM_QNAME2 || metric == TM_QNAME3) {
         int q2, q3; uint64_t h2, h3;
         const uint32_t sfx = (P.f_flags & PVDF_ONLY_QSUFFIX) ? P.sfx_of[rep] : 0u;
-        if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx); else { q2 = 0; q3 = -1; }
+        if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx); else { q2 = 0; q3 = -1; }
         start = metric == TM_QNAME2 ? q2 : q3;
         if (start < 0) start = (int)n;
     }
@@ -229,7 +230,7 @@ __device__ __forceinline__ TPos tpos(PV_CREF(PvParams) P, uint32_t slot, uint64_
     const uint64_t h = tkey_hash(key);
     TPos t;
     t.rmask = (1u << rsl) - 1;
-    t.rbase = ((uint64_t)slot << P.tcap_log2) + ((uint64_t)tregion(P, h) << rsl);
+    t.rbase = ((uint64_t)PV_TSLOT(slot, PV_KEY_METRIC(key)) << P.tcap_log2) + ((uint64_t)tregion(P, h) << rsl);
     t.pos = (uint32_t)h & t.rmask;
     return t;
 }
@@ -402,6 +403,14 @@ __device__ __forceinline__ uint32_t period_of(PV_CREF(PvParams) P, uint64_t i)
     while (p < P.n_shift && i >= P.pstart[p]) p++;
     return p;
 }
+// DNS period of a DNS event at second `sec` (the DNS manager's own shifts; timestamps of a
+// batch with DNS shifts are monotone, so the second decides)
+__device__ __forceinline__ uint32_t dperiod_of(PV_CREF(PvParams) P, int64_t sec)
+{
+    uint32_t p = 0;
+    while (p < P.n_dshift && sec >= P.dthresh[p]) p++;
+    return p;
+}
 __device__ __forceinline__ uint64_t uni64(uint64_t v)
 {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
@@ -455,8 +464,10 @@ __device__ __forceinline__ uint32_t dns_port(uint32_t pw)
 }
 template <class A>
 __device__ __forceinline__ DnsMsg dns_msg_of(PV_CREF(PvParams) P, const A &R, const Parsed &o, uint64_t i, uint32_t port,
-                                             uint32_t period, bool upd, bool with_key = true)
+                                             bool with_key = true)
 {
+    const uint32_t period = P.n_dshift ? dperiod_of(P, o.sec) : 0u;
+    const bool upd = period >= P.dskip_before;
     DnsMsg d;
     d.idx = (uint32_t)i;
     d.moff = (uint32_t)(o.l4off + 8);
@@ -473,9 +484,50 @@ __device__ __forceinline__ DnsMsg dns_msg_of(PV_CREF(PvParams) P, const A &R, co
     return d;
 }
 
+// The 12 header bytes of a DNS message as three little-endian words; bytes past the
+// capture read as 0 (the reference over-reads there)
+template <class A>
+__device__ __forceinline__ void dns_header(const A &R, uint64_t m, uint32_t mcap, uint32_t &w0, uint32_t &w1, uint32_t &w2)
+{
+    if (mcap >= 12) { w0 = R.u32(m); w1 = R.u32(m + 4); w2 = R.u32(m + 8); return; }
+    w0 = w1 = w2 = 0;
+    for (uint32_t b = 0; b < 12; b++) {
+        const uint32_t v = b < mcap ? R.u8(m + b) : 0;
+        if (b < 4) w0 |= v << (8 * b); else if (b < 8) w1 |= v << (8 * (b - 4)); else w2 |= v << (8 * (b - 8));
+    }
+}
+// The input proxy's UDP predicates (PcapInputEventProxy::process_udp_packet_cb,
+// src/inputs/pcap/PcapInputStream.h:213-252, installed by DnsStreamHandler's
+// _register_predicate_filter, dns/v1/DnsStreamHandler.cpp:485-537): only_rcode passes a
+// response whose rcode is listed; only_qname a message whose lower-case first-query name is
+// listed. A packet they reject never reaches the handler (no event, no window shift).
+template <class A>
+__device__ __forceinline__ bool dns_predicates(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen, uint32_t w0,
+                                               uint32_t w1, uint32_t w2)
+{
+    const uint32_t qr = (w0 >> 23) & 1, rcode = (w0 >> 24) & 15;
+    if ((P.f_flags & PVDF_ONLY_RCODE) && (!qr || !((P.f_rcode_mask >> rcode) & 1))) return false;
+    if (P.f_flags & PVDF_ONLY_QNAME) {
+        const uint32_t qd = ((w1 & 0xff) << 8) | ((w1 >> 8) & 0xff), an = ((w1 >> 8) & 0xff00) | (w1 >> 24);
+        const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff), ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+        DnsInfo qi;
+        dns_parse(R, m, dlen, qd, an, ns, ar, qi);
+        bool hit = false;
+        if (qi.ok && qi.has_query && qi.name_len_enc > 0) {
+            NameStats st;
+            st.init();
+            name_stats(R, m, dlen, 12, st);
+            const uint64_t fp = fp56(st.ph, st.n, 0);
+            for (uint32_t k = 0; k < P.f_nqn; k++) hit |= st.n > 0 && fp == P.f_qn[k];
+        }
+        if (!hit) return false;
+    }
+    return true;
+}
+
 // DnsMetricsBucket::process_dns_layer (:910-1049) + the transaction event of one DNS
-// message. `cache` null = boundary path (direct HBM updates); counters go to `c` when
-// `own` (this lane's slot is the wave's register slot), else straight to HBM.
+// message, in the bucket of its DNS period. Counters go to `c` when `own` (this lane's
+// DNS slot is the wave's register slot), else straight to HBM.
 template <class A, class Cache>
 __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, uint32_t *nev,
                                             uint32_t *nresp, uint64_t ebase, const A &R, const DnsMsg &dm, bool own,
@@ -483,20 +535,12 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
 {
     const bool upd = dm.flags & 8;
     const uint32_t period = dm.period;
-    const uint32_t slot = P.slot_of[period];
+    const uint32_t slot = P.dslot_of[period];
     const uint64_t m = dm.moff;
     const uint32_t dlen = dm.mlen;
     const uint32_t i = dm.idx;
-    // header words; bytes past the capture read as 0 (the reference over-reads there)
     uint32_t w0, w1, w2;
-    if (dm.mcap >= 12) { w0 = R.u32(m); w1 = R.u32(m + 4); w2 = R.u32(m + 8); }
-    else {
-        w0 = w1 = w2 = 0;
-        for (uint32_t b = 0; b < 12; b++) {
-            const uint32_t v = b < dm.mcap ? R.u8(m + b) : 0;
-            if (b < 4) w0 |= v << (8 * b); else if (b < 8) w1 |= v << (8 * (b - 4)); else w2 |= v << (8 * (b - 8));
-        }
-    }
+    dns_header(R, m, dm.mcap, w0, w1, w2);
     const uint32_t txid = ((w0 & 0xff) << 8) | ((w0 >> 8) & 0xff);
     const uint32_t qr = (w0 >> 23) & 1;
     const uint32_t rcode = (w0 >> 24) & 15;
@@ -506,23 +550,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
     uint32_t sfx = 0; // only_qname_suffix's suffix_size for aggregateDomain
     if (P.f_flags) {
-        // only_rcode is the input proxy's UDP predicate (dns/v1/DnsStreamHandler.cpp:485-508):
-        // a query, or a response with an unlisted rcode, never reaches the handler (no event)
-        if ((P.f_flags & PVDF_ONLY_RCODE) && (!qr || !((P.f_rcode_mask >> rcode) & 1))) return;
-        // only_qname's predicate (:509-524): the lower-case first-query name must be listed
-        if (P.f_flags & PVDF_ONLY_QNAME) {
-            DnsInfo qi;
-            dns_parse(R, m, dlen, qd, ancount, ns, ar, qi);
-            bool hit = false;
-            if (qi.ok && qi.has_query && qi.name_len_enc > 0) {
-                NameStats st;
-                st.init();
-                name_stats(R, m, dlen, 12, st);
-                const uint64_t fp = fp56(st.ph, st.n, 0);
-                for (uint32_t k = 0; k < P.f_nqn; k++) hit |= st.n > 0 && fp == P.f_qn[k];
-            }
-            if (!hit) return;
-        }
+        if ((P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
         // DnsStreamHandler::_filtering (:538-648), in its order
         bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
                     ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
@@ -536,14 +564,10 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             filt = !fd.ok || !fd.has_query || !hit;
         }
         if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) {
-            // matched by pv_dns_suffix before this pass (0xff: no listed suffix); the
-            // boundary path, whose records that kernel does not see, matches here
-            uint32_t r;
-            if constexpr (!std::is_same<Cache, KeyCache<2>>::value) r = P.sfx_of[i];
-            else r = dns_suffix_of(P, R, m, dlen, qd, ancount, ns, ar);
+            // matched by pv_dns_suffix before this pass (0xff: no listed suffix)
+            const uint32_t r = P.sfx_of[i];
             filt = r == 0xffu;
             sfx = filt ? 0u : r;
-            if constexpr (std::is_same<Cache, KeyCache<2>>::value) P.sfx_of[i] = (uint8_t)r;
         }
         if (filt) {
             // process_filtered (:1341-1347): an event (sampled at rate 100) and `filtered`
@@ -555,12 +579,9 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                     if (P.dns_groups & PV_DNS_COUNTERS_BIT) sum_add(P, slot, PV_OFF_DNS + DC_FILTERED, 1);
                 }
             }
-            P.dns_first[0] = 1; // a DNS event without a transaction record: the DNS window moves
-            if (period > 0 && (int64_t)dm.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
             return;
         }
     }
-    if (!P.want_events) P.dns_first[0] = 1;
     // top-N / dense update: cache, else log (hashed) or HBM atomic (dense); boundary: global table
     auto top = [&](uint32_t metric, uint64_t payload, uint32_t w) {
         const uint64_t key = PV_KEY(metric, payload);
@@ -664,53 +685,6 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         P.events[e] = ev;
         P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)(P.ekey_base + i);
     }
-    if (period > 0 && (int64_t)dm.sec == P.thresh[period - 1]) P.dns_at_thresh[period] = 1;
-}
-
-// cardinality + top IPs of one record (NetworkMetricsBucket::process_net_layer :745-763).
-// One cache entry per (direction, address) carries both the top-N count and the
-// smallest record index, which makes the CPC coupon update of a repeated address free.
-template <class A, class Cache>
-__device__ __forceinline__ void net_ips(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, const A &R, const Parsed &o,
-                                        uint64_t i, uint32_t slot)
-{
-    const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
-    if (o.dir == 2 || !(card || tops)) return;
-    uint64_t key, lpay;
-    uint32_t lm;
-    uint64_t h1, h2;
-    bool hashed = false;
-    if (o.has4) {
-        const uint32_t ip = R.u32(o.dir == 0 ? o.v4 + 12 : o.v4 + 16);
-        if (!ip) return;
-        key = PV_KEY(TM_IPV4, ip);
-        lm = TM_IPV4;
-        lpay = ((uint64_t)o.dir << 32) | ip;
-    } else if (o.has6) {
-        const uint64_t a = o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
-        const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
-        const uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
-        if (!(w0 | w1)) return;
-        murmur_16(w0, w1, h1, h2);
-        hashed = true;
-        const uint64_t hk = (h1 ^ (h2 << 1)) & ((1ull << 55) - 1);
-        key = PV_KEY(TM_IPV6, hk);
-        lm = TM_IPV6;
-        lpay = ((uint64_t)o.dir << 55) | hk;
-    } else {
-        return;
-    }
-    uint32_t first = 0xffffffffu;
-    bool in_cache = false;
-    if (cache) in_cache = cache->add(PV_LKEY(slot, lm, lpay), tops ? 1 : 0, (uint32_t)i, first);
-    if (card && !(in_cache && first < (uint32_t)i)) {
-        if (!hashed) murmur_8((uint64_t)(int64_t)(int32_t)(uint32_t)(key & 0xffffffffu), h1, h2);
-        cpc_min(P, slot, o.dir == 0 ? CPC_SRC : CPC_DST, cpc_coupon(h1, h2), (int64_t)(P.gbase + i));
-    }
-    if (tops && !in_cache) {
-        if (cache) log_put(P, mq_n, slot, key, 1, (uint32_t)i);
-        else global_add(P, slot, key, 1, (uint32_t)i);
-    }
 }
 
 // Flush a workgroup's key cache: hashed keys to the update log, dense keys to HBM.
@@ -779,6 +753,22 @@ struct NetK {
     PV_G uint32_t *flags;
     uint32_t n_shift, skip_before, slot0, net_groups, dbg;
 };
+// Net v1 counters of one record straight to HBM (a lane whose slot is not the wave's
+// register slot: records of a 64-record tile that holds a period shift)
+__device__ __noinline__ void knet_direct(PV_G uint64_t *sum, uint32_t net_groups, uint32_t s, uint32_t dir, uint32_t l3,
+                                         uint32_t l4, uint32_t syn)
+{
+    PV_G uint64_t *b = sum + (uint64_t)s * PV_SUM_WORDS + PV_OFF_NET;
+    auto add = [&](uint32_t w) { __hip_atomic_fetch_add(b + w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    add(NC_EVENTS);
+    add(NC_SAMPLES);
+    if (!(net_groups & PV_NET_COUNTERS_BIT)) return;
+    add(NC_TOTAL);
+    add(dir == 0 ? NC_IN : (dir == 1 ? NC_OUT : NC_UNK));
+    if (l3) add(l3 == 4 ? NC_V4 : NC_V6);
+    add(l4 == 17 ? NC_UDP : (l4 == 6 ? NC_TCP : NC_OTHER));
+    if (l4 == 6 && syn) add(NC_SYN);
+}
 __device__ __forceinline__ void ksum_add(const NetK &K, uint32_t slot, uint32_t word, uint64_t w)
 {
     __hip_atomic_fetch_add(K.sum + (uint64_t)slot * PV_SUM_WORDS + word, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1018,7 +1008,7 @@ struct SlowOut {
     uint8_t dir, l3, l4, syn;
 };
 __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF(PvParams) P, const NetK K, uint64_t off,
-                                         uint64_t i, uint32_t slot, uint32_t p_lo, bool upd)
+                                         uint64_t i, uint32_t slot, bool upd)
 {
     SlowOut so;
     so.ek = 0;
@@ -1032,7 +1022,7 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
     if (o.l4 == 17 && !(K.dbg & 4)) {
         const uint32_t port = dns_port(R.u32(o.l4off));
         if (port) {
-            so.dm = msg_words(dns_msg_of(P, R, o, i, port, p_lo, upd, true));
+            so.dm = msg_words(dns_msg_of(P, R, o, i, port, true));
             so.isdns = 1;
         }
     }
@@ -1129,15 +1119,20 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         const uint64_t r0 = t * PV_WT;
         const uint64_t r1 = min<uint64_t>(r0 + PV_WT, n) - 1;
         const uint32_t p_lo = __builtin_amdgcn_readfirstlane(period(r0)), p_hi = __builtin_amdgcn_readfirstlane(period(r1));
-        const bool straddle = p_lo != p_hi; // pv_boundary_kernel's tile
-        const bool upd = !straddle && p_lo >= K.skip_before;
-        const uint32_t slot = slot_of(p_lo);
-        if (upd && slot != wslot) {
+        // a tile that holds a period shift: each lane resolves its own period, and lanes
+        // outside the wave's register slot update HBM directly
+        const bool straddle = p_lo != p_hi;
+        const uint32_t tslot = slot_of(p_lo);
+        if (p_lo >= K.skip_before && tslot != wslot) {
             if (wslot != 0xffffffffu) knet_flush(K, wslot, c);
-            wslot = slot;
+            wslot = tslot;
         }
         const uint64_t i = r0 + lane;
-        const bool active = i <= r1 && !straddle;
+        const bool active = i <= r1;
+        const uint32_t lp = straddle ? period(min(i, r1)) : p_lo;
+        const bool upd = lp >= K.skip_before;
+        const uint32_t slot = straddle ? slot_of(lp) : tslot;
+        const bool own = slot == wslot;
         const uint64_t off = NW.lo[row][lane];
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
         const uint32_t b1 = r0 + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row][63]);
@@ -1162,7 +1157,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                 fast = fast_parse(rw, C, P, off, o);
             }
             if (!fast) {
-                const SlowOut so = net_slow(R, C, P, K, off, i, slot, p_lo, upd);
+                const SlowOut so = net_slow(R, C, P, K, off, i, slot, upd);
                 o.caplen = so.caplen; o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
                 ek = so.ek;
                 dm = so.dm;
@@ -1173,7 +1168,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                 c.add(o);
             } else {
                 if (upd) {
-                    c.add(o);
+                    if (own) c.add(o);
+                    else knet_direct(K.sum, K.net_groups, slot, o.dir, o.l3, o.l4, o.syn);
                     uint32_t cl = o.caplen;
                     if (cl > 65535) { atomicOr(K.flags, PVF_BIG_CAPLEN); cl = 65535; }
                     if (slot == hslot && cl < PV_HBINS) hv = cl;
@@ -1197,7 +1193,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                 if (fast && o.l4 == 17 && !(K.dbg & 4)) {
                     const uint32_t port = dns_port(rw.at(50));
                     if (port) {
-                        DnsMsg d = dns_msg_of(P, R, o, i, port, p_lo, upd, false);
+                        DnsMsg d = dns_msg_of(P, R, o, i, port, false);
                         d.fkey = fast_flowkey(rw);
                         dm = msg_words(d);
                         isdns = true;
@@ -1238,6 +1234,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
     if (threadIdx.x == 0) {
         P.mq_cnt[blockIdx.x] = 0;
         P.dq_cnt[blockIdx.x] = S.nd;
+        if (S.nd) atomicAdd(P.n_dns, S.nd);
     }
 }
 
@@ -1329,14 +1326,14 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *
             m_n = m_nn;
         }
         // the wave's register counters follow the slot of its first message
-        const uint32_t s0 = P.slot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
+        const uint32_t s0 = P.dslot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
         if (s0 != wslot) {
             if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
             wslot = s0;
         }
         if (active) {
             const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
-            const bool own = P.slot_of[dm.period] == wslot;
+            const bool own = P.dslot_of[dm.period] == wslot;
             dns_process(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
         }
     }
@@ -1540,8 +1537,13 @@ struct MergeState {
     uint32_t mn[2][PV_RS]; // smallest record index of an IPv4 key per direction (CPC)
     uint32_t nidx[PV_RS]; // entries created in this batch: region index, source record
     uint32_t nrep[PV_RS];
-    uint32_t nnew, slots, nbase;
+    uint32_t nnew, tabs, nbase;
 };
+// table of an update-log entry (slot in bits 60..63, the key's metric)
+__device__ __forceinline__ uint32_t entry_table(uint64_t e0)
+{
+    return PV_TSLOT((uint32_t)(e0 >> 60), PV_KEY_METRIC(e0 & ((1ull << 60) - 1)));
+}
 
 extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams *__restrict__ Pp)
 {
@@ -1569,15 +1571,17 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
     __shared__ MergeState S;
     const uint32_t rsl = P.tcap_log2 - P.reg_log2;
     const uint32_t rs = 1u << rsl;
-    if (threadIdx.x == 0) S.slots = 0;
+    if (threadIdx.x == 0) S.tabs = 0;
     __syncthreads();
-    batched<8>(n, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) { atomicOr(&S.slots, 1u << (uint32_t)(e0 >> 60)); });
+    batched<8>(n, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) { atomicOr(&S.tabs, 1u << entry_table(e0)); });
     __syncthreads();
-    uint32_t slots = S.slots;
-    while (slots) {
-        const uint32_t s = __builtin_ctz(slots);
-        slots &= slots - 1;
-        const uint64_t rbase = ((uint64_t)s << P.tcap_log2) + ((uint64_t)r << rsl);
+    static_assert(PV_TABLES <= 32, "table mask");
+    uint32_t tabs = S.tabs;
+    while (tabs) {
+        const uint32_t tb = __builtin_ctz(tabs);
+        const uint32_t s = tb % PV_SLOTS; // the handler slot (Net for tb < PV_SLOTS, else DNS)
+        tabs &= tabs - 1;
+        const uint64_t rbase = ((uint64_t)tb << P.tcap_log2) + ((uint64_t)r << rsl);
         batched<4>(rs, [&](uint64_t i) { return make_ulonglong2(P.tkeys[rbase + i], P.tcnt[rbase + i]); },
                    [&](uint64_t i, ulonglong2 kc) {
                        S.key[i] = kc.x;
@@ -1589,7 +1593,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         __syncthreads();
         batched<8>(n, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
             const uint64_t e0 = e.x;
-            if ((uint32_t)(e0 >> 60) != s) return;
+            if (entry_table(e0) != tb) return;
             const uint64_t e1 = e.y;
             const uint64_t key = e0 & ((1ull << 60) - 1);
             uint32_t pos = (uint32_t)tkey_hash(key) & (rs - 1);
@@ -1637,7 +1641,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         for (uint32_t k = threadIdx.x; k < nnew; k += blockDim.x) {
             const uint32_t g = S.nbase + k;
             const uint64_t pos = rbase + S.nidx[k];
-            if (g < P.nn_cap) P.nn[g] = PvNewName{s, S.nrep[k], pos};
+            if (g < P.nn_cap) P.nn[g] = PvNewName{tb, S.nrep[k], pos};
             else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k]);
         }
         __syncthreads();
@@ -1707,7 +1711,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                     int q2, q3;
                     uint64_t h2, h3;
                     const uint32_t sfx = (P.f_flags & PVDF_ONLY_QSUFFIX) ? P.sfx_of[e.rep] : 0u;
-                    if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx);
+                    if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx);
                     else { q2 = 0; q3 = -1; }
                     const int st0 = metric == TM_QNAME2 ? q2 : q3;
                     start = st0 < 0 ? nch : (uint32_t)st0;
@@ -1756,53 +1760,37 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
     }
 }
 
-// 64-record tiles that hold a period shift: one wave per tile, each lane resolves its
-// own period and updates HBM directly. Runs after the DNS pass on the same stream;
-// its DNS events go to regions after the DNS pass's.
-extern "C" __global__ void __launch_bounds__(64) pv_boundary_kernel(const PvParams *__restrict__ Pp)
+// DNS events of a batch for the DNS manager's own window (AbstractMetricsManager::new_event,
+// src/AbstractMetricsManager.h:318-333): bit i of dbits is set when record i reaches the DNS
+// handler as an event: a UDP datagram on a DNS port with a non-zero metric port
+// (DnsStreamHandler::process_udp_packet_cb, dns/v1/DnsStreamHandler.cpp:270-302) that the
+// input predicates pass (only_rcode / only_qname). The host walks the bits for the DNS
+// period shifts. One lane per record, one 64-bit store per 64-record tile.
+extern "C" __global__ void __launch_bounds__(256) pv_dns_prescan(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ uint32_t nev, nresp;
-    if (threadIdx.x == 0) { nev = 0; nresp = 0; }
-    __syncthreads();
-    const uint64_t ebase = ((uint64_t)P.grid_main * P.wt_per_block + blockIdx.x) * PV_WT;
-    const uint64_t i = (uint64_t)P.btile[blockIdx.x] * PV_WT + threadIdx.x;
-    if (i < P.n) {
-        const GAcc R{P.recs};
-        Parsed o;
-        parse_record(R, P, P.offs[i], o);
-        const uint32_t period = period_of(P, i);
-        const uint32_t slot = P.slot_of[period];
-        const bool upd = period >= P.skip_before;
-        if (upd) {
-            const bool nc = P.net_groups & PV_NET_COUNTERS_BIT;
-            sum_add(P, slot, PV_OFF_NET + NC_EVENTS, 1);
-            sum_add(P, slot, PV_OFF_NET + NC_SAMPLES, 1);
-            if (nc) {
-                sum_add(P, slot, PV_OFF_NET + NC_TOTAL, 1);
-                sum_add(P, slot, PV_OFF_NET + (o.dir == 0 ? NC_IN : (o.dir == 1 ? NC_OUT : NC_UNK)), 1);
-                if (o.l3) sum_add(P, slot, PV_OFF_NET + (o.l3 == 4 ? NC_V4 : NC_V6), 1);
-                sum_add(P, slot, PV_OFF_NET + (o.l4 == 17 ? NC_UDP : (o.l4 == 6 ? NC_TCP : NC_OTHER)), 1);
-                if (o.l4 == 6 && o.syn) sum_add(P, slot, PV_OFF_NET + NC_SYN, 1);
-            }
-            if (o.caplen > 65535) atomicOr(P.flags, PVF_BIG_CAPLEN);
-            sum_add(P, slot, PV_OFF_PAYLOAD + (o.caplen > 65535 ? 65535 : o.caplen), 1);
-            net_ips(P, (KeyCache<2> *)nullptr, nullptr, R, o, i, slot);
-        }
-        if (o.l4 == 17) {
-            const uint32_t port = dns_port(R.u32(o.l4off));
-            if (port) {
-                const DnsMsg dm = dns_msg_of(P, R, o, i, port, period, upd);
-                DnsCtr c;
-                c.zero();
-                dns_process(P, (KeyCache<2> *)nullptr, nullptr, &nev, &nresp, ebase, R, dm, false, c);
+    const GAcc R{P.recs};
+    const uint64_t ntiles = (P.n + 63) / 64;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntiles; t += (uint64_t)gridDim.x * 4) {
+        const uint64_t i = t * 64 + (threadIdx.x & 63);
+        bool ev = false;
+        if (i < P.n) {
+            Parsed o;
+            parse_record(R, P, P.offs[i], o);
+            if (o.l4 == 17 && dns_port(R.u32(o.l4off))) {
+                ev = true;
+                if (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) {
+                    const uint64_t m = o.l4off + 8;
+                    const uint64_t cap_end = o.frame + o.caplen;
+                    const uint32_t mcap = cap_end > m ? (uint32_t)min<uint64_t>(cap_end - m, 65535) : 0u;
+                    uint32_t w0, w1, w2;
+                    dns_header(R, m, mcap, w0, w1, w2);
+                    ev = dns_predicates(P, R, m, o.l4len - 8, w0, w1, w2);
+                }
             }
         }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        P.blk_events[P.grid_main + blockIdx.x] = nev;
-        if (nresp) atomicAdd(P.n_events + 1, nresp);
+        const uint64_t b = __ballot(ev);
+        if ((threadIdx.x & 63) == 0) P.dbits[t] = b;
     }
 }
 
@@ -1821,9 +1809,7 @@ extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint
     const uint32_t base = part[0] + part[1] + part[2] + part[3];
     const uint32_t cnt = P.blk_events[blockIdx.x];
     if (threadIdx.x == 0 && blockIdx.x == nblk - 1) P.n_events[0] = base + cnt;
-    const uint64_t region = (uint64_t)P.wt_per_block * PV_WT;
-    const uint64_t src = blockIdx.x < P.grid_main ? (uint64_t)blockIdx.x * region
-                                                  : (uint64_t)P.grid_main * region + (uint64_t)(blockIdx.x - P.grid_main) * PV_WT;
+    const uint64_t src = (uint64_t)blockIdx.x * P.wt_per_block * PV_WT;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         P.skeys[base + j] = P.ekeys[src + j];
         P.svals[base + j] = (uint32_t)(src + j);
@@ -1868,8 +1854,8 @@ namespace {
 // query started at `sec`; returns 0 if none inside this batch
 __device__ __forceinline__ uint32_t purge_period(PV_CREF(PvParams) P, uint32_t ttl_s, uint32_t a, int64_t sec)
 {
-    for (uint32_t k = a + 1; k <= P.n_shift; k++)
-        if (P.thresh[k - 1] >= (int64_t)ttl_s + sec) return k;
+    for (uint32_t k = a + 1; k <= P.n_dshift; k++)
+        if (P.dthresh[k - 1] >= (int64_t)ttl_s + sec) return k;
     return 0;
 }
 // Workgroup-local staging: transaction counters per period and the quantile / slow
@@ -1905,7 +1891,7 @@ __device__ void slow_check(PV_CREF(PvXactParams) X, uint32_t idx, uint32_t perio
     RawName rn{0, 0};
     if (d.name_len_enc > 0) name_emit(R, m, len, 12, rn);
     const uint32_t metric = dir == 0 ? TM_SLOW_OUT : TM_SLOW_IN;
-    global_add(P, P.slot_of[period], PV_KEY(metric, fp56(rn.ph, rn.n, 1)), 1, idx);
+    global_add(P, P.dslot_of[period], PV_KEY(metric, fp56(rn.ph, rn.n, 1)), 1, idx);
 }
 } // namespace
 
@@ -1931,7 +1917,7 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
             const uint32_t k = atomicAdd(X.n_orph, 1u);
             if (k < X.orph_cap) {
                 PvXEvent o = e;
-                o.pad = (uint8_t)(P.slot_of[e.period] | (e.period >= P.skip_before ? 0x80u : 0u));
+                o.pad = (uint8_t)(P.dslot_of[e.period] | (e.period >= P.dskip_before ? 0x80u : 0u));
                 X.orph[k] = o;
             }
             return;
@@ -1940,7 +1926,7 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         if (qe.qr) return; // previous event was a response: erased => NotExist
         uint32_t kp = purge_period(P, X.ttl_s, qe.period, qe.sec);
         if (kp && kp <= e.period) return; // purged at a period shift before this response
-        const bool kept = e.period >= P.skip_before;
+        const bool kept = e.period >= P.dskip_before;
         // timespec_diff(endTS, startTS) (TransactionManager.h:24-37)
         int64_t dsec = e.sec > qe.sec ? e.sec - qe.sec : qe.sec - e.sec;
         int64_t dnsec = (int64_t)e.nsec - (int64_t)qe.nsec;
@@ -1974,7 +1960,7 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         for (; q < X.n && (uint32_t)(X.skeys[q] >> 32) == h; q++)
             if (xev(X, q).key == e.key) break;
         if (q < X.n && (uint32_t)(X.skeys[q] >> 32) == h && xev(X, q).period < kp) return;
-        if (kp < P.skip_before) return;
+        if (kp < P.dskip_before) return;
         xctr(T, kp, XC_TIMEOUT);
     }
 }
@@ -1994,8 +1980,8 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvX
     if (threadIdx.x < (PV_MAX_SHIFTS + 1) * XC_N) {
         const uint32_t per = threadIdx.x / XC_N, c = threadIdx.x % XC_N;
         const uint32_t v = T.ctr[per][c];
-        if (v && per <= P.n_shift)
-            atomicAdd((unsigned long long *)&P.sum[(uint64_t)P.slot_of[per] * PV_SUM_WORDS + PV_OFF_DNS + dc[c]],
+        if (v && per <= P.n_dshift)
+            atomicAdd((unsigned long long *)&P.sum[(uint64_t)P.dslot_of[per] * PV_SUM_WORDS + PV_OFF_DNS + dc[c]],
                       (unsigned long long)v);
     }
     if (threadIdx.x == 0) {

@@ -1,19 +1,25 @@
 // SPDX-License-Identifier: MPL-2.0
 // pv_layout.h — device-state layout shared by the HIP kernels and the host runtime.
 //
-// One "slot" holds one metrics bucket (a 60 s period, AbstractMetricsManager.h:276-308)
-// of both handlers. Slots form a ring of PV_SLOTS; the live window is the last
-// num_periods slots. Per slot, in HBM:
-//   SUM region   uint64  net counters | dns counters | payload-size histogram |
-//                        udp-port / qtype / rcode tables     (all-reduce SUM)
-//   MIN region   int64   CPC first-occurrence global record index per coupon, 3 x 2^17
-//                                                           (all-reduce MIN)
-//   top-N table  open addressing (key u64, count u64, aux u32) + name arena
+// A bucket (a 60 s period, AbstractMetricsManager.h:276-308) belongs to one handler. The
+// Net and DNS managers shift independently (each on the first of *its own* events at or
+// after its next_shift, :318-333), so each handler has its own window of bucket slots.
+// Slot ids are the handler's period ordinal mod PV_SLOTS (deterministic, so every rank of a
+// sharded run holds a period in the same slot). Physical slot s stores the Net bucket of
+// Net slot s and the DNS bucket of DNS slot s side by side, in disjoint parts:
+//   SUM region   uint64  [net part: net counters | payload-size histogram]
+//                        [dns part: dns counters | udp-port / qtype / rcode tables]  (all-reduce SUM)
+//   MIN region   int64   CPC first-occurrence global record index per coupon
+//                        [net part: src, dst][dns part: qname]                      (all-reduce MIN)
+//   top-N tables open addressing (key u64, count u64, aux u32) + name arena: table s
+//                holds the Net metrics of Net slot s, table PV_SLOTS + s the DNS metrics
+//                of DNS slot s (pv_tslot)
 #pragma once
 #include <stdint.h>
 
-#define PV_SLOTS 16
-#define PV_MAX_SHIFTS 6 // period shifts handled inside one device batch
+#define PV_SLOTS 16  // per handler: num_periods (<= 10) live + PV_MAX_SHIFTS new in one batch
+#define PV_TABLES (2 * PV_SLOTS)
+#define PV_MAX_SHIFTS 6 // period shifts per handler inside one device batch (the host splits longer batches)
 #define PV_MAX_SUBNETS 16
 // name arena partitions per slot: workgroup b allocates from partition b % PV_ARENA_PARTS,
 // so no bump pointer is shared by more than a few workgroups
@@ -44,12 +50,13 @@
 #define PV_QTYPE_BINS 65536
 #define PV_RCODE_BINS 16
 #define PV_OFF_NET 0
-#define PV_OFF_DNS (PV_OFF_NET + PV_NET_CTRS)
-#define PV_OFF_PAYLOAD (PV_OFF_DNS + PV_DNS_CTRS)
-#define PV_OFF_PORT (PV_OFF_PAYLOAD + PV_PAYLOAD_BINS)
+#define PV_OFF_PAYLOAD (PV_OFF_NET + PV_NET_CTRS)
+#define PV_SUM_NET_WORDS (PV_OFF_PAYLOAD + PV_PAYLOAD_BINS) // net part [0, PV_SUM_NET_WORDS)
+#define PV_OFF_DNS PV_SUM_NET_WORDS
+#define PV_OFF_PORT (PV_OFF_DNS + PV_DNS_CTRS)
 #define PV_OFF_QTYPE (PV_OFF_PORT + PV_PORT_BINS)
 #define PV_OFF_RCODE (PV_OFF_QTYPE + PV_QTYPE_BINS)
-#define PV_SUM_WORDS (PV_OFF_RCODE + PV_RCODE_BINS)
+#define PV_SUM_WORDS (PV_OFF_RCODE + PV_RCODE_BINS)      // dns part [PV_OFF_DNS, PV_SUM_WORDS)
 
 // net counters (src/handlers/net/v1/NetStreamHandler.h:69-96 + base event counters)
 enum {
@@ -66,6 +73,7 @@ enum {
 #define PV_CPC_COUPONS (2048 * 64)
 enum { CPC_SRC = 0, CPC_DST = 1, CPC_QNAME = 2, CPC_SKETCHES = 3 };
 #define PV_MIN_WORDS (CPC_SKETCHES * PV_CPC_COUPONS)
+#define PV_MIN_NET_WORDS (2 * PV_CPC_COUPONS) // net part [0, 2 * coupons), dns part after
 #define PV_CPC_EMPTY 0x7fffffffffffffffLL
 
 // ---- top-N metrics: key = metric << 56 | payload (56 bits)
@@ -77,6 +85,9 @@ enum {
 };
 #define PV_KEY(metric, payload) (((uint64_t)(metric) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
 #define PV_KEY_METRIC(k) ((uint32_t)((k) >> 56))
+// table of a (handler slot, metric): Net metrics (IPv4 / IPv6) in table slot, the DNS
+// metrics in table PV_SLOTS + slot
+#define PV_TSLOT(slot, metric) ((uint32_t)(slot) + (((metric) == TM_IPV4 || (metric) == TM_IPV6) ? 0u : (uint32_t)PV_SLOTS))
 
 // Each slot's table is cut into regions of 2^PV_REGION_LOG2 entries (fewer when the table
 // is smaller). A key lives in region (hash >> 40) & (regions - 1), at hash & (region - 1)
@@ -88,7 +99,7 @@ enum {
 #define PV_PROBES 256
 // entry of the new-name list (pv_topn_merge -> pv_topn_names)
 struct PvNewName {
-    uint32_t slot;
+    uint32_t slot; // table (PV_TSLOT)
     uint32_t rep;  // record index in the batch the name is decoded from
     uint64_t pos;  // table index (slot-relative offset included)
 };
@@ -114,7 +125,7 @@ struct PvXEvent {
     int32_t nsec;
     uint8_t qr;     // 1 = response
     uint8_t dir;    // PacketDirection: 0 toHost, 1 fromHost, 2 unknown
-    uint8_t period; // period index within the batch
+    uint8_t period; // DNS period index within the batch
     uint8_t pad;
 };
 
@@ -166,24 +177,32 @@ struct PvParams {
     uint32_t linktype;
     uint32_t ts_nano;
     uint32_t net_groups, dns_groups;
-    // periods inside this batch: period p (0..n_shift) covers ts_sec in [thresh[p-1], thresh[p])
+    // Net periods inside this batch: period p (0..n_shift) covers records [pstart[p-1], pstart[p])
+    // (ts_sec in [thresh[p-1], thresh[p])); Net slot of each
     uint32_t n_shift;
     int64_t thresh[PV_MAX_SHIFTS];
     uint32_t slot_of[PV_MAX_SHIFTS + 1];
     uint32_t skip_before; // periods < skip_before are outside the kept window (no bucket updates)
     uint64_t pstart[PV_MAX_SHIFTS]; // first record index (in this batch) of period p+1
+    // DNS periods (the DNS manager's own shifts): a DNS event with ts_sec in
+    // [dthresh[p-1], dthresh[p]) is in DNS period p, kept iff p >= dskip_before
+    uint32_t n_dshift;
+    int64_t dthresh[PV_MAX_SHIFTS];
+    uint32_t dslot_of[PV_MAX_SHIFTS + 1];
+    uint32_t dskip_before;
     uint64_t gbase;
     PvSubnets nets;
     // device state
     PV_G uint64_t *sum;    // PV_SLOTS x PV_SUM_WORDS
     PV_G int64_t *cpc;     // PV_SLOTS x PV_MIN_WORDS
-    PV_G uint64_t *tkeys;  // PV_SLOTS x tcap
+    PV_G uint64_t *tkeys;  // PV_TABLES x tcap
     PV_G uint64_t *tcnt;
     PV_G uint32_t *taux;
     uint32_t tcap_log2;
-    PV_G uint8_t *arena;      // PV_SLOTS x arena_cap, each slot split in PV_ARENA_PARTS partitions
-    PV_G uint64_t *arena_top; // PV_SLOTS x PV_ARENA_PARTS bump pointers (bytes used in the partition)
-    uint64_t arena_cap;  // bytes per slot
+    PV_G uint8_t *arena;      // PV_TABLES x arena_cap, each table's split in PV_ARENA_PARTS partitions
+    PV_G uint64_t *arena_top; // PV_TABLES x PV_ARENA_PARTS bump pointers (bytes used in the partition)
+    uint64_t arena_cap;  // bytes per table
+    PV_G uint64_t *dbits;      // pv_dns_prescan: one bit per record, set for a DNS event (after predicates)
     PV_G PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
     PV_G uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
     PV_G uint32_t *blk_events; // events appended by each workgroup
@@ -199,10 +218,9 @@ struct PvParams {
     PV_G uint64_t *stamps; // diagnostic builds (-DPV_STAMPS): 8 phase cycle sums per wave
     uint32_t mq_cap;
     uint32_t grid_main;   // workgroups of pv_net_kernel / pv_dns_kernel
-    uint32_t n_btiles;    // 64-record tiles holding a period shift (pv_boundary_kernel)
     PV_G uint64_t *dq;    // per-workgroup DNS work lists (32-B DnsMsg), region = wt_per_block * 64
     PV_G uint32_t *dq_cnt;
-    uint32_t btile[PV_MAX_SHIFTS];
+    PV_G uint32_t *n_dns; // DNS messages found by the Net pass (status word)
     // top-N merge: regions per slot table (log2), per-region update counts / offsets /
     // fill pointers into the region-sorted update buffer, and the new-name list
     uint32_t reg_log2;
@@ -220,8 +238,6 @@ struct PvParams {
     uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane,
                   // 16 no DNS name decode, 32 no DNS table updates
     PV_G uint32_t *flags;
-    PV_G uint32_t *dns_first; // per period: min record index of a DNS event in that period
-    PV_G uint32_t *dns_at_thresh; // per period: 1 if a DNS event had ts_sec == thresh[p-1]
     // DNS v1 filters (DnsStreamHandler::_filtering, dns/v1/DnsStreamHandler.cpp:538-648)
     uint32_t f_flags, f_rcode_mask, f_ancount, f_nq;
     uint16_t f_qt[PV_MAX_QTYPES];
@@ -255,7 +271,7 @@ struct PvXactParams {
     uint32_t n;
     uint32_t ttl_s, ttl_ms;
     uint32_t quantiles;
-    uint32_t slot_gen[PV_MAX_SHIFTS + 1]; // slot | generation << 8 per period
+    uint32_t slot_gen[PV_MAX_SHIFTS + 1]; // DNS slot | generation << 8 per DNS period
     float thr_from[PV_MAX_SHIFTS + 1];    // p90 slow thresholds per period, < 0 = not known yet
     float thr_to[PV_MAX_SHIFTS + 1];
     PV_G PvXValue *vals;

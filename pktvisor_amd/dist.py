@@ -1,5 +1,10 @@
 """Multi-GPU reduce of per-shard metric buckets (one process per GPU).
 
+Period boundaries are global: the ranks exchange each shard's record seconds and DNS-event
+seconds, compute both managers' shifts once (plan_windows), and each rank applies the
+shifts owned by other shards as window operations, so every rank's windows hold the same
+periods in the same slots (a contiguous split of a capture that crosses 60 s marks merges).
+
 Packets shard trivially: each rank processes a contiguous record range and its
 own buckets; one collective round then merges them, the analog of
 AbstractMetricsBucket::merge (src/AbstractMetricsManager.h:177-195) and
@@ -67,11 +72,12 @@ def reduce_regions(sum_parts, min_parts, group=None):
 
 
 def bucket_views(handlers, device):
-    """Tensors over the live-window slots of a PvHandlers' SUM and MIN regions."""
-    sum_ptr, _, min_ptr, _ = handlers.state_regions()
-    slots, sw, mw = handlers.window_slots()
-    sums = [device_view(sum_ptr + s * sw * 8, sw, torch.int64, device) for s in slots]
-    mins = [device_view(min_ptr + s * mw * 8, mw, torch.int64, device) for s in slots]
+    """Tensors over the live windows' device regions (pv_window_regions): the Net slots' net
+    parts and the DNS slots' dns parts, split by reduce op."""
+    from pktvisor_amd import PV_REDUCE_SUM
+    sums, mins = [], []
+    for ptr, words, op in handlers.window_regions():
+        (sums if op == PV_REDUCE_SUM else mins).append(device_view(ptr, words, torch.int64, device))
     return sums, mins
 
 
@@ -83,16 +89,72 @@ def reduce_handlers(handlers, device, group=None):
     torch.cuda.synchronize(device)
 
 
+# ---- the global period table: every rank's windows must hold the same periods
+def shifts_of(start_sec: int, per_rank_secs):
+    """One manager's shifts over a stream cut into contiguous shards: per_rank_secs[r] lists,
+    in stream order, the seconds in which shard r holds an event of that manager. The manager
+    shifts on the first event with ts_sec >= next_shift, then next_shift = that second + 60
+    (AbstractMetricsManager::new_event / _period_shift, src/AbstractMetricsManager.h:276-333).
+    Returns [(threshold second, owner rank)], the owner being the shard holding that event."""
+    out, nxt = [], start_sec + 60
+    for r, secs in enumerate(per_rank_secs):
+        for s in secs:
+            if s >= nxt:
+                out.append((int(s), r))
+                nxt = int(s) + 60
+    return out
+
+
+def plan_windows(handlers, start_sec: int, rec_secs, dns_secs, group=None):
+    """All-gather each rank's record seconds (Net events) and DNS-event seconds, compute both
+    managers' global shifts, and return this rank's part of the plan:
+    {"net": (leading, trailing), "dns": (leading, trailing)} — the shifts owned by earlier and
+    by later ranks, which this rank applies as window operations (pv_advance_windows)."""
+    world, me = dist.get_world_size(group), dist.get_rank(group)
+    allv = [None] * world
+    dist.all_gather_object(allv, ([int(x) for x in rec_secs], [int(x) for x in dns_secs]), group=group)
+    plan = {}
+    for key, k in (("net", 0), ("dns", 1)):
+        sh = shifts_of(start_sec, [v[k] for v in allv])
+        plan[key] = ([t for t, r in sh if r < me], [t for t, r in sh if r > me])
+    return plan
+
+
+def apply_plan(handlers, plan, which: int):
+    """which = 0: the leading shifts (before the shard's first batch), 1: the trailing ones"""
+    from pktvisor_amd import PART_DNS, PART_NET
+    handlers.advance_windows(PART_NET, plan["net"][which])
+    handlers.advance_windows(PART_DNS, plan["dns"][which])
+
+
+def record_seconds(index):
+    """distinct record seconds of a RecordIndex, in stream order"""
+    return [int(x) for x in index.sc_sec[: index.info.n_sec_changes]]
+
+
+def process_shard(handlers, recs, index, start_sec: int, start_nsec: int = 0, group=None):
+    """A rank's whole shard of a capture held in host memory: the capture's start_tstamp,
+    the global period plan, the shard's batches, the later ranks' shifts. Afterwards every
+    rank's windows hold the same periods in the same slots."""
+    handlers.set_start_tstamp(start_sec, start_nsec)
+    dns = handlers.dns_event_seconds_host(recs) if len(recs) else []
+    plan = plan_windows(handlers, start_sec, record_seconds(index) if index is not None and index.n else [], dns, group)
+    apply_plan(handlers, plan, 0)
+    if len(recs):
+        handlers.process_host(recs)
+    apply_plan(handlers, plan, 1)
+    return plan
+
+
 def check_aligned(handlers, group=None):
-    """The bucket merge pairs slots by id: every rank's live window must hold the same
-    periods (slot, start second). Ranks start their windows at the global first second
-    (pv_set_start_tstamp); a shard that ends in a different period is refused."""
-    mine = handlers.window_periods()
+    """The bucket merge pairs slots by id: every rank's windows must hold the same periods
+    (slot, start second) — what the global plan guarantees; checked before the merge."""
+    from pktvisor_amd import PART_DNS, PART_NET
+    mine = (handlers.window_periods(PART_NET), handlers.window_periods(PART_DNS))
     allv = [None] * dist.get_world_size(group)
     dist.all_gather_object(allv, mine, group=group)
     if any(v != allv[0] for v in allv):
         raise RuntimeError(f"shard windows differ across ranks: {allv}")
-
 
 def merge_edges(handlers, group=None):
     exports = [None] * dist.get_world_size(group)

@@ -52,3 +52,33 @@ def pcap_bytes(cfg: int, n: int, seed: int | None = None, ts_step_us: int = 1) -
     from pktvisor_amd import pcap_file_bytes
     buf, _, used = records(cfg, n, seed, ts_step_us)
     return pcap_file_bytes(buf[:used].tobytes())
+
+
+def records_of(pcap: bytes):
+    """[(ts_sec, ts_usec, record bytes)] of a classic little-endian pcap image"""
+    import struct
+    out, pos = [], 24
+    while pos + 16 <= len(pcap):
+        sec, usec, incl, _ = struct.unpack_from("<IIII", pcap, pos)
+        out.append((sec, usec, pcap[pos:pos + 16 + incl]))
+        pos += 16 + incl
+    return out
+
+
+def is_udp_dns(rec: bytes) -> bool:
+    """Ethernet + IPv4 (no options) UDP datagram on port 53 (the generator's DNS frames)"""
+    f = rec[16:]
+    return (len(f) >= 38 and f[12:14] == b"\x08\x00" and f[14] == 0x45 and f[23] == 17
+            and (f[34:36] == b"\x00\x35" or f[36:38] == b"\x00\x35"))
+
+
+def sparse_dns_pcap(n: int = 120000, ts_step_us: int = 2500, quiet=(52, 9), seed: int | None = None) -> bytes:
+    """C4 traffic spanning several minutes with no DNS packet in the seconds around every 60 s
+    mark after the capture's start (second offsets whose remainder mod 60 is >= quiet[0] or
+    < quiet[1]): the DNS manager then shifts seconds after the Net manager, and the gap between
+    the two boundaries drifts from one period to the next."""
+    from pktvisor_amd import pcap_file_bytes
+    recs = records_of(pcap_bytes(4, n, seed=seed, ts_step_us=ts_step_us))
+    t0 = recs[0][0]
+    keep = [r for s, _, r in recs if not (is_udp_dns(r) and ((s - t0) % 60 >= quiet[0] or (s - t0) % 60 < quiet[1]))]
+    return pcap_file_bytes(b"".join(keep))

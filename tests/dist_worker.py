@@ -52,9 +52,10 @@ def gpu_main(pcap_path, out, host, periods):
     try:
         h.set_global_base(lo)
         sec, frac = struct.unpack_from("<II", recs, offs[0])
-        h.set_start_tstamp(sec, frac if ts_nano else frac * 1000)  # the capture's start_tstamp on every rank
-        if hi > lo:
-            h.process_host(recs[offs[lo]:offs[hi]])
+        shard = recs[offs[lo]:offs[hi]]
+        sidx = pa.RecordIndex(shard, ts_nano) if hi > lo else None
+        # the capture's start_tstamp on every rank, the global period plan, the shard
+        pvdist.process_shard(h, shard, sidx, sec, frac if ts_nano else frac * 1000)
         h.set_end_tstamp(*pa.last_record_ts(recs, idx, ts_nano))
         pvdist.merge_window(h, dev)
         if rank == 0:

@@ -15,3 +15,24 @@ def test_gloo_two_ranks(tmp_path):
     assert r0["min"] == r1["min"] == [100, 4, 3]
     assert r0["ranges"] == [[0, 5], [5, 10]]
     assert r0["gathered"] == r1["gathered"] == [[0, "00"], [1, "0101"]]
+
+
+def test_global_shift_plan():
+    """dist.shifts_of over contiguous shards equals one manager's shifts over the whole
+    stream, and names the shard holding each shifting event"""
+    from pktvisor_amd.dist import shifts_of
+    secs = [0, 1, 30, 59, 60, 61, 118, 121, 125, 180, 181, 250, 400, 460, 461]
+    want, nxt = [], 60
+    for s in secs:
+        if s >= nxt:
+            want.append(s)
+            nxt = s + 60
+    for cuts in ([5], [3, 9], [0, 7, 7, 15], [14]):
+        shards, a = [], 0
+        for c in cuts + [len(secs)]:
+            shards.append(secs[a:c])
+            a = c
+        got = shifts_of(0, shards)
+        assert [t for t, _ in got] == want
+        for t, r in got:
+            assert t in shards[r] and all(t not in shards[q] for q in range(r))
