@@ -59,6 +59,9 @@ enum pv_dns_group {
     PV_DNS_TRANSACTIONS = 1u << 4, PV_DNS_TOP_ECS = 1u << 5, PV_DNS_TOP_QNAMES = 1u << 6,
     PV_DNS_TOP_QNAMES_DETAILS = 1u << 7, PV_DNS_TOP_PORTS = 1u << 8
 };
+/* OR'ed into pv_config.net_groups / dns_groups: the bits are the enabled set even when it is
+ * empty ("disable: [all]"); without it 0 selects the handler's default groups */
+#define PV_GROUPS_SET 0x80000000u
 #define PV_NET_DEFAULT_GROUPS (PV_NET_COUNTERS | PV_NET_CARDINALITY | PV_NET_TOP_GEO | PV_NET_TOP_IPS)
 #define PV_DNS_DEFAULT_GROUPS (PV_DNS_CARDINALITY | PV_DNS_COUNTERS | PV_DNS_QUANTILES | PV_DNS_TRANSACTIONS | \
                                PV_DNS_TOP_QNAMES | PV_DNS_TOP_PORTS)
@@ -68,13 +71,16 @@ typedef struct pv_config {
     uint32_t num_periods;    /* window history 1..10 ("num_periods", default 5) */
     uint32_t topn_count;     /* "topn_count", default 10 */
     uint32_t xact_ttl_ms;    /* "xact_ttl_ms", default 5000 */
-    uint32_t net_groups;     /* pv_net_group bits; 0 => defaults */
-    uint32_t dns_groups;     /* pv_dns_group bits; 0 => defaults */
+    uint32_t net_groups;     /* pv_net_group bits (| PV_GROUPS_SET); 0 => defaults */
+    uint32_t dns_groups;     /* pv_dns_group bits (| PV_GROUPS_SET); 0 => defaults */
     uint32_t linktype;       /* pcap linktype of the records (1 = Ethernet) */
     uint32_t ts_nano;        /* 1 if record timestamps are ns (magic a1b23c4d) */
     int32_t device;          /* HIP device ordinal, -1 => current */
     uint32_t table_log2;     /* log2 slots of each per-period top-N table, 0 => 22 */
     uint64_t max_records;    /* largest batch that will be submitted (sizes scratch) */
+    uint32_t topn_percentile_threshold; /* "topn_percentile_threshold" 0..99 (TopN::to_json, src/Metrics.h:510-521,577-590) */
+    uint32_t net_filter_all; /* nonzero: every packet is a filtered Net event (geo / ASN filters without a geo
+                                database, NetStreamHandler::_filtering, net/v1/NetStreamHandler.cpp:223-283) */
 } pv_config;
 
 /* DNS v1 filters, the typed form of the "exclude_noerror", "only_rcode", "answer_count",
@@ -100,6 +106,8 @@ typedef struct pv_dns_filters {
     const char *const *qname_suffixes; /* lower-cased; the first one the name ends with sets the
                                           aggregateDomain suffix size (at most one dot after its first char) */
     uint32_t only_dnssec_response; /* nonzero: filter all but responses with an RRSIG answer */
+    uint32_t filter_all;        /* nonzero: filter every DNS event that passes the predicates (geoloc_notfound /
+                                   asn_notfound without a geo database, :619-642) */
 } pv_dns_filters;
 
 /* Replaces DnsStreamHandler::start's filter setup (dns/v1/DnsStreamHandler.cpp:60-150). Call

@@ -327,6 +327,9 @@ static const std::map<uint16_t, std::string> &rcode_names()
 }
 
 // ---------------------------------------------------------------- config
+enum { NG_COUNTERS = 1, NG_CARDINALITY = 2, NG_TOP_GEO = 4, NG_TOP_IPS = 8 };
+enum { DG_CARDINALITY = 1, DG_COUNTERS = 2, DG_QUANTILES = 4, DG_HISTOGRAMS = 8, DG_TRANSACTIONS = 16, DG_TOP_ECS = 32,
+       DG_TOP_QNAMES = 64, DG_TOP_QNAMES_DETAILS = 128, DG_TOP_PORTS = 256 };
 struct V4Net { uint32_t addr; uint8_t cidr; };  // addr: network-order bytes as LE u32 (in_addr.s_addr)
 struct V6Net { uint8_t addr[16]; uint8_t cidr; };
 
@@ -337,8 +340,15 @@ struct Config {
     unsigned window = 5; // output window: 1 => single bucket 0 ("1m"), N>=2 => merged N ("Nm")
     size_t topn_count = 10;
     uint32_t xact_ttl_ms = 5000;
-    bool dns_details = false; // enable top_qnames_details group
     bool recorded_stream = true;
+    // metric groups (StreamMetricsHandler::process_groups, src/StreamHandler.h:111-133), as the
+    // handler's _groups bits: net v1 defaults (NetStreamHandler.cpp:53-56), dns v1 defaults
+    // (DnsStreamHandler.cpp:52-57); "dns_details=1" adds top_qnames_details
+    uint32_t net_groups = NG_COUNTERS | NG_CARDINALITY | NG_TOP_GEO | NG_TOP_IPS;
+    uint32_t dns_groups = DG_CARDINALITY | DG_COUNTERS | DG_QUANTILES | DG_TRANSACTIONS | DG_TOP_QNAMES | DG_TOP_PORTS;
+    uint32_t topn_pct = 0;   // topn_percentile_threshold
+    bool net_filter_all = false; // net geo / ASN filters with no geo database: every packet filtered (:223-283)
+    bool filter_all = false; // geoloc_notfound / asn_notfound with no geo database: every packet filtered (:619-642)
     // DNS v1 filters (DnsStreamHandler::start, dns/v1/DnsStreamHandler.cpp:60-160)
     bool exclude_noerror = false;   // "exclude_noerror" (:61-63)
     uint32_t only_rcode_mask = 0;   // "only_rcode": bit r set = rcode r wanted (:64-113); predicate mode
@@ -716,6 +726,67 @@ static DnsParse parse_resources(const DnsMsg &m)
     return r;
 }
 
+// The first additional record, as DnsLayer::parseResources(false, true, true) finds it
+// (libs/visor_dns/DnsLayer.cpp:119-209): questions, answers, authorities, then the first
+// additional, each in bounds; its offset or -1.
+static long first_additional(const DnsMsg &m)
+{
+    uint16_t qd = rd16be(m.d + 4), an = rd16be(m.d + 6), ns = rd16be(m.d + 8), ar = rd16be(m.d + 10);
+    uint32_t total = (uint32_t)qd + an + ns + ar;
+    if (total > 100 || m.len < 12 || ar == 0) return -1;
+    size_t off = 12;
+    for (uint32_t i = 0; i < total; i++) {
+        const bool is_q = i < qd;
+        std::string nm;
+        size_t nl = decode_name(m, off, nm, 1);
+        size_t sz;
+        if (is_q) sz = nl + 4;
+        else {
+            size_t dl_off = off + nl + 8;
+            uint16_t dl = (dl_off + 2 <= m.len) ? rd16be(m.d + dl_off) : 0;
+            sz = nl + 10 + dl;
+        }
+        const size_t start = off;
+        off += sz;
+        if (off > m.len) return -1;
+        if (i == (uint32_t)qd + an + ns) return (long)start;
+    }
+    return -1;
+}
+
+// parse_additional_records_ecs (libs/visor_dns/DnsAdditionalRecord.h:49-101): an OPT record
+// whose data (at least 9 bytes) opens with option CSUBNET (8); family 1 takes the data bytes
+// from offset 8 as the IPv4 address (the reference copies them all into a 4-byte array: only
+// the first 4 are kept here), family 2 takes data bytes 8 .. min(len, 16) as the start of
+// the IPv6 address. inet_ntop text, empty for other families.
+static std::string ecs_subnet(const DnsMsg &m)
+{
+    const long a = first_additional(m);
+    if (a < 0) return "";
+    std::string nm;
+    const size_t nl = decode_name(m, (size_t)a, nm, 1);
+    const uint8_t *r = m.d + a + nl;
+    const uint16_t type = rd16be(r), dlen = rd16be(r + 8);
+    if (type != 41 || dlen < 9) return "";
+    const uint8_t *x = r + 10;
+    if (rd16be(x) != 8) return "";
+    const uint16_t family = rd16be(x + 4);
+    char buf[64];
+    if (family == 1) {
+        uint8_t v4[4] = {0, 0, 0, 0};
+        for (size_t i = 8; i < dlen && i < 12; i++) v4[i - 8] = x[i];
+        inet_ntop(AF_INET, v4, buf, sizeof buf);
+        return buf;
+    }
+    if (family == 2) {
+        uint8_t v6[16] = {0};
+        for (size_t i = 8; i < std::min<size_t>(dlen, 16); i++) v6[i - 8] = x[i];
+        inet_ntop(AF_INET6, v6, buf, sizeof buf);
+        return buf;
+    }
+    return "";
+}
+
 static std::string lower(const std::string &s)
 {
     std::string o = s;
@@ -784,11 +855,12 @@ struct NetBucket : BaseBucket {
 struct DnsBucket : BaseBucket {
     uint64_t xacts_total = 0, xacts_in = 0, xacts_out = 0, xacts_timed_out = 0, queries = 0, replies = 0, UDP = 0,
              TCP = 0, IPv4 = 0, IPv6 = 0, NX = 0, REFUSED = 0, SRVFAIL = 0, NOERROR = 0, NODATA = 0, total = 0,
-             filtered = 0;
+             filtered = 0, query_ecs = 0;
     ExactQuantile<uint64_t> xact_from, xact_to; // "out" / "in" quantiles_us
+    ExactQuantile<uint64_t> hist_from, hist_to; // "out" / "in" histogram_us (Histogram, src/Metrics.h:189-327)
     ExactQuantile<double> ratio;
     Cpc qname;
-    ExactTop<std::string> qname2, qname3, nx, refused, srvfail, nodata, noerror, sized_resp, slow_in, slow_out;
+    ExactTop<std::string> qname2, qname3, nx, refused, srvfail, nodata, noerror, sized_resp, slow_in, slow_out, ecs;
     ExactTop<uint16_t> udp_port, qtype, rcode;
 
     void merge(const DnsBucket &o)
@@ -796,8 +868,9 @@ struct DnsBucket : BaseBucket {
         xacts_total += o.xacts_total; xacts_in += o.xacts_in; xacts_out += o.xacts_out;
         xacts_timed_out += o.xacts_timed_out; queries += o.queries; replies += o.replies; UDP += o.UDP;
         TCP += o.TCP; IPv4 += o.IPv4; IPv6 += o.IPv6; NX += o.NX; REFUSED += o.REFUSED; SRVFAIL += o.SRVFAIL;
-        NOERROR += o.NOERROR; NODATA += o.NODATA; total += o.total; filtered += o.filtered;
+        NOERROR += o.NOERROR; NODATA += o.NODATA; total += o.total; filtered += o.filtered; query_ecs += o.query_ecs;
         xact_from.merge(o.xact_from); xact_to.merge(o.xact_to); ratio.merge(o.ratio);
+        hist_from.merge(o.hist_from); hist_to.merge(o.hist_to); ecs.merge(o.ecs);
         qname.merge(o.qname);
         qname2.merge(o.qname2); qname3.merge(o.qname3); nx.merge(o.nx); refused.merge(o.refused);
         srvfail.merge(o.srvfail); nodata.merge(o.nodata); noerror.merge(o.noerror); sized_resp.merge(o.sized_resp);
@@ -885,29 +958,36 @@ struct Engine {
         net.maybe_shift(p.ts);
         net.new_event(true);
         NetBucket &b = net.live();
-        b.total++;
-        if (p.dir == DIR_FROM_HOST) b.out++;
-        else if (p.dir == DIR_TO_HOST) b.in++;
-        else b.unk++;
-        if (p.l3 == L3_IPV6) b.IPv6++;
-        else if (p.l3 == L3_IPV4) b.IPv4++;
-        if (p.l4 == L4_UDP) b.UDP++;
-        else if (p.l4 == L4_TCP) { b.TCP++; if (p.syn) b.TCP_SYN++; }
-        else b.OtherL4++;
+        if (cfg.net_filter_all) { // process_filtered (net/v1/NetStreamHandler.cpp:507-514)
+            if (cfg.net_groups & NG_COUNTERS) b.filtered++;
+            return;
+        }
+        if (cfg.net_groups & NG_COUNTERS) {
+            b.total++;
+            if (p.dir == DIR_FROM_HOST) b.out++;
+            else if (p.dir == DIR_TO_HOST) b.in++;
+            else b.unk++;
+            if (p.l3 == L3_IPV6) b.IPv6++;
+            else if (p.l3 == L3_IPV4) b.IPv4++;
+            if (p.l4 == L4_UDP) b.UDP++;
+            else if (p.l4 == L4_TCP) { b.TCP++; if (p.syn) b.TCP_SYN++; }
+            else b.OtherL4++;
+        }
         b.payload.update(p.caplen);
+        const bool card = cfg.net_groups & NG_CARDINALITY, tops = cfg.net_groups & NG_TOP_IPS;
         if (p.has_v4) {
             uint32_t in = 0, out = 0;
             if (p.dir == DIR_TO_HOST) in = rd32le(p.v4hdr + 12);
             else if (p.dir == DIR_FROM_HOST) out = rd32le(p.v4hdr + 16);
-            if (p.l3 == L3_IPV4 && in) { b.src.update_u32(in); b.top4.update(in); }
-            if (p.l3 == L3_IPV4 && out) { b.dst.update_u32(out); b.top4.update(out); }
+            if (p.l3 == L3_IPV4 && in) { if (card) b.src.update_u32(in); if (tops) b.top4.update(in); }
+            if (p.l3 == L3_IPV4 && out) { if (card) b.dst.update_u32(out); if (tops) b.top4.update(out); }
         } else if (p.has_v6) {
             static const uint8_t zero[16] = {0};
             const uint8_t *in = nullptr, *out = nullptr;
             if (p.dir == DIR_TO_HOST) in = p.v6hdr + 8;
             else if (p.dir == DIR_FROM_HOST) out = p.v6hdr + 24;
-            if (p.l3 == L3_IPV6 && in && memcmp(in, zero, 16)) { b.src.update_bytes(in, 16); b.top6.update(ipv6_str(in)); }
-            if (p.l3 == L3_IPV6 && out && memcmp(out, zero, 16)) { b.dst.update_bytes(out, 16); b.top6.update(ipv6_str(out)); }
+            if (p.l3 == L3_IPV6 && in && memcmp(in, zero, 16)) { if (card) b.src.update_bytes(in, 16); if (tops) b.top6.update(ipv6_str(in)); }
+            if (p.l3 == L3_IPV6 && out && memcmp(out, zero, 16)) { if (card) b.dst.update_bytes(out, 16); if (tops) b.top6.update(ipv6_str(out)); }
         }
     }
 
@@ -976,10 +1056,11 @@ struct Engine {
             }
             filt = !hit;
         }
+        if (!filt && cfg.filter_all) filt = true;
         if (filt) {
             if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
             dns.new_event(true);
-            dns.live().filtered++;
+            if (cfg.dns_groups & DG_COUNTERS) dns.live().filtered++;
             return;
         }
 
@@ -987,18 +1068,21 @@ struct Engine {
         if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
         dns.new_event(true);
         DnsBucket &b = dns.live();
-        b.total++;
-        if (p.l3 == L3_IPV6) b.IPv6++;
-        else if (p.l3 == L3_IPV4) b.IPv4++;
-        b.UDP++;
-        if (qr) {
-            b.replies++;
-            if (rcode == 0) { b.NOERROR++; if (!ancount) b.NODATA++; }
-            else if (rcode == 2) b.SRVFAIL++;
-            else if (rcode == 3) b.NX++;
-            else if (rcode == 5) b.REFUSED++;
-        } else b.queries++;
-        b.udp_port.update(metric_port);
+        const uint32_t g = cfg.dns_groups;
+        if (g & DG_COUNTERS) {
+            b.total++;
+            if (p.l3 == L3_IPV6) b.IPv6++;
+            else if (p.l3 == L3_IPV4) b.IPv4++;
+            b.UDP++;
+            if (qr) {
+                b.replies++;
+                if (rcode == 0) { b.NOERROR++; if (!ancount) b.NODATA++; }
+                else if (rcode == 2) b.SRVFAIL++;
+                else if (rcode == 3) b.NX++;
+                else if (rcode == 5) b.REFUSED++;
+            } else b.queries++;
+        }
+        if (g & DG_TOP_PORTS) b.udp_port.update(metric_port);
         DnsParse r;
         if (m.len >= 12) r = parse_resources(m);
         else {
@@ -1010,24 +1094,36 @@ struct Engine {
             if (qr) b.rcode.update(rcode);
             if (r.has_query) {
                 name_lower = lower(r.name);
-                b.qname.update_str(name_lower);
+                if (g & DG_CARDINALITY) b.qname.update_str(name_lower);
                 b.qtype.update(r.qtype);
-                if (qr) {
-                    if (rcode == 2) b.srvfail.update(name_lower);
-                    else if (rcode == 3) b.nx.update(name_lower);
-                    else if (rcode == 5) b.refused.update(name_lower);
-                    else if (rcode == 0) {
-                        if (cfg.dns_details) b.noerror.update(name_lower);
-                        if (!ancount) b.nodata.update(name_lower);
+                if (g & DG_TOP_QNAMES) {
+                    const bool det = g & DG_TOP_QNAMES_DETAILS;
+                    if (qr) {
+                        if (rcode == 2) b.srvfail.update(name_lower);
+                        else if (rcode == 3) b.nx.update(name_lower);
+                        else if (rcode == 5) b.refused.update(name_lower);
+                        else if (rcode == 0) {
+                            if (det) b.noerror.update(name_lower);
+                            if (!ancount) b.nodata.update(name_lower);
+                        }
+                        if (det) b.sized_resp.update(name_lower, m.len);
                     }
-                    if (cfg.dns_details) b.sized_resp.update(name_lower, m.len);
+                    std::string q2, q3;
+                    aggregate_domain(name_lower, suffix_size, q2, q3);
+                    b.qname2.update(q2);
+                    if (!q3.empty()) b.qname3.update(q3);
                 }
-                std::string q2, q3;
-                aggregate_domain(name_lower, suffix_size, q2, q3);
-                b.qname2.update(q2);
-                if (!q3.empty()) b.qname3.update(q3);
+            }
+            // top_ecs (:1026-1048): a query's first additional record, its EDNS Client Subnet
+            if ((g & DG_TOP_ECS) && !qr && rd16be(hm.d + 10) > 0) {
+                std::string subnet = ecs_subnet(m);
+                if (!subnet.empty()) {
+                    if (g & DG_COUNTERS) b.query_ecs++;
+                    b.ecs.update(subnet);
+                }
             }
         }
+        if (!(g & DG_TRANSACTIONS)) return;
         // transactions
         XactKey k{flowkey, txid};
         if (qr) {
@@ -1066,9 +1162,10 @@ struct Engine {
     void new_xact(DnsBucket &b, const Pkt &p, TS d, const Xact &x, const DnsParse &r)
     {
         uint64_t us = (uint64_t)((d.sec * 1000000000LL) + d.nsec) / 1000;
+        const bool q = cfg.dns_groups & DG_QUANTILES, h = cfg.dns_groups & DG_HISTOGRAMS;
         b.xacts_total++;
-        if (p.dir == DIR_TO_HOST) { b.xacts_out++; b.xact_from.update(us); }
-        else if (p.dir == DIR_FROM_HOST) { b.xacts_in++; b.xact_to.update(us); }
+        if (p.dir == DIR_TO_HOST) { b.xacts_out++; if (q) b.xact_from.update(us); if (h) b.hist_from.update(us); }
+        else if (p.dir == DIR_FROM_HOST) { b.xacts_in++; if (q) b.xact_to.update(us); if (h) b.hist_to.update(us); }
         size_t resp_len = p.l4len - 8;
         if (x.query_size) b.ratio.update((double)resp_len / (double)x.query_size);
         if (r.ok && r.has_query) {
@@ -1102,6 +1199,10 @@ struct Engine {
 };
 
 // ---------------------------------------------------------------- JSON rendering
+static thread_local uint32_t topn_pct = 0; // topn_percentile_threshold of the current run
+
+// TopN::to_json (src/Metrics.h:510-521,577-590): the first n by estimate, cut at the first one
+// below the topn_percentile_threshold quantile (KLL inclusive rule) of those n estimates
 template <typename K, typename F>
 static void top_json(J &j, const std::string &key, const ExactTop<K> &t, size_t n, F fmt)
 {
@@ -1111,9 +1212,13 @@ static void top_json(J &j, const std::string &key, const ExactTop<K> &t, size_t 
         if (a.second != b.second) return a.second > b.second;
         return a.first < b.first;
     });
+    const size_t k = std::min(n, v.size());
+    ExactQuantile<uint64_t> est;
+    for (size_t i = 0; i < k; i++) est.update(v[i].second);
+    const uint64_t thr = k ? est.p((double)topn_pct / 100.0) : 0;
     j.key(key);
     j.arr();
-    for (size_t i = 0; i < std::min(n, v.size()); i++) {
+    for (size_t i = 0; i < k && v[i].second >= thr; i++) {
         j.obj();
         j.key("name"); j.str(v[i].first);
         j.key("estimate"); j.u64(v[i].second);
@@ -1140,7 +1245,38 @@ static void quant_json(J &j, const std::string &key, const ExactQuantile<T> &q)
 
 static std::string id_str(const std::string &s) { return s; }
 
-static void net_json(J &j, const NetBucket &b, size_t topn)
+// Histogram::to_json (src/Metrics.h:243-262) on exact data: the split points are the distinct
+// uint64 values of 10^(b/18) * 10^e (e in [-9, 18), b in [0, 18)); a point is kept when the
+// inclusive PMF interval ending at it holds an item; each kept point's value is the inclusive
+// CDF times n (a double), then "+Inf" = n
+static void hist_json(J &j, const std::string &key, const ExactQuantile<uint64_t> &h)
+{
+    if (h.empty()) return;
+    std::vector<uint64_t> pts;
+    for (int e = -9; e < 18; e++)
+        for (int k = 0; k < 18; k++) {
+            const float f = static_cast<float>(k) / 18;
+            const uint64_t v = static_cast<uint64_t>(std::pow(10.0, f) * std::pow(10.0, e));
+            if (pts.empty() || pts.back() != v) pts.push_back(v);
+        }
+    std::vector<uint64_t> s = h.v;
+    std::sort(s.begin(), s.end());
+    const double n = (double)s.size();
+    auto le = [&](uint64_t x) { return (uint64_t)(std::upper_bound(s.begin(), s.end(), x) - s.begin()); };
+    j.key(key); j.obj();
+    j.key("buckets"); j.obj();
+    uint64_t prev = 0;
+    for (uint64_t x : pts) {
+        const uint64_t c = le(x);
+        if (c != prev) { j.key(std::to_string(x)); j.dbl(((double)c / n) * n); }
+        prev = c;
+    }
+    j.key("+Inf"); j.dbl(1.0 * n);
+    j.end_obj();
+    j.end_obj();
+}
+
+static void net_json(J &j, const NetBucket &b, size_t topn, uint32_t g)
 {
     j.key("period"); j.obj();
     j.key("start_ts"); j.i64(b.start.sec);
@@ -1148,29 +1284,37 @@ static void net_json(J &j, const NetBucket &b, size_t topn)
     j.end_obj();
     j.key("events"); j.u64(b.num_events);
     j.key("deep_samples"); j.u64(b.num_samples);
-    j.key("udp"); j.u64(b.UDP);
-    j.key("tcp"); j.u64(b.TCP);
-    j.key("protocol"); j.obj(); j.key("tcp"); j.obj(); j.key("syn"); j.u64(b.TCP_SYN); j.end_obj(); j.end_obj();
-    j.key("other_l4"); j.u64(b.OtherL4);
-    j.key("ipv4"); j.u64(b.IPv4);
-    j.key("ipv6"); j.u64(b.IPv6);
-    j.key("in"); j.u64(b.in);
-    j.key("out"); j.u64(b.out);
-    j.key("unknown_dir"); j.u64(b.unk);
-    j.key("total"); j.u64(b.total);
-    j.key("filtered"); j.u64(b.filtered);
-    j.key("cardinality"); j.obj();
-    j.key("src_ips_in"); j.i64(lround(b.src.estimate()));
-    j.key("dst_ips_out"); j.i64(lround(b.dst.estimate()));
-    j.end_obj();
-    top_json(j, "top_ipv4", b.top4, topn, ipv4_str);
-    top_json(j, "top_ipv6", b.top6, topn, id_str);
-    j.key("top_geoLoc"); j.arr(); j.end_arr();
-    j.key("top_ASN"); j.arr(); j.end_arr();
+    if (g & NG_COUNTERS) {
+        j.key("udp"); j.u64(b.UDP);
+        j.key("tcp"); j.u64(b.TCP);
+        j.key("protocol"); j.obj(); j.key("tcp"); j.obj(); j.key("syn"); j.u64(b.TCP_SYN); j.end_obj(); j.end_obj();
+        j.key("other_l4"); j.u64(b.OtherL4);
+        j.key("ipv4"); j.u64(b.IPv4);
+        j.key("ipv6"); j.u64(b.IPv6);
+        j.key("in"); j.u64(b.in);
+        j.key("out"); j.u64(b.out);
+        j.key("unknown_dir"); j.u64(b.unk);
+        j.key("total"); j.u64(b.total);
+        j.key("filtered"); j.u64(b.filtered);
+    }
+    if (g & NG_CARDINALITY) {
+        j.key("cardinality"); j.obj();
+        j.key("src_ips_in"); j.i64(lround(b.src.estimate()));
+        j.key("dst_ips_out"); j.i64(lround(b.dst.estimate()));
+        j.end_obj();
+    }
+    if (g & NG_TOP_IPS) {
+        top_json(j, "top_ipv4", b.top4, topn, ipv4_str);
+        top_json(j, "top_ipv6", b.top6, topn, id_str);
+    }
+    if (g & NG_TOP_GEO) {
+        j.key("top_geoLoc"); j.arr(); j.end_arr();
+        j.key("top_ASN"); j.arr(); j.end_arr();
+    }
     quant_json(j, "payload_size", b.payload);
 }
 
-static void dns_json(J &j, const DnsBucket &b, size_t topn, bool details)
+static void dns_json(J &j, const DnsBucket &b, size_t topn, uint32_t g)
 {
     auto u16s = [](const uint16_t &v) { return std::to_string(v); };
     auto rc = [](const uint16_t &v) { auto &m = rcode_names(); auto it = m.find(v); return it != m.end() ? it->second : std::to_string(v); };
@@ -1182,43 +1326,58 @@ static void dns_json(J &j, const DnsBucket &b, size_t topn, bool details)
     j.key("wire_packets"); j.obj();
     j.key("events"); j.u64(b.num_events);
     j.key("deep_samples"); j.u64(b.num_samples);
-    j.key("queries"); j.u64(b.queries);
-    j.key("replies"); j.u64(b.replies);
-    j.key("tcp"); j.u64(b.TCP);
-    j.key("udp"); j.u64(b.UDP);
-    j.key("ipv4"); j.u64(b.IPv4);
-    j.key("ipv6"); j.u64(b.IPv6);
-    j.key("nxdomain"); j.u64(b.NX);
-    j.key("refused"); j.u64(b.REFUSED);
-    j.key("srvfail"); j.u64(b.SRVFAIL);
-    j.key("noerror"); j.u64(b.NOERROR);
-    j.key("nodata"); j.u64(b.NODATA);
-    j.key("total"); j.u64(b.total);
-    j.key("filtered"); j.u64(b.filtered);
+    if (g & DG_COUNTERS) {
+        j.key("queries"); j.u64(b.queries);
+        j.key("replies"); j.u64(b.replies);
+        j.key("tcp"); j.u64(b.TCP);
+        j.key("udp"); j.u64(b.UDP);
+        j.key("ipv4"); j.u64(b.IPv4);
+        j.key("ipv6"); j.u64(b.IPv6);
+        j.key("nxdomain"); j.u64(b.NX);
+        j.key("refused"); j.u64(b.REFUSED);
+        j.key("srvfail"); j.u64(b.SRVFAIL);
+        j.key("noerror"); j.u64(b.NOERROR);
+        j.key("nodata"); j.u64(b.NODATA);
+        j.key("total"); j.u64(b.total);
+        j.key("filtered"); j.u64(b.filtered);
+        if (g & DG_TOP_ECS) { j.key("query_ecs"); j.u64(b.query_ecs); }
+    }
     j.end_obj();
-    j.key("cardinality"); j.obj(); j.key("qname"); j.i64(lround(b.qname.estimate())); j.end_obj();
-    j.key("xact"); j.obj();
-    j.key("counts"); j.obj(); j.key("total"); j.u64(b.xacts_total); j.key("timed_out"); j.u64(b.xacts_timed_out); j.end_obj();
-    j.key("in"); j.obj(); j.key("total"); j.u64(b.xacts_in);
-    top_json(j, "top_slow", b.slow_in, topn, id_str);
-    quant_json(j, "quantiles_us", b.xact_to);
-    j.end_obj();
-    j.key("out"); j.obj(); j.key("total"); j.u64(b.xacts_out);
-    top_json(j, "top_slow", b.slow_out, topn, id_str);
-    quant_json(j, "quantiles_us", b.xact_from);
-    j.end_obj();
-    if (!b.ratio.empty()) { j.key("ratio"); j.obj(); quant_json(j, "quantiles", b.ratio); j.end_obj(); }
-    j.end_obj();
-    top_json(j, "top_udp_ports", b.udp_port, topn, u16s);
-    top_json(j, "top_qname2", b.qname2, topn, id_str);
-    top_json(j, "top_qname3", b.qname3, topn, id_str);
-    top_json(j, "top_nxdomain", b.nx, topn, id_str);
-    top_json(j, "top_refused", b.refused, topn, id_str);
-    top_json(j, "top_srvfail", b.srvfail, topn, id_str);
-    top_json(j, "top_nodata", b.nodata, topn, id_str);
-    if (details) {
-        top_json(j, "top_qname_by_resp_bytes", b.sized_resp, topn, id_str);
-        top_json(j, "top_noerror", b.noerror, topn, id_str);
+    if (g & DG_CARDINALITY) { j.key("cardinality"); j.obj(); j.key("qname"); j.i64(lround(b.qname.estimate())); j.end_obj(); }
+    if (g & DG_TRANSACTIONS) {
+        j.key("xact"); j.obj();
+        j.key("counts"); j.obj(); j.key("total"); j.u64(b.xacts_total); j.key("timed_out"); j.u64(b.xacts_timed_out); j.end_obj();
+        j.key("in"); j.obj(); j.key("total"); j.u64(b.xacts_in);
+        top_json(j, "top_slow", b.slow_in, topn, id_str);
+        if (g & DG_QUANTILES) quant_json(j, "quantiles_us", b.xact_to);
+        if (g & DG_HISTOGRAMS) hist_json(j, "histogram_us", b.hist_to);
+        j.end_obj();
+        j.key("out"); j.obj(); j.key("total"); j.u64(b.xacts_out);
+        top_json(j, "top_slow", b.slow_out, topn, id_str);
+        if (g & DG_QUANTILES) quant_json(j, "quantiles_us", b.xact_from);
+        if (g & DG_HISTOGRAMS) hist_json(j, "histogram_us", b.hist_from);
+        j.end_obj();
+        if ((g & DG_QUANTILES) && !b.ratio.empty()) { j.key("ratio"); j.obj(); quant_json(j, "quantiles", b.ratio); j.end_obj(); }
+        j.end_obj();
+    }
+    if (g & DG_TOP_PORTS) top_json(j, "top_udp_ports", b.udp_port, topn, u16s);
+    if (g & DG_TOP_ECS) {
+        // geo / ASN lookups need a MaxMind database: none is enabled (HandlerModulePlugin::city/asn)
+        j.key("top_geoLoc_ecs"); j.arr(); j.end_arr();
+        j.key("top_asn_ecs"); j.arr(); j.end_arr();
+        top_json(j, "top_query_ecs", b.ecs, topn, id_str);
+    }
+    if (g & DG_TOP_QNAMES) {
+        top_json(j, "top_qname2", b.qname2, topn, id_str);
+        top_json(j, "top_qname3", b.qname3, topn, id_str);
+        top_json(j, "top_nxdomain", b.nx, topn, id_str);
+        top_json(j, "top_refused", b.refused, topn, id_str);
+        top_json(j, "top_srvfail", b.srvfail, topn, id_str);
+        top_json(j, "top_nodata", b.nodata, topn, id_str);
+        if (g & DG_TOP_QNAMES_DETAILS) {
+            top_json(j, "top_qname_by_resp_bytes", b.sized_resp, topn, id_str);
+            top_json(j, "top_noerror", b.noerror, topn, id_str);
+        }
     }
     top_json(j, "top_rcode", b.rcode, topn, rc);
     top_json(j, "top_qtype", b.qtype, topn, qt);
@@ -1300,7 +1459,12 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "window") c.window = (unsigned)atoi(v.c_str());
         else if (k == "topn_count") c.topn_count = (size_t)atoll(v.c_str());
         else if (k == "xact_ttl_ms") c.xact_ttl_ms = (uint32_t)atoll(v.c_str());
-        else if (k == "dns_details") c.dns_details = atoi(v.c_str()) != 0;
+        else if (k == "dns_details") { if (atoi(v.c_str())) c.dns_groups |= DG_TOP_QNAMES_DETAILS; }
+        else if (k == "net_groups") c.net_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
+        else if (k == "dns_groups") c.dns_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
+        else if (k == "filter_all") c.filter_all = atoi(v.c_str()) != 0;
+        else if (k == "net_filter_all") c.net_filter_all = atoi(v.c_str()) != 0;
+        else if (k == "topn_pct") c.topn_pct = (uint32_t)atoi(v.c_str());
         else if (k == "exclude_noerror") c.exclude_noerror = atoi(v.c_str()) != 0;
         else if (k == "only_rcode_mask") c.only_rcode_mask = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "answer_count") { c.has_answer_count = true; c.answer_count = (uint32_t)atoll(v.c_str()); }
@@ -1358,6 +1522,7 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
     if (!f.open(file, len, err)) { *out = strdup(err.c_str()); return -2; }
     Engine e(c);
     e.linktype = f.linktype;
+    topn_pct = c.topn_pct;
     Pkt pk;
     TS last;
     bool first = true;
@@ -1373,9 +1538,9 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
     j.key(std::to_string(w) + "m");
     j.obj();
     auto nb = window_bucket(e.net, w);
-    j.key("packets"); j.obj(); net_json(j, *nb, c.topn_count); j.end_obj();
+    j.key("packets"); j.obj(); net_json(j, *nb, c.topn_count, c.net_groups); j.end_obj();
     auto db = window_bucket(e.dns, w);
-    j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_details); j.end_obj();
+    j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_groups); j.end_obj();
     j.end_obj();
     j.end_obj();
     *out = strdup(j.s.c_str());

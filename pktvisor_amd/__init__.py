@@ -38,15 +38,15 @@ DNS_DEFAULT = sum(DNS_GROUPS[g] for g in ("cardinality", "counters", "quantiles"
 NET_DEFAULT = 15
 
 
-class PvError(RuntimeError):
-    pass
+from pktvisor_amd.config import PvError  # noqa: E402  (base of every error this package raises)
 
 
 class pv_config(ctypes.Structure):
     _fields_ = [("host_spec", ctypes.c_char_p), ("num_periods", ctypes.c_uint32), ("topn_count", ctypes.c_uint32),
                 ("xact_ttl_ms", ctypes.c_uint32), ("net_groups", ctypes.c_uint32), ("dns_groups", ctypes.c_uint32),
                 ("linktype", ctypes.c_uint32), ("ts_nano", ctypes.c_uint32), ("device", ctypes.c_int32),
-                ("table_log2", ctypes.c_uint32), ("max_records", ctypes.c_uint64)]
+                ("table_log2", ctypes.c_uint32), ("max_records", ctypes.c_uint64),
+                ("topn_percentile_threshold", ctypes.c_uint32), ("net_filter_all", ctypes.c_uint32)]
 
 
 class pv_dns_filters(ctypes.Structure):
@@ -54,11 +54,12 @@ class pv_dns_filters(ctypes.Structure):
                 ("answer_count", ctypes.c_int32), ("only_queries", ctypes.c_uint32), ("only_responses", ctypes.c_uint32),
                 ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16), ("n_qnames", ctypes.c_uint32),
                 ("qnames", ctypes.POINTER(ctypes.c_char_p)), ("n_qname_suffixes", ctypes.c_uint32),
-                ("qname_suffixes", ctypes.POINTER(ctypes.c_char_p)), ("only_dnssec_response", ctypes.c_uint32)]
+                ("qname_suffixes", ctypes.POINTER(ctypes.c_char_p)), ("only_dnssec_response", ctypes.c_uint32),
+                ("filter_all", ctypes.c_uint32)]
 
 
-class ConfigError(PvError):
-    """The reference's ConfigException (src/Configurable.h), same messages."""
+from pktvisor_amd.config import ConfigException as ConfigError  # noqa: E402  (the reference's texts)
+from pktvisor_amd.config import StreamHandlerException  # noqa: E402,F401
 
 
 DNS_FILTER_KEYS = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype",
@@ -76,13 +77,20 @@ def dns_filter_config(cfg: dict) -> dict:
     """DnsStreamHandler::start's filter setup (src/handlers/dns/v1/DnsStreamHandler.cpp:60-150):
     typed values in, the pv_dns_filters fields out; ConfigError with the reference's text."""
     out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[],
-               only_qname=[], only_qname_suffix=[], only_dnssec_response=0)
+               only_qname=[], only_qname_suffix=[], only_dnssec_response=0, filter_all=0)
     for k in cfg:
         if k in DNS_FILTER_NOT_BUILT:
             raise ConfigError(f"DnsStreamHandler: filter {k} is not supported by the GPU handler")
         if k not in DNS_FILTER_KEYS:
             raise ConfigError(f"{k} is an invalid/unsupported config or filter. The valid configs/filters are: "
                               + ", ".join(DNS_FILTER_KEYS))
+    # Configurable::config_get<T> (src/Configurable.h:101-112): a value of another type throws
+    for k in ("exclude_noerror", "only_queries", "only_responses", "only_dnssec_response"):
+        if k in cfg and not isinstance(cfg[k], bool):
+            raise ConfigError(f"wrong type for key: {k}")
+    for k in ("only_qtype", "only_qname", "only_qname_suffix"):
+        if k in cfg and (not isinstance(cfg[k], (list, tuple)) or not all(isinstance(x, str) for x in cfg[k])):
+            raise ConfigError(f"wrong type for key: {k}")
     if cfg.get("exclude_noerror"):
         out["exclude_noerror"] = 1
     elif "only_rcode" in cfg:
@@ -262,17 +270,38 @@ class RecordIndex:
 
 
 class PvHandlers:
-    """Net v1 ("packets") + DNS v1 ("dns") handlers on one MI355X."""
+    """Net v1 ("packets") + DNS v1 ("dns") handlers on one MI355X.
+
+    net_config / dns_config: the handlers' own config maps with the reference's keys and
+    validation (enable / disable groups, filters, xact_ttl_*, window keys; see
+    pktvisor_amd.config), raising the reference's StreamHandlerException / ConfigException
+    texts. The older keyword form (net_groups / dns_groups bits, dns_filters) stays."""
 
     def __init__(self, host_spec: Optional[str] = None, num_periods: int = 5, topn_count: int = 10,
                  xact_ttl_ms: int = 5000, linktype: int = 1, ts_nano: int = 0, device: int = -1,
                  table_log2: int = 0, max_records: int = 1 << 20, net_groups: int = 0, dns_groups: int = 0,
-                 dns_filters: Optional[dict] = None):
+                 dns_filters: Optional[dict] = None, net_config: Optional[dict] = None,
+                 dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0):
+        from pktvisor_amd import config as pvcfg
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
+        net_filter_all = 0
+        if net_config is not None or dns_config is not None:
+            ncfg, dcfg = dict(net_config or {}), dict(dns_config or {})
+            win = pvcfg.window_config([ncfg, dcfg])
+            if win.get("deep_sample_rate", 100) != 100:
+                raise pvcfg.ConfigException("deep_sample_rate below 100 is not supported by the GPU handler")
+            num_periods = win.get("num_periods", num_periods)
+            topn_count = win.get("topn_count", topn_count)
+            topn_percentile_threshold = win.get("topn_percentile_threshold", topn_percentile_threshold)
+            n, d = pvcfg.net_start(ncfg), pvcfg.dns_start(dcfg)
+            net_groups, dns_groups, net_filter_all = n["groups"], d["groups"], int(n["filter_all"])
+            filt = d["filters"]
+            if d["xact_ttl_ms"] is not None:
+                xact_ttl_ms = d["xact_ttl_ms"]
         self._host = host_spec.encode() if host_spec else None
         cfg = pv_config(self._host, num_periods, topn_count, xact_ttl_ms, net_groups, dns_groups, linktype, ts_nano,
-                        device, table_log2, max_records)
+                        device, table_log2, max_records, topn_percentile_threshold, net_filter_all)
         self.num_periods = num_periods
         self.ctx = ctypes.c_void_p()
         rc = self.lib.pv_create(ctypes.byref(cfg), ctypes.byref(self.ctx))
@@ -287,6 +316,7 @@ class PvHandlers:
             for k, q in enumerate(filt["only_qtype"]):
                 f.qtypes[k] = q
             f.only_dnssec_response = filt["only_dnssec_response"]
+            f.filter_all = filt.get("filter_all", 0)
             if filt["only_qname"]:
                 self._qnames = (ctypes.c_char_p * len(filt["only_qname"]))(*[q.encode() for q in filt["only_qname"]])
                 f.n_qnames = len(filt["only_qname"])

@@ -1,0 +1,171 @@
+"""Handler configuration with the reference's validation and error texts.
+
+Mirrors what StreamMetricsHandler::start does before any packet flows
+(src/StreamHandler.h:94-152) for the two handlers on the path:
+
+  * validate_configs: every key of the handler config must be one of the handler's
+    _config_defs, a window config key, "enable" or "disable"
+    (NetStreamHandler.h:204-209, DnsStreamHandler.h:381-397);
+  * process_groups: the handler's default groups, then "disable", then "enable", each
+    list stopping at "all" (src/StreamHandler.h:111-133; defaults
+    NetStreamHandler.cpp:53-56, DnsStreamHandler.cpp:52-57);
+  * the DNS filters and configs (DnsStreamHandler::start, :60-201).
+
+The result is the typed pv_config / pv_dns_filters content the C-ABI takes; the GPU
+path never sees a config it does not implement (unbuilt keys raise, never ignored).
+"""
+from __future__ import annotations
+
+
+class PvError(RuntimeError):
+    """Base of every error pktvisor_amd raises."""
+
+
+class StreamHandlerException(PvError):
+    """visor::StreamHandlerException (src/StreamHandler.h)"""
+
+
+class ConfigException(PvError):
+    """visor::ConfigException (src/Configurable.h)"""
+
+
+WINDOW_CONFIG_DEFS = ("deep_sample_rate", "num_periods", "topn_count", "topn_percentile_threshold")
+NET_CONFIG_DEFS = ("geoloc_notfound", "asn_notfound", "only_geoloc_prefix", "only_asn_number", "recorded_stream")
+DNS_CONFIG_DEFS = ("exclude_noerror", "only_rcode", "only_queries", "only_responses", "only_dnssec_response",
+                   "answer_count", "only_qtype", "only_qname", "only_qname_suffix", "geoloc_notfound", "asn_notfound",
+                   "dnstap_msg_type", "public_suffix_list", "recorded_stream", "xact_ttl_secs", "xact_ttl_ms")
+# group name -> pv_net_group / pv_dns_group bit (include/pvgpu.h); listed sorted, as std::map iterates
+NET_GROUP_DEFS = {"cardinality": 1 << 1, "counters": 1 << 0, "top_geo": 1 << 2, "top_ips": 1 << 3}
+DNS_GROUP_DEFS = {"cardinality": 1 << 0, "counters": 1 << 1, "dns_transaction": 1 << 4, "histograms": 1 << 3,
+                  "quantiles": 1 << 2, "top_ecs": 1 << 5, "top_ports": 1 << 8, "top_qnames": 1 << 6,
+                  "top_qnames_details": 1 << 7}
+NET_DEFAULT_GROUPS = ("counters", "cardinality", "top_geo", "top_ips")
+DNS_DEFAULT_GROUPS = ("cardinality", "counters", "quantiles", "dns_transaction", "top_qnames", "top_ports")
+DNSTAP_MSG_TYPES = ("auth", "client", "forwarder", "resolver", "stub", "tool", "update")
+GROUPS_SET = 0x80000000  # PV_GROUPS_SET
+
+
+def validate_configs(cfg: dict, defs) -> None:
+    """StreamMetricsHandler::validate_configs (src/StreamHandler.h:135-152)"""
+    for key in cfg:
+        if key in WINDOW_CONFIG_DEFS or key in defs or key in ("enable", "disable", "_internal_tap_name"):
+            continue
+        raise StreamHandlerException(f"{key} is an invalid/unsupported config or filter. The valid configs/filters are: "
+                                     f"{', '.join(defs)}, {', '.join(WINDOW_CONFIG_DEFS)}")
+
+
+def _string_list(cfg: dict, key: str) -> list:
+    v = cfg[key]
+    if not isinstance(v, (list, tuple)) or not all(isinstance(x, str) for x in v):
+        raise ConfigException(f"wrong type for key: {key}")  # Configurable::config_get (src/Configurable.h:110)
+    return list(v)
+
+
+def process_groups(cfg: dict, group_defs: dict, defaults) -> int:
+    """StreamMetricsHandler::process_groups (src/StreamHandler.h:94-133): the enabled group bits"""
+    bits = 0
+    for g in defaults:
+        bits |= group_defs[g]
+
+    def one(g):
+        if g not in group_defs:
+            raise StreamHandlerException(f"{g} is an invalid/unsupported metric group. The valid groups are: all, "
+                                         + ", ".join(sorted(group_defs)))
+        return group_defs[g]
+
+    if "disable" in cfg:
+        for g in _string_list(cfg, "disable"):
+            if g == "all":
+                bits = 0
+                break
+            bits &= ~one(g)
+    if "enable" in cfg:
+        for g in _string_list(cfg, "enable"):
+            if g == "all":
+                for v in group_defs.values():
+                    bits |= v
+                break
+            bits |= one(g)
+    return bits
+
+
+def _bool(cfg: dict, key: str) -> bool:
+    v = cfg.get(key, False)
+    if not isinstance(v, bool):
+        raise ConfigException(f"wrong type for key: {key}")
+    return v
+
+
+def _uint(cfg: dict, key: str) -> int:
+    v = cfg[key]
+    if isinstance(v, bool) or not isinstance(v, int) or v < 0:
+        raise ConfigException(f"wrong type for key: {key}")
+    return v
+
+
+def window_config(cfgs) -> dict:
+    """The window config keys (AbstractMetricsManager::AbstractMetricsManager,
+    src/AbstractMetricsManager.h:351-389): num_periods 1..10, deep_sample_rate 1..100, topn_count,
+    topn_percentile_threshold 0..99 — one value shared by both handlers here."""
+    out = {}
+    for cfg in cfgs:
+        for k in WINDOW_CONFIG_DEFS:
+            if k in cfg:
+                v = _uint(cfg, k)
+                if k in out and out[k] != v:
+                    raise ConfigException(f"{k} differs between the net and dns handler configs")
+                out[k] = v
+    np = out.get("num_periods", 5)
+    if not 1 <= np <= 10:
+        raise ConfigException("num_periods must be between 1 and 10")
+    rate = out.get("deep_sample_rate", 100)
+    if not 1 <= rate <= 100:
+        raise ConfigException("deep_sample_rate must be between 1 and 100")
+    if out.get("topn_percentile_threshold", 0) > 99:
+        raise ConfigException("topn_percentile_threshold must be between 0 and 99")
+    return out
+
+
+def net_start(cfg: dict) -> dict:
+    """NetStreamHandler::start (src/handlers/net/v1/NetStreamHandler.cpp:45-130) up to the
+    signal wiring: {"groups": bits | GROUPS_SET, "filter_all": bool}"""
+    validate_configs(cfg, NET_CONFIG_DEFS)
+    groups = process_groups(cfg, NET_GROUP_DEFS, NET_DEFAULT_GROUPS)
+    out = {"groups": groups | GROUPS_SET, "filter_all": False}
+    # the geo / ASN filters match a MaxMind lookup; with no database enabled every packet is
+    # filtered (_filtering :223-283: !city->enabled() => will_filter)
+    if _bool(cfg, "geoloc_notfound") or _bool(cfg, "asn_notfound"):
+        out["filter_all"] = True
+    if "only_geoloc_prefix" in cfg:
+        _string_list(cfg, "only_geoloc_prefix")
+        out["filter_all"] = True
+    if "only_asn_number" in cfg:
+        for number in _string_list(cfg, "only_asn_number"):
+            if not number.isdigit():
+                raise ConfigException(f"NetStreamHandler: only_asn_number filter contained an invalid/unsupported value: {number}")
+        out["filter_all"] = True
+    return out
+
+
+def dns_start(cfg: dict) -> dict:
+    """DnsStreamHandler::start (src/handlers/dns/v1/DnsStreamHandler.cpp:43-201) up to the signal
+    wiring: {"groups": bits | GROUPS_SET, "filters": pv_dns_filters fields, "xact_ttl_ms": int|None}"""
+    from pktvisor_amd import dns_filter_config
+    validate_configs(cfg, DNS_CONFIG_DEFS)
+    groups = process_groups(cfg, DNS_GROUP_DEFS, DNS_DEFAULT_GROUPS)
+    fkeys = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype",
+             "only_qname", "only_qname_suffix", "only_dnssec_response")
+    filters = dns_filter_config({k: cfg[k] for k in fkeys if k in cfg})
+    # with no geo database enabled, geoloc_notfound / asn_notfound filter every packet (:619-642)
+    filters["filter_all"] = 1 if (_bool(cfg, "geoloc_notfound") or _bool(cfg, "asn_notfound")) else 0
+    if "dnstap_msg_type" in cfg and cfg["dnstap_msg_type"] not in DNSTAP_MSG_TYPES:
+        raise ConfigException("DnsStreamHandler: dnstap_msg_type contained an invalid/unsupported type. Valid types: "
+                              + ", ".join(DNSTAP_MSG_TYPES))
+    if _bool(cfg, "public_suffix_list"):
+        raise ConfigException("DnsStreamHandler: public_suffix_list is not supported by the GPU handler")
+    ttl = None
+    if "xact_ttl_ms" in cfg:
+        ttl = _uint(cfg, "xact_ttl_ms")
+    elif "xact_ttl_secs" in cfg:
+        ttl = _uint(cfg, "xact_ttl_secs") * 1000
+    return {"groups": groups | GROUPS_SET, "filters": filters, "xact_ttl_ms": ttl}

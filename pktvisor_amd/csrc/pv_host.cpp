@@ -577,6 +577,11 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out) // s: table (PV_T
                     char b[64];
                     inet_ntop(AF_INET6, &arena[p + 2], b, sizeof b);
                     r.name = b;
+                } else if (m == TM_ECS && len == 17) {
+                    // ECS client subnet text (inet_ntop, DnsAdditionalRecord.h:86,95)
+                    char b[64];
+                    inet_ntop(arena[p + 2] == 1 ? AF_INET : AF_INET6, &arena[p + 3], b, sizeof b);
+                    r.name = b;
                 } else {
                     r.name.assign((const char *)&arena[p + 2], len);
                 }
@@ -693,16 +698,28 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int 
     return 0;
 }
 
-void top_json(Json &j, const char *key, const std::vector<std::pair<std::string, uint64_t>> &v0, size_t n)
+// TopN::to_json (src/Metrics.h:577-590): the first topn_count items by estimate, cut at the
+// first one below the topn_percentile_threshold quantile of those estimates (_get_threshold,
+// :510-521, the KLL inclusive rank rule on them)
+void top_json(Json &j, const char *key, const std::vector<std::pair<std::string, uint64_t>> &v0, size_t n, uint32_t pct)
 {
     auto v = v0;
     std::sort(v.begin(), v.end(), [](const auto &a, const auto &b) {
         if (a.second != b.second) return a.second > b.second;
         return a.first < b.first;
     });
+    const size_t k = std::min(n, v.size());
+    uint64_t thr = 0;
+    if (k) {
+        std::vector<uint64_t> est;
+        for (size_t i = 0; i < k; i++) est.push_back(v[i].second);
+        std::sort(est.begin(), est.end());
+        const uint64_t w = (uint64_t)std::ceil((double)pct / 100.0 * (double)k);
+        thr = est[w == 0 ? 0 : std::min<size_t>(w - 1, k - 1)];
+    }
     j.key(key);
     j.arr();
-    for (size_t i = 0; i < std::min(n, v.size()); i++) {
+    for (size_t i = 0; i < k && v[i].second >= thr; i++) {
         j.obj();
         j.key("name").str(v[i].first);
         j.key("estimate").u(v[i].second);
@@ -735,6 +752,37 @@ std::vector<std::pair<std::string, uint64_t>> dense_tops(const uint64_t *t, size
     return v;
 }
 
+// Histogram::to_json (src/Metrics.h:193-262) over exact values: split points are the distinct
+// uint64 values of 10^(b/18) * 10^e, e in [-9, 18), b in [0, 18); a point is listed when the
+// inclusive PMF interval that ends at it holds a value, with the inclusive CDF times n (a
+// double, as KLL's normalized rank times get_n()); "+Inf" closes with n
+void hist_json(Json &j, const char *key, std::vector<uint64_t> v)
+{
+    if (v.empty()) return;
+    static const std::vector<uint64_t> pts = [] {
+        std::vector<uint64_t> p;
+        for (int e = -9; e < 18; e++)
+            for (int k = 0; k < 18; k++) {
+                const uint64_t x = static_cast<uint64_t>(std::pow(10.0, static_cast<float>(k) / 18) * std::pow(10.0, e));
+                if (p.empty() || p.back() != x) p.push_back(x);
+            }
+        return p;
+    }();
+    std::sort(v.begin(), v.end());
+    const double n = (double)v.size();
+    j.key(key).obj();
+    j.key("buckets").obj();
+    uint64_t prev = 0;
+    for (uint64_t x : pts) {
+        const uint64_t c = (uint64_t)(std::upper_bound(v.begin(), v.end(), x) - v.begin());
+        if (c != prev) j.key(std::to_string(x)).d(((double)c / n) * n);
+        prev = c;
+    }
+    j.key("+Inf").d(1.0 * n);
+    j.end_obj();
+    j.end_obj();
+}
+
 template <typename T>
 void quant_json(Json &j, const char *key, const std::vector<T> &v)
 {
@@ -755,6 +803,7 @@ void net_json(pv_ctx *c, Json &j, const HostBucket &b)
 {
     const uint64_t *n = &b.sum[PV_OFF_NET];
     size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
     j.key("period").obj();
     j.key("start_ts").i(b.start_sec);
     j.key("length").u(b.period_length);
@@ -781,8 +830,8 @@ void net_json(pv_ctx *c, Json &j, const HostBucket &b)
         j.end_obj();
     }
     if (c->net_groups & PV_NET_TOP_IPS) {
-        top_json(j, "top_ipv4", tops_of(b, TM_IPV4), topn);
-        top_json(j, "top_ipv6", tops_of(b, TM_IPV6), topn);
+        top_json(j, "top_ipv4", tops_of(b, TM_IPV4), topn, pct);
+        top_json(j, "top_ipv6", tops_of(b, TM_IPV6), topn, pct);
     }
     if (c->net_groups & PV_NET_TOP_GEO) {
         j.key("top_geoLoc").arr(); j.end_arr();
@@ -801,6 +850,7 @@ void dns_json(pv_ctx *c, Json &j, const HostBucket &b)
 {
     const uint64_t *d = &b.sum[PV_OFF_DNS];
     size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
     uint32_t g = c->dns_groups;
     j.key("period").obj();
     j.key("start_ts").i(b.start_sec);
@@ -823,6 +873,7 @@ void dns_json(pv_ctx *c, Json &j, const HostBucket &b)
         j.key("nodata").u(d[DC_NODATA]);
         j.key("total").u(d[DC_TOTAL]);
         j.key("filtered").u(d[DC_FILTERED]);
+        if (g & PV_DNS_TOP_ECS) j.key("query_ecs").u(d[DC_QECS]);
     }
     j.end_obj();
     if (g & PV_DNS_CARDINALITY) {
@@ -835,32 +886,40 @@ void dns_json(pv_ctx *c, Json &j, const HostBucket &b)
         j.key("counts").obj(); j.key("total").u(d[DC_XTOTAL]); j.key("timed_out").u(d[DC_XTIMEOUT]); j.end_obj();
         j.key("in").obj();
         j.key("total").u(d[DC_XIN]);
-        top_json(j, "top_slow", tops_of(b, TM_SLOW_IN), topn);
+        top_json(j, "top_slow", tops_of(b, TM_SLOW_IN), topn, pct);
         if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.to_us);
+        if (g & PV_DNS_HISTOGRAMS) hist_json(j, "histogram_us", b.to_us);
         j.end_obj();
         j.key("out").obj();
         j.key("total").u(d[DC_XOUT]);
-        top_json(j, "top_slow", tops_of(b, TM_SLOW_OUT), topn);
+        top_json(j, "top_slow", tops_of(b, TM_SLOW_OUT), topn, pct);
         if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.from_us);
+        if (g & PV_DNS_HISTOGRAMS) hist_json(j, "histogram_us", b.from_us);
         j.end_obj();
         if ((g & PV_DNS_QUANTILES) && !b.ratio.empty()) { j.key("ratio").obj(); quant_json(j, "quantiles", b.ratio); j.end_obj(); }
         j.end_obj();
     }
-    if (g & PV_DNS_TOP_PORTS) top_json(j, "top_udp_ports", dense_tops(&b.sum[PV_OFF_PORT], PV_PORT_BINS, 0), topn);
+    if (g & PV_DNS_TOP_PORTS) top_json(j, "top_udp_ports", dense_tops(&b.sum[PV_OFF_PORT], PV_PORT_BINS, 0), topn, pct);
+    if (g & PV_DNS_TOP_ECS) {
+        // geo / ASN of the subnet need a MaxMind database; none is enabled (HandlerModulePlugin::city/asn)
+        j.key("top_geoLoc_ecs").arr(); j.end_arr();
+        j.key("top_asn_ecs").arr(); j.end_arr();
+        top_json(j, "top_query_ecs", tops_of(b, TM_ECS), topn, pct);
+    }
     if (g & PV_DNS_TOP_QNAMES) {
-        top_json(j, "top_qname2", tops_of(b, TM_QNAME2), topn);
-        top_json(j, "top_qname3", tops_of(b, TM_QNAME3), topn);
-        top_json(j, "top_nxdomain", tops_of(b, TM_NX), topn);
-        top_json(j, "top_refused", tops_of(b, TM_REFUSED), topn);
-        top_json(j, "top_srvfail", tops_of(b, TM_SRVFAIL), topn);
-        top_json(j, "top_nodata", tops_of(b, TM_NODATA), topn);
+        top_json(j, "top_qname2", tops_of(b, TM_QNAME2), topn, pct);
+        top_json(j, "top_qname3", tops_of(b, TM_QNAME3), topn, pct);
+        top_json(j, "top_nxdomain", tops_of(b, TM_NX), topn, pct);
+        top_json(j, "top_refused", tops_of(b, TM_REFUSED), topn, pct);
+        top_json(j, "top_srvfail", tops_of(b, TM_SRVFAIL), topn, pct);
+        top_json(j, "top_nodata", tops_of(b, TM_NODATA), topn, pct);
         if (g & PV_DNS_TOP_QNAMES_DETAILS) {
-            top_json(j, "top_qname_by_resp_bytes", tops_of(b, TM_SIZED), topn);
-            top_json(j, "top_noerror", tops_of(b, TM_NOERROR), topn);
+            top_json(j, "top_qname_by_resp_bytes", tops_of(b, TM_SIZED), topn, pct);
+            top_json(j, "top_noerror", tops_of(b, TM_NOERROR), topn, pct);
         }
     }
-    top_json(j, "top_rcode", dense_tops(&b.sum[PV_OFF_RCODE], PV_RCODE_BINS, 2), topn);
-    top_json(j, "top_qtype", dense_tops(&b.sum[PV_OFF_QTYPE], PV_QTYPE_BINS, 1), topn);
+    top_json(j, "top_rcode", dense_tops(&b.sum[PV_OFF_RCODE], PV_RCODE_BINS, 2), topn, pct);
+    top_json(j, "top_qtype", dense_tops(&b.sum[PV_OFF_QTYPE], PV_QTYPE_BINS, 1), topn, pct);
 }
 
 // KLL inclusive rank rule on exact data
@@ -970,6 +1029,7 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
     if (f->only_queries) fl |= PVDF_ONLY_QUERIES;
     if (f->only_responses) fl |= PVDF_ONLY_RESPONSES;
     if (f->only_dnssec_response) fl |= PVDF_ONLY_DNSSEC;
+    if (f->filter_all) fl |= PVDF_FILTER_ALL;
     if (f->n_qtypes > PV_MAX_QTYPES) return c->fail(PV_EINVAL, "only_qtype: at most %d qtypes", PV_MAX_QTYPES);
     for (uint32_t k = 0; k < f->n_qtypes; k++)
         if (!qtype_names().count(f->qtypes[k]))
@@ -1026,8 +1086,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     if (c->cfg.topn_count == 0) c->cfg.topn_count = 10;
     if (c->cfg.xact_ttl_ms == 0) c->cfg.xact_ttl_ms = 5000;
     if (c->cfg.linktype == 0) c->cfg.linktype = 1;
-    if (c->cfg.net_groups) c->net_groups = c->cfg.net_groups;
-    if (c->cfg.dns_groups) c->dns_groups = c->cfg.dns_groups;
+    // group bits, 0 = the handler's defaults; PV_GROUPS_SET marks an explicit set (which may be empty)
+    if (c->cfg.net_groups) c->net_groups = c->cfg.net_groups & ~PV_GROUPS_SET;
+    if (c->cfg.dns_groups) c->dns_groups = c->cfg.dns_groups & ~PV_GROUPS_SET;
     if (c->cfg.table_log2) c->tcap_log2 = c->cfg.table_log2;
     if (c->tcap_log2 < 8 || c->tcap_log2 > PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2) {
         *out = c;
@@ -1274,6 +1335,7 @@ void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t
     P.ts_nano = c->cfg.ts_nano;
     P.net_groups = c->net_groups;
     P.dns_groups = c->dns_groups;
+    P.net_filter_all = c->cfg.net_filter_all ? 1u : 0u;
     P.nets = c->nets;
     P.f_flags = c->f_flags;
     P.f_rcode_mask = c->f_rcode_mask;
@@ -1492,7 +1554,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint6
         X.n = nev;
         X.ttl_s = c->ttl_s;
         X.ttl_ms = c->ttl_ms;
-        X.quantiles = (c->dns_groups & PV_DNS_QUANTILES) ? 1 : 0;
+        X.quantiles = ((c->dns_groups & PV_DNS_QUANTILES) ? 1u : 0u) | ((c->dns_groups & PV_DNS_HISTOGRAMS) ? 2u : 0u);
         for (uint32_t k = 0; k <= P.n_dshift; k++) {
             X.slot_gen[k] = P.dslot_of[k] | (c->gen[P.dslot_of[k]] << 8);
             X.thr_from[k] = k == 0 ? c->from90 : -1.0f;

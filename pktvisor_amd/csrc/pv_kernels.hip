@@ -188,6 +188,17 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     // DNS names: re-derive the first query name of the record
     uint64_t m = o.l4off + 8;
     uint32_t len = o.l4len - 8;
+    if (metric == TM_ECS) {
+        // the query's ECS address: family byte + 16 address bytes (the host formats it)
+        uint64_t addr = 0;
+        const uint32_t fam = dns_ecs(R, m, len, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8), be16(R, m + 10), addr);
+        uint64_t pos = atomicAdd(top, 19ull);
+        if (pos + 19 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+        pos += part * pcap;
+        arena[pos] = 17; arena[pos + 1] = 0; arena[pos + 2] = (uint8_t)fam;
+        for (int i = 0; i < 16; i++) arena[pos + 3 + i] = i < 8 ? (uint8_t)(addr >> (8 * i)) : 0;
+        return (uint32_t)pos + 1;
+    }
     NameStats st;
     st.init();
     uint32_t nl = name_len_l1(R, m, len, 12);
@@ -357,8 +368,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 
 // Net v1 counters of the wave's current slot, in registers
 struct NetCtr {
-    uint32_t nev, nin, nout, nunk, n4, n6, nudp, ntcp, nsyn, noth;
-    __device__ __forceinline__ void zero() { nev = nin = nout = nunk = n4 = n6 = nudp = ntcp = nsyn = noth = 0; }
+    uint32_t nev, nin, nout, nunk, n4, n6, nudp, ntcp, nsyn, noth, nfilt;
+    __device__ __forceinline__ void zero() { nev = nin = nout = nunk = n4 = n6 = nudp = ntcp = nsyn = noth = nfilt = 0; }
     __device__ __forceinline__ void add(const Parsed &o)
     {
         nev++;
@@ -380,8 +391,8 @@ __device__ void net_flush(PV_CREF(PvParams) P, uint32_t s, NetCtr &c)
 }
 // DNS v1 counters of the wave's current slot
 struct DnsCtr {
-    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata, dfilt;
-    __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = dfilt = 0; }
+    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata, dfilt, dqecs;
+    __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = dfilt = dqecs = 0; }
 };
 __device__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
 {
@@ -394,6 +405,7 @@ __device__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
     PV_FLUSH1(s, PV_OFF_DNS + DC_NX, c.dnx, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REFUSED, c.dref, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_SRVFAIL, c.dsrv, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_NOERROR, c.dnoerr, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_NODATA, c.dnodata, dc)
+    if (P.dns_groups & PV_DNS_TOP_ECS_BIT) PV_FLUSH1(s, PV_OFF_DNS + DC_QECS, c.dqecs, dc)
     c.zero();
 }
 
@@ -555,7 +567,8 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
                     ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
                     ((P.f_flags & PVDF_ONLY_QUERIES) && qr) || ((P.f_flags & PVDF_ONLY_RESPONSES) && !qr) ||
-                    ((P.f_flags & PVDF_ONLY_DNSSEC) && (!qr || !ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar)));
+                    ((P.f_flags & PVDF_ONLY_DNSSEC) && (!qr || !ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar))) ||
+                    (P.f_flags & PVDF_FILTER_ALL);
         if (!filt && (P.f_flags & PVDF_ONLY_QTYPE)) {
             DnsInfo fd;
             dns_parse(R, m, dlen, qd, ancount, ns, ar, fd);
@@ -666,6 +679,16 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                     }
                 }
             }
+            // top_ecs (DnsMetricsBucket::process_dns_layer :1026-1048): a query's EDNS Client Subnet
+            if ((P.dns_groups & PV_DNS_TOP_ECS_BIT) && !qr && ar) {
+                uint64_t addr;
+                const uint32_t fam = dns_ecs(R, m, dlen, qd, ancount, ns, ar, addr);
+                if (fam) {
+                    if (own) c.dqecs++;
+                    else if (P.dns_groups & PV_DNS_COUNTERS_BIT) sum_add(P, slot, PV_OFF_DNS + DC_QECS, 1);
+                    global_add(P, slot, PV_KEY(TM_ECS, fmix64(addr ^ ((uint64_t)fam << 62) ^ 0xec5ull)), 1, i);
+                }
+            }
         }
     }
     if (P.want_events) {
@@ -751,7 +774,7 @@ struct NetK {
     PV_G uint64_t *iplog;
     PV_G uint64_t *dq;
     PV_G uint32_t *flags;
-    uint32_t n_shift, skip_before, slot0, net_groups, dbg;
+    uint32_t n_shift, skip_before, slot0, net_groups, dbg, net_filter_all;
 };
 // Net v1 counters of one record straight to HBM (a lane whose slot is not the wave's
 // register slot: records of a 64-record tile that holds a period shift)
@@ -787,11 +810,12 @@ __device__ void knet_flush(const NetK &K, uint32_t s, NetCtr &c)
 {
     const bool nc = K.net_groups & PV_NET_COUNTERS_BIT;
     PV_KFLUSH1(s, PV_OFF_NET + NC_EVENTS, c.nev, true) PV_KFLUSH1(s, PV_OFF_NET + NC_SAMPLES, c.nev, true)
-    PV_KFLUSH1(s, PV_OFF_NET + NC_TOTAL, c.nev, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_IN, c.nin, nc)
+    PV_KFLUSH1(s, PV_OFF_NET + NC_TOTAL, c.nev - c.nfilt, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_IN, c.nin, nc)
     PV_KFLUSH1(s, PV_OFF_NET + NC_OUT, c.nout, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_UNK, c.nunk, nc)
     PV_KFLUSH1(s, PV_OFF_NET + NC_V4, c.n4, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_V6, c.n6, nc)
     PV_KFLUSH1(s, PV_OFF_NET + NC_UDP, c.nudp, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_TCP, c.ntcp, nc)
     PV_KFLUSH1(s, PV_OFF_NET + NC_SYN, c.nsyn, nc) PV_KFLUSH1(s, PV_OFF_NET + NC_OTHER, c.noth, nc)
+    if (K.net_filter_all) PV_KFLUSH1(s, PV_OFF_NET + NC_FILTERED, c.nfilt, nc)
     c.zero();
 }
 
@@ -1049,7 +1073,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
     K.recs = P.recs; K.offs = P.offs; K.n = P.n; K.rec_bytes = P.rec_bytes; K.gbase = P.gbase;
     K.sum = P.sum; K.cpc = P.cpc; K.iplog = P.iplog; K.dq = P.dq; K.flags = P.flags;
     K.n_shift = P.n_shift; K.skip_before = P.skip_before; K.slot0 = P.slot_of[0];
-    K.net_groups = P.net_groups; K.dbg = P.dbg;
+    K.net_groups = P.net_groups; K.dbg = P.dbg; K.net_filter_all = P.net_filter_all;
     const ParseCfg C = parse_cfg(P);
     const uint64_t n = K.n, last = n - 1;
     const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
@@ -1157,7 +1181,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                 fast = fast_parse(rw, C, P, off, o);
             }
             if (!fast) {
-                const SlowOut so = net_slow(R, C, P, K, off, i, slot, upd);
+                const SlowOut so = net_slow(R, C, P, K, off, i, slot, upd && !K.net_filter_all);
                 o.caplen = so.caplen; o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
                 ek = so.ek;
                 dm = so.dm;
@@ -1166,6 +1190,17 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
             STAMP(4)
             if (K.dbg & 2) {
                 c.add(o);
+            } else if (K.net_filter_all) {
+                // process_filtered (net/v1/NetStreamHandler.cpp:507-514): an event and `filtered` only
+                if (upd) {
+                    if (own) { c.nev++; c.nfilt++; }
+                    else {
+                        ksum_add(K, slot, PV_OFF_NET + NC_EVENTS, 1);
+                        ksum_add(K, slot, PV_OFF_NET + NC_SAMPLES, 1);
+                        if (K.net_groups & PV_NET_COUNTERS_BIT) ksum_add(K, slot, PV_OFF_NET + NC_FILTERED, 1);
+                    }
+                }
+                ek = 0;
             } else {
                 if (upd) {
                     if (own) c.add(o);
@@ -1190,14 +1225,15 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                         }
                     }
                 }
-                if (fast && o.l4 == 17 && !(K.dbg & 4)) {
-                    const uint32_t port = dns_port(rw.at(50));
-                    if (port) {
-                        DnsMsg d = dns_msg_of(P, R, o, i, port, false);
-                        d.fkey = fast_flowkey(rw);
-                        dm = msg_words(d);
-                        isdns = true;
-                    }
+            }
+            // the DNS handler takes the pcap input's UDP signal itself (not chained behind Net)
+            if (!(K.dbg & 2) && fast && o.l4 == 17 && !(K.dbg & 4)) {
+                const uint32_t port = dns_port(rw.at(50));
+                if (port) {
+                    DnsMsg d = dns_msg_of(P, R, o, i, port, false);
+                    d.fkey = fast_flowkey(rw);
+                    dm = msg_words(d);
+                    isdns = true;
                 }
             }
         } else if (K.dbg & 1) {
@@ -1944,8 +1980,9 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         if (X.quantiles) {
             if (e.dir == 0) xval(X, T, e.period, XV_FROM_US, us);
             else if (e.dir == 1) xval(X, T, e.period, XV_TO_US, us);
-            if (qe.len && kept) xval(X, T, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
         }
+        if ((X.quantiles & 1) && qe.len && kept)
+            xval(X, T, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
         if (!kept || e.dir == 2) return;
         if (X.thr_from[e.period] < 0.0f) {
             T.valid[atomicAdd(&T.nvalid, 1u)] = PvXValid{e.idx, (uint8_t)e.period, (uint8_t)e.dir, 0, 0, us};

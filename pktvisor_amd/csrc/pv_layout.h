@@ -37,6 +37,8 @@
 #define PV_DNS_CARDINALITY_BIT (1u << 0)
 #define PV_DNS_COUNTERS_BIT (1u << 1)
 #define PV_DNS_QUANTILES_BIT (1u << 2)
+#define PV_DNS_HISTOGRAMS_BIT (1u << 3)
+#define PV_DNS_TOP_ECS_BIT (1u << 5)
 #define PV_DNS_TRANSACTIONS_BIT (1u << 4)
 #define PV_DNS_TOP_QNAMES_BIT (1u << 6)
 #define PV_DNS_TOP_QNAMES_DETAILS_BIT (1u << 7)
@@ -66,7 +68,7 @@ enum {
 // dns counters (src/handlers/dns/v1/DnsStreamHandler.h:94-139 + base event counters)
 enum {
     DC_EVENTS = 0, DC_SAMPLES, DC_QUERIES, DC_REPLIES, DC_TCP, DC_UDP, DC_V4, DC_V6, DC_NX, DC_REFUSED, DC_SRVFAIL,
-    DC_NOERROR, DC_NODATA, DC_TOTAL, DC_FILTERED, DC_XTOTAL, DC_XIN, DC_XOUT, DC_XTIMEOUT, DC_COUNT
+    DC_NOERROR, DC_NODATA, DC_TOTAL, DC_FILTERED, DC_XTOTAL, DC_XIN, DC_XOUT, DC_XTIMEOUT, DC_QECS, DC_COUNT
 };
 
 // ---- MIN region (int64 global record index), per slot: CPC lg_k = 11 => 2048 rows x 64 cols
@@ -81,7 +83,10 @@ enum {
     TM_NONE = 0, TM_IPV4 = 1, TM_IPV6 = 2, TM_QNAME2 = 3, TM_QNAME3 = 4, TM_NX = 5, TM_REFUSED = 6, TM_SRVFAIL = 7,
     TM_NODATA = 8, TM_NOERROR = 9, TM_SIZED = 10, TM_SLOW_IN = 11, TM_SLOW_OUT = 12,
     // dense metrics share the block cache, flushed into the SUM region
-    TM_DENSE_PORT = 13, TM_DENSE_QTYPE = 14, TM_DENSE_RCODE = 15
+    TM_DENSE_PORT = 13, TM_DENSE_QTYPE = 14, TM_DENSE_RCODE = 15,
+    // inserted straight into the global table (never through the block cache or update log,
+    // whose keys carry 4-bit metric ids)
+    TM_ECS = 16 // EDNS Client Subnet of a query (name record: family byte + 16 address bytes)
 };
 #define PV_KEY(metric, payload) (((uint64_t)(metric) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
 #define PV_KEY_METRIC(k) ((uint32_t)((k) >> 56))
@@ -169,7 +174,7 @@ struct PvSubnets {
 #define PV_MAX_SUFFIXES 4
 enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
        PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64, PVDF_ONLY_QSUFFIX = 128,
-       PVDF_ONLY_DNSSEC = 256 };
+       PVDF_ONLY_DNSSEC = 256, PVDF_FILTER_ALL = 512 };
 struct PvParams {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
@@ -177,6 +182,7 @@ struct PvParams {
     uint32_t linktype;
     uint32_t ts_nano;
     uint32_t net_groups, dns_groups;
+    uint32_t net_filter_all; // every packet a filtered Net event (NetStreamHandler::_filtering without a geo database)
     // Net periods inside this batch: period p (0..n_shift) covers records [pstart[p-1], pstart[p])
     // (ts_sec in [thresh[p-1], thresh[p])); Net slot of each
     uint32_t n_shift;
@@ -270,7 +276,7 @@ struct PvXactParams {
     const PV_G uint32_t *svals; // event position for each sorted key
     uint32_t n;
     uint32_t ttl_s, ttl_ms;
-    uint32_t quantiles;
+    uint32_t quantiles; // bit 0: quantiles group (time and ratio values), bit 1: histograms (time values)
     uint32_t slot_gen[PV_MAX_SHIFTS + 1]; // DNS slot | generation << 8 per DNS period
     float thr_from[PV_MAX_SHIFTS + 1];    // p90 slow thresholds per period, < 0 = not known yet
     float thr_to[PV_MAX_SHIFTS + 1];

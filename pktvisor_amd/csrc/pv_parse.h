@@ -698,6 +698,52 @@ PV_FN bool dns_dnssec(const A &R, uint64_t m, uint32_t len, uint32_t qd, uint32_
     return sig;
 }
 
+// Offset of the first additional record as DnsLayer::parseResources(false, true, true) reaches
+// it (questions, answers, authorities, then the first additional, each in bounds;
+// libs/visor_dns/DnsLayer.cpp:119-209), 0 if none
+template <class A>
+PV_FN uint32_t dns_first_additional(const A &R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns,
+                                    uint32_t ar)
+{
+    const uint32_t total = qd + an + ns + ar;
+    if (total > 100 || len < 12 || ar == 0) return 0;
+    uint32_t off = 12;
+    for (uint32_t i = 0; i < total; i++) {
+        const uint32_t nl = name_len_l1(R, m, len, off);
+        const uint32_t start = off;
+        if (i < qd) off += nl + 4;
+        else {
+            const uint32_t dl = (off + nl + 10 <= len) ? be16(R, m + off + nl + 8) : 0u;
+            off += nl + 10 + dl;
+        }
+        if (off > len) return 0;
+        if (i == qd + an + ns) return start;
+    }
+    return 0;
+}
+// parse_additional_records_ecs (libs/visor_dns/DnsAdditionalRecord.h:49-101) on a query's
+// first additional record: an OPT record whose data (>= 9 bytes) opens with option CSUBNET
+// (8). Returns the family (1 IPv4, 2 IPv6; 0 = no ECS) and the address bytes the reference
+// keeps, little-endian in lo | hi: IPv4 data bytes 8 .. 12 (it copies them all into a 4-byte
+// array; bytes past 4 are not kept), IPv6 data bytes 8 .. min(len, 16).
+template <class A>
+PV_FN uint32_t dns_ecs(const A &R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns, uint32_t ar,
+                       uint64_t &addr)
+{
+    addr = 0;
+    const uint32_t a = dns_first_additional(R, m, len, qd, an, ns, ar);
+    if (!a) return 0;
+    const uint32_t nl = name_len_l1(R, m, len, a);
+    const uint32_t type = be16(R, m + a + nl), dlen = be16(R, m + a + nl + 8);
+    if (type != 41 || dlen < 9) return 0;
+    const uint64_t x = m + a + nl + 10;
+    if (be16(R, x) != 8) return 0;
+    const uint32_t family = be16(R, x + 4);
+    const uint32_t lim = family == 1 ? (dlen < 12 ? dlen : 12u) : (family == 2 ? (dlen < 16 ? dlen : 16u) : 8u);
+    for (uint32_t i = 8; i < lim; i++) addr |= (uint64_t)R.u8(x + i) << (8 * (i - 8));
+    return family == 1 || family == 2 ? family : 0u;
+}
+
 template <class A>
 PV_FN void dns_parse(const A &R, uint64_t m, uint32_t len, uint32_t qd, uint32_t an, uint32_t ns,
                           uint32_t ar, DnsInfo &d)
