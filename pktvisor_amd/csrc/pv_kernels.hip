@@ -476,10 +476,8 @@ __device__ __forceinline__ uint32_t dns_port(uint32_t pw)
 }
 template <class A>
 __device__ __forceinline__ DnsMsg dns_msg_of(PV_CREF(PvParams) P, const A &R, const Parsed &o, uint64_t i, uint32_t port,
-                                             bool with_key = true)
+                                             uint32_t period, bool upd, bool with_key = true)
 {
-    const uint32_t period = P.n_dshift ? dperiod_of(P, o.sec) : 0u;
-    const bool upd = period >= P.dskip_before;
     DnsMsg d;
     d.idx = (uint32_t)i;
     d.moff = (uint32_t)(o.l4off + 8);
@@ -774,7 +772,7 @@ struct NetK {
     PV_G uint64_t *iplog;
     PV_G uint64_t *dq;
     PV_G uint32_t *flags;
-    uint32_t n_shift, skip_before, slot0, net_groups, dbg, net_filter_all;
+    uint32_t n_shift, skip_before, slot0, net_groups, dbg, net_filter_all, n_dshift, dskip_before;
 };
 // Net v1 counters of one record straight to HBM (a lane whose slot is not the wave's
 // register slot: records of a 64-record tile that holds a period shift)
@@ -882,10 +880,19 @@ struct NetWave {
     uint32_t lo[PV_NL_OROWS][PV_WT]; // each lane's record start
     uint32_t hi[PV_NL_OROWS][PV_WT]; // each lane's record end (the next start)
 };
+// the batch's period tables, staged in LDS: lanes that need a per-record period (a tile that
+// holds a shift, a DNS message's DNS period) read them with LDS loads; a per-lane load from
+// the parameter block would be a vector load whose wait also drains the tiles in flight
+struct PeriodTab {
+    uint64_t pstart[PV_MAX_SHIFTS];
+    int64_t dthresh[PV_MAX_SHIFTS];
+    uint32_t slot[PV_MAX_SHIFTS + 1];
+};
 struct NetState {
     NetWave w[4];
     uint32_t hist[PV_HBINS];
     uint32_t nd; // DNS messages found
+    PeriodTab pt;
 };
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
@@ -1046,7 +1053,8 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
     if (o.l4 == 17 && !(K.dbg & 4)) {
         const uint32_t port = dns_port(R.u32(o.l4off));
         if (port) {
-            so.dm = msg_words(dns_msg_of(P, R, o, i, port, true));
+            const uint32_t dp = P.n_dshift ? dperiod_of(P, o.sec) : 0u;
+            so.dm = msg_words(dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, true));
             so.isdns = 1;
         }
     }
@@ -1068,12 +1076,18 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x == 0) S.nd = 0;
+    if (threadIdx.x < PV_MAX_SHIFTS) {
+        S.pt.pstart[threadIdx.x] = P.pstart[threadIdx.x];
+        S.pt.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+    }
+    if (threadIdx.x <= PV_MAX_SHIFTS) S.pt.slot[threadIdx.x] = P.slot_of[threadIdx.x];
     __syncthreads();
     NetK K;
     K.recs = P.recs; K.offs = P.offs; K.n = P.n; K.rec_bytes = P.rec_bytes; K.gbase = P.gbase;
     K.sum = P.sum; K.cpc = P.cpc; K.iplog = P.iplog; K.dq = P.dq; K.flags = P.flags;
     K.n_shift = P.n_shift; K.skip_before = P.skip_before; K.slot0 = P.slot_of[0];
     K.net_groups = P.net_groups; K.dbg = P.dbg; K.net_filter_all = P.net_filter_all;
+    K.n_dshift = P.n_dshift; K.dskip_before = P.dskip_before;
     const ParseCfg C = parse_cfg(P);
     const uint64_t n = K.n, last = n - 1;
     const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
@@ -1153,9 +1167,13 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         }
         const uint64_t i = r0 + lane;
         const bool active = i <= r1;
-        const uint32_t lp = straddle ? period(min(i, r1)) : p_lo;
+        uint32_t lp = p_lo, slot = tslot;
+        if (straddle) {
+            lp = 0;
+            for (uint32_t q = 0; q < K.n_shift; q++) lp += i >= S.pt.pstart[q];
+            slot = S.pt.slot[lp];
+        }
         const bool upd = lp >= K.skip_before;
-        const uint32_t slot = straddle ? slot_of(lp) : tslot;
         const bool own = slot == wslot;
         const uint64_t off = NW.lo[row][lane];
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
@@ -1230,7 +1248,9 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
             if (!(K.dbg & 2) && fast && o.l4 == 17 && !(K.dbg & 4)) {
                 const uint32_t port = dns_port(rw.at(50));
                 if (port) {
-                    DnsMsg d = dns_msg_of(P, R, o, i, port, false);
+                    uint32_t dp = 0;
+                    for (uint32_t q = 0; q < K.n_dshift; q++) dp += (int64_t)o.sec >= S.pt.dthresh[q];
+                    DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= K.dskip_before, false);
                     d.fkey = fast_flowkey(rw);
                     dm = msg_words(d);
                     isdns = true;
