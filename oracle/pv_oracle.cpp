@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <list>
 #include <map>
 #include <memory>
 #include <string>
@@ -429,6 +430,8 @@ struct Pkt {
     bool has_v4 = false, has_v6 = false;
     const uint8_t *v4hdr = nullptr; // first IPv4 layer header
     const uint8_t *v6hdr = nullptr; // first IPv6 layer header
+    const uint8_t *ip1 = nullptr;   // first IP layer of either version (getLayerOfType<IPLayer>)
+    bool ip1_v6 = false;
     const uint8_t *l4hdr = nullptr;
     uint32_t l4len = 0; // L4 layer data length (incl. L4 header), IP-length trimmed
     bool syn = false;
@@ -455,6 +458,7 @@ static void parse_l4(Pkt &p, int proto, const uint8_t *d, size_t len)
 static void parse_ipv4(Pkt &p, const uint8_t *d, size_t len, int depth)
 {
     if (!p.has_v4) { p.has_v4 = true; p.v4hdr = d; }
+    if (!p.ip1) { p.ip1 = d; p.ip1_v6 = false; }
     size_t total = rd16be(d + 2);
     if (total < len && total != 0) len = total; // IPv4Layer ctor trims to totalLength
     size_t hl = (size_t)(d[0] & 0x0f) * 4;
@@ -471,6 +475,7 @@ static void parse_ipv4(Pkt &p, const uint8_t *d, size_t len, int depth)
 static void parse_ipv6(Pkt &p, const uint8_t *d, size_t len, int depth)
 {
     if (!p.has_v6) { p.has_v6 = true; p.v6hdr = d; }
+    if (!p.ip1) { p.ip1 = d; p.ip1_v6 = true; }
     // IPv6Layer::parseExtensions
     uint8_t next = d[6];
     size_t off = 40;
@@ -1000,11 +1005,33 @@ struct Engine {
         if (is_dns(dport)) metric_port = sport;
         else if (is_dns(sport)) metric_port = dport;
         if (!metric_port) return;
-        DnsMsg m{p.l4hdr + 8, p.l4len - 8};
+        DnsEv e;
+        e.msg = p.l4hdr + 8; e.len = p.l4len - 8; e.cap_end = p.data + p.caplen;
+        e.ts = p.ts; e.l3 = p.l3; e.dir = p.dir; e.flowkey = flowkey; e.port = metric_port; e.tcp = false;
+        dns_event(e);
+    }
+
+    // One DNS message into the handler: a UDP payload, or a message the DnsTcpSessionData
+    // framing cut from a reassembled TCP stream (dns/v1 ...cpp:406-429)
+    struct DnsEv {
+        const uint8_t *msg, *cap_end;
+        size_t len;
+        TS ts;
+        int l3;
+        Dir dir;
+        uint32_t flowkey;
+        uint16_t port;
+        bool tcp;
+    };
+    void dns_event(const DnsEv &p)
+    {
+        const uint32_t flowkey = p.flowkey;
+        const uint16_t metric_port = p.port;
+        DnsMsg m{p.msg, p.len};
         // A DNS message shorter than the 12-byte header is read past its end by
         // the reference (UB); we read the bytes that follow inside the capture, else 0.
         uint8_t hdr_buf[12];
-        const uint8_t *cap_end = p.data + p.caplen;
+        const uint8_t *cap_end = p.cap_end;
         for (int i = 0; i < 12; i++) hdr_buf[i] = (m.d + i < cap_end) ? m.d[i] : 0;
         DnsMsg hm = m;
         std::vector<uint8_t> tmp;
@@ -1020,17 +1047,21 @@ struct Engine {
 
         // only_rcode installs a UDP predicate in the input proxy (dns/v1 ...cpp:485-508): a
         // non-response or a response whose rcode is not listed never reaches the handler
-        if (cfg.only_rcode_mask && !cfg.exclude_noerror && (!qr || !((cfg.only_rcode_mask >> rcode) & 1))) return;
+        // A TCP message takes no predicate: _filtering applies only_rcode and only_qname as
+        // ordinary filters there (_predicate_filter_type stays FiltersMAX, :546-551,593-602)
+        if (!p.tcp && cfg.only_rcode_mask && !cfg.exclude_noerror && (!qr || !((cfg.only_rcode_mask >> rcode) & 1))) return;
         // only_qname's predicate (:509-524): parse failure or no query never matches a listed name
-        if (!cfg.only_qname.empty()) {
+        auto qname_listed = [&]() {
             DnsParse qp = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{hdr_buf, m.len});
-            if (!qp.ok || !qp.has_query) return;
-            if (std::find(cfg.only_qname.begin(), cfg.only_qname.end(), lower(qp.name)) == cfg.only_qname.end()) return;
-        }
+            if (!qp.ok || !qp.has_query) return false;
+            return std::find(cfg.only_qname.begin(), cfg.only_qname.end(), lower(qp.name)) != cfg.only_qname.end();
+        };
+        if (!p.tcp && !cfg.only_qname.empty() && !qname_listed()) return;
         // DnsStreamHandler::_filtering (:538-648) in its order; a filtered packet is
         // process_filtered: an event without a sample of its own and the `filtered` counter
         bool filt = false;
         if (cfg.exclude_noerror && rcode == 0) filt = true;
+        else if (p.tcp && cfg.only_rcode_mask && !cfg.exclude_noerror && !((cfg.only_rcode_mask >> rcode) & 1)) filt = true;
         else if (cfg.has_answer_count && ancount != cfg.answer_count) filt = true;
         else if (cfg.only_queries && qr) filt = true;
         else if (cfg.only_responses && !qr) filt = true;
@@ -1040,6 +1071,7 @@ struct Engine {
             if (!fr.ok || !fr.has_query) filt = true;
             else if (std::find(cfg.only_qtype.begin(), cfg.only_qtype.end(), fr.qtype) == cfg.only_qtype.end()) filt = true;
         }
+        else if (p.tcp && !cfg.only_qname.empty() && !qname_listed()) filt = true;
         // only_qname_suffix (:615-630): the first listed suffix the name ends with sets suffix_size
         size_t suffix_size = 0;
         if (!filt && !cfg.only_qname_suffix.empty()) {
@@ -1073,7 +1105,8 @@ struct Engine {
             b.total++;
             if (p.l3 == L3_IPV6) b.IPv6++;
             else if (p.l3 == L3_IPV4) b.IPv4++;
-            b.UDP++;
+            if (p.tcp) b.TCP++;
+            else b.UDP++;
             if (qr) {
                 b.replies++;
                 if (rcode == 0) { b.NOERROR++; if (!ancount) b.NODATA++; }
@@ -1159,14 +1192,14 @@ struct Engine {
     }
 
     // DnsMetricsBucket::new_dns_transaction (:1093-1138)
-    void new_xact(DnsBucket &b, const Pkt &p, TS d, const Xact &x, const DnsParse &r)
+    void new_xact(DnsBucket &b, const DnsEv &p, TS d, const Xact &x, const DnsParse &r)
     {
         uint64_t us = (uint64_t)((d.sec * 1000000000LL) + d.nsec) / 1000;
         const bool q = cfg.dns_groups & DG_QUANTILES, h = cfg.dns_groups & DG_HISTOGRAMS;
         b.xacts_total++;
         if (p.dir == DIR_TO_HOST) { b.xacts_out++; if (q) b.xact_from.update(us); if (h) b.hist_from.update(us); }
         else if (p.dir == DIR_FROM_HOST) { b.xacts_in++; if (q) b.xact_to.update(us); if (h) b.hist_to.update(us); }
-        size_t resp_len = p.l4len - 8;
+        size_t resp_len = p.len;
         if (x.query_size) b.ratio.update((double)resp_len / (double)x.query_size);
         if (r.ok && r.has_query) {
             if (p.dir == DIR_TO_HOST && from90 > 0 && (float)us >= from90) b.slow_out.update(r.name);
@@ -1188,13 +1221,307 @@ struct Engine {
         if (!b1.xact_to.empty()) to90 = (float)b1.xact_to.p(0.90);
     }
 
+    // ------------------------------------------------------------ DNS over TCP
+    // PcapPlusPlus 23.09 TcpReassembly (third-party, not vendored in the reference; its
+    // algorithm restated here) as PcapInputStream drives it (PcapInputStream.cpp:75-79,
+    // 254-283, 429-465): config removeConnInfo, closedConnectionDelay 1 s, maxOutOfOrder 50.
+    // A closed connection's info is purged by wall clock (time(nullptr)), which a replay
+    // cannot reproduce; here a closed flow stays closed for the rest of the run.
+    struct TcpFrag {
+        uint32_t seq;
+        std::vector<uint8_t> data;
+    };
+    struct TcpSide {
+        uint8_t ip[16] = {0};
+        bool v6 = false;
+        uint16_t port = 0;
+        uint32_t seq = 0;
+        bool fin = false; // gotFinOrRst
+        std::vector<TcpFrag> frags;
+    };
+    struct DnsTcpSession { // DnsTcpSessionData (dns/v1/DnsStreamHandler.cpp:337-373)
+        std::vector<uint8_t> buf;
+        bool invalid = false;
+    };
+    struct TcpConn {
+        TcpSide side[2];
+        int nsides = 0, prev = -1;
+        bool closed = false;
+        TS end;                 // ConnectionData::endTime (timeval precision), {0,0} until a 2nd packet
+        uint16_t sport = 0, dport = 0;
+        bool v4 = true;
+        // DnsStreamHandler::_tcp_connections entry (TcpFlowData)
+        bool tracked = false;
+        uint16_t port = 0;
+        std::unique_ptr<DnsTcpSession> sess[2];
+    };
+    static constexpr size_t MIN_DNS_QUERY_SIZE = 17;
+    static constexpr size_t TCP_MAX_OOO = 50;
+    static constexpr int64_t TCP_TIMEOUT = 30;       // PcapInputStream.h:97
+    static constexpr int MAX_TCP_CLEANUPS = 100;     // PcapInputStream.h:98
+    static constexpr size_t LRU_SIZE = 30 * 10000;   // DEFAULT_LRULIST_SIZE
+    std::unordered_map<uint32_t, TcpConn> tcp_conns;
+    std::list<std::pair<uint32_t, TS>> lru; // VisorLRUList: front = most recently put
+    std::unordered_map<uint32_t, std::list<std::pair<uint32_t, TS>>::iterator> lru_at;
+    std::vector<uint32_t> lru_overflow;
+    Dir tcp_dir = DIR_UNKNOWN; // _packet_dir_cache of the packet being reassembled
+    bool ooo_busy = false;     // m_ProcessingOutOfOrder
+
+    static bool seq_lt(uint32_t a, uint32_t b) { return (int32_t)(a - b) < 0; }
+    static bool seq_gt(uint32_t a, uint32_t b) { return (int32_t)(b - a) < 0; }
+    static bool is_dns_port(uint16_t x) { return x == 53 || x == 5353 || x == 5355 || x == 53000; }
+
+    void lru_put(uint32_t fk, TS t)
+    {
+        auto it = lru_at.find(fk);
+        if (it != lru_at.end()) lru.erase(it->second);
+        lru.emplace_front(fk, t);
+        lru_at[fk] = lru.begin();
+        if (lru_at.size() > LRU_SIZE) {
+            uint32_t old = lru.back().first;
+            lru_at.erase(old);
+            lru.pop_back();
+            lru_overflow.push_back(old);
+        }
+    }
+    void lru_erase(uint32_t fk)
+    {
+        auto it = lru_at.find(fk);
+        if (it == lru_at.end()) return;
+        lru.erase(it->second);
+        lru_at.erase(it);
+    }
+
+    // DnsStreamHandler::tcp_connection_start_cb (:438-455) / tcp_connection_end_cb (:457-469)
+    void conn_track(TcpConn &c)
+    {
+        uint16_t mp = is_dns_port(c.dport) ? c.sport : (is_dns_port(c.sport) ? c.dport : 0);
+        if (!c.tracked && mp) { c.tracked = true; c.port = mp; }
+    }
+    void conn_untrack(TcpConn &c)
+    {
+        c.tracked = false;
+        c.sess[0].reset();
+        c.sess[1].reset();
+    }
+
+    // onMessageReady -> PcapInputStream::tcp_message_ready (PcapInputStream.cpp:254-263) ->
+    // DnsStreamHandler::tcp_message_ready_cb (:375-436) -> DnsTcpSessionData framing
+    void tcp_deliver(uint32_t fk, TcpConn &c, int side, const uint8_t *d, size_t n)
+    {
+        conn_track(c);
+        if (c.tracked) {
+            if (!c.sess[side]) c.sess[side].reset(new DnsTcpSession());
+            DnsTcpSession &s = *c.sess[side];
+            if (!s.invalid) {
+                s.buf.insert(s.buf.end(), d, d + n);
+                size_t pos = 0;
+                for (;;) {
+                    if (s.buf.size() - pos < MIN_DNS_QUERY_SIZE + 2) break;
+                    size_t size = ((size_t)s.buf[pos] << 8) | s.buf[pos + 1];
+                    if (size < MIN_DNS_QUERY_SIZE) { s.buf.clear(); pos = 0; s.invalid = true; break; }
+                    if (s.buf.size() - pos < 2 + size) break;
+                    std::vector<uint8_t> msg(s.buf.begin() + pos + 2, s.buf.begin() + pos + 2 + size);
+                    pos += 2 + size;
+                    DnsEv e;
+                    e.msg = msg.data(); e.len = size; e.cap_end = msg.data() + size;
+                    e.ts = c.end; e.l3 = c.v4 ? L3_IPV4 : L3_IPV6; e.dir = tcp_dir;
+                    e.flowkey = fk; e.port = c.port; e.tcp = true;
+                    dns_event(e);
+                }
+                if (pos) s.buf.erase(s.buf.begin(), s.buf.begin() + pos);
+            }
+        }
+        lru_put(fk, c.end);
+    }
+
+    // TcpReassembly::checkOutOfOrderFragments
+    void tcp_check_ooo(uint32_t fk, TcpConn &c, int side, bool clean)
+    {
+        if (ooo_busy) return;
+        ooo_busy = true;
+        TcpSide &s = c.side[side];
+        bool found;
+        do {
+            do {
+                found = false;
+                size_t i = 0;
+                while (i < s.frags.size()) {
+                    TcpFrag &f = s.frags[i];
+                    if (f.seq == s.seq) {
+                        s.seq += (uint32_t)f.data.size();
+                        std::vector<uint8_t> d = std::move(f.data);
+                        s.frags.erase(s.frags.begin() + i);
+                        tcp_deliver(fk, c, side, d.data(), d.size());
+                        found = true;
+                        continue;
+                    }
+                    if (seq_lt(f.seq, s.seq)) {
+                        uint32_t nseq = f.seq + (uint32_t)f.data.size();
+                        std::vector<uint8_t> d = std::move(f.data);
+                        s.frags.erase(s.frags.begin() + i);
+                        if (seq_gt(nseq, s.seq)) {
+                            uint32_t nl = s.seq - (nseq - (uint32_t)d.size());
+                            s.seq += (uint32_t)d.size() - nl;
+                            tcp_deliver(fk, c, side, d.data() + nl, d.size() - nl);
+                            found = true;
+                        }
+                        continue;
+                    }
+                    i++;
+                }
+            } while (found);
+            if (!clean && s.frags.size() <= TCP_MAX_OOO) break;
+            // missing data: deliver the fragment with the lowest sequence behind a
+            // "[N bytes missing]" text, then start over
+            int best = -1;
+            uint32_t closest = 0xffffffffu;
+            for (size_t i = 0; i < s.frags.size(); i++)
+                if (best < 0 || seq_lt(s.frags[i].seq, closest)) { closest = s.frags[i].seq; best = (int)i; }
+            if (best >= 0) {
+                TcpFrag f = std::move(s.frags[best]);
+                s.frags.erase(s.frags.begin() + best);
+                uint32_t missing = f.seq - s.seq;
+                s.seq = f.seq + (uint32_t)f.data.size();
+                std::string text = "[" + std::to_string(missing) + " bytes missing]";
+                std::vector<uint8_t> d(text.begin(), text.end());
+                d.insert(d.end(), f.data.begin(), f.data.end());
+                tcp_deliver(fk, c, side, d.data(), d.size());
+                found = true;
+            }
+        } while (found);
+        ooo_busy = false;
+    }
+
+    // TcpReassembly::closeConnectionInternal
+    void tcp_close(uint32_t fk)
+    {
+        auto it = tcp_conns.find(fk);
+        if (it == tcp_conns.end() || it->second.closed) return;
+        TcpConn &c = it->second;
+        tcp_check_ooo(fk, c, 0, true);
+        tcp_check_ooo(fk, c, 1, true);
+        conn_untrack(c);  // onConnectionEnd -> tcp_connection_end
+        lru_erase(fk);
+        c.closed = true;
+    }
+
+    // TcpReassembly::handleFinOrRst
+    void tcp_fin_rst(uint32_t fk, TcpConn &c, int side, bool rst)
+    {
+        if (c.side[side].fin) return;
+        c.side[side].fin = true;
+        if (c.side[1 - side].fin || rst) tcp_close(fk);
+        else tcp_check_ooo(fk, c, side, true);
+    }
+
+    // TcpReassembly::reassemblePacket
+    void tcp_reassemble(const Pkt &p)
+    {
+        if (!p.ip1) return;                          // NonIpPacket
+        const uint8_t *th = p.l4hdr;
+        size_t hl = (size_t)(th[12] >> 4) * 4;
+        if (hl < 20 || hl > p.l4len) return;         // no TcpLayer (TcpLayer::isDataValid)
+        const uint8_t *pl = th + hl;
+        const uint32_t plen = (uint32_t)(p.l4len - hl);
+        const bool syn = th[13] & 0x02, fin = th[13] & 0x01, rst = th[13] & 0x04;
+        if (plen == 0 && !syn && !fin && !rst) return; // Ignore_PacketWithNoData
+        const uint32_t fk = hash5tuple(p);
+        const uint16_t sport = rd16be(th), dport = rd16be(th + 2);
+        const uint8_t *src = p.ip1 + (p.ip1_v6 ? 8 : 12);
+        const size_t alen = p.ip1_v6 ? 16 : 4;
+        TS now{p.ts.sec, p.ts.nsec / 1000 * 1000}; // timespec -> ConnectionData timeval
+        auto it = tcp_conns.find(fk);
+        TcpConn *cp;
+        if (it == tcp_conns.end()) {
+            cp = &tcp_conns[fk];
+            cp->sport = sport; cp->dport = dport; cp->v4 = !p.ip1_v6;
+            // onConnectionStart -> tcp_connection_start (PcapInputStream.cpp:265-274)
+            conn_track(*cp);
+            lru_put(fk, now);
+        } else {
+            cp = &it->second;
+            if (cp->closed) return;                  // Ignore_PacketOfClosedFlow
+            if (now.sec > cp->end.sec || (now.sec == cp->end.sec && now.nsec > cp->end.nsec)) cp->end = now;
+        }
+        TcpConn &c = *cp;
+        int side = -1;
+        bool first = false;
+        auto is_side = [&](int k) {
+            return c.side[k].port == sport && c.side[k].v6 == p.ip1_v6 && !memcmp(c.side[k].ip, src, alen);
+        };
+        if (c.nsides < 2 && !(c.nsides == 1 && is_side(0))) {
+            side = c.nsides++;
+            memcpy(c.side[side].ip, src, alen);
+            c.side[side].v6 = p.ip1_v6;
+            c.side[side].port = sport;
+            first = true;
+        } else if (is_side(0)) side = 0;
+        else if (c.nsides == 2 && is_side(1)) side = 1;
+        else return;                                 // Error_PacketDoesNotMatchFlow
+        TcpSide &s = c.side[side];
+        if (s.fin) return;
+        if ((fin || rst) && plen == 0) { tcp_fin_rst(fk, c, side, rst); return; }
+        if (c.prev != -1 && c.prev != side) tcp_check_ooo(fk, c, c.prev, true);
+        c.prev = side;
+        const uint32_t seq = ((uint32_t)th[4] << 24) | ((uint32_t)th[5] << 16) | ((uint32_t)th[6] << 8) | th[7];
+        if (first) {
+            s.seq = seq + plen + (syn ? 1 : 0);
+            if (plen) tcp_deliver(fk, c, side, pl, plen);
+        } else if (seq_lt(seq, s.seq)) {
+            uint32_t nseq = seq + plen;
+            if (seq_gt(nseq, s.seq)) {
+                uint32_t nl = s.seq - seq;
+                s.seq += plen - nl;
+                tcp_deliver(fk, c, side, pl + nl, plen - nl);
+            }
+        } else if (seq == s.seq) {
+            if (plen) {
+                s.seq += plen + (syn ? 1 : 0);
+                tcp_deliver(fk, c, side, pl, plen);
+                tcp_check_ooo(fk, c, side, false);
+            }
+        } else if (plen) {
+            s.frags.push_back(TcpFrag{seq, std::vector<uint8_t>(pl, pl + plen)});
+            if (s.frags.size() > TCP_MAX_OOO) tcp_check_ooo(fk, c, side, true);
+        }
+        if (fin || rst) tcp_fin_rst(fk, c, side, rst);
+    }
+
+    // PcapInputStream::process_raw_packet, TCP branch (PcapInputStream.cpp:429-465)
+    void tcp_packet(const Pkt &p)
+    {
+        tcp_reassemble(p);
+        for (int k = 0; k < MAX_TCP_CLEANUPS && !lru.empty(); k++) {
+            auto back = lru.back();
+            if (p.ts.sec < back.second.sec + TCP_TIMEOUT) break;
+            tcp_close(back.first);
+            lru_erase(back.first);
+        }
+        // indexed: a close can flush data whose LRU put overflows again
+        for (size_t k = 0; k < lru_overflow.size(); k++) tcp_close(lru_overflow[k]);
+        lru_overflow.clear();
+    }
+
+    // TcpReassembly::closeAllConnections at the end of the capture (PcapInputStream.cpp:243-244)
+    void tcp_close_all()
+    {
+        std::vector<uint32_t> keys;
+        for (auto &kv : tcp_conns)
+            if (!kv.second.closed) keys.push_back(kv.first);
+        std::sort(keys.begin(), keys.end());
+        for (uint32_t fk : keys) tcp_close(fk);
+    }
+
     void process(const Pkt &p0)
     {
         Pkt p = p0;
         parse_packet(p, linktype);
         set_direction(p, cfg);
+        tcp_dir = p.dir;
         net_packet(p);
         if (p.l4 == L4_UDP) dns_udp_packet(p, hash5tuple(p));
+        else if (p.l4 == L4_TCP) tcp_packet(p);
     }
 };
 
@@ -1532,6 +1859,7 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
         last = pk.ts;
     }
     if (!first) e.end(last);
+    e.tcp_close_all(); // after end_tstamp_cb (PcapInputStream.cpp:514-522)
     J j;
     j.obj();
     unsigned w = c.window <= 1 ? 1 : c.window;

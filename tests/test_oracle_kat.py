@@ -10,14 +10,16 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 KAT = json.load(open(os.path.join(GOLD, "kat_reference.json")))["cases"]
 
 
-@pytest.mark.parametrize("case", KAT, ids=[c["fixture"] for c in KAT])
+@pytest.mark.parametrize("case", KAT, ids=[c["fixture"] + str(i) for i, c in enumerate(KAT)])
 def test_oracle_matches_reference_kats(oracle, case):
     out = oracle.run_file(os.path.join(GOLD, case["fixture"]), host_spec=case["host_spec"],
-                          num_periods=case["periods"], window=case["periods"])
+                          num_periods=case["periods"], window=case["periods"], **case.get("cfg", {}))
     for path, want in case["checks"]:
         assert jget(out, path) == want, (case["cite"], path)
     for path, lo in case.get("ge", []):
         assert jget(out, path) >= lo, (case["cite"], path)
+    for path, n in case.get("len", []):
+        assert len(jget(out, path)) == n, (case["cite"], path)
 
 
 def test_readme_sample_shape(oracle):
