@@ -1265,6 +1265,8 @@ struct Engine {
     std::unordered_map<uint32_t, std::list<std::pair<uint32_t, TS>>::iterator> lru_at;
     std::vector<uint32_t> lru_overflow;
     Dir tcp_dir = DIR_UNKNOWN; // _packet_dir_cache of the packet being reassembled
+    uint64_t rec_no = 0;       // records seen (debug log of TCP messages: PVO_TCP_LOG)
+    FILE *tcp_log = nullptr;
     bool ooo_busy = false;     // m_ProcessingOutOfOrder
 
     static bool seq_lt(uint32_t a, uint32_t b) { return (int32_t)(a - b) < 0; }
@@ -1323,6 +1325,8 @@ struct Engine {
                     if (s.buf.size() - pos < 2 + size) break;
                     std::vector<uint8_t> msg(s.buf.begin() + pos + 2, s.buf.begin() + pos + 2 + size);
                     pos += 2 + size;
+                    if (tcp_log) fprintf(tcp_log, "%llu %u %u %lld %lld\n", (unsigned long long)rec_no, (unsigned)size,
+                                         (unsigned)((msg[0] << 8) | msg[1]), (long long)c.end.sec, (long long)c.end.nsec);
                     DnsEv e;
                     e.msg = msg.data(); e.len = size; e.cap_end = msg.data() + size;
                     e.ts = c.end; e.l3 = c.v4 ? L3_IPV4 : L3_IPV6; e.dir = tcp_dir;
@@ -1522,6 +1526,7 @@ struct Engine {
         net_packet(p);
         if (p.l4 == L4_UDP) dns_udp_packet(p, hash5tuple(p));
         else if (p.l4 == L4_TCP) tcp_packet(p);
+        rec_no++;
     }
 };
 
@@ -1849,6 +1854,7 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
     if (!f.open(file, len, err)) { *out = strdup(err.c_str()); return -2; }
     Engine e(c);
     e.linktype = f.linktype;
+    if (const char *lp = getenv("PVO_TCP_LOG")) e.tcp_log = fopen(lp, "w");
     topn_pct = c.topn_pct;
     Pkt pk;
     TS last;
@@ -1860,6 +1866,7 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
     }
     if (!first) e.end(last);
     e.tcp_close_all(); // after end_tstamp_cb (PcapInputStream.cpp:514-522)
+    if (e.tcp_log) fclose(e.tcp_log);
     J j;
     j.obj();
     unsigned w = c.window <= 1 ? 1 : c.window;

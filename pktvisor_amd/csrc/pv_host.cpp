@@ -90,11 +90,21 @@ extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, con
                                            uint32_t at);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
                                           uint32_t *vout, size_t n, hipStream_t s);
+extern "C" __global__ void pv_dns_tcp(const PvParams *P);
+extern "C" __global__ void pv_tcp_keys(const PvTcpSeg *seg, uint32_t n, uint64_t *key, uint32_t *val);
+extern "C" __global__ void pv_tcp_scan(const PvTcpParams *T);
+extern "C" __global__ void pv_tcp_lookup(const PvTcpParams *T);
+extern "C" __global__ void pv_tcp_insert(const PvTcpParams *T);
+extern "C" __global__ void pv_tcp_flow(const PvTcpParams *T);
+extern "C" __global__ void pv_tcp_migrate(const PvTcpParams *T);
+extern "C" hipError_t pv_tcp_sort(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin, uint32_t *vout,
+                                  size_t n, hipStream_t s);
 
 namespace {
 
 // status words (device): flags, n_events, n_resp, n_vals, DNS messages, new top-N names
-enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNEW = 5, ST_WORDS = 6 };
+enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNEW = 5, ST_TSEG = 6, ST_TSEG_BYTES = 7,
+       ST_WORDS = 8 };
 // after the status words (one allocation, zeroed per batch up to the live region count):
 // per-region update counts, then offsets and fill pointers
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
@@ -379,6 +389,41 @@ struct pv_ctx {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     double kernel_ms = 0;
     uint64_t kernel_launches = 0;
+    // DNS over TCP (pv_tcp.hip): segments emitted per batch, the TCP record tile masks and
+    // their prefix maxima; the stage's buffers (allocated on first use), the flow table and
+    // the double-buffered carry arena with its carried-flow lists
+    PvTcpSeg *d_tseg = nullptr;
+    uint32_t tseg_cap = 0;
+    uint64_t *d_tmask = nullptr;
+    uint32_t *d_tpm = nullptr;
+    uint32_t *d_tcpcnt = nullptr, *h_tcpcnt = nullptr; // PVT_WORDS, then the LT carry word
+    PvTcpParams *d_tparams = nullptr, *h_tparams = nullptr;
+    bool tcp_alloced = false;
+    uint64_t *d_tkey[2] = {nullptr, nullptr};
+    uint32_t *d_tval[2] = {nullptr, nullptr};
+    uint32_t *d_run_flow = nullptr;
+    void *d_tsort_tmp = nullptr;
+    size_t tsort_tmp_bytes = 0;
+    PvTcpFlow *d_flows = nullptr;
+    uint32_t flow_cap_log2 = 18;
+    uint8_t *d_carry[2] = {nullptr, nullptr};
+    uint64_t carry_cap[2] = {0, 0};
+    uint32_t *d_clist[2] = {nullptr, nullptr};
+    uint32_t carry_cur = 0, n_clist = 0;
+    uint64_t carry_used = 0;
+    PvTcpFrag *d_frags = nullptr;
+    uint32_t frag_cap = 0;
+    uint8_t *d_marena = nullptr;
+    uint64_t marena_cap = 0;
+    uint32_t *d_moffs = nullptr;
+    uint64_t *d_tmq = nullptr; // 32-B DnsMsg items
+    uint8_t *d_tsfx = nullptr;
+    uint32_t tmsg_cap = 0;
+    uint32_t tcp_stage = 0;   // stage ordinal (flow entries remember the last one that touched them)
+    bool tcp_active = false;  // a stage has run since the last reset
+    bool tcp_pre = false;     // this batch's stage runs ahead of the Net pass (prescan emits)
+    uint32_t tcp_nmsg = 0;    // messages of the current batch
+    std::vector<std::pair<uint64_t, int64_t>> tcp_ords; // (ord, second) of the batch's messages, by ord
 
     int fail(int code, const char *fmt, ...)
     {
@@ -1125,7 +1170,12 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     // event / DNS work-list regions: main workgroups own wt_per_block * 64 slots each (the
     // last may overhang the batch by < wt_per_block tiles), boundary workgroups 64 each
     // (the last workgroup's region may overhang the batch by < wt_per_block tiles)
-    const uint64_t ev_cap = mr + mr / ((uint64_t)c->wg_per_cu * c->cus) + 64 * 64 + 16 * 256;
+    // DNS over TCP messages of one batch (pv_dns_tcp appends their events behind the UDP
+    // regions: one more region of slack)
+    c->tmsg_cap = (uint32_t)std::min<uint64_t>(mr + 65536, 0x7fffffffull);
+    c->tseg_cap = (uint32_t)std::min<uint64_t>(mr + 64, 0xffffffffull);
+    const uint64_t region_max = mr / ((uint64_t)c->wg_per_cu * c->cus) + 64 * 64;
+    const uint64_t ev_cap = mr + region_max + 64 * 64 + 16 * 256 + c->tmsg_cap + 2 * region_max;
     c->pend_cap = 2 * mr; // open queries carried between batches
     c->orph_cap = (uint32_t)std::min<uint64_t>(2 * mr, 1u << 30);
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
@@ -1150,10 +1200,10 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_pend[1], (size_t)(c->pend_cap + mr) * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_pkeys[0], (size_t)(c->pend_cap + mr) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_pkeys[1], (size_t)(c->pend_cap + mr) * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)(mr + c->pend_cap) * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)(mr + c->pend_cap) * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_svals, (size_t)(mr + c->pend_cap) * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)(mr + c->pend_cap) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_svals, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
@@ -1162,18 +1212,25 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_iplog, (size_t)(mr + 64) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_trash, (size_t)PV_TRASH_WAVES * 2048)) ||
         !hip_ok(e = hipMalloc(&c->d_cb_cnt, 65536 * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_params, sizeof(PvParams))) ||
-        !hip_ok(e = hipHostMalloc((void **)&c->h_params, sizeof(PvParams), hipHostMallocDefault)) ||
+        !hip_ok(e = hipMalloc(&c->d_params, 2 * sizeof(PvParams))) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_params, 2 * sizeof(PvParams), hipHostMallocDefault)) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_xparams, sizeof(PvXactParams), hipHostMallocDefault)) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_status, ST_ALLOC * 4, hipHostMallocDefault)) ||
+        !hip_ok(e = hipMalloc(&c->d_tseg, (size_t)c->tseg_cap * sizeof(PvTcpSeg))) ||
+        !hip_ok(e = hipMalloc(&c->d_tmask, (size_t)(mr / 64 + 2) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_tpm, (size_t)(mr / 64 + 2) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_tcpcnt, (PVT_WORDS + 1) * 4)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_tcpcnt, (PVT_WORDS + 1) * 4, hipHostMallocDefault)) ||
+        !hip_ok(e = hipMalloc(&c->d_tparams, sizeof(PvTcpParams))) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_tparams, sizeof(PvTcpParams), hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_xparams, sizeof(PvXactParams))) || !hip_ok(e = hipEventCreate(&c->ev_start)) ||
         !hip_ok(e = hipEventCreate(&c->ev_stop))) {
         *out = c;
         return c->hipfail(e, "device allocation");
     }
     size_t tmp = 0;
-    pv_radix_sort_pairs(nullptr, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, (size_t)(mr + c->pend_cap),
-                        c->stream);
+    pv_radix_sort_pairs(nullptr, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
+                        (size_t)(mr + c->tmsg_cap + c->pend_cap), c->stream);
     c->sort_tmp_bytes = std::max<size_t>(tmp, 256);
     if (!hip_ok(e = hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes))) { *out = c; return c->hipfail(e, "sort scratch"); }
     *out = c;
@@ -1188,10 +1245,14 @@ void pv_destroy(pv_ctx *c)
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
                     c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
-                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx};
+                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx,
+                    c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
+                    c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
+                    c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
-    for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits})
+    for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
+                     (void *)c->h_tparams})
         if (hp) hipHostFree(hp);
     for (auto &st : c->stage) {
         if (st.h_recs) hipHostFree(st.h_recs);
@@ -1227,6 +1288,12 @@ int pv_reset(pv_ctx *c)
     c->pend_base = -1;
     c->dns_shifts.clear();
     launch_fill32(c, c->d_nvals, 4, 0); // with the next batch's slot clears
+    // TCP: no connection, no carried bytes, no TCP record seen
+    launch_fill32(c, c->d_tcpcnt + PVT_WORDS, 1, 0);
+    if (c->d_flows) launch_fill32(c, (uint32_t *)c->d_flows, ((uint64_t)sizeof(PvTcpFlow) / 4) << c->flow_cap_log2, 0);
+    c->n_clist = 0;
+    c->carry_used = 0;
+    c->tcp_active = false;
     return 0;
 }
 
@@ -1279,6 +1346,7 @@ namespace {
 struct Shift {
     int64_t sec;
     uint64_t idx;
+    uint64_t ord; // DNS shifts: position of the shifting event (record * 4, + sub for a TCP message)
 };
 
 // The Net manager's shifts: every packet is a Net event, so the first record with
@@ -1288,7 +1356,7 @@ void net_shifts_of(int64_t T, const pv_index_info *info, const uint32_t *sc_idx,
 {
     for (uint32_t k = 0; k < info->n_sec_changes; k++)
         if ((int64_t)sc_sec[k] >= T) {
-            out.push_back({(int64_t)sc_sec[k], sc_idx[k]});
+            out.push_back({(int64_t)sc_sec[k], sc_idx[k], (uint64_t)sc_idx[k] * 4});
             T = (int64_t)sc_sec[k] + 60;
         }
 }
@@ -1306,21 +1374,47 @@ uint64_t next_bit(const uint64_t *bits, uint64_t from, uint64_t n)
     return n;
 }
 
-// The DNS manager's shifts: the first DNS event (pv_dns_prescan's bits) with ts_sec >=
-// next_shift, then next_shift = its second + 60, repeatedly (monotone batch).
+// The DNS manager's shifts: the first DNS event with ts_sec >= next_shift, then next_shift =
+// its second + 60, repeatedly (monotone batch). DNS events: the UDP datagrams of
+// pv_dns_prescan's bits, and the TCP messages (ord, stamp second) of the batch's TCP stage,
+// whose stamps (a connection's end time) may lag their position.
 void dns_shifts_of(int64_t T, const uint64_t *bits, uint64_t n, const pv_index_info *info, const uint32_t *sc_idx,
-                   const uint32_t *sc_sec, std::vector<Shift> &out)
+                   const uint32_t *sc_sec, const std::vector<std::pair<uint64_t, int64_t>> &tcp, std::vector<Shift> &out)
 {
     const uint32_t nsc = info->n_sec_changes;
     uint32_t k = 0;
+    size_t t = 0;
+    uint64_t after = 0; // events at ord >= after are still candidates
     for (;;) {
+        // UDP: the first event in a second >= T (later than the last shift: times are monotone)
         while (k < nsc && (int64_t)sc_sec[k] < T) k++;
-        if (k == nsc) return;
-        const uint64_t i = next_bit(bits, sc_idx[k], n);
-        if (i >= n) return;
-        while (k + 1 < nsc && sc_idx[k + 1] <= i) k++;
-        out.push_back({(int64_t)sc_sec[k], i});
-        T = (int64_t)sc_sec[k] + 60;
+        uint64_t ui = n, uord = ~0ull;
+        int64_t usec = 0;
+        if (k < nsc) {
+            ui = next_bit(bits, sc_idx[k], n);
+            if (ui < n) {
+                uint32_t kk = k;
+                while (kk + 1 < nsc && sc_idx[kk + 1] <= ui) kk++;
+                usec = (int64_t)sc_sec[kk];
+                uord = ui * 4;
+            }
+        }
+        // TCP: the first message after the last shift whose stamp second is >= T
+        while (t < tcp.size() && tcp[t].first < after) t++;
+        size_t tt = t;
+        while (tt < tcp.size() && tcp[tt].second < T && tcp[tt].first < uord) tt++;
+        const bool tcp_first = tt < tcp.size() && tcp[tt].second >= T && tcp[tt].first < uord;
+        if (tcp_first) {
+            out.push_back({tcp[tt].second, tcp[tt].first / 4, tcp[tt].first});
+            T = tcp[tt].second + 60;
+            after = tcp[tt].first + 1;
+            t = tt + 1;
+            continue;
+        }
+        if (uord == ~0ull) return;
+        out.push_back({usec, ui, uord});
+        T = usec + 60;
+        after = uord + 1;
     }
 }
 
@@ -1348,14 +1442,22 @@ void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t
     P.sfx_of = c->d_sfx;
     for (uint32_t k = 0; k < c->f_nsx; k++) { P.f_sxl[k] = c->f_sxl[k]; P.f_sxh[k] = c->f_sxh[k]; }
     P.dbits = c->d_dbits;
+    P.tseg = c->d_tseg;
+    P.tseg_cap = c->tseg_cap;
+    P.tseg_cnt = c->d_status + ST_TSEG;
+    P.tmask = c->d_tmask;
 }
 
-// pv_dns_prescan over a batch, its bits copied to c->h_dbits (synchronises)
-int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, hipStream_t st)
+// pv_dns_prescan over a batch, its bits copied to c->h_dbits (synchronises); with tcp_emit
+// also the batch's TCP segments and tile masks (their counts into tseg[2])
+int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, hipStream_t st, bool tcp_emit,
+                uint32_t *tseg)
 {
+    launch_fill32(c, c->d_status + ST_TSEG, 2, 0);
     flush_fills(c);
     PvParams P;
     params_common(c, P, d_recs, d_offs, n);
+    P.tcp_emit = tcp_emit ? 1u : 0u;
     hipError_t e;
     *c->h_params = P;
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
@@ -1365,19 +1467,212 @@ int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64
     hipLaunchKernelGGL(pv_dns_prescan, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_dns_prescan");
     if (!hip_ok(e = hipMemcpyAsync(c->h_dbits, c->d_dbits, tiles * 8, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(c->h_status + ST_TSEG, c->d_status + ST_TSEG, 8, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "DNS prescan");
+    tseg[0] = c->h_status[ST_TSEG];
+    tseg[1] = c->h_status[ST_TSEG_BYTES];
     return 0;
+}
+
+// ---- DNS over TCP (pv_tcp.hip)
+int grow_bytes(pv_ctx *c, void **p, uint64_t &cap, uint64_t need, size_t elem, const char *what)
+{
+    if (need <= cap && *p) return 0;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    const uint64_t n = std::max<uint64_t>(need + need / 2, 1u << 16);
+    hipError_t e;
+    if (!hip_ok(e = hipMalloc(p, n * elem))) return c->hipfail(e, what);
+    cap = n;
+    return 0;
+}
+#define PV_GROW(c, p, cap, need, what) grow_bytes(c, (void **)&(p), cap, need, sizeof(*(p)), what)
+
+// the stage's fixed buffers, on the first batch that holds a DNS-port TCP segment
+int tcp_alloc(pv_ctx *c)
+{
+    if (c->tcp_alloced) return 0;
+    hipError_t e;
+    const uint64_t ns = c->tseg_cap, fc = 1ull << c->flow_cap_log2;
+    if (!hip_ok(e = hipMalloc(&c->d_tkey[0], ns * 8)) || !hip_ok(e = hipMalloc(&c->d_tkey[1], ns * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_tval[0], ns * 4)) || !hip_ok(e = hipMalloc(&c->d_tval[1], ns * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_run_flow, ns * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_flows, fc * sizeof(PvTcpFlow))) ||
+        !hip_ok(e = hipMemsetAsync(c->d_flows, 0, fc * sizeof(PvTcpFlow), c->stream)) ||
+        !hip_ok(e = hipMalloc(&c->d_clist[0], fc * 4)) || !hip_ok(e = hipMalloc(&c->d_clist[1], fc * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_moffs, (size_t)c->tmsg_cap * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_tmq, (size_t)c->tmsg_cap * 32)) ||
+        !hip_ok(e = hipMalloc(&c->d_tsfx, (size_t)c->tmsg_cap)))
+        return c->hipfail(e, "TCP stage allocation");
+    size_t tmp = 0;
+    pv_tcp_sort(nullptr, &tmp, c->d_tkey[0], c->d_tkey[1], c->d_tval[0], c->d_tval[1], ns, c->stream);
+    c->tsort_tmp_bytes = std::max<size_t>(tmp, 256);
+    if (!hip_ok(e = hipMalloc(&c->d_tsort_tmp, c->tsort_tmp_bytes))) return c->hipfail(e, "TCP sort scratch");
+    c->tcp_alloced = true;
+    return 0;
+}
+
+// The TCP stage of a batch: its segments (n_seg, seg_bytes payload) through reassembly and
+// framing into message records. d_offs / n: the whole batch. With want_ords the messages'
+// (ord, second) pairs come back for the DNS shift plan.
+int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, uint32_t n_seg, uint64_t seg_bytes,
+              uint32_t now_sec, bool want_ords, hipStream_t st)
+{
+    c->tcp_nmsg = 0;
+    c->tcp_ords.clear();
+    if (n_seg > c->tseg_cap)
+        return c->fail(PV_ECAPACITY, "%u DNS-over-TCP segments in one batch exceed the capacity %u (max_records)", n_seg,
+                       c->tseg_cap);
+    if (n_seg == 0 && !c->tcp_active) return 0;
+    if (int rc = tcp_alloc(c)) return rc;
+    hipError_t e;
+    // bounds of this stage's output: every byte a flow can deliver (payloads, carried bytes,
+    // missing-data texts) lands in at most one message record, reserved at most three times
+    const uint64_t B = seg_bytes + c->carry_used + 32ull * (n_seg + c->carry_used / 8);
+    if (int rc = PV_GROW(c, c->d_marena, c->marena_cap, 3 * B + 44 * (B / 17 + 2ull * n_seg) + 4096 + PV_RECS_PAD, "TCP message arena"))
+        return rc;
+    uint64_t fcap = c->frag_cap;
+    if (int rc = PV_GROW(c, c->d_frags, fcap, n_seg + c->carry_used / 8 + 64, "TCP fragment pool")) return rc;
+    c->frag_cap = (uint32_t)std::min<uint64_t>(fcap, 0xffffffffull);
+    const uint32_t out = c->carry_cur ^ 1;
+    if (int rc = PV_GROW(c, c->d_carry[out], c->carry_cap[out], 2 * B + 8 * (n_seg + c->carry_used / 8) + 4096, "TCP carry arena"))
+        return rc;
+    if (!c->d_carry[c->carry_cur]) {
+        if (int rc = PV_GROW(c, c->d_carry[c->carry_cur], c->carry_cap[c->carry_cur], 4096, "TCP carry arena")) return rc;
+    }
+    c->tcp_stage++;
+    PvTcpParams &T = *c->h_tparams;
+    memset(&T, 0, sizeof T);
+    T.seg = c->d_tseg;
+    T.skey = c->d_tkey[1];
+    T.sval = c->d_tval[1];
+    T.n_seg = n_seg;
+    T.stage = c->tcp_stage;
+    T.now_sec = now_sec;
+    T.flow_cap_log2 = c->flow_cap_log2;
+    T.flows = c->d_flows;
+    T.run_flow = c->d_run_flow;
+    T.tmask = c->d_tmask;
+    T.tpm = c->d_tpm;
+    T.lt_carry = c->d_tcpcnt + PVT_WORDS;
+    T.recs = d_recs;
+    T.offs = d_offs;
+    T.n_tiles = (uint32_t)((n + 63) / 64);
+    T.ts_nano = c->cfg.ts_nano;
+    T.carry_in = c->d_carry[c->carry_cur];
+    T.carry_out = c->d_carry[out];
+    T.carry_cap = c->carry_cap[out];
+    T.clist_in = c->d_clist[c->carry_cur];
+    T.n_clist_in = c->n_clist;
+    T.clist_out = c->d_clist[out];
+    T.frags = c->d_frags;
+    T.frag_cap = c->frag_cap;
+    T.marena = c->d_marena;
+    T.marena_cap = c->marena_cap;
+    T.moffs = c->d_moffs;
+    T.mq = c->d_tmq;
+    T.mq_cap = c->tmsg_cap;
+    T.cnt = c->d_tcpcnt;
+    flush_fills(c);
+    if (!hip_ok(e = hipMemsetAsync(c->d_tcpcnt, 0, PVT_WORDS * 4, st)) ||
+        !hip_ok(e = hipMemcpyAsync(c->d_tparams, c->h_tparams, sizeof T, hipMemcpyHostToDevice, st)))
+        return c->hipfail(e, "TCP stage upload");
+    const PvTcpParams *dT = c->d_tparams;
+    hipLaunchKernelGGL(pv_tcp_scan, dim3(1), dim3(1024), 0, st, dT);
+    if (n_seg) {
+        const uint32_t blocks = (n_seg + 255) / 256;
+        hipLaunchKernelGGL(pv_tcp_keys, dim3(blocks), dim3(256), 0, st, (const PvTcpSeg *)c->d_tseg, n_seg, c->d_tkey[0],
+                           c->d_tval[0]);
+        size_t tmp = c->tsort_tmp_bytes;
+        if (!hip_ok(e = pv_tcp_sort(c->d_tsort_tmp, &tmp, c->d_tkey[0], c->d_tkey[1], c->d_tval[0], c->d_tval[1], n_seg, st)))
+            return c->hipfail(e, "TCP segment sort");
+        hipLaunchKernelGGL(pv_tcp_lookup, dim3(blocks), dim3(256), 0, st, dT);
+        hipLaunchKernelGGL(pv_tcp_insert, dim3(blocks), dim3(256), 0, st, dT);
+        hipLaunchKernelGGL(pv_tcp_flow, dim3(blocks), dim3(256), 0, st, dT);
+        if (c->n_clist) hipLaunchKernelGGL(pv_tcp_migrate, dim3((c->n_clist + 255) / 256), dim3(256), 0, st, dT);
+    }
+    if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch TCP stage");
+    if (!hip_ok(e = hipMemcpyAsync(c->h_tcpcnt, c->d_tcpcnt, PVT_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "TCP stage");
+    c->tcp_active = true;
+    if (!n_seg) return 0; // the TCP record seconds advanced; no flow moved
+    const uint32_t *k = c->h_tcpcnt;
+    if (k[PVT_FLAGS] & PVT_F_TABLE)
+        return c->fail(PV_ECAPACITY, "TCP flow table full (%u entries)", 1u << c->flow_cap_log2);
+    if (k[PVT_FLAGS] & PVT_F_MSGS)
+        return c->fail(PV_ECAPACITY, "more than %u DNS-over-TCP messages in one batch", c->tmsg_cap);
+    if (k[PVT_FLAGS] & (PVT_F_ARENA | PVT_F_CARRY | PVT_F_FRAGS))
+        return c->fail(PV_ECAPACITY, "TCP stage buffer overflow (flags 0x%x)", k[PVT_FLAGS]);
+    c->tcp_nmsg = k[PVT_NMSG];
+    c->n_clist = k[PVT_NCARRY];
+    c->carry_used = k[PVT_CARRY];
+    c->carry_cur = out;
+    if (const char *dp = getenv("PV_TCP_DUMP")) {
+        // debug: the batch's messages as "record sub length txid stamp_sec stamp_nsec"
+        std::vector<uint32_t> items((size_t)c->tcp_nmsg * 8);
+        std::vector<uint8_t> arena(k[PVT_ARENA]);
+        if (c->tcp_nmsg) hipMemcpy(items.data(), c->d_tmq, items.size() * 4, hipMemcpyDeviceToHost);
+        if (!arena.empty()) hipMemcpy(arena.data(), c->d_marena, arena.size(), hipMemcpyDeviceToHost);
+        if (FILE *f = fopen(dp, "a")) {
+            for (uint32_t q = 0; q < c->tcp_nmsg; q++) {
+                const uint32_t *it = &items[(size_t)q * 8];
+                const uint32_t mo = it[1];
+                fprintf(f, "%llu %u %u %u %u %u\n", (unsigned long long)(c->records_seen + it[7] / 4), it[7] & 3, it[2] & 0xffff,
+                        mo + 1 < arena.size() ? (arena[mo] << 8 | arena[mo + 1]) : 0u, it[5], it[6]);
+            }
+            fclose(f);
+        }
+    }
+    if (want_ords && c->tcp_nmsg) {
+        std::vector<uint32_t> items((size_t)c->tcp_nmsg * 8);
+        if (!hip_ok(e = hipMemcpy(items.data(), c->d_tmq, items.size() * 4, hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "TCP message order");
+        c->tcp_ords.resize(c->tcp_nmsg);
+        for (uint32_t q = 0; q < c->tcp_nmsg; q++) c->tcp_ords[q] = {items[(size_t)q * 8 + 7], (int64_t)items[(size_t)q * 8 + 5]};
+        std::sort(c->tcp_ords.begin(), c->tcp_ords.end());
+    }
+    return 0;
+}
+
+// The TCP DNS pass of a span: the batch's messages with ord in [4 * a, 4 * b), events in
+// the workgroup regions behind the span's grid; returns the workgroups it used
+uint32_t tcp_pass(pv_ctx *c, const PvParams &P, uint64_t a, uint64_t b, hipStream_t st, PvParams *d_slot)
+{
+    if (!c->tcp_nmsg) return 0;
+    PvParams Q = P;
+    Q.recs = c->d_marena;
+    Q.offs = c->d_moffs;
+    Q.linktype = 101;
+    Q.dq = c->d_tmq;
+    Q.sfx_of = c->d_tsfx;
+    Q.tcp_pass = 1;
+    Q.tcp_emit = 0;
+    Q.tcp_nmsg = c->tcp_nmsg;
+    Q.ord_lo = (uint32_t)(a * 4);
+    Q.ord_hi = (uint32_t)std::min<uint64_t>(b * 4, 0xffffffffull);
+    Q.ord_base = (uint32_t)(a * 4);
+    const uint64_t region = (uint64_t)P.wt_per_block * 64;
+    const uint32_t gt = (uint32_t)((c->tcp_nmsg + region - 1) / region);
+    *d_slot = Q; // pinned host staging of the second parameter block
+    hipMemcpyAsync(c->d_params + 1, d_slot, sizeof Q, hipMemcpyHostToDevice, st);
+    hipLaunchKernelGGL(pv_dns_tcp, dim3(gt), dim3(256), 0, st, (const PvParams *)(c->d_params + 1));
+    return gt;
 }
 
 // One device batch with at most PV_MAX_SHIFTS shifts of each manager. nsh / dsh: the Net and
 // DNS shifts inside it (record indices relative to d_offs).
-int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, uint64_t rec_bytes,
-                 const std::vector<Shift> &nsh, const std::vector<Shift> &dsh, hipStream_t st)
+int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint64_t a, uint64_t n, uint64_t rec_bytes,
+                 const std::vector<Shift> &nsh, const std::vector<Shift> &dsh, uint32_t first_sec, hipStream_t st)
 {
     const uint32_t np = c->cfg.num_periods;
+    const uint32_t *d_offs = d_boffs + a;
     PvParams P;
     params_common(c, P, d_recs, d_offs, n);
+    // a batch with no TCP stage ahead of it is one span: its Net pass emits the TCP segments
+    P.tcp_emit = c->tcp_pre ? 0u : 1u;
     P.gbase = c->global_base + c->records_seen;
     // Net periods and slots: period 0 -> the live bucket, each shift -> the next ordinal's slot
     P.n_shift = (uint32_t)nsh.size();
@@ -1389,7 +1684,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint6
     }
     // DNS periods and slots, from the DNS manager's own shifts
     P.n_dshift = (uint32_t)dsh.size();
-    for (size_t k = 0; k < dsh.size(); k++) P.dthresh[k] = dsh[k].sec;
+    for (size_t k = 0; k < dsh.size(); k++) { P.dthresh[k] = dsh[k].sec; P.dpos[k] = (uint32_t)dsh[k].ord; }
     P.dskip_before = P.n_dshift + 1 > np ? P.n_dshift + 1 - np : 0;
     for (uint32_t k = 0; k <= P.n_dshift; k++) {
         P.dslot_of[k] = c->dns.slot_at(k);
@@ -1414,8 +1709,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint6
     P.want_events = (c->dns_groups & PV_DNS_TRANSACTIONS) ? 1 : 0;
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
-    if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0xffffffffull)
-        return c->fail(PV_ECAPACITY, "open DNS queries carried over more than 2^32 records without a response");
+    if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0x3fffffffull)
+        return c->fail(PV_ECAPACITY, "open DNS queries carried over more than 2^30 records without a response");
     P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
     P.flags = c->d_status + ST_FLAGS;
     launch_fill32(c, c->d_status, ST_TP_CNT + (1u << c->reg_log2), 0);
@@ -1500,8 +1795,23 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint6
         if (hipEventElapsedTime(&ms, c->ev_start, c->ev_stop) == hipSuccess) { c->kernel_ms += ms; c->kernel_launches++; }
     }
     // the parts this batch wrote are no longer clean
+    // ---- DNS over TCP: the stage of a one-span batch (its segments came from the Net pass),
+    // then this span's messages through the DNS pass, their events behind the UDP ones
+    if (!c->tcp_pre) {
+        if (int rc = tcp_stage(c, d_recs, d_offs, n, status[ST_TSEG], status[ST_TSEG_BYTES], first_sec, false, st)) return rc;
+    }
+    const uint32_t gt = tcp_pass(c, P, a, a + n, st, c->h_params + 1);
+    if (gt) {
+        if (P.want_events)
+            hipLaunchKernelGGL(pv_xact_compact, dim3(grid + gt), dim3(256), 0, st, (const PvParams *)c->d_params, grid + gt);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_dns_tcp");
+        if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "TCP DNS pass");
+        memcpy(status, c->h_status, sizeof status);
+    }
     for (uint32_t k = 0; k <= P.n_shift; k++) c->net.clean[P.slot_of[k]] = false;
-    if (status[ST_NDNS])
+    if (status[ST_NDNS] || gt)
         for (uint32_t k = 0; k <= P.n_dshift; k++) c->dns.clean[P.dslot_of[k]] = false;
     uint32_t flags = status[ST_FLAGS];
     if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
@@ -1572,6 +1882,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint6
         X.orph = c->d_orph;
         X.n_orph = c->d_nvals + 3;
         X.orph_cap = c->orph_cap;
+        X.trecs = c->d_marena;
+        X.toffs = c->d_moffs;
         if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
             !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
             return c->hipfail(e, "parameter upload");
@@ -1638,11 +1950,17 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint6
     return 0;
 }
 
-// Both managers' shifts of a batch (Net from the record seconds, DNS from the prescan bits)
+// Both managers' shifts of a batch (Net from the record seconds, DNS from the prescan bits
+// and the TCP messages). A batch that may shift DNS windows, or that the Net shifts split
+// into spans, runs its TCP stage here, ahead of the spans (the prescan emits the segments);
+// any other batch runs it inside its one span, behind the Net pass (c->tcp_pre).
 int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
                  const uint32_t *sc_idx, const uint32_t *sc_sec, hipStream_t st, std::vector<Shift> &nsh,
                  std::vector<Shift> &dsh)
 {
+    c->tcp_pre = false;
+    c->tcp_nmsg = 0;
+    c->tcp_ords.clear();
     if (c->cfg.num_periods <= 1) return 0;
     const bool net_may = info->last_sec >= c->net.next_shift_sec, dns_may = info->last_sec >= c->dns.next_shift_sec;
     if (!net_may && !dns_may) return 0;
@@ -1654,10 +1972,14 @@ int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const
         return 0;
     }
     if (net_may) net_shifts_of(c->net.next_shift_sec, info, sc_idx, sc_sec, nsh);
-    if (dns_may) {
-        if (int rc = dns_prescan(c, d_recs, d_offs, info->n_records, st)) return rc;
-        dns_shifts_of(c->dns.next_shift_sec, c->h_dbits, info->n_records, info, sc_idx, sc_sec, dsh);
+    c->tcp_pre = dns_may || nsh.size() > PV_MAX_SHIFTS;
+    if (c->tcp_pre) {
+        uint32_t tseg[2] = {0, 0};
+        if (int rc = dns_prescan(c, d_recs, d_offs, info->n_records, st, true, tseg)) return rc;
+        if (int rc = tcp_stage(c, d_recs, d_offs, info->n_records, tseg[0], tseg[1], (uint32_t)info->first_sec, dns_may, st))
+            return rc;
     }
+    if (dns_may) dns_shifts_of(c->dns.next_shift_sec, c->h_dbits, info->n_records, info, sc_idx, sc_sec, c->tcp_ords, dsh);
     return 0;
 }
 
@@ -1687,8 +2009,8 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
         if (nsh.size() - ni > PV_MAX_SHIFTS) b = std::min<uint64_t>(b, nsh[ni + PV_MAX_SHIFTS].idx);
         if (dsh.size() - di > PV_MAX_SHIFTS) b = std::min<uint64_t>(b, dsh[di + PV_MAX_SHIFTS].idx);
         std::vector<Shift> ns, ds;
-        for (; ni < nsh.size() && nsh[ni].idx < b; ni++) ns.push_back({nsh[ni].sec, nsh[ni].idx - a});
-        for (; di < dsh.size() && dsh[di].idx < b; di++) ds.push_back({dsh[di].sec, dsh[di].idx - a});
+        for (; ni < nsh.size() && nsh[ni].idx < b; ni++) ns.push_back({nsh[ni].sec, nsh[ni].idx - a, 0});
+        for (; di < dsh.size() && dsh[di].idx < b; di++) ds.push_back({dsh[di].sec, dsh[di].idx - a, dsh[di].ord - 4 * a});
         uint64_t rec_bytes = info->bytes_used;
         if (b < n) {
             uint32_t ob = 0;
@@ -1697,7 +2019,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
                 return c->hipfail(e, "span end");
             rec_bytes = ob;
         }
-        if (int rc = process_span(c, d_recs, d_offs + a, b - a, rec_bytes, ns, ds, st)) return rc;
+        if (int rc = process_span(c, d_recs, d_offs, a, b - a, rec_bytes, ns, ds, (uint32_t)info->first_sec, st)) return rc;
         a = b;
     }
     c->last_sec = info->last_sec;
@@ -2332,7 +2654,8 @@ int pv_dns_event_seconds(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_off
     const uint64_t nr = info->n_records;
     if (!nr) return 0;
     if (nr > c->max_records) return c->fail(PV_ECAPACITY, "batch exceeds max_records");
-    if (int rc = dns_prescan(c, d_recs, d_offs, nr, c->stream)) return rc;
+    uint32_t tseg[2];
+    if (int rc = dns_prescan(c, d_recs, d_offs, nr, c->stream, false, tseg)) return rc;
     uint32_t k = 0;
     for (uint32_t j = 0; j < info->n_sec_changes; j++) {
         const uint64_t lo = sc_idx[j], hi = j + 1 < info->n_sec_changes ? sc_idx[j + 1] : nr;

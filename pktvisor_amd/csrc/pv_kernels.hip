@@ -166,11 +166,23 @@ __device__ __forceinline__ uint32_t dns_suffix_of(PV_CREF(PvParams) P, const A &
 }
 
 // Writes the name record for a newly created global top-N entry (arena: u16 len + bytes).
-__device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, uint32_t metric, uint32_t rep)
+// where a name is decoded from when it is not the batch's record `rep`: a TCP message record
+struct NameSrc {
+    const PV_G uint8_t *recs;
+    const PV_G uint32_t *offs;
+};
+__device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, uint32_t metric, uint32_t rep,
+                                            const NameSrc *ns = nullptr)
 {
     Parsed o;
-    const GAcc R{P.recs};
-    parse_record(R, P, P.offs[rep], o);
+    const GAcc R{ns ? ns->recs : P.recs};
+    if (ns) {
+        ParseCfg C = parse_cfg(P);
+        C.linktype = 101;
+        parse_record(R, C, P, ns->offs[rep], o);
+    } else {
+        parse_record(R, P, P.offs[rep], o);
+    }
     const uint32_t part = (blockIdx.x * 7 + threadIdx.x / 64) & (PV_ARENA_PARTS - 1);
     const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
     const uint32_t tab = PV_TSLOT(slot, metric);
@@ -248,7 +260,8 @@ __device__ __forceinline__ TPos tpos(PV_CREF(PvParams) P, uint32_t slot, uint64_
 
 // Direct insert into the global table (boundary tiles, slow transactions, regions with
 // few updates in a batch): device-scope CAS / add, probing inside the key's region.
-__device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
+__device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep,
+                                        const NameSrc *ns = nullptr)
 {
     uint32_t metric = PV_KEY_METRIC(key);
     uint64_t *sum = slot_sum(P, slot);
@@ -276,7 +289,7 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
         }
     }
     if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
-    if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep);
+    if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns);
 }
 
 // ------------------------------------------------------------------ LDS key cache
@@ -511,27 +524,32 @@ __device__ __forceinline__ void dns_header(const A &R, uint64_t m, uint32_t mcap
 // _register_predicate_filter, dns/v1/DnsStreamHandler.cpp:485-537): only_rcode passes a
 // response whose rcode is listed; only_qname a message whose lower-case first-query name is
 // listed. A packet they reject never reaches the handler (no event, no window shift).
+// only_qname: the lower-case first-query name is listed
+template <class A>
+__device__ __forceinline__ bool dns_qname_listed(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen, uint32_t w1,
+                                                 uint32_t w2)
+{
+    const uint32_t qd = ((w1 & 0xff) << 8) | ((w1 >> 8) & 0xff), an = ((w1 >> 8) & 0xff00) | (w1 >> 24);
+    const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff), ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+    DnsInfo qi;
+    dns_parse(R, m, dlen, qd, an, ns, ar, qi);
+    bool hit = false;
+    if (qi.ok && qi.has_query && qi.name_len_enc > 0) {
+        NameStats st;
+        st.init();
+        name_stats(R, m, dlen, 12, st);
+        const uint64_t fp = fp56(st.ph, st.n, 0);
+        for (uint32_t k = 0; k < P.f_nqn; k++) hit |= st.n > 0 && fp == P.f_qn[k];
+    }
+    return hit;
+}
 template <class A>
 __device__ __forceinline__ bool dns_predicates(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen, uint32_t w0,
                                                uint32_t w1, uint32_t w2)
 {
     const uint32_t qr = (w0 >> 23) & 1, rcode = (w0 >> 24) & 15;
     if ((P.f_flags & PVDF_ONLY_RCODE) && (!qr || !((P.f_rcode_mask >> rcode) & 1))) return false;
-    if (P.f_flags & PVDF_ONLY_QNAME) {
-        const uint32_t qd = ((w1 & 0xff) << 8) | ((w1 >> 8) & 0xff), an = ((w1 >> 8) & 0xff00) | (w1 >> 24);
-        const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff), ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
-        DnsInfo qi;
-        dns_parse(R, m, dlen, qd, an, ns, ar, qi);
-        bool hit = false;
-        if (qi.ok && qi.has_query && qi.name_len_enc > 0) {
-            NameStats st;
-            st.init();
-            name_stats(R, m, dlen, 12, st);
-            const uint64_t fp = fp56(st.ph, st.n, 0);
-            for (uint32_t k = 0; k < P.f_nqn; k++) hit |= st.n > 0 && fp == P.f_qn[k];
-        }
-        if (!hit) return false;
-    }
+    if ((P.f_flags & PVDF_ONLY_QNAME) && !dns_qname_listed(P, R, m, dlen, w1, w2)) return false;
     return true;
 }
 
@@ -559,10 +577,16 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
     const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
     uint32_t sfx = 0; // only_qname_suffix's suffix_size for aggregateDomain
+    // a message's order in the span: record * 4 (+ sub for a TCP message), for the CPC
+    // first-occurrence index and the transaction sort rank
+    const uint32_t ordr = P.tcp_pass ? dm.pad - P.ord_base : (i << 2);
     if (P.f_flags) {
-        if ((P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
+        // a TCP message takes no input predicate: _filtering applies only_rcode and only_qname
+        // to it as ordinary filters (_predicate_filter_type stays FiltersMAX, :546-551,593-602)
+        if (!P.tcp_pass && (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
         // DnsStreamHandler::_filtering (:538-648), in its order
         bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
+                    (P.tcp_pass && (P.f_flags & PVDF_ONLY_RCODE) && !((P.f_rcode_mask >> rcode) & 1)) ||
                     ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
                     ((P.f_flags & PVDF_ONLY_QUERIES) && qr) || ((P.f_flags & PVDF_ONLY_RESPONSES) && !qr) ||
                     ((P.f_flags & PVDF_ONLY_DNSSEC) && (!qr || !ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar))) ||
@@ -574,6 +598,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             for (uint32_t k = 0; k < P.f_nq; k++) hit |= fd.qtype == P.f_qt[k];
             filt = !fd.ok || !fd.has_query || !hit;
         }
+        if (!filt && P.tcp_pass && (P.f_flags & PVDF_ONLY_QNAME)) filt = !dns_qname_listed(P, R, m, dlen, w1, w2);
         if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) {
             // matched by pv_dns_suffix before this pass (0xff: no listed suffix)
             const uint32_t r = P.sfx_of[i];
@@ -620,7 +645,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
             if (dc) {
                 sum_add(P, slot, PV_OFF_DNS + DC_TOTAL, 1);
-                sum_add(P, slot, PV_OFF_DNS + DC_UDP, 1);
+                sum_add(P, slot, PV_OFF_DNS + (P.tcp_pass ? DC_TCP : DC_UDP), 1);
                 sum_add(P, slot, PV_OFF_DNS + (d6 ? DC_V6 : DC_V4), 1);
                 sum_add(P, slot, PV_OFF_DNS + (qr ? DC_REPLIES : DC_QUERIES), 1);
                 if (qr && rcode == 0) sum_add(P, slot, PV_OFF_DNS + DC_NOERROR, 1);
@@ -651,7 +676,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                     uint32_t first = 0xffffffffu;
                     // same name => same coupon: skip when a smaller record index already submitted it
                     if (!(cache && cache->add(PV_LKEY(slot, LM_CPCQ, coupon), 0, i, first) && first < i))
-                        cpc_min(P, slot, CPC_QNAME, coupon, (int64_t)(P.gbase + i));
+                        cpc_min(P, slot, CPC_QNAME, coupon, (int64_t)((P.gbase << 2) + ordr));
                 }
                 top(TM_DENSE_QTYPE, d.qtype, 1);
                 if (P.dns_groups & PV_DNS_TOP_QNAMES_BIT) {
@@ -695,7 +720,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         if (qr) atomicAdd(nresp, 1u);
         PvXEvent ev;
         ev.key = ((uint64_t)dm.fkey << 16) | txid;
-        ev.idx = i;
+        ev.idx = P.tcp_pass ? (i | PV_TCP_IDX) : i;
         ev.len = dlen;
         ev.sec = dm.sec;
         ev.nsec = (int32_t)dm.nsec;
@@ -704,7 +729,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         ev.period = (uint8_t)period;
         ev.pad = 0;
         P.events[e] = ev;
-        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)(P.ekey_base + i);
+        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
     }
 }
 
@@ -773,6 +798,10 @@ struct NetK {
     PV_G uint64_t *dq;
     PV_G uint32_t *flags;
     uint32_t n_shift, skip_before, slot0, net_groups, dbg, net_filter_all, n_dshift, dskip_before;
+    uint32_t tcp_emit, tseg_cap;
+    PV_G PvTcpSeg *tseg;
+    PV_G uint32_t *tseg_cnt;
+    PV_G uint64_t *tmask;
 };
 // Net v1 counters of one record straight to HBM (a lane whose slot is not the wave's
 // register slot: records of a 64-record tile that holds a period shift)
@@ -1024,6 +1053,97 @@ __device__ __forceinline__ uint32_t fast_flowkey(const RecW &r)
     return fnv_bytes(h, r.w[9] >> 24, 1);
 }
 
+// ---- DNS over TCP: the segment of a TCP packet of a DNS-port flow (PvTcpSeg), or false
+// when TcpReassembly would not look at it (no payload and none of SYN / FIN / RST: dropped
+// before the connection lookup) or its header is not a TcpLayer (TcpLayer::isDataValid)
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xff) << 8) | ((x >> 8) & 0xff); }
+__device__ __forceinline__ bool tcp_dns_pw(uint32_t pw)
+{
+    const uint32_t sp = bswap16(pw & 0xffff), dp = bswap16(pw >> 16);
+    return sp == 53 || sp == 5353 || sp == 5355 || sp == 53000 || dp == 53 || dp == 5353 || dp == 5355 || dp == 53000;
+}
+// the side of a packet: its first IP layer's source address and source port
+__device__ __forceinline__ uint64_t tcp_ep4(uint32_t a, uint32_t sport_raw)
+{
+    return fmix64((((uint64_t)a << 16) | sport_raw) ^ 0x7463703400000000ull);
+}
+__device__ __forceinline__ uint64_t tcp_ep6(uint64_t w0, uint64_t w1, uint32_t sport_raw)
+{
+    return fmix64(w0 ^ fmix64(w1 ^ ((uint64_t)sport_raw << 48) ^ 0x7463703600000000ull));
+}
+__device__ __forceinline__ bool tcp_seg_fill(PvTcpSeg &g, uint32_t pw, uint32_t w3, uint32_t seq_raw, uint32_t l4len, uint64_t l4off,
+                                             uint64_t i, uint32_t fkey, int64_t sec, int32_t nsec, uint64_t ep, uint32_t dirv6)
+{
+    const uint32_t hl = ((w3 >> 4) & 0xf) * 4; // data offset (byte 12), flags (byte 13)
+    if (hl < 20 || hl > l4len) return false;
+    const uint32_t fl = (w3 >> 8) & 7;
+    const uint32_t plen = l4len - hl;
+    if (!plen && !fl) return false;
+    g.idx = (uint32_t)i;
+    g.poff = (uint32_t)(l4off + hl);
+    g.seq = __builtin_bswap32(seq_raw);
+    g.fkey = fkey;
+    g.sec = (uint32_t)sec;
+    g.usec = (uint32_t)nsec / 1000u;
+    g.ep = ep;
+    g.plen = (uint16_t)plen;
+    g.sport = (uint16_t)bswap16(pw & 0xffff);
+    g.dport = (uint16_t)bswap16(pw >> 16);
+    g.flags = (uint8_t)fl;
+    g.dirv6 = (uint8_t)dirv6;
+    g.pad[0] = g.pad[1] = 0;
+    return true;
+}
+template <class A>
+__device__ __forceinline__ bool tcp_seg_of(const A &R, const Parsed &o, uint64_t i, PvTcpSeg &g)
+{
+    if (o.l4 != 6) return false;
+    const uint32_t pw = R.u32(o.l4off);
+    if (!tcp_dns_pw(pw)) return false;
+    const bool v6first = o.has6 && (!o.has4 || o.v6 < o.v4);
+    uint64_t ep;
+    if (!v6first) ep = tcp_ep4(R.u32(o.v4 + 12), pw & 0xffff);
+    else {
+        const uint64_t a = o.v6 + 8;
+        ep = tcp_ep6((uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32), (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32),
+                     pw & 0xffff);
+    }
+    return tcp_seg_fill(g, pw, R.u32(o.l4off + 12), R.u32(o.l4off + 4), o.l4len, o.l4off, i, flowkey(R, o), o.sec, o.nsec, ep,
+                        o.dir | (v6first ? 4u : 0u));
+}
+// the same from a fast-path record's words (Ethernet + IPv4 without options: TCP at record offset 50)
+__device__ __forceinline__ bool tcp_seg_fast(const RecW &r, const Parsed &o, uint64_t i, PvTcpSeg &g)
+{
+    const uint32_t pw = r.at(50);
+    if (!tcp_dns_pw(pw)) return false;
+    return tcp_seg_fill(g, pw, r.w[15] >> 16, r.at(54), o.l4len, o.l4off, i, fast_flowkey(r), o.sec, o.nsec,
+                        tcp_ep4(r.at(42), pw & 0xffff), o.dir);
+}
+// wave-compacted append of the lanes' segments (one atomic per wave), with their payload bytes
+__device__ __forceinline__ void tcp_seg_store(PV_G PvTcpSeg *out, PV_G uint32_t *cnt, uint32_t cap, bool has, const PvTcpSeg &g,
+                                              uint32_t lane)
+{
+    const uint64_t m = __ballot(has);
+    if (!m) return;
+    uint32_t bytes = has ? g.plen : 0u;
+    for (int o = 32; o > 0; o >>= 1) bytes += __shfl_xor(bytes, o, 64);
+    uint32_t q = 0;
+    if (lane == 0) {
+        q = atomicAdd(cnt, (uint32_t)__popcll(m));
+        atomicAdd(cnt + 1, bytes);
+    }
+    q = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (has) {
+        if (q < cap) {
+            PV_G uint4 *d = reinterpret_cast<PV_G uint4 *>(out + q);
+            d[0] = make_uint4(g.idx, g.poff, g.seq, g.fkey);
+            d[1] = make_uint4(g.sec, g.usec, (uint32_t)g.ep, (uint32_t)(g.ep >> 32));
+            d[2] = make_uint4((uint32_t)g.plen | ((uint32_t)g.sport << 16), (uint32_t)g.dport | ((uint32_t)g.flags << 16) |
+                              ((uint32_t)g.dirv6 << 24), 0u, 0u);
+        }
+    }
+}
+
 } // namespace
 
 // The general per-record path (every frame the fast path does not take: VLAN, IPv6,
@@ -1037,6 +1157,8 @@ struct SlowOut {
     DnsMsgW dm;
     uint32_t caplen, isdns;
     uint8_t dir, l3, l4, syn;
+    uint32_t hasseg;
+    PvTcpSeg seg;
 };
 __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF(PvParams) P, const NetK K, uint64_t off,
                                          uint64_t i, uint32_t slot, bool upd)
@@ -1048,7 +1170,9 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
     Parsed o;
     parse_record(R, C, P, off, o);
     so.caplen = o.caplen; so.dir = o.dir; so.l3 = o.l3; so.l4 = o.l4; so.syn = o.syn;
+    so.hasseg = 0;
     if (K.dbg & 2) return so;
+    if (K.tcp_emit && o.l4 == 6) so.hasseg = tcp_seg_of(R, o, i, so.seg) ? 1u : 0u;
     if (upd) so.ek = net_ip_entry(K, R, o, i, slot);
     if (o.l4 == 17 && !(K.dbg & 4)) {
         const uint32_t port = dns_port(R.u32(o.l4off));
@@ -1088,6 +1212,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
     K.n_shift = P.n_shift; K.skip_before = P.skip_before; K.slot0 = P.slot_of[0];
     K.net_groups = P.net_groups; K.dbg = P.dbg; K.net_filter_all = P.net_filter_all;
     K.n_dshift = P.n_dshift; K.dskip_before = P.dskip_before;
+    K.tcp_emit = P.tcp_emit; K.tseg_cap = P.tseg_cap; K.tseg = P.tseg; K.tseg_cnt = P.tseg_cnt; K.tmask = P.tmask;
     const ParseCfg C = parse_cfg(P);
     const uint64_t n = K.n, last = n - 1;
     const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
@@ -1184,6 +1309,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         uint64_t ek = 0;
         DnsMsgW dm{};
         bool isdns = false;
+        bool istcp = false, hasseg = false;
+        PvTcpSeg seg;
         if (active && !(K.dbg & 1)) {
             const SAcc R = packed ? SAcc{K.recs, NW.slot[sl], base, nch * 16 - 4, 0u, 1u}
                                   : SAcc{K.recs, NW.slot[sl], off & ~15ull, PV_NL_SLOT / PV_WT - 4, lane * 4, 0u};
@@ -1204,7 +1331,12 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                 ek = so.ek;
                 dm = so.dm;
                 isdns = so.isdns;
+                hasseg = so.hasseg;
+                seg = so.seg;
+            } else if (K.tcp_emit && o.l4 == 6) {
+                hasseg = tcp_seg_fast(rw, o, i, seg);
             }
+            istcp = o.l4 == 6;
             STAMP(4)
             if (K.dbg & 2) {
                 c.add(o);
@@ -1278,6 +1410,12 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                 }
             }
             if (tops && i <= r1) K.iplog[i] = ek;
+            if (K.tcp_emit) {
+                // DNS over TCP: the tile's TCP records, then its DNS-port segments
+                const uint64_t tm = __ballot(istcp);
+                if (lane == 0) K.tmask[t] = tm;
+                if (tm) tcp_seg_store(K.tseg, K.tseg_cnt, K.tseg_cap, hasseg, seg, lane);
+            }
         }
         STAMP(6)
     }
@@ -1829,10 +1967,13 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_prescan(const PvParams 
     const uint64_t ntiles = (P.n + 63) / 64;
     for (uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntiles; t += (uint64_t)gridDim.x * 4) {
         const uint64_t i = t * 64 + (threadIdx.x & 63);
-        bool ev = false;
+        bool ev = false, istcp = false, hasseg = false;
+        PvTcpSeg g;
         if (i < P.n) {
             Parsed o;
             parse_record(R, P, P.offs[i], o);
+            istcp = o.l4 == 6;
+            if (P.tcp_emit && istcp) hasseg = tcp_seg_of(R, o, i, g);
             if (o.l4 == 17 && dns_port(R.u32(o.l4off))) {
                 ev = true;
                 if (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) {
@@ -1847,6 +1988,61 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_prescan(const PvParams 
         }
         const uint64_t b = __ballot(ev);
         if ((threadIdx.x & 63) == 0) P.dbits[t] = b;
+        if (P.tcp_emit) {
+            // DNS over TCP for a batch the TCP stage runs ahead of the Net pass (pv_tcp.hip)
+            const uint64_t tm = __ballot(istcp);
+            if ((threadIdx.x & 63) == 0) P.tmask[t] = tm;
+            if (tm) tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, g, threadIdx.x & 63);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ the TCP DNS pass
+// The DNS messages pv_tcp_flow cut from reassembled streams, through the same per-message
+// work as UDP datagrams (DnsStreamHandler::tcp_message_ready_cb -> _filtering ->
+// process_dns_layer, dns/v1/DnsStreamHandler.cpp:375-436). P is the span's parameter block
+// with recs / offs replaced by the message records (linktype 101) and dq by the message
+// list; the messages of this span (ord in [ord_lo, ord_hi)) take the DNS period of their
+// position. Workgroup b handles messages [b * region, (b + 1) * region) and appends its
+// events to the event region of workgroup grid_main + b, so pv_xact_compact packs them
+// with the UDP events. Top-N updates go straight to the global tables (names decoded from
+// the message records at once), the counters to HBM: TCP messages are few.
+extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t nev, nresp;
+    if (threadIdx.x == 0) { nev = 0; nresp = 0; }
+    __syncthreads();
+    const uint64_t region = (uint64_t)P.wt_per_block * PV_WT;
+    const uint64_t j0 = (uint64_t)blockIdx.x * region, j1 = min<uint64_t>(j0 + region, P.tcp_nmsg);
+    const GAcc R{P.recs};
+    DnsCtr c;
+    c.zero();
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+        const PV_G uint4 *q = reinterpret_cast<const PV_G uint4 *>(P.dq) + 2 * j;
+        const uint4 a = q[0], b = q[1];
+        DnsMsg dm;
+        dm.idx = a.x; dm.moff = a.y; dm.mlen = (uint16_t)(a.z & 0xffff); dm.mcap = (uint16_t)(a.z >> 16);
+        dm.port = (uint16_t)(a.w & 0xffff); dm.flags = (uint8_t)((a.w >> 16) & 0xff);
+        dm.fkey = b.x; dm.sec = b.y; dm.nsec = b.z; dm.pad = b.w;
+        if (dm.pad < P.ord_lo || dm.pad >= P.ord_hi) continue;
+        const uint32_t ordr = dm.pad - P.ord_base;
+        uint32_t p = 0;
+        for (uint32_t k = 0; k < P.n_dshift; k++) p += ordr >= P.dpos[k];
+        dm.period = (uint8_t)p;
+        if (p >= P.dskip_before) dm.flags |= 8;
+        if (P.f_flags & PVDF_ONLY_QSUFFIX) {
+            const uint64_t m = dm.moff;
+            P.sfx_of[dm.idx] = (uint8_t)dns_suffix_of(P, R, m, dm.mlen, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8),
+                                                      be16(R, m + 10));
+        }
+        dns_process(P, (KeyCache<PV_NCACHE> *)nullptr, nullptr, &nev, &nresp, (uint64_t)(P.grid_main + blockIdx.x) * region, R,
+                    dm, false, c);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        P.blk_events[P.grid_main + blockIdx.x] = nev;
+        if (nresp) atomicAdd(P.n_events + 1, nresp);
     }
 }
 
@@ -1937,8 +2133,16 @@ __device__ void slow_check(PV_CREF(PvXactParams) X, uint32_t idx, uint32_t perio
     if (!(thr > 0.0f && (float)us >= thr)) return;
     PV_CREF(PvParams) P = X.P;
     Parsed o;
-    const GAcc R{P.recs};
-    parse_record(R, P, P.offs[idx], o);
+    const bool tcp = idx & PV_TCP_IDX;
+    const GAcc R{tcp ? X.trecs : P.recs};
+    if (tcp) {
+        ParseCfg C = parse_cfg(P);
+        C.linktype = 101;
+        idx &= ~PV_TCP_IDX;
+        parse_record(R, C, P, X.toffs[idx], o);
+    } else {
+        parse_record(R, P, P.offs[idx], o);
+    }
     uint64_t m = o.l4off + 8;
     uint32_t len = o.l4len - 8;
     DnsInfo d;
@@ -1947,7 +2151,8 @@ __device__ void slow_check(PV_CREF(PvXactParams) X, uint32_t idx, uint32_t perio
     RawName rn{0, 0};
     if (d.name_len_enc > 0) name_emit(R, m, len, 12, rn);
     const uint32_t metric = dir == 0 ? TM_SLOW_OUT : TM_SLOW_IN;
-    global_add(P, P.dslot_of[period], PV_KEY(metric, fp56(rn.ph, rn.n, 1)), 1, idx);
+    const NameSrc ns{X.trecs, X.toffs};
+    global_add(P, P.dslot_of[period], PV_KEY(metric, fp56(rn.ph, rn.n, 1)), 1, idx, tcp ? &ns : nullptr);
 }
 } // namespace
 

@@ -144,10 +144,74 @@ struct PvXValue {
 
 // a valid transaction whose period's slow threshold is not known yet
 struct PvXValid {
-    uint32_t idx; // response record index within the batch
+    uint32_t idx; // response record index within the batch (PV_TCP_IDX: a TCP message record)
     uint8_t period, dir, pad0, pad1;
     uint64_t us;
 };
+
+// ---- DNS over TCP (PcapPlusPlus TcpReassembly + DnsTcpSessionData, device-resident)
+// A DNS message cut from a reassembled TCP stream becomes a "message record" in the
+// batch's TCP message arena: a classic-pcap record holding a raw-IPv4 (linktype 101)
+// frame, IPv4 header (total length 0: no trim) + UDP header + the message, so every
+// kernel that re-derives a name from a record (pv_topn_names, write_name, slow_check)
+// reads it unchanged. Its index in the arena's offset list carries PV_TCP_IDX in events.
+#define PV_TCP_IDX 0x80000000u
+#define PV_TCP_REC_HDR 44u          // pcap record header 16 + IPv4 20 + UDP 8
+#define PV_TCP_MIN_MSG 17u          // DnsTcpSessionData MIN_DNS_QUERY_SIZE
+#define PV_TCP_MAX_OOO 50u          // TcpReassemblyConfiguration maxOutOfOrderFragments (PcapInputStream.cpp:79)
+#define PV_TCP_TIMEOUT 30u          // PcapInputStream::TCP_TIMEOUT (PcapInputStream.h:97)
+#define PV_TCP_RECLAIM 300u         // seconds after which a closed / timed-out flow entry is reused
+
+// One TCP packet of a DNS-port flow that TcpReassembly does not drop at once (payload, or
+// SYN / FIN / RST), emitted by the Net pass or, for a batch that may shift DNS windows,
+// by pv_dns_prescan.
+struct PvTcpSeg {
+    uint32_t idx;        // record index in the batch
+    uint32_t poff;       // absolute offset of the TCP payload in the record blob
+    uint32_t seq;        // sequence number
+    uint32_t fkey;       // hash5Tuple
+    uint32_t sec, usec;  // packet timestamp at ConnectionData's timeval precision
+    uint64_t ep;         // side: hash of (first IP layer's source address, source port)
+    uint16_t plen, sport, dport;
+    uint8_t flags;       // PV_TF_*
+    uint8_t dirv6;       // PacketDirection | (first IP layer is IPv6) << 2
+    uint32_t pad[2];
+};
+enum { PV_TF_FIN = 1, PV_TF_SYN = 2, PV_TF_RST = 4 };
+static_assert(sizeof(PvTcpSeg) == 48, "three 16-B stores");
+
+// TcpReassemblyData + DnsStreamHandler's TcpFlowData of one connection, carried across batches
+struct PvTcpFlow {
+    uint64_t tag;        // 0 empty, else 1 << 32 | flowKey
+    uint32_t stage;      // TCP stage ordinal that last touched the entry
+    uint8_t closed, tracked, v6, nsides;
+    int8_t prev;         // prevSide
+    uint8_t fin[2];
+    uint8_t live;        // the connection exists (its first packet was seen)
+    uint16_t sport, dport, port, pad1; // connData ports, metric port
+    uint64_t ep[2];      // sides
+    uint32_t seq[2];     // expected sequence per side
+    uint32_t end_sec, end_usec; // ConnectionData::endTime (0 until a second packet)
+    uint32_t lru_sec;    // time of the last LRU put (connection start / message ready)
+    uint32_t close_sec;
+    // DnsTcpSessionData per side: length bytes seen (0..2), message size, bytes held
+    uint8_t inval[2], lenb[2];
+    uint16_t size[2];
+    uint32_t got[2];
+    // carried bytes (carry arena): per side the held message bytes, then per side the
+    // out-of-order fragments as {seq u32, len u32, bytes padded to 4}
+    uint32_t blob, blob_len;
+    uint16_t nfrag[2];
+    uint32_t pad2[3];
+};
+static_assert(sizeof(PvTcpFlow) == 112, "flow entry size");
+#define PV_TCP_FRAG_NIL 0xffffffffu
+struct PvTcpFrag {
+    uint64_t src;  // device address of the bytes
+    uint32_t seq, len;
+    uint32_t next, pad;
+};
+
 
 
 // Device pointers carry the global address space in the device compile, so the kernels
@@ -253,6 +317,18 @@ struct PvParams {
     uint32_t f_sxl[PV_MAX_SUFFIXES];   // its length and
     uint64_t f_sxh[PV_MAX_SUFFIXES];   // its polynomial hash (ph_step over the lower-case chars)
     PV_G uint8_t *sfx_of;              // per record of the batch: the matched suffix size (DNS pass writes)
+    // DNS over TCP. Emission (Net pass of a one-span batch, else pv_dns_prescan): segments of
+    // DNS-port TCP flows, their payload bytes, and per 64-record tile the mask of TCP records
+    uint32_t tcp_emit;
+    uint32_t tseg_cap;
+    PV_G PvTcpSeg *tseg;
+    PV_G uint32_t *tseg_cnt;           // [0] segments [1] payload bytes
+    PV_G uint64_t *tmask;
+    // the TCP DNS pass (pv_dns_tcp): message records replace recs / offs (linktype 101), dq
+    // holds the messages; a message's order in the batch is ord = record * 4 + sub
+    uint32_t tcp_pass, tcp_nmsg;
+    uint32_t ord_lo, ord_hi, ord_base; // this span's messages: ord in [ord_lo, ord_hi); ord_base = span start * 4
+    uint32_t dpos[PV_MAX_SHIFTS];      // span-relative ord of the event that shifts DNS period k+1
 };
 
 // pv_fill_multi's segment list (kernel argument)
@@ -298,5 +374,47 @@ struct PvXactParams {
     PV_G PvXEvent *orph;
     PV_G uint32_t *n_orph;
     uint32_t orph_cap;
+    // TCP message records (events whose idx carries PV_TCP_IDX)
+    const PV_G uint8_t *trecs;
+    const PV_G uint32_t *toffs;
 };
 #define PV_PEND_FLAG 0x80000000u
+
+// TCP stage parameters (pv_tcp_* kernels)
+struct PvTcpParams {
+    const PV_G PvTcpSeg *seg;     // segments of the batch (emission order)
+    const PV_G uint64_t *skey;    // sorted (fkey << 32 | record index)
+    const PV_G uint32_t *sval;    // segment index per sorted key
+    uint32_t n_seg;
+    uint32_t stage;               // ordinal of this stage (>= 1)
+    uint32_t now_sec;             // first record second of the batch (entry reclaim)
+    uint32_t flow_cap_log2;
+    PV_G PvTcpFlow *flows;
+    PV_G uint32_t *run_flow;      // per sorted segment: flow entry of the run it starts (else ~0)
+    // last-TCP-second structure: per 64-record tile the mask of TCP records, and the prefix
+    // maximum (+1) of TCP record seconds over earlier tiles (carried over batches in lt_carry)
+    const PV_G uint64_t *tmask;
+    PV_G uint32_t *tpm;
+    PV_G uint32_t *lt_carry;
+    const PV_G uint8_t *recs;     // the batch's records (segment payloads, TCP record seconds)
+    const PV_G uint32_t *offs;
+    uint32_t n_tiles, ts_nano;
+    // carried bytes: in (previous stage) and out (this stage), with the carried-flow lists
+    const PV_G uint8_t *carry_in;
+    PV_G uint8_t *carry_out;
+    uint64_t carry_cap;
+    const PV_G uint32_t *clist_in;
+    uint32_t n_clist_in;
+    PV_G uint32_t *clist_out;
+    PV_G PvTcpFrag *frags;        // fragment node pool
+    uint32_t frag_cap;
+    // message output: arena of message records, their offsets and DnsMsg work items
+    PV_G uint8_t *marena;
+    uint64_t marena_cap;
+    PV_G uint32_t *moffs;
+    PV_G uint64_t *mq;            // 32-B DnsMsg items (same layout as the UDP work lists)
+    uint32_t mq_cap;
+    PV_G uint32_t *cnt;           // [0] messages [1] arena bytes [2] carry bytes [3] carried flows [4] frag nodes [5] flags
+};
+enum { PVT_NMSG = 0, PVT_ARENA, PVT_CARRY, PVT_NCARRY, PVT_NFRAG, PVT_FLAGS, PVT_WORDS };
+enum { PVT_F_TABLE = 1, PVT_F_ARENA = 2, PVT_F_CARRY = 4, PVT_F_FRAGS = 8, PVT_F_MSGS = 16 };

@@ -82,3 +82,172 @@ def sparse_dns_pcap(n: int = 120000, ts_step_us: int = 2500, quiet=(52, 9), seed
     t0 = recs[0][0]
     keep = [r for s, _, r in recs if not (is_udp_dns(r) and ((s - t0) % 60 >= quiet[0] or (s - t0) % 60 < quiet[1]))]
     return pcap_file_bytes(b"".join(keep))
+
+
+# ---------------------------------------------------------------- DNS over TCP
+def _dns_msg(rng, txid: int, qr: bool, name: str, qtype: int, rcode: int = 0, answers: int = 0) -> bytes:
+    import struct
+    q = b"".join(bytes([len(l)]) + l.encode() for l in name.split(".")) + b"\x00" + struct.pack(">HH", qtype, 1)
+    flags = (0x8180 | rcode) if qr else 0x0100
+    hdr = struct.pack(">HHHHHH", txid, flags, 1, answers, 0, 0)
+    ans = b"".join(struct.pack(">HHHIH", 0xC00C, 1, 1, 300, 4) + bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+                   for _ in range(answers))
+    return hdr + q + ans
+
+
+def _frame(src, dst, sport, dport, seq, flags, payload, v6):
+    """Ethernet + IPv4 / IPv6 + TCP (ack 0, window 0) carrying payload"""
+    import struct
+    tcp = struct.pack(">HHIIBBHHH", sport, dport, seq & 0xffffffff, 0, 0x50, flags, 65535, 0, 0) + payload
+    if v6:
+        ip = struct.pack(">IHBB", 0x60000000, len(tcp), 6, 64) + src + dst
+        return b"\x00\x11\x22\x33\x44\x55\x66\x77\x88\x99\xaa\xbb\x86\xdd" + ip + tcp
+    ip = struct.pack(">BBHHHBBH", 0x45, 0, 20 + len(tcp), 0, 0, 64, 6, 0) + src + dst
+    return b"\x00\x11\x22\x33\x44\x55\x66\x77\x88\x99\xaa\xbb\x08\x00" + ip + tcp
+
+
+def tcp_dns_pcap(seed: int = 1, flows: int = 60, duration_s: float = 20.0, udp_share: float = 0.3,
+                 noise_share: float = 0.3, pauses: int = 0) -> bytes:
+    """DNS over TCP traffic for the reassembly parity tests: connections to port 53 (IPv4 and
+    IPv6) carrying pipelined queries and responses that are cut into segments at random byte
+    boundaries, with out-of-order segments, duplicate and overlapping retransmissions, a
+    lost SYN (the first captured packet carries data), invalid framing (a length below 17),
+    FIN and RST closes, a reused client port after a close; interleaved with UDP DNS and
+    non-DNS TCP noise (port 443). With pauses > 0 that many connections fall silent for 35 s
+    while the noise goes on (PcapInputStream's 30 s TCP timeout). Timestamps are monotone.
+    Every connection with a gap left in its stream ends with FIN or RST, so no data is left
+    for the end-of-capture flush (which the device path does not model)."""
+    import struct
+    from pktvisor_amd import pcap_file_bytes
+    rng = np.random.default_rng(seed)
+    names = [f"{''.join(chr(97 + int(c)) for c in rng.integers(0, 26, 6))}.example.{tld}" for tld in ("com", "net", "org")
+             for _ in range(7)]
+
+    def addr(v6, server):
+        if v6:
+            return (bytes.fromhex("20014860000000000000000000008888") if server else
+                    bytes.fromhex("20010db8") + bytes(rng.integers(0, 256, 12, dtype=np.uint8)))
+        return bytes([8, 8, 8, 8]) if server else bytes([10, int(rng.integers(0, 256)), int(rng.integers(0, 256)),
+                                                         int(rng.integers(1, 255))])
+
+    streams = []  # per connection: its packets in send order
+    used_ports = []
+    # connections that fall silent for 35 s keep their segments in order (a timeout that
+    # flushes buffered data is ordered differently on the device, see pv_tcp.hip)
+    pause_flows = set(rng.choice(flows, size=min(pauses, flows), replace=False).tolist()) if pauses else set()
+    for f in range(flows):
+        v6 = bool(rng.random() < 0.3)
+        cli, srv = addr(v6, False), addr(v6, True)
+        cport = int(rng.integers(1024, 60000))
+        if cport in (5353, 5355, 53000):
+            cport += 1
+        if used_ports and rng.random() < 0.05:  # a client port reused after a close
+            cli, srv, cport, v6 = used_ports[int(rng.integers(0, len(used_ports)))]
+        used_ports.append((cli, srv, cport, v6))
+        cseq, sseq = int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32))
+        ntx = int(rng.integers(1, 6))
+        cbytes, sbytes = b"", b""
+        for t in range(ntx):
+            name = names[int(rng.integers(0, len(names)))]
+            qt = [1, 28, 15, 16][int(rng.integers(0, 4))]
+            txid = int(rng.integers(0, 65536))
+            q = _dns_msg(rng, txid, False, name, qt)
+            r = _dns_msg(rng, txid, True, name, qt, [0, 0, 0, 3, 2][int(rng.integers(0, 5))], int(rng.integers(0, 3)))
+            cbytes += struct.pack(">H", len(q)) + q
+            sbytes += struct.pack(">H", len(r)) + r
+        if rng.random() < 0.05:  # invalid framing on the client side: a length below 17
+            cbytes += b"\x00\x05" + bytes(30)
+        pkts = []
+        lost_syn = rng.random() < 0.08 and f not in pause_flows
+        if not lost_syn:
+            pkts.append((cli, srv, cport, 53, cseq, 0x02, b""))
+            pkts.append((srv, cli, 53, cport, sseq, 0x12, b""))
+        cseq += 1
+        sseq += 1
+
+        def cut(data, seq0, src, dst, sp, dp):
+            out, pos = [], 0
+            while pos < len(data):
+                n = int(rng.integers(1, 120)) if rng.random() < 0.7 else len(data) - pos
+                out.append((src, dst, sp, dp, seq0 + pos, 0x18, data[pos:pos + n]))
+                pos += n
+            return out
+
+        csegs = cut(cbytes, cseq, cli, srv, cport, 53)
+        ssegs = cut(sbytes, sseq, srv, cli, 53, cport)
+        gaps = False
+        for segs in (csegs, ssegs):
+            # out-of-order pairs, duplicates and overlapping retransmissions
+            for k in range(len(segs) - 1):
+                if rng.random() < 0.12 and f not in pause_flows:
+                    segs[k], segs[k + 1] = segs[k + 1], segs[k]
+                    gaps = True
+            k = 0
+            while k < len(segs):
+                if rng.random() < 0.06:
+                    s = segs[k]
+                    if rng.random() < 0.5 or k + 1 >= len(segs):
+                        segs.insert(k + 1, s)  # duplicate
+                    else:
+                        nxt = segs[k + 1]
+                        segs.insert(k + 1, (s[0], s[1], s[2], s[3], s[4], 0x18, s[6] + nxt[6][:max(1, len(nxt[6]) // 2)]))
+                    k += 1
+                k += 1
+        pkts += csegs + ssegs if rng.random() < 0.5 else [p for pair in zip(csegs, ssegs) for p in pair] + \
+            csegs[len(ssegs):] + ssegs[len(csegs):]
+        end = rng.random()
+        if end < 0.6 or gaps:
+            pkts.append((cli, srv, cport, 53, cseq + len(cbytes), 0x11, b""))
+            pkts.append((srv, cli, 53, cport, sseq + len(sbytes), 0x11, b""))
+        elif end < 0.85:
+            pkts.append((srv, cli, 53, cport, sseq + len(sbytes), 0x04, b""))
+        streams.append([p for p in pkts])
+    # interleave: connections start at random times, their packets keep order
+    t0 = 1700000000.0
+    n_total = sum(len(s) for s in streams)
+    events = []
+    for f, s in enumerate(streams):
+        start = rng.random() * duration_s
+        t = start
+        for k, p in enumerate(s):
+            t += float(rng.exponential(0.02))
+            if f in pause_flows and k == len(s) // 2:
+                t += 35.0
+            events.append((t, f, k, p))
+    tmax = max(e[0] for e in events) if events else 0.0
+    # UDP DNS and non-DNS TCP noise over the whole span (the noise carries the clock)
+    n_udp, n_noise = int(n_total * udp_share), int(n_total * noise_share) + (int(tmax * 20) if pauses else 0)
+    for _ in range(n_udp):
+        t = rng.random() * tmax
+        name = names[int(rng.integers(0, len(names)))]
+        m = _dns_msg(rng, int(rng.integers(0, 65536)), bool(rng.random() < 0.5), name, 1)
+        sp = int(rng.integers(1024, 60000))
+        udp = struct.pack(">HHHH", sp, 53, 8 + len(m), 0) + m
+        ip = struct.pack(">BBHHHBBH", 0x45, 0, 20 + len(udp), 0, 0, 64, 17, 0) + bytes([10, 9, 9, 9]) + bytes([8, 8, 8, 8])
+        events.append((t, -1, 0, b"\x00\x11\x22\x33\x44\x55\x66\x77\x88\x99\xaa\xbb\x08\x00" + ip + udp))
+    # noise: eight long-lived port-443 connections (SYN, then in-order data), and every 20 s an
+    # "anchor" connection that opens and stays silent. PcapInputStream closes the LRU list's
+    # least recently used connection once it is 30 s old; a connection whose first captured
+    # packet carries data enters that list with time 0 (ConnectionData::endTime is unset
+    # until a second packet), and dies as soon as it is the list's oldest: an anchor keeps
+    # an older entry alive, as a busy capture does (the device path dates that entry by
+    # the packet instead, pv_tcp.hip).
+    nseq = [int(rng.integers(0, 2**32)) for _ in range(8)]
+    for c in range(8):
+        events.append((0.0, -2, -100 + c, _frame(bytes([10, 1, 1, 1]), bytes([1, 2, 3, c]), 40000 + c, 443, nseq[c], 0x02, b"", False)))
+        nseq[c] += 1
+    for a in range(int(tmax // 20) + 2):
+        events.append((a * 20.0, -2, -200 + a, _frame(bytes([10, 1, 1, 2]), bytes([1, 2, 4, 4]), 30000 + a, 443, 7, 0x02, b"", False)))
+    for k in range(n_noise):
+        t = (k + rng.random()) * tmax / max(n_noise, 1)
+        c = k % 8
+        pl = bytes(int(rng.integers(1, 40)))
+        events.append((t, -2, k, _frame(bytes([10, 1, 1, 1]), bytes([1, 2, 3, c]), 40000 + c, 443, nseq[c], 0x18, pl, False)))
+        nseq[c] += len(pl)
+    events.sort(key=lambda e: (e[0], e[1], e[2]))
+    out = bytearray()
+    for t, f, k, p in events:
+        fr = _frame(*p[:6], p[6], len(p[0]) == 16) if f >= 0 else p
+        us = int(round((t0 + t) * 1e6))
+        out += struct.pack("<IIII", us // 1000000, us % 1000000, len(fr), len(fr)) + fr
+    return pcap_file_bytes(bytes(out))
