@@ -1672,7 +1672,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     PvParams P;
     params_common(c, P, d_recs, d_offs, n);
     // a batch with no TCP stage ahead of it is one span: its Net pass emits the TCP segments
+    // and the tile masks of its TCP records (zeroed here; the pass stores non-zero masks only)
     P.tcp_emit = c->tcp_pre ? 0u : 1u;
+    if (P.tcp_emit) launch_fill64(c, c->d_tmask, (n + 63) / 64, 0);
     P.gbase = c->global_base + c->records_seen;
     // Net periods and slots: period 0 -> the live bucket, each shift -> the next ordinal's slot
     P.n_shift = (uint32_t)nsh.size();

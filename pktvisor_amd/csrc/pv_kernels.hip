@@ -556,7 +556,7 @@ __device__ __forceinline__ bool dns_predicates(PV_CREF(PvParams) P, const A &R, 
 // DnsMetricsBucket::process_dns_layer (:910-1049) + the transaction event of one DNS
 // message, in the bucket of its DNS period. Counters go to `c` when `own` (this lane's
 // DNS slot is the wave's register slot), else straight to HBM.
-template <class A, class Cache>
+template <bool TCP, class A, class Cache>
 __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, uint32_t *nev,
                                             uint32_t *nresp, uint64_t ebase, const A &R, const DnsMsg &dm, bool own,
                                             DnsCtr &c)
@@ -579,14 +579,14 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     uint32_t sfx = 0; // only_qname_suffix's suffix_size for aggregateDomain
     // a message's order in the span: record * 4 (+ sub for a TCP message), for the CPC
     // first-occurrence index and the transaction sort rank
-    const uint32_t ordr = P.tcp_pass ? dm.pad - P.ord_base : (i << 2);
+    const uint32_t ordr = TCP ? dm.pad - P.ord_base : (i << 2);
     if (P.f_flags) {
         // a TCP message takes no input predicate: _filtering applies only_rcode and only_qname
         // to it as ordinary filters (_predicate_filter_type stays FiltersMAX, :546-551,593-602)
-        if (!P.tcp_pass && (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
+        if (!TCP && (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
         // DnsStreamHandler::_filtering (:538-648), in its order
         bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
-                    (P.tcp_pass && (P.f_flags & PVDF_ONLY_RCODE) && !((P.f_rcode_mask >> rcode) & 1)) ||
+                    (TCP && (P.f_flags & PVDF_ONLY_RCODE) && !((P.f_rcode_mask >> rcode) & 1)) ||
                     ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
                     ((P.f_flags & PVDF_ONLY_QUERIES) && qr) || ((P.f_flags & PVDF_ONLY_RESPONSES) && !qr) ||
                     ((P.f_flags & PVDF_ONLY_DNSSEC) && (!qr || !ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar))) ||
@@ -598,7 +598,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             for (uint32_t k = 0; k < P.f_nq; k++) hit |= fd.qtype == P.f_qt[k];
             filt = !fd.ok || !fd.has_query || !hit;
         }
-        if (!filt && P.tcp_pass && (P.f_flags & PVDF_ONLY_QNAME)) filt = !dns_qname_listed(P, R, m, dlen, w1, w2);
+        if (!filt && TCP && (P.f_flags & PVDF_ONLY_QNAME)) filt = !dns_qname_listed(P, R, m, dlen, w1, w2);
         if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) {
             // matched by pv_dns_suffix before this pass (0xff: no listed suffix)
             const uint32_t r = P.sfx_of[i];
@@ -645,7 +645,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
             if (dc) {
                 sum_add(P, slot, PV_OFF_DNS + DC_TOTAL, 1);
-                sum_add(P, slot, PV_OFF_DNS + (P.tcp_pass ? DC_TCP : DC_UDP), 1);
+                sum_add(P, slot, PV_OFF_DNS + (TCP ? DC_TCP : DC_UDP), 1);
                 sum_add(P, slot, PV_OFF_DNS + (d6 ? DC_V6 : DC_V4), 1);
                 sum_add(P, slot, PV_OFF_DNS + (qr ? DC_REPLIES : DC_QUERIES), 1);
                 if (qr && rcode == 0) sum_add(P, slot, PV_OFF_DNS + DC_NOERROR, 1);
@@ -720,7 +720,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         if (qr) atomicAdd(nresp, 1u);
         PvXEvent ev;
         ev.key = ((uint64_t)dm.fkey << 16) | txid;
-        ev.idx = P.tcp_pass ? (i | PV_TCP_IDX) : i;
+        ev.idx = TCP ? (i | PV_TCP_IDX) : i;
         ev.len = dlen;
         ev.sec = dm.sec;
         ev.nsec = (int32_t)dm.nsec;
@@ -1157,8 +1157,6 @@ struct SlowOut {
     DnsMsgW dm;
     uint32_t caplen, isdns;
     uint8_t dir, l3, l4, syn;
-    uint32_t hasseg;
-    PvTcpSeg seg;
 };
 __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF(PvParams) P, const NetK K, uint64_t off,
                                          uint64_t i, uint32_t slot, bool upd)
@@ -1170,9 +1168,16 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
     Parsed o;
     parse_record(R, C, P, off, o);
     so.caplen = o.caplen; so.dir = o.dir; so.l3 = o.l3; so.l4 = o.l4; so.syn = o.syn;
-    so.hasseg = 0;
     if (K.dbg & 2) return so;
-    if (K.tcp_emit && o.l4 == 6) so.hasseg = tcp_seg_of(R, o, i, so.seg) ? 1u : 0u;
+    if (K.tcp_emit && o.l4 == 6) {
+        // a DNS-port TCP segment of a general-path frame: appended by this lane alone
+        PvTcpSeg g;
+        if (tcp_seg_of(R, o, i, g)) {
+            const uint32_t q = atomicAdd(K.tseg_cnt, 1u);
+            atomicAdd(K.tseg_cnt + 1, (uint32_t)g.plen);
+            if (q < K.tseg_cap) K.tseg[q] = g;
+        }
+    }
     if (upd) so.ek = net_ip_entry(K, R, o, i, slot);
     if (o.l4 == 17 && !(K.dbg & 4)) {
         const uint32_t port = dns_port(R.u32(o.l4off));
@@ -1331,8 +1336,6 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                 ek = so.ek;
                 dm = so.dm;
                 isdns = so.isdns;
-                hasseg = so.hasseg;
-                seg = so.seg;
             } else if (K.tcp_emit && o.l4 == 6) {
                 hasseg = tcp_seg_fast(rw, o, i, seg);
             }
@@ -1412,9 +1415,13 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
             if (tops && i <= r1) K.iplog[i] = ek;
             if (K.tcp_emit) {
                 // DNS over TCP: the tile's TCP records, then its DNS-port segments
+                // (tiles without TCP keep the zero the batch's fill wrote: no store, so no
+                // extra vector operation in the ring's exact vmcnt accounting on UDP-only tiles)
                 const uint64_t tm = __ballot(istcp);
-                if (lane == 0) K.tmask[t] = tm;
-                if (tm) tcp_seg_store(K.tseg, K.tseg_cnt, K.tseg_cap, hasseg, seg, lane);
+                if (tm) {
+                    if (lane == 0) K.tmask[t] = tm;
+                    tcp_seg_store(K.tseg, K.tseg_cnt, K.tseg_cap, hasseg, seg, lane);
+                }
             }
         }
         STAMP(6)
@@ -1528,7 +1535,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *
         if (active) {
             const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
             const bool own = P.dslot_of[dm.period] == wslot;
-            dns_process(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
+            dns_process<false>(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
         }
     }
     if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
@@ -2036,7 +2043,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp(const PvParams *__r
             P.sfx_of[dm.idx] = (uint8_t)dns_suffix_of(P, R, m, dm.mlen, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8),
                                                       be16(R, m + 10));
         }
-        dns_process(P, (KeyCache<PV_NCACHE> *)nullptr, nullptr, &nev, &nresp, (uint64_t)(P.grid_main + blockIdx.x) * region, R,
+        dns_process<true>(P, (KeyCache<PV_NCACHE> *)nullptr, nullptr, &nev, &nresp, (uint64_t)(P.grid_main + blockIdx.x) * region, R,
                     dm, false, c);
     }
     __syncthreads();
