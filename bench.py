@@ -91,14 +91,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    step_ms, net_ms = [], []
     for _ in range(args.steps):
-        step()
+        ts = time.perf_counter()
+        step()  # ends with a device synchronisation
+        step_ms.append((time.perf_counter() - ts) * 1e3)
+        k, l = h.kernel_timing(reset=True)
+        net_ms.append(k / max(l, 1))
     h.synchronize()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    kms, launches = h.kernel_timing()
+    kms, launches = sum(net_ms), len(net_ms)
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed, kms / max(launches, 1)], dtype=torch.float64, device=device)
@@ -125,6 +130,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step_median": round(float(np.median(step_ms)), 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -136,6 +142,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profile(args.config, n),
                          "kernel": "pv_net_kernel", "kernel_ms": round(kernel_ms, 4),
+                         "kernel_ms_median": round(float(np.median(net_ms)), 4),
+                         "frac_median": round(algo_bytes / (float(np.median(net_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "bytes_per_launch": algo_bytes},
         }
         if args.read_ceiling:
@@ -214,6 +222,16 @@ def traffic_from_profile(cfg: int, n: int):
     return None
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg: int, seconds: float):
     """The oracle (CPU restatement of the reference handlers, oracle/pv_oracle.cpp) on a
     bounded sample of the same workload, timed on this host: one thread, then one
@@ -253,7 +271,7 @@ def cpu_baseline(cfg: int, seconds: float):
         t.join()
     dtn = time.perf_counter() - t0
     raten = n * reps_t * threads / dtn
-    return {"value": round(raten / 1e6, 4), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+    return {"value": round(raten / 1e6, 4), "unit": "Mpkt/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "sample": (f"{n} records of the same synthetic workload (in-memory pcap), oracle/pv_oracle.cpp: "
                        f"{threads} threads x {reps_t} passes in {dtn:.1f} s; one thread {rate1 / 1e6:.3f} Mpkt/s "
                        f"({reps} passes, {dt1:.1f} s)")}

@@ -238,6 +238,25 @@ typedef struct pv_region {
     uint32_t pad;
 } pv_region;
 int pv_window_regions(pv_ctx *ctx, pv_region *regions, uint32_t max, uint32_t *n);
+
+/* ---- RCCL over xGMI: one communicator per context (one process or thread per GPU).
+ * Replaces the reference's single-process merge of per-input handler buckets
+ * (AbstractMetricsManager::window_merged_json, src/AbstractMetricsManager.h:601-647, and
+ * the Policies' handler merge, src/Policies.cpp:420-446) for a context sharded across GPUs:
+ * SUM / MIN all-reduce of the live window regions in device memory, and an all-gather of
+ * host byte blobs (top-N lists, shard-edge stubs, quantile inputs). */
+#define PV_COMM_ID_BYTES 128
+/* ncclGetUniqueId: called on one rank, the bytes passed to every rank out of band */
+int pv_comm_unique_id(uint8_t id[PV_COMM_ID_BYTES]);
+/* ncclCommInitRank on the context's device */
+int pv_comm_init(pv_ctx *ctx, const uint8_t id[PV_COMM_ID_BYTES], int nranks, int rank);
+/* in-place all-reduce of every region pv_window_regions lists (u64 SUM / i64 MIN), one
+ * RCCL group on the context's stream; returns after the reduction completed */
+int pv_comm_allreduce_window(pv_ctx *ctx);
+/* all-gather of one host byte blob per rank: *out (pv_free) holds the blobs of ranks
+ * 0..n-1 back to back, sizes[r] their lengths (sizes has nranks entries) */
+int pv_comm_allgather(pv_ctx *ctx, const void *buf, size_t bytes, uint8_t **out, uint64_t *sizes);
+int pv_comm_destroy(pv_ctx *ctx);
 /* Compact the top-N tables of all live buckets into a host buffer of
  * (slot, metric, key, count, name) records (see pvgpu_topn_rec) for exchange;
  * pv_merge_topn adds such records from another rank into this context's view. */

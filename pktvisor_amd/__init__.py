@@ -156,7 +156,8 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_merge_topn", "pv_kernel_timing", "pv_window_regions", "pv_index_records_mt", "pv_host_register",
            "pv_host_unregister", "pv_ingest_timing", "pv_edge_export", "pv_edge_merge", "pv_values_export",
            "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code", "pv_advance_windows",
-           "pv_dns_event_seconds", "pv_dns_event_seconds_host"]
+           "pv_dns_event_seconds", "pv_dns_event_seconds_host", "pv_comm_unique_id", "pv_comm_init",
+           "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy"]
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
 
@@ -217,8 +218,21 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_window_periods.argtypes = [P, ctypes.c_int, P, P, U32, ctypes.POINTER(U32)]
     lib.pv_set_dns_filters.argtypes = [P, ctypes.POINTER(pv_dns_filters)]
     lib.pv_dns_code.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(U32)]
+    lib.pv_comm_unique_id.argtypes = [P]
+    lib.pv_comm_init.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
+    lib.pv_comm_allreduce_window.argtypes = [P]
+    lib.pv_comm_allgather.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), P]
+    lib.pv_comm_destroy.argtypes = [P]
     _lib = lib
     return lib
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId bytes for pv_comm_init (one rank creates, every rank receives)"""
+    buf = ctypes.create_string_buffer(128)
+    if load_library().pv_comm_unique_id(buf) != 0:
+        raise PvError("pv_comm_unique_id failed")
+    return buf.raw
 
 
 def device_count() -> int:
@@ -390,6 +404,34 @@ class PvHandlers:
         self._check(self.lib.pv_kernel_timing(self.ctx, ctypes.byref(ms), ctypes.byref(n), int(reset)),
                     "pv_kernel_timing")
         return ms.value, n.value
+
+    # ---- RCCL communicator in the library (pv_comm_*): a C++ host needs no torch
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        b = ctypes.create_string_buffer(bytes(uid), 128)
+        self._check(self.lib.pv_comm_init(self.ctx, b, nranks, rank), "pv_comm_init")
+        self.comm_ranks, self.comm_rank = nranks, rank
+
+    def comm_allreduce_window(self):
+        self._check(self.lib.pv_comm_allreduce_window(self.ctx), "pv_comm_allreduce_window")
+
+    def comm_allgather(self, blob: bytes):
+        """every rank's blob, in rank order"""
+        out = ctypes.c_void_p()
+        sizes = (ctypes.c_uint64 * self.comm_ranks)()
+        src = ctypes.create_string_buffer(bytes(blob), max(1, len(blob)))
+        self._check(self.lib.pv_comm_allgather(self.ctx, src, len(blob), ctypes.byref(out), sizes), "pv_comm_allgather")
+        try:
+            data = ctypes.string_at(out.value, sum(sizes)) if sum(sizes) else b""
+        finally:
+            self.lib.pv_free(out)
+        res, at = [], 0
+        for n in sizes:
+            res.append(data[at:at + n])
+            at += n
+        return res
+
+    def comm_destroy(self):
+        self._check(self.lib.pv_comm_destroy(self.ctx), "pv_comm_destroy")
 
     def window_regions(self):
         """[(device ptr, 64-bit words, PV_REDUCE_SUM | PV_REDUCE_MIN)] of both live windows, in the

@@ -17,6 +17,7 @@
 // reference estimator replayed exactly from per-coupon first-occurrence indices
 // (HIP for a single bucket, ICON after a union), bit-identical to datasketches.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <array>
@@ -112,7 +113,8 @@ enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNE
 #define ST_TP_CNT 32
 #define ST_TP_OFF (ST_TP_CNT + (1 << PV_MAX_REGIONS_LOG2))
 #define ST_TP_FILL (ST_TP_OFF + (1 << PV_MAX_REGIONS_LOG2))
-#define ST_ALLOC (ST_TP_FILL + (1 << PV_MAX_REGIONS_LOG2))
+#define ST_TP_TABS (ST_TP_FILL + (1 << PV_MAX_REGIONS_LOG2))
+#define ST_ALLOC (ST_TP_TABS + (1 << PV_MAX_REGIONS_LOG2))
 
 struct SlotMeta {
     int64_t start_sec = 0, start_nsec = 0, end_sec = 0, end_nsec = 0;
@@ -389,6 +391,9 @@ struct pv_ctx {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     double kernel_ms = 0;
     uint64_t kernel_launches = 0;
+    // RCCL communicator (pv_comm_*)
+    ncclComm_t comm = nullptr;
+    int comm_ranks = 0, comm_rank = 0;
     // DNS over TCP (pv_tcp.hip): segments emitted per batch, the TCP record tile masks and
     // their prefix maxima; the stage's buffers (allocated on first use), the flow table and
     // the double-buffered carry arena with its carried-flow lists
@@ -1240,6 +1245,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
 void pv_destroy(pv_ctx *c)
 {
     if (!c) return;
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
@@ -1716,6 +1722,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
     P.flags = c->d_status + ST_FLAGS;
     launch_fill32(c, c->d_status, ST_TP_CNT + (1u << c->reg_log2), 0);
+    launch_fill32(c, c->d_status + ST_TP_TABS, 1u << c->reg_log2, 0);
     hipError_t e;
     const uint64_t tiles = (n + 63) / 64; // 64-record wave tiles
     // persistent grid: exactly the workgroups that are resident at once (LDS/VGPR
@@ -1751,6 +1758,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.tp_cnt = c->d_status + ST_TP_CNT;
     P.tp_off = c->d_status + ST_TP_OFF;
     P.tp_fill = c->d_status + ST_TP_FILL;
+    P.tp_tabs = c->d_status + ST_TP_TABS;
     P.tp_buf = c->d_tpbuf;
     P.nn_cnt = c->d_status + ST_NNEW;
     P.nn = c->d_nn;
@@ -2373,6 +2381,105 @@ int pv_window_regions(pv_ctx *c, pv_region *r, uint32_t max, uint32_t *n)
     }
     *n = (uint32_t)v.size();
     for (uint32_t i = 0; i < v.size() && i < max; i++) r[i] = v[i];
+    return 0;
+}
+
+int pv_comm_unique_id(uint8_t id[PV_COMM_ID_BYTES])
+{
+    static_assert(sizeof(ncclUniqueId) == PV_COMM_ID_BYTES, "unique id size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return PV_EHIP;
+    memcpy(id, &u, sizeof u);
+    return 0;
+}
+
+int pv_comm_init(pv_ctx *c, const uint8_t id[PV_COMM_ID_BYTES], int nranks, int rank)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->comm) return c->fail(PV_EINVAL, "communicator already initialised");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return c->fail(PV_EINVAL, "rank %d of %d", rank, nranks);
+    hipSetDevice(c->device);
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        c->comm = nullptr;
+        return c->fail(PV_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    c->comm_ranks = nranks;
+    c->comm_rank = rank;
+    return 0;
+}
+
+int pv_comm_allreduce_window(pv_ctx *c)
+{
+    if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
+    std::vector<pv_region> v(4 * PV_SLOTS);
+    uint32_t n = 0;
+    if (int rc = pv_window_regions(c, v.data(), (uint32_t)v.size(), &n)) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    flush_fills(c);
+    ncclResult_t r = ncclGroupStart();
+    for (uint32_t i = 0; i < n && r == ncclSuccess; i++)
+        r = ncclAllReduce(v[i].ptr, v[i].ptr, v[i].words, v[i].op == PV_REDUCE_SUM ? ncclUint64 : ncclInt64,
+                          v[i].op == PV_REDUCE_SUM ? ncclSum : ncclMin, c->comm, c->stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess) return c->fail(PV_EHIP, "ncclAllReduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+    hipError_t e;
+    if (!hip_ok(e = hipStreamSynchronize(c->stream))) return c->hipfail(e, "window all-reduce");
+    return 0;
+}
+
+int pv_comm_allgather(pv_ctx *c, const void *buf, size_t bytes, uint8_t **out, uint64_t *sizes)
+{
+    *out = nullptr;
+    if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    const int R = c->comm_ranks;
+    hipError_t e;
+    uint64_t *d_sz = nullptr;
+    uint8_t *d_in = nullptr, *d_all = nullptr;
+    struct Free {
+        void *a, *b, *c;
+        ~Free() { for (void *p : {a, b, c}) if (p) hipFree(p); }
+    } fr{nullptr, nullptr, nullptr};
+    if (!hip_ok(e = hipMalloc(&d_sz, (size_t)R * 16))) return c->hipfail(e, "all-gather sizes");
+    fr.a = d_sz;
+    const uint64_t mine = bytes;
+    if (!hip_ok(e = hipMemcpyAsync(d_sz + R, &mine, 8, hipMemcpyHostToDevice, c->stream))) return c->hipfail(e, "all-gather sizes");
+    ncclResult_t r = ncclAllGather(d_sz + R, d_sz, 1, ncclUint64, c->comm, c->stream);
+    if (r != ncclSuccess) return c->fail(PV_EHIP, "ncclAllGather: %s", ncclGetErrorString(r));
+    if (!hip_ok(e = hipMemcpyAsync(sizes, d_sz, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "all-gather sizes");
+    uint64_t mx = 0, tot = 0;
+    for (int k = 0; k < R; k++) { mx = std::max(mx, sizes[k]); tot += sizes[k]; }
+    const size_t chunk = (size_t)std::max<uint64_t>(mx, 1);
+    if (!hip_ok(e = hipMalloc(&d_in, chunk)) || !hip_ok(e = hipMalloc(&d_all, chunk * R))) return c->hipfail(e, "all-gather buffers");
+    fr.b = d_in;
+    fr.c = d_all;
+    if (bytes && !hip_ok(e = hipMemcpyAsync(d_in, buf, bytes, hipMemcpyHostToDevice, c->stream))) return c->hipfail(e, "all-gather upload");
+    r = ncclAllGather(d_in, d_all, chunk, ncclUint8, c->comm, c->stream);
+    if (r != ncclSuccess) return c->fail(PV_EHIP, "ncclAllGather: %s", ncclGetErrorString(r));
+    std::vector<uint8_t> all(chunk * R);
+    if (!hip_ok(e = hipMemcpyAsync(all.data(), d_all, all.size(), hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "all-gather download");
+    uint8_t *o = (uint8_t *)malloc(std::max<uint64_t>(tot, 1));
+    if (!o) return c->fail(PV_ECAPACITY, "all-gather result");
+    uint64_t at = 0;
+    for (int k = 0; k < R; k++) { memcpy(o + at, all.data() + (size_t)k * chunk, sizes[k]); at += sizes[k]; }
+    *out = o;
+    return 0;
+}
+
+int pv_comm_destroy(pv_ctx *c)
+{
+    if (!c->comm) return 0;
+    ncclCommDestroy(c->comm);
+    c->comm = nullptr;
     return 0;
 }
 

@@ -56,6 +56,7 @@
 #endif
 #define PV_WINW (PV_WIN / 4)
 #define PV_NWIN 192 // bytes of each record staged by pv_topn_names
+#define PV_NOUT 6144 // bytes of name records a pv_topn_names wave packs in LDS before its copy-out
 
 // ------------------------------------------------------------------ byte access
 // recs is 256-B aligned and padded by >= 256 bytes: two aligned dword loads and
@@ -190,8 +191,8 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     uint8_t *arena = P.arena + (uint64_t)tab * P.arena_cap;
     if (metric == TM_IPV6) {
         uint64_t a = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
-        uint64_t pos = atomicAdd(top, 18ull);
-        if (pos + 18 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+        uint64_t pos = atomicAdd(top, 20ull); // records are 4-byte multiples (pv_topn_names copies dwords)
+        if (pos + 20 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
         pos += part * pcap;
         arena[pos] = 16; arena[pos + 1] = 0;
         for (int i = 0; i < 16; i++) arena[pos + 2 + i] = (uint8_t)R.u8(a + i);
@@ -204,8 +205,8 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
         // the query's ECS address: family byte + 16 address bytes (the host formats it)
         uint64_t addr = 0;
         const uint32_t fam = dns_ecs(R, m, len, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8), be16(R, m + 10), addr);
-        uint64_t pos = atomicAdd(top, 19ull);
-        if (pos + 19 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+        uint64_t pos = atomicAdd(top, 20ull);
+        if (pos + 20 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
         pos += part * pcap;
         arena[pos] = 17; arena[pos + 1] = 0; arena[pos + 2] = (uint8_t)fam;
         for (int i = 0; i < 16; i++) arena[pos + 3 + i] = i < 8 ? (uint8_t)(addr >> (8 * i)) : 0;
@@ -225,7 +226,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
         if (start < 0) start = (int)n;
     }
     uint32_t slen = n - (uint32_t)start;
-    uint64_t pos = atomicAdd(top, (unsigned long long)(slen + 2));
+    uint64_t pos = atomicAdd(top, (unsigned long long)((slen + 2 + 3) & ~3u));
     if (pos + slen + 2 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
     pos += part * pcap;
     arena[pos] = (uint8_t)(slen & 0xff);
@@ -1588,6 +1589,11 @@ __device__ __forceinline__ uint32_t ip4_coupon(uint32_t ip)
     return cpc_coupon(h1, h2);
 }
 
+// table of an update-log entry (slot in bits 60..63, the key's metric)
+__device__ __forceinline__ uint32_t entry_table(uint64_t e0)
+{
+    return PV_TSLOT((uint32_t)(e0 >> 60), PV_KEY_METRIC(e0 & ((1ull << 60) - 1)));
+}
 __device__ __forceinline__ uint32_t log_region(PV_CREF(PvParams) P, uint64_t e0)
 {
     return tregion(P, tkey_hash(e0 & ((1ull << 60) - 1)));
@@ -1716,15 +1722,24 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_scatter(const PvParams
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ uint32_t h[1u << PV_MAX_REGIONS_LOG2];
+    __shared__ uint32_t tb[1u << PV_MAX_REGIONS_LOG2]; // tables (bit per PV_TSLOT) with updates in each region
     const uint32_t nreg = 1u << P.reg_log2;
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) h[r] = 0;
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) { h[r] = 0; tb[r] = 0; }
     __syncthreads();
     const uint32_t cnt = P.cb_cnt[blockIdx.x];
     const PV_G uint64_t *q = P.cb + (uint64_t)blockIdx.x * P.mq_cap * 2;
-    batched<8>(cnt, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) { atomicAdd(&h[log_region(P, e0)], 1u); });
+    batched<8>(cnt, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) {
+        const uint32_t r = log_region(P, e0);
+        atomicAdd(&h[r], 1u);
+        const uint32_t bit = 1u << entry_table(e0);
+        if (!(tb[r] & bit)) atomicOr(&tb[r], bit);
+    });
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
-        if (h[r]) h[r] = atomicAdd(&P.tp_fill[r], h[r]);
+        if (h[r]) {
+            h[r] = atomicAdd(&P.tp_fill[r], h[r]);
+            atomicOr(&P.tp_tabs[r], tb[r]);
+        }
     __syncthreads();
     batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
         const uint32_t pos = atomicAdd(&h[log_region(P, e.x)], 1u);
@@ -1738,13 +1753,8 @@ struct MergeState {
     uint32_t mn[2][PV_RS]; // smallest record index of an IPv4 key per direction (CPC)
     uint32_t nidx[PV_RS]; // entries created in this batch: region index, source record
     uint32_t nrep[PV_RS];
-    uint32_t nnew, tabs, nbase;
+    uint32_t nnew, nbase;
 };
-// table of an update-log entry (slot in bits 60..63, the key's metric)
-__device__ __forceinline__ uint32_t entry_table(uint64_t e0)
-{
-    return PV_TSLOT((uint32_t)(e0 >> 60), PV_KEY_METRIC(e0 & ((1ull << 60) - 1)));
-}
 
 extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams *__restrict__ Pp)
 {
@@ -1772,12 +1782,9 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
     __shared__ MergeState S;
     const uint32_t rsl = P.tcap_log2 - P.reg_log2;
     const uint32_t rs = 1u << rsl;
-    if (threadIdx.x == 0) S.tabs = 0;
-    __syncthreads();
-    batched<8>(n, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) { atomicOr(&S.tabs, 1u << entry_table(e0)); });
-    __syncthreads();
     static_assert(PV_TABLES <= 32, "table mask");
-    uint32_t tabs = S.tabs;
+    uint32_t tabs = P.tp_tabs[r]; // the tables pv_topn_scatter saw in this region's updates
+    const bool one = !(tabs & (tabs - 1));
     while (tabs) {
         const uint32_t tb = __builtin_ctz(tabs);
         const uint32_t s = tb % PV_SLOTS; // the handler slot (Net for tb < PV_SLOTS, else DNS)
@@ -1794,7 +1801,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         __syncthreads();
         batched<8>(n, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
             const uint64_t e0 = e.x;
-            if (entry_table(e0) != tb) return;
+            if (!one && entry_table(e0) != tb) return;
             const uint64_t e1 = e.y;
             const uint64_t key = e0 & ((1ull << 60) - 1);
             uint32_t pos = (uint32_t)tkey_hash(key) & (rs - 1);
@@ -1860,9 +1867,13 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
     // headers and, for a plain DNS message, the whole first question, so the record is
     // parsed and its name decoded from LDS after one round of loads
     __shared__ uint32_t stage[4][PV_NWIN / 4 * 64];
+    // the wave's name records, packed as they will lie in the arena, then copied out with
+    // coalesced dword stores (byte stores of each lane's name were one write request per byte)
+    __shared__ uint32_t obuf[4][PV_NOUT / 4];
     const uint32_t n = min(*P.nn_cnt, P.nn_cap);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t *L = stage[threadIdx.x >> 6];
+    uint8_t *O = reinterpret_cast<uint8_t *>(obuf[threadIdx.x >> 6]);
     const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
     const GAcc G{P.recs};
     for (uint32_t b = blockIdx.x * blockDim.x; b < n; b += gridDim.x * blockDim.x) {
@@ -1928,34 +1939,52 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
             if (lane >= (uint32_t)o2) incl += v;
         }
         const uint32_t tot = __shfl(incl, 63, 64);
+        const uint32_t tot4 = (tot + 3) & ~3u; // arena allocations are dword multiples
         const uint32_t part = (blockIdx.x * 4 + (threadIdx.x >> 6)) & (PV_ARENA_PARTS - 1);
         const uint32_t s0 = __shfl(e.slot, 0, 64);
         const bool uniform = __all(!act || e.slot == s0);
-        uint64_t pos = 0;
+        const bool packed = uniform && tot4 <= PV_NOUT;
+        auto emit_to = [&](uint8_t *dst) {
+            const uint32_t slen = size - 2;
+            dst[0] = (uint8_t)(slen & 0xff);
+            dst[1] = (uint8_t)(slen >> 8);
+            if (metric == TM_IPV6) {
+                for (int k = 0; k < 16; k++) dst[2 + k] = (uint8_t)G.u8(a6 + k);
+            } else if (slen > 0 && nl > 0) {
+                CopyEmit ce{dst + 2, start, 0, (metric == TM_SLOW_IN || metric == TM_SLOW_OUT) ? 1u : 0u};
+                name_emit(R, m, mlen, 12, ce);
+            }
+        };
         if (uniform) {
             unsigned long long wb = 0;
-            if (lane == 0 && tot) wb = atomicAdd((unsigned long long *)&P.arena_top[s0 * PV_ARENA_PARTS + part], (unsigned long long)tot);
+            if (lane == 0 && tot) wb = atomicAdd((unsigned long long *)&P.arena_top[s0 * PV_ARENA_PARTS + part], (unsigned long long)tot4);
             wb = __shfl(wb, 0, 64);
-            pos = wb + incl - size;
+            const bool room = wb + tot4 <= pcap;
+            if (!room) {
+                if (act) atomicOr(P.flags, PVF_ARENA_FULL);
+            } else {
+                uint8_t *arena = P.arena + (uint64_t)s0 * P.arena_cap + part * pcap + wb;
+                if (packed) {
+                    if (act) emit_to(O + incl - size);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (uint32_t k = lane * 4; k < tot4; k += 256)
+                        *reinterpret_cast<uint32_t *>(arena + k) = *reinterpret_cast<const uint32_t *>(O + k);
+                    __builtin_amdgcn_wave_barrier();
+                } else if (act) {
+                    emit_to(arena + incl - size);
+                }
+                if (act) P.taux[e.pos] = (uint32_t)(part * pcap + wb + incl - size) + 1;
+            }
         } else if (act) {
-            pos = atomicAdd((unsigned long long *)&P.arena_top[e.slot * PV_ARENA_PARTS + part], (unsigned long long)size);
-        }
-        if (act) {
+            const uint64_t pos = atomicAdd((unsigned long long *)&P.arena_top[e.slot * PV_ARENA_PARTS + part],
+                                           (unsigned long long)((size + 3) & ~3u));
             if (pos + size > pcap) {
                 atomicOr(P.flags, PVF_ARENA_FULL);
             } else {
-                pos += part * pcap;
-                uint8_t *arena = P.arena + (uint64_t)e.slot * P.arena_cap;
-                const uint32_t slen = size - 2;
-                arena[pos] = (uint8_t)(slen & 0xff);
-                arena[pos + 1] = (uint8_t)(slen >> 8);
-                if (metric == TM_IPV6) {
-                    for (int k = 0; k < 16; k++) arena[pos + 2 + k] = (uint8_t)G.u8(a6 + k);
-                } else if (slen > 0 && nl > 0) {
-                    CopyEmit ce{arena + pos + 2, start, 0, (metric == TM_SLOW_IN || metric == TM_SLOW_OUT) ? 1u : 0u};
-                    name_emit(R, m, mlen, 12, ce);
-                }
-                P.taux[e.pos] = (uint32_t)pos + 1;
+                emit_to(P.arena + (uint64_t)e.slot * P.arena_cap + part * pcap + pos);
+                P.taux[e.pos] = (uint32_t)(part * pcap + pos) + 1;
             }
         }
     }

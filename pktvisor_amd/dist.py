@@ -146,49 +146,59 @@ def process_shard(handlers, recs, index, start_sec: int, start_nsec: int = 0, gr
     return plan
 
 
-def check_aligned(handlers, group=None):
+def _allgather(handlers, blob, group=None, comm=None):
+    """every rank's host blob, in rank order: the library's RCCL communicator (comm="pv",
+    pv_comm_allgather) or torch.distributed"""
+    if comm == "pv":
+        return handlers.comm_allgather(blob)
+    allv = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allv, blob, group=group)
+    return allv
+
+
+def _rank(handlers, group=None, comm=None):
+    return handlers.comm_rank if comm == "pv" else dist.get_rank(group)
+
+
+def check_aligned(handlers, group=None, comm=None):
     """The bucket merge pairs slots by id: every rank's windows must hold the same periods
     (slot, start second) — what the global plan guarantees; checked before the merge."""
+    import json
     from pktvisor_amd import PART_DNS, PART_NET
-    mine = (handlers.window_periods(PART_NET), handlers.window_periods(PART_DNS))
-    allv = [None] * dist.get_world_size(group)
-    dist.all_gather_object(allv, mine, group=group)
+    mine = json.dumps([handlers.window_periods(PART_NET), handlers.window_periods(PART_DNS)]).encode()
+    allv = _allgather(handlers, mine, group, comm)
     if any(v != allv[0] for v in allv):
         raise RuntimeError(f"shard windows differ across ranks: {allv}")
 
-def merge_edges(handlers, group=None):
-    exports = [None] * dist.get_world_size(group)
-    dist.all_gather_object(exports, handlers.edge_export(), group=group)
-    handlers.edge_merge(exports, dist.get_rank(group))
+
+def merge_edges(handlers, group=None, comm=None):
+    handlers.edge_merge(_allgather(handlers, handlers.edge_export(), group, comm), _rank(handlers, group, comm))
 
 
-def merge_values(handlers, group=None):
-    world = dist.get_world_size(group)
-    allv = [None] * world
-    dist.all_gather_object(allv, handlers.values_export(), group=group)
-    me = dist.get_rank(group)
-    for r, data in enumerate(allv):
+def merge_values(handlers, group=None, comm=None):
+    me = _rank(handlers, group, comm)
+    for r, data in enumerate(_allgather(handlers, handlers.values_export(), group, comm)):
         if r != me and data:
             handlers.values_merge(data)
 
 
-def merge_window(handlers, device, group=None):
-    """Full merge of every rank's shard into every rank's handlers (read path)."""
+def merge_window(handlers, device, group=None, comm=None):
+    """Full merge of every rank's shard into every rank's handlers (read path). comm="pv"
+    runs every collective on the library's own RCCL communicator (pv_comm_init first)."""
     handlers.synchronize()
-    check_aligned(handlers, group)
-    merge_edges(handlers, group)
-    merge_values(handlers, group)
-    reduce_handlers(handlers, device, group)
-    merge_topn(handlers, group)
+    check_aligned(handlers, group, comm)
+    merge_edges(handlers, group, comm)
+    merge_values(handlers, group, comm)
+    if comm == "pv":
+        handlers.comm_allreduce_window()
+    else:
+        reduce_handlers(handlers, device, group)
+    merge_topn(handlers, group, comm)
 
 
-def merge_topn(handlers, group=None):
+def merge_topn(handlers, group=None, comm=None):
     """Exchange exact per-rank top-N counts (host records) and add the other ranks' into this view."""
-    mine = handlers.export_topn()
-    world = dist.get_world_size(group)
-    allv = [None] * world
-    dist.all_gather_object(allv, mine, group=group)
-    me = dist.get_rank(group)
-    for r, data in enumerate(allv):
+    me = _rank(handlers, group, comm)
+    for r, data in enumerate(_allgather(handlers, handlers.export_topn(), group, comm)):
         if r != me and data:
             handlers.merge_topn(data)

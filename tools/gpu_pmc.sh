@@ -1,16 +1,21 @@
 #!/bin/bash
-# PMC passes (one counter group per run, kernel-trace only) on the C2 bench + ablation timings
+# rocprofv3 PMC passes (one counter group per run, each under its own time limit) over the
+# bench's C2 / C3 / C4 steps; tools/pmc_summary.py folds them into per-kernel means.
+set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-mkdir -p gpurun_out
+OUT=${OUT:-gpurun_out/pmc}
+mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
-P="rocprofv3 --kernel-trace --output-format csv"
-timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --net-groups 1 --dns-groups 2 > gpurun_out/pmc_abl_ctr.log 2>&1 &&
-timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --net-groups 3 --dns-groups 2 > gpurun_out/pmc_abl_card.log 2>&1 &&
-timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --net-groups 9 --dns-groups 2 > gpurun_out/pmc_abl_top.log 2>&1 &&
-timeout -k 10 300 $P --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/pmc1 -o c2 -- $B > gpurun_out/pmc1.log 2>&1 &&
-timeout -k 10 300 $P --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE -d gpurun_out/pmc2 -o c2 -- $B > gpurun_out/pmc2.log 2>&1 &&
-timeout -k 10 300 $P --pmc FETCH_SIZE -d gpurun_out/pmc3 -o c2 -- $B > gpurun_out/pmc3.log 2>&1 &&
-timeout -k 10 300 $P --pmc WRITE_SIZE -d gpurun_out/pmc4 -o c2 -- $B > gpurun_out/pmc4.log 2>&1 &&
-timeout -k 10 300 $P --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum -d gpurun_out/pmc5 -o c2 -- $B > gpurun_out/pmc5.log 2>&1
-echo "chain exit $?"
+B="$PWD/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e"
+P1="FETCH_SIZE"
+P2="WRITE_SIZE TCC_HIT TCC_MISS"
+P3="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"
+P4="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM"
+for c in ${CFGS:-2 3 4}; do
+  for p in 1 2 3 4; do
+    eval "CTR=\$P$p"
+    (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc $CTR --kernel-include-regex 'pv_.*' --output-format csv \
+        -d $GRAFT_REPO_ROOT/$OUT/c${c}_p$p -o run -- python3 $B --config $c > $GRAFT_REPO_ROOT/$OUT/c${c}_p$p.log 2>&1) || exit 1
+    echo "c$c p$p done"
+  done
+done
