@@ -308,6 +308,8 @@ struct pv_ctx {
     uint64_t *d_tpbuf = nullptr; // the logs bucketed by table region (same size)
     uint64_t *d_cb = nullptr;    // combined update lists (same size)
     uint32_t *d_cb_cnt = nullptr;
+    uint32_t *d_cb_h = nullptr;  // per combine workgroup: entries per region
+    uint32_t cb_h_grid = 0;
     PvNewName *d_nn = nullptr;   // entries created by pv_topn_merge (names pending)
     uint64_t *d_iplog = nullptr; // dense IP log, one u64 per record (max_records + one tile)
     uint64_t *d_trash = nullptr; // 64 B per Net-pass wave
@@ -1249,7 +1251,7 @@ void pv_destroy(pv_ctx *c)
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
-                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
+                    c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_cb_h, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
                     c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx,
                     c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
@@ -1743,14 +1745,23 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         if (need > c->mq_bytes) {
             if (c->d_mq) hipFree(c->d_mq);
             if (c->d_tpbuf) hipFree(c->d_tpbuf);
+
             if (c->d_cb) hipFree(c->d_cb);
             c->d_mq = c->d_tpbuf = c->d_cb = nullptr;
             c->mq_bytes = 0;
             if (!hip_ok(e = hipMalloc(&c->d_mq, need)) || !hip_ok(e = hipMalloc(&c->d_tpbuf, need)) ||
+
                 !hip_ok(e = hipMalloc(&c->d_cb, need)))
                 return c->hipfail(e, "top-N update log");
             c->mq_bytes = need;
         }
+    }
+    if (grid > c->cb_h_grid) {
+        if (c->d_cb_h) hipFree(c->d_cb_h);
+        c->d_cb_h = nullptr;
+        c->cb_h_grid = 0;
+        if (!hip_ok(e = hipMalloc(&c->d_cb_h, (size_t)grid << (PV_MAX_REGIONS_LOG2 + 2)))) return c->hipfail(e, "region counts");
+        c->cb_h_grid = grid;
     }
     P.mq = c->d_mq;
     P.mq_cnt = c->d_mq_cnt;
@@ -1759,6 +1770,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.tp_off = c->d_status + ST_TP_OFF;
     P.tp_fill = c->d_status + ST_TP_FILL;
     P.tp_tabs = c->d_status + ST_TP_TABS;
+    P.cb_h = c->d_cb_h;
     P.tp_buf = c->d_tpbuf;
     P.nn_cnt = c->d_status + ST_NNEW;
     P.nn = c->d_nn;

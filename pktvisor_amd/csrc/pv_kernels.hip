@@ -1687,8 +1687,12 @@ extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine(cons
     for (uint32_t j = threadIdx.x; j < PV_CB_N; j += blockDim.x)
         if (S.key[j]) comb_out(P, S, out, S.key[j], S.cnt[j], S.rep[j]);
     __syncthreads();
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
+    // the workgroup's region counts, for pv_topn_scatter's reservations
+    PV_G uint32_t *hc = P.cb_h + (uint64_t)blockIdx.x * nreg;
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) {
+        hc[r] = S.h[r];
         if (S.h[r]) atomicAdd(&P.tp_cnt[r], S.h[r]);
+    }
     if (threadIdx.x == 0) P.cb_cnt[blockIdx.x] = S.nout;
 }
 
@@ -1724,27 +1728,27 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_scatter(const PvParams
     __shared__ uint32_t h[1u << PV_MAX_REGIONS_LOG2];
     __shared__ uint32_t tb[1u << PV_MAX_REGIONS_LOG2]; // tables (bit per PV_TSLOT) with updates in each region
     const uint32_t nreg = 1u << P.reg_log2;
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) { h[r] = 0; tb[r] = 0; }
+    // reserve this workgroup's share of every region (counts from pv_topn_combine), then
+    // one pass over its combined entries: place each, note the tables each region touches
+    const PV_G uint32_t *hc = P.cb_h + (uint64_t)blockIdx.x * nreg;
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) {
+        const uint32_t c = hc[r];
+        h[r] = c ? atomicAdd(&P.tp_fill[r], c) : 0u;
+        tb[r] = 0;
+    }
     __syncthreads();
     const uint32_t cnt = P.cb_cnt[blockIdx.x];
     const PV_G uint64_t *q = P.cb + (uint64_t)blockIdx.x * P.mq_cap * 2;
-    batched<8>(cnt, [&](uint64_t j) { return q[2 * j]; }, [&](uint64_t, uint64_t e0) {
-        const uint32_t r = log_region(P, e0);
-        atomicAdd(&h[r], 1u);
-        const uint32_t bit = 1u << entry_table(e0);
+    batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
+        const uint32_t r = log_region(P, e.x);
+        const uint32_t pos = atomicAdd(&h[r], 1u);
+        reinterpret_cast<PV_G ulonglong2 *>(P.tp_buf)[pos] = e;
+        const uint32_t bit = 1u << entry_table(e.x);
         if (!(tb[r] & bit)) atomicOr(&tb[r], bit);
     });
     __syncthreads();
     for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
-        if (h[r]) {
-            h[r] = atomicAdd(&P.tp_fill[r], h[r]);
-            atomicOr(&P.tp_tabs[r], tb[r]);
-        }
-    __syncthreads();
-    batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
-        const uint32_t pos = atomicAdd(&h[log_region(P, e.x)], 1u);
-        reinterpret_cast<PV_G ulonglong2 *>(P.tp_buf)[pos] = e;
-    });
+        if (tb[r]) atomicOr(&P.tp_tabs[r], tb[r]);
 }
 
 struct MergeState {

@@ -116,6 +116,21 @@ PV_FN uint64_t ph_step(uint64_t h, uint32_t c)
     const uint32_t lo = (uint32_t)h * PB1 + (c + 1), hi = (uint32_t)(h >> 32) * PB2 + (c + 1);
     return ((uint64_t)hi << 32) | lo;
 }
+// four ph_steps over the bytes of x (low byte first), in one Horner step per lane:
+// h * B^4 + (c0+1) B^3 + (c1+1) B^2 + (c2+1) B + (c3+1)  (mod 2^32 per lane)
+#define PB1_2 (PB1 * PB1)
+#define PB1_3 (PB1_2 * PB1)
+#define PB1_4 (PB1_2 * PB1_2)
+#define PB2_2 (PB2 * PB2)
+#define PB2_3 (PB2_2 * PB2)
+#define PB2_4 (PB2_2 * PB2_2)
+PV_FN uint64_t ph_step4(uint64_t h, uint32_t x)
+{
+    const uint32_t c0 = (x & 0xff) + 1, c1 = ((x >> 8) & 0xff) + 1, c2 = ((x >> 16) & 0xff) + 1, c3 = (x >> 24) + 1;
+    const uint32_t lo = (uint32_t)h * PB1_4 + c0 * PB1_3 + c1 * PB1_2 + c2 * PB1 + c3;
+    const uint32_t hi = (uint32_t)(h >> 32) * PB2_4 + c0 * PB2_3 + c1 * PB2_2 + c2 * PB2 + c3;
+    return ((uint64_t)hi << 32) | lo;
+}
 PV_FN uint64_t powb(uint32_t e) // (PB1^e, PB2^e)
 {
     uint32_t r1 = 1, r2 = 1, b1 = PB1, b2 = PB2;
@@ -589,19 +604,24 @@ PV_FN bool name_stats_fast(const A &R, uint64_t m, uint32_t len, uint32_t off, N
             bad |= ((~ok & 0x80808080u) & vm & ~dm) != 0;
             x = ((x & ~dm) | (0x2e2e2e2eu & dm)) & vm;
             w[q] = x;
-            // Horner over the valid bytes; a tracked dot takes the hash before its byte
-            uint64_t hv[4];
+            // Horner over the valid bytes; a tracked dot takes the hash before its byte. A
+            // whole dword without a tracked dot (the common case) is one ph_step4.
+            const bool tracked = ((t[0] - p) < 4) | ((t[1] - p) < 4) | ((t[2] - p) < 4) | ((t[3] - p) < 4);
+            if (nv == 4 && !tracked) {
+                ph = ph_step4(ph, x);
+            } else {
+                uint64_t hv[4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                hv[r] = ph;
-                if ((uint32_t)r < nv) ph = ph_step(ph, (x >> (8 * r)) & 0xff);
-            }
-            // a tracked dot in this dword is rare: test all four at once, select only then
-            if (((t[0] - p) < 4) | ((t[1] - p) < 4) | ((t[2] - p) < 4) | ((t[3] - p) < 4)) {
+                for (int r = 0; r < 4; r++) {
+                    hv[r] = ph;
+                    if ((uint32_t)r < nv) ph = ph_step(ph, (x >> (8 * r)) & 0xff);
+                }
+                if (tracked) {
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t rel = t[k] - p;
-                    if (rel < 4) hk[k] = rel == 0 ? hv[0] : rel == 1 ? hv[1] : rel == 2 ? hv[2] : hv[3];
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t rel = t[k] - p;
+                        if (rel < 4) hk[k] = rel == 0 ? hv[0] : rel == 1 ? hv[1] : rel == 2 ? hv[2] : hv[3];
+                    }
                 }
             }
         }
