@@ -28,6 +28,9 @@ def _lib():
         g.pvgen_records.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                     ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]
         g.pvgen_records.restype = ctypes.c_int64
+        g.pvgen_records_at.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]
+        g.pvgen_records_at.restype = ctypes.c_int64
         g.pvgen_bound.argtypes = [ctypes.c_int, ctypes.c_uint64]
         g.pvgen_bound.restype = ctypes.c_uint64
         _gen = g
@@ -46,6 +49,37 @@ def records(cfg: int, n: int, seed: int | None = None, ts_step_us: int = 1, with
     if got != n:
         raise RuntimeError(f"pvgen failed for cfg {cfg}: {got}")
     return buf[: used.value + 256], offs, used.value
+
+
+T0_US = 1700000000 * 1000000  # the generator's first timestamp
+
+
+def stream_shard(cfg: int, lo: int, hi: int, seed: int, ts_step_us: int = 1, chunk: int = 10_000_000, progress=None):
+    """Records [lo, hi) of a synthetic stream of the config's shape at ts_step_us per record:
+    generated in chunks of `chunk` records (each its own seed, timestamps continuing at
+    T0 + index * step), returned as one np.uint8 array (+256 B zero padding) and its used bytes."""
+    g = _lib()
+    parts, total = [], 0
+    for a in range(lo, hi, chunk):
+        b = min(hi, a + chunk)
+        cap = int(g.pvgen_bound(cfg, b - a))
+        buf = np.zeros(cap, dtype=np.uint8)
+        used = ctypes.c_size_t()
+        got = g.pvgen_records_at(cfg, b - a, seed + 104729 * (a // chunk), ts_step_us, T0_US + a * ts_step_us,
+                                 buf.ctypes.data, cap, ctypes.byref(used), None)
+        if got != b - a:
+            raise RuntimeError(f"pvgen failed for cfg {cfg}: {got}")
+        parts.append(buf[: used.value].copy())
+        del buf
+        total += used.value
+        if progress:
+            progress(b - lo)
+    out = np.zeros(total + 256, dtype=np.uint8)
+    at = 0
+    for p in parts:
+        out[at:at + len(p)] = p
+        at += len(p)
+    return out, total
 
 
 def pcap_bytes(cfg: int, n: int, seed: int | None = None, ts_step_us: int = 1) -> bytes:

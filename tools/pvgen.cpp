@@ -387,10 +387,10 @@ extern "C" {
 // Generates `n` records for config `cfg` into buf[cap] (classic-pcap record
 // format, no global header). offs (optional) receives each record's offset.
 // Returns the number of records written, or -1 if cap was too small.
-int64_t pvgen_records(int cfg, uint64_t n, uint64_t seed, uint32_t ts_step_us, uint8_t *buf, size_t cap, size_t *used,
-                      uint32_t *offs)
+int64_t pvgen_records_at(int cfg, uint64_t n, uint64_t seed, uint32_t ts_step_us, uint64_t start_us, uint8_t *buf, size_t cap,
+                         size_t *used, uint32_t *offs)
 {
-    Out o{buf, cap, 0, offs, 0, 1700000000ull * 1000000ull, ts_step_us ? ts_step_us : 1u};
+    Out o{buf, cap, 0, offs, 0, start_us, ts_step_us ? ts_step_us : 1u};
     Rng r(seed);
     switch (cfg) {
     case 1: gen_mix(o, n, r, 1.0, 200); break;
@@ -402,6 +402,12 @@ int64_t pvgen_records(int cfg, uint64_t n, uint64_t seed, uint32_t ts_step_us, u
     }
     *used = o.used;
     return o.ok ? (int64_t)o.nrec : -1;
+}
+
+int64_t pvgen_records(int cfg, uint64_t n, uint64_t seed, uint32_t ts_step_us, uint8_t *buf, size_t cap, size_t *used,
+                      uint32_t *offs)
+{
+    return pvgen_records_at(cfg, n, seed, ts_step_us, 1700000000ull * 1000000ull, buf, cap, used, offs);
 }
 
 // Upper bound of bytes needed for n records of a config.
