@@ -81,6 +81,8 @@ extern "C" __global__ void pv_topn_combine(const PvParams *P);
 extern "C" __global__ void pv_topn_scan(const PvParams *P);
 extern "C" __global__ void pv_topn_scatter(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
+extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_t *theta_out);
+extern "C" __global__ void pv_topn_compact(const PvParams *P, uint32_t tb, uint8_t *tmp, unsigned long long *tmp_top);
 extern "C" __global__ void pv_topn_names(const PvParams *P);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
@@ -346,6 +348,13 @@ struct pv_ctx {
     size_t xvals_synced = 0;
     float from90 = 0.0f, to90 = 0.0f; // DnsMetricsManager::_from90th / _to90th
     uint32_t *d_status = nullptr;
+    // bounded top-N tables: entries per table (device, read back with each batch's status),
+    // each purged region's accumulated theta (the estimate offset of its survivors)
+    uint32_t *d_tab_live = nullptr, *h_tab_live = nullptr, *d_theta = nullptr;
+    uint8_t *d_ctmp = nullptr;          // arena compaction scratch (one table's arena)
+    unsigned long long *d_ctop = nullptr;
+    std::vector<uint64_t> roff[PV_TABLES];
+    uint64_t purges = 0;
     // DNS v1 filters (pv_set_dns_filters): PVF_* bits, only_rcode mask, answer_count, only_qtype
     uint32_t f_flags = 0, f_rcode_mask = 0, f_ancount = 0, f_nq = 0;
     uint16_t f_qt[PV_MAX_QTYPES] = {};
@@ -546,6 +555,8 @@ void clear_part(pv_ctx *c, int part, uint32_t s)
     launch_fill64(c, c->d_tcnt + t * tcap, tcap, 0);
     launch_fill32(c, c->d_taux + t * tcap, tcap, 0);
     launch_fill64(c, c->d_arena_top + (uint64_t)t * PV_ARENA_PARTS, PV_ARENA_PARTS, 0);
+    launch_fill32(c, c->d_tab_live + t, 1, 0);
+    c->roff[t].clear();
     w.clean[s] = true;
 }
 
@@ -610,9 +621,13 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out) // s: table (PV_T
         if (used && !hip_ok(e = hipMemcpy(parts[p].data(), c->d_arena + s * c->arena_cap + p * pcap, used, hipMemcpyDeviceToHost)))
             return c->hipfail(e, "read name arena");
     }
+    const std::vector<uint64_t> &roff = c->roff[s];
     for (uint64_t i = 0; i < tcap; i++) {
         if (!keys[i]) continue;
-        TopRec r{keys[i], cnt[i], std::string()};
+        // a purged region's survivors report count + the thetas its purges subtracted (the
+        // frequent-items estimate, exact for a key no purge dropped)
+        const uint64_t off = roff.empty() ? 0 : roff[(i >> (c->tcap_log2 - c->reg_log2))];
+        TopRec r{keys[i], cnt[i] + off, std::string()};
         uint32_t m = PV_KEY_METRIC(keys[i]);
         if (m == TM_IPV4) {
             uint32_t ip = (uint32_t)keys[i];
@@ -1215,6 +1230,10 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
         !hip_ok(e = hipMalloc(&c->d_status, ST_ALLOC * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_tab_live, PV_TABLES * 4)) ||
+        !hip_ok(e = hipMemset(c->d_tab_live, 0, PV_TABLES * 4)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_tab_live, PV_TABLES * 4, hipHostMallocDefault)) ||
+        !hip_ok(e = hipMalloc(&c->d_theta, ((size_t)1 << c->reg_log2) * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
         !hip_ok(e = hipMalloc(&c->d_iplog, (size_t)(mr + 64) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_trash, (size_t)PV_TRASH_WAVES * 2048)) ||
@@ -1256,11 +1275,12 @@ void pv_destroy(pv_ctx *c)
                     c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx,
                     c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
-                    c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx};
+                    c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
+                    c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
     for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
-                     (void *)c->h_tparams})
+                     (void *)c->h_tparams, (void *)c->h_tab_live})
         if (hp) hipHostFree(hp);
     for (auto &st : c->stage) {
         if (st.h_recs) hipHostFree(st.h_recs);
@@ -1672,6 +1692,53 @@ uint32_t tcp_pass(pv_ctx *c, const PvParams &P, uint64_t a, uint64_t b, hipStrea
 
 // One device batch with at most PV_MAX_SHIFTS shifts of each manager. nsh / dsh: the Net and
 // DNS shifts inside it (record indices relative to d_offs).
+// Bounded top-N (the frequent-items sketch's purge as TopN uses it, src/Metrics.h:488-503):
+// a table holding more than half its capacity after a batch has each region purged at its
+// median count (pv_topn_purge); the thetas become the estimate offsets read_topn adds. The
+// name arena of a purged table is compacted once its fullest partition is half used. The
+// live counts are the ones read back with the batch status (names added by the transaction
+// pass afterwards are counted at the next batch).
+int purge_tables(pv_ctx *c, hipStream_t st)
+{
+    const uint64_t tcap = 1ull << c->tcap_log2;
+    const uint32_t nreg = 1u << c->reg_log2;
+    hipError_t e;
+    for (uint32_t t = 0; t < PV_TABLES; t++) {
+        if (c->h_tab_live[t] <= tcap / 2) continue;
+        c->h_tab_live[t] = 0; // stale until the next batch reads the device count back
+        hipLaunchKernelGGL(pv_topn_purge, dim3(nreg), dim3(1024), 0, st, (const PvParams *)c->d_params, t, c->d_theta);
+        std::vector<uint32_t> th(nreg);
+        uint64_t tops[PV_ARENA_PARTS];
+        if (!hip_ok(e = hipGetLastError()) ||
+            !hip_ok(e = hipMemcpyAsync(th.data(), c->d_theta, nreg * 4, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipMemcpyAsync(tops, c->d_arena_top + (uint64_t)t * PV_ARENA_PARTS, sizeof tops, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "top-N purge");
+        std::vector<uint64_t> &ro = c->roff[t];
+        ro.resize(nreg, 0);
+        for (uint32_t r = 0; r < nreg; r++) ro[r] += th[r];
+        c->purges++;
+        const uint64_t pcap = c->arena_cap / PV_ARENA_PARTS;
+        uint64_t most = 0;
+        for (uint64_t u : tops) most = std::max(most, u);
+        if (most <= pcap / 2) continue;
+        if (!c->d_ctmp) {
+            if (!hip_ok(e = hipMalloc(&c->d_ctmp, c->arena_cap)) || !hip_ok(e = hipMalloc(&c->d_ctop, PV_ARENA_PARTS * 8)))
+                return c->hipfail(e, "arena compaction scratch");
+        }
+        uint8_t *arena = c->d_arena + (uint64_t)t * c->arena_cap;
+        if (!hip_ok(e = hipMemsetAsync(c->d_ctop, 0, PV_ARENA_PARTS * 8, st))) return c->hipfail(e, "arena compaction");
+        hipLaunchKernelGGL(pv_topn_compact, dim3((uint32_t)c->cus * 8), dim3(256), 0, st, (const PvParams *)c->d_params, t,
+                           c->d_ctmp, c->d_ctop);
+        if (!hip_ok(e = hipGetLastError()) ||
+            !hip_ok(e = hipMemcpyAsync(arena, c->d_ctmp, c->arena_cap, hipMemcpyDeviceToDevice, st)) ||
+            !hip_ok(e = hipMemcpyAsync(c->d_arena_top + (uint64_t)t * PV_ARENA_PARTS, c->d_ctop, PV_ARENA_PARTS * 8,
+                                       hipMemcpyDeviceToDevice, st)))
+            return c->hipfail(e, "arena compaction");
+    }
+    return 0;
+}
+
 int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint64_t a, uint64_t n, uint64_t rec_bytes,
                  const std::vector<Shift> &nsh, const std::vector<Shift> &dsh, uint32_t first_sec, hipStream_t st)
 {
@@ -1770,6 +1837,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.tp_off = c->d_status + ST_TP_OFF;
     P.tp_fill = c->d_status + ST_TP_FILL;
     P.tp_tabs = c->d_status + ST_TP_TABS;
+    P.tab_live = c->d_tab_live;
     P.cb_h = c->d_cb_h;
     P.tp_buf = c->d_tpbuf;
     P.nn_cnt = c->d_status + ST_NNEW;
@@ -1808,7 +1876,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
     uint32_t status[ST_WORDS];
-    if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
+    if (!hip_ok(e = hipMemcpyAsync(c->h_tab_live, c->d_tab_live, PV_TABLES * 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "kernel execution");
     memcpy(status, c->h_status, sizeof status);
@@ -1969,7 +2038,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         c->dns_shifts.emplace_back(sh.sec, c->dns.slot_at(0));
     }
     c->records_seen += n;
-    return 0;
+    return purge_tables(c, st);
 }
 
 // Both managers' shifts of a batch (Net from the record seconds, DNS from the prescan bits

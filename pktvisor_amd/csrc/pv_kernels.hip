@@ -290,6 +290,7 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
         }
     }
     if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
+    if (created >= 0) atomicAdd(&P.tab_live[PV_TSLOT(slot, metric)], 1u);
     if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns);
 }
 
@@ -1757,7 +1758,7 @@ struct MergeState {
     uint32_t mn[2][PV_RS]; // smallest record index of an IPv4 key per direction (CPC)
     uint32_t nidx[PV_RS]; // entries created in this batch: region index, source record
     uint32_t nrep[PV_RS];
-    uint32_t nnew, nbase;
+    uint32_t nnew, nbase, ncr;
 };
 
 extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams *__restrict__ Pp)
@@ -1801,7 +1802,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                        S.mn[0][i] = 0xffffffffu;
                        S.mn[1][i] = 0xffffffffu;
                    });
-        if (threadIdx.x == 0) S.nnew = 0;
+        if (threadIdx.x == 0) { S.nnew = 0; S.ncr = 0; }
         __syncthreads();
         batched<8>(n, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
             const uint64_t e0 = e.x;
@@ -1826,6 +1827,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                     } else {
                         atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)w);
                     }
+                    if (created) atomicAdd(&S.ncr, 1u);
                     if (created && PV_KEY_METRIC(key) != TM_IPV4) {
                         const uint32_t k = atomicAdd(&S.nnew, 1u);
                         S.nidx[k] = pos;
@@ -1849,6 +1851,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         }
         const uint32_t nnew = S.nnew;
         if (threadIdx.x == 0 && nnew) S.nbase = atomicAdd(P.nn_cnt, nnew);
+        if (threadIdx.x == 0 && S.ncr) atomicAdd(&P.tab_live[tb], S.ncr);
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < nnew; k += blockDim.x) {
             const uint32_t g = S.nbase + k;
@@ -1857,6 +1860,110 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
             else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k]);
         }
         __syncthreads();
+    }
+}
+
+// Bounded top-N tables: the frequent-items sketch's purge (Apache DataSketches
+// frequent_items_sketch / reverse_purge_hash_map, as TopN holds it, src/Metrics.h:488-538;
+// the library is not vendored in the reference). Once a table holds more than half its
+// capacity between batches, every region of it takes its median count theta, subtracts it
+// from every entry and drops those left at zero or below, rehashing the survivors; theta is
+// added to the region's offset. The host reports count + offset: exact for a key never
+// dropped, and for any key an upper bound on its true count with count as the lower bound,
+// as the sketch's get_estimate / get_lower_bound are. Each purge removes at least
+// theta x (half the region) of stored weight, so the offset stays below 4 x (the region's
+// updates) / (region size).
+extern "C" __global__ void __launch_bounds__(1024) pv_topn_purge(const PvParams *__restrict__ Pp, uint32_t tb,
+                                                                 uint32_t *theta_out)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t r = blockIdx.x;
+    const uint32_t rsl = P.tcap_log2 - P.reg_log2;
+    const uint32_t rs = 1u << rsl;
+    const uint64_t rbase = ((uint64_t)tb << P.tcap_log2) + ((uint64_t)r << rsl);
+    __shared__ uint64_t K[PV_RS];
+    __shared__ uint64_t C[PV_RS];
+    __shared__ uint32_t A[PV_RS];
+    __shared__ uint32_t hist[1024];
+    __shared__ uint32_t live, theta, removed;
+    for (uint32_t b = threadIdx.x; b < 1024; b += blockDim.x) hist[b] = 0;
+    if (threadIdx.x == 0) { live = 0; removed = 0; theta = 0; }
+    __syncthreads();
+    // this thread's entries (rs / blockDim.x of them) stay in registers across the rebuild
+    constexpr uint32_t PER = PV_RS / 1024;
+    uint64_t k[PER], c[PER];
+    uint32_t a[PER];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        const uint32_t i = threadIdx.x + q * blockDim.x;
+        k[q] = i < rs ? P.tkeys[rbase + i] : 0;
+        c[q] = i < rs ? P.tcnt[rbase + i] : 0;
+        a[q] = i < rs ? P.taux[rbase + i] : 0;
+        if (k[q]) {
+            atomicAdd(&live, 1u);
+            atomicAdd(&hist[c[q] < 1023 ? (uint32_t)c[q] : 1023u], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && live) {
+        // smallest theta with at least half the entries at count <= theta
+        uint32_t acc = 0, t = 0;
+        while (t < 1023 && acc + hist[t] < (live + 1) / 2) acc += hist[t++];
+        theta = t;
+    }
+    __syncthreads();
+    const uint32_t th = theta;
+    if (!live) { if (threadIdx.x == 0) theta_out[r] = 0; return; }
+    for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) { K[i] = 0; C[i] = 0; A[i] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        if (!k[q]) continue;
+        if (c[q] <= th) { atomicAdd(&removed, 1u); continue; }
+        uint32_t pos = (uint32_t)tkey_hash(k[q]) & (rs - 1);
+        for (uint32_t probe = 0; probe < rs; probe++) {
+            if (atomicCAS((unsigned long long *)&K[pos], 0ull, (unsigned long long)k[q]) == 0) {
+                C[pos] = c[q] - th;
+                A[pos] = a[q];
+                break;
+            }
+            pos = (pos + 1) & (rs - 1);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+        P.tkeys[rbase + i] = K[i];
+        P.tcnt[rbase + i] = C[i];
+        P.taux[rbase + i] = A[i];
+    }
+    if (threadIdx.x == 0) {
+        theta_out[r] = th;
+        atomicSub(&P.tab_live[tb], removed);
+    }
+}
+
+// Name-arena compaction of one table after a purge: every live entry's name record moves,
+// within its own partition, to a scratch arena packed from the partition start, and its aux
+// is re-pointed; the host copies the scratch over the table's arena and takes the scratch
+// tops as the partitions' new tops. A partition never grows, so nothing can overflow.
+extern "C" __global__ void pv_topn_compact(const PvParams *__restrict__ Pp, uint32_t tb, uint8_t *tmp,
+                                           unsigned long long *tmp_top)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint64_t tcap = 1ull << P.tcap_log2;
+    const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
+    const uint8_t *arena = P.arena + (uint64_t)tb * P.arena_cap;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < tcap; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t at = ((uint64_t)tb << P.tcap_log2) + i;
+        const uint32_t aux = P.taux[at];
+        if (!P.tkeys[at] || !aux) continue;
+        const uint64_t part = (aux - 1) / pcap;
+        const uint8_t *src = arena + (aux - 1);
+        const uint32_t len = src[0] | (src[1] << 8);
+        const uint32_t bytes = (len + 2 + 3) & ~3u;
+        const uint64_t pos = part * pcap + atomicAdd(&tmp_top[part], (unsigned long long)bytes);
+        for (uint32_t b = 0; b < len + 2; b++) tmp[pos + b] = src[b];
+        P.taux[at] = (uint32_t)pos + 1;
     }
 }
 

@@ -299,6 +299,7 @@ struct PvParams {
     PV_G uint32_t *tp_fill;
     PV_G uint32_t *tp_tabs; // per region: bit t set when the region's updates touch table t
     PV_G uint32_t *cb_h;    // per combine workgroup: its entries per region
+    PV_G uint32_t *tab_live; // per table: entries held (bounded by pv_topn_purge)
     PV_G uint64_t *tp_buf;
     PV_G uint32_t *nn_cnt;
     PV_G PvNewName *nn;

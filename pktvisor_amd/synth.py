@@ -285,3 +285,29 @@ def tcp_dns_pcap(seed: int = 1, flows: int = 60, duration_s: float = 20.0, udp_s
         us = int(round((t0 + t) * 1e6))
         out += struct.pack("<IIII", us // 1000000, us % 1000000, len(fr), len(fr)) + fr
     return pcap_file_bytes(bytes(out))
+
+
+# ---------------------------------------------------------------- random-subdomain flood
+def qname_flood_pcap(seed: int = 1, heavy: int = 24, flood: int = 40000, duration_s: float = 40.0):
+    """UDP DNS queries for a random-subdomain flood: `flood` distinct one-off names
+    <random>.victim.example next to `heavy` repeated names www<i>.victim.example with
+    Zipf-like counts, interleaved at random over duration_s (inside one 60 s period).
+    Returns (pcap bytes, {heavy name: count}, total queries)."""
+    import struct
+    from pktvisor_amd import pcap_file_bytes
+    rng = np.random.default_rng(seed)
+    counts = {f"www{i}.victim.example": int(3000 // (i + 1)) + 40 for i in range(heavy)}
+    names = [n for n, c in counts.items() for _ in range(c)]
+    names += [f"{rng.integers(1 << 40):010x}.victim.example" for _ in range(flood)]
+    order = rng.permutation(len(names))
+    t0 = 1_700_000_000_000_000
+    step = int(duration_s * 1e6 / len(names))
+    out = []
+    for k, j in enumerate(order):
+        msg = _dns_msg(rng, int(rng.integers(65536)), False, names[j], 1)
+        udp = struct.pack(">HHHH", 1024 + k % 50000, 53, 8 + len(msg), 0) + msg
+        ip = struct.pack(">BBHHHBBH", 0x45, 0, 20 + len(udp), 0, 0, 64, 17, 0) + bytes([10, 0, k % 200, 1]) + bytes([8, 8, 8, 8])
+        f = b"\x00\x11\x22\x33\x44\x55\x66\x77\x88\x99\xaa\xbb\x08\x00" + ip + udp
+        ts = t0 + k * step
+        out.append(struct.pack("<IIII", ts // 1_000_000, ts % 1_000_000, len(f), len(f)) + f)
+    return pcap_file_bytes(b"".join(out)), counts, len(names)

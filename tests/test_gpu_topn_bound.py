@@ -1,0 +1,55 @@
+"""Bounded top-N tables under a random-subdomain flood (pv_topn_purge, the frequent-items
+sketch's purge that TopN relies on, src/Metrics.h:488-538): with a table far smaller than the
+flood's distinct names, the heavy names still come out on top with estimates in
+[true count, true count + the sketch's error bound], while a table large enough for every
+name keeps the result exact (the oracle's counts)."""
+import numpy as np
+import pytest
+
+import pktvisor_amd as pa
+from pktvisor_amd import synth
+from tests.test_gpu_parity import diff
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(pcap, table_log2, batch):
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    offs = list(idx.offsets) + [len(recs)]
+    h = pa.PvHandlers(host_spec="10.0.0.0/8", num_periods=1, table_log2=table_log2, max_records=1 << 17,
+                      topn_count=10)
+    try:
+        for i in range(0, idx.n, batch):
+            h.process_host(recs[offs[i]:offs[min(idx.n, i + batch)]])
+        return h.window_json(0)
+    finally:
+        h.close()
+
+
+@pytest.mark.parametrize("table_log2,batch", [(12, 1000), (13, 1500)])
+def test_flood_bounded_estimates(table_log2, batch):
+    pcap, heavy, total = synth.qname_flood_pcap(7, flood=60000)
+    w = _run(pcap, table_log2, batch)
+    dns = w["dns"]
+    top3 = dns["top_qname3"]
+    assert [e["name"] for e in top3] == sorted(heavy, key=lambda n: -heavy[n])[:10]
+    # offset bound: each purge removes theta x (half a region) of stored weight
+    rs = 1 << min(table_log2, 12)
+    bound = 4 * total * rs // (1 << table_log2) // rs + 2
+    for e in top3:
+        t = heavy[e["name"]]
+        assert t <= e["estimate"] <= t + bound, (e, t, bound)
+    # the second-level name is one key, never purged: exact
+    assert dns["top_qname2"][0] == {"name": ".victim.example", "estimate": total}
+    assert dns["wire_packets"]["total"] == total
+
+
+def test_flood_large_table_exact(oracle, tmp_path):
+    """no purge when the table holds every name: bit-exact with the oracle"""
+    pcap, heavy, total = synth.qname_flood_pcap(3, flood=20000)
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec="10.0.0.0/8", periods=1)
+    ref = oracle.run_bytes(pcap, host_spec="10.0.0.0/8", num_periods=1, window=1)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
