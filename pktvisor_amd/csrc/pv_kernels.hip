@@ -1198,7 +1198,14 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
 // payload sizes go to an LDS histogram, the IP of each record to the dense IP log
 // (coalesced stores) and DNS messages to the workgroup's DNS work list. No table lookups
 // and no atomics with a return on the per-record path.
-extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *__restrict__ Pp)
+#ifndef PV_NET_MINB
+#define PV_NET_MINB 1 // tuning: resident workgroups per CU the register allocation must allow
+#endif
+// The Net pass body. GEN = false is the common batch, specialised: no period shift inside
+// the batch, no filter-all mode and no profiling knobs, so the per-tile period and slot
+// logic and the direct-update paths compile away (fewer live scalars in the tile loop).
+template <bool GEN>
+__device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ NetState S;
@@ -1216,8 +1223,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
     NetK K;
     K.recs = P.recs; K.offs = P.offs; K.n = P.n; K.rec_bytes = P.rec_bytes; K.gbase = P.gbase;
     K.sum = P.sum; K.cpc = P.cpc; K.iplog = P.iplog; K.dq = P.dq; K.flags = P.flags;
-    K.n_shift = P.n_shift; K.skip_before = P.skip_before; K.slot0 = P.slot_of[0];
-    K.net_groups = P.net_groups; K.dbg = P.dbg; K.net_filter_all = P.net_filter_all;
+    K.n_shift = GEN ? P.n_shift : 0u; K.skip_before = P.skip_before; K.slot0 = P.slot_of[0];
+    K.net_groups = P.net_groups; K.dbg = GEN ? P.dbg : 0u; K.net_filter_all = GEN ? P.net_filter_all : 0u;
     K.n_dshift = P.n_dshift; K.dskip_before = P.dskip_before;
     K.tcp_emit = P.tcp_emit; K.tseg_cap = P.tseg_cap; K.tseg = P.tseg; K.tseg_cnt = P.tseg_cnt; K.tmask = P.tmask;
     const ParseCfg C = parse_cfg(P);
@@ -1275,16 +1282,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         }
     }
     STAMP_DECL
-    for (uint32_t k = 0; k < ntl; k++) {
-        // step: rows k + Q + 1, then tile k + Q - 1, whose rows came two steps earlier:
-        // younger than them are that step's tile, the last step's rows and tile, and this
-        // step's rows
-        issue_rows(k + PV_NL_Q + 1);
-        PV_VMCNT(2 * PV_NL_OPS);
-        issue_tile(k + PV_NL_Q - 1);
-        PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed
-        STAMP(1)
-        const uint32_t sl = k % PV_NL_Q, row = k % PV_NL_OROWS;
+    // one tile's records from its staged copy Ls (off: this lane's record start, [b0, b1): the tile's span)
+    auto tile_body = [&](uint32_t k, uint64_t off, uint32_t b0, uint32_t b1, const uint32_t *Ls) {
         const uint64_t t = tile_of(k);
         const uint64_t r0 = t * PV_WT;
         const uint64_t r1 = min<uint64_t>(r0 + PV_WT, n) - 1;
@@ -1307,9 +1306,6 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         }
         const bool upd = lp >= K.skip_before;
         const bool own = slot == wslot;
-        const uint64_t off = NW.lo[row][lane];
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
-        const uint32_t b1 = r0 + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row][63]);
         const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
         const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
         uint32_t hv = PV_NOH;
@@ -1319,8 +1315,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         bool istcp = false, hasseg = false;
         PvTcpSeg seg;
         if (active && !(K.dbg & 1)) {
-            const SAcc R = packed ? SAcc{K.recs, NW.slot[sl], base, nch * 16 - 4, 0u, 1u}
-                                  : SAcc{K.recs, NW.slot[sl], off & ~15ull, PV_NL_SLOT / PV_WT - 4, lane * 4, 0u};
+            const SAcc R = packed ? SAcc{K.recs, Ls, base, nch * 16 - 4, 0u, 1u}
+                                  : SAcc{K.recs, Ls, off & ~15ull, PV_NL_SLOT / PV_WT - 4, lane * 4, 0u};
             // fast path: the 17 staged dwords recw_load reads (the record's first 64 bytes
             // plus the alignment spill) are inside the staged range; in window mode that
             // holds for every record (start within 15 bytes of the 16-B aligned window)
@@ -1400,7 +1396,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         asm volatile("" ::: "memory");
         STAMP(5)
         if (!(K.dbg & 1)) {
-            hist_add(S.hist, hv, lane);
+            if (!(K.dbg & 64)) hist_add(S.hist, hv, lane); // 64: profiling knob, no histogram
             // DNS messages: wave-compacted into the workgroup's work list
             const uint64_t m = __ballot(isdns);
             if (m) {
@@ -1414,7 +1410,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
                     dd[1] = dm.b;
                 }
             }
-            if (tops && i <= r1) K.iplog[i] = ek;
+            if (tops && i <= r1 && !(K.dbg & 128)) K.iplog[i] = ek; // 128: profiling knob, no IP log
             if (K.tcp_emit) {
                 // DNS over TCP: the tile's TCP records, then its DNS-port segments
                 // (tiles without TCP keep the zero the batch's fill wrote: no store, so no
@@ -1427,6 +1423,19 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
             }
         }
         STAMP(6)
+    };
+    for (uint32_t k = 0; k < ntl; k++) {
+        // step: rows k + Q + 1, then tile k + Q - 1, whose rows came two steps earlier:
+        // younger than them are that step's tile, the last step's rows and tile, and this
+        // step's rows
+        issue_rows(k + PV_NL_Q + 1);
+        PV_VMCNT(2 * PV_NL_OPS);
+        issue_tile(k + PV_NL_Q - 1);
+        PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed
+        STAMP(1)
+        const uint32_t sl = k % PV_NL_Q, row = k % PV_NL_OROWS;
+        tile_body(k, NW.lo[row][lane], __builtin_amdgcn_readfirstlane(NW.lo[row][0]),
+                  tile_of(k) * PV_WT + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row][63]), NW.slot[sl]);
     }
     PV_VMCNT(0); // the sequence's trailing copies land before the workgroup ends
     if (wslot != 0xffffffffu) knet_flush(K, wslot, c);
@@ -1440,6 +1449,9 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_kernel(const PvParams *
         if (S.nd) atomicAdd(P.n_dns, S.nd);
     }
 }
+
+extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(const PvParams *__restrict__ Pp) { net_pass<true>(Pp); }
+extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(const PvParams *__restrict__ Pp) { net_pass<false>(Pp); }
 
 // ------------------------------------------------------------------ the DNS pass
 // One lane per DNS message of the Net pass's work list (same workgroup mapping).
