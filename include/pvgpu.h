@@ -59,6 +59,12 @@ enum pv_dns_group {
     PV_DNS_TRANSACTIONS = 1u << 4, PV_DNS_TOP_ECS = 1u << 5, PV_DNS_TOP_QNAMES = 1u << 6,
     PV_DNS_TOP_QNAMES_DETAILS = 1u << 7, PV_DNS_TOP_PORTS = 1u << 8
 };
+/* Net v2 handler groups (src/handlers/net/v2/NetStreamHandler.h:25-31, _group_defs :262-267). */
+enum pv_net2_group {
+    PV_NET2_COUNTERS = 1u << 0, PV_NET2_CARDINALITY = 1u << 1, PV_NET2_QUANTILES = 1u << 2, PV_NET2_TOP_GEO = 1u << 3,
+    PV_NET2_TOP_IPS = 1u << 4
+};
+#define PV_NET2_DEFAULT_GROUPS (PV_NET2_COUNTERS | PV_NET2_CARDINALITY | PV_NET2_QUANTILES | PV_NET2_TOP_GEO | PV_NET2_TOP_IPS)
 /* OR'ed into pv_config.net_groups / dns_groups: the bits are the enabled set even when it is
  * empty ("disable: [all]"); without it 0 selects the handler's default groups */
 #define PV_GROUPS_SET 0x80000000u
@@ -81,7 +87,10 @@ typedef struct pv_config {
     uint32_t topn_percentile_threshold; /* "topn_percentile_threshold" 0..99 (TopN::to_json, src/Metrics.h:510-521,577-590) */
     uint32_t net_filter_all; /* nonzero: every packet is a filtered Net event (geo / ASN filters without a geo
                                 database, NetStreamHandler::_filtering, net/v1/NetStreamHandler.cpp:223-283) */
+    uint32_t net2_groups;    /* Net v2 handler ("net", src/handlers/net/v2) attached next to v1: pv_net2_group bits
+                                | PV_GROUPS_SET, or PV_NET2_ATTACH for its default groups; 0 = not attached */
 } pv_config;
+#define PV_NET2_ATTACH 0x40000000u
 
 /* DNS v1 filters, the typed form of the "exclude_noerror", "only_rcode", "answer_count",
  * "only_queries", "only_responses" and "only_qtype" handler config keys

@@ -329,6 +329,8 @@ static const std::map<uint16_t, std::string> &rcode_names()
 
 // ---------------------------------------------------------------- config
 enum { NG_COUNTERS = 1, NG_CARDINALITY = 2, NG_TOP_GEO = 4, NG_TOP_IPS = 8 };
+// Net v2 groups (src/handlers/net/v2/NetStreamHandler.h:25-31): Counters, Cardinality, Quantiles, TopGeo, TopIps
+enum { N2G_COUNTERS = 1, N2G_CARDINALITY = 2, N2G_QUANTILES = 4, N2G_TOP_GEO = 8, N2G_TOP_IPS = 16 };
 enum { DG_CARDINALITY = 1, DG_COUNTERS = 2, DG_QUANTILES = 4, DG_HISTOGRAMS = 8, DG_TRANSACTIONS = 16, DG_TOP_ECS = 32,
        DG_TOP_QNAMES = 64, DG_TOP_QNAMES_DETAILS = 128, DG_TOP_PORTS = 256 };
 struct V4Net { uint32_t addr; uint8_t cidr; };  // addr: network-order bytes as LE u32 (in_addr.s_addr)
@@ -349,6 +351,8 @@ struct Config {
     uint32_t dns_groups = DG_CARDINALITY | DG_COUNTERS | DG_QUANTILES | DG_TRANSACTIONS | DG_TOP_QNAMES | DG_TOP_PORTS;
     uint32_t topn_pct = 0;   // topn_percentile_threshold
     bool net_filter_all = false; // net geo / ASN filters with no geo database: every packet filtered (:223-283)
+    // Net v2 handler attached ("net"): its groups (N2G_*), 0 = not attached
+    uint32_t net2_groups = 0;
     bool filter_all = false; // geoloc_notfound / asn_notfound with no geo database: every packet filtered (:619-642)
     // DNS v1 filters (DnsStreamHandler::start, dns/v1/DnsStreamHandler.cpp:60-160)
     bool exclude_noerror = false;   // "exclude_noerror" (:61-63)
@@ -857,6 +861,34 @@ struct NetBucket : BaseBucket {
     }
 };
 
+// Net v2 (src/handlers/net/v2/NetStreamHandler.h:61-156): every metric per direction
+struct Net2Dir {
+    uint64_t UDP = 0, TCP = 0, OtherL4 = 0, IPv4 = 0, IPv6 = 0, TCP_SYN = 0, total = 0;
+    uint64_t seen = 0; // packets of this direction (the reference's _net map entry exists once one arrived)
+    ExactQuantile<uint64_t> payload;
+    Cpc ips;
+    ExactTop<uint32_t> top4;
+    ExactTop<std::string> top6;
+    void merge(const Net2Dir &o)
+    {
+        UDP += o.UDP; TCP += o.TCP; OtherL4 += o.OtherL4; IPv4 += o.IPv4; IPv6 += o.IPv6; TCP_SYN += o.TCP_SYN;
+        total += o.total; seen += o.seen;
+        payload.merge(o.payload);
+        ips.merge(o.ips);
+        top4.merge(o.top4);
+        top6.merge(o.top6);
+    }
+};
+struct Net2Bucket : BaseBucket {
+    uint64_t filtered = 0;
+    Net2Dir dir[3]; // in (toHost), out (fromHost), unknown
+    void merge(const Net2Bucket &o)
+    {
+        filtered += o.filtered;
+        for (int d = 0; d < 3; d++) dir[d].merge(o.dir[d]);
+    }
+};
+
 struct DnsBucket : BaseBucket {
     uint64_t xacts_total = 0, xacts_in = 0, xacts_out = 0, xacts_timed_out = 0, queries = 0, replies = 0, UDP = 0,
              TCP = 0, IPv4 = 0, IPv6 = 0, NX = 0, REFUSED = 0, SRVFAIL = 0, NOERROR = 0, NODATA = 0, total = 0,
@@ -934,12 +966,13 @@ struct Engine {
     Config cfg;
     uint32_t linktype = 1;
     Window<NetBucket> net;
+    Window<Net2Bucket> net2;
     Window<DnsBucket> dns;
     std::unordered_map<XactKey, Xact, XactKeyHash> xacts;
     uint32_t ttl_s = 0, ttl_ms = 0;
     float to90 = 0.0f, from90 = 0.0f;
 
-    explicit Engine(const Config &c) : cfg(c), net(c.num_periods), dns(c.num_periods)
+    explicit Engine(const Config &c) : cfg(c), net(c.num_periods), net2(c.num_periods), dns(c.num_periods)
     {
         // TransactionManager.h:60-68
         if (c.xact_ttl_ms > 1000) { ttl_s = c.xact_ttl_ms / 1000; ttl_ms = c.xact_ttl_ms - ttl_s * 1000; }
@@ -949,11 +982,13 @@ struct Engine {
     void start(TS ts)
     {
         net.set_start(ts);
+        net2.set_start(ts);
         dns.set_start(ts);
     }
     void end(TS ts)
     {
         net.set_end(ts);
+        net2.set_end(ts);
         dns.set_end(ts);
     }
 
@@ -993,6 +1028,53 @@ struct Engine {
             else if (p.dir == DIR_FROM_HOST) out = p.v6hdr + 24;
             if (p.l3 == L3_IPV6 && in && memcmp(in, zero, 16)) { if (card) b.src.update_bytes(in, 16); if (tops) b.top6.update(ipv6_str(in)); }
             if (p.l3 == L3_IPV6 && out && memcmp(out, zero, 16)) { if (card) b.dst.update_bytes(out, 16); if (tops) b.top6.update(ipv6_str(out)); }
+        }
+    }
+
+    // Net v2: NetworkMetricsManager::process_packet + NetworkMetricsBucket::process_packet /
+    // process_net_layer(NetworkPacket&) (net/v2/NetStreamHandler.cpp:494-532,650-716,756-762).
+    // Deep path (deep_sample_rate 100): toHost keeps the source address, fromHost the
+    // destination, unknown both; an address counts only when the packet's l3 matches its
+    // layer and it is not the unspecified address (isValid)
+    void net2_packet(const Pkt &p)
+    {
+        net2.maybe_shift(p.ts);
+        net2.new_event(true);
+        Net2Bucket &b = net2.live();
+        const int d = p.dir == DIR_TO_HOST ? 0 : (p.dir == DIR_FROM_HOST ? 1 : 2);
+        Net2Dir &x = b.dir[d];
+        x.seen++;
+        const uint32_t g = cfg.net2_groups;
+        if (g & N2G_COUNTERS) {
+            x.total++;
+            if (p.l3 == L3_IPV6) x.IPv6++;
+            else if (p.l3 == L3_IPV4) x.IPv4++;
+            if (p.l4 == L4_UDP) x.UDP++;
+            else if (p.l4 == L4_TCP) { x.TCP++; if (p.syn) x.TCP_SYN++; }
+            else x.OtherL4++;
+        }
+        x.payload.update(p.caplen);
+        const bool card = g & N2G_CARDINALITY, tops = g & N2G_TOP_IPS;
+        const bool want_src = d != 1, want_dst = d != 0;
+        if (p.has_v4) {
+            if (p.l3 != L3_IPV4) return;
+            for (int side = 0; side < 2; side++) {
+                if (side == 0 ? !want_src : !want_dst) continue;
+                const uint32_t ip = rd32le(p.v4hdr + (side ? 16 : 12));
+                if (!ip) continue;
+                if (card) x.ips.update_u32(ip);
+                if (tops) x.top4.update(ip);
+            }
+        } else if (p.has_v6) {
+            if (p.l3 != L3_IPV6) return;
+            static const uint8_t zero[16] = {0};
+            for (int side = 0; side < 2; side++) {
+                if (side == 0 ? !want_src : !want_dst) continue;
+                const uint8_t *a = p.v6hdr + (side ? 24 : 8);
+                if (!memcmp(a, zero, 16)) continue;
+                if (card) x.ips.update_bytes(a, 16);
+                if (tops) x.top6.update(ipv6_str(a));
+            }
         }
     }
 
@@ -1524,6 +1606,7 @@ struct Engine {
         set_direction(p, cfg);
         tcp_dir = p.dir;
         net_packet(p);
+        if (cfg.net2_groups) net2_packet(p);
         if (p.l4 == L4_UDP) dns_udp_packet(p, hash5tuple(p));
         else if (p.l4 == L4_TCP) tcp_packet(p);
         rec_no++;
@@ -1644,6 +1727,48 @@ static void net_json(J &j, const NetBucket &b, size_t topn, uint32_t g)
         j.key("top_ASN"); j.arr(); j.end_arr();
     }
     quant_json(j, "payload_size", b.payload);
+}
+
+// NetworkMetricsBucket::to_json, Net v2 (net/v2/NetStreamHandler.cpp:436-484); rates excluded
+static void net2_json(J &j, const Net2Bucket &b, size_t topn, uint32_t g)
+{
+    j.key("period"); j.obj();
+    j.key("start_ts"); j.i64(b.start.sec);
+    j.key("length"); j.u64(b.period_length);
+    j.end_obj();
+    j.key("observed_packets"); j.u64(b.num_events);
+    j.key("deep_sampled_packets"); j.u64(b.num_samples);
+    if (g & N2G_COUNTERS) { j.key("filtered_packets"); j.u64(b.filtered); }
+    static const char *names[3] = {"in", "out", "unknown"};
+    for (int d = 0; d < 3; d++) {
+        const Net2Dir &x = b.dir[d];
+        if (!x.seen) continue;
+        j.key(names[d]); j.obj();
+        if (g & N2G_COUNTERS) {
+            j.key("udp_packets"); j.u64(x.UDP);
+            j.key("tcp_packets"); j.u64(x.TCP);
+            j.key("other_l4_packets"); j.u64(x.OtherL4);
+            j.key("ipv4_packets"); j.u64(x.IPv4);
+            j.key("ipv6_packets"); j.u64(x.IPv6);
+            j.key("tcp"); j.obj(); j.key("syn_packets"); j.u64(x.TCP_SYN); j.end_obj();
+            j.key("total_packets"); j.u64(x.total);
+        }
+        if (g & N2G_CARDINALITY) {
+            j.key("cardinality"); j.obj();
+            j.key("ips"); j.i64(lround(x.ips.estimate()));
+            j.end_obj();
+        }
+        if (g & N2G_TOP_IPS) {
+            top_json(j, "top_ipv4_packets", x.top4, topn, ipv4_str);
+            top_json(j, "top_ipv6_packets", x.top6, topn, id_str);
+        }
+        if (g & N2G_TOP_GEO) {
+            j.key("top_geo_loc_packets"); j.arr(); j.end_arr();
+            j.key("top_asn_packets"); j.arr(); j.end_arr();
+        }
+        if (g & N2G_QUANTILES) quant_json(j, "payload_size_bytes", x.payload);
+        j.end_obj();
+    }
 }
 
 static void dns_json(J &j, const DnsBucket &b, size_t topn, uint32_t g)
@@ -1796,6 +1921,7 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "dns_groups") c.dns_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "filter_all") c.filter_all = atoi(v.c_str()) != 0;
         else if (k == "net_filter_all") c.net_filter_all = atoi(v.c_str()) != 0;
+        else if (k == "net2_groups") c.net2_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "topn_pct") c.topn_pct = (uint32_t)atoi(v.c_str());
         else if (k == "exclude_noerror") c.exclude_noerror = atoi(v.c_str()) != 0;
         else if (k == "only_rcode_mask") c.only_rcode_mask = (uint32_t)strtoul(v.c_str(), nullptr, 0);
@@ -1874,6 +2000,10 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
     j.obj();
     auto nb = window_bucket(e.net, w);
     j.key("packets"); j.obj(); net_json(j, *nb, c.topn_count, c.net_groups); j.end_obj();
+    if (c.net2_groups) {
+        auto n2 = window_bucket(e.net2, w);
+        j.key("net"); j.obj(); net2_json(j, *n2, c.topn_count, c.net2_groups); j.end_obj();
+    }
     auto db = window_bucket(e.dns, w);
     j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_groups); j.end_obj();
     j.end_obj();

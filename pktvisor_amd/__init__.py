@@ -46,7 +46,8 @@ class pv_config(ctypes.Structure):
                 ("xact_ttl_ms", ctypes.c_uint32), ("net_groups", ctypes.c_uint32), ("dns_groups", ctypes.c_uint32),
                 ("linktype", ctypes.c_uint32), ("ts_nano", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("table_log2", ctypes.c_uint32), ("max_records", ctypes.c_uint64),
-                ("topn_percentile_threshold", ctypes.c_uint32), ("net_filter_all", ctypes.c_uint32)]
+                ("topn_percentile_threshold", ctypes.c_uint32), ("net_filter_all", ctypes.c_uint32),
+                ("net2_groups", ctypes.c_uint32)]
 
 
 class pv_dns_filters(ctypes.Structure):
@@ -295,14 +296,19 @@ class PvHandlers:
                  xact_ttl_ms: int = 5000, linktype: int = 1, ts_nano: int = 0, device: int = -1,
                  table_log2: int = 0, max_records: int = 1 << 20, net_groups: int = 0, dns_groups: int = 0,
                  dns_filters: Optional[dict] = None, net_config: Optional[dict] = None,
-                 dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0):
+                 dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0,
+                 net2_config: Optional[dict] = None):
         from pktvisor_amd import config as pvcfg
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
         net_filter_all = 0
-        if net_config is not None or dns_config is not None:
+        net2_groups = 0
+        if net2_config is not None:
+            # the Net v2 handler ("net") attached next to v1 ("packets")
+            net2_groups = pvcfg.net2_start(dict(net2_config))
+        if net_config is not None or dns_config is not None or net2_config is not None:
             ncfg, dcfg = dict(net_config or {}), dict(dns_config or {})
-            win = pvcfg.window_config([ncfg, dcfg])
+            win = pvcfg.window_config([ncfg, dcfg, dict(net2_config or {})])
             if win.get("deep_sample_rate", 100) != 100:
                 raise pvcfg.ConfigException("deep_sample_rate below 100 is not supported by the GPU handler")
             num_periods = win.get("num_periods", num_periods)
@@ -315,7 +321,7 @@ class PvHandlers:
                 xact_ttl_ms = d["xact_ttl_ms"]
         self._host = host_spec.encode() if host_spec else None
         cfg = pv_config(self._host, num_periods, topn_count, xact_ttl_ms, net_groups, dns_groups, linktype, ts_nano,
-                        device, table_log2, max_records, topn_percentile_threshold, net_filter_all)
+                        device, table_log2, max_records, topn_percentile_threshold, net_filter_all, net2_groups)
         self.num_periods = num_periods
         self.ctx = ctypes.c_void_p()
         rc = self.lib.pv_create(ctypes.byref(cfg), ctypes.byref(self.ctx))

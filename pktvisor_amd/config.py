@@ -147,6 +147,23 @@ def net_start(cfg: dict) -> dict:
     return out
 
 
+# Net v2 (src/handlers/net/v2/NetStreamHandler.h:25-31,262-267; defaults :47-52)
+NET2_GROUP_DEFS = {"cardinality": 1 << 1, "counters": 1 << 0, "quantiles": 1 << 2, "top_geo": 1 << 3, "top_ips": 1 << 4}
+NET2_DEFAULT_GROUPS = ("counters", "cardinality", "quantiles", "top_geo", "top_ips")
+
+
+def net2_start(cfg: dict) -> int:
+    """NetStreamHandler v2 start (src/handlers/net/v2/NetStreamHandler.cpp:45-95) up to the
+    signal wiring: the enabled group bits | GROUPS_SET. Its geo / ASN filters need a MaxMind
+    database and are not built for v2."""
+    validate_configs(cfg, NET_CONFIG_DEFS)
+    groups = process_groups(cfg, NET2_GROUP_DEFS, NET2_DEFAULT_GROUPS)
+    for k in ("geoloc_notfound", "asn_notfound", "only_geoloc_prefix", "only_asn_number"):
+        if k in cfg:
+            raise ConfigException(f"{k} is not supported by the GPU Net v2 handler")
+    return groups | GROUPS_SET
+
+
 def dns_start(cfg: dict) -> dict:
     """DnsStreamHandler::start (src/handlers/dns/v1/DnsStreamHandler.cpp:43-201) up to the signal
     wiring: {"groups": bits | GROUPS_SET, "filters": pv_dns_filters fields, "xact_ttl_ms": int|None}"""

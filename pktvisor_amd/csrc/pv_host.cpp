@@ -82,6 +82,7 @@ extern "C" __global__ void pv_topn_combine(const PvParams *P);
 extern "C" __global__ void pv_topn_scan(const PvParams *P);
 extern "C" __global__ void pv_topn_scatter(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
+extern "C" __global__ void pv_net2_kernel(const PvParams *P);
 extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_t *theta_out);
 extern "C" __global__ void pv_topn_compact(const PvParams *P, uint32_t tb, uint8_t *tmp, unsigned long long *tmp_top);
 extern "C" __global__ void pv_topn_names(const PvParams *P);
@@ -295,6 +296,7 @@ struct pv_ctx {
     PvSubnets nets{};
     uint32_t ttl_s = 0, ttl_ms = 0;
     uint32_t net_groups = PV_NET_DEFAULT_GROUPS, dns_groups = PV_DNS_DEFAULT_GROUPS;
+    uint32_t net2_groups = 0; // Net v2 attached: PV_NET2_* bits | PV_N2G_ON
     // device state
     uint64_t *d_sum = nullptr;
     int64_t *d_cpc = nullptr;
@@ -663,6 +665,16 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out) // s: table (PV_T
     return 0;
 }
 
+// Host-side metric of a top-N entry: its key's metric, or for Net v2 keys a metric per
+// direction (TMH_V2_IP4 + dir, TMH_V2_IP6 + dir)
+enum { TMH_V2_IP4 = 32, TMH_V2_IP6 = 36 };
+uint32_t host_metric(uint64_t key)
+{
+    if (PV_IS_V2_IP4(key)) return TMH_V2_IP4 + (uint32_t)((key >> 34) & 3);
+    if (PV_IS_V2_IP6(key)) return TMH_V2_IP6 + (uint32_t)((key >> 53) & 3);
+    return PV_KEY_METRIC(key);
+}
+
 // A finalised bucket (possibly the merge of several slots) on the host.
 struct HostBucket {
     int64_t start_sec = 0;
@@ -753,7 +765,7 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int 
         std::vector<TopRec> recs;
         int rc = read_topn(c, s + (part == PART_DNS ? PV_SLOTS : 0), recs);
         if (rc) return rc;
-        for (auto &r : recs) b.tops[PV_KEY_METRIC(r.key)][r.name] += r.count;
+        for (auto &r : recs) b.tops[host_metric(r.key)][r.name] += r.count;
         if (part != PART_DNS) continue;
         const uint32_t sg = s | (c->gen[s] << 8);
         for (auto &v : c->xvals_host) {
@@ -910,6 +922,62 @@ void net_json(pv_ctx *c, Json &j, const HostBucket &b)
     if (cnt) {
         j.key("payload_size").obj();
         j.key("p50").u(q[0]); j.key("p90").u(q[1]); j.key("p95").u(q[2]); j.key("p99").u(q[3]);
+        j.end_obj();
+    }
+}
+
+// NetworkMetricsBucket::to_json, Net v2 (src/handlers/net/v2/NetStreamHandler.cpp:436-484):
+// base event counts, `filtered_packets`, then one object per direction the bucket has seen
+// (the reference creates a direction's entry on its first packet)
+void net2_json(pv_ctx *c, Json &j, const HostBucket &b)
+{
+    const uint64_t *n = &b.sum[PV_OFF_NET2];
+    const uint32_t g = c->net2_groups;
+    const size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
+    j.key("period").obj();
+    j.key("start_ts").i(b.start_sec);
+    j.key("length").u(b.period_length);
+    j.end_obj();
+    j.key("observed_packets").u(n[N2_EVENTS]);
+    j.key("deep_sampled_packets").u(n[N2_SAMPLES]);
+    if (g & PV_N2G_COUNTERS) j.key("filtered_packets").u(n[N2_FILTERED]);
+    static const char *dirs[3] = {"in", "out", "unknown"};
+    for (uint32_t d = 0; d < 3; d++) {
+        const uint64_t *dc = n + N2_DIR + 8 * d;
+        if (!dc[N2_TOTAL]) continue;
+        j.key(dirs[d]).obj();
+        if (g & PV_N2G_COUNTERS) {
+            j.key("udp_packets").u(dc[N2_UDP]);
+            j.key("tcp_packets").u(dc[N2_TCP]);
+            j.key("other_l4_packets").u(dc[N2_OTHER]);
+            j.key("ipv4_packets").u(dc[N2_V4]);
+            j.key("ipv6_packets").u(dc[N2_V6]);
+            j.key("tcp").obj(); j.key("syn_packets").u(dc[N2_SYN]); j.end_obj();
+            j.key("total_packets").u(dc[N2_TOTAL]);
+        }
+        if (g & PV_N2G_CARDINALITY) {
+            j.key("cardinality").obj();
+            j.key("ips").i(lround(cpc_estimate(&b.cpc[(CPC_V2 + d) * PV_CPC_COUPONS], b.merged)));
+            j.end_obj();
+        }
+        if (g & PV_N2G_TOP_IPS) {
+            top_json(j, "top_ipv4_packets", tops_of(b, TMH_V2_IP4 + d), topn, pct);
+            top_json(j, "top_ipv6_packets", tops_of(b, TMH_V2_IP6 + d), topn, pct);
+        }
+        if (g & PV_N2G_TOP_GEO) {
+            j.key("top_geo_loc_packets").arr(); j.end_arr();
+            j.key("top_asn_packets").arr(); j.end_arr();
+        }
+        if (g & PV_N2G_QUANTILES) {
+            uint64_t cnt;
+            auto q = hist_quantiles(&b.sum[PV_OFF_PAYLOAD2 + d * PV_PAYLOAD_BINS], PV_PAYLOAD_BINS, cnt);
+            if (cnt) {
+                j.key("payload_size_bytes").obj();
+                j.key("p50").u(q[0]); j.key("p90").u(q[1]); j.key("p95").u(q[2]); j.key("p99").u(q[3]);
+                j.end_obj();
+            }
+        }
         j.end_obj();
     }
 }
@@ -1157,6 +1225,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     // group bits, 0 = the handler's defaults; PV_GROUPS_SET marks an explicit set (which may be empty)
     if (c->cfg.net_groups) c->net_groups = c->cfg.net_groups & ~PV_GROUPS_SET;
     if (c->cfg.dns_groups) c->dns_groups = c->cfg.dns_groups & ~PV_GROUPS_SET;
+    if (c->cfg.net2_groups)
+        c->net2_groups = PV_N2G_ON | ((c->cfg.net2_groups & PV_GROUPS_SET) ? (c->cfg.net2_groups & PV_NET2_DEFAULT_GROUPS)
+                                                                           : PV_NET2_DEFAULT_GROUPS);
     if (c->cfg.table_log2) c->tcap_log2 = c->cfg.table_log2;
     if (c->tcap_log2 < 8 || c->tcap_log2 > PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2) {
         *out = c;
@@ -1458,6 +1529,7 @@ void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t
     P.ts_nano = c->cfg.ts_nano;
     P.net_groups = c->net_groups;
     P.dns_groups = c->dns_groups;
+    P.net2_groups = c->net2_groups;
     P.net_filter_all = c->cfg.net_filter_all ? 1u : 0u;
     P.nets = c->nets;
     P.f_flags = c->f_flags;
@@ -1807,7 +1879,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     grid = (uint32_t)((tiles + P.wt_per_block - 1) / P.wt_per_block);
     P.grid_main = grid;
     // per workgroup: at most 6 hashed updates per record, plus one cache flush per pass
-    P.mq_cap = P.wt_per_block * 64u * PV_MQ_PER_REC + PV_CACHE_MAX * 2;
+    // (Net v2: two more updates per record and one more cache flush)
+    P.mq_cap = P.wt_per_block * 64u * (PV_MQ_PER_REC + (c->net2_groups ? 2u : 0u)) + PV_CACHE_MAX * (c->net2_groups ? 3u : 2u);
     {
         const size_t need = (size_t)grid * P.mq_cap * 16;
         if (need > c->mq_bytes) {
@@ -1868,6 +1941,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (P.f_flags & PVDF_ONLY_QSUFFIX)
         hipLaunchKernelGGL(pv_dns_suffix, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates, bucket them by table region, merge each
     // region in LDS, decode the names of new entries
     hipLaunchKernelGGL(pv_topn_combine, dim3(grid), dim3(PV_CB_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -2378,6 +2452,11 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
         j.key("packets").obj();
         net_json(c, j, b);
         j.end_obj();
+        if (c->net2_groups) {
+            j.key("net").obj();
+            net2_json(c, j, b);
+            j.end_obj();
+        }
     }
     {
         if ((rc = window_slots(c, c->dns, period, merged != 0, slots))) return rc;

@@ -168,12 +168,33 @@ __device__ __forceinline__ uint32_t dns_suffix_of(PV_CREF(PvParams) P, const A &
 
 // Writes the name record for a newly created global top-N entry (arena: u16 len + bytes).
 // where a name is decoded from when it is not the batch's record `rep`: a TCP message record
+// Net v2 IPv6 top-N key of the 16-byte address at a (PV_V2_IP6)
+template <class A>
+__device__ __forceinline__ uint64_t v2_ip6_key(const A &R, uint64_t a, uint32_t dir)
+{
+    const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
+    const uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
+    uint64_t h1, h2;
+    murmur_16(w0, w1, h1, h2);
+    return PV_V2_IP6(dir, h1 ^ (h2 << 1));
+}
+// the IPv6 address an IPv6 top-N entry names: v1 keys the address of the packet's
+// direction (source to the host, else destination); a v2 key of the unknown direction
+// may be either address, the one whose key it is
+template <class A>
+__device__ __forceinline__ uint64_t ip6_name_addr(const A &R, const Parsed &o, uint64_t key)
+{
+    if (!PV_IS_V2_IP6(key)) return o.dir == 0 ? o.v6 + 8 : o.v6 + 24;
+    const uint32_t d = (uint32_t)(key >> 53) & 3;
+    if (d != 2) return d == 0 ? o.v6 + 8 : o.v6 + 24;
+    return v2_ip6_key(R, o.v6 + 8, 2) == key ? o.v6 + 8 : o.v6 + 24;
+}
 struct NameSrc {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
 };
 __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, uint32_t metric, uint32_t rep,
-                                            const NameSrc *ns = nullptr)
+                                            const NameSrc *ns = nullptr, uint64_t key = 0)
 {
     Parsed o;
     const GAcc R{ns ? ns->recs : P.recs};
@@ -190,7 +211,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     unsigned long long *top = (unsigned long long *)&P.arena_top[tab * PV_ARENA_PARTS + part];
     uint8_t *arena = P.arena + (uint64_t)tab * P.arena_cap;
     if (metric == TM_IPV6) {
-        uint64_t a = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
+        const uint64_t a = ip6_name_addr(R, o, key);
         uint64_t pos = atomicAdd(top, 20ull); // records are 4-byte multiples (pv_topn_names copies dwords)
         if (pos + 20 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
         pos += part * pcap;
@@ -291,7 +312,7 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
     }
     if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
     if (created >= 0) atomicAdd(&P.tab_live[PV_TSLOT(slot, metric)], 1u);
-    if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns);
+    if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns, key);
 }
 
 // ------------------------------------------------------------------ LDS key cache
@@ -1563,6 +1584,131 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *
     }
 }
 
+// ------------------------------------------------------------------ Net v2
+// record range of workgroup b (the Net pass mapping), clipped to the batch
+__device__ __forceinline__ void wg_records(PV_CREF(PvParams) P, uint32_t b, uint64_t &r0, uint64_t &r1)
+{
+    r0 = min<uint64_t>((uint64_t)b * P.wt_per_block * PV_WT, P.n);
+    r1 = min<uint64_t>(r0 + (uint64_t)P.wt_per_block * PV_WT, P.n);
+}
+// NetworkMetricsBucket v2 (src/handlers/net/v2/NetStreamHandler.cpp:494-532,650-716): every
+// metric per direction (in = toHost, out = fromHost, unknown). In: the source address, out:
+// the destination, unknown: both. Counters, payload sizes, IP cardinality and top IPv4 /
+// IPv6. The v2 manager sees the same events as v1's (every packet), so its periods are the
+// Net window's and it lives in the Net part of each slot. One lane per record over the Net
+// pass's workgroup ranges (same grid), records parsed straight from HBM; counters and the
+// payload histogram of the range's first period in LDS, top-N keys and CPC coupons through
+// an LDS key cache into the workgroup's update log (after the DNS pass's entries).
+#define PV_N2_HBINS 1024
+#define LM2_CPC 3 // cache-local: CPC coupon of a direction (payload dir << 17 | coupon)
+struct Net2State {
+    KeyCache<PV_NCACHE> C;
+    uint32_t ctr[PV_MAX_SHIFTS + 1][PV_NET2_CTRS];
+    uint32_t hist[3][PV_N2_HBINS];
+    uint32_t mq_n;
+};
+__device__ __forceinline__ void n2_key(PV_CREF(PvParams) P, Net2State &S, uint32_t slot, uint64_t key, uint32_t idx)
+{
+    uint32_t first;
+    if (!S.C.add((key & ((1ull << 60) - 1)) | ((uint64_t)slot << 60), 1, idx, first)) log_put(P, &S.mq_n, slot, key, 1, idx);
+}
+__device__ __forceinline__ void n2_coupon(PV_CREF(PvParams) P, Net2State &S, uint32_t slot, uint32_t dir, uint32_t coupon,
+                                          uint32_t idx)
+{
+    uint32_t first;
+    if (!S.C.add(PV_LKEY(slot, LM2_CPC, ((uint64_t)dir << 17) | coupon), 1, idx, first))
+        cpc_min(P, slot, CPC_V2 + dir, coupon, (int64_t)(P.gbase + idx));
+}
+extern "C" __global__ void __launch_bounds__(256) pv_net2_kernel(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ Net2State S;
+    S.C.clear();
+    for (uint32_t i = threadIdx.x; i < (PV_MAX_SHIFTS + 1) * PV_NET2_CTRS; i += blockDim.x) (&S.ctr[0][0])[i] = 0;
+    for (uint32_t i = threadIdx.x; i < 3 * PV_N2_HBINS; i += blockDim.x) (&S.hist[0][0])[i] = 0;
+    if (threadIdx.x == 0) S.mq_n = P.mq_cnt[blockIdx.x];
+    __syncthreads();
+    const uint32_t g = P.net2_groups;
+    const bool card = g & PV_N2G_CARDINALITY, tops = g & PV_N2G_TOP_IPS;
+    uint64_t r0, r1;
+    wg_records(P, blockIdx.x, r0, r1);
+    const uint32_t p0 = r0 < r1 ? period_of(P, r0) : 0u;
+    const ParseCfg C = parse_cfg(P);
+    const GAcc R{P.recs};
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
+        const uint32_t p = period_of(P, i);
+        if (p < P.skip_before) continue; // a period already outside the window
+        const uint32_t slot = P.slot_of[p];
+        uint32_t *ctr = S.ctr[p];
+        atomicAdd(&ctr[N2_EVENTS], 1u);
+        atomicAdd(&ctr[N2_SAMPLES], 1u);
+        Parsed o;
+        parse_record(R, C, P, P.offs[i], o);
+        const uint32_t d = o.dir;
+        uint32_t *dc = ctr + N2_DIR + 8 * d;
+        atomicAdd(&dc[N2_TOTAL], 1u);
+        if (o.l3 == 4) atomicAdd(&dc[N2_V4], 1u);
+        else if (o.l3 == 6) atomicAdd(&dc[N2_V6], 1u);
+        if (o.l4 == 17) atomicAdd(&dc[N2_UDP], 1u);
+        else if (o.l4 == 6) {
+            atomicAdd(&dc[N2_TCP], 1u);
+            if (o.syn) atomicAdd(&dc[N2_SYN], 1u);
+        } else atomicAdd(&dc[N2_OTHER], 1u);
+        const uint32_t cl = min(o.caplen, 65535u);
+        if (p == p0 && cl < PV_N2_HBINS) atomicAdd(&S.hist[d][cl], 1u);
+        else sum_add(P, slot, PV_OFF_PAYLOAD2 + d * PV_PAYLOAD_BINS + cl, 1);
+        if (!(card || tops)) continue;
+        const uint32_t idx = (uint32_t)i;
+        if (o.has4) {
+            if (o.l3 != 4) continue;
+            for (uint32_t side = 0; side < 2; side++) { // source, then destination
+                if (side == 0 ? d == 1 : d == 0) continue;
+                const uint32_t ip = R.u32(o.v4 + (side ? 16 : 12));
+                if (!ip) continue;
+                if (card) {
+                    uint64_t h1, h2;
+                    murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+                    n2_coupon(P, S, slot, d, cpc_coupon(h1, h2), idx);
+                }
+                if (tops) n2_key(P, S, slot, PV_V2_IP4(d, ip), idx);
+            }
+        } else if (o.has6) {
+            if (o.l3 != 6) continue;
+            for (uint32_t side = 0; side < 2; side++) {
+                if (side == 0 ? d == 1 : d == 0) continue;
+                const uint64_t a = side ? o.v6 + 24 : o.v6 + 8;
+                const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
+                const uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
+                if (!(w0 | w1)) continue;
+                uint64_t h1, h2;
+                murmur_16(w0, w1, h1, h2);
+                if (card) n2_coupon(P, S, slot, d, cpc_coupon(h1, h2), idx);
+                if (tops) n2_key(P, S, slot, PV_V2_IP6(d, h1 ^ (h2 << 1)), idx);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (P.n_shift + 1) * PV_NET2_CTRS; i += blockDim.x) {
+        const uint32_t p = i / PV_NET2_CTRS, w = i % PV_NET2_CTRS;
+        if (S.ctr[p][w]) sum_add(P, P.slot_of[p], PV_OFF_NET2 + w, S.ctr[p][w]);
+    }
+    if (r0 < r1 && p0 >= P.skip_before)
+        for (uint32_t i = threadIdx.x; i < 3 * PV_N2_HBINS; i += blockDim.x)
+            if ((&S.hist[0][0])[i])
+                sum_add(P, P.slot_of[p0], PV_OFF_PAYLOAD2 + (i / PV_N2_HBINS) * PV_PAYLOAD_BINS + i % PV_N2_HBINS,
+                        (&S.hist[0][0])[i]);
+    for (uint32_t j = threadIdx.x; j < PV_NCACHE; j += blockDim.x) {
+        const uint64_t k = S.C.key[j];
+        if (!k || !S.C.cnt[j]) continue;
+        const uint32_t slot = (uint32_t)(k >> 60), lm = (uint32_t)(k >> 56) & 15;
+        const uint64_t pay = k & 0x00ffffffffffffffULL;
+        if (lm == LM2_CPC) cpc_min(P, slot, CPC_V2 + (uint32_t)(pay >> 17), (uint32_t)(pay & 0x1ffff), (int64_t)(P.gbase + S.C.rep[j]));
+        else log_put(P, &S.mq_n, slot, PV_KEY(lm, pay), S.C.cnt[j], S.C.rep[j]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) P.mq_cnt[blockIdx.x] = S.mq_n;
+}
+
 // ------------------------------------------------------------------ top-N merge
 // The parse passes leave per-workgroup update logs. They are bucketed by table region
 // (count -> scan -> scatter); then one workgroup per region merges the region's updates:
@@ -1616,12 +1762,6 @@ __device__ __forceinline__ uint64_t ip_tkey(uint64_t e)
 {
     return PV_KEY_METRIC(e & ((1ull << 60) - 1)) == TM_IPV4 ? (e & (0xffull << 56)) | (e & 0xffffffffull) : e;
 }
-// record range of workgroup b (the Net pass mapping), clipped to the batch
-__device__ __forceinline__ void wg_records(PV_CREF(PvParams) P, uint32_t b, uint64_t &r0, uint64_t &r1)
-{
-    r0 = min<uint64_t>((uint64_t)b * P.wt_per_block * PV_WT, P.n);
-    r1 = min<uint64_t>(r0 + (uint64_t)P.wt_per_block * PV_WT, P.n);
-}
 
 // Combine: one workgroup per Net/DNS workgroup range aggregates its update log and its
 // records' dense IP entries in an LDS table (key -> weight, smallest record index), so a
@@ -1645,7 +1785,8 @@ __device__ __forceinline__ void comb_out(PV_CREF(PvParams) P, CombState &S, uint
                                          uint32_t rep)
 {
     uint64_t e0 = ck;
-    if (PV_KEY_METRIC(ck & ((1ull << 60) - 1)) == TM_IPV4) {
+    if (PV_KEY_METRIC(ck & ((1ull << 60) - 1)) == TM_IPV4 && !PV_IS_V2_IP4(ck & ((1ull << 60) - 1))) {
+        // a dense IP log entry (v1): table key without the card / dir bits
         e0 = ip_tkey(ck);
         w = PV_W_IP4 | ((uint32_t)(ck >> 32) & 1u) << 30 | ((uint32_t)(ck >> 33) & 1u) << 29 | (w & PV_W_CNT);
     }
@@ -1869,7 +2010,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
             const uint32_t g = S.nbase + k;
             const uint64_t pos = rbase + S.nidx[k];
             if (g < P.nn_cap) P.nn[g] = PvNewName{tb, S.nrep[k], pos};
-            else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k]);
+            else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k], nullptr, S.key[S.nidx[k]]);
         }
         __syncthreads();
     }
@@ -2003,13 +2144,15 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
         const uint32_t i = b + threadIdx.x;
         const bool act = i < n;
         PvNewName e{0, 0, 0};
+        uint64_t tkey = 0;
         uint32_t metric = 0, size = 0, start = 0, nl = 0, mlen = 0;
         uint64_t m = 0, a6 = 0;
         Parsed o;
         uint64_t roff = 0;
         if (act) {
             e = P.nn[i];
-            metric = PV_KEY_METRIC(P.tkeys[e.pos]);
+            tkey = P.tkeys[e.pos];
+            metric = PV_KEY_METRIC(tkey);
             roff = P.offs[e.rep];
         }
         const uint64_t wbase = roff & ~15ull;
@@ -2034,7 +2177,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
         }
         if (act) {
             if (metric == TM_IPV6) {
-                a6 = (o.dir == 0) ? o.v6 + 8 : o.v6 + 24;
+                a6 = ip6_name_addr(R, o, tkey);
                 size = 18;
             } else {
                 NameStats st;

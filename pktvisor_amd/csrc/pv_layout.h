@@ -30,7 +30,13 @@
 #define PV_MQ_PER_REC 7
 #define PV_CACHE_MAX 4096
 
-// group bits (same values as pv_net_group / pv_dns_group in include/pvgpu.h)
+// group bits (same values as pv_net_group / pv_dns_group / pv_net2_group in include/pvgpu.h)
+#define PV_N2G_COUNTERS 1u
+#define PV_N2G_CARDINALITY 2u
+#define PV_N2G_QUANTILES 4u
+#define PV_N2G_TOP_GEO 8u
+#define PV_N2G_TOP_IPS 16u
+#define PV_N2G_ON 0x40000000u
 #define PV_NET_COUNTERS_BIT 1u
 #define PV_NET_CARDINALITY_BIT 2u
 #define PV_NET_TOP_IPS_BIT 8u
@@ -53,7 +59,11 @@
 #define PV_RCODE_BINS 16
 #define PV_OFF_NET 0
 #define PV_OFF_PAYLOAD (PV_OFF_NET + PV_NET_CTRS)
-#define PV_SUM_NET_WORDS (PV_OFF_PAYLOAD + PV_PAYLOAD_BINS) // net part [0, PV_SUM_NET_WORDS)
+// Net v2 (src/handlers/net/v2): its counters, then one payload-size histogram per direction
+#define PV_NET2_CTRS 32
+#define PV_OFF_NET2 (PV_OFF_PAYLOAD + PV_PAYLOAD_BINS)
+#define PV_OFF_PAYLOAD2 (PV_OFF_NET2 + PV_NET2_CTRS) // + dir * PV_PAYLOAD_BINS
+#define PV_SUM_NET_WORDS (PV_OFF_PAYLOAD2 + 3 * PV_PAYLOAD_BINS) // net part [0, PV_SUM_NET_WORDS)
 #define PV_OFF_DNS PV_SUM_NET_WORDS
 #define PV_OFF_PORT (PV_OFF_DNS + PV_DNS_CTRS)
 #define PV_OFF_QTYPE (PV_OFF_PORT + PV_PORT_BINS)
@@ -65,6 +75,10 @@ enum {
     NC_EVENTS = 0, NC_SAMPLES, NC_UDP, NC_TCP, NC_OTHER, NC_V4, NC_V6, NC_SYN, NC_IN, NC_OUT, NC_UNK, NC_TOTAL,
     NC_FILTERED, NC_COUNT
 };
+// Net v2 counters (src/handlers/net/v2/NetStreamHandler.h:61-96): base events, then per
+// direction d (0 in, 1 out, 2 unknown) at N2_DIR + 8 d
+enum { N2_EVENTS = 0, N2_SAMPLES = 1, N2_FILTERED = 2, N2_DIR = 8 };
+enum { N2_TOTAL = 0, N2_V4, N2_V6, N2_UDP, N2_TCP, N2_OTHER, N2_SYN };
 // dns counters (src/handlers/dns/v1/DnsStreamHandler.h:94-139 + base event counters)
 enum {
     DC_EVENTS = 0, DC_SAMPLES, DC_QUERIES, DC_REPLIES, DC_TCP, DC_UDP, DC_V4, DC_V6, DC_NX, DC_REFUSED, DC_SRVFAIL,
@@ -73,9 +87,10 @@ enum {
 
 // ---- MIN region (int64 global record index), per slot: CPC lg_k = 11 => 2048 rows x 64 cols
 #define PV_CPC_COUPONS (2048 * 64)
-enum { CPC_SRC = 0, CPC_DST = 1, CPC_QNAME = 2, CPC_SKETCHES = 3 };
+// v1 src_ips_in / dst_ips_out, v2 ips per direction (in, out, unknown), then the DNS qname
+enum { CPC_SRC = 0, CPC_DST = 1, CPC_V2 = 2, CPC_QNAME = 5, CPC_SKETCHES = 6 };
 #define PV_MIN_WORDS (CPC_SKETCHES * PV_CPC_COUPONS)
-#define PV_MIN_NET_WORDS (2 * PV_CPC_COUPONS) // net part [0, 2 * coupons), dns part after
+#define PV_MIN_NET_WORDS (CPC_QNAME * PV_CPC_COUPONS) // net part [0, 5 * coupons), dns part after
 #define PV_CPC_EMPTY 0x7fffffffffffffffLL
 
 // ---- top-N metrics: key = metric << 56 | payload (56 bits)
@@ -89,6 +104,13 @@ enum {
     TM_ECS = 16 // EDNS Client Subnet of a query (name record: family byte + 16 address bytes)
 };
 #define PV_KEY(metric, payload) (((uint64_t)(metric) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
+// Net v2 top IPs share the Net table with v1's, told apart by a payload bit and carrying
+// the direction: IPv4 payload 1 << 40 | dir << 34 | address, IPv6 1 << 55 | dir << 53 |
+// 53-bit address hash
+#define PV_V2_IP4(dir, ip) PV_KEY(TM_IPV4, (1ull << 40) | ((uint64_t)(dir) << 34) | (uint32_t)(ip))
+#define PV_V2_IP6(dir, h) PV_KEY(TM_IPV6, (1ull << 55) | ((uint64_t)(dir) << 53) | ((h) & ((1ull << 53) - 1)))
+#define PV_IS_V2_IP4(k) ((((k) >> 56) == TM_IPV4) && (((k) >> 40) & 1))
+#define PV_IS_V2_IP6(k) ((((k) >> 56) == TM_IPV6) && (((k) >> 55) & 1))
 #define PV_KEY_METRIC(k) ((uint32_t)((k) >> 56))
 // table of a (handler slot, metric): Net metrics (IPv4 / IPv6) in table slot, the DNS
 // metrics in table PV_SLOTS + slot
@@ -300,6 +322,7 @@ struct PvParams {
     PV_G uint32_t *tp_tabs; // per region: bit t set when the region's updates touch table t
     PV_G uint32_t *cb_h;    // per combine workgroup: its entries per region
     PV_G uint32_t *tab_live; // per table: entries held (bounded by pv_topn_purge)
+    uint32_t net2_groups;   // Net v2 handler attached: PV_N2G_* group bits | PV_N2G_ON (0 = not attached)
     PV_G uint64_t *tp_buf;
     PV_G uint32_t *nn_cnt;
     PV_G PvNewName *nn;

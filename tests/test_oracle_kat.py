@@ -20,6 +20,11 @@ def test_oracle_matches_reference_kats(oracle, case):
         assert jget(out, path) >= lo, (case["cite"], path)
     for path, n in case.get("len", []):
         assert len(jget(out, path)) == n, (case["cite"], path)
+    for paths, want in case.get("sums", []):
+        assert sum(jget(out, q) for q in paths) == want, (case["cite"], paths)
+    for path in case.get("absent", []):
+        with pytest.raises((KeyError, IndexError, TypeError)):
+            jget(out, path)
 
 
 def test_readme_sample_shape(oracle):
