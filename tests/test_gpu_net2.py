@@ -31,7 +31,7 @@ def run_both(oracle, pcap, host, periods, tmp_path, net2_config=None, groups=ALL
 def test_net2_fixture_parity(oracle, tmp_path, fixture, host, periods):
     pcap = open(os.path.join(GOLD, fixture), "rb").read()
     gpu, ref = run_both(oracle, pcap, host, periods, tmp_path)
-    assert "net" in gpu
+    assert all("net" in w for w in gpu.values())
     assert diff(gpu, ref) is None, diff(gpu, ref)
 
 
