@@ -64,6 +64,14 @@ enum pv_net2_group {
     PV_NET2_COUNTERS = 1u << 0, PV_NET2_CARDINALITY = 1u << 1, PV_NET2_QUANTILES = 1u << 2, PV_NET2_TOP_GEO = 1u << 3,
     PV_NET2_TOP_IPS = 1u << 4
 };
+/* DNS v2 handler groups (src/handlers/dns/v2/DnsStreamHandler.h:40-52, _group_defs :565-575). */
+enum pv_dns2_group {
+    PV_DNS2_CARDINALITY = 1u << 0, PV_DNS2_COUNTERS = 1u << 1, PV_DNS2_QUANTILES = 1u << 2, PV_DNS2_TOP_ECS = 1u << 3,
+    PV_DNS2_TOP_QTYPES = 1u << 4, PV_DNS2_TOP_RCODES = 1u << 5, PV_DNS2_TOP_SIZE = 1u << 6, PV_DNS2_TOP_QNAMES = 1u << 7,
+    PV_DNS2_TOP_PORTS = 1u << 8, PV_DNS2_XACT_TIMES = 1u << 9
+};
+#define PV_DNS2_DEFAULT_GROUPS (PV_DNS2_CARDINALITY | PV_DNS2_COUNTERS | PV_DNS2_QUANTILES | PV_DNS2_TOP_QNAMES | \
+                                PV_DNS2_TOP_RCODES | PV_DNS2_TOP_QTYPES)
 #define PV_NET2_DEFAULT_GROUPS (PV_NET2_COUNTERS | PV_NET2_CARDINALITY | PV_NET2_QUANTILES | PV_NET2_TOP_GEO | PV_NET2_TOP_IPS)
 /* OR'ed into pv_config.net_groups / dns_groups: the bits are the enabled set even when it is
  * empty ("disable: [all]"); without it 0 selects the handler's default groups */
@@ -89,6 +97,9 @@ typedef struct pv_config {
                                 database, NetStreamHandler::_filtering, net/v1/NetStreamHandler.cpp:223-283) */
     uint32_t net2_groups;    /* Net v2 handler ("net", src/handlers/net/v2) attached next to v1: pv_net2_group bits
                                 | PV_GROUPS_SET, or PV_NET2_ATTACH for its default groups; 0 = not attached */
+    uint32_t dns2_groups;    /* DNS v2 handler ("dns", src/handlers/dns/v2) in place of v1: pv_dns2_group bits
+                                | PV_GROUPS_SET, or PV_NET2_ATTACH for its default groups; 0 = DNS v1. Its
+                                filters, top_ecs and multi-GPU edge replay are not built */
 } pv_config;
 #define PV_NET2_ATTACH 0x40000000u
 

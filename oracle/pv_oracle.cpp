@@ -329,6 +329,9 @@ static const std::map<uint16_t, std::string> &rcode_names()
 
 // ---------------------------------------------------------------- config
 enum { NG_COUNTERS = 1, NG_CARDINALITY = 2, NG_TOP_GEO = 4, NG_TOP_IPS = 8 };
+// DNS v2 groups (src/handlers/dns/v2/DnsStreamHandler.h:40-52, _group_defs :565-575)
+enum { D2G_CARDINALITY = 1, D2G_COUNTERS = 2, D2G_QUANTILES = 4, D2G_TOP_ECS = 8, D2G_TOP_QTYPES = 16,
+       D2G_TOP_RCODES = 32, D2G_TOP_SIZE = 64, D2G_TOP_QNAMES = 128, D2G_TOP_PORTS = 256, D2G_XACT_TIMES = 512 };
 // Net v2 groups (src/handlers/net/v2/NetStreamHandler.h:25-31): Counters, Cardinality, Quantiles, TopGeo, TopIps
 enum { N2G_COUNTERS = 1, N2G_CARDINALITY = 2, N2G_QUANTILES = 4, N2G_TOP_GEO = 8, N2G_TOP_IPS = 16 };
 enum { DG_CARDINALITY = 1, DG_COUNTERS = 2, DG_QUANTILES = 4, DG_HISTOGRAMS = 8, DG_TRANSACTIONS = 16, DG_TOP_ECS = 32,
@@ -353,6 +356,8 @@ struct Config {
     bool net_filter_all = false; // net geo / ASN filters with no geo database: every packet filtered (:223-283)
     // Net v2 handler attached ("net"): its groups (N2G_*), 0 = not attached
     uint32_t net2_groups = 0;
+    // DNS v2 handler in place of v1 ("dns" is both versions' schema key): its groups (D2G_*), 0 = v1
+    uint32_t dns2_groups = 0;
     bool filter_all = false; // geoloc_notfound / asn_notfound with no geo database: every packet filtered (:619-642)
     // DNS v1 filters (DnsStreamHandler::start, dns/v1/DnsStreamHandler.cpp:60-160)
     bool exclude_noerror = false;   // "exclude_noerror" (:61-63)
@@ -889,6 +894,38 @@ struct Net2Bucket : BaseBucket {
     }
 };
 
+// DNS v2 (src/handlers/dns/v2/DnsStreamHandler.h:75-291): transaction-centric, per direction
+struct Dns2Dir {
+    uint64_t xacts = 0, UDP = 0, TCP = 0, IPv4 = 0, IPv6 = 0, NX = 0, ECS = 0, REFUSED = 0, SRVFAIL = 0, NOERROR = 0,
+             NODATA = 0, AD = 0, AA = 0, CD = 0, timeout = 0, orphan = 0;
+    bool seen = false; // DnsMetricsBucket::dir_setup ran for this direction
+    ExactQuantile<uint64_t> time;
+    ExactQuantile<double> ratio;
+    Cpc qname;
+    ExactTop<std::string> ecs, qname2, qname3, nx, refused, sized, srvfail, nodata, noerror, slow;
+    ExactTop<uint16_t> port, qtype, rcode;
+    void merge(const Dns2Dir &o)
+    {
+        xacts += o.xacts; UDP += o.UDP; TCP += o.TCP; IPv4 += o.IPv4; IPv6 += o.IPv6; NX += o.NX; ECS += o.ECS;
+        REFUSED += o.REFUSED; SRVFAIL += o.SRVFAIL; NOERROR += o.NOERROR; NODATA += o.NODATA; AD += o.AD; AA += o.AA;
+        CD += o.CD; timeout += o.timeout; orphan += o.orphan;
+        seen = seen || o.seen;
+        time.merge(o.time); ratio.merge(o.ratio); qname.merge(o.qname);
+        ecs.merge(o.ecs); qname2.merge(o.qname2); qname3.merge(o.qname3); nx.merge(o.nx); refused.merge(o.refused);
+        sized.merge(o.sized); srvfail.merge(o.srvfail); nodata.merge(o.nodata); noerror.merge(o.noerror);
+        slow.merge(o.slow); port.merge(o.port); qtype.merge(o.qtype); rcode.merge(o.rcode);
+    }
+};
+struct Dns2Bucket : BaseBucket {
+    uint64_t filtered = 0;
+    Dns2Dir dir[3]; // in, out, unknown
+    void merge(const Dns2Bucket &o)
+    {
+        filtered += o.filtered;
+        for (int d = 0; d < 3; d++) dir[d].merge(o.dir[d]);
+    }
+};
+
 struct DnsBucket : BaseBucket {
     uint64_t xacts_total = 0, xacts_in = 0, xacts_out = 0, xacts_timed_out = 0, queries = 0, replies = 0, UDP = 0,
              TCP = 0, IPv4 = 0, IPv6 = 0, NX = 0, REFUSED = 0, SRVFAIL = 0, NOERROR = 0, NODATA = 0, total = 0,
@@ -968,11 +1005,21 @@ struct Engine {
     Window<NetBucket> net;
     Window<Net2Bucket> net2;
     Window<DnsBucket> dns;
+    Window<Dns2Bucket> dns2;
     std::unordered_map<XactKey, Xact, XactKeyHash> xacts;
+    // DNS v2: one TransactionManager per direction (DnsMetricsManager::_pair_manager, v2 .h:421-437)
+    struct Xact2 {
+        TS start;
+        size_t query_size;
+        bool cd;
+        std::string ecs;
+    };
+    std::unordered_map<XactKey, Xact2, XactKeyHash> xacts2[3];
+    float per90_2[3] = {0.0f, 0.0f, 0.0f};
     uint32_t ttl_s = 0, ttl_ms = 0;
     float to90 = 0.0f, from90 = 0.0f;
 
-    explicit Engine(const Config &c) : cfg(c), net(c.num_periods), net2(c.num_periods), dns(c.num_periods)
+    explicit Engine(const Config &c) : cfg(c), net(c.num_periods), net2(c.num_periods), dns(c.num_periods), dns2(c.num_periods)
     {
         // TransactionManager.h:60-68
         if (c.xact_ttl_ms > 1000) { ttl_s = c.xact_ttl_ms / 1000; ttl_ms = c.xact_ttl_ms - ttl_s * 1000; }
@@ -984,12 +1031,14 @@ struct Engine {
         net.set_start(ts);
         net2.set_start(ts);
         dns.set_start(ts);
+        dns2.set_start(ts);
     }
     void end(TS ts)
     {
         net.set_end(ts);
         net2.set_end(ts);
         dns.set_end(ts);
+        dns2.set_end(ts);
     }
 
     // NetworkMetricsManager::process_packet + bucket (net/v1 ...cpp:516-548,682-764)
@@ -1178,6 +1227,10 @@ struct Engine {
             return;
         }
 
+        if (cfg.dns2_groups) {
+            dns2_event(p, m, hm.d, qr, rcode, ancount, txid, suffix_size);
+            return;
+        }
         // DnsMetricsManager::process_dns_layer (:1350-1370)
         if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
         dns.new_event(true);
@@ -1259,6 +1312,100 @@ struct Engine {
             }
         } else {
             xacts[k] = Xact{p.ts, m.len};
+        }
+    }
+
+    // ---------------------------------------------------------------- DNS v2
+    // DnsMetricsManager::process_dns_layer, v2 (dns/v2/DnsStreamHandler.cpp:1100-1145): every
+    // message is an event; a query opens a transaction in its direction's map (toHost query:
+    // "in"), a response looks in the swapped direction's map and accounts the transaction
+    void dns2_event(const DnsEv &p, const DnsMsg &m, const uint8_t *h, bool qr, uint8_t rcode, uint16_t ancount,
+                    uint16_t txid, size_t suffix_size)
+    {
+        if (dns2.maybe_shift(p.ts)) on_dns2_period_shift(p.ts);
+        dns2.new_event(true);
+        Dns2Bucket &b = dns2.live();
+        const uint32_t g = cfg.dns2_groups;
+        const XactKey k{p.flowkey, txid};
+        if (qr) {
+            const int xd = p.dir == DIR_TO_HOST ? 1 : (p.dir == DIR_FROM_HOST ? 0 : 2);
+            Dns2Dir &x = b.dir[xd];
+            x.seen = true;
+            auto it = xacts2[xd].find(k);
+            if (it == xacts2[xd].end()) { x.orphan++; return; }
+            Xact2 q = it->second;
+            xacts2[xd].erase(it);
+            TS d;
+            d.sec = p.ts.sec > q.start.sec ? p.ts.sec - q.start.sec : q.start.sec - p.ts.sec;
+            d.nsec = p.ts.nsec - q.start.nsec;
+            if (d.nsec < 0) { d.sec--; d.nsec += 1000000000L; }
+            if (d.sec > (int64_t)ttl_s || (d.sec == (int64_t)ttl_s && (d.nsec / 1.0e6) >= ttl_ms)) { x.timeout++; return; }
+            // DnsMetricsBucket::new_dns_transaction, v2 (:925-1089)
+            const uint64_t us = (uint64_t)((d.sec * 1000000000LL) + d.nsec) / 1000;
+            if (g & D2G_COUNTERS) {
+                x.xacts++;
+                if (p.l3 == L3_IPV6) x.IPv6++;
+                else if (p.l3 == L3_IPV4) x.IPv4++;
+                if (p.tcp) x.TCP++;
+                else x.UDP++;
+                if (q.cd) x.CD++;
+                if (rcode == 0) { x.NOERROR++; if (!ancount) x.NODATA++; }
+                else if (rcode == 2) x.SRVFAIL++;
+                else if (rcode == 3) x.NX++;
+                else if (rcode == 5) x.REFUSED++;
+                if (h[2] & 0x04) x.AA++;
+                if (h[3] & 0x20) x.AD++;
+            }
+            if (q.query_size && (g & D2G_TOP_SIZE)) x.ratio.update((double)m.len / (double)q.query_size);
+            if (p.port && (g & D2G_TOP_PORTS)) x.port.update(p.port);
+            if (g & D2G_XACT_TIMES) x.time.update(us);
+            DnsParse r = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{h, m.len});
+            if (r.ok) {
+                x.rcode.update(rcode);
+                if (r.has_query) {
+                    const std::string name = lower(r.name);
+                    if (g & D2G_CARDINALITY) x.qname.update_str(name);
+                    x.qtype.update(r.qtype);
+                    if (g & D2G_TOP_RCODES) {
+                        if (rcode == 2) x.srvfail.update(name);
+                        else if (rcode == 3) x.nx.update(name);
+                        else if (rcode == 5) x.refused.update(name);
+                        else if (rcode == 0) { x.noerror.update(name); if (!ancount) x.nodata.update(name); }
+                    }
+                    if (g & D2G_TOP_SIZE) x.sized.update(name, m.len);
+                    if (per90_2[xd] > 0 && (float)us >= per90_2[xd] && (g & D2G_XACT_TIMES)) x.slow.update(name);
+                    if (g & D2G_TOP_QNAMES) {
+                        std::string q2, q3;
+                        aggregate_domain(name, suffix_size, q2, q3);
+                        x.qname2.update(q2);
+                        if (!q3.empty()) x.qname3.update(q3);
+                    }
+                }
+                if ((g & D2G_TOP_ECS) && !q.ecs.empty()) {
+                    if (g & D2G_COUNTERS) x.ECS++;
+                    x.ecs.update(q.ecs);
+                }
+            }
+        } else {
+            const int xd = p.dir == DIR_TO_HOST ? 0 : (p.dir == DIR_FROM_HOST ? 1 : 2);
+            std::string subnet;
+            if ((g & D2G_TOP_ECS) && m.len >= 12 && rd16be(h + 10) > 0) subnet = ecs_subnet(m);
+            xacts2[xd][k] = Xact2{p.ts, m.len, (h[3] & 0x10) != 0, subnet};
+        }
+    }
+
+    // DnsMetricsManager::on_period_shift, v2 (dns/v2/DnsStreamHandler.h:440-453)
+    void on_dns2_period_shift(TS ts)
+    {
+        for (int d = 0; d < 3; d++) {
+            uint64_t timed_out = 0;
+            for (auto it = xacts2[d].begin(); it != xacts2[d].end();) {
+                if (ts.sec >= (int64_t)ttl_s + it->second.start.sec) { it = xacts2[d].erase(it); timed_out++; }
+                else ++it;
+            }
+            if (timed_out) { dns2.live().dir[d].seen = true; dns2.live().dir[d].timeout += timed_out; }
+            const Dns2Bucket &b1 = *dns2.buckets.at(1);
+            if (b1.dir[d].seen && !b1.dir[d].time.empty()) per90_2[d] = (float)b1.dir[d].time.p(0.90);
         }
     }
 
@@ -1771,6 +1918,67 @@ static void net2_json(J &j, const Net2Bucket &b, size_t topn, uint32_t g)
     }
 }
 
+// DnsMetricsBucket::to_json, DNS v2 (dns/v2/DnsStreamHandler.cpp:678-757); rates excluded
+static void dns2_json(J &j, const Dns2Bucket &b, size_t topn, uint32_t g)
+{
+    auto u16s = [](const uint16_t &v) { return std::to_string(v); };
+    auto rc = [](const uint16_t &v) { auto &m = rcode_names(); auto it = m.find(v); return it != m.end() ? it->second : std::to_string(v); };
+    auto qt = [](const uint16_t &v) { auto &m = qtype_names(); auto it = m.find(v); return it != m.end() ? it->second : std::to_string(v); };
+    j.key("period"); j.obj();
+    j.key("start_ts"); j.i64(b.start.sec);
+    j.key("length"); j.u64(b.period_length);
+    j.end_obj();
+    j.key("observed_packets"); j.u64(b.num_events);
+    j.key("deep_sampled_packets"); j.u64(b.num_samples);
+    if (g & D2G_COUNTERS) { j.key("filtered_packets"); j.u64(b.filtered); }
+    static const char *names[3] = {"in", "out", "unknown"};
+    for (int d = 0; d < 3; d++) {
+        const Dns2Dir &x = b.dir[d];
+        if (!x.seen) continue;
+        j.key(names[d]); j.obj();
+        if (g & D2G_COUNTERS) {
+            const std::pair<const char *, uint64_t> ctr[] = {
+                {"xacts", x.xacts}, {"udp_xacts", x.UDP}, {"tcp_xacts", x.TCP}, {"dot_xacts", 0}, {"doh_xacts", 0},
+                {"dnscrypt_udp_xacts", 0}, {"dnscrypt_tcp_xacts", 0}, {"doq_xacts", 0}, {"ipv4_xacts", x.IPv4},
+                {"ipv6_xacts", x.IPv6}, {"nxdomain_xacts", x.NX}, {"ecs_xacts", x.ECS}, {"refused_xacts", x.REFUSED},
+                {"srvfail_xacts", x.SRVFAIL}, {"noerror_xacts", x.NOERROR}, {"nodata_xacts", x.NODATA},
+                {"authenticated_data_xacts", x.AD}, {"authoritative_answer_xacts", x.AA},
+                {"checking_disabled_xacts", x.CD}, {"timeout_queries", x.timeout}, {"orphan_responses", x.orphan}};
+            for (auto &c : ctr) { j.key(c.first); j.u64(c.second); }
+        }
+        if (g & D2G_CARDINALITY) { j.key("cardinality"); j.obj(); j.key("qname"); j.i64(lround(x.qname.estimate())); j.end_obj(); }
+        if (g & D2G_TOP_PORTS) top_json(j, "top_udp_ports_xacts", x.port, topn, u16s);
+        if (g & D2G_TOP_ECS) {
+            j.key("top_geo_loc_ecs_xacts"); j.arr(); j.end_arr();
+            j.key("top_asn_ecs_xacts"); j.arr(); j.end_arr();
+            top_json(j, "top_ecs_xacts", x.ecs, topn, id_str);
+        }
+        if (g & D2G_TOP_RCODES) {
+            top_json(j, "top_nxdomain_xacts", x.nx, topn, id_str);
+            top_json(j, "top_refused_xacts", x.refused, topn, id_str);
+            top_json(j, "top_srvfail_xacts", x.srvfail, topn, id_str);
+            top_json(j, "top_nodata_xacts", x.nodata, topn, id_str);
+            top_json(j, "top_noerror_xacts", x.noerror, topn, id_str);
+            top_json(j, "top_rcode_xacts", x.rcode, topn, rc);
+        }
+        if (g & D2G_TOP_QNAMES) {
+            top_json(j, "top_qname2_xacts", x.qname2, topn, id_str);
+            top_json(j, "top_qname3_xacts", x.qname3, topn, id_str);
+        }
+        if (g & D2G_TOP_SIZE) {
+            top_json(j, "top_response_bytes", x.sized, topn, id_str);
+            quant_json(j, "response_query_size_ratio", x.ratio);
+        }
+        if (g & D2G_TOP_QTYPES) top_json(j, "top_qtype_xacts", x.qtype, topn, qt);
+        if (g & D2G_XACT_TIMES) {
+            quant_json(j, "xact_time_us", x.time);
+            hist_json(j, "xact_histogram_us", x.time);
+            top_json(j, "top_slow_xacts", x.slow, topn, id_str);
+        }
+        j.end_obj();
+    }
+}
+
 static void dns_json(J &j, const DnsBucket &b, size_t topn, uint32_t g)
 {
     auto u16s = [](const uint16_t &v) { return std::to_string(v); };
@@ -1922,6 +2130,7 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "filter_all") c.filter_all = atoi(v.c_str()) != 0;
         else if (k == "net_filter_all") c.net_filter_all = atoi(v.c_str()) != 0;
         else if (k == "net2_groups") c.net2_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
+        else if (k == "dns2_groups") c.dns2_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "topn_pct") c.topn_pct = (uint32_t)atoi(v.c_str());
         else if (k == "exclude_noerror") c.exclude_noerror = atoi(v.c_str()) != 0;
         else if (k == "only_rcode_mask") c.only_rcode_mask = (uint32_t)strtoul(v.c_str(), nullptr, 0);
@@ -2004,8 +2213,13 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
         auto n2 = window_bucket(e.net2, w);
         j.key("net"); j.obj(); net2_json(j, *n2, c.topn_count, c.net2_groups); j.end_obj();
     }
-    auto db = window_bucket(e.dns, w);
-    j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_groups); j.end_obj();
+    if (c.dns2_groups) {
+        auto d2 = window_bucket(e.dns2, w);
+        j.key("dns"); j.obj(); dns2_json(j, *d2, c.topn_count, c.dns2_groups); j.end_obj();
+    } else {
+        auto db = window_bucket(e.dns, w);
+        j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_groups); j.end_obj();
+    }
     j.end_obj();
     j.end_obj();
     *out = strdup(j.s.c_str());

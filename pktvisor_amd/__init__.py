@@ -47,7 +47,7 @@ class pv_config(ctypes.Structure):
                 ("linktype", ctypes.c_uint32), ("ts_nano", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("table_log2", ctypes.c_uint32), ("max_records", ctypes.c_uint64),
                 ("topn_percentile_threshold", ctypes.c_uint32), ("net_filter_all", ctypes.c_uint32),
-                ("net2_groups", ctypes.c_uint32)]
+                ("net2_groups", ctypes.c_uint32), ("dns2_groups", ctypes.c_uint32)]
 
 
 class pv_dns_filters(ctypes.Structure):
@@ -297,7 +297,7 @@ class PvHandlers:
                  table_log2: int = 0, max_records: int = 1 << 20, net_groups: int = 0, dns_groups: int = 0,
                  dns_filters: Optional[dict] = None, net_config: Optional[dict] = None,
                  dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0,
-                 net2_config: Optional[dict] = None):
+                 net2_config: Optional[dict] = None, dns2_config: Optional[dict] = None):
         from pktvisor_amd import config as pvcfg
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
@@ -306,9 +306,18 @@ class PvHandlers:
         if net2_config is not None:
             # the Net v2 handler ("net") attached next to v1 ("packets")
             net2_groups = pvcfg.net2_start(dict(net2_config))
-        if net_config is not None or dns_config is not None or net2_config is not None:
+        dns2_groups = 0
+        if dns2_config is not None:
+            # the DNS v2 handler in place of v1 (both use the "dns" schema key)
+            if dns_config:
+                raise PvError("dns_config and dns2_config are exclusive: one DNS handler version")
+            d2 = pvcfg.dns2_start(dict(dns2_config))
+            dns2_groups = d2["groups"]
+            if d2["xact_ttl_ms"] is not None:
+                xact_ttl_ms = d2["xact_ttl_ms"]
+        if net_config is not None or dns_config is not None or net2_config is not None or dns2_config is not None:
             ncfg, dcfg = dict(net_config or {}), dict(dns_config or {})
-            win = pvcfg.window_config([ncfg, dcfg, dict(net2_config or {})])
+            win = pvcfg.window_config([ncfg, dcfg, dict(net2_config or {}), dict(dns2_config or {})])
             if win.get("deep_sample_rate", 100) != 100:
                 raise pvcfg.ConfigException("deep_sample_rate below 100 is not supported by the GPU handler")
             num_periods = win.get("num_periods", num_periods)
@@ -317,11 +326,12 @@ class PvHandlers:
             n, d = pvcfg.net_start(ncfg), pvcfg.dns_start(dcfg)
             net_groups, dns_groups, net_filter_all = n["groups"], d["groups"], int(n["filter_all"])
             filt = d["filters"]
-            if d["xact_ttl_ms"] is not None:
+            if d["xact_ttl_ms"] is not None and dns2_config is None:
                 xact_ttl_ms = d["xact_ttl_ms"]
         self._host = host_spec.encode() if host_spec else None
         cfg = pv_config(self._host, num_periods, topn_count, xact_ttl_ms, net_groups, dns_groups, linktype, ts_nano,
-                        device, table_log2, max_records, topn_percentile_threshold, net_filter_all, net2_groups)
+                        device, table_log2, max_records, topn_percentile_threshold, net_filter_all, net2_groups,
+                        dns2_groups)
         self.num_periods = num_periods
         self.ctx = ctypes.c_void_p()
         rc = self.lib.pv_create(ctypes.byref(cfg), ctypes.byref(self.ctx))
@@ -442,9 +452,9 @@ class PvHandlers:
     def window_regions(self):
         """[(device ptr, 64-bit words, PV_REDUCE_SUM | PV_REDUCE_MIN)] of both live windows, in the
         order every rank with the same windows lists them (pv_window_regions)"""
-        regs = (pv_region * 64)()
+        regs = (pv_region * 256)()
         n = ctypes.c_uint32()
-        self._check(self.lib.pv_window_regions(self.ctx, regs, 64, ctypes.byref(n)), "pv_window_regions")
+        self._check(self.lib.pv_window_regions(self.ctx, regs, 256, ctypes.byref(n)), "pv_window_regions")
         return [(int(r.ptr), int(r.words), int(r.op)) for r in regs[: n.value]]
 
     def advance_windows(self, part: int, thresholds):

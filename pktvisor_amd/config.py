@@ -164,6 +164,35 @@ def net2_start(cfg: dict) -> int:
     return groups | GROUPS_SET
 
 
+# DNS v2 (src/handlers/dns/v2/DnsStreamHandler.h:40-52,549-575; defaults .cpp:51-57)
+DNS2_GROUP_DEFS = {"cardinality": 1 << 0, "counters": 1 << 1, "quantiles": 1 << 2, "top_ecs": 1 << 3,
+                   "top_qtypes": 1 << 4, "top_rcodes": 1 << 5, "top_size": 1 << 6, "top_qnames": 1 << 7,
+                   "top_ports": 1 << 8, "xact_times": 1 << 9}
+DNS2_DEFAULT_GROUPS = ("cardinality", "counters", "quantiles", "top_qnames", "top_rcodes", "top_qtypes")
+DNS2_CONFIG_DEFS = ("exclude_noerror", "only_rcode", "only_dnssec_response", "answer_count", "only_qtype", "only_qname",
+                    "only_qname_suffix", "geoloc_notfound", "asn_notfound", "dnstap_msg_type", "public_suffix_list",
+                    "recorded_stream", "xact_ttl_secs", "xact_ttl_ms")
+
+
+def dns2_start(cfg: dict) -> dict:
+    """DnsStreamHandler v2 start (src/handlers/dns/v2/DnsStreamHandler.cpp:43-236) up to the
+    signal wiring: {"groups": bits | GROUPS_SET, "xact_ttl_ms": int|None}. The v2 filters and
+    top_ecs are not built for the GPU handler and are refused."""
+    validate_configs(cfg, DNS2_CONFIG_DEFS)
+    groups = process_groups(cfg, DNS2_GROUP_DEFS, DNS2_DEFAULT_GROUPS)
+    for k in DNS2_CONFIG_DEFS:
+        if k in cfg and k not in ("recorded_stream", "xact_ttl_secs", "xact_ttl_ms"):
+            raise ConfigException(f"{k} is not supported by the GPU DNS v2 handler")
+    if groups & DNS2_GROUP_DEFS["top_ecs"]:
+        raise ConfigException("top_ecs is not supported by the GPU DNS v2 handler")
+    ttl = None
+    if "xact_ttl_ms" in cfg:
+        ttl = _uint(cfg, "xact_ttl_ms")
+    elif "xact_ttl_secs" in cfg:
+        ttl = _uint(cfg, "xact_ttl_secs") * 1000
+    return {"groups": groups | GROUPS_SET, "xact_ttl_ms": ttl}
+
+
 def dns_start(cfg: dict) -> dict:
     """DnsStreamHandler::start (src/handlers/dns/v1/DnsStreamHandler.cpp:43-201) up to the signal
     wiring: {"groups": bits | GROUPS_SET, "filters": pv_dns_filters fields, "xact_ttl_ms": int|None}"""

@@ -297,6 +297,8 @@ struct pv_ctx {
     uint32_t ttl_s = 0, ttl_ms = 0;
     uint32_t net_groups = PV_NET_DEFAULT_GROUPS, dns_groups = PV_DNS_DEFAULT_GROUPS;
     uint32_t net2_groups = 0; // Net v2 attached: PV_NET2_* bits | PV_N2G_ON
+    uint32_t dns2_groups = 0; // DNS v2 in place of v1: PV_DNS2_* bits | PV_N2G_ON
+    float p90_2[3] = {0.0f, 0.0f, 0.0f}; // DNS v2 per-direction p90 of the last closed bucket (per_90th)
     // device state
     uint64_t *d_sum = nullptr;
     int64_t *d_cpc = nullptr;
@@ -667,11 +669,12 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out) // s: table (PV_T
 
 // Host-side metric of a top-N entry: its key's metric, or for Net v2 keys a metric per
 // direction (TMH_V2_IP4 + dir, TMH_V2_IP6 + dir)
-enum { TMH_V2_IP4 = 32, TMH_V2_IP6 = 36 };
+enum { TMH_V2_IP4 = 32, TMH_V2_IP6 = 36, TMH_V2_DNS = 64 }; // DNS v2: 64 + 4 * metric + dir
 uint32_t host_metric(uint64_t key)
 {
     if (PV_IS_V2_IP4(key)) return TMH_V2_IP4 + (uint32_t)((key >> 34) & 3);
     if (PV_IS_V2_IP6(key)) return TMH_V2_IP6 + (uint32_t)((key >> 53) & 3);
+    if (PV_IS_V2_DKEY(key)) return TMH_V2_DNS + 4 * PV_KEY_METRIC(key) + (uint32_t)((key >> 53) & 3);
     return PV_KEY_METRIC(key);
 }
 
@@ -684,6 +687,8 @@ struct HostBucket {
     std::map<uint32_t, std::map<std::string, uint64_t>> tops; // metric -> name -> count
     std::vector<uint64_t> from_us, to_us;
     std::vector<double> ratio;
+    std::vector<uint64_t> time2[3]; // DNS v2 per direction
+    std::vector<double> ratio2[3];
     bool merged = false;
 };
 
@@ -772,7 +777,13 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int 
             if (v.slot != sg) continue;
             if (v.kind == XV_FROM_US) b.from_us.push_back(v.bits);
             else if (v.kind == XV_TO_US) b.to_us.push_back(v.bits);
-            else { double d; memcpy(&d, &v.bits, 8); b.ratio.push_back(d); }
+            else if (v.kind == XV_RATIO) { double d; memcpy(&d, &v.bits, 8); b.ratio.push_back(d); }
+            else if (v.kind >= XV2_TIME && v.kind < XV2_TIME + 3) b.time2[v.kind - XV2_TIME].push_back(v.bits);
+            else if (v.kind >= XV2_RATIO && v.kind < XV2_RATIO + 3) {
+                double d;
+                memcpy(&d, &v.bits, 8);
+                b.ratio2[v.kind - XV2_RATIO].push_back(d);
+            }
         }
     }
     return 0;
@@ -977,6 +988,73 @@ void net2_json(pv_ctx *c, Json &j, const HostBucket &b)
                 j.key("p50").u(q[0]); j.key("p90").u(q[1]); j.key("p95").u(q[2]); j.key("p99").u(q[3]);
                 j.end_obj();
             }
+        }
+        j.end_obj();
+    }
+}
+
+// DnsMetricsBucket::to_json, DNS v2 (src/handlers/dns/v2/DnsStreamHandler.cpp:678-757): base
+// event counts (the DNS pass's event counters), `filtered_packets`, then per transaction
+// direction the bucket has set up: counters, qname cardinality and the top / quantile groups
+void dns2_json(pv_ctx *c, Json &j, const HostBucket &b)
+{
+    const uint64_t *d = &b.sum[PV_OFF_DNS];
+    const uint32_t g = c->dns2_groups;
+    const size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
+    j.key("period").obj();
+    j.key("start_ts").i(b.start_sec);
+    j.key("length").u(b.period_length);
+    j.end_obj();
+    j.key("observed_packets").u(d[DC_EVENTS]);
+    j.key("deep_sampled_packets").u(d[DC_SAMPLES]);
+    if (g & PV_DNS2_COUNTERS) j.key("filtered_packets").u(d[DC_FILTERED]);
+    static const char *dirs[3] = {"in", "out", "unknown"};
+    for (uint32_t x = 0; x < 3; x++) {
+        const uint64_t *c2 = &b.sum[PV_OFF_DNS2 + x * PV_DNS2_CTRS];
+        if (!c2[D2_SEEN]) continue;
+        auto tops = [&](uint32_t metric) { return tops_of(b, TMH_V2_DNS + 4 * metric + x); };
+        j.key(dirs[x]).obj();
+        if (g & PV_DNS2_COUNTERS) {
+            const std::pair<const char *, uint64_t> ctr[] = {
+                {"xacts", c2[D2_XACTS]}, {"udp_xacts", c2[D2_UDP]}, {"tcp_xacts", c2[D2_TCP]}, {"dot_xacts", 0},
+                {"doh_xacts", 0}, {"dnscrypt_udp_xacts", 0}, {"dnscrypt_tcp_xacts", 0}, {"doq_xacts", 0},
+                {"ipv4_xacts", c2[D2_V4]}, {"ipv6_xacts", c2[D2_V6]}, {"nxdomain_xacts", c2[D2_NX]}, {"ecs_xacts", 0},
+                {"refused_xacts", c2[D2_REFUSED]}, {"srvfail_xacts", c2[D2_SRVFAIL]}, {"noerror_xacts", c2[D2_NOERROR]},
+                {"nodata_xacts", c2[D2_NODATA]}, {"authenticated_data_xacts", c2[D2_AD]},
+                {"authoritative_answer_xacts", c2[D2_AA]}, {"checking_disabled_xacts", c2[D2_CD]},
+                {"timeout_queries", c2[D2_TIMEOUT]}, {"orphan_responses", c2[D2_ORPHAN]}};
+            for (auto &kv : ctr) j.key(kv.first).u(kv.second);
+        }
+        if (g & PV_DNS2_CARDINALITY) {
+            j.key("cardinality").obj();
+            j.key("qname").i(lround(cpc_estimate(&b.cpc[(CPC_QNAME2 + x) * PV_CPC_COUPONS], b.merged)));
+            j.end_obj();
+        }
+        if (g & PV_DNS2_TOP_PORTS)
+            top_json(j, "top_udp_ports_xacts", dense_tops(&b.sum[PV_OFF_PORT2 + x * PV_PORT_BINS], PV_PORT_BINS, 0), topn, pct);
+        if (g & PV_DNS2_TOP_RCODES) {
+            top_json(j, "top_nxdomain_xacts", tops(TM_NX), topn, pct);
+            top_json(j, "top_refused_xacts", tops(TM_REFUSED), topn, pct);
+            top_json(j, "top_srvfail_xacts", tops(TM_SRVFAIL), topn, pct);
+            top_json(j, "top_nodata_xacts", tops(TM_NODATA), topn, pct);
+            top_json(j, "top_noerror_xacts", tops(TM_NOERROR), topn, pct);
+            top_json(j, "top_rcode_xacts", dense_tops(&b.sum[PV_OFF_RCODE2 + x * PV_RCODE_BINS], PV_RCODE_BINS, 2), topn, pct);
+        }
+        if (g & PV_DNS2_TOP_QNAMES) {
+            top_json(j, "top_qname2_xacts", tops(TM_QNAME2), topn, pct);
+            top_json(j, "top_qname3_xacts", tops(TM_QNAME3), topn, pct);
+        }
+        if (g & PV_DNS2_TOP_SIZE) {
+            top_json(j, "top_response_bytes", tops(TM_SIZED), topn, pct);
+            quant_json(j, "response_query_size_ratio", b.ratio2[x]);
+        }
+        if (g & PV_DNS2_TOP_QTYPES)
+            top_json(j, "top_qtype_xacts", dense_tops(&b.sum[PV_OFF_QTYPE2 + x * PV_QTYPE_BINS], PV_QTYPE_BINS, 1), topn, pct);
+        if (g & PV_DNS2_XACT_TIMES) {
+            quant_json(j, "xact_time_us", b.time2[x]);
+            hist_json(j, "xact_histogram_us", b.time2[x]);
+            top_json(j, "top_slow_xacts", tops(TM_SLOW_OUT), topn, pct);
         }
         j.end_obj();
     }
@@ -1228,6 +1306,16 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     if (c->cfg.net2_groups)
         c->net2_groups = PV_N2G_ON | ((c->cfg.net2_groups & PV_GROUPS_SET) ? (c->cfg.net2_groups & PV_NET2_DEFAULT_GROUPS)
                                                                            : PV_NET2_DEFAULT_GROUPS);
+    if (c->cfg.dns2_groups) {
+        c->dns2_groups = PV_N2G_ON | ((c->cfg.dns2_groups & PV_GROUPS_SET) ? (c->cfg.dns2_groups & 0x3ffu)
+                                                                           : PV_DNS2_DEFAULT_GROUPS);
+        if (c->dns2_groups & PV_DNS2_TOP_ECS) {
+            *out = c;
+            return c->fail(PV_EUNSUPPORTED, "DNS v2 top_ecs is not built");
+        }
+        // v1's DNS pass runs for the events (and their counts) only
+        c->dns_groups = PV_DNS_TRANSACTIONS;
+    }
     if (c->cfg.table_log2) c->tcap_log2 = c->cfg.table_log2;
     if (c->tcap_log2 < 8 || c->tcap_log2 > PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2) {
         *out = c;
@@ -1383,6 +1471,7 @@ int pv_reset(pv_ctx *c)
     c->xvals_host.clear();
     c->xvals_synced = 0;
     c->from90 = c->to90 = 0.0f;
+    c->p90_2[0] = c->p90_2[1] = c->p90_2[2] = 0.0f;
     c->remote_topn.clear();
     c->n_pend = 0;
     c->pend_base = -1;
@@ -1530,6 +1619,7 @@ void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t
     P.net_groups = c->net_groups;
     P.dns_groups = c->dns_groups;
     P.net2_groups = c->net2_groups;
+    P.dns2_groups = c->dns2_groups;
     P.net_filter_all = c->cfg.net_filter_all ? 1u : 0u;
     P.nets = c->nets;
     P.f_flags = c->f_flags;
@@ -1856,7 +1946,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.svals = c->d_svals;
     P.n_events = c->d_status + ST_NEV; // [0] packed total, [1] responses (ST_NRESP)
     P.n_dns = c->d_status + ST_NDNS;
-    P.want_events = (c->dns_groups & PV_DNS_TRANSACTIONS) ? 1 : 0;
+    P.want_events = ((c->dns_groups & PV_DNS_TRANSACTIONS) || c->dns2_groups) ? 1 : 0;
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
     if ((uint64_t)((int64_t)(c->records_seen + n) - c->pend_base) >= 0x3fffffffull)
@@ -2039,6 +2129,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             X.slot_gen[k] = P.dslot_of[k] | (c->gen[P.dslot_of[k]] << 8);
             X.thr_from[k] = k == 0 ? c->from90 : -1.0f;
             X.thr_to[k] = k == 0 ? c->to90 : -1.0f;
+            for (uint32_t d = 0; d < 3; d++) X.thr2[k][d] = k == 0 ? c->p90_2[d] : -1.0f;
         }
         X.vals = c->d_xvals;
         X.n_vals = c->d_nvals;
@@ -2061,23 +2152,29 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
         hipLaunchKernelGGL(pv_xact_carry, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_carry");
-        if (P.n_dshift > 0 && (c->dns_groups & PV_DNS_QUANTILES)) {
+        if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
             // on_period_shift: slow thresholds = p90 of the bucket that just closed
             // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
             int rc = sync_xvals(c);
             if (rc) return rc;
             for (uint32_t k = 1; k <= P.n_dshift; k++) {
                 const uint32_t sg = P.dslot_of[k - 1] | (c->gen[P.dslot_of[k - 1]] << 8);
-                std::vector<uint64_t> fr, to;
+                std::vector<uint64_t> fr, to, t2[3];
                 for (auto &v : c->xvals_host) {
                     if (v.slot != sg) continue;
                     if (v.kind == XV_FROM_US) fr.push_back(v.bits);
                     else if (v.kind == XV_TO_US) to.push_back(v.bits);
+                    else if (v.kind >= XV2_TIME && v.kind < XV2_TIME + 3) t2[v.kind - XV2_TIME].push_back(v.bits);
                 }
                 if (!fr.empty()) c->from90 = (float)quantile_at(fr, 0.90);
                 if (!to.empty()) c->to90 = (float)quantile_at(to, 0.90);
                 X.thr_from[k] = c->from90;
                 X.thr_to[k] = c->to90;
+                // DNS v2: per direction (dns/v2/DnsStreamHandler.h:440-453)
+                for (uint32_t d = 0; d < 3; d++) {
+                    if (!t2[d].empty()) c->p90_2[d] = (float)quantile_at(t2[d], 0.90);
+                    X.thr2[k][d] = c->p90_2[d];
+                }
             }
             uint32_t nvalid = 0;
             if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
@@ -2463,7 +2560,8 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
         HostBucket b;
         if ((rc = load_bucket(c, slots, merged != 0, PART_DNS, b))) return rc;
         j.key("dns").obj();
-        dns_json(c, j, b);
+        if (c->dns2_groups) dns2_json(c, j, b);
+        else dns_json(c, j, b);
         j.end_obj();
     }
     j.end_obj();
@@ -2533,15 +2631,27 @@ int pv_window_regions(pv_ctx *c, pv_region *r, uint32_t max, uint32_t *n)
     std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     std::vector<pv_region> v;
+    // the parts of each slot the attached handler versions use (the others stay zero)
+    auto sum = [&](uint32_t s, size_t a, size_t b) { v.push_back(pv_region{c->d_sum + (size_t)s * PV_SUM_WORDS + a, b - a, PV_REDUCE_SUM, 0}); };
+    auto cpc = [&](uint32_t s, size_t k0, size_t k1) {
+        v.push_back(pv_region{c->d_cpc + (size_t)s * PV_MIN_WORDS + k0 * PV_CPC_COUPONS, (k1 - k0) * PV_CPC_COUPONS,
+                              PV_REDUCE_MIN, 0});
+    };
     for (uint32_t s : c->net.slots) {
-        v.push_back(pv_region{c->d_sum + (size_t)s * PV_SUM_WORDS, PV_SUM_NET_WORDS, PV_REDUCE_SUM, 0});
-        v.push_back(pv_region{c->d_cpc + (size_t)s * PV_MIN_WORDS, PV_MIN_NET_WORDS, PV_REDUCE_MIN, 0});
+        sum(s, 0, PV_OFF_NET2);
+        cpc(s, CPC_SRC, CPC_V2);
+        if (c->net2_groups) { sum(s, PV_OFF_NET2, PV_SUM_NET_WORDS); cpc(s, CPC_V2, CPC_QNAME); }
         c->net.clean[s] = false;
     }
     for (uint32_t s : c->dns.slots) {
-        v.push_back(pv_region{c->d_sum + (size_t)s * PV_SUM_WORDS + PV_OFF_DNS, PV_SUM_WORDS - PV_OFF_DNS, PV_REDUCE_SUM, 0});
-        v.push_back(pv_region{c->d_cpc + (size_t)s * PV_MIN_WORDS + PV_MIN_NET_WORDS, PV_MIN_WORDS - PV_MIN_NET_WORDS,
-                              PV_REDUCE_MIN, 0});
+        if (c->dns2_groups) {
+            sum(s, PV_OFF_DNS, PV_OFF_DNS + PV_DNS_CTRS);
+            sum(s, PV_OFF_DNS2, PV_SUM_WORDS);
+            cpc(s, CPC_QNAME2, CPC_QNAME2 + 3);
+        } else {
+            sum(s, PV_OFF_DNS, PV_OFF_DNS2);
+            cpc(s, CPC_QNAME, CPC_QNAME + 1);
+        }
         c->dns.clean[s] = false;
     }
     *n = (uint32_t)v.size();
@@ -2579,7 +2689,7 @@ int pv_comm_init(pv_ctx *c, const uint8_t id[PV_COMM_ID_BYTES], int nranks, int 
 int pv_comm_allreduce_window(pv_ctx *c)
 {
     if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
-    std::vector<pv_region> v(4 * PV_SLOTS);
+    std::vector<pv_region> v(8 * PV_SLOTS);
     uint32_t n = 0;
     if (int rc = pv_window_regions(c, v.data(), (uint32_t)v.size(), &n)) return rc;
     std::lock_guard<std::mutex> g(c->mu);

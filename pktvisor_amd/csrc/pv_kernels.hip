@@ -253,7 +253,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     arena[pos] = (uint8_t)(slen & 0xff);
     arena[pos + 1] = (uint8_t)(slen >> 8);
     if (slen > 0 && nl > 0) {
-        CopyEmit ce{arena + pos + 2, (uint32_t)start, 0, (metric == TM_SLOW_IN || metric == TM_SLOW_OUT) ? 1u : 0u};
+        CopyEmit ce{arena + pos + 2, (uint32_t)start, 0, ((metric == TM_SLOW_IN || metric == TM_SLOW_OUT) && !PV_IS_V2_DKEY(key)) ? 1u : 0u};
         name_emit(R, m, len, 12, ce);
     }
     return (uint32_t)pos + 1;
@@ -751,6 +751,15 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         ev.dir = dm.flags & 3;
         ev.period = (uint8_t)period;
         ev.pad = 0;
+        if (P.dns2_groups) {
+            // DNS v2: one transaction map per direction (DnsMetricsManager::_pair_manager); a
+            // response looks in the swapped direction's map (dns/v2 ...cpp:1100-1145). pad: the
+            // query's CD bit, the message's l3 (bit 1: IPv6)
+            const uint32_t dir = dm.flags & 3;
+            const uint32_t xd = dir == 2 ? 2u : (qr ? dir ^ 1u : dir);
+            ev.key |= (uint64_t)(xd + 1) << 48;
+            ev.pad = (uint8_t)(((w0 >> 28) & 1) | ((dm.flags & 4) ? 2u : 0u));
+        }
         P.events[e] = ev;
         P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
     }
@@ -2418,6 +2427,7 @@ __device__ __forceinline__ uint32_t purge_period(PV_CREF(PvParams) P, uint32_t t
 enum { XC_TOTAL, XC_OUT, XC_IN, XC_TIMEOUT, XC_N };
 struct XState {
     uint32_t ctr[PV_MAX_SHIFTS + 1][XC_N];
+    uint32_t c2[PV_MAX_SHIFTS + 1][3][D2_N]; // DNS v2 counters per period and direction
     PvXValue val[PV_BLOCK * 3];
     PvXValid valid[PV_BLOCK];
     uint32_t nval, nvalid, vbase, dbase;
@@ -2455,6 +2465,118 @@ __device__ void slow_check(PV_CREF(PvXactParams) X, uint32_t idx, uint32_t perio
     const uint32_t metric = dir == 0 ? TM_SLOW_OUT : TM_SLOW_IN;
     const NameSrc ns{X.trecs, X.toffs};
     global_add(P, P.dslot_of[period], PV_KEY(metric, fp56(rn.ph, rn.n, 1)), 1, idx, tcp ? &ns : nullptr);
+}
+// DnsMetricsBucket::new_dns_transaction, DNS v2 (dns/v2/DnsStreamHandler.cpp:925-1089): a
+// valid, kept transaction accounted on its response (record e.idx of this batch) in the
+// response's transaction direction xd; qe is its query. Name tops and dense tables go
+// straight to the period's tables (v2 keys carry the direction).
+__device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e, const PvXEvent &qe, uint32_t xd,
+                          uint64_t us, int64_t order)
+{
+    PV_CREF(PvParams) P = X.P;
+    const uint32_t g = P.dns2_groups;
+    const uint32_t period = e.period, slot = P.dslot_of[period];
+    const bool tcp = e.idx & PV_TCP_IDX;
+    const uint32_t idx = e.idx & ~PV_TCP_IDX;
+    Parsed o;
+    const GAcc R{tcp ? X.trecs : P.recs};
+    if (tcp) {
+        ParseCfg C = parse_cfg(P);
+        C.linktype = 101;
+        parse_record(R, C, P, X.toffs[idx], o);
+    } else {
+        parse_record(R, P, P.offs[idx], o);
+    }
+    const uint64_t m = o.l4off + 8;
+    const uint32_t len = e.len;
+    const uint32_t b23 = R.u32(m) >> 16; // header bytes 2, 3
+    const uint32_t rcode = (b23 >> 8) & 15;
+    const uint32_t qd = be16(R, m + 4), an = be16(R, m + 6), ns = be16(R, m + 8), ar = be16(R, m + 10);
+    uint32_t *c = T.c2[period][xd];
+    if (g & PV_D2G_COUNTERS) {
+        atomicAdd(&c[D2_XACTS], 1u);
+        atomicAdd(&c[(e.pad & 2) ? D2_V6 : D2_V4], 1u);
+        atomicAdd(&c[tcp ? D2_TCP : D2_UDP], 1u);
+        if (qe.pad & 1) atomicAdd(&c[D2_CD], 1u);
+        if (rcode == 0) { atomicAdd(&c[D2_NOERROR], 1u); if (!an) atomicAdd(&c[D2_NODATA], 1u); }
+        else if (rcode == 2) atomicAdd(&c[D2_SRVFAIL], 1u);
+        else if (rcode == 3) atomicAdd(&c[D2_NX], 1u);
+        else if (rcode == 5) atomicAdd(&c[D2_REFUSED], 1u);
+        if (b23 & 0x04) atomicAdd(&c[D2_AA], 1u);
+        if (b23 & 0x2000) atomicAdd(&c[D2_AD], 1u);
+    }
+    if (qe.len && (g & PV_D2G_TOP_SIZE))
+        xval(X, T, period, XV2_RATIO + xd, (uint64_t)__double_as_longlong((double)len / (double)qe.len));
+    const uint32_t port = dns_port(R.u32(o.l4off));
+    if (port && (g & PV_D2G_TOP_PORTS)) sum_add(P, slot, PV_OFF_PORT2 + xd * PV_PORT_BINS + port, 1);
+    if (g & PV_D2G_XACT_TIMES) xval(X, T, period, XV2_TIME + xd, us);
+    DnsInfo d;
+    dns_parse(R, m, len, qd, an, ns, ar, d);
+    if (!d.ok) return;
+    sum_add(P, slot, PV_OFF_RCODE2 + xd * PV_RCODE_BINS + rcode, 1);
+    if (!d.has_query) return;
+    NameStats st;
+    st.init();
+    if (d.name_len_enc > 0) name_stats(R, m, len, 12, st);
+    uint64_t h1, h2;
+    st.mm.finish(h1, h2);
+    if (st.n > 0 && (g & PV_D2G_CARDINALITY)) cpc_min(P, slot, CPC_QNAME2 + xd, cpc_coupon(h1, h2), order);
+    sum_add(P, slot, PV_OFF_QTYPE2 + xd * PV_QTYPE_BINS + (d.qtype & 0xffff), 1);
+    const NameSrc ns_{X.trecs, X.toffs};
+    const NameSrc *nsp = tcp ? &ns_ : nullptr;
+    const uint64_t fp = fp56(st.ph, st.n, 0);
+    auto add = [&](uint32_t metric, uint64_t f, uint32_t w) { global_add(P, slot, PV_V2_DKEY(metric, xd, f), w, idx, nsp); };
+    if (g & PV_D2G_TOP_RCODES) {
+        if (rcode == 2) add(TM_SRVFAIL, fp, 1);
+        else if (rcode == 3) add(TM_NX, fp, 1);
+        else if (rcode == 5) add(TM_REFUSED, fp, 1);
+        else if (rcode == 0) { add(TM_NOERROR, fp, 1); if (!an) add(TM_NODATA, fp, 1); }
+    }
+    if (g & PV_D2G_TOP_SIZE) add(TM_SIZED, fp, len);
+    if (g & PV_D2G_XACT_TIMES) {
+        const float thr = X.thr2[period][xd];
+        if (thr < 0.0f) T.valid[atomicAdd(&T.nvalid, 1u)] = PvXValid{e.idx, (uint8_t)period, (uint8_t)(4 + xd), 0, 0, us};
+        else if (thr > 0.0f && (float)us >= thr) add(TM_SLOW_OUT, fp, 1);
+    }
+    if (g & PV_D2G_TOP_QNAMES) {
+        int q2, q3;
+        uint64_t h2p, h3p;
+        agg_domain(st, q2, q3, h2p, h3p, 0);
+        const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
+        add(TM_QNAME2, fp56(k2, st.n - q2, 0), 1);
+        if (q3 >= 0 && (uint32_t)q3 < st.n) {
+            const uint64_t k3 = q3 == 0 ? st.ph : suffix_hash(st, q3, h3p);
+            add(TM_QNAME3, fp56(k3, st.n - q3, 0), 1);
+        }
+    }
+}
+// the deferred slow check of a DNS v2 transaction (its period's p90 was not known at resolve)
+__device__ void dns2_slow(PV_CREF(PvXactParams) X, uint32_t eidx, uint32_t period, uint32_t xd, uint64_t us)
+{
+    const float thr = X.thr2[period][xd];
+    if (!(thr > 0.0f && (float)us >= thr)) return;
+    PV_CREF(PvParams) P = X.P;
+    const bool tcp = eidx & PV_TCP_IDX;
+    const uint32_t idx = eidx & ~PV_TCP_IDX;
+    Parsed o;
+    const GAcc R{tcp ? X.trecs : P.recs};
+    if (tcp) {
+        ParseCfg C = parse_cfg(P);
+        C.linktype = 101;
+        parse_record(R, C, P, X.toffs[idx], o);
+    } else {
+        parse_record(R, P, P.offs[idx], o);
+    }
+    const uint64_t m = o.l4off + 8;
+    const uint32_t len = o.l4len - 8;
+    DnsInfo d;
+    dns_parse(R, m, len, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8), be16(R, m + 10), d);
+    if (!(d.ok && d.has_query)) return;
+    NameStats st;
+    st.init();
+    if (d.name_len_enc > 0) name_stats(R, m, len, 12, st);
+    const NameSrc ns_{X.trecs, X.toffs};
+    global_add(P, P.dslot_of[period], PV_V2_DKEY(TM_SLOW_OUT, xd, fp56(st.ph, st.n, 0)), 1, idx, tcp ? &ns_ : nullptr);
 }
 } // namespace
 
@@ -2529,17 +2651,76 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
     }
 }
 
+// TransactionManager per direction, DNS v2 (dns/v2/DnsStreamHandler.cpp:1100-1145 and the
+// manager's on_period_shift, .h:440-453): a response of transaction direction xd is
+// Valid, TimedOut or NotExist (orphan) against the latest event of its key (the key holds
+// xd); every outcome sets the direction up in the response's bucket. An open query
+// purged at a later shift is a time-out of that period. Queries account nothing.
+__device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
+{
+    PV_CREF(PvParams) P = X.P;
+    const PvXEvent e = xev(X, p);
+    const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
+    const uint32_t xd = (uint32_t)((e.key >> 48) & 3) - 1;
+    if (e.qr) {
+        const bool kept = e.period >= P.dskip_before;
+        uint32_t *c = T.c2[e.period][xd];
+        if (kept) atomicAdd(&c[D2_SEEN], 1u);
+        int q = (int)p - 1;
+        for (; q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h; q--)
+            if (xev(X, q).key == e.key) break;
+        const bool found = q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h && !xev(X, q).qr;
+        const PvXEvent qe = found ? xev(X, q) : e;
+        const uint32_t kp = found ? purge_period(P, X.ttl_s, qe.period, qe.sec) : 0u;
+        if (!found || (kp && kp <= e.period)) { if (kept) atomicAdd(&c[D2_ORPHAN], 1u); return; }
+        int64_t dsec = e.sec > qe.sec ? e.sec - qe.sec : qe.sec - e.sec;
+        int64_t dnsec = (int64_t)e.nsec - (int64_t)qe.nsec;
+        if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
+        const bool timed_out = dsec > (int64_t)X.ttl_s || (dsec == (int64_t)X.ttl_s && ((double)dnsec / 1.0e6) >= (double)X.ttl_ms);
+        if (timed_out) { if (kept) atomicAdd(&c[D2_TIMEOUT], 1u); return; }
+        const uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
+        if (!kept) {
+            // a period outside the window still feeds the next period's p90
+            if (P.dns2_groups & PV_D2G_XACT_TIMES) xval(X, T, e.period, XV2_TIME + xd, us);
+            return;
+        }
+        // the response's first-occurrence order (the DNS pass's CPC order: batch base * 4 + rank)
+        const int64_t order = (int64_t)((P.gbase << 2) + ((uint32_t)X.skeys[p] - (P.ekey_base << 2)));
+        dns2_xact(X, T, e, qe, xd, us, order);
+    } else {
+        const uint32_t kp = purge_period(P, X.ttl_s, e.period, e.sec);
+        if (!kp) return;
+        uint32_t q = p + 1;
+        for (; q < X.n && (uint32_t)(X.skeys[q] >> 32) == h; q++)
+            if (xev(X, q).key == e.key) break;
+        if (q < X.n && (uint32_t)(X.skeys[q] >> 32) == h && xev(X, q).period < kp) return;
+        if (kp < P.dskip_before) return;
+        atomicAdd(&T.c2[kp][xd][D2_TIMEOUT], 1u);
+        atomicAdd(&T.c2[kp][xd][D2_SEEN], 1u);
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvXactParams *__restrict__ Xp)
 {
     PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
     PV_CREF(PvParams) P = X.P;
     __shared__ XState T;
     for (uint32_t j = threadIdx.x; j < (PV_MAX_SHIFTS + 1) * XC_N; j += blockDim.x) (&T.ctr[0][0])[j] = 0;
+    for (uint32_t j = threadIdx.x; j < (PV_MAX_SHIFTS + 1) * 3 * D2_N; j += blockDim.x) (&T.c2[0][0][0])[j] = 0;
     if (threadIdx.x == 0) { T.nval = 0; T.nvalid = 0; }
     __syncthreads();
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < X.n) resolve_one(X, T, p);
+    if (p < X.n) {
+        if (P.dns2_groups) resolve_one2(X, T, p);
+        else resolve_one(X, T, p);
+    }
     __syncthreads();
+    if (P.dns2_groups)
+        for (uint32_t j = threadIdx.x; j < (P.n_dshift + 1) * 3 * D2_N; j += blockDim.x) {
+            const uint32_t per = j / (3 * D2_N), w = j % (3 * D2_N);
+            const uint32_t v = (&T.c2[0][0][0])[j];
+            if (v) sum_add(P, P.dslot_of[per], PV_OFF_DNS2 + (w / D2_N) * PV_DNS2_CTRS + w % D2_N, v);
+        }
     static const uint8_t dc[XC_N] = {DC_XTOTAL, DC_XOUT, DC_XIN, DC_XTIMEOUT};
     if (threadIdx.x < (PV_MAX_SHIFTS + 1) * XC_N) {
         const uint32_t per = threadIdx.x / XC_N, c = threadIdx.x % XC_N;
@@ -2606,7 +2787,8 @@ extern "C" __global__ void pv_xact_slow(const PvXactParams *__restrict__ Xp, uin
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_valid) return;
     const PvXValid v = X.valid[i];
-    slow_check(X, v.idx, v.period, v.dir, v.us);
+    if (v.dir >= 4) dns2_slow(X, v.idx, v.period, v.dir - 4, v.us);
+    else slow_check(X, v.idx, v.period, v.dir, v.us);
 }
 
 // Stable LSD radix sort of (key, value) pairs over all 64 key bits (rocPRIM onesweep).

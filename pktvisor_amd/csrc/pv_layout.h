@@ -37,6 +37,16 @@
 #define PV_N2G_TOP_GEO 8u
 #define PV_N2G_TOP_IPS 16u
 #define PV_N2G_ON 0x40000000u
+#define PV_D2G_CARDINALITY (1u << 0)
+#define PV_D2G_COUNTERS (1u << 1)
+#define PV_D2G_QUANTILES (1u << 2)
+#define PV_D2G_TOP_ECS (1u << 3)
+#define PV_D2G_TOP_QTYPES (1u << 4)
+#define PV_D2G_TOP_RCODES (1u << 5)
+#define PV_D2G_TOP_SIZE (1u << 6)
+#define PV_D2G_TOP_QNAMES (1u << 7)
+#define PV_D2G_TOP_PORTS (1u << 8)
+#define PV_D2G_XACT_TIMES (1u << 9)
 #define PV_NET_COUNTERS_BIT 1u
 #define PV_NET_CARDINALITY_BIT 2u
 #define PV_NET_TOP_IPS_BIT 8u
@@ -68,12 +78,25 @@
 #define PV_OFF_PORT (PV_OFF_DNS + PV_DNS_CTRS)
 #define PV_OFF_QTYPE (PV_OFF_PORT + PV_PORT_BINS)
 #define PV_OFF_RCODE (PV_OFF_QTYPE + PV_QTYPE_BINS)
-#define PV_SUM_WORDS (PV_OFF_RCODE + PV_RCODE_BINS)      // dns part [PV_OFF_DNS, PV_SUM_WORDS)
+// DNS v2 (src/handlers/dns/v2), in place of v1 when configured: per transaction direction
+// (0 in, 1 out, 2 unknown) its counters, then its port / qtype / rcode tables
+#define PV_DNS2_CTRS 16
+#define PV_OFF_DNS2 (PV_OFF_RCODE + PV_RCODE_BINS)              // + dir * PV_DNS2_CTRS
+#define PV_OFF_PORT2 (PV_OFF_DNS2 + 4 * PV_DNS2_CTRS)           // + dir * PV_PORT_BINS
+#define PV_OFF_QTYPE2 (PV_OFF_PORT2 + 3 * PV_PORT_BINS)         // + dir * PV_QTYPE_BINS
+#define PV_OFF_RCODE2 (PV_OFF_QTYPE2 + 3 * PV_QTYPE_BINS)       // + dir * PV_RCODE_BINS
+#define PV_SUM_WORDS (PV_OFF_RCODE2 + 4 * PV_RCODE_BINS)        // dns part [PV_OFF_DNS, PV_SUM_WORDS)
 
 // net counters (src/handlers/net/v1/NetStreamHandler.h:69-96 + base event counters)
 enum {
     NC_EVENTS = 0, NC_SAMPLES, NC_UDP, NC_TCP, NC_OTHER, NC_V4, NC_V6, NC_SYN, NC_IN, NC_OUT, NC_UNK, NC_TOTAL,
     NC_FILTERED, NC_COUNT
+};
+// DNS v2 counters per direction (src/handlers/dns/v2/DnsStreamHandler.h:75-120); D2_SEEN counts
+// the responses and purge time-outs that set the direction up (DnsMetricsBucket::dir_setup)
+enum {
+    D2_SEEN = 0, D2_XACTS, D2_UDP, D2_TCP, D2_V4, D2_V6, D2_NX, D2_REFUSED, D2_SRVFAIL, D2_NOERROR, D2_NODATA, D2_AA,
+    D2_AD, D2_CD, D2_TIMEOUT, D2_ORPHAN, D2_N
 };
 // Net v2 counters (src/handlers/net/v2/NetStreamHandler.h:61-96): base events, then per
 // direction d (0 in, 1 out, 2 unknown) at N2_DIR + 8 d
@@ -88,7 +111,7 @@ enum {
 // ---- MIN region (int64 global record index), per slot: CPC lg_k = 11 => 2048 rows x 64 cols
 #define PV_CPC_COUPONS (2048 * 64)
 // v1 src_ips_in / dst_ips_out, v2 ips per direction (in, out, unknown), then the DNS qname
-enum { CPC_SRC = 0, CPC_DST = 1, CPC_V2 = 2, CPC_QNAME = 5, CPC_SKETCHES = 6 };
+enum { CPC_SRC = 0, CPC_DST = 1, CPC_V2 = 2, CPC_QNAME = 5, CPC_QNAME2 = 6, CPC_SKETCHES = 9 }; // CPC_QNAME2 + dir: DNS v2
 #define PV_MIN_WORDS (CPC_SKETCHES * PV_CPC_COUPONS)
 #define PV_MIN_NET_WORDS (CPC_QNAME * PV_CPC_COUPONS) // net part [0, 5 * coupons), dns part after
 #define PV_CPC_EMPTY 0x7fffffffffffffffLL
@@ -111,6 +134,9 @@ enum {
 #define PV_V2_IP6(dir, h) PV_KEY(TM_IPV6, (1ull << 55) | ((uint64_t)(dir) << 53) | ((h) & ((1ull << 53) - 1)))
 #define PV_IS_V2_IP4(k) ((((k) >> 56) == TM_IPV4) && (((k) >> 40) & 1))
 #define PV_IS_V2_IP6(k) ((((k) >> 56) == TM_IPV6) && (((k) >> 55) & 1))
+// DNS v2 name keys: 1 << 55 | dir << 53 | 53-bit name fingerprint (v1 and v2 DNS never share a table)
+#define PV_V2_DKEY(metric, dir, fp) PV_KEY(metric, (1ull << 55) | ((uint64_t)(dir) << 53) | ((fp) & ((1ull << 53) - 1)))
+#define PV_IS_V2_DKEY(k) ((((k) >> 56) >= TM_QNAME2) && (((k) >> 55) & 1))
 #define PV_KEY_METRIC(k) ((uint32_t)((k) >> 56))
 // table of a (handler slot, metric): Net metrics (IPv4 / IPv6) in table slot, the DNS
 // metrics in table PV_SLOTS + slot
@@ -157,7 +183,7 @@ struct PvXEvent {
 };
 
 // one transaction-derived value (quantile input), grouped per slot/kind on the host
-enum { XV_FROM_US = 0, XV_TO_US = 1, XV_RATIO = 2 };
+enum { XV_FROM_US = 0, XV_TO_US = 1, XV_RATIO = 2, XV2_TIME = 3, XV2_RATIO = 6 }; // XV2_* + dir: DNS v2
 struct PvXValue {
     uint64_t bits; // uint64 microseconds, or the IEEE-754 bits of the double ratio
     uint32_t slot; // slot | generation << 8
@@ -323,6 +349,7 @@ struct PvParams {
     PV_G uint32_t *cb_h;    // per combine workgroup: its entries per region
     PV_G uint32_t *tab_live; // per table: entries held (bounded by pv_topn_purge)
     uint32_t net2_groups;   // Net v2 handler attached: PV_N2G_* group bits | PV_N2G_ON (0 = not attached)
+    uint32_t dns2_groups;   // DNS v2 in place of v1: PV_D2G_* group bits | PV_N2G_ON (0 = DNS v1)
     PV_G uint64_t *tp_buf;
     PV_G uint32_t *nn_cnt;
     PV_G PvNewName *nn;
@@ -403,6 +430,8 @@ struct PvXactParams {
     // TCP message records (events whose idx carries PV_TCP_IDX)
     const PV_G uint8_t *trecs;
     const PV_G uint32_t *toffs;
+    // DNS v2: per period and direction the p90 slow threshold (< 0 = not known yet)
+    float thr2[PV_MAX_SHIFTS + 1][3];
 };
 #define PV_PEND_FLAG 0x80000000u
 

@@ -1,0 +1,96 @@
+"""DNS v2 ("dns", src/handlers/dns/v2) on the device against the oracle's restatement
+(oracle/pv_oracle.cpp dns2_event / dns2_json), bit-exact: per-direction transaction maps in
+the sorted event keys, accounting on the response in pv_xact_resolve (dns2_xact).
+
+The reference's own v2 KATs (test_dns_layer.cpp v2 :57-302) run through the GPU path in
+test_gpu_kat.py; these cases cover every fixture (UDP and TCP), synthetic query/response
+mixes with all rcodes, every group but top_ecs (not built), period shifts with time-outs,
+per-direction p90 slow tops, and transactions carried across many small batches."""
+import os
+
+import numpy as np
+import pytest
+
+import pktvisor_amd as pa
+from pktvisor_amd import synth
+from tests.test_gpu_parity import FIXTURES, GOLD, diff
+
+pytestmark = pytest.mark.gpu
+ALL = 0x3ff & ~(1 << 3)  # every v2 group but top_ecs
+ALL_NAMES = ["cardinality", "counters", "quantiles", "top_qtypes", "top_rcodes", "top_size", "top_qnames", "top_ports",
+             "xact_times"]
+DEFAULT = 1 | 2 | 4 | 16 | 32 | 128
+
+
+def run_both(oracle, pcap, host, periods, tmp_path, groups=ALL, dns2_config=None):
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    if dns2_config is None:
+        dns2_config = {"enable": ALL_NAMES} if groups == ALL else {}
+    gpu = pa.pktvisor_reader(str(p), host_spec=host or None, periods=periods, dns2_config=dns2_config)
+    ref = oracle.run_bytes(pcap, host_spec=host, num_periods=periods, window=periods, dns2_groups=groups)
+    return gpu, ref
+
+
+@pytest.mark.parametrize("periods", [1, 5])
+@pytest.mark.parametrize("fixture,host", FIXTURES, ids=[f[0] for f in FIXTURES])
+def test_dns2_fixture_parity(oracle, tmp_path, fixture, host, periods):
+    pcap = open(os.path.join(GOLD, fixture), "rb").read()
+    gpu, ref = run_both(oracle, pcap, host, periods, tmp_path)
+    assert all("observed_packets" in w["dns"] for w in gpu.values())
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_dns2_default_groups(oracle, tmp_path):
+    pcap = open(os.path.join(GOLD, "dns_udp_mixed_rcode.pcap"), "rb").read()
+    gpu, ref = run_both(oracle, pcap, "192.168.0.0/24", 1, tmp_path, DEFAULT, {})
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("cfg,n", [(1, 1000), (4, 60000)])
+@pytest.mark.parametrize("periods", [1, 5])
+def test_dns2_synthetic_parity(oracle, tmp_path, cfg, n, periods):
+    gpu, ref = run_both(oracle, synth.pcap_bytes(cfg, n), synth.HOST_SPEC, periods, tmp_path)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("periods", [2, 5])
+def test_dns2_period_shifts(oracle, tmp_path, periods):
+    """shifts inside the batch: purge time-outs per direction, p90 slow thresholds per direction"""
+    pcap = synth.pcap_bytes(4, 200000, ts_step_us=900)
+    gpu, ref = run_both(oracle, pcap, synth.HOST_SPEC, periods, tmp_path)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_dns2_sparse_boundaries(oracle, tmp_path):
+    """DNS shifts seconds after the Net shifts (no DNS traffic around the 60 s marks)"""
+    gpu, ref = run_both(oracle, synth.sparse_dns_pcap(), synth.HOST_SPEC, 5, tmp_path)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_dns2_small_batches(oracle):
+    """open queries carried across many small batches (per-direction keys in the carried list)"""
+    pcap = synth.pcap_bytes(1, 1000)
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    offs = list(idx.offsets) + [len(recs)]
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=1, max_records=512, dns2_config={"enable": ALL_NAMES})
+    try:
+        rng = np.random.default_rng(4)
+        i = 0
+        while i < idx.n:
+            j = min(idx.n, i + int(rng.integers(1, 60)))
+            h.process_host(recs[offs[i]:offs[j]])
+            i = j
+        h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+        gpu = h.window_json(0)
+    finally:
+        h.close()
+    ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=1, window=1, dns2_groups=ALL)
+    assert diff(gpu["dns"], ref["1m"]["dns"]) is None, diff(gpu["dns"], ref["1m"]["dns"])
+
+
+def test_dns2_tcp_parity(oracle, tmp_path):
+    """DNS over TCP messages as v2 transactions (reassembly as in test_gpu_tcp.py)"""
+    gpu, ref = run_both(oracle, synth.tcp_dns_pcap(2), "10.0.0.0/8,2001:db8::/32", 1, tmp_path)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
