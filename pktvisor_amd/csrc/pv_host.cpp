@@ -670,11 +670,12 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out) // s: table (PV_T
 // Host-side metric of a top-N entry: its key's metric, or for Net v2 keys a metric per
 // direction (TMH_V2_IP4 + dir, TMH_V2_IP6 + dir)
 enum { TMH_V2_IP4 = 32, TMH_V2_IP6 = 36, TMH_V2_DNS = 64 }; // DNS v2: 64 + 4 * metric + dir
-uint32_t host_metric(uint64_t key)
+uint32_t host_metric(const pv_ctx *c, uint64_t key)
 {
     if (PV_IS_V2_IP4(key)) return TMH_V2_IP4 + (uint32_t)((key >> 34) & 3);
     if (PV_IS_V2_IP6(key)) return TMH_V2_IP6 + (uint32_t)((key >> 53) & 3);
-    if (PV_IS_V2_DKEY(key)) return TMH_V2_DNS + 4 * PV_KEY_METRIC(key) + (uint32_t)((key >> 53) & 3);
+    // (v1 name keys carry a full 56-bit fingerprint: only a DNS v2 context holds v2 name keys)
+    if (c->dns2_groups && PV_IS_V2_DKEY(key)) return TMH_V2_DNS + 4 * PV_KEY_METRIC(key) + (uint32_t)((key >> 53) & 3);
     return PV_KEY_METRIC(key);
 }
 
@@ -770,7 +771,7 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int 
         std::vector<TopRec> recs;
         int rc = read_topn(c, s + (part == PART_DNS ? PV_SLOTS : 0), recs);
         if (rc) return rc;
-        for (auto &r : recs) b.tops[host_metric(r.key)][r.name] += r.count;
+        for (auto &r : recs) b.tops[host_metric(c, r.key)][r.name] += r.count;
         if (part != PART_DNS) continue;
         const uint32_t sg = s | (c->gen[s] << 8);
         for (auto &v : c->xvals_host) {

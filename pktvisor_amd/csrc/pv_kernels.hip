@@ -253,7 +253,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     arena[pos] = (uint8_t)(slen & 0xff);
     arena[pos + 1] = (uint8_t)(slen >> 8);
     if (slen > 0 && nl > 0) {
-        CopyEmit ce{arena + pos + 2, (uint32_t)start, 0, ((metric == TM_SLOW_IN || metric == TM_SLOW_OUT) && !PV_IS_V2_DKEY(key)) ? 1u : 0u};
+        CopyEmit ce{arena + pos + 2, (uint32_t)start, 0, ((metric == TM_SLOW_IN || metric == TM_SLOW_OUT) && !(P.dns2_groups && PV_IS_V2_DKEY(key))) ? 1u : 0u};
         name_emit(R, m, len, 12, ce);
     }
     return (uint32_t)pos + 1;

@@ -80,7 +80,10 @@ __device__ void emit_msg(PV_CREF(PvTcpParams) T, Flow &F, int s)
     uint8_t *r = T.marena + off;
     // classic-pcap record: ts, incl_len, orig_len; raw IPv4 (total length 0), UDP
     const uint32_t incl = 28u + size;
-    const uint32_t hw[11] = {F.f.end_sec, F.f.end_usec, incl, incl, 0x00000045u, 0u, 0x00001140u, 0u, 0u, 0u,
+    // UDP ports: the connection's metric port as the source, 53 as the destination, so the
+    // record's ports give the metric port as a datagram's would (dns_port)
+    const uint32_t pw = ((uint32_t)F.f.port >> 8) | (((uint32_t)F.f.port & 0xffu) << 8) | (53u << 24);
+    const uint32_t hw[11] = {F.f.end_sec, F.f.end_usec, incl, incl, 0x00000045u, 0u, 0x00001140u, 0u, 0u, pw,
                              (((8u + size) >> 8) & 0xffu) | ((8u + size) & 0xffu) << 8};
     for (int k = 0; k < 11; k++)
         for (int b = 0; b < 4; b++) r[k * 4 + b] = (uint8_t)(hw[k] >> (8 * b));
