@@ -271,7 +271,9 @@ def end_to_end(h, blob, n: int, steps: int) -> dict:
     lib = pa.load_library()
     buf = np.frombuffer(blob, dtype=np.uint8).copy()
     out = {"unit": "Mpkt/s", "steps": steps, "chunk_mb": int(os.environ.get("PV_INGEST_CHUNK_MB", "64")),
-           "path": "record blob in host RAM -> parallel index + (pageable only) copy to pinned -> H2D -> kernels"}
+           "path": ("record blob in host RAM -> (pageable only) parallel copy to pinned staging -> H2D of fixed "
+                    "chunks on two copy streams into a 3-slot device ring -> record index on the device "
+                    "(pv_index.hip) -> kernels")}
     for mode in ("pageable", "registered"):
         if mode == "registered" and lib.pv_host_register(buf.ctypes.data, buf.nbytes) != 0:
             out[mode] = None
@@ -289,7 +291,7 @@ def end_to_end(h, blob, n: int, steps: int) -> dict:
             dt = (time.perf_counter() - t0) / steps
             t = [round(x / steps, 3) for x in h.ingest_timing(reset=True)]
             out[mode] = {"value": round(n / dt / 1e6, 2), "ms_per_step": round(dt * 1e3, 3),
-                         "copy_index_ms": t[0], "index_ms": t[1], "h2d_enqueue_ms": t[2], "device_ms": t[3]}
+                         "staging_copy_ms": t[0], "wait_index_ms": t[1], "device_ms": t[3]}
         finally:
             if mode == "registered":
                 lib.pv_host_unregister(buf.ctypes.data)

@@ -161,6 +161,15 @@ const char *pv_last_error(const pv_ctx *ctx);
 int pv_index_records(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uint32_t *offsets, uint64_t max_records,
                      uint32_t *sec_change_idx, uint32_t *sec_change_sec, uint32_t max_changes, pv_index_info *info);
 
+/* The same index computed on the device (pv_index.hip: segment guesses validated along the
+ * true chain, then offsets and ts_sec change points), for a block of at most one ingest
+ * chunk (64 MiB, PV_INGEST_CHUNK_MB); the outputs equal pv_index_records'. A block whose
+ * guesses do not settle within 64 validation passes (payloads forged to look like record
+ * chains across more than 64 segments) is walked on the host instead. */
+int pv_index_records_device(pv_ctx *ctx, const uint8_t *recs, size_t bytes, uint32_t *offsets, uint64_t max_records,
+                            uint32_t *sec_change_idx, uint32_t *sec_change_sec, uint32_t max_changes,
+                            pv_index_info *info);
+
 /* Bytes of device memory past the end of the last record that the kernels may read (the
  * LDS windows of pv_topn_names and the DNS pass load whole 16-B aligned windows of up to
  * 192 bytes from a record's start). Every d_recs buffer must be readable this far. */
@@ -182,17 +191,23 @@ int pv_index_records_mt(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uin
                         uint32_t *sec_change_idx, uint32_t *sec_change_sec, uint32_t max_changes, pv_index_info *info,
                         uint32_t nthreads);
 
-/* Process records in host memory, pipelined over 64 MiB chunks (PV_INGEST_CHUNK_MB):
- * parallel copy into pinned staging (skipped when recs is pinned, e.g. registered
- * with pv_host_register), parallel record index, H2D on a copy stream overlapping
- * the previous chunk's kernels. Returns when every record has been processed. */
+/* Process records in host memory, pipelined over 64 MiB chunks (PV_INGEST_CHUNK_MB). The
+ * blob is copied to the device in fixed chunks (through pinned staging unless recs is
+ * pinned, e.g. registered with pv_host_register) on two copy streams into a ring of three
+ * device buffers, ahead of the kernels; each chunk, joined to the previous batch's tail on
+ * the device, is indexed there (pv_index_records_device's kernels) and processed as batches
+ * that end at a ts_sec boundary. PV_INGEST_INDEX=host selects the host-walk pipeline
+ * (parallel host index, H2D of records + offsets). Returns when every record has been
+ * processed. */
 int pv_process_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes);
 /* Page-lock a host range so pv_process_host DMAs from it directly (hipHostRegister). */
 int pv_host_register(void *ptr, size_t bytes);
 int pv_host_unregister(void *ptr);
-/* Accumulated ms of the host-memory path: [0] copy into pinned staging + record index
- * (pageable source), [1] record index (pinned source),
- * [2] H2D enqueue, [3] device processing as seen by the calling thread. */
+/* Accumulated ms of the host-memory path. Device index (default): [0] copy into pinned
+ * staging (pageable source, producer thread), [1] waiting for a chunk's copy + its record
+ * index on the device, [3] device processing, as seen by the calling thread. Host index
+ * (PV_INGEST_INDEX=host): [0] copy + index (pageable), [1] index (pinned), [2] H2D enqueue,
+ * [3] device processing. */
 int pv_ingest_timing(pv_ctx *ctx, double *ms4, int reset);
 /* Multi-GPU shard edges (one context per rank, contiguous shards in rank order).
  * pv_edge_export: this shard's DNS transaction stubs (queries open at its end, responses

@@ -152,6 +152,7 @@ class pv_index_info(ctypes.Structure):
 
 # every symbol include/pvgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_error", "pv_index_records",
+           "pv_index_records_device",
            "pv_process_device", "pv_process_host", "pv_set_start_tstamp", "pv_set_end_tstamp", "pv_synchronize",
            "pv_reset", "pv_window_json", "pv_free", "pv_state_regions", "pv_set_global_base", "pv_export_topn",
            "pv_merge_topn", "pv_kernel_timing", "pv_window_regions", "pv_index_records_mt", "pv_host_register",
@@ -188,6 +189,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_last_error.argtypes = [P]
     lib.pv_last_error.restype = ctypes.c_char_p
     lib.pv_index_records.argtypes = [P, ctypes.c_size_t, U32, P, U64, P, P, U32, ctypes.POINTER(pv_index_info)]
+    lib.pv_index_records_device.argtypes = [P, P, ctypes.c_size_t, P, U64, P, P, U32, ctypes.POINTER(pv_index_info)]
     lib.pv_process_device.argtypes = [P, P, P, ctypes.POINTER(pv_index_info), P, P, P]
     lib.pv_index_records_mt.argtypes = [P, ctypes.c_size_t, U32, P, U64, P, P, U32, ctypes.POINTER(pv_index_info),
                                         U32]
@@ -376,6 +378,21 @@ class PvHandlers:
     def process_host(self, recs):
         buf = recs if isinstance(recs, np.ndarray) else np.frombuffer(recs, dtype=np.uint8)
         self._check(self.lib.pv_process_host(self.ctx, buf.ctypes.data, buf.nbytes), "pv_process_host")
+
+    def index_device(self, recs, max_records: Optional[int] = None, max_changes: int = 1 << 16):
+        """pv_index_records_device: the record index of one block computed on the device;
+        returns (offsets, sc_idx, sc_sec, pv_index_info) as RecordIndex holds them."""
+        buf = np.frombuffer(recs, dtype=np.uint8) if not isinstance(recs, np.ndarray) else recs
+        if max_records is None:
+            max_records = max(1, len(buf) // 16)
+        offs = np.empty(max_records, dtype=np.uint32)
+        sci = np.empty(max_changes, dtype=np.uint32)
+        scs = np.empty(max_changes, dtype=np.uint32)
+        info = pv_index_info()
+        self._check(self.lib.pv_index_records_device(self.ctx, buf.ctypes.data, len(buf), offs.ctypes.data, max_records,
+                                                     sci.ctypes.data, scs.ctypes.data, max_changes, ctypes.byref(info)),
+                    "pv_index_records_device")
+        return offs[: info.n_records], sci, scs, info
 
     def ingest_timing(self, reset: bool = False):
         """ms spent by pv_process_host: copy + index (pageable), index (pinned), H2D enqueue, device."""

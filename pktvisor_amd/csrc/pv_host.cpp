@@ -83,6 +83,11 @@ extern "C" __global__ void pv_topn_scan(const PvParams *P);
 extern "C" __global__ void pv_topn_scatter(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
 extern "C" __global__ void pv_net2_kernel(const PvParams *P);
+extern "C" __global__ void pv_ix_guess(const PvIxParams *X);
+extern "C" __global__ void pv_ix_fix(const PvIxParams *X, uint32_t src);
+extern "C" __global__ void pv_ix_scan(const PvIxParams *X);
+extern "C" __global__ void pv_ix_write(const PvIxParams *X);
+extern "C" __global__ void pv_ix_secs(const PvIxParams *X, uint32_t n);
 extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_t *theta_out);
 extern "C" __global__ void pv_topn_compact(const PvParams *P, uint32_t tb, uint8_t *tmp, unsigned long long *tmp_top);
 extern "C" __global__ void pv_topn_names(const PvParams *P);
@@ -384,7 +389,21 @@ struct pv_ctx {
         hipEvent_t copied = nullptr;
         std::vector<uint32_t> sci, scs;
         pv_index_info info{};
+        // device record index (pv_index.hip): segment state, status words, change points
+        uint8_t *d_ix = nullptr;    // PvIxParams + arrays, one allocation
+        PvIxParams *h_ix = nullptr; // pinned: params, then status / small read-backs
+        uint32_t ix_nseg = 0;
     };
+    bool device_index = true; // PV_INGEST_INDEX=host selects the host walk
+    // device-index ingest ring: raw chunks land at offset chunk of 2 x chunk buffers, the
+    // previous chunk's tail (records after its ts_sec cut) is moved in front of them on the device
+    struct Ring {
+        uint8_t *d_buf = nullptr;
+        uint32_t *d_offs = nullptr;
+        uint8_t *h_stage = nullptr;         // pinned staging of a pageable source
+        hipEvent_t landed = nullptr;
+    } ring[3];
+    hipStream_t copy_stream2 = nullptr;
     std::unique_ptr<pvi::Pool> pool;
     Stage stage[2];
     size_t stage_bytes = 0;   // record bytes per chunk
@@ -1392,7 +1411,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
         !hip_ok(e = hipMalloc(&c->d_status, ST_ALLOC * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_tab_live, PV_TABLES * 4)) ||
-        !hip_ok(e = hipMemset(c->d_tab_live, 0, PV_TABLES * 4)) ||
+        !hip_ok(e = hipMemsetAsync(c->d_tab_live, 0, PV_TABLES * 4, c->stream)) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_tab_live, PV_TABLES * 4, hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_theta, ((size_t)1 << c->reg_log2) * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
@@ -1444,11 +1463,20 @@ void pv_destroy(pv_ctx *c)
                      (void *)c->h_tparams, (void *)c->h_tab_live})
         if (hp) hipHostFree(hp);
     for (auto &st : c->stage) {
+        if (st.d_ix) hipFree(st.d_ix);
+        if (st.h_ix) hipHostFree(st.h_ix);
         if (st.h_recs) hipHostFree(st.h_recs);
         if (st.h_offs) hipHostFree(st.h_offs);
         if (st.copied) hipEventDestroy(st.copied);
     }
+    for (auto &r : c->ring) {
+        if (r.d_buf) hipFree(r.d_buf);
+        if (r.d_offs) hipFree(r.d_offs);
+        if (r.h_stage) hipHostFree(r.h_stage);
+        if (r.landed) hipEventDestroy(r.landed);
+    }
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+    if (c->copy_stream2) hipStreamDestroy(c->copy_stream2);
     c->pool.reset();
     if (c->ev_start) hipEventDestroy(c->ev_start);
     if (c->ev_stop) hipEventDestroy(c->ev_stop);
@@ -2324,7 +2352,148 @@ int ingest_setup(pv_ctx *c)
             return c->hipfail(e, "ingest staging");
         st.sci.resize(1 << 16);
         st.scs.resize(1 << 16);
+        // device record index state for a chunk of up to `chunk` bytes
+        const uint32_t nseg = (uint32_t)((2 * chunk + PV_IX_SEG - 1) / PV_IX_SEG); // a ring run: tail + chunk
+        const size_t bytes = 256 + (size_t)nseg * 8 * 3 + (size_t)(nseg + 1) * 4 * 2 + 64 + st.sci.size() * 8 + 1024;
+        if (!hip_ok(e = hipMalloc(&st.d_ix, bytes)) ||
+            !hip_ok(e = hipHostMalloc((void **)&st.h_ix, 256 + 64 + st.sci.size() * 8 + 1024, hipHostMallocDefault)))
+            return c->hipfail(e, "device index state");
+        st.ix_nseg = nseg;
     }
+    if (const char *v = getenv("PV_INGEST_INDEX")) c->device_index = strcmp(v, "host") != 0;
+    return 0;
+}
+
+// The record index of the records at [first, end) of d_base (256-B aligned, first < 256),
+// already on the device, on the device (pv_index.hip): offsets (relative to d_base) into
+// d_offs, the ts_sec change points into st.sci / st.scs (sorted), st.info as pv_index_records
+// fills it (bytes_used relative to d_base), *capped when more complete records follow the
+// first stage_recs. `hfirst` is byte `first` in host memory (headers of the first and last
+// records). Returns 1 when the validation passes do not settle (adversarial bytes: the caller
+// walks the block on the host), < 0 on an error.
+int device_index(pv_ctx *c, pv_ctx::Stage &st, const uint8_t *d_base, uint32_t first, const uint8_t *hfirst, size_t L,
+                 uint32_t *d_offs, hipStream_t s, bool *capped)
+{
+    const uint32_t nseg = (uint32_t)((L + PV_IX_SEG - 1) / PV_IX_SEG);
+    if (nseg > st.ix_nseg) return c->fail(PV_ECAPACITY, "index block of %zu bytes exceeds the index state", L);
+    *capped = false;
+    uint8_t *d = st.d_ix;
+    PvIxParams X;
+    memset(&X, 0, sizeof X);
+    size_t at = 256;
+    auto take = [&](size_t b) { uint8_t *q = d + at; at += (b + 63) & ~(size_t)63; return q; };
+    X.recs = d_base;
+    X.bytes = L;
+    X.first = first;
+    X.nseg = nseg;
+    X.frac_lim = c->cfg.ts_nano ? 1000000000u : 1000000u;
+    memcpy(&X.sec0, hfirst, 4);
+    X.start = (uint64_t *)take((size_t)nseg * 8);
+    X.exit[0] = (uint64_t *)take((size_t)nseg * 8);
+    X.exit[1] = (uint64_t *)take((size_t)nseg * 8);
+    X.cnt = (uint32_t *)take((size_t)nseg * 4);
+    X.base = (uint32_t *)take((size_t)(nseg + 1) * 4);
+    X.status = (uint32_t *)take(16);
+    X.sci = (uint32_t *)take(st.sci.size() * 4);
+    X.scs = (uint32_t *)take(st.sci.size() * 4);
+    X.offs = d_offs;
+    X.max_records = c->stage_recs;
+    X.max_changes = (uint32_t)st.sci.size();
+    uint32_t *h = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(st.h_ix) + 256); // read-back words
+    *st.h_ix = X;
+    const PvIxParams *dX = reinterpret_cast<const PvIxParams *>(d);
+    const dim3 g((nseg + 255) / 256), b(256);
+    hipError_t e;
+    if (!hip_ok(e = hipMemcpyAsync(d, st.h_ix, sizeof X, hipMemcpyHostToDevice, s)) ||
+        !hip_ok(e = hipMemsetAsync(X.status, 0, 16, s)))
+        return c->hipfail(e, "device index");
+    hipLaunchKernelGGL(pv_ix_guess, g, b, 0, s, dX);
+    uint32_t src = 0;
+    bool settled = false;
+    for (int pass = 0; pass < 64 && !settled; pass++) {
+        hipMemsetAsync(X.status, 0, 4, s);
+        hipLaunchKernelGGL(pv_ix_fix, g, b, 0, s, dX, src);
+        src ^= 1;
+        if (!hip_ok(e = hipMemcpyAsync(h, X.status, 4, hipMemcpyDeviceToHost, s)) || !hip_ok(e = hipStreamSynchronize(s)))
+            return c->hipfail(e, "device index pass");
+        settled = h[0] == 0;
+    }
+    if (!settled) return 1;
+    hipLaunchKernelGGL(pv_ix_scan, dim3(1), dim3(1024), 0, s, dX);
+    uint64_t chain_end = 0;
+    if (!hip_ok(e = hipMemcpyAsync(h, X.base + nseg, 4, hipMemcpyDeviceToHost, s)) ||
+        !hip_ok(e = hipMemcpyAsync(h + 2, X.exit[src] + nseg - 1, 8, hipMemcpyDeviceToHost, s)) ||
+        !hip_ok(e = hipStreamSynchronize(s)))
+        return c->hipfail(e, "device index scan");
+    const uint64_t total = h[0];
+    memcpy(&chain_end, h + 2, 8);
+    const uint64_t n = std::min<uint64_t>(total, c->stage_recs);
+    pv_index_info &info = st.info;
+    memset(&info, 0, sizeof info);
+    info.monotone = 1;
+    info.n_records = n;
+    info.bytes_used = chain_end & ~PV_IX_STOP;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(pv_ix_write, g, b, 0, s, dX);
+    hipLaunchKernelGGL(pv_ix_secs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, dX, (uint32_t)n);
+    const uint32_t pre = 1024; // change points read back with the status; more in a second copy
+    if (!hip_ok(e = hipGetLastError()) ||
+        !hip_ok(e = hipMemcpyAsync(h, X.status, 16, hipMemcpyDeviceToHost, s)) ||
+        !hip_ok(e = hipMemcpyAsync(h + 4, X.offs + n - 1, 4, hipMemcpyDeviceToHost, s)) ||
+        !hip_ok(e = hipMemcpyAsync(h + 16, X.sci, pre * 4, hipMemcpyDeviceToHost, s)) ||
+        !hip_ok(e = hipMemcpyAsync(h + 16 + st.sci.size(), X.scs, pre * 4, hipMemcpyDeviceToHost, s)) ||
+        !hip_ok(e = hipStreamSynchronize(s)))
+        return c->hipfail(e, "device index read-back");
+    const uint32_t nc = h[1];
+    const uint32_t last_off = h[4];
+    if (nc > st.sci.size()) return c->fail(PV_ECAPACITY, "more than %zu ts_sec changes in one ingest chunk", st.sci.size());
+    if (nc > pre &&
+        (!hip_ok(e = hipMemcpyAsync(h + 16, X.sci, (size_t)nc * 4, hipMemcpyDeviceToHost, s)) ||
+         !hip_ok(e = hipMemcpyAsync(h + 16 + st.sci.size(), X.scs, (size_t)nc * 4, hipMemcpyDeviceToHost, s)) ||
+         !hip_ok(e = hipStreamSynchronize(s))))
+        return c->hipfail(e, "device index change points");
+    std::vector<std::pair<uint32_t, uint32_t>> ch(nc);
+    for (uint32_t k = 0; k < nc; k++) ch[k] = {h[16 + k], h[16 + st.sci.size() + k]};
+    std::sort(ch.begin(), ch.end());
+    for (uint32_t k = 0; k < nc; k++) { st.sci[k] = ch[k].first; st.scs[k] = ch[k].second; }
+    info.n_sec_changes = nc;
+    info.monotone = h[2] ? 0 : 1;
+    uint32_t h0[4], h1[4];
+    memcpy(h0, hfirst, 16);
+    memcpy(h1, hfirst + (last_off - first), 16);
+    if (n < total) {
+        info.bytes_used = (uint64_t)last_off + 16 + h1[2];
+        *capped = true;
+    }
+    info.first_sec = h0[0];
+    info.first_nsec = c->cfg.ts_nano ? (int64_t)h0[1] : (int64_t)h0[1] * 1000;
+    info.last_sec = h1[0];
+    info.last_nsec = c->cfg.ts_nano ? (int64_t)h1[1] : (int64_t)h1[1] * 1000;
+    return 0;
+}
+
+// device_index's fallback: the host walk of the block, its offsets copied to d_offs
+int host_index_run(pv_ctx *c, pv_ctx::Stage &st, const uint8_t *d_base, uint32_t first, const uint8_t *hfirst, size_t end,
+                   uint32_t *d_offs, bool *capped)
+{
+    (void)d_base;
+    pv_index_info &info = st.info;
+    if (int rc = pv_index_records(hfirst, end - first, c->cfg.ts_nano, st.h_offs, c->stage_recs, st.sci.data(), st.scs.data(),
+                                  (uint32_t)st.sci.size(), &info))
+        return c->fail(rc, "record index failed");
+    const uint64_t n = info.n_records;
+    *capped = false;
+    if (n == c->stage_recs && info.bytes_used + 16 <= end - first) {
+        uint32_t cl;
+        memcpy(&cl, hfirst + info.bytes_used + 8, 4);
+        *capped = info.bytes_used + 16 + (uint64_t)cl <= end - first;
+    }
+    for (uint64_t i = 0; i < n; i++) st.h_offs[i] += first;
+    info.bytes_used += first;
+    hipError_t e;
+    if (n && (!hip_ok(e = hipMemcpyAsync(d_offs, st.h_offs, n * 4, hipMemcpyHostToDevice, c->stream)) ||
+              !hip_ok(e = hipStreamSynchronize(c->stream))))
+        return c->hipfail(e, "H2D offsets");
     return 0;
 }
 
@@ -2382,6 +2551,178 @@ int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int6
     return 0;
 }
 
+// Host-memory path with the record index on the device. The blob is cut into fixed
+// chunk-sized pieces in host order, so their H2D copies stream back to back (a producer
+// thread, two copy streams, a ring of three device buffers of two chunks each) without
+// waiting on any index. The calling thread, per piece: moves the previous batch's tail (the
+// records after its last ts_sec cut) in front of the piece on the device, indexes the joined
+// run there (pv_index.hip), cuts it at its last ts_sec boundary and runs the batch. The host
+// reads a few header words only. Batches are cut as pv_process_host's host-index path cuts
+// them (at most stage_recs records, ending at a ts_sec boundary unless the data ends).
+int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
+{
+    const size_t L = c->stage_bytes; // a multiple of 256: runs start 256-B aligned (+ first)
+    hipError_t e;
+    for (auto &r : c->ring) {
+        if (r.d_buf) continue;
+        if (!hip_ok(e = hipMalloc(&r.d_buf, 2 * L + PV_RECS_PAD)) || !hip_ok(e = hipMalloc(&r.d_offs, c->stage_recs * 4)) ||
+            !hip_ok(e = hipEventCreateWithFlags(&r.landed, hipEventDisableTiming)) ||
+            // on the context's stream: a null-stream memset is not ordered with the
+            // non-blocking copy streams and could land after a piece's copy
+            !hip_ok(e = hipMemsetAsync(r.d_buf, 0, 2 * L + PV_RECS_PAD, c->stream)) ||
+            !hip_ok(e = hipStreamSynchronize(c->stream)))
+            return c->hipfail(e, "ingest ring");
+    }
+    if (!c->copy_stream2 && !hip_ok(e = hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking)))
+        return c->hipfail(e, "copy stream");
+    const bool pinned = host_pinned(recs);
+    if (!pinned)
+        for (auto &r : c->ring)
+            if (!r.h_stage && !hip_ok(e = hipHostMalloc((void **)&r.h_stage, L, hipHostMallocDefault)))
+                return c->hipfail(e, "ingest staging");
+    const uint64_t npieces = (bytes + L - 1) / L;
+    // producer: piece p's copy into ring slot p % 3 at offset L. Slot p % 3 last held run
+    // p - 3, whose batches are done and whose tail run p - 2 has moved out: issued once the
+    // consumer has finished run p - 2 (freed > p - 3). The consumer synchronises its stream
+    // after each run, so the host-side order is the device-side order.
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t issued = 0, freed = 0;
+    bool abort = false;
+    int prod_rc = 0;
+    std::string prod_err;
+    auto producer = [&] {
+        for (uint64_t k = 0; k < npieces; k++) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return abort || k < freed + 3; });
+                if (abort) return;
+            }
+            pv_ctx::Ring &r = c->ring[k % 3];
+            const size_t len = std::min(L, bytes - k * L);
+            const uint8_t *src = recs + k * L;
+            if (!pinned) {
+                auto t1 = std::chrono::steady_clock::now();
+                pvi::copy_parallel(*c->pool, r.h_stage, src, len);
+                src = r.h_stage;
+                c->ingest_ms[0] += ms_since(t1);
+            }
+            hipStream_t cs = (k & 1) ? c->copy_stream2 : c->copy_stream;
+            if (!hip_ok(e = hipMemcpyAsync(r.d_buf + L, src, len, hipMemcpyHostToDevice, cs)) ||
+                !hip_ok(e = hipEventRecord(r.landed, cs))) {
+                std::lock_guard<std::mutex> g(mu);
+                prod_rc = PV_EHIP;
+                prod_err = std::string("H2D: ") + hipGetErrorString(e);
+                abort = true;
+                cv.notify_all();
+                return;
+            }
+            std::lock_guard<std::mutex> g(mu);
+            issued = k + 1;
+            cv.notify_all();
+        }
+    };
+    std::thread th(producer);
+    pv_ctx::Stage &st = c->stage[0]; // index state, change lists, host offsets (fallback)
+    int rc = 0;
+    size_t tail = 0;
+    const uint8_t *tail_src = nullptr;
+    for (uint64_t k = 0; k < npieces && !rc; k++) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return abort || issued > k; });
+            if (abort) break;
+        }
+        pv_ctx::Ring &r = c->ring[k % 3];
+        const size_t len = std::min(L, bytes - k * L);
+        const bool last_piece = k + 1 == npieces;
+        // the run: the tail at [L - tail, L), the piece at [L, L + len); b is 256-B aligned and
+        // the first record at b + first; hf is that record in host memory
+        uint8_t *b = r.d_buf + ((L - tail) & ~(size_t)255);
+        uint32_t first = (uint32_t)((L - tail) & 255);
+        const uint8_t *hf = recs + k * L - tail;
+        size_t end = first + tail + len;
+        auto t0 = std::chrono::steady_clock::now();
+        if (!hip_ok(e = hipStreamWaitEvent(c->stream, r.landed, 0)) ||
+            (tail && !hip_ok(e = hipMemcpyAsync(b + first, tail_src, tail, hipMemcpyDeviceToDevice, c->stream)))) {
+            rc = c->hipfail(e, "ingest run");
+            break;
+        }
+        tail = 0;
+        for (;;) {
+            bool capped = false;
+            int ix = device_index(c, st, b, first, hf, end, r.d_offs, c->stream, &capped);
+            if (ix < 0) { rc = ix; break; }
+            if (ix > 0 && (rc = host_index_run(c, st, b, first, hf, end, r.d_offs, &capped))) break;
+            pv_index_info info = st.info;
+            c->ingest_ms[1] += ms_since(t0);
+            const bool more = !last_piece || capped; // records follow this batch
+            if (info.n_records == 0) {
+                if (!last_piece && end - first >= L) { rc = c->fail(PV_ECAPACITY, "record larger than the ingest chunk"); break; }
+                if (!last_piece) { tail = end - first; tail_src = b + first; }
+                break;
+            }
+            // a batch that more records follow ends at its last ts_sec boundary when it spans
+            // more than one second, so a period shift and the DNS records of its first second
+            // reach the device in the same batch
+            if (more && info.n_sec_changes > 1 && info.n_sec_changes <= st.sci.size()) {
+                const uint32_t cut = st.sci[info.n_sec_changes - 1];
+                uint32_t o[2];
+                if (!hip_ok(e = hipMemcpyAsync(o, r.d_offs + cut - 1, 8, hipMemcpyDeviceToHost, c->stream)) ||
+                    !hip_ok(e = hipStreamSynchronize(c->stream))) {
+                    rc = c->hipfail(e, "cut read-back");
+                    break;
+                }
+                info.n_records = cut;
+                info.bytes_used = o[1];
+                info.n_sec_changes -= 1;
+                uint32_t h[2];
+                memcpy(h, hf + (o[0] - first), 8);
+                info.last_sec = h[0];
+                info.last_nsec = c->cfg.ts_nano ? (int64_t)h[1] : (int64_t)h[1] * 1000;
+                capped = true;
+            }
+            auto t2 = std::chrono::steady_clock::now();
+            rc = pv_process_device(c, b, r.d_offs, &info, st.sci.data(), st.scs.data(), nullptr);
+            if (!rc) rc = pv_synchronize(c);
+            c->ingest_ms[3] += ms_since(t2);
+            if (rc) break;
+            t0 = std::chrono::steady_clock::now();
+            const size_t used = info.bytes_used;
+            const size_t rest = end - used;
+            if (!capped && last_piece) break;          // the data ends (at most a partial record)
+            if (!last_piece && (!capped || rest <= L)) {
+                if (rest > L) { rc = c->fail(PV_ECAPACITY, "record larger than the ingest chunk"); break; }
+                tail = rest;
+                tail_src = b + used;
+                break;
+            }
+            // more batches from this run, in place
+            hf += used - first;
+            b += used & ~(size_t)255;
+            first = (uint32_t)(used & 255);
+            end -= used & ~(size_t)255;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu);
+            freed = k; // slot (k - 1) % 3 is free: its tail has moved into this run
+            cv.notify_all();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (rc) abort = true;
+        freed = npieces + 3;
+        cv.notify_all();
+    }
+    th.join();
+    hipStreamSynchronize(c->copy_stream);
+    hipStreamSynchronize(c->copy_stream2);
+    if (rc) return rc;
+    if (prod_rc) return c->fail(prod_rc, "%s", prod_err.c_str());
+    return 0;
+}
+
 // Host-memory path, pipelined over chunks of the record blob: a producer thread stages
 // chunk k + 1 (parallel copy into pinned memory unless the caller's buffer is already
 // pinned, parallel record index, H2D on the copy stream) while the calling thread runs
@@ -2390,6 +2731,7 @@ int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
 {
     hipSetDevice(c->device);
     if (int rc = ingest_setup(c)) return rc;
+    if (c->device_index && bytes >= 4096) return process_host_ring(c, recs, bytes);
     const bool pinned = host_pinned(recs);
     std::mutex mu;
     std::condition_variable cv;
@@ -2414,11 +2756,10 @@ int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
             auto t1 = std::chrono::steady_clock::now();
             // pageable source: copied into pinned staging by the threads that index it
             rc = pvi::index_records_parallel(*c->pool, src, L, c->cfg.ts_nano, st.h_offs, c->stage_recs, st.sci.data(),
-                                             st.scs.data(), (uint32_t)st.sci.size(), &st.info,
-                                             pinned ? nullptr : st.h_recs);
+                                             st.scs.data(), (uint32_t)st.sci.size(), &st.info, pinned ? nullptr : st.h_recs);
+            if (rc) { prod_err = "record index failed"; break; }
             const uint8_t *base = pinned ? src : st.h_recs;
             c->ingest_ms[pinned ? 1 : 0] += ms_since(t1);
-            if (rc) { prod_err = "record index failed"; break; }
             if (st.info.n_records == 0) {
                 if (L == c->stage_bytes && pos + L < bytes) { rc = PV_ECAPACITY; prod_err = "record larger than the ingest chunk"; }
                 break;
@@ -2440,12 +2781,12 @@ int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
             }
             auto t2 = std::chrono::steady_clock::now();
             const size_t used = st.info.bytes_used;
-            hipError_t e;
-            if (!hip_ok(e = hipMemcpyAsync(st.d_recs, base, used, hipMemcpyHostToDevice, c->copy_stream)) ||
-                !hip_ok(e = hipMemsetAsync(st.d_recs + used, 0, PV_RECS_PAD, c->copy_stream)) ||
-                !hip_ok(e = hipMemcpyAsync(st.d_offs, st.h_offs, st.info.n_records * 4, hipMemcpyHostToDevice,
-                                           c->copy_stream)) ||
-                !hip_ok(e = hipEventRecord(st.copied, c->copy_stream))) {
+            hipError_t e = hipSuccess;
+            const bool ok = hip_ok(e = hipMemcpyAsync(st.d_recs, base, used, hipMemcpyHostToDevice, c->copy_stream)) &&
+                             hip_ok(e = hipMemsetAsync(st.d_recs + used, 0, PV_RECS_PAD, c->copy_stream)) &&
+                             hip_ok(e = hipMemcpyAsync(st.d_offs, st.h_offs, st.info.n_records * 4, hipMemcpyHostToDevice,
+                                                       c->copy_stream));
+            if (!ok || !hip_ok(e = hipEventRecord(st.copied, c->copy_stream))) {
                 rc = PV_EHIP;
                 prod_err = std::string("H2D: ") + hipGetErrorString(e);
                 break;
@@ -2489,6 +2830,56 @@ int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
     if (rc) return rc;
     if (prod_rc) return c->fail(prod_rc, "%s", prod_err.c_str());
     return 0;
+}
+
+// The device record index (pv_index.hip) of one block in host memory, filled as
+// pv_index_records fills its outputs (a block of at most one ingest chunk).
+int pv_index_records_device(pv_ctx *c, const uint8_t *recs, size_t bytes, uint32_t *offsets, uint64_t max_records,
+                            uint32_t *sc_idx, uint32_t *sc_sec, uint32_t max_changes, pv_index_info *info)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (int rc = ingest_setup(c)) return rc;
+    if (bytes > c->stage_bytes) return c->fail(PV_EINVAL, "block of %zu bytes exceeds the ingest chunk", bytes);
+    if (bytes < 16) { // no complete record header
+        memset(info, 0, sizeof *info);
+        info->monotone = 1;
+        return 0;
+    }
+    pv_ctx::Stage &st = c->stage[0];
+    hipError_t e;
+    if (!hip_ok(e = hipMemcpyAsync(st.d_recs, recs, bytes, hipMemcpyHostToDevice, c->copy_stream)) ||
+        !hip_ok(e = hipMemsetAsync(st.d_recs + bytes, 0, PV_RECS_PAD, c->copy_stream)))
+        return c->hipfail(e, "H2D");
+    bool capped = false;
+    hipStreamSynchronize(c->copy_stream);
+    int rc = device_index(c, st, st.d_recs, 0, recs, bytes, st.d_offs, c->stream, &capped);
+    if (rc < 0) return rc;
+    if (rc > 0 && (rc = host_index_run(c, st, st.d_recs, 0, recs, bytes, st.d_offs, &capped))) return rc;
+    const uint64_t n = std::min<uint64_t>(st.info.n_records, max_records);
+    if (n && (!hip_ok(e = hipMemcpyAsync(offsets, st.d_offs, n * 4, hipMemcpyDeviceToHost, c->copy_stream)) ||
+              !hip_ok(e = hipStreamSynchronize(c->copy_stream))))
+        return c->hipfail(e, "D2H offsets");
+    *info = st.info;
+    info->n_records = n;
+    uint32_t nch = (uint32_t)st.info.n_sec_changes;
+    if (n && n < st.info.n_records) {
+        // capped at max_records: the walk as pv_index_records stops it there
+        uint32_t hl[4];
+        memcpy(hl, recs + offsets[n - 1], 16);
+        info->bytes_used = offsets[n - 1] + 16 + (uint64_t)hl[2];
+        info->last_sec = hl[0];
+        info->last_nsec = c->cfg.ts_nano ? (int64_t)hl[1] : (int64_t)hl[1] * 1000;
+        while (nch && st.sci[nch - 1] >= n) nch--;
+        info->n_sec_changes = nch;
+        // monotonicity of the first n records
+        info->monotone = 1;
+        for (uint32_t k = 1; k < nch; k++)
+            if (st.scs[k] < st.scs[k - 1]) info->monotone = 0;
+    }
+    const uint32_t nc = std::min<uint32_t>(nch, max_changes);
+    for (uint32_t k = 0; k < nc; k++) { sc_idx[k] = st.sci[k]; sc_sec[k] = st.scs[k]; }
+    return nch > max_changes ? PV_ECAPACITY : 0;
 }
 
 int pv_ingest_timing(pv_ctx *c, double *ms4, int reset)

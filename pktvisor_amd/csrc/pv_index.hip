@@ -1,0 +1,218 @@
+// SPDX-License-Identifier: MPL-2.0
+//
+// pv_index.hip — the pcap record index on the device, for the host-memory ingest path.
+//
+// The reference walks a capture one record at a time (PcapInputStream::_open_pcap,
+// src/inputs/pcap/PcapInputStream.cpp:471-527). pv_index_records is that walk on the host;
+// here it runs on the chunk the ingest has just copied to HBM, so the host only copies.
+// The chunk is cut into PV_IX_SEG-byte segments, one lane each:
+//
+//   1. pv_ix_guess: segment 0 starts at the first record (X.first); segment s > 0 guesses its first record
+//      start (the first offset from which four headers are plausible, as the host's
+//      parallel index guesses) and walks to its end: records starting in the segment,
+//      and the position after them (its exit).
+//   2. pv_ix_fix, repeated until nothing changes: the true first start of segment s is
+//      segment s - 1's exit; a segment whose guess differs walks again from there.
+//      Exits are double-buffered, so one pass moves the validated chain on by at least
+//      one segment and a correct guess settles in one pass.
+//   3. pv_ix_scan: record counts to per-segment bases (one workgroup).
+//   4. pv_ix_write: each segment writes its record offsets.
+//   5. pv_ix_secs: the ts_sec change points and monotonicity, one lane per record.
+//
+// Walks are deterministic and the chain is validated from byte 0, so the offsets equal the
+// sequential walk's for any input; the guesses only decide how many fix passes run.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pv_layout.h"
+
+#define PV_IX_BACK 4096u // segments a fix pass looks back over for an exit (8 MiB)
+
+
+
+namespace {
+
+__device__ __forceinline__ void hdr(const uint8_t *r, uint64_t p, uint32_t &sec, uint32_t &frac, uint32_t &cl, uint32_t &len)
+{
+    // record headers are 4-byte aligned only when every caplen is: byte loads in general
+    const uint8_t *h = r + p;
+    if ((p & 3) == 0) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(h);
+        sec = w[0]; frac = w[1]; cl = w[2]; len = w[3];
+        return;
+    }
+    uint32_t w[4];
+    for (int k = 0; k < 4; k++)
+        w[k] = (uint32_t)h[4 * k] | ((uint32_t)h[4 * k + 1] << 8) | ((uint32_t)h[4 * k + 2] << 16) | ((uint32_t)h[4 * k + 3] << 24);
+    sec = w[0]; frac = w[1]; cl = w[2]; len = w[3];
+}
+__device__ __forceinline__ uint32_t caplen_at(const uint8_t *r, uint64_t p)
+{
+    const uint8_t *h = r + p + 8;
+    if ((p & 3) == 0) return *reinterpret_cast<const uint32_t *>(h);
+    return (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+}
+
+// the host's plausibility test (pv_ingest.cpp plausible): four headers with ts_sec within a
+// day of the chunk's first, the sub-second field in range, caplen <= min(len, 256 KiB)
+__device__ bool plausible(const PvIxParams &X, uint64_t p)
+{
+    for (int k = 0; k < 4; k++) {
+        if (p == X.bytes) return true;
+        if (p + 16 > X.bytes) return k > 0;
+        uint32_t sec, frac, cl, len;
+        hdr(X.recs, p, sec, frac, cl, len);
+        const uint32_t dsec = sec > X.sec0 ? sec - X.sec0 : X.sec0 - sec;
+        if (dsec > 86400 || cl > (256u << 10) || cl > len || frac >= X.frac_lim) return false;
+        if (p + 16 + (uint64_t)cl > X.bytes) return k > 0;
+        p += 16 + (uint64_t)cl;
+    }
+    return true;
+}
+
+// records starting in [p, hi) from p: their count and the position after them
+__device__ uint64_t walk(const PvIxParams &X, uint64_t p, uint64_t hi, uint32_t &n)
+{
+    n = 0;
+    while (p < hi) {
+        if (p + 16 > X.bytes) return p | PV_IX_STOP;
+        const uint32_t cl = caplen_at(X.recs, p);
+        if (p + 16 + (uint64_t)cl > X.bytes) return p | PV_IX_STOP;
+        n++;
+        p += 16 + (uint64_t)cl;
+    }
+    return p;
+}
+
+__device__ __forceinline__ uint64_t seg_lo(const PvIxParams &X, uint32_t s) { return (uint64_t)s * PV_IX_SEG; }
+__device__ __forceinline__ uint64_t seg_hi(const PvIxParams &X, uint32_t s) { return min<uint64_t>(X.bytes, (uint64_t)(s + 1) * PV_IX_SEG); }
+
+} // namespace
+
+extern "C" __global__ void pv_ix_guess(const PvIxParams *__restrict__ Xp)
+{
+    const PvIxParams X = *Xp;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= X.nseg) return;
+    const uint64_t lo = seg_lo(X, s), hi = seg_hi(X, s);
+    uint64_t p = s ? lo : X.first;
+    if (s > 0) {
+        while (p < hi && !plausible(X, p)) p++;
+        if (p >= hi) {
+            X.start[s] = PV_IX_NONE;
+            X.cnt[s] = 0;
+            X.exit[0][s] = PV_IX_NONE;
+            return;
+        }
+    }
+    uint32_t n;
+    X.start[s] = p;
+    X.exit[0][s] = walk(X, p, hi, n);
+    X.cnt[s] = n;
+}
+
+// one validation pass: exit[src] -> exit[src ^ 1]
+extern "C" __global__ void pv_ix_fix(const PvIxParams *__restrict__ Xp, uint32_t src)
+{
+    const PvIxParams X = *Xp;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= X.nseg) return;
+    const uint64_t *ein = X.exit[src];
+    uint64_t *eout = X.exit[src ^ 1];
+    if (s == 0) { eout[0] = ein[0]; return; }
+    // the exit of the nearest earlier segment that has one: segments with no start of their
+    // own (inside a long record) are skipped, so a record spanning many segments settles in
+    // one pass instead of one segment per pass
+    uint32_t t = s - 1;
+    while (t > 0 && ein[t] == PV_IX_NONE && s - t < PV_IX_BACK) t--;
+    const uint64_t prev = ein[t];
+    uint64_t cur = ein[s];
+    // the chain has not reached here yet, or lands in a skipped segment that walks first
+    if (prev == PV_IX_NONE || (!(prev & PV_IX_STOP) && prev < seg_lo(X, s))) { eout[s] = cur; return; }
+    const uint64_t hi = seg_hi(X, s);
+    if (prev & PV_IX_STOP) {
+        // the walk stopped before this segment: no records here
+        if (X.start[s] != prev || cur != prev) {
+            X.start[s] = prev;
+            X.cnt[s] = 0;
+            cur = prev;
+            atomicOr(&X.status[0], 1u);
+        }
+    } else if (prev >= hi) {
+        // a record spans this whole segment
+        if (X.start[s] != prev || cur != prev) {
+            X.start[s] = prev;
+            X.cnt[s] = 0;
+            cur = prev;
+            atomicOr(&X.status[0], 1u);
+        }
+    } else if (X.start[s] != prev) {
+        uint32_t n;
+        X.start[s] = prev;
+        cur = walk(X, prev, hi, n);
+        X.cnt[s] = n;
+        atomicOr(&X.status[0], 1u);
+    }
+    eout[s] = cur;
+}
+
+// exclusive prefix of the segment counts (one workgroup of 1024)
+extern "C" __global__ void __launch_bounds__(1024) pv_ix_scan(const PvIxParams *__restrict__ Xp)
+{
+    const PvIxParams X = *Xp;
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (X.nseg + 1023) / 1024;
+    const uint32_t a = threadIdx.x * per, b = min(X.nseg, a + per);
+    uint32_t sum = 0;
+    for (uint32_t s = a; s < b; s++) sum += X.cnt[s];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (uint32_t s = a; s < b; s++) { X.base[s] = run; run += X.cnt[s]; }
+    if (threadIdx.x == 1023) X.base[X.nseg] = part[1023];
+}
+
+extern "C" __global__ void pv_ix_write(const PvIxParams *__restrict__ Xp)
+{
+    const PvIxParams X = *Xp;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= X.nseg || !X.cnt[s]) return;
+    uint64_t p = X.start[s];
+    uint64_t i = X.base[s];
+    for (uint32_t k = 0; k < X.cnt[s] && i < X.max_records; k++, i++) {
+        X.offs[i] = (uint32_t)p;
+        p += 16 + (uint64_t)caplen_at(X.recs, p);
+    }
+}
+
+// ts_sec change points (record i whose ts_sec differs from record i - 1's) and monotonicity
+extern "C" __global__ void pv_ix_secs(const PvIxParams *__restrict__ Xp, uint32_t n)
+{
+    const PvIxParams X = *Xp;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t p = X.offs[i];
+    const uint32_t sec = ((p & 3) == 0) ? *reinterpret_cast<const uint32_t *>(X.recs + p)
+                                         : (uint32_t)X.recs[p] | ((uint32_t)X.recs[p + 1] << 8) |
+                                               ((uint32_t)X.recs[p + 2] << 16) | ((uint32_t)X.recs[p + 3] << 24);
+    int64_t prev = -1;
+    if (i) {
+        const uint64_t q = X.offs[i - 1];
+        prev = ((q & 3) == 0) ? *reinterpret_cast<const uint32_t *>(X.recs + q)
+                              : (uint32_t)X.recs[q] | ((uint32_t)X.recs[q + 1] << 8) | ((uint32_t)X.recs[q + 2] << 16) |
+                                    ((uint32_t)X.recs[q + 3] << 24);
+    }
+    if ((int64_t)sec == prev) return;
+    if ((int64_t)sec < prev) atomicOr(&X.status[2], 1u);
+    const uint32_t k = atomicAdd(&X.status[1], 1u);
+    if (k < X.max_changes) {
+        X.sci[k] = i;
+        X.scs[k] = sec;
+    }
+}

@@ -473,3 +473,23 @@ struct PvTcpParams {
 };
 enum { PVT_NMSG = 0, PVT_ARENA, PVT_CARRY, PVT_NCARRY, PVT_NFRAG, PVT_FLAGS, PVT_WORDS };
 enum { PVT_F_TABLE = 1, PVT_F_ARENA = 2, PVT_F_CARRY = 4, PVT_F_FRAGS = 8, PVT_F_MSGS = 16 };
+
+// Device record index of an ingest chunk (pv_index.hip)
+#define PV_IX_SEG 2048u
+#define PV_IX_NONE 0xffffffffffffffffull
+#define PV_IX_STOP (1ull << 63) // exit flag: the walk stopped at a truncated record / the end
+struct PvIxParams {
+    const PV_G uint8_t *recs;
+    uint64_t bytes;
+    uint32_t nseg, frac_lim, sec0, first; // first: offset of the first record (< PV_IX_SEG)
+    PV_G uint64_t *start;      // per segment: first record start (PV_IX_NONE: none found)
+    PV_G uint64_t *exit[2];    // per segment: position after its records (| PV_IX_STOP), double-buffered
+    PV_G uint32_t *cnt;        // per segment: records starting in it
+    PV_G uint32_t *base;       // per segment + 1: exclusive prefix of cnt
+    PV_G uint32_t *offs;       // record offsets
+    uint64_t max_records;
+    PV_G uint32_t *status;     // [0] fix pass changed something, [1] sec changes, [2] non-monotone
+    PV_G uint32_t *sci, *scs;  // sec change points (unordered; the host sorts them)
+    uint32_t max_changes;
+};
+
