@@ -200,6 +200,19 @@ int pv_index_records_mt(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uin
  * (parallel host index, H2D of records + offsets). Returns when every record has been
  * processed. */
 int pv_process_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes);
+/* dnstap input: a Frame Streams file of dnstap.Dnstap protobuf frames (DnstapInputStream,
+ * src/inputs/dnstap/DnstapInputStream.cpp:33-92) through both handlers' process_dnstap
+ * (NetworkMetricsBucket::process_dnstap, net/v1/NetStreamHandler.cpp:549-620;
+ * DnsMetricsBucket::process_dnstap, dns/v1/DnsStreamHandler.cpp:839-909; the managers at
+ * :832-843 and :1376-1412). msg_type_mask is the DNS handler's "dnstap_msg_type" filter
+ * (bit t: dnstap Message.Type t passes; 0 = no filter, :171-184,260-266): a message of
+ * another type is a filtered DNS event. Timestamps: the response time of CLIENT / AUTH /
+ * RESOLVER responses, the query time of their queries, else the wall clock. Not built: the
+ * v2 handlers' dnstap paths (PV_EUNSUPPORTED) and the input's only_hosts filter. */
+int pv_process_dnstap(pv_ctx *ctx, const uint8_t *frames, size_t bytes, uint32_t msg_type_mask);
+/* Frame Streams decode only: data frames read and dnstap MESSAGE events in them. */
+int pv_dnstap_count(const uint8_t *frames, size_t bytes, uint32_t *n_frames, uint32_t *n_events);
+
 /* Page-lock a host range so pv_process_host DMAs from it directly (hipHostRegister). */
 int pv_host_register(void *ptr, size_t bytes);
 int pv_host_unregister(void *ptr);

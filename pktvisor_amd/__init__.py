@@ -159,7 +159,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_host_unregister", "pv_ingest_timing", "pv_edge_export", "pv_edge_merge", "pv_values_export",
            "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code", "pv_advance_windows",
            "pv_dns_event_seconds", "pv_dns_event_seconds_host", "pv_comm_unique_id", "pv_comm_init",
-           "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy"]
+           "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count"]
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
 
@@ -226,6 +226,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_comm_allreduce_window.argtypes = [P]
     lib.pv_comm_allgather.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), P]
     lib.pv_comm_destroy.argtypes = [P]
+    lib.pv_process_dnstap.argtypes = [P, P, ctypes.c_size_t, U32]
+    lib.pv_dnstap_count.argtypes = [P, ctypes.c_size_t, ctypes.POINTER(U32), ctypes.POINTER(U32)]
     _lib = lib
     return lib
 
@@ -255,6 +257,28 @@ def read_pcap(path: str):
         raise PvError("Cannot open pcap/pcapng file (only little-endian classic pcap is supported)")
     linktype = struct.unpack_from("<I", data, 20)[0]
     return linktype, int(magic == 0xA1B23C4D), data[24:]
+
+
+def dnstap_count(frames: bytes):
+    """(data frames, dnstap MESSAGE events) of a Frame Streams file (host decode only)."""
+    nf, ne = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    buf = np.frombuffer(frames, dtype=np.uint8)
+    load_library().pv_dnstap_count(buf.ctypes.data, buf.nbytes, ctypes.byref(nf), ctypes.byref(ne))
+    return nf.value, ne.value
+
+
+def dnstap_reader(path: str, periods: int = 1, **kw) -> dict:
+    """A dnstap file (DnstapInputStream "dnstap_file") through the Net v1 ("packets") and DNS v1
+    ("dns") handlers: {"<periods>m": window}."""
+    with open(path, "rb") as f:
+        frames = f.read()
+    h = PvHandlers(num_periods=periods, **kw)
+    try:
+        h.process_dnstap(frames)
+        key = f"{1 if periods == 1 else periods}m"
+        return {key: h.window_json(0 if periods == 1 else periods, merged=periods != 1)}
+    finally:
+        h.close()
 
 
 def pcap_file_bytes(records: bytes, linktype: int = 1, ts_nano: int = 0) -> bytes:
@@ -304,6 +328,7 @@ class PvHandlers:
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
         net_filter_all = 0
+        self.dnstap_mask = 0
         net2_groups = 0
         if net2_config is not None:
             # the Net v2 handler ("net") attached next to v1 ("packets")
@@ -328,6 +353,7 @@ class PvHandlers:
             n, d = pvcfg.net_start(ncfg), pvcfg.dns_start(dcfg)
             net_groups, dns_groups, net_filter_all = n["groups"], d["groups"], int(n["filter_all"])
             filt = d["filters"]
+            self.dnstap_mask = d["dnstap_mask"]
             if d["xact_ttl_ms"] is not None and dns2_config is None:
                 xact_ttl_ms = d["xact_ttl_ms"]
         self._host = host_spec.encode() if host_spec else None
@@ -378,6 +404,13 @@ class PvHandlers:
     def process_host(self, recs):
         buf = recs if isinstance(recs, np.ndarray) else np.frombuffer(recs, dtype=np.uint8)
         self._check(self.lib.pv_process_host(self.ctx, buf.ctypes.data, buf.nbytes), "pv_process_host")
+
+    def process_dnstap(self, frames):
+        """pv_process_dnstap: a dnstap Frame Streams file's events through both handlers (the
+        DNS handler's dnstap_msg_type from dns_config)."""
+        buf = frames if isinstance(frames, np.ndarray) else np.frombuffer(frames, dtype=np.uint8)
+        self._check(self.lib.pv_process_dnstap(self.ctx, buf.ctypes.data, buf.nbytes, self.dnstap_mask),
+                    "pv_process_dnstap")
 
     def index_device(self, recs, max_records: Optional[int] = None, max_changes: int = 1 << 16):
         """pv_index_records_device: the record index of one block computed on the device;

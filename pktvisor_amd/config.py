@@ -42,6 +42,9 @@ DNS_GROUP_DEFS = {"cardinality": 1 << 0, "counters": 1 << 1, "dns_transaction": 
 NET_DEFAULT_GROUPS = ("counters", "cardinality", "top_geo", "top_ips")
 DNS_DEFAULT_GROUPS = ("cardinality", "counters", "quantiles", "dns_transaction", "top_qnames", "top_ports")
 DNSTAP_MSG_TYPES = ("auth", "client", "forwarder", "resolver", "stub", "tool", "update")
+# dnstap Message.Type numbers of each dnstap_msg_type (DnsStreamHandler.h:340-347; dnstap.proto:160-227)
+DNSTAP_TYPE_PAIRS = {"auth": (1, 2), "resolver": (3, 4), "client": (5, 6), "forwarder": (7, 8), "stub": (9, 10),
+                     "tool": (11, 12), "update": (13, 14)}
 GROUPS_SET = 0x80000000  # PV_GROUPS_SET
 
 
@@ -214,4 +217,8 @@ def dns_start(cfg: dict) -> dict:
         ttl = _uint(cfg, "xact_ttl_ms")
     elif "xact_ttl_secs" in cfg:
         ttl = _uint(cfg, "xact_ttl_secs") * 1000
-    return {"groups": groups | GROUPS_SET, "filters": filters, "xact_ttl_ms": ttl}
+    mask = 0
+    if "dnstap_msg_type" in cfg:
+        q, r = DNSTAP_TYPE_PAIRS[cfg["dnstap_msg_type"]]
+        mask = (1 << q) | (1 << r)
+    return {"groups": groups | GROUPS_SET, "filters": filters, "xact_ttl_ms": ttl, "dnstap_mask": mask}

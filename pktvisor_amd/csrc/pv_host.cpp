@@ -38,6 +38,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <memory>
+
+#include "pv_dnstap.h"
 #include <thread>
 
 #include "../../include/pvgpu.h"
@@ -101,6 +103,7 @@ extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, con
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
                                           uint32_t *vout, size_t n, hipStream_t s);
 extern "C" __global__ void pv_dns_tcp(const PvParams *P);
+extern "C" __global__ void pv_dnstap_kernel(const PvParams *P);
 extern "C" __global__ void pv_tcp_keys(const PvTcpSeg *seg, uint32_t n, uint64_t *key, uint32_t *val);
 extern "C" __global__ void pv_tcp_scan(const PvTcpParams *T);
 extern "C" __global__ void pv_tcp_lookup(const PvTcpParams *T);
@@ -2548,6 +2551,198 @@ int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int6
         pos += used;
     }
     *n = k;
+    return 0;
+}
+
+// dnstap input (DnstapInputStream, src/inputs/dnstap/DnstapInputStream.cpp:33-92) into the Net
+// and DNS handlers' process_dnstap paths (net/v1 NetStreamHandler.cpp:549-620,832-843;
+// dns/v1 DnsStreamHandler.cpp:260-266,839-909,1376-1412). The host decodes the Frame Streams
+// file (pv_dnstap.cpp) and lays each event out as a PvDtEv plus a linktype-101 record (IP
+// header with the query / response addresses, UDP header, the DNS message); the managers'
+// period shifts are applied between spans of events; pv_dnstap_kernel does the accounting.
+int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_type_mask)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (c->net2_groups || c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "dnstap input with the v2 handlers is not built");
+    std::vector<pvi::DtMessage> msgs;
+    uint32_t frames = 0;
+    pvi::dnstap_decode(buf, bytes, msgs, &frames);
+    const size_t n = msgs.size();
+    if (n == 0) return 0;
+    if (n > 0x3fffffffull) return c->fail(PV_ECAPACITY, "too many dnstap events in one call");
+    std::vector<PvDtEv> ev(n);
+    std::vector<uint32_t> offs(n);
+    std::vector<int64_t> ssec(n), snsec(n);
+    std::vector<uint8_t> arena;
+    arena.reserve(n * 96 + bytes);
+    timespec now{};
+    for (size_t j = 0; j < n; j++) {
+        const pvi::DtMessage &m = msgs[j];
+        PvDtEv &e = ev[j];
+        memset(&e, 0, sizeof e);
+        const uint32_t t = m.type;
+        // the event's timestamp (DnsMetricsManager::process_dnstap :1379-1402): the response
+        // time for CLIENT/AUTH/RESOLVER responses, the query time for their queries, else now
+        // (also when that time is absent, where the reference leaves the stamp unset)
+        int64_t sec = -1, nsec = 0;
+        if ((t == 6 || t == 2 || t == 4) && m.has_rsec) { sec = (int64_t)m.rsec; nsec = m.rnsec; }
+        else if ((t == 5 || t == 1 || t == 3) && m.has_qsec) { sec = (int64_t)m.qsec; nsec = m.qnsec; }
+        if (sec < 0) {
+            if (!now.tv_sec) timespec_get(&now, TIME_UTC);
+            sec = now.tv_sec;
+            nsec = now.tv_nsec;
+        }
+        ssec[j] = sec;
+        snsec[j] = nsec;
+        e.sec = (uint32_t)sec;
+        e.nsec = (uint32_t)nsec;
+        e.size = m.frame_len;
+        // Net direction by message type (net/v1 :578-597)
+        switch (t) {
+        case 5: case 10: case 4: case 1: case 8: case 13: case 12: e.dir = 0; break;
+        case 9: case 6: case 3: case 2: case 7: case 14: case 11: e.dir = 1; break;
+        default: e.dir = 2;
+        }
+        e.side = (t >= 1 && t <= 14 && (t & 1) == 0) ? 1 : 0; // responses have even type numbers
+        e.l3 = m.has_family ? (m.family == 2 ? 6 : (m.family == 1 ? 4 : 0)) : 0;
+        e.l4 = m.has_protocol ? (m.protocol == 1 ? 17 : (m.protocol == 2 ? 6 : 0)) : 0;
+        e.qport = m.has_qport ? (uint16_t)m.qport : 0;
+        e.filtered = (msg_type_mask && !((msg_type_mask >> t) & 1)) ? 1 : 0;
+        const uint8_t *msg = nullptr;
+        size_t mlen = 0;
+        if (!m.has_qmsg && !m.has_rmsg) e.dns_mode = PV_DT_SIDE;
+        else if (e.side == 0 && m.has_qmsg) { e.dns_mode = PV_DT_MESSAGE; msg = m.qmsg; mlen = m.qmsg_len; }
+        else if (e.side == 1 && m.has_rmsg) { e.dns_mode = PV_DT_MESSAGE; msg = m.rmsg; mlen = m.rmsg_len; }
+        else e.dns_mode = PV_DT_EVENT_ONLY;
+        if (mlen > 65535 - 48) mlen = 65535 - 48; // a DNS message fits 16 bits (TCP framing)
+        e.qlen = m.has_qaddr ? (uint8_t)std::min<size_t>(m.qaddr.size(), 255) : 0;
+        e.rlen = m.has_raddr ? (uint8_t)std::min<size_t>(m.raddr.size(), 255) : 0;
+        if (e.qlen == 4 || e.qlen == 16) memcpy(e.qaddr, m.qaddr.data(), e.qlen);
+        if (e.rlen == 4 || e.rlen == 16) memcpy(e.raddr, m.raddr.data(), e.rlen);
+        // the record: pcap header, IPv4 (or IPv6) header, UDP header, message
+        const bool v6 = e.l3 == 6;
+        const uint32_t iph = v6 ? 40 : 20;
+        const uint32_t incl = iph + 8 + (uint32_t)mlen;
+        const size_t r = arena.size();
+        arena.resize(r + ((16 + incl + 3) & ~3u), 0);
+        uint8_t *h = arena.data() + r;
+        const uint32_t hw[4] = {(uint32_t)sec, c->cfg.ts_nano ? (uint32_t)nsec : (uint32_t)(nsec / 1000), incl, incl};
+        memcpy(h, hw, 16);
+        uint8_t *ip = h + 16;
+        const uint32_t udp_len = 8 + (uint32_t)mlen;
+        if (v6) {
+            ip[0] = 0x60;
+            ip[4] = (uint8_t)(udp_len >> 8); ip[5] = (uint8_t)udp_len;
+            ip[6] = 17; ip[7] = 64;
+            if (e.qlen == 16) memcpy(ip + 8, e.qaddr, 16);
+            if (e.rlen == 16) memcpy(ip + 24, e.raddr, 16);
+        } else {
+            const uint32_t tot = 20 + udp_len;
+            ip[0] = 0x45;
+            if (tot <= 65535) { ip[2] = (uint8_t)(tot >> 8); ip[3] = (uint8_t)tot; }
+            ip[8] = 64; ip[9] = 17;
+            if (e.qlen == 4) memcpy(ip + 12, e.qaddr, 4);
+            if (e.rlen == 4) memcpy(ip + 16, e.raddr, 4);
+        }
+        uint8_t *u = ip + iph;
+        u[0] = (uint8_t)(e.qport >> 8); u[1] = (uint8_t)e.qport;
+        u[2] = 0; u[3] = 53;
+        u[4] = (uint8_t)(udp_len >> 8); u[5] = (uint8_t)udp_len;
+        if (mlen) memcpy(u + 8, msg, mlen);
+        offs[j] = (uint32_t)r;
+        e.rec = (uint32_t)r;
+        e.moff = (uint32_t)(r + 16 + iph + 8);
+        e.mlen = (uint32_t)mlen;
+        if (arena.size() > 0xfffff000ull) return c->fail(PV_ECAPACITY, "dnstap events exceed 4 GiB of records");
+    }
+    arena.resize(arena.size() + PV_RECS_PAD, 0);
+    hipError_t e;
+    uint8_t *d_arena = nullptr;
+    uint32_t *d_offs = nullptr;
+    PvDtEv *d_ev = nullptr;
+    struct Free {
+        void *p[3];
+        ~Free() { for (void *q : p) if (q) hipFree(q); }
+    } fr{{nullptr, nullptr, nullptr}};
+    if (!hip_ok(e = hipMalloc(&d_arena, arena.size())) || !hip_ok(e = hipMalloc(&d_offs, n * 4)) ||
+        !hip_ok(e = hipMalloc(&d_ev, n * sizeof(PvDtEv))))
+        return c->hipfail(e, "dnstap buffers");
+    fr.p[0] = d_arena; fr.p[1] = d_offs; fr.p[2] = d_ev;
+    hipStream_t st = c->stream;
+    if (!hip_ok(e = hipMemcpyAsync(d_arena, arena.data(), arena.size(), hipMemcpyHostToDevice, st)) ||
+        !hip_ok(e = hipMemcpyAsync(d_offs, offs.data(), n * 4, hipMemcpyHostToDevice, st)) ||
+        !hip_ok(e = hipMemcpyAsync(d_ev, ev.data(), n * sizeof(PvDtEv), hipMemcpyHostToDevice, st)))
+        return c->hipfail(e, "dnstap H2D");
+    ensure_started(c, ssec[0], snsec[0]);
+    const uint32_t np = c->cfg.num_periods;
+    auto span = [&](size_t a, size_t b) -> int {
+        if (b <= a) return 0;
+        PvParams P;
+        params_common(c, P, d_arena, d_offs + a, b - a);
+        P.linktype = 101;
+        P.tap = 1;
+        P.f_flags = 0; // the DNS filters do not apply to dnstap events (only dnstap_msg_type)
+        P.dq = reinterpret_cast<uint64_t *>(d_ev + a);
+        P.gbase = c->global_base + c->records_seen;
+        P.slot_of[0] = c->net.slot_at(0);
+        P.dslot_of[0] = c->dns.slot_at(0);
+        P.sum = c->d_sum;
+        P.cpc = c->d_cpc;
+        P.tkeys = c->d_tkeys;
+        P.tcnt = c->d_tcnt;
+        P.taux = c->d_taux;
+        P.tcap_log2 = c->tcap_log2;
+        P.reg_log2 = c->reg_log2;
+        P.arena = c->d_arena;
+        P.arena_top = c->d_arena_top;
+        P.arena_cap = c->arena_cap;
+        P.flags = c->d_status + ST_FLAGS;
+        P.tab_live = c->d_tab_live;
+        P.want_events = 0;
+        launch_fill32(c, c->d_status + ST_FLAGS, 1, 0);
+        flush_fills(c);
+        *c->h_params = P;
+        if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
+            return c->hipfail(e, "parameter upload");
+        hipLaunchKernelGGL(pv_dnstap_kernel, dim3((uint32_t)((b - a + 255) / 256)), dim3(256), 0, st, (const PvParams *)c->d_params);
+        if (!hip_ok(e = hipGetLastError()) ||
+            !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipMemcpyAsync(c->h_tab_live, c->d_tab_live, PV_TABLES * 4, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "pv_dnstap_kernel");
+        const uint32_t flags = c->h_status[ST_FLAGS];
+        if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
+        if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
+        c->net.clean[P.slot_of[0]] = false;
+        c->dns.clean[P.dslot_of[0]] = false;
+        c->records_seen += b - a;
+        return purge_tables(c, st);
+    };
+    size_t a = 0;
+    for (size_t j = 0; j < n; j++) {
+        // each manager shifts on the first of its events at or after its next shift
+        // (AbstractMetricsManager::new_event, src/AbstractMetricsManager.h:318-333)
+        const bool ns = np > 1 && ssec[j] >= c->net.next_shift_sec;
+        const bool ds = np > 1 && ssec[j] >= c->dns.next_shift_sec;
+        if (!ns && !ds) continue;
+        if (int rc = span(a, j)) return rc;
+        if (ns) { clear_part(c, PART_NET, c->net.slot_at(1)); win_shift(c, c->net, ssec[j]); }
+        if (ds) { clear_part(c, PART_DNS, c->dns.slot_at(1)); win_shift(c, c->dns, ssec[j]); }
+        a = j;
+    }
+    if (int rc = span(a, n)) return rc;
+    c->last_sec = ssec[n - 1];
+    c->last_nsec = snsec[n - 1];
+    return 0;
+}
+
+// Frame Streams decode only (tests): data frames read and dnstap MESSAGE events found.
+int pv_dnstap_count(const uint8_t *buf, size_t bytes, uint32_t *frames, uint32_t *events)
+{
+    std::vector<pvi::DtMessage> msgs;
+    pvi::dnstap_decode(buf, bytes, msgs, frames);
+    *events = (uint32_t)msgs.size();
     return 0;
 }
 

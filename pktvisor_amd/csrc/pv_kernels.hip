@@ -189,6 +189,16 @@ __device__ __forceinline__ uint64_t ip6_name_addr(const A &R, const Parsed &o, u
     if (d != 2) return d == 0 ? o.v6 + 8 : o.v6 + 24;
     return v2_ip6_key(R, o.v6 + 8, 2) == key ? o.v6 + 8 : o.v6 + 24;
 }
+// the v1 top-N payload of a 16-byte address (net_ip_entry's IPv6 key)
+template <class A>
+__device__ __forceinline__ uint64_t v1_ip6_key(const A &R, uint64_t a)
+{
+    const uint64_t w0 = (uint64_t)R.u32(a) | ((uint64_t)R.u32(a + 4) << 32);
+    const uint64_t w1 = (uint64_t)R.u32(a + 8) | ((uint64_t)R.u32(a + 12) << 32);
+    uint64_t h1, h2;
+    murmur_16(w0, w1, h1, h2);
+    return (h1 ^ (h2 << 1)) & ((1ull << 55) - 1);
+}
 struct NameSrc {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
@@ -211,7 +221,8 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     unsigned long long *top = (unsigned long long *)&P.arena_top[tab * PV_ARENA_PARTS + part];
     uint8_t *arena = P.arena + (uint64_t)tab * P.arena_cap;
     if (metric == TM_IPV6) {
-        const uint64_t a = ip6_name_addr(R, o, key);
+        const uint64_t a = P.tap ? (v1_ip6_key(R, o.v6 + 8) == (key & ((1ull << 55) - 1)) ? o.v6 + 8 : o.v6 + 24)
+                                 : ip6_name_addr(R, o, key);
         uint64_t pos = atomicAdd(top, 20ull); // records are 4-byte multiples (pv_topn_names copies dwords)
         if (pos + 20 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
         pos += part * pcap;
@@ -579,7 +590,10 @@ __device__ __forceinline__ bool dns_predicates(PV_CREF(PvParams) P, const A &R, 
 // DnsMetricsBucket::process_dns_layer (:910-1049) + the transaction event of one DNS
 // message, in the bucket of its DNS period. Counters go to `c` when `own` (this lane's
 // DNS slot is the wave's register slot), else straight to HBM.
-template <bool TCP, class A, class Cache>
+// TAP: a dnstap event (DnsMetricsBucket::process_dnstap, :839-909): no filters, l3 / l4 from
+// the socket fields (flags bit 4: l3 unknown; bits 5-6: 0 UDP, 1 TCP, 2 other), the query
+// port as the port (top_udp_ports only when non-zero), no transaction event.
+template <bool TCP, bool TAP = false, class A, class Cache>
 __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, uint32_t *nev,
                                             uint32_t *nresp, uint64_t ebase, const A &R, const DnsMsg &dm, bool own,
                                             DnsCtr &c)
@@ -602,8 +616,8 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     uint32_t sfx = 0; // only_qname_suffix's suffix_size for aggregateDomain
     // a message's order in the span: record * 4 (+ sub for a TCP message), for the CPC
     // first-occurrence index and the transaction sort rank
-    const uint32_t ordr = TCP ? dm.pad - P.ord_base : (i << 2);
-    if (P.f_flags) {
+    const uint32_t ordr = (TCP || TAP) ? dm.pad - P.ord_base : (i << 2);
+    if (P.f_flags && !TAP) {
         // a TCP message takes no input predicate: _filtering applies only_rcode and only_qname
         // to it as ordinary filters (_predicate_filter_type stays FiltersMAX, :546-551,593-602)
         if (!TCP && (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
@@ -655,7 +669,9 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         }
     };
     if (upd) {
-        const uint32_t d4 = !(dm.flags & 4), d6 = (dm.flags & 4) ? 1 : 0;
+        const uint32_t l3u = TAP && (dm.flags & 16);
+        const uint32_t d4 = !(dm.flags & 4) && !l3u, d6 = (dm.flags & 4) ? 1 : 0;
+        const uint32_t l4c = TAP ? (dm.flags >> 5) & 3 : (TCP ? 1u : 0u); // 0 UDP, 1 TCP, 2 other
         if (own) {
             c.dev++;
             c.d4 += d4; c.d6 += d6;
@@ -668,8 +684,8 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
             if (dc) {
                 sum_add(P, slot, PV_OFF_DNS + DC_TOTAL, 1);
-                sum_add(P, slot, PV_OFF_DNS + (TCP ? DC_TCP : DC_UDP), 1);
-                sum_add(P, slot, PV_OFF_DNS + (d6 ? DC_V6 : DC_V4), 1);
+                if (l4c < 2) sum_add(P, slot, PV_OFF_DNS + (l4c ? DC_TCP : DC_UDP), 1);
+                if (d4 | d6) sum_add(P, slot, PV_OFF_DNS + (d6 ? DC_V6 : DC_V4), 1);
                 sum_add(P, slot, PV_OFF_DNS + (qr ? DC_REPLIES : DC_QUERIES), 1);
                 if (qr && rcode == 0) sum_add(P, slot, PV_OFF_DNS + DC_NOERROR, 1);
                 if (qr && rcode == 0 && ancount == 0) sum_add(P, slot, PV_OFF_DNS + DC_NODATA, 1);
@@ -682,7 +698,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
         // client ports spread over 64 K values and rarely repeat inside a workgroup: a
         // no-return HBM atomic on the dense table, not an LDS cache probe (boundary: as before)
-        if (P.dns_groups & PV_DNS_TOP_PORTS_BIT) {
+        if ((P.dns_groups & PV_DNS_TOP_PORTS_BIT) && (!TAP || dm.port)) {
             if (cache && !(P.dbg & 32)) sum_add(P, slot, PV_OFF_PORT + (dm.port & 0xffff), 1);
             else top(TM_DENSE_PORT, dm.port, 1);
         }
@@ -737,7 +753,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             }
         }
     }
-    if (P.want_events) {
+    if (P.want_events && !TAP) {
         // the workgroup's event region; LDS counter, order irrelevant (sorted by key, index)
         const uint64_t e = ebase + atomicAdd(nev, 1u);
         if (qr) atomicAdd(nresp, 1u);
@@ -2354,6 +2370,92 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp(const PvParams *__r
     if (threadIdx.x == 0) {
         P.blk_events[P.grid_main + blockIdx.x] = nev;
         if (nresp) atomicAdd(P.n_events + 1, nresp);
+    }
+}
+
+// ------------------------------------------------------------------ dnstap events
+// One lane per dnstap event, in the bucket of the span's period (spans hold no shift): the
+// Net handler's NetworkMetricsBucket::process_dnstap (net/v1 ...cpp:549-620: direction by
+// message type, l3 / l4 from the socket fields, the frame length as the payload size, the
+// query address as "in" and the response address as "out", no SYN) and the DNS handler's
+// DnsMetricsManager / DnsMetricsBucket::process_dnstap (dns/v1 ...cpp:839-909,1376-1412:
+// dnstap_msg_type filter, counters by side without a message, else process_dns_layer on the
+// message). Events are few next to packets: counters and tables are updated in HBM directly.
+extern "C" __global__ void __launch_bounds__(256) pv_dnstap_kernel(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.n) return;
+    const PvDtEv e = reinterpret_cast<const PV_G PvDtEv *>(P.dq)[j];
+    const GAcc R{P.recs};
+    const uint64_t gidx = P.gbase + j;
+    // ---- Net v1
+    {
+        const uint32_t s = P.slot_of[0];
+        sum_add(P, s, PV_OFF_NET + NC_EVENTS, 1);
+        sum_add(P, s, PV_OFF_NET + NC_SAMPLES, 1);
+        if (P.net_groups & PV_NET_COUNTERS_BIT) {
+            sum_add(P, s, PV_OFF_NET + NC_TOTAL, 1);
+            sum_add(P, s, PV_OFF_NET + (e.dir == 0 ? NC_IN : (e.dir == 1 ? NC_OUT : NC_UNK)), 1);
+            if (e.l3) sum_add(P, s, PV_OFF_NET + (e.l3 == 4 ? NC_V4 : NC_V6), 1);
+            sum_add(P, s, PV_OFF_NET + (e.l4 == 17 ? NC_UDP : (e.l4 == 6 ? NC_TCP : NC_OTHER)), 1);
+        }
+        sum_add(P, s, PV_OFF_PAYLOAD + min(e.size, 65535u), 1);
+        const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
+        for (int side = 0; side < 2; side++) {
+            const uint8_t *a = side ? e.raddr : e.qaddr;
+            const uint32_t alen = side ? e.rlen : e.qlen;
+            const uint32_t sketch = side ? CPC_DST : CPC_SRC;
+            if (e.l3 == 4 && alen == 4) {
+                const uint32_t ip = (uint32_t)a[0] | ((uint32_t)a[1] << 8) | ((uint32_t)a[2] << 16) | ((uint32_t)a[3] << 24);
+                if (!ip) continue;
+                if (card) cpc_min(P, s, sketch, ip4_coupon(ip), (int64_t)gidx);
+                if (tops) global_add(P, s, PV_KEY(TM_IPV4, ip), 1, j);
+            } else if (e.l3 == 6 && alen == 16) {
+                uint64_t w0 = 0, w1 = 0;
+                for (int b = 0; b < 8; b++) { w0 |= (uint64_t)a[b] << (8 * b); w1 |= (uint64_t)a[8 + b] << (8 * b); }
+                if (!(w0 | w1)) continue;
+                uint64_t h1, h2;
+                murmur_16(w0, w1, h1, h2);
+                if (card) cpc_min(P, s, sketch, cpc_coupon(h1, h2), (int64_t)gidx);
+                if (tops) global_add(P, s, PV_KEY(TM_IPV6, (h1 ^ (h2 << 1)) & ((1ull << 55) - 1)), 1, j);
+            }
+        }
+    }
+    // ---- DNS v1
+    {
+        const uint32_t s = P.dslot_of[0];
+        const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
+        if (e.filtered || e.dns_mode != PV_DT_MESSAGE) {
+            sum_add(P, s, PV_OFF_DNS + DC_EVENTS, 1);
+            sum_add(P, s, PV_OFF_DNS + DC_SAMPLES, 1);
+            if (e.filtered) {
+                if (dc) sum_add(P, s, PV_OFF_DNS + DC_FILTERED, 1);
+            } else if (e.dns_mode == PV_DT_SIDE && dc) {
+                // process_dns_layer(l3, l4, side) (:1051-1091)
+                sum_add(P, s, PV_OFF_DNS + DC_TOTAL, 1);
+                if (e.l3) sum_add(P, s, PV_OFF_DNS + (e.l3 == 6 ? DC_V6 : DC_V4), 1);
+                if (e.l4 == 17 || e.l4 == 6) sum_add(P, s, PV_OFF_DNS + (e.l4 == 6 ? DC_TCP : DC_UDP), 1);
+                sum_add(P, s, PV_OFF_DNS + (e.side ? DC_REPLIES : DC_QUERIES), 1);
+            }
+            return;
+        }
+        DnsMsg dm;
+        dm.idx = j;
+        dm.moff = e.moff;
+        dm.mlen = (uint16_t)min(e.mlen, 65535u);
+        dm.mcap = dm.mlen;
+        dm.port = e.qport;
+        dm.flags = (uint8_t)(8u | (e.l3 == 6 ? 4u : 0u) | (e.l3 == 0 ? 16u : 0u) |
+                             ((e.l4 == 17 ? 0u : (e.l4 == 6 ? 1u : 2u)) << 5));
+        dm.period = 0;
+        dm.fkey = 0;
+        dm.sec = e.sec;
+        dm.nsec = e.nsec;
+        dm.pad = j << 2;
+        DnsCtr c;
+        c.zero();
+        dns_process<false, true>(P, (KeyCache<PV_NCACHE> *)nullptr, nullptr, nullptr, nullptr, 0, R, dm, false, c);
     }
 }
 

@@ -287,6 +287,30 @@ struct PvSubnets {
 enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
        PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64, PVDF_ONLY_QSUFFIX = 128,
        PVDF_ONLY_DNSSEC = 256, PVDF_FILTER_ALL = 512 };
+// One dnstap event for pv_dnstap_kernel (DnstapInputStream -> process_dnstap_cb of the Net
+// and DNS handlers): the fields both handlers read, and the record (linktype 101: IPv4 or IPv6
+// header with the query / response addresses, UDP header, the DNS message) write_name parses.
+enum { PV_DT_EVENT_ONLY = 0, PV_DT_SIDE = 1, PV_DT_MESSAGE = 2 };
+struct PvDtEv {
+    uint32_t rec;      // record offset in the event arena
+    uint32_t moff;     // absolute offset of the DNS message
+    uint32_t mlen;     // DNS message bytes (PV_DT_MESSAGE)
+    uint32_t size;     // protobuf frame length (the Net handler's payload size)
+    uint32_t sec, nsec;
+    uint16_t qport;
+    uint8_t dir;       // Net: 0 toHost, 1 fromHost, 2 unknown (by message type)
+    uint8_t l3;        // 0 unknown, 4, 6 (socket_family)
+    uint8_t l4;        // 17, 6, 0 other (socket_protocol)
+    uint8_t dns_mode;  // PV_DT_*
+    uint8_t side;      // 0 query, 1 response (by message type)
+    uint8_t filtered;  // dnstap_msg_type filter
+    uint8_t qlen, rlen; // query / response address bytes (4, 16, else unusable)
+    uint8_t pad[2];
+    uint8_t qaddr[16], raddr[16];
+    uint8_t pad2[12];
+};
+static_assert(sizeof(PvDtEv) == 80, "PvDtEv is five 16-B words");
+
 struct PvParams {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
@@ -381,6 +405,7 @@ struct PvParams {
     // holds the messages; a message's order in the batch is ord = record * 4 + sub
     uint32_t tcp_pass, tcp_nmsg;
     uint32_t ord_lo, ord_hi, ord_base; // this span's messages: ord in [ord_lo, ord_hi); ord_base = span start * 4
+    uint32_t tap; // dnstap events (pv_dnstap_kernel): IPv6 top-N names take the address the key hashes
     uint32_t dpos[PV_MAX_SHIFTS];      // span-relative ord of the event that shifts DNS period k+1
 };
 

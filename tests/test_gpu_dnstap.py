@@ -1,0 +1,77 @@
+"""dnstap input (pv_process_dnstap) against the reference's own dnstap KATs on its fixture
+(tests/golden/fixture.dnstap = src/inputs/dnstap/tests/fixtures/fixture.dnstap):
+src/handlers/dns/v1/tests/test_dnstap.cpp:12-151 and
+src/handlers/net/v1/tests/test_net_layer.cpp:324-361."""
+import os
+
+import pytest
+
+import pktvisor_amd as pa
+from tests.oracle_ctypes import jget
+
+pytestmark = pytest.mark.gpu
+FIX = os.path.join(os.path.dirname(__file__), "golden", "fixture.dnstap")
+
+
+def run(dns_config=None):
+    return pa.dnstap_reader(FIX, periods=1, net_config={}, dns_config=dns_config or {})
+
+
+def test_dns_dnstap_kat():
+    """test_dnstap.cpp:12-63 "Parse DNSTAP" """
+    out = run()
+    want = {"events": 153, "deep_samples": 153, "tcp": 0, "udp": 153, "ipv4": 153, "ipv6": 0, "queries": 79,
+            "replies": 74, "noerror": 70, "nxdomain": 0, "refused": 0, "srvfail": 4, "filtered": 0}
+    for k, v in want.items():
+        assert jget(out, "1m.dns.wire_packets." + k) == v, k
+    for k in ("total", "in.total", "out.total"):
+        assert jget(out, "1m.dns.xact." + ("counts." + k if k == "total" else k)) == 0, k
+    assert jget(out, "1m.dns.xact.counts.timed_out") == 0
+    assert jget(out, "1m.dns.cardinality.qname") == 70
+    assert jget(out, "1m.dns.top_qname2.0.name") == ".google.com"
+    assert jget(out, "1m.dns.top_qname2.0.estimate") == 18
+    assert jget(out, "1m.dns.top_udp_ports.0.name") == "33000"
+    assert jget(out, "1m.dns.top_udp_ports.0.estimate") == 4
+    assert jget(out, "1m.dns.top_qtype.0.name") == "A"
+    assert jget(out, "1m.dns.top_qtype.0.estimate") == 149
+    assert jget(out, "1m.dns.top_qtype.1.name") == "HTTPS"
+    assert jget(out, "1m.dns.top_qtype.1.estimate") == 4
+
+
+def test_dns_dnstap_filtered_empty():
+    """test_dnstap.cpp:65-101: dnstap_msg_type "auth" filters every (client) message"""
+    out = run({"dnstap_msg_type": "auth"})
+    assert jget(out, "1m.dns.wire_packets.events") == 153
+    assert jget(out, "1m.dns.wire_packets.deep_samples") == 153
+    for k in ("tcp", "udp", "ipv4", "ipv6", "queries", "replies", "noerror", "nxdomain", "refused", "srvfail"):
+        assert jget(out, "1m.dns.wire_packets." + k) == 0, k
+    assert jget(out, "1m.dns.wire_packets.filtered") == 153
+
+
+def test_dns_dnstap_filtered_with_data():
+    """test_dnstap.cpp:103-151: dnstap_msg_type "client" keeps them"""
+    out = run({"dnstap_msg_type": "client"})
+    want = {"events": 153, "deep_samples": 153, "tcp": 0, "udp": 153, "ipv4": 153, "ipv6": 0, "queries": 79,
+            "replies": 74, "noerror": 70, "srvfail": 4, "filtered": 0}
+    for k, v in want.items():
+        assert jget(out, "1m.dns.wire_packets." + k) == v, k
+
+
+def test_net_dnstap_kat():
+    """test_net_layer.cpp:324-361 "Parse net dnstap stream" """
+    out = run()
+    want = {"events": 153, "deep_samples": 153, "tcp": 0, "udp": 153, "ipv4": 153, "ipv6": 0, "in": 79,
+            "out": 74, "protocol.tcp.syn": 0}
+    for k, v in want.items():
+        assert jget(out, "1m.packets." + k) == v, k
+    assert jget(out, "1m.packets.cardinality.dst_ips_out") == 1
+    assert jget(out, "1m.packets.cardinality.src_ips_in") == 1
+    assert jget(out, "1m.packets.top_ipv4.0.name") == "192.168.0.54"
+    assert jget(out, "1m.packets.top_ipv4.0.estimate") == 153
+    assert jget(out, "1m.packets.payload_size.p50") == 100
+
+
+def test_dnstap_invalid_msg_type():
+    with pytest.raises(Exception, match="dnstap_msg_type contained an invalid/unsupported type. Valid types: auth, "
+                                        "client, forwarder, resolver, stub, tool, update"):
+        run({"dnstap_msg_type": "bogus"})
