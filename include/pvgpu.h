@@ -213,6 +213,15 @@ int pv_process_dnstap(pv_ctx *ctx, const uint8_t *frames, size_t bytes, uint32_t
 /* Frame Streams decode only: data frames read and dnstap MESSAGE events in them. */
 int pv_dnstap_count(const uint8_t *frames, size_t bytes, uint32_t *n_frames, uint32_t *n_events);
 
+/* pcapng capture (PcapInputStream opens "pcap or pcapng", PcapInputStream.cpp:475-481, via
+ * PcapPlusPlus / LightPcapNg) -> classic pcap records with nanosecond fractions (feed them
+ * with pv_config.ts_nano = 1): Enhanced, Simple and obsolete Packet blocks of every section,
+ * timestamps in each interface's if_tsresol units. All interfaces must share one linktype
+ * (*linktype; PV_EUNSUPPORTED otherwise). out == NULL: sizes only; PV_ECAPACITY if out_cap is
+ * too small; PV_EINVAL for a malformed file. Host function, no context. */
+int pv_pcapng_records(const uint8_t *buf, size_t bytes, uint8_t *out, size_t out_cap, size_t *out_bytes,
+                      uint32_t *linktype, uint64_t *n_records);
+
 /* Page-lock a host range so pv_process_host DMAs from it directly (hipHostRegister). */
 int pv_host_register(void *ptr, size_t bytes);
 int pv_host_unregister(void *ptr);

@@ -159,7 +159,8 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_host_unregister", "pv_ingest_timing", "pv_edge_export", "pv_edge_merge", "pv_values_export",
            "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code", "pv_advance_windows",
            "pv_dns_event_seconds", "pv_dns_event_seconds_host", "pv_comm_unique_id", "pv_comm_init",
-           "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count"]
+           "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count",
+           "pv_pcapng_records"]
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
 
@@ -227,6 +228,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_comm_allgather.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), P]
     lib.pv_comm_destroy.argtypes = [P]
     lib.pv_process_dnstap.argtypes = [P, P, ctypes.c_size_t, U32]
+    lib.pv_pcapng_records.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.POINTER(U32), ctypes.POINTER(U64)]
     lib.pv_dnstap_count.argtypes = [P, ctypes.c_size_t, ctypes.POINTER(U32), ctypes.POINTER(U32)]
     _lib = lib
     return lib
@@ -246,10 +249,30 @@ def device_count() -> int:
     return n.value
 
 
+def pcapng_records(data: bytes):
+    """pcapng bytes -> (linktype, classic pcap records with nanosecond fractions) (pv_pcapng_records)."""
+    lib = load_library()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    nb, lt, nr = ctypes.c_size_t(0), ctypes.c_uint32(0), ctypes.c_uint64(0)
+    rc = lib.pv_pcapng_records(buf.ctypes.data, buf.nbytes, None, 0, ctypes.byref(nb), ctypes.byref(lt), ctypes.byref(nr))
+    if rc:
+        raise PvError("Cannot open pcap/pcapng file" + (" (interfaces with different linktypes)" if rc == -7 else ""))
+    out = np.empty(nb.value, dtype=np.uint8)
+    rc = lib.pv_pcapng_records(buf.ctypes.data, buf.nbytes, out.ctypes.data, out.nbytes, ctypes.byref(nb),
+                               ctypes.byref(lt), ctypes.byref(nr))
+    if rc:
+        raise PvError(f"pv_pcapng_records failed ({rc})")
+    return lt.value, out.tobytes()
+
+
 def read_pcap(path: str):
-    """Classic pcap file -> (linktype, ts_nano, record bytes after the 24-byte global header)."""
+    """pcap or pcapng file -> (linktype, ts_nano, record bytes): classic pcap records after the
+    24-byte global header, or a pcapng file's packets as records with ns fractions (ts_nano 1)."""
     with open(path, "rb") as f:
         data = f.read()
+    if len(data) >= 12 and struct.unpack_from("<I", data, 0)[0] == 0x0A0D0D0A:
+        lt, recs = pcapng_records(data)
+        return lt, 1, recs
     if len(data) < 24:
         raise PvError("Cannot open pcap/pcapng file")
     magic = struct.unpack_from("<I", data, 0)[0]

@@ -40,6 +40,7 @@
 #include <memory>
 
 #include "pv_dnstap.h"
+#include "pv_pcapng.h"
 #include <thread>
 
 #include "../../include/pvgpu.h"
@@ -2734,6 +2735,22 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
     if (int rc = span(a, n)) return rc;
     c->last_sec = ssec[n - 1];
     c->last_nsec = snsec[n - 1];
+    return 0;
+}
+
+// pcapng -> classic pcap records with nanosecond fractions (pv_pcapng.cpp). out == NULL (or too
+// small): only *out_bytes / *n_records are set (PV_ECAPACITY when out is too small).
+int pv_pcapng_records(const uint8_t *buf, size_t bytes, uint8_t *out, size_t out_cap, size_t *out_bytes,
+                      uint32_t *linktype, uint64_t *n_records)
+{
+    std::vector<uint8_t> v;
+    const int rc = pvi::pcapng_to_records(buf, bytes, &v, linktype, n_records);
+    if (rc == pvi::PVNG_ELINKTYPES) return PV_EUNSUPPORTED;
+    if (rc) return PV_EINVAL;
+    *out_bytes = v.size();
+    if (!out) return 0;
+    if (out_cap < v.size()) return PV_ECAPACITY;
+    memcpy(out, v.data(), v.size());
     return 0;
 }
 
