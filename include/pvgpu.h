@@ -222,6 +222,16 @@ int pv_dnstap_count(const uint8_t *frames, size_t bytes, uint32_t *n_frames, uin
 int pv_pcapng_records(const uint8_t *buf, size_t bytes, uint8_t *out, size_t out_cap, size_t *out_bytes,
                       uint32_t *linktype, uint64_t *n_records);
 
+/* AF_PACKET TPACKET_V3 ingest: one ring block the kernel handed to user space (the block
+ * walk of AFPacket::walk_block, src/inputs/pcap/afpacket.cpp:72-86) -> classic pcap records
+ * with nanosecond fractions appended at out + *out_bytes (*out_bytes advanced, *n_records
+ * incremented), for pv_process_host (pv_config.ts_nano = 1, linktype 1). Every packet takes
+ * the block's ts_last_pkt, as the reference's RawPacket does (:81). The socket, ring mmap and
+ * poll loop stay the caller's (CAP_NET_RAW). PV_EINVAL: a malformed block; PV_ECAPACITY: out
+ * is full (nothing of this block's remaining packets is appended past out_cap). */
+int pv_tpacket3_block_records(const uint8_t *block, size_t block_size, uint8_t *out, size_t out_cap, size_t *out_bytes,
+                              uint64_t *n_records);
+
 /* Page-lock a host range so pv_process_host DMAs from it directly (hipHostRegister). */
 int pv_host_register(void *ptr, size_t bytes);
 int pv_host_unregister(void *ptr);

@@ -160,7 +160,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code", "pv_advance_windows",
            "pv_dns_event_seconds", "pv_dns_event_seconds_host", "pv_comm_unique_id", "pv_comm_init",
            "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count",
-           "pv_pcapng_records"]
+           "pv_pcapng_records", "pv_tpacket3_block_records"]
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
 
@@ -228,6 +228,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_comm_allgather.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), P]
     lib.pv_comm_destroy.argtypes = [P]
     lib.pv_process_dnstap.argtypes = [P, P, ctypes.c_size_t, U32]
+    lib.pv_tpacket3_block_records.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                              ctypes.POINTER(U64)]
     lib.pv_pcapng_records.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                       ctypes.POINTER(U32), ctypes.POINTER(U64)]
     lib.pv_dnstap_count.argtypes = [P, ctypes.c_size_t, ctypes.POINTER(U32), ctypes.POINTER(U32)]
@@ -280,6 +282,20 @@ def read_pcap(path: str):
         raise PvError("Cannot open pcap/pcapng file (only little-endian classic pcap is supported)")
     linktype = struct.unpack_from("<I", data, 20)[0]
     return linktype, int(magic == 0xA1B23C4D), data[24:]
+
+
+def tpacket3_records(blocks, out_cap: int = 1 << 26) -> bytes:
+    """TPACKET_V3 ring blocks (bytes each) -> pcap records with ns fractions (pv_tpacket3_block_records)."""
+    lib = load_library()
+    out = np.empty(out_cap, dtype=np.uint8)
+    used, n = ctypes.c_size_t(0), ctypes.c_uint64(0)
+    for b in blocks:
+        buf = np.frombuffer(b, dtype=np.uint8)
+        rc = lib.pv_tpacket3_block_records(buf.ctypes.data, buf.nbytes, out.ctypes.data, out.nbytes, ctypes.byref(used),
+                                           ctypes.byref(n))
+        if rc:
+            raise PvError(f"pv_tpacket3_block_records failed ({rc})")
+    return out[: used.value].tobytes()
 
 
 def dnstap_count(frames: bytes):

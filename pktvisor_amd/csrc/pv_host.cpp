@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <array>
 #include <arpa/inet.h>
+#include <linux/if_packet.h>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -2751,6 +2752,40 @@ int pv_pcapng_records(const uint8_t *buf, size_t bytes, uint8_t *out, size_t out
     if (!out) return 0;
     if (out_cap < v.size()) return PV_ECAPACITY;
     memcpy(out, v.data(), v.size());
+    return 0;
+}
+
+// One TPACKET_V3 ring block (AFPacket::walk_block, src/inputs/pcap/afpacket.cpp:72-86) ->
+// classic pcap records with nanosecond fractions, appended at out + *out_bytes. As the
+// reference hands them on, every packet takes the block's ts_last_pkt (not its own tp_sec /
+// tp_nsec) and its snap length as both lengths (RawPacket(data, tp_snaplen, ...)).
+int pv_tpacket3_block_records(const uint8_t *block, size_t block_size, uint8_t *out, size_t out_cap, size_t *out_bytes,
+                              uint64_t *n_records)
+{
+    if (block_size < sizeof(tpacket_block_desc)) return PV_EINVAL;
+    const tpacket_block_desc *bd = reinterpret_cast<const tpacket_block_desc *>(block);
+    const tpacket_hdr_v1 &h = bd->hdr.bh1;
+    const uint32_t ts_sec = h.ts_last_pkt.ts_sec, ts_nsec = h.ts_last_pkt.ts_nsec;
+    size_t o = *out_bytes;
+    uint64_t n = 0;
+    size_t p = h.offset_to_first_pkt;
+    for (uint32_t i = 0; i < h.num_pkts; i++) {
+        if (p + sizeof(tpacket3_hdr) > block_size) return PV_EINVAL;
+        tpacket3_hdr ph;
+        memcpy(&ph, block + p, sizeof ph);
+        const size_t d = p + ph.tp_mac;
+        if (d + ph.tp_snaplen > block_size) return PV_EINVAL;
+        if (o + 16 + ph.tp_snaplen > out_cap) return PV_ECAPACITY;
+        const uint32_t rh[4] = {ts_sec, ts_nsec, ph.tp_snaplen, ph.tp_snaplen};
+        memcpy(out + o, rh, 16);
+        memcpy(out + o + 16, block + d, ph.tp_snaplen);
+        o += 16 + ph.tp_snaplen;
+        n++;
+        if (i + 1 < h.num_pkts && ph.tp_next_offset == 0) return PV_EINVAL;
+        p += ph.tp_next_offset;
+    }
+    *out_bytes = o;
+    if (n_records) *n_records += n;
     return 0;
 }
 

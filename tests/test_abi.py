@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     txt = open(os.path.join(ROOT, "include", "pvgpu.h")).read()
-    return sorted(set(re.findall(r"\b(pv_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(pv_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_matches_python_export_list():
