@@ -952,7 +952,7 @@ __device__ __forceinline__ uint64_t net_ip_entry(const NetK &K, const A &R, cons
 static_assert(PV_NL_SLOT % 1024 == 0, "whole DMA pieces");
 static_assert(PV_NL_SLOT / PV_WT >= 80, "window must cover Eth + IPv4 + UDP from a 16-B aligned start");
 
-struct NetWave {
+struct alignas(16) NetWave {
     uint32_t slot[PV_NL_Q][PV_NL_SLOT / 4];
     uint32_t lo[PV_NL_OROWS][PV_WT]; // each lane's record start
     uint32_t hi[PV_NL_OROWS][PV_WT]; // each lane's record end (the next start)
@@ -1043,14 +1043,37 @@ struct RecW {
         return (off & 3) ? __builtin_amdgcn_alignbyte(w[(off >> 2) + 1], w[off >> 2], off & 3) : w[off >> 2];
     }
 };
-__device__ __forceinline__ void recw_load(const uint32_t *L, uint32_t d0, uint32_t sh, bool packed, uint32_t lane4, RecW &r)
+// packed tile: the record's dwords are consecutive in the slot (one base address, immediate
+// offsets)
+__device__ __forceinline__ void recw_load_packed(const uint32_t *L, uint32_t d0, uint32_t sh, RecW &r)
 {
+    const uint32_t *p = L + d0;
     uint32_t x[17];
 #pragma unroll
-    for (int j = 0; j < 17; j++) {
-        const uint32_t d = d0 + j;
-        x[j] = L[packed ? d : ((d >> 2) << 8) + lane4 + (d & 3)];
+    for (int j = 0; j < 17; j++) x[j] = p[j];
+#pragma unroll
+    for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+}
+// window tile: the lane's 80-B window as five 16-B pieces (piece k at L[k * 256 + lane4]: lanes
+// contiguous, so each ds_read_b128 is conflict-free), then the record's dwords d0 .. d0 + 16
+// (d0 < 4) picked with two select levels
+__device__ __forceinline__ void recw_load_window(const uint32_t *L, uint32_t d0, uint32_t sh, uint32_t lane4, RecW &r)
+{
+    const uint4 *q = reinterpret_cast<const uint4 *>(L + lane4);
+    uint32_t w[20];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint4 v = q[k * 64];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
     }
+    // bit selects (v_bfi), not ternaries the compiler turns into a dynamically indexed
+    // (scratch) array
+    const uint32_t m0 = 0u - (d0 & 1), m1 = 0u - ((d0 >> 1) & 1);
+    uint32_t a[19], x[17];
+#pragma unroll
+    for (int j = 0; j < 19; j++) a[j] = (w[j + 1] & m0) | (w[j] & ~m0);
+#pragma unroll
+    for (int j = 0; j < 17; j++) x[j] = (a[j + 2] & m1) | (a[j] & ~m1);
 #pragma unroll
     for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
 }
@@ -1371,7 +1394,8 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
             bool fast = (rel >> 2) + 17 <= (R.lim + 4) >> 2;
             Parsed o;
             if (fast) {
-                recw_load(R.L, rel >> 2, rel & 3, packed, lane * 4, rw);
+                if (packed) recw_load_packed(R.L, rel >> 2, rel & 3, rw);
+                else recw_load_window(R.L, rel >> 2, rel & 3, lane * 4, rw);
                 fast = fast_parse(rw, C, P, off, o);
             }
             if (!fast) {
