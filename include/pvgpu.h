@@ -100,6 +100,10 @@ typedef struct pv_config {
     uint32_t dns2_groups;    /* DNS v2 handler ("dns", src/handlers/dns/v2) in place of v1: pv_dns2_group bits
                                 | PV_GROUPS_SET, or PV_NET2_ATTACH for its default groups; 0 = DNS v1. Its
                                 filters, top_ecs and multi-GPU edge replay are not built */
+    uint32_t deep_sample_rate; /* "deep_sample_rate" 1..100 (0 = 100): each manager draws jsf32() % 100 < rate
+                                  per event (AbstractMetricsManager::new_event, src/AbstractMetricsManager.h:318-333);
+                                  a non-deep event counts in the counters only. Below 100 not with DNS filters,
+                                  geo filters, the v2 handlers or DNS over TCP (PV_EUNSUPPORTED) */
 } pv_config;
 #define PV_NET2_ATTACH 0x40000000u
 

@@ -354,6 +354,7 @@ struct Config {
     uint32_t dns_groups = DG_CARDINALITY | DG_COUNTERS | DG_QUANTILES | DG_TRANSACTIONS | DG_TOP_QNAMES | DG_TOP_PORTS;
     uint32_t topn_pct = 0;   // topn_percentile_threshold
     bool net_filter_all = false; // net geo / ASN filters with no geo database: every packet filtered (:223-283)
+    unsigned deep_sample_rate = 100; // window config "deep_sample_rate" (AbstractMetricsManager.h:357-365), clamped 1..100
     // Net v2 handler attached ("net"): its groups (N2G_*), 0 = not attached
     uint32_t net2_groups = 0;
     // DNS v2 handler in place of v1 ("dns" is both versions' schema key): its groups (D2G_*), 0 = v1
@@ -985,6 +986,36 @@ struct Window {
     }
 };
 
+// jsf32 (3rd/rng/jsf.h:38-70,111,151: jsf<uint32_t, uint32_t, 27, 17, 0>, seed 1, 20 rounds)
+struct Jsf32 {
+    uint32_t a = 0xf1ea5eedu, b = 1, c = 1, d = 1;
+    Jsf32() { for (int i = 0; i < 20; i++) (*this)(); }
+    static uint32_t rot(uint32_t x, unsigned k) { return (x << k) | (x >> (32 - k)); }
+    uint32_t operator()()
+    {
+        uint32_t e = a - rot(b, 27);
+        a = b ^ rot(c, 17);
+        b = c + d;
+        c = d + e;
+        d = e + a;
+        return d;
+    }
+};
+
+// AbstractMetricsManager::new_event's sampling (src/AbstractMetricsManager.h:318-333): each
+// manager draws once per sampled event when the rate is not 100 and keeps the flag; an event
+// with sample=false (process_filtered) counts the stale flag
+struct Sampler {
+    Jsf32 rng;
+    unsigned rate = 100;
+    bool now = true;
+    bool draw(bool sample)
+    {
+        if (sample && rate != 100) now = rng() % 100u < rate;
+        return now;
+    }
+};
+
 struct XactKey {
     uint32_t flow;
     uint16_t txid;
@@ -1018,9 +1049,11 @@ struct Engine {
     float per90_2[3] = {0.0f, 0.0f, 0.0f};
     uint32_t ttl_s = 0, ttl_ms = 0;
     float to90 = 0.0f, from90 = 0.0f;
+    Sampler net_s, dns_s; // the Net and DNS managers' generators
 
     explicit Engine(const Config &c) : cfg(c), net(c.num_periods), net2(c.num_periods), dns(c.num_periods), dns2(c.num_periods)
     {
+        net_s.rate = dns_s.rate = c.deep_sample_rate;
         // TransactionManager.h:60-68
         if (c.xact_ttl_ms > 1000) { ttl_s = c.xact_ttl_ms / 1000; ttl_ms = c.xact_ttl_ms - ttl_s * 1000; }
         else ttl_ms = c.xact_ttl_ms;
@@ -1044,13 +1077,15 @@ struct Engine {
     // NetworkMetricsManager::process_packet + bucket (net/v1 ...cpp:516-548,682-764)
     void net_packet(const Pkt &p)
     {
+        const bool deep = net_s.draw(!cfg.net_filter_all);
         net.maybe_shift(p.ts);
-        net.new_event(true);
+        net.new_event(deep);
         NetBucket &b = net.live();
         if (cfg.net_filter_all) { // process_filtered (net/v1/NetStreamHandler.cpp:507-514)
             if (cfg.net_groups & NG_COUNTERS) b.filtered++;
             return;
         }
+        // not deep: process_net_layer(dir, l3, l4, size) — counters without SYN, payload size (:518-521,620-680)
         if (cfg.net_groups & NG_COUNTERS) {
             b.total++;
             if (p.dir == DIR_FROM_HOST) b.out++;
@@ -1059,10 +1094,11 @@ struct Engine {
             if (p.l3 == L3_IPV6) b.IPv6++;
             else if (p.l3 == L3_IPV4) b.IPv4++;
             if (p.l4 == L4_UDP) b.UDP++;
-            else if (p.l4 == L4_TCP) { b.TCP++; if (p.syn) b.TCP_SYN++; }
+            else if (p.l4 == L4_TCP) { b.TCP++; if (p.syn && deep) b.TCP_SYN++; }
             else b.OtherL4++;
         }
         b.payload.update(p.caplen);
+        if (!deep) return;
         const bool card = cfg.net_groups & NG_CARDINALITY, tops = cfg.net_groups & NG_TOP_IPS;
         if (p.has_v4) {
             uint32_t in = 0, out = 0;
@@ -1221,8 +1257,9 @@ struct Engine {
         }
         if (!filt && cfg.filter_all) filt = true;
         if (filt) {
+            const bool stale = dns_s.draw(false);
             if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
-            dns.new_event(true);
+            dns.new_event(stale);
             if (cfg.dns_groups & DG_COUNTERS) dns.live().filtered++;
             return;
         }
@@ -1232,8 +1269,9 @@ struct Engine {
             return;
         }
         // DnsMetricsManager::process_dns_layer (:1350-1370)
+        const bool deep = dns_s.draw(true);
         if (dns.maybe_shift(p.ts)) on_dns_period_shift(p.ts);
-        dns.new_event(true);
+        dns.new_event(deep);
         DnsBucket &b = dns.live();
         const uint32_t g = cfg.dns_groups;
         if (g & DG_COUNTERS) {
@@ -1250,15 +1288,17 @@ struct Engine {
                 else if (rcode == 5) b.REFUSED++;
             } else b.queries++;
         }
-        if (g & DG_TOP_PORTS) b.udp_port.update(metric_port);
         DnsParse r;
+        if (deep) {
+        if (g & DG_TOP_PORTS) b.udp_port.update(metric_port);
         if (m.len >= 12) r = parse_resources(m);
         else {
             DnsMsg mm{hdr_buf, m.len};
             r = parse_resources_short(mm);
         }
+        }
         std::string name_lower;
-        if (r.ok) {
+        if (deep && r.ok) {
             if (qr) b.rcode.update(rcode);
             if (r.has_query) {
                 name_lower = lower(r.name);
@@ -1308,7 +1348,7 @@ struct Engine {
                 if (d.sec > (int64_t)ttl_s) timed_out = true;
                 else if (d.sec == (int64_t)ttl_s && (d.nsec / 1.0e6) >= ttl_ms) timed_out = true;
                 if (timed_out) b.xacts_timed_out++;
-                else new_xact(b, p, d, x, r);
+                else new_xact(b, p, d, x, r, deep);
             }
         } else {
             xacts[k] = Xact{p.ts, m.len};
@@ -1421,13 +1461,14 @@ struct Engine {
     }
 
     // DnsMetricsBucket::new_dns_transaction (:1093-1138)
-    void new_xact(DnsBucket &b, const DnsEv &p, TS d, const Xact &x, const DnsParse &r)
+    void new_xact(DnsBucket &b, const DnsEv &p, TS d, const Xact &x, const DnsParse &r, bool deep)
     {
         uint64_t us = (uint64_t)((d.sec * 1000000000LL) + d.nsec) / 1000;
-        const bool q = cfg.dns_groups & DG_QUANTILES, h = cfg.dns_groups & DG_HISTOGRAMS;
+        const bool q = deep && (cfg.dns_groups & DG_QUANTILES), h = deep && (cfg.dns_groups & DG_HISTOGRAMS);
         b.xacts_total++;
         if (p.dir == DIR_TO_HOST) { b.xacts_out++; if (q) b.xact_from.update(us); if (h) b.hist_from.update(us); }
         else if (p.dir == DIR_FROM_HOST) { b.xacts_in++; if (q) b.xact_to.update(us); if (h) b.hist_to.update(us); }
+        if (!deep) return; // new_dns_transaction (:1121-1136): ratio and slow tops only when deep
         size_t resp_len = p.len;
         if (x.query_size) b.ratio.update((double)resp_len / (double)x.query_size);
         if (r.ok && r.has_query) {
@@ -2129,6 +2170,7 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "dns_groups") c.dns_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "filter_all") c.filter_all = atoi(v.c_str()) != 0;
         else if (k == "net_filter_all") c.net_filter_all = atoi(v.c_str()) != 0;
+        else if (k == "deep_sample_rate") c.deep_sample_rate = std::max(1, std::min(100, atoi(v.c_str())));
         else if (k == "net2_groups") c.net2_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "dns2_groups") c.dns2_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "topn_pct") c.topn_pct = (uint32_t)atoi(v.c_str());
@@ -2271,6 +2313,14 @@ void pvo_aggregate_domain(const char *name, size_t n, size_t suffix, size_t *q2_
     pvo::aggregate_domain(d, suffix, q2, q3);
     *q2_start = d.size() - q2.size();
     *q3_start = q3.empty() ? -1 : (long)(d.size() - q3.size());
+}
+
+// the oracle's jsf32 restatement, first n draws (pinned against oracle/_ref/ref_jsf)
+int pvo_jsf32(uint32_t n, uint32_t *out)
+{
+    pvo::Jsf32 r;
+    for (uint32_t i = 0; i < n; i++) out[i] = r();
+    return 0;
 }
 
 } // extern "C"

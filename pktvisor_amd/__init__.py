@@ -47,7 +47,8 @@ class pv_config(ctypes.Structure):
                 ("linktype", ctypes.c_uint32), ("ts_nano", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("table_log2", ctypes.c_uint32), ("max_records", ctypes.c_uint64),
                 ("topn_percentile_threshold", ctypes.c_uint32), ("net_filter_all", ctypes.c_uint32),
-                ("net2_groups", ctypes.c_uint32), ("dns2_groups", ctypes.c_uint32)]
+                ("net2_groups", ctypes.c_uint32), ("dns2_groups", ctypes.c_uint32),
+                ("deep_sample_rate", ctypes.c_uint32)]
 
 
 class pv_dns_filters(ctypes.Structure):
@@ -362,7 +363,8 @@ class PvHandlers:
                  table_log2: int = 0, max_records: int = 1 << 20, net_groups: int = 0, dns_groups: int = 0,
                  dns_filters: Optional[dict] = None, net_config: Optional[dict] = None,
                  dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0,
-                 net2_config: Optional[dict] = None, dns2_config: Optional[dict] = None):
+                 net2_config: Optional[dict] = None, dns2_config: Optional[dict] = None,
+                 deep_sample_rate: int = 100):
         from pktvisor_amd import config as pvcfg
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
@@ -384,8 +386,7 @@ class PvHandlers:
         if net_config is not None or dns_config is not None or net2_config is not None or dns2_config is not None:
             ncfg, dcfg = dict(net_config or {}), dict(dns_config or {})
             win = pvcfg.window_config([ncfg, dcfg, dict(net2_config or {}), dict(dns2_config or {})])
-            if win.get("deep_sample_rate", 100) != 100:
-                raise pvcfg.ConfigException("deep_sample_rate below 100 is not supported by the GPU handler")
+            deep_sample_rate = win.get("deep_sample_rate", deep_sample_rate)
             num_periods = win.get("num_periods", num_periods)
             topn_count = win.get("topn_count", topn_count)
             topn_percentile_threshold = win.get("topn_percentile_threshold", topn_percentile_threshold)
@@ -398,7 +399,7 @@ class PvHandlers:
         self._host = host_spec.encode() if host_spec else None
         cfg = pv_config(self._host, num_periods, topn_count, xact_ttl_ms, net_groups, dns_groups, linktype, ts_nano,
                         device, table_log2, max_records, topn_percentile_threshold, net_filter_all, net2_groups,
-                        dns2_groups)
+                        dns2_groups, deep_sample_rate)
         self.num_periods = num_periods
         self.ctx = ctypes.c_void_p()
         rc = self.lib.pv_create(ctypes.byref(cfg), ctypes.byref(self.ctx))

@@ -121,9 +121,9 @@ def window_config(cfgs) -> dict:
     np = out.get("num_periods", 5)
     if not 1 <= np <= 10:
         raise ConfigException("num_periods must be between 1 and 10")
-    rate = out.get("deep_sample_rate", 100)
-    if not 1 <= rate <= 100:
-        raise ConfigException("deep_sample_rate must be between 1 and 100")
+    if "deep_sample_rate" in out:
+        # clamped, not refused (AbstractMetricsManager.h:357-365)
+        out["deep_sample_rate"] = max(1, min(100, out["deep_sample_rate"]))
     if out.get("topn_percentile_threshold", 0) > 99:
         raise ConfigException("topn_percentile_threshold must be between 0 and 99")
     return out

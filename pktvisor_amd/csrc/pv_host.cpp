@@ -147,6 +147,23 @@ struct SlotMeta {
 // src/AbstractMetricsManager.h:233,264-305). The bucket of period ordinal k lives in slot
 // k % PV_SLOTS of this handler's part of the device state.
 enum { PART_NET = 0, PART_DNS = 1 };
+
+// jsf32 (3rd/rng/jsf.h:38-70,111,151: jsf<uint32_t, uint32_t, 27, 17, 0>), the managers' deep
+// sampling generator, default seed itype(0xcafe5eed00000001) = 1, 20 warm-up rounds
+struct Jsf32 {
+    uint32_t a = 0xf1ea5eedu, b = 1, c = 1, d = 1;
+    Jsf32() { for (int i = 0; i < 20; i++) next(); }
+    static uint32_t rot(uint32_t x, uint32_t k) { return (x << k) | (x >> (32 - k)); }
+    uint32_t next()
+    {
+        const uint32_t e = a - rot(b, 27);
+        a = b ^ rot(c, 17);
+        b = c + d;
+        c = d + e;
+        d = e + a;
+        return d;
+    }
+};
 struct Window {
     std::deque<uint32_t> slots; // front = live bucket
     int64_t next_shift_sec = 0;
@@ -468,6 +485,12 @@ struct pv_ctx {
     bool tcp_active = false;  // a stage has run since the last reset
     bool tcp_pre = false;     // this batch's stage runs ahead of the Net pass (prescan emits)
     uint32_t tcp_nmsg = 0;    // messages of the current batch
+    // deep sampling (deep_sample_rate < 100): each manager's generator, the span's "not deep"
+    // bitmaps (Net by record, DNS by the record of its event), pinned staging + device copies
+    uint32_t sample_rate = 100;
+    Jsf32 rng_net, rng_dns;
+    uint32_t *h_ndeep = nullptr, *d_ndeep = nullptr;
+    uint64_t ndeep_words = 0;
     std::vector<std::pair<uint64_t, int64_t>> tcp_ords; // (ord, second) of the batch's messages, by ord
 
     int fail(int code, const char *fmt, ...)
@@ -1306,6 +1329,7 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
         if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
             return c->hipfail(e, "only_qname_suffix record buffer");
     }
+    if (fl && c->sample_rate < 100) return c->fail(PV_EUNSUPPORTED, "DNS filters with deep_sample_rate below 100 are not built");
     c->f_flags = fl;
     c->f_rcode_mask = (fl & PVDF_ONLY_RCODE) ? f->only_rcode_mask : 0;
     c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
@@ -1350,6 +1374,12 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     c->nn_cap = (uint32_t)std::min<uint64_t>(1ull << c->tcap_log2, 1ull << 22);
     if (c->cfg.max_records == 0) c->cfg.max_records = 1 << 20;
     c->max_records = c->cfg.max_records;
+    // deep_sample_rate (AbstractMetricsManager::configure, src/AbstractMetricsManager.h:357-365: > 100 -> 100, < 1 -> 1)
+    c->sample_rate = c->cfg.deep_sample_rate == 0 ? 100u : std::max(1u, std::min(c->cfg.deep_sample_rate, 100u));
+    if (c->sample_rate < 100 && (c->cfg.net_filter_all || c->net2_groups || c->dns2_groups)) {
+        *out = c;
+        return c->fail(PV_EUNSUPPORTED, "deep_sample_rate below 100 with geo filters or the v2 handlers is not built");
+    }
     // TransactionManager(ttl_ms) split (TransactionManager.h:60-68)
     if (c->cfg.xact_ttl_ms > 1000) { c->ttl_s = c->cfg.xact_ttl_ms / 1000; c->ttl_ms = c->cfg.xact_ttl_ms - c->ttl_s * 1000; }
     else c->ttl_ms = c->cfg.xact_ttl_ms;
@@ -1482,6 +1512,8 @@ void pv_destroy(pv_ctx *c)
     }
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
     if (c->copy_stream2) hipStreamDestroy(c->copy_stream2);
+    if (c->d_ndeep) hipFree(c->d_ndeep);
+    if (c->h_ndeep) hipHostFree(c->h_ndeep);
     c->pool.reset();
     if (c->ev_start) hipEventDestroy(c->ev_start);
     if (c->ev_stop) hipEventDestroy(c->ev_stop);
@@ -1502,6 +1534,8 @@ int pv_reset(pv_ctx *c)
     }
     c->started = c->ended = false;
     c->records_seen = 0;
+    c->rng_net = Jsf32();
+    c->rng_dns = Jsf32();
     c->xvals_host.clear();
     c->xvals_synced = 0;
     c->from90 = c->to90 = 0.0f;
@@ -1948,6 +1982,37 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.tcp_emit = c->tcp_pre ? 0u : 1u;
     if (P.tcp_emit) launch_fill64(c, c->d_tmask, (n + 63) / 64, 0);
     P.gbase = c->global_base + c->records_seen;
+    if (c->sample_rate < 100) {
+        // AbstractMetricsManager::new_event (:318-323): one draw per event of each manager, in
+        // stream order; Net events are the records, DNS events the DNS-port UDP records the
+        // prescan finds (DNS filters are refused with sampling, so every one is an event)
+        const uint64_t words = n / 32 + 64; // padded: inactive lanes of the last tile read in bounds
+        if (words > c->ndeep_words) {
+            if (c->d_ndeep) hipFree(c->d_ndeep);
+            if (c->h_ndeep) hipHostFree(c->h_ndeep);
+            c->d_ndeep = nullptr;
+            c->h_ndeep = nullptr;
+            c->ndeep_words = 0;
+            hipError_t e;
+            if (!hip_ok(e = hipMalloc(&c->d_ndeep, words * 8)) || !hip_ok(e = hipHostMalloc((void **)&c->h_ndeep, words * 8, hipHostMallocDefault)))
+                return c->hipfail(e, "deep sampling bitmaps");
+            c->ndeep_words = words;
+        }
+        uint32_t tseg[2];
+        if (int rc = dns_prescan(c, d_recs, d_offs, n, st, false, tseg)) return rc;
+        uint32_t *hn = c->h_ndeep, *hd = c->h_ndeep + words;
+        memset(hn, 0, words * 8);
+        for (uint64_t i = 0; i < n; i++) {
+            if (!(c->rng_net.next() % 100u < c->sample_rate)) hn[i >> 5] |= 1u << (i & 31);
+            if ((c->h_dbits[i >> 6] >> (i & 63)) & 1)
+                if (!(c->rng_dns.next() % 100u < c->sample_rate)) hd[i >> 5] |= 1u << (i & 31);
+        }
+        hipError_t e;
+        if (!hip_ok(e = hipMemcpyAsync(c->d_ndeep, c->h_ndeep, words * 8, hipMemcpyHostToDevice, st)))
+            return c->hipfail(e, "deep sampling bitmaps");
+        P.ndeep_net = c->d_ndeep;
+        P.ndeep_dns = c->d_ndeep + words;
+    }
     // Net periods and slots: period 0 -> the live bucket, each shift -> the next ordinal's slot
     P.n_shift = (uint32_t)nsh.size();
     for (size_t k = 0; k < nsh.size(); k++) { P.thresh[k] = nsh[k].sec; P.pstart[k] = nsh[k].idx; }
@@ -2055,7 +2120,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
     // the specialised pass when nothing in the batch needs the general one
-    if (P.n_shift || P.net_filter_all || P.dbg)
+    if (P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net)
         hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else
         hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -2094,6 +2159,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (!c->tcp_pre) {
         if (int rc = tcp_stage(c, d_recs, d_offs, n, status[ST_TSEG], status[ST_TSEG_BYTES], first_sec, false, st)) return rc;
     }
+    if (c->sample_rate < 100 && c->tcp_nmsg)
+        return c->fail(PV_EUNSUPPORTED, "deep_sample_rate below 100 with DNS over TCP is not built");
     const uint32_t gt = tcp_pass(c, P, a, a + n, st, c->h_params + 1);
     if (gt) {
         if (P.want_events)

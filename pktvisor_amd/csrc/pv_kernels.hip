@@ -438,13 +438,13 @@ __device__ void net_flush(PV_CREF(PvParams) P, uint32_t s, NetCtr &c)
 }
 // DNS v1 counters of the wave's current slot
 struct DnsCtr {
-    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata, dfilt, dqecs;
-    __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = dfilt = dqecs = 0; }
+    uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata, dfilt, dqecs, dnd;
+    __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = dfilt = dqecs = dnd = 0; }
 };
 __device__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
 {
     const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
-    PV_FLUSH1(s, PV_OFF_DNS + DC_EVENTS, c.dev + c.dfilt, true) PV_FLUSH1(s, PV_OFF_DNS + DC_SAMPLES, c.dev + c.dfilt, true)
+    PV_FLUSH1(s, PV_OFF_DNS + DC_EVENTS, c.dev + c.dfilt, true) PV_FLUSH1(s, PV_OFF_DNS + DC_SAMPLES, c.dev + c.dfilt - c.dnd, true)
     PV_FLUSH1(s, PV_OFF_DNS + DC_TOTAL, c.dev, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_UDP, c.dev, dc)
     if (P.f_flags) PV_FLUSH1(s, PV_OFF_DNS + DC_FILTERED, c.dfilt, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_QUERIES, c.dq, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REPLIES, c.dr, dc)
@@ -668,12 +668,17 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             global_add(P, slot, key, w, i);
         }
     };
+    // deep sampling: an event that drew "not deep" counts as an event and in the counters only
+    // (DnsMetricsBucket::process_dns_layer !deep, dns/v1/DnsStreamHandler.cpp:968-970); its
+    // transaction still pairs, and a response's flag decides new_dns_transaction's deep part
+    const bool deep = TAP || !(dm.flags & 16);
     if (upd) {
         const uint32_t l3u = TAP && (dm.flags & 16);
         const uint32_t d4 = !(dm.flags & 4) && !l3u, d6 = (dm.flags & 4) ? 1 : 0;
         const uint32_t l4c = TAP ? (dm.flags >> 5) & 3 : (TCP ? 1u : 0u); // 0 UDP, 1 TCP, 2 other
         if (own) {
             c.dev++;
+            c.dnd += !deep;
             c.d4 += d4; c.d6 += d6;
             c.dq += !qr; c.dr += qr;
             c.dnoerr += qr && rcode == 0; c.dnodata += qr && rcode == 0 && ancount == 0;
@@ -681,7 +686,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         } else {
             const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
             sum_add(P, slot, PV_OFF_DNS + DC_EVENTS, 1);
-            sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
+            if (deep) sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
             if (dc) {
                 sum_add(P, slot, PV_OFF_DNS + DC_TOTAL, 1);
                 if (l4c < 2) sum_add(P, slot, PV_OFF_DNS + (l4c ? DC_TCP : DC_UDP), 1);
@@ -694,6 +699,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                 if (qr && rcode == 5) sum_add(P, slot, PV_OFF_DNS + DC_REFUSED, 1);
             }
         }
+        if (deep) {
         DnsInfo d;
         dns_parse(R, m, dlen, qd, ancount, ns, ar, d);
         // client ports spread over 64 K values and rarely repeat inside a workgroup: a
@@ -752,6 +758,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                 }
             }
         }
+        }
     }
     if (P.want_events && !TAP) {
         // the workgroup's event region; LDS counter, order irrelevant (sorted by key, index)
@@ -766,7 +773,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         ev.qr = (uint8_t)qr;
         ev.dir = dm.flags & 3;
         ev.period = (uint8_t)period;
-        ev.pad = 0;
+        ev.pad = deep ? 0 : 4; // v1: bit 2 = the event is not deep
         if (P.dns2_groups) {
             // DNS v2: one transaction map per direction (DnsMetricsManager::_pair_manager); a
             // response looks in the swapped direction's map (dns/v2 ...cpp:1100-1145). pad: the
@@ -850,6 +857,7 @@ struct NetK {
     PV_G PvTcpSeg *tseg;
     PV_G uint32_t *tseg_cnt;
     PV_G uint64_t *tmask;
+    const PV_G uint32_t *ndeep_net, *ndeep_dns; // deep sampling (general pass only)
 };
 // Net v1 counters of one record straight to HBM (a lane whose slot is not the wave's
 // register slot: records of a 64-record tile that holds a period shift)
@@ -1296,6 +1304,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
     K.net_groups = P.net_groups; K.dbg = GEN ? P.dbg : 0u; K.net_filter_all = GEN ? P.net_filter_all : 0u;
     K.n_dshift = P.n_dshift; K.dskip_before = P.dskip_before;
     K.tcp_emit = P.tcp_emit; K.tseg_cap = P.tseg_cap; K.tseg = P.tseg; K.tseg_cnt = P.tseg_cnt; K.tmask = P.tmask;
+    K.ndeep_net = GEN ? P.ndeep_net : nullptr; K.ndeep_dns = GEN ? P.ndeep_dns : nullptr;
     const ParseCfg C = parse_cfg(P);
     const uint64_t n = K.n, last = n - 1;
     const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
@@ -1375,6 +1384,13 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
         }
         const bool upd = lp >= K.skip_before;
         const bool own = slot == wslot;
+        // deep sampling: the Net manager's draw for this record's event, the DNS manager's for
+        // its DNS event (bitmaps padded past the span, so inactive lanes read in bounds)
+        bool deep = true, ddeep = true;
+        if (GEN && K.ndeep_net) {
+            deep = !((K.ndeep_net[i >> 5] >> (i & 31)) & 1);
+            ddeep = !((K.ndeep_dns[i >> 5] >> (i & 31)) & 1);
+        }
         const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
         const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
         uint32_t hv = PV_NOH;
@@ -1399,15 +1415,33 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
                 fast = fast_parse(rw, C, P, off, o);
             }
             if (!fast) {
-                const SlowOut so = net_slow(R, C, P, K, off, i, slot, upd && !K.net_filter_all);
-                o.caplen = so.caplen; o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
+                // a record that is not deep: no IPs, no SYN (NetworkMetricsBucket::process_packet
+                // !deep, net/v1/NetStreamHandler.cpp:518-521)
+                const SlowOut so = net_slow(R, C, P, K, off, i, slot, upd && !K.net_filter_all && deep);
+                o.caplen = so.caplen; o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn && deep;
                 ek = so.ek;
                 dm = so.dm;
                 isdns = so.isdns;
+                if (!ddeep) dm.a.w |= 16u << 16; // DnsMsg flags bit 4: the DNS event is not deep
             } else if (K.tcp_emit && o.l4 == 6) {
                 hasseg = tcp_seg_fast(rw, o, i, seg);
             }
             istcp = o.l4 == 6;
+            if (!deep) o.syn = 0;
+            if (GEN && K.ndeep_net) {
+                // deep_samples counts deep events only: one subtraction per wave (per lane in a
+                // tile whose records fall in several periods)
+                const bool nd = upd && !deep && !(K.dbg & 2);
+                const uint64_t m = __ballot(nd);
+                if (m) {
+                    if (!straddle) {
+                        if (lane == (uint32_t)__builtin_ctzll(m))
+                            ksum_add(K, slot, PV_OFF_NET + NC_SAMPLES, (uint64_t)0 - (uint64_t)__popcll(m));
+                    } else if (nd) {
+                        ksum_add(K, slot, PV_OFF_NET + NC_SAMPLES, ~0ull);
+                    }
+                }
+            }
             STAMP(4)
             if (K.dbg & 2) {
                 c.add(o);
@@ -1430,7 +1464,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
                     if (cl > 65535) { atomicOr(K.flags, PVF_BIG_CAPLEN); cl = 65535; }
                     if (slot == hslot && cl < PV_HBINS) hv = cl;
                     else ksum_add(K, slot, PV_OFF_PAYLOAD + cl, 1);
-                    if (fast) {
+                    if (fast && deep) {
                         // net_ip_entry on the words (IPv4 only)
                         const bool card = K.net_groups & PV_NET_CARDINALITY_BIT;
                         const uint32_t ip = o.dir == 0 ? rw.at(42) : rw.at(46);
@@ -1456,6 +1490,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
                     DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= K.dskip_before, false);
                     d.fkey = fast_flowkey(rw);
                     dm = msg_words(d);
+                    if (!ddeep) dm.a.w |= 16u << 16; // not deep
                     isdns = true;
                 }
             }
@@ -2751,14 +2786,16 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
             if (e.dir == 0) xctr(T, e.period, XC_OUT);
             else if (e.dir == 1) xctr(T, e.period, XC_IN);
         }
+        // a response that is not deep: counts only (new_dns_transaction !deep, :1105-1121)
+        const bool rdeep = !(e.pad & 4);
         // quantile inputs of every period (skipped ones still feed the next period's p90)
-        if (X.quantiles) {
+        if (X.quantiles && rdeep) {
             if (e.dir == 0) xval(X, T, e.period, XV_FROM_US, us);
             else if (e.dir == 1) xval(X, T, e.period, XV_TO_US, us);
         }
-        if ((X.quantiles & 1) && qe.len && kept)
+        if ((X.quantiles & 1) && qe.len && kept && rdeep)
             xval(X, T, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
-        if (!kept || e.dir == 2) return;
+        if (!kept || e.dir == 2 || !rdeep) return;
         if (X.thr_from[e.period] < 0.0f) {
             T.valid[atomicAdd(&T.nvalid, 1u)] = PvXValid{e.idx, (uint8_t)e.period, (uint8_t)e.dir, 0, 0, us};
         } else {

@@ -406,6 +406,9 @@ struct PvParams {
     uint32_t tcp_pass, tcp_nmsg;
     uint32_t ord_lo, ord_hi, ord_base; // this span's messages: ord in [ord_lo, ord_hi); ord_base = span start * 4
     uint32_t tap; // dnstap events (pv_dnstap_kernel): IPv6 top-N names take the address the key hashes
+    // deep sampling (deep_sample_rate < 100, AbstractMetricsManager::new_event): bit i set =
+    // record i's Net event / DNS event draws "not deep" (the managers' jsf32 draws, on the host)
+    const PV_G uint32_t *ndeep_net, *ndeep_dns;
     uint32_t dpos[PV_MAX_SHIFTS];      // span-relative ord of the event that shifts DNS period k+1
 };
 
