@@ -27,6 +27,10 @@
  *                                    AbstractMetricsManager.h:423-437)
  *   pv_window_json ................ StreamHandler::window_json(j, period, merged)
  *                                   (src/StreamHandler.h:71-77, AbstractMetricsManager.h:480-504,601-647)
+ *   pv_window_prometheus .......... StreamHandler::window_prometheus(out, add_labels)
+ *                                   (src/StreamHandler.h:71-77, AbstractMetricsManager.h:506-531;
+ *                                    NetStreamHandler.cpp:332-388, DnsStreamHandler.cpp:1139-1238)
+ *   pv_add_static_label ........... Metric::add_static_label (src/Metrics.h, Metrics.cpp:129-155)
  *   pv_state_* / pv_reduce_* ...... the bucket merge (AbstractMetricsBucket::merge,
  *                                   AbstractMetricsManager.h:177-195) split into
  *                                   collective-friendly regions for a multi-GPU reduce
@@ -289,6 +293,16 @@ int pv_reset(pv_ctx *ctx);
  * recent buckets (window_merged_json). *out is malloc'd; free with pv_free. */
 int pv_window_json(pv_ctx *ctx, uint32_t period, int merged, char **out);
 void pv_free(void *p);
+
+/* Prometheus text exposition of bucket `period` (0 = live) of each attached v1 handler,
+ * Net ("packets_*") then DNS ("dns_*"), in the reference's metric order, names, HELP texts
+ * and number formatting; labels: the static labels, then these n_labels added ones (each
+ * set in key order). Rates are timer-driven and not kept: nothing is written for them, as
+ * for an empty Rate. The v2 handlers are refused (PV_EUNSUPPORTED). *out: pv_free. */
+int pv_window_prometheus(pv_ctx *ctx, uint32_t period, const char *const *label_keys, const char *const *label_values,
+                         uint32_t n_labels, char **out);
+/* Process-wide label on every Prometheus sample (Metric::add_static_label). */
+int pv_add_static_label(const char *key, const char *value);
 
 /* Device-state regions of the live window, for a multi-GPU reduce:
  *   SUM region: uint64 counters and dense tables (all-reduce SUM)

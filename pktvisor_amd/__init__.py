@@ -161,7 +161,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code", "pv_advance_windows",
            "pv_dns_event_seconds", "pv_dns_event_seconds_host", "pv_comm_unique_id", "pv_comm_init",
            "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count",
-           "pv_pcapng_records", "pv_tpacket3_block_records"]
+           "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label"]
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
 
@@ -204,6 +204,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_synchronize.argtypes = [P]
     lib.pv_reset.argtypes = [P]
     lib.pv_window_json.argtypes = [P, U32, ctypes.c_int, ctypes.POINTER(P)]
+    lib.pv_window_prometheus.argtypes = [P, U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), U32,
+                                         ctypes.POINTER(P)]
+    lib.pv_add_static_label.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     lib.pv_free.argtypes = [P]
     lib.pv_free.restype = None
     lib.pv_state_regions.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(P),
@@ -348,6 +351,12 @@ class RecordIndex:
             raise PvError(f"pv_index_records failed ({rc})")
         self.offsets = self.offsets[: self.info.n_records]
         self.n = int(self.info.n_records)
+
+
+def add_static_label(key: str, value: str) -> None:
+    """Metric::add_static_label: a label on every Prometheus sample of every handler."""
+    if load_library().pv_add_static_label(key.encode(), value.encode()):
+        raise PvError(f"pv_add_static_label({key!r}) failed")
 
 
 class PvHandlers:
@@ -497,6 +506,19 @@ class PvHandlers:
         txt = ctypes.string_at(out.value).decode()
         self.lib.pv_free(out)
         return json.loads(txt)
+
+    def window_prometheus(self, period: int = 0, labels: Optional[dict] = None) -> str:
+        """StreamHandler::window_prometheus (src/AbstractMetricsManager.h:506-531): the
+        Prometheus text of bucket `period`, with `labels` added to every sample."""
+        labels = labels or {}
+        keys = (ctypes.c_char_p * max(1, len(labels)))(*[k.encode() for k in labels])
+        vals = (ctypes.c_char_p * max(1, len(labels)))(*[str(v).encode() for v in labels.values()])
+        out = ctypes.c_void_p()
+        self._check(self.lib.pv_window_prometheus(self.ctx, period, keys, vals, len(labels), ctypes.byref(out)),
+                    "pv_window_prometheus")
+        txt = ctypes.string_at(out.value).decode()
+        self.lib.pv_free(out)
+        return txt
 
     def state_regions(self):
         sp, mp = ctypes.c_void_p(), ctypes.c_void_p()

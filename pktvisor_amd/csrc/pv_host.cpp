@@ -32,6 +32,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <sstream>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -83,8 +84,7 @@ extern "C" __global__ void pv_fill_multi(PvFillList L);
 extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
 extern "C" __global__ void pv_dns_prescan(const PvParams *P);
 extern "C" __global__ void pv_topn_combine(const PvParams *P);
-extern "C" __global__ void pv_topn_scan(const PvParams *P);
-extern "C" __global__ void pv_topn_scatter(const PvParams *P);
+extern "C" __global__ void pv_topn_combine_r12(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
 extern "C" __global__ void pv_net2_kernel(const PvParams *P);
 extern "C" __global__ void pv_ix_guess(const PvIxParams *X);
@@ -119,16 +119,11 @@ namespace {
 
 // status words (device): flags, n_events, n_resp, n_vals, DNS messages, new top-N names
 enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNEW = 5, ST_TSEG = 6, ST_TSEG_BYTES = 7,
-       ST_WORDS = 8 };
-// after the status words (one allocation, zeroed per batch up to the live region count):
-// per-region update counts, then offsets and fill pointers
+       ST_WORDS = 8, ST_HANDS = 8 /* top-N handlers with entries (device only) */ };
+// status allocation (zeroed per batch): the words above, padded
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
 #define PV_TRASH_WAVES 16384 // Net-pass waves with a 2-KiB trash area (grid <= 4096)
-#define ST_TP_CNT 32
-#define ST_TP_OFF (ST_TP_CNT + (1 << PV_MAX_REGIONS_LOG2))
-#define ST_TP_FILL (ST_TP_OFF + (1 << PV_MAX_REGIONS_LOG2))
-#define ST_TP_TABS (ST_TP_FILL + (1 << PV_MAX_REGIONS_LOG2))
-#define ST_ALLOC (ST_TP_TABS + (1 << PV_MAX_REGIONS_LOG2))
+#define ST_ALLOC 32
 
 struct SlotMeta {
     int64_t start_sec = 0, start_nsec = 0, end_sec = 0, end_nsec = 0;
@@ -603,9 +598,10 @@ void clear_part(pv_ctx *c, int part, uint32_t s)
         launch_fill64(c, sum + PV_OFF_DNS, PV_SUM_WORDS - PV_OFF_DNS, 0);
         launch_fill64(c, cpc + PV_MIN_NET_WORDS, PV_MIN_WORDS - PV_MIN_NET_WORDS, (uint64_t)PV_CPC_EMPTY);
     }
+    // keys only: a count or name word is read only behind a non-zero key, and whoever
+    // claims an entry overwrites its name word and adds net of the stale count (global_add,
+    // pv_topn_merge)
     launch_fill64(c, c->d_tkeys + t * tcap, tcap, 0);
-    launch_fill64(c, c->d_tcnt + t * tcap, tcap, 0);
-    launch_fill32(c, c->d_taux + t * tcap, tcap, 0);
     launch_fill64(c, c->d_arena_top + (uint64_t)t * PV_ARENA_PARTS, PV_ARENA_PARTS, 0);
     launch_fill32(c, c->d_tab_live + t, 1, 0);
     c->roff[t].clear();
@@ -895,9 +891,8 @@ std::vector<std::pair<std::string, uint64_t>> dense_tops(const uint64_t *t, size
 // uint64 values of 10^(b/18) * 10^e, e in [-9, 18), b in [0, 18); a point is listed when the
 // inclusive PMF interval that ends at it holds a value, with the inclusive CDF times n (a
 // double, as KLL's normalized rank times get_n()); "+Inf" closes with n
-void hist_json(Json &j, const char *key, std::vector<uint64_t> v)
+const std::vector<uint64_t> &hist_points()
 {
-    if (v.empty()) return;
     static const std::vector<uint64_t> pts = [] {
         std::vector<uint64_t> p;
         for (int e = -9; e < 18; e++)
@@ -907,6 +902,12 @@ void hist_json(Json &j, const char *key, std::vector<uint64_t> v)
             }
         return p;
     }();
+    return pts;
+}
+void hist_json(Json &j, const char *key, std::vector<uint64_t> v)
+{
+    if (v.empty()) return;
+    const std::vector<uint64_t> &pts = hist_points();
     std::sort(v.begin(), v.end());
     const double n = (double)v.size();
     j.key(key).obj();
@@ -1182,6 +1183,218 @@ void dns_json(pv_ctx *c, Json &j, const HostBucket &b)
     }
     top_json(j, "top_rcode", dense_tops(&b.sum[PV_OFF_RCODE], PV_RCODE_BINS, 2), topn, pct);
     top_json(j, "top_qtype", dense_tops(&b.sum[PV_OFF_QTYPE], PV_QTYPE_BINS, 1), topn, pct);
+}
+
+// ---- Prometheus exposition (window_single_prometheus, src/AbstractMetricsManager.h:506-531)
+// Metric text as the reference's primitives write it (src/Metrics.cpp:15-20,75-80,120-155;
+// src/Metrics.h:264-289,416-448,614-691): "# HELP <schema>_<names> <desc>", "# TYPE ...", then
+// samples named <schema>_<names>[_suffix]{static labels, then the added labels, each set in key
+// order}. Numbers go through an ostream, as the reference's do (doubles with precision 6).
+// Rates are timer-driven and not kept by this handler: an empty Rate writes nothing.
+using PromLabels = std::map<std::string, std::string>;
+std::mutex g_static_mu;
+PromLabels g_static_labels; // Metric::_static_labels (Metric::add_static_label)
+
+struct Prom {
+    std::ostringstream o;
+    PromLabels add;
+    std::string lbl(const PromLabels &a) const
+    {
+        std::string t = "{";
+        {
+            std::lock_guard<std::mutex> g(g_static_mu);
+            for (auto &kv : g_static_labels) t += kv.first + "=\"" + kv.second + "\",";
+        }
+        for (auto &kv : a) t += kv.first + "=\"" + kv.second + "\",";
+        if (t.back() == ',') t.pop_back();
+        return t + "}";
+    }
+    void head(const std::string &name, const char *desc, const char *type)
+    {
+        o << "# HELP " << name << ' ' << desc << '\n' << "# TYPE " << name << ' ' << type << '\n';
+    }
+    template <typename V>
+    void gauge(const std::string &name, const char *desc, V v)
+    {
+        head(name, desc, "gauge");
+        o << name << lbl(add) << ' ' << v << '\n';
+    }
+    // Quantile::to_prometheus: p50..p99, _sum = the sketch's max item, _count = n
+    template <typename T>
+    void summary(const std::string &name, const char *desc, const std::vector<T> &q, T max_item, uint64_t n)
+    {
+        if (q.empty()) return;
+        head(name, desc, "summary");
+        static const char *qs[4] = {"0.5", "0.9", "0.95", "0.99"};
+        for (int i = 0; i < 4; i++) {
+            PromLabels l(add);
+            l["quantile"] = qs[i];
+            o << name << lbl(l) << ' ' << q[i] << '\n';
+        }
+        o << name << "_sum" << lbl(add) << ' ' << max_item << '\n';
+        o << name << "_count" << lbl(add) << ' ' << n << '\n';
+    }
+    // TopN::to_prometheus: the to_json selection, one sample per item labelled item_key=name
+    void topn(const std::string &name, const char *item_key, const char *desc,
+              const std::vector<std::pair<std::string, uint64_t>> &v0, size_t n, uint32_t pct)
+    {
+        auto v = v0;
+        std::sort(v.begin(), v.end(), [](const auto &a, const auto &b) {
+            if (a.second != b.second) return a.second > b.second;
+            return a.first < b.first;
+        });
+        const size_t k = std::min(n, v.size());
+        if (!k) return;
+        std::vector<uint64_t> est;
+        for (size_t i = 0; i < k; i++) est.push_back(v[i].second);
+        std::sort(est.begin(), est.end());
+        const uint64_t w = (uint64_t)std::ceil((double)pct / 100.0 * (double)k);
+        const uint64_t thr = est[w == 0 ? 0 : std::min<size_t>(w - 1, k - 1)];
+        head(name, desc, "gauge");
+        PromLabels l(add);
+        for (size_t i = 0; i < k && v[i].second >= thr; i++) {
+            l[item_key] = v[i].first;
+            o << name << lbl(l) << ' ' << v[i].second << '\n';
+        }
+    }
+    // Histogram::to_prometheus over exact values (the split points of hist_json)
+    void histogram(const std::string &name, const char *desc, std::vector<uint64_t> v)
+    {
+        if (v.empty()) return;
+        std::sort(v.begin(), v.end());
+        head(name, desc, "histogram");
+        const double n = (double)v.size();
+        uint64_t prev = 0;
+        for (uint64_t x : hist_points()) {
+            const uint64_t c = (uint64_t)(std::upper_bound(v.begin(), v.end(), x) - v.begin());
+            if (c != prev) {
+                PromLabels l(add);
+                l["le"] = std::to_string(x);
+                o << name << "_bucket" << lbl(l) << ' ' << ((double)c / n) * n << '\n';
+            }
+            prev = c;
+        }
+        PromLabels l(add);
+        l["le"] = "+Inf";
+        o << name << "_bucket" << lbl(l) << ' ' << 1.0 * n << '\n';
+        o << name << "_count" << lbl(add) << ' ' << v.size() << '\n';
+    }
+};
+
+// NetworkMetricsBucket::to_prometheus (src/handlers/net/v1/NetStreamHandler.cpp:332-388);
+// names and descriptions from NetStreamHandler.h:81-127
+void net_prom(pv_ctx *c, Prom &p, const HostBucket &b)
+{
+    const uint64_t *n = &b.sum[PV_OFF_NET];
+    const size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
+    p.gauge("packets_events", "Total packets events generated", n[NC_EVENTS]);
+    p.gauge("packets_deep_samples", "Total packets that were sampled for deep inspection", n[NC_SAMPLES]);
+    if (c->net_groups & PV_NET_COUNTERS) {
+        p.gauge("packets_udp", "Count of UDP packets", n[NC_UDP]);
+        p.gauge("packets_tcp", "Count of TCP packets", n[NC_TCP]);
+        p.gauge("packets_protocol_tcp_syn", "Count of TCP SYN packets", n[NC_SYN]);
+        p.gauge("packets_other_l4", "Count of packets which are not UDP or TCP", n[NC_OTHER]);
+        p.gauge("packets_ipv4", "Count of IPv4 packets", n[NC_V4]);
+        p.gauge("packets_ipv6", "Count of IPv6 packets", n[NC_V6]);
+        p.gauge("packets_in", "Count of total ingress packets", n[NC_IN]);
+        p.gauge("packets_out", "Count of total egress packets", n[NC_OUT]);
+        p.gauge("packets_unknown_dir", "Count of total unknown direction packets", n[NC_UNK]);
+        p.gauge("packets_total", "Count of total packets matching the configured filter(s)", n[NC_TOTAL]);
+        p.gauge("packets_filtered", "Count of total packets that did not match the configured filter(s) (if any)", n[NC_FILTERED]);
+    }
+    if (c->net_groups & PV_NET_CARDINALITY) {
+        p.gauge("packets_cardinality_src_ips_in", "Source IP cardinality", lround(cpc_estimate(&b.cpc[CPC_SRC * PV_CPC_COUPONS], b.merged)));
+        p.gauge("packets_cardinality_dst_ips_out", "Destination IP cardinality", lround(cpc_estimate(&b.cpc[CPC_DST * PV_CPC_COUPONS], b.merged)));
+    }
+    if (c->net_groups & PV_NET_TOP_IPS) {
+        p.topn("packets_top_ipv4", "ipv4", "Top IPv4 IP addresses", tops_of(b, TM_IPV4), topn, pct);
+        p.topn("packets_top_ipv6", "ipv6", "Top IPv6 IP addresses", tops_of(b, TM_IPV6), topn, pct);
+    }
+    // top_geo: no MaxMind database, the TopNs stay empty and write nothing
+    uint64_t cnt;
+    const uint64_t *h = &b.sum[PV_OFF_PAYLOAD];
+    auto q = hist_quantiles(h, PV_PAYLOAD_BINS, cnt);
+    uint64_t mx = 0;
+    for (size_t i = 0; i < PV_PAYLOAD_BINS; i++)
+        if (h[i]) mx = i;
+    p.summary<uint64_t>("packets_payload_size", "Quantiles of payload sizes, in bytes", q, mx, cnt);
+}
+
+// DnsMetricsBucket::to_prometheus (src/handlers/dns/v1/DnsStreamHandler.cpp:1139-1238);
+// names and descriptions from DnsStreamHandler.h:116-171
+void dns_prom(pv_ctx *c, Prom &p, const HostBucket &b)
+{
+    const uint64_t *d = &b.sum[PV_OFF_DNS];
+    const size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
+    const uint32_t g = c->dns_groups;
+    p.gauge("dns_wire_packets_events", "Total DNS wire packets events", d[DC_EVENTS]);
+    p.gauge("dns_wire_packets_deep_samples", "Total DNS wire packets that were sampled for deep inspection", d[DC_SAMPLES]);
+    if (g & PV_DNS_COUNTERS) {
+        p.gauge("dns_wire_packets_queries", "Total DNS wire packets flagged as query (ingress and egress)", d[DC_QUERIES]);
+        p.gauge("dns_wire_packets_replies", "Total DNS wire packets flagged as reply (ingress and egress)", d[DC_REPLIES]);
+        p.gauge("dns_wire_packets_tcp", "Total DNS wire packets received over TCP (ingress and egress)", d[DC_TCP]);
+        p.gauge("dns_wire_packets_udp", "Total DNS wire packets received over UDP (ingress and egress)", d[DC_UDP]);
+        p.gauge("dns_wire_packets_ipv4", "Total DNS wire packets received over IPv4 (ingress and egress)", d[DC_V4]);
+        p.gauge("dns_wire_packets_ipv6", "Total DNS wire packets received over IPv6 (ingress and egress)", d[DC_V6]);
+        p.gauge("dns_wire_packets_nxdomain", "Total DNS wire packets flagged as reply with response code NXDOMAIN (ingress and egress)", d[DC_NX]);
+        p.gauge("dns_wire_packets_refused", "Total DNS wire packets flagged as reply with response code REFUSED (ingress and egress)", d[DC_REFUSED]);
+        p.gauge("dns_wire_packets_srvfail", "Total DNS wire packets flagged as reply with response code SRVFAIL (ingress and egress)", d[DC_SRVFAIL]);
+        p.gauge("dns_wire_packets_noerror", "Total DNS wire packets flagged as reply with response code NOERROR (ingress and egress)", d[DC_NOERROR]);
+        p.gauge("dns_wire_packets_nodata", "Total DNS wire packets flagged as reply with response code NOERROR and no answer section data (ingress and egress)", d[DC_NODATA]);
+        p.gauge("dns_wire_packets_total", "Total DNS wire packets matching the configured filter(s)", d[DC_TOTAL]);
+        p.gauge("dns_wire_packets_filtered", "Total DNS wire packets seen that did not match the configured filter(s) (if any)", d[DC_FILTERED]);
+    }
+    if (g & PV_DNS_CARDINALITY)
+        p.gauge("dns_cardinality_qname", "Cardinality of unique QNAMES, both ingress and egress", lround(cpc_estimate(&b.cpc[CPC_QNAME * PV_CPC_COUPONS], b.merged)));
+    auto vmax = [](const auto &v) { return v.empty() ? 0 : *std::max_element(v.begin(), v.end()); };
+    if (g & PV_DNS_TRANSACTIONS) {
+        p.gauge("dns_xact_counts_total", "Total DNS transactions (query/reply pairs)", d[DC_XTOTAL]);
+        p.gauge("dns_xact_counts_timed_out", "Total number of DNS transactions that timed out", d[DC_XTIMEOUT]);
+        p.gauge("dns_xact_in_total", "Total ingress DNS transactions (host is server)", d[DC_XIN]);
+        p.topn("dns_xact_in_top_slow", "qname", "Top QNAMES in transactions where host is the server and transaction speed is slower than p90",
+               tops_of(b, TM_SLOW_IN), topn, pct);
+        if (g & PV_DNS_QUANTILES) {
+            if (!b.from_us.empty())
+                p.summary<uint64_t>("dns_xact_out_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is client, in microseconds",
+                                    quantiles(b.from_us), vmax(b.from_us), b.from_us.size());
+            if (!b.to_us.empty())
+                p.summary<uint64_t>("dns_xact_in_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is server, in microseconds",
+                                    quantiles(b.to_us), vmax(b.to_us), b.to_us.size());
+            if (!b.ratio.empty())
+                p.summary<double>("dns_xact_ratio_quantiles", "Quantiles of ratio of packet sizes in a DNS transaction (reply/query)",
+                                  quantiles(b.ratio), vmax(b.ratio), b.ratio.size());
+        }
+        if (g & PV_DNS_HISTOGRAMS) {
+            p.histogram("dns_xact_out_histogram_us", "Histogram of transaction timing (query/reply pairs) when host is client, in microseconds", b.from_us);
+            p.histogram("dns_xact_in_histogram_us", "Histogram of transaction timing (query/reply pairs) when host is server, in microseconds", b.to_us);
+        }
+        p.gauge("dns_xact_out_total", "Total egress DNS transactions (host is client)", d[DC_XOUT]);
+        p.topn("dns_xact_out_top_slow", "qname", "Top QNAMES in transactions where host is the client and transaction speed is slower than p90",
+               tops_of(b, TM_SLOW_OUT), topn, pct);
+    }
+    if (g & PV_DNS_TOP_PORTS)
+        p.topn("dns_top_udp_ports", "port", "Top UDP source port on the query side of a transaction", dense_tops(&b.sum[PV_OFF_PORT], PV_PORT_BINS, 0), topn, pct);
+    if (g & PV_DNS_TOP_ECS) {
+        if (g & PV_DNS_COUNTERS) p.gauge("dns_wire_packets_query_ecs", "Total queries that have EDNS Client Subnet (ECS) field set", d[DC_QECS]);
+        // geo / ASN of the subnet: no MaxMind database, those TopNs write nothing
+        p.topn("dns_top_query_ecs", "ecs", "Top EDNS Client Subnet (ECS) observed in DNS queries", tops_of(b, TM_ECS), topn, pct);
+    }
+    if (g & PV_DNS_TOP_QNAMES) {
+        p.topn("dns_top_qname2", "qname", "Top QNAMES, aggregated at a depth of two labels", tops_of(b, TM_QNAME2), topn, pct);
+        p.topn("dns_top_qname3", "qname", "Top QNAMES, aggregated at a depth of three labels", tops_of(b, TM_QNAME3), topn, pct);
+        p.topn("dns_top_nxdomain", "qname", "Top QNAMES with result code NXDOMAIN", tops_of(b, TM_NX), topn, pct);
+        p.topn("dns_top_refused", "qname", "Top QNAMES with result code REFUSED", tops_of(b, TM_REFUSED), topn, pct);
+        p.topn("dns_top_srvfail", "qname", "Top QNAMES with result code SRVFAIL", tops_of(b, TM_SRVFAIL), topn, pct);
+        p.topn("dns_top_nodata", "qname", "Top QNAMES with result code NOERROR and no answer section", tops_of(b, TM_NODATA), topn, pct);
+        if (g & PV_DNS_TOP_QNAMES_DETAILS) {
+            p.topn("dns_top_qname_by_resp_bytes", "qname", "Top QNAMES by response volume in bytes", tops_of(b, TM_SIZED), topn, pct);
+            p.topn("dns_top_noerror", "qname", "Top QNAMES with result code NOERROR", tops_of(b, TM_NOERROR), topn, pct);
+        }
+    }
+    p.topn("dns_top_rcode", "rcode", "Top result codes", dense_tops(&b.sum[PV_OFF_RCODE], PV_RCODE_BINS, 2), topn, pct);
+    p.topn("dns_top_qtype", "qtype", "Top query types", dense_tops(&b.sum[PV_OFF_QTYPE], PV_QTYPE_BINS, 1), topn, pct);
 }
 
 // KLL inclusive rank rule on exact data
@@ -2052,8 +2265,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         return c->fail(PV_ECAPACITY, "open DNS queries carried over more than 2^30 records without a response");
     P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
     P.flags = c->d_status + ST_FLAGS;
-    launch_fill32(c, c->d_status, ST_TP_CNT + (1u << c->reg_log2), 0);
-    launch_fill32(c, c->d_status + ST_TP_TABS, 1u << c->reg_log2, 0);
+    launch_fill32(c, c->d_status, ST_ALLOC, 0);
     hipError_t e;
     const uint64_t tiles = (n + 63) / 64; // 64-record wave tiles
     // persistent grid: exactly the workgroups that are resident at once (LDS/VGPR
@@ -2086,22 +2298,23 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             c->mq_bytes = need;
         }
     }
+    if (grid > PV_MAX_GRID) return c->fail(PV_ECAPACITY, "grid of %u workgroups exceeds %d", grid, PV_MAX_GRID);
+    if (P.mq_cap >= (1u << 24)) return c->fail(PV_ECAPACITY, "batch too large: %u update-log entries per workgroup", P.mq_cap);
     if (grid > c->cb_h_grid) {
         if (c->d_cb_h) hipFree(c->d_cb_h);
         c->d_cb_h = nullptr;
         c->cb_h_grid = 0;
-        if (!hip_ok(e = hipMalloc(&c->d_cb_h, (size_t)grid << (PV_MAX_REGIONS_LOG2 + 2)))) return c->hipfail(e, "region counts");
+        // run table: (2 << PV_MAX_REGIONS_LOG2) run keys x the grid padded to a multiple of 8
+        if (!hip_ok(e = hipMalloc(&c->d_cb_h, (size_t)((grid + 7) & ~7u) << (PV_MAX_REGIONS_LOG2 + 4))))
+            return c->hipfail(e, "region runs");
         c->cb_h_grid = grid;
     }
     P.mq = c->d_mq;
     P.mq_cnt = c->d_mq_cnt;
     P.reg_log2 = c->reg_log2;
-    P.tp_cnt = c->d_status + ST_TP_CNT;
-    P.tp_off = c->d_status + ST_TP_OFF;
-    P.tp_fill = c->d_status + ST_TP_FILL;
-    P.tp_tabs = c->d_status + ST_TP_TABS;
     P.tab_live = c->d_tab_live;
-    P.cb_h = c->d_cb_h;
+    P.cb_run = (uint64_t *)c->d_cb_h;
+    P.tp_hands = c->d_status + ST_HANDS;
     P.tp_buf = c->d_tpbuf;
     P.nn_cnt = c->d_status + ST_NNEW;
     P.nn = c->d_nn;
@@ -2131,12 +2344,11 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         hipLaunchKernelGGL(pv_dns_suffix, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
-    // top-N: combine each workgroup's updates, bucket them by table region, merge each
-    // region in LDS, decode the names of new entries
-    hipLaunchKernelGGL(pv_topn_combine, dim3(grid), dim3(PV_CB_THREADS), 0, st, (const PvParams *)c->d_params);
-    hipLaunchKernelGGL(pv_topn_scan, dim3(1), dim3(1024), 0, st, (const PvParams *)c->d_params);
-    hipLaunchKernelGGL(pv_topn_scatter, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
-    hipLaunchKernelGGL(pv_topn_merge, dim3(1u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);
+    // top-N: combine each workgroup's updates into a list sorted by table region, merge
+    // each region's runs in LDS, decode the names of new entries
+    hipLaunchKernelGGL(c->reg_log2 <= 10 ? pv_topn_combine : pv_topn_combine_r12, dim3(grid), dim3(PV_CB_THREADS), 0, st,
+                       (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 8), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (P.want_events)
         hipLaunchKernelGGL(pv_xact_compact, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params, grid);
@@ -3272,6 +3484,51 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
     }
     j.end_obj();
     *out = strdup(j.s.c_str());
+    return 0;
+}
+
+int pv_add_static_label(const char *key, const char *value)
+{
+    if (!key || !value || !*key) return PV_EINVAL;
+    std::lock_guard<std::mutex> g(g_static_mu);
+    g_static_labels[key] = value;
+    return 0;
+}
+
+int pv_window_prometheus(pv_ctx *c, uint32_t period, const char *const *label_keys, const char *const *label_values,
+                         uint32_t n_labels, char **out)
+{
+    *out = nullptr;
+    int rc = sync_xvals(c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    flush_fills(c);
+    if (!c->started) return c->fail(PV_EINVAL, "no data");
+    if (c->net2_groups || c->dns2_groups)
+        return c->fail(PV_EUNSUPPORTED, "window_prometheus: the v2 handlers' Prometheus output is not built");
+    if (period >= c->cfg.num_periods)
+        return c->fail(PV_EINVAL, "invalid metrics period, specify [0, %u]", c->cfg.num_periods - 1);
+    Prom p;
+    for (uint32_t i = 0; i < n_labels; i++) {
+        if (!label_keys || !label_values || !label_keys[i] || !label_values[i]) return c->fail(PV_EINVAL, "label %u missing", i);
+        p.add[label_keys[i]] = label_values[i];
+    }
+    std::vector<uint32_t> slots;
+    // each handler's own window (its manager's window_single_prometheus); a handler with
+    // every group disabled writes nothing (AbstractMetricsManager.h:522-524)
+    if (c->net_groups) {
+        if ((rc = window_slots(c, c->net, period, false, slots))) return rc;
+        HostBucket b;
+        if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
+        net_prom(c, p, b);
+    }
+    if (c->dns_groups) {
+        if ((rc = window_slots(c, c->dns, period, false, slots))) return rc;
+        HostBucket b;
+        if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;
+        dns_prom(c, p, b);
+    }
+    *out = strdup(p.o.str().c_str());
     return 0;
 }
 

@@ -309,13 +309,19 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
     for (int probe = 0; probe < PV_PROBES && !done; probe++) {
         uint64_t *kp = &P.tkeys[t.rbase + t.pos];
         uint64_t k = __atomic_load_n(kp, __ATOMIC_RELAXED);
+        uint64_t add = w;
         if (k == 0) {
+            // slot clears reset keys only: an empty entry's count word holds what its last
+            // occupant left, and nobody adds to it before its key is claimed, so the claimer
+            // reads it first (complete before the CAS issues) and adds its weight net of it
+            const uint64_t stale = __atomic_load_n(&P.tcnt[t.rbase + t.pos], __ATOMIC_RELAXED);
+            asm volatile("" ::"v"((uint32_t)stale), "v"((uint32_t)(stale >> 32)) : "memory");
             uint64_t prev = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)key);
-            if (prev == 0) created = (int64_t)(t.rbase + t.pos);
+            if (prev == 0) { created = (int64_t)(t.rbase + t.pos); add = w - stale; }
             k = prev == 0 ? key : prev;
         }
         if (k == key) {
-            atomicAdd((unsigned long long *)&P.tcnt[t.rbase + t.pos], (unsigned long long)w);
+            atomicAdd((unsigned long long *)&P.tcnt[t.rbase + t.pos], (unsigned long long)add);
             done = true;
         } else {
             t.pos = (t.pos + 1) & t.rmask;
@@ -1592,7 +1598,10 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_suffix(const PvParams *
     }
 }
 
-extern "C" __global__ void __launch_bounds__(256) pv_dns_kernel(const PvParams *__restrict__ Pp)
+#ifndef PV_DNS_MINW
+#define PV_DNS_MINW 1 // tuning: waves per SIMD the DNS pass's register allocation must allow
+#endif
+extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ DnsState S;
@@ -1841,6 +1850,17 @@ __device__ __forceinline__ uint32_t log_region(PV_CREF(PvParams) P, uint64_t e0)
 {
     return tregion(P, tkey_hash(e0 & ((1ull << 60) - 1)));
 }
+// run table word: start (24 bits) | count (24 bits) << 24 | the handler's tables << 48
+__device__ __forceinline__ uint64_t pv_run_word(uint32_t start, uint32_t cnt, uint32_t tabs)
+{
+    return (uint64_t)start | (uint64_t)cnt << 24 | (uint64_t)((tabs | tabs >> PV_SLOTS) & 0xffffu) << 48;
+}
+// run key of an entry: its table region, split by handler (Net tables, DNS tables), so a
+// merge workgroup reads only entries of its own handler's tables (one table, usually)
+__device__ __forceinline__ uint32_t run_key(PV_CREF(PvParams) P, uint64_t e0)
+{
+    return (entry_table(e0) / PV_SLOTS) << P.reg_log2 | log_region(P, e0);
+}
 // table key (slot bits kept) of a dense IP log entry: IPv4 drops the card / dir bits
 __device__ __forceinline__ uint64_t ip_tkey(uint64_t e)
 {
@@ -1850,23 +1870,25 @@ __device__ __forceinline__ uint64_t ip_tkey(uint64_t e)
 // Combine: one workgroup per Net/DNS workgroup range aggregates its update log and its
 // records' dense IP entries in an LDS table (key -> weight, smallest record index), so a
 // heavy hitter leaves one entry per range instead of one per packet; entries the table
-// cannot take pass through unchanged. The combined list goes to the workgroup's cb
-// region and its entries are counted per table region.
-#ifndef PV_CB_N
-#define PV_CB_N 8192 // combine: LDS table entries per workgroup (128 KiB: one workgroup per CU)
-#endif
+// cannot take spill to the workgroup's part of tp_buf. Then the workgroup writes its
+// combined list sorted by table region (counting sort in LDS) and publishes, per region,
+// where its run starts and how long it is (cb_run): pv_topn_merge reads each region's runs
+// straight from the lists, so no bucketing pass over the entries is needed.
 #define PV_W_CNT ((1u << 29) - 1) // weight bits of a dense IPv4 entry
+template <uint32_t CN, uint32_t NR>
 struct CombState {
-    uint64_t key[PV_CB_N];
-    uint32_t cnt[PV_CB_N];
-    uint32_t rep[PV_CB_N];
-    uint32_t h[1u << PV_MAX_REGIONS_LOG2];
-    uint32_t nout;
+    uint64_t key[CN];
+    uint32_t cnt[CN];
+    uint32_t rep[CN];
+    uint32_t h[NR];   // entries per region, then the placement cursors
+    uint32_t tb[NR];  // tables (bit per PV_TSLOT) among each region's entries
+    uint32_t st[NR];  // each region's run start in the sorted list
+    uint32_t wsum[16];
+    uint32_t nsp;
 };
 // combined entry (e0 = slot | table key, e1 = weight word | rep << 32) of a cache key;
 // IPv4 cache keys are dense entries (card << 33 | dir << 32 | address)
-__device__ __forceinline__ void comb_out(PV_CREF(PvParams) P, CombState &S, uint64_t *out, uint64_t ck, uint32_t w,
-                                         uint32_t rep)
+__device__ __forceinline__ ulonglong2 comb_entry(uint64_t ck, uint32_t w, uint32_t rep)
 {
     uint64_t e0 = ck;
     if (PV_KEY_METRIC(ck & ((1ull << 60) - 1)) == TM_IPV4 && !PV_IS_V2_IP4(ck & ((1ull << 60) - 1))) {
@@ -1874,15 +1896,21 @@ __device__ __forceinline__ void comb_out(PV_CREF(PvParams) P, CombState &S, uint
         e0 = ip_tkey(ck);
         w = PV_W_IP4 | ((uint32_t)(ck >> 32) & 1u) << 30 | ((uint32_t)(ck >> 33) & 1u) << 29 | (w & PV_W_CNT);
     }
-    const uint32_t k = atomicAdd(&S.nout, 1u);
-    out[2 * (uint64_t)k] = e0;
-    out[2 * (uint64_t)k + 1] = (uint64_t)w | ((uint64_t)rep << 32);
-    atomicAdd(&S.h[log_region(P, e0)], 1u);
+    return make_ulonglong2(e0, (uint64_t)w | ((uint64_t)rep << 32));
 }
-__device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, CombState &S, uint64_t *out, uint64_t ck, uint32_t w,
+template <class St>
+__device__ __forceinline__ void comb_count(PV_CREF(PvParams) P, St &S, uint64_t e0)
+{
+    const uint32_t r = run_key(P, e0);
+    atomicAdd(&S.h[r], 1u);
+    const uint32_t bit = 1u << entry_table(e0);
+    if (!(S.tb[r] & bit)) atomicOr(&S.tb[r], bit);
+}
+template <uint32_t CN, class St>
+__device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, St &S, PV_G ulonglong2 *sp, uint64_t ck, uint32_t w,
                                          uint32_t rep)
 {
-    uint32_t pos = (uint32_t)(fmix64(ck) >> 20) & (PV_CB_N - 1);
+    uint32_t pos = (uint32_t)(fmix64(ck) >> 20) & (CN - 1);
     for (int probe = 0; probe < 16; probe++) {
         uint64_t cur = S.key[pos];
         if (cur == 0) {
@@ -1891,102 +1919,117 @@ __device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, CombState &S, uint
         }
         if (cur == ck) {
             atomicAdd(&S.cnt[pos], w);
-            atomicMin(&S.rep[pos], rep);
+            if (rep < S.rep[pos]) atomicMin(&S.rep[pos], rep);
             return;
         }
-        pos = (pos + 1) & (PV_CB_N - 1);
+        pos = (pos + 1) & (CN - 1);
     }
-    comb_out(P, S, out, ck, w, rep);
+    const ulonglong2 e = comb_entry(ck, w, rep);
+    sp[atomicAdd(&S.nsp, 1u)] = e;
+    comb_count(P, S, e.x);
 }
 
-extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine(const PvParams *__restrict__ Pp)
+// exclusive prefix of v over the workgroup (all threads call it); *total = the sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, uint32_t &total)
 {
-    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ CombState S;
-    const uint32_t nreg = 1u << P.reg_log2;
-    for (uint32_t j = threadIdx.x; j < PV_CB_N; j += blockDim.x) { S.key[j] = 0; S.cnt[j] = 0; S.rep[j] = 0xffffffffu; }
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) S.h[r] = 0;
-    if (threadIdx.x == 0) S.nout = 0;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += t;
+    }
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    uint64_t *out = P.cb + (uint64_t)blockIdx.x * P.mq_cap * 2;
+    uint32_t base = 0, tot = 0;
+    for (uint32_t k = 0; k < nw; k++) {
+        const uint32_t s = wsum[k];
+        if (k < wv) base += s;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return base + incl - v;
+}
+
+template <uint32_t CN, uint32_t NR>
+__device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
+{
+    using St = CombState<CN, NR>;
+    __shared__ St S;
+    const uint32_t nreg = 2u << P.reg_log2; // run keys
+    for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x) { S.key[j] = 0; S.cnt[j] = 0; S.rep[j] = 0xffffffffu; }
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) { S.h[r] = 0; S.tb[r] = 0; }
+    if (threadIdx.x == 0) S.nsp = 0;
+    __syncthreads();
+    const uint64_t wbase = (uint64_t)blockIdx.x * P.mq_cap;
+    PV_G ulonglong2 *sp = reinterpret_cast<PV_G ulonglong2 *>(P.tp_buf) + wbase;
+    PV_G ulonglong2 *out = reinterpret_cast<PV_G ulonglong2 *>(P.cb) + wbase;
     const uint32_t cnt = P.mq_cnt[blockIdx.x];
-    const PV_G uint64_t *q = P.mq + (uint64_t)blockIdx.x * P.mq_cap * 2;
+    const PV_G uint64_t *q = P.mq + wbase * 2;
     batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; },
-               [&](uint64_t, ulonglong2 e) { comb_add(P, S, out, e.x, (uint32_t)e.y, (uint32_t)(e.y >> 32)); });
+               [&](uint64_t, ulonglong2 e) { comb_add<CN>(P, S, sp, e.x, (uint32_t)e.y, (uint32_t)(e.y >> 32)); });
     if (P.net_groups & PV_NET_TOP_IPS_BIT) {
         uint64_t a, z;
         wg_records(P, blockIdx.x, a, z);
         const PV_G uint64_t *ipl = P.iplog + a;
         batched<8>(z - a, [&](uint64_t j) { return ipl[j]; }, [&](uint64_t j, uint64_t e) {
-            if (e) comb_add(P, S, out, e, 1u, (uint32_t)(a + j));
+            if (e) comb_add<CN>(P, S, sp, e, 1u, (uint32_t)(a + j));
         });
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < PV_CB_N; j += blockDim.x)
-        if (S.key[j]) comb_out(P, S, out, S.key[j], S.cnt[j], S.rep[j]);
+    // the table's entries per region (the spilled ones were counted as they spilled)
+    for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x)
+        if (S.key[j]) comb_count(P, S, comb_entry(S.key[j], S.cnt[j], S.rep[j]).x);
     __syncthreads();
-    // the workgroup's region counts, for pv_topn_scatter's reservations
-    PV_G uint32_t *hc = P.cb_h + (uint64_t)blockIdx.x * nreg;
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) {
-        hc[r] = S.h[r];
-        if (S.h[r]) atomicAdd(&P.tp_cnt[r], S.h[r]);
-    }
-    if (threadIdx.x == 0) P.cb_cnt[blockIdx.x] = S.nout;
-}
-
-// exclusive scan of the region counts (one workgroup)
-extern "C" __global__ void __launch_bounds__(1024) pv_topn_scan(const PvParams *__restrict__ Pp)
-{
-    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ uint32_t part[1024];
-    const uint32_t nreg = 1u << P.reg_log2;
-    const uint32_t per = (nreg + 1023) / 1024;
-    const uint32_t r0 = threadIdx.x * per;
+    // region run starts: each thread scans a contiguous share of the regions
+    const uint32_t per = (nreg + blockDim.x - 1) / blockDim.x;
+    const uint32_t r0 = min(threadIdx.x * per, nreg), r1 = min(r0 + per, nreg);
     uint32_t s = 0;
-    for (uint32_t r = r0; r < r0 + per && r < nreg; r++) s += P.tp_cnt[r];
-    part[threadIdx.x] = s;
+    for (uint32_t r = r0; r < r1; r++) s += S.h[r];
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, S.wsum, total);
+    // handlers with entries in this batch (pv_topn_merge's workgroups of the other exit early)
+    if (threadIdx.x < 2) {
+        const uint32_t half = 1u << P.reg_log2;
+        uint32_t any = 0;
+        for (uint32_t r = threadIdx.x * half; r < (threadIdx.x + 1) * half && !any; r++) any = S.h[r];
+        if (any) atomicOr(P.tp_hands, 1u << threadIdx.x);
+    }
+    // this workgroup's column of the run table: [run key][XCD][workgroup / 8], so the
+    // workgroups of one XCD (blockIdx % 8) fill whole lines of its L2
+    const uint32_t ng8 = (P.grid_main + 7) / 8;
+    PV_G uint64_t *col = P.cb_run + (blockIdx.x % 8) * ng8 + blockIdx.x / 8;
+    for (uint32_t r = r0; r < r1; r++) {
+        const uint32_t c = S.h[r];
+        S.st[r] = run;
+        col[(uint64_t)r * 8 * ng8] = pv_run_word(run, c, S.tb[r]);
+        S.h[r] = run; // the placement cursor
+        run += c;
+    }
     __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-        const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - s;
-    for (uint32_t r = r0; r < r0 + per && r < nreg; r++) {
-        P.tp_off[r] = run;
-        P.tp_fill[r] = run;
-        run += P.tp_cnt[r];
-    }
+    for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x)
+        if (S.key[j]) {
+            const ulonglong2 e = comb_entry(S.key[j], S.cnt[j], S.rep[j]);
+            out[atomicAdd(&S.h[run_key(P, e.x)], 1u)] = e;
+        }
+    // spilled entries (this workgroup's own writes: same CU, coherent after the barrier)
+    const uint32_t nsp = S.nsp;
+    batched<8>(nsp, [&](uint64_t j) { return sp[j]; },
+               [&](uint64_t, ulonglong2 e) { out[atomicAdd(&S.h[run_key(P, e.x)], 1u)] = e; });
+    if (threadIdx.x == 0) P.cb_cnt[blockIdx.x] = total;
 }
-
-extern "C" __global__ void __launch_bounds__(256) pv_topn_scatter(const PvParams *__restrict__ Pp)
+// LDS: an 8192-entry table with up to 2^10 regions per table (152 KiB), 2048 entries with
+// more (128 KiB); two run keys per region
+extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ uint32_t h[1u << PV_MAX_REGIONS_LOG2];
-    __shared__ uint32_t tb[1u << PV_MAX_REGIONS_LOG2]; // tables (bit per PV_TSLOT) with updates in each region
-    const uint32_t nreg = 1u << P.reg_log2;
-    // reserve this workgroup's share of every region (counts from pv_topn_combine), then
-    // one pass over its combined entries: place each, note the tables each region touches
-    const PV_G uint32_t *hc = P.cb_h + (uint64_t)blockIdx.x * nreg;
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) {
-        const uint32_t c = hc[r];
-        h[r] = c ? atomicAdd(&P.tp_fill[r], c) : 0u;
-        tb[r] = 0;
-    }
-    __syncthreads();
-    const uint32_t cnt = P.cb_cnt[blockIdx.x];
-    const PV_G uint64_t *q = P.cb + (uint64_t)blockIdx.x * P.mq_cap * 2;
-    batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
-        const uint32_t r = log_region(P, e.x);
-        const uint32_t pos = atomicAdd(&h[r], 1u);
-        reinterpret_cast<PV_G ulonglong2 *>(P.tp_buf)[pos] = e;
-        const uint32_t bit = 1u << entry_table(e.x);
-        if (!(tb[r] & bit)) atomicOr(&tb[r], bit);
-    });
-    __syncthreads();
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x)
-        if (tb[r]) atomicOr(&P.tp_tabs[r], tb[r]);
+    topn_combine<8192, 2048>(P);
+}
+extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine_r12(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    topn_combine<2048, 2u << PV_MAX_REGIONS_LOG2>(P);
 }
 
 struct MergeState {
@@ -1997,17 +2040,63 @@ struct MergeState {
     uint32_t nrep[PV_RS];
     uint32_t nnew, nbase, ncr;
 };
+// The region's runs in the combine workgroups' region-sorted lists (cb_run): run w holds
+// entries [pref[w], pref[w+1]) of the region, from list w at start[w].
+struct MergeRuns {
+    uint32_t start[PV_MAX_GRID + 8];
+    uint32_t list[PV_MAX_GRID + 8];
+    uint32_t pref[PV_MAX_GRID + 9];
+    uint32_t wsum[16];
+    uint32_t tabs;
+};
 
 extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    const uint32_t r = blockIdx.x;
-    const uint32_t n = P.tp_cnt[r];
+    const uint32_t rk = blockIdx.x;                  // run key: handler << reg_log2 | region
+    const uint32_t r = rk & ((1u << P.reg_log2) - 1);
+    const uint32_t hd = rk >> P.reg_log2;            // 0 Net tables, 1 DNS tables
+    if (!((*P.tp_hands >> hd) & 1)) return; // no entry of this handler in the batch
+    __shared__ MergeRuns U;
+    const uint32_t ng8 = (P.grid_main + 7) / 8, ng = 8 * ng8;
+    uint32_t n;
+    {
+        uint32_t c = 0, tb = 0;
+        if (threadIdx.x == 0) U.tabs = 0;
+        if (threadIdx.x < ng) {
+            const uint32_t w = (threadIdx.x % ng8) * 8 + threadIdx.x / ng8; // the combine workgroup
+            if (w < P.grid_main) {
+                const uint64_t v = P.cb_run[(uint64_t)rk * ng + threadIdx.x];
+                U.start[threadIdx.x] = (uint32_t)v & 0xffffffu;
+                U.list[threadIdx.x] = w;
+                c = (uint32_t)(v >> 24) & 0xffffffu;
+                tb = (uint32_t)(v >> 48);
+            }
+        }
+        uint32_t total;
+        const uint32_t pre = block_excl_scan(c, U.wsum, total);
+        if (threadIdx.x < ng) U.pref[threadIdx.x] = pre;
+        if (threadIdx.x == 0) U.pref[ng] = total;
+        if (tb) atomicOr(&U.tabs, tb);
+        __syncthreads();
+        n = total;
+    }
     if (n == 0) return;
-    const PV_G uint64_t *q = P.tp_buf + 2 * (uint64_t)P.tp_off[r];
+    // entry j of the region: its run by binary search over the run prefixes
+    uint32_t top = 1;
+    while (top * 2 < ng) top *= 2;
+    const PV_G ulonglong2 *cb = reinterpret_cast<const PV_G ulonglong2 *>(P.cb);
+    auto ld = [&](uint64_t j) -> ulonglong2 {
+        uint32_t lo = 0;
+        for (uint32_t st = top; st; st >>= 1) {
+            const uint32_t m = lo + st;
+            if (m < ng && U.pref[m] <= (uint32_t)j) lo = m;
+        }
+        return cb[(uint64_t)U.list[lo] * P.mq_cap + U.start[lo] + ((uint32_t)j - U.pref[lo])];
+    };
     if (n <= PV_MERGE_DIRECT) {
         for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            const ulonglong2 e = PV_E16(q)[j];
+            const ulonglong2 e = ld(j);
             const uint64_t e0 = e.x, e1 = e.y;
             const uint32_t s = (uint32_t)(e0 >> 60), w = (uint32_t)e1, rep = (uint32_t)(e1 >> 32);
             const uint64_t key = e0 & ((1ull << 60) - 1);
@@ -2025,7 +2114,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
     const uint32_t rsl = P.tcap_log2 - P.reg_log2;
     const uint32_t rs = 1u << rsl;
     static_assert(PV_TABLES <= 32, "table mask");
-    uint32_t tabs = P.tp_tabs[r]; // the tables pv_topn_scatter saw in this region's updates
+    uint32_t tabs = U.tabs << (hd * PV_SLOTS); // the tables among this run key's entries
     const bool one = !(tabs & (tabs - 1));
     while (tabs) {
         const uint32_t tb = __builtin_ctz(tabs);
@@ -2035,13 +2124,13 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         batched<4>(rs, [&](uint64_t i) { return make_ulonglong2(P.tkeys[rbase + i], P.tcnt[rbase + i]); },
                    [&](uint64_t i, ulonglong2 kc) {
                        S.key[i] = kc.x;
-                       S.cnt[i] = kc.y;
+                       S.cnt[i] = kc.x ? kc.y : 0; // an empty entry's count word is stale
                        S.mn[0][i] = 0xffffffffu;
                        S.mn[1][i] = 0xffffffffu;
                    });
         if (threadIdx.x == 0) { S.nnew = 0; S.ncr = 0; }
         __syncthreads();
-        batched<8>(n, [&](uint64_t j) { return PV_E16(q)[j]; }, [&](uint64_t, ulonglong2 e) {
+        batched<8>(n, ld, [&](uint64_t, ulonglong2 e) {
             const uint64_t e0 = e.x;
             if (!one && entry_table(e0) != tb) return;
             const uint64_t e1 = e.y;
@@ -2192,8 +2281,10 @@ extern "C" __global__ void pv_topn_compact(const PvParams *__restrict__ Pp, uint
     const uint8_t *arena = P.arena + (uint64_t)tb * P.arena_cap;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < tcap; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t at = ((uint64_t)tb << P.tcap_log2) + i;
+        const uint64_t key = P.tkeys[at];
+        if (!key || PV_KEY_METRIC(key) == TM_IPV4) continue; // IPv4 entries have no name (stale aux)
         const uint32_t aux = P.taux[at];
-        if (!P.tkeys[at] || !aux) continue;
+        if (!aux) continue;
         const uint64_t part = (aux - 1) / pcap;
         const uint8_t *src = arena + (aux - 1);
         const uint32_t len = src[0] | (src[1] << 8);
@@ -2311,7 +2402,10 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
             wb = __shfl(wb, 0, 64);
             const bool room = wb + tot4 <= pcap;
             if (!room) {
-                if (act) atomicOr(P.flags, PVF_ARENA_FULL);
+                if (act) {
+                    atomicOr(P.flags, PVF_ARENA_FULL);
+                    P.taux[e.pos] = 0;
+                }
             } else {
                 uint8_t *arena = P.arena + (uint64_t)s0 * P.arena_cap + part * pcap + wb;
                 if (packed) {
@@ -2332,6 +2426,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                                            (unsigned long long)((size + 3) & ~3u));
             if (pos + size > pcap) {
                 atomicOr(P.flags, PVF_ARENA_FULL);
+                P.taux[e.pos] = 0;
             } else {
                 emit_to(P.arena + (uint64_t)e.slot * P.arena_cap + part * pcap + pos);
                 P.taux[e.pos] = (uint32_t)(part * pcap + pos) + 1;

@@ -148,6 +148,7 @@ enum {
 // can own a region outright and merge a batch's updates into it in LDS.
 #define PV_REGION_LOG2 12
 #define PV_CB_THREADS 1024 // pv_topn_combine workgroup size
+#define PV_MAX_GRID 1024   // Net/DNS-pass workgroups per batch (pv_topn_merge's run table)
 #define PV_MAX_REGIONS_LOG2 12 // table_log2 <= PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2
 #define PV_PROBES 256
 // entry of the new-name list (pv_topn_merge -> pv_topn_names)
@@ -363,24 +364,21 @@ struct PvParams {
     PV_G uint64_t *dq;    // per-workgroup DNS work lists (32-B DnsMsg), region = wt_per_block * 64
     PV_G uint32_t *dq_cnt;
     PV_G uint32_t *n_dns; // DNS messages found by the Net pass (status word)
-    // top-N merge: regions per slot table (log2), per-region update counts / offsets /
-    // fill pointers into the region-sorted update buffer, and the new-name list
+    // top-N merge: regions per slot table (log2), the run table and the new-name list
     uint32_t reg_log2;
-    PV_G uint32_t *tp_cnt;
-    PV_G uint32_t *tp_off;
-    PV_G uint32_t *tp_fill;
-    PV_G uint32_t *tp_tabs; // per region: bit t set when the region's updates touch table t
-    PV_G uint32_t *cb_h;    // per combine workgroup: its entries per region
+    PV_G uint32_t *tp_hands; // status word: bit h set when handler h (0 Net, 1 DNS) has top-N entries
+    PV_G uint64_t *cb_run;  // [run key][XCD][combine workgroup / 8]: the workgroup's run of that
+                            // run key in its sorted list (start | count << 24 | tables << 48)
     PV_G uint32_t *tab_live; // per table: entries held (bounded by pv_topn_purge)
     uint32_t net2_groups;   // Net v2 handler attached: PV_N2G_* group bits | PV_N2G_ON (0 = not attached)
     uint32_t dns2_groups;   // DNS v2 in place of v1: PV_D2G_* group bits | PV_N2G_ON (0 = DNS v1)
-    PV_G uint64_t *tp_buf;
+    PV_G uint64_t *tp_buf; // pv_topn_combine: entries its LDS table could not take (spill)
     PV_G uint32_t *nn_cnt;
     PV_G PvNewName *nn;
     uint32_t nn_cap;
     PV_G uint64_t *iplog; // dense IP log: one entry per record of the batch (Net pass)
     PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
-    PV_G uint64_t *cb;    // combined update lists, one region of mq_cap entries per workgroup
+    PV_G uint64_t *cb;    // combined update lists sorted by table region, mq_cap entries per workgroup
     PV_G uint32_t *cb_cnt;
     uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane,
                   // 16 no DNS name decode, 32 no DNS table updates
