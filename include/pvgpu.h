@@ -294,13 +294,16 @@ int pv_reset(pv_ctx *ctx);
 int pv_window_json(pv_ctx *ctx, uint32_t period, int merged, char **out);
 void pv_free(void *p);
 
-/* Prometheus text exposition of bucket `period` (0 = live) of each attached v1 handler,
- * Net ("packets_*") then DNS ("dns_*"), in the reference's metric order, names, HELP texts
- * and number formatting; labels: the static labels, then these n_labels added ones (each
- * set in key order). Rates are timer-driven and not kept: nothing is written for them, as
- * for an empty Rate. The v2 handlers are refused (PV_EUNSUPPORTED). *out: pv_free. */
-int pv_window_prometheus(pv_ctx *ctx, uint32_t period, const char *const *label_keys, const char *const *label_values,
-                         uint32_t n_labels, char **out);
+/* Prometheus text exposition of bucket `period` (0 = live) of the v1 handlers selected by
+ * `handlers` (PV_HANDLER_NET: "packets_*", PV_HANDLER_DNS: "dns_*"; both: Net then DNS), in
+ * the reference's metric order, names, HELP texts and number formatting; labels: the static
+ * labels, then these n_labels added ones (each set in key order). Rates are timer-driven and
+ * not kept: nothing is written for them, as for an empty Rate. The v2 handlers are refused
+ * (PV_EUNSUPPORTED). *out: pv_free. */
+#define PV_HANDLER_NET 1u
+#define PV_HANDLER_DNS 2u
+int pv_window_prometheus(pv_ctx *ctx, uint32_t period, uint32_t handlers, const char *const *label_keys,
+                         const char *const *label_values, uint32_t n_labels, char **out);
 /* Process-wide label on every Prometheus sample (Metric::add_static_label). */
 int pv_add_static_label(const char *key, const char *value);
 

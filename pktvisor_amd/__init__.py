@@ -204,8 +204,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_synchronize.argtypes = [P]
     lib.pv_reset.argtypes = [P]
     lib.pv_window_json.argtypes = [P, U32, ctypes.c_int, ctypes.POINTER(P)]
-    lib.pv_window_prometheus.argtypes = [P, U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), U32,
-                                         ctypes.POINTER(P)]
+    lib.pv_window_prometheus.argtypes = [P, U32, U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                         U32, ctypes.POINTER(P)]
     lib.pv_add_static_label.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     lib.pv_free.argtypes = [P]
     lib.pv_free.restype = None
@@ -507,14 +507,16 @@ class PvHandlers:
         self.lib.pv_free(out)
         return json.loads(txt)
 
-    def window_prometheus(self, period: int = 0, labels: Optional[dict] = None) -> str:
+    def window_prometheus(self, period: int = 0, labels: Optional[dict] = None, handlers: str = "net,dns") -> str:
         """StreamHandler::window_prometheus (src/AbstractMetricsManager.h:506-531): the
-        Prometheus text of bucket `period`, with `labels` added to every sample."""
+        Prometheus text of bucket `period` of the named handlers ("net", "dns"), with
+        `labels` added to every sample."""
+        hmask = sum({"net": 1, "dns": 2}[x] for x in handlers.split(","))
         labels = labels or {}
         keys = (ctypes.c_char_p * max(1, len(labels)))(*[k.encode() for k in labels])
         vals = (ctypes.c_char_p * max(1, len(labels)))(*[str(v).encode() for v in labels.values()])
         out = ctypes.c_void_p()
-        self._check(self.lib.pv_window_prometheus(self.ctx, period, keys, vals, len(labels), ctypes.byref(out)),
+        self._check(self.lib.pv_window_prometheus(self.ctx, period, hmask, keys, vals, len(labels), ctypes.byref(out)),
                     "pv_window_prometheus")
         txt = ctypes.string_at(out.value).decode()
         self.lib.pv_free(out)

@@ -2349,7 +2349,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     hipLaunchKernelGGL(c->reg_log2 <= 10 ? pv_topn_combine : pv_topn_combine_r12, dim3(grid), dim3(PV_CB_THREADS), 0, st,
                        (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);
-    hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 8), dim3(256), 0, st, (const PvParams *)c->d_params);
+    // names: as many workgroups as are resident (LDS: two per CU), each pipelining its entries
+    hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 2), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (P.want_events)
         hipLaunchKernelGGL(pv_xact_compact, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params, grid);
     if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch");
@@ -3495,8 +3496,8 @@ int pv_add_static_label(const char *key, const char *value)
     return 0;
 }
 
-int pv_window_prometheus(pv_ctx *c, uint32_t period, const char *const *label_keys, const char *const *label_values,
-                         uint32_t n_labels, char **out)
+int pv_window_prometheus(pv_ctx *c, uint32_t period, uint32_t handlers, const char *const *label_keys,
+                         const char *const *label_values, uint32_t n_labels, char **out)
 {
     *out = nullptr;
     int rc = sync_xvals(c);
@@ -3516,13 +3517,13 @@ int pv_window_prometheus(pv_ctx *c, uint32_t period, const char *const *label_ke
     std::vector<uint32_t> slots;
     // each handler's own window (its manager's window_single_prometheus); a handler with
     // every group disabled writes nothing (AbstractMetricsManager.h:522-524)
-    if (c->net_groups) {
+    if ((handlers & PV_HANDLER_NET) && c->net_groups) {
         if ((rc = window_slots(c, c->net, period, false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
         net_prom(c, p, b);
     }
-    if (c->dns_groups) {
+    if ((handlers & PV_HANDLER_DNS) && c->dns_groups) {
         if ((rc = window_slots(c, c->dns, period, false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;

@@ -814,7 +814,7 @@ __device__ void cache_flush(PV_CREF(PvParams) P, Cache &C, uint32_t n, uint32_t 
 #define PV_WT 64      // records per wave tile
 #define PV_WSTAGE 8192 // DNS pass: LDS staging bytes per wave (128-B message windows)
 #ifndef PV_NCACHE
-#define PV_NCACHE 1024
+#define PV_NCACHE 2048
 #endif
 static_assert(PV_NCACHE <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cache entries per flush");
 
@@ -2315,34 +2315,38 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
     uint8_t *O = reinterpret_cast<uint8_t *>(obuf[threadIdx.x >> 6]);
     const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
     const GAcc G{P.recs};
-    for (uint32_t b = blockIdx.x * blockDim.x; b < n; b += gridDim.x * blockDim.x) {
-        const uint32_t i = b + threadIdx.x;
+    // Software pipeline over the lane's entries i, i + step, ...: the window of the next entry
+    // and the table key / record offset of the one after are loaded while this entry's arena
+    // reservation (a returning atomic the wave waits for anyway) is in flight, and the new-name
+    // record two ahead right after it, so each iteration waits for memory once.
+    const uint32_t step = gridDim.x * blockDim.x;
+    auto ld_e = [&](uint32_t j) { return j < n ? P.nn[j] : PvNewName{0, 0, 0}; };
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    PvNewName e = ld_e(i);
+    uint64_t tkey = i < n ? P.tkeys[e.pos] : 0, roff = i < n ? P.offs[e.rep] : 0;
+    uint4 pf[PV_NWIN / 16];
+    auto ld_win = [&](uint64_t ro, bool a) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + (ro & ~15ull));
+#pragma unroll
+        for (int j = 0; j < PV_NWIN / 16; j++) pf[j] = a ? src[j] : make_uint4(0, 0, 0, 0);
+    };
+    ld_win(roff, i < n);
+    PvNewName e_n = ld_e(i + step);
+    uint64_t tkey_n = i + step < n ? P.tkeys[e_n.pos] : 0, roff_n = i + step < n ? P.offs[e_n.rep] : 0;
+    PvNewName e_nn = ld_e(i + 2 * step);
+    for (uint32_t b = blockIdx.x * blockDim.x; b < n; b += step, i += step) {
         const bool act = i < n;
-        PvNewName e{0, 0, 0};
-        uint64_t tkey = 0;
-        uint32_t metric = 0, size = 0, start = 0, nl = 0, mlen = 0;
+        const uint32_t metric = PV_KEY_METRIC(tkey);
+        uint32_t size = 0, start = 0, nl = 0, mlen = 0;
         uint64_t m = 0, a6 = 0;
         Parsed o;
-        uint64_t roff = 0;
-        if (act) {
-            e = P.nn[i];
-            tkey = P.tkeys[e.pos];
-            metric = PV_KEY_METRIC(tkey);
-            roff = P.offs[e.rep];
-        }
         const uint64_t wbase = roff & ~15ull;
-        {
-            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + wbase);
-            uint4 pf[PV_NWIN / 16];
 #pragma unroll
-            for (int j = 0; j < PV_NWIN / 16; j++) pf[j] = act ? src[j] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < PV_NWIN / 16; j++) {
-                L[(4 * j + 0) * 64 + lane] = pf[j].x;
-                L[(4 * j + 1) * 64 + lane] = pf[j].y;
-                L[(4 * j + 2) * 64 + lane] = pf[j].z;
-                L[(4 * j + 3) * 64 + lane] = pf[j].w;
-            }
+        for (int j = 0; j < PV_NWIN / 16; j++) {
+            L[(4 * j + 0) * 64 + lane] = pf[j].x;
+            L[(4 * j + 1) * 64 + lane] = pf[j].y;
+            L[(4 * j + 2) * 64 + lane] = pf[j].z;
+            L[(4 * j + 3) * 64 + lane] = pf[j].w;
         }
         const TAcc R{P.recs, L, wbase, PV_NWIN - 4, 64u, lane};
         if (act) {
@@ -2385,6 +2389,10 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
         const uint32_t s0 = __shfl(e.slot, 0, 64);
         const bool uniform = __all(!act || e.slot == s0);
         const bool packed = uniform && tot4 <= PV_NOUT;
+        // prefetch (see above): issued before the reservation, whose wait covers them
+        const uint32_t i_n = i + step, i_nn = i + 2 * step;
+        ld_win(roff_n, i_n < n);
+        const uint64_t tkey_nn = i_nn < n ? P.tkeys[e_nn.pos] : 0, roff_nn = i_nn < n ? P.offs[e_nn.rep] : 0;
         auto emit_to = [&](uint8_t *dst) {
             const uint32_t slen = size - 2;
             dst[0] = (uint8_t)(slen & 0xff);
@@ -2432,6 +2440,9 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 P.taux[e.pos] = (uint32_t)(part * pcap + pos) + 1;
             }
         }
+        e = e_n; tkey = tkey_n; roff = roff_n;
+        e_n = e_nn; tkey_n = tkey_nn; roff_n = roff_nn;
+        e_nn = ld_e(i + 3 * step);
     }
 }
 

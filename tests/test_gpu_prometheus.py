@@ -50,7 +50,7 @@ def parse(txt):
             continue
         m = SAMPLE.match(ln)
         assert m, ln
-        labels = dict(re.findall(r'([a-z_]+)="([^"]*)"', m.group(2)))
+        labels = dict(re.findall(r'([a-z0-9_]+)="([^"]*)"', m.group(2)))
         out.append((m.group(1), labels, m.group(3), m.group(2)))
         i += 1
     return out, heads
@@ -151,5 +151,24 @@ def test_prometheus_groups_and_errors():
         h.process_host(recs)
         with pytest.raises(pa.PvError, match=r"invalid metrics period, specify \[0, 1\]"):
             h.window_prometheus(2)
+    finally:
+        h.close()
+
+
+def test_prometheus_per_handler():
+    """each plugin alias renders only its own schema key (one StreamHandler per alias)"""
+    path = os.path.join(GOLD, "dns_ipv4_udp.pcap")
+    linktype, ts_nano, recs = pa.read_pcap(path)
+    h = pa.PvHandlers(host_spec="192.168.0.0/24", num_periods=1, linktype=linktype, ts_nano=ts_nano, max_records=1024)
+    try:
+        h.process_host(recs)
+        both = h.window_prometheus(0, {"policy": "p"})
+        net = h.window_prometheus(0, {"policy": "p"}, handlers="net")
+        dns = h.window_prometheus(0, {"policy": "p"}, handlers="dns")
+        assert net and dns and net + dns == both
+        def names(txt):
+            return [ln.split(" ")[2] if ln.startswith("#") else ln.split("{")[0] for ln in txt.splitlines()]
+        assert names(net) and all(x.startswith("packets_") for x in names(net))
+        assert names(dns) and all(x.startswith("dns_") for x in names(dns))
     finally:
         h.close()
