@@ -30,6 +30,8 @@
  *   pv_window_prometheus .......... StreamHandler::window_prometheus(out, add_labels)
  *                                   (src/StreamHandler.h:71-77, AbstractMetricsManager.h:506-531;
  *                                    NetStreamHandler.cpp:332-388, DnsStreamHandler.cpp:1139-1238)
+ *   pv_window_opentelemetry ....... StreamHandler::window_opentelemetry(scope, start, end, add_labels)
+ *                                   (AbstractMetricsManager.h:533-575; Metrics.cpp:22-36,82-96)
  *   pv_add_static_label ........... Metric::add_static_label (src/Metrics.h, Metrics.cpp:129-155)
  *   pv_state_* / pv_reduce_* ...... the bucket merge (AbstractMetricsBucket::merge,
  *                                   AbstractMetricsManager.h:177-195) split into
@@ -304,6 +306,12 @@ void pv_free(void *p);
 #define PV_HANDLER_DNS 2u
 int pv_window_prometheus(pv_ctx *ctx, uint32_t period, uint32_t handlers, const char *const *label_keys,
                          const char *const *label_values, uint32_t n_labels, char **out);
+/* OpenTelemetry metrics of bucket `period` of the selected v1 handlers, as the protobuf
+ * wire bytes of the ScopeMetrics fields the reference's primitives fill (the repeated
+ * `metrics`, in the handlers' order): append them to a ScopeMetrics with MergeFromString.
+ * Attributes: the n_labels added labels. *out: pv_free. */
+int pv_window_opentelemetry(pv_ctx *ctx, uint32_t period, uint32_t handlers, const char *const *label_keys,
+                            const char *const *label_values, uint32_t n_labels, uint8_t **out, size_t *bytes);
 /* Process-wide label on every Prometheus sample (Metric::add_static_label). */
 int pv_add_static_label(const char *key, const char *value);
 

@@ -161,7 +161,8 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_values_merge", "pv_window_periods", "pv_set_dns_filters", "pv_dns_code", "pv_advance_windows",
            "pv_dns_event_seconds", "pv_dns_event_seconds_host", "pv_comm_unique_id", "pv_comm_init",
            "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count",
-           "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label"]
+           "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label",
+           "pv_window_opentelemetry"]
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
 
@@ -207,6 +208,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_window_prometheus.argtypes = [P, U32, U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
                                          U32, ctypes.POINTER(P)]
     lib.pv_add_static_label.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    lib.pv_window_opentelemetry.argtypes = [P, U32, U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                            U32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_free.argtypes = [P]
     lib.pv_free.restype = None
     lib.pv_state_regions.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(P),
@@ -521,6 +524,21 @@ class PvHandlers:
         txt = ctypes.string_at(out.value).decode()
         self.lib.pv_free(out)
         return txt
+
+    def window_opentelemetry(self, period: int = 0, labels: Optional[dict] = None, handlers: str = "net,dns") -> bytes:
+        """StreamHandler::window_opentelemetry (src/AbstractMetricsManager.h:533-575): the
+        protobuf bytes of the ScopeMetrics `metrics` the named handlers add for bucket
+        `period`, with `labels` as attributes."""
+        labels = labels or {}
+        hmask = sum({"net": 1, "dns": 2}[x] for x in handlers.split(","))
+        keys = (ctypes.c_char_p * max(1, len(labels)))(*[k.encode() for k in labels])
+        vals = (ctypes.c_char_p * max(1, len(labels)))(*[str(v).encode() for v in labels.values()])
+        out, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self.lib.pv_window_opentelemetry(self.ctx, period, hmask, keys, vals, len(labels), ctypes.byref(out),
+                                                     ctypes.byref(n)), "pv_window_opentelemetry")
+        data = ctypes.string_at(out.value, n.value)
+        self.lib.pv_free(out)
+        return data
 
     def state_regions(self):
         sp, mp = ctypes.c_void_p(), ctypes.c_void_p()

@@ -1281,9 +1281,171 @@ struct Prom {
     }
 };
 
+// ---- OpenTelemetry (window_single_opentelemetry, src/AbstractMetricsManager.h:533-575): the
+// metrics the reference's primitives add to a ScopeMetrics (src/Metrics.cpp:22-36,82-96;
+// src/Metrics.h:289-327,450-481,523-533,693-769), as protobuf wire bytes of the ScopeMetrics
+// fields they fill (repeated `metrics`, field 2), serialized as protobuf does: fields in
+// number order, proto3 defaults omitted, oneof members always written, packed repeated
+// scalars. Messages of opentelemetry-proto metrics/v1 (the reference links
+// opentelemetry-cpp 1.17.0's opentelemetry_proto; not vendored, field numbers restated):
+// Metric{name 1, description 2, gauge 5, histogram 9, summary 11}; Gauge/Summary/Histogram
+// {data_points 1; Histogram.aggregation_temporality 2}; NumberDataPoint{start 2, time 3,
+// as_int 6, attributes 7}; SummaryDataPoint{start 2, time 3, quantile_values 6, attributes 7};
+// ValueAtQuantile{quantile 1, value 2}; HistogramDataPoint{start 2, time 3, count 4,
+// bucket_counts 6, explicit_bounds 7, attributes 9}; KeyValue{key 1, value 2};
+// AnyValue{string_value 1}. Attributes are the added labels only (no static labels).
+struct Pb {
+    std::string s;
+    void varint(uint64_t v)
+    {
+        while (v >= 0x80) { s.push_back((char)(uint8_t)(v | 0x80)); v >>= 7; }
+        s.push_back((char)(uint8_t)v);
+    }
+    void tag(uint32_t f, uint32_t wt) { varint((uint64_t)f << 3 | wt); }
+    void bytes(uint32_t f, const std::string &v) { tag(f, 2); varint(v.size()); s += v; }
+    void str(uint32_t f, const std::string &v) { if (!v.empty()) bytes(f, v); }
+    void fx64(uint32_t f, uint64_t v, bool always = false)
+    {
+        if (!v && !always) return;
+        tag(f, 1);
+        s.append(reinterpret_cast<const char *>(&v), 8);
+    }
+    void dbl(uint32_t f, double v)
+    {
+        uint64_t u;
+        memcpy(&u, &v, 8);
+        fx64(f, u);
+    }
+    void enm(uint32_t f, uint32_t v) { if (v) { tag(f, 0); varint(v); } }
+};
+struct Otlp {
+    Pb out; // ScopeMetrics fields
+    PromLabels add;
+    uint64_t t0 = 0, t1 = 0;
+    std::string attrs(uint32_t f, const PromLabels &l) const
+    {
+        Pb p;
+        for (auto &kv : l) {
+            Pb any, kvm;
+            any.bytes(1, kv.second); // oneof string_value: written even when empty
+            kvm.str(1, kv.first);
+            kvm.bytes(2, any.s);
+            p.bytes(f, kvm.s);
+        }
+        return p.s;
+    }
+    std::string number_point(const PromLabels &l, int64_t v) const
+    {
+        Pb d;
+        d.fx64(2, t0);
+        d.fx64(3, t1);
+        d.fx64(6, (uint64_t)v, true); // oneof as_int
+        d.s += attrs(7, l);
+        return d.s;
+    }
+    void metric(const std::string &name, const char *desc, uint32_t field, const std::string &data, bool has_data = true)
+    {
+        Pb m;
+        m.str(1, name);
+        m.str(2, desc);
+        if (has_data) m.bytes(field, data);
+        out.bytes(2, m.s);
+    }
+    // Counter / Cardinality: a gauge of one int point
+    template <typename V>
+    void gauge(const std::string &name, const char *desc, V v)
+    {
+        Pb g;
+        g.bytes(1, number_point(add, (int64_t)v));
+        metric(name, desc, 5, g.s);
+    }
+    // Quantile: a summary point with the four quantiles (no count / sum, as the reference)
+    template <typename T>
+    void summary(const std::string &name, const char *desc, const std::vector<T> &q, T, uint64_t)
+    {
+        if (q.empty()) return;
+        static const double fr[4] = {0.50, 0.90, 0.95, 0.99};
+        Pb d;
+        d.fx64(2, t0);
+        d.fx64(3, t1);
+        for (int i = 0; i < 4; i++) {
+            Pb qv;
+            qv.dbl(1, fr[i]);
+            qv.dbl(2, (double)q[i]);
+            d.bytes(6, qv.s);
+        }
+        d.s += attrs(7, add);
+        Pb sm;
+        sm.bytes(1, d.s);
+        metric(name, desc, 11, sm.s);
+    }
+    // TopN: one gauge point per reported item (items with an empty name are skipped)
+    void topn(const std::string &name, const char *item_key, const char *desc,
+              const std::vector<std::pair<std::string, uint64_t>> &v0, size_t n, uint32_t pct)
+    {
+        auto v = v0;
+        std::sort(v.begin(), v.end(), [](const auto &a, const auto &b) {
+            if (a.second != b.second) return a.second > b.second;
+            return a.first < b.first;
+        });
+        const size_t k = std::min(n, v.size());
+        if (!k) return;
+        std::vector<uint64_t> est;
+        for (size_t i = 0; i < k; i++) est.push_back(v[i].second);
+        std::sort(est.begin(), est.end());
+        const uint64_t w = (uint64_t)std::ceil((double)pct / 100.0 * (double)k);
+        const uint64_t thr = est[w == 0 ? 0 : std::min<size_t>(w - 1, k - 1)];
+        PromLabels l(add);
+        Pb g;
+        bool any = false;
+        for (size_t i = 0; i < k && v[i].second >= thr; i++) {
+            if (v[i].first.empty()) continue;
+            l[item_key] = v[i].first;
+            g.bytes(1, number_point(l, (int64_t)v[i].second));
+            any = true;
+        }
+        metric(name, desc, 5, g.s, any);
+    }
+    // Histogram: bounds at the listed split points, bucket_counts as the reference computes
+    // them (static_cast<uint64_t>(cdf) * n: n where the CDF reached 1, else 0)
+    void histogram(const std::string &name, const char *desc, std::vector<uint64_t> v)
+    {
+        if (v.empty()) return;
+        std::sort(v.begin(), v.end());
+        const uint64_t n = v.size();
+        std::vector<uint64_t> cnt;
+        std::vector<double> bnd;
+        uint64_t prev = 0;
+        for (uint64_t x : hist_points()) {
+            const uint64_t c = (uint64_t)(std::upper_bound(v.begin(), v.end(), x) - v.begin());
+            if (c != prev) {
+                bnd.push_back((double)x);
+                cnt.push_back(static_cast<uint64_t>((double)c / (double)n) * n);
+            }
+            prev = c;
+        }
+        Pb d;
+        d.fx64(2, t0);
+        d.fx64(3, t1);
+        d.fx64(4, n);
+        d.tag(6, 2);
+        d.varint(cnt.size() * 8);
+        d.s.append(reinterpret_cast<const char *>(cnt.data()), cnt.size() * 8);
+        d.tag(7, 2);
+        d.varint(bnd.size() * 8);
+        d.s.append(reinterpret_cast<const char *>(bnd.data()), bnd.size() * 8);
+        d.s += attrs(9, add);
+        Pb h;
+        h.bytes(1, d.s);
+        h.enm(2, 2); // AGGREGATION_TEMPORALITY_CUMULATIVE
+        metric(name, desc, 9, h.s);
+    }
+};
+
 // NetworkMetricsBucket::to_prometheus (src/handlers/net/v1/NetStreamHandler.cpp:332-388);
 // names and descriptions from NetStreamHandler.h:81-127
-void net_prom(pv_ctx *c, Prom &p, const HostBucket &b)
+template <class Sink>
+void net_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
 {
     const uint64_t *n = &b.sum[PV_OFF_NET];
     const size_t topn = c->cfg.topn_count;
@@ -1318,12 +1480,13 @@ void net_prom(pv_ctx *c, Prom &p, const HostBucket &b)
     uint64_t mx = 0;
     for (size_t i = 0; i < PV_PAYLOAD_BINS; i++)
         if (h[i]) mx = i;
-    p.summary<uint64_t>("packets_payload_size", "Quantiles of payload sizes, in bytes", q, mx, cnt);
+    p.template summary<uint64_t>("packets_payload_size", "Quantiles of payload sizes, in bytes", q, mx, cnt);
 }
 
 // DnsMetricsBucket::to_prometheus (src/handlers/dns/v1/DnsStreamHandler.cpp:1139-1238);
 // names and descriptions from DnsStreamHandler.h:116-171
-void dns_prom(pv_ctx *c, Prom &p, const HostBucket &b)
+template <class Sink>
+void dns_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
 {
     const uint64_t *d = &b.sum[PV_OFF_DNS];
     const size_t topn = c->cfg.topn_count;
@@ -1357,13 +1520,13 @@ void dns_prom(pv_ctx *c, Prom &p, const HostBucket &b)
                tops_of(b, TM_SLOW_IN), topn, pct);
         if (g & PV_DNS_QUANTILES) {
             if (!b.from_us.empty())
-                p.summary<uint64_t>("dns_xact_out_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is client, in microseconds",
+                p.template summary<uint64_t>("dns_xact_out_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is client, in microseconds",
                                     quantiles(b.from_us), vmax(b.from_us), b.from_us.size());
             if (!b.to_us.empty())
-                p.summary<uint64_t>("dns_xact_in_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is server, in microseconds",
+                p.template summary<uint64_t>("dns_xact_in_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is server, in microseconds",
                                     quantiles(b.to_us), vmax(b.to_us), b.to_us.size());
             if (!b.ratio.empty())
-                p.summary<double>("dns_xact_ratio_quantiles", "Quantiles of ratio of packet sizes in a DNS transaction (reply/query)",
+                p.template summary<double>("dns_xact_ratio_quantiles", "Quantiles of ratio of packet sizes in a DNS transaction (reply/query)",
                                   quantiles(b.ratio), vmax(b.ratio), b.ratio.size());
         }
         if (g & PV_DNS_HISTOGRAMS) {
@@ -3521,15 +3684,67 @@ int pv_window_prometheus(pv_ctx *c, uint32_t period, uint32_t handlers, const ch
         if ((rc = window_slots(c, c->net, period, false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
-        net_prom(c, p, b);
+        net_metrics(c, p, b);
     }
     if ((handlers & PV_HANDLER_DNS) && c->dns_groups) {
         if ((rc = window_slots(c, c->dns, period, false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;
-        dns_prom(c, p, b);
+        dns_metrics(c, p, b);
     }
     *out = strdup(p.o.str().c_str());
+    return 0;
+}
+
+int pv_window_opentelemetry(pv_ctx *c, uint32_t period, uint32_t handlers, const char *const *label_keys,
+                            const char *const *label_values, uint32_t n_labels, uint8_t **out, size_t *bytes)
+{
+    *out = nullptr;
+    *bytes = 0;
+    int rc = sync_xvals(c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    flush_fills(c);
+    if (!c->started) return c->fail(PV_EINVAL, "no data");
+    if (c->net2_groups || c->dns2_groups)
+        return c->fail(PV_EUNSUPPORTED, "window_opentelemetry: the v2 handlers' OpenTelemetry output is not built");
+    if (period >= c->cfg.num_periods)
+        return c->fail(PV_EINVAL, "invalid metrics period, specify [0, %u]", c->cfg.num_periods - 1);
+    Otlp p;
+    for (uint32_t i = 0; i < n_labels; i++) {
+        if (!label_keys || !label_values || !label_keys[i] || !label_values[i]) return c->fail(PV_EINVAL, "label %u missing", i);
+        p.add[label_keys[i]] = label_values[i];
+    }
+    std::vector<uint32_t> slots;
+    // the bucket's start / end stamps (end unset: now, as window_single_opentelemetry does)
+    auto stamps = [&](const Window &w, uint32_t slot) {
+        const SlotMeta &m = w.meta[slot];
+        p.t0 = (uint64_t)m.start_sec * 1000000000ull + (uint64_t)m.start_nsec;
+        if (m.end_sec) p.t1 = (uint64_t)m.end_sec * 1000000000ull + (uint64_t)m.end_nsec;
+        else {
+            timespec now;
+            timespec_get(&now, TIME_UTC);
+            p.t1 = (uint64_t)now.tv_sec * 1000000000ull + (uint64_t)now.tv_nsec;
+        }
+    };
+    if ((handlers & PV_HANDLER_NET) && c->net_groups) {
+        if ((rc = window_slots(c, c->net, period, false, slots))) return rc;
+        HostBucket b;
+        if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
+        stamps(c->net, slots[0]);
+        net_metrics(c, p, b);
+    }
+    if ((handlers & PV_HANDLER_DNS) && c->dns_groups) {
+        if ((rc = window_slots(c, c->dns, period, false, slots))) return rc;
+        HostBucket b;
+        if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;
+        stamps(c->dns, slots[0]);
+        dns_metrics(c, p, b);
+    }
+    *out = (uint8_t *)malloc(p.out.s.size() ? p.out.s.size() : 1);
+    if (!*out) return c->fail(PV_ECAPACITY, "window_opentelemetry: out of host memory");
+    memcpy(*out, p.out.s.data(), p.out.s.size());
+    *bytes = p.out.s.size();
     return 0;
 }
 

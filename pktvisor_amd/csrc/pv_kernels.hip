@@ -1875,6 +1875,12 @@ __device__ __forceinline__ uint64_t ip_tkey(uint64_t e)
 // where its run starts and how long it is (cb_run): pv_topn_merge reads each region's runs
 // straight from the lists, so no bucketing pass over the entries is needed.
 #define PV_W_CNT ((1u << 29) - 1) // weight bits of a dense IPv4 entry
+#ifndef PV_CB_U
+#define PV_CB_U 8 // tuning: dense IP log loads in flight per combine thread
+#endif
+#ifndef PV_MG_U
+#define PV_MG_U 8 // tuning: run entries in flight per merge thread
+#endif
 template <uint32_t CN, uint32_t NR>
 struct CombState {
     uint64_t key[CN];
@@ -1973,7 +1979,7 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
         uint64_t a, z;
         wg_records(P, blockIdx.x, a, z);
         const PV_G uint64_t *ipl = P.iplog + a;
-        batched<8>(z - a, [&](uint64_t j) { return ipl[j]; }, [&](uint64_t j, uint64_t e) {
+        batched<PV_CB_U>(z - a, [&](uint64_t j) { return ipl[j]; }, [&](uint64_t j, uint64_t e) {
             if (e) comb_add<CN>(P, S, sp, e, 1u, (uint32_t)(a + j));
         });
     }
@@ -2130,7 +2136,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                    });
         if (threadIdx.x == 0) { S.nnew = 0; S.ncr = 0; }
         __syncthreads();
-        batched<8>(n, ld, [&](uint64_t, ulonglong2 e) {
+        batched<PV_MG_U>(n, ld, [&](uint64_t, ulonglong2 e) {
             const uint64_t e0 = e.x;
             if (!one && entry_table(e0) != tb) return;
             const uint64_t e1 = e.y;
