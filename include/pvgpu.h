@@ -119,7 +119,7 @@ typedef struct pv_config {
  * _filtering :538-648). A filtered DNS packet is an event plus the `filtered` counter and
  * nothing else (process_filtered, :1341-1347). only_rcode is the input-proxy predicate
  * (:485-508): packets it rejects (queries, other rcodes) are not events at all.
- * geoloc / asn / public_suffix_list are not built. only_qname is matched by the DNS
+ * geoloc / asn are not built (no geo database). only_qname is matched by the DNS
  * pass's 56-bit name fingerprint (the key its top-N tables use), only_qname_suffix by the
  * 64-bit polynomial hash of the name's last L characters. */
 typedef struct pv_dns_filters {
@@ -134,10 +134,14 @@ typedef struct pv_dns_filters {
     const char *const *qnames;  /* first-query names wanted (compared lower-case); not with only_rcode */
     uint32_t n_qname_suffixes;  /* "only_qname_suffix" entries (<= 4), 0 = off */
     const char *const *qname_suffixes; /* lower-cased; the first one the name ends with sets the
-                                          aggregateDomain suffix size (at most one dot after its first char) */
+                                          aggregateDomain suffix size */
     uint32_t only_dnssec_response; /* nonzero: filter all but responses with an RRSIG answer */
     uint32_t filter_all;        /* nonzero: filter every DNS event that passes the predicates (geoloc_notfound /
                                    asn_notfound without a geo database, :619-642) */
+    uint32_t public_suffix_list; /* nonzero: "public_suffix_list" config (DnsStreamHandler::_configs,
+                                   :648-657): the first query's match_public_suffix size is the
+                                   aggregateDomain suffix size for top_qname2/3; ignored with
+                                   only_qname_suffix, as in the reference */
 } pv_dns_filters;
 
 /* Replaces DnsStreamHandler::start's filter setup (dns/v1/DnsStreamHandler.cpp:60-150). Call

@@ -367,6 +367,7 @@ struct Config {
     uint32_t answer_count = 0;
     bool only_queries = false, only_responses = false; // (:114-119)
     bool only_dnssec = false;                           // "only_dnssec_response" (:120-122)
+    bool psl = false;                                   // "public_suffix_list" config (:187-189)
     std::vector<uint16_t> only_qtype;                   // "only_qtype" (:131-150)
     std::vector<std::string> only_qname;                // "only_qname" (:151-160), lower-case; predicate mode
     std::vector<std::string> only_qname_suffix;         // "only_qname_suffix" (:161-169), lower-case
@@ -807,6 +808,33 @@ static std::string lower(const std::string &s)
     std::string o = s;
     for (auto &c : o) c = (char)tolower((unsigned char)c);
     return o;
+}
+
+// match_public_suffix (libs/visor_dns/PublicSuffixList.h:226-250): the last label picks a
+// list; the first listed suffix the whole name ends with (a byte compare, no label
+// boundary) gives its size + 1, else the label's size + 1; 0 without a listed label.
+// The table is pv_psl_data.h, generated from the reference's ICANN section (tools/gen_psl.py).
+#include "../pktvisor_amd/csrc/pv_psl_data.h"
+static size_t match_public_suffix(const std::string &str)
+{
+    static const std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> icann = [] {
+        std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> m;
+        uint32_t first = 0;
+        for (uint32_t t = 0; t < PV_PSL_NTLD; t++) {
+            m.emplace(pv_psl_tld[t], std::make_pair(first, (uint32_t)pv_psl_count[t]));
+            first += pv_psl_count[t];
+        }
+        return m;
+    }();
+    const size_t pos = str.find_last_of('.');
+    if (pos == std::string::npos || pos + 1 == str.size()) return 0;
+    auto it = icann.find(str.substr(pos + 1));
+    if (it == icann.end()) return 0;
+    for (uint32_t k = it->second.first; k < it->second.first + it->second.second; k++) {
+        const std::string sub = pv_psl_sfx[k];
+        if (str.size() >= sub.size() && str.compare(str.size() - sub.size(), sub.size(), sub) == 0) return sub.size() + 1;
+    }
+    return it->first.size() + 1;
 }
 
 // libs/visor_dns/dns.cpp:9-43
@@ -1267,6 +1295,12 @@ struct Engine {
         if (cfg.dns2_groups) {
             dns2_event(p, m, hm.d, qr, rcode, ancount, txid, suffix_size);
             return;
+        }
+        // DnsStreamHandler::_configs (:648-657): public_suffix_list sets suffix_size from the
+        // first query's lower-case name, only while only_qname_suffix is off
+        if (cfg.psl && cfg.only_qname_suffix.empty()) {
+            DnsParse pp = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{hdr_buf, m.len});
+            if (pp.ok && pp.has_query) suffix_size = match_public_suffix(lower(pp.name));
         }
         // DnsMetricsManager::process_dns_layer (:1350-1370)
         const bool deep = dns_s.draw(true);
@@ -2180,6 +2214,7 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "only_queries") c.only_queries = atoi(v.c_str()) != 0;
         else if (k == "only_responses") c.only_responses = atoi(v.c_str()) != 0;
         else if (k == "only_dnssec_response") c.only_dnssec = atoi(v.c_str()) != 0;
+        else if (k == "public_suffix_list") c.psl = atoi(v.c_str()) != 0;
         else if (k == "only_qname_suffix") {
             size_t q = 0;
             while (q < v.size()) {

@@ -57,7 +57,7 @@ class pv_dns_filters(ctypes.Structure):
                 ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16), ("n_qnames", ctypes.c_uint32),
                 ("qnames", ctypes.POINTER(ctypes.c_char_p)), ("n_qname_suffixes", ctypes.c_uint32),
                 ("qname_suffixes", ctypes.POINTER(ctypes.c_char_p)), ("only_dnssec_response", ctypes.c_uint32),
-                ("filter_all", ctypes.c_uint32)]
+                ("filter_all", ctypes.c_uint32), ("public_suffix_list", ctypes.c_uint32)]
 
 
 from pktvisor_amd.config import ConfigException as ConfigError  # noqa: E402  (the reference's texts)
@@ -65,9 +65,8 @@ from pktvisor_amd.config import StreamHandlerException  # noqa: E402,F401
 
 
 DNS_FILTER_KEYS = ("exclude_noerror", "only_rcode", "answer_count", "only_queries", "only_responses", "only_qtype",
-                   "only_qname", "only_qname_suffix", "only_dnssec_response")
-DNS_FILTER_NOT_BUILT = ( "geoloc_notfound", "asn_notfound",
-                        "dnstap_msg_type", "public_suffix_list")
+                   "only_qname", "only_qname_suffix", "only_dnssec_response", "public_suffix_list")
+DNS_FILTER_NOT_BUILT = ("geoloc_notfound", "asn_notfound", "dnstap_msg_type")
 
 
 def _dns_code(kind: int, name: str):
@@ -79,7 +78,8 @@ def dns_filter_config(cfg: dict) -> dict:
     """DnsStreamHandler::start's filter setup (src/handlers/dns/v1/DnsStreamHandler.cpp:60-150):
     typed values in, the pv_dns_filters fields out; ConfigError with the reference's text."""
     out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[],
-               only_qname=[], only_qname_suffix=[], only_dnssec_response=0, filter_all=0)
+               only_qname=[], only_qname_suffix=[], only_dnssec_response=0, filter_all=0,
+               public_suffix_list=0)
     for k in cfg:
         if k in DNS_FILTER_NOT_BUILT:
             raise ConfigError(f"DnsStreamHandler: filter {k} is not supported by the GPU handler")
@@ -87,7 +87,7 @@ def dns_filter_config(cfg: dict) -> dict:
             raise ConfigError(f"{k} is an invalid/unsupported config or filter. The valid configs/filters are: "
                               + ", ".join(DNS_FILTER_KEYS))
     # Configurable::config_get<T> (src/Configurable.h:101-112): a value of another type throws
-    for k in ("exclude_noerror", "only_queries", "only_responses", "only_dnssec_response"):
+    for k in ("exclude_noerror", "only_queries", "only_responses", "only_dnssec_response", "public_suffix_list"):
         if k in cfg and not isinstance(cfg[k], bool):
             raise ConfigError(f"wrong type for key: {k}")
     for k in ("only_qtype", "only_qname", "only_qname_suffix"):
@@ -120,6 +120,10 @@ def dns_filter_config(cfg: dict) -> dict:
         out["only_responses"] = 1
     if cfg.get("only_dnssec_response"):
         out["only_dnssec_response"] = 1
+    # public_suffix_list (:187-189, applied in _configs :648-657): a config, ignored while
+    # only_qname_suffix is set
+    if cfg.get("public_suffix_list"):
+        out["public_suffix_list"] = 1
     if "answer_count" in cfg:
         v = cfg["answer_count"]
         if isinstance(v, bool) or not isinstance(v, int):
@@ -427,6 +431,7 @@ class PvHandlers:
                 f.qtypes[k] = q
             f.only_dnssec_response = filt["only_dnssec_response"]
             f.filter_all = filt.get("filter_all", 0)
+            f.public_suffix_list = filt.get("public_suffix_list", 0)
             if filt["only_qname"]:
                 self._qnames = (ctypes.c_char_p * len(filt["only_qname"]))(*[q.encode() for q in filt["only_qname"]])
                 f.n_qnames = len(filt["only_qname"])

@@ -57,6 +57,39 @@ namespace pvname {
 inline uint32_t pv_clz64(uint64_t x) { return (uint32_t)__builtin_clzll(x); }
 inline uint32_t pv_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) { return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh)); }
 #include "pv_parse.h"
+#include "pv_psl_data.h"
+
+// The device form of the public suffix table (pv_psl_data.h, generated from the reference's
+// ICANN_DOMAINS): PV_PSL_SLOTS open-addressed slots of {FNV-1a of the label, byte offset,
+// length, first suffix | count << 16} (length 0 = empty), then {byte offset, length} per
+// suffix, then the strings. psl_match (pv_kernels.hip) reads it.
+static std::vector<uint32_t> psl_blob()
+{
+    std::vector<uint32_t> w(PV_PSL_SFX_WORD + 2 * PV_PSL_NSFX, 0);
+    std::string str;
+    const size_t base = w.size() * 4;
+    auto put = [&](const char *x) { const size_t o = base + str.size(); str += x; return (uint32_t)o; };
+    uint32_t first = 0;
+    for (uint32_t t = 0; t < PV_PSL_NTLD; t++) {
+        const char *k = pv_psl_tld[t];
+        uint32_t h = 0x811C9DC5u;
+        for (const char *x = k; *x; x++) h = (h ^ (uint8_t)*x) * 16777619u;
+        uint32_t s = h & (PV_PSL_SLOTS - 1);
+        while (w[s * 4 + 2]) s = (s + 1) & (PV_PSL_SLOTS - 1);
+        w[s * 4] = h; w[s * 4 + 2] = (uint32_t)strlen(k); w[s * 4 + 1] = put(k);
+        w[s * 4 + 3] = first | ((uint32_t)pv_psl_count[t] << 16);
+        first += pv_psl_count[t];
+    }
+    for (uint32_t j = 0; j < PV_PSL_NSFX; j++) {
+        w[PV_PSL_SFX_WORD + 2 * j + 1] = (uint32_t)strlen(pv_psl_sfx[j]);
+        w[PV_PSL_SFX_WORD + 2 * j] = put(pv_psl_sfx[j]);
+    }
+    str.resize((str.size() + 3) & ~(size_t)3, '\0');
+    const size_t n0 = w.size();
+    w.resize(n0 + str.size() / 4);
+    memcpy(w.data() + n0, str.data(), str.size());
+    return w;
+}
 #undef PV_FN
 #undef PV_CREF
 inline uint64_t name_ph(const char *s, size_t n) // polynomial hash of the lower-case string
@@ -77,6 +110,7 @@ inline uint64_t name_fp(const char *s, size_t n)
 extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ns(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
+extern "C" __global__ void pv_dns_kernel_sfx(const PvParams *P);
 extern "C" __global__ void pv_dns_suffix(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
@@ -388,6 +422,7 @@ struct pv_ctx {
     uint32_t f_nqn = 0;
     uint64_t f_qn[PV_MAX_QNAMES] = {};
     uint8_t *d_sfx = nullptr; // only_qname_suffix: suffix_size per record of the batch (names kernels)
+    uint32_t *d_psl = nullptr; // public_suffix_list table (psl_blob)
     uint32_t f_nsx = 0, f_sxl[PV_MAX_SUFFIXES] = {};
     uint64_t f_sxh[PV_MAX_SUFFIXES] = {};
     PvParams *d_params = nullptr;      // kernel parameter blocks (device memory)
@@ -1689,16 +1724,25 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
     for (uint32_t k = 0; k < f->n_qname_suffixes; k++) {
         const char *q = f->qname_suffixes ? f->qname_suffixes[k] : nullptr;
         if (!q || strlen(q) > 254) return c->fail(PV_EINVAL, "only_qname_suffix: missing or over-long suffix");
-        // aggregateDomain(name, suffix_size) looks for three dots at or before the suffix start;
-        // the DNS pass tracks a name's last four dots, so the suffix may hold one more
-        uint32_t dots = 0;
-        for (const char *x = q + (*q ? 1 : 0); *x; x++) dots += *x == '.';
-        if (dots > 1)
-            return c->fail(PV_EUNSUPPORTED, "only_qname_suffix: '%s' has more than one dot after its first character", q);
         c->f_sxl[k] = (uint32_t)strlen(q);
         c->f_sxh[k] = pvname::name_ph(q, strlen(q));
     }
     c->f_nsx = f->n_qname_suffixes;
+    // public_suffix_list (DnsStreamHandler::_configs, dns/v1/DnsStreamHandler.cpp:648-657): a
+    // config, not a filter, and only while only_qname_suffix is off
+    if (f->public_suffix_list && !f->n_qname_suffixes) {
+        if (c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "public_suffix_list with the DNS v2 handler is not built");
+        hipError_t e = hipSuccess;
+        if (!c->d_psl) {
+            const std::vector<uint32_t> blob = pvname::psl_blob();
+            if (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_psl, blob.size() * 4)) ||
+                !hip_ok(e = hipMemcpy(c->d_psl, blob.data(), blob.size() * 4, hipMemcpyHostToDevice)))
+                return c->hipfail(e, "public_suffix_list table");
+        }
+        if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
+            return c->hipfail(e, "public_suffix_list record buffer");
+        fl |= PVDF_PSL;
+    }
     if (f->n_qname_suffixes) {
         fl |= PVDF_ONLY_QSUFFIX;
         hipError_t e;
@@ -1863,7 +1907,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
                     c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_cb_h, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
-                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx,
+                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx, c->d_psl,
                     c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
@@ -2075,6 +2119,7 @@ void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t
     for (uint32_t k = 0; k < c->f_nqn; k++) P.f_qn[k] = c->f_qn[k];
     P.f_nsx = c->f_nsx;
     P.sfx_of = c->d_sfx;
+    P.psl = c->d_psl;
     for (uint32_t k = 0; k < c->f_nsx; k++) { P.f_sxl[k] = c->f_sxl[k]; P.f_sxh[k] = c->f_sxh[k]; }
     P.dbits = c->d_dbits;
     P.tseg = c->d_tseg;
@@ -2503,9 +2548,12 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
     hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
-    if (P.f_flags & PVDF_ONLY_QSUFFIX)
+    if (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))
         hipLaunchKernelGGL(pv_dns_suffix, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
-    hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    if (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))
+        hipLaunchKernelGGL(pv_dns_kernel_sfx, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    else
+        hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates into a list sorted by table region, merge
     // each region's runs in LDS, decode the names of new entries

@@ -150,14 +150,58 @@ __device__ __noinline__ int qname_suffix(PV_CREF(PvParams) P, A R, uint64_t m, u
     return -1;
 }
 
+// match_public_suffix (libs/visor_dns/PublicSuffixList.h:226-250) of the lower-case first-query
+// name (DnsStreamHandler::_configs, dns/v1/DnsStreamHandler.cpp:648-657): the last label picks
+// a list; the first listed suffix the name ends with (byte compare, no label boundary) gives
+// its size + 1, else the label's size + 1; 0 when the label is not listed. Exact compares
+// against the table's strings, one decode into a private buffer.
+template <class A>
+__device__ __noinline__ uint32_t psl_match(PV_CREF(PvParams) P, A R, uint64_t m, uint32_t len)
+{
+    uint8_t nm[320];
+    BufEmit be{nm, 0, 320};
+    name_emit(R, m, len, 12, be);
+    const uint32_t n = be.n;
+    if (n == 0 || n > 320) return 0;
+    int pos = (int)n - 1;
+    while (pos >= 0 && nm[pos] != '.') pos--;
+    if (pos < 0 || (uint32_t)pos + 1 == n) return 0;
+    const uint32_t lab = (uint32_t)pos + 1, tl = n - lab;
+    uint32_t h = 0x811C9DC5u;
+    for (uint32_t k = lab; k < n; k++) h = (h ^ nm[k]) * 16777619u;
+    const PV_G uint32_t *W = P.psl;
+    const PV_G uint8_t *B = reinterpret_cast<const PV_G uint8_t *>(P.psl);
+    for (uint32_t s = h & (PV_PSL_SLOTS - 1), probe = 0; probe < PV_PSL_SLOTS; s = (s + 1) & (PV_PSL_SLOTS - 1), probe++) {
+        const uint32_t L = W[s * 4 + 2];
+        if (L == 0) return 0;
+        if (W[s * 4] != h || L != tl) continue;
+        const uint32_t off = W[s * 4 + 1];
+        bool eq = true;
+        for (uint32_t k = 0; k < tl && eq; k++) eq = B[off + k] == nm[lab + k];
+        if (!eq) continue;
+        const uint32_t fc = W[s * 4 + 3], first = fc & 0xffff, cnt = fc >> 16;
+        for (uint32_t j = first; j < first + cnt; j++) {
+            const uint32_t so = W[PV_PSL_SFX_WORD + 2 * j], sl = W[PV_PSL_SFX_WORD + 2 * j + 1];
+            if (sl > n) continue;
+            bool e2 = true;
+            for (uint32_t k = 1; k <= sl && e2; k++) e2 = B[so + sl - k] == nm[n - k];
+            if (e2) return sl + 1;
+        }
+        return tl + 1;
+    }
+    return 0;
+}
+
 // only_qname_suffix result of one DNS message: the matched suffix size, 0xff if the
-// message has no first query or no listed suffix matches
+// message has no first query or no listed suffix matches; with public_suffix_list
+// (PVDF_PSL) match_public_suffix's size, 0 without a first query
 template <class A>
 __device__ __forceinline__ uint32_t dns_suffix_of(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen,
                                                   uint32_t qd, uint32_t an, uint32_t ns, uint32_t ar)
 {
     DnsInfo si;
     dns_parse(R, m, dlen, qd, an, ns, ar, si);
+    if (P.f_flags & PVDF_PSL) return (si.ok && si.has_query && si.name_len_enc > 0) ? psl_match(P, R, m, dlen) : 0u;
     if (!si.ok || !si.has_query) return 0xffu;
     NameStats st;
     st.init();
@@ -252,8 +296,8 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     uint32_t n = nl > 0 ? st.n : 0;
     if (metric == TM_QNAME2 || metric == TM_QNAME3) {
         int q2, q3; uint64_t h2, h3;
-        const uint32_t sfx = (P.f_flags & PVDF_ONLY_QSUFFIX) ? P.sfx_of[rep] : 0u;
-        if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx); else { q2 = 0; q3 = -1; }
+        const uint32_t sfx = (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) ? P.sfx_of[rep] : 0u;
+        if (nl > 0) agg_domain_r(R, m, len, st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx); else { q2 = 0; q3 = -1; }
         start = metric == TM_QNAME2 ? q2 : q3;
         if (start < 0) start = (int)n;
     }
@@ -599,7 +643,7 @@ __device__ __forceinline__ bool dns_predicates(PV_CREF(PvParams) P, const A &R, 
 // TAP: a dnstap event (DnsMetricsBucket::process_dnstap, :839-909): no filters, l3 / l4 from
 // the socket fields (flags bit 4: l3 unknown; bits 5-6: 0 UDP, 1 TCP, 2 other), the query
 // port as the port (top_udp_ports only when non-zero), no transaction event.
-template <bool TCP, bool TAP = false, class A, class Cache>
+template <bool TCP, bool TAP = false, bool SFX = true, class A, class Cache>
 __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, uint32_t *nev,
                                             uint32_t *nresp, uint64_t ebase, const A &R, const DnsMsg &dm, bool own,
                                             DnsCtr &c)
@@ -642,9 +686,16 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             filt = !fd.ok || !fd.has_query || !hit;
         }
         if (!filt && TCP && (P.f_flags & PVDF_ONLY_QNAME)) filt = !dns_qname_listed(P, R, m, dlen, w1, w2);
-        if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) {
-            // matched by pv_dns_suffix before this pass (0xff: no listed suffix)
-            const uint32_t r = P.sfx_of[i];
+        // only_qname_suffix, or _configs' public_suffix_list (:648-657, never 0xff): matched by
+        // pv_dns_suffix before this pass (0xff: no listed suffix); such runs use the SFX pass
+        if constexpr (SFX) {
+            if (!filt && (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))) {
+                const uint32_t r = P.sfx_of[i];
+                filt = r == 0xffu;
+                sfx = filt ? 0u : r;
+            }
+        } else if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) {
+            const uint32_t r = P.sfx_of[i]; // not launched this way (host picks the SFX pass)
             filt = r == 0xffu;
             sfx = filt ? 0u : r;
         }
@@ -744,7 +795,10 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                     }
                     int q2, q3;
                     uint64_t h2p, h3p;
-                    agg_domain(st, q2, q3, h2p, h3p, sfx);
+                    // SFX: a suffix size may be set (only_qname_suffix / public_suffix_list runs);
+                    // the common pass (sfx always 0) carries no re-walk code
+                    if constexpr (SFX) agg_domain_r(R, m, dlen, st, q2, q3, h2p, h3p, sfx);
+                    else agg_domain(st, q2, q3, h2p, h3p, sfx);
                     const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
                     top(TM_QNAME2, fp56(k2, st.n - q2, 0), 1);
                     if (q3 >= 0 && (uint32_t)q3 < st.n) {
@@ -1601,7 +1655,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_suffix(const PvParams *
 #ifndef PV_DNS_MINW
 #define PV_DNS_MINW 1 // tuning: waves per SIMD the DNS pass's register allocation must allow
 #endif
-extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel(const PvParams *__restrict__ Pp)
+template <bool SFX>
+__device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ DnsState S;
@@ -1663,7 +1718,7 @@ extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel(con
         if (active) {
             const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
             const bool own = P.dslot_of[dm.period] == wslot;
-            dns_process<false>(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
+            dns_process<false, false, SFX>(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
         }
     }
     if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
@@ -1675,6 +1730,15 @@ extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel(con
         P.blk_events[blockIdx.x] = S.nev;
         if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
     }
+}
+extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel(const PvParams *__restrict__ Pp)
+{
+    dns_pass<false>(Pp);
+}
+// only_qname_suffix / public_suffix_list runs: suffix sizes of any length (agg_domain_r)
+extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel_sfx(const PvParams *__restrict__ Pp)
+{
+    dns_pass<true>(Pp);
 }
 
 // ------------------------------------------------------------------ Net v2
@@ -2373,8 +2437,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 if (metric == TM_QNAME2 || metric == TM_QNAME3) {
                     int q2, q3;
                     uint64_t h2, h3;
-                    const uint32_t sfx = (P.f_flags & PVDF_ONLY_QSUFFIX) ? P.sfx_of[e.rep] : 0u;
-                    if (nl > 0) agg_domain(st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx);
+                    const uint32_t sfx = (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) ? P.sfx_of[e.rep] : 0u;
+                    if (nl > 0) agg_domain_r(R, m, mlen, st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx);
                     else { q2 = 0; q3 = -1; }
                     const int st0 = metric == TM_QNAME2 ? q2 : q3;
                     start = st0 < 0 ? nch : (uint32_t)st0;
@@ -2529,7 +2593,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp(const PvParams *__r
         for (uint32_t k = 0; k < P.n_dshift; k++) p += ordr >= P.dpos[k];
         dm.period = (uint8_t)p;
         if (p >= P.dskip_before) dm.flags |= 8;
-        if (P.f_flags & PVDF_ONLY_QSUFFIX) {
+        if (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) {
             const uint64_t m = dm.moff;
             P.sfx_of[dm.idx] = (uint8_t)dns_suffix_of(P, R, m, dm.mlen, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8),
                                                       be16(R, m + 10));
@@ -2626,7 +2690,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dnstap_kernel(const PvParam
         dm.pad = j << 2;
         DnsCtr c;
         c.zero();
-        dns_process<false, true>(P, (KeyCache<PV_NCACHE> *)nullptr, nullptr, nullptr, nullptr, 0, R, dm, false, c);
+        dns_process<false, true, false>(P, (KeyCache<PV_NCACHE> *)nullptr, nullptr, nullptr, nullptr, 0, R, dm, false, c);
     }
 }
 

@@ -287,7 +287,11 @@ struct PvSubnets {
 #define PV_MAX_SUFFIXES 4
 enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
        PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64, PVDF_ONLY_QSUFFIX = 128,
-       PVDF_ONLY_DNSSEC = 256, PVDF_FILTER_ALL = 512 };
+       PVDF_ONLY_DNSSEC = 256, PVDF_FILTER_ALL = 512, PVDF_PSL = 1024 };
+// public_suffix_list table on the device (pv_host.cpp psl_blob): 512 slots of {FNV-1a of the
+// last label, byte offset, length, first suffix | count << 16}, then per suffix {offset, length}
+#define PV_PSL_SLOTS 512
+#define PV_PSL_SFX_WORD (PV_PSL_SLOTS * 4)
 // One dnstap event for pv_dnstap_kernel (DnstapInputStream -> process_dnstap_cb of the Net
 // and DNS handlers): the fields both handlers read, and the record (linktype 101: IPv4 or IPv6
 // header with the query / response addresses, UDP header, the DNS message) write_name parses.
@@ -408,6 +412,7 @@ struct PvParams {
     // record i's Net event / DNS event draws "not deep" (the managers' jsf32 draws, on the host)
     const PV_G uint32_t *ndeep_net, *ndeep_dns;
     uint32_t dpos[PV_MAX_SHIFTS];      // span-relative ord of the event that shifts DNS period k+1
+    PV_G const uint32_t *psl;          // public_suffix_list table (PVDF_PSL)
 };
 
 // pv_fill_multi's segment list (kernel argument)

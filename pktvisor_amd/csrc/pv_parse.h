@@ -527,6 +527,69 @@ PV_FN uint64_t suffix_hash(const NameStats &s, int start, uint64_t ph_start)
     return ph_submul(s.ph, ph_start, powb(s.n - (uint32_t)start));
 }
 
+// The dots of a name at positions <= lim, newest first, with the prefix hash in front of
+// each. aggregateDomain's rfinds (libs/visor_dns/dns.cpp:20-36) never look past endDot, so
+// these are the only dots it can use; NameStats keeps the last four dots of the whole name,
+// which is too few once a suffix (only_qname_suffix, public_suffix_list) covers two of them.
+struct DotsUpTo {
+    uint64_t ph = 0;
+    uint32_t n = 0;
+    int32_t lim;
+    int32_t d0 = -1, d1 = -1, d2 = -1;
+    uint64_t h0 = 0, h1 = 0, h2 = 0;
+    PV_FN void put(uint32_t c)
+    {
+        c = lower(c);
+        if (c == '.' && (int32_t)n <= lim) { d2 = d1; h2 = h1; d1 = d0; h1 = h0; d0 = (int32_t)n; h0 = ph; }
+        ph = ph_step(ph, c);
+        n++;
+    }
+};
+#ifndef PV_OOL
+#if defined(__HIP__)
+#define PV_OOL __host__ __device__ __noinline__
+#else
+#define PV_OOL __attribute__((noinline))
+#endif
+#endif
+struct DotsOut {
+    int32_t d0, d1, d2;
+    uint64_t h0, h1, h2;
+};
+// out of line with by-value arguments and result, so the DNS pass keeps no stack frame for it
+template <class A>
+PV_OOL DotsOut dots_up_to(A R, uint64_t m, uint32_t len, int32_t lim)
+{
+    DotsUpTo d;
+    d.lim = lim;
+    name_emit(R, m, len, 12, d);
+    return DotsOut{d.d0, d.d1, d.d2, d.h0, d.h1, d.h2};
+}
+// agg_domain with any suffix size: when two or more of the tracked dots lie past endDot, the
+// name is walked again for the dots at or before it (rare: long suffixes on many-label names)
+template <class A>
+PV_FN void agg_domain_r(const A &R, uint64_t m, uint32_t len, const NameStats &s, int &q2, int &q3, uint64_t &ph2,
+                        uint64_t &ph3, uint32_t suffix_size)
+{
+    agg_domain(s, q2, q3, ph2, ph3, suffix_size);
+    if (suffix_size > 0 && s.n > suffix_size && s.d3 >= 0 && s.d1 > (int)(s.n - suffix_size)) {
+        const DotsOut d = dots_up_to(R, m, len, (int32_t)(s.n - suffix_size));
+        NameStats t = s;
+        t.d0 = d.d0; t.h0 = d.h0; t.d1 = d.d1; t.h1 = d.h1; t.d2 = d.d2; t.h2 = d.h2; t.d3 = -1; t.h3 = 0;
+        agg_domain(t, q2, q3, ph2, ph3, suffix_size);
+    }
+}
+// the lower-case name into a buffer (public_suffix_list)
+struct BufEmit {
+    uint8_t *d;
+    uint32_t n, cap;
+    PV_FN void put(uint32_t c)
+    {
+        if (n < cap) d[n] = (uint8_t)lower(c);
+        n++;
+    }
+};
+
 // ------------------------------------------------------------------ name fast path
 // A level-1 name made of plain labels (lengths 1..63, no pointer, no NUL and no '.'
 // byte inside a label, at most 8 inner dots, terminated inside the message within the

@@ -148,16 +148,3 @@ def test_dnssec_reference_kat():
     assert (w["events"], w["udp"], w["replies"], w["noerror"], w["queries"]) == (14, 6, 6, 6, 0)
     assert d["cardinality"]["qname"] == 3
     assert [(e["name"], e["estimate"]) for e in d["top_qtype"][:3]] == [("DNSKEY", 3), ("DS", 2), ("A", 1)]
-
-
-def test_qname_suffix_limit_refused():
-    """A suffix with more than one dot after its first character is refused loudly
-    (the DNS pass tracks a name's last four dots), never silently mismatched."""
-    path = os.path.join(GOLD, "dns_udp_mixed_rcode.pcap")
-    with pytest.raises(pa.PvError, match="more than one dot"):
-        pa.pktvisor_reader(path, host_spec="192.168.0.0/24", periods=1,
-                           dns_filters={"only_qname_suffix": ["www.google.com"]})
-    # one dot after the first character is within the limit
-    j = pa.pktvisor_reader(path, host_spec="192.168.0.0/24", periods=1,
-                           dns_filters={"only_qname_suffix": [".google.com"]})["1m"]["dns"]
-    assert j["wire_packets"]["udp"] > 0

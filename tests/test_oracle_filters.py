@@ -26,6 +26,9 @@ KAT = [
     ("test_dns_layer.cpp:639-673 only_queries", dict(only_queries=1),
      dict(udp=12, noerror=0, srvfail=0, refused=0, nxdomain=0, filtered=12),
      dict(top_qname2=".mwbsys.com", top_qname3="sirius.mwbsys.com")),
+    ("test_dns_layer.cpp:603-637 public_suffix_list", dict(public_suffix_list=1),
+     dict(udp=24, noerror=10, srvfail=0, refused=1, nxdomain=1, filtered=0),
+     dict(top_qname2=".mwbsys.com", top_qname3="sirius.mwbsys.com")),
     ("test_dns_layer.cpp:675-705 only_responses", dict(only_responses=1),
      dict(udp=12, noerror=10, srvfail=0, refused=1, nxdomain=1, filtered=12), {}),
 ]
@@ -68,8 +71,10 @@ def test_filter_config_parsing():
         assert str(e.value) == msg
     assert dns_filter_config({"only_qname": ["play.GooGle.com"]})["only_qname"] == ["play.google.com"]
     assert dns_filter_config({"only_qname_suffix": ["GooGle.com"]})["only_qname_suffix"] == ["google.com"]
-    with pytest.raises(ConfigError):
-        dns_filter_config({"public_suffix_list": True})  # not built on the GPU path: refused loudly
+    assert dns_filter_config({"public_suffix_list": True})["public_suffix_list"] == 1
+    with pytest.raises(ConfigError) as e:
+        dns_filter_config({"public_suffix_list": 1})  # config_get<bool> of an int
+    assert str(e.value) == "wrong type for key: public_suffix_list"
 
 
 def test_oracle_dnssec_kat(oracle):
