@@ -109,6 +109,7 @@ inline uint64_t name_fp(const char *s, size_t n)
 
 extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ns(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_fast(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel_sfx(const PvParams *P);
 extern "C" __global__ void pv_dns_suffix(const PvParams *P);
@@ -2540,11 +2541,19 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
-    // the specialised pass when nothing in the batch needs the general one
-    if (P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net)
-        hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-    else
-        hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    // the specialised passes when nothing in the batch needs the general one: the lean pass
+    // (one Net period, Ethernet, at most two IPv4 host subnets, a wave's tiles below 2^16 for
+    // its packed lane counters), else the shift-free general pass. PV_NET_KERNEL=ns|general
+    // forces one for A/B runs.
+    {
+        static const char *force = getenv("PV_NET_KERNEL");
+        const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || (force && !strcmp(force, "general"));
+        const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && P.wt_per_block / 4 < 65535 &&
+                          !(force && !strcmp(force, "ns"));
+        if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+        else if (lean) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+        else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
     hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
@@ -3058,6 +3067,11 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
     if (c->net2_groups || c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "dnstap input with the v2 handlers is not built");
+    // each manager draws per dnstap event (new_event: net/v1 :840, dns/v1 :1409); the
+    // dnstap kernel has no not-deep path, so a sampled context refuses rather than report
+    // every event as deep and leave the generators out of step
+    if (c->sample_rate < 100)
+        return c->fail(PV_EUNSUPPORTED, "dnstap input with deep_sample_rate below 100 is not built");
     std::vector<pvi::DtMessage> msgs;
     uint32_t frames = 0;
     pvi::dnstap_decode(buf, bytes, msgs, &frames);
@@ -3101,7 +3115,7 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         e.l3 = m.has_family ? (m.family == 2 ? 6 : (m.family == 1 ? 4 : 0)) : 0;
         e.l4 = m.has_protocol ? (m.protocol == 1 ? 17 : (m.protocol == 2 ? 6 : 0)) : 0;
         e.qport = m.has_qport ? (uint16_t)m.qport : 0;
-        e.filtered = (msg_type_mask && !((msg_type_mask >> t) & 1)) ? 1 : 0;
+        e.filtered = (msg_type_mask && !(t < 32 && ((msg_type_mask >> t) & 1))) ? 1 : 0; // a type past the mask's bits never matches
         const uint8_t *msg = nullptr;
         size_t mlen = 0;
         if (!m.has_qmsg && !m.has_rmsg) e.dns_mode = PV_DT_SIDE;

@@ -883,21 +883,28 @@ struct DnsState {
     uint32_t nev, nresp;
 };
 
-// Adds one to H[v] for every lane with v != PV_NOH. The two most common values of the
-// wave are added once each by a leader lane (packet sizes repeat: a whole wave often
-// shares one), the rest per lane.
-__device__ __forceinline__ void hist_add(uint32_t *H, uint32_t v, uint32_t lane)
+// Adds one to bin v for every lane with v != PV_NOH: bins below PV_HBINS in the LDS
+// histogram H, larger ones straight to the HBM table G (G[v]: the slot's payload-size words).
+// The two most common values of the wave are added once each by a leader lane (packet sizes
+// repeat: a whole wave often shares one), the rest per lane.
+__device__ __forceinline__ void hist_add(uint32_t *H, PV_G uint64_t *G, uint32_t v, uint32_t lane)
 {
     uint64_t m = __ballot(v != PV_NOH);
     for (int it = 0; it < 2 && m; it++) {
         const uint32_t ld = (uint32_t)__builtin_ctzll(m);
         const uint32_t lv = __builtin_amdgcn_readlane(v, ld);
         const uint64_t eq = __ballot(v == lv);
-        if (lane == ld) atomicAdd(&H[lv], (uint32_t)__popcll(eq));
+        if (lane == ld) {
+            if (lv < PV_HBINS) atomicAdd(&H[lv], (uint32_t)__popcll(eq));
+            else __hip_atomic_fetch_add(G + lv, (uint64_t)__popcll(eq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (v == lv) v = PV_NOH;
         m &= ~eq;
     }
-    if (v != PV_NOH) atomicAdd(&H[v], 1u);
+    if (v != PV_NOH) {
+        if (v < PV_HBINS) atomicAdd(&H[v], 1u);
+        else __hip_atomic_fetch_add(G + v, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // Loop-invariant values of the Net pass, read from the parameter block once: inside the
@@ -1009,21 +1016,22 @@ __device__ __forceinline__ uint64_t net_ip_entry(const NetK &K, const A &R, cons
 // with an exact vmcnt. The wave's other memory operations (stores, rare HBM reads) only
 // make such a wait wait for a little more.
 #ifndef PV_NL_Q
-#define PV_NL_Q 3 // ring slots per wave
+#define PV_NL_Q 3 // ring slots per wave (all of them in flight while the wave parses a tile)
 #endif
 #ifndef PV_NL_SLOT
 #define PV_NL_SLOT 5120 // bytes per slot: the packed span of a tile, or 80-B windows
 #endif
 #define PV_NL_NJ (PV_NL_SLOT / 1024)     // 1-KiB DMA pieces per tile
 #define PV_NL_OPS (PV_NL_NJ + 2)         // DMA operations per tile
-#define PV_NL_OROWS (PV_NL_Q + 2)        // offset-row pairs per wave (tiles k .. k + Q + 1)
+#define PV_NL_OROWS (PV_NL_Q + 3)        // offset rows per wave (tiles k .. k + Q + 2)
 static_assert(PV_NL_SLOT % 1024 == 0, "whole DMA pieces");
 static_assert(PV_NL_SLOT / PV_WT >= 80, "window must cover Eth + IPv4 + UDP from a 16-B aligned start");
 
 struct alignas(16) NetWave {
     uint32_t slot[PV_NL_Q][PV_NL_SLOT / 4];
     uint32_t lo[PV_NL_OROWS][PV_WT]; // each lane's record start
-    uint32_t hi[PV_NL_OROWS][PV_WT]; // each lane's record end (the next start)
+    uint32_t hi[PV_NL_OROWS];        // the tile's end (start of the record after its last)
+    uint32_t pad[(4 - PV_NL_OROWS % 4) % 4];
 };
 // the batch's period tables, staged in LDS: lanes that need a per-record period (a tile that
 // holds a shift, a DNS message's DNS period) read them with LDS loads; a per-lane load from
@@ -1111,16 +1119,36 @@ struct RecW {
         return (off & 3) ? __builtin_amdgcn_alignbyte(w[(off >> 2) + 1], w[off >> 2], off & 3) : w[off >> 2];
     }
 };
-// packed tile: the record's dwords are consecutive in the slot (one base address, immediate
-// offsets)
-__device__ __forceinline__ void recw_load_packed(const uint32_t *L, uint32_t d0, uint32_t sh, RecW &r)
+// the record's dwords d0 .. d0 + 16 (d0 < 4) from the five 16-B pieces that hold them, picked
+// with two select levels, then byte-aligned
+__device__ __forceinline__ void recw_pick(const uint32_t (&w)[20], uint32_t d0, uint32_t sh, RecW &r)
 {
-    const uint32_t *p = L + d0;
-    uint32_t x[17];
+    // bit selects (v_bfi), not ternaries the compiler turns into a dynamically indexed
+    // (scratch) array
+    const uint32_t m0 = 0u - (d0 & 1), m1 = 0u - ((d0 >> 1) & 1);
+    uint32_t a[19], x[17];
 #pragma unroll
-    for (int j = 0; j < 17; j++) x[j] = p[j];
+    for (int j = 0; j < 19; j++) a[j] = (w[j + 1] & m0) | (w[j] & ~m0);
+#pragma unroll
+    for (int j = 0; j < 17; j++) x[j] = (a[j + 2] & m1) | (a[j] & ~m1);
 #pragma unroll
     for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+}
+// packed tile: the record's bytes are consecutive in the slot. Read as five ds_read_b128 from
+// the record's 16-B aligned start (not 17 ds_read_b32 at the record's own dword: at an 80-B
+// record stride those put 32 lanes on 8 of the 32 dword banks, a 4-way conflict on every
+// read; b128 banks are (a/4) mod 64 in 16-lane groups, and 16 consecutive 80-B strides land
+// on 16 distinct 16-B bank slots)
+__device__ __forceinline__ void recw_load_packed(const uint32_t *L, uint32_t rel, RecW &r)
+{
+    const uint4 *q = reinterpret_cast<const uint4 *>(L + ((rel >> 4) << 2));
+    uint32_t w[20];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint4 v = q[k];
+        w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+    }
+    recw_pick(w, (rel >> 2) & 3, rel & 3, r);
 }
 // window tile: the lane's 80-B window as five 16-B pieces (piece k at L[k * 256 + lane4]: lanes
 // contiguous, so each ds_read_b128 is conflict-free), then the record's dwords d0 .. d0 + 16
@@ -1134,16 +1162,7 @@ __device__ __forceinline__ void recw_load_window(const uint32_t *L, uint32_t d0,
         const uint4 v = q[k * 64];
         w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
     }
-    // bit selects (v_bfi), not ternaries the compiler turns into a dynamically indexed
-    // (scratch) array
-    const uint32_t m0 = 0u - (d0 & 1), m1 = 0u - ((d0 >> 1) & 1);
-    uint32_t a[19], x[17];
-#pragma unroll
-    for (int j = 0; j < 19; j++) a[j] = (w[j + 1] & m0) | (w[j] & ~m0);
-#pragma unroll
-    for (int j = 0; j < 17; j++) x[j] = (a[j + 2] & m1) | (a[j] & ~m1);
-#pragma unroll
-    for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+    recw_pick(w, d0, sh, r);
 }
 // parse_record's fast path from the words (o as parse_record sets it); false: not this shape
 __device__ __forceinline__ bool fast_parse(const RecW &r, const ParseCfg &C, PV_CREF(PvParams) P, uint64_t rec, Parsed &o)
@@ -1380,14 +1399,16 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
         const uint64_t r = tile_of(k) * PV_WT + lane;
         const uint32_t row = k % PV_NL_OROWS;
         dma4(K.offs + min<uint64_t>(r, last), lds_addr(&NW.lo[row][0]));
-        dma4(K.offs + min<uint64_t>(r + 1, last), lds_addr(&NW.hi[row][0]));
+        // the tile's end: lane 63's next offset, landing at hi[row] (LDS-DMA writes m0 + 4 * lane)
+        const uint32_t ha = lds_addr(&NW.hi[row]) - 4 * 63;
+        if (lane == 63) dma4(K.offs + min<uint64_t>(r + 1, last), ha);
     };
     auto issue_tile = [&](uint32_t k) {
         const uint32_t row = k % PV_NL_OROWS;
         const uint64_t t = tile_of(k);
         const uint32_t o = NW.lo[row][lane];
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
-        const uint32_t b1 = t * PV_WT + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row][63]);
+        const uint32_t b1 = t * PV_WT + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row]);
         const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
         const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
         const uint32_t dst = lds_addr(&NW.slot[k % PV_NL_Q][0]);
@@ -1406,22 +1427,36 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
     NetCtr c;
     c.zero();
     uint32_t wslot = 0xffffffffu;
+    // The ring: step k waits for tile k, reads each lane's record words out of slot k % Q
+    // into registers and, once no lane needs the slot any more (every lane took the fast
+    // path: the common case), refills it at once with [rows k + Q + 2][tile k + Q]; a tile
+    // with general-path records refills after its body. So Q tiles (not Q - 1) are in
+    // flight while a wave parses, and Q = 2 slots per wave leave LDS for three workgroups per
+    // CU. A tile's rows are issued two refills before the tile, so the wait for them is
+    // for loads two steps old; every refill of the sequence is issued even past the range's
+    // end (a clamped copy), so the count of DMA operations younger than any tile is fixed
+    // and the waits are exact vmcnt counts (the wave's stores between them only make a wait
+    // wait for a little more).
+    auto refill = [&](uint32_t k) {
+        issue_rows(k + PV_NL_Q + 2);
+        PV_VMCNT(2 * PV_NL_OPS); // rows k + Q landed: younger are tile k + Q - 2, refill k - 1, rows k + Q + 2
+        issue_tile(k + PV_NL_Q);
+    };
     if (ntl) {
-        // prologue: rows 0 and 1, then the sequence's first Q - 1 steps, each
-        // [rows t + 2][tile t] for t = 0 .. Q - 2 (the steady state's pattern, so the
-        // vmcnt counts below hold from the first loop step on)
+        // prologue: rows 0 and 1, then the refills of steps -Q .. -1, [rows j + 2][tile j] for
+        // j = 0 .. Q - 1 (the steady state's pattern, so the counts hold from step 0 on)
         issue_rows(0);
         issue_rows(1);
         PV_VMCNT(0);
-        for (uint32_t t = 0; t + 1 < PV_NL_Q; t++) {
-            issue_rows(t + 2);
-            if (t >= 2) PV_VMCNT(2 * PV_NL_OPS); // rows t landed (issued two steps earlier)
-            issue_tile(t);
+        for (uint32_t j = 0; j < PV_NL_Q; j++) {
+            issue_rows(j + 2);
+            if (j >= 2) PV_VMCNT(2 * PV_NL_OPS);
+            issue_tile(j);
         }
     }
     STAMP_DECL
     // one tile's records from its staged copy Ls (off: this lane's record start, [b0, b1): the tile's span)
-    auto tile_body = [&](uint32_t k, uint64_t off, uint32_t b0, uint32_t b1, const uint32_t *Ls) {
+    auto tile_body = [&](uint32_t k, uint64_t off, uint32_t b0, uint32_t b1, const uint32_t *Ls) -> bool {
         const uint64_t t = tile_of(k);
         const uint64_t r0 = t * PV_WT;
         const uint64_t r1 = min<uint64_t>(r0 + PV_WT, n) - 1;
@@ -1457,23 +1492,31 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
         uint64_t ek = 0;
         DnsMsgW dm{};
         bool isdns = false;
-        bool istcp = false, hasseg = false;
+        bool istcp = false, hasseg = false, released = false;
         PvTcpSeg seg;
-        if (active && !(K.dbg & 1)) {
-            const SAcc R = packed ? SAcc{K.recs, Ls, base, nch * 16 - 4, 0u, 1u}
-                                  : SAcc{K.recs, Ls, off & ~15ull, PV_NL_SLOT / PV_WT - 4, lane * 4, 0u};
-            // fast path: the 17 staged dwords recw_load reads (the record's first 64 bytes
-            // plus the alignment spill) are inside the staged range; in window mode that
-            // holds for every record (start within 15 bytes of the 16-B aligned window)
-            const uint32_t rel = (uint32_t)(off - R.gbase);
-            RecW rw;
-            bool fast = (rel >> 2) + 17 <= (R.lim + 4) >> 2;
-            Parsed o;
-            if (fast) {
-                if (packed) recw_load_packed(R.L, rel >> 2, rel & 3, rw);
-                else recw_load_window(R.L, rel >> 2, rel & 3, lane * 4, rw);
-                fast = fast_parse(rw, C, P, off, o);
-            }
+        const bool work = active && !(K.dbg & 1);
+        const SAcc R = packed ? SAcc{K.recs, Ls, base, nch * 16 - 4, 0u, 1u}
+                              : SAcc{K.recs, Ls, off & ~15ull, PV_NL_SLOT / PV_WT - 4, lane * 4, 0u};
+        // fast path: the 17 staged dwords recw_load reads (the record's first 64 bytes
+        // plus the alignment spill) are inside the staged range; in window mode that
+        // holds for every record (start within 15 bytes of the 16-B aligned window)
+        const uint32_t rel = (uint32_t)(off - R.gbase);
+        RecW rw;
+        Parsed o;
+        bool fast = false;
+        if (work && (rel >> 2) + 17 <= (R.lim + 4) >> 2) {
+            if (packed) recw_load_packed(R.L, rel, rw);
+            else recw_load_window(R.L, rel >> 2, rel & 3, lane * 4, rw);
+            fast = fast_parse(rw, C, P, off, o);
+        }
+        // every lane's words are in registers: unless a general-path record still reads the
+        // slot, it is refilled now (whole wave, uniform branch), before the body's work
+        if (__ballot(work && !fast) == 0) {
+            asm volatile("" ::: "memory");
+            refill(k);
+            released = true;
+        }
+        if (work) {
             if (!fast) {
                 // a record that is not deep: no IPs, no SYN (NetworkMetricsBucket::process_packet
                 // !deep, net/v1/NetStreamHandler.cpp:518-521)
@@ -1522,7 +1565,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
                     else knet_direct(K.sum, K.net_groups, slot, o.dir, o.l3, o.l4, o.syn);
                     uint32_t cl = o.caplen;
                     if (cl > 65535) { atomicOr(K.flags, PVF_BIG_CAPLEN); cl = 65535; }
-                    if (slot == hslot && cl < PV_HBINS) hv = cl;
+                    if (slot == hslot) hv = cl;
                     else ksum_add(K, slot, PV_OFF_PAYLOAD + cl, 1);
                     if (fast && deep) {
                         // net_ip_entry on the words (IPv4 only)
@@ -1561,7 +1604,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
         asm volatile("" ::: "memory");
         STAMP(5)
         if (!(K.dbg & 1)) {
-            if (!(K.dbg & 64)) hist_add(S.hist, hv, lane); // 64: profiling knob, no histogram
+            if (!(K.dbg & 64)) hist_add(S.hist, K.sum + (uint64_t)hslot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane); // 64: profiling knob
             // DNS messages: wave-compacted into the workgroup's work list
             const uint64_t m = __ballot(isdns);
             if (m) {
@@ -1588,19 +1631,16 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
             }
         }
         STAMP(6)
+        return released;
     };
     for (uint32_t k = 0; k < ntl; k++) {
-        // step: rows k + Q + 1, then tile k + Q - 1, whose rows came two steps earlier:
-        // younger than them are that step's tile, the last step's rows and tile, and this
-        // step's rows
-        issue_rows(k + PV_NL_Q + 1);
-        PV_VMCNT(2 * PV_NL_OPS);
-        issue_tile(k + PV_NL_Q - 1);
-        PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed
+        PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed: younger are the refills of steps k - Q + 1 .. k - 1
         STAMP(1)
         const uint32_t sl = k % PV_NL_Q, row = k % PV_NL_OROWS;
-        tile_body(k, NW.lo[row][lane], __builtin_amdgcn_readfirstlane(NW.lo[row][0]),
-                  tile_of(k) * PV_WT + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row][63]), NW.slot[sl]);
+        const bool rel = tile_body(k, NW.lo[row][lane], __builtin_amdgcn_readfirstlane(NW.lo[row][0]),
+                                   tile_of(k) * PV_WT + PV_WT >= n ? (uint32_t)K.rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row]),
+                                   NW.slot[sl]);
+        if (!rel) refill(k);
     }
     PV_VMCNT(0); // the sequence's trailing copies land before the workgroup ends
     if (wslot != 0xffffffffu) knet_flush(K, wslot, c);
@@ -1615,8 +1655,321 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
     }
 }
 
+
+// ------------------------------------------------------------------ the lean Net pass
+// The common batch: one Net period (no shift inside the batch), no filter-all, no deep
+// sampling, no profiling knobs, Ethernet link type, at most two IPv4 host subnets. Same ring
+// and the same results as net_pass, with a tile's work written for the instruction budget:
+// the general pass is issue-bound (rocprofv3 on C2: ~300 VALU and ~320 SALU
+// wave-instructions per 64-record tile, each wave issuing 40 % of its cycles), most of it exec
+// masking of nested per-lane branches and spilled scalars. Here the fast path (Ethernet II +
+// IPv4 without options) is straight-line selects, the fast lanes' nine counters are three
+// packed lane registers, every rarely taken piece (DNS messages, TCP segments, caplen > 65535,
+// cardinality without top IPs) sits behind a uniform ballot branch, and general-path records
+// go to an out-of-line call that reads its parameters itself (so nothing it needs is live
+// across the loop).
+
+// fast-path fields of one record (parse_record's fast path, branch-free)
+struct FastRec {
+    uint32_t ok, caplen, dir, l4, syn, l4len;
+};
+struct HostNets {
+    uint32_t a0, m0, a1, m1, e0, e1; // e: subnet present (all-ones / zero)
+};
+PV_FN uint32_t hit4(const HostNets &h, uint32_t ip)
+{
+    const uint32_t m = (((ip ^ h.a0) & h.m0) == 0 ? h.e0 : 0u) | (((ip ^ h.a1) & h.m1) == 0 ? h.e1 : 0u);
+    return ip ? m : 0u;
+}
+PV_FN FastRec fast_fields(const RecW &r, const HostNets &h)
+{
+    FastRec f;
+    f.caplen = r.w[2];
+    const uint32_t w3 = r.w[7], w4 = r.w[8], w5 = r.w[9];
+    const uint32_t proto = w5 >> 24;
+    f.ok = (f.caplen >= 34) & ((w3 & 0xffffffu) == 0x450008u) & (proto != 4) & (proto != 41);
+    const uint32_t total = ((w4 & 0xff) << 8) | ((w4 >> 8) & 0xff);
+    const uint32_t frag = ((w5 & 0xff) << 8) | ((w5 >> 8) & 0xff);
+    const uint32_t l = f.caplen - 14;
+    const uint32_t len = (total != 0 && total < l) ? total : l;
+    const uint32_t pll = len - 20;
+    const bool l4ok = (len > 20) & !(frag & 0x3fff);
+    const bool udp = l4ok & (proto == 17) & (pll >= 8);
+    const bool tcp = l4ok & (proto == 6) & (pll >= 20);
+    f.l4 = udp ? 17u : (tcp ? 6u : 0u);
+    f.syn = tcp ? (r.w[15] >> 25) & 1 : 0u; // TCP flags at record offset 63
+    f.l4len = pll;
+    const uint32_t dst = hit4(h, r.at(46)), src = hit4(h, r.at(42));
+    f.dir = dst ? 0u : (src ? 1u : 2u);
+    return f;
+}
+// dns_port without short-circuit branches
+PV_FN uint32_t dns_port_bf(uint32_t pw)
+{
+    const uint32_t sport = ((pw & 0xff) << 8) | ((pw >> 8) & 0xff);
+    const uint32_t dport = ((pw >> 8) & 0xff00) | (pw >> 24);
+    const bool dd = (dport == 53) | (dport == 5353) | (dport == 5355) | (dport == 53000);
+    const bool sd = (sport == 53) | (sport == 5353) | (sport == 5355) | (sport == 53000);
+    return dd ? sport : (sd ? dport : 0u);
+}
+// the Parsed a fast record's consumers (DNS message, TCP segment) read
+PV_FN Parsed fast_parsed(const FastRec &f, const RecW &r, uint32_t ts_nano, uint64_t off)
+{
+    Parsed o;
+    o.caplen = f.caplen;
+    o.sec = r.w[0];
+    o.nsec = ts_nano ? (int32_t)r.w[1] : (int32_t)(r.w[1] * 1000u);
+    o.frame = off + 16;
+    o.l3 = 4; o.l4 = (uint8_t)f.l4; o.has4 = 1; o.has6 = 0; o.syn = (uint8_t)f.syn; o.dir = (uint8_t)f.dir;
+    o.v4 = o.frame + 14; o.v6 = 0;
+    o.l4off = f.l4 ? o.frame + 34 : 0;
+    o.l4len = f.l4 ? f.l4len : 0;
+    return o;
+}
+// a general-path record of the lean pass: net_slow with the parameters read here, not held
+// live across the caller's loop
+__device__ __noinline__ SlowOut net_slow_p(const PvParams *__restrict__ Pp, const SAcc R, uint64_t off, uint64_t i)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    NetK K;
+    K.recs = P.recs; K.offs = P.offs; K.n = P.n; K.rec_bytes = P.rec_bytes; K.gbase = P.gbase;
+    K.sum = P.sum; K.cpc = P.cpc; K.iplog = P.iplog; K.dq = P.dq; K.flags = P.flags;
+    K.n_shift = 0; K.skip_before = 0; K.slot0 = P.slot_of[0];
+    K.net_groups = P.net_groups; K.dbg = 0; K.net_filter_all = 0;
+    K.n_dshift = P.n_dshift; K.dskip_before = P.dskip_before;
+    K.tcp_emit = P.tcp_emit; K.tseg_cap = P.tseg_cap; K.tseg = P.tseg; K.tseg_cnt = P.tseg_cnt; K.tmask = P.tmask;
+    K.ndeep_net = nullptr; K.ndeep_dns = nullptr;
+    return net_slow(R, parse_cfg(P), P, K, off, i, K.slot0, true);
+}
+
+#ifndef PV_LEAN_LEVEL
+#define PV_LEAN_LEVEL 0 // tuning: 1 ring only, 2 + parse and counters, 3 + histogram, 4 + IP log, 0 everything
+#endif
+__device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ NetState S;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
+    if (threadIdx.x == 0) S.nd = 0;
+    if (threadIdx.x < PV_MAX_SHIFTS) S.pt.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+    __syncthreads();
+    const PV_G uint8_t *const recs = P.recs;
+    const PV_G uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint32_t rec_bytes = (uint32_t)P.rec_bytes;
+    const uint32_t slot = P.slot_of[0];
+    const uint32_t groups = P.net_groups;
+    const bool tops = groups & PV_NET_TOP_IPS_BIT, card = groups & PV_NET_CARDINALITY_BIT;
+    const uint32_t ts_nano = P.ts_nano;
+    HostNets h;
+    {
+        const uint32_t n4 = P.nets.n4;
+        h.a0 = P.nets.v4_addr[0]; h.m0 = P.nets.v4_mask[0]; h.e0 = n4 > 0 ? ~0u : 0u;
+        h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
+    }
+    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
+    const uint64_t wbeg = (uint64_t)blockIdx.x * P.wt_per_block;
+    const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + 3) / 4) : 0u;
+    NetWave &NW = S.w[wave];
+    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + 4ull * min(k, ntl - 1); };
+    auto issue_rows = [&](uint32_t k) {
+        const uint64_t r = tile_of(k) * PV_WT + lane;
+        const uint32_t row = k % PV_NL_OROWS;
+        dma4(offs + min<uint64_t>(r, last), lds_addr(&NW.lo[row][0]));
+        const uint32_t ha = lds_addr(&NW.hi[row]) - 4 * 63;
+        if (lane == 63) dma4(offs + min<uint64_t>(r + 1, last), ha);
+    };
+    auto issue_tile = [&](uint32_t k) {
+        const uint32_t row = k % PV_NL_OROWS;
+        const uint64_t t = tile_of(k);
+        const uint32_t o = NW.lo[row][lane];
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
+        const uint32_t b1 = t * PV_WT + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row]);
+        const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
+        const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
+        const uint32_t dst = lds_addr(&NW.slot[k % PV_NL_Q][0]);
+#pragma unroll
+        for (int j = 0; j < PV_NL_NJ; j++) {
+            const uint32_t ch = (uint32_t)(j * 64) + lane;
+            const uint32_t src = packed ? base + min(ch, nch - 1) * 16 : (o & ~15u) + 16u * j;
+            dma16(recs + src, dst + j * 1024);
+        }
+    };
+    auto refill = [&](uint32_t k) {
+        issue_rows(k + PV_NL_Q + 2);
+        PV_VMCNT(2 * PV_NL_OPS);
+        issue_tile(k + PV_NL_Q);
+    };
+    if (ntl) {
+        issue_rows(0);
+        issue_rows(1);
+        PV_VMCNT(0);
+        for (uint32_t j = 0; j < PV_NL_Q; j++) {
+            issue_rows(j + 2);
+            if (j >= 2) PV_VMCNT(2 * PV_NL_OPS);
+            issue_tile(j);
+        }
+    }
+    // fast lanes' counters, 16-bit fields (a lane counts at most one record per tile of its
+    // wave, and the host keeps a wave's tiles below 2^16): in | out << 16 | unknown << 32,
+    // udp | tcp << 16 | other << 32 | syn << 48
+    uint64_t cd = 0, cl = 0;
+    NetCtr c; // general-path records
+    c.zero();
+    for (uint32_t k = 0; k < ntl; k++) {
+        PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed
+        const uint32_t sl = k % PV_NL_Q, row = k % PV_NL_OROWS;
+        const uint64_t t = tile_of(k);
+        const uint64_t r0 = t * PV_WT, i = r0 + lane;
+        const bool active = i < n;
+        const uint32_t off = NW.lo[row][lane];
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
+        const uint32_t b1 = r0 + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row]);
+        const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
+        const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
+        const uint32_t *Ls = NW.slot[sl];
+        const uint32_t gb = packed ? base : (off & ~15u);
+        const uint32_t lim = packed ? nch * 16 - 4 : PV_NL_SLOT / PV_WT - 4;
+        const uint32_t rel = off - gb;
+        if (PV_LEAN_LEVEL == 1) {
+            cd += active ? 1ull : 0ull;
+            asm volatile("" ::: "memory");
+            refill(k);
+            continue;
+        }
+        RecW rw;
+        if (packed) recw_load_packed(Ls, rel, rw);
+        else recw_load_window(Ls, rel >> 2, rel & 3, lane * 4, rw);
+        FastRec f = fast_fields(rw, h);
+        const bool fast = active & ((rel >> 2) + 17 <= (lim + 4) >> 2) & (f.ok != 0);
+        const uint64_t slowm = __ballot(active & !fast);
+        if (!slowm) {
+            asm volatile("" ::: "memory");
+            refill(k);
+        }
+        cd += fast ? 1ull << (f.dir * 16) : 0ull;
+        cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
+        uint32_t hv = fast ? f.caplen : PV_NOH;
+        const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
+        const bool ipok = fast & (f.dir != 2) & (ip != 0);
+        uint64_t ek = tops && ipok ? ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
+                                         ((uint64_t)f.dir << 32) | ip
+                                   : 0ull;
+        if (card && !tops) {
+            // cardinality without top IPs: first-occurrence coupons straight to the table
+            if (ipok) {
+                uint64_t h1, h2;
+                murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+                __hip_atomic_fetch_min(P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)(f.dir == 0 ? CPC_SRC : CPC_DST) * PV_CPC_COUPONS +
+                                           cpc_coupon(h1, h2),
+                                       (int64_t)(P.gbase + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        // DNS over UDP (the DNS handler takes the pcap input's UDP signal itself)
+        const uint32_t port = (fast & (f.l4 == 17)) ? dns_port_bf(rw.at(50)) : 0u;
+        DnsMsgW dm{};
+        bool isdns = port != 0;
+        if (__ballot(isdns)) {
+            if (isdns) {
+                const Parsed o = fast_parsed(f, rw, ts_nano, off);
+                uint32_t dp = 0;
+                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)o.sec >= S.pt.dthresh[q];
+                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
+                DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
+                d.fkey = fast_flowkey(rw);
+                dm = msg_words(d);
+            }
+        }
+        bool istcp = fast & (f.l4 == 6), hasseg = false;
+        PvTcpSeg seg;
+        const uint32_t temit = P.tcp_emit;
+        if (temit && __ballot(istcp)) {
+            if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
+        }
+        // general-path records of the tile (VLAN, IPv6, options, tunnels, short windows)
+        if (slowm) {
+            if (active && !fast) {
+                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
+                const SlowOut so = net_slow_p(Pp, R, off, i);
+                Parsed o;
+                o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
+                c.add(o);
+                hv = so.caplen;
+                ek = so.ek;
+                dm = so.dm;
+                isdns = so.isdns;
+                istcp = so.l4 == 6;
+            }
+            asm volatile("" ::: "memory");
+        }
+        if (PV_LEAN_LEVEL == 2) {
+            if (slowm) refill(k);
+            asm volatile("" ::: "memory");
+            continue;
+        }
+        if (__ballot(hv != PV_NOH && hv > 65535)) {
+            if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
+        }
+        hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
+        if (PV_LEAN_LEVEL == 3) {
+            if (slowm) refill(k);
+            continue;
+        }
+        const uint64_t m = __ballot(isdns);
+        if (m) {
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(&S.nd, (uint32_t)__popcll(m));
+            q = __builtin_amdgcn_readlane(q, 0);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (isdns) {
+                PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(P.dq) + 2 * (wbeg * PV_WT + q + below);
+                dd[0] = dm.a;
+                dd[1] = dm.b;
+            }
+        }
+        if (tops && active) P.iplog[i] = ek;
+        if (PV_LEAN_LEVEL == 4) {
+            if (slowm) refill(k);
+            continue;
+        }
+        if (temit) {
+            const uint64_t tm = __ballot(istcp);
+            if (tm) {
+                if (lane == 0) P.tmask[t] = tm;
+                tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, seg, lane);
+            }
+        }
+        if (slowm) refill(k);
+    }
+    PV_VMCNT(0);
+    // fast lanes' fields into the counters (every fast record is Ethernet + IPv4: an event,
+    // a deep sample, total and IPv4)
+    {
+        const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
+        const uint32_t nf = fin + fout + funk;
+        c.nev += nf; c.n4 += nf;
+        c.nin += fin; c.nout += fout; c.nunk += funk;
+        c.nudp += (uint32_t)(cl & 0xffff); c.ntcp += (uint32_t)((cl >> 16) & 0xffff);
+        c.noth += (uint32_t)((cl >> 32) & 0xffff); c.nsyn += (uint32_t)(cl >> 48);
+    }
+    NetK K;
+    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
+    if (ntl) knet_flush(K, slot, c);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
+        if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
+    if (threadIdx.x == 0) {
+        P.mq_cnt[blockIdx.x] = 0;
+        P.dq_cnt[blockIdx.x] = S.nd;
+        if (S.nd) atomicAdd(P.n_dns, S.nd);
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(const PvParams *__restrict__ Pp) { net_pass<true>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(const PvParams *__restrict__ Pp) { net_pass<false>(Pp); }
+extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
 
 // ------------------------------------------------------------------ the DNS pass
 // One lane per DNS message of the Net pass's work list (same workgroup mapping).

@@ -64,7 +64,7 @@ void ts_of(const Iface &f, uint64_t t, uint32_t &sec, uint32_t &nsec)
         return;
     }
     uint64_t div = 1;
-    for (uint32_t k = 0; k < f.tsres && k < 19; k++) div *= 10;
+    for (uint32_t k = 0; k < f.tsres; k++) div *= 10; // tsres <= 19 (checked at the IDB)
     sec = (uint32_t)(t / div);
     const uint64_t frac = t % div;
     if (f.tsres <= 9) {
@@ -133,6 +133,9 @@ int pcapng_to_records(const uint8_t *buf, size_t bytes, std::vector<uint8_t> *ou
                     const uint8_t v = b[q + 4];
                     f.pow2 = (v & 0x80) != 0;
                     f.tsres = v & 0x7f;
+                    // 10^-20 s and finer do not fit the 64-bit timestamp arithmetic (and no
+                    // capture writes them): refused, not silently wrapped
+                    if (!f.pow2 && f.tsres > 19) return PVNG_EFORMAT;
                 }
                 q += 4 + ((olen + 3u) & ~3u);
             }

@@ -75,3 +75,10 @@ def test_dnstap_invalid_msg_type():
     with pytest.raises(Exception, match="dnstap_msg_type contained an invalid/unsupported type. Valid types: auth, "
                                         "client, forwarder, resolver, stub, tool, update"):
         run({"dnstap_msg_type": "bogus"})
+
+
+def test_dnstap_deep_sampling_refused():
+    """each manager draws per dnstap event (net/v1 :840, dns/v1 :1409); the dnstap path has no
+    not-deep accounting, so a sampled context refuses instead of reporting every event as deep"""
+    with pytest.raises(pa.PvError, match="deep_sample_rate"):
+        pa.dnstap_reader(FIX, periods=1, net_config={}, dns_config={}, deep_sample_rate=50)

@@ -57,3 +57,20 @@ def test_pcapng_errors(tmp_path):
     p.write_bytes(ng)
     lt, nano, recs = pa.read_pcap(str(p))
     assert nano == 1 and len(records(recs)) == len(pcap_packets(pcap)[1])
+
+
+@pytest.mark.parametrize("tsresol", [20, 29, 73, 127])
+def test_pcapng_decimal_resolution_out_of_range(tsresol):
+    """if_tsresol 10^-k with k > 19 does not fit 64-bit timestamp arithmetic: refused as a
+    format error (no SIGFPE, no wrapped timestamps)"""
+    pcap = open(os.path.join(GOLD, "dns_udp_mixed_rcode.pcap"), "rb").read()
+    lt, pk = pcap_packets(pcap)
+    ng = to_pcapng(pcap[:24] + pcap[24:24 + 16 + pk[0][2]])  # one packet, default 10^-6
+    # rewrite the IDB with the resolution option
+    from tests.pcapng_util import _blk, _opt
+    shb_len, = struct.unpack_from("<I", ng, 4)
+    idb = _blk(1, struct.pack("<HHI", lt, 0, 262144) + _opt(9, bytes([tsresol])) + _opt(0, b""))
+    rest = ng[shb_len:]
+    old_idb_len, = struct.unpack_from("<I", rest, 4)
+    with pytest.raises(pa.PvError):
+        pa.pcapng_records(ng[:shb_len] + idb + rest[old_idb_len:])
