@@ -308,6 +308,10 @@ void pv_free(void *p);
  * (PV_EUNSUPPORTED). *out: pv_free. */
 #define PV_HANDLER_NET 1u
 #define PV_HANDLER_DNS 2u
+/* period argument of pv_window_prometheus / pv_window_opentelemetry: what
+ * StreamMetricsHandler::window_prometheus / window_opentelemetry read (src/StreamHandler.h:226-247):
+ * bucket 1 of a handler whose manager holds more than one bucket, else bucket 0 */
+#define PV_PERIOD_AUTO 0xFFFFFFFFu
 int pv_window_prometheus(pv_ctx *ctx, uint32_t period, uint32_t handlers, const char *const *label_keys,
                          const char *const *label_values, uint32_t n_labels, char **out);
 /* OpenTelemetry metrics of bucket `period` of the selected v1 handlers, as the protobuf
@@ -318,6 +322,40 @@ int pv_window_opentelemetry(pv_ctx *ctx, uint32_t period, uint32_t handlers, con
                             const char *const *label_values, uint32_t n_labels, uint8_t **out, size_t *bytes);
 /* Process-wide label on every Prometheus sample (Metric::add_static_label). */
 int pv_add_static_label(const char *key, const char *value);
+
+/* Heartbeat (PcapInputEventProxy::heartbeat_signal -> StreamMetricsHandler::check_period_shift,
+ * src/StreamHandler.h:254-257, src/AbstractMetricsManager.h:462-470; wired in
+ * net/v1/NetStreamHandler.cpp:99-102 and dns/v1/DnsStreamHandler.cpp:219-222): each manager
+ * whose next shift second the stamp has reached shifts its window with no event (num_periods
+ * > 1); the DNS manager's on_period_shift (dns/v1/DnsStreamHandler.h:252-267) times out the
+ * open transactions the stamp expires into the new live bucket and takes the top_slow p90
+ * thresholds from the bucket just closed. A context that has seen no record ignores it. */
+int pv_check_period_shift(pv_ctx *ctx, int64_t sec, int64_t nsec);
+
+/* External metrics buckets: the bucket half of the handler object
+ * (StreamHandler::merge / window_json(j, bucket) / window_prometheus(out, bucket, labels) /
+ * window_opentelemetry(scope, bucket, labels), src/StreamHandler.h:72-77,221-269), which a policy
+ * uses to fold like handlers across taps (Policy::_get_merged_buckets, src/Policies.cpp:420-446).
+ * A pv_bucket is a host-side snapshot of one handler's bucket (handler = PV_HANDLER_NET or
+ * PV_HANDLER_DNS, v1 handlers). */
+typedef struct pv_bucket pv_bucket;
+/* StreamMetricsHandler::merge(bucket, period, prometheus, merged): *bucket == NULL -> a new bucket
+ * holding this context's bucket `period` (merged: the fold of its `period` newest buckets,
+ * multiple_merge), as simple_merge / multiple_merge create it (src/AbstractMetricsManager.h:649-706);
+ * *bucket != NULL (a bucket of the same handler, from any context) -> this context's bucket folded
+ * into it with Aggregate::SUM (quantiles summed p-wise, src/Metrics.h:356-372). prometheus != 0:
+ * period 1 when the manager holds more than one bucket, else 0, never merged. Period errors
+ * carry the reference's PeriodException texts. */
+int pv_bucket_merge(pv_ctx *ctx, uint32_t handler, pv_bucket **bucket, uint32_t period, int prometheus, int merged);
+/* window_external_json / _prometheus / _opentelemetry (src/AbstractMetricsManager.h:565-599),
+ * rendered with ctx's handler config (groups, topn_count, percentile threshold). JSON:
+ * {"packets": {...}} or {"dns": {...}}. *out: pv_free. */
+int pv_bucket_json(pv_ctx *ctx, const pv_bucket *bucket, char **out);
+int pv_bucket_prometheus(pv_ctx *ctx, const pv_bucket *bucket, const char *const *label_keys,
+                         const char *const *label_values, uint32_t n_labels, char **out);
+int pv_bucket_opentelemetry(pv_ctx *ctx, const pv_bucket *bucket, const char *const *label_keys,
+                            const char *const *label_values, uint32_t n_labels, uint8_t **out, size_t *bytes);
+void pv_bucket_free(pv_bucket *bucket);
 
 /* Device-state regions of the live window, for a multi-GPU reduce:
  *   SUM region: uint64 counters and dense tables (all-reduce SUM)

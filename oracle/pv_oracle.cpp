@@ -205,10 +205,23 @@ struct Cpc {
 template <typename T>
 struct ExactQuantile {
     std::vector<T> v;
+    std::vector<T> qsum; // Quantile::_quantiles_sum (src/Metrics.h:338-372)
     void update(T x) { v.push_back(x); }
     void merge(const ExactQuantile &o) { v.insert(v.end(), o.v.begin(), o.v.end()); }
+    // Quantile::merge(other, Aggregate::SUM) (src/Metrics.h:356-372): once this sketch holds
+    // data, the p50..p99 of every further non-empty sketch are added p-wise to a sum that the
+    // output prefers; the sketch itself stays as it was. An empty sketch merges as usual.
+    void merge_sum(const ExactQuantile &o)
+    {
+        if (v.empty()) { merge(o); return; }
+        if (o.v.empty()) return;
+        const std::vector<T> oq = o.quantiles_of_sketch();
+        if (qsum.empty()) qsum = quantiles_of_sketch();
+        for (int i = 0; i < 4; i++) qsum[i] += oq[i];
+    }
     bool empty() const { return v.empty(); }
-    std::vector<T> quantiles() const
+    std::vector<T> quantiles() const { return qsum.empty() ? quantiles_of_sketch() : qsum; }
+    std::vector<T> quantiles_of_sketch() const
     {
         std::vector<T> s = v;
         std::sort(s.begin(), s.end());
@@ -368,6 +381,9 @@ struct Config {
     bool only_queries = false, only_responses = false; // (:114-119)
     bool only_dnssec = false;                           // "only_dnssec_response" (:120-122)
     bool psl = false;                                   // "public_suffix_list" config (:187-189)
+    std::vector<int64_t> heartbeats; // heartbeat stamps (seconds, ascending): each fires before the first
+                                     // packet past it (or at the end of the capture, before end_tstamp)
+    int single = -1;                 // >= 0: output bucket `single` alone (window_single_json)
     std::vector<uint16_t> only_qtype;                   // "only_qtype" (:131-150)
     std::vector<std::string> only_qname;                // "only_qname" (:151-160), lower-case; predicate mode
     std::vector<std::string> only_qname_suffix;         // "only_qname_suffix" (:161-169), lower-case
@@ -883,11 +899,14 @@ struct NetBucket : BaseBucket {
     ExactTop<uint32_t> top4;
     ExactTop<std::string> top6;
 
-    void merge(const NetBucket &o)
+    // NetworkMetricsBucket::specialized_merge (net/v1/NetStreamHandler.cpp:285-330); sum:
+    // Aggregate::SUM, the quantile rule of a policy's merged handlers
+    void merge(const NetBucket &o, bool sum = false)
     {
         UDP += o.UDP; TCP += o.TCP; OtherL4 += o.OtherL4; IPv4 += o.IPv4; IPv6 += o.IPv6; TCP_SYN += o.TCP_SYN;
         in += o.in; out += o.out; unk += o.unk; total += o.total; filtered += o.filtered;
-        payload.merge(o.payload);
+        if (sum) payload.merge_sum(o.payload);
+        else payload.merge(o.payload);
         src.merge(o.src);
         dst.merge(o.dst);
         top4.merge(o.top4);
@@ -966,13 +985,15 @@ struct DnsBucket : BaseBucket {
     ExactTop<std::string> qname2, qname3, nx, refused, srvfail, nodata, noerror, sized_resp, slow_in, slow_out, ecs;
     ExactTop<uint16_t> udp_port, qtype, rcode;
 
-    void merge(const DnsBucket &o)
+    // DnsMetricsBucket::specialized_merge (dns/v1/DnsStreamHandler.cpp:658-733); sum: Aggregate::SUM
+    void merge(const DnsBucket &o, bool sum = false)
     {
         xacts_total += o.xacts_total; xacts_in += o.xacts_in; xacts_out += o.xacts_out;
         xacts_timed_out += o.xacts_timed_out; queries += o.queries; replies += o.replies; UDP += o.UDP;
         TCP += o.TCP; IPv4 += o.IPv4; IPv6 += o.IPv6; NX += o.NX; REFUSED += o.REFUSED; SRVFAIL += o.SRVFAIL;
         NOERROR += o.NOERROR; NODATA += o.NODATA; total += o.total; filtered += o.filtered; query_ecs += o.query_ecs;
-        xact_from.merge(o.xact_from); xact_to.merge(o.xact_to); ratio.merge(o.ratio);
+        if (sum) { xact_from.merge_sum(o.xact_from); xact_to.merge_sum(o.xact_to); ratio.merge_sum(o.ratio); }
+        else { xact_from.merge(o.xact_from); xact_to.merge(o.xact_to); ratio.merge(o.ratio); }
         hist_from.merge(o.hist_from); hist_to.merge(o.hist_to); ecs.merge(o.ecs);
         qname.merge(o.qname);
         qname2.merge(o.qname2); qname3.merge(o.qname3); nx.merge(o.nx); refused.merge(o.refused);
@@ -1087,6 +1108,16 @@ struct Engine {
         else ttl_ms = c.xact_ttl_ms;
     }
 
+    // heartbeat_signal -> check_period_shift in each handler (src/AbstractMetricsManager.h:462-470;
+    // net/v1/NetStreamHandler.cpp:99-102, dns/v1/DnsStreamHandler.cpp:219-222): a shift with no
+    // event, the DNS manager's on_period_shift included
+    void heartbeat(TS ts)
+    {
+        net.maybe_shift(ts);
+        net2.maybe_shift(ts);
+        if (dns.maybe_shift(ts)) on_dns_period_shift(ts);
+        if (dns2.maybe_shift(ts)) on_dns2_period_shift(ts);
+    }
     void start(TS ts)
     {
         net.set_start(ts);
@@ -2124,28 +2155,45 @@ static void dns_json(J &j, const DnsBucket &b, size_t topn, uint32_t g)
 }
 
 // merged window (AbstractMetricsManager::window_merged_json) or a single bucket
+// AbstractMetricsBucket::merge (src/AbstractMetricsManager.h:177-195): base fields, then the
+// handler's specialized_merge (sum: Aggregate::SUM)
 template <typename B>
-static std::unique_ptr<B> window_bucket(const Window<B> &w, unsigned window)
+static void bucket_merge(B &out, const B &m, bool firstb, bool sum = false)
+{
+    out.num_events += m.num_events;
+    out.num_samples += m.num_samples;
+    out.period_length += m.period_length;
+    if (firstb || m.start.sec < out.start.sec) out.start.sec = m.start.sec;
+    if (firstb || m.end.sec > out.end.sec) out.end.sec = m.end.sec;
+    if constexpr (std::is_same<B, NetBucket>::value || std::is_same<B, DnsBucket>::value) out.merge(m, sum);
+    else out.merge(m);
+}
+// a fresh bucket folding buckets [from, from + count) of the window (DEFAULT aggregate); a
+// union of CPC sketches reports the ICON estimate even for one input
+template <typename B>
+static std::unique_ptr<B> fold_buckets(const Window<B> &w, unsigned from, unsigned count)
 {
     std::unique_ptr<B> out(new B());
+    bool firstb = true;
+    for (unsigned k = from; k < from + count && k < w.buckets.size(); k++) {
+        bucket_merge(*out, *w.buckets[k], firstb);
+        firstb = false;
+    }
+    return out;
+}
+template <typename B>
+static std::unique_ptr<B> window_bucket(const Window<B> &w, unsigned window, int single = -1)
+{
+    std::unique_ptr<B> out(new B());
+    if (single >= 0) {
+        *out = *w.buckets.at((size_t)single);
+        return out;
+    }
     if (window <= 1) {
         *out = *w.buckets.at(0);
         return out;
     }
-    bool firstb = true;
-    unsigned p = window;
-    for (auto &m : w.buckets) {
-        if (p-- == 0) break;
-        out->num_events += m->num_events;
-        out->num_samples += m->num_samples;
-        out->period_length += m->period_length;
-        if (firstb || m->start.sec < out->start.sec) out->start.sec = m->start.sec;
-        if (firstb || m->end.sec > out->end.sec) out->end.sec = m->end.sec;
-        firstb = false;
-        out->merge(*m);
-        // a union of CPC sketches reports the ICON estimate even for one input
-    }
-    return out;
+    return fold_buckets(w, 0, window);
 }
 
 // ---------------------------------------------------------------- pcap reader
@@ -2215,6 +2263,15 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "only_responses") c.only_responses = atoi(v.c_str()) != 0;
         else if (k == "only_dnssec_response") c.only_dnssec = atoi(v.c_str()) != 0;
         else if (k == "public_suffix_list") c.psl = atoi(v.c_str()) != 0;
+        else if (k == "single") c.single = atoi(v.c_str());
+        else if (k == "heartbeats") {
+            size_t q = 0;
+            while (q < v.size()) {
+                size_t e2 = v.find(',', q);
+                c.heartbeats.push_back(atoll(v.substr(q, e2 == std::string::npos ? std::string::npos : e2 - q).c_str()));
+                q = e2 == std::string::npos ? v.size() : e2 + 1;
+            }
+        }
         else if (k == "only_qname_suffix") {
             size_t q = 0;
             while (q < v.size()) {
@@ -2271,30 +2328,38 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
     Pkt pk;
     TS last;
     bool first = true;
+    size_t hb = 0;
     while (f.next(pk)) {
         if (first) { e.start(pk.ts); first = false; }
+        for (; hb < c.heartbeats.size() && c.heartbeats[hb] < pk.ts.sec; hb++) e.heartbeat(TS{c.heartbeats[hb], 0});
         e.process(pk);
         last = pk.ts;
     }
+    if (!first)
+        for (; hb < c.heartbeats.size(); hb++) e.heartbeat(TS{c.heartbeats[hb], 0});
     if (!first) e.end(last);
     e.tcp_close_all(); // after end_tstamp_cb (PcapInputStream.cpp:514-522)
     if (e.tcp_log) fclose(e.tcp_log);
     J j;
     j.obj();
     unsigned w = c.window <= 1 ? 1 : c.window;
-    j.key(std::to_string(w) + "m");
+    j.key(c.single >= 0 ? "p" + std::to_string(c.single) : std::to_string(w) + "m");
     j.obj();
-    auto nb = window_bucket(e.net, w);
+    if (c.single >= 0 && ((size_t)c.single >= e.net.buckets.size() || (size_t)c.single >= e.dns.buckets.size())) {
+        *out = strdup("requested metrics period has not yet accumulated");
+        return -3;
+    }
+    auto nb = window_bucket(e.net, w, c.single);
     j.key("packets"); j.obj(); net_json(j, *nb, c.topn_count, c.net_groups); j.end_obj();
     if (c.net2_groups) {
-        auto n2 = window_bucket(e.net2, w);
+        auto n2 = window_bucket(e.net2, w, c.single);
         j.key("net"); j.obj(); net2_json(j, *n2, c.topn_count, c.net2_groups); j.end_obj();
     }
     if (c.dns2_groups) {
-        auto d2 = window_bucket(e.dns2, w);
+        auto d2 = window_bucket(e.dns2, w, c.single);
         j.key("dns"); j.obj(); dns2_json(j, *d2, c.topn_count, c.dns2_groups); j.end_obj();
     } else {
-        auto db = window_bucket(e.dns, w);
+        auto db = window_bucket(e.dns, w, c.single);
         j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_groups); j.end_obj();
     }
     j.end_obj();
@@ -2304,6 +2369,64 @@ int pvo_run(const uint8_t *file, size_t len, const char *cfg, char **out)
 }
 
 void pvo_free(char *p) { free(p); }
+
+// Policy::_get_merged_buckets (src/Policies.cpp:420-446) over like handlers, one per capture:
+// StreamMetricsHandler::merge(bucket, period, prometheus, merged) (src/StreamHandler.h:259-269)
+// -> simple_merge / multiple_merge (src/AbstractMetricsManager.h:649-706). The first handler
+// makes a fresh bucket of its period (or of its `period` newest buckets, merged); each further
+// one folds its own into it with Aggregate::SUM. prometheus: period 1 of a manager holding more
+// than one, else 0, never merged. Output {"packets": {...}, "dns": {...}} (window_external_json).
+int pvo_run_policy(const uint8_t *const *files, const size_t *lens, uint32_t n, const char *cfg, uint32_t period,
+                   int merged, int prometheus, char **out)
+{
+    using namespace pvo;
+    Config c;
+    std::string err;
+    *out = nullptr;
+    if (!parse_config(cfg, c, err)) { *out = strdup(err.c_str()); return -1; }
+    topn_pct = c.topn_pct;
+    std::vector<std::unique_ptr<Engine>> engines;
+    for (uint32_t i = 0; i < n; i++) {
+        PcapFile f;
+        if (!f.open(files[i], lens[i], err)) { *out = strdup(err.c_str()); return -2; }
+        engines.emplace_back(new Engine(c));
+        Engine &e = *engines.back();
+        e.linktype = f.linktype;
+        Pkt pk;
+        TS last;
+        bool first = true;
+        size_t hb = 0;
+        while (f.next(pk)) {
+            if (first) { e.start(pk.ts); first = false; }
+            for (; hb < c.heartbeats.size() && c.heartbeats[hb] < pk.ts.sec; hb++) e.heartbeat(TS{c.heartbeats[hb], 0});
+            e.process(pk);
+            last = pk.ts;
+        }
+        if (!first) e.end(last);
+        e.tcp_close_all();
+    }
+    auto pick = [&](auto &win, std::unique_ptr<typename std::remove_reference<decltype(*win.buckets[0])>::type> &acc, bool firstb) {
+        uint64_t p = period;
+        bool m = merged != 0;
+        if (prometheus) { p = win.buckets.size() > 1 ? 1 : 0; m = false; }
+        auto b = m ? fold_buckets(win, 0, (unsigned)p) : fold_buckets(win, (unsigned)p, 1);
+        if (firstb) acc = std::move(b);
+        else bucket_merge(*acc, *b, false, true);
+    };
+    std::unique_ptr<NetBucket> nb;
+    std::unique_ptr<DnsBucket> db;
+    for (uint32_t i = 0; i < n; i++) {
+        pick(engines[i]->net, nb, i == 0);
+        pick(engines[i]->dns, db, i == 0);
+    }
+    J j;
+    j.obj();
+    j.key("packets"); j.obj(); net_json(j, *nb, c.topn_count, c.net_groups); j.end_obj();
+    j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_groups); j.end_obj();
+    j.end_obj();
+    *out = strdup(j.s.c_str());
+    return 0;
+}
 
 // Exposed for the sketch pinning tests: estimate of a CPC sketch fed with the
 // given sequence of uint32 values (update(uint32_t)) or byte strings.

@@ -166,7 +166,10 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_dns_event_seconds", "pv_dns_event_seconds_host", "pv_comm_unique_id", "pv_comm_init",
            "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count",
            "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label",
-           "pv_window_opentelemetry"]
+           "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
+           "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free"]
+PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
+PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
 
@@ -216,6 +219,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                             U32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_free.argtypes = [P]
     lib.pv_free.restype = None
+    lib.pv_check_period_shift.argtypes = [P, I64, I64]
+    lib.pv_bucket_merge.argtypes = [P, U32, ctypes.POINTER(P), U32, ctypes.c_int, ctypes.c_int]
+    lib.pv_bucket_json.argtypes = [P, P, ctypes.POINTER(P)]
+    lib.pv_bucket_prometheus.argtypes = [P, P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), U32,
+                                         ctypes.POINTER(P)]
+    lib.pv_bucket_opentelemetry.argtypes = [P, P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                            U32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_bucket_free.argtypes = [P]
+    lib.pv_bucket_free.restype = None
     lib.pv_state_regions.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(P),
                                      ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_set_global_base.argtypes = [P, U64]
@@ -334,6 +346,24 @@ def dnstap_reader(path: str, periods: int = 1, **kw) -> dict:
 def pcap_file_bytes(records: bytes, linktype: int = 1, ts_nano: int = 0) -> bytes:
     magic = 0xA1B23C4D if ts_nano else 0xA1B2C3D4
     return struct.pack("<IHHiIII", magic, 2, 4, 0, 0, 262144, linktype) + records
+
+
+class Bucket:
+    """A pv_bucket: one handler's metrics bucket taken out of a context (StreamHandler::merge)."""
+
+    def __init__(self, lib, ptr: int, handler: str):
+        self.lib, self.ptr, self.handler = lib, ptr, handler
+
+    def free(self):
+        if self.ptr:
+            self.lib.pv_bucket_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class RecordIndex:
@@ -497,6 +527,56 @@ class PvHandlers:
 
     def set_end_tstamp(self, sec: int, nsec: int):
         self._check(self.lib.pv_set_end_tstamp(self.ctx, sec, nsec), "pv_set_end_tstamp")
+
+    def set_start_tstamp(self, sec: int, nsec: int):
+        self._check(self.lib.pv_set_start_tstamp(self.ctx, sec, nsec), "pv_set_start_tstamp")
+
+    def check_period_shift(self, sec: int, nsec: int = 0):
+        """heartbeat_signal -> check_period_shift in both handlers (pv_check_period_shift)."""
+        self._check(self.lib.pv_check_period_shift(self.ctx, sec, nsec), "pv_check_period_shift")
+
+    def merge(self, handler: str, bucket: Optional["Bucket"], period: int, prometheus: bool = False,
+              merged: bool = False) -> "Bucket":
+        """StreamHandler::merge(bucket, period, prometheus, merged) of handler "net" or "dns":
+        a new Bucket when bucket is None, else this handler's bucket folded into it with
+        Aggregate::SUM (the same Bucket is returned)."""
+        h = {"net": PV_HANDLER_NET, "dns": PV_HANDLER_DNS}[handler]
+        ptr = ctypes.c_void_p(bucket.ptr if bucket is not None else None)
+        self._check(self.lib.pv_bucket_merge(self.ctx, h, ctypes.byref(ptr), period, int(prometheus), int(merged)),
+                    "pv_bucket_merge")
+        if bucket is not None:
+            return bucket
+        return Bucket(self.lib, ptr.value, handler)
+
+    def bucket_json(self, bucket: "Bucket") -> dict:
+        """window_json(j, bucket): {"packets": {...}} or {"dns": {...}}."""
+        out = ctypes.c_void_p()
+        self._check(self.lib.pv_bucket_json(self.ctx, bucket.ptr, ctypes.byref(out)), "pv_bucket_json")
+        txt = ctypes.string_at(out.value).decode()
+        self.lib.pv_free(out)
+        return json.loads(txt)
+
+    def bucket_prometheus(self, bucket: "Bucket", labels: Optional[dict] = None) -> str:
+        labels = labels or {}
+        keys = (ctypes.c_char_p * max(1, len(labels)))(*[k.encode() for k in labels])
+        vals = (ctypes.c_char_p * max(1, len(labels)))(*[str(v).encode() for v in labels.values()])
+        out = ctypes.c_void_p()
+        self._check(self.lib.pv_bucket_prometheus(self.ctx, bucket.ptr, keys, vals, len(labels), ctypes.byref(out)),
+                    "pv_bucket_prometheus")
+        txt = ctypes.string_at(out.value).decode()
+        self.lib.pv_free(out)
+        return txt
+
+    def bucket_opentelemetry(self, bucket: "Bucket", labels: Optional[dict] = None) -> bytes:
+        labels = labels or {}
+        keys = (ctypes.c_char_p * max(1, len(labels)))(*[k.encode() for k in labels])
+        vals = (ctypes.c_char_p * max(1, len(labels)))(*[str(v).encode() for v in labels.values()])
+        out, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self.lib.pv_bucket_opentelemetry(self.ctx, bucket.ptr, keys, vals, len(labels), ctypes.byref(out),
+                                                     ctypes.byref(n)), "pv_bucket_opentelemetry")
+        data = ctypes.string_at(out.value, n.value)
+        self.lib.pv_free(out)
+        return data
 
     def set_global_base(self, base: int):
         self._check(self.lib.pv_set_global_base(self.ctx, base), "pv_set_global_base")

@@ -647,13 +647,14 @@ void clear_part(pv_ctx *c, int part, uint32_t s)
 // _period_shift (src/AbstractMetricsManager.h:276-305) on the host mirror of one window: the
 // live bucket becomes read-only at T, the next ordinal's slot (reserved and cleared before
 // the batch that shifts) becomes live, the oldest beyond num_periods drops out.
-void win_shift(pv_ctx *c, Window &w, int64_t T)
+void win_shift(pv_ctx *c, Window &w, int64_t T, int64_t Tns = 0)
 {
-    w.meta[w.slots.front()].set_read_only(T, 0);
+    w.meta[w.slots.front()].set_read_only(T, Tns);
     w.ordinal++;
     const uint32_t s = w.slot_at(0);
     w.meta[s] = SlotMeta();
     w.meta[s].start_sec = T;
+    w.meta[s].start_nsec = Tns;
     w.slots.push_front(s);
     if (w.slots.size() > c->cfg.num_periods) w.slots.pop_back();
     w.next_shift_sec = T + 60;
@@ -770,6 +771,16 @@ struct HostBucket {
     std::vector<uint64_t> time2[3]; // DNS v2 per direction
     std::vector<double> ratio2[3];
     bool merged = false;
+    // an exported bucket (pv_bucket) after an Aggregate::SUM merge: Quantile::_quantiles_sum
+    // (src/Metrics.h:338-372), which the output prefers to the sketch's own quantiles, and the
+    // Histogram values, which keep merging while the quantile sketches do not
+    std::vector<uint64_t> qs_payload, qs_from, qs_to;
+    std::vector<double> qs_ratio;
+    bool hist_sep = false;
+    std::vector<uint64_t> hfrom_us, hto_us;
+    int64_t start_nsec = 0, end_sec = 0, end_nsec = 0;
+    const std::vector<uint64_t> &hist_from() const { return hist_sep ? hfrom_us : from_us; }
+    const std::vector<uint64_t> &hist_to() const { return hist_sep ? hto_us : to_us; }
 };
 
 template <typename T>
@@ -845,7 +856,8 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int 
         for (size_t i = m0; i < m1; i++) b.cpc[i] = std::min(b.cpc[i], cpc[i]);
         const SlotMeta &m = win.meta[s];
         b.period_length += m.read_only ? m.period_length : 0;
-        if (first || m.start_sec < b.start_sec) b.start_sec = m.start_sec;
+        if (first || m.start_sec < b.start_sec) { b.start_sec = m.start_sec; b.start_nsec = m.start_nsec; }
+        if (m.end_sec > b.end_sec) { b.end_sec = m.end_sec; b.end_nsec = m.end_nsec; }
         first = false;
         std::vector<TopRec> recs;
         int rc = read_topn(c, s + (part == PART_DNS ? PV_SLOTS : 0), recs);
@@ -960,10 +972,10 @@ void hist_json(Json &j, const char *key, std::vector<uint64_t> v)
 }
 
 template <typename T>
-void quant_json(Json &j, const char *key, const std::vector<T> &v)
+void quant_json(Json &j, const char *key, const std::vector<T> &v, const std::vector<T> *qsum = nullptr)
 {
     if (v.empty()) return;
-    auto q = quantiles(v);
+    auto q = qsum && !qsum->empty() ? *qsum : quantiles(v);
     const char *names[4] = {"p50", "p90", "p95", "p99"};
     j.key(key);
     j.obj();
@@ -1015,6 +1027,7 @@ void net_json(pv_ctx *c, Json &j, const HostBucket &b)
     }
     uint64_t cnt;
     auto q = hist_quantiles(&b.sum[PV_OFF_PAYLOAD], PV_PAYLOAD_BINS, cnt);
+    if (!b.qs_payload.empty()) q = b.qs_payload;
     if (cnt) {
         j.key("payload_size").obj();
         j.key("p50").u(q[0]); j.key("p90").u(q[1]); j.key("p95").u(q[2]); j.key("p99").u(q[3]);
@@ -1186,16 +1199,16 @@ void dns_json(pv_ctx *c, Json &j, const HostBucket &b)
         j.key("in").obj();
         j.key("total").u(d[DC_XIN]);
         top_json(j, "top_slow", tops_of(b, TM_SLOW_IN), topn, pct);
-        if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.to_us);
-        if (g & PV_DNS_HISTOGRAMS) hist_json(j, "histogram_us", b.to_us);
+        if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.to_us, &b.qs_to);
+        if (g & PV_DNS_HISTOGRAMS) hist_json(j, "histogram_us", b.hist_to());
         j.end_obj();
         j.key("out").obj();
         j.key("total").u(d[DC_XOUT]);
         top_json(j, "top_slow", tops_of(b, TM_SLOW_OUT), topn, pct);
-        if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.from_us);
-        if (g & PV_DNS_HISTOGRAMS) hist_json(j, "histogram_us", b.from_us);
+        if (g & PV_DNS_QUANTILES) quant_json(j, "quantiles_us", b.from_us, &b.qs_from);
+        if (g & PV_DNS_HISTOGRAMS) hist_json(j, "histogram_us", b.hist_from());
         j.end_obj();
-        if ((g & PV_DNS_QUANTILES) && !b.ratio.empty()) { j.key("ratio").obj(); quant_json(j, "quantiles", b.ratio); j.end_obj(); }
+        if ((g & PV_DNS_QUANTILES) && !b.ratio.empty()) { j.key("ratio").obj(); quant_json(j, "quantiles", b.ratio, &b.qs_ratio); j.end_obj(); }
         j.end_obj();
     }
     if (g & PV_DNS_TOP_PORTS) top_json(j, "top_udp_ports", dense_tops(&b.sum[PV_OFF_PORT], PV_PORT_BINS, 0), topn, pct);
@@ -1513,6 +1526,7 @@ void net_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
     uint64_t cnt;
     const uint64_t *h = &b.sum[PV_OFF_PAYLOAD];
     auto q = hist_quantiles(h, PV_PAYLOAD_BINS, cnt);
+    if (!b.qs_payload.empty() && cnt) q = b.qs_payload;
     uint64_t mx = 0;
     for (size_t i = 0; i < PV_PAYLOAD_BINS; i++)
         if (h[i]) mx = i;
@@ -1557,17 +1571,17 @@ void dns_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
         if (g & PV_DNS_QUANTILES) {
             if (!b.from_us.empty())
                 p.template summary<uint64_t>("dns_xact_out_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is client, in microseconds",
-                                    quantiles(b.from_us), vmax(b.from_us), b.from_us.size());
+                                    b.qs_from.empty() ? quantiles(b.from_us) : b.qs_from, vmax(b.from_us), b.from_us.size());
             if (!b.to_us.empty())
                 p.template summary<uint64_t>("dns_xact_in_quantiles_us", "Quantiles of transaction timing (query/reply pairs) when host is server, in microseconds",
-                                    quantiles(b.to_us), vmax(b.to_us), b.to_us.size());
+                                    b.qs_to.empty() ? quantiles(b.to_us) : b.qs_to, vmax(b.to_us), b.to_us.size());
             if (!b.ratio.empty())
                 p.template summary<double>("dns_xact_ratio_quantiles", "Quantiles of ratio of packet sizes in a DNS transaction (reply/query)",
-                                  quantiles(b.ratio), vmax(b.ratio), b.ratio.size());
+                                  b.qs_ratio.empty() ? quantiles(b.ratio) : b.qs_ratio, vmax(b.ratio), b.ratio.size());
         }
         if (g & PV_DNS_HISTOGRAMS) {
-            p.histogram("dns_xact_out_histogram_us", "Histogram of transaction timing (query/reply pairs) when host is client, in microseconds", b.from_us);
-            p.histogram("dns_xact_in_histogram_us", "Histogram of transaction timing (query/reply pairs) when host is server, in microseconds", b.to_us);
+            p.histogram("dns_xact_out_histogram_us", "Histogram of transaction timing (query/reply pairs) when host is client, in microseconds", b.hist_from());
+            p.histogram("dns_xact_in_histogram_us", "Histogram of transaction timing (query/reply pairs) when host is server, in microseconds", b.hist_to());
         }
         p.gauge("dns_xact_out_total", "Total egress DNS transactions (host is client)", d[DC_XOUT]);
         p.topn("dns_xact_out_top_slow", "qname", "Top QNAMES in transactions where host is the client and transaction speed is slower than p90",
@@ -2392,6 +2406,131 @@ int purge_tables(pv_ctx *c, hipStream_t st)
     return 0;
 }
 
+// The DNS transaction stage of a batch (TransactionManager state across batches): a batch with
+// responses or a DNS period shift pairs (sort + resolve) its nev_b events together with the
+// queries carried in; a batch of queries only just appends them to the carried list. Also the
+// heartbeat's DNS shift (nev_b = 0, one shift): the carried queries the shift purges time out
+// in the new live bucket, the rest carry on.
+int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uint64_t n, hipStream_t st)
+{
+    hipError_t e;
+    const bool dns_here = nev_b > 0;
+    bool pair = (dns_here && (nresp > 0 || P.n_dshift > 0)) || (!dns_here && P.n_dshift > 0 && c->n_pend > 0);
+    if (dns_here && !pair && c->n_pend + nev_b > c->pend_cap) pair = true; // compact the carried list
+    if (dns_here && !pair) {
+        hipLaunchKernelGGL(pv_xact_defer, dim3((nev_b + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
+                           c->d_events, nev_b, c->d_pend[c->pend_cur], c->d_pkeys[c->pend_cur], (uint32_t)c->n_pend);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_defer");
+        c->n_pend += nev_b;
+    }
+    if (pair) {
+        const uint32_t np_in = (uint32_t)c->n_pend;
+        if (np_in) {
+            hipLaunchKernelGGL(pv_xact_pend_in, dim3((np_in + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
+                               c->d_pkeys[c->pend_cur], np_in, nev_b);
+            if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_pend_in");
+        }
+        const uint32_t nev = nev_b + np_in;
+        uint32_t threads = 256, blocks = (nev + threads - 1) / threads;
+        size_t tmp = c->sort_tmp_bytes;
+        if (!hip_ok(e = pv_radix_sort_pairs(c->d_sort_tmp, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
+                                             (size_t)nev, st)))
+            return c->hipfail(e, "radix sort");
+        PvXactParams X;
+        memset(&X, 0, sizeof X);
+        X.P = P;
+        X.events = c->d_events;
+        X.skeys = c->d_skeys2;
+        X.svals = c->d_svals2;
+        X.n = nev;
+        X.ttl_s = c->ttl_s;
+        X.ttl_ms = c->ttl_ms;
+        X.quantiles = ((c->dns_groups & PV_DNS_QUANTILES) ? 1u : 0u) | ((c->dns_groups & PV_DNS_HISTOGRAMS) ? 2u : 0u);
+        for (uint32_t k = 0; k <= P.n_dshift; k++) {
+            X.slot_gen[k] = P.dslot_of[k] | (c->gen[P.dslot_of[k]] << 8);
+            X.thr_from[k] = k == 0 ? c->from90 : -1.0f;
+            X.thr_to[k] = k == 0 ? c->to90 : -1.0f;
+            for (uint32_t d = 0; d < 3; d++) X.thr2[k][d] = k == 0 ? c->p90_2[d] : -1.0f;
+        }
+        X.vals = c->d_xvals;
+        X.n_vals = c->d_nvals;
+        X.vals_cap = (uint32_t)(c->max_records * 2);
+        X.valid = c->d_valid;
+        X.n_valid = c->d_nvals + 1;
+        X.pend = c->d_pend[c->pend_cur];
+        X.pend_out = c->d_pend[c->pend_cur ^ 1];
+        X.pkeys_out = c->d_pkeys[c->pend_cur ^ 1];
+        X.n_pend_out = c->d_nvals + 2;
+        X.orph = c->d_orph;
+        X.n_orph = c->d_nvals + 3;
+        X.orph_cap = c->orph_cap;
+        X.trecs = c->d_marena;
+        X.toffs = c->d_moffs;
+        if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
+            !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
+            return c->hipfail(e, "parameter upload");
+        hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
+        hipLaunchKernelGGL(pv_xact_carry, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_carry");
+        if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
+            // on_period_shift: slow thresholds = p90 of the bucket that just closed
+            // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
+            int rc = sync_xvals(c);
+            if (rc) return rc;
+            for (uint32_t k = 1; k <= P.n_dshift; k++) {
+                const uint32_t sg = P.dslot_of[k - 1] | (c->gen[P.dslot_of[k - 1]] << 8);
+                std::vector<uint64_t> fr, to, t2[3];
+                for (auto &v : c->xvals_host) {
+                    if (v.slot != sg) continue;
+                    if (v.kind == XV_FROM_US) fr.push_back(v.bits);
+                    else if (v.kind == XV_TO_US) to.push_back(v.bits);
+                    else if (v.kind >= XV2_TIME && v.kind < XV2_TIME + 3) t2[v.kind - XV2_TIME].push_back(v.bits);
+                }
+                if (!fr.empty()) c->from90 = (float)quantile_at(fr, 0.90);
+                if (!to.empty()) c->to90 = (float)quantile_at(to, 0.90);
+                X.thr_from[k] = c->from90;
+                X.thr_to[k] = c->to90;
+                // DNS v2: per direction (dns/v2/DnsStreamHandler.h:440-453)
+                for (uint32_t d = 0; d < 3; d++) {
+                    if (!t2[d].empty()) c->p90_2[d] = (float)quantile_at(t2[d], 0.90);
+                    X.thr2[k][d] = c->p90_2[d];
+                }
+            }
+            uint32_t nvalid = 0;
+            if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
+            if (nvalid) {
+                if (!hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
+                    return c->hipfail(e, "parameter upload");
+                hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st,
+                                   (const PvXactParams *)c->d_xparams, nvalid);
+                if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_slow");
+            }
+            uint32_t zero = 0;
+            hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st);
+            hipStreamSynchronize(st);
+        }
+        uint32_t nv3[3] = {0, 0, 0};
+        if (!hip_ok(e = hipMemcpyAsync(nv3, c->d_nvals, 12, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "carried queries");
+        const uint32_t npo = nv3[2];
+        if (nv3[0] > c->max_records) {
+            // drain the device value buffer to the host copy: every batch then has the
+            // whole 2 x max_records capacity (at most two values per response)
+            if (int rc = sync_xvals(c)) return rc;
+            c->xvals_synced = 0;
+            if (!hip_ok(e = hipMemsetAsync(c->d_nvals, 0, 4, st))) return c->hipfail(e, "value buffer drain");
+        }
+        if (npo > c->pend_cap) return c->fail(PV_ECAPACITY, "%u open DNS queries exceed the carried-list capacity", npo);
+        c->n_pend = npo;
+        c->pend_cur ^= 1;
+        c->pend_base = (int64_t)(c->records_seen + n) - 1;
+    }
+
+    return 0;
+}
+
 int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint64_t a, uint64_t n, uint64_t rec_bytes,
                  const std::vector<Shift> &nsh, const std::vector<Shift> &dsh, uint32_t first_sec, hipStream_t st)
 {
@@ -2624,122 +2763,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     }
     const uint32_t nev_b = status[ST_NEV];
     const uint32_t nresp = status[ST_NRESP];
-    // TransactionManager state across batches: a batch with responses or a DNS period shift
-    // pairs (sort + resolve) its events together with the queries carried in; a batch of
-    // queries only just appends them to the carried list
-    const bool dns_here = nev_b > 0;
-    bool pair = dns_here && (nresp > 0 || P.n_dshift > 0);
-    if (dns_here && !pair && c->n_pend + nev_b > c->pend_cap) pair = true; // compact the carried list
-    if (dns_here && !pair) {
-        hipLaunchKernelGGL(pv_xact_defer, dim3((nev_b + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
-                           c->d_events, nev_b, c->d_pend[c->pend_cur], c->d_pkeys[c->pend_cur], (uint32_t)c->n_pend);
-        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_defer");
-        c->n_pend += nev_b;
-    }
-    if (pair) {
-        const uint32_t np_in = (uint32_t)c->n_pend;
-        if (np_in) {
-            hipLaunchKernelGGL(pv_xact_pend_in, dim3((np_in + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
-                               c->d_pkeys[c->pend_cur], np_in, nev_b);
-            if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_pend_in");
-        }
-        const uint32_t nev = nev_b + np_in;
-        uint32_t threads = 256, blocks = (nev + threads - 1) / threads;
-        size_t tmp = c->sort_tmp_bytes;
-        if (!hip_ok(e = pv_radix_sort_pairs(c->d_sort_tmp, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
-                                             (size_t)nev, st)))
-            return c->hipfail(e, "radix sort");
-        PvXactParams X;
-        memset(&X, 0, sizeof X);
-        X.P = P;
-        X.events = c->d_events;
-        X.skeys = c->d_skeys2;
-        X.svals = c->d_svals2;
-        X.n = nev;
-        X.ttl_s = c->ttl_s;
-        X.ttl_ms = c->ttl_ms;
-        X.quantiles = ((c->dns_groups & PV_DNS_QUANTILES) ? 1u : 0u) | ((c->dns_groups & PV_DNS_HISTOGRAMS) ? 2u : 0u);
-        for (uint32_t k = 0; k <= P.n_dshift; k++) {
-            X.slot_gen[k] = P.dslot_of[k] | (c->gen[P.dslot_of[k]] << 8);
-            X.thr_from[k] = k == 0 ? c->from90 : -1.0f;
-            X.thr_to[k] = k == 0 ? c->to90 : -1.0f;
-            for (uint32_t d = 0; d < 3; d++) X.thr2[k][d] = k == 0 ? c->p90_2[d] : -1.0f;
-        }
-        X.vals = c->d_xvals;
-        X.n_vals = c->d_nvals;
-        X.vals_cap = (uint32_t)(c->max_records * 2);
-        X.valid = c->d_valid;
-        X.n_valid = c->d_nvals + 1;
-        X.pend = c->d_pend[c->pend_cur];
-        X.pend_out = c->d_pend[c->pend_cur ^ 1];
-        X.pkeys_out = c->d_pkeys[c->pend_cur ^ 1];
-        X.n_pend_out = c->d_nvals + 2;
-        X.orph = c->d_orph;
-        X.n_orph = c->d_nvals + 3;
-        X.orph_cap = c->orph_cap;
-        X.trecs = c->d_marena;
-        X.toffs = c->d_moffs;
-        if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
-            !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
-            return c->hipfail(e, "parameter upload");
-        hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
-        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
-        hipLaunchKernelGGL(pv_xact_carry, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
-        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_carry");
-        if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
-            // on_period_shift: slow thresholds = p90 of the bucket that just closed
-            // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
-            int rc = sync_xvals(c);
-            if (rc) return rc;
-            for (uint32_t k = 1; k <= P.n_dshift; k++) {
-                const uint32_t sg = P.dslot_of[k - 1] | (c->gen[P.dslot_of[k - 1]] << 8);
-                std::vector<uint64_t> fr, to, t2[3];
-                for (auto &v : c->xvals_host) {
-                    if (v.slot != sg) continue;
-                    if (v.kind == XV_FROM_US) fr.push_back(v.bits);
-                    else if (v.kind == XV_TO_US) to.push_back(v.bits);
-                    else if (v.kind >= XV2_TIME && v.kind < XV2_TIME + 3) t2[v.kind - XV2_TIME].push_back(v.bits);
-                }
-                if (!fr.empty()) c->from90 = (float)quantile_at(fr, 0.90);
-                if (!to.empty()) c->to90 = (float)quantile_at(to, 0.90);
-                X.thr_from[k] = c->from90;
-                X.thr_to[k] = c->to90;
-                // DNS v2: per direction (dns/v2/DnsStreamHandler.h:440-453)
-                for (uint32_t d = 0; d < 3; d++) {
-                    if (!t2[d].empty()) c->p90_2[d] = (float)quantile_at(t2[d], 0.90);
-                    X.thr2[k][d] = c->p90_2[d];
-                }
-            }
-            uint32_t nvalid = 0;
-            if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
-            if (nvalid) {
-                if (!hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
-                    return c->hipfail(e, "parameter upload");
-                hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st,
-                                   (const PvXactParams *)c->d_xparams, nvalid);
-                if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_slow");
-            }
-            uint32_t zero = 0;
-            hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st);
-            hipStreamSynchronize(st);
-        }
-        uint32_t nv3[3] = {0, 0, 0};
-        if (!hip_ok(e = hipMemcpyAsync(nv3, c->d_nvals, 12, hipMemcpyDeviceToHost, st)) ||
-            !hip_ok(e = hipStreamSynchronize(st)))
-            return c->hipfail(e, "carried queries");
-        const uint32_t npo = nv3[2];
-        if (nv3[0] > c->max_records) {
-            // drain the device value buffer to the host copy: every batch then has the
-            // whole 2 x max_records capacity (at most two values per response)
-            if (int rc = sync_xvals(c)) return rc;
-            c->xvals_synced = 0;
-            if (!hip_ok(e = hipMemsetAsync(c->d_nvals, 0, 4, st))) return c->hipfail(e, "value buffer drain");
-        }
-        if (npo > c->pend_cap) return c->fail(PV_ECAPACITY, "%u open DNS queries exceed the carried-list capacity", npo);
-        c->n_pend = npo;
-        c->pend_cur ^= 1;
-        c->pend_base = (int64_t)(c->records_seen + n) - 1;
-    }
+    if (int rc = pair_stage(c, P, status[ST_NEV], status[ST_NRESP], n, st)) return rc;
 
     // ---- window bookkeeping (host mirror of each manager's _period_shift)
     for (const Shift &sh : nsh) win_shift(c, c->net, sh.sec);
@@ -3675,6 +3699,79 @@ int pv_set_end_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
     return 0;
 }
 
+// heartbeat_signal -> StreamMetricsHandler::check_period_shift in both handlers
+// (src/AbstractMetricsManager.h:462-470; net/v1/NetStreamHandler.cpp:99-102,
+// dns/v1/DnsStreamHandler.cpp:219-222): each manager shifts its window at `stamp` when
+// num_periods > 1 and stamp.sec has reached its next shift, with no event. The DNS manager's
+// on_period_shift (dns/v1/DnsStreamHandler.h:252-267; v2 .h:440-453) then purges the open
+// transactions the stamp expires (timed out in the new live bucket) and takes the slow
+// thresholds from the bucket just closed.
+int pv_check_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (!c->started || c->cfg.num_periods <= 1) return 0;
+    if (sec >= c->net.next_shift_sec) {
+        clear_part(c, PART_NET, c->net.slot_at(1));
+        c->net.clean[c->net.slot_at(1)] = false;
+        win_shift(c, c->net, sec, nsec);
+    }
+    if (sec < c->dns.next_shift_sec) return 0;
+    hipStream_t st = c->stream;
+    const uint32_t s0 = c->dns.slot_at(0), s1 = c->dns.slot_at(1);
+    clear_part(c, PART_DNS, s1);
+    c->dns.clean[s1] = false;
+    const bool xacts = (c->dns_groups & PV_DNS_TRANSACTIONS) || c->dns2_groups;
+    if (xacts && c->n_pend > 0) {
+        // the carried queries through the pairing stage with one shift at the stamp and no
+        // events: purge_period() times out those with stamp.sec >= ttl_s + start.sec
+        PvParams P;
+        params_common(c, P, nullptr, nullptr, 0);
+        P.n_dshift = 1;
+        P.dthresh[0] = sec;
+        P.dskip_before = 0;
+        P.dslot_of[0] = s0;
+        P.dslot_of[1] = s1;
+        P.slot_of[0] = c->net.slot_at(0);
+        P.sum = c->d_sum;
+        P.cpc = c->d_cpc;
+        P.tkeys = c->d_tkeys;
+        P.tcnt = c->d_tcnt;
+        P.taux = c->d_taux;
+        P.tcap_log2 = c->tcap_log2;
+        P.reg_log2 = c->reg_log2;
+        P.arena = c->d_arena;
+        P.arena_top = c->d_arena_top;
+        P.arena_cap = c->arena_cap;
+        P.events = c->d_events;
+        P.gbase = c->global_base + c->records_seen;
+        P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
+        P.flags = c->d_status + ST_FLAGS;
+        flush_fills(c);
+        if (int rc = pair_stage(c, P, 0, 0, 0, st)) return rc;
+    } else if (xacts && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
+        // nothing open: only the slow thresholds of the closed bucket (kept when it had none)
+        if (int rc = sync_xvals(c)) return rc;
+        const uint32_t sg = s0 | (c->gen[s0] << 8);
+        std::vector<uint64_t> fr, to, t2[3];
+        for (auto &v : c->xvals_host) {
+            if (v.slot != sg) continue;
+            if (v.kind == XV_FROM_US) fr.push_back(v.bits);
+            else if (v.kind == XV_TO_US) to.push_back(v.bits);
+            else if (v.kind >= XV2_TIME && v.kind < XV2_TIME + 3) t2[v.kind - XV2_TIME].push_back(v.bits);
+        }
+        if (!fr.empty()) c->from90 = (float)quantile_at(fr, 0.90);
+        if (!to.empty()) c->to90 = (float)quantile_at(to, 0.90);
+        for (uint32_t d = 0; d < 3; d++)
+            if (!t2[d].empty()) c->p90_2[d] = (float)quantile_at(t2[d], 0.90);
+    }
+    win_shift(c, c->dns, sec, nsec);
+    c->dns_shifts.emplace_back(sec, c->dns.slot_at(0));
+    flush_fills(c);
+    hipError_t e = hipStreamSynchronize(st);
+    return hip_ok(e) ? 0 : c->hipfail(e, "heartbeat period shift");
+}
+
 int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
 {
     *out = nullptr;
@@ -3713,6 +3810,171 @@ int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
     return 0;
 }
 
+// ---- external buckets: the bucket half of the handler object (StreamHandler::merge and the
+// window_*(..., AbstractMetricsBucket *) overloads, src/StreamHandler.h:72-77,221-269), which
+// a policy uses to fold like handlers across taps (Policy::_get_merged_buckets,
+// src/Policies.cpp:420-446)
+} // extern "C"
+struct pv_bucket {
+    int part;            // PART_NET / PART_DNS
+    uint32_t handler;    // PV_HANDLER_NET / PV_HANDLER_DNS
+    HostBucket b;
+};
+namespace {
+// Quantile::merge(other, Aggregate::SUM) (src/Metrics.h:356-372) on exact values: the sketch of
+// a non-empty bucket stays, the p-wise sum of the quantiles grows; an empty one merges
+template <typename T>
+void qsum_fold(std::vector<T> &dv, std::vector<T> &qs, const std::vector<T> &ov, const std::vector<T> &oqs)
+{
+    if (dv.empty()) { dv.insert(dv.end(), ov.begin(), ov.end()); return; }
+    if (ov.empty()) return;
+    const std::vector<T> oq = quantiles(ov);
+    (void)oqs; // the other sketch's own quantiles (get_quantiles(other._quantile)), not its sums
+    if (qs.empty()) qs = quantiles(dv);
+    for (int i = 0; i < 4; i++) qs[i] += oq[i];
+}
+// AbstractMetricsBucket::merge(other, Aggregate::SUM) (src/AbstractMetricsManager.h:177-195) and
+// the handlers' specialized_merge (net/v1/NetStreamHandler.cpp:285-330,
+// dns/v1/DnsStreamHandler.cpp:658-733)
+void bucket_fold_sum(HostBucket &d, const HostBucket &o, int part)
+{
+    d.period_length += o.period_length;
+    if (o.start_sec < d.start_sec) { d.start_sec = o.start_sec; d.start_nsec = o.start_nsec; }
+    if (o.end_sec > d.end_sec) { d.end_sec = o.end_sec; d.end_nsec = o.end_nsec; }
+    if (part == PART_NET) {
+        for (size_t i = 0; i < PV_SUM_NET_WORDS; i++)
+            if (i < PV_OFF_PAYLOAD || i >= PV_OFF_PAYLOAD + PV_PAYLOAD_BINS) d.sum[i] += o.sum[i];
+        // payload_size, a Quantile over the dense histogram
+        uint64_t dn = 0, on = 0;
+        const auto dq = hist_quantiles(&d.sum[PV_OFF_PAYLOAD], PV_PAYLOAD_BINS, dn);
+        const auto oq = hist_quantiles(&o.sum[PV_OFF_PAYLOAD], PV_PAYLOAD_BINS, on);
+        if (!dn) {
+            for (size_t i = 0; i < PV_PAYLOAD_BINS; i++) d.sum[PV_OFF_PAYLOAD + i] += o.sum[PV_OFF_PAYLOAD + i];
+        } else if (on) {
+            if (d.qs_payload.empty()) d.qs_payload = dq;
+            for (int i = 0; i < 4; i++) d.qs_payload[i] += oq[i];
+        }
+    } else {
+        for (size_t i = PV_OFF_DNS; i < PV_SUM_WORDS; i++) d.sum[i] += o.sum[i];
+        // histograms merge their sketches; the quantiles follow the SUM rule
+        if (!d.hist_sep) { d.hfrom_us = d.from_us; d.hto_us = d.to_us; d.hist_sep = true; }
+        const auto &ohf = o.hist_from(), &oht = o.hist_to();
+        d.hfrom_us.insert(d.hfrom_us.end(), ohf.begin(), ohf.end());
+        d.hto_us.insert(d.hto_us.end(), oht.begin(), oht.end());
+        qsum_fold(d.from_us, d.qs_from, o.from_us, o.qs_from);
+        qsum_fold(d.to_us, d.qs_to, o.to_us, o.qs_to);
+        qsum_fold(d.ratio, d.qs_ratio, o.ratio, o.qs_ratio);
+    }
+    for (size_t i = 0; i < PV_MIN_WORDS; i++) d.cpc[i] = std::min(d.cpc[i], o.cpc[i]); // CPC union (ICON)
+    for (auto &m : o.tops)
+        for (auto &kv : m.second) d.tops[m.first][kv.first] += kv.second;
+}
+} // namespace
+extern "C" {
+
+int pv_bucket_merge(pv_ctx *c, uint32_t handler, pv_bucket **bucket, uint32_t period, int prometheus, int merged)
+{
+    if (!bucket || (handler != PV_HANDLER_NET && handler != PV_HANDLER_DNS)) return c->fail(PV_EINVAL, "bucket merge: one handler");
+    int rc = sync_xvals(c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    flush_fills(c);
+    if (!c->started) return c->fail(PV_EINVAL, "no data");
+    if (c->net2_groups || c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "bucket merge: the v2 handlers' buckets are not built");
+    const int part = handler == PV_HANDLER_NET ? PART_NET : PART_DNS;
+    const Window &w = part == PART_NET ? c->net : c->dns;
+    if (*bucket && (*bucket)->part != part) return c->fail(PV_EINVAL, "bucket merge: a bucket of another handler");
+    // StreamMetricsHandler::merge: Prometheus output reads period 1 once the manager holds more
+    // than one, never merged
+    if (prometheus) { period = w.slots.size() > 1 ? 1 : 0; merged = 0; }
+    std::vector<uint32_t> slots;
+    if ((rc = window_slots(c, w, period, merged != 0, slots))) return rc;
+    HostBucket b;
+    // a fresh bucket merged from this handler's bucket(s): CPC through a union (ICON)
+    if ((rc = load_bucket(c, slots, true, part, b))) return rc;
+    if (!*bucket) {
+        pv_bucket *nb = new (std::nothrow) pv_bucket;
+        if (!nb) return c->fail(PV_ECAPACITY, "bucket merge: out of host memory");
+        nb->part = part;
+        nb->handler = handler;
+        nb->b = std::move(b);
+        *bucket = nb;
+        return 0;
+    }
+    bucket_fold_sum((*bucket)->b, b, part);
+    return 0;
+}
+
+void pv_bucket_free(pv_bucket *b) { delete b; }
+
+int pv_bucket_json(pv_ctx *c, const pv_bucket *bk, char **out)
+{
+    *out = nullptr;
+    if (!bk) return c->fail(PV_EINVAL, "bucket json: no bucket");
+    std::lock_guard<std::mutex> g(c->mu);
+    Json j;
+    j.obj();
+    // window_external_json: {"<schema key>": {period, metrics}} (AbstractMetricsManager.h:589-599)
+    if (bk->part == PART_NET) {
+        if (c->net_groups) { j.key("packets").obj(); net_json(c, j, bk->b); j.end_obj(); }
+    } else if (c->dns_groups) {
+        j.key("dns").obj();
+        dns_json(c, j, bk->b);
+        j.end_obj();
+    }
+    j.end_obj();
+    *out = strdup(j.s.c_str());
+    return 0;
+}
+
+int pv_bucket_prometheus(pv_ctx *c, const pv_bucket *bk, const char *const *label_keys, const char *const *label_values,
+                         uint32_t n_labels, char **out)
+{
+    *out = nullptr;
+    if (!bk) return c->fail(PV_EINVAL, "bucket prometheus: no bucket");
+    std::lock_guard<std::mutex> g(c->mu);
+    Prom p;
+    for (uint32_t i = 0; i < n_labels; i++) {
+        if (!label_keys || !label_values || !label_keys[i] || !label_values[i]) return c->fail(PV_EINVAL, "label %u missing", i);
+        p.add[label_keys[i]] = label_values[i];
+    }
+    // window_external_prometheus (AbstractMetricsManager.h:580-587)
+    if (bk->part == PART_NET && c->net_groups) net_metrics(c, p, bk->b);
+    if (bk->part == PART_DNS && c->dns_groups) dns_metrics(c, p, bk->b);
+    *out = strdup(p.o.str().c_str());
+    return 0;
+}
+
+int pv_bucket_opentelemetry(pv_ctx *c, const pv_bucket *bk, const char *const *label_keys, const char *const *label_values,
+                            uint32_t n_labels, uint8_t **out, size_t *bytes)
+{
+    *out = nullptr;
+    *bytes = 0;
+    if (!bk) return c->fail(PV_EINVAL, "bucket opentelemetry: no bucket");
+    std::lock_guard<std::mutex> g(c->mu);
+    Otlp p;
+    for (uint32_t i = 0; i < n_labels; i++) {
+        if (!label_keys || !label_values || !label_keys[i] || !label_values[i]) return c->fail(PV_EINVAL, "label %u missing", i);
+        p.add[label_keys[i]] = label_values[i];
+    }
+    // window_external_opentelemetry (AbstractMetricsManager.h:565-578): the bucket's stamps,
+    // now for an end it does not have
+    p.t0 = (uint64_t)bk->b.start_sec * 1000000000ull + (uint64_t)bk->b.start_nsec;
+    if (bk->b.end_sec) p.t1 = (uint64_t)bk->b.end_sec * 1000000000ull + (uint64_t)bk->b.end_nsec;
+    else {
+        timespec now;
+        timespec_get(&now, TIME_UTC);
+        p.t1 = (uint64_t)now.tv_sec * 1000000000ull + (uint64_t)now.tv_nsec;
+    }
+    if (bk->part == PART_NET && c->net_groups) net_metrics(c, p, bk->b);
+    if (bk->part == PART_DNS && c->dns_groups) dns_metrics(c, p, bk->b);
+    *out = (uint8_t *)malloc(p.out.s.size() ? p.out.s.size() : 1);
+    if (!*out) return c->fail(PV_ECAPACITY, "bucket opentelemetry: out of host memory");
+    memcpy(*out, p.out.s.data(), p.out.s.size());
+    *bytes = p.out.s.size();
+    return 0;
+}
+
 int pv_add_static_label(const char *key, const char *value)
 {
     if (!key || !value || !*key) return PV_EINVAL;
@@ -3732,8 +3994,11 @@ int pv_window_prometheus(pv_ctx *c, uint32_t period, uint32_t handlers, const ch
     if (!c->started) return c->fail(PV_EINVAL, "no data");
     if (c->net2_groups || c->dns2_groups)
         return c->fail(PV_EUNSUPPORTED, "window_prometheus: the v2 handlers' Prometheus output is not built");
-    if (period >= c->cfg.num_periods)
+    if (period >= c->cfg.num_periods && period != PV_PERIOD_AUTO)
         return c->fail(PV_EINVAL, "invalid metrics period, specify [0, %u]", c->cfg.num_periods - 1);
+    // StreamMetricsHandler::window_prometheus (src/StreamHandler.h:226-233): period 1 of a
+    // manager holding more than one bucket, else 0 (each handler's own manager)
+    auto per = [&](const Window &w) -> uint32_t { return period != PV_PERIOD_AUTO ? period : (w.slots.size() > 1 ? 1u : 0u); };
     Prom p;
     for (uint32_t i = 0; i < n_labels; i++) {
         if (!label_keys || !label_values || !label_keys[i] || !label_values[i]) return c->fail(PV_EINVAL, "label %u missing", i);
@@ -3743,13 +4008,13 @@ int pv_window_prometheus(pv_ctx *c, uint32_t period, uint32_t handlers, const ch
     // each handler's own window (its manager's window_single_prometheus); a handler with
     // every group disabled writes nothing (AbstractMetricsManager.h:522-524)
     if ((handlers & PV_HANDLER_NET) && c->net_groups) {
-        if ((rc = window_slots(c, c->net, period, false, slots))) return rc;
+        if ((rc = window_slots(c, c->net, per(c->net), false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
         net_metrics(c, p, b);
     }
     if ((handlers & PV_HANDLER_DNS) && c->dns_groups) {
-        if ((rc = window_slots(c, c->dns, period, false, slots))) return rc;
+        if ((rc = window_slots(c, c->dns, per(c->dns), false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;
         dns_metrics(c, p, b);
@@ -3770,8 +4035,10 @@ int pv_window_opentelemetry(pv_ctx *c, uint32_t period, uint32_t handlers, const
     if (!c->started) return c->fail(PV_EINVAL, "no data");
     if (c->net2_groups || c->dns2_groups)
         return c->fail(PV_EUNSUPPORTED, "window_opentelemetry: the v2 handlers' OpenTelemetry output is not built");
-    if (period >= c->cfg.num_periods)
+    if (period >= c->cfg.num_periods && period != PV_PERIOD_AUTO)
         return c->fail(PV_EINVAL, "invalid metrics period, specify [0, %u]", c->cfg.num_periods - 1);
+    // StreamMetricsHandler::window_opentelemetry (src/StreamHandler.h:240-247)
+    auto per = [&](const Window &w) -> uint32_t { return period != PV_PERIOD_AUTO ? period : (w.slots.size() > 1 ? 1u : 0u); };
     Otlp p;
     for (uint32_t i = 0; i < n_labels; i++) {
         if (!label_keys || !label_values || !label_keys[i] || !label_values[i]) return c->fail(PV_EINVAL, "label %u missing", i);
@@ -3790,14 +4057,14 @@ int pv_window_opentelemetry(pv_ctx *c, uint32_t period, uint32_t handlers, const
         }
     };
     if ((handlers & PV_HANDLER_NET) && c->net_groups) {
-        if ((rc = window_slots(c, c->net, period, false, slots))) return rc;
+        if ((rc = window_slots(c, c->net, per(c->net), false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
         stamps(c->net, slots[0]);
         net_metrics(c, p, b);
     }
     if ((handlers & PV_HANDLER_DNS) && c->dns_groups) {
-        if ((rc = window_slots(c, c->dns, period, false, slots))) return rc;
+        if ((rc = window_slots(c, c->dns, per(c->dns), false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;
         stamps(c->dns, slots[0]);

@@ -29,6 +29,23 @@ class Oracle:
             raise RuntimeError(f"oracle failed ({rc}): {txt}")
         return json.loads(txt)
 
+    def run_policy(self, files, period: int = 0, merged: bool = False, prometheus: bool = False, **cfg) -> dict:
+        """Policy::_get_merged_buckets over like handlers, one per capture (pvo_run_policy)."""
+        s = ";".join(f"{k}={v}" for k, v in cfg.items() if v is not None and v != "")
+        bufs = [ctypes.create_string_buffer(f, len(f)) for f in files]
+        arr = (ctypes.c_void_p * len(files))(*[ctypes.cast(b, ctypes.c_void_p) for b in bufs])
+        lens = (ctypes.c_size_t * len(files))(*[len(f) for f in files])
+        out = ctypes.c_void_p()
+        self.lib.pvo_run_policy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p,
+                                            ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        rc = self.lib.pvo_run_policy(arr, lens, len(files), s.encode(), period, int(merged), int(prometheus),
+                                     ctypes.byref(out))
+        txt = ctypes.string_at(out.value).decode() if out.value else ""
+        self.lib.pvo_free(out)
+        if rc != 0:
+            raise RuntimeError(f"oracle failed ({rc}): {txt}")
+        return json.loads(txt)
+
     def run_file(self, path, **cfg) -> dict:
         with open(path, "rb") as f:
             return self.run_bytes(f.read(), **cfg)
