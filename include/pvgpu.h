@@ -265,6 +265,27 @@ int pv_ingest_timing(pv_ctx *ctx, double *ms4, int reset);
  * (libs/visor_transaction/TransactionManager.h:51-106) across shard boundaries. */
 int pv_edge_export(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
 int pv_edge_merge(pv_ctx *ctx, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks, uint32_t my_rank);
+/* Sharded top_slow. A slow transaction is counted against the p90 of the bucket that closed
+ * at the last DNS shift (DnsMetricsManager::on_period_shift, dns/v1/DnsStreamHandler.h:252-267),
+ * a bucket that spans several shards. With pv_set_slow_defer(ctx, 1) (before the first batch;
+ * DNS v1) a rank keeps every slow candidate (valid, deep transaction of known direction,
+ * edge pairs included) with its response record instead of checking it against its own
+ * shard's p90. At the merge, after pv_edge_merge and before pv_values_merge / the top-N
+ * exchange: pv_slow_values_export (this rank's transaction times per DNS period ordinal),
+ * all-gather, pv_slow_finish (each live-window period's thresholds from every rank's values,
+ * then this rank's candidates of those periods into their top_slow tables). */
+int pv_set_slow_defer(pv_ctx *ctx, int defer);
+/* Shard-edge transactions of such a run, carried in rank order (replaces pv_edge_export /
+ * pv_edge_merge there): `in` = the DNS queries the earlier shards leave open (the previous
+ * rank's *out; empty for rank 0). Each meets the first event of its (flow, txid) in this shard
+ * as the TransactionManager would (libs/visor_transaction/TransactionManager.h:51-106): a
+ * response pairs with it (counted, its times and top_slow candidate kept), a query overwrites
+ * it, a DNS shift of this shard at or after ttl + its start purges it first (a time-out there,
+ * dns/v1/DnsStreamHandler.h:252-267). *out: the queries still open at this shard's end, the
+ * earlier shards' survivors and this shard's own (pv_free). */
+int pv_edge_carry(pv_ctx *ctx, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes);
+int pv_slow_values_export(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
+int pv_slow_finish(pv_ctx *ctx, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks);
 /* Quantile inputs of the live window, (slot, kind, value) records, for the merge of the
  * dns_xact_* quantiles across ranks (DnsMetricsBucket::specialized_merge of the KLL
  * sketches, src/handlers/dns/v1/DnsStreamHandler.cpp:692). */
@@ -286,6 +307,13 @@ int pv_dns_event_seconds(pv_ctx *ctx, const uint8_t *d_recs, const uint32_t *d_o
                          const uint32_t *sc_idx, const uint32_t *sc_sec, int64_t *secs, uint32_t max, uint32_t *n);
 /* The same over records in host memory (staged through the ingest chunks). */
 int pv_dns_event_seconds_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes, int64_t *secs, uint32_t max, uint32_t *n);
+/* Record cuts of a capture into `world` contiguous shards (cuts[0..world], cuts[world] = n):
+ * about equal sizes, each cut at a record boundary that no DNS-over-TCP flow (a TCP packet with
+ * a DNS port, keyed as the TCP stage keys it) spans, so DNS over TCP across shard edges matches a
+ * single pass (PcapInputStream.cpp:254-283, 429-465 reassemble per connection in capture order).
+ * offs: the records' byte offsets in recs (pv_index_records). */
+int pv_shard_cuts(const uint8_t *recs, size_t bytes, const uint32_t *offs, uint64_t n, uint32_t linktype, uint32_t ts_nano,
+                  uint32_t world, uint64_t *cuts);
 
 
 int pv_set_start_tstamp(pv_ctx *ctx, int64_t sec, int64_t nsec);

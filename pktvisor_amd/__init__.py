@@ -167,7 +167,8 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_comm_allreduce_window", "pv_comm_allgather", "pv_comm_destroy", "pv_process_dnstap", "pv_dnstap_count",
            "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label",
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
-           "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free"]
+           "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
+           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts"]
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
@@ -240,6 +241,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_kernel_timing.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.c_int]
     lib.pv_edge_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_edge_merge.argtypes = [P, P, P, U32, U32]
+    lib.pv_set_slow_defer.argtypes = [P, ctypes.c_int]
+    lib.pv_shard_cuts.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, U32, U32, U32, P]
+    lib.pv_edge_carry.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_slow_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_slow_finish.argtypes = [P, P, P, U32]
     lib.pv_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_values_merge.argtypes = [P, P, ctypes.c_size_t]
     lib.pv_window_periods.argtypes = [P, ctypes.c_int, P, P, U32, ctypes.POINTER(U32)]
@@ -388,6 +394,19 @@ class RecordIndex:
             raise PvError(f"pv_index_records failed ({rc})")
         self.offsets = self.offsets[: self.info.n_records]
         self.n = int(self.info.n_records)
+
+
+def shard_cuts(recs, index: RecordIndex, linktype: int, ts_nano: int, world: int):
+    """world + 1 record cuts of a capture for a sharded run (pv_shard_cuts): about equal shards,
+    no DNS-over-TCP flow across a cut"""
+    buf = np.frombuffer(recs, dtype=np.uint8) if not isinstance(recs, np.ndarray) else recs
+    offs = np.ascontiguousarray(index.offsets, dtype=np.uint32)
+    cuts = np.zeros(world + 1, dtype=np.uint64)
+    rc = load_library().pv_shard_cuts(buf.ctypes.data, len(buf), offs.ctypes.data, index.n, linktype, ts_nano, world,
+                                      cuts.ctypes.data)
+    if rc:
+        raise PvError(f"pv_shard_cuts failed ({rc})")
+    return [int(x) for x in cuts]
 
 
 def add_static_label(key: str, value: str) -> None:
@@ -726,8 +745,35 @@ class PvHandlers:
         sizes = (ctypes.c_size_t * len(bufs))(*[len(b) for b in exports])
         self._check(self.lib.pv_edge_merge(self.ctx, ptrs, sizes, len(bufs), rank), "pv_edge_merge")
 
+    def edge_carry(self, open_in: bytes) -> bytes:
+        """sharded runs in rank order (pv_edge_carry): account the queries the earlier shards leave
+        open against this shard's events; returns the queries still open at this shard's end"""
+        buf = np.frombuffer(open_in, dtype=np.uint8) if open_in else np.zeros(1, dtype=np.uint8)
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self.lib.pv_edge_carry(self.ctx, buf.ctypes.data, len(open_in), ctypes.byref(p), ctypes.byref(n)),
+                    "pv_edge_carry")
+        data = ctypes.string_at(p.value, n.value) if n.value else b""
+        self.lib.pv_free(p)
+        return data
+
     def values_export(self) -> bytes:
         return self._export(self.lib.pv_values_export, "pv_values_export")
+
+    def set_slow_defer(self, on: bool = True):
+        """sharded top_slow: keep the slow candidates for pv_slow_finish (before the first batch)"""
+        self._check(self.lib.pv_set_slow_defer(self.ctx, int(on)), "pv_set_slow_defer")
+        self.slow_defer = on
+
+    def slow_values_export(self) -> bytes:
+        return self._export(self.lib.pv_slow_values_export, "pv_slow_values_export")
+
+    def slow_finish(self, exports):
+        """every rank's slow_values_export (rank order): the window's slow thresholds over the
+        whole stream, then this rank's deferred candidates into the top_slow tables"""
+        bufs = [np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, dtype=np.uint8) for b in exports]
+        ptrs = (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+        sizes = (ctypes.c_size_t * len(bufs))(*[len(b) for b in exports])
+        self._check(self.lib.pv_slow_finish(self.ctx, ptrs, sizes, len(bufs)), "pv_slow_finish")
 
     def values_merge(self, data: bytes):
         buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)

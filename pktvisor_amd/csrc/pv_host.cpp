@@ -90,13 +90,38 @@ static std::vector<uint32_t> psl_blob()
     memcpy(w.data() + n0, str.data(), str.size());
     return w;
 }
-#undef PV_FN
-#undef PV_CREF
 inline uint64_t name_ph(const char *s, size_t n) // polynomial hash of the lower-case string
 {
     uint64_t ph = 0;
     for (size_t k = 0; k < n; k++) ph = ph_step(ph, lower((uint8_t)s[k]));
     return ph;
+}
+// bounds-checked byte access to records in host memory (pv_shard_cuts)
+struct HostRecs {
+    const uint8_t *p;
+    size_t n;
+    uint32_t u8(uint64_t o) const { return o < n ? p[o] : 0u; }
+    uint32_t u32(uint64_t o) const
+    {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; k++) v |= u8(o + k) << (8 * k);
+        return v;
+    }
+};
+// the TCP stage's flow key of a record that may carry a DNS-over-TCP segment (tcp_seg_of,
+// pv_kernels.hip: TCP with a DNS port on either side); false for any other record
+inline bool tcp_dns_flow(const HostRecs &R, const PvParams &P, uint64_t rec, uint32_t *key)
+{
+    Parsed o;
+    parse_record(R, parse_cfg(P), P, rec, o);
+    if (o.l4 != 6) return false;
+    const uint32_t pw = R.u32(o.l4off);
+    auto bs = [](uint32_t x) { return ((x & 0xff) << 8) | ((x >> 8) & 0xff); };
+    const uint32_t sp = bs(pw & 0xffff), dp = bs(pw >> 16);
+    auto dns = [](uint32_t x) { return x == 53 || x == 5353 || x == 5355 || x == 53000; };
+    if (!dns(sp) && !dns(dp)) return false;
+    *key = flowkey(R, o);
+    return true;
 }
 inline uint64_t name_fp(const char *s, size_t n)
 {
@@ -105,11 +130,18 @@ inline uint64_t name_fp(const char *s, size_t n)
     for (size_t k = 0; k < n; k++) st.put((uint8_t)s[k]);
     return fp56(st.ph, st.n, 0);
 }
+#undef PV_FN
+#undef PV_CREF
 } // namespace pvname
 
 extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ns(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_fast(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
+extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
+                                        const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
+extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
+                                         const uint32_t *idx, uint32_t stride, uint32_t n, const uint32_t *dst_off, uint8_t *out);
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel_sfx(const PvParams *P);
 extern "C" __global__ void pv_dns_suffix(const PvParams *P);
@@ -523,6 +555,32 @@ struct pv_ctx {
     uint32_t *h_ndeep = nullptr, *d_ndeep = nullptr;
     uint64_t ndeep_words = 0;
     std::vector<std::pair<uint64_t, int64_t>> tcp_ords; // (ord, second) of the batch's messages, by ord
+    // sharded top_slow (pv_set_slow_defer): the DNS period ordinal of each slot | generation,
+    // the deferred slow-transaction candidates with their response records, and the records of
+    // the orphan stubs (in d_orph order), which may become edge pairs
+    bool slow_defer = false;
+    std::unordered_map<uint32_t, uint64_t> sg_ord;
+    struct SlowCand {
+        uint64_t ord, us;
+        uint32_t off;      // record in sstore
+        uint8_t dir, tcp;
+    };
+    std::vector<uint8_t> sstore;
+    std::vector<SlowCand> scands, sorph;
+    uint32_t orph_done = 0;
+    size_t xv_local_end = SIZE_MAX;     // xvals_host entries of this rank's own batches
+    std::vector<std::pair<uint64_t, PvXValue>> slow_xv; // edge-pair times by period ordinal
+    // shard-edge stubs kept on the host (sharded runs): the first event of a key in this shard
+    // that may meet a query an earlier shard leaves open (orphan responses, first queries below
+    // the edge horizon), in stream order, with the record of a response (for top_slow)
+    struct EdgeStub {
+        PvXEvent e;
+        uint64_t ord;
+        int64_t cand; // SlowCand template in sorph (responses), -1 for queries
+    };
+    std::vector<EdgeStub> stubs;
+    int64_t edge_h = 0;                                        // first record second + ttl + 61
+    std::vector<std::pair<int64_t, uint64_t>> dns_shift_ord;   // (threshold second, ordinal) of local DNS shifts
 
     int fail(int code, const char *fmt, ...)
     {
@@ -616,9 +674,11 @@ void clear_part(pv_ctx *c, int part, uint32_t s)
     if (part == PART_DNS) {
         // quantile inputs of the slot's previous bucket no longer match (bounded host memory)
         c->gen[s] = (c->gen[s] + 1) & 0xffffff;
-        c->xvals_host.erase(std::remove_if(c->xvals_host.begin(), c->xvals_host.end(),
-                                           [s](const PvXValue &v) { return (v.slot & 0xff) == s; }),
-                            c->xvals_host.end());
+        // (a sharded run keeps them: the merge computes every period's slow thresholds)
+        if (!c->slow_defer)
+            c->xvals_host.erase(std::remove_if(c->xvals_host.begin(), c->xvals_host.end(),
+                                               [s](const PvXValue &v) { return (v.slot & 0xff) == s; }),
+                                c->xvals_host.end());
     }
     const uint32_t t = s + (part == PART_DNS ? PV_SLOTS : 0);
     c->remote_topn.erase(t);
@@ -658,6 +718,7 @@ void win_shift(pv_ctx *c, Window &w, int64_t T, int64_t Tns = 0)
     w.slots.push_front(s);
     if (w.slots.size() > c->cfg.num_periods) w.slots.pop_back();
     w.next_shift_sec = T + 60;
+    if (&w == &c->dns) c->sg_ord[s | (c->gen[s] << 8)] = w.ordinal;
 }
 
 int ensure_started(pv_ctx *c, int64_t sec, int64_t nsec)
@@ -673,6 +734,7 @@ int ensure_started(pv_ctx *c, int64_t sec, int64_t nsec)
         w.slots.assign(1, 0);
         w.next_shift_sec = sec + 60;
     }
+    c->sg_ord[0 | (c->gen[0] << 8)] = 0;
     c->started = true;
     return 0;
 }
@@ -1835,9 +1897,12 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
     {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_net_kernel), PV_NET_THREADS, 0) ==
+        // the persistent grid is sized for the lean register-window pass (the common batch);
+        // PV_NET_WGCU overrides it for A/B runs
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_net_kernel_reg), PV_NET_THREADS, 0) ==
                 hipSuccess && nb > 0)
             c->wg_per_cu = nb;
+        if (const char *w = getenv("PV_NET_WGCU")) c->wg_per_cu = std::max(1, atoi(w));
     }
     // event / DNS work-list regions: main workgroups own wt_per_block * 64 slots each (the
     // last may overhang the batch by < wt_per_block tiles), boundary workgroups 64 each
@@ -1956,6 +2021,16 @@ void pv_destroy(pv_ctx *c)
     delete c;
 }
 
+// TCP: no connection, no carried bytes, no TCP record seen
+static void tcp_reset(pv_ctx *c)
+{
+    launch_fill32(c, c->d_tcpcnt + PVT_WORDS, 1, 0);
+    if (c->d_flows) launch_fill32(c, (uint32_t *)c->d_flows, ((uint64_t)sizeof(PvTcpFlow) / 4) << c->flow_cap_log2, 0);
+    c->n_clist = 0;
+    c->carry_used = 0;
+    c->tcp_active = false;
+}
+
 int pv_reset(pv_ctx *c)
 {
     std::lock_guard<std::mutex> g(c->mu);
@@ -1979,13 +2054,18 @@ int pv_reset(pv_ctx *c)
     c->n_pend = 0;
     c->pend_base = -1;
     c->dns_shifts.clear();
+    c->sg_ord.clear();
+    c->sstore.clear();
+    c->scands.clear();
+    c->sorph.clear();
+    c->orph_done = 0;
+    c->xv_local_end = SIZE_MAX;
+    c->slow_xv.clear();
+    c->stubs.clear();
+    c->edge_h = 0;
+    c->dns_shift_ord.clear();
     launch_fill32(c, c->d_nvals, 4, 0); // with the next batch's slot clears
-    // TCP: no connection, no carried bytes, no TCP record seen
-    launch_fill32(c, c->d_tcpcnt + PVT_WORDS, 1, 0);
-    if (c->d_flows) launch_fill32(c, (uint32_t *)c->d_flows, ((uint64_t)sizeof(PvTcpFlow) / 4) << c->flow_cap_log2, 0);
-    c->n_clist = 0;
-    c->carry_used = 0;
-    c->tcp_active = false;
+    tcp_reset(c);
     return 0;
 }
 
@@ -2406,6 +2486,109 @@ int purge_tables(pv_ctx *c, hipStream_t st)
     return 0;
 }
 
+// Records of `n` batch indices (d_idx[i * stride], PV_TCP_IDX: the TCP message arena) appended
+// to the context's slow store; offs_out[i] = each record's offset there
+int gather_records(pv_ctx *c, const PvParams &P, const uint32_t *d_idx, uint32_t stride, uint32_t n,
+                   std::vector<uint32_t> &offs_out, hipStream_t st)
+{
+    offs_out.assign(n, 0);
+    if (!n) return 0;
+    hipError_t e;
+    uint32_t *d_sz = nullptr, *d_off = nullptr;
+    uint8_t *d_out = nullptr;
+    struct Free { void *p[3]; ~Free() { for (void *q : p) if (q) hipFree(q); } } fr{{nullptr, nullptr, nullptr}};
+    if (!hip_ok(e = hipMalloc(&d_sz, (size_t)n * 4)) || !hip_ok(e = hipMalloc(&d_off, (size_t)n * 4)))
+        return c->hipfail(e, "slow store scratch");
+    fr.p[0] = d_sz; fr.p[1] = d_off;
+    hipLaunchKernelGGL(pv_rec_sizes, dim3((n + 255) / 256), dim3(256), 0, st, P.recs, P.offs, c->d_marena, c->d_moffs, d_idx, stride,
+                       n, d_sz);
+    std::vector<uint32_t> sz(n);
+    if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipMemcpyAsync(sz.data(), d_sz, (size_t)n * 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "slow store sizes");
+    uint64_t tot = 0;
+    std::vector<uint32_t> rel(n);
+    for (uint32_t i = 0; i < n; i++) { rel[i] = (uint32_t)tot; tot += sz[i]; }
+    if (c->sstore.size() + tot > 0xfffffff0ull) return c->fail(PV_ECAPACITY, "deferred slow-transaction records exceed 4 GiB");
+    if (!hip_ok(e = hipMalloc(&d_out, tot ? tot : 4))) return c->hipfail(e, "slow store scratch");
+    fr.p[2] = d_out;
+    if (!hip_ok(e = hipMemcpyAsync(d_off, rel.data(), (size_t)n * 4, hipMemcpyHostToDevice, st))) return c->hipfail(e, "slow store");
+    hipLaunchKernelGGL(pv_rec_gather, dim3((n + 3) / 4), dim3(256), 0, st, P.recs, P.offs, c->d_marena, c->d_moffs, d_idx, stride, n,
+                       d_off, d_out);
+    const size_t base = c->sstore.size();
+    c->sstore.resize(base + tot);
+    if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipMemcpyAsync(c->sstore.data() + base, d_out, tot, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "slow store");
+    for (uint32_t i = 0; i < n; i++) offs_out[i] = (uint32_t)(base + rel[i]);
+    return 0;
+}
+
+// Sharded top_slow (pv_set_slow_defer): the batch's slow-transaction candidates (every valid,
+// deep transaction of known direction: the resolve was given no threshold) and its new orphan
+// stubs are kept with their response records; pv_slow_finish checks them against the
+// thresholds of the whole stream (DnsMetricsManager::on_period_shift, dns/v1/DnsStreamHandler.h:
+// 252-267) once the ranks' values are merged.
+int defer_slow(pv_ctx *c, const PvParams &P, hipStream_t st)
+{
+    hipError_t e;
+    uint32_t nv[4];
+    if (!hip_ok(e = hipMemcpyAsync(nv, c->d_nvals, 16, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "deferred candidates");
+    auto ord_of = [&](uint32_t period) -> uint64_t {
+        const uint32_t s = P.dslot_of[period];
+        auto it = c->sg_ord.find(s | (c->gen[s] << 8));
+        return it == c->sg_ord.end() ? ~0ull : it->second;
+    };
+    if (nv[1]) {
+        std::vector<PvXValid> v(nv[1]);
+        std::vector<uint32_t> offs;
+        if (!hip_ok(e = hipMemcpy(v.data(), c->d_valid, v.size() * sizeof(PvXValid), hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "deferred candidates");
+        if (int rc = gather_records(c, P, reinterpret_cast<const uint32_t *>(c->d_valid), sizeof(PvXValid) / 4, nv[1], offs, st))
+            return rc;
+        for (uint32_t i = 0; i < nv[1]; i++)
+            if (v[i].dir < 2)
+                c->scands.push_back(pv_ctx::SlowCand{ord_of(v[i].period), v[i].us, offs[i], v[i].dir, (uint8_t)((v[i].idx & PV_TCP_IDX) != 0)});
+        const uint32_t zero = 0;
+        if (!hip_ok(e = hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st))) return c->hipfail(e, "deferred candidates");
+    }
+    const uint32_t no = std::min(nv[3], c->orph_cap);
+    if (nv[3] > c->orph_cap) return c->fail(PV_ECAPACITY, "%u shard-edge stubs exceed the stub capacity", nv[3]);
+    if (no > c->orph_done) {
+        const uint32_t k = no - c->orph_done;
+        std::vector<PvXEvent> o(k);
+        if (!hip_ok(e = hipMemcpy(o.data(), c->d_orph + c->orph_done, (size_t)k * sizeof(PvXEvent), hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "orphan stubs");
+        // the records of the responses (an edge pair's top_slow candidate needs its name)
+        std::vector<uint32_t> ridx;
+        for (auto &x : o)
+            if (x.qr) ridx.push_back(x.idx);
+        std::vector<uint32_t> offs;
+        if (!ridx.empty()) {
+            uint32_t *d_idx = nullptr;
+            if (!hip_ok(e = hipMalloc(&d_idx, ridx.size() * 4)) ||
+                !hip_ok(e = hipMemcpy(d_idx, ridx.data(), ridx.size() * 4, hipMemcpyHostToDevice)))
+                return c->hipfail(e, "orphan stubs");
+            const int rc = gather_records(c, P, d_idx, 1, (uint32_t)ridx.size(), offs, st);
+            hipFree(d_idx);
+            if (rc) return rc;
+        }
+        size_t r = 0;
+        for (uint32_t i = 0; i < k; i++) {
+            const uint64_t ord = ord_of(o[i].period);
+            int64_t cand = -1;
+            if (o[i].qr) {
+                cand = (int64_t)c->sorph.size();
+                c->sorph.push_back(pv_ctx::SlowCand{ord, 0, offs[r++], o[i].dir, (uint8_t)((o[i].idx & PV_TCP_IDX) != 0)});
+            }
+            c->stubs.push_back(pv_ctx::EdgeStub{o[i], ord, cand});
+        }
+        c->orph_done = no;
+    }
+    return hip_ok(e = hipStreamSynchronize(st)) ? 0 : c->hipfail(e, "deferred candidates");
+}
+
 // The DNS transaction stage of a batch (TransactionManager state across batches): a batch with
 // responses or a DNS period shift pairs (sort + resolve) its nev_b events together with the
 // queries carried in; a batch of queries only just appends them to the carried list. Also the
@@ -2448,8 +2631,8 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         X.quantiles = ((c->dns_groups & PV_DNS_QUANTILES) ? 1u : 0u) | ((c->dns_groups & PV_DNS_HISTOGRAMS) ? 2u : 0u);
         for (uint32_t k = 0; k <= P.n_dshift; k++) {
             X.slot_gen[k] = P.dslot_of[k] | (c->gen[P.dslot_of[k]] << 8);
-            X.thr_from[k] = k == 0 ? c->from90 : -1.0f;
-            X.thr_to[k] = k == 0 ? c->to90 : -1.0f;
+            X.thr_from[k] = k == 0 && !c->slow_defer ? c->from90 : -1.0f;
+            X.thr_to[k] = k == 0 && !c->slow_defer ? c->to90 : -1.0f;
             for (uint32_t d = 0; d < 3; d++) X.thr2[k][d] = k == 0 ? c->p90_2[d] : -1.0f;
         }
         X.vals = c->d_xvals;
@@ -2466,6 +2649,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         X.orph_cap = c->orph_cap;
         X.trecs = c->d_marena;
         X.toffs = c->d_moffs;
+        X.edge_h = c->slow_defer && !c->dns2_groups ? c->edge_h : 0;
         if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
             !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
             return c->hipfail(e, "parameter upload");
@@ -2473,7 +2657,9 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
         hipLaunchKernelGGL(pv_xact_carry, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_carry");
-        if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
+        if (c->slow_defer) {
+            if (int rc = defer_slow(c, P, st)) return rc;
+        } else if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
             // on_period_shift: slow thresholds = p90 of the bucket that just closed
             // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
             int rc = sync_xvals(c);
@@ -2543,6 +2729,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.tcp_emit = c->tcp_pre ? 0u : 1u;
     if (P.tcp_emit) launch_fill64(c, c->d_tmask, (n + 63) / 64, 0);
     P.gbase = c->global_base + c->records_seen;
+    if (c->slow_defer && !c->edge_h) c->edge_h = (int64_t)first_sec + c->ttl_s + 61;
     if (c->sample_rate < 100) {
         // AbstractMetricsManager::new_event (:318-323): one draw per event of each manager, in
         // stream order; Net events are the records, DNS events the DNS-port UDP records the
@@ -2689,8 +2876,11 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || (force && !strcmp(force, "general"));
         const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && P.wt_per_block / 4 < 65535 &&
                           !(force && !strcmp(force, "ns"));
+        // lean: the register-window pass (pv_net_kernel_reg) unless PV_NET_KERNEL=fast asks for the LDS ring
+        const bool ring = force && !strcmp(force, "fast");
         if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-        else if (lean) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+        else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+        else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
         else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     }
     e = hipGetLastError();
@@ -2761,8 +2951,6 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             fprintf(stderr, "\n");
         }
     }
-    const uint32_t nev_b = status[ST_NEV];
-    const uint32_t nresp = status[ST_NRESP];
     if (int rc = pair_stage(c, P, status[ST_NEV], status[ST_NRESP], n, st)) return rc;
 
     // ---- window bookkeeping (host mirror of each manager's _period_shift)
@@ -2770,6 +2958,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     for (const Shift &sh : dsh) {
         win_shift(c, c->dns, sh.sec);
         c->dns_shifts.emplace_back(sh.sec, c->dns.slot_at(0));
+        c->dns_shift_ord.emplace_back(sh.sec, c->dns.ordinal);
     }
     c->records_seen += n;
     return purge_tables(c, st);
@@ -3044,10 +3233,14 @@ double ms_since(std::chrono::steady_clock::time_point t0)
 } // namespace
 
 // pv_dns_event_seconds over records in host memory, through the ingest staging (chunked).
+static int dns_event_seconds_batch(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
+                                   const uint32_t *sc_idx, const uint32_t *sc_sec, int64_t *secs, uint32_t max, uint32_t *n);
 int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int64_t *secs, uint32_t max, uint32_t *n)
 {
     hipSetDevice(c->device);
     *n = 0;
+    if (c->tcp_active) return c->fail(PV_EINVAL, "pv_dns_event_seconds_host after DNS-over-TCP state (call it before the first batch)");
+    struct TcpClean { pv_ctx *c; ~TcpClean() { std::lock_guard<std::mutex> g(c->mu); tcp_reset(c); } } clean{c};
     if (int rc = ingest_setup(c)) return rc;
     pv_ctx::Stage &st = c->stage[0];
     size_t pos = 0;
@@ -3064,11 +3257,14 @@ int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int6
             !hip_ok(e = hipMemsetAsync(st.d_recs + used, 0, PV_RECS_PAD, c->stream)) ||
             !hip_ok(e = hipMemcpyAsync(st.d_offs, st.h_offs, st.info.n_records * 4, hipMemcpyHostToDevice, c->stream)))
             return c->hipfail(e, "H2D");
-        std::vector<int64_t> part(st.info.n_sec_changes);
+        std::vector<int64_t> part(st.info.n_records + 1);
         uint32_t m = 0;
-        if ((rc = pv_dns_event_seconds(c, st.d_recs, st.d_offs, &st.info, st.sci.data(), st.scs.data(), part.data(),
-                                       (uint32_t)part.size(), &m)))
-            return rc;
+        {
+            std::lock_guard<std::mutex> g(c->mu);
+            if ((rc = dns_event_seconds_batch(c, st.d_recs, st.d_offs, &st.info, st.sci.data(), st.scs.data(), part.data(),
+                                              (uint32_t)part.size(), &m)))
+                return rc;
+        }
         for (uint32_t j = 0; j < m; j++) {
             if (k && secs[k - 1] == part[j]) continue; // a second split across chunks
             if (k >= max) return c->fail(PV_ECAPACITY, "more than %u DNS seconds", max);
@@ -3767,6 +3963,7 @@ int pv_check_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
     }
     win_shift(c, c->dns, sec, nsec);
     c->dns_shifts.emplace_back(sec, c->dns.slot_at(0));
+    c->dns_shift_ord.emplace_back(sec, c->dns.ordinal);
     flush_fills(c);
     hipError_t e = hipStreamSynchronize(st);
     return hip_ok(e) ? 0 : c->hipfail(e, "heartbeat period shift");
@@ -4391,6 +4588,11 @@ int pv_edge_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
 
 int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks, uint32_t me)
 {
+    if (c->slow_defer) {
+        // this rank's own transaction times end here (the edge pairs' follow)
+        if (int rc = sync_xvals(c)) return rc;
+        c->xv_local_end = c->xvals_host.size();
+    }
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
     if (me >= nranks) return c->fail(PV_EINVAL, "rank %u of %u", me, nranks);
@@ -4406,8 +4608,9 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
         for (auto &q : v[j].open) M[q.key] = q;
     }
     if (M.empty()) return 0;
+    // the earliest orphan of each key (stubs are appended in stream order, one per key and batch)
     std::unordered_map<uint64_t, const PvXEvent *> orph;
-    for (auto &o : v[me].orph) orph[o.key] = &o;
+    for (auto &o : v[me].orph) orph.emplace(o.key, &o);
     std::map<uint32_t, std::array<uint64_t, 4>> add; // slot -> total, out, in, timeout
     const bool quant = c->dns_groups & PV_DNS_QUANTILES;
     for (auto &kv : M) {
@@ -4435,6 +4638,19 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
                 if (r.dir == 0) a[1]++;
                 else if (r.dir == 1) a[2]++;
             }
+            // sharded top_slow: the edge pair is a candidate like any valid transaction (its
+            // response record was kept with the stub)
+            const size_t oi = (size_t)(it->second - v[me].orph.data());
+            if (c->slow_defer && oi < c->sorph.size()) {
+                pv_ctx::SlowCand sc = c->sorph[oi];
+                if (quant && r.dir < 2)
+                    c->slow_xv.push_back({sc.ord, PvXValue{us, 0, r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US}});
+                if (kept && r.dir < 2) {
+                    sc.us = us;
+                    sc.dir = r.dir;
+                    c->scands.push_back(sc);
+                }
+            }
             if (quant && in_dns_window(c, slot)) {
                 const uint32_t sg = slot | (c->gen[slot] << 8);
                 if (r.dir == 0) c->xvals_host.push_back(PvXValue{us, sg, XV_FROM_US});
@@ -4455,6 +4671,287 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
         const uint64_t a4[4] = {kv.second[0], kv.second[1], kv.second[2], kv.second[3]};
         if (int rc = add_dns_words(c, kv.first, a4)) return rc;
     }
+    return 0;
+}
+
+// Sharded runs, in rank order (pv_set_slow_defer): `in` holds the DNS queries the earlier shards
+// leave open at this shard's start (the previous rank's *out); each meets the first event of its
+// key in this shard as TransactionManager would (libs/visor_transaction/TransactionManager.h:51-106):
+// a response pairs with it (valid or timed out), a query overwrites it, a DNS shift of this shard
+// at or after ttl + its start purges it first (a time-out there, DnsStreamHandler.h:252-267);
+// the rest stay open. *out: those, and this shard's own queries open at its end (pv_free).
+int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes)
+{
+    *out = nullptr;
+    *out_bytes = 0;
+    if (!c->slow_defer) return c->fail(PV_EINVAL, "pv_edge_carry needs pv_set_slow_defer");
+    if (in_bytes % sizeof(PvXEvent)) return c->fail(PV_EINVAL, "malformed open-query buffer");
+    if (int rc = sync_xvals(c)) return rc;
+    if (c->xv_local_end == SIZE_MAX) c->xv_local_end = c->xvals_host.size();
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return c->hipfail(e, "synchronize");
+    std::unordered_map<uint64_t, size_t> first;
+    first.reserve(c->stubs.size() * 2);
+    for (size_t i = 0; i < c->stubs.size(); i++) first.emplace(c->stubs[i].e.key, i);
+    const uint64_t live = c->dns.ordinal;
+    auto in_win = [&](uint64_t ord) { return ord <= live && ord + c->dns.slots.size() > live; };
+    const bool quant = c->dns_groups & PV_DNS_QUANTILES;
+    std::map<uint32_t, std::array<uint64_t, 4>> add; // slot -> total, out, in, timeout
+    std::vector<PvXEvent> keep;
+    const size_t nin = in_bytes / sizeof(PvXEvent);
+    for (size_t k = 0; k < nin; k++) {
+        PvXEvent qe;
+        memcpy(&qe, in + k * sizeof(PvXEvent), sizeof qe);
+        int ps = -1;
+        for (size_t i = 0; i < c->dns_shift_ord.size(); i++)
+            if (c->dns_shift_ord[i].first >= (int64_t)c->ttl_s + qe.sec) { ps = (int)i; break; }
+        auto purged = [&]() {
+            const uint64_t o = c->dns_shift_ord[ps].second;
+            if (in_win(o)) add[c->dns.slots[live - o]][3]++;
+        };
+        auto it = first.find(qe.key);
+        if (it == first.end()) {
+            if (ps >= 0) purged();
+            else keep.push_back(qe);
+            continue;
+        }
+        const pv_ctx::EdgeStub &st = c->stubs[it->second];
+        if (ps >= 0 && st.ord >= c->dns_shift_ord[ps].second) { purged(); continue; } // purged before its key's next event
+        if (!st.e.qr) continue;                                                          // overwritten by a new query
+        const PvXEvent &r = st.e;
+        const bool kept = (r.pad & 0x80) && in_win(st.ord);
+        const uint32_t slot = r.pad & 0x7f;
+        int64_t dsec = r.sec > qe.sec ? r.sec - qe.sec : qe.sec - r.sec;
+        int64_t dnsec = (int64_t)r.nsec - (int64_t)qe.nsec;
+        if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
+        const bool timed_out = dsec > (int64_t)c->ttl_s || (dsec == (int64_t)c->ttl_s && ((double)dnsec / 1.0e6) >= (double)c->ttl_ms);
+        if (timed_out) { if (kept) add[slot][3]++; continue; }
+        const uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
+        if (kept) {
+            auto &a = add[slot];
+            a[0]++;
+            if (r.dir == 0) a[1]++;
+            else if (r.dir == 1) a[2]++;
+        }
+        if (quant && r.dir < 2) {
+            const uint32_t kind = r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US;
+            c->slow_xv.push_back({st.ord, PvXValue{us, 0, kind}});
+            if (in_win(st.ord)) {
+                const uint32_t sg = slot | (c->gen[slot] << 8);
+                c->xvals_host.push_back(PvXValue{us, sg, kind});
+                if (qe.len && kept) {
+                    const double ratio = (double)r.len / (double)qe.len;
+                    uint64_t bits;
+                    memcpy(&bits, &ratio, 8);
+                    c->xvals_host.push_back(PvXValue{bits, sg, XV_RATIO});
+                }
+            }
+        }
+        if (kept && r.dir < 2 && st.cand >= 0) {
+            pv_ctx::SlowCand sc = c->sorph[(size_t)st.cand];
+            sc.us = us;
+            sc.dir = r.dir;
+            c->scands.push_back(sc);
+        }
+    }
+    for (auto &kv : add) {
+        const uint64_t a4[4] = {kv.second[0], kv.second[1], kv.second[2], kv.second[3]};
+        if (int rc = add_dns_words(c, kv.first, a4)) return rc;
+    }
+    // this shard's own open queries (the carried list, latest event per key)
+    if (c->n_pend) {
+        std::vector<PvXEvent> pend(c->n_pend);
+        std::vector<uint64_t> pk(c->n_pend);
+        if (!hip_ok(e = hipMemcpy(pend.data(), c->d_pend[c->pend_cur], c->n_pend * sizeof(PvXEvent), hipMemcpyDeviceToHost)) ||
+            !hip_ok(e = hipMemcpy(pk.data(), c->d_pkeys[c->pend_cur], c->n_pend * 8, hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "open queries");
+        std::unordered_map<uint64_t, size_t> last;
+        last.reserve(pend.size() * 2);
+        for (size_t i = 0; i < pend.size(); i++) {
+            auto it = last.find(pend[i].key);
+            if (it == last.end() || (uint32_t)pk[i] >= (uint32_t)pk[it->second]) last[pend[i].key] = i;
+        }
+        for (auto &kv : last) keep.push_back(pend[kv.second]);
+    }
+    *out_bytes = keep.size() * sizeof(PvXEvent);
+    *out = (uint8_t *)malloc(*out_bytes ? *out_bytes : 1);
+    if (!*out) return c->fail(PV_ECAPACITY, "out of host memory");
+    if (!keep.empty()) memcpy(*out, keep.data(), *out_bytes);
+    return 0;
+}
+
+int pv_set_slow_defer(pv_ctx *c, int defer)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    if (defer && c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "sharded top_slow with the DNS v2 handler is not built");
+    if (c->records_seen) return c->fail(PV_EINVAL, "set the slow-transaction mode before the first batch");
+    c->slow_defer = defer != 0;
+    return 0;
+}
+
+// This rank's own transaction times per DNS period ordinal: (ordinal u32, kind u32, value u64)
+// records of kinds XV_FROM_US / XV_TO_US. Call before pv_values_merge (which appends the other
+// ranks' values).
+int pv_slow_values_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (int rc = sync_xvals(c)) return rc;
+    std::vector<uint8_t> o;
+    auto put = [&](uint32_t ord, const PvXValue &v) {
+        const size_t p = o.size();
+        o.resize(p + 16);
+        memcpy(&o[p], &ord, 4);
+        memcpy(&o[p + 4], &v.kind, 4);
+        memcpy(&o[p + 8], &v.bits, 8);
+    };
+    const size_t nloc = std::min(c->xv_local_end, c->xvals_host.size());
+    for (size_t i = 0; i < nloc; i++) {
+        const PvXValue &v = c->xvals_host[i];
+        if (v.kind != XV_FROM_US && v.kind != XV_TO_US) continue;
+        auto it = c->sg_ord.find(v.slot);
+        if (it != c->sg_ord.end()) put((uint32_t)it->second, v);
+    }
+    for (auto &ev : c->slow_xv) put((uint32_t)ev.first, ev.second);
+    *bytes = o.size();
+    *buf = (uint8_t *)malloc(o.size() ? o.size() : 1);
+    if (!o.empty()) memcpy(*buf, o.data(), o.size());
+    return 0;
+}
+
+// Every rank's pv_slow_values_export (bufs[0..nranks)): the slow thresholds of each period of
+// the live DNS window over the whole stream (DnsMetricsManager::on_period_shift: at each shift
+// the p90 of the bucket that closed, kept when it had no value; 0 before the first), then this
+// rank's deferred candidates of those periods checked against them and counted into the
+// periods' top_slow tables (DnsMetricsBucket::new_dns_transaction, dns/v1/DnsStreamHandler.cpp:
+// 1121-1136). Call before the top-N exchange.
+int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (!c->slow_defer) return c->fail(PV_EINVAL, "pv_slow_finish without pv_set_slow_defer");
+    // thresholds come from the quantile sketches: none without the quantiles group
+    if (!c->started || !(c->dns_groups & PV_DNS_QUANTILES) || !(c->dns_groups & PV_DNS_TRANSACTIONS)) return 0;
+    // merged values per ordinal
+    std::map<uint64_t, std::vector<uint64_t>> vals[2];
+    for (uint32_t r = 0; r < nranks; r++) {
+        if (sizes[r] % 16) return c->fail(PV_EINVAL, "malformed slow-value buffer of rank %u", r);
+        for (size_t p = 0; p < sizes[r]; p += 16) {
+            uint32_t ord, kind;
+            uint64_t bits;
+            memcpy(&ord, bufs[r] + p, 4);
+            memcpy(&kind, bufs[r] + p + 4, 4);
+            memcpy(&bits, bufs[r] + p + 8, 8);
+            if (kind == XV_FROM_US || kind == XV_TO_US) vals[kind == XV_TO_US][ord].push_back(bits);
+        }
+    }
+    // thresholds of every ordinal up to the live one
+    const uint64_t live = c->dns.ordinal;
+    std::vector<float> thr[2];
+    for (int k = 0; k < 2; k++) {
+        thr[k].assign(live + 1, 0.0f);
+        float t = 0.0f;
+        for (uint64_t o = 1; o <= live; o++) {
+            auto it = vals[k].find(o - 1);
+            if (it != vals[k].end() && !it->second.empty()) t = (float)quantile_at(it->second, 0.90);
+            thr[k][o] = t;
+        }
+    }
+    // the window's periods: ordinal -> slot
+    std::map<uint64_t, uint32_t> win;
+    for (size_t i = 0; i < c->dns.slots.size(); i++) win[live - i] = c->dns.slots[i];
+    std::vector<pv_ctx::SlowCand> sel;
+    for (auto &sc : c->scands) {
+        if (!win.count(sc.ord) || sc.ord > live) continue;
+        const float t = thr[sc.dir == 1][sc.ord]; // dir 0 (toHost): from; 1 (fromHost): to
+        if (t > 0.0f && (float)sc.us >= t) sel.push_back(sc);
+    }
+    if (sel.empty()) return 0;
+    // mini blobs (Ethernet records, TCP message records) and the valid list, by groups of at
+    // most PV_MAX_SHIFTS + 1 periods (the resolve parameters' period arrays)
+    std::vector<uint64_t> ords;
+    for (auto &kv : win) ords.push_back(kv.first);
+    for (size_t g0 = 0; g0 < ords.size(); g0 += PV_MAX_SHIFTS + 1) {
+        const size_t g1 = std::min(ords.size(), g0 + PV_MAX_SHIFTS + 1);
+        std::vector<uint8_t> blob[2];
+        std::vector<uint32_t> offs[2];
+        std::vector<PvXValid> valid;
+        for (auto &sc : sel) {
+            auto it = std::find(ords.begin() + g0, ords.begin() + g1, sc.ord);
+            if (it == ords.begin() + g1) continue;
+            const uint8_t *rec = c->sstore.data() + sc.off;
+            uint32_t cap;
+            memcpy(&cap, rec + 8, 4);
+            const uint32_t sz = (16 + cap + 3) & ~3u;
+            offs[sc.tcp].push_back((uint32_t)blob[sc.tcp].size());
+            blob[sc.tcp].insert(blob[sc.tcp].end(), rec, rec + sz);
+            PvXValid v{};
+            v.idx = (uint32_t)(offs[sc.tcp].size() - 1) | (sc.tcp ? PV_TCP_IDX : 0u);
+            v.period = (uint8_t)(it - (ords.begin() + g0));
+            v.dir = sc.dir;
+            v.us = sc.us;
+            valid.push_back(v);
+        }
+        if (valid.empty()) continue;
+        for (int k = 0; k < 2; k++) blob[k].resize(blob[k].size() + PV_RECS_PAD, 0);
+        hipError_t e;
+        uint8_t *d_blob[2] = {nullptr, nullptr};
+        uint32_t *d_offs[2] = {nullptr, nullptr};
+        PvXValid *d_valid = nullptr;
+        struct Free { void *p[5]; ~Free() { for (void *q : p) if (q) hipFree(q); } } fr{{nullptr, nullptr, nullptr, nullptr, nullptr}};
+        for (int k = 0; k < 2; k++) {
+            if (!hip_ok(e = hipMalloc(&d_blob[k], blob[k].size())) || !hip_ok(e = hipMalloc(&d_offs[k], (offs[k].size() + 1) * 4)))
+                return c->hipfail(e, "slow finish");
+            fr.p[2 * k] = d_blob[k];
+            fr.p[2 * k + 1] = d_offs[k];
+            if (!hip_ok(e = hipMemcpy(d_blob[k], blob[k].data(), blob[k].size(), hipMemcpyHostToDevice)) ||
+                (!offs[k].empty() && !hip_ok(e = hipMemcpy(d_offs[k], offs[k].data(), offs[k].size() * 4, hipMemcpyHostToDevice))))
+                return c->hipfail(e, "slow finish");
+        }
+        if (!hip_ok(e = hipMalloc(&d_valid, valid.size() * sizeof(PvXValid))) ||
+            !hip_ok(e = hipMemcpy(d_valid, valid.data(), valid.size() * sizeof(PvXValid), hipMemcpyHostToDevice)))
+            return c->hipfail(e, "slow finish");
+        fr.p[4] = d_valid;
+        PvParams P;
+        params_common(c, P, d_blob[0], d_offs[0], offs[0].size());
+        P.sum = c->d_sum;
+        P.cpc = c->d_cpc;
+        P.tkeys = c->d_tkeys;
+        P.tcnt = c->d_tcnt;
+        P.taux = c->d_taux;
+        P.tcap_log2 = c->tcap_log2;
+        P.reg_log2 = c->reg_log2;
+        P.arena = c->d_arena;
+        P.arena_top = c->d_arena_top;
+        P.arena_cap = c->arena_cap;
+        P.flags = c->d_status + ST_FLAGS;
+        PvXactParams X;
+        memset(&X, 0, sizeof X);
+        for (size_t j = g0; j < g1; j++) {
+            const uint32_t k = (uint32_t)(j - g0);
+            P.dslot_of[k] = win[ords[j]];
+            X.thr_from[k] = thr[0][ords[j]];
+            X.thr_to[k] = thr[1][ords[j]];
+            c->dns.clean[P.dslot_of[k]] = false;
+        }
+        X.P = P;
+        X.valid = d_valid;
+        X.trecs = d_blob[1];
+        X.toffs = d_offs[1];
+        flush_fills(c);
+        *c->h_xparams = X;
+        if (!hip_ok(e = hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, c->stream)))
+            return c->hipfail(e, "slow finish");
+        hipLaunchKernelGGL(pv_xact_slow, dim3((uint32_t)((valid.size() + 255) / 256)), dim3(256), 0, c->stream,
+                           (const PvXactParams *)c->d_xparams, (uint32_t)valid.size());
+        if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipStreamSynchronize(c->stream))) return c->hipfail(e, "pv_xact_slow");
+    }
+    uint32_t flags = 0;
+    hipError_t e;
+    if (!hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
+    if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
     return 0;
 }
 
@@ -4537,26 +5034,98 @@ int pv_advance_windows(pv_ctx *c, int part, const int64_t *thresh, uint32_t n)
 
 // The seconds (stream order, each once) in which a batch holds a DNS event, by pv_dns_prescan.
 // A sharded run's ranks exchange these to compute the DNS manager's global shifts.
+// One batch of pv_dns_event_seconds: the UDP events from the prescan bits, the DNS-over-TCP
+// messages from a run of the TCP stage (which advances the TCP state: the callers reset it).
+static int dns_event_seconds_batch(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
+                                   const uint32_t *sc_idx, const uint32_t *sc_sec, int64_t *secs, uint32_t max, uint32_t *n)
+{
+    *n = 0;
+    const uint64_t nr = info->n_records;
+    if (!nr) return 0;
+    if (nr > c->max_records) return c->fail(PV_ECAPACITY, "batch exceeds max_records");
+    uint32_t tseg[2];
+    if (int rc = dns_prescan(c, d_recs, d_offs, nr, c->stream, true, tseg)) return rc;
+    if (int rc = tcp_stage(c, d_recs, d_offs, nr, tseg[0], tseg[1], (uint32_t)info->first_sec, true, c->stream)) return rc;
+    // (ord, second) of every DNS event in stream order: a second's first UDP event, the messages
+    std::vector<std::pair<uint64_t, int64_t>> ev;
+    for (uint32_t j = 0; j < info->n_sec_changes; j++) {
+        const uint64_t lo = sc_idx[j], hi = j + 1 < info->n_sec_changes ? sc_idx[j + 1] : nr;
+        const uint64_t b = next_bit(c->h_dbits, lo, nr);
+        if (b < hi) ev.push_back({b * 4, (int64_t)sc_sec[j]});
+    }
+    const size_t nu = ev.size();
+    ev.insert(ev.end(), c->tcp_ords.begin(), c->tcp_ords.end());
+    std::inplace_merge(ev.begin(), ev.begin() + nu, ev.end());
+    c->tcp_ords.clear();
+    c->tcp_nmsg = 0;
+    uint32_t k = 0;
+    for (auto &x : ev) {
+        if (k && secs[k - 1] == x.second) continue;
+        if (k >= max) return c->fail(PV_ECAPACITY, "more than %u DNS seconds", max);
+        secs[k++] = x.second;
+    }
+    *n = k;
+    return 0;
+}
+
 int pv_dns_event_seconds(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
                          const uint32_t *sc_idx, const uint32_t *sc_sec, int64_t *secs, uint32_t max, uint32_t *n)
 {
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
     *n = 0;
-    const uint64_t nr = info->n_records;
-    if (!nr) return 0;
-    if (nr > c->max_records) return c->fail(PV_ECAPACITY, "batch exceeds max_records");
-    uint32_t tseg[2];
-    if (int rc = dns_prescan(c, d_recs, d_offs, nr, c->stream, false, tseg)) return rc;
-    uint32_t k = 0;
-    for (uint32_t j = 0; j < info->n_sec_changes; j++) {
-        const uint64_t lo = sc_idx[j], hi = j + 1 < info->n_sec_changes ? sc_idx[j + 1] : nr;
-        if (next_bit(c->h_dbits, lo, nr) >= hi) continue;
-        if (k >= max) return c->fail(PV_ECAPACITY, "more than %u DNS seconds", max);
-        secs[k++] = sc_sec[j];
-    }
-    *n = k;
-    return 0;
+    if (c->tcp_active) return c->fail(PV_EINVAL, "pv_dns_event_seconds after DNS-over-TCP state (call it before the first batch)");
+    const int rc = dns_event_seconds_batch(c, d_recs, d_offs, info, sc_idx, sc_sec, secs, max, n);
+    tcp_reset(c);
+    return rc;
 }
 
 } // extern "C"
+
+// Shard cuts of a capture for a sharded run: world contiguous record ranges of about equal
+// size, each cut moved to the nearest record boundary that no DNS-over-TCP flow spans (every
+// flow key seen before the cut has its last packet before it), so each shard's TCP stage
+// starts from the empty state a single pass holds for those flows there. A capture with a
+// flow across a whole shard moves the cut past it (shards grow, some may be empty).
+int pv_shard_cuts(const uint8_t *recs, size_t bytes, const uint32_t *offs, uint64_t n, uint32_t linktype, uint32_t ts_nano,
+                  uint32_t world, uint64_t *cuts)
+{
+    if (!world) return PV_EINVAL;
+    PvParams P;
+    memset(&P, 0, sizeof P);
+    P.linktype = linktype;
+    P.ts_nano = ts_nano;
+    const pvname::HostRecs R{recs, bytes};
+    std::vector<uint32_t> key(n);
+    std::vector<uint8_t> tcp(n, 0);
+    std::unordered_map<uint32_t, uint64_t> last;
+    for (uint64_t i = 0; i < n; i++) {
+        if (offs[i] + 16ull > bytes) return PV_EINVAL;
+        if (pvname::tcp_dns_flow(R, P, offs[i], &key[i])) {
+            tcp[i] = 1;
+            last[key[i]] = i;
+        }
+    }
+    // ok[c]: no flow has packets on both sides of record boundary c
+    std::vector<uint8_t> ok(n + 1, 1);
+    int64_t reach = -1;
+    for (uint64_t i = 0; i < n; i++) {
+        if (tcp[i]) reach = std::max<int64_t>(reach, (int64_t)last[key[i]]);
+        ok[i + 1] = reach <= (int64_t)i;
+    }
+    const uint64_t per = (n + world - 1) / world;
+    cuts[0] = 0;
+    for (uint32_t r = 1; r < world; r++) {
+        const uint64_t lo = cuts[r - 1], ideal = std::max(lo, std::min<uint64_t>(n, (uint64_t)r * per));
+        uint64_t best = n;
+        for (uint64_t d = 0;; d++) {
+            const bool up = ideal + d <= n, down = ideal >= lo + d;
+            if (!up && !down) break;
+            if (up && ok[ideal + d]) { best = ideal + d; break; }
+            if (down && ok[ideal - d]) { best = ideal - d; break; }
+        }
+        cuts[r] = best;
+    }
+    cuts[world] = n;
+    return 0;
+}

@@ -1967,9 +1967,203 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
     }
 }
 
+// ------------------------------------------------------------------ the lean Net pass, register windows
+// The lean pass without the LDS ring: each lane loads its own record's first 80 bytes straight
+// into registers (five 16-B loads from the record's dword-aligned start, so the record's
+// dwords are one alignbyte away: no selects), the next tile's windows in flight while the wave
+// parses this one (two register buffers, the loop unrolled by two so no copy waits on them).
+// tools/stream_probe.hip measured the pattern alone at 5.8 TB/s (modes 7/8) against 4.2 TB/s
+// for the LDS-DMA ring's staging; the LDS keeps only the histogram and the DNS list counter.
+#ifndef PV_REG_MINW
+#define PV_REG_MINW 3 // waves per SIMD the register allocation must allow
+#endif
+struct NetRegState {
+    uint32_t hist[PV_HBINS];
+    uint32_t nd;
+    int64_t dthresh[PV_MAX_SHIFTS];
+};
+__device__ __forceinline__ void win_load(const PV_G uint8_t *recs, uint32_t off, uint4 (&W)[5])
+{
+    const PV_G uint4 *p = reinterpret_cast<const PV_G uint4 *>(recs + (off & ~3u));
+#pragma unroll
+    for (int j = 0; j < 5; j++) W[j] = p[j];
+}
+__device__ __forceinline__ void win_words(const uint4 (&W)[5], uint32_t sh, RecW &r)
+{
+    uint32_t x[17];
+#pragma unroll
+    for (int k = 0; k < 4; k++) { x[4 * k] = W[k].x; x[4 * k + 1] = W[k].y; x[4 * k + 2] = W[k].z; x[4 * k + 3] = W[k].w; }
+    x[16] = W[4].x;
+#pragma unroll
+    for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+}
+__device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ NetRegState S;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
+    if (threadIdx.x == 0) S.nd = 0;
+    if (threadIdx.x < PV_MAX_SHIFTS) S.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+    __syncthreads();
+    const PV_G uint8_t *const recs = P.recs;
+    const PV_G uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint32_t slot = P.slot_of[0];
+    const uint32_t groups = P.net_groups;
+    const bool tops = groups & PV_NET_TOP_IPS_BIT, card = groups & PV_NET_CARDINALITY_BIT;
+    const uint32_t ts_nano = P.ts_nano;
+    HostNets h;
+    {
+        const uint32_t n4 = P.nets.n4;
+        h.a0 = P.nets.v4_addr[0]; h.m0 = P.nets.v4_mask[0]; h.e0 = n4 > 0 ? ~0u : 0u;
+        h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
+    }
+    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
+    const uint64_t wbeg = (uint64_t)blockIdx.x * P.wt_per_block;
+    const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + 3) / 4) : 0u;
+    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + 4ull * min(k, ntl - 1); };
+    auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
+    uint64_t cd = 0, cl = 0; // fast lanes' packed counters (net_fast)
+    NetCtr c;
+    c.zero();
+    // one tile from its windows W (off: this lane's record start)
+    auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
+        const uint64_t t = tile_of(k);
+        const uint64_t r0 = t * PV_WT, i = r0 + lane;
+        const bool active = i < n;
+        RecW rw;
+        win_words(W, off & 3, rw);
+        const FastRec f = fast_fields(rw, h);
+        const bool fast = active & (f.ok != 0);
+        const uint64_t slowm = __ballot(active & !fast);
+        cd += fast ? 1ull << (f.dir * 16) : 0ull;
+        cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
+        uint32_t hv = fast ? f.caplen : PV_NOH;
+        const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
+        const bool ipok = fast & (f.dir != 2) & (ip != 0);
+        uint64_t ek = tops && ipok ? ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
+                                         ((uint64_t)f.dir << 32) | ip
+                                   : 0ull;
+        if (card && !tops) {
+            if (ipok) {
+                uint64_t h1, h2;
+                murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+                __hip_atomic_fetch_min(P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)(f.dir == 0 ? CPC_SRC : CPC_DST) * PV_CPC_COUPONS +
+                                           cpc_coupon(h1, h2),
+                                       (int64_t)(P.gbase + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        const uint32_t port = (fast & (f.l4 == 17)) ? dns_port_bf(rw.at(50)) : 0u;
+        DnsMsgW dm{};
+        bool isdns = port != 0;
+        if (__ballot(isdns)) {
+            if (isdns) {
+                const Parsed o = fast_parsed(f, rw, ts_nano, off);
+                uint32_t dp = 0;
+                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)o.sec >= S.dthresh[q];
+                const SAcc R{recs, nullptr, 0, 0, 0, 1};
+                DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
+                d.fkey = fast_flowkey(rw);
+                dm = msg_words(d);
+            }
+        }
+        bool istcp = fast & (f.l4 == 6), hasseg = false;
+        PvTcpSeg seg;
+        const uint32_t temit = P.tcp_emit;
+        if (temit && __ballot(istcp)) {
+            if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
+        }
+        if (slowm) {
+            // general-path records (VLAN, IPv6, options, tunnels, other link types): every byte from HBM
+            if (active && !fast) {
+                const SAcc R{recs, nullptr, 0, 0, 0, 1};
+                const SlowOut so = net_slow_p(Pp, R, off, i);
+                Parsed o;
+                o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
+                c.add(o);
+                hv = so.caplen;
+                ek = so.ek;
+                dm = so.dm;
+                isdns = so.isdns;
+                istcp = so.l4 == 6;
+            }
+        }
+        if (__ballot(hv != PV_NOH && hv > 65535)) {
+            if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
+        }
+        hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
+        const uint64_t m = __ballot(isdns);
+        if (m) {
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(&S.nd, (uint32_t)__popcll(m));
+            q = __builtin_amdgcn_readlane(q, 0);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (isdns) {
+                PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(P.dq) + 2 * (wbeg * PV_WT + q + below);
+                dd[0] = dm.a;
+                dd[1] = dm.b;
+            }
+        }
+        if (tops && active) P.iplog[i] = ek;
+        if (temit) {
+            const uint64_t tm = __ballot(istcp);
+            if (tm) {
+                if (lane == 0) P.tmask[t] = tm;
+                tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, seg, lane);
+            }
+        }
+    };
+    // software pipeline, unrolled by two: while tile k is parsed from one buffer the windows of
+    // tile k + 1 land in the other; tile k + 2's offsets are loaded ahead of tile k + 1's windows
+    uint4 WA[5], WB[5];
+    uint32_t oA = 0, oB = 0;
+    if (ntl) {
+        oA = off_of(0);
+        oB = off_of(1);
+        win_load(recs, oA, WA);
+    }
+    // Issue order per tile j: offsets of tile j + 2, windows of tile j + 1, then tile j's work.
+    // Loads retire in order, so the offsets a window load needs were issued before the windows
+    // still in flight, and each wait the compiler places (for offsets, then for windows) leaves
+    // the younger loads and the previous tile's stores in flight.
+    for (uint32_t k = 0; k < ntl; k += 2) {
+        const uint32_t oN = off_of(k + 2);
+        win_load(recs, oB, WB);              // tile k + 1 (a clamped copy past the range's end)
+        tile(k, oA, WA);
+        if (k + 1 >= ntl) break;
+        const uint32_t oN2 = off_of(k + 3);
+        win_load(recs, oN, WA);              // tile k + 2
+        oA = oN;
+        tile(k + 1, oB, WB);
+        oB = oN2;
+    }
+    {
+        const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
+        const uint32_t nf = fin + fout + funk;
+        c.nev += nf; c.n4 += nf;
+        c.nin += fin; c.nout += fout; c.nunk += funk;
+        c.nudp += (uint32_t)(cl & 0xffff); c.ntcp += (uint32_t)((cl >> 16) & 0xffff);
+        c.noth += (uint32_t)((cl >> 32) & 0xffff); c.nsyn += (uint32_t)(cl >> 48);
+    }
+    NetK K;
+    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
+    if (ntl) knet_flush(K, slot, c);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
+        if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
+    if (threadIdx.x == 0) {
+        P.mq_cnt[blockIdx.x] = 0;
+        P.dq_cnt[blockIdx.x] = S.nd;
+        if (S.nd) atomicAdd(P.n_dns, S.nd);
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(const PvParams *__restrict__ Pp) { net_pass<true>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(const PvParams *__restrict__ Pp) { net_pass<false>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg(Pp); }
 
 // ------------------------------------------------------------------ the DNS pass
 // One lane per DNS message of the Net pass's work list (same workgroup mapping).
@@ -3331,6 +3525,21 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
             slow_check(X, e.idx, e.period, e.dir, us);
         }
     } else {
+        if (X.edge_h && e.sec < X.edge_h) {
+            // sharded runs: the first query of its key may overwrite an open query of an earlier
+            // shard (the stub list holds it next to the orphan responses)
+            int q = (int)p - 1;
+            for (; q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h; q--)
+                if (xev(X, q).key == e.key) break;
+            if (q < 0 || (uint32_t)(X.skeys[q] >> 32) != h) {
+                const uint32_t k = atomicAdd(X.n_orph, 1u);
+                if (k < X.orph_cap) {
+                    PvXEvent o = e;
+                    o.pad = (uint8_t)(P.dslot_of[e.period] | (e.period >= P.dskip_before ? 0x80u : 0u));
+                    X.orph[k] = o;
+                }
+            }
+        }
         // an open query purged at a later period shift counts as timed out there
         uint32_t kp = purge_period(P, X.ttl_s, e.period, e.sec);
         if (!kp) return;
@@ -3488,4 +3697,37 @@ extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t
                                           uint32_t *vout, size_t n, hipStream_t s)
 {
     return rocprim::radix_sort_pairs(tmp, *tmp_bytes, kin, kout, vin, vout, n, 0, 64, s);
+}
+
+// ------------------------------------------------------------------ record gather (sharded top_slow)
+// The records of a list of batch record indices (idx[i * stride], PV_TCP_IDX: a TCP message
+// record of the batch's message arena), copied whole (16-B header + capture, 4-B padded) into
+// one blob: the deferred slow-transaction candidates of a sharded run keep their response
+// records this way until the merge knows every period's threshold (pv_slow_finish).
+extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
+                                        const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t id = idx[(uint64_t)i * stride];
+    const bool tcp = id & PV_TCP_IDX;
+    const uint8_t *r = tcp ? trecs + toffs[id & ~PV_TCP_IDX] : recs + offs[id];
+    const uint32_t cap = min((uint32_t)r[8] | (uint32_t)r[9] << 8 | (uint32_t)r[10] << 16 | (uint32_t)r[11] << 24, 65535u);
+    sizes[i] = (16u + cap + 3u) & ~3u;
+}
+extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
+                                         const uint32_t *idx, uint32_t stride, uint32_t n, const uint32_t *dst_off, uint8_t *out)
+{
+    // one wave per record, dword copies
+    const uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= n) return;
+    const uint32_t id = idx[(uint64_t)i * stride];
+    const bool tcp = id & PV_TCP_IDX;
+    const uint8_t *r = tcp ? trecs + toffs[id & ~PV_TCP_IDX] : recs + offs[id];
+    const uint32_t cap = min((uint32_t)r[8] | (uint32_t)r[9] << 8 | (uint32_t)r[10] << 16 | (uint32_t)r[11] << 24, 65535u);
+    const uint32_t bytes = 16u + cap;
+    uint8_t *o = out + dst_off[i];
+    for (uint32_t b = lane; b < bytes; b += 64) o[b] = r[b];
+    if (lane == 0) *reinterpret_cast<uint32_t *>(o + 8) = cap; // a clamped capture length stays consistent
+    for (uint32_t b = bytes + lane; b < ((bytes + 3u) & ~3u); b += 64) o[b] = 0;
 }

@@ -463,6 +463,10 @@ struct PvXactParams {
     const PV_G uint32_t *toffs;
     // DNS v2: per period and direction the p90 slow threshold (< 0 = not known yet)
     float thr2[PV_MAX_SHIFTS + 1][3];
+    // sharded runs (pv_set_slow_defer): queries with no earlier event of their key whose second
+    // is below this horizon are appended to the stub list too (a query of an earlier shard still
+    // open there is overwritten by them, TransactionManager::start_transaction); 0 = none
+    int64_t edge_h;
 };
 #define PV_PEND_FLAG 0x80000000u
 

@@ -20,7 +20,11 @@ Policy::_get_merged_buckets (src/Policies.cpp:420-446):
     end, responses that are the first event of their (flow, txid) in it, its period
     shifts) are all-gathered; each rank pairs its own stub responses with what the
     earlier shards leave open, before the SUM round (pv_edge_merge);
-  * quantile inputs of the live window: all-gathered and appended (pv_values_*).
+  * quantile inputs of the live window: all-gathered and appended (pv_values_*);
+  * top_slow: a slow transaction is judged against the p90 of the bucket that closed at the last
+    DNS shift, a bucket spread over several shards; each rank keeps its candidates with their
+    response records (pv_set_slow_defer) and, once every rank's transaction times per period
+    are gathered, counts the ones above the whole stream's thresholds (pv_slow_finish).
 
 merge_window() runs the whole sequence; reduce_handlers() is the device part alone
 (the per-step collective of the bench).
@@ -137,6 +141,11 @@ def process_shard(handlers, recs, index, start_sec: int, start_nsec: int = 0, gr
     the global period plan, the shard's batches, the later ranks' shifts. Afterwards every
     rank's windows hold the same periods in the same slots."""
     handlers.set_start_tstamp(start_sec, start_nsec)
+    if not getattr(handlers, "slow_defer", False):
+        try:
+            handlers.set_slow_defer(True)
+        except Exception:  # DNS v2: its slow tops keep the rank's own thresholds
+            handlers.slow_defer = False
     dns = handlers.dns_event_seconds_host(recs) if len(recs) else []
     plan = plan_windows(handlers, start_sec, record_seconds(index) if index is not None and index.n else [], dns, group)
     apply_plan(handlers, plan, 0)
@@ -172,7 +181,27 @@ def check_aligned(handlers, group=None, comm=None):
 
 
 def merge_edges(handlers, group=None, comm=None):
+    """DNS transactions across shard edges. Deferred runs carry the open queries rank by rank
+    (pv_edge_carry: W gather rounds, rank r computes its carry in round r from rank r-1's), so a
+    query meets the first event of its key in ANY later shard, after that shard's purges;
+    otherwise every rank's stubs are gathered once and paired with the previous shards'."""
+    if getattr(handlers, "slow_defer", False):
+        me = _rank(handlers, group, comm)
+        world = handlers.comm_ranks if comm == "pv" else dist.get_world_size(group)
+        carried = b""
+        for r in range(world):
+            mine = handlers.edge_carry(carried) if r == me else b""
+            got = _allgather(handlers, mine, group, comm)
+            carried = got[r]
+        return
     handlers.edge_merge(_allgather(handlers, handlers.edge_export(), group, comm), _rank(handlers, group, comm))
+
+
+def merge_slow(handlers, group=None, comm=None):
+    """top_slow over the whole stream: every rank's transaction times per DNS period ordinal,
+    then each rank's deferred candidates (after the edge merge, before the value merge)"""
+    if getattr(handlers, "slow_defer", False):
+        handlers.slow_finish(_allgather(handlers, handlers.slow_values_export(), group, comm))
 
 
 def merge_values(handlers, group=None, comm=None):
@@ -188,6 +217,7 @@ def merge_window(handlers, device, group=None, comm=None):
     handlers.synchronize()
     check_aligned(handlers, group, comm)
     merge_edges(handlers, group, comm)
+    merge_slow(handlers, group, comm)
     merge_values(handlers, group, comm)
     if comm == "pv":
         handlers.comm_allreduce_window()

@@ -118,6 +118,24 @@ def sparse_dns_pcap(n: int = 120000, ts_step_us: int = 2500, quiet=(52, 9), seed
     return pcap_file_bytes(b"".join(keep))
 
 
+def merged_pcap(*pcaps) -> bytes:
+    """the records of several classic pcaps in one capture, in timestamp order (ties: argument
+    order, then each capture's own order)"""
+    from pktvisor_amd import pcap_file_bytes
+    allr = []
+    for k, pc in enumerate(pcaps):
+        allr += [(s, u, k, i, r) for i, (s, u, r) in enumerate(records_of(pc))]
+    allr.sort(key=lambda x: x[:4])
+    return pcap_file_bytes(b"".join(x[4] for x in allr))
+
+
+def c4_tcp_pcap(n: int = 120000, ts_step_us: int = 2500, flows: int = 300, seed: int = 3) -> bytes:
+    """C4 traffic over n * ts_step_us (300 s by default: several 60 s marks) with DNS-over-TCP
+    connections (tcp_dns_pcap) spread over the same span"""
+    dur = n * ts_step_us / 1e6
+    return merged_pcap(pcap_bytes(4, n, ts_step_us=ts_step_us), tcp_dns_pcap(seed=seed, flows=flows, duration_s=dur * 0.95))
+
+
 # ---------------------------------------------------------------- DNS over TCP
 def _dns_msg(rng, txid: int, qr: bool, name: str, qtype: int, rcode: int = 0, answers: int = 0) -> bytes:
     import struct

@@ -45,7 +45,8 @@ def gpu_main(pcap_path, out, host, periods):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     linktype, ts_nano, recs = pa.read_pcap(pcap_path)
     idx = pa.RecordIndex(recs, ts_nano)
-    lo, hi = pvdist.shard_range(idx.n, world, rank)
+    cuts = pa.shard_cuts(recs, idx, linktype, ts_nano, world)
+    lo, hi = cuts[rank], cuts[rank + 1]
     offs = [int(x) for x in idx.offsets] + [len(recs)]
     h = pa.PvHandlers(host_spec=host or None, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
                       max_records=max(1, hi - lo), device=dev.index)

@@ -9,6 +9,9 @@
 //   mode 4: mode 3 + an 8-B per-lane store per tile (dense IP log)
 //   mode 5: mode 4 + two 16-B per-lane stores per tile into a per-wave 2-KiB area
 //   mode 6: mode 4 + two 16-B stores per tile, all lanes of a wave to one address
+//   mode 7: mode 2 with per-lane windows: each lane loads its own record's 80 B (five
+//           16-B loads from the 16-B aligned record start), no LDS
+//   mode 8: mode 7 from the dword-aligned record start (unaligned 16-B loads)
 // usage: stream_probe [records]
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -28,7 +31,7 @@ __global__ void __launch_bounds__(256) probe(const uint8_t *__restrict__ recs, c
     const uint64_t wbeg = blockIdx.x * wtpb, wend = min(wbeg + wtpb, nwt);
     const uint64_t last = n - 1;
     uint32_t acc = 0;
-    constexpr int NJ = MODE == 0 ? 5 : 6;
+    constexpr int NJ = (MODE == 0 || MODE >= 7) ? 5 : 6;
     uint4 pf[NJ];
 #define ISSUE(B0, B1)                                                                  \
     {                                                                                  \
@@ -44,7 +47,13 @@ __global__ void __launch_bounds__(256) probe(const uint8_t *__restrict__ recs, c
     uint64_t t = wbeg + wave;
     uint32_t off_n = 0, end_n = 0;
     if (t < wend) {
-        if (MODE >= 2) {
+        if (MODE >= 7) {
+            const uint32_t o0 = lane_off(t);
+            const uint32_t a = MODE == 7 ? (o0 & ~15u) : (o0 & ~3u);
+#pragma unroll
+            for (int j = 0; j < NJ; j++) pf[j] = *reinterpret_cast<const uint4 *>(recs + a + 16 * j);
+            off_n = lane_off(t + 4);
+        } else if (MODE >= 2) {
             const uint32_t o0 = lane_off(t), e0 = lane_end(t);
             ISSUE(__builtin_amdgcn_readlane(o0, 0), __builtin_amdgcn_readlane(e0, 63));
             off_n = lane_off(t + 4);
@@ -54,7 +63,7 @@ __global__ void __launch_bounds__(256) probe(const uint8_t *__restrict__ recs, c
         }
     }
     for (; t < wend; t += 4) {
-        if (MODE >= 3) {
+        if (MODE >= 3 && MODE < 7) {
 #pragma unroll
             for (int j = 0; j < NJ; j++) stage[wave][j * 64 + lane] = pf[j];
         } else {
@@ -62,7 +71,12 @@ __global__ void __launch_bounds__(256) probe(const uint8_t *__restrict__ recs, c
             for (int j = 0; j < NJ; j++) acc += pf[j].x ^ pf[j].y ^ pf[j].z ^ pf[j].w;
         }
         if (t + 4 < wend) {
-            if (MODE >= 2) {
+            if (MODE >= 7) {
+                const uint32_t a = MODE == 7 ? (off_n & ~15u) : (off_n & ~3u);
+#pragma unroll
+                for (int j = 0; j < NJ; j++) pf[j] = *reinterpret_cast<const uint4 *>(recs + a + 16 * j);
+                off_n = lane_off(t + 8);
+            } else if (MODE >= 2) {
                 ISSUE(__builtin_amdgcn_readlane(off_n, 0), __builtin_amdgcn_readlane(end_n, 63));
                 off_n = lane_off(t + 8);
                 end_n = lane_end(t + 8);
@@ -70,8 +84,8 @@ __global__ void __launch_bounds__(256) probe(const uint8_t *__restrict__ recs, c
                 ISSUE((uint32_t)((t + 4) * WT * REC), (uint32_t)((t + 5) * WT * REC));
             }
         }
-        if (MODE >= 3) acc += stage[wave][(lane * 5) % 320].x;
-        if (MODE >= 4) log[t * WT + lane] = acc;
+        if (MODE >= 3 && MODE < 7) acc += stage[wave][(lane * 5) % 320].x;
+        if (MODE >= 4 && MODE < 7) log[t * WT + lane] = acc;
         if (MODE == 5) { uint4 *tr = reinterpret_cast<uint4 *>(log + 20000000) + (blockIdx.x * 4 + wave) * 128; tr[lane] = pf[0]; tr[64 + lane] = pf[1]; }
         if (MODE == 6) { uint4 *tr = reinterpret_cast<uint4 *>(log + 20000000) + (blockIdx.x * 4 + wave) * 2; tr[0] = pf[0]; tr[1] = pf[1]; }
     }
@@ -99,8 +113,8 @@ int main(int argc, char **argv)
     hipEventCreate(&a);
     hipEventCreate(&b);
     const uint64_t nwt = (n + WT - 1) / WT;
-    for (int mode = 0; mode < 7; mode++)
-        for (int wpc : {2, 4}) {
+    for (int mode = 0; mode < 9; mode++)
+        for (int wpc : {2, 4, 8}) {
             const uint64_t grid = (uint64_t)cus * wpc;
             const uint64_t wtpb = (nwt + grid - 1) / grid;
             float best = 1e9f;
@@ -113,7 +127,9 @@ int main(int argc, char **argv)
                 case 3: hipLaunchKernelGGL(probe<3>, dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); break;
                 case 4: hipLaunchKernelGGL(probe<4>, dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); break;
                 case 5: hipLaunchKernelGGL(probe<5>, dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); break;
-                default: hipLaunchKernelGGL(probe<6>, dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); break;
+                case 6: hipLaunchKernelGGL(probe<6>, dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); break;
+                case 7: hipLaunchKernelGGL(probe<7>, dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); break;
+                default: hipLaunchKernelGGL(probe<8>, dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); break;
                 }
                 hipEventRecord(b);
                 hipEventSynchronize(b);
