@@ -159,6 +159,7 @@ extern "C" __global__ void pv_ix_fix(const PvIxParams *X, uint32_t src);
 extern "C" __global__ void pv_ix_scan(const PvIxParams *X);
 extern "C" __global__ void pv_ix_write(const PvIxParams *X);
 extern "C" __global__ void pv_ix_secs(const PvIxParams *X, uint32_t n);
+extern "C" __global__ void pv_topn_retry(const PvParams *P, const PvOvf *src, uint32_t n);
 extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_t *theta_out);
 extern "C" __global__ void pv_topn_compact(const PvParams *P, uint32_t tb, uint8_t *tmp, unsigned long long *tmp_top);
 extern "C" __global__ void pv_topn_names(const PvParams *P);
@@ -415,7 +416,8 @@ struct pv_ctx {
     uint32_t *d_mq_cnt = nullptr;
     uint64_t *d_stamps = nullptr; // diagnostic phase stamps (PV_STAMPS env + -DPV_STAMPS build)
     int cus = 256;
-    int wg_per_cu = 2; // resident Net-pass workgroups per CU (occupancy API)
+    int wg_per_cu = 3;     // grid workgroups per CU (the batch's partition)
+    int reg_wg_per_cu = 1; // workgroups per CU of the register-window Net pass
     uint64_t *d_dq = nullptr; // DNS work lists (32-B messages)
     uint32_t *d_dq_cnt = nullptr;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
@@ -445,6 +447,9 @@ struct pv_ctx {
     // bounded top-N tables: entries per table (device, read back with each batch's status),
     // each purged region's accumulated theta (the estimate offset of its survivors)
     uint32_t *d_tab_live = nullptr, *h_tab_live = nullptr, *d_theta = nullptr;
+    PvOvf *d_ovf = nullptr, *d_ovf2 = nullptr; // top-N overflow list and its retry copy
+    uint32_t *d_ovf_cnt = nullptr, ovf_cap = 0;
+    uint64_t ovf_rounds = 0;                    // purge-and-retry rounds so far
     uint8_t *d_ctmp = nullptr;          // arena compaction scratch (one table's arena)
     unsigned long long *d_ctop = nullptr;
     std::vector<uint64_t> roff[PV_TABLES];
@@ -1672,6 +1677,143 @@ void dns_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
     p.topn("dns_top_qtype", "qtype", "Top query types", dense_tops(&b.sum[PV_OFF_QTYPE], PV_QTYPE_BINS, 1), topn, pct);
 }
 
+// NetworkMetricsBucket::to_prometheus / to_opentelemetry, Net v2
+// (src/handlers/net/v2/NetStreamHandler.cpp:333-383; names NetStreamHandler.h:72-181): the
+// event counts, `filtered_packets`, then per direction the bucket has seen, labelled
+// direction=in|out|unknown (rates are timer-driven and out of scope; geo / ASN TopNs empty)
+template <class Sink>
+void net2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
+{
+    const uint64_t *n = &b.sum[PV_OFF_NET2];
+    const uint32_t g = c->net2_groups;
+    const size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
+    p.gauge("net_observed_packets", "Total packets events generated", n[N2_EVENTS]);
+    p.gauge("net_deep_sampled_packets", "Total packets that were sampled for deep inspection", n[N2_SAMPLES]);
+    if (g & PV_N2G_COUNTERS) p.gauge("net_filtered_packets", "Total packets seen that did not match the configured filter(s) (if any)", n[N2_FILTERED]);
+    static const char *dirs[3] = {"in", "out", "unknown"};
+    const PromLabels base = p.add;
+    for (uint32_t d = 0; d < 3; d++) {
+        const uint64_t *dc = n + N2_DIR + 8 * d;
+        if (!dc[N2_TOTAL]) continue;
+        p.add = base;
+        p.add["direction"] = dirs[d];
+        if (g & PV_N2G_COUNTERS) {
+            p.gauge("net_udp_packets", "Count of UDP packets", dc[N2_UDP]);
+            p.gauge("net_tcp_packets", "Count of TCP packets", dc[N2_TCP]);
+            p.gauge("net_other_l4_packets", "Count of packets which are not UDP or TCP", dc[N2_OTHER]);
+            p.gauge("net_ipv4_packets", "Count of IPv4 packets", dc[N2_V4]);
+            p.gauge("net_ipv6_packets", "Count of IPv6 packets", dc[N2_V6]);
+            p.gauge("net_tcp_syn_packets", "Count of TCP SYN packets", dc[N2_SYN]);
+            p.gauge("net_total_packets", "Count of total packets matching the configured filter(s)", dc[N2_TOTAL]);
+        }
+        if (g & PV_N2G_CARDINALITY)
+            p.gauge("net_cardinality_ips", "IP cardinality", lround(cpc_estimate(&b.cpc[(CPC_V2 + d) * PV_CPC_COUPONS], b.merged)));
+        if (g & PV_N2G_TOP_IPS) {
+            p.topn("net_top_ipv4_packets", "ipv4", "Top IPv4 addresses", tops_of(b, TMH_V2_IP4 + d), topn, pct);
+            p.topn("net_top_ipv6_packets", "ipv6", "Top IPv6 addresses", tops_of(b, TMH_V2_IP6 + d), topn, pct);
+        }
+        if (g & PV_N2G_QUANTILES) {
+            uint64_t cnt;
+            const uint64_t *h = &b.sum[PV_OFF_PAYLOAD2 + d * PV_PAYLOAD_BINS];
+            auto q = hist_quantiles(h, PV_PAYLOAD_BINS, cnt);
+            uint64_t mx = 0;
+            for (size_t i = 0; i < PV_PAYLOAD_BINS; i++)
+                if (h[i]) mx = i;
+            if (cnt) p.template summary<uint64_t>("net_payload_size_bytes", "Quantiles of payload sizes, in bytes", q, mx, cnt);
+        }
+    }
+    p.add = base;
+}
+
+// DnsMetricsBucket::to_prometheus / to_opentelemetry, DNS v2
+// (src/handlers/dns/v2/DnsStreamHandler.cpp:759-842; names DnsStreamHandler.h:98-115,250-270):
+// the event counts, `filtered_packets`, then per transaction direction the bucket has set up
+template <class Sink>
+void dns2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
+{
+    const uint64_t *d = &b.sum[PV_OFF_DNS];
+    const uint32_t g = c->dns2_groups;
+    const size_t topn = c->cfg.topn_count;
+    const uint32_t pct = c->cfg.topn_percentile_threshold;
+    p.gauge("dns_observed_packets", "Total DNS wire packets events", d[DC_EVENTS]);
+    p.gauge("dns_deep_sampled_packets", "Total DNS wire packets that were sampled for deep inspection", d[DC_SAMPLES]);
+    if (g & PV_DNS2_COUNTERS)
+        p.gauge("dns_filtered_packets", "Total DNS wire packets seen that did not match the configured filter(s) (if any)", d[DC_FILTERED]);
+    static const char *dirs[3] = {"in", "out", "unknown"};
+    auto vmax = [](const auto &v) { return v.empty() ? 0 : *std::max_element(v.begin(), v.end()); };
+    const PromLabels base = p.add;
+    for (uint32_t x = 0; x < 3; x++) {
+        const uint64_t *c2 = &b.sum[PV_OFF_DNS2 + x * PV_DNS2_CTRS];
+        if (!c2[D2_SEEN]) continue;
+        auto tops = [&](uint32_t metric) { return tops_of(b, TMH_V2_DNS + 4 * metric + x); };
+        p.add = base;
+        p.add["direction"] = dirs[x];
+        if (g & PV_DNS2_COUNTERS) {
+            p.gauge("dns_xacts", "Total DNS transactions (query/reply pairs)", c2[D2_XACTS]);
+            p.gauge("dns_udp_xacts", "Total DNS transactions (query/reply pairs) received over UDP", c2[D2_UDP]);
+            p.gauge("dns_tcp_xacts", "Total DNS transactions (query/reply pairs) received over TCP", c2[D2_TCP]);
+            p.gauge("dns_dot_xacts", "Total DNS transactions (query/reply pairs) received over DNS over TLS", 0);
+            p.gauge("dns_doh_xacts", "Total DNS transactions (query/reply pairs) received over DNS over HTTPS", 0);
+            p.gauge("dns_dnscrypt_udp_xacts", "Total DNS transactions (query/reply pairs) received over DNSCrypt over UDP", 0);
+            p.gauge("dns_dnscrypt_tcp_xacts", "Total DNS transactions (query/reply pairs) received over DNSCrypt over TCP", 0);
+            p.gauge("dns_doq_xacts", "Total DNS transactions (query/reply pairs) received over DNS over QUIC", 0);
+            p.gauge("dns_ipv4_xacts", "Total DNS transactions (query/reply pairs) received over IPv4", c2[D2_V4]);
+            p.gauge("dns_ipv6_xacts", "Total DNS transactions (query/reply pairs) received over IPv6", c2[D2_V6]);
+            p.gauge("dns_nxdomain_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code NXDOMAIN", c2[D2_NX]);
+            p.gauge("dns_ecs_xacts", "Total DNS transactions (query/reply pairs) with the EDNS Client Subnet option set", 0);
+            p.gauge("dns_refused_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code REFUSED", c2[D2_REFUSED]);
+            p.gauge("dns_srvfail_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code SRVFAIL", c2[D2_SRVFAIL]);
+            p.gauge("dns_noerror_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code NOERROR", c2[D2_NOERROR]);
+            p.gauge("dns_nodata_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code NOERROR but with an empty answers section", c2[D2_NODATA]);
+            p.gauge("dns_authenticated_data_xacts", "Total DNS transactions (query/reply pairs) with the AD flag set in the response", c2[D2_AD]);
+            p.gauge("dns_authoritative_answer_xacts", "Total DNS transactions (query/reply pairs) with the AA flag set in the response", c2[D2_AA]);
+            p.gauge("dns_checking_disabled_xacts", "Total DNS transactions (query/reply pairs) with the CD flag set in the query", c2[D2_CD]);
+            p.gauge("dns_timeout_queries", "Total number of DNS queries that timed out", c2[D2_TIMEOUT]);
+            p.gauge("dns_orphan_responses", "Total number of DNS responses that do not have a corresponding query", c2[D2_ORPHAN]);
+        }
+        if (g & PV_DNS2_CARDINALITY)
+            p.gauge("dns_cardinality_qname", "Cardinality of unique QNAMES, both ingress and egress",
+                    lround(cpc_estimate(&b.cpc[(CPC_QNAME2 + x) * PV_CPC_COUPONS], b.merged)));
+        if (g & PV_DNS2_TOP_PORTS)
+            p.topn("dns_top_udp_ports_xacts", "port", "Top UDP source port on the query side of a transaction",
+                   dense_tops(&b.sum[PV_OFF_PORT2 + x * PV_PORT_BINS], PV_PORT_BINS, 0), topn, pct);
+        if (g & PV_DNS2_TOP_RCODES) {
+            p.topn("dns_top_nxdomain_xacts", "qname", "Top QNAMES with result code NXDOMAIN", tops(TM_NX), topn, pct);
+            p.topn("dns_top_refused_xacts", "qname", "Top QNAMES with result code REFUSED", tops(TM_REFUSED), topn, pct);
+            p.topn("dns_top_srvfail_xacts", "qname", "Top QNAMES with result code SRVFAIL", tops(TM_SRVFAIL), topn, pct);
+            p.topn("dns_top_nodata_xacts", "qname", "Top QNAMES with result code NOERROR and empty answer section", tops(TM_NODATA), topn, pct);
+            p.topn("dns_top_noerror_xacts", "qname", "Top QNAMES with result code NOERROR", tops(TM_NOERROR), topn, pct);
+            p.topn("dns_top_rcode_xacts", "rcode", "Top result codes", dense_tops(&b.sum[PV_OFF_RCODE2 + x * PV_RCODE_BINS], PV_RCODE_BINS, 2),
+                   topn, pct);
+        }
+        if (g & PV_DNS2_TOP_QNAMES) {
+            p.topn("dns_top_qname2_xacts", "qname", "Top QNAMES, aggregated at a depth of two labels", tops(TM_QNAME2), topn, pct);
+            p.topn("dns_top_qname3_xacts", "qname", "Top QNAMES, aggregated at a depth of three labels", tops(TM_QNAME3), topn, pct);
+        }
+        if (g & PV_DNS2_TOP_SIZE) {
+            p.topn("dns_top_response_bytes", "qname", "Top QNAMES by response volume in bytes", tops(TM_SIZED), topn, pct);
+            const auto &r = b.ratio2[x];
+            if (!r.empty())
+                p.template summary<double>("dns_response_query_size_ratio", "Quantiles of ratio of packet sizes in a DNS transaction (reply/query)",
+                                           quantiles(r), vmax(r), r.size());
+        }
+        if (g & PV_DNS2_TOP_QTYPES)
+            p.topn("dns_top_qtype_xacts", "qtype", "Top query types", dense_tops(&b.sum[PV_OFF_QTYPE2 + x * PV_QTYPE_BINS], PV_QTYPE_BINS, 1),
+                   topn, pct);
+        if (g & PV_DNS2_XACT_TIMES) {
+            const auto &t = b.time2[x];
+            if (!t.empty())
+                p.template summary<uint64_t>("dns_xact_time_us", "Quantiles of transaction timing (query/reply pairs) in microseconds",
+                                             quantiles(t), vmax(t), t.size());
+            p.histogram("dns_xact_histogram_us", "Histogram of transaction timing (query/reply pairs) in microseconds", t);
+            p.topn("dns_top_slow_xacts", "qname", "Top QNAMES in transactions where host is the server and transaction speed is slower than p90",
+                   tops(TM_SLOW_OUT), topn, pct);
+        }
+    }
+    p.add = base;
+}
+
 // KLL inclusive rank rule on exact data
 uint64_t quantile_at(std::vector<uint64_t> v, double r)
 {
@@ -1871,6 +2013,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     c->nn_cap = (uint32_t)std::min<uint64_t>(1ull << c->tcap_log2, 1ull << 22);
     if (c->cfg.max_records == 0) c->cfg.max_records = 1 << 20;
     c->max_records = c->cfg.max_records;
+    c->ovf_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2 * c->max_records, 1u << 16), 1ull << 28);
     // deep_sample_rate (AbstractMetricsManager::configure, src/AbstractMetricsManager.h:357-365: > 100 -> 100, < 1 -> 1)
     c->sample_rate = c->cfg.deep_sample_rate == 0 ? 100u : std::max(1u, std::min(c->cfg.deep_sample_rate, 100u));
     if (c->sample_rate < 100 && (c->cfg.net_filter_all || c->net2_groups || c->dns2_groups)) {
@@ -1896,13 +2039,12 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     uint64_t mr = c->max_records;
     hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
     {
-        int nb = 0;
-        // the persistent grid is sized for the lean register-window pass (the common batch);
-        // PV_NET_WGCU overrides it for A/B runs
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_net_kernel_reg), PV_NET_THREADS, 0) ==
-                hipSuccess && nb > 0)
-            c->wg_per_cu = nb;
+        // the grid's partition of a batch (DNS pass, combine, merge and the general Net passes):
+        // three workgroups per CU; the register-window Net pass walks it with one workgroup per
+        // CU (reg_wg_per_cu). PV_NET_WGCU / PV_REG_WGCU override them for A/B runs
+        c->wg_per_cu = 3;
         if (const char *w = getenv("PV_NET_WGCU")) c->wg_per_cu = std::max(1, atoi(w));
+        if (const char *w = getenv("PV_REG_WGCU")) c->reg_wg_per_cu = std::max(1, atoi(w));
     }
     // event / DNS work-list regions: main workgroups own wt_per_block * 64 slots each (the
     // last may overhang the batch by < wt_per_block tiles), boundary workgroups 64 each
@@ -1949,6 +2091,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMemsetAsync(c->d_tab_live, 0, PV_TABLES * 4, c->stream)) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_tab_live, PV_TABLES * 4, hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_theta, ((size_t)1 << c->reg_log2) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_ovf, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
+        !hip_ok(e = hipMalloc(&c->d_ovf2, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
+        !hip_ok(e = hipMalloc(&c->d_ovf_cnt, 8)) || !hip_ok(e = hipMemsetAsync(c->d_ovf_cnt, 0, 8, c->stream)) ||
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
         !hip_ok(e = hipMalloc(&c->d_iplog, (size_t)(mr + 64) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_trash, (size_t)PV_TRASH_WAVES * 2048)) ||
@@ -1991,7 +2136,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
-                    c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop};
+                    c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_ovf_cnt};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
     for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
@@ -2445,13 +2590,47 @@ uint32_t tcp_pass(pv_ctx *c, const PvParams &P, uint64_t a, uint64_t b, hipStrea
 // name arena of a purged table is compacted once its fullest partition is half used. The
 // live counts are the ones read back with the batch status (names added by the transaction
 // pass afterwards are counted at the next batch).
+int purge_table(pv_ctx *c, uint32_t t, hipStream_t st);
 int purge_tables(pv_ctx *c, hipStream_t st)
 {
     const uint64_t tcap = 1ull << c->tcap_log2;
-    const uint32_t nreg = 1u << c->reg_log2;
-    hipError_t e;
     for (uint32_t t = 0; t < PV_TABLES; t++) {
         if (c->h_tab_live[t] <= tcap / 2) continue;
+        if (int rc = purge_table(c, t, st)) return rc;
+    }
+    return 0;
+}
+
+// Updates full regions could not take in this batch (PvOvf list): purge each table they belong
+// to, as the sketch purges when its map is full, and insert them again, until none is left.
+// Each round at least halves the live entries of every region it purges, so the rounds end.
+int drain_overflow(pv_ctx *c, hipStream_t st)
+{
+    hipError_t e;
+    for (int round = 0;; round++) {
+        uint32_t oc[2];
+        if (!hip_ok(e = hipMemcpyAsync(oc, c->d_ovf_cnt, 8, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "top-N overflow");
+        if (!oc[0]) return 0;
+        if (oc[0] > c->ovf_cap) return c->fail(PV_ECAPACITY, "top-N overflow list full (%u updates)", oc[0]);
+        if (round >= 64) return c->fail(PV_ECAPACITY, "top-N overflow not drained after %d purge rounds", round);
+        for (uint32_t t = 0; t < PV_TABLES; t++)
+            if ((oc[1] >> t) & 1)
+                if (int rc = purge_table(c, t, st)) return rc;
+        if (!hip_ok(e = hipMemcpyAsync(c->d_ovf2, c->d_ovf, (size_t)oc[0] * sizeof(PvOvf), hipMemcpyDeviceToDevice, st)) ||
+            !hip_ok(e = hipMemsetAsync(c->d_ovf_cnt, 0, 8, st)))
+            return c->hipfail(e, "top-N overflow");
+        hipLaunchKernelGGL(pv_topn_retry, dim3((oc[0] + 255) / 256), dim3(256), 0, st, (const PvParams *)c->d_params, c->d_ovf2, oc[0]);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_topn_retry");
+        c->ovf_rounds++;
+    }
+}
+
+int purge_table(pv_ctx *c, uint32_t t, hipStream_t st)
+{
+    const uint32_t nreg = 1u << c->reg_log2;
+    hipError_t e;
+    {
         c->h_tab_live[t] = 0; // stale until the next batch reads the device count back
         hipLaunchKernelGGL(pv_topn_purge, dim3(nreg), dim3(1024), 0, st, (const PvParams *)c->d_params, t, c->d_theta);
         std::vector<uint32_t> th(nreg);
@@ -2468,7 +2647,7 @@ int purge_tables(pv_ctx *c, hipStream_t st)
         const uint64_t pcap = c->arena_cap / PV_ARENA_PARTS;
         uint64_t most = 0;
         for (uint64_t u : tops) most = std::max(most, u);
-        if (most <= pcap / 2) continue;
+        if (most <= pcap / 2) return 0;
         if (!c->d_ctmp) {
             if (!hip_ok(e = hipMalloc(&c->d_ctmp, c->arena_cap)) || !hip_ok(e = hipMalloc(&c->d_ctop, PV_ARENA_PARTS * 8)))
                 return c->hipfail(e, "arena compaction scratch");
@@ -2848,6 +3027,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.mq_cnt = c->d_mq_cnt;
     P.reg_log2 = c->reg_log2;
     P.tab_live = c->d_tab_live;
+    P.ovf = c->d_ovf;
+    P.ovf_cnt = c->d_ovf_cnt;
+    P.ovf_cap = c->ovf_cap;
     P.cb_run = (uint64_t *)c->d_cb_h;
     P.tp_hands = c->d_status + ST_HANDS;
     P.tp_buf = c->d_tpbuf;
@@ -2874,13 +3056,15 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     {
         static const char *force = getenv("PV_NET_KERNEL");
         const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || (force && !strcmp(force, "general"));
-        const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && P.wt_per_block / 4 < 65535 &&
+        const uint32_t reg_grid = std::min<uint32_t>(grid, (uint32_t)(c->cus * c->reg_wg_per_cu));
+        const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
+        const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
                           !(force && !strcmp(force, "ns"));
         // lean: the register-window pass (pv_net_kernel_reg) unless PV_NET_KERNEL=fast asks for the LDS ring
         const bool ring = force && !strcmp(force, "fast");
         if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
         else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-        else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+        else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
         else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     }
     e = hipGetLastError();
@@ -2936,7 +3120,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     for (uint32_t k = 0; k <= P.n_shift; k++) c->net.clean[P.slot_of[k]] = false;
     if (status[ST_NDNS] || gt)
         for (uint32_t k = 0; k <= P.n_dshift; k++) c->dns.clean[P.dslot_of[k]] = false;
+    if (int rc = drain_overflow(c, st)) return rc;
     uint32_t flags = status[ST_FLAGS];
+    if (!hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
     if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
     if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
     if (getenv("PV_STAMPS")) {
@@ -2952,6 +3138,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         }
     }
     if (int rc = pair_stage(c, P, status[ST_NEV], status[ST_NRESP], n, st)) return rc;
+    if (int rc = drain_overflow(c, st)) return rc; // top_slow tables of the transaction stage
 
     // ---- window bookkeeping (host mirror of each manager's _period_shift)
     for (const Shift &sh : nsh) win_shift(c, c->net, sh.sec);
@@ -3426,6 +3613,9 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         P.arena_cap = c->arena_cap;
         P.flags = c->d_status + ST_FLAGS;
         P.tab_live = c->d_tab_live;
+        P.ovf = c->d_ovf;
+        P.ovf_cnt = c->d_ovf_cnt;
+        P.ovf_cap = c->ovf_cap;
         P.want_events = 0;
         launch_fill32(c, c->d_status + ST_FLAGS, 1, 0);
         flush_fills(c);
@@ -3438,7 +3628,9 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
             !hip_ok(e = hipMemcpyAsync(c->h_tab_live, c->d_tab_live, PV_TABLES * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "pv_dnstap_kernel");
-        const uint32_t flags = c->h_status[ST_FLAGS];
+        if (int rc = drain_overflow(c, st)) return rc;
+        uint32_t flags = 0;
+        if (!hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
         if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
         if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
         c->net.clean[P.slot_of[0]] = false;
@@ -4189,8 +4381,6 @@ int pv_window_prometheus(pv_ctx *c, uint32_t period, uint32_t handlers, const ch
     std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
-    if (c->net2_groups || c->dns2_groups)
-        return c->fail(PV_EUNSUPPORTED, "window_prometheus: the v2 handlers' Prometheus output is not built");
     if (period >= c->cfg.num_periods && period != PV_PERIOD_AUTO)
         return c->fail(PV_EINVAL, "invalid metrics period, specify [0, %u]", c->cfg.num_periods - 1);
     // StreamMetricsHandler::window_prometheus (src/StreamHandler.h:226-233): period 1 of a
@@ -4209,12 +4399,14 @@ int pv_window_prometheus(pv_ctx *c, uint32_t period, uint32_t handlers, const ch
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
         net_metrics(c, p, b);
+        if (c->net2_groups) net2_metrics(c, p, b);
     }
     if ((handlers & PV_HANDLER_DNS) && c->dns_groups) {
         if ((rc = window_slots(c, c->dns, per(c->dns), false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;
-        dns_metrics(c, p, b);
+        if (c->dns2_groups) dns2_metrics(c, p, b);
+        else dns_metrics(c, p, b);
     }
     *out = strdup(p.o.str().c_str());
     return 0;
@@ -4230,8 +4422,6 @@ int pv_window_opentelemetry(pv_ctx *c, uint32_t period, uint32_t handlers, const
     std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
-    if (c->net2_groups || c->dns2_groups)
-        return c->fail(PV_EUNSUPPORTED, "window_opentelemetry: the v2 handlers' OpenTelemetry output is not built");
     if (period >= c->cfg.num_periods && period != PV_PERIOD_AUTO)
         return c->fail(PV_EINVAL, "invalid metrics period, specify [0, %u]", c->cfg.num_periods - 1);
     // StreamMetricsHandler::window_opentelemetry (src/StreamHandler.h:240-247)
@@ -4259,13 +4449,15 @@ int pv_window_opentelemetry(pv_ctx *c, uint32_t period, uint32_t handlers, const
         if ((rc = load_bucket(c, slots, false, PART_NET, b))) return rc;
         stamps(c->net, slots[0]);
         net_metrics(c, p, b);
+        if (c->net2_groups) net2_metrics(c, p, b);
     }
     if ((handlers & PV_HANDLER_DNS) && c->dns_groups) {
         if ((rc = window_slots(c, c->dns, per(c->dns), false, slots))) return rc;
         HostBucket b;
         if ((rc = load_bucket(c, slots, false, PART_DNS, b))) return rc;
         stamps(c->dns, slots[0]);
-        dns_metrics(c, p, b);
+        if (c->dns2_groups) dns2_metrics(c, p, b);
+        else dns_metrics(c, p, b);
     }
     *out = (uint8_t *)malloc(p.out.s.size() ? p.out.s.size() : 1);
     if (!*out) return c->fail(PV_ECAPACITY, "window_opentelemetry: out of host memory");
@@ -4735,18 +4927,15 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
             if (r.dir == 0) a[1]++;
             else if (r.dir == 1) a[2]++;
         }
-        if (quant && r.dir < 2) {
-            const uint32_t kind = r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US;
-            c->slow_xv.push_back({st.ord, PvXValue{us, 0, kind}});
-            if (in_win(st.ord)) {
-                const uint32_t sg = slot | (c->gen[slot] << 8);
-                c->xvals_host.push_back(PvXValue{us, sg, kind});
-                if (qe.len && kept) {
-                    const double ratio = (double)r.len / (double)qe.len;
-                    uint64_t bits;
-                    memcpy(&bits, &ratio, 8);
-                    c->xvals_host.push_back(PvXValue{bits, sg, XV_RATIO});
-                }
+        if (quant && r.dir < 2) c->slow_xv.push_back({st.ord, PvXValue{us, 0, r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US}});
+        if (quant && in_win(st.ord)) {
+            const uint32_t sg = slot | (c->gen[slot] << 8);
+            if (r.dir < 2) c->xvals_host.push_back(PvXValue{us, sg, r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US});
+            if (qe.len && kept) {
+                const double ratio = (double)r.len / (double)qe.len;
+                uint64_t bits;
+                memcpy(&bits, &ratio, 8);
+                c->xvals_host.push_back(PvXValue{bits, sg, XV_RATIO});
             }
         }
         if (kept && r.dir < 2 && st.cand >= 0) {

@@ -335,6 +335,18 @@ __device__ __forceinline__ TPos tpos(PV_CREF(PvParams) P, uint32_t slot, uint64_
     return t;
 }
 
+// an update its full region could not take: kept for pv_topn_retry (after the host purges the
+// table); past the list's capacity, or without a record to name the key from, the batch fails
+__device__ __forceinline__ void table_overflow(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep,
+                                               bool named)
+{
+    if (!P.ovf || !named) { atomicOr(P.flags, PVF_TABLE_FULL); return; }
+    const uint32_t k = atomicAdd(P.ovf_cnt, 1u);
+    if (k >= P.ovf_cap) { atomicOr(P.flags, PVF_TABLE_FULL); return; }
+    P.ovf[k] = PvOvf{key, (uint32_t)w, rep, slot, 0};
+    atomicOr(P.ovf_cnt + 1, 1u << PV_TSLOT(slot, PV_KEY_METRIC(key)));
+}
+
 // Direct insert into the global table (boundary tiles, slow transactions, regions with
 // few updates in a batch): device-scope CAS / add, probing inside the key's region.
 __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep,
@@ -371,7 +383,7 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
             t.pos = (t.pos + 1) & t.rmask;
         }
     }
-    if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
+    if (!done) table_overflow(P, slot, key, w, rep, ns == nullptr);
     if (created >= 0) atomicAdd(&P.tab_live[PV_TSLOT(slot, metric)], 1u);
     if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns, key);
 }
@@ -1975,7 +1987,10 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
 // tools/stream_probe.hip measured the pattern alone at 5.8 TB/s (modes 7/8) against 4.2 TB/s
 // for the LDS-DMA ring's staging; the LDS keeps only the histogram and the DNS list counter.
 #ifndef PV_REG_MINW
-#define PV_REG_MINW 3 // waves per SIMD the register allocation must allow
+#define PV_REG_MINW 2 // waves per SIMD the register allocation must allow
+#endif
+#ifndef PV_REG_DEPTH
+#define PV_REG_DEPTH 2 // tiles whose windows are in registers (the parsed one + those in flight)
 #endif
 struct NetRegState {
     uint32_t hist[PV_HBINS];
@@ -2020,14 +2035,20 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
     }
     const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
-    const uint64_t wbeg = (uint64_t)blockIdx.x * P.wt_per_block;
-    const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
-    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + 3) / 4) : 0u;
-    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + 4ull * min(k, ntl - 1); };
-    auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
     uint64_t cd = 0, cl = 0; // fast lanes' packed counters (net_fast)
     NetCtr c;
     c.zero();
+    bool any = false;
+    // each workgroup walks the ranges of several grid workgroups (lb = blockIdx.x, + gridDim.x,
+    // ...): the DNS pass, combine and merge keep the grid's partition, while the Net pass runs
+    // one workgroup per CU (fewer, longer streams measured faster: tools/gpu_reg2.sh)
+    for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
+    const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
+    const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + 3) / 4) : 0u;
+    any |= ntl != 0;
+    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + 4ull * min(k, ntl - 1); };
+    auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
     // one tile from its windows W (off: this lane's record start)
     auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
         const uint64_t t = tile_of(k);
@@ -2035,17 +2056,31 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         const bool active = i < n;
         RecW rw;
         win_words(W, off & 3, rw);
+        if (PV_LEAN_LEVEL == 1) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int j = 0; j < 16; j++) x ^= rw.w[j];
+            cd += active ? x : 0u;
+            return;
+        }
         const FastRec f = fast_fields(rw, h);
         const bool fast = active & (f.ok != 0);
         const uint64_t slowm = __ballot(active & !fast);
         cd += fast ? 1ull << (f.dir * 16) : 0ull;
         cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
         uint32_t hv = fast ? f.caplen : PV_NOH;
+        if (PV_LEAN_LEVEL == 2) return;
+        if (PV_LEAN_LEVEL == 3) { hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane); return; }
         const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
         const bool ipok = fast & (f.dir != 2) & (ip != 0);
         uint64_t ek = tops && ipok ? ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
                                          ((uint64_t)f.dir << 32) | ip
                                    : 0ull;
+        if (PV_LEAN_LEVEL == 4) {
+            hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
+            if (tops && active) P.iplog[i] = ek;
+            return;
+        }
         if (card && !tops) {
             if (ipok) {
                 uint64_t h1, h2;
@@ -2115,6 +2150,34 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
             }
         }
     };
+#if PV_REG_DEPTH == 3
+    // three buffers: the windows of tiles k + 1 and k + 2 in flight while tile k is parsed
+    uint4 W0[5], W1[5], W2[5];
+    uint32_t o0 = 0, o1 = 0, o2 = 0;
+    if (ntl) {
+        o0 = off_of(0);
+        o1 = off_of(1);
+        o2 = off_of(2);
+        win_load(recs, o0, W0);
+        win_load(recs, o1, W1);
+    }
+    for (uint32_t k = 0; k < ntl; k += 3) {
+        const uint32_t oN = off_of(k + 3);
+        win_load(recs, o2, W2);              // tile k + 2
+        tile(k, o0, W0);
+        if (k + 1 >= ntl) break;
+        const uint32_t oN1 = off_of(k + 4);
+        win_load(recs, oN, W0);              // tile k + 3
+        o0 = oN;
+        tile(k + 1, o1, W1);
+        if (k + 2 >= ntl) break;
+        const uint32_t oN2 = off_of(k + 5);
+        win_load(recs, oN1, W1);             // tile k + 4
+        o1 = oN1;
+        tile(k + 2, o2, W2);
+        o2 = oN2;
+    }
+#else
     // software pipeline, unrolled by two: while tile k is parsed from one buffer the windows of
     // tile k + 1 land in the other; tile k + 2's offsets are loaded ahead of tile k + 1's windows
     uint4 WA[5], WB[5];
@@ -2139,6 +2202,17 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         tile(k + 1, oB, WB);
         oB = oN2;
     }
+#endif
+    // this range's DNS list: its count, and the slot counter reset for the next range
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        P.mq_cnt[lb] = 0;
+        P.dq_cnt[lb] = S.nd;
+        if (S.nd) atomicAdd(P.n_dns, S.nd);
+        S.nd = 0;
+    }
+    __syncthreads();
+    }
     {
         const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
         const uint32_t nf = fin + fout + funk;
@@ -2149,15 +2223,10 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     }
     NetK K;
     K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
-    if (ntl) knet_flush(K, slot, c);
+    if (any) knet_flush(K, slot, c);
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
         if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
-    if (threadIdx.x == 0) {
-        P.mq_cnt[blockIdx.x] = 0;
-        P.dq_cnt[blockIdx.x] = S.nd;
-        if (S.nd) atomicAdd(P.n_dns, S.nd);
-    }
 }
 
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(const PvParams *__restrict__ Pp) { net_pass<true>(Pp); }
@@ -2781,7 +2850,15 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                     pos = (pos + 1) & (rs - 1);
                 }
             }
-            if (!done) atomicOr(P.flags, PVF_TABLE_FULL);
+            if (!done) {
+                const uint32_t w = (uint32_t)e1, rep = (uint32_t)(e1 >> 32);
+                if (w & PV_W_IP4) {
+                    if ((w >> 29) & 1) cpc_min(P, s, ((w >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
+                    table_overflow(P, s, key, w & PV_W_CNT, rep, true);
+                } else {
+                    table_overflow(P, s, key, w, rep, true);
+                }
+            }
         });
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
@@ -2804,6 +2881,17 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         }
         __syncthreads();
     }
+}
+
+// The updates full regions could not take in this batch, once the host has purged their tables:
+// inserted again (those that still find no room go back to the overflow list for another round)
+extern "C" __global__ void pv_topn_retry(const PvParams *__restrict__ Pp, const PvOvf *__restrict__ src, uint32_t n)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const PvOvf e = src[j];
+    global_add(P, e.slot, e.key, e.w, e.rep);
 }
 
 // Bounded top-N tables: the frequent-items sketch's purge (Apache DataSketches

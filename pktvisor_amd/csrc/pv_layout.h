@@ -316,6 +316,13 @@ struct PvDtEv {
 };
 static_assert(sizeof(PvDtEv) == 80, "PvDtEv is five 16-B words");
 
+// an update a full top-N region could not take inside a batch: kept for the retry after the
+// table's purge (pv_topn_retry), so a burst of distinct keys degrades like the sketch's purge
+struct PvOvf {
+    uint64_t key;
+    uint32_t w, rep, slot, pad;
+};
+
 struct PvParams {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
@@ -374,6 +381,9 @@ struct PvParams {
     PV_G uint64_t *cb_run;  // [run key][XCD][combine workgroup / 8]: the workgroup's run of that
                             // run key in its sorted list (start | count << 24 | tables << 48)
     PV_G uint32_t *tab_live; // per table: entries held (bounded by pv_topn_purge)
+    PV_G PvOvf *ovf;          // top-N updates a full region could not take (pv_topn_retry after a purge)
+    PV_G uint32_t *ovf_cnt;   // [0] entries, [1] tables they belong to (bit mask)
+    uint32_t ovf_cap;
     uint32_t net2_groups;   // Net v2 handler attached: PV_N2G_* group bits | PV_N2G_ON (0 = not attached)
     uint32_t dns2_groups;   // DNS v2 in place of v1: PV_D2G_* group bits | PV_N2G_ON (0 = DNS v1)
     PV_G uint64_t *tp_buf; // pv_topn_combine: entries its LDS table could not take (spill)

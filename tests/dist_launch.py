@@ -30,7 +30,9 @@ def run_ranks(world, args, timeout=240):
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    for p, o in zip(procs, outs):
-        if p.returncode != 0:
-            raise RuntimeError(f"rank failed ({p.returncode}):\n{o[-3000:]}")
+    failed = [(r, p.returncode, o) for r, (p, o) in enumerate(zip(procs, outs)) if p.returncode != 0]
+    if failed:
+        # the root cause first: a rank whose peers then saw their connection close
+        failed.sort(key=lambda f: "Connection closed by peer" in f[2])
+        raise RuntimeError("\n".join(f"rank {r} failed ({rc}):\n{o[-2500:]}" for r, rc, o in failed[:2]))
     return outs

@@ -65,7 +65,11 @@ def run_gpu(hdr, parts, beats, periods=5, **kw):
         h.set_end_tstamp(last[0], last[1] * 1000)
         out = {"5m": h.window_json(5, merged=True)}
         for k in range(5):
-            out[f"p{k}"] = h.window_json(k)
+            try:
+                out[f"p{k}"] = h.window_json(k)
+            except pa.PvError as e:  # fewer periods than the window holds
+                assert "not yet accumulated" in str(e)
+                break
         return out
     finally:
         h.close()
@@ -90,7 +94,7 @@ def test_heartbeat_rotates_both_windows(oracle):
     assert gpu["p1"]["dns"]["xact"]["counts"]["timed_out"] > 0
     # without the heartbeats the windows differ (the shifts then come from the packets alone)
     plain = run_gpu(hdr, [a, b, c], [[], [], []])
-    assert [plain[f"p{k}"]["packets"]["period"]["start_ts"] - t0 for k in range(5)] != starts
+    assert [plain[f"p{k}"]["packets"]["period"]["start_ts"] - t0 for k in range(5) if f"p{k}" in plain] != starts
 
 
 def test_heartbeat_before_next_shift_and_before_start(oracle):

@@ -53,3 +53,21 @@ def test_flood_large_table_exact(oracle, tmp_path):
     gpu = pa.pktvisor_reader(str(p), host_spec="10.0.0.0/8", periods=1)
     ref = oracle.run_bytes(pcap, host_spec="10.0.0.0/8", num_periods=1, window=1)
     assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("table_log2", [10, 12])
+def test_flood_one_batch_degrades(table_log2):
+    """the whole flood in ONE batch, far more distinct names than the table holds: full regions
+    hand their updates to the overflow list, the table is purged and they are inserted again
+    (drain_overflow) instead of the batch failing; the same bounds hold"""
+    pcap, heavy, total = synth.qname_flood_pcap(11, flood=60000)
+    w = _run(pcap, table_log2, 1 << 17)
+    dns = w["dns"]
+    top3 = dns["top_qname3"]
+    assert [e["name"] for e in top3] == sorted(heavy, key=lambda n: -heavy[n])[:10]
+    rounds_bound = 64  # drain_overflow's rounds, each adds one theta (1 here: singletons)
+    for e in top3:
+        t = heavy[e["name"]]
+        assert t <= e["estimate"] <= t + rounds_bound, (e, t)
+    assert dns["top_qname2"][0] == {"name": ".victim.example", "estimate": total}
+    assert dns["wire_packets"]["total"] == total
