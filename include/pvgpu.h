@@ -142,6 +142,13 @@ typedef struct pv_dns_filters {
                                    :648-657): the first query's match_public_suffix size is the
                                    aggregateDomain suffix size for top_qname2/3; ignored with
                                    only_qname_suffix, as in the reference */
+    uint32_t v2;                /* nonzero: the DNS v2 handler's filters (dns/v2/DnsStreamHandler.cpp:
+                                   61-170,484-609): rcode (exclude_noerror / only_rcode), answer_count,
+                                   DNSSEC and qtype test responses, qname and qname suffix test queries,
+                                   no input predicate; a filtered message still opens / ends its
+                                   transaction (process_filtered :1147-1174). only_queries /
+                                   only_responses / public_suffix_list / filter_all are not v2 keys */
+    uint32_t xact_dirs_disabled; /* v2 only_xact_directions: bit 0 in, 1 out, 2 unknown filtered */
 } pv_dns_filters;
 
 /* Replaces DnsStreamHandler::start's filter setup (dns/v1/DnsStreamHandler.cpp:60-150). Call

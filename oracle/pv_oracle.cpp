@@ -387,6 +387,9 @@ struct Config {
     std::vector<uint16_t> only_qtype;                   // "only_qtype" (:131-150)
     std::vector<std::string> only_qname;                // "only_qname" (:151-160), lower-case; predicate mode
     std::vector<std::string> only_qname_suffix;         // "only_qname_suffix" (:161-169), lower-case
+    // DNS v2 (dns/v2/DnsStreamHandler.cpp:61-170): the filter keys above read with v2's
+    // semantics (_filtering :484-609), plus only_xact_directions: bit 0 in, 1 out, 2 unknown off
+    uint32_t xact_dirs_disabled = 0;
 };
 
 // libs/visor_utils/utils.cpp:128-164
@@ -1093,6 +1096,7 @@ struct Engine {
         size_t query_size;
         bool cd;
         std::string ecs;
+        bool filtered = false; // DnsTransaction::filtered (dns/v2/DnsStreamHandler.h:55-60)
     };
     std::unordered_map<XactKey, Xact2, XactKeyHash> xacts2[3];
     float per90_2[3] = {0.0f, 0.0f, 0.0f};
@@ -1270,6 +1274,10 @@ struct Engine {
         bool qr = (h[2] & 0x80) != 0;
         uint8_t rcode = h[3] & 0x0f;
         uint16_t ancount = rd16be(h + 6);
+        if (cfg.dns2_groups) { // DNS v2: its own filters, no input predicate
+            dns2_event(p, m, hm, hdr_buf, qr, rcode, ancount, txid);
+            return;
+        }
 
         // only_rcode installs a UDP predicate in the input proxy (dns/v1 ...cpp:485-508): a
         // non-response or a response whose rcode is not listed never reaches the handler
@@ -1323,10 +1331,6 @@ struct Engine {
             return;
         }
 
-        if (cfg.dns2_groups) {
-            dns2_event(p, m, hm.d, qr, rcode, ancount, txid, suffix_size);
-            return;
-        }
         // DnsStreamHandler::_configs (:648-657): public_suffix_list sets suffix_size from the
         // first query's lower-case name, only while only_qname_suffix is off
         if (cfg.psl && cfg.only_qname_suffix.empty()) {
@@ -1424,14 +1428,87 @@ struct Engine {
     // DnsMetricsManager::process_dns_layer, v2 (dns/v2/DnsStreamHandler.cpp:1100-1145): every
     // message is an event; a query opens a transaction in its direction's map (toHost query:
     // "in"), a response looks in the swapped direction's map and accounts the transaction
-    void dns2_event(const DnsEv &p, const DnsMsg &m, const uint8_t *h, bool qr, uint8_t rcode, uint16_t ancount,
-                    uint16_t txid, size_t suffix_size)
+    // DnsStreamHandler::_filtering, v2 (dns/v2/DnsStreamHandler.cpp:484-609): the direction
+    // filters for both kinds, rcode / answer_count / DNSSEC / qtype on responses, qname and
+    // qname suffix on queries (the suffix size it sets is consumed by the query's own
+    // process_dns_layer, which does not use it: a response always aggregates with 0)
+    bool dns2_filtering(const DnsEv &p, const DnsMsg &m, const uint8_t *hdr12, bool qr, uint8_t rcode, uint16_t ancount)
     {
+        const uint32_t dis = cfg.xact_dirs_disabled;
+        if ((dis & 4) && p.dir == DIR_UNKNOWN) return true;
+        auto parsed = [&]() { return m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{hdr12, m.len}); };
+        if (qr) {
+            if ((dis & 1) && p.dir == DIR_FROM_HOST) return true;
+            if ((dis & 2) && p.dir == DIR_TO_HOST) return true;
+            if (cfg.exclude_noerror) { if (rcode == 0) return true; }
+            else if (cfg.only_rcode_mask && !((cfg.only_rcode_mask >> rcode) & 1)) return true;
+            if (cfg.has_answer_count && ancount != cfg.answer_count) return true;
+            if (cfg.only_dnssec && (!ancount || !dnssec_answer(m))) return true;
+            if (!cfg.only_qtype.empty()) {
+                DnsParse fr = parsed();
+                if (!fr.ok || !fr.has_query) return true;
+                if (std::find(cfg.only_qtype.begin(), cfg.only_qtype.end(), fr.qtype) == cfg.only_qtype.end()) return true;
+            }
+        } else {
+            if ((dis & 1) && p.dir == DIR_TO_HOST) return true;
+            if ((dis & 2) && p.dir == DIR_FROM_HOST) return true;
+            if (!cfg.only_qname.empty()) {
+                DnsParse qp = parsed();
+                if (!qp.ok || !qp.has_query) return true;
+                if (std::find(cfg.only_qname.begin(), cfg.only_qname.end(), lower(qp.name)) == cfg.only_qname.end()) return true;
+            }
+            if (!cfg.only_qname_suffix.empty()) {
+                DnsParse sp = parsed();
+                if (!sp.ok || !sp.has_query) return true;
+                const std::string nl = lower(sp.name);
+                bool hit = false;
+                for (const auto &sfx : cfg.only_qname_suffix)
+                    if (nl.size() >= sfx.size() && nl.compare(nl.size() - sfx.size(), sfx.size(), sfx) == 0) { hit = true; break; }
+                if (!hit) return true;
+            }
+        }
+        return false;
+    }
+
+    void dns2_event(const DnsEv &p, const DnsMsg &m, const DnsMsg &hm, const uint8_t *hdr12, bool qr, uint8_t rcode,
+                    uint16_t ancount, uint16_t txid)
+    {
+        const uint8_t *h = hm.d;
+        const size_t suffix_size = 0;
+        const bool filt = dns2_filtering(p, m, hdr12, qr, rcode, ancount);
         if (dns2.maybe_shift(p.ts)) on_dns2_period_shift(p.ts);
         dns2.new_event(true);
         Dns2Bucket &b = dns2.live();
         const uint32_t g = cfg.dns2_groups;
         const XactKey k{p.flowkey, txid};
+        auto elapsed = [&](const Xact2 &q) {
+            TS d;
+            d.sec = p.ts.sec > q.start.sec ? p.ts.sec - q.start.sec : q.start.sec - p.ts.sec;
+            d.nsec = p.ts.nsec - q.start.nsec;
+            if (d.nsec < 0) { d.sec--; d.nsec += 1000000000L; }
+            return d;
+        };
+        auto timed_out = [&](const TS &d) { return d.sec > (int64_t)ttl_s || (d.sec == (int64_t)ttl_s && (d.nsec / 1.0e6) >= ttl_ms); };
+        if (filt) {
+            // DnsMetricsManager::process_filtered, v2 (:1147-1174)
+            if (qr) {
+                const int xd = p.dir == DIR_TO_HOST ? 1 : (p.dir == DIR_FROM_HOST ? 0 : 2);
+                auto it = xacts2[xd].find(k);
+                b.dir[xd].seen = true;
+                if (it != xacts2[xd].end()) {
+                    const Xact2 q = it->second;
+                    xacts2[xd].erase(it);
+                    if (!timed_out(elapsed(q)) && !q.filtered && (g & D2G_COUNTERS)) b.filtered++;
+                }
+            } else {
+                const int xd = p.dir == DIR_TO_HOST ? 0 : (p.dir == DIR_FROM_HOST ? 1 : 2);
+                Xact2 q{p.ts, 0, false, std::string()};
+                q.filtered = true;
+                xacts2[xd][k] = q;
+            }
+            if (g & D2G_COUNTERS) b.filtered++;
+            return;
+        }
         if (qr) {
             const int xd = p.dir == DIR_TO_HOST ? 1 : (p.dir == DIR_FROM_HOST ? 0 : 2);
             Dns2Dir &x = b.dir[xd];
@@ -1440,11 +1517,9 @@ struct Engine {
             if (it == xacts2[xd].end()) { x.orphan++; return; }
             Xact2 q = it->second;
             xacts2[xd].erase(it);
-            TS d;
-            d.sec = p.ts.sec > q.start.sec ? p.ts.sec - q.start.sec : q.start.sec - p.ts.sec;
-            d.nsec = p.ts.nsec - q.start.nsec;
-            if (d.nsec < 0) { d.sec--; d.nsec += 1000000000L; }
-            if (d.sec > (int64_t)ttl_s || (d.sec == (int64_t)ttl_s && (d.nsec / 1.0e6) >= ttl_ms)) { x.timeout++; return; }
+            const TS d = elapsed(q);
+            if (q.filtered) { if (g & D2G_COUNTERS) b.filtered++; return; } // the query was filtered out
+            if (timed_out(d)) { x.timeout++; return; }
             // DnsMetricsBucket::new_dns_transaction, v2 (:925-1089)
             const uint64_t us = (uint64_t)((d.sec * 1000000000LL) + d.nsec) / 1000;
             if (g & D2G_COUNTERS) {
@@ -2263,6 +2338,7 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "only_responses") c.only_responses = atoi(v.c_str()) != 0;
         else if (k == "only_dnssec_response") c.only_dnssec = atoi(v.c_str()) != 0;
         else if (k == "public_suffix_list") c.psl = atoi(v.c_str()) != 0;
+        else if (k == "xact_dirs_disabled") c.xact_dirs_disabled = (uint32_t)atoi(v.c_str());
         else if (k == "single") c.single = atoi(v.c_str());
         else if (k == "heartbeats") {
             size_t q = 0;

@@ -57,7 +57,8 @@ class pv_dns_filters(ctypes.Structure):
                 ("n_qtypes", ctypes.c_uint32), ("qtypes", ctypes.c_uint16 * 16), ("n_qnames", ctypes.c_uint32),
                 ("qnames", ctypes.POINTER(ctypes.c_char_p)), ("n_qname_suffixes", ctypes.c_uint32),
                 ("qname_suffixes", ctypes.POINTER(ctypes.c_char_p)), ("only_dnssec_response", ctypes.c_uint32),
-                ("filter_all", ctypes.c_uint32), ("public_suffix_list", ctypes.c_uint32)]
+                ("filter_all", ctypes.c_uint32), ("public_suffix_list", ctypes.c_uint32), ("v2", ctypes.c_uint32),
+                ("xact_dirs_disabled", ctypes.c_uint32)]
 
 
 from pktvisor_amd.config import ConfigException as ConfigError  # noqa: E402  (the reference's texts)
@@ -74,7 +75,7 @@ def _dns_code(kind: int, name: str):
     return int(v.value) if load_library().pv_dns_code(kind, str(name).encode(), ctypes.byref(v)) == 0 else None
 
 
-def dns_filter_config(cfg: dict) -> dict:
+def dns_filter_config(cfg: dict, v2: bool = False) -> dict:
     """DnsStreamHandler::start's filter setup (src/handlers/dns/v1/DnsStreamHandler.cpp:60-150):
     typed values in, the pv_dns_filters fields out; ConfigError with the reference's text."""
     out = dict(exclude_noerror=0, only_rcode_mask=0, answer_count=-1, only_queries=0, only_responses=0, only_qtype=[],
@@ -136,7 +137,7 @@ def dns_filter_config(cfg: dict) -> dict:
         out["only_qtype"].append(c)
     # only_qname (:151-160): lower-cased; an input predicate, as only_rcode is
     out["only_qname"] = [str(q).lower() for q in cfg.get("only_qname", [])]
-    if out["only_qname"] and out["only_rcode_mask"]:
+    if out["only_qname"] and out["only_rcode_mask"] and not v2:
         raise ConfigError("DnsStreamHandler: only_qname and only_rcode both install an input predicate: use one")
     if len(out["only_qname"]) > 8 or any(not q or len(q) > 255 for q in out["only_qname"]):
         raise ConfigError("DnsStreamHandler: only_qname: 1..8 names of 1..255 characters")
@@ -446,6 +447,7 @@ class PvHandlers:
                 raise PvError("dns_config and dns2_config are exclusive: one DNS handler version")
             d2 = pvcfg.dns2_start(dict(dns2_config))
             dns2_groups = d2["groups"]
+            filt = d2["filters"]
             if d2["xact_ttl_ms"] is not None:
                 xact_ttl_ms = d2["xact_ttl_ms"]
         if net_config is not None or dns_config is not None or net2_config is not None or dns2_config is not None:
@@ -457,7 +459,8 @@ class PvHandlers:
             topn_percentile_threshold = win.get("topn_percentile_threshold", topn_percentile_threshold)
             n, d = pvcfg.net_start(ncfg), pvcfg.dns_start(dcfg)
             net_groups, dns_groups, net_filter_all = n["groups"], d["groups"], int(n["filter_all"])
-            filt = d["filters"]
+            if dns2_config is None:
+                filt = d["filters"]
             self.dnstap_mask = d["dnstap_mask"]
             if d["xact_ttl_ms"] is not None and dns2_config is None:
                 xact_ttl_ms = d["xact_ttl_ms"]
@@ -481,6 +484,8 @@ class PvHandlers:
             f.only_dnssec_response = filt["only_dnssec_response"]
             f.filter_all = filt.get("filter_all", 0)
             f.public_suffix_list = filt.get("public_suffix_list", 0)
+            f.v2 = filt.get("v2", 0)
+            f.xact_dirs_disabled = filt.get("xact_dirs_disabled", 0)
             if filt["only_qname"]:
                 self._qnames = (ctypes.c_char_p * len(filt["only_qname"]))(*[q.encode() for q in filt["only_qname"]])
                 f.n_qnames = len(filt["only_qname"])

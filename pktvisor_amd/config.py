@@ -172,20 +172,37 @@ DNS2_GROUP_DEFS = {"cardinality": 1 << 0, "counters": 1 << 1, "quantiles": 1 << 
                    "top_qtypes": 1 << 4, "top_rcodes": 1 << 5, "top_size": 1 << 6, "top_qnames": 1 << 7,
                    "top_ports": 1 << 8, "xact_times": 1 << 9}
 DNS2_DEFAULT_GROUPS = ("cardinality", "counters", "quantiles", "top_qnames", "top_rcodes", "top_qtypes")
-DNS2_CONFIG_DEFS = ("exclude_noerror", "only_rcode", "only_dnssec_response", "answer_count", "only_qtype", "only_qname",
-                    "only_qname_suffix", "geoloc_notfound", "asn_notfound", "dnstap_msg_type", "public_suffix_list",
-                    "recorded_stream", "xact_ttl_secs", "xact_ttl_ms")
+DNS2_CONFIG_DEFS = ("exclude_noerror", "only_rcode", "only_dnssec_response", "only_xact_directions", "answer_count",
+                    "only_qtype", "only_qname", "only_qname_suffix", "geoloc_notfound", "asn_notfound", "dnstap_msg_type",
+                    "public_suffix_list", "recorded_stream", "xact_ttl_secs", "xact_ttl_ms")
+DNS2_FILTER_KEYS = ("exclude_noerror", "only_rcode", "only_dnssec_response", "answer_count", "only_qtype", "only_qname",
+                    "only_qname_suffix")
 
 
 def dns2_start(cfg: dict) -> dict:
     """DnsStreamHandler v2 start (src/handlers/dns/v2/DnsStreamHandler.cpp:43-236) up to the
-    signal wiring: {"groups": bits | GROUPS_SET, "xact_ttl_ms": int|None}. The v2 filters and
-    top_ecs are not built for the GPU handler and are refused."""
+    signal wiring: {"groups": bits | GROUPS_SET, "filters": pv_dns_filters fields (v2) or None,
+    "xact_ttl_ms": int|None}. The geo / ASN filters (no MaxMind database), dnstap_msg_type (no
+    v2 dnstap path), public_suffix_list and top_ecs are not built for the GPU v2 handler."""
+    from pktvisor_amd import dns_filter_config
     validate_configs(cfg, DNS2_CONFIG_DEFS)
     groups = process_groups(cfg, DNS2_GROUP_DEFS, DNS2_DEFAULT_GROUPS)
-    for k in DNS2_CONFIG_DEFS:
-        if k in cfg and k not in ("recorded_stream", "xact_ttl_secs", "xact_ttl_ms"):
+    for k in ("geoloc_notfound", "asn_notfound", "dnstap_msg_type", "public_suffix_list"):
+        if k in cfg:
             raise ConfigException(f"{k} is not supported by the GPU DNS v2 handler")
+    filters = None
+    if any(k in cfg for k in DNS2_FILTER_KEYS) or "only_xact_directions" in cfg:
+        filters = dns_filter_config({k: cfg[k] for k in DNS2_FILTER_KEYS if k in cfg}, v2=True)
+        filters["v2"] = 1
+        # only_xact_directions (:107-122): every direction filtered but the listed ones
+        if "only_xact_directions" in cfg:
+            dis = 7
+            for d in _string_list(cfg, "only_xact_directions"):
+                if d not in ("in", "out", "unknown"):
+                    raise ConfigException("DnsStreamHandler: only_xact_directions filter contained an invalid/unsupported "
+                                          f"direction: {d}")
+                dis &= ~{"in": 1, "out": 2, "unknown": 4}[d]
+            filters["xact_dirs_disabled"] = dis
     if groups & DNS2_GROUP_DEFS["top_ecs"]:
         raise ConfigException("top_ecs is not supported by the GPU DNS v2 handler")
     ttl = None
@@ -193,7 +210,7 @@ def dns2_start(cfg: dict) -> dict:
         ttl = _uint(cfg, "xact_ttl_ms")
     elif "xact_ttl_secs" in cfg:
         ttl = _uint(cfg, "xact_ttl_secs") * 1000
-    return {"groups": groups | GROUPS_SET, "xact_ttl_ms": ttl}
+    return {"groups": groups | GROUPS_SET, "filters": filters, "xact_ttl_ms": ttl}
 
 
 def dns_start(cfg: dict) -> dict:

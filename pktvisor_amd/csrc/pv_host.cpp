@@ -1909,6 +1909,64 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
     if (c->records_seen) return c->fail(PV_EINVAL, "DNS filters must be set before the first batch");
     if (!f) { c->f_flags = c->f_rcode_mask = c->f_ancount = c->f_nq = c->f_nqn = c->f_nsx = 0; return 0; }
     uint32_t fl = 0;
+    if (f->v2) {
+        // DnsStreamHandler v2 start (dns/v2/DnsStreamHandler.cpp:61-170): one rcode mask for
+        // exclude_noerror (every rcode but NOERROR) or only_rcode, tested on responses only
+        if (!c->dns2_groups) return c->fail(PV_EINVAL, "v2 DNS filters without the DNS v2 handler");
+        if (f->only_queries || f->only_responses || f->filter_all || f->public_suffix_list)
+            return c->fail(PV_EUNSUPPORTED, "only_queries / only_responses / geo filters / public_suffix_list are not DNS v2 filters here");
+        fl |= PVDF_V2;
+        uint32_t mask = 0;
+        if (f->exclude_noerror) mask = 0xfffeu;
+        else if (f->only_rcode_mask) {
+            for (uint32_t r = 0; r < 32; r++)
+                if ((f->only_rcode_mask >> r) & 1 && (r > 15 || !rcode_names().count((uint16_t)r)))
+                    return c->fail(PV_EINVAL, "DnsStreamHandler: only_rcode filter contained an invalid/unsupported rcode");
+            mask = f->only_rcode_mask;
+        }
+        if (mask) fl |= PVDF2_RCODE;
+        if (f->answer_count >= 0) fl |= PVDF_ANSWER_COUNT;
+        if (f->only_dnssec_response) fl |= PVDF_ONLY_DNSSEC;
+        if (f->xact_dirs_disabled & 1) fl |= PVDF2_NOIN;
+        if (f->xact_dirs_disabled & 2) fl |= PVDF2_NOOUT;
+        if (f->xact_dirs_disabled & 4) fl |= PVDF2_NOUNK;
+        if (f->n_qtypes > PV_MAX_QTYPES) return c->fail(PV_EINVAL, "only_qtype: at most %d qtypes", PV_MAX_QTYPES);
+        for (uint32_t k = 0; k < f->n_qtypes; k++)
+            if (!qtype_names().count(f->qtypes[k]))
+                return c->fail(PV_EINVAL, "DnsStreamHandler: only_qtype filter contained an invalid/unsupported qtype: %u",
+                               (unsigned)f->qtypes[k]);
+        if (f->n_qtypes) fl |= PVDF_ONLY_QTYPE;
+        if (f->n_qnames > PV_MAX_QNAMES) return c->fail(PV_EINVAL, "only_qname: at most %d names", PV_MAX_QNAMES);
+        for (uint32_t k = 0; k < f->n_qnames; k++) {
+            const char *q = f->qnames ? f->qnames[k] : nullptr;
+            if (!q || !*q || strlen(q) > 255) return c->fail(PV_EINVAL, "only_qname: empty or over-long name");
+            c->f_qn[k] = pvname::name_fp(q, strlen(q));
+        }
+        c->f_nqn = f->n_qnames;
+        if (f->n_qnames) fl |= PVDF2_QNAME;
+        if (f->n_qname_suffixes > PV_MAX_SUFFIXES)
+            return c->fail(PV_EINVAL, "only_qname_suffix: at most %d suffixes", PV_MAX_SUFFIXES);
+        for (uint32_t k = 0; k < f->n_qname_suffixes; k++) {
+            const char *q = f->qname_suffixes ? f->qname_suffixes[k] : nullptr;
+            if (!q || strlen(q) > 254) return c->fail(PV_EINVAL, "only_qname_suffix: missing or over-long suffix");
+            c->f_sxl[k] = (uint32_t)strlen(q);
+            c->f_sxh[k] = pvname::name_ph(q, strlen(q));
+        }
+        c->f_nsx = f->n_qname_suffixes;
+        if (f->n_qname_suffixes) {
+            fl |= PVDF_ONLY_QSUFFIX;
+            hipError_t e;
+            if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
+                return c->hipfail(e, "only_qname_suffix record buffer");
+        }
+        if (c->sample_rate < 100) return c->fail(PV_EUNSUPPORTED, "DNS filters with deep_sample_rate below 100 are not built");
+        c->f_flags = fl;
+        c->f_rcode_mask = mask;
+        c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
+        c->f_nq = f->n_qtypes;
+        for (uint32_t k = 0; k < f->n_qtypes; k++) c->f_qt[k] = f->qtypes[k];
+        return 0;
+    }
     if (f->exclude_noerror) fl |= PVDF_EXCLUDE_NOERROR;
     else if (f->only_rcode_mask) {
         for (uint32_t r = 0; r < 32; r++)
@@ -2965,6 +3023,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.arena = c->d_arena;
     P.arena_top = c->d_arena_top;
     P.arena_cap = c->arena_cap;
+    P.tab_live = c->d_tab_live; // global_add counts the entries it creates
     P.events = c->d_events;
     P.ekeys = c->d_ekeys;
     P.blk_events = c->d_blk_events;
@@ -4131,6 +4190,7 @@ int pv_check_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
         P.arena = c->d_arena;
         P.arena_top = c->d_arena_top;
         P.arena_cap = c->arena_cap;
+        P.tab_live = c->d_tab_live; // global_add counts the entries it creates
         P.events = c->d_events;
         P.gbase = c->global_base + c->records_seen;
         P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
@@ -5115,6 +5175,7 @@ int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, u
         P.arena = c->d_arena;
         P.arena_top = c->d_arena_top;
         P.arena_cap = c->arena_cap;
+        P.tab_live = c->d_tab_live; // global_add counts the entries it creates
         P.flags = c->d_status + ST_FLAGS;
         PvXactParams X;
         memset(&X, 0, sizeof X);

@@ -296,7 +296,7 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     uint32_t n = nl > 0 ? st.n : 0;
     if (metric == TM_QNAME2 || metric == TM_QNAME3) {
         int q2, q3; uint64_t h2, h3;
-        const uint32_t sfx = (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) ? P.sfx_of[rep] : 0u;
+        const uint32_t sfx = ((P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) && !(P.f_flags & PVDF_V2)) ? P.sfx_of[rep] : 0u;
         if (nl > 0) agg_domain_r(R, m, len, st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx); else { q2 = 0; q3 = -1; }
         start = metric == TM_QNAME2 ? q2 : q3;
         if (start < 0) start = (int)n;
@@ -508,7 +508,7 @@ __device__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
     const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
     PV_FLUSH1(s, PV_OFF_DNS + DC_EVENTS, c.dev + c.dfilt, true) PV_FLUSH1(s, PV_OFF_DNS + DC_SAMPLES, c.dev + c.dfilt - c.dnd, true)
     PV_FLUSH1(s, PV_OFF_DNS + DC_TOTAL, c.dev, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_UDP, c.dev, dc)
-    if (P.f_flags) PV_FLUSH1(s, PV_OFF_DNS + DC_FILTERED, c.dfilt, dc)
+    if (P.f_flags) PV_FLUSH1(s, PV_OFF_DNS + DC_FILTERED, c.dfilt, dc || (P.dns2_groups & PV_D2G_COUNTERS))
     PV_FLUSH1(s, PV_OFF_DNS + DC_QUERIES, c.dq, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REPLIES, c.dr, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_V4, c.d4, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_V6, c.d6, dc)
     PV_FLUSH1(s, PV_OFF_DNS + DC_NX, c.dnx, dc) PV_FLUSH1(s, PV_OFF_DNS + DC_REFUSED, c.dref, dc)
@@ -679,7 +679,74 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     // a message's order in the span: record * 4 (+ sub for a TCP message), for the CPC
     // first-occurrence index and the transaction sort rank
     const uint32_t ordr = (TCP || TAP) ? dm.pad - P.ord_base : (i << 2);
-    if (P.f_flags && !TAP) {
+    // the message's transaction event (filtered: a DNS v2 event its filters rejected, which
+    // still opens or ends a transaction, DnsMetricsManager::process_filtered, dns/v2 ...cpp:1147-1174)
+    auto emit = [&](bool deep, bool filtered) {
+        if (!P.want_events || TAP) return;
+        // the workgroup's event region; LDS counter, order irrelevant (sorted by key, index)
+        const uint64_t e = ebase + atomicAdd(nev, 1u);
+        if (qr) atomicAdd(nresp, 1u);
+        PvXEvent ev;
+        ev.key = ((uint64_t)dm.fkey << 16) | txid;
+        ev.idx = TCP ? (i | PV_TCP_IDX) : i;
+        ev.len = dlen;
+        ev.sec = dm.sec;
+        ev.nsec = (int32_t)dm.nsec;
+        ev.qr = (uint8_t)qr;
+        ev.dir = dm.flags & 3;
+        ev.period = (uint8_t)period;
+        ev.pad = deep ? 0 : 4; // v1: bit 2 = the event is not deep
+        if (P.dns2_groups) {
+            // DNS v2: one transaction map per direction (DnsMetricsManager::_pair_manager); a
+            // response looks in the swapped direction's map (dns/v2 ...cpp:1100-1145). pad: the
+            // query's CD bit, the message's l3 (bit 1: IPv6), bit 2: filtered
+            const uint32_t dir = dm.flags & 3;
+            const uint32_t xd = dir == 2 ? 2u : (qr ? dir ^ 1u : dir);
+            ev.key |= (uint64_t)(xd + 1) << 48;
+            ev.pad = (uint8_t)(((w0 >> 28) & 1) | ((dm.flags & 4) ? 2u : 0u) | (filtered ? 4u : 0u));
+        }
+        P.events[e] = ev;
+        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
+    };
+    if ((P.f_flags & PVDF_V2) && !TAP) {
+        // DnsStreamHandler::_filtering, DNS v2 (dns/v2/DnsStreamHandler.cpp:484-609): the
+        // direction filters for both, the rcode / answer / DNSSEC / qtype filters on responses,
+        // the qname filters on queries; no input predicate (every DNS packet is an event)
+        const uint32_t dir = dm.flags & 3; // 0 toHost, 1 fromHost, 2 unknown
+        bool filt = (P.f_flags & PVDF2_NOUNK) && dir == 2;
+        if (!filt && qr) {
+            filt = ((P.f_flags & PVDF2_NOIN) && dir == 1) || ((P.f_flags & PVDF2_NOOUT) && dir == 0) ||
+                   ((P.f_flags & PVDF2_RCODE) && !((P.f_rcode_mask >> rcode) & 1)) ||
+                   ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
+                   ((P.f_flags & PVDF_ONLY_DNSSEC) && (!ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar)));
+            if (!filt && (P.f_flags & PVDF_ONLY_QTYPE)) {
+                DnsInfo fd;
+                dns_parse(R, m, dlen, qd, ancount, ns, ar, fd);
+                bool hit = false;
+                for (uint32_t k = 0; k < P.f_nq; k++) hit |= fd.qtype == P.f_qt[k];
+                filt = !fd.ok || !fd.has_query || !hit;
+            }
+        } else if (!filt) {
+            filt = ((P.f_flags & PVDF2_NOIN) && dir == 0) || ((P.f_flags & PVDF2_NOOUT) && dir == 1);
+            if (!filt && (P.f_flags & PVDF2_QNAME)) filt = !dns_qname_listed(P, R, m, dlen, w1, w2);
+            if constexpr (SFX) {
+                if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) filt = P.sfx_of[i] == 0xffu;
+            }
+        }
+        if (filt) {
+            // process_filtered: an event (sampled at rate 100), `filtered`, and the transaction
+            if (upd) {
+                if (own) c.dfilt++;
+                else {
+                    sum_add(P, slot, PV_OFF_DNS + DC_EVENTS, 1);
+                    sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
+                    if (P.dns2_groups & PV_D2G_COUNTERS) sum_add(P, slot, PV_OFF_DNS + DC_FILTERED, 1);
+                }
+            }
+            emit(true, true);
+            return;
+        }
+    } else if (P.f_flags && !TAP) {
         // a TCP message takes no input predicate: _filtering applies only_rcode and only_qname
         // to it as ordinary filters (_predicate_filter_type stays FiltersMAX, :546-551,593-602)
         if (!TCP && (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
@@ -832,32 +899,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         }
         }
     }
-    if (P.want_events && !TAP) {
-        // the workgroup's event region; LDS counter, order irrelevant (sorted by key, index)
-        const uint64_t e = ebase + atomicAdd(nev, 1u);
-        if (qr) atomicAdd(nresp, 1u);
-        PvXEvent ev;
-        ev.key = ((uint64_t)dm.fkey << 16) | txid;
-        ev.idx = TCP ? (i | PV_TCP_IDX) : i;
-        ev.len = dlen;
-        ev.sec = dm.sec;
-        ev.nsec = (int32_t)dm.nsec;
-        ev.qr = (uint8_t)qr;
-        ev.dir = dm.flags & 3;
-        ev.period = (uint8_t)period;
-        ev.pad = deep ? 0 : 4; // v1: bit 2 = the event is not deep
-        if (P.dns2_groups) {
-            // DNS v2: one transaction map per direction (DnsMetricsManager::_pair_manager); a
-            // response looks in the swapped direction's map (dns/v2 ...cpp:1100-1145). pad: the
-            // query's CD bit, the message's l3 (bit 1: IPv6)
-            const uint32_t dir = dm.flags & 3;
-            const uint32_t xd = dir == 2 ? 2u : (qr ? dir ^ 1u : dir);
-            ev.key |= (uint64_t)(xd + 1) << 48;
-            ev.pad = (uint8_t)(((w0 >> 28) & 1) | ((dm.flags & 4) ? 2u : 0u));
-        }
-        P.events[e] = ev;
-        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
-    }
+    emit(deep, false);
 }
 
 // Flush a workgroup's key cache: hashed keys to the update log, dense keys to HBM.
@@ -3072,7 +3114,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 if (metric == TM_QNAME2 || metric == TM_QNAME3) {
                     int q2, q3;
                     uint64_t h2, h3;
-                    const uint32_t sfx = (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) ? P.sfx_of[e.rep] : 0u;
+                    const uint32_t sfx = ((P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) && !(P.f_flags & PVDF_V2)) ? P.sfx_of[e.rep] : 0u;
                     if (nl > 0) agg_domain_r(R, m, mlen, st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx);
                     else { q2 = 0; q3 = -1; }
                     const int st0 = metric == TM_QNAME2 ? q2 : q3;
@@ -3661,11 +3703,19 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         const bool found = q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h && !xev(X, q).qr;
         const PvXEvent qe = found ? xev(X, q) : e;
         const uint32_t kp = found ? purge_period(P, X.ttl_s, qe.period, qe.sec) : 0u;
-        if (!found || (kp && kp <= e.period)) { if (kept) atomicAdd(&c[D2_ORPHAN], 1u); return; }
+        const bool rf = e.pad & 4, qf = found && (qe.pad & 4); // filtered response / query (v2 filters)
+        // process_filtered's second `filtered` (a valid pair with an unfiltered query), or a
+        // response to a filtered query (dns/v2 ...cpp:1115-1119,1160-1164)
+        auto filtered = [&]() {
+            if (kept && (P.dns2_groups & PV_D2G_COUNTERS)) sum_add(P, P.dslot_of[e.period], PV_OFF_DNS + DC_FILTERED, 1);
+        };
+        if (!found || (kp && kp <= e.period)) { if (kept && !rf) atomicAdd(&c[D2_ORPHAN], 1u); return; }
         int64_t dsec = e.sec > qe.sec ? e.sec - qe.sec : qe.sec - e.sec;
         int64_t dnsec = (int64_t)e.nsec - (int64_t)qe.nsec;
         if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
         const bool timed_out = dsec > (int64_t)X.ttl_s || (dsec == (int64_t)X.ttl_s && ((double)dnsec / 1.0e6) >= (double)X.ttl_ms);
+        if (rf) { if (!timed_out && !qf) filtered(); return; }
+        if (qf) { filtered(); return; }
         if (timed_out) { if (kept) atomicAdd(&c[D2_TIMEOUT], 1u); return; }
         const uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
         if (!kept) {

@@ -287,7 +287,12 @@ struct PvSubnets {
 #define PV_MAX_SUFFIXES 4
 enum { PVDF_EXCLUDE_NOERROR = 1, PVDF_ONLY_RCODE = 2, PVDF_ANSWER_COUNT = 4, PVDF_ONLY_QUERIES = 8, PVDF_ONLY_RESPONSES = 16,
        PVDF_ONLY_QTYPE = 32, PVDF_ONLY_QNAME = 64, PVDF_ONLY_QSUFFIX = 128,
-       PVDF_ONLY_DNSSEC = 256, PVDF_FILTER_ALL = 512, PVDF_PSL = 1024 };
+       PVDF_ONLY_DNSSEC = 256, PVDF_FILTER_ALL = 512, PVDF_PSL = 1024,
+       // DNS v2 filters (dns/v2/DnsStreamHandler.cpp:61-170,484-609): PVDF_V2 selects their semantics
+       // (responses: rcode / answer_count / DNSSEC / qtype, queries: qname / suffix, both: the
+       // transaction directions; filtered messages stay transaction events)
+       PVDF_V2 = 2048, PVDF2_NOIN = 4096, PVDF2_NOOUT = 8192, PVDF2_NOUNK = 16384, PVDF2_RCODE = 32768,
+       PVDF2_QNAME = 65536 };
 // public_suffix_list table on the device (pv_host.cpp psl_blob): 512 slots of {FNV-1a of the
 // last label, byte offset, length, first suffix | count << 16}, then per suffix {offset, length}
 #define PV_PSL_SLOTS 512

@@ -114,3 +114,18 @@ def test_schema_checker_catches_missing_keys(oracle):
     # default groups: no top_ecs / details keys, which the reference's schema requires
     errs = errors(_schema("dns"), {"dns": out["dns"]})
     assert any("top_query_ecs" in e for e in errs) and any("top_noerror" in e for e in errs)
+
+
+def test_dns2_filter_config():
+    """DnsStreamHandler v2 start (dns/v2/DnsStreamHandler.cpp:61-170): typed filters with v2's
+    key set, only_xact_directions to disabled bits, the reference's error texts"""
+    from pktvisor_amd.config import ConfigException, dns2_start
+    d = dns2_start({"exclude_noerror": True, "only_xact_directions": ["in", "unknown"]})
+    assert d["filters"]["v2"] == 1 and d["filters"]["exclude_noerror"] == 1 and d["filters"]["xact_dirs_disabled"] == 2
+    d = dns2_start({"only_rcode": ["nxdomain", "5"], "only_qname": ["A.b"]})
+    assert d["filters"]["only_rcode_mask"] == (1 << 3) | (1 << 5) and d["filters"]["only_qname"] == ["a.b"]
+    assert dns2_start({})["filters"] is None
+    with pytest.raises(ConfigException, match="only_xact_directions filter contained an invalid/unsupported direction: up"):
+        dns2_start({"only_xact_directions": ["up"]})
+    with pytest.raises(ConfigException, match="geoloc_notfound is not supported"):
+        dns2_start({"geoloc_notfound": True})

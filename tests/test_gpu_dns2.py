@@ -94,3 +94,47 @@ def test_dns2_tcp_parity(oracle, tmp_path):
     """DNS over TCP messages as v2 transactions (reassembly as in test_gpu_tcp.py)"""
     gpu, ref = run_both(oracle, synth.tcp_dns_pcap(2), "10.0.0.0/8,2001:db8::/32", 1, tmp_path)
     assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+# ---- DNS v2 filters (dns/v2/DnsStreamHandler.cpp:61-170,484-609; process_filtered :1147-1174)
+def oracle2_kw(f):
+    """the oracle's v2 filter keys: the v1 typed keys plus only_xact_directions' disabled bits"""
+    from tests.test_gpu_filters import oracle_kw
+    kw = oracle_kw({k: v for k, v in f.items() if k != "only_xact_directions"})
+    if "only_xact_directions" in f:
+        kw["xact_dirs_disabled"] = 7 & ~sum({"in": 1, "out": 2, "unknown": 4}[d] for d in f["only_xact_directions"])
+    return kw
+
+
+V2_FILTERS = [{"exclude_noerror": True}, {"only_rcode": ["nxdomain", "refused"]}, {"only_rcode": 0, "answer_count": 0},
+              {"only_qtype": ["AAAA", "TXT"]}, {"only_xact_directions": ["in"]}, {"only_xact_directions": ["out", "unknown"]},
+              {"only_qname_suffix": ["test.com"]}, {"only_qname": ["nonexistent.google.com"]},
+              {"only_dnssec_response": True, "only_xact_directions": ["unknown", "in"]}]
+
+
+@pytest.mark.parametrize("periods", [1, 5])
+@pytest.mark.parametrize("f", V2_FILTERS, ids=[",".join(f) for f in V2_FILTERS])
+@pytest.mark.parametrize("fixture,host", [("dns_udp_tcp_random.pcap", "192.168.0.0/24"),
+                                          ("dns_udp_mixed_rcode.pcap", "192.168.0.0/26")])
+def test_dns2_filters_parity(oracle, tmp_path, fixture, host, periods, f):
+    """filtered messages are events and `filtered_packets`, and still open / end transactions:
+    a response to a filtered query counts as filtered, a filtered response to a valid query twice"""
+    pcap = open(os.path.join(GOLD, fixture), "rb").read()
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec=host, periods=periods, dns2_config={"enable": ALL_NAMES, **f})
+    ref = oracle.run_bytes(pcap, host_spec=host, num_periods=periods, window=periods, dns2_groups=ALL, **oracle2_kw(f))
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("f", [{"exclude_noerror": True}, {"only_xact_directions": ["out"]}, {"only_qtype": ["A"]}],
+                         ids=["noerror", "dir_out", "qtype"])
+def test_dns2_filters_synthetic_shifts(oracle, tmp_path, f):
+    """C4 traffic over several 60 s marks, periods 5: filtered queries purged at shifts count as
+    time-outs, responses to them as filtered, across batches (carried transactions)"""
+    pcap = synth.pcap_bytes(4, 120000, ts_step_us=2500)
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec=synth.HOST_SPEC, periods=5, dns2_config={"enable": ALL_NAMES, **f})
+    ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5, dns2_groups=ALL, **oracle2_kw(f))
+    assert diff(gpu, ref) is None, diff(gpu, ref)

@@ -26,6 +26,7 @@ def samples(txt):
         m = LINE.match(ln)
         assert m, ln
         labels = dict(re.findall(r'(\w+)="([^"]*)"', m.group(2)))
+        labels.pop("instance", None)  # a static label another test may have added (process-wide)
         out[(m.group(1), tuple(sorted(labels.items())))] = float(m.group(3))
     return out
 
