@@ -146,7 +146,7 @@ def main():
                        "parallelism": f"dp{world} (contiguous record shards, RCCL all-reduce of live buckets)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profile(args.config, n),
-                         "kernel": "pv_net_kernel", "kernel_ms": round(kernel_ms, 4),
+                         "kernel": h.net_kernel_name(), "kernel_ms": round(kernel_ms, 4),
                          "kernel_ms_median": round(float(np.median(net_ms)), 4),
                          "frac_median": round(algo_bytes / (float(np.median(net_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "bytes_per_launch": algo_bytes},

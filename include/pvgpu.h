@@ -439,6 +439,9 @@ int pv_merge_topn(pv_ctx *ctx, const uint8_t *buf, size_t bytes);
 /* Device time of the Net-pass kernel (pv_net_kernel), from HIP events
  * recorded on the launch stream around every launch since the last reset:
  * total milliseconds and number of launches. */
+/* The Net-pass kernel the last span launched ("pv_net_kernel_reg", "pv_net_kernel", ...): the
+ * name rocprofv3 reports for the launches pv_kernel_timing times. */
+const char *pv_net_kernel_name(pv_ctx *ctx);
 int pv_kernel_timing(pv_ctx *ctx, double *total_ms, uint64_t *launches, int reset);
 
 #ifdef __cplusplus

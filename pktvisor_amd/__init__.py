@@ -169,7 +169,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label",
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
-           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts"]
+           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name"]
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
@@ -243,6 +243,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_edge_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_edge_merge.argtypes = [P, P, P, U32, U32]
     lib.pv_set_slow_defer.argtypes = [P, ctypes.c_int]
+    lib.pv_net_kernel_name.argtypes = [P]
+    lib.pv_net_kernel_name.restype = ctypes.c_char_p
     lib.pv_shard_cuts.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, U32, U32, U32, P]
     lib.pv_edge_carry.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_slow_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
@@ -749,6 +751,10 @@ class PvHandlers:
         ptrs = (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
         sizes = (ctypes.c_size_t * len(bufs))(*[len(b) for b in exports])
         self._check(self.lib.pv_edge_merge(self.ctx, ptrs, sizes, len(bufs), rank), "pv_edge_merge")
+
+    def net_kernel_name(self) -> str:
+        """the Net-pass kernel the last span launched (pv_net_kernel_name)"""
+        return self.lib.pv_net_kernel_name(self.ctx).decode()
 
     def edge_carry(self, open_in: bytes) -> bytes:
         """sharded runs in rank order (pv_edge_carry): account the queries the earlier shards leave

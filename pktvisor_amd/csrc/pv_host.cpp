@@ -160,6 +160,7 @@ extern "C" __global__ void pv_ix_scan(const PvIxParams *X);
 extern "C" __global__ void pv_ix_write(const PvIxParams *X);
 extern "C" __global__ void pv_ix_secs(const PvIxParams *X, uint32_t n);
 extern "C" __global__ void pv_topn_retry(const PvParams *P, const PvOvf *src, uint32_t n);
+extern "C" __global__ void pv_dns_tcp_filter(const PvParams *P);
 extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_t *theta_out);
 extern "C" __global__ void pv_topn_compact(const PvParams *P, uint32_t tb, uint8_t *tmp, unsigned long long *tmp_top);
 extern "C" __global__ void pv_topn_names(const PvParams *P);
@@ -418,6 +419,7 @@ struct pv_ctx {
     int cus = 256;
     int wg_per_cu = 3;     // grid workgroups per CU (the batch's partition)
     int reg_wg_per_cu = 1; // workgroups per CU of the register-window Net pass
+    const char *net_kernel = "none"; // the Net-pass kernel the last span launched (pv_net_kernel_name)
     uint64_t *d_dq = nullptr; // DNS work lists (32-B messages)
     uint32_t *d_dq_cnt = nullptr;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
@@ -557,6 +559,12 @@ struct pv_ctx {
     // bitmaps (Net by record, DNS by the record of its event), pinned staging + device copies
     uint32_t sample_rate = 100;
     Jsf32 rng_net, rng_dns;
+    bool dns_deep_now = true;   // the DNS manager's _deep_sampling_now (a filtered event counts it)
+    uint64_t *d_fbits = nullptr, *h_fbits = nullptr;   // per record: a filtered DNS event (sampling)
+    uint64_t *d_tfbits = nullptr, *h_tfbits = nullptr; // per TCP message
+    uint32_t *d_ntcp = nullptr, *h_ntcp = nullptr;     // per TCP message: not deep
+    uint64_t tmsg_bits_cap = 0;                        // messages the three TCP bitmaps hold
+    std::vector<std::pair<uint64_t, uint32_t>> tcp_items; // (ord, message item) of the batch, by ord
     uint32_t *h_ndeep = nullptr, *d_ndeep = nullptr;
     uint64_t ndeep_words = 0;
     std::vector<std::pair<uint64_t, int64_t>> tcp_ords; // (ord, second) of the batch's messages, by ord
@@ -2026,7 +2034,6 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
         if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
             return c->hipfail(e, "only_qname_suffix record buffer");
     }
-    if (fl && c->sample_rate < 100) return c->fail(PV_EUNSUPPORTED, "DNS filters with deep_sample_rate below 100 are not built");
     c->f_flags = fl;
     c->f_rcode_mask = (fl & PVDF_ONLY_RCODE) ? f->only_rcode_mask : 0;
     c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
@@ -2217,6 +2224,8 @@ void pv_destroy(pv_ctx *c)
     if (c->copy_stream2) hipStreamDestroy(c->copy_stream2);
     if (c->d_ndeep) hipFree(c->d_ndeep);
     if (c->h_ndeep) hipHostFree(c->h_ndeep);
+    for (void *p : {(void *)c->d_fbits, (void *)c->d_tfbits, (void *)c->d_ntcp}) if (p) hipFree(p);
+    for (void *p : {(void *)c->h_fbits, (void *)c->h_tfbits, (void *)c->h_ntcp}) if (p) hipHostFree(p);
     c->pool.reset();
     if (c->ev_start) hipEventDestroy(c->ev_start);
     if (c->ev_stop) hipEventDestroy(c->ev_stop);
@@ -2249,6 +2258,7 @@ int pv_reset(pv_ctx *c)
     c->records_seen = 0;
     c->rng_net = Jsf32();
     c->rng_dns = Jsf32();
+    c->dns_deep_now = true;
     c->xvals_host.clear();
     c->xvals_synced = 0;
     c->from90 = c->to90 = 0.0f;
@@ -2429,13 +2439,14 @@ void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t
 // pv_dns_prescan over a batch, its bits copied to c->h_dbits (synchronises); with tcp_emit
 // also the batch's TCP segments and tile masks (their counts into tseg[2])
 int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, hipStream_t st, bool tcp_emit,
-                uint32_t *tseg)
+                uint32_t *tseg, bool fbits = false)
 {
     launch_fill32(c, c->d_status + ST_TSEG, 2, 0);
     flush_fills(c);
     PvParams P;
     params_common(c, P, d_recs, d_offs, n);
     P.tcp_emit = tcp_emit ? 1u : 0u;
+    if (fbits) P.fbits = c->d_fbits;
     hipError_t e;
     *c->h_params = P;
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
@@ -2450,6 +2461,9 @@ int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64
         return c->hipfail(e, "DNS prescan");
     tseg[0] = c->h_status[ST_TSEG];
     tseg[1] = c->h_status[ST_TSEG_BYTES];
+    if (fbits && (!hip_ok(e = hipMemcpyAsync(c->h_fbits, c->d_fbits, tiles * 8, hipMemcpyDeviceToHost, st)) ||
+                  !hip_ok(e = hipStreamSynchronize(st))))
+        return c->hipfail(e, "DNS filter prescan");
     return 0;
 }
 
@@ -2611,6 +2625,9 @@ int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t
         c->tcp_ords.resize(c->tcp_nmsg);
         for (uint32_t q = 0; q < c->tcp_nmsg; q++) c->tcp_ords[q] = {items[(size_t)q * 8 + 7], (int64_t)items[(size_t)q * 8 + 5]};
         std::sort(c->tcp_ords.begin(), c->tcp_ords.end());
+        c->tcp_items.resize(c->tcp_nmsg);
+        for (uint32_t q = 0; q < c->tcp_nmsg; q++) c->tcp_items[q] = {items[(size_t)q * 8 + 7], q};
+        std::sort(c->tcp_items.begin(), c->tcp_items.end());
     }
     return 0;
 }
@@ -2627,6 +2644,7 @@ uint32_t tcp_pass(pv_ctx *c, const PvParams &P, uint64_t a, uint64_t b, hipStrea
     Q.dq = c->d_tmq;
     Q.sfx_of = c->d_tsfx;
     Q.tcp_pass = 1;
+    Q.ndeep_dns = c->sample_rate < 100 ? c->d_ntcp : nullptr; // per message item (pv_dns_tcp)
     Q.tcp_emit = 0;
     Q.tcp_nmsg = c->tcp_nmsg;
     Q.ord_lo = (uint32_t)(a * 4);
@@ -2968,32 +2986,91 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.gbase = c->global_base + c->records_seen;
     if (c->slow_defer && !c->edge_h) c->edge_h = (int64_t)first_sec + c->ttl_s + 61;
     if (c->sample_rate < 100) {
-        // AbstractMetricsManager::new_event (:318-323): one draw per event of each manager, in
-        // stream order; Net events are the records, DNS events the DNS-port UDP records the
-        // prescan finds (DNS filters are refused with sampling, so every one is an event)
+        // AbstractMetricsManager::new_event (:318-333): one draw per event of each manager, in
+        // stream order. Net events are the records. DNS events are the DNS-port UDP records the
+        // input predicates pass and the DNS-over-TCP messages (their order: record * 4 + the
+        // message's rank); an event _filtering rejects is process_filtered, new_event(stamp,
+        // false): no draw, the manager's last flag (dns/v1/DnsStreamHandler.cpp:1341-1375)
         const uint64_t words = n / 32 + 64; // padded: inactive lanes of the last tile read in bounds
+        hipError_t e;
         if (words > c->ndeep_words) {
             if (c->d_ndeep) hipFree(c->d_ndeep);
             if (c->h_ndeep) hipHostFree(c->h_ndeep);
             c->d_ndeep = nullptr;
             c->h_ndeep = nullptr;
             c->ndeep_words = 0;
-            hipError_t e;
             if (!hip_ok(e = hipMalloc(&c->d_ndeep, words * 8)) || !hip_ok(e = hipHostMalloc((void **)&c->h_ndeep, words * 8, hipHostMallocDefault)))
                 return c->hipfail(e, "deep sampling bitmaps");
             c->ndeep_words = words;
         }
+        const bool filt = c->f_flags != 0;
+        if (filt && !c->d_fbits) {
+            const size_t fw = (size_t)(c->max_records / 64 + 2);
+            if (!hip_ok(e = hipMalloc(&c->d_fbits, fw * 8)) || !hip_ok(e = hipHostMalloc((void **)&c->h_fbits, fw * 8, hipHostMallocDefault)))
+                return c->hipfail(e, "deep sampling filter bits");
+        }
         uint32_t tseg[2];
-        if (int rc = dns_prescan(c, d_recs, d_offs, n, st, false, tseg)) return rc;
+        if (int rc = dns_prescan(c, d_recs, d_offs, n, st, false, tseg, filt)) return rc;
+        // the span's messages (ord in [4a, 4(a + n))), and which of them are filtered
+        const uint32_t nmsg = c->tcp_nmsg;
+        if (nmsg) {
+            if (nmsg + 64 > c->tmsg_bits_cap) {
+                for (void *p : {(void *)c->d_tfbits, (void *)c->d_ntcp}) if (p) hipFree(p);
+                for (void *p : {(void *)c->h_tfbits, (void *)c->h_ntcp}) if (p) hipHostFree(p);
+                c->d_tfbits = c->h_tfbits = nullptr;
+                c->d_ntcp = c->h_ntcp = nullptr;
+                const uint64_t cap = (uint64_t)nmsg + 4096;
+                if (!hip_ok(e = hipMalloc(&c->d_tfbits, (cap / 64 + 2) * 8)) ||
+                    !hip_ok(e = hipHostMalloc((void **)&c->h_tfbits, (cap / 64 + 2) * 8, hipHostMallocDefault)) ||
+                    !hip_ok(e = hipMalloc(&c->d_ntcp, (cap / 32 + 64) * 4)) ||
+                    !hip_ok(e = hipHostMalloc((void **)&c->h_ntcp, (cap / 32 + 64) * 4, hipHostMallocDefault)))
+                    return c->hipfail(e, "deep sampling message bitmaps");
+                c->tmsg_bits_cap = cap;
+            }
+            if (filt) {
+                PvParams Q = P;
+                Q.recs = c->d_marena;
+                Q.offs = c->d_moffs;
+                Q.linktype = 101;
+                Q.dq = c->d_tmq;
+                Q.tcp_nmsg = nmsg;
+                Q.fbits = c->d_tfbits;
+                c->h_params[1] = Q;
+                if (!hip_ok(e = hipMemcpyAsync(c->d_params + 1, c->h_params + 1, sizeof Q, hipMemcpyHostToDevice, st)))
+                    return c->hipfail(e, "parameter upload");
+                const uint32_t tiles = (nmsg + 63) / 64;
+                hipLaunchKernelGGL(pv_dns_tcp_filter, dim3(std::min<uint32_t>((tiles + 3) / 4, (uint32_t)c->cus * 8)), dim3(256), 0, st,
+                                   (const PvParams *)(c->d_params + 1));
+                if (!hip_ok(e = hipGetLastError()) ||
+                    !hip_ok(e = hipMemcpyAsync(c->h_tfbits, c->d_tfbits, (size_t)tiles * 8, hipMemcpyDeviceToHost, st)) ||
+                    !hip_ok(e = hipStreamSynchronize(st)))
+                    return c->hipfail(e, "DNS-over-TCP filter prescan");
+            }
+            memset(c->h_ntcp, 0, ((size_t)nmsg / 32 + 1) * 4);
+        }
         uint32_t *hn = c->h_ndeep, *hd = c->h_ndeep + words;
         memset(hn, 0, words * 8);
+        auto dns_draw = [&](bool filtered) {
+            if (!filtered) c->dns_deep_now = c->rng_dns.next() % 100u < c->sample_rate;
+            return c->dns_deep_now;
+        };
+        const uint64_t olo = a * 4, ohi = (a + n) * 4;
+        auto it = std::lower_bound(c->tcp_items.begin(), c->tcp_items.end(), std::make_pair(olo, 0u));
         for (uint64_t i = 0; i < n; i++) {
             if (!(c->rng_net.next() % 100u < c->sample_rate)) hn[i >> 5] |= 1u << (i & 31);
-            if ((c->h_dbits[i >> 6] >> (i & 63)) & 1)
-                if (!(c->rng_dns.next() % 100u < c->sample_rate)) hd[i >> 5] |= 1u << (i & 31);
+            if ((c->h_dbits[i >> 6] >> (i & 63)) & 1) {
+                const bool f = filt && ((c->h_fbits[i >> 6] >> (i & 63)) & 1);
+                if (!dns_draw(f)) hd[i >> 5] |= 1u << (i & 31);
+            }
+            // the messages a TCP record completes (ord (a + i) * 4 + sub)
+            for (; it != c->tcp_items.end() && it->first < ohi && (it->first >> 2) == a + i; ++it) {
+                const uint32_t q = it->second;
+                const bool f = filt && ((c->h_tfbits[q >> 6] >> (q & 63)) & 1);
+                if (!dns_draw(f)) c->h_ntcp[q >> 5] |= 1u << (q & 31);
+            }
         }
-        hipError_t e;
-        if (!hip_ok(e = hipMemcpyAsync(c->d_ndeep, c->h_ndeep, words * 8, hipMemcpyHostToDevice, st)))
+        if (!hip_ok(e = hipMemcpyAsync(c->d_ndeep, c->h_ndeep, words * 8, hipMemcpyHostToDevice, st)) ||
+            (nmsg && !hip_ok(e = hipMemcpyAsync(c->d_ntcp, c->h_ntcp, ((size_t)nmsg / 32 + 1) * 4, hipMemcpyHostToDevice, st))))
             return c->hipfail(e, "deep sampling bitmaps");
         P.ndeep_net = c->d_ndeep;
         P.ndeep_dns = c->d_ndeep + words;
@@ -3121,6 +3198,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
                           !(force && !strcmp(force, "ns"));
         // lean: the register-window pass (pv_net_kernel_reg) unless PV_NET_KERNEL=fast asks for the LDS ring
         const bool ring = force && !strcmp(force, "fast");
+        c->net_kernel = general ? "pv_net_kernel" : (lean ? (ring ? "pv_net_kernel_fast" : "pv_net_kernel_reg") : "pv_net_kernel_ns");
         if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
         else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
         else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -3164,8 +3242,6 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (!c->tcp_pre) {
         if (int rc = tcp_stage(c, d_recs, d_offs, n, status[ST_TSEG], status[ST_TSEG_BYTES], first_sec, false, st)) return rc;
     }
-    if (c->sample_rate < 100 && c->tcp_nmsg)
-        return c->fail(PV_EUNSUPPORTED, "deep_sample_rate below 100 with DNS over TCP is not built");
     const uint32_t gt = tcp_pass(c, P, a, a + n, st, c->h_params + 1);
     if (gt) {
         if (P.want_events)
@@ -3221,6 +3297,29 @@ int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const
     c->tcp_pre = false;
     c->tcp_nmsg = 0;
     c->tcp_ords.clear();
+    c->tcp_items.clear();
+    if (c->sample_rate < 100) {
+        // deep sampling draws per DNS event in stream order, DNS-over-TCP messages among them:
+        // the TCP stage runs ahead of the spans so their order is known first
+        c->tcp_pre = true;
+        uint32_t tseg[2] = {0, 0};
+        if (int rc = dns_prescan(c, d_recs, d_offs, info->n_records, st, true, tseg)) return rc;
+        const bool dns_may = c->cfg.num_periods > 1 && info->last_sec >= c->dns.next_shift_sec;
+        if (int rc = tcp_stage(c, d_recs, d_offs, info->n_records, tseg[0], tseg[1], (uint32_t)info->first_sec, true, st))
+            return rc;
+        if (c->cfg.num_periods <= 1) return 0;
+        const bool net_may = info->last_sec >= c->net.next_shift_sec;
+        if (!net_may && !dns_may) return 0;
+        if (!info->monotone) {
+            for (uint32_t k = 0; k < info->n_sec_changes; k++)
+                if ((int64_t)sc_sec[k] >= std::min(c->net.next_shift_sec, c->dns.next_shift_sec))
+                    return c->fail(PV_EUNSUPPORTED, "period shift inside a batch with non-monotone timestamps");
+            return 0;
+        }
+        if (net_may) net_shifts_of(c->net.next_shift_sec, info, sc_idx, sc_sec, nsh);
+        if (dns_may) dns_shifts_of(c->dns.next_shift_sec, c->h_dbits, info->n_records, info, sc_idx, sc_sec, c->tcp_ords, dsh);
+        return 0;
+    }
     if (c->cfg.num_periods <= 1) return 0;
     const bool net_may = info->last_sec >= c->net.next_shift_sec, dns_may = info->last_sec >= c->dns.next_shift_sec;
     if (!net_may && !dns_may) return 0;
@@ -5378,4 +5477,10 @@ int pv_shard_cuts(const uint8_t *recs, size_t bytes, const uint32_t *offs, uint6
     }
     cuts[world] = n;
     return 0;
+}
+
+// the Net-pass kernel the context's last span launched (the symbol rocprofv3 reports)
+const char *pv_net_kernel_name(pv_ctx *c)
+{
+    return c ? c->net_kernel : "none";
 }

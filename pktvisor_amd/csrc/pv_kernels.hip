@@ -383,7 +383,8 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
             t.pos = (t.pos + 1) & t.rmask;
         }
     }
-    if (!done) table_overflow(P, slot, key, w, rep, ns == nullptr);
+    // (a TCP message's record lives in the TCP pass's arena, not the batch the retry reads: fail)
+    if (!done) table_overflow(P, slot, key, w, rep, ns == nullptr && !P.tcp_pass);
     if (created >= 0) atomicAdd(&P.tab_live[PV_TSLOT(slot, metric)], 1u);
     if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns, key);
 }
@@ -649,6 +650,38 @@ __device__ __forceinline__ bool dns_predicates(PV_CREF(PvParams) P, const A &R, 
     return true;
 }
 
+// DnsStreamHandler::_filtering, v1 (:538-648), for a message the input predicates passed: true
+// when it is filtered (process_filtered). The deep-sampling prescans use it to know which events
+// draw (a filtered one takes the manager's stale flag); it restates the filter block of
+// dns_process below, with the suffix match (0xff: no listed suffix) computed here.
+template <class A>
+__device__ bool dns_v1_filtered(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen, uint32_t mcap, bool tcp)
+{
+    uint32_t w0, w1, w2;
+    dns_header(R, m, mcap, w0, w1, w2);
+    const uint32_t qr = (w0 >> 23) & 1, rcode = (w0 >> 24) & 15;
+    const uint32_t qd = ((w1 & 0xff) << 8) | ((w1 >> 8) & 0xff);
+    const uint32_t ancount = ((w1 >> 8) & 0xff00) | (w1 >> 24);
+    const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
+    const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+    bool filt = ((P.f_flags & PVDF_EXCLUDE_NOERROR) && rcode == 0) ||
+                (tcp && (P.f_flags & PVDF_ONLY_RCODE) && !((P.f_rcode_mask >> rcode) & 1)) ||
+                ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
+                ((P.f_flags & PVDF_ONLY_QUERIES) && qr) || ((P.f_flags & PVDF_ONLY_RESPONSES) && !qr) ||
+                ((P.f_flags & PVDF_ONLY_DNSSEC) && (!qr || !ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar))) ||
+                (P.f_flags & PVDF_FILTER_ALL);
+    if (!filt && (P.f_flags & PVDF_ONLY_QTYPE)) {
+        DnsInfo fd;
+        dns_parse(R, m, dlen, qd, ancount, ns, ar, fd);
+        bool hit = false;
+        for (uint32_t k = 0; k < P.f_nq; k++) hit |= fd.qtype == P.f_qt[k];
+        filt = !fd.ok || !fd.has_query || !hit;
+    }
+    if (!filt && tcp && (P.f_flags & PVDF_ONLY_QNAME)) filt = !dns_qname_listed(P, R, m, dlen, w1, w2);
+    if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) filt = dns_suffix_of(P, R, m, dlen, qd, ancount, ns, ar) == 0xffu;
+    return filt;
+}
+
 // DnsMetricsBucket::process_dns_layer (:910-1049) + the transaction event of one DNS
 // message, in the bucket of its DNS period. Counters go to `c` when `own` (this lane's
 // DNS slot is the wave's register slot), else straight to HBM.
@@ -779,12 +812,14 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             sfx = filt ? 0u : r;
         }
         if (filt) {
-            // process_filtered (:1341-1347): an event (sampled at rate 100) and `filtered`
+            // process_filtered (:1341-1347): an event, counted deep when the manager's stale
+            // flag is (the not-deep bit deep sampling sets), and `filtered`
+            const bool fdeep = !(dm.flags & 16);
             if (upd) {
-                if (own) c.dfilt++;
+                if (own) { c.dfilt++; c.dnd += !fdeep; }
                 else {
                     sum_add(P, slot, PV_OFF_DNS + DC_EVENTS, 1);
-                    sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
+                    if (fdeep) sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
                     if (P.dns_groups & PV_DNS_COUNTERS_BIT) sum_add(P, slot, PV_OFF_DNS + DC_FILTERED, 1);
                 }
             }
@@ -3227,6 +3262,20 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_prescan(const PvParams 
         }
         const uint64_t b = __ballot(ev);
         if ((threadIdx.x & 63) == 0) P.dbits[t] = b;
+        if (P.fbits) {
+            // deep sampling with DNS filters: which of these events _filtering rejects
+            bool f = false;
+            if (ev) {
+                Parsed o;
+                parse_record(R, P, P.offs[i], o);
+                const uint64_t m = o.l4off + 8;
+                const uint64_t cap_end = o.frame + o.caplen;
+                const uint32_t mcap = cap_end > m ? (uint32_t)min<uint64_t>(cap_end - m, 65535) : 0u;
+                f = dns_v1_filtered(P, R, m, o.l4len - 8, mcap, false);
+            }
+            const uint64_t fb = __ballot(f);
+            if ((threadIdx.x & 63) == 0) P.fbits[t] = fb;
+        }
         if (P.tcp_emit) {
             // DNS over TCP for a batch the TCP stage runs ahead of the Net pass (pv_tcp.hip)
             const uint64_t tm = __ballot(istcp);
@@ -3265,6 +3314,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp(const PvParams *__r
         dm.port = (uint16_t)(a.w & 0xffff); dm.flags = (uint8_t)((a.w >> 16) & 0xff);
         dm.fkey = b.x; dm.sec = b.y; dm.nsec = b.z; dm.pad = b.w;
         if (dm.pad < P.ord_lo || dm.pad >= P.ord_hi) continue;
+        if (P.ndeep_dns && ((P.ndeep_dns[j >> 5] >> (j & 31)) & 1)) dm.flags |= 16; // deep sampling: not deep
         const uint32_t ordr = dm.pad - P.ord_base;
         uint32_t p = 0;
         for (uint32_t k = 0; k < P.n_dshift; k++) p += ordr >= P.dpos[k];
@@ -3282,6 +3332,26 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp(const PvParams *__r
     if (threadIdx.x == 0) {
         P.blk_events[P.grid_main + blockIdx.x] = nev;
         if (nresp) atomicAdd(P.n_events + 1, nresp);
+    }
+}
+
+// Deep sampling with DNS filters over the messages of the TCP stage (P: the TCP pass's block,
+// recs / offs the message records, dq the message list): bit j of fbits set when message j is
+// filtered (dns_v1_filtered), so the host knows which events draw.
+extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp_filter(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const GAcc R{P.recs};
+    const uint64_t nt = ((uint64_t)P.tcp_nmsg + 63) / 64;
+    for (uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < nt; t += (uint64_t)gridDim.x * 4) {
+        const uint64_t j = t * 64 + (threadIdx.x & 63);
+        bool f = false;
+        if (j < P.tcp_nmsg) {
+            const uint4 a = reinterpret_cast<const PV_G uint4 *>(P.dq)[2 * j];
+            f = dns_v1_filtered(P, R, a.y, a.z & 0xffff, a.z >> 16, true);
+        }
+        const uint64_t fb = __ballot(f);
+        if ((threadIdx.x & 63) == 0) P.fbits[t] = fb;
     }
 }
 

@@ -362,6 +362,8 @@ struct PvParams {
     PV_G uint64_t *arena_top; // PV_TABLES x PV_ARENA_PARTS bump pointers (bytes used in the partition)
     uint64_t arena_cap;  // bytes per table
     PV_G uint64_t *dbits;      // pv_dns_prescan: one bit per record, set for a DNS event (after predicates)
+    PV_G uint64_t *fbits;      // deep sampling with DNS filters: one bit per record (pv_dns_prescan) or per
+                               // TCP message (pv_dns_tcp_filter), set for an event _filtering rejects
     PV_G PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
     PV_G uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
     PV_G uint32_t *blk_events; // events appended by each workgroup

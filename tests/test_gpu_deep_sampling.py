@@ -1,7 +1,9 @@
 """deep_sample_rate < 100 on the GPU path against the oracle's restatement (jsf32 draws per
 manager in stream order; not-deep events count in the counters only; a not-deep response
 pairs but feeds no quantile, ratio or slow top): reference fixtures and a synthetic C4 capture
-over many ingest batches. Combinations that are not built fail loudly."""
+over many ingest batches; DNS filters (a filtered event draws nothing and counts the manager's
+last flag, process_filtered) and DNS over TCP (messages draw in stream order among the UDP
+events). The v2 handlers with sampling are not built and fail loudly."""
 import os
 
 import pytest
@@ -13,11 +15,13 @@ from tests.test_gpu_parity import GOLD, diff
 pytestmark = pytest.mark.gpu
 
 
-def both(oracle, pcap, tmp_path, host, periods, rate, **kw):
+def both(oracle, pcap, tmp_path, host, periods, rate, f=None, **kw):
+    from tests.test_gpu_filters import oracle_kw
     p = tmp_path / "in.pcap"
     p.write_bytes(pcap)
-    gpu = pa.pktvisor_reader(str(p), host_spec=host or None, periods=periods, deep_sample_rate=rate, **kw)
-    ref = oracle.run_bytes(pcap, host_spec=host, num_periods=periods, window=periods, deep_sample_rate=rate)
+    gpu = pa.pktvisor_reader(str(p), host_spec=host or None, periods=periods, deep_sample_rate=rate, dns_filters=f, **kw)
+    ref = oracle.run_bytes(pcap, host_spec=host, num_periods=periods, window=periods, deep_sample_rate=rate,
+                           **(oracle_kw(f) if f else {}))
     return gpu, ref
 
 
@@ -38,9 +42,28 @@ def test_synthetic_sampled_parity_many_batches(oracle, tmp_path, monkeypatch, ra
     assert diff(gpu, ref) is None, diff(gpu, ref)
 
 
+SAMPLED_FILTERS = [None, {"only_qtype": ["AAAA", "TXT"]}, {"exclude_noerror": True}, {"only_queries": True},
+                   {"only_rcode": ["noerror"]}, {"only_qname_suffix": ["test.com"]}, {"answer_count": 0}]
+
+
+@pytest.mark.parametrize("rate", [1, 50, 99])
+@pytest.mark.parametrize("f", SAMPLED_FILTERS, ids=["none"] + [",".join(f) for f in SAMPLED_FILTERS[1:]])
+@pytest.mark.parametrize("periods", [1, 5])
+def test_sampled_filters_udp_tcp(oracle, tmp_path, rate, f, periods):
+    """the reference's mixed UDP / TCP capture with DNS filters at rates 1 / 50 / 99"""
+    pcap = open(os.path.join(GOLD, "dns_udp_tcp_random.pcap"), "rb").read()
+    gpu, ref = both(oracle, pcap, tmp_path, "192.168.0.0/24", periods, rate, f)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("rate", [20, 70])
+def test_sampled_tcp_synthetic(oracle, tmp_path, rate):
+    """DNS-over-TCP connections (out-of-order, retransmitted, cut at random bytes) among UDP DNS"""
+    pcap = synth.tcp_dns_pcap(seed=4, flows=80, duration_s=150.0)
+    gpu, ref = both(oracle, pcap, tmp_path, "10.0.0.0/8", 5, rate, {"only_qtype": ["A", "AAAA", "MX"]})
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
 def test_sampling_refusals(tmp_path):
-    with pytest.raises(pa.PvError, match="DNS filters"):
-        pa.PvHandlers(deep_sample_rate=50, dns_filters={"only_queries": True})
-    p = os.path.join(GOLD, "dns_ipv4_tcp.pcap")
-    with pytest.raises(pa.PvError, match="DNS over TCP"):
-        pa.pktvisor_reader(p, periods=1, deep_sample_rate=50)
+    with pytest.raises(pa.PvError, match="v2 handlers"):
+        pa.PvHandlers(deep_sample_rate=50, dns2_config={})
