@@ -451,6 +451,7 @@ struct pv_ctx {
     uint32_t *d_tab_live = nullptr, *h_tab_live = nullptr, *d_theta = nullptr;
     PvOvf *d_ovf = nullptr, *d_ovf2 = nullptr; // top-N overflow list and its retry copy
     uint32_t *d_ovf_cnt = nullptr, ovf_cap = 0;
+    uint32_t *h_ovf = nullptr;                  // pinned copy of the two overflow words (read with the status)
     uint64_t ovf_rounds = 0;                    // purge-and-retry rounds so far
     uint8_t *d_ctmp = nullptr;          // arena compaction scratch (one table's arena)
     unsigned long long *d_ctop = nullptr;
@@ -2159,6 +2160,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_ovf, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
         !hip_ok(e = hipMalloc(&c->d_ovf2, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
         !hip_ok(e = hipMalloc(&c->d_ovf_cnt, 8)) || !hip_ok(e = hipMemsetAsync(c->d_ovf_cnt, 0, 8, c->stream)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_ovf, 8, hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
         !hip_ok(e = hipMalloc(&c->d_iplog, (size_t)(mr + 64) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_trash, (size_t)PV_TRASH_WAVES * 2048)) ||
@@ -2204,7 +2206,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_ovf_cnt};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
-    for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
+    for (void *hp : {(void *)c->h_ovf, (void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
                      (void *)c->h_tparams, (void *)c->h_tab_live})
         if (hp) hipHostFree(hp);
     for (auto &st : c->stage) {
@@ -2680,14 +2682,18 @@ int purge_tables(pv_ctx *c, hipStream_t st)
 // Updates full regions could not take in this batch (PvOvf list): purge each table they belong
 // to, as the sketch purges when its map is full, and insert them again, until none is left.
 // Each round at least halves the live entries of every region it purges, so the rounds end.
-int drain_overflow(pv_ctx *c, hipStream_t st)
+// known: c->h_ovf already holds the words (read back with the batch status).
+int drain_overflow(pv_ctx *c, hipStream_t st, bool known = false, bool *drained = nullptr)
 {
     hipError_t e;
     for (int round = 0;; round++) {
         uint32_t oc[2];
-        if (!hip_ok(e = hipMemcpyAsync(oc, c->d_ovf_cnt, 8, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)))
+        if (!(known && round == 0) &&
+            (!hip_ok(e = hipMemcpyAsync(c->h_ovf, c->d_ovf_cnt, 8, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st))))
             return c->hipfail(e, "top-N overflow");
+        memcpy(oc, c->h_ovf, 8);
         if (!oc[0]) return 0;
+        if (drained) *drained = true;
         if (oc[0] > c->ovf_cap) return c->fail(PV_ECAPACITY, "top-N overflow list full (%u updates)", oc[0]);
         if (round >= 64) return c->fail(PV_ECAPACITY, "top-N overflow not drained after %d purge rounds", round);
         for (uint32_t t = 0; t < PV_TABLES; t++)
@@ -2790,11 +2796,11 @@ int defer_slow(pv_ctx *c, const PvParams &P, hipStream_t st)
     uint32_t nv[4];
     if (!hip_ok(e = hipMemcpyAsync(nv, c->d_nvals, 16, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "deferred candidates");
-    auto ord_of = [&](uint32_t period) -> uint64_t {
-        const uint32_t s = P.dslot_of[period];
-        auto it = c->sg_ord.find(s | (c->gen[s] << 8));
-        return it == c->sg_ord.end() ? ~0ull : it->second;
-    };
+    // period k of the span: the k-th DNS shift after the live one (the window bookkeeping of
+    // this span's shifts runs after the transaction stage, so the slots' ordinals are not
+    // recorded yet)
+    (void)P;
+    auto ord_of = [&](uint32_t period) -> uint64_t { return c->dns.ordinal + period; };
     if (nv[1]) {
         std::vector<PvXValid> v(nv[1]);
         std::vector<uint32_t> offs;
@@ -3229,6 +3235,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     uint32_t status[ST_WORDS];
     if (!hip_ok(e = hipMemcpyAsync(c->h_tab_live, c->d_tab_live, PV_TABLES * 4, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(c->h_ovf, c->d_ovf_cnt, 8, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "kernel execution");
     memcpy(status, c->h_status, sizeof status);
@@ -3248,6 +3255,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             hipLaunchKernelGGL(pv_xact_compact, dim3(grid + gt), dim3(256), 0, st, (const PvParams *)c->d_params, grid + gt);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_dns_tcp");
         if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipMemcpyAsync(c->h_ovf, c->d_ovf_cnt, 8, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "TCP DNS pass");
         memcpy(status, c->h_status, sizeof status);
@@ -3255,9 +3263,10 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     for (uint32_t k = 0; k <= P.n_shift; k++) c->net.clean[P.slot_of[k]] = false;
     if (status[ST_NDNS] || gt)
         for (uint32_t k = 0; k <= P.n_dshift; k++) c->dns.clean[P.dslot_of[k]] = false;
-    if (int rc = drain_overflow(c, st)) return rc;
+    bool drained = false;
+    if (int rc = drain_overflow(c, st, true, &drained)) return rc;
     uint32_t flags = status[ST_FLAGS];
-    if (!hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
+    if (drained && !hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
     if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
     if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
     if (getenv("PV_STAMPS")) {
@@ -3273,7 +3282,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         }
     }
     if (int rc = pair_stage(c, P, status[ST_NEV], status[ST_NRESP], n, st)) return rc;
-    if (int rc = drain_overflow(c, st)) return rc; // top_slow tables of the transaction stage
+    // top_slow updates of the transaction stage (only when it ran)
+    if ((status[ST_NEV] || c->n_pend) && P.want_events)
+        if (int rc = drain_overflow(c, st)) return rc;
 
     // ---- window bookkeeping (host mirror of each manager's _period_shift)
     for (const Shift &sh : nsh) win_shift(c, c->net, sh.sec);
