@@ -313,6 +313,13 @@ int pv_advance_windows(pv_ctx *ctx, int part, const int64_t *thresh, uint32_t n)
 int pv_dns_event_seconds(pv_ctx *ctx, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
                          const uint32_t *sc_idx, const uint32_t *sc_sec, int64_t *secs, uint32_t max, uint32_t *n);
 /* The same over records in host memory (staged through the ingest chunks). */
+/* Deep sampling across shards: the DNS manager's draws (unfiltered DNS events, TCP messages
+ * included) the last pv_dns_event_seconds_host call counted (0 at deep_sample_rate 100), and
+ * the generators of a rank stepped past the earlier shards' draws before its first batch:
+ * net_draws = their records, dns_draws = the sum of their pv_plan_dns_draws
+ * (AbstractMetricsManager::new_event's per-manager jsf32 draws, src/AbstractMetricsManager.h:318-323). */
+int pv_plan_dns_draws(pv_ctx *ctx, uint64_t *draws);
+int pv_sample_skip(pv_ctx *ctx, uint64_t net_draws, uint64_t dns_draws);
 int pv_dns_event_seconds_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes, int64_t *secs, uint32_t max, uint32_t *n);
 /* Record cuts of a capture into `world` contiguous shards (cuts[0..world], cuts[world] = n):
  * about equal sizes, each cut at a record boundary that no DNS-over-TCP flow (a TCP packet with

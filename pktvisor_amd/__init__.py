@@ -169,7 +169,8 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label",
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
-           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name"]
+           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name",
+           "pv_plan_dns_draws", "pv_sample_skip"]
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
@@ -243,6 +244,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_edge_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_edge_merge.argtypes = [P, P, P, U32, U32]
     lib.pv_set_slow_defer.argtypes = [P, ctypes.c_int]
+    lib.pv_plan_dns_draws.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
+    lib.pv_sample_skip.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64]
     lib.pv_net_kernel_name.argtypes = [P]
     lib.pv_net_kernel_name.restype = ctypes.c_char_p
     lib.pv_shard_cuts.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, U32, U32, U32, P]
@@ -751,6 +754,16 @@ class PvHandlers:
         ptrs = (ctypes.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
         sizes = (ctypes.c_size_t * len(bufs))(*[len(b) for b in exports])
         self._check(self.lib.pv_edge_merge(self.ctx, ptrs, sizes, len(bufs), rank), "pv_edge_merge")
+
+    def plan_dns_draws(self) -> int:
+        """DNS draws the last dns_event_seconds_host call counted (pv_plan_dns_draws)"""
+        v = ctypes.c_uint64()
+        self._check(self.lib.pv_plan_dns_draws(self.ctx, ctypes.byref(v)), "pv_plan_dns_draws")
+        return int(v.value)
+
+    def sample_skip(self, net_draws: int, dns_draws: int):
+        """step the generators past the earlier shards' draws (pv_sample_skip)"""
+        self._check(self.lib.pv_sample_skip(self.ctx, net_draws, dns_draws), "pv_sample_skip")
 
     def net_kernel_name(self) -> str:
         """the Net-pass kernel the last span launched (pv_net_kernel_name)"""

@@ -561,6 +561,7 @@ struct pv_ctx {
     uint32_t sample_rate = 100;
     Jsf32 rng_net, rng_dns;
     bool dns_deep_now = true;   // the DNS manager's _deep_sampling_now (a filtered event counts it)
+    uint64_t plan_draws = 0;    // DNS draws (unfiltered DNS events) pv_dns_event_seconds_host counted
     uint64_t *d_fbits = nullptr, *h_fbits = nullptr;   // per record: a filtered DNS event (sampling)
     uint64_t *d_tfbits = nullptr, *h_tfbits = nullptr; // per TCP message
     uint32_t *d_ntcp = nullptr, *h_ntcp = nullptr;     // per TCP message: not deep
@@ -2978,6 +2979,55 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
     return 0;
 }
 
+// the per-message bitmaps of deep sampling (filtered, not deep), for nmsg messages
+int tcp_bits_alloc(pv_ctx *c, uint32_t nmsg)
+{
+    if (nmsg + 64 <= c->tmsg_bits_cap) return 0;
+    for (void *p : {(void *)c->d_tfbits, (void *)c->d_ntcp}) if (p) hipFree(p);
+    for (void *p : {(void *)c->h_tfbits, (void *)c->h_ntcp}) if (p) hipHostFree(p);
+    c->d_tfbits = c->h_tfbits = nullptr;
+    c->d_ntcp = c->h_ntcp = nullptr;
+    c->tmsg_bits_cap = 0;
+    const uint64_t cap = (uint64_t)nmsg + 4096;
+    hipError_t e;
+    if (!hip_ok(e = hipMalloc(&c->d_tfbits, (cap / 64 + 2) * 8)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_tfbits, (cap / 64 + 2) * 8, hipHostMallocDefault)) ||
+        !hip_ok(e = hipMalloc(&c->d_ntcp, (cap / 32 + 64) * 4)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_ntcp, (cap / 32 + 64) * 4, hipHostMallocDefault)))
+        return c->hipfail(e, "deep sampling message bitmaps");
+    c->tmsg_bits_cap = cap;
+    return 0;
+}
+
+// which of the batch's DNS-over-TCP messages _filtering rejects (pv_dns_tcp_filter) into
+// c->h_tfbits (synchronises)
+int tcp_filter_bits(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n, hipStream_t st)
+{
+    const uint32_t nmsg = c->tcp_nmsg;
+    if (!nmsg) return 0;
+    if (int rc = tcp_bits_alloc(c, nmsg)) return rc;
+    PvParams Q;
+    params_common(c, Q, d_recs, d_offs, n);
+    Q.recs = c->d_marena;
+    Q.offs = c->d_moffs;
+    Q.linktype = 101;
+    Q.dq = c->d_tmq;
+    Q.tcp_nmsg = nmsg;
+    Q.fbits = c->d_tfbits;
+    c->h_params[1] = Q;
+    hipError_t e;
+    if (!hip_ok(e = hipMemcpyAsync(c->d_params + 1, c->h_params + 1, sizeof Q, hipMemcpyHostToDevice, st)))
+        return c->hipfail(e, "parameter upload");
+    const uint32_t tiles = (nmsg + 63) / 64;
+    hipLaunchKernelGGL(pv_dns_tcp_filter, dim3(std::min<uint32_t>((tiles + 3) / 4, (uint32_t)c->cus * 8)), dim3(256), 0, st,
+                       (const PvParams *)(c->d_params + 1));
+    if (!hip_ok(e = hipGetLastError()) ||
+        !hip_ok(e = hipMemcpyAsync(c->h_tfbits, c->d_tfbits, (size_t)tiles * 8, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "DNS-over-TCP filter prescan");
+    return 0;
+}
+
 int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint64_t a, uint64_t n, uint64_t rec_bytes,
                  const std::vector<Shift> &nsh, const std::vector<Shift> &dsh, uint32_t first_sec, hipStream_t st)
 {
@@ -3020,38 +3070,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         // the span's messages (ord in [4a, 4(a + n))), and which of them are filtered
         const uint32_t nmsg = c->tcp_nmsg;
         if (nmsg) {
-            if (nmsg + 64 > c->tmsg_bits_cap) {
-                for (void *p : {(void *)c->d_tfbits, (void *)c->d_ntcp}) if (p) hipFree(p);
-                for (void *p : {(void *)c->h_tfbits, (void *)c->h_ntcp}) if (p) hipHostFree(p);
-                c->d_tfbits = c->h_tfbits = nullptr;
-                c->d_ntcp = c->h_ntcp = nullptr;
-                const uint64_t cap = (uint64_t)nmsg + 4096;
-                if (!hip_ok(e = hipMalloc(&c->d_tfbits, (cap / 64 + 2) * 8)) ||
-                    !hip_ok(e = hipHostMalloc((void **)&c->h_tfbits, (cap / 64 + 2) * 8, hipHostMallocDefault)) ||
-                    !hip_ok(e = hipMalloc(&c->d_ntcp, (cap / 32 + 64) * 4)) ||
-                    !hip_ok(e = hipHostMalloc((void **)&c->h_ntcp, (cap / 32 + 64) * 4, hipHostMallocDefault)))
-                    return c->hipfail(e, "deep sampling message bitmaps");
-                c->tmsg_bits_cap = cap;
-            }
-            if (filt) {
-                PvParams Q = P;
-                Q.recs = c->d_marena;
-                Q.offs = c->d_moffs;
-                Q.linktype = 101;
-                Q.dq = c->d_tmq;
-                Q.tcp_nmsg = nmsg;
-                Q.fbits = c->d_tfbits;
-                c->h_params[1] = Q;
-                if (!hip_ok(e = hipMemcpyAsync(c->d_params + 1, c->h_params + 1, sizeof Q, hipMemcpyHostToDevice, st)))
-                    return c->hipfail(e, "parameter upload");
-                const uint32_t tiles = (nmsg + 63) / 64;
-                hipLaunchKernelGGL(pv_dns_tcp_filter, dim3(std::min<uint32_t>((tiles + 3) / 4, (uint32_t)c->cus * 8)), dim3(256), 0, st,
-                                   (const PvParams *)(c->d_params + 1));
-                if (!hip_ok(e = hipGetLastError()) ||
-                    !hip_ok(e = hipMemcpyAsync(c->h_tfbits, c->d_tfbits, (size_t)tiles * 8, hipMemcpyDeviceToHost, st)) ||
-                    !hip_ok(e = hipStreamSynchronize(st)))
-                    return c->hipfail(e, "DNS-over-TCP filter prescan");
-            }
+            if (int rc = tcp_bits_alloc(c, nmsg)) return rc;
+            if (filt)
+                if (int rc = tcp_filter_bits(c, d_recs, d_offs, n, st)) return rc;
             memset(c->h_ntcp, 0, ((size_t)nmsg / 32 + 1) * 4);
         }
         uint32_t *hn = c->h_ndeep, *hd = c->h_ndeep + words;
@@ -3595,6 +3616,7 @@ int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int6
 {
     hipSetDevice(c->device);
     *n = 0;
+    c->plan_draws = 0;
     if (c->tcp_active) return c->fail(PV_EINVAL, "pv_dns_event_seconds_host after DNS-over-TCP state (call it before the first batch)");
     struct TcpClean { pv_ctx *c; ~TcpClean() { std::lock_guard<std::mutex> g(c->mu); tcp_reset(c); } } clean{c};
     if (int rc = ingest_setup(c)) return rc;
@@ -5404,8 +5426,31 @@ static int dns_event_seconds_batch(pv_ctx *c, const uint8_t *d_recs, const uint3
     if (!nr) return 0;
     if (nr > c->max_records) return c->fail(PV_ECAPACITY, "batch exceeds max_records");
     uint32_t tseg[2];
-    if (int rc = dns_prescan(c, d_recs, d_offs, nr, c->stream, true, tseg)) return rc;
+    const bool filt = c->sample_rate < 100 && c->f_flags;
+    if (filt && !c->d_fbits) {
+        hipError_t e;
+        const size_t fw = (size_t)(c->max_records / 64 + 2);
+        if (!hip_ok(e = hipMalloc(&c->d_fbits, fw * 8)) || !hip_ok(e = hipHostMalloc((void **)&c->h_fbits, fw * 8, hipHostMallocDefault)))
+            return c->hipfail(e, "deep sampling filter bits");
+    }
+    if (int rc = dns_prescan(c, d_recs, d_offs, nr, c->stream, true, tseg, filt)) return rc;
     if (int rc = tcp_stage(c, d_recs, d_offs, nr, tseg[0], tseg[1], (uint32_t)info->first_sec, true, c->stream)) return rc;
+    if (c->sample_rate < 100) {
+        // the DNS manager's draws in this batch: its unfiltered events (a sharded run steps
+        // each rank's generator past the earlier shards' draws, pv_sample_skip)
+        uint64_t d = 0;
+        for (uint64_t t = 0; t < (nr + 63) / 64; t++) d += __builtin_popcountll(c->h_dbits[t] & ~(filt ? c->h_fbits[t] : 0ull));
+        uint64_t dt = c->tcp_nmsg;
+        if (filt && c->tcp_nmsg) {
+            if (int rc = tcp_filter_bits(c, d_recs, d_offs, nr, c->stream)) return rc;
+            for (uint64_t t = 0; t < ((uint64_t)c->tcp_nmsg + 63) / 64; t++) {
+                uint64_t w = c->h_tfbits[t];
+                if (t == (c->tcp_nmsg - 1) / 64 && (c->tcp_nmsg & 63)) w &= (1ull << (c->tcp_nmsg & 63)) - 1;
+                dt -= __builtin_popcountll(w);
+            }
+        }
+        c->plan_draws += d + dt;
+    }
     // (ord, second) of every DNS event in stream order: a second's first UDP event, the messages
     std::vector<std::pair<uint64_t, int64_t>> ev;
     for (uint32_t j = 0; j < info->n_sec_changes; j++) {
@@ -5494,4 +5539,25 @@ int pv_shard_cuts(const uint8_t *recs, size_t bytes, const uint32_t *offs, uint6
 const char *pv_net_kernel_name(pv_ctx *c)
 {
     return c ? c->net_kernel : "none";
+}
+
+// Deep sampling over a sharded stream: each manager's generator stepped past the draws the
+// earlier shards make (net_draws: their records, dns_draws: their unfiltered DNS events, as
+// pv_dns_event_seconds_host counts them in pv_plan_dns_draws), so every rank draws what the
+// single pass draws for its events (AbstractMetricsManager::new_event, :318-323); the DNS
+// manager's flag is the last of those draws (a filtered event at the shard start counts it).
+int pv_sample_skip(pv_ctx *c, uint64_t net_draws, uint64_t dns_draws)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->records_seen) return c->fail(PV_EINVAL, "pv_sample_skip after the first batch");
+    if (c->sample_rate >= 100) return 0;
+    for (uint64_t k = 0; k < net_draws; k++) c->rng_net.next();
+    for (uint64_t k = 0; k < dns_draws; k++) c->dns_deep_now = c->rng_dns.next() % 100u < c->sample_rate;
+    return 0;
+}
+
+int pv_plan_dns_draws(pv_ctx *c, uint64_t *draws)
+{
+    *draws = c->plan_draws;
+    return 0;
 }

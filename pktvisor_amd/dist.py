@@ -109,18 +109,21 @@ def shifts_of(start_sec: int, per_rank_secs):
     return out
 
 
-def plan_windows(handlers, start_sec: int, rec_secs, dns_secs, group=None):
+def plan_windows(handlers, start_sec: int, rec_secs, dns_secs, group=None, draws=(0, 0)):
     """All-gather each rank's record seconds (Net events) and DNS-event seconds, compute both
     managers' global shifts, and return this rank's part of the plan:
-    {"net": (leading, trailing), "dns": (leading, trailing)} — the shifts owned by earlier and
-    by later ranks, which this rank applies as window operations (pv_advance_windows)."""
+    {"net": (leading, trailing), "dns": (leading, trailing), "skip": (net, dns)} — the shifts
+    owned by earlier and by later ranks, which this rank applies as window operations
+    (pv_advance_windows), and the deep-sampling draws of the earlier ranks (pv_sample_skip)."""
     world, me = dist.get_world_size(group), dist.get_rank(group)
     allv = [None] * world
-    dist.all_gather_object(allv, ([int(x) for x in rec_secs], [int(x) for x in dns_secs]), group=group)
+    dist.all_gather_object(allv, ([int(x) for x in rec_secs], [int(x) for x in dns_secs], [int(d) for d in draws]),
+                           group=group)
     plan = {}
     for key, k in (("net", 0), ("dns", 1)):
         sh = shifts_of(start_sec, [v[k] for v in allv])
         plan[key] = ([t for t, r in sh if r < me], [t for t, r in sh if r > me])
+    plan["skip"] = (sum(v[2][0] for v in allv[:me]), sum(v[2][1] for v in allv[:me]))
     return plan
 
 
@@ -147,7 +150,10 @@ def process_shard(handlers, recs, index, start_sec: int, start_nsec: int = 0, gr
         except Exception:  # DNS v2: its slow tops keep the rank's own thresholds
             handlers.slow_defer = False
     dns = handlers.dns_event_seconds_host(recs) if len(recs) else []
-    plan = plan_windows(handlers, start_sec, record_seconds(index) if index is not None and index.n else [], dns, group)
+    draws = (index.n if index is not None else 0, handlers.plan_dns_draws() if len(recs) else 0)
+    plan = plan_windows(handlers, start_sec, record_seconds(index) if index is not None and index.n else [], dns, group,
+                        draws)
+    handlers.sample_skip(*plan["skip"])
     apply_plan(handlers, plan, 0)
     if len(recs):
         handlers.process_host(recs)

@@ -5,7 +5,7 @@ share cuda:0 under gloo), the ranks merge with pktvisor_amd.dist.merge_window, a
 rank 0 writes the merged window JSON. CPU mode ("cpu"): exercises the collective
 helpers of pktvisor_amd.dist alone and writes what each rank saw.
 
-usage: python -m tests.dist_worker gpu PCAP OUT HOST_SPEC PERIODS
+usage: python -m tests.dist_worker gpu PCAP OUT HOST_SPEC PERIODS [DEEP_SAMPLE_RATE [DNS_FILTERS_JSON]]
        python -m tests.dist_worker cpu OUT
 (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the environment)"""
 import json
@@ -33,7 +33,7 @@ def cpu_main(out):
     dist.destroy_process_group()
 
 
-def gpu_main(pcap_path, out, host, periods):
+def gpu_main(pcap_path, out, host, periods, rate=100, filters=None):
     import torch
     import torch.distributed as dist
     import pktvisor_amd as pa
@@ -49,7 +49,7 @@ def gpu_main(pcap_path, out, host, periods):
     lo, hi = cuts[rank], cuts[rank + 1]
     offs = [int(x) for x in idx.offsets] + [len(recs)]
     h = pa.PvHandlers(host_spec=host or None, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
-                      max_records=max(1, hi - lo), device=dev.index)
+                      max_records=max(1, hi - lo), device=dev.index, deep_sample_rate=rate, dns_filters=filters)
     try:
         h.set_global_base(lo)
         sec, frac = struct.unpack_from("<II", recs, offs[0])
@@ -71,4 +71,5 @@ if __name__ == "__main__":
     if sys.argv[1] == "cpu":
         cpu_main(sys.argv[2])
     else:
-        gpu_main(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]))
+        gpu_main(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]) if len(sys.argv) > 6 else 100,
+                 json.loads(sys.argv[7]) if len(sys.argv) > 7 else None)

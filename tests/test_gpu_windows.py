@@ -114,3 +114,20 @@ def test_sharded_world8_c4_tcp(oracle, tmp_path):
     d = ref["5m"]["dns"]
     assert d["wire_packets"]["tcp"] > 0 and d["xact"]["counts"]["total"] > 0
     assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("rate,f", [(40, None), (75, {"only_qtype": ["A", "AAAA"]})], ids=["plain", "qtype"])
+def test_sharded_deep_sampling(oracle, tmp_path, rate, f):
+    """3 ranks, deep_sample_rate < 100, C4 traffic with DNS over TCP: each rank steps its
+    managers' generators past the earlier shards' draws (pv_sample_skip; the DNS draws counted
+    by the planning prescan, filtered events excluded), so the merged window equals the single pass"""
+    from tests.test_gpu_filters import oracle_kw
+    pcap = synth.c4_tcp_pcap(n=60000, ts_step_us=2500, flows=150)
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    out = tmp_path / "out.json"
+    run_ranks(3, ["gpu", str(p), str(out), synth.HOST_SPEC, "5", str(rate)] + ([json.dumps(f)] if f else []))
+    gpu = json.load(open(out))
+    ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5, deep_sample_rate=rate,
+                           **(oracle_kw(f) if f else {}))
+    assert diff(gpu, ref) is None, diff(gpu, ref)
