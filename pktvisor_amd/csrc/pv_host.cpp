@@ -5003,7 +5003,8 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
         auto it = orph.find(kv.first);
         if (it != orph.end() && (ps < 0 || it->second->sec < c->dns_shifts[ps].first)) {
             const PvXEvent &r = *it->second;
-            const uint32_t slot = r.pad & 0x7f;
+            const uint32_t slot = r.pad & 0x3f;
+            const bool rdeep = !(r.pad & 0x40); // a response that is not deep: counts only
             const bool kept = (r.pad & 0x80) && in_dns_window(c, slot);
             // pv_xact_resolve's pairing arithmetic (timespec_diff, TransactionManager.h:24-37)
             int64_t dsec = r.sec > qe.sec ? r.sec - qe.sec : qe.sec - r.sec;
@@ -5027,15 +5028,15 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
             const size_t oi = (size_t)(it->second - v[me].orph.data());
             if (c->slow_defer && oi < c->sorph.size()) {
                 pv_ctx::SlowCand sc = c->sorph[oi];
-                if (quant && r.dir < 2)
+                if (quant && rdeep && r.dir < 2)
                     c->slow_xv.push_back({sc.ord, PvXValue{us, 0, r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US}});
-                if (kept && r.dir < 2) {
+                if (kept && rdeep && r.dir < 2) {
                     sc.us = us;
                     sc.dir = r.dir;
                     c->scands.push_back(sc);
                 }
             }
-            if (quant && in_dns_window(c, slot)) {
+            if (quant && rdeep && in_dns_window(c, slot)) {
                 const uint32_t sg = slot | (c->gen[slot] << 8);
                 if (r.dir == 0) c->xvals_host.push_back(PvXValue{us, sg, XV_FROM_US});
                 else if (r.dir == 1) c->xvals_host.push_back(PvXValue{us, sg, XV_TO_US});
@@ -5106,7 +5107,8 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
         if (!st.e.qr) continue;                                                          // overwritten by a new query
         const PvXEvent &r = st.e;
         const bool kept = (r.pad & 0x80) && in_win(st.ord);
-        const uint32_t slot = r.pad & 0x7f;
+        const uint32_t slot = r.pad & 0x3f;
+        const bool rdeep = !(r.pad & 0x40); // a response that is not deep: counts only
         int64_t dsec = r.sec > qe.sec ? r.sec - qe.sec : qe.sec - r.sec;
         int64_t dnsec = (int64_t)r.nsec - (int64_t)qe.nsec;
         if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
@@ -5119,8 +5121,8 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
             if (r.dir == 0) a[1]++;
             else if (r.dir == 1) a[2]++;
         }
-        if (quant && r.dir < 2) c->slow_xv.push_back({st.ord, PvXValue{us, 0, r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US}});
-        if (quant && in_win(st.ord)) {
+        if (quant && rdeep && r.dir < 2) c->slow_xv.push_back({st.ord, PvXValue{us, 0, r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US}});
+        if (quant && rdeep && in_win(st.ord)) {
             const uint32_t sg = slot | (c->gen[slot] << 8);
             if (r.dir < 2) c->xvals_host.push_back(PvXValue{us, sg, r.dir == 0 ? (uint32_t)XV_FROM_US : (uint32_t)XV_TO_US});
             if (qe.len && kept) {
@@ -5130,7 +5132,7 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
                 c->xvals_host.push_back(PvXValue{bits, sg, XV_RATIO});
             }
         }
-        if (kept && r.dir < 2 && st.cand >= 0) {
+        if (kept && rdeep && r.dir < 2 && st.cand >= 0) {
             pv_ctx::SlowCand sc = c->sorph[(size_t)st.cand];
             sc.us = us;
             sc.dir = r.dir;

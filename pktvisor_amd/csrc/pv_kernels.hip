@@ -3686,7 +3686,7 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
             const uint32_t k = atomicAdd(X.n_orph, 1u);
             if (k < X.orph_cap) {
                 PvXEvent o = e;
-                o.pad = (uint8_t)(P.dslot_of[e.period] | (e.period >= P.dskip_before ? 0x80u : 0u));
+                o.pad = (uint8_t)(P.dslot_of[e.period] | (e.period >= P.dskip_before ? 0x80u : 0u) | ((e.pad & 4) ? 0x40u : 0u));
                 X.orph[k] = o;
             }
             return;
@@ -3735,7 +3735,7 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
                 const uint32_t k = atomicAdd(X.n_orph, 1u);
                 if (k < X.orph_cap) {
                     PvXEvent o = e;
-                    o.pad = (uint8_t)(P.dslot_of[e.period] | (e.period >= P.dskip_before ? 0x80u : 0u));
+                    o.pad = (uint8_t)(P.dslot_of[e.period] | (e.period >= P.dskip_before ? 0x80u : 0u) | ((e.pad & 4) ? 0x40u : 0u));
                     X.orph[k] = o;
                 }
             }
