@@ -504,7 +504,7 @@ struct DnsCtr {
     uint32_t dev, dq, dr, d4, d6, dnx, dref, dsrv, dnoerr, dnodata, dfilt, dqecs, dnd;
     __device__ __forceinline__ void zero() { dev = dq = dr = d4 = d6 = dnx = dref = dsrv = dnoerr = dnodata = dfilt = dqecs = dnd = 0; }
 };
-__device__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
+__device__ __forceinline__ void dns_flush(PV_CREF(PvParams) P, uint32_t s, DnsCtr &c)
 {
     const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
     PV_FLUSH1(s, PV_OFF_DNS + DC_EVENTS, c.dev + c.dfilt, true) PV_FLUSH1(s, PV_OFF_DNS + DC_SAMPLES, c.dev + c.dfilt - c.dnd, true)
