@@ -410,6 +410,8 @@ struct pv_ctx {
     uint32_t cb_h_grid = 0;
     PvNewName *d_nn = nullptr;   // entries created by pv_topn_merge (names pending)
     uint64_t *d_iplog = nullptr; // dense IP log, one u64 per record (max_records + one tile)
+    uint32_t *d_iplog32 = nullptr, *d_ipx_cnt = nullptr, *d_ipx_rep = nullptr; // compact IP log (register pass)
+    uint64_t *d_ipdir = nullptr;
     uint64_t *d_trash = nullptr; // 64 B per Net-pass wave
     uint32_t nn_cap = 0;
     uint32_t reg_log2 = 0;
@@ -2164,6 +2166,10 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipHostMalloc((void **)&c->h_ovf, 8, hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
         !hip_ok(e = hipMalloc(&c->d_iplog, (size_t)(mr + 64) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_iplog32, (size_t)(mr + 64) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_ipx_rep, (size_t)(mr + 64) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_ipdir, (size_t)(mr / 64 + 2) * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_ipx_cnt, (size_t)PV_MAX_GRID * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_trash, (size_t)PV_TRASH_WAVES * 2048)) ||
         !hip_ok(e = hipMalloc(&c->d_cb_cnt, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_params, 2 * sizeof(PvParams))) ||
@@ -2204,7 +2210,8 @@ void pv_destroy(pv_ctx *c)
                     c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
-                    c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_ovf_cnt};
+                    c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_ovf_cnt, c->d_iplog32,
+                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
     for (void *hp : {(void *)c->h_ovf, (void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
@@ -3200,6 +3207,10 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.nn = c->d_nn;
     P.nn_cap = c->nn_cap;
     P.iplog = c->d_iplog;
+    P.iplog32 = c->d_iplog32;
+    P.ipdir = c->d_ipdir;
+    P.ipx_cnt = c->d_ipx_cnt;
+    P.ipx_rep = c->d_ipx_rep;
     P.trash = c->d_trash;
     if ((uint64_t)grid * 4 > PV_TRASH_WAVES) return c->fail(PV_ECAPACITY, "grid of %u workgroups exceeds the trash area", grid);
     P.cb = c->d_cb;
@@ -3207,30 +3218,32 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.stamps = c->d_stamps;
     P.dq = c->d_dq;
     P.dq_cnt = c->d_dq_cnt;
+    // the specialised passes when nothing in the batch needs the general one: the lean pass
+    // (one Net period, Ethernet, at most two IPv4 host subnets, a wave's tiles below 2^16 for
+    // its packed lane counters), else the shift-free general pass. PV_NET_KERNEL=ns|general
+    // forces one for A/B runs.
+    static const char *force = getenv("PV_NET_KERNEL");
+    const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || (force && !strcmp(force, "general"));
+    const uint32_t reg_grid = std::min<uint32_t>(grid, (uint32_t)(c->cus * c->reg_wg_per_cu));
+    const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
+    const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
+                      !(force && !strcmp(force, "ns"));
+    // lean: the register-window pass (pv_net_kernel_reg) unless PV_NET_KERNEL=fast asks for the LDS ring
+    const bool ring = force && !strcmp(force, "fast");
+    // the register pass writes the compact IP log (4 B + a direction bit per record)
+    P.ip_compact = lean && !ring ? 1u : 0u;
+    P.ip_base = ((uint64_t)P.slot_of[0] << 60) | ((uint64_t)TM_IPV4 << 56) |
+                ((uint64_t)((c->net_groups & PV_NET_CARDINALITY) ? 1 : 0) << 33);
     flush_fills(c);
     *c->h_params = P;
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
-    // the specialised passes when nothing in the batch needs the general one: the lean pass
-    // (one Net period, Ethernet, at most two IPv4 host subnets, a wave's tiles below 2^16 for
-    // its packed lane counters), else the shift-free general pass. PV_NET_KERNEL=ns|general
-    // forces one for A/B runs.
-    {
-        static const char *force = getenv("PV_NET_KERNEL");
-        const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || (force && !strcmp(force, "general"));
-        const uint32_t reg_grid = std::min<uint32_t>(grid, (uint32_t)(c->cus * c->reg_wg_per_cu));
-        const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
-        const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
-                          !(force && !strcmp(force, "ns"));
-        // lean: the register-window pass (pv_net_kernel_reg) unless PV_NET_KERNEL=fast asks for the LDS ring
-        const bool ring = force && !strcmp(force, "fast");
-        c->net_kernel = general ? "pv_net_kernel" : (lean ? (ring ? "pv_net_kernel_fast" : "pv_net_kernel_reg") : "pv_net_kernel_ns");
-        if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-        else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-        else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-        else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-    }
+    c->net_kernel = general ? "pv_net_kernel" : (lean ? (ring ? "pv_net_kernel_fast" : "pv_net_kernel_reg") : "pv_net_kernel_ns");
+    if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
     hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)

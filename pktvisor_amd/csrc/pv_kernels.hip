@@ -2071,7 +2071,7 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
 #endif
 struct NetRegState {
     uint32_t hist[PV_HBINS];
-    uint32_t nd;
+    uint32_t nd, nx;
     int64_t dthresh[PV_MAX_SHIFTS];
 };
 __device__ __forceinline__ void win_load(const PV_G uint8_t *recs, uint32_t off, uint4 (&W)[5])
@@ -2095,10 +2095,11 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     __shared__ NetRegState S;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
-    if (threadIdx.x == 0) S.nd = 0;
+    if (threadIdx.x == 0) { S.nd = 0; S.nx = 0; }
     if (threadIdx.x < PV_MAX_SHIFTS) S.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
     __syncthreads();
     const PV_G uint8_t *const recs = P.recs;
+    const bool compact = P.ip_compact;
     const PV_G uint32_t *const offs = P.offs;
     const uint64_t n = P.n, last = n - 1;
     const uint32_t slot = P.slot_of[0];
@@ -2155,7 +2156,29 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                                    : 0ull;
         if (PV_LEAN_LEVEL == 4) {
             hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
-            if (tops && active) P.iplog[i] = ek;
+            if (tops) {
+            if (compact) {
+                // the IPv4 entry as its address and a direction bit; anything else (an IPv6
+                // key of a general-path record) into the range's exception list
+                const bool v4 = ek && (ek >> 32 & ~1ull) == (P.ip_base >> 32);
+                const uint64_t xm = __ballot(active && ek && !v4);
+                if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
+                const uint64_t dm1 = __ballot(v4 && ((ek >> 32) & 1));
+                if (lane == 0) P.ipdir[t] = dm1;
+                if (xm) {
+                    uint32_t q = 0;
+                    if (lane == 0) q = atomicAdd(&S.nx, (uint32_t)__popcll(xm));
+                    q = __builtin_amdgcn_readlane(q, 0);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(xm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xm, 0u));
+                    if (active && ek && !v4) {
+                        P.iplog[wbeg * PV_WT + q + below] = ek;
+                        P.ipx_rep[wbeg * PV_WT + q + below] = (uint32_t)i;
+                    }
+                }
+            } else if (active) {
+                P.iplog[i] = ek;
+            }
+        }
             return;
         }
         if (card && !tops) {
@@ -2285,8 +2308,10 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     if (threadIdx.x == 0) {
         P.mq_cnt[lb] = 0;
         P.dq_cnt[lb] = S.nd;
+        if (compact) P.ipx_cnt[lb] = S.nx;
         if (S.nd) atomicAdd(P.n_dns, S.nd);
         S.nd = 0;
+        S.nx = 0;
     }
     __syncthreads();
     }
@@ -2736,9 +2761,24 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
         uint64_t a, z;
         wg_records(P, blockIdx.x, a, z);
         const PV_G uint64_t *ipl = P.iplog + a;
-        batched<PV_CB_U>(z - a, [&](uint64_t j) { return ipl[j]; }, [&](uint64_t j, uint64_t e) {
-            if (e) comb_add<CN>(P, S, sp, e, 1u, (uint32_t)(a + j));
-        });
+        if (P.ip_compact) {
+            // the register-window pass's compact log: address + direction bit, then the
+            // range's exception entries
+            const PV_G uint32_t *ip4 = P.iplog32;
+            batched<PV_CB_U>(z - a, [&](uint64_t j) { return (uint64_t)ip4[a + j]; }, [&](uint64_t j, uint64_t ip) {
+                if (ip) {
+                    const uint64_t r = a + j;
+                    const uint64_t e = P.ip_base | ((P.ipdir[r >> 6] >> (r & 63)) & 1) << 32 | ip;
+                    comb_add<CN>(P, S, sp, e, 1u, (uint32_t)r);
+                }
+            });
+            const uint32_t nx = P.ipx_cnt[blockIdx.x];
+            for (uint32_t q = threadIdx.x; q < nx; q += blockDim.x) comb_add<CN>(P, S, sp, ipl[q], 1u, P.ipx_rep[a + q]);
+        } else {
+            batched<PV_CB_U>(z - a, [&](uint64_t j) { return ipl[j]; }, [&](uint64_t j, uint64_t e) {
+                if (e) comb_add<CN>(P, S, sp, e, 1u, (uint32_t)(a + j));
+            });
+        }
     }
     __syncthreads();
     // the table's entries per region (the spilled ones were counted as they spilled)

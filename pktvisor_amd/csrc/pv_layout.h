@@ -398,6 +398,15 @@ struct PvParams {
     PV_G PvNewName *nn;
     uint32_t nn_cap;
     PV_G uint64_t *iplog; // dense IP log: one entry per record of the batch (Net pass)
+    // compact IP log of the register-window Net pass (ip_compact): the IPv4 address of each
+    // record (0: no entry), its direction bit per 64-record tile, and per grid workgroup range
+    // the other entries (IPv6 keys of general-path records) in iplog at the range's base
+    PV_G uint32_t *iplog32;
+    PV_G uint64_t *ipdir;
+    PV_G uint32_t *ipx_cnt;
+    PV_G uint32_t *ipx_rep; // the exception entries' record indices (names of IPv6 keys)
+    uint64_t ip_base;     // slot << 60 | TM_IPV4 << 56 | cardinality << 33: the entries' common bits
+    uint32_t ip_compact;
     PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
     PV_G uint64_t *cb;    // combined update lists sorted by table region, mq_cap entries per workgroup
     PV_G uint32_t *cb_cnt;
