@@ -144,6 +144,7 @@ extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *of
                                          const uint32_t *idx, uint32_t stride, uint32_t n, const uint32_t *dst_off, uint8_t *out);
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel_sfx(const PvParams *P);
+extern "C" __global__ void pv_dns_kernel_f(const PvParams *P);
 extern "C" __global__ void pv_dns_suffix(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
@@ -3251,6 +3252,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         hipLaunchKernelGGL(pv_dns_suffix, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))
         hipLaunchKernelGGL(pv_dns_kernel_sfx, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    else if (P.f_flags)
+        hipLaunchKernelGGL(pv_dns_kernel_f, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     else
         hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);

@@ -688,7 +688,9 @@ __device__ bool dns_v1_filtered(PV_CREF(PvParams) P, const A &R, uint64_t m, uin
 // TAP: a dnstap event (DnsMetricsBucket::process_dnstap, :839-909): no filters, l3 / l4 from
 // the socket fields (flags bit 4: l3 unknown; bits 5-6: 0 UDP, 1 TCP, 2 other), the query
 // port as the port (top_udp_ports only when non-zero), no transaction event.
-template <bool TCP, bool TAP = false, bool SFX = true, class A, class Cache>
+// FILT: the DNS filter blocks compiled in (the common pass of an unfiltered context has none:
+// their code would cost it registers even when no filter is set)
+template <bool TCP, bool TAP = false, bool SFX = true, bool FILT = true, class A, class Cache>
 __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, uint32_t *mq_n, uint32_t *nev,
                                             uint32_t *nresp, uint64_t ebase, const A &R, const DnsMsg &dm, bool own,
                                             DnsCtr &c)
@@ -741,7 +743,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         P.events[e] = ev;
         P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
     };
-    if ((P.f_flags & PVDF_V2) && !TAP) {
+    if (FILT && (P.f_flags & PVDF_V2) && !TAP) {
         // DnsStreamHandler::_filtering, DNS v2 (dns/v2/DnsStreamHandler.cpp:484-609): the
         // direction filters for both, the rcode / answer / DNSSEC / qtype filters on responses,
         // the qname filters on queries; no input predicate (every DNS packet is an event)
@@ -779,7 +781,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             emit(true, true);
             return;
         }
-    } else if (P.f_flags && !TAP) {
+    } else if (FILT && P.f_flags && !TAP) {
         // a TCP message takes no input predicate: _filtering applies only_rcode and only_qname
         // to it as ordinary filters (_predicate_filter_type stays FiltersMAX, :546-551,593-602)
         if (!TCP && (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) && !dns_predicates(P, R, m, dlen, w0, w1, w2)) return;
@@ -2156,29 +2158,7 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                                    : 0ull;
         if (PV_LEAN_LEVEL == 4) {
             hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
-            if (tops) {
-            if (compact) {
-                // the IPv4 entry as its address and a direction bit; anything else (an IPv6
-                // key of a general-path record) into the range's exception list
-                const bool v4 = ek && (ek >> 32 & ~1ull) == (P.ip_base >> 32);
-                const uint64_t xm = __ballot(active && ek && !v4);
-                if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
-                const uint64_t dm1 = __ballot(v4 && ((ek >> 32) & 1));
-                if (lane == 0) P.ipdir[t] = dm1;
-                if (xm) {
-                    uint32_t q = 0;
-                    if (lane == 0) q = atomicAdd(&S.nx, (uint32_t)__popcll(xm));
-                    q = __builtin_amdgcn_readlane(q, 0);
-                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(xm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xm, 0u));
-                    if (active && ek && !v4) {
-                        P.iplog[wbeg * PV_WT + q + below] = ek;
-                        P.ipx_rep[wbeg * PV_WT + q + below] = (uint32_t)i;
-                    }
-                }
-            } else if (active) {
-                P.iplog[i] = ek;
-            }
-        }
+            if (tops && active) P.iplog[i] = ek;
             return;
         }
         if (card && !tops) {
@@ -2241,7 +2221,29 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                 dd[1] = dm.b;
             }
         }
-        if (tops && active) P.iplog[i] = ek;
+        if (tops) {
+            if (compact) {
+                // the IPv4 entry as its address and a direction bit; anything else (an IPv6
+                // key of a general-path record) into the range's exception list
+                const bool v4 = ek && ((ek >> 32) & ~1ull) == (P.ip_base >> 32);
+                const uint64_t xm = __ballot(active && ek && !v4);
+                if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
+                const uint64_t dbit = __ballot(v4 && ((ek >> 32) & 1));
+                if (lane == 0) P.ipdir[t] = dbit;
+                if (xm) {
+                    uint32_t q = 0;
+                    if (lane == 0) q = atomicAdd(&S.nx, (uint32_t)__popcll(xm));
+                    q = __builtin_amdgcn_readlane(q, 0);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(xm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xm, 0u));
+                    if (active && ek && !v4) {
+                        P.iplog[wbeg * PV_WT + q + below] = ek;
+                        P.ipx_rep[wbeg * PV_WT + q + below] = (uint32_t)i;
+                    }
+                }
+            } else if (active) {
+                P.iplog[i] = ek;
+            }
+        }
         if (temit) {
             const uint64_t tm = __ballot(istcp);
             if (tm) {
@@ -2373,7 +2375,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_suffix(const PvParams *
 #ifndef PV_DNS_MINW
 #define PV_DNS_MINW 1 // tuning: waves per SIMD the DNS pass's register allocation must allow
 #endif
-template <bool SFX>
+template <bool SFX, bool FILT>
 __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
@@ -2436,7 +2438,7 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
         if (active) {
             const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
             const bool own = P.dslot_of[dm.period] == wslot;
-            dns_process<false, false, SFX>(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
+            dns_process<false, false, SFX, FILT>(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
         }
     }
     if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
@@ -2451,12 +2453,17 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
 }
 extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel(const PvParams *__restrict__ Pp)
 {
-    dns_pass<false>(Pp);
+    dns_pass<false, false>(Pp);
+}
+// a context with DNS filters (v1 or v2), no suffix
+extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel_f(const PvParams *__restrict__ Pp)
+{
+    dns_pass<false, true>(Pp);
 }
 // only_qname_suffix / public_suffix_list runs: suffix sizes of any length (agg_domain_r)
 extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel_sfx(const PvParams *__restrict__ Pp)
 {
-    dns_pass<true>(Pp);
+    dns_pass<true, true>(Pp);
 }
 
 // ------------------------------------------------------------------ Net v2
