@@ -229,6 +229,113 @@ struct Jsf32 {
         return d;
     }
 };
+// One manager's deep-sampling draws, generated ahead by a producer thread: the draw sequence
+// depends on nothing but the seed and the rate, so the bits (1 = deep: jsf32() % 100 < rate,
+// AbstractMetricsManager::new_event :318-323) are ready before a batch needs them and the
+// batch's serial work is a bit copy (Net: one draw per record) or a bit read per event (DNS).
+class DrawStream {
+  public:
+    ~DrawStream() { stop(); }
+    // the generator state the next start() draws from (a fresh Jsf32, or one stepped past a
+    // shard's earlier draws)
+    void reset(const Jsf32 &from)
+    {
+        stop();
+        seed_ = from;
+    }
+    // the next draw (starting the producer at `rate` on first use)
+    bool next(uint32_t rate)
+    {
+        if (!th_.joinable()) start(rate);
+        if (tail_ == avail_) wait_more();
+        const uint64_t k = tail_++;
+        return (bits_[(k / 64) % kWords] >> (k % 64)) & 1;
+    }
+    // n draws as not-deep bits: bit i of out (32-bit words, zeroed by the caller) set when
+    // draw i is not deep
+    void take_not_deep(uint32_t rate, uint32_t *out, uint64_t n)
+    {
+        if (!th_.joinable()) start(rate);
+        for (uint64_t i = 0; i < n;) {
+            if (tail_ == avail_) wait_more();
+            const uint64_t k = tail_, o = k % 64;
+            const uint64_t m = std::min<uint64_t>({64 - o, n - i, avail_ - tail_});
+            uint64_t v = ~(bits_[(k / 64) % kWords] >> o);
+            if (m < 64) v &= (1ull << m) - 1;
+            for (uint64_t b = 0; b < m;) {
+                const uint64_t oi = i + b, ob = oi % 32, take = std::min<uint64_t>(32 - ob, m - b);
+                out[oi / 32] |= (uint32_t)(((v >> b) & ((1ull << take) - 1)) << ob);
+                b += take;
+            }
+            tail_ += m;
+            i += m;
+        }
+    }
+
+  private:
+    static constexpr uint64_t kWords = 1u << 19; // at most 32M draws ahead
+    static constexpr uint64_t kChunk = 1024;     // words the producer writes per round
+    void start(uint32_t rate)
+    {
+        rng_ = seed_;
+        rate_ = rate;
+        bits_.assign(kWords, 0);
+        head_ = tail_ = avail_ = done_ = 0;
+        quit_ = false;
+        th_ = std::thread([this] { produce(); });
+    }
+    void stop()
+    {
+        if (!th_.joinable()) return;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // publish what was consumed (the producer may reuse those words) and wait for more draws
+    void wait_more()
+    {
+        std::unique_lock<std::mutex> g(mu_);
+        done_ = tail_;
+        cv_.notify_all();
+        cv_.wait(g, [&] { return head_ > tail_; });
+        avail_ = head_;
+    }
+    void produce()
+    {
+        for (;;) {
+            uint64_t h;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                // never overwrite the word holding the consumer's next draw
+                cv_.wait(g, [&] { return quit_ || head_ / 64 + kChunk <= done_ / 64 + kWords; });
+                if (quit_) return;
+                h = head_ / 64;
+            }
+            for (uint64_t j = 0; j < kChunk; j++) {
+                uint64_t v = 0;
+                for (int b = 0; b < 64; b++) v |= (uint64_t)(rng_.next() % 100u < rate_) << b;
+                bits_[(h + j) % kWords] = v;
+            }
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                head_ = (h + kChunk) * 64;
+            }
+            cv_.notify_all();
+        }
+    }
+    Jsf32 seed_, rng_;
+    uint32_t rate_ = 100;
+    std::vector<uint64_t> bits_;
+    uint64_t head_ = 0, tail_ = 0, avail_ = 0, done_ = 0; // draw counts: produced, consumed, visible, released
+    bool quit_ = false;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::thread th_;
+};
+
 struct Window {
     std::deque<uint32_t> slots; // front = live bucket
     int64_t next_shift_sec = 0;
@@ -562,7 +669,7 @@ struct pv_ctx {
     // deep sampling (deep_sample_rate < 100): each manager's generator, the span's "not deep"
     // bitmaps (Net by record, DNS by the record of its event), pinned staging + device copies
     uint32_t sample_rate = 100;
-    Jsf32 rng_net, rng_dns;
+    DrawStream draws_net, draws_dns;
     bool dns_deep_now = true;   // the DNS manager's _deep_sampling_now (a filtered event counts it)
     uint64_t plan_draws = 0;    // DNS draws (unfiltered DNS events) pv_dns_event_seconds_host counted
     uint64_t *d_fbits = nullptr, *h_fbits = nullptr;   // per record: a filtered DNS event (sampling)
@@ -2267,8 +2374,8 @@ int pv_reset(pv_ctx *c)
     }
     c->started = c->ended = false;
     c->records_seen = 0;
-    c->rng_net = Jsf32();
-    c->rng_dns = Jsf32();
+    c->draws_net.reset(Jsf32());
+    c->draws_dns.reset(Jsf32());
     c->dns_deep_now = true;
     c->xvals_host.clear();
     c->xvals_synced = 0;
@@ -3086,24 +3193,33 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         uint32_t *hn = c->h_ndeep, *hd = c->h_ndeep + words;
         memset(hn, 0, words * 8);
         auto dns_draw = [&](bool filtered) {
-            if (!filtered) c->dns_deep_now = c->rng_dns.next() % 100u < c->sample_rate;
+            if (!filtered) c->dns_deep_now = c->draws_dns.next(c->sample_rate);
             return c->dns_deep_now;
         };
         const uint64_t olo = a * 4, ohi = (a + n) * 4;
         auto it = std::lower_bound(c->tcp_items.begin(), c->tcp_items.end(), std::make_pair(olo, 0u));
-        for (uint64_t i = 0; i < n; i++) {
-            if (!(c->rng_net.next() % 100u < c->sample_rate)) hn[i >> 5] |= 1u << (i & 31);
-            if ((c->h_dbits[i >> 6] >> (i & 63)) & 1) {
-                const bool f = filt && ((c->h_fbits[i >> 6] >> (i & 63)) & 1);
-                if (!dns_draw(f)) hd[i >> 5] |= 1u << (i & 31);
-            }
-            // the messages a TCP record completes (ord (a + i) * 4 + sub)
-            for (; it != c->tcp_items.end() && it->first < ohi && (it->first >> 2) == a + i; ++it) {
+        c->draws_net.take_not_deep(c->sample_rate, hn, n);
+        // the DNS events in stream order: each DNS-port UDP record, then the messages a TCP
+        // record completes (ord (a + i) * 4 + sub) after the records before it
+        auto tcp_upto = [&](uint64_t rec_end) {
+            for (; it != c->tcp_items.end() && it->first < ohi && (it->first >> 2) < a + rec_end; ++it) {
                 const uint32_t q = it->second;
                 const bool f = filt && ((c->h_tfbits[q >> 6] >> (q & 63)) & 1);
                 if (!dns_draw(f)) c->h_ntcp[q >> 5] |= 1u << (q & 31);
             }
+        };
+        for (uint64_t w = 0; w < (n + 63) / 64; w++) {
+            uint64_t m = c->h_dbits[w];
+            if (w == (n - 1) / 64 && n % 64) m &= (1ull << (n % 64)) - 1;
+            while (m) {
+                const uint64_t i = w * 64 + __builtin_ctzll(m);
+                m &= m - 1;
+                tcp_upto(i);
+                const bool f = filt && ((c->h_fbits[i >> 6] >> (i & 63)) & 1);
+                if (!dns_draw(f)) hd[i >> 5] |= 1u << (i & 31);
+            }
         }
+        tcp_upto(n);
         if (!hip_ok(e = hipMemcpyAsync(c->d_ndeep, c->h_ndeep, words * 8, hipMemcpyHostToDevice, st)) ||
             (nmsg && !hip_ok(e = hipMemcpyAsync(c->d_ntcp, c->h_ntcp, ((size_t)nmsg / 32 + 1) * 4, hipMemcpyHostToDevice, st))))
             return c->hipfail(e, "deep sampling bitmaps");
@@ -5569,8 +5685,11 @@ int pv_sample_skip(pv_ctx *c, uint64_t net_draws, uint64_t dns_draws)
     std::lock_guard<std::mutex> g(c->mu);
     if (c->records_seen) return c->fail(PV_EINVAL, "pv_sample_skip after the first batch");
     if (c->sample_rate >= 100) return 0;
-    for (uint64_t k = 0; k < net_draws; k++) c->rng_net.next();
-    for (uint64_t k = 0; k < dns_draws; k++) c->dns_deep_now = c->rng_dns.next() % 100u < c->sample_rate;
+    Jsf32 rn, rd;
+    for (uint64_t k = 0; k < net_draws; k++) rn.next();
+    for (uint64_t k = 0; k < dns_draws; k++) c->dns_deep_now = rd.next() % 100u < c->sample_rate;
+    c->draws_net.reset(rn);
+    c->draws_dns.reset(rd);
     return 0;
 }
 
