@@ -183,7 +183,8 @@ def dns2_start(cfg: dict) -> dict:
     """DnsStreamHandler v2 start (src/handlers/dns/v2/DnsStreamHandler.cpp:43-236) up to the
     signal wiring: {"groups": bits | GROUPS_SET, "filters": pv_dns_filters fields (v2) or None,
     "xact_ttl_ms": int|None}. The geo / ASN filters (no MaxMind database), dnstap_msg_type (no
-    v2 dnstap path), public_suffix_list and top_ecs are not built for the GPU v2 handler."""
+    v2 dnstap path) and public_suffix_list are not built for the GPU v2 handler; top_ecs keeps
+    its geo / ASN tops empty (no MaxMind database)."""
     from pktvisor_amd import dns_filter_config
     validate_configs(cfg, DNS2_CONFIG_DEFS)
     groups = process_groups(cfg, DNS2_GROUP_DEFS, DNS2_DEFAULT_GROUPS)
@@ -203,8 +204,6 @@ def dns2_start(cfg: dict) -> dict:
                                           f"direction: {d}")
                 dis &= ~{"in": 1, "out": 2, "unknown": 4}[d]
             filters["xact_dirs_disabled"] = dis
-    if groups & DNS2_GROUP_DEFS["top_ecs"]:
-        raise ConfigException("top_ecs is not supported by the GPU DNS v2 handler")
     ttl = None
     if "xact_ttl_ms" in cfg:
         ttl = _uint(cfg, "xact_ttl_ms")

@@ -169,7 +169,7 @@ extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" __global__ void pv_xact_carry(const PvXactParams *X);
 extern "C" __global__ void pv_xact_defer(const uint64_t *skeys, const uint32_t *svals, const PvXEvent *events, uint32_t n,
-                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at);
+                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at, const uint64_t *eecs, uint64_t *pecs);
 extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, uint32_t n_pend,
                                            uint32_t at);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
@@ -529,6 +529,7 @@ struct pv_ctx {
     int cus = 256;
     int wg_per_cu = 3;     // grid workgroups per CU (the batch's partition)
     int reg_wg_per_cu = 1; // workgroups per CU of the register-window Net pass
+    int dns_wg_per_cu = 1; // resident workgroups per CU of the DNS pass (its register count)
     const char *net_kernel = "none"; // the Net-pass kernel the last span launched (pv_net_kernel_name)
     uint64_t *d_dq = nullptr; // DNS work lists (32-B messages)
     uint32_t *d_dq_cnt = nullptr;
@@ -542,6 +543,8 @@ struct pv_ctx {
     // DNS queries still open at the end of the last batch (double-buffered), in sort-key
     // rank order; ranks of later records count from pend_base
     PvXEvent *d_pend[2] = {nullptr, nullptr};
+    // DNS v2 top_ecs: the ECS address of each query event, and of each carried query
+    uint64_t *d_eecs = nullptr, *d_pecs[2] = {nullptr, nullptr};
     uint64_t *d_pkeys[2] = {nullptr, nullptr};
     uint32_t pend_cur = 0;
     uint64_t n_pend = 0, pend_cap = 0;
@@ -1304,7 +1307,7 @@ void dns2_json(pv_ctx *c, Json &j, const HostBucket &b)
             const std::pair<const char *, uint64_t> ctr[] = {
                 {"xacts", c2[D2_XACTS]}, {"udp_xacts", c2[D2_UDP]}, {"tcp_xacts", c2[D2_TCP]}, {"dot_xacts", 0},
                 {"doh_xacts", 0}, {"dnscrypt_udp_xacts", 0}, {"dnscrypt_tcp_xacts", 0}, {"doq_xacts", 0},
-                {"ipv4_xacts", c2[D2_V4]}, {"ipv6_xacts", c2[D2_V6]}, {"nxdomain_xacts", c2[D2_NX]}, {"ecs_xacts", 0},
+                {"ipv4_xacts", c2[D2_V4]}, {"ipv6_xacts", c2[D2_V6]}, {"nxdomain_xacts", c2[D2_NX]}, {"ecs_xacts", c2[D2_ECS]},
                 {"refused_xacts", c2[D2_REFUSED]}, {"srvfail_xacts", c2[D2_SRVFAIL]}, {"noerror_xacts", c2[D2_NOERROR]},
                 {"nodata_xacts", c2[D2_NODATA]}, {"authenticated_data_xacts", c2[D2_AD]},
                 {"authoritative_answer_xacts", c2[D2_AA]}, {"checking_disabled_xacts", c2[D2_CD]},
@@ -1318,6 +1321,12 @@ void dns2_json(pv_ctx *c, Json &j, const HostBucket &b)
         }
         if (g & PV_DNS2_TOP_PORTS)
             top_json(j, "top_udp_ports_xacts", dense_tops(&b.sum[PV_OFF_PORT2 + x * PV_PORT_BINS], PV_PORT_BINS, 0), topn, pct);
+        if (g & PV_DNS2_TOP_ECS) {
+            // geo / ASN of the subnet need a MaxMind database; none is enabled (HandlerModulePlugin::city/asn)
+            j.key("top_geo_loc_ecs_xacts").arr(); j.end_arr();
+            j.key("top_asn_ecs_xacts").arr(); j.end_arr();
+            top_json(j, "top_ecs_xacts", tops(TM_ECS), topn, pct);
+        }
         if (g & PV_DNS2_TOP_RCODES) {
             top_json(j, "top_nxdomain_xacts", tops(TM_NX), topn, pct);
             top_json(j, "top_refused_xacts", tops(TM_REFUSED), topn, pct);
@@ -1881,7 +1890,7 @@ void dns2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
             p.gauge("dns_ipv4_xacts", "Total DNS transactions (query/reply pairs) received over IPv4", c2[D2_V4]);
             p.gauge("dns_ipv6_xacts", "Total DNS transactions (query/reply pairs) received over IPv6", c2[D2_V6]);
             p.gauge("dns_nxdomain_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code NXDOMAIN", c2[D2_NX]);
-            p.gauge("dns_ecs_xacts", "Total DNS transactions (query/reply pairs) with the EDNS Client Subnet option set", 0);
+            p.gauge("dns_ecs_xacts", "Total DNS transactions (query/reply pairs) with the EDNS Client Subnet option set", c2[D2_ECS]);
             p.gauge("dns_refused_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code REFUSED", c2[D2_REFUSED]);
             p.gauge("dns_srvfail_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code SRVFAIL", c2[D2_SRVFAIL]);
             p.gauge("dns_noerror_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code NOERROR", c2[D2_NOERROR]);
@@ -1898,6 +1907,9 @@ void dns2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
         if (g & PV_DNS2_TOP_PORTS)
             p.topn("dns_top_udp_ports_xacts", "port", "Top UDP source port on the query side of a transaction",
                    dense_tops(&b.sum[PV_OFF_PORT2 + x * PV_PORT_BINS], PV_PORT_BINS, 0), topn, pct);
+        if (g & PV_DNS2_TOP_ECS)
+            // geo / ASN of the subnet: no MaxMind database, those TopNs write nothing
+            p.topn("dns_top_ecs_xacts", "ecs", "Top EDNS Client Subnet (ECS) observed in DNS transaction", tops(TM_ECS), topn, pct);
         if (g & PV_DNS2_TOP_RCODES) {
             p.topn("dns_top_nxdomain_xacts", "qname", "Top QNAMES with result code NXDOMAIN", tops(TM_NX), topn, pct);
             p.topn("dns_top_refused_xacts", "qname", "Top QNAMES with result code REFUSED", tops(TM_REFUSED), topn, pct);
@@ -2174,10 +2186,6 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     if (c->cfg.dns2_groups) {
         c->dns2_groups = PV_N2G_ON | ((c->cfg.dns2_groups & PV_GROUPS_SET) ? (c->cfg.dns2_groups & 0x3ffu)
                                                                            : PV_DNS2_DEFAULT_GROUPS);
-        if (c->dns2_groups & PV_DNS2_TOP_ECS) {
-            *out = c;
-            return c->fail(PV_EUNSUPPORTED, "DNS v2 top_ecs is not built");
-        }
         // v1's DNS pass runs for the events (and their counts) only
         c->dns_groups = PV_DNS_TRANSACTIONS;
     }
@@ -2222,6 +2230,13 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         c->wg_per_cu = 3;
         if (const char *w = getenv("PV_NET_WGCU")) c->wg_per_cu = std::max(1, atoi(w));
         if (const char *w = getenv("PV_REG_WGCU")) c->reg_wg_per_cu = std::max(1, atoi(w));
+        {
+            int nb = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_dns_kernel), 64 * PV_DNS_WAVES, 0) == hipSuccess &&
+                nb > 0)
+                c->dns_wg_per_cu = nb;
+        }
+        if (const char *w = getenv("PV_DNS_WGCU")) c->dns_wg_per_cu = std::max(1, atoi(w));
     }
     // event / DNS work-list regions: main workgroups own wt_per_block * 64 slots each (the
     // last may overhang the batch by < wt_per_block tiles), boundary workgroups 64 each
@@ -2269,6 +2284,10 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipHostMalloc((void **)&c->h_tab_live, PV_TABLES * 4, hipHostMallocDefault)) ||
         !hip_ok(e = hipMalloc(&c->d_theta, ((size_t)1 << c->reg_log2) * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_ovf, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
+        ((c->dns2_groups & PV_DNS2_TOP_ECS) &&
+         (!hip_ok(e = hipMalloc(&c->d_eecs, (size_t)ev_cap * 8)) ||
+          !hip_ok(e = hipMalloc(&c->d_pecs[0], (size_t)(c->pend_cap + mr) * 8)) ||
+          !hip_ok(e = hipMalloc(&c->d_pecs[1], (size_t)(c->pend_cap + mr) * 8)))) ||
         !hip_ok(e = hipMalloc(&c->d_ovf2, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
         !hip_ok(e = hipMalloc(&c->d_ovf_cnt, 8)) || !hip_ok(e = hipMemsetAsync(c->d_ovf_cnt, 0, 8, c->stream)) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_ovf, 8, hipHostMallocDefault)) ||
@@ -2319,7 +2338,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
                     c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_ovf_cnt, c->d_iplog32,
-                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt};
+                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_eecs, c->d_pecs[0], c->d_pecs[1]};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
     for (void *hp : {(void *)c->h_ovf, (void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
@@ -2979,7 +2998,8 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
     if (dns_here && !pair && c->n_pend + nev_b > c->pend_cap) pair = true; // compact the carried list
     if (dns_here && !pair) {
         hipLaunchKernelGGL(pv_xact_defer, dim3((nev_b + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
-                           c->d_events, nev_b, c->d_pend[c->pend_cur], c->d_pkeys[c->pend_cur], (uint32_t)c->n_pend);
+                           c->d_events, nev_b, c->d_pend[c->pend_cur], c->d_pkeys[c->pend_cur], (uint32_t)c->n_pend,
+                           c->d_eecs, c->d_pecs[c->pend_cur]);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_defer");
         c->n_pend += nev_b;
     }
@@ -3019,6 +3039,8 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         X.n_valid = c->d_nvals + 1;
         X.pend = c->d_pend[c->pend_cur];
         X.pend_out = c->d_pend[c->pend_cur ^ 1];
+        X.pecs = c->d_pecs[c->pend_cur];
+        X.pecs_out = c->d_pecs[c->pend_cur ^ 1];
         X.pkeys_out = c->d_pkeys[c->pend_cur ^ 1];
         X.n_pend_out = c->d_nvals + 2;
         X.orph = c->d_orph;
@@ -3253,6 +3275,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.arena_cap = c->arena_cap;
     P.tab_live = c->d_tab_live; // global_add counts the entries it creates
     P.events = c->d_events;
+    P.eecs = c->d_eecs;
     P.ekeys = c->d_ekeys;
     P.blk_events = c->d_blk_events;
     P.skeys = c->d_skeys;
@@ -3366,12 +3389,14 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
     if (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))
         hipLaunchKernelGGL(pv_dns_suffix, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    // the DNS pass walks the logical grid's ranges with its resident grid
+    const uint32_t dns_grid = std::min<uint32_t>(grid, (uint32_t)(c->cus * c->dns_wg_per_cu));
     if (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))
-        hipLaunchKernelGGL(pv_dns_kernel_sfx, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+        hipLaunchKernelGGL(pv_dns_kernel_sfx, dim3(dns_grid), dim3(64 * PV_DNS_WAVES), 0, st, (const PvParams *)c->d_params);
     else if (P.f_flags)
-        hipLaunchKernelGGL(pv_dns_kernel_f, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+        hipLaunchKernelGGL(pv_dns_kernel_f, dim3(dns_grid), dim3(64 * PV_DNS_WAVES), 0, st, (const PvParams *)c->d_params);
     else
-        hipLaunchKernelGGL(pv_dns_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+        hipLaunchKernelGGL(pv_dns_kernel, dim3(dns_grid), dim3(64 * PV_DNS_WAVES), 0, st, (const PvParams *)c->d_params);
     if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates into a list sorted by table region, merge
     // each region's runs in LDS, decode the names of new entries
@@ -4456,6 +4481,7 @@ int pv_check_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
         P.arena_cap = c->arena_cap;
         P.tab_live = c->d_tab_live; // global_add counts the entries it creates
         P.events = c->d_events;
+        P.eecs = c->d_eecs;
         P.gbase = c->global_base + c->records_seen;
         P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
         P.flags = c->d_status + ST_FLAGS;

@@ -246,10 +246,27 @@ __device__ __forceinline__ uint64_t v1_ip6_key(const A &R, uint64_t a)
 struct NameSrc {
     const PV_G uint8_t *recs;
     const PV_G uint32_t *offs;
+    uint64_t ecs_addr; // an ECS name given directly (ecs_fam 1 / 2): no record to decode
+    uint32_t ecs_fam;
 };
 __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, uint32_t metric, uint32_t rep,
                                             const NameSrc *ns = nullptr, uint64_t key = 0)
 {
+    const uint32_t part = (blockIdx.x * 7 + threadIdx.x / 64) & (PV_ARENA_PARTS - 1);
+    const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
+    const uint32_t tab = PV_TSLOT(slot, metric);
+    unsigned long long *top = (unsigned long long *)&P.arena_top[tab * PV_ARENA_PARTS + part];
+    uint8_t *arena = P.arena + (uint64_t)tab * P.arena_cap;
+    // an ECS address: family byte + 16 address bytes (the host formats it)
+    auto ecs_name = [&](uint32_t fam, uint64_t addr) -> uint32_t {
+        uint64_t pos = atomicAdd(top, 20ull);
+        if (pos + 20 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
+        pos += part * pcap;
+        arena[pos] = 17; arena[pos + 1] = 0; arena[pos + 2] = (uint8_t)fam;
+        for (int i = 0; i < 16; i++) arena[pos + 3 + i] = i < 8 ? (uint8_t)(addr >> (8 * i)) : 0;
+        return (uint32_t)pos + 1;
+    };
+    if (ns && ns->ecs_fam) return ecs_name(ns->ecs_fam, ns->ecs_addr);
     Parsed o;
     const GAcc R{ns ? ns->recs : P.recs};
     if (ns) {
@@ -259,11 +276,6 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     } else {
         parse_record(R, P, P.offs[rep], o);
     }
-    const uint32_t part = (blockIdx.x * 7 + threadIdx.x / 64) & (PV_ARENA_PARTS - 1);
-    const uint64_t pcap = P.arena_cap / PV_ARENA_PARTS;
-    const uint32_t tab = PV_TSLOT(slot, metric);
-    unsigned long long *top = (unsigned long long *)&P.arena_top[tab * PV_ARENA_PARTS + part];
-    uint8_t *arena = P.arena + (uint64_t)tab * P.arena_cap;
     if (metric == TM_IPV6) {
         const uint64_t a = P.tap ? (v1_ip6_key(R, o.v6 + 8) == (key & ((1ull << 55) - 1)) ? o.v6 + 8 : o.v6 + 24)
                                  : ip6_name_addr(R, o, key);
@@ -278,15 +290,10 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     uint64_t m = o.l4off + 8;
     uint32_t len = o.l4len - 8;
     if (metric == TM_ECS) {
-        // the query's ECS address: family byte + 16 address bytes (the host formats it)
+        // the query's ECS address
         uint64_t addr = 0;
         const uint32_t fam = dns_ecs(R, m, len, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8), be16(R, m + 10), addr);
-        uint64_t pos = atomicAdd(top, 20ull);
-        if (pos + 20 > pcap) { atomicOr(P.flags, PVF_ARENA_FULL); return 0; }
-        pos += part * pcap;
-        arena[pos] = 17; arena[pos + 1] = 0; arena[pos + 2] = (uint8_t)fam;
-        for (int i = 0; i < 16; i++) arena[pos + 3 + i] = i < 8 ? (uint8_t)(addr >> (8 * i)) : 0;
-        return (uint32_t)pos + 1;
+        return ecs_name(fam, addr);
     }
     NameStats st;
     st.init();
@@ -431,15 +438,16 @@ struct KeyCache {
     }
 };
 
-// Top-N updates the LDS cache does not absorb go to the workgroup's HBM update log
-// (fire-and-forget stores, slot in key bits 60..63); the top-N merge kernels apply the
-// logs to the global tables after the parse kernels, so no lane waits on an HBM round trip for
-// a table update.
+// Top-N updates the LDS cache does not absorb go to the update log of the grid range being
+// processed (fire-and-forget stores, slot in key bits 60..63); the top-N merge kernels apply
+// the logs to the global tables after the parse kernels, so no lane waits on an HBM round trip
+// for a table update. mq_n: the range's LDS log count, then the range (a workgroup may walk
+// several ranges of the logical grid).
 __device__ __forceinline__ void log_put(PV_CREF(PvParams) P, uint32_t *mq_n, uint32_t slot, uint64_t key, uint32_t w,
                                         uint32_t rep)
 {
     const uint32_t q = atomicAdd(mq_n, 1u);
-    PV_G uint64_t *e = P.mq + ((uint64_t)blockIdx.x * P.mq_cap + q) * 2;
+    PV_G uint64_t *e = P.mq + ((uint64_t)mq_n[1] * P.mq_cap + q) * 2;
     e[0] = (key & ((1ull << 60) - 1)) | ((uint64_t)slot << 60);
     e[1] = (uint64_t)w | ((uint64_t)rep << 32);
 }
@@ -716,7 +724,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     const uint32_t ordr = (TCP || TAP) ? dm.pad - P.ord_base : (i << 2);
     // the message's transaction event (filtered: a DNS v2 event its filters rejected, which
     // still opens or ends a transaction, DnsMetricsManager::process_filtered, dns/v2 ...cpp:1147-1174)
-    auto emit = [&](bool deep, bool filtered) {
+    auto emit = [&](bool deep, bool filtered, uint32_t efam, uint64_t eaddr) {
         if (!P.want_events || TAP) return;
         // the workgroup's event region; LDS counter, order irrelevant (sorted by key, index)
         const uint64_t e = ebase + atomicAdd(nev, 1u);
@@ -738,7 +746,8 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             const uint32_t dir = dm.flags & 3;
             const uint32_t xd = dir == 2 ? 2u : (qr ? dir ^ 1u : dir);
             ev.key |= (uint64_t)(xd + 1) << 48;
-            ev.pad = (uint8_t)(((w0 >> 28) & 1) | ((dm.flags & 4) ? 2u : 0u) | (filtered ? 4u : 0u));
+            ev.pad = (uint8_t)(((w0 >> 28) & 1) | ((dm.flags & 4) ? 2u : 0u) | (filtered ? 4u : 0u) | (efam << 3));
+            if (efam) P.eecs[e] = eaddr;
         }
         P.events[e] = ev;
         P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
@@ -778,7 +787,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                     if (P.dns2_groups & PV_D2G_COUNTERS) sum_add(P, slot, PV_OFF_DNS + DC_FILTERED, 1);
                 }
             }
-            emit(true, true);
+            emit(true, true, 0, 0);
             return;
         }
     } else if (FILT && P.f_flags && !TAP) {
@@ -936,7 +945,15 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         }
         }
     }
-    emit(deep, false);
+    if (!TAP && (P.dns2_groups & PV_D2G_TOP_ECS) && !qr && ar) {
+        // DNS v2 top_ecs: the query's EDNS Client Subnet rides with its transaction event (the
+        // subnet DnsMetricsManager::process_dns_layer hands start_transaction, dns/v2 ...cpp:1131-1144)
+        uint64_t addr;
+        const uint32_t fam = dns_ecs(R, m, dlen, qd, ancount, ns, ar, addr);
+        emit(deep, false, fam, addr);
+        return;
+    }
+    emit(deep, false, 0, 0);
 }
 
 // Flush a workgroup's key cache: hashed keys to the update log, dense keys to HBM.
@@ -968,9 +985,9 @@ static_assert(PV_NCACHE <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cach
 #endif
 #define PV_NOH 0xffffffffu
 struct DnsState {
-    uint32_t stage[4][PV_WSTAGE / 4];
+    uint32_t stage[PV_DNS_WAVES][PV_WSTAGE / 4];
     KeyCache<PV_NCACHE> C;
-    uint32_t mq_n;
+    uint32_t mq_n[2]; // the range's update-log count, the range
     uint32_t nev, nresp;
 };
 
@@ -2375,93 +2392,104 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_suffix(const PvParams *
 #ifndef PV_DNS_MINW
 #define PV_DNS_MINW 1 // tuning: waves per SIMD the DNS pass's register allocation must allow
 #endif
+// The DNS pass: each workgroup (PV_DNS_WAVES waves, one resident per CU at this kernel's register
+// count) walks ranges of the logical grid (lb = blockIdx.x, + gridDim.x), so the grid's three
+// ranges per CU are three per workgroup and no partial round of workgroups idles part of the
+// chip. Per range: its DNS list, its event region and update log; the key cache and the register
+// counters span the workgroup's ranges (the cache is flushed once, into the last range's log).
 template <bool SFX, bool FILT>
 __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ DnsState S;
     S.C.clear();
-    if (threadIdx.x == 0) { S.mq_n = P.mq_cnt[blockIdx.x]; S.nev = 0; S.nresp = 0; }
-    __syncthreads();
+    if (threadIdx.x == 0) S.nresp = 0;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t *L = S.stage[wave];
-    const uint32_t nd = P.dq_cnt[blockIdx.x];
-    const uint64_t region = (uint64_t)blockIdx.x * P.wt_per_block * PV_WT;
-    const PV_G DnsMsg *Q = reinterpret_cast<const PV_G DnsMsg *>(P.dq) + region;
-    const uint32_t ntl = (nd + PV_WT - 1) / PV_WT;
     DnsCtr c;
     c.zero();
     uint32_t wslot = 0xffffffffu;
-    // message and window loads are unconditional (clamped index; an inactive lane's copy is
-    // never read), so every iteration issues the same number of loads in the same order and
-    // the compiler's vmcnt waits stay exact instead of falling back to vmcnt(0)
-    auto msg = [&](uint32_t t) -> DnsMsg { return Q[min(t * PV_WT + lane, nd - 1)]; };
-    uint32_t t = wave;
-    DnsMsg m_cur{}, m_n{};
-    uint4 pf[8];
-    auto issue = [&](const DnsMsg &d, bool) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + ((uint64_t)d.moff & ~15ull));
+    for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
+        if (threadIdx.x == 0) { S.mq_n[0] = P.mq_cnt[lb]; S.mq_n[1] = lb; S.nev = 0; }
+        __syncthreads();
+        const uint32_t nd = P.dq_cnt[lb];
+        const uint64_t region = (uint64_t)lb * P.wt_per_block * PV_WT;
+        const PV_G DnsMsg *Q = reinterpret_cast<const PV_G DnsMsg *>(P.dq) + region;
+        const uint32_t ntl = (nd + PV_WT - 1) / PV_WT;
+        // message and window loads are unconditional (clamped index; an inactive lane's copy is
+        // never read), so every iteration issues the same number of loads in the same order and
+        // the compiler's vmcnt waits stay exact instead of falling back to vmcnt(0)
+        auto msg = [&](uint32_t t) -> DnsMsg { return Q[min(t * PV_WT + lane, nd - 1)]; };
+        constexpr uint32_t NW = PV_DNS_WAVES;
+        uint32_t t = wave;
+        DnsMsg m_cur{}, m_n{};
+        uint4 pf[8];
+        auto issue = [&](const DnsMsg &d, bool) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + ((uint64_t)d.moff & ~15ull));
 #pragma unroll
-        for (int j = 0; j < 8; j++) pf[j] = src[j];
-    };
-    if (t < ntl) {
-        m_cur = msg(t);
-        issue(m_cur, t * PV_WT + lane < nd);
-        m_n = msg(t + 4);
-    }
-    for (; t < ntl; t += 4) {
-        t = __builtin_amdgcn_readfirstlane(t);
-        const bool active = t * PV_WT + lane < nd;
-        const DnsMsg dm = m_cur;
+            for (int j = 0; j < 8; j++) pf[j] = src[j];
+        };
+        if (t < ntl) {
+            m_cur = msg(t);
+            issue(m_cur, t * PV_WT + lane < nd);
+            m_n = msg(t + NW);
+        }
+        for (; t < ntl; t += NW) {
+            t = __builtin_amdgcn_readfirstlane(t);
+            const bool active = t * PV_WT + lane < nd;
+            const DnsMsg dm = m_cur;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            L[(4 * j + 0) * PV_WT + lane] = pf[j].x;
-            L[(4 * j + 1) * PV_WT + lane] = pf[j].y;
-            L[(4 * j + 2) * PV_WT + lane] = pf[j].z;
-            L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
+            for (int j = 0; j < 8; j++) {
+                L[(4 * j + 0) * PV_WT + lane] = pf[j].x;
+                L[(4 * j + 1) * PV_WT + lane] = pf[j].y;
+                L[(4 * j + 2) * PV_WT + lane] = pf[j].z;
+                L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
+            }
+            if (t + NW < ntl) {
+                // the message after next is loaded before the next windows: loads retire in
+                // issue order, so the register moves of the message rotation then wait for
+                // the message alone, never for the windows still in flight
+                const DnsMsg m_nn = msg(t + 2 * NW);
+                issue(m_n, (t + NW) * PV_WT + lane < nd);
+                m_cur = m_n;
+                m_n = m_nn;
+            }
+            // the wave's register counters follow the slot of its first message
+            const uint32_t s0 = P.dslot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
+            if (s0 != wslot) {
+                if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
+                wslot = s0;
+            }
+            if (active) {
+                const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
+                const bool own = P.dslot_of[dm.period] == wslot;
+                dns_process<false, false, SFX, FILT>(P, &S.C, S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
+            }
         }
-        if (t + 4 < ntl) {
-            // the message after next is loaded before the next windows: loads retire in
-            // issue order, so the register moves of the message rotation then wait for
-            // the message alone, never for the windows still in flight
-            const DnsMsg m_nn = msg(t + 8);
-            issue(m_n, (t + 4) * PV_WT + lane < nd);
-            m_cur = m_n;
-            m_n = m_nn;
+        __syncthreads();
+        if (lb + gridDim.x >= P.grid_main) {
+            cache_flush(P, S.C, PV_NCACHE, S.mq_n);
+            __syncthreads();
         }
-        // the wave's register counters follow the slot of its first message
-        const uint32_t s0 = P.dslot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
-        if (s0 != wslot) {
-            if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
-            wslot = s0;
-        }
-        if (active) {
-            const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
-            const bool own = P.dslot_of[dm.period] == wslot;
-            dns_process<false, false, SFX, FILT>(P, &S.C, &S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
+        if (threadIdx.x == 0) {
+            P.mq_cnt[lb] = S.mq_n[0];
+            P.blk_events[lb] = S.nev;
         }
     }
     if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
-    __syncthreads();
-    cache_flush(P, S.C, PV_NCACHE, &S.mq_n);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        P.mq_cnt[blockIdx.x] = S.mq_n;
-        P.blk_events[blockIdx.x] = S.nev;
-        if (S.nresp) atomicAdd(P.n_events + 1, S.nresp);
-    }
+    if (threadIdx.x == 0 && S.nresp) atomicAdd(P.n_events + 1, S.nresp);
 }
-extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel(const PvParams *__restrict__ Pp)
+extern "C" __global__ void __launch_bounds__(64 * PV_DNS_WAVES, PV_DNS_MINW) pv_dns_kernel(const PvParams *__restrict__ Pp)
 {
     dns_pass<false, false>(Pp);
 }
 // a context with DNS filters (v1 or v2), no suffix
-extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel_f(const PvParams *__restrict__ Pp)
+extern "C" __global__ void __launch_bounds__(64 * PV_DNS_WAVES, PV_DNS_MINW) pv_dns_kernel_f(const PvParams *__restrict__ Pp)
 {
     dns_pass<false, true>(Pp);
 }
 // only_qname_suffix / public_suffix_list runs: suffix sizes of any length (agg_domain_r)
-extern "C" __global__ void __launch_bounds__(256, PV_DNS_MINW) pv_dns_kernel_sfx(const PvParams *__restrict__ Pp)
+extern "C" __global__ void __launch_bounds__(64 * PV_DNS_WAVES, PV_DNS_MINW) pv_dns_kernel_sfx(const PvParams *__restrict__ Pp)
 {
     dns_pass<true, true>(Pp);
 }
@@ -2487,12 +2515,12 @@ struct Net2State {
     KeyCache<PV_NCACHE> C;
     uint32_t ctr[PV_MAX_SHIFTS + 1][PV_NET2_CTRS];
     uint32_t hist[3][PV_N2_HBINS];
-    uint32_t mq_n;
+    uint32_t mq_n[2];
 };
 __device__ __forceinline__ void n2_key(PV_CREF(PvParams) P, Net2State &S, uint32_t slot, uint64_t key, uint32_t idx)
 {
     uint32_t first;
-    if (!S.C.add((key & ((1ull << 60) - 1)) | ((uint64_t)slot << 60), 1, idx, first)) log_put(P, &S.mq_n, slot, key, 1, idx);
+    if (!S.C.add((key & ((1ull << 60) - 1)) | ((uint64_t)slot << 60), 1, idx, first)) log_put(P, S.mq_n, slot, key, 1, idx);
 }
 __device__ __forceinline__ void n2_coupon(PV_CREF(PvParams) P, Net2State &S, uint32_t slot, uint32_t dir, uint32_t coupon,
                                           uint32_t idx)
@@ -2508,7 +2536,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_net2_kernel(const PvParams 
     S.C.clear();
     for (uint32_t i = threadIdx.x; i < (PV_MAX_SHIFTS + 1) * PV_NET2_CTRS; i += blockDim.x) (&S.ctr[0][0])[i] = 0;
     for (uint32_t i = threadIdx.x; i < 3 * PV_N2_HBINS; i += blockDim.x) (&S.hist[0][0])[i] = 0;
-    if (threadIdx.x == 0) S.mq_n = P.mq_cnt[blockIdx.x];
+    if (threadIdx.x == 0) { S.mq_n[0] = P.mq_cnt[blockIdx.x]; S.mq_n[1] = blockIdx.x; }
     __syncthreads();
     const uint32_t g = P.net2_groups;
     const bool card = g & PV_N2G_CARDINALITY, tops = g & PV_N2G_TOP_IPS;
@@ -2585,10 +2613,10 @@ extern "C" __global__ void __launch_bounds__(256) pv_net2_kernel(const PvParams 
         const uint32_t slot = (uint32_t)(k >> 60), lm = (uint32_t)(k >> 56) & 15;
         const uint64_t pay = k & 0x00ffffffffffffffULL;
         if (lm == LM2_CPC) cpc_min(P, slot, CPC_V2 + (uint32_t)(pay >> 17), (uint32_t)(pay & 0x1ffff), (int64_t)(P.gbase + S.C.rep[j]));
-        else log_put(P, &S.mq_n, slot, PV_KEY(lm, pay), S.C.cnt[j], S.C.rep[j]);
+        else log_put(P, S.mq_n, slot, PV_KEY(lm, pay), S.C.cnt[j], S.C.rep[j]);
     }
     __syncthreads();
-    if (threadIdx.x == 0) P.mq_cnt[blockIdx.x] = S.mq_n;
+    if (threadIdx.x == 0) P.mq_cnt[blockIdx.x] = S.mq_n[0];
 }
 
 // ------------------------------------------------------------------ top-N merge
@@ -3602,7 +3630,7 @@ __device__ void slow_check(PV_CREF(PvXactParams) X, uint32_t idx, uint32_t perio
 // response's transaction direction xd; qe is its query. Name tops and dense tables go
 // straight to the period's tables (v2 keys carry the direction).
 __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e, const PvXEvent &qe, uint32_t xd,
-                          uint64_t us, int64_t order)
+                          uint64_t us, int64_t order, uint64_t qaddr)
 {
     PV_CREF(PvParams) P = X.P;
     const uint32_t g = P.dns2_groups;
@@ -3645,6 +3673,14 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
     dns_parse(R, m, len, qd, an, ns, ar, d);
     if (!d.ok) return;
     sum_add(P, slot, PV_OFF_RCODE2 + xd * PV_RCODE_BINS + rcode, 1);
+    // top_ecs (:1077-1089): the query's subnet, past the resources parse and with or without a
+    // question; its name record straight from the carried address
+    const uint32_t qfam = (qe.pad >> 3) & 3;
+    if ((g & PV_D2G_TOP_ECS) && qfam) {
+        if (g & PV_D2G_COUNTERS) atomicAdd(&c[D2_ECS], 1u);
+        const NameSrc es{nullptr, nullptr, qaddr, qfam};
+        global_add(P, slot, PV_V2_DKEY(TM_ECS, xd, fmix64(qaddr ^ ((uint64_t)qfam << 62) ^ 0xec5ull)), 1, idx, &es);
+    }
     if (!d.has_query) return;
     NameStats st;
     st.init();
@@ -3716,6 +3752,12 @@ __device__ __forceinline__ PvXEvent xev(PV_CREF(PvXactParams) X, uint32_t p)
 {
     const uint32_t v = X.svals[p];
     return (v & PV_PEND_FLAG) ? X.pend[v & ~PV_PEND_FLAG] : X.events[v];
+}
+// the ECS address of a DNS v2 query event (top_ecs), carried or of this batch
+__device__ __forceinline__ uint64_t xecs(PV_CREF(PvXactParams) X, uint32_t p)
+{
+    const uint32_t v = X.svals[p];
+    return (v & PV_PEND_FLAG) ? X.pecs[v & ~PV_PEND_FLAG] : X.P.eecs[v];
 }
 
 __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
@@ -3842,7 +3884,7 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         }
         // the response's first-occurrence order (the DNS pass's CPC order: batch base * 4 + rank)
         const int64_t order = (int64_t)((P.gbase << 2) + ((uint32_t)X.skeys[p] - (P.ekey_base << 2)));
-        dns2_xact(X, T, e, qe, xd, us, order);
+        dns2_xact(X, T, e, qe, xd, us, order, ((qe.pad >> 3) & 3) ? xecs(X, q) : 0ull);
     } else {
         const uint32_t kp = purge_period(P, X.ttl_s, e.period, e.sec);
         if (!kp) return;
@@ -3914,17 +3956,20 @@ extern "C" __global__ void pv_xact_carry(const PvXactParams *__restrict__ Xp)
     e.period = 0;
     const uint32_t k = atomicAdd(X.n_pend_out, 1u);
     X.pend_out[k] = e;
+    if (X.pecs_out) X.pecs_out[k] = ((e.pad >> 3) & 3) ? xecs(X, p) : 0ull;
     X.pkeys_out[k] = (uint64_t)h << 32;
 }
 // A batch with queries only and no period shift pairs nothing: its events join the
 // carried list unresolved, in rank order behind the earlier ones.
 extern "C" __global__ void pv_xact_defer(const uint64_t *skeys, const uint32_t *svals, const PvXEvent *events, uint32_t n,
-                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at)
+                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at, const uint64_t *eecs, uint64_t *pecs)
 {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
-    pend[at + j] = events[svals[j]];
+    const uint32_t v = svals[j];
+    pend[at + j] = events[v];
     pkeys[at + j] = skeys[j];
+    if (pecs) pecs[at + j] = ((events[v].pad >> 3) & 3) ? eecs[v] : 0ull;
 }
 // the carried list's keys behind this batch's compacted keys, values flagged
 extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, uint32_t n_pend,

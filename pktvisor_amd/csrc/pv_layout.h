@@ -19,6 +19,9 @@
 
 #define PV_SLOTS 16  // per handler: num_periods (<= 10) live + PV_MAX_SHIFTS new in one batch
 #define PV_TABLES (2 * PV_SLOTS)
+#ifndef PV_DNS_WAVES
+#define PV_DNS_WAVES 8 // DNS pass: waves per workgroup (one resident workgroup per CU at its register count)
+#endif
 #define PV_MAX_SHIFTS 6 // period shifts per handler inside one device batch (the host splits longer batches)
 #define PV_MAX_SUBNETS 16
 // name arena partitions per slot: workgroup b allocates from partition b % PV_ARENA_PARTS,
@@ -80,7 +83,7 @@
 #define PV_OFF_RCODE (PV_OFF_QTYPE + PV_QTYPE_BINS)
 // DNS v2 (src/handlers/dns/v2), in place of v1 when configured: per transaction direction
 // (0 in, 1 out, 2 unknown) its counters, then its port / qtype / rcode tables
-#define PV_DNS2_CTRS 16
+#define PV_DNS2_CTRS 20
 #define PV_OFF_DNS2 (PV_OFF_RCODE + PV_RCODE_BINS)              // + dir * PV_DNS2_CTRS
 #define PV_OFF_PORT2 (PV_OFF_DNS2 + 4 * PV_DNS2_CTRS)           // + dir * PV_PORT_BINS
 #define PV_OFF_QTYPE2 (PV_OFF_PORT2 + 3 * PV_PORT_BINS)         // + dir * PV_QTYPE_BINS
@@ -96,7 +99,7 @@ enum {
 // the responses and purge time-outs that set the direction up (DnsMetricsBucket::dir_setup)
 enum {
     D2_SEEN = 0, D2_XACTS, D2_UDP, D2_TCP, D2_V4, D2_V6, D2_NX, D2_REFUSED, D2_SRVFAIL, D2_NOERROR, D2_NODATA, D2_AA,
-    D2_AD, D2_CD, D2_TIMEOUT, D2_ORPHAN, D2_N
+    D2_AD, D2_CD, D2_TIMEOUT, D2_ORPHAN, D2_ECS, D2_N
 };
 // Net v2 counters (src/handlers/net/v2/NetStreamHandler.h:61-96): base events, then per
 // direction d (0 in, 1 out, 2 unknown) at N2_DIR + 8 d
@@ -365,6 +368,7 @@ struct PvParams {
     PV_G uint64_t *fbits;      // deep sampling with DNS filters: one bit per record (pv_dns_prescan) or per
                                // TCP message (pv_dns_tcp_filter), set for an event _filtering rejects
     PV_G PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
+    PV_G uint64_t *eecs;       // DNS v2 top_ecs: the ECS address of a query event (pad bits 3-4: family)
     PV_G uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
     PV_G uint32_t *blk_events; // events appended by each workgroup
     PV_G uint64_t *skeys;      // packed keys (sort input)
@@ -476,6 +480,8 @@ struct PvXactParams {
     // queries still open after this batch to pend_out / pkeys_out, counting n_pend_out
     const PV_G PvXEvent *pend;
     PV_G PvXEvent *pend_out;
+    const PV_G uint64_t *pecs; // DNS v2 top_ecs: ECS addresses of the carried queries (pend), and of pend_out
+    PV_G uint64_t *pecs_out;
     PV_G uint64_t *pkeys_out;
     PV_G uint32_t *n_pend_out;
     // shard-edge stubs: responses that are the first event of their (flow, txid) in this

@@ -4,7 +4,7 @@ the sorted event keys, accounting on the response in pv_xact_resolve (dns2_xact)
 
 The reference's own v2 KATs (test_dns_layer.cpp v2 :57-302) run through the GPU path in
 test_gpu_kat.py; these cases cover every fixture (UDP and TCP), synthetic query/response
-mixes with all rcodes, every group but top_ecs (not built), period shifts with time-outs,
+mixes with all rcodes, every group (top_ecs: the query's subnet carried with its event), period shifts with time-outs,
 per-direction p90 slow tops, and transactions carried across many small batches."""
 import os
 
@@ -16,9 +16,9 @@ from pktvisor_amd import synth
 from tests.test_gpu_parity import FIXTURES, GOLD, diff
 
 pytestmark = pytest.mark.gpu
-ALL = 0x3ff & ~(1 << 3)  # every v2 group but top_ecs
-ALL_NAMES = ["cardinality", "counters", "quantiles", "top_qtypes", "top_rcodes", "top_size", "top_qnames", "top_ports",
-             "xact_times"]
+ALL = 0x3ff  # every v2 group
+ALL_NAMES = ["cardinality", "counters", "quantiles", "top_ecs", "top_qtypes", "top_rcodes", "top_size", "top_qnames",
+             "top_ports", "xact_times"]
 DEFAULT = 1 | 2 | 4 | 16 | 32 | 128
 
 
@@ -87,6 +87,31 @@ def test_dns2_small_batches(oracle):
     finally:
         h.close()
     ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=1, window=1, dns2_groups=ALL)
+    assert diff(gpu["dns"], ref["1m"]["dns"]) is None, diff(gpu["dns"], ref["1m"]["dns"])
+
+
+@pytest.mark.parametrize("most", [1, 3])
+def test_dns2_ecs_carried(oracle, most):
+    """top_ecs with the queries in earlier batches than their responses: the subnet rides in the
+    carried list (pv_xact_defer / pv_xact_carry) to the response's resolve"""
+    pcap = open(os.path.join(GOLD, "ecs.pcap"), "rb").read()
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    offs = list(idx.offsets) + [len(recs)]
+    h = pa.PvHandlers(num_periods=1, max_records=64, dns2_config={"enable": ALL_NAMES})
+    try:
+        rng = np.random.default_rng(most)
+        i = 0
+        while i < idx.n:
+            j = min(idx.n, i + int(rng.integers(1, most + 1)))
+            h.process_host(recs[offs[i]:offs[j]])
+            i = j
+        h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+        gpu = h.window_json(0)
+    finally:
+        h.close()
+    ref = oracle.run_bytes(pcap, host_spec="", num_periods=1, window=1, dns2_groups=ALL)
+    assert gpu["dns"]["unknown"]["ecs_xacts"] == 2
     assert diff(gpu["dns"], ref["1m"]["dns"]) is None, diff(gpu["dns"], ref["1m"]["dns"])
 
 
