@@ -1102,11 +1102,12 @@ struct Engine {
     float per90_2[3] = {0.0f, 0.0f, 0.0f};
     uint32_t ttl_s = 0, ttl_ms = 0;
     float to90 = 0.0f, from90 = 0.0f;
-    Sampler net_s, dns_s; // the Net and DNS managers' generators
+    Sampler net_s, dns_s;   // the Net and DNS managers' generators
+    Sampler net2_s, dns2_s; // the v2 managers' own (same default seed: jsf32 default-constructed)
 
     explicit Engine(const Config &c) : cfg(c), net(c.num_periods), net2(c.num_periods), dns(c.num_periods), dns2(c.num_periods)
     {
-        net_s.rate = dns_s.rate = c.deep_sample_rate;
+        net_s.rate = dns_s.rate = net2_s.rate = dns2_s.rate = c.deep_sample_rate;
         // TransactionManager.h:60-68
         if (c.xact_ttl_ms > 1000) { ttl_s = c.xact_ttl_ms / 1000; ttl_ms = c.xact_ttl_ms - ttl_s * 1000; }
         else ttl_ms = c.xact_ttl_ms;
@@ -1184,10 +1185,13 @@ struct Engine {
     // Deep path (deep_sample_rate 100): toHost keeps the source address, fromHost the
     // destination, unknown both; an address counts only when the packet's l3 matches its
     // layer and it is not the unspecified address (isValid)
+    // Not deep (deep_sample_rate < 100, :494-500): process_net_layer(dir, l3, l4, size), the
+    // counters without SYN and the payload size
     void net2_packet(const Pkt &p)
     {
+        const bool deep = net2_s.draw(true);
         net2.maybe_shift(p.ts);
-        net2.new_event(true);
+        net2.new_event(deep);
         Net2Bucket &b = net2.live();
         const int d = p.dir == DIR_TO_HOST ? 0 : (p.dir == DIR_FROM_HOST ? 1 : 2);
         Net2Dir &x = b.dir[d];
@@ -1198,10 +1202,11 @@ struct Engine {
             if (p.l3 == L3_IPV6) x.IPv6++;
             else if (p.l3 == L3_IPV4) x.IPv4++;
             if (p.l4 == L4_UDP) x.UDP++;
-            else if (p.l4 == L4_TCP) { x.TCP++; if (p.syn) x.TCP_SYN++; }
+            else if (p.l4 == L4_TCP) { x.TCP++; if (p.syn && deep) x.TCP_SYN++; }
             else x.OtherL4++;
         }
         x.payload.update(p.caplen);
+        if (!deep) return;
         const bool card = g & N2G_CARDINALITY, tops = g & N2G_TOP_IPS;
         const bool want_src = d != 1, want_dst = d != 0;
         if (p.has_v4) {
@@ -1476,8 +1481,10 @@ struct Engine {
         const uint8_t *h = hm.d;
         const size_t suffix_size = 0;
         const bool filt = dns2_filtering(p, m, hdr12, qr, rcode, ancount);
+        // new_event(stamp) draws; process_filtered's new_event(stamp, false) keeps the last flag
+        const bool deep = dns2_s.draw(!filt);
         if (dns2.maybe_shift(p.ts)) on_dns2_period_shift(p.ts);
-        dns2.new_event(true);
+        dns2.new_event(deep);
         Dns2Bucket &b = dns2.live();
         const uint32_t g = cfg.dns2_groups;
         const XactKey k{p.flowkey, txid};
@@ -1536,6 +1543,7 @@ struct Engine {
                 if (h[2] & 0x04) x.AA++;
                 if (h[3] & 0x20) x.AD++;
             }
+            if (!deep) return; // new_dns_transaction v2 (:1006-1008): the rest only when deep
             if (q.query_size && (g & D2G_TOP_SIZE)) x.ratio.update((double)m.len / (double)q.query_size);
             if (p.port && (g & D2G_TOP_PORTS)) x.port.update(p.port);
             if (g & D2G_XACT_TIMES) x.time.update(us);

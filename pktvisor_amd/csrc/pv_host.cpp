@@ -2091,7 +2091,6 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
             if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
                 return c->hipfail(e, "only_qname_suffix record buffer");
         }
-        if (c->sample_rate < 100) return c->fail(PV_EUNSUPPORTED, "DNS filters with deep_sample_rate below 100 are not built");
         c->f_flags = fl;
         c->f_rcode_mask = mask;
         c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
@@ -2201,9 +2200,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     c->ovf_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2 * c->max_records, 1u << 16), 1ull << 28);
     // deep_sample_rate (AbstractMetricsManager::configure, src/AbstractMetricsManager.h:357-365: > 100 -> 100, < 1 -> 1)
     c->sample_rate = c->cfg.deep_sample_rate == 0 ? 100u : std::max(1u, std::min(c->cfg.deep_sample_rate, 100u));
-    if (c->sample_rate < 100 && (c->cfg.net_filter_all || c->net2_groups || c->dns2_groups)) {
+    if (c->sample_rate < 100 && c->cfg.net_filter_all) {
         *out = c;
-        return c->fail(PV_EUNSUPPORTED, "deep_sample_rate below 100 with geo filters or the v2 handlers is not built");
+        return c->fail(PV_EUNSUPPORTED, "deep_sample_rate below 100 with geo filters is not built");
     }
     // TransactionManager(ttl_ms) split (TransactionManager.h:60-68)
     if (c->cfg.xact_ttl_ms > 1000) { c->ttl_s = c->cfg.xact_ttl_ms / 1000; c->ttl_ms = c->cfg.xact_ttl_ms - c->ttl_s * 1000; }

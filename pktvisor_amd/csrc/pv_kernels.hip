@@ -689,6 +689,45 @@ __device__ bool dns_v1_filtered(PV_CREF(PvParams) P, const A &R, uint64_t m, uin
     if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) filt = dns_suffix_of(P, R, m, dlen, qd, ancount, ns, ar) == 0xffu;
     return filt;
 }
+// DnsStreamHandler::_filtering, v2 (dns/v2/DnsStreamHandler.cpp:484-609), for the deep-sampling
+// prescans: the filter block of dns_process's PVDF_V2 branch below, restated with the suffix
+// match computed here. dir: 0 toHost, 1 fromHost, 2 unknown.
+template <class A>
+__device__ bool dns_v2_filtered(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen, uint32_t mcap, uint32_t dir)
+{
+    uint32_t w0, w1, w2;
+    dns_header(R, m, mcap, w0, w1, w2);
+    const uint32_t qr = (w0 >> 23) & 1, rcode = (w0 >> 24) & 15;
+    const uint32_t qd = ((w1 & 0xff) << 8) | ((w1 >> 8) & 0xff);
+    const uint32_t ancount = ((w1 >> 8) & 0xff00) | (w1 >> 24);
+    const uint32_t ns = ((w2 & 0xff) << 8) | ((w2 >> 8) & 0xff);
+    const uint32_t ar = ((w2 >> 8) & 0xff00) | (w2 >> 24);
+    bool filt = (P.f_flags & PVDF2_NOUNK) && dir == 2;
+    if (!filt && qr) {
+        filt = ((P.f_flags & PVDF2_NOIN) && dir == 1) || ((P.f_flags & PVDF2_NOOUT) && dir == 0) ||
+               ((P.f_flags & PVDF2_RCODE) && !((P.f_rcode_mask >> rcode) & 1)) ||
+               ((P.f_flags & PVDF_ANSWER_COUNT) && ancount != P.f_ancount) ||
+               ((P.f_flags & PVDF_ONLY_DNSSEC) && (!ancount || !dns_dnssec(R, m, dlen, qd, ancount, ns, ar)));
+        if (!filt && (P.f_flags & PVDF_ONLY_QTYPE)) {
+            DnsInfo fd;
+            dns_parse(R, m, dlen, qd, ancount, ns, ar, fd);
+            bool hit = false;
+            for (uint32_t k = 0; k < P.f_nq; k++) hit |= fd.qtype == P.f_qt[k];
+            filt = !fd.ok || !fd.has_query || !hit;
+        }
+    } else if (!filt) {
+        filt = ((P.f_flags & PVDF2_NOIN) && dir == 0) || ((P.f_flags & PVDF2_NOOUT) && dir == 1);
+        if (!filt && (P.f_flags & PVDF2_QNAME)) filt = !dns_qname_listed(P, R, m, dlen, w1, w2);
+        if (!filt && (P.f_flags & PVDF_ONLY_QSUFFIX)) filt = dns_suffix_of(P, R, m, dlen, qd, ancount, ns, ar) == 0xffu;
+    }
+    return filt;
+}
+template <class A>
+__device__ __forceinline__ bool dns_filtered(PV_CREF(PvParams) P, const A &R, uint64_t m, uint32_t dlen, uint32_t mcap, bool tcp,
+                                             uint32_t dir)
+{
+    return (P.f_flags & PVDF_V2) ? dns_v2_filtered(P, R, m, dlen, mcap, dir) : dns_v1_filtered(P, R, m, dlen, mcap, tcp);
+}
 
 // DnsMetricsBucket::process_dns_layer (:910-1049) + the transaction event of one DNS
 // message, in the bucket of its DNS period. Counters go to `c` when `own` (this lane's
@@ -742,11 +781,13 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         if (P.dns2_groups) {
             // DNS v2: one transaction map per direction (DnsMetricsManager::_pair_manager); a
             // response looks in the swapped direction's map (dns/v2 ...cpp:1100-1145). pad: the
-            // query's CD bit, the message's l3 (bit 1: IPv6), bit 2: filtered
+            // query's CD bit, the message's l3 (bit 1: IPv6), bit 2: filtered, bits 3-4: the
+            // ECS family, bit 5: not deep (a response's draw decides new_dns_transaction's deep part)
             const uint32_t dir = dm.flags & 3;
             const uint32_t xd = dir == 2 ? 2u : (qr ? dir ^ 1u : dir);
             ev.key |= (uint64_t)(xd + 1) << 48;
-            ev.pad = (uint8_t)(((w0 >> 28) & 1) | ((dm.flags & 4) ? 2u : 0u) | (filtered ? 4u : 0u) | (efam << 3));
+            ev.pad = (uint8_t)(((w0 >> 28) & 1) | ((dm.flags & 4) ? 2u : 0u) | (filtered ? 4u : 0u) | (efam << 3) |
+                              (deep ? 0u : 32u));
             if (efam) P.eecs[e] = eaddr;
         }
         P.events[e] = ev;
@@ -778,12 +819,14 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             }
         }
         if (filt) {
-            // process_filtered: an event (sampled at rate 100), `filtered`, and the transaction
+            // process_filtered: an event counted deep when the manager's stale flag is (the
+            // not-deep bit deep sampling sets), `filtered`, and the transaction
+            const bool fdeep = !(dm.flags & 16);
             if (upd) {
-                if (own) c.dfilt++;
+                if (own) { c.dfilt++; c.dnd += !fdeep; }
                 else {
                     sum_add(P, slot, PV_OFF_DNS + DC_EVENTS, 1);
-                    sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
+                    if (fdeep) sum_add(P, slot, PV_OFF_DNS + DC_SAMPLES, 1);
                     if (P.dns2_groups & PV_D2G_COUNTERS) sum_add(P, slot, PV_OFF_DNS + DC_FILTERED, 1);
                 }
             }
@@ -2550,8 +2593,11 @@ extern "C" __global__ void __launch_bounds__(256) pv_net2_kernel(const PvParams 
         if (p < P.skip_before) continue; // a period already outside the window
         const uint32_t slot = P.slot_of[p];
         uint32_t *ctr = S.ctr[p];
+        // deep sampling: the v2 manager's draws equal v1's (same generator seed, one draw per
+        // packet); not deep: counters without SYN and the payload size only (net/v2 ...cpp:494-500)
+        const bool deep = !P.ndeep_net || !((P.ndeep_net[i >> 5] >> (i & 31)) & 1);
         atomicAdd(&ctr[N2_EVENTS], 1u);
-        atomicAdd(&ctr[N2_SAMPLES], 1u);
+        if (deep) atomicAdd(&ctr[N2_SAMPLES], 1u);
         Parsed o;
         parse_record(R, C, P, P.offs[i], o);
         const uint32_t d = o.dir;
@@ -2562,12 +2608,12 @@ extern "C" __global__ void __launch_bounds__(256) pv_net2_kernel(const PvParams 
         if (o.l4 == 17) atomicAdd(&dc[N2_UDP], 1u);
         else if (o.l4 == 6) {
             atomicAdd(&dc[N2_TCP], 1u);
-            if (o.syn) atomicAdd(&dc[N2_SYN], 1u);
+            if (o.syn && deep) atomicAdd(&dc[N2_SYN], 1u);
         } else atomicAdd(&dc[N2_OTHER], 1u);
         const uint32_t cl = min(o.caplen, 65535u);
         if (p == p0 && cl < PV_N2_HBINS) atomicAdd(&S.hist[d][cl], 1u);
         else sum_add(P, slot, PV_OFF_PAYLOAD2 + d * PV_PAYLOAD_BINS + cl, 1);
-        if (!(card || tops)) continue;
+        if (!(card || tops) || !deep) continue;
         const uint32_t idx = (uint32_t)i;
         if (o.has4) {
             if (o.l3 != 4) continue;
@@ -3346,7 +3392,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_prescan(const PvParams 
                 const uint64_t m = o.l4off + 8;
                 const uint64_t cap_end = o.frame + o.caplen;
                 const uint32_t mcap = cap_end > m ? (uint32_t)min<uint64_t>(cap_end - m, 65535) : 0u;
-                f = dns_v1_filtered(P, R, m, o.l4len - 8, mcap, false);
+                f = dns_filtered(P, R, m, o.l4len - 8, mcap, false, o.dir);
             }
             const uint64_t fb = __ballot(f);
             if ((threadIdx.x & 63) == 0) P.fbits[t] = fb;
@@ -3412,7 +3458,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp(const PvParams *__r
 
 // Deep sampling with DNS filters over the messages of the TCP stage (P: the TCP pass's block,
 // recs / offs the message records, dq the message list): bit j of fbits set when message j is
-// filtered (dns_v1_filtered), so the host knows which events draw.
+// filtered (dns_v1_filtered, or dns_v2_filtered in a DNS v2 context), so the host knows which
+// events draw.
 extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp_filter(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
@@ -3423,7 +3470,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp_filter(const PvPara
         bool f = false;
         if (j < P.tcp_nmsg) {
             const uint4 a = reinterpret_cast<const PV_G uint4 *>(P.dq)[2 * j];
-            f = dns_v1_filtered(P, R, a.y, a.z & 0xffff, a.z >> 16, true);
+            f = dns_filtered(P, R, a.y, a.z & 0xffff, a.z >> 16, true, (a.w >> 16) & 3);
         }
         const uint64_t fb = __ballot(f);
         if ((threadIdx.x & 63) == 0) P.fbits[t] = fb;
@@ -3664,6 +3711,8 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
         if (b23 & 0x04) atomicAdd(&c[D2_AA], 1u);
         if (b23 & 0x2000) atomicAdd(&c[D2_AD], 1u);
     }
+    // deep sampling: a response that drew "not deep" stops after the counters (:1006-1008)
+    if (e.pad & 32) return;
     if (qe.len && (g & PV_D2G_TOP_SIZE))
         xval(X, T, period, XV2_RATIO + xd, (uint64_t)__double_as_longlong((double)len / (double)qe.len));
     const uint32_t port = dns_port(R.u32(o.l4off));

@@ -3,7 +3,8 @@ manager in stream order; not-deep events count in the counters only; a not-deep 
 pairs but feeds no quantile, ratio or slow top): reference fixtures and a synthetic C4 capture
 over many ingest batches; DNS filters (a filtered event draws nothing and counts the manager's
 last flag, process_filtered) and DNS over TCP (messages draw in stream order among the UDP
-events). The v2 handlers with sampling are not built and fail loudly."""
+events), and the v2 handlers (Net v2's draws equal v1's; a DNS v2 response's draw decides
+new_dns_transaction's deep part; v2 filters draw nothing). Geo filters with sampling fail loudly."""
 import os
 
 import pytest
@@ -64,6 +65,60 @@ def test_sampled_tcp_synthetic(oracle, tmp_path, rate):
     assert diff(gpu, ref) is None, diff(gpu, ref)
 
 
+# ---- the v2 handlers (net/v2 ...cpp:494-500,756-762; dns/v2 ...cpp:1006-1008,1092-1174)
+V2_ALL = ["cardinality", "counters", "quantiles", "top_ecs", "top_qtypes", "top_rcodes", "top_size", "top_qnames",
+          "top_ports", "xact_times"]
+
+
+@pytest.mark.parametrize("rate", [1, 50, 99])
+@pytest.mark.parametrize("periods", [1, 5])
+@pytest.mark.parametrize("fixture,host", [("dns_udp_tcp_random.pcap", "192.168.0.0/24"),
+                                          ("dns_udp_mixed_rcode.pcap", "192.168.0.0/26"), ("dns_ipv6_udp.pcap", "")])
+def test_v2_sampled_parity(oracle, tmp_path, fixture, host, rate, periods):
+    """Net v2 next to v1 and DNS v2, every v2 group, UDP and TCP DNS"""
+    pcap = open(os.path.join(GOLD, fixture), "rb").read()
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec=host or None, periods=periods, deep_sample_rate=rate, net2_config={},
+                             dns2_config={"enable": V2_ALL})
+    ref = oracle.run_bytes(pcap, host_spec=host, num_periods=periods, window=periods, deep_sample_rate=rate,
+                           net2_groups=0x1f, dns2_groups=0x3ff)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+V2_SAMPLED_FILTERS = [{"exclude_noerror": True}, {"only_qtype": ["AAAA", "TXT"]}, {"only_xact_directions": ["in"]},
+                      {"only_qname_suffix": ["test.com"]}]
+
+
+@pytest.mark.parametrize("rate", [1, 50, 99])
+@pytest.mark.parametrize("f", V2_SAMPLED_FILTERS, ids=[",".join(f) for f in V2_SAMPLED_FILTERS])
+def test_v2_sampled_filters(oracle, tmp_path, rate, f):
+    """DNS v2 filters with sampling: a filtered message draws nothing and counts the last flag"""
+    from tests.test_gpu_dns2 import oracle2_kw
+    pcap = open(os.path.join(GOLD, "dns_udp_tcp_random.pcap"), "rb").read()
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec="192.168.0.0/24", periods=5, deep_sample_rate=rate,
+                             dns2_config={"enable": V2_ALL, **f})
+    ref = oracle.run_bytes(pcap, host_spec="192.168.0.0/24", num_periods=5, window=5, deep_sample_rate=rate,
+                           dns2_groups=0x3ff, **oracle2_kw(f))
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("rate", [30, 90])
+def test_v2_sampled_synthetic_shifts(oracle, tmp_path, monkeypatch, rate):
+    """C4 traffic over several 60 s marks in 1 MiB ingest batches, Net v2 + DNS v2"""
+    monkeypatch.setenv("PV_INGEST_CHUNK_MB", "1")
+    pcap = synth.pcap_bytes(4, 80000, ts_step_us=2500)
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec=synth.HOST_SPEC, periods=5, deep_sample_rate=rate, net2_config={},
+                             dns2_config={"enable": V2_ALL})
+    ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5, deep_sample_rate=rate,
+                           net2_groups=0x1f, dns2_groups=0x3ff)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
 def test_sampling_refusals(tmp_path):
-    with pytest.raises(pa.PvError, match="v2 handlers"):
-        pa.PvHandlers(deep_sample_rate=50, dns2_config={})
+    with pytest.raises(pa.PvError, match="geo filters"):
+        pa.PvHandlers(deep_sample_rate=50, net_config={"geoloc_notfound": True})
