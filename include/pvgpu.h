@@ -155,6 +155,13 @@ typedef struct pv_dns_filters {
  * before the first batch; NULL clears. PV_EINVAL with the reference's ConfigException text
  * for an unknown rcode/qtype. */
 int pv_set_dns_filters(pv_ctx *ctx, const pv_dns_filters *f);
+
+/* PcapInputStream's "tcp_packet_reassembly_cache_limit" (src/inputs/pcap/PcapInputStream.cpp:97-99):
+ * the capacity of the LRU list of TCP connections (254-283,449-465); a connection start or a
+ * message delivery beyond it evicts the least recently used connection, which is closed
+ * (closeConnection). 0 (the default): the reference's DEFAULT_LRULIST_SIZE behaviour without
+ * the capacity check. Call before the first batch. */
+int pv_set_tcp_reassembly_limit(pv_ctx *ctx, uint64_t limit);
 /* Name or decimal -> code for kind 0 = rcode (RCodeNumbers) or 1 = qtype (QTypeNumbers),
  * case-insensitive, libs/visor_dns/dns.h:31-265; PV_EINVAL if unknown. Pure host function. */
 int pv_dns_code(int kind, const char *name, uint32_t *value);

@@ -359,6 +359,9 @@ struct Config {
     unsigned window = 5; // output window: 1 => single bucket 0 ("1m"), N>=2 => merged N ("Nm")
     size_t topn_count = 10;
     uint32_t xact_ttl_ms = 5000;
+    // PcapInputStream's tcp_packet_reassembly_cache_limit (PcapInputStream.cpp:97-99): the LRU
+    // list's capacity, DEFAULT_LRULIST_SIZE = TCP_TIMEOUT * 10000 without it (PcapInputStream.h:99)
+    uint64_t tcp_cache_limit = 30 * 10000;
     bool recorded_stream = true;
     // metric groups (StreamMetricsHandler::process_groups, src/StreamHandler.h:111-133), as the
     // handler's _groups bits: net v1 defaults (NetStreamHandler.cpp:53-56), dns v1 defaults
@@ -1677,7 +1680,6 @@ struct Engine {
     static constexpr size_t TCP_MAX_OOO = 50;
     static constexpr int64_t TCP_TIMEOUT = 30;       // PcapInputStream.h:97
     static constexpr int MAX_TCP_CLEANUPS = 100;     // PcapInputStream.h:98
-    static constexpr size_t LRU_SIZE = 30 * 10000;   // DEFAULT_LRULIST_SIZE
     std::unordered_map<uint32_t, TcpConn> tcp_conns;
     std::list<std::pair<uint32_t, TS>> lru; // VisorLRUList: front = most recently put
     std::unordered_map<uint32_t, std::list<std::pair<uint32_t, TS>>::iterator> lru_at;
@@ -1697,7 +1699,7 @@ struct Engine {
         if (it != lru_at.end()) lru.erase(it->second);
         lru.emplace_front(fk, t);
         lru_at[fk] = lru.begin();
-        if (lru_at.size() > LRU_SIZE) {
+        if (cfg.tcp_cache_limit && lru_at.size() > cfg.tcp_cache_limit) {
             uint32_t old = lru.back().first;
             lru_at.erase(old);
             lru.pop_back();
@@ -2330,6 +2332,7 @@ static bool parse_config(const char *s, Config &c, std::string &err)
         else if (k == "window") c.window = (unsigned)atoi(v.c_str());
         else if (k == "topn_count") c.topn_count = (size_t)atoll(v.c_str());
         else if (k == "xact_ttl_ms") c.xact_ttl_ms = (uint32_t)atoll(v.c_str());
+        else if (k == "tcp_packet_reassembly_cache_limit") c.tcp_cache_limit = (uint64_t)strtoull(v.c_str(), nullptr, 0);
         else if (k == "dns_details") { if (atoi(v.c_str())) c.dns_groups |= DG_TOP_QNAMES_DETAILS; }
         else if (k == "net_groups") c.net_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "dns_groups") c.dns_groups = (uint32_t)strtoul(v.c_str(), nullptr, 0);

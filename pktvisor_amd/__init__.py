@@ -170,7 +170,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
            "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name",
-           "pv_plan_dns_draws", "pv_sample_skip"]
+           "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit"]
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
@@ -256,6 +256,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_values_merge.argtypes = [P, P, ctypes.c_size_t]
     lib.pv_window_periods.argtypes = [P, ctypes.c_int, P, P, U32, ctypes.POINTER(U32)]
     lib.pv_set_dns_filters.argtypes = [P, ctypes.POINTER(pv_dns_filters)]
+    lib.pv_set_tcp_reassembly_limit.argtypes = [P, ctypes.c_uint64]
     lib.pv_dns_code.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(U32)]
     lib.pv_comm_unique_id.argtypes = [P]
     lib.pv_comm_init.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
@@ -435,7 +436,7 @@ class PvHandlers:
                  dns_filters: Optional[dict] = None, net_config: Optional[dict] = None,
                  dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0,
                  net2_config: Optional[dict] = None, dns2_config: Optional[dict] = None,
-                 deep_sample_rate: int = 100):
+                 deep_sample_rate: int = 100, tcp_packet_reassembly_cache_limit: int = 0):
         from pktvisor_amd import config as pvcfg
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
@@ -501,6 +502,10 @@ class PvHandlers:
                 f.n_qname_suffixes = len(sx)
                 f.qname_suffixes = ctypes.cast(self._qsfx, ctypes.POINTER(ctypes.c_char_p))
             self._check(self.lib.pv_set_dns_filters(self.ctx, ctypes.byref(f)), "pv_set_dns_filters")
+        if tcp_packet_reassembly_cache_limit:
+            # the pcap input's config (PcapInputStream.cpp:97-99)
+            self._check(self.lib.pv_set_tcp_reassembly_limit(self.ctx, int(tcp_packet_reassembly_cache_limit)),
+                        "pv_set_tcp_reassembly_limit")
 
     def _check(self, rc, what):
         if rc:

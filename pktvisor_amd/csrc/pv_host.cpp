@@ -30,6 +30,7 @@
 #include <cctype>
 #include <cstring>
 #include <deque>
+#include <list>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -194,6 +195,7 @@ enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNE
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
 #define PV_TRASH_WAVES 16384 // Net-pass waves with a 2-KiB trash area (grid <= 4096)
 #define ST_ALLOC 32
+#define ST_RB_WORDS (ST_ALLOC + PV_TABLES + 2) // status | tables' live counts | overflow words
 
 struct SlotMeta {
     int64_t start_sec = 0, start_nsec = 0, end_sec = 0, end_nsec = 0;
@@ -669,6 +671,14 @@ struct pv_ctx {
     bool tcp_active = false;  // a stage has run since the last reset
     bool tcp_pre = false;     // this batch's stage runs ahead of the Net pass (prescan emits)
     uint32_t tcp_nmsg = 0;    // messages of the current batch
+    // tcp_packet_reassembly_cache_limit (0: not set): PcapInputStream's LRU list of connections,
+    // replayed on the host across batches (front = most recently put; value = the put's second)
+    uint64_t tcp_limit = 0;
+    std::list<std::pair<uint32_t, uint32_t>> lru;
+    std::unordered_map<uint32_t, std::list<std::pair<uint32_t, uint32_t>>::iterator> lru_at;
+    std::unordered_map<uint32_t, bool> lru_pending; // evicted with no segment in their batch: closed at their next
+    uint32_t *d_lru_ev = nullptr, *d_fclose = nullptr;
+    uint64_t lru_ev_cap = 0, fclose_cap = 0;
     // deep sampling (deep_sample_rate < 100): each manager's generator, the span's "not deep"
     // bitmaps (Net by record, DNS by the record of its event), pinned staging + device copies
     uint32_t sample_rate = 100;
@@ -2035,6 +2045,14 @@ int pv_dns_code(int kind, const char *name, uint32_t *value)
     return PV_EINVAL;
 }
 
+int pv_set_tcp_reassembly_limit(pv_ctx *c, uint64_t limit)
+{
+    if (!c) return PV_EINVAL;
+    if (c->records_seen) return c->fail(PV_EINVAL, "tcp_packet_reassembly_cache_limit must be set before the first batch");
+    c->tcp_limit = limit;
+    return 0;
+}
+
 int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
 {
     if (!c) return PV_EINVAL;
@@ -2277,10 +2295,11 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
-        !hip_ok(e = hipMalloc(&c->d_status, ST_ALLOC * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_tab_live, PV_TABLES * 4)) ||
-        !hip_ok(e = hipMemsetAsync(c->d_tab_live, 0, PV_TABLES * 4, c->stream)) ||
-        !hip_ok(e = hipHostMalloc((void **)&c->h_tab_live, PV_TABLES * 4, hipHostMallocDefault)) ||
+        // one read-back block: the status words, the tables' live counts, the two overflow
+        // words (a batch reads them back with one copy)
+        !hip_ok(e = hipMalloc(&c->d_status, ST_RB_WORDS * 4)) ||
+        !hip_ok(e = (c->d_tab_live = c->d_status + ST_ALLOC, c->d_ovf_cnt = c->d_tab_live + PV_TABLES, hipSuccess)) ||
+        !hip_ok(e = hipMemsetAsync(c->d_status, 0, ST_RB_WORDS * 4, c->stream)) ||
         !hip_ok(e = hipMalloc(&c->d_theta, ((size_t)1 << c->reg_log2) * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_ovf, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
         ((c->dns2_groups & PV_DNS2_TOP_ECS) &&
@@ -2288,8 +2307,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
           !hip_ok(e = hipMalloc(&c->d_pecs[0], (size_t)(c->pend_cap + mr) * 8)) ||
           !hip_ok(e = hipMalloc(&c->d_pecs[1], (size_t)(c->pend_cap + mr) * 8)))) ||
         !hip_ok(e = hipMalloc(&c->d_ovf2, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
-        !hip_ok(e = hipMalloc(&c->d_ovf_cnt, 8)) || !hip_ok(e = hipMemsetAsync(c->d_ovf_cnt, 0, 8, c->stream)) ||
-        !hip_ok(e = hipHostMalloc((void **)&c->h_ovf, 8, hipHostMallocDefault)) ||
+
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
         !hip_ok(e = hipMalloc(&c->d_iplog, (size_t)(mr + 64) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_iplog32, (size_t)(mr + 64) * 4)) ||
@@ -2301,7 +2319,8 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_params, 2 * sizeof(PvParams))) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_params, 2 * sizeof(PvParams), hipHostMallocDefault)) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_xparams, sizeof(PvXactParams), hipHostMallocDefault)) ||
-        !hip_ok(e = hipHostMalloc((void **)&c->h_status, ST_ALLOC * 4, hipHostMallocDefault)) ||
+        !hip_ok(e = hipHostMalloc((void **)&c->h_status, ST_RB_WORDS * 4, hipHostMallocDefault)) ||
+        !hip_ok(e = (c->h_tab_live = c->h_status + ST_ALLOC, c->h_ovf = c->h_tab_live + PV_TABLES, hipSuccess)) ||
         !hip_ok(e = hipMalloc(&c->d_tseg, (size_t)c->tseg_cap * sizeof(PvTcpSeg))) ||
         !hip_ok(e = hipMalloc(&c->d_tmask, (size_t)(mr / 64 + 2) * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_tpm, (size_t)(mr / 64 + 2) * 4)) ||
@@ -2336,12 +2355,12 @@ void pv_destroy(pv_ctx *c)
                     c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
-                    c->d_tab_live, c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_ovf_cnt, c->d_iplog32,
-                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_eecs, c->d_pecs[0], c->d_pecs[1]};
+                    c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_iplog32,
+                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
-    for (void *hp : {(void *)c->h_ovf, (void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
-                     (void *)c->h_tparams, (void *)c->h_tab_live})
+    for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
+                     (void *)c->h_tparams})
         if (hp) hipHostFree(hp);
     for (auto &st : c->stage) {
         if (st.d_ix) hipFree(st.d_ix);
@@ -2377,6 +2396,9 @@ static void tcp_reset(pv_ctx *c)
     c->n_clist = 0;
     c->carry_used = 0;
     c->tcp_active = false;
+    c->lru.clear();
+    c->lru_at.clear();
+    c->lru_pending.clear();
 }
 
 int pv_reset(pv_ctx *c)
@@ -2581,7 +2603,8 @@ int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64
     flush_fills(c);
     PvParams P;
     params_common(c, P, d_recs, d_offs, n);
-    P.tcp_emit = tcp_emit ? 1u : 0u;
+    // 2: every TCP packet (tcp_packet_reassembly_cache_limit: the LRU holds every connection)
+    P.tcp_emit = tcp_emit ? (c->tcp_limit ? 3u : 1u) : 0u;
     if (fbits) P.fbits = c->d_fbits;
     hipError_t e;
     *c->h_params = P;
@@ -2640,6 +2663,77 @@ int tcp_alloc(pv_ctx *c)
     if (!hip_ok(e = hipMalloc(&c->d_tsort_tmp, c->tsort_tmp_bytes))) return c->hipfail(e, "TCP sort scratch");
     c->tcp_alloced = true;
     return 0;
+}
+
+// PcapInputStream's LRU list under tcp_packet_reassembly_cache_limit (PcapInputStream.cpp:97-99,
+// 254-283,449-465), replayed over the batch's segments in capture order from the dry run's
+// events (skey: sorted fkey << 32 | record index; ev: flags | dir << 8, second, latest TCP second
+// + 1 before the record). Before a segment, the cleanup of the earlier TCP packets: connections
+// whose last put is 30 s older than the latest TCP second leave (the device closes them at
+// their next packet by the same rule). A connection start and a message delivery put the
+// connection at the head; a new one beyond the limit evicts the tail, which the stage closes
+// after this record (closeConnection); a FIN/RST close or a time-out erases. An evicted
+// connection's later segments in the batch are ignored (Ignore_PacketOfClosedFlow). fclose gets,
+// at the evicted flow's first sorted segment, the record, its second and its direction.
+void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vector<uint32_t> &ev,
+                    std::vector<uint32_t> &fclose)
+{
+    const size_t n = skey.size();
+    std::vector<uint32_t> run0(n), order(n);
+    for (size_t k = 0; k < n; k++) {
+        run0[k] = (k && (skey[k] >> 32) == (skey[k - 1] >> 32)) ? run0[k - 1] : (uint32_t)k;
+        order[k] = (uint32_t)k;
+    }
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return (uint32_t)skey[a] < (uint32_t)skey[b]; });
+    auto erase = [&](uint32_t f) {
+        auto it = c->lru_at.find(f);
+        if (it == c->lru_at.end()) return;
+        c->lru.erase(it->second);
+        c->lru_at.erase(it);
+    };
+    std::unordered_map<uint32_t, uint32_t> evicted; // flow -> its first sorted segment
+    // connections evicted in an earlier batch that had no segment there: closed ahead of their
+    // first segment here
+    for (size_t k = 0; k < n && !c->lru_pending.empty(); k++) {
+        const uint32_t f = (uint32_t)(skey[k] >> 32);
+        if (run0[k] != k || !c->lru_pending.erase(f)) continue;
+        evicted[f] = (uint32_t)k;
+        fclose[3 * k] = PVT_FCLOSE_FIRST;
+        fclose[3 * k + 1] = ev[3 * k + 1];
+        fclose[3 * k + 2] = (ev[3 * k] >> 8) & 3;
+    }
+    for (uint32_t k : order) {
+        const uint32_t f = (uint32_t)(skey[k] >> 32), idx = (uint32_t)skey[k];
+        const uint32_t fl = ev[3 * k] & 0xff, dir = (ev[3 * k] >> 8) & 3, sec = ev[3 * k + 1], lt = ev[3 * k + 2];
+        if (evicted.count(f)) continue;
+        while (lt && !c->lru.empty() && lt - 1 >= c->lru.back().second + PV_TCP_TIMEOUT) {
+            c->lru_at.erase(c->lru.back().first);
+            c->lru.pop_back();
+        }
+        if (fl & (PVT_EV_NEW | PVT_EV_PUT)) {
+            erase(f);
+            c->lru.emplace_front(f, sec);
+            c->lru_at[f] = c->lru.begin();
+            if (c->lru_at.size() > c->tcp_limit) {
+                const uint32_t v = c->lru.back().first;
+                c->lru_at.erase(v);
+                c->lru.pop_back();
+                // the victim's first sorted segment; a flow with none in this batch is closed
+                // ahead of its next segment (lru_pending)
+                auto it = std::lower_bound(skey.begin(), skey.end(), (uint64_t)v << 32);
+                if (it != skey.end() && (uint32_t)(*it >> 32) == v) {
+                    const uint32_t r = run0[it - skey.begin()];
+                    evicted[v] = r;
+                    fclose[3 * r] = idx;
+                    fclose[3 * r + 1] = sec;
+                    fclose[3 * r + 2] = dir;
+                } else {
+                    c->lru_pending[v] = true;
+                }
+            }
+        }
+        if (fl & (PVT_EV_CLOSE | PVT_EV_TIMEOUT)) erase(f);
+    }
 }
 
 // The TCP stage of a batch: its segments (n_seg, seg_bytes payload) through reassembly and
@@ -2704,24 +2798,56 @@ int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t
     T.mq_cap = c->tmsg_cap;
     T.cnt = c->d_tcpcnt;
     flush_fills(c);
-    if (!hip_ok(e = hipMemsetAsync(c->d_tcpcnt, 0, PVT_WORDS * 4, st)) ||
-        !hip_ok(e = hipMemcpyAsync(c->d_tparams, c->h_tparams, sizeof T, hipMemcpyHostToDevice, st)))
-        return c->hipfail(e, "TCP stage upload");
     const PvTcpParams *dT = c->d_tparams;
-    hipLaunchKernelGGL(pv_tcp_scan, dim3(1), dim3(1024), 0, st, dT);
-    if (n_seg) {
-        const uint32_t blocks = (n_seg + 255) / 256;
-        hipLaunchKernelGGL(pv_tcp_keys, dim3(blocks), dim3(256), 0, st, (const PvTcpSeg *)c->d_tseg, n_seg, c->d_tkey[0],
-                           c->d_tval[0]);
-        size_t tmp = c->tsort_tmp_bytes;
-        if (!hip_ok(e = pv_tcp_sort(c->d_tsort_tmp, &tmp, c->d_tkey[0], c->d_tkey[1], c->d_tval[0], c->d_tval[1], n_seg, st)))
-            return c->hipfail(e, "TCP segment sort");
-        hipLaunchKernelGGL(pv_tcp_lookup, dim3(blocks), dim3(256), 0, st, dT);
-        hipLaunchKernelGGL(pv_tcp_insert, dim3(blocks), dim3(256), 0, st, dT);
-        hipLaunchKernelGGL(pv_tcp_flow, dim3(blocks), dim3(256), 0, st, dT);
-        if (c->n_clist) hipLaunchKernelGGL(pv_tcp_migrate, dim3((c->n_clist + 255) / 256), dim3(256), 0, st, dT);
+    const uint32_t blocks = (n_seg + 255) / 256;
+    // one run of the stage's kernels (dry: the cache-limit replay's recording run)
+    auto run = [&](bool dry) -> int {
+        T.dry = dry ? 1u : 0u;
+        if (!hip_ok(e = hipMemsetAsync(c->d_tcpcnt, 0, PVT_WORDS * 4, st)) ||
+            !hip_ok(e = hipMemcpyAsync(c->d_tparams, c->h_tparams, sizeof T, hipMemcpyHostToDevice, st)))
+            return c->hipfail(e, "TCP stage upload");
+        hipLaunchKernelGGL(pv_tcp_scan, dim3(1), dim3(1024), 0, st, dT);
+        if (n_seg) {
+            {
+                hipLaunchKernelGGL(pv_tcp_keys, dim3(blocks), dim3(256), 0, st, (const PvTcpSeg *)c->d_tseg, n_seg, c->d_tkey[0],
+                                   c->d_tval[0]);
+                size_t tmp = c->tsort_tmp_bytes;
+                if (!hip_ok(e = pv_tcp_sort(c->d_tsort_tmp, &tmp, c->d_tkey[0], c->d_tkey[1], c->d_tval[0], c->d_tval[1], n_seg, st)))
+                    return c->hipfail(e, "TCP segment sort");
+            }
+            hipLaunchKernelGGL(pv_tcp_lookup, dim3(blocks), dim3(256), 0, st, dT);
+            hipLaunchKernelGGL(pv_tcp_insert, dim3(blocks), dim3(256), 0, st, dT);
+            hipLaunchKernelGGL(pv_tcp_flow, dim3(blocks), dim3(256), 0, st, dT);
+            if (c->n_clist && !dry) hipLaunchKernelGGL(pv_tcp_migrate, dim3((c->n_clist + 255) / 256), dim3(256), 0, st, dT);
+        }
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch TCP stage");
+        return 0;
+    };
+    if (c->tcp_limit && n_seg) {
+        // tcp_packet_reassembly_cache_limit: record the segments' LRU events, replay the LRU
+        // list on the host, then run the stage with the evictions it found
+        if (int rc = PV_GROW(c, c->d_lru_ev, c->lru_ev_cap, 3ull * n_seg, "TCP LRU events")) return rc;
+        if (int rc = PV_GROW(c, c->d_fclose, c->fclose_cap, 3ull * n_seg, "TCP LRU closes")) return rc;
+        T.lru_ev = c->d_lru_ev;
+        T.fclose = nullptr;
+        if (int rc = run(true)) return rc;
+        std::vector<uint64_t> skey(n_seg);
+        std::vector<uint32_t> ev(3ull * n_seg);
+        if (!hip_ok(e = hipMemcpyAsync(skey.data(), c->d_tkey[1], (size_t)n_seg * 8, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipMemcpyAsync(ev.data(), c->d_lru_ev, ev.size() * 4, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "TCP LRU events");
+        std::vector<uint32_t> fclose(3ull * n_seg, PVT_FCLOSE_NONE);
+        tcp_lru_replay(c, skey, ev, fclose);
+        if (!hip_ok(e = hipMemcpyAsync(c->d_fclose, fclose.data(), fclose.size() * 4, hipMemcpyHostToDevice, st)))
+            return c->hipfail(e, "TCP LRU closes");
+        c->tcp_stage++;
+        T.stage = c->tcp_stage;
+        T.lru_ev = nullptr;
+        T.fclose = c->d_fclose;
+        if (!hip_ok(e = hipStreamSynchronize(st))) return c->hipfail(e, "TCP LRU closes");
     }
-    if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch TCP stage");
+    if (int rc = run(false)) return rc;
     if (!hip_ok(e = hipMemcpyAsync(c->h_tcpcnt, c->d_tcpcnt, PVT_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "TCP stage");
@@ -3173,7 +3299,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     params_common(c, P, d_recs, d_offs, n);
     // a batch with no TCP stage ahead of it is one span: its Net pass emits the TCP segments
     // and the tile masks of its TCP records (zeroed here; the pass stores non-zero masks only)
-    P.tcp_emit = c->tcp_pre ? 0u : 1u;
+    P.tcp_emit = c->tcp_pre ? 0u : (c->tcp_limit ? 3u : 1u);
     if (P.tcp_emit) launch_fill64(c, c->d_tmask, (n + 63) / 64, 0);
     P.gbase = c->global_base + c->records_seen;
     if (c->slow_defer && !c->edge_h) c->edge_h = (int64_t)first_sec + c->ttl_s + 61;
@@ -3362,7 +3488,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     // its packed lane counters), else the shift-free general pass. PV_NET_KERNEL=ns|general
     // forces one for A/B runs.
     static const char *force = getenv("PV_NET_KERNEL");
-    const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || (force && !strcmp(force, "general"));
+    // (every TCP segment for the cache-limit replay: the general pass emits them)
+    const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || c->tcp_limit || (force && !strcmp(force, "general"));
     const uint32_t reg_grid = std::min<uint32_t>(grid, (uint32_t)(c->cus * c->reg_wg_per_cu));
     const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
     const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
@@ -3410,9 +3537,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
     uint32_t status[ST_WORDS];
-    if (!hip_ok(e = hipMemcpyAsync(c->h_tab_live, c->d_tab_live, PV_TABLES * 4, hipMemcpyDeviceToHost, st)) ||
-        !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
-        !hip_ok(e = hipMemcpyAsync(c->h_ovf, c->d_ovf_cnt, 8, hipMemcpyDeviceToHost, st)) ||
+    if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_RB_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "kernel execution");
     memcpy(status, c->h_status, sizeof status);
@@ -3431,8 +3556,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         if (P.want_events)
             hipLaunchKernelGGL(pv_xact_compact, dim3(grid + gt), dim3(256), 0, st, (const PvParams *)c->d_params, grid + gt);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_dns_tcp");
-        if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, sizeof status, hipMemcpyDeviceToHost, st)) ||
-            !hip_ok(e = hipMemcpyAsync(c->h_ovf, c->d_ovf_cnt, 8, hipMemcpyDeviceToHost, st)) ||
+        if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_RB_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "TCP DNS pass");
         memcpy(status, c->h_status, sizeof status);
@@ -3821,11 +3945,6 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
     if (c->net2_groups || c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "dnstap input with the v2 handlers is not built");
-    // each manager draws per dnstap event (new_event: net/v1 :840, dns/v1 :1409); the
-    // dnstap kernel has no not-deep path, so a sampled context refuses rather than report
-    // every event as deep and leave the generators out of step
-    if (c->sample_rate < 100)
-        return c->fail(PV_EUNSUPPORTED, "dnstap input with deep_sample_rate below 100 is not built");
     std::vector<pvi::DtMessage> msgs;
     uint32_t frames = 0;
     pvi::dnstap_decode(buf, bytes, msgs, &frames);
@@ -3870,6 +3989,15 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         e.l4 = m.has_protocol ? (m.protocol == 1 ? 17 : (m.protocol == 2 ? 6 : 0)) : 0;
         e.qport = m.has_qport ? (uint16_t)m.qport : 0;
         e.filtered = (msg_type_mask && !(t < 32 && ((msg_type_mask >> t) & 1))) ? 1 : 0; // a type past the mask's bits never matches
+        // deep sampling: each manager draws per dnstap event in stream order (new_event:
+        // net/v1 ...cpp:840, dns/v1 ...cpp:1409); a dnstap_msg_type-filtered event is the DNS
+        // manager's process_filtered, new_event(stamp, false): no draw, the last flag.
+        // pad[0]: bit 0 not deep for the Net manager, bit 1 for the DNS manager
+        if (c->sample_rate < 100) {
+            const bool net_deep = c->draws_net.next(c->sample_rate);
+            if (!e.filtered) c->dns_deep_now = c->draws_dns.next(c->sample_rate);
+            e.pad[0] = (uint8_t)((net_deep ? 0u : 1u) | (c->dns_deep_now ? 0u : 2u));
+        }
         const uint8_t *msg = nullptr;
         size_t mlen = 0;
         if (!m.has_qmsg && !m.has_rmsg) e.dns_mode = PV_DT_SIDE;

@@ -1362,7 +1362,8 @@ __device__ __forceinline__ uint32_t fast_flowkey(const RecW &r)
     return fnv_bytes(h, r.w[9] >> 24, 1);
 }
 
-// ---- DNS over TCP: the segment of a TCP packet of a DNS-port flow (PvTcpSeg), or false
+// ---- DNS over TCP: the segment of a TCP packet of a DNS-port flow (PvTcpSeg; of any flow
+// with `all`, the tcp_packet_reassembly_cache_limit replay's LRU holds every connection), or false
 // when TcpReassembly would not look at it (no payload and none of SYN / FIN / RST: dropped
 // before the connection lookup) or its header is not a TcpLayer (TcpLayer::isDataValid)
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xff) << 8) | ((x >> 8) & 0xff); }
@@ -1404,11 +1405,11 @@ __device__ __forceinline__ bool tcp_seg_fill(PvTcpSeg &g, uint32_t pw, uint32_t 
     return true;
 }
 template <class A>
-__device__ __forceinline__ bool tcp_seg_of(const A &R, const Parsed &o, uint64_t i, PvTcpSeg &g)
+__device__ __forceinline__ bool tcp_seg_of(const A &R, const Parsed &o, uint64_t i, PvTcpSeg &g, bool all = false)
 {
     if (o.l4 != 6) return false;
     const uint32_t pw = R.u32(o.l4off);
-    if (!tcp_dns_pw(pw)) return false;
+    if (!all && !tcp_dns_pw(pw)) return false;
     const bool v6first = o.has6 && (!o.has4 || o.v6 < o.v4);
     uint64_t ep;
     if (!v6first) ep = tcp_ep4(R.u32(o.v4 + 12), pw & 0xffff);
@@ -1421,10 +1422,10 @@ __device__ __forceinline__ bool tcp_seg_of(const A &R, const Parsed &o, uint64_t
                         o.dir | (v6first ? 4u : 0u));
 }
 // the same from a fast-path record's words (Ethernet + IPv4 without options: TCP at record offset 50)
-__device__ __forceinline__ bool tcp_seg_fast(const RecW &r, const Parsed &o, uint64_t i, PvTcpSeg &g)
+__device__ __forceinline__ bool tcp_seg_fast(const RecW &r, const Parsed &o, uint64_t i, PvTcpSeg &g, bool all = false)
 {
     const uint32_t pw = r.at(50);
-    if (!tcp_dns_pw(pw)) return false;
+    if (!all && !tcp_dns_pw(pw)) return false;
     return tcp_seg_fill(g, pw, r.w[15] >> 16, r.at(54), o.l4len, o.l4off, i, fast_flowkey(r), o.sec, o.nsec,
                         tcp_ep4(r.at(42), pw & 0xffff), o.dir);
 }
@@ -1481,7 +1482,7 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
     if (K.tcp_emit && o.l4 == 6) {
         // a DNS-port TCP segment of a general-path frame: appended by this lane alone
         PvTcpSeg g;
-        if (tcp_seg_of(R, o, i, g)) {
+        if (tcp_seg_of(R, o, i, g, K.tcp_emit & 2)) {
             const uint32_t q = atomicAdd(K.tseg_cnt, 1u);
             atomicAdd(K.tseg_cnt + 1, (uint32_t)g.plen);
             if (q < K.tseg_cap) K.tseg[q] = g;
@@ -1678,7 +1679,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
                 isdns = so.isdns;
                 if (!ddeep) dm.a.w |= 16u << 16; // DnsMsg flags bit 4: the DNS event is not deep
             } else if (K.tcp_emit && o.l4 == 6) {
-                hasseg = tcp_seg_fast(rw, o, i, seg);
+                hasseg = tcp_seg_fast(rw, o, i, seg, GEN && (K.tcp_emit & 2));
             }
             istcp = o.l4 == 6;
             if (!deep) o.syn = 0;
@@ -3368,7 +3369,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_prescan(const PvParams 
             Parsed o;
             parse_record(R, P, P.offs[i], o);
             istcp = o.l4 == 6;
-            if (P.tcp_emit && istcp) hasseg = tcp_seg_of(R, o, i, g);
+            if (P.tcp_emit && istcp) hasseg = tcp_seg_of(R, o, i, g, P.tcp_emit & 2);
             if (o.l4 == 17 && dns_port(R.u32(o.l4off))) {
                 ev = true;
                 if (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) {
@@ -3496,8 +3497,10 @@ extern "C" __global__ void __launch_bounds__(256) pv_dnstap_kernel(const PvParam
     // ---- Net v1
     {
         const uint32_t s = P.slot_of[0];
+        // deep sampling, not deep: process_net_layer(dir, l3, l4, size) only (net/v1 ...cpp:599-602)
+        const bool deep = !(e.pad[0] & 1);
         sum_add(P, s, PV_OFF_NET + NC_EVENTS, 1);
-        sum_add(P, s, PV_OFF_NET + NC_SAMPLES, 1);
+        if (deep) sum_add(P, s, PV_OFF_NET + NC_SAMPLES, 1);
         if (P.net_groups & PV_NET_COUNTERS_BIT) {
             sum_add(P, s, PV_OFF_NET + NC_TOTAL, 1);
             sum_add(P, s, PV_OFF_NET + (e.dir == 0 ? NC_IN : (e.dir == 1 ? NC_OUT : NC_UNK)), 1);
@@ -3506,7 +3509,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dnstap_kernel(const PvParam
         }
         sum_add(P, s, PV_OFF_PAYLOAD + min(e.size, 65535u), 1);
         const bool card = P.net_groups & PV_NET_CARDINALITY_BIT, tops = P.net_groups & PV_NET_TOP_IPS_BIT;
-        for (int side = 0; side < 2; side++) {
+        for (int side = 0; side < 2 && deep; side++) {
             const uint8_t *a = side ? e.raddr : e.qaddr;
             const uint32_t alen = side ? e.rlen : e.qlen;
             const uint32_t sketch = side ? CPC_DST : CPC_SRC;
@@ -3530,12 +3533,15 @@ extern "C" __global__ void __launch_bounds__(256) pv_dnstap_kernel(const PvParam
     {
         const uint32_t s = P.dslot_of[0];
         const bool dc = P.dns_groups & PV_DNS_COUNTERS_BIT;
-        if (e.filtered || e.dns_mode != PV_DT_MESSAGE) {
+        // deep sampling: a not-deep event takes process_dns_layer(l3, l4, side) (dns/v1 ...cpp:882-885);
+        // a filtered one counts the manager's last flag
+        const bool ddeep = !(e.pad[0] & 2);
+        if (e.filtered || e.dns_mode != PV_DT_MESSAGE || !ddeep) {
             sum_add(P, s, PV_OFF_DNS + DC_EVENTS, 1);
-            sum_add(P, s, PV_OFF_DNS + DC_SAMPLES, 1);
+            if (ddeep) sum_add(P, s, PV_OFF_DNS + DC_SAMPLES, 1);
             if (e.filtered) {
                 if (dc) sum_add(P, s, PV_OFF_DNS + DC_FILTERED, 1);
-            } else if (e.dns_mode == PV_DT_SIDE && dc) {
+            } else if ((e.dns_mode == PV_DT_SIDE || !ddeep) && dc) {
                 // process_dns_layer(l3, l4, side) (:1051-1091)
                 sum_add(P, s, PV_OFF_DNS + DC_TOTAL, 1);
                 if (e.l3) sum_add(P, s, PV_OFF_DNS + (e.l3 == 6 ? DC_V6 : DC_V4), 1);

@@ -537,8 +537,21 @@ struct PvTcpParams {
     PV_G uint64_t *mq;            // 32-B DnsMsg items (same layout as the UDP work lists)
     uint32_t mq_cap;
     PV_G uint32_t *cnt;           // [0] messages [1] arena bytes [2] carry bytes [3] carried flows [4] frag nodes [5] flags
+    // tcp_packet_reassembly_cache_limit (PcapInputStream's LRU capacity): a dry run records the
+    // LRU events of every sorted segment (lru_ev: flags | dir << 8, second, latest TCP second
+    // + 1 before it) and leaves the flow table, the carried bytes and lt_carry as they were; the
+    // run after it closes each flow the host's LRU replay evicted (fclose at the flow's first
+    // sorted segment: record index after which it closes, that record's second and direction)
+    uint32_t dry;
+    PV_G uint32_t *lru_ev;
+    const PV_G uint32_t *fclose;
 };
 enum { PVT_NMSG = 0, PVT_ARENA, PVT_CARRY, PVT_NCARRY, PVT_NFRAG, PVT_FLAGS, PVT_WORDS };
+// LRU events of one segment (lru_ev flags): a connection start's put, a message delivery's put,
+// the connection closed (FIN/RST) in it, closed by the 30 s timeout ahead of it
+enum { PVT_EV_NEW = 1, PVT_EV_PUT = 2, PVT_EV_CLOSE = 4, PVT_EV_TIMEOUT = 8 };
+#define PVT_FCLOSE_NONE 0xffffffffu
+#define PVT_FCLOSE_FIRST 0xfffffffeu // closed ahead of the flow's first segment of the batch
 enum { PVT_F_TABLE = 1, PVT_F_ARENA = 2, PVT_F_CARRY = 4, PVT_F_FRAGS = 8, PVT_F_MSGS = 16 };
 
 // Device record index of an ingest chunk (pv_index.hip)

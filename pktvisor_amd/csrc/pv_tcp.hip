@@ -22,10 +22,14 @@
 //                       new carry arena
 // The messages then go through the DNS pass like UDP datagrams (pv_dns_tcp).
 //
-// Approximations: the LRU's 100-closures-per-packet limit, its capacity and the
-// closed-connection purge (wall clock in PcapPlusPlus) are not modelled; a timed-out flow is
-// closed lazily at its next packet (data it flushes is ordered there); no flush of open
-// connections at the end of a capture.
+// tcp_packet_reassembly_cache_limit: a dry run of pv_tcp_flow records each segment's LRU events,
+// the host replays the LRU list over them in capture order and the real run closes the flows it
+// evicts (pv_host.cpp tcp_lru_replay).
+// Approximations: the LRU's 100-closures-per-packet limit and the closed-connection
+// purge (wall clock in PcapPlusPlus) are not modelled; a timed-out flow is closed lazily at its
+// next packet (data it flushes is ordered there); the LRU holds the DNS-port connections only;
+// the puts of data an eviction flushes are not replayed; no flush of open connections at the
+// end of a capture.
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -71,6 +75,7 @@ struct Flow {
     uint32_t budget;          // bound on bytes this flow can deliver in this batch
     uint32_t fkey;
     uint32_t cur_idx, cur_dir, cur_sec, sub;
+    uint32_t ev; // PVT_EV_* of the packet being replayed (tcp_packet_reassembly_cache_limit dry run)
 };
 
 __device__ void emit_msg(PV_CREF(PvTcpParams) T, Flow &F, int s)
@@ -163,6 +168,7 @@ __device__ void deliver(PV_CREF(PvTcpParams) T, Flow &F, int s, const uint8_t *s
 {
     if (F.f.port) frame(T, F, s, src, n);
     F.f.lru_sec = F.cur_sec;
+    F.ev |= PVT_EV_PUT;
 }
 
 __device__ uint32_t frag_new(PV_CREF(PvTcpParams) T, const uint8_t *src, uint32_t seq, uint32_t len)
@@ -251,6 +257,7 @@ __device__ void check_ooo(PV_CREF(PvTcpParams) T, Flow &F, int s, bool clean)
                 frame(T, F, s, (const uint8_t *)(uintptr_t)fr.src, fr.len);
             }
             F.f.lru_sec = F.cur_sec;
+            F.ev |= PVT_EV_PUT;
             found = true;
         }
     } while (found);
@@ -263,6 +270,7 @@ __device__ void close_conn(PV_CREF(PvTcpParams) T, Flow &F, uint32_t when)
     check_ooo(T, F, 1, true);
     F.f.closed = 1;
     F.f.close_sec = when;
+    F.ev |= PVT_EV_CLOSE;
     F.f.port = 0; // untracked: the sessions are gone
     for (int s = 0; s < 2; s++) { F.f.inval[s] = 0; F.f.lenb[s] = 0; F.f.size[s] = 0; F.f.got[s] = 0; F.rec[s] = PV_NOREC; }
 }
@@ -302,7 +310,10 @@ __device__ void packet(PV_CREF(PvTcpParams) T, Flow &F, const PvTcpSeg &g)
     if (f.live && !f.closed) {
         // PcapInputStream's LRU cleanup after an earlier TCP packet at >= last put + 30 s
         const uint32_t lt = lt_before(T, g.idx);
-        if (lt && lt - 1 >= f.lru_sec + PV_TCP_TIMEOUT) close_conn(T, F, f.lru_sec + PV_TCP_TIMEOUT);
+        if (lt && lt - 1 >= f.lru_sec + PV_TCP_TIMEOUT) {
+            close_conn(T, F, f.lru_sec + PV_TCP_TIMEOUT);
+            F.ev = PVT_EV_TIMEOUT;
+        }
     }
     if (f.closed) return; // Ignore_PacketOfClosedFlow
     const bool fin = g.flags & PV_TF_FIN, syn = g.flags & PV_TF_SYN, rst = g.flags & PV_TF_RST;
@@ -318,6 +329,7 @@ __device__ void packet(PV_CREF(PvTcpParams) T, Flow &F, const PvTcpSeg &g)
         f.end_sec = f.end_usec = 0;
         f.prev = -1;
         f.lru_sec = g.sec;
+        F.ev |= PVT_EV_NEW;
     } else if (g.sec > f.end_sec || (g.sec == f.end_sec && g.usec > f.end_usec)) {
         f.end_sec = g.sec;
         f.end_usec = g.usec;
@@ -398,6 +410,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_tcp_scan(const PvTcpParams
         part[threadIdx.x] = max(part[threadIdx.x], v);
         __syncthreads();
     }
+    // a dry run (cache-limit replay) leaves the carried value for the run after it
     const uint32_t carry = *T.lt_carry;
     uint32_t run = max(carry, threadIdx.x ? part[threadIdx.x - 1] : 0u);
     for (uint32_t t = a; t < b; t++) {
@@ -405,7 +418,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_tcp_scan(const PvTcpParams
         run = max(run, tile_max(t));
     }
     __syncthreads();
-    if (threadIdx.x == 0) *T.lt_carry = max(carry, part[1023]);
+    if (threadIdx.x == 0 && !T.dry) *T.lt_carry = max(carry, part[1023]);
 }
 
 // the flow-table entry of every run (a flow's first sorted segment): found, or PV_RUN_NEW
@@ -479,6 +492,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
     F.cur_dir = 2;
     F.cur_sec = 0;
     F.sub = 0;
+    F.ev = 0;
     // bytes this flow can deliver in this batch: carried bytes, payloads, missing-data texts
     uint64_t budget = F.f.blob_len + 32ull * (F.f.nfrag[0] + F.f.nfrag[1]);
     for (uint32_t k = j; k < je; k++) budget += T.seg[T.sval[k]].plen + 32u;
@@ -505,7 +519,32 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
     }
     F.f.blob_len = 0;
     F.f.nfrag[0] = F.f.nfrag[1] = 0;
-    for (uint32_t k = j; k < je; k++) packet(T, F, T.seg[T.sval[k]]);
+    // the close the host's LRU replay decided (an overflow eviction after record fc_idx, possibly
+    // another flow's): closeConnection with that record's second and direction; its flushed
+    // messages rank behind the record's own (sub 3)
+    uint32_t fc_idx = PVT_FCLOSE_NONE, fc_sec = 0, fc_dir = 2;
+    if (T.fclose) { fc_idx = T.fclose[3 * j]; fc_sec = T.fclose[3 * j + 1]; fc_dir = T.fclose[3 * j + 2]; }
+    auto force_close = [&]() {
+        F.cur_idx = fc_idx == PVT_FCLOSE_FIRST ? T.seg[T.sval[j]].idx : fc_idx;
+        F.sub = 3;
+        F.cur_sec = fc_sec;
+        F.cur_dir = fc_dir;
+        close_conn(T, F, fc_sec);
+    };
+    for (uint32_t k = j; k < je; k++) {
+        const PvTcpSeg g = T.seg[T.sval[k]];
+        if (fc_idx != PVT_FCLOSE_NONE && (fc_idx == PVT_FCLOSE_FIRST || g.idx > fc_idx) && F.f.live && !F.f.closed)
+            force_close();
+        F.ev = 0;
+        packet(T, F, g);
+        if (T.lru_ev) {
+            T.lru_ev[3 * k] = F.ev | (g.dirv6 & 3) << 8;
+            T.lru_ev[3 * k + 1] = g.sec;
+            T.lru_ev[3 * k + 2] = lt_before(T, g.idx);
+        }
+    }
+    if (fc_idx != PVT_FCLOSE_NONE && F.f.live && !F.f.closed) force_close();
+    if (T.dry) return; // the LRU replay's dry run: flow state and carried bytes as they were
     // carry out: held message bytes (from their records) and the fragments left
     if (!F.f.closed) {
         uint32_t bytes = 0;

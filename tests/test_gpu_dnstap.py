@@ -77,8 +77,34 @@ def test_dnstap_invalid_msg_type():
         run({"dnstap_msg_type": "bogus"})
 
 
-def test_dnstap_deep_sampling_refused():
-    """each manager draws per dnstap event (net/v1 :840, dns/v1 :1409); the dnstap path has no
-    not-deep accounting, so a sampled context refuses instead of reporting every event as deep"""
-    with pytest.raises(pa.PvError, match="deep_sample_rate"):
-        pa.dnstap_reader(FIX, periods=1, net_config={}, dns_config={}, deep_sample_rate=50)
+@pytest.mark.parametrize("rate", [1, 30, 70, 99])
+@pytest.mark.parametrize("msg_type", [None, "auth"])
+def test_dnstap_deep_sampling(rate, msg_type):
+    """deep_sample_rate < 100 over dnstap: each manager draws per event in stream order
+    (new_event, net/v1 ...cpp:840, dns/v1 ...cpp:1409); a dnstap_msg_type-filtered event draws
+    nothing in the DNS manager (process_filtered) and counts its last flag. A not-deep event
+    takes the Net handler's process_net_layer(dir, l3, l4, size) and the DNS handler's
+    process_dns_layer(l3, l4, side) (net/v1 ...cpp:599-602, dns/v1 ...cpp:882-885). The oracle has
+    no dnstap path: the expected numbers come from the reference generator's draws
+    (tests/golden/jsf32_seed1.json, oracle/_ref/ref_jsf) and the unsampled KATs above."""
+    import json
+    first = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "jsf32_seed1.json")))["first"]
+    deep = sum(1 for x in first[:153] if x % 100 < rate)
+    out = pa.dnstap_reader(FIX, periods=1, net_config={}, dns_config={"dnstap_msg_type": msg_type} if msg_type else {},
+                           deep_sample_rate=rate)
+    # Net: every event draws; counters and payload sizes for all, addresses for the deep ones
+    for k, v in {"events": 153, "deep_samples": deep, "udp": 153, "ipv4": 153, "in": 79, "out": 74}.items():
+        assert jget(out, "1m.packets." + k) == v, k
+    assert jget(out, "1m.packets.top_ipv4.0.estimate") == deep
+    assert jget(out, "1m.packets.payload_size.p50") == 100
+    dns = jget(out, "1m.dns.wire_packets")
+    if msg_type == "auth":
+        # every event filtered: no DNS draw, the manager's initial flag (deep) on each
+        assert (dns["events"], dns["deep_samples"], dns["filtered"], dns["queries"]) == (153, 153, 153, 0)
+    else:
+        # counters by side for every event; the message's rcode and names for the deep ones
+        for k, v in {"events": 153, "deep_samples": deep, "udp": 153, "ipv4": 153, "queries": 79, "replies": 74}.items():
+            assert dns[k] == v, k
+        assert dns["noerror"] + dns["srvfail"] <= 74
+        q = sum(e["estimate"] for e in jget(out, "1m.dns.top_qtype"))
+        assert q <= deep and (deep == 0 or q > 0)

@@ -17,7 +17,8 @@ KAT = json.load(open(os.path.join(GOLD, "kat_reference.json")))["cases"]
 def test_gpu_matches_reference_kats(case):
     out = pa.pktvisor_reader(os.path.join(GOLD, case["fixture"]), host_spec=case["host_spec"] or None,
                              periods=case["periods"], net_config={}, dns_config=case.get("dns_config", {}),
-                             net2_config=case.get("net2_config"), dns2_config=case.get("dns2_config"))
+                             net2_config=case.get("net2_config"), dns2_config=case.get("dns2_config"),
+                             **case.get("input_config", {}))
     for path, want in case["checks"]:
         assert jget(out, path) == want, (case["cite"], path)
     for path, lo in case.get("ge", []):
