@@ -139,6 +139,7 @@ extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ns(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_fast(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
 extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
@@ -531,6 +532,7 @@ struct pv_ctx {
     int cus = 256;
     int wg_per_cu = 3;     // grid workgroups per CU (the batch's partition)
     int reg_wg_per_cu = 1; // workgroups per CU of the register-window Net pass
+    int reg_waves = 4;     // its waves per workgroup (4 or 8; PV_REG_WAVES)
     int dns_wg_per_cu = 1; // resident workgroups per CU of the DNS pass (its register count)
     const char *net_kernel = "none"; // the Net-pass kernel the last span launched (pv_net_kernel_name)
     uint64_t *d_dq = nullptr; // DNS work lists (32-B messages)
@@ -2247,6 +2249,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         c->wg_per_cu = 3;
         if (const char *w = getenv("PV_NET_WGCU")) c->wg_per_cu = std::max(1, atoi(w));
         if (const char *w = getenv("PV_REG_WGCU")) c->reg_wg_per_cu = std::max(1, atoi(w));
+        if (const char *w = getenv("PV_REG_WAVES")) c->reg_waves = atoi(w) == 8 ? 8 : 4;
         {
             int nb = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_dns_kernel), 64 * PV_DNS_WAVES, 0) == hipSuccess &&
@@ -3505,9 +3508,10 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
-    c->net_kernel = general ? "pv_net_kernel" : (lean ? (ring ? "pv_net_kernel_fast" : "pv_net_kernel_reg") : "pv_net_kernel_ns");
+    c->net_kernel = general ? "pv_net_kernel" : (lean ? (ring ? "pv_net_kernel_fast" : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : "pv_net_kernel_reg")) : "pv_net_kernel_ns");
     if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    else if (lean && c->reg_waves == 8) hipLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, (const PvParams *)c->d_params);
     else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     e = hipGetLastError();

@@ -2152,6 +2152,8 @@ __device__ __forceinline__ void win_words(const uint4 (&W)[5], uint32_t sh, RecW
 #pragma unroll
     for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
 }
+// NW: waves of the workgroup (one workgroup per CU); wave w takes tiles w, w + NW, ... of each range
+template <uint32_t NW>
 __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
@@ -2186,9 +2188,9 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
     const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
     const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
-    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + 3) / 4) : 0u;
+    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u;
     any |= ntl != 0;
-    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + 4ull * min(k, ntl - 1); };
+    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
     auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
     // one tile from its windows W (off: this lane's record start)
     auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
@@ -2397,7 +2399,9 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(const PvParams *__restrict__ Pp) { net_pass<true>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(const PvParams *__restrict__ Pp) { net_pass<false>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg(Pp); }
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg<4>(Pp); }
+// eight waves in the one workgroup of a CU: two per SIMD to hide instruction latency, one record stream per CU
+extern "C" __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg8(const PvParams *__restrict__ Pp) { net_fast_reg<8>(Pp); }
 
 // ------------------------------------------------------------------ the DNS pass
 // One lane per DNS message of the Net pass's work list (same workgroup mapping).
