@@ -385,8 +385,8 @@ int pv_check_period_shift(pv_ctx *ctx, int64_t sec, int64_t nsec);
  * (StreamHandler::merge / window_json(j, bucket) / window_prometheus(out, bucket, labels) /
  * window_opentelemetry(scope, bucket, labels), src/StreamHandler.h:72-77,221-269), which a policy
  * uses to fold like handlers across taps (Policy::_get_merged_buckets, src/Policies.cpp:420-446).
- * A pv_bucket is a host-side snapshot of one handler's bucket (handler = PV_HANDLER_NET or
- * PV_HANDLER_DNS, v1 handlers). */
+ * A pv_bucket is a host-side snapshot of one handler's bucket (handler = PV_HANDLER_NET: the
+ * Net v1 part and, when attached, Net v2's; PV_HANDLER_DNS: DNS v1 or v2, as configured). */
 typedef struct pv_bucket pv_bucket;
 /* StreamMetricsHandler::merge(bucket, period, prometheus, merged): *bucket == NULL -> a new bucket
  * holding this context's bucket `period` (merged: the fold of its `period` newest buckets,

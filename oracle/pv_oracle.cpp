@@ -928,11 +928,14 @@ struct Net2Dir {
     Cpc ips;
     ExactTop<uint32_t> top4;
     ExactTop<std::string> top6;
-    void merge(const Net2Dir &o)
+    // NetworkMetricsBucket::specialized_merge, v2 (net/v2/NetStreamHandler.cpp:286-331); sum:
+    // Aggregate::SUM (a policy's merged handlers)
+    void merge(const Net2Dir &o, bool sum = false)
     {
         UDP += o.UDP; TCP += o.TCP; OtherL4 += o.OtherL4; IPv4 += o.IPv4; IPv6 += o.IPv6; TCP_SYN += o.TCP_SYN;
         total += o.total; seen += o.seen;
-        payload.merge(o.payload);
+        if (sum) payload.merge_sum(o.payload);
+        else payload.merge(o.payload);
         ips.merge(o.ips);
         top4.merge(o.top4);
         top6.merge(o.top6);
@@ -941,10 +944,10 @@ struct Net2Dir {
 struct Net2Bucket : BaseBucket {
     uint64_t filtered = 0;
     Net2Dir dir[3]; // in (toHost), out (fromHost), unknown
-    void merge(const Net2Bucket &o)
+    void merge(const Net2Bucket &o, bool sum = false)
     {
         filtered += o.filtered;
-        for (int d = 0; d < 3; d++) dir[d].merge(o.dir[d]);
+        for (int d = 0; d < 3; d++) dir[d].merge(o.dir[d], sum);
     }
 };
 
@@ -954,17 +957,22 @@ struct Dns2Dir {
              NODATA = 0, AD = 0, AA = 0, CD = 0, timeout = 0, orphan = 0;
     bool seen = false; // DnsMetricsBucket::dir_setup ran for this direction
     ExactQuantile<uint64_t> time;
+    ExactQuantile<uint64_t> hist; // dnsHistTimeUs (a Histogram: its sketch merges under any aggregate)
     ExactQuantile<double> ratio;
     Cpc qname;
     ExactTop<std::string> ecs, qname2, qname3, nx, refused, sized, srvfail, nodata, noerror, slow;
     ExactTop<uint16_t> port, qtype, rcode;
-    void merge(const Dns2Dir &o)
+    // DnsMetricsBucket::specialized_merge, v2 (dns/v2/DnsStreamHandler.cpp:619-676); sum: Aggregate::SUM
+    void merge(const Dns2Dir &o, bool sum = false)
     {
         xacts += o.xacts; UDP += o.UDP; TCP += o.TCP; IPv4 += o.IPv4; IPv6 += o.IPv6; NX += o.NX; ECS += o.ECS;
         REFUSED += o.REFUSED; SRVFAIL += o.SRVFAIL; NOERROR += o.NOERROR; NODATA += o.NODATA; AD += o.AD; AA += o.AA;
         CD += o.CD; timeout += o.timeout; orphan += o.orphan;
         seen = seen || o.seen;
-        time.merge(o.time); ratio.merge(o.ratio); qname.merge(o.qname);
+        if (sum) { time.merge_sum(o.time); ratio.merge_sum(o.ratio); }
+        else { time.merge(o.time); ratio.merge(o.ratio); }
+        hist.merge(o.hist);
+        qname.merge(o.qname);
         ecs.merge(o.ecs); qname2.merge(o.qname2); qname3.merge(o.qname3); nx.merge(o.nx); refused.merge(o.refused);
         sized.merge(o.sized); srvfail.merge(o.srvfail); nodata.merge(o.nodata); noerror.merge(o.noerror);
         slow.merge(o.slow); port.merge(o.port); qtype.merge(o.qtype); rcode.merge(o.rcode);
@@ -973,10 +981,10 @@ struct Dns2Dir {
 struct Dns2Bucket : BaseBucket {
     uint64_t filtered = 0;
     Dns2Dir dir[3]; // in, out, unknown
-    void merge(const Dns2Bucket &o)
+    void merge(const Dns2Bucket &o, bool sum = false)
     {
         filtered += o.filtered;
-        for (int d = 0; d < 3; d++) dir[d].merge(o.dir[d]);
+        for (int d = 0; d < 3; d++) dir[d].merge(o.dir[d], sum);
     }
 };
 
@@ -1549,7 +1557,7 @@ struct Engine {
             if (!deep) return; // new_dns_transaction v2 (:1006-1008): the rest only when deep
             if (q.query_size && (g & D2G_TOP_SIZE)) x.ratio.update((double)m.len / (double)q.query_size);
             if (p.port && (g & D2G_TOP_PORTS)) x.port.update(p.port);
-            if (g & D2G_XACT_TIMES) x.time.update(us);
+            if (g & D2G_XACT_TIMES) { x.time.update(us); x.hist.update(us); }
             DnsParse r = m.len >= 12 ? parse_resources(m) : parse_resources_short(DnsMsg{h, m.len});
             if (r.ok) {
                 x.rcode.update(rcode);
@@ -2163,7 +2171,7 @@ static void dns2_json(J &j, const Dns2Bucket &b, size_t topn, uint32_t g)
         if (g & D2G_TOP_QTYPES) top_json(j, "top_qtype_xacts", x.qtype, topn, qt);
         if (g & D2G_XACT_TIMES) {
             quant_json(j, "xact_time_us", x.time);
-            hist_json(j, "xact_histogram_us", x.time);
+            hist_json(j, "xact_histogram_us", x.hist);
             top_json(j, "top_slow_xacts", x.slow, topn, id_str);
         }
         j.end_obj();
@@ -2250,8 +2258,7 @@ static void bucket_merge(B &out, const B &m, bool firstb, bool sum = false)
     out.period_length += m.period_length;
     if (firstb || m.start.sec < out.start.sec) out.start.sec = m.start.sec;
     if (firstb || m.end.sec > out.end.sec) out.end.sec = m.end.sec;
-    if constexpr (std::is_same<B, NetBucket>::value || std::is_same<B, DnsBucket>::value) out.merge(m, sum);
-    else out.merge(m);
+    out.merge(m, sum);
 }
 // a fresh bucket folding buckets [from, from + count) of the window (DEFAULT aggregate); a
 // union of CPC sketches reports the ICON estimate even for one input
@@ -2502,14 +2509,22 @@ int pvo_run_policy(const uint8_t *const *files, const size_t *lens, uint32_t n, 
     };
     std::unique_ptr<NetBucket> nb;
     std::unique_ptr<DnsBucket> db;
+    std::unique_ptr<Net2Bucket> n2b;
+    std::unique_ptr<Dns2Bucket> d2b;
     for (uint32_t i = 0; i < n; i++) {
         pick(engines[i]->net, nb, i == 0);
         pick(engines[i]->dns, db, i == 0);
+        if (c.net2_groups) pick(engines[i]->net2, n2b, i == 0);
+        if (c.dns2_groups) pick(engines[i]->dns2, d2b, i == 0);
     }
     J j;
     j.obj();
     j.key("packets"); j.obj(); net_json(j, *nb, c.topn_count, c.net_groups); j.end_obj();
-    j.key("dns"); j.obj(); dns_json(j, *db, c.topn_count, c.dns_groups); j.end_obj();
+    if (c.net2_groups) { j.key("net"); j.obj(); net2_json(j, *n2b, c.topn_count, c.net2_groups); j.end_obj(); }
+    j.key("dns"); j.obj();
+    if (c.dns2_groups) dns2_json(j, *d2b, c.topn_count, c.dns2_groups);
+    else dns_json(j, *db, c.topn_count, c.dns_groups);
+    j.end_obj();
     j.end_obj();
     *out = strdup(j.s.c_str());
     return 0;

@@ -983,6 +983,13 @@ struct HostBucket {
     int64_t start_nsec = 0, end_sec = 0, end_nsec = 0;
     const std::vector<uint64_t> &hist_from() const { return hist_sep ? hfrom_us : from_us; }
     const std::vector<uint64_t> &hist_to() const { return hist_sep ? hto_us : to_us; }
+    // the same for the v2 handlers, per direction: payload sizes (Net v2), transaction times and
+    // size ratios (DNS v2) after a SUM merge, and the xact time histograms that keep merging
+    std::vector<uint64_t> qs_payload2[3], qs_time2[3];
+    std::vector<double> qs_ratio2[3];
+    bool hist2_sep = false;
+    std::vector<uint64_t> htime2[3];
+    const std::vector<uint64_t> &hist_time2(uint32_t x) const { return hist2_sep ? htime2[x] : time2[x]; }
 };
 
 template <typename T>
@@ -1283,6 +1290,7 @@ void net2_json(pv_ctx *c, Json &j, const HostBucket &b)
         if (g & PV_N2G_QUANTILES) {
             uint64_t cnt;
             auto q = hist_quantiles(&b.sum[PV_OFF_PAYLOAD2 + d * PV_PAYLOAD_BINS], PV_PAYLOAD_BINS, cnt);
+            if (cnt && !b.qs_payload2[d].empty()) q = b.qs_payload2[d];
             if (cnt) {
                 j.key("payload_size_bytes").obj();
                 j.key("p50").u(q[0]); j.key("p90").u(q[1]); j.key("p95").u(q[2]); j.key("p99").u(q[3]);
@@ -1353,13 +1361,13 @@ void dns2_json(pv_ctx *c, Json &j, const HostBucket &b)
         }
         if (g & PV_DNS2_TOP_SIZE) {
             top_json(j, "top_response_bytes", tops(TM_SIZED), topn, pct);
-            quant_json(j, "response_query_size_ratio", b.ratio2[x]);
+            quant_json(j, "response_query_size_ratio", b.ratio2[x], &b.qs_ratio2[x]);
         }
         if (g & PV_DNS2_TOP_QTYPES)
             top_json(j, "top_qtype_xacts", dense_tops(&b.sum[PV_OFF_QTYPE2 + x * PV_QTYPE_BINS], PV_QTYPE_BINS, 1), topn, pct);
         if (g & PV_DNS2_XACT_TIMES) {
-            quant_json(j, "xact_time_us", b.time2[x]);
-            hist_json(j, "xact_histogram_us", b.time2[x]);
+            quant_json(j, "xact_time_us", b.time2[x], &b.qs_time2[x]);
+            hist_json(j, "xact_histogram_us", b.hist_time2(x));
             top_json(j, "top_slow_xacts", tops(TM_SLOW_OUT), topn, pct);
         }
         j.end_obj();
@@ -1858,6 +1866,7 @@ void net2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
             uint64_t cnt;
             const uint64_t *h = &b.sum[PV_OFF_PAYLOAD2 + d * PV_PAYLOAD_BINS];
             auto q = hist_quantiles(h, PV_PAYLOAD_BINS, cnt);
+            if (cnt && !b.qs_payload2[d].empty()) q = b.qs_payload2[d];
             uint64_t mx = 0;
             for (size_t i = 0; i < PV_PAYLOAD_BINS; i++)
                 if (h[i]) mx = i;
@@ -1940,7 +1949,7 @@ void dns2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
             const auto &r = b.ratio2[x];
             if (!r.empty())
                 p.template summary<double>("dns_response_query_size_ratio", "Quantiles of ratio of packet sizes in a DNS transaction (reply/query)",
-                                           quantiles(r), vmax(r), r.size());
+                                           b.qs_ratio2[x].empty() ? quantiles(r) : b.qs_ratio2[x], vmax(r), r.size());
         }
         if (g & PV_DNS2_TOP_QTYPES)
             p.topn("dns_top_qtype_xacts", "qtype", "Top query types", dense_tops(&b.sum[PV_OFF_QTYPE2 + x * PV_QTYPE_BINS], PV_QTYPE_BINS, 1),
@@ -1949,8 +1958,8 @@ void dns2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
             const auto &t = b.time2[x];
             if (!t.empty())
                 p.template summary<uint64_t>("dns_xact_time_us", "Quantiles of transaction timing (query/reply pairs) in microseconds",
-                                             quantiles(t), vmax(t), t.size());
-            p.histogram("dns_xact_histogram_us", "Histogram of transaction timing (query/reply pairs) in microseconds", t);
+                                             b.qs_time2[x].empty() ? quantiles(t) : b.qs_time2[x], vmax(t), t.size());
+            p.histogram("dns_xact_histogram_us", "Histogram of transaction timing (query/reply pairs) in microseconds", b.hist_time2(x));
             p.topn("dns_top_slow_xacts", "qname", "Top QNAMES in transactions where host is the server and transaction speed is slower than p90",
                    tops(TM_SLOW_OUT), topn, pct);
         }
@@ -4711,19 +4720,26 @@ void bucket_fold_sum(HostBucket &d, const HostBucket &o, int part)
     d.period_length += o.period_length;
     if (o.start_sec < d.start_sec) { d.start_sec = o.start_sec; d.start_nsec = o.start_nsec; }
     if (o.end_sec > d.end_sec) { d.end_sec = o.end_sec; d.end_nsec = o.end_nsec; }
-    if (part == PART_NET) {
-        for (size_t i = 0; i < PV_SUM_NET_WORDS; i++)
-            if (i < PV_OFF_PAYLOAD || i >= PV_OFF_PAYLOAD + PV_PAYLOAD_BINS) d.sum[i] += o.sum[i];
-        // payload_size, a Quantile over the dense histogram
+    // payload_size, a Quantile over a dense histogram: an empty one merges the other's sketch,
+    // else the p-wise sums grow
+    auto payload_fold = [&](size_t off, std::vector<uint64_t> &qs) {
         uint64_t dn = 0, on = 0;
-        const auto dq = hist_quantiles(&d.sum[PV_OFF_PAYLOAD], PV_PAYLOAD_BINS, dn);
-        const auto oq = hist_quantiles(&o.sum[PV_OFF_PAYLOAD], PV_PAYLOAD_BINS, on);
+        const auto dq = hist_quantiles(&d.sum[off], PV_PAYLOAD_BINS, dn);
+        const auto oq = hist_quantiles(&o.sum[off], PV_PAYLOAD_BINS, on);
         if (!dn) {
-            for (size_t i = 0; i < PV_PAYLOAD_BINS; i++) d.sum[PV_OFF_PAYLOAD + i] += o.sum[PV_OFF_PAYLOAD + i];
+            for (size_t i = 0; i < PV_PAYLOAD_BINS; i++) d.sum[off + i] += o.sum[off + i];
         } else if (on) {
-            if (d.qs_payload.empty()) d.qs_payload = dq;
-            for (int i = 0; i < 4; i++) d.qs_payload[i] += oq[i];
+            if (qs.empty()) qs = dq;
+            for (int i = 0; i < 4; i++) qs[i] += oq[i];
         }
+    };
+    if (part == PART_NET) {
+        // counters (v1, and v2's per direction); Net v2 specialized_merge
+        // (net/v2/NetStreamHandler.cpp:286-331): per direction the same rules
+        for (size_t i = 0; i < PV_SUM_NET_WORDS; i++)
+            if ((i < PV_OFF_PAYLOAD || i >= PV_OFF_PAYLOAD + PV_PAYLOAD_BINS) && i < PV_OFF_PAYLOAD2) d.sum[i] += o.sum[i];
+        payload_fold(PV_OFF_PAYLOAD, d.qs_payload);
+        for (uint32_t x = 0; x < 3; x++) payload_fold(PV_OFF_PAYLOAD2 + x * PV_PAYLOAD_BINS, d.qs_payload2[x]);
     } else {
         for (size_t i = PV_OFF_DNS; i < PV_SUM_WORDS; i++) d.sum[i] += o.sum[i];
         // histograms merge their sketches; the quantiles follow the SUM rule
@@ -4734,6 +4750,18 @@ void bucket_fold_sum(HostBucket &d, const HostBucket &o, int part)
         qsum_fold(d.from_us, d.qs_from, o.from_us, o.qs_from);
         qsum_fold(d.to_us, d.qs_to, o.to_us, o.qs_to);
         qsum_fold(d.ratio, d.qs_ratio, o.ratio, o.qs_ratio);
+        // DNS v2 specialized_merge (dns/v2/DnsStreamHandler.cpp:619-676), per direction:
+        // dnsTimeUs and dnsRatio by the SUM rule, dnsHistTimeUs merging its sketch
+        if (!d.hist2_sep) {
+            for (uint32_t x = 0; x < 3; x++) d.htime2[x] = d.time2[x];
+            d.hist2_sep = true;
+        }
+        for (uint32_t x = 0; x < 3; x++) {
+            const auto &oh = o.hist_time2(x);
+            d.htime2[x].insert(d.htime2[x].end(), oh.begin(), oh.end());
+            qsum_fold(d.time2[x], d.qs_time2[x], o.time2[x], o.qs_time2[x]);
+            qsum_fold(d.ratio2[x], d.qs_ratio2[x], o.ratio2[x], o.qs_ratio2[x]);
+        }
     }
     for (size_t i = 0; i < PV_MIN_WORDS; i++) d.cpc[i] = std::min(d.cpc[i], o.cpc[i]); // CPC union (ICON)
     for (auto &m : o.tops)
@@ -4750,7 +4778,6 @@ int pv_bucket_merge(pv_ctx *c, uint32_t handler, pv_bucket **bucket, uint32_t pe
     std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
-    if (c->net2_groups || c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "bucket merge: the v2 handlers' buckets are not built");
     const int part = handler == PV_HANDLER_NET ? PART_NET : PART_DNS;
     const Window &w = part == PART_NET ? c->net : c->dns;
     if (*bucket && (*bucket)->part != part) return c->fail(PV_EINVAL, "bucket merge: a bucket of another handler");
@@ -4785,11 +4812,14 @@ int pv_bucket_json(pv_ctx *c, const pv_bucket *bk, char **out)
     Json j;
     j.obj();
     // window_external_json: {"<schema key>": {period, metrics}} (AbstractMetricsManager.h:589-599)
+    // (as pv_window_json: a Net bucket holds the v1 and v2 Net handlers' parts)
     if (bk->part == PART_NET) {
         if (c->net_groups) { j.key("packets").obj(); net_json(c, j, bk->b); j.end_obj(); }
+        if (c->net2_groups) { j.key("net").obj(); net2_json(c, j, bk->b); j.end_obj(); }
     } else if (c->dns_groups) {
         j.key("dns").obj();
-        dns_json(c, j, bk->b);
+        if (c->dns2_groups) dns2_json(c, j, bk->b);
+        else dns_json(c, j, bk->b);
         j.end_obj();
     }
     j.end_obj();
@@ -4809,8 +4839,14 @@ int pv_bucket_prometheus(pv_ctx *c, const pv_bucket *bk, const char *const *labe
         p.add[label_keys[i]] = label_values[i];
     }
     // window_external_prometheus (AbstractMetricsManager.h:580-587)
-    if (bk->part == PART_NET && c->net_groups) net_metrics(c, p, bk->b);
-    if (bk->part == PART_DNS && c->dns_groups) dns_metrics(c, p, bk->b);
+    if (bk->part == PART_NET && c->net_groups) {
+        net_metrics(c, p, bk->b);
+        if (c->net2_groups) net2_metrics(c, p, bk->b);
+    }
+    if (bk->part == PART_DNS && c->dns_groups) {
+        if (c->dns2_groups) dns2_metrics(c, p, bk->b);
+        else dns_metrics(c, p, bk->b);
+    }
     *out = strdup(p.o.str().c_str());
     return 0;
 }
@@ -4836,8 +4872,14 @@ int pv_bucket_opentelemetry(pv_ctx *c, const pv_bucket *bk, const char *const *l
         timespec_get(&now, TIME_UTC);
         p.t1 = (uint64_t)now.tv_sec * 1000000000ull + (uint64_t)now.tv_nsec;
     }
-    if (bk->part == PART_NET && c->net_groups) net_metrics(c, p, bk->b);
-    if (bk->part == PART_DNS && c->dns_groups) dns_metrics(c, p, bk->b);
+    if (bk->part == PART_NET && c->net_groups) {
+        net_metrics(c, p, bk->b);
+        if (c->net2_groups) net2_metrics(c, p, bk->b);
+    }
+    if (bk->part == PART_DNS && c->dns_groups) {
+        if (c->dns2_groups) dns2_metrics(c, p, bk->b);
+        else dns_metrics(c, p, bk->b);
+    }
     *out = (uint8_t *)malloc(p.out.s.size() ? p.out.s.size() : 1);
     if (!*out) return c->fail(PV_ECAPACITY, "bucket opentelemetry: out of host memory");
     memcpy(*out, p.out.s.data(), p.out.s.size());

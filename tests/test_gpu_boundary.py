@@ -166,6 +166,46 @@ def test_policy_bucket_merge(oracle, period, merged, prometheus):
             h.close()
 
 
+V2_ALL = ["cardinality", "counters", "quantiles", "top_ecs", "top_qtypes", "top_rcodes", "top_size", "top_qnames",
+          "top_ports", "xact_times"]
+
+
+def _ctx2(recs, periods=5):
+    h = pa.PvHandlers(host_spec=HOST, num_periods=periods, max_records=1 << 16, net2_config={},
+                      dns2_config={"enable": V2_ALL})
+    h.process_host(rec_bytes(recs))
+    h.set_end_tstamp(recs[-1][0], recs[-1][1] * 1000)
+    return h
+
+
+@pytest.mark.parametrize("period,merged,prometheus", [(0, False, False), (2, True, False), (0, False, True)])
+def test_policy_bucket_merge_v2(oracle, period, merged, prometheus):
+    """the v2 handlers' buckets (Net v2 "net", DNS v2 "dns") folded through pv_bucket_merge == the
+    oracle's policy merge (net/v2 ...cpp:286-331, dns/v2 ...cpp:619-676: per direction, quantiles
+    by the SUM rule, the xact time histogram merging)"""
+    pcaps = [open(os.path.join(GOLD, f), "rb").read() for f in CAPS]
+    parts = [records(p) for p in pcaps]
+    parts[0] = parts[0] + shifted(parts[0], 70)
+    files = [pcaps[0][:24] + rec_bytes(parts[0])] + pcaps[1:]
+    ctxs = [_ctx2(r) for r in parts]
+    try:
+        ref = oracle.run_policy(files, period=period, merged=merged, prometheus=prometheus, host_spec=HOST,
+                                num_periods=5, net2_groups=31, dns2_groups=0x3ff)
+        for handler, key in (("net", "net"), ("dns", "dns")):
+            b = None
+            for h in ctxs:
+                b = h.merge(handler, b, period, prometheus=prometheus, merged=merged)
+            got = ctxs[0].bucket_json(b)
+            assert diff(got[key], ref[key]) is None, (handler, diff(got[key], ref[key]))
+            txt = ctxs[0].bucket_prometheus(b, {"policy": "p"})
+            assert txt and ("net_" if key == "net" else "dns_xacts") in txt
+            assert len(ctxs[0].bucket_opentelemetry(b, {"policy": "p"})) > 0
+            b.free()
+    finally:
+        for h in ctxs:
+            h.close()
+
+
 def test_bucket_merge_quantile_sum(oracle):
     """Aggregate::SUM: quantiles of a merged bucket are the p-wise sums (Quantile::merge)"""
     pcaps = [open(os.path.join(GOLD, f), "rb").read() for f in CAPS[:2]]
