@@ -238,6 +238,11 @@ int pv_process_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes);
  * RESOLVER responses, the query time of their queries, else the wall clock. Not built: the
  * v2 handlers' dnstap paths (PV_EUNSUPPORTED) and the input's only_hosts filter. */
 int pv_process_dnstap(pv_ctx *ctx, const uint8_t *frames, size_t bytes, uint32_t msg_type_mask);
+/* The dnstap input proxy's "only_hosts" (DnstapInputEventProxy, src/inputs/dnstap/DnstapInputStream.h:
+ * 96-146): comma-separated CIDRs, parsed with parse_host_specs' error texts; NULL clears. A message is
+ * kept only when it has both addresses and one of them matches, with the reference's
+ * match_subnet(..., std::string) reading the raw address bytes as text. */
+int pv_set_dnstap_only_hosts(pv_ctx *ctx, const char *hosts);
 /* Frame Streams decode only: data frames read and dnstap MESSAGE events in them. */
 int pv_dnstap_count(const uint8_t *frames, size_t bytes, uint32_t *n_frames, uint32_t *n_events);
 

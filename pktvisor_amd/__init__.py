@@ -170,7 +170,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
            "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name",
-           "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit"]
+           "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_dnstap_only_hosts"]
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
@@ -257,6 +257,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_window_periods.argtypes = [P, ctypes.c_int, P, P, U32, ctypes.POINTER(U32)]
     lib.pv_set_dns_filters.argtypes = [P, ctypes.POINTER(pv_dns_filters)]
     lib.pv_set_tcp_reassembly_limit.argtypes = [P, ctypes.c_uint64]
+    lib.pv_set_dnstap_only_hosts.argtypes = [P, ctypes.c_char_p]
     lib.pv_dns_code.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(U32)]
     lib.pv_comm_unique_id.argtypes = [P]
     lib.pv_comm_init.argtypes = [P, P, ctypes.c_int, ctypes.c_int]
@@ -342,13 +343,15 @@ def dnstap_count(frames: bytes):
     return nf.value, ne.value
 
 
-def dnstap_reader(path: str, periods: int = 1, **kw) -> dict:
+def dnstap_reader(path: str, periods: int = 1, only_hosts: Optional[list] = None, **kw) -> dict:
     """A dnstap file (DnstapInputStream "dnstap_file") through the Net v1 ("packets") and DNS v1
-    ("dns") handlers: {"<periods>m": window}."""
+    ("dns") handlers: {"<periods>m": window}. only_hosts: the input proxy's filter config."""
     with open(path, "rb") as f:
         frames = f.read()
     h = PvHandlers(num_periods=periods, **kw)
     try:
+        if only_hosts is not None:
+            h._check(h.lib.pv_set_dnstap_only_hosts(h.ctx, ",".join(only_hosts).encode()), "pv_set_dnstap_only_hosts")
         h.process_dnstap(frames)
         key = f"{1 if periods == 1 else periods}m"
         return {key: h.window_json(0 if periods == 1 else periods, merged=periods != 1)}

@@ -676,6 +676,10 @@ struct pv_ctx {
     // tcp_packet_reassembly_cache_limit (0: not set): PcapInputStream's LRU list of connections,
     // replayed on the host across batches (front = most recently put; value = the put's second)
     uint64_t tcp_limit = 0;
+    // dnstap input proxy's only_hosts (DnstapInputEventProxy, src/inputs/dnstap/DnstapInputStream.h:96-146)
+    bool dt_only_hosts = false;
+    std::vector<std::pair<uint32_t, uint32_t>> dt_v4; // network (network order), cidr
+    std::vector<std::pair<std::array<uint8_t, 16>, uint32_t>> dt_v6;
     std::list<std::pair<uint32_t, uint32_t>> lru;
     std::unordered_map<uint32_t, std::list<std::pair<uint32_t, uint32_t>>::iterator> lru_at;
     std::unordered_map<uint32_t, bool> lru_pending; // evicted with no segment in their batch: closed at their next
@@ -3953,6 +3957,73 @@ int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int6
 // file (pv_dnstap.cpp) and lays each event out as a PvDtEv plus a linktype-101 record (IP
 // header with the query / response addresses, UDP header, the DNS message); the managers'
 // period shifts are applied between spans of events; pv_dnstap_kernel does the accounting.
+// lib::utils::match_subnet(IPv4subnetList &, IPv6subnetList &, const std::string &) as the
+// dnstap proxy calls it (libs/visor_utils/utils.cpp:26-80): the std::string is the message's raw
+// address bytes, which pcpp::IPv4Address / IPv6Address parse as TEXT (inet_pton on the string up
+// to its first NUL; an unparsable one is the unspecified address, which isValid() rejects), so a
+// 4- or 16-byte binary address practically never matches
+static bool dt_match_subnet(const pv_ctx *c, const std::vector<uint8_t> &raw)
+{
+    const std::string txt(raw.begin(), std::find(raw.begin(), raw.end(), (uint8_t)0));
+    in_addr a4{};
+    if (inet_pton(AF_INET, txt.c_str(), &a4) == 1 && a4.s_addr != 0) {
+        for (auto &n : c->dt_v4) {
+            if (n.second == 0) return true;
+            const uint32_t mask = htonl(0xFFFFFFFFu << (32 - n.second));
+            if (((a4.s_addr ^ n.first) & mask) == 0) return true;
+        }
+        return false;
+    }
+    uint8_t a6[16] = {0};
+    static const uint8_t zero[16] = {0};
+    if (inet_pton(AF_INET6, txt.c_str(), a6) == 1 && memcmp(a6, zero, 16) != 0) {
+        for (auto &n : c->dt_v6) {
+            const uint32_t bytes = n.second / 8, bits = n.second % 8;
+            bool r = false;
+            if (bytes > 0) r = memcmp(n.first.data(), a6, bytes) == 0;
+            if ((r || n.second < 8) && bits > 0) r = (n.first[bytes] >> (8 - bits)) == (a6[bytes] >> (8 - bits));
+            if (r) return true;
+        }
+    }
+    return false;
+}
+
+int pv_set_dnstap_only_hosts(pv_ctx *c, const char *hosts)
+{
+    if (!c) return PV_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->dt_v4.clear();
+    c->dt_v6.clear();
+    c->dt_only_hosts = hosts != nullptr;
+    if (!hosts) return 0;
+    // parse_host_specs (libs/visor_utils/utils.cpp:128-164), its error texts
+    const std::string s = hosts;
+    size_t pos = 0;
+    while (pos < s.size()) {
+        const size_t e = s.find(',', pos);
+        const std::string host = s.substr(pos, e == std::string::npos ? std::string::npos : e - pos);
+        pos = e == std::string::npos ? s.size() : e + 1;
+        if (host.empty()) continue;
+        const size_t d = host.find('/');
+        if (d == std::string::npos) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+        const std::string ip = host.substr(0, d), cs = host.substr(d + 1);
+        if (cs.empty() || !std::all_of(cs.begin(), cs.end(), ::isdigit)) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+        const int cidr = atoi(cs.c_str());
+        if (ip.find(':') != std::string::npos) {
+            std::array<uint8_t, 16> a{};
+            if (cidr < 0 || cidr > 128) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+            if (inet_pton(AF_INET6, ip.c_str(), a.data()) != 1) return c->fail(PV_EINVAL, "invalid IPv6 address: %s", ip.c_str());
+            c->dt_v6.push_back({a, (uint32_t)cidr});
+        } else {
+            in_addr a{};
+            if (cidr < 0 || cidr > 32) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
+            if (inet_pton(AF_INET, ip.c_str(), &a) != 1) return c->fail(PV_EINVAL, "invalid IPv4 address: %s", ip.c_str());
+            c->dt_v4.push_back({a.s_addr, (uint32_t)cidr});
+        }
+    }
+    return 0;
+}
+
 int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_type_mask)
 {
     std::lock_guard<std::mutex> g(c->mu);
@@ -3961,6 +4032,21 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
     std::vector<pvi::DtMessage> msgs;
     uint32_t frames = 0;
     pvi::dnstap_decode(buf, bytes, msgs, &frames);
+    if (c->dt_only_hosts) {
+        // DnstapInputEventProxy::dnstap_cb's only_hosts block, in its branch order: both addresses
+        // and neither matches, one address that does not match, and (its final else) every
+        // other message: filtered before any handler sees it
+        std::vector<pvi::DtMessage> kept;
+        for (auto &m : msgs) {
+            bool filt;
+            if (m.has_qaddr && m.has_raddr) filt = !dt_match_subnet(c, m.qaddr) && !dt_match_subnet(c, m.raddr);
+            else if (m.has_qaddr && !dt_match_subnet(c, m.qaddr)) filt = true;
+            else if (m.has_raddr && !dt_match_subnet(c, m.raddr)) filt = true;
+            else filt = true;
+            if (!filt) kept.push_back(std::move(m));
+        }
+        msgs.swap(kept);
+    }
     const size_t n = msgs.size();
     if (n == 0) return 0;
     if (n > 0x3fffffffull) return c->fail(PV_ECAPACITY, "too many dnstap events in one call");
