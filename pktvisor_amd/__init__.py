@@ -457,6 +457,7 @@ class PvHandlers:
             d2 = pvcfg.dns2_start(dict(dns2_config))
             dns2_groups = d2["groups"]
             filt = d2["filters"]
+            self.dnstap_mask = d2["dnstap_mask"]
             if d2["xact_ttl_ms"] is not None:
                 xact_ttl_ms = d2["xact_ttl_ms"]
         if net_config is not None or dns_config is not None or net2_config is not None or dns2_config is not None:
@@ -470,7 +471,8 @@ class PvHandlers:
             net_groups, dns_groups, net_filter_all = n["groups"], d["groups"], int(n["filter_all"])
             if dns2_config is None:
                 filt = d["filters"]
-            self.dnstap_mask = d["dnstap_mask"]
+            if dns2_config is None:
+                self.dnstap_mask = d["dnstap_mask"]
             if d["xact_ttl_ms"] is not None and dns2_config is None:
                 xact_ttl_ms = d["xact_ttl_ms"]
         self._host = host_spec.encode() if host_spec else None

@@ -182,15 +182,23 @@ DNS2_FILTER_KEYS = ("exclude_noerror", "only_rcode", "only_dnssec_response", "an
 def dns2_start(cfg: dict) -> dict:
     """DnsStreamHandler v2 start (src/handlers/dns/v2/DnsStreamHandler.cpp:43-236) up to the
     signal wiring: {"groups": bits | GROUPS_SET, "filters": pv_dns_filters fields (v2) or None,
-    "xact_ttl_ms": int|None}. The geo / ASN filters (no MaxMind database), dnstap_msg_type (no
-    v2 dnstap path) and public_suffix_list are not built for the GPU v2 handler; top_ecs keeps
+    "xact_ttl_ms": int|None}. The geo / ASN filters (no MaxMind database) and public_suffix_list are
+    not built for the GPU v2 handler; top_ecs keeps
     its geo / ASN tops empty (no MaxMind database)."""
     from pktvisor_amd import dns_filter_config
     validate_configs(cfg, DNS2_CONFIG_DEFS)
     groups = process_groups(cfg, DNS2_GROUP_DEFS, DNS2_DEFAULT_GROUPS)
-    for k in ("geoloc_notfound", "asn_notfound", "dnstap_msg_type", "public_suffix_list"):
+    for k in ("geoloc_notfound", "asn_notfound", "public_suffix_list"):
         if k in cfg:
             raise ConfigException(f"{k} is not supported by the GPU DNS v2 handler")
+    # dnstap_msg_type (dns/v2/DnsStreamHandler.cpp:176-190): as v1's
+    if "dnstap_msg_type" in cfg and cfg["dnstap_msg_type"] not in DNSTAP_MSG_TYPES:
+        raise ConfigException("DnsStreamHandler: dnstap_msg_type contained an invalid/unsupported type. Valid types: "
+                              + ", ".join(DNSTAP_MSG_TYPES))
+    mask = 0
+    if "dnstap_msg_type" in cfg:
+        q, r = DNSTAP_TYPE_PAIRS[cfg["dnstap_msg_type"]]
+        mask = (1 << q) | (1 << r)
     filters = None
     if any(k in cfg for k in DNS2_FILTER_KEYS) or "only_xact_directions" in cfg:
         filters = dns_filter_config({k: cfg[k] for k in DNS2_FILTER_KEYS if k in cfg}, v2=True)
@@ -209,7 +217,7 @@ def dns2_start(cfg: dict) -> dict:
         ttl = _uint(cfg, "xact_ttl_ms")
     elif "xact_ttl_secs" in cfg:
         ttl = _uint(cfg, "xact_ttl_secs") * 1000
-    return {"groups": groups | GROUPS_SET, "filters": filters, "xact_ttl_ms": ttl}
+    return {"groups": groups | GROUPS_SET, "filters": filters, "xact_ttl_ms": ttl, "dnstap_mask": mask}
 
 
 def dns_start(cfg: dict) -> dict:

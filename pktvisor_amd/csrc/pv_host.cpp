@@ -1329,8 +1329,9 @@ void dns2_json(pv_ctx *c, Json &j, const HostBucket &b)
         j.key(dirs[x]).obj();
         if (g & PV_DNS2_COUNTERS) {
             const std::pair<const char *, uint64_t> ctr[] = {
-                {"xacts", c2[D2_XACTS]}, {"udp_xacts", c2[D2_UDP]}, {"tcp_xacts", c2[D2_TCP]}, {"dot_xacts", 0},
-                {"doh_xacts", 0}, {"dnscrypt_udp_xacts", 0}, {"dnscrypt_tcp_xacts", 0}, {"doq_xacts", 0},
+                {"xacts", c2[D2_XACTS]}, {"udp_xacts", c2[D2_UDP]}, {"tcp_xacts", c2[D2_TCP]}, {"dot_xacts", c2[D2_DOT]},
+                {"doh_xacts", c2[D2_DOH]}, {"dnscrypt_udp_xacts", c2[D2_CRYPT_UDP]}, {"dnscrypt_tcp_xacts", c2[D2_CRYPT_TCP]},
+                {"doq_xacts", c2[D2_DOQ]},
                 {"ipv4_xacts", c2[D2_V4]}, {"ipv6_xacts", c2[D2_V6]}, {"nxdomain_xacts", c2[D2_NX]}, {"ecs_xacts", c2[D2_ECS]},
                 {"refused_xacts", c2[D2_REFUSED]}, {"srvfail_xacts", c2[D2_SRVFAIL]}, {"noerror_xacts", c2[D2_NOERROR]},
                 {"nodata_xacts", c2[D2_NODATA]}, {"authenticated_data_xacts", c2[D2_AD]},
@@ -1907,11 +1908,11 @@ void dns2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
             p.gauge("dns_xacts", "Total DNS transactions (query/reply pairs)", c2[D2_XACTS]);
             p.gauge("dns_udp_xacts", "Total DNS transactions (query/reply pairs) received over UDP", c2[D2_UDP]);
             p.gauge("dns_tcp_xacts", "Total DNS transactions (query/reply pairs) received over TCP", c2[D2_TCP]);
-            p.gauge("dns_dot_xacts", "Total DNS transactions (query/reply pairs) received over DNS over TLS", 0);
-            p.gauge("dns_doh_xacts", "Total DNS transactions (query/reply pairs) received over DNS over HTTPS", 0);
-            p.gauge("dns_dnscrypt_udp_xacts", "Total DNS transactions (query/reply pairs) received over DNSCrypt over UDP", 0);
-            p.gauge("dns_dnscrypt_tcp_xacts", "Total DNS transactions (query/reply pairs) received over DNSCrypt over TCP", 0);
-            p.gauge("dns_doq_xacts", "Total DNS transactions (query/reply pairs) received over DNS over QUIC", 0);
+            p.gauge("dns_dot_xacts", "Total DNS transactions (query/reply pairs) received over DNS over TLS", c2[D2_DOT]);
+            p.gauge("dns_doh_xacts", "Total DNS transactions (query/reply pairs) received over DNS over HTTPS", c2[D2_DOH]);
+            p.gauge("dns_dnscrypt_udp_xacts", "Total DNS transactions (query/reply pairs) received over DNSCrypt over UDP", c2[D2_CRYPT_UDP]);
+            p.gauge("dns_dnscrypt_tcp_xacts", "Total DNS transactions (query/reply pairs) received over DNSCrypt over TCP", c2[D2_CRYPT_TCP]);
+            p.gauge("dns_doq_xacts", "Total DNS transactions (query/reply pairs) received over DNS over QUIC", c2[D2_DOQ]);
             p.gauge("dns_ipv4_xacts", "Total DNS transactions (query/reply pairs) received over IPv4", c2[D2_V4]);
             p.gauge("dns_ipv6_xacts", "Total DNS transactions (query/reply pairs) received over IPv6", c2[D2_V6]);
             p.gauge("dns_nxdomain_xacts", "Total DNS transactions (query/reply pairs) flagged as reply with response code NXDOMAIN", c2[D2_NX]);
@@ -3957,6 +3958,7 @@ int pv_dns_event_seconds_host(pv_ctx *c, const uint8_t *recs, size_t bytes, int6
 // file (pv_dnstap.cpp) and lays each event out as a PvDtEv plus a linktype-101 record (IP
 // header with the query / response addresses, UDP header, the DNS message); the managers'
 // period shifts are applied between spans of events; pv_dnstap_kernel does the accounting.
+int dns_period_shift(pv_ctx *c, int64_t sec, int64_t nsec);
 // lib::utils::match_subnet(IPv4subnetList &, IPv6subnetList &, const std::string &) as the
 // dnstap proxy calls it (libs/visor_utils/utils.cpp:26-80): the std::string is the message's raw
 // address bytes, which pcpp::IPv4Address / IPv6Address parse as TEXT (inet_pton on the string up
@@ -4028,7 +4030,6 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
 {
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
-    if (c->net2_groups || c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "dnstap input with the v2 handlers is not built");
     std::vector<pvi::DtMessage> msgs;
     uint32_t frames = 0;
     pvi::dnstap_decode(buf, bytes, msgs, &frames);
@@ -4099,7 +4100,19 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         }
         const uint8_t *msg = nullptr;
         size_t mlen = 0;
-        if (!m.has_qmsg && !m.has_rmsg) e.dns_mode = PV_DT_SIDE;
+        if (c->dns2_groups) {
+            // DNS v2 (dns/v2 ...cpp:1176-1270): the transaction direction by message type, a
+            // response with its message ends a transaction, else a query message starts one.
+            // pad[1]: direction | response << 2 | a message << 3 | socket protocol << 4
+            const uint32_t xd = (t == 5 || t == 6 || t == 1 || t == 2 || t == 13 || t == 14) ? 0u
+                              : ((t >= 3 && t <= 4) || (t >= 7 && t <= 12)) ? 1u : 2u;
+            uint32_t v2 = xd;
+            if (e.side == 1 && m.has_rmsg) { v2 |= 4u | 8u; msg = m.rmsg; mlen = m.rmsg_len; }
+            else if (m.has_qmsg) { v2 |= 8u; msg = m.qmsg; mlen = m.qmsg_len; }
+            if (m.has_protocol && m.protocol >= 1 && m.protocol <= 7) v2 |= (uint32_t)m.protocol << 4;
+            e.pad[1] = (uint8_t)v2;
+            e.dns_mode = msg ? PV_DT_MESSAGE : PV_DT_EVENT_ONLY;
+        } else if (!m.has_qmsg && !m.has_rmsg) e.dns_mode = PV_DT_SIDE;
         else if (e.side == 0 && m.has_qmsg) { e.dns_mode = PV_DT_MESSAGE; msg = m.qmsg; mlen = m.qmsg_len; }
         else if (e.side == 1 && m.has_rmsg) { e.dns_mode = PV_DT_MESSAGE; msg = m.rmsg; mlen = m.rmsg_len; }
         else e.dns_mode = PV_DT_EVENT_ONLY;
@@ -4190,18 +4203,40 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         P.ovf = c->d_ovf;
         P.ovf_cnt = c->d_ovf_cnt;
         P.ovf_cap = c->ovf_cap;
-        P.want_events = 0;
+        const uint32_t blocks = (uint32_t)((b - a + 255) / 256);
+        // DNS v2: transaction events, one 256-event region per block (pv_xact_compact), paired by
+        // the transaction stage as a pcap batch's are
+        P.want_events = c->dns2_groups ? 1u : 0u;
+        if (P.want_events) {
+            if (b - a > c->max_records) return c->fail(PV_ECAPACITY, "a dnstap period span exceeds max_records events");
+            P.events = c->d_events;
+            P.eecs = c->d_eecs;
+            P.ekeys = c->d_ekeys;
+            P.blk_events = c->d_blk_events;
+            P.skeys = c->d_skeys;
+            P.svals = c->d_svals;
+            P.n_events = c->d_status + ST_NEV;
+            P.wt_per_block = 4; // 64-record tiles: 256 events per block
+            P.grid_main = blocks;
+            if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
+            P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
+            launch_fill32(c, c->d_status, ST_ALLOC, 0);
+        }
         launch_fill32(c, c->d_status + ST_FLAGS, 1, 0);
         flush_fills(c);
         *c->h_params = P;
         if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
             return c->hipfail(e, "parameter upload");
-        hipLaunchKernelGGL(pv_dnstap_kernel, dim3((uint32_t)((b - a + 255) / 256)), dim3(256), 0, st, (const PvParams *)c->d_params);
+        hipLaunchKernelGGL(pv_dnstap_kernel, dim3(blocks), dim3(256), 0, st, (const PvParams *)c->d_params);
+        if (P.want_events) hipLaunchKernelGGL(pv_xact_compact, dim3(blocks), dim3(256), 0, st, (const PvParams *)c->d_params, blocks);
         if (!hip_ok(e = hipGetLastError()) ||
-            !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
-            !hip_ok(e = hipMemcpyAsync(c->h_tab_live, c->d_tab_live, PV_TABLES * 4, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_RB_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "pv_dnstap_kernel");
+        if (P.want_events) {
+            const uint32_t nev = c->h_status[ST_NEV], nresp = c->h_status[ST_NRESP];
+            if (int rc = pair_stage(c, P, nev, nresp, b - a, st)) return rc;
+        }
         if (int rc = drain_overflow(c, st)) return rc;
         uint32_t flags = 0;
         if (!hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
@@ -4221,7 +4256,10 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         if (!ns && !ds) continue;
         if (int rc = span(a, j)) return rc;
         if (ns) { clear_part(c, PART_NET, c->net.slot_at(1)); win_shift(c, c->net, ssec[j]); }
-        if (ds) { clear_part(c, PART_DNS, c->dns.slot_at(1)); win_shift(c, c->dns, ssec[j]); }
+        if (ds && c->dns2_groups) {
+            // DNS v2's on_period_shift purge of the open transactions (as a heartbeat shift)
+            if (int rc = dns_period_shift(c, ssec[j], snsec[j])) return rc;
+        } else if (ds) { clear_part(c, PART_DNS, c->dns.slot_at(1)); win_shift(c, c->dns, ssec[j]); }
         a = j;
     }
     if (int rc = span(a, n)) return rc;
@@ -4679,6 +4717,14 @@ int pv_check_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
         win_shift(c, c->net, sec, nsec);
     }
     if (sec < c->dns.next_shift_sec) return 0;
+    return dns_period_shift(c, sec, nsec);
+}
+
+// The DNS manager's shift at `sec` with no event (a heartbeat, or a dnstap span boundary): the
+// new live bucket, DnsMetricsManager::on_period_shift's purge of the open transactions through
+// the pairing stage, the slow thresholds of the bucket just closed
+int dns_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
+{
     hipStream_t st = c->stream;
     const uint32_t s0 = c->dns.slot_at(0), s1 = c->dns.slot_at(1);
     clear_part(c, PART_DNS, s1);

@@ -1019,7 +1019,7 @@ __device__ void cache_flush(PV_CREF(PvParams) P, Cache &C, uint32_t n, uint32_t 
 #define PV_WT 64      // records per wave tile
 #define PV_WSTAGE 8192 // DNS pass: LDS staging bytes per wave (128-B message windows)
 #ifndef PV_NCACHE
-#define PV_NCACHE 2048
+#define PV_NCACHE 4096 // DNS-pass key cache entries (4096: C3 combine + merge 573 -> 543 us, profiles/r3_s2/nc4096)
 #endif
 static_assert(PV_NCACHE <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cache entries per flush");
 
@@ -3490,11 +3490,25 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_tcp_filter(const PvPara
 // DnsMetricsManager / DnsMetricsBucket::process_dnstap (dns/v1 ...cpp:839-909,1376-1412:
 // dnstap_msg_type filter, counters by side without a message, else process_dns_layer on the
 // message). Events are few next to packets: counters and tables are updated in HBM directly.
+__device__ void dnstap_event(PV_CREF(PvParams) P, uint32_t j, uint32_t *nev, uint32_t *nresp);
 extern "C" __global__ void __launch_bounds__(256) pv_dnstap_kernel(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t nev, nresp;
+    if (threadIdx.x == 0) { nev = 0; nresp = 0; }
+    __syncthreads();
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= P.n) return;
+    if (j < P.n) dnstap_event(P, j, &nev, &nresp);
+    if (!P.want_events) return;
+    // DNS v2: this block's transaction events (pv_xact_compact packs the regions)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        P.blk_events[blockIdx.x] = nev;
+        if (nresp) atomicAdd(P.n_events + 1, nresp);
+    }
+}
+__device__ void dnstap_event(PV_CREF(PvParams) P, uint32_t j, uint32_t *nev, uint32_t *nresp)
+{
     const PvDtEv e = reinterpret_cast<const PV_G PvDtEv *>(P.dq)[j];
     const GAcc R{P.recs};
     const uint64_t gidx = P.gbase + j;
@@ -3532,6 +3546,70 @@ extern "C" __global__ void __launch_bounds__(256) pv_dnstap_kernel(const PvParam
                 if (tops) global_add(P, s, PV_KEY(TM_IPV6, (h1 ^ (h2 << 1)) & ((1ull << 55) - 1)), 1, j);
             }
         }
+    }
+    // ---- Net v2 (net/v2/NetStreamHandler.cpp:533-604): the same events by direction; deep, the
+    // query address as the source and the response address as the destination, both counted
+    if (P.net2_groups) {
+        const uint32_t s = P.slot_of[0], d = e.dir;
+        const bool deep = !(e.pad[0] & 1);
+        sum_add(P, s, PV_OFF_NET2 + N2_EVENTS, 1);
+        if (deep) sum_add(P, s, PV_OFF_NET2 + N2_SAMPLES, 1);
+        const uint32_t dc = PV_OFF_NET2 + N2_DIR + 8 * d;
+        sum_add(P, s, dc + N2_TOTAL, 1);
+        if (e.l3) sum_add(P, s, dc + (e.l3 == 4 ? N2_V4 : N2_V6), 1);
+        sum_add(P, s, dc + (e.l4 == 17 ? N2_UDP : (e.l4 == 6 ? N2_TCP : N2_OTHER)), 1);
+        sum_add(P, s, PV_OFF_PAYLOAD2 + d * PV_PAYLOAD_BINS + min(e.size, 65535u), 1);
+        const bool card = P.net2_groups & PV_N2G_CARDINALITY, tops = P.net2_groups & PV_N2G_TOP_IPS;
+        for (int side = 0; side < 2 && deep; side++) {
+            const uint8_t *a = side ? e.raddr : e.qaddr;
+            const uint32_t alen = side ? e.rlen : e.qlen;
+            if (e.l3 == 4 && alen == 4) {
+                const uint32_t ip = (uint32_t)a[0] | ((uint32_t)a[1] << 8) | ((uint32_t)a[2] << 16) | ((uint32_t)a[3] << 24);
+                if (!ip) continue;
+                if (card) cpc_min(P, s, CPC_V2 + d, ip4_coupon(ip), (int64_t)(P.gbase + j));
+                if (tops) global_add(P, s, PV_V2_IP4(d, ip), 1, j);
+            } else if (e.l3 == 6 && alen == 16) {
+                uint64_t w0 = 0, w1 = 0;
+                for (int b = 0; b < 8; b++) { w0 |= (uint64_t)a[b] << (8 * b); w1 |= (uint64_t)a[8 + b] << (8 * b); }
+                if (!(w0 | w1)) continue;
+                uint64_t h1, h2;
+                murmur_16(w0, w1, h1, h2);
+                if (card) cpc_min(P, s, CPC_V2 + d, cpc_coupon(h1, h2), (int64_t)(P.gbase + j));
+                if (tops) global_add(P, s, PV_V2_IP6(d, h1 ^ (h2 << 1)), 1, j);
+            }
+        }
+    }
+    // ---- DNS v2 (DnsMetricsManager::process_dnstap, dns/v2/DnsStreamHandler.cpp:1176-1270): the
+    // transaction direction by message type; a response with its message ends the transaction
+    // DnsXactID(transactionID, 2) of that direction's map, else a query message starts one
+    if (P.dns2_groups) {
+        const uint32_t s = P.dslot_of[0];
+        const bool ddeep = !(e.pad[0] & 2);
+        sum_add(P, s, PV_OFF_DNS + DC_EVENTS, 1);
+        if (ddeep) sum_add(P, s, PV_OFF_DNS + DC_SAMPLES, 1);
+        if (e.filtered) {
+            if (P.dns2_groups & PV_D2G_COUNTERS) sum_add(P, s, PV_OFF_DNS + DC_FILTERED, 1);
+            return;
+        }
+        const uint32_t v2 = e.pad[1]; // xd | qr << 2 | has a message << 3 | socket protocol << 4
+        if (!(v2 & 8) || !P.want_events) return;
+        const GAcc R{P.recs};
+        const uint32_t txid = e.mlen >= 2 ? (R.u8(e.moff) << 8) | R.u8(e.moff + 1) : 0u;
+        PvXEvent ev;
+        ev.key = ((uint64_t)txid << 16) | 2u | ((uint64_t)((v2 & 3) + 1) << 48);
+        ev.idx = j;
+        ev.len = e.mlen;
+        ev.sec = e.sec;
+        ev.nsec = (int32_t)e.nsec;
+        ev.qr = (uint8_t)((v2 >> 2) & 1);
+        ev.dir = (uint8_t)(0x80u | ((e.l3 == 4 ? 1u : (e.l3 == 6 ? 2u : 0u)) << 4) | ((v2 >> 4) & 7));
+        ev.period = 0;
+        ev.pad = ddeep ? 0 : 32; // a dnstap query: CD false, no subnet (start_transaction :1265-1268)
+        const uint64_t eidx = (uint64_t)blockIdx.x * P.wt_per_block * PV_WT + atomicAdd(nev, 1u);
+        if (ev.qr) atomicAdd(nresp, 1u);
+        P.events[eidx] = ev;
+        P.ekeys[eidx] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + (j << 2));
+        return;
     }
     // ---- DNS v1
     {
@@ -3711,8 +3789,18 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
     uint32_t *c = T.c2[period][xd];
     if (g & PV_D2G_COUNTERS) {
         atomicAdd(&c[D2_XACTS], 1u);
-        atomicAdd(&c[(e.pad & 2) ? D2_V6 : D2_V4], 1u);
-        atomicAdd(&c[tcp ? D2_TCP : D2_UDP], 1u);
+        if (e.dir & 0x80) {
+            // a dnstap event: l3 from socket_family, l4 the socket protocol (new_dns_transaction :936-970)
+            const uint32_t l3 = (e.dir >> 4) & 3, pr = e.dir & 7;
+            if (l3) atomicAdd(&c[l3 == 2 ? D2_V6 : D2_V4], 1u);
+            if (pr) {
+                const uint32_t w[8] = {0, D2_UDP, D2_TCP, D2_DOT, D2_DOH, D2_CRYPT_UDP, D2_CRYPT_TCP, D2_DOQ};
+                atomicAdd(&c[w[pr]], 1u);
+            }
+        } else {
+            atomicAdd(&c[(e.pad & 2) ? D2_V6 : D2_V4], 1u);
+            atomicAdd(&c[tcp ? D2_TCP : D2_UDP], 1u);
+        }
         if (qe.pad & 1) atomicAdd(&c[D2_CD], 1u);
         if (rcode == 0) { atomicAdd(&c[D2_NOERROR], 1u); if (!an) atomicAdd(&c[D2_NODATA], 1u); }
         else if (rcode == 2) atomicAdd(&c[D2_SRVFAIL], 1u);

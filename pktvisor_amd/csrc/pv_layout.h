@@ -83,7 +83,7 @@
 #define PV_OFF_RCODE (PV_OFF_QTYPE + PV_QTYPE_BINS)
 // DNS v2 (src/handlers/dns/v2), in place of v1 when configured: per transaction direction
 // (0 in, 1 out, 2 unknown) its counters, then its port / qtype / rcode tables
-#define PV_DNS2_CTRS 20
+#define PV_DNS2_CTRS 24
 #define PV_OFF_DNS2 (PV_OFF_RCODE + PV_RCODE_BINS)              // + dir * PV_DNS2_CTRS
 #define PV_OFF_PORT2 (PV_OFF_DNS2 + 4 * PV_DNS2_CTRS)           // + dir * PV_PORT_BINS
 #define PV_OFF_QTYPE2 (PV_OFF_PORT2 + 3 * PV_PORT_BINS)         // + dir * PV_QTYPE_BINS
@@ -99,7 +99,9 @@ enum {
 // the responses and purge time-outs that set the direction up (DnsMetricsBucket::dir_setup)
 enum {
     D2_SEEN = 0, D2_XACTS, D2_UDP, D2_TCP, D2_V4, D2_V6, D2_NX, D2_REFUSED, D2_SRVFAIL, D2_NOERROR, D2_NODATA, D2_AA,
-    D2_AD, D2_CD, D2_TIMEOUT, D2_ORPHAN, D2_ECS, D2_N
+    D2_AD, D2_CD, D2_TIMEOUT, D2_ORPHAN, D2_ECS,
+    D2_DOT, D2_DOH, D2_CRYPT_UDP, D2_CRYPT_TCP, D2_DOQ, // dnstap socket protocols (Protocol, dns/v2 ...h:62-73)
+    D2_N
 };
 // Net v2 counters (src/handlers/net/v2/NetStreamHandler.h:61-96): base events, then per
 // direction d (0 in, 1 out, 2 unknown) at N2_DIR + 8 d

@@ -146,3 +146,48 @@ def test_dnstap_only_hosts_invalid(spec, err):
             h._check(h.lib.pv_set_dnstap_only_hosts(h.ctx, spec.encode()), "pv_set_dnstap_only_hosts")
     finally:
         h.close()
+
+
+# ---- the v2 handlers over dnstap (net/v2 ...cpp:533-604, dns/v2 ...cpp:1176-1270)
+def test_dns2_dnstap_kat():
+    """src/handlers/dns/v2/tests/test_dnstap.cpp:12-64 "Parse DNSTAP" (enable top_size, top_ports):
+    transactions DnsXactID(transactionID, 2) per direction of the message type"""
+    out = pa.dnstap_reader(FIX, periods=1, dns2_config={"enable": ["top_size", "top_ports"]})
+    d = out["1m"]["dns"]
+    assert (d["observed_packets"], d["deep_sampled_packets"]) == (153, 153)
+    want = {"tcp_xacts": 0, "udp_xacts": 72, "dot_xacts": 0, "doh_xacts": 0, "dnscrypt_udp_xacts": 0,
+            "dnscrypt_tcp_xacts": 0, "doq_xacts": 0, "ipv4_xacts": 72, "ipv6_xacts": 0, "xacts": 72,
+            "timeout_queries": 0, "orphan_responses": 2, "noerror_xacts": 68, "nxdomain_xacts": 0,
+            "refused_xacts": 0, "srvfail_xacts": 4}
+    for k, v in want.items():
+        assert d["in"][k] == v, k
+    assert d["in"]["cardinality"]["qname"] == 65
+    assert d["in"]["top_qname2_xacts"][0] == {"name": ".google.com", "estimate": 9}
+    assert d["in"]["top_udp_ports_xacts"][0]["estimate"] == 2
+    assert d["in"]["top_qtype_xacts"][:2] == [{"name": "A", "estimate": 70}, {"name": "HTTPS", "estimate": 2}]
+
+
+def test_net2_dnstap_kat():
+    """src/handlers/net/v2/tests/test_net_layer.cpp:321-358 "Parse net dnstap stream" """
+    out = pa.dnstap_reader(FIX, periods=1, net2_config={})
+    n = out["1m"]["net"]
+    assert (n["observed_packets"], n["deep_sampled_packets"]) == (153, 153)
+    for k, v in {"tcp_packets": 0, "udp_packets": 79, "ipv4_packets": 79, "ipv6_packets": 0, "total_packets": 79}.items():
+        assert n["in"][k] == v, k
+    assert n["in"]["tcp"]["syn_packets"] == 0
+    assert n["in"]["cardinality"]["ips"] == 2
+    assert n["in"]["top_ipv4_packets"][0] == {"name": "192.168.0.54", "estimate": 79}
+    assert n["in"]["payload_size_bytes"]["p50"] == 89
+
+
+@pytest.mark.parametrize("periods", [1, 3])
+def test_dns2_dnstap_windows_and_filter(periods):
+    """dnstap_msg_type with DNS v2 (process_filtered(stamp): an event, `filtered_packets`, no
+    transaction) and the window shifts between dnstap spans (the open transactions' purge)"""
+    out = pa.dnstap_reader(FIX, periods=periods, dns2_config={"dnstap_msg_type": "auth"})
+    d = out[f"{periods}m"]["dns"]
+    assert (d["observed_packets"], d["filtered_packets"]) == (153, 153)
+    assert "in" not in d and "out" not in d
+    out = pa.dnstap_reader(FIX, periods=periods, dns2_config={})
+    d = out[f"{periods}m"]["dns"]
+    assert d["observed_packets"] == 153 and d["in"]["xacts"] == 72
