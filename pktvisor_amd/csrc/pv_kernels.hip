@@ -2927,6 +2927,7 @@ struct MergeState {
     uint32_t mn[2][PV_RS]; // smallest record index of an IPv4 key per direction (CPC)
     uint32_t nidx[PV_RS]; // entries created in this batch: region index, source record
     uint32_t nrep[PV_RS];
+    uint8_t dirty[PV_RS]; // entries this batch changed (only those are written back)
     uint32_t nnew, nbase, ncr;
 };
 // The region's runs in the combine workgroups' region-sorted lists (cb_run): run w holds
@@ -3014,6 +3015,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                    [&](uint64_t i, ulonglong2 kc) {
                        S.key[i] = kc.x;
                        S.cnt[i] = kc.x ? kc.y : 0; // an empty entry's count word is stale
+                       S.dirty[i] = !kc.x && kc.y;  // written back as zero
                        S.mn[0][i] = 0xffffffffu;
                        S.mn[1][i] = 0xffffffffu;
                    });
@@ -3036,6 +3038,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                 }
                 if (cur == key) {
                     const uint32_t w = (uint32_t)e1;
+                    S.dirty[pos] = 1;
                     if (w & PV_W_IP4) {
                         atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)(w & PV_W_CNT));
                         if ((w >> 29) & 1) atomicMin(&S.mn[(w >> 30) & 1][pos], (uint32_t)(e1 >> 32));
@@ -3065,8 +3068,10 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         });
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
-            P.tkeys[rbase + i] = S.key[i];
-            P.tcnt[rbase + i] = S.cnt[i];
+            if (S.dirty[i]) {
+                P.tkeys[rbase + i] = S.key[i];
+                P.tcnt[rbase + i] = S.cnt[i];
+            }
             // IPv4 cardinality: one first-occurrence update per address and direction
             for (uint32_t d = 0; d < 2; d++)
                 if (S.mn[d][i] != 0xffffffffu)
