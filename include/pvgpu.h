@@ -265,6 +265,51 @@ int pv_pcapng_records(const uint8_t *buf, size_t bytes, uint8_t *out, size_t out
 int pv_tpacket3_block_records(const uint8_t *block, size_t block_size, uint8_t *out, size_t out_cap, size_t *out_bytes,
                               uint64_t *n_records);
 
+/* AF_PACKET live capture (visor::input::pcap::AFPacket, src/inputs/pcap/afpacket.cpp:22-262):
+ * the TPACKET_V3 ring loop in front of pv_process_host. A capture thread waits on the ring
+ * (poll), turns every block the kernel hands over into pcap records in a page-locked staging
+ * buffer (pv_tpacket3_block_records) and gives the block back at once; a processing thread runs
+ * pv_process_host on each full buffer (batch_bytes, or after flush_ms without a full one) while
+ * the other fills. The context must be created with linktype 1 and ts_nano = 1. */
+typedef struct pv_afpacket pv_afpacket;
+typedef struct pv_afpacket_config {
+    const char *interface;  /* "any" (default) or an interface name (AFPacket::set_interface) */
+    int fanout_group_id;    /* -1: no fanout; else a PACKET_FANOUT_LB group (AFPacket::setup) */
+    uint32_t block_size;    /* ring block bytes (0: 1 << 22, afpacket.h) */
+    uint32_t frame_size;    /* 0: 1 << 11 */
+    uint32_t num_blocks;    /* 0: 64 */
+    const void *bpf_insns;  /* a compiled classic BPF program (struct sock_filter[]) or NULL: what
+                               filter_try_compile hands to SO_ATTACH_FILTER (no libpcap here) */
+    uint32_t bpf_len;       /* instructions */
+    uint32_t batch_bytes;   /* staging bytes per pv_process_host call (0: 64 MiB) */
+    uint32_t flush_ms;      /* a partial batch goes after this long without a new block (0: 100) */
+} pv_afpacket_config;
+typedef struct pv_afpacket_counters {
+    uint64_t blocks, packets, batches, bytes;            /* ring blocks walked, packets, batches, record bytes */
+    uint64_t kernel_packets, kernel_drops, kernel_freezes; /* PACKET_STATISTICS (tpacket_stats_v3), socket mode */
+} pv_afpacket_counters;
+/* Records of one staging buffer, in capture order; nonzero return stops the capture. */
+typedef int (*pv_afpacket_sink)(void *user, const uint8_t *recs, size_t bytes, uint64_t n_records);
+/* The socket, ring and fanout of AFPacket::AFPacket / set_socket_opts / setup. Needs CAP_NET_RAW
+ * (PV_EUNSUPPORTED without it). Messages: pv_afpacket_last_error (this thread). */
+int pv_afpacket_open(const pv_afpacket_config *cfg, pv_afpacket **out);
+/* The same loop over a ring mapped by the caller: num_blocks blocks of block_size bytes laid out
+ * as the kernel fills them (tpacket_block_desc + tpacket3_hdr packets); a block is the loop's
+ * when its block_status has TP_STATUS_USER and is returned with TP_STATUS_KERNEL. wake_fd: an
+ * eventfd the ring's producer signals (polled as the socket would be), or -1 to spin. */
+int pv_afpacket_attach(uint8_t *ring, uint32_t block_size, uint32_t num_blocks, int wake_fd, const pv_afpacket_config *cfg,
+                       pv_afpacket **out);
+/* Capture on the calling thread until pv_afpacket_stop (from another thread), feeding sink;
+ * returns the first sink / ring failure, 0 after a stop (the last partial batch delivered). */
+int pv_afpacket_run(pv_afpacket *a, pv_afpacket_sink sink, void *user);
+/* AFPacket::start_capture: the loop on its own thread feeding pv_process_host(ctx). */
+int pv_afpacket_start(pv_afpacket *a, pv_ctx *ctx);
+/* AFPacket::stop_capture: ends the loop (after delivering the partial batch); the loop's status. */
+int pv_afpacket_stop(pv_afpacket *a);
+int pv_afpacket_stats(pv_afpacket *a, pv_afpacket_counters *out);
+void pv_afpacket_close(pv_afpacket *a);
+const char *pv_afpacket_last_error(void);
+
 /* Page-lock a host range so pv_process_host DMAs from it directly (hipHostRegister). */
 int pv_host_register(void *ptr, size_t bytes);
 int pv_host_unregister(void *ptr);

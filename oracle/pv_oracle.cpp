@@ -1490,7 +1490,7 @@ struct Engine {
                     uint16_t ancount, uint16_t txid)
     {
         const uint8_t *h = hm.d;
-        const size_t suffix_size = 0;
+        size_t suffix_size = 0; // DnsStreamHandler::_configs, v2 (:612-619): set below for a response
         const bool filt = dns2_filtering(p, m, hdr12, qr, rcode, ancount);
         // new_event(stamp) draws; process_filtered's new_event(stamp, false) keeps the last flag
         const bool deep = dns2_s.draw(!filt);
@@ -1563,6 +1563,9 @@ struct Engine {
                 x.rcode.update(rcode);
                 if (r.has_query) {
                     const std::string name = lower(r.name);
+                    // public_suffix_list while only_qname_suffix is off: match_public_suffix of the
+                    // response's first query name, new_dns_transaction's suffix_size (:1067-1072)
+                    if (cfg.psl && cfg.only_qname_suffix.empty()) suffix_size = match_public_suffix(name);
                     if (g & D2G_CARDINALITY) x.qname.update_str(name);
                     x.qtype.update(r.qtype);
                     if (g & D2G_TOP_RCODES) {

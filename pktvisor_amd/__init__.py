@@ -170,11 +170,27 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
            "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name",
-           "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_dnstap_only_hosts"]
+           "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_dnstap_only_hosts",
+           "pv_afpacket_open", "pv_afpacket_attach", "pv_afpacket_run", "pv_afpacket_start", "pv_afpacket_stop",
+           "pv_afpacket_stats", "pv_afpacket_close", "pv_afpacket_last_error"]
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
+
+
+class pv_afpacket_config(ctypes.Structure):
+    _fields_ = [("interface", ctypes.c_char_p), ("fanout_group_id", ctypes.c_int), ("block_size", ctypes.c_uint32),
+                ("frame_size", ctypes.c_uint32), ("num_blocks", ctypes.c_uint32), ("bpf_insns", ctypes.c_void_p),
+                ("bpf_len", ctypes.c_uint32), ("batch_bytes", ctypes.c_uint32), ("flush_ms", ctypes.c_uint32)]
+
+
+class pv_afpacket_counters(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in ("blocks", "packets", "batches", "bytes", "kernel_packets", "kernel_drops",
+                                              "kernel_freezes")]
+
+
+AFPACKET_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64)
 
 
 class pv_region(ctypes.Structure):
@@ -270,6 +286,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_pcapng_records.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                       ctypes.POINTER(U32), ctypes.POINTER(U64)]
     lib.pv_dnstap_count.argtypes = [P, ctypes.c_size_t, ctypes.POINTER(U32), ctypes.POINTER(U32)]
+    lib.pv_afpacket_open.argtypes = [ctypes.POINTER(pv_afpacket_config), ctypes.POINTER(P)]
+    lib.pv_afpacket_attach.argtypes = [P, U32, U32, ctypes.c_int, ctypes.POINTER(pv_afpacket_config), ctypes.POINTER(P)]
+    lib.pv_afpacket_run.argtypes = [P, AFPACKET_SINK, P]
+    lib.pv_afpacket_start.argtypes = [P, P]
+    lib.pv_afpacket_stop.argtypes = [P]
+    lib.pv_afpacket_stats.argtypes = [P, ctypes.POINTER(pv_afpacket_counters)]
+    lib.pv_afpacket_close.argtypes = [P]
+    lib.pv_afpacket_close.restype = None
+    lib.pv_afpacket_last_error.restype = ctypes.c_char_p
     _lib = lib
     return lib
 
@@ -423,6 +448,89 @@ def add_static_label(key: str, value: str) -> None:
     """Metric::add_static_label: a label on every Prometheus sample of every handler."""
     if load_library().pv_add_static_label(key.encode(), value.encode()):
         raise PvError(f"pv_add_static_label({key!r}) failed")
+
+
+class AfPacket:
+    """The AF_PACKET TPACKET_V3 capture loop (pv_afpacket_*, AFPacket in
+    src/inputs/pcap/afpacket.cpp): AfPacket.open(interface, ...) binds a raw socket and its ring
+    (CAP_NET_RAW); AfPacket.attach(ring, block_size, num_blocks, wake_fd) runs the same loop over a
+    ring the caller maps. start(handlers) feeds pv_process_host on a capture thread (handlers made
+    with linktype 1, ts_nano 1); run(fn) captures on the calling thread into fn(records_bytes,
+    n_records) until stop() is called from another thread."""
+
+    def __init__(self, ptr, keep=None):
+        self.lib = load_library()
+        self.ptr = ptr
+        self._keep = keep
+
+    @staticmethod
+    def _cfg(**kw):
+        c = pv_afpacket_config()
+        c.interface = kw.get("interface", "any").encode()
+        c.fanout_group_id = kw.get("fanout_group_id", -1)
+        for k in ("block_size", "frame_size", "num_blocks", "batch_bytes", "flush_ms"):
+            setattr(c, k, int(kw.get(k, 0)))
+        bpf = kw.get("bpf")  # bytes of struct sock_filter[] (8 B each)
+        if bpf:
+            buf = ctypes.create_string_buffer(bytes(bpf), len(bpf))
+            c.bpf_insns = ctypes.cast(buf, ctypes.c_void_p)
+            c.bpf_len = len(bpf) // 8
+            c._buf = buf
+        return c
+
+    @classmethod
+    def open(cls, interface: str = "any", **kw) -> "AfPacket":
+        lib = load_library()
+        cfg = cls._cfg(interface=interface, **kw)
+        p = ctypes.c_void_p()
+        rc = lib.pv_afpacket_open(ctypes.byref(cfg), ctypes.byref(p))
+        if rc != 0:
+            raise PvError(f"pv_afpacket_open failed ({rc}): {lib.pv_afpacket_last_error().decode()}")
+        return cls(p.value, cfg)
+
+    @classmethod
+    def attach(cls, ring_addr: int, block_size: int, num_blocks: int, wake_fd: int = -1, **kw) -> "AfPacket":
+        lib = load_library()
+        cfg = cls._cfg(**kw)
+        p = ctypes.c_void_p()
+        rc = lib.pv_afpacket_attach(ring_addr, block_size, num_blocks, wake_fd, ctypes.byref(cfg), ctypes.byref(p))
+        if rc != 0:
+            raise PvError(f"pv_afpacket_attach failed ({rc}): {lib.pv_afpacket_last_error().decode()}")
+        return cls(p.value, cfg)
+
+    def run(self, fn) -> int:
+        def sink(user, recs, nbytes, n):
+            try:
+                return int(fn(ctypes.string_at(recs, nbytes), n) or 0)
+            except Exception:  # noqa: BLE001 - a failing sink stops the capture
+                return -1
+        cb = AFPACKET_SINK(sink)
+        self._cb = cb
+        return self.lib.pv_afpacket_run(self.ptr, cb, None)
+
+    def start(self, handlers: "PvHandlers"):
+        rc = self.lib.pv_afpacket_start(self.ptr, handlers.ctx)
+        if rc != 0:
+            raise PvError(f"pv_afpacket_start failed ({rc})")
+
+    def stop(self) -> int:
+        return self.lib.pv_afpacket_stop(self.ptr)
+
+    def stats(self) -> dict:
+        c = pv_afpacket_counters()
+        self.lib.pv_afpacket_stats(self.ptr, ctypes.byref(c))
+        return {k: getattr(c, k) for k, _ in c._fields_}
+
+    def close(self):
+        if self.ptr:
+            self.lib.pv_afpacket_close(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 class PvHandlers:

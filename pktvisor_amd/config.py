@@ -182,13 +182,13 @@ DNS2_FILTER_KEYS = ("exclude_noerror", "only_rcode", "only_dnssec_response", "an
 def dns2_start(cfg: dict) -> dict:
     """DnsStreamHandler v2 start (src/handlers/dns/v2/DnsStreamHandler.cpp:43-236) up to the
     signal wiring: {"groups": bits | GROUPS_SET, "filters": pv_dns_filters fields (v2) or None,
-    "xact_ttl_ms": int|None}. The geo / ASN filters (no MaxMind database) and public_suffix_list are
-    not built for the GPU v2 handler; top_ecs keeps
+    "xact_ttl_ms": int|None}. The geo / ASN filters (no MaxMind database) are not built for the
+    GPU v2 handler; top_ecs keeps
     its geo / ASN tops empty (no MaxMind database)."""
     from pktvisor_amd import dns_filter_config
     validate_configs(cfg, DNS2_CONFIG_DEFS)
     groups = process_groups(cfg, DNS2_GROUP_DEFS, DNS2_DEFAULT_GROUPS)
-    for k in ("geoloc_notfound", "asn_notfound", "public_suffix_list"):
+    for k in ("geoloc_notfound", "asn_notfound"):
         if k in cfg:
             raise ConfigException(f"{k} is not supported by the GPU DNS v2 handler")
     # dnstap_msg_type (dns/v2/DnsStreamHandler.cpp:176-190): as v1's
@@ -200,9 +200,11 @@ def dns2_start(cfg: dict) -> dict:
         q, r = DNSTAP_TYPE_PAIRS[cfg["dnstap_msg_type"]]
         mask = (1 << q) | (1 << r)
     filters = None
-    if any(k in cfg for k in DNS2_FILTER_KEYS) or "only_xact_directions" in cfg:
+    psl = _bool(cfg, "public_suffix_list")  # _configs (dns/v2/DnsStreamHandler.cpp:192-194,612-619)
+    if any(k in cfg for k in DNS2_FILTER_KEYS) or "only_xact_directions" in cfg or psl:
         filters = dns_filter_config({k: cfg[k] for k in DNS2_FILTER_KEYS if k in cfg}, v2=True)
         filters["v2"] = 1
+        filters["public_suffix_list"] = 1 if psl else 0
         # only_xact_directions (:107-122): every direction filtered but the listed ones
         if "only_xact_directions" in cfg:
             dis = 7
@@ -234,8 +236,9 @@ def dns_start(cfg: dict) -> dict:
     if "dnstap_msg_type" in cfg and cfg["dnstap_msg_type"] not in DNSTAP_MSG_TYPES:
         raise ConfigException("DnsStreamHandler: dnstap_msg_type contained an invalid/unsupported type. Valid types: "
                               + ", ".join(DNSTAP_MSG_TYPES))
-    if _bool(cfg, "public_suffix_list"):
-        raise ConfigException("DnsStreamHandler: public_suffix_list is not supported by the GPU handler")
+    # public_suffix_list (_configs, dns/v1/DnsStreamHandler.cpp:187-189,648-657): a config the DNS
+    # pass applies (pv_dns_filters.public_suffix_list)
+    filters["public_suffix_list"] = 1 if _bool(cfg, "public_suffix_list") else 0
     ttl = None
     if "xact_ttl_ms" in cfg:
         ttl = _uint(cfg, "xact_ttl_ms")

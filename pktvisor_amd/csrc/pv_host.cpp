@@ -140,6 +140,7 @@ extern "C" __global__ void pv_net_kernel_ns(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_fast(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
 extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
@@ -2079,8 +2080,8 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
         // DnsStreamHandler v2 start (dns/v2/DnsStreamHandler.cpp:61-170): one rcode mask for
         // exclude_noerror (every rcode but NOERROR) or only_rcode, tested on responses only
         if (!c->dns2_groups) return c->fail(PV_EINVAL, "v2 DNS filters without the DNS v2 handler");
-        if (f->only_queries || f->only_responses || f->filter_all || f->public_suffix_list)
-            return c->fail(PV_EUNSUPPORTED, "only_queries / only_responses / geo filters / public_suffix_list are not DNS v2 filters here");
+        if (f->only_queries || f->only_responses || f->filter_all)
+            return c->fail(PV_EUNSUPPORTED, "only_queries / only_responses / geo filters are not DNS v2 filters here");
         fl |= PVDF_V2;
         uint32_t mask = 0;
         if (f->exclude_noerror) mask = 0xfffeu;
@@ -2170,10 +2171,11 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
         c->f_sxh[k] = pvname::name_ph(q, strlen(q));
     }
     c->f_nsx = f->n_qname_suffixes;
-    // public_suffix_list (DnsStreamHandler::_configs, dns/v1/DnsStreamHandler.cpp:648-657): a
-    // config, not a filter, and only while only_qname_suffix is off
+    // public_suffix_list (DnsStreamHandler::_configs, dns/v1/DnsStreamHandler.cpp:648-657,
+    // v2 :612-619): a config, not a filter, and only while only_qname_suffix is off. v2 applies
+    // the size of a response's own first query name to its transaction's top_qname2/3
+    // (new_dns_transaction :1067-1072)
     if (f->public_suffix_list && !f->n_qname_suffixes) {
-        if (c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "public_suffix_list with the DNS v2 handler is not built");
         hipError_t e = hipSuccess;
         if (!c->d_psl) {
             const std::vector<uint32_t> blob = pvname::psl_blob();
@@ -3190,6 +3192,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         X.orph_cap = c->orph_cap;
         X.trecs = c->d_marena;
         X.toffs = c->d_moffs;
+        X.tsfx = c->d_tsfx;
         X.edge_h = c->slow_defer && !c->dns2_groups ? c->edge_h : 0;
         if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
             !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
@@ -3511,9 +3514,11 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
     const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
                       !(force && !strcmp(force, "ns"));
-    // lean: the register-window pass (pv_net_kernel_reg) unless PV_NET_KERNEL=fast asks for the LDS ring
+    // lean: the LDS-DMA ring pass (pv_net_kernel_ring, one workgroup per CU); PV_NET_KERNEL=reg
+    // asks for the register-window pass, =fast for the earlier per-grid-workgroup LDS ring
     const bool ring = force && !strcmp(force, "fast");
-    // the register pass writes the compact IP log (4 B + a direction bit per record)
+    const bool regw = force && !strcmp(force, "reg");
+    // the ring and register passes write the compact IP log (4 B + a direction bit per record)
     P.ip_compact = lean && !ring ? 1u : 0u;
     P.ip_base = ((uint64_t)P.slot_of[0] << 60) | ((uint64_t)TM_IPV4 << 56) |
                 ((uint64_t)((c->net_groups & PV_NET_CARDINALITY) ? 1 : 0) << 33);
@@ -3522,9 +3527,13 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
-    c->net_kernel = general ? "pv_net_kernel" : (lean ? (ring ? "pv_net_kernel_fast" : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : "pv_net_kernel_reg")) : "pv_net_kernel_ns");
+    c->net_kernel = general ? "pv_net_kernel"
+                            : (lean ? (ring ? "pv_net_kernel_fast"
+                                            : (!regw ? "pv_net_kernel_ring" : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : "pv_net_kernel_reg")))
+                                    : "pv_net_kernel_ns");
     if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    else if (lean && !regw) hipLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     else if (lean && c->reg_waves == 8) hipLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, (const PvParams *)c->d_params);
     else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -3588,6 +3597,28 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (drained && !hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
     if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
     if (flags & PVF_ARENA_FULL) return c->fail(PV_ECAPACITY, "top-N name arena full");
+    if (getenv("PV_TSTAMPS")) {
+        // -DPV_TSTAMPS builds: mean cycles per workgroup of the top-N combine / merge phases
+        std::vector<uint64_t> tv(65536 + (2u << c->reg_log2) * 8);
+        if (hip_ok(hipMemcpy(tv.data(), c->d_stamps + (1u << 20), tv.size() * 8, hipMemcpyDeviceToHost))) {
+            double cs[8] = {0}, ms[8] = {0};
+            uint64_t nm = 0;
+            for (uint32_t w = 0; w < grid; w++)
+                for (int k = 0; k < 8; k++) cs[k] += (double)tv[w * 8 + k];
+            for (uint32_t w = 0; w < (2u << c->reg_log2); w++) {
+                const uint64_t *m = &tv[65536 + w * 8];
+                if (!m[0] && !m[1]) continue;
+                nm++;
+                for (int k = 0; k < 8; k++) ms[k] += (double)m[k];
+            }
+            fprintf(stderr, "pv_tstamps combine (%u wg): init=%.0f insert=%.0f count=%.0f scan=%.0f out=%.0f | merge (%lu wg): "
+                            "runs=%.0f load=%.0f insert=%.0f wb=%.0f names=%.0f\n",
+                    grid, cs[0] / grid, cs[1] / grid, cs[2] / grid, cs[3] / grid, cs[4] / grid, (unsigned long)nm,
+                    ms[0] / std::max<uint64_t>(nm, 1), ms[1] / std::max<uint64_t>(nm, 1), ms[2] / std::max<uint64_t>(nm, 1),
+                    ms[3] / std::max<uint64_t>(nm, 1), ms[4] / std::max<uint64_t>(nm, 1));
+            hipMemset(c->d_stamps + (1u << 20), 0, tv.size() * 8);
+        }
+    }
     if (getenv("PV_STAMPS")) {
         std::vector<uint64_t> stv((size_t)grid * 4 * 8);
         if (hip_ok(hipMemcpy(stv.data(), c->d_stamps, stv.size() * 8, hipMemcpyDeviceToHost))) {
@@ -3994,11 +4025,18 @@ int pv_set_dnstap_only_hosts(pv_ctx *c, const char *hosts)
 {
     if (!c) return PV_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    c->dt_v4.clear();
-    c->dt_v6.clear();
-    c->dt_only_hosts = hosts != nullptr;
-    if (!hosts) return 0;
-    // parse_host_specs (libs/visor_utils/utils.cpp:128-164), its error texts
+    if (!hosts) {
+        c->dt_v4.clear();
+        c->dt_v6.clear();
+        c->dt_only_hosts = false;
+        return 0;
+    }
+    // parse_host_specs (libs/visor_utils/utils.cpp:128-164), its error texts. The lists are
+    // parsed into locals and committed together with the flag only when every spec parses: a
+    // failing call leaves the previous filter as it was (the reference throws from the input
+    // proxy's constructor, so no half-applied filter ever exists)
+    decltype(c->dt_v4) v4;
+    decltype(c->dt_v6) v6;
     const std::string s = hosts;
     size_t pos = 0;
     while (pos < s.size()) {
@@ -4015,14 +4053,17 @@ int pv_set_dnstap_only_hosts(pv_ctx *c, const char *hosts)
             std::array<uint8_t, 16> a{};
             if (cidr < 0 || cidr > 128) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
             if (inet_pton(AF_INET6, ip.c_str(), a.data()) != 1) return c->fail(PV_EINVAL, "invalid IPv6 address: %s", ip.c_str());
-            c->dt_v6.push_back({a, (uint32_t)cidr});
+            v6.push_back({a, (uint32_t)cidr});
         } else {
             in_addr a{};
             if (cidr < 0 || cidr > 32) return c->fail(PV_EINVAL, "invalid CIDR: %s", host.c_str());
             if (inet_pton(AF_INET, ip.c_str(), &a) != 1) return c->fail(PV_EINVAL, "invalid IPv4 address: %s", ip.c_str());
-            c->dt_v4.push_back({a.s_addr, (uint32_t)cidr});
+            v4.push_back({a.s_addr, (uint32_t)cidr});
         }
     }
+    c->dt_v4 = std::move(v4);
+    c->dt_v6 = std::move(v6);
+    c->dt_only_hosts = true;
     return 0;
 }
 
@@ -4686,11 +4727,13 @@ int pv_index_records_mt(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uin
 
 int pv_set_start_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
 {
+    std::lock_guard<std::mutex> g(c->mu);
     return ensure_started(c, sec, nsec);
 }
 
 int pv_set_end_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
 {
+    std::lock_guard<std::mutex> g(c->mu);
     if (!c->started) return 0;
     // end_tstamp_signal: the live bucket of each manager becomes read-only
     c->net.meta[c->net.slots.front()].set_read_only(sec, nsec);
@@ -4786,9 +4829,11 @@ int dns_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
 int pv_window_json(pv_ctx *c, uint32_t period, int merged, char **out)
 {
     *out = nullptr;
+    // the transaction values are drained under the lock: a batch the producer runs between
+    // the drain and the read would otherwise show its counters without its values
+    std::lock_guard<std::mutex> g(c->mu);
     int rc = sync_xvals(c);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
     Json j;
@@ -4905,9 +4950,9 @@ extern "C" {
 int pv_bucket_merge(pv_ctx *c, uint32_t handler, pv_bucket **bucket, uint32_t period, int prometheus, int merged)
 {
     if (!bucket || (handler != PV_HANDLER_NET && handler != PV_HANDLER_DNS)) return c->fail(PV_EINVAL, "bucket merge: one handler");
+    std::lock_guard<std::mutex> g(c->mu); // values drained under the lock (pv_window_json)
     int rc = sync_xvals(c);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
     const int part = handler == PV_HANDLER_NET ? PART_NET : PART_DNS;
@@ -5031,9 +5076,9 @@ int pv_window_prometheus(pv_ctx *c, uint32_t period, uint32_t handlers, const ch
                          const char *const *label_values, uint32_t n_labels, char **out)
 {
     *out = nullptr;
+    std::lock_guard<std::mutex> g(c->mu); // values drained under the lock (pv_window_json)
     int rc = sync_xvals(c);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
     if (period >= c->cfg.num_periods && period != PV_PERIOD_AUTO)
@@ -5072,9 +5117,9 @@ int pv_window_opentelemetry(pv_ctx *c, uint32_t period, uint32_t handlers, const
 {
     *out = nullptr;
     *bytes = 0;
+    std::lock_guard<std::mutex> g(c->mu); // values drained under the lock (pv_window_json)
     int rc = sync_xvals(c);
     if (rc) return rc;
-    std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     if (!c->started) return c->fail(PV_EINVAL, "no data");
     if (period >= c->cfg.num_periods && period != PV_PERIOD_AUTO)
@@ -6011,14 +6056,18 @@ const char *pv_net_kernel_name(pv_ctx *c)
 // pv_dns_event_seconds_host counts them in pv_plan_dns_draws), so every rank draws what the
 // single pass draws for its events (AbstractMetricsManager::new_event, :318-323); the DNS
 // manager's flag is the last of those draws (a filtered event at the shard start counts it).
+// Cost: O(net_draws + dns_draws) generator steps on the calling thread (jsf32 has no jump-ahead),
+// about 1 ns each; a rank calls it once, before its first batch.
 int pv_sample_skip(pv_ctx *c, uint64_t net_draws, uint64_t dns_draws)
 {
+    if (!c) return PV_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     if (c->records_seen) return c->fail(PV_EINVAL, "pv_sample_skip after the first batch");
     if (c->sample_rate >= 100) return 0;
     Jsf32 rn, rd;
     for (uint64_t k = 0; k < net_draws; k++) rn.next();
-    for (uint64_t k = 0; k < dns_draws; k++) c->dns_deep_now = rd.next() % 100u < c->sample_rate;
+    for (uint64_t k = 1; k < dns_draws; k++) rd.next();
+    if (dns_draws) c->dns_deep_now = rd.next() % 100u < c->sample_rate; // the manager's last flag
     c->draws_net.reset(rn);
     c->draws_dns.reset(rd);
     return 0;

@@ -48,6 +48,24 @@
 #define STAMP(k)
 #define STAMP_FLUSH
 #endif
+// diagnostic build (-DPV_TSTAMPS): per-workgroup cycles of each top-N combine / merge phase
+// (thread 0, after the phase's barrier), at stamps[1 << 20 ...]
+#ifdef PV_TSTAMPS
+#define TST_DECL uint64_t tst_prev = __builtin_amdgcn_s_memtime(), tst_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define TST(k)                                                                               \
+    {                                                                                        \
+        const uint64_t now = __builtin_amdgcn_s_memtime();                                   \
+        tst_acc[k] += now - tst_prev;                                                        \
+        tst_prev = now;                                                                      \
+    }
+#define TST_FLUSH(base)                                                                      \
+    if (threadIdx.x == 0)                                                                    \
+        for (int k_ = 0; k_ < 8; k_++) P.stamps[(1u << 20) + (base) + (uint64_t)blockIdx.x * 8 + k_] = tst_acc[k_];
+#else
+#define TST_DECL
+#define TST(k)
+#define TST_FLUSH(base)
+#endif
 #ifndef PV_WIN
 #define PV_WIN 128 // bytes of each record staged into LDS (record header + frame start)
 #endif
@@ -248,7 +266,21 @@ struct NameSrc {
     const PV_G uint32_t *offs;
     uint64_t ecs_addr; // an ECS name given directly (ecs_fam 1 / 2): no record to decode
     uint32_t ecs_fam;
+    const PV_G uint8_t *sfx; // suffix sizes of these records (DNS v2 public_suffix_list)
 };
+// suffix_size of a record's top_qname2/3 aggregation (aggregateDomain): v1 only_qname_suffix or
+// public_suffix_list (sfx_of, 0xff: none); v2 public_suffix_list only (v2 hands a response its
+// own _configs size; only_qname_suffix is a query filter there), from the record's source
+__device__ __forceinline__ uint32_t name_sfx(PV_CREF(PvParams) P, uint32_t rep, const PV_G uint8_t *v2src)
+{
+    if (P.f_flags & PVDF_V2) {
+        if (!(P.f_flags & PVDF_PSL) || (P.f_flags & PVDF_ONLY_QSUFFIX) || !v2src) return 0;
+        return v2src[rep];
+    }
+    if (!(P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))) return 0;
+    const uint32_t r = P.sfx_of[rep];
+    return r == 0xffu ? 0u : r;
+}
 __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, uint32_t metric, uint32_t rep,
                                             const NameSrc *ns = nullptr, uint64_t key = 0)
 {
@@ -303,8 +335,8 @@ __device__ __noinline__ uint32_t write_name(PV_CREF(PvParams) P, uint32_t slot, 
     uint32_t n = nl > 0 ? st.n : 0;
     if (metric == TM_QNAME2 || metric == TM_QNAME3) {
         int q2, q3; uint64_t h2, h3;
-        const uint32_t sfx = ((P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) && !(P.f_flags & PVDF_V2)) ? P.sfx_of[rep] : 0u;
-        if (nl > 0) agg_domain_r(R, m, len, st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx); else { q2 = 0; q3 = -1; }
+        const uint32_t sfx = name_sfx(P, rep, ns ? ns->sfx : P.sfx_of);
+        if (nl > 0) agg_domain_r(R, m, len, st, q2, q3, h2, h3, sfx); else { q2 = 0; q3 = -1; }
         start = metric == TM_QNAME2 ? q2 : q3;
         if (start < 0) start = (int)n;
     }
@@ -2396,10 +2428,281 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
 }
 
+// ------------------------------------------------------------------ the lean Net pass, LDS-DMA ring
+// The lean pass with its records staged in LDS by LDS-DMA (global_load_lds_dwordx4), one
+// workgroup of four waves per CU. tools/ring_probe.hip measured the staging alone: the register
+// windows at one workgroup per CU 201-211 us on C2 (two tiles, 10 KiB, in flight per wave: ~40 KiB
+// per CU, too few to cover an HBM miss), this ring 138-143 us against 133-137 us for a plain
+// coalesced read of the blob: a wave keeps Q - 1 tiles in flight in LDS while it parses one,
+// which costs no VGPRs (profiles/r4_head/ring_probe.log).
+//   - each wave's tiles: w, w + 4, ... of its workgroup's contiguous run of grid ranges (one
+//     workgroup per CU walks ceil(grid / CUs) consecutive ranges, so the DNS pass, combine and merge
+//     keep the grid's partition; per-range DNS list and exception counters in LDS);
+//   - per tile, two offset rows by LDS-DMA (each lane's record start, the tile's end) issued 2Q
+//     tiles ahead, and NJ 1-KiB pieces: the tile's packed span from its 16-B aligned start when it
+//     fits (C2: 64 x 80 B), else each lane's own 80-B window (C3 / C4: headers only);
+//   - waits are counted vmcnt: the ops a step issues are fixed (rows + NJ pieces, a window-mode
+//     tile's unused pieces re-read one shared 16 B), so "tile k landed" is vmcnt((Q - 1) * OPS);
+//     the pass's own stores only make that wait a little longer (they are never counted);
+//   - the per-record work is net_fast_reg's (fast path from the words, general path out of line).
+#ifndef PV_RING_Q
+#define PV_RING_Q 4 // tile slots per wave (Q - 1 in flight while one is parsed)
+#endif
+#ifndef PV_RING_NJ
+#define PV_RING_NJ 6 // 1-KiB pieces per slot (a packed tile spans at most NJ KiB - 15 B)
+#endif
+#define PV_RING_R (2 * PV_RING_Q + 1)  // offset rows per wave
+#define PV_RING_OPS (PV_RING_NJ + 2)   // vector-memory ops one step issues (rows + pieces)
+#define PV_RING_MAXG 8                 // grid ranges one ring workgroup may own
+static_assert(PV_RING_NJ >= 5, "a window-mode tile needs five pieces");
+static_assert(PV_RING_NJ + PV_RING_Q * PV_RING_OPS + 2 <= 63 || PV_RING_Q * PV_RING_OPS < 63, "vmcnt range");
+struct RingWave {
+    uint32_t slot[PV_RING_Q][PV_RING_NJ * 256];
+    uint32_t lo[PV_RING_R][PV_WT]; // each lane's record start
+    uint32_t hi[PV_RING_R][PV_WT]; // the tile's end (the record after its last; all lanes alike)
+};
+struct NetRingState {
+    RingWave w[4];
+    uint32_t hist[PV_HBINS];
+    uint32_t nd[PV_RING_MAXG], nx[PV_RING_MAXG];
+    int64_t dthresh[PV_MAX_SHIFTS];
+};
+template <int N>
+__device__ __forceinline__ void ring_vmcnt()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ NetRingState S;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
+    if (threadIdx.x < PV_RING_MAXG) { S.nd[threadIdx.x] = 0; S.nx[threadIdx.x] = 0; }
+    if (threadIdx.x < PV_MAX_SHIFTS) S.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+    __syncthreads();
+    const PV_G uint8_t *const recs = P.recs;
+    const bool compact = P.ip_compact;
+    const PV_G uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint32_t rec_bytes = (uint32_t)P.rec_bytes;
+    const uint32_t slot = P.slot_of[0];
+    const uint32_t groups = P.net_groups;
+    const bool tops = groups & PV_NET_TOP_IPS_BIT, card = groups & PV_NET_CARDINALITY_BIT;
+    const uint32_t ts_nano = P.ts_nano;
+    const uint32_t wtpb = P.wt_per_block;
+    HostNets h;
+    {
+        const uint32_t n4 = P.nets.n4;
+        h.a0 = P.nets.v4_addr[0]; h.m0 = P.nets.v4_mask[0]; h.e0 = n4 > 0 ? ~0u : 0u;
+        h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
+    }
+    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
+    // this workgroup's ranges [lb0, lb1) and their tiles [T0, T1)
+    const uint32_t G = (P.grid_main + gridDim.x - 1) / gridDim.x;
+    const uint32_t lb0 = min(blockIdx.x * G, P.grid_main), lb1 = min(lb0 + G, P.grid_main);
+    const uint64_t T0 = (uint64_t)lb0 * wtpb, T1 = min<uint64_t>((uint64_t)lb1 * wtpb, nwt);
+    const uint32_t ntl = T1 > T0 + wave ? (uint32_t)((T1 - T0 - wave + 3) / 4) : 0u;
+    RingWave &W = S.w[wave];
+    auto tile_of = [&](int64_t k) -> uint64_t {
+        return T0 + wave + 4ull * (uint64_t)min<int64_t>(max<int64_t>(k, 0), (int64_t)ntl - 1);
+    };
+    auto rows = [&](int64_t k) {
+        const uint64_t t = tile_of(k), r = t * PV_WT + lane;
+        const uint32_t row = (uint32_t)(k % PV_RING_R);
+        dma4(offs + min<uint64_t>(r, last), lds_addr(&W.lo[row][0]));
+        dma4(offs + min<uint64_t>(t * PV_WT + PV_WT, last), lds_addr(&W.hi[row][0]));
+    };
+    // the span of tile k in HBM: [base, b1), packed when it fits a slot
+    auto span = [&](int64_t k, uint32_t &base, uint32_t &nch) {
+        const uint32_t row = (uint32_t)(k % PV_RING_R);
+        const uint64_t t = tile_of(k);
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(W.lo[row][0]);
+        const uint32_t b1 = t * PV_WT + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(W.hi[row][0]);
+        base = b0 & ~15u;
+        nch = (b1 - base + 15) >> 4;
+    };
+    auto pieces = [&](int64_t k) {
+        uint32_t base, nch;
+        span(k, base, nch);
+        const bool packed = nch <= (uint32_t)(PV_RING_NJ * 64);
+        const uint32_t o = W.lo[k % PV_RING_R][lane];
+        const uint32_t dst = lds_addr(&W.slot[k % PV_RING_Q][0]);
+#pragma unroll
+        for (int j = 0; j < PV_RING_NJ; j++) {
+            const uint32_t ch = (uint32_t)(j * 64) + lane;
+            const uint32_t src = packed ? base + min(ch, nch - 1) * 16 : (j < 5 ? (o & ~15u) + 16u * j : base);
+            dma16(recs + src, dst + j * 1024);
+        }
+    };
+    uint64_t cd = 0, cl = 0; // fast lanes' packed counters (net_fast)
+    NetCtr c;
+    c.zero();
+    if (ntl) {
+        // rows of tiles 0 .. Q, then Q - 1 steps without a tile (rows k + 2Q, pieces k + Q - 1,
+        // k = 1 - Q .. -1), so every step of the loop sees the same ops younger than its tile
+        for (int k = 0; k <= PV_RING_Q; k++) rows(k);
+        ring_vmcnt<0>();
+        for (int k = 1 - PV_RING_Q; k < 0; k++) {
+            rows(k + 2 * PV_RING_Q);
+            pieces(k + PV_RING_Q - 1);
+        }
+    }
+    for (uint32_t k = 0; k < ntl; k++) {
+        rows((int64_t)k + 2 * PV_RING_Q);
+        // the rows of tile k + Q - 1 (issued Q + 1 steps ago) landed
+        ring_vmcnt<(PV_RING_NJ + PV_RING_Q * PV_RING_OPS + 2 < 63 ? PV_RING_NJ + PV_RING_Q * PV_RING_OPS + 2 : 63)>();
+        pieces((int64_t)k + PV_RING_Q - 1);
+        ring_vmcnt<(PV_RING_Q - 1) * PV_RING_OPS>(); // tile k landed
+        const uint32_t row = k % PV_RING_R;
+        const uint64_t t = tile_of(k);
+        const uint32_t lb = (uint32_t)(t / wtpb), lr = lb - lb0; // the tile's grid range
+        const uint64_t wbeg = (uint64_t)lb * wtpb;
+        const uint64_t r0 = t * PV_WT, i = r0 + lane;
+        const bool active = i < n;
+        const uint32_t off = W.lo[row][lane];
+        uint32_t base, nch;
+        span(k, base, nch);
+        const bool packed = nch <= (uint32_t)(PV_RING_NJ * 64);
+        const uint32_t *Ls = W.slot[k % PV_RING_Q];
+        const uint32_t gb = packed ? base : (off & ~15u);
+        const uint32_t lim = packed ? nch * 16 - 4 : 76;
+        const uint32_t rel = off - gb;
+        RecW rw;
+        if (packed) recw_load_packed(Ls, rel, rw);
+        else recw_load_window(Ls, rel >> 2, rel & 3, lane * 4, rw);
+        const FastRec f = fast_fields(rw, h);
+        const bool fast = active & ((rel >> 2) + 17 <= (lim + 4) >> 2) & (f.ok != 0);
+        const uint64_t slowm = __ballot(active & !fast);
+        cd += fast ? 1ull << (f.dir * 16) : 0ull;
+        cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
+        uint32_t hv = fast ? f.caplen : PV_NOH;
+        const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
+        const bool ipok = fast & (f.dir != 2) & (ip != 0);
+        uint64_t ek = tops && ipok ? ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
+                                         ((uint64_t)f.dir << 32) | ip
+                                   : 0ull;
+        if (card && !tops) {
+            if (ipok) {
+                uint64_t h1, h2;
+                murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
+                __hip_atomic_fetch_min(P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)(f.dir == 0 ? CPC_SRC : CPC_DST) * PV_CPC_COUPONS +
+                                           cpc_coupon(h1, h2),
+                                       (int64_t)(P.gbase + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        const uint32_t port = (fast & (f.l4 == 17)) ? dns_port_bf(rw.at(50)) : 0u;
+        DnsMsgW dm{};
+        bool isdns = port != 0;
+        if (__ballot(isdns)) {
+            if (isdns) {
+                const Parsed o = fast_parsed(f, rw, ts_nano, off);
+                uint32_t dp = 0;
+                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)o.sec >= S.dthresh[q];
+                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
+                DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
+                d.fkey = fast_flowkey(rw);
+                dm = msg_words(d);
+            }
+        }
+        bool istcp = fast & (f.l4 == 6), hasseg = false;
+        PvTcpSeg seg;
+        const uint32_t temit = P.tcp_emit;
+        if (temit && __ballot(istcp)) {
+            if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
+        }
+        if (slowm) {
+            // general-path records (VLAN, IPv6, options, tunnels, other link types): the staged
+            // window where it reaches, else HBM
+            if (active && !fast) {
+                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
+                const SlowOut so = net_slow_p(Pp, R, off, i);
+                Parsed o;
+                o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
+                c.add(o);
+                hv = so.caplen;
+                ek = so.ek;
+                dm = so.dm;
+                isdns = so.isdns;
+                istcp = so.l4 == 6;
+            }
+        }
+        if (__ballot(hv != PV_NOH && hv > 65535)) {
+            if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
+        }
+        hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
+        const uint64_t m = __ballot(isdns);
+        if (m) {
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(&S.nd[lr], (uint32_t)__popcll(m));
+            q = __builtin_amdgcn_readlane(q, 0);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (isdns) {
+                PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(P.dq) + 2 * (wbeg * PV_WT + q + below);
+                dd[0] = dm.a;
+                dd[1] = dm.b;
+            }
+        }
+        if (tops) {
+            if (compact) {
+                const bool v4 = ek && ((ek >> 32) & ~1ull) == (P.ip_base >> 32);
+                const uint64_t xm = __ballot(active && ek && !v4);
+                if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
+                const uint64_t dbit = __ballot(v4 && ((ek >> 32) & 1));
+                if (lane == 0) P.ipdir[t] = dbit;
+                if (xm) {
+                    uint32_t q = 0;
+                    if (lane == 0) q = atomicAdd(&S.nx[lr], (uint32_t)__popcll(xm));
+                    q = __builtin_amdgcn_readlane(q, 0);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(xm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xm, 0u));
+                    if (active && ek && !v4) {
+                        P.iplog[wbeg * PV_WT + q + below] = ek;
+                        P.ipx_rep[wbeg * PV_WT + q + below] = (uint32_t)i;
+                    }
+                }
+            } else if (active) {
+                P.iplog[i] = ek;
+            }
+        }
+        if (temit) {
+            const uint64_t tm = __ballot(istcp);
+            if (tm) {
+                if (lane == 0) P.tmask[t] = tm;
+                tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, seg, lane);
+            }
+        }
+    }
+    ring_vmcnt<0>();
+    {
+        const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
+        const uint32_t nf = fin + fout + funk;
+        c.nev += nf; c.n4 += nf;
+        c.nin += fin; c.nout += fout; c.nunk += funk;
+        c.nudp += (uint32_t)(cl & 0xffff); c.ntcp += (uint32_t)((cl >> 16) & 0xffff);
+        c.noth += (uint32_t)((cl >> 32) & 0xffff); c.nsyn += (uint32_t)(cl >> 48);
+    }
+    NetK K;
+    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
+    if (ntl) knet_flush(K, slot, c);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
+        if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
+    // the ranges' DNS list counts (and the update-log counters the DNS pass starts from)
+    for (uint32_t lb = lb0 + threadIdx.x; lb < lb1; lb += blockDim.x) {
+        const uint32_t nd = S.nd[lb - lb0];
+        P.mq_cnt[lb] = 0;
+        P.dq_cnt[lb] = nd;
+        if (compact) P.ipx_cnt[lb] = S.nx[lb - lb0];
+        if (nd) atomicAdd(P.n_dns, nd);
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(const PvParams *__restrict__ Pp) { net_pass<true>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(const PvParams *__restrict__ Pp) { net_pass<false>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg<4>(Pp); }
+extern "C" __global__ void __launch_bounds__(256) pv_net_kernel_ring(const PvParams *__restrict__ Pp) { net_ring(Pp); }
 // eight waves in the one workgroup of a CU: two per SIMD to hide instruction latency, one record stream per CU
 extern "C" __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg8(const PvParams *__restrict__ Pp) { net_fast_reg<8>(Pp); }
 
@@ -2831,11 +3134,13 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
 {
     using St = CombState<CN, NR>;
     __shared__ St S;
+    TST_DECL
     const uint32_t nreg = 2u << P.reg_log2; // run keys
     for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x) { S.key[j] = 0; S.cnt[j] = 0; S.rep[j] = 0xffffffffu; }
     for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) { S.h[r] = 0; S.tb[r] = 0; }
     if (threadIdx.x == 0) S.nsp = 0;
     __syncthreads();
+    TST(0)
     const uint64_t wbase = (uint64_t)blockIdx.x * P.mq_cap;
     PV_G ulonglong2 *sp = reinterpret_cast<PV_G ulonglong2 *>(P.tp_buf) + wbase;
     PV_G ulonglong2 *out = reinterpret_cast<PV_G ulonglong2 *>(P.cb) + wbase;
@@ -2843,7 +3148,10 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     const PV_G uint64_t *q = P.mq + wbase * 2;
     batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; },
                [&](uint64_t, ulonglong2 e) { comb_add<CN>(P, S, sp, e.x, (uint32_t)e.y, (uint32_t)(e.y >> 32)); });
-    if (P.net_groups & PV_NET_TOP_IPS_BIT) {
+#ifndef PV_ABL_COMB_NOIP
+#define PV_ABL_COMB_NOIP 0 // tuning/ablation only: skip the dense IP log
+#endif
+    if ((P.net_groups & PV_NET_TOP_IPS_BIT) && !PV_ABL_COMB_NOIP) {
         uint64_t a, z;
         wg_records(P, blockIdx.x, a, z);
         const PV_G uint64_t *ipl = P.iplog + a;
@@ -2867,10 +3175,12 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
         }
     }
     __syncthreads();
+    TST(1)
     // the table's entries per region (the spilled ones were counted as they spilled)
     for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x)
         if (S.key[j]) comb_count(P, S, comb_entry(S.key[j], S.cnt[j], S.rep[j]).x);
     __syncthreads();
+    TST(2)
     // region run starts: each thread scans a contiguous share of the regions
     const uint32_t per = (nreg + blockDim.x - 1) / blockDim.x;
     const uint32_t r0 = min(threadIdx.x * per, nreg), r1 = min(r0 + per, nreg);
@@ -2897,6 +3207,11 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
         run += c;
     }
     __syncthreads();
+    TST(3)
+#ifndef PV_ABL_COMB_NOOUT
+#define PV_ABL_COMB_NOOUT 0 // tuning/ablation only: skip writing the combined list
+#endif
+    if (!PV_ABL_COMB_NOOUT)
     for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x)
         if (S.key[j]) {
             const ulonglong2 e = comb_entry(S.key[j], S.cnt[j], S.rep[j]);
@@ -2907,6 +3222,11 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     batched<8>(nsp, [&](uint64_t j) { return sp[j]; },
                [&](uint64_t, ulonglong2 e) { out[atomicAdd(&S.h[run_key(P, e.x)], 1u)] = e; });
     if (threadIdx.x == 0) P.cb_cnt[blockIdx.x] = total;
+#ifdef PV_TSTAMPS
+    __syncthreads();
+#endif
+    TST(4)
+    TST_FLUSH(0)
 }
 // LDS: an 8192-entry table with up to 2^10 regions per table (152 KiB), 2048 entries with
 // more (128 KiB); two run keys per region
@@ -2948,6 +3268,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
     const uint32_t hd = rk >> P.reg_log2;            // 0 Net tables, 1 DNS tables
     if (!((*P.tp_hands >> hd) & 1)) return; // no entry of this handler in the batch
     __shared__ MergeRuns U;
+    TST_DECL
     const uint32_t ng8 = (P.grid_main + 7) / 8, ng = 8 * ng8;
     uint32_t n;
     {
@@ -2971,6 +3292,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         __syncthreads();
         n = total;
     }
+    TST(0)
     if (n == 0) return;
     // entry j of the region: its run by binary search over the run prefixes
     uint32_t top = 1;
@@ -3021,6 +3343,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                    });
         if (threadIdx.x == 0) { S.nnew = 0; S.ncr = 0; }
         __syncthreads();
+        TST(1)
         batched<PV_MG_U>(n, ld, [&](uint64_t, ulonglong2 e) {
             const uint64_t e0 = e.x;
             if (!one && entry_table(e0) != tb) return;
@@ -3067,20 +3390,25 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
             }
         });
         __syncthreads();
+        TST(2)
+#ifndef PV_ABL_MERGE
+#define PV_ABL_MERGE 0 // tuning/ablation only: 1 no CPC updates, 2 no write-back, 3 neither
+#endif
         for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
-            if (S.dirty[i]) {
+            if ((PV_ABL_MERGE & 2) == 0 && S.dirty[i]) {
                 P.tkeys[rbase + i] = S.key[i];
                 P.tcnt[rbase + i] = S.cnt[i];
             }
             // IPv4 cardinality: one first-occurrence update per address and direction
             for (uint32_t d = 0; d < 2; d++)
-                if (S.mn[d][i] != 0xffffffffu)
+                if ((PV_ABL_MERGE & 1) == 0 && S.mn[d][i] != 0xffffffffu)
                     cpc_min(P, s, d ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)S.key[i]), (int64_t)(P.gbase + S.mn[d][i]));
         }
         const uint32_t nnew = S.nnew;
         if (threadIdx.x == 0 && nnew) S.nbase = atomicAdd(P.nn_cnt, nnew);
         if (threadIdx.x == 0 && S.ncr) atomicAdd(&P.tab_live[tb], S.ncr);
         __syncthreads();
+        TST(3)
         for (uint32_t k = threadIdx.x; k < nnew; k += blockDim.x) {
             const uint32_t g = S.nbase + k;
             const uint64_t pos = rbase + S.nidx[k];
@@ -3088,7 +3416,9 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
             else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k], nullptr, S.key[S.nidx[k]]);
         }
         __syncthreads();
+        TST(4)
     }
+    TST_FLUSH(65536)
 }
 
 // The updates full regions could not take in this batch, once the host has purged their tables:
@@ -3280,8 +3610,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 if (metric == TM_QNAME2 || metric == TM_QNAME3) {
                     int q2, q3;
                     uint64_t h2, h3;
-                    const uint32_t sfx = ((P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) && !(P.f_flags & PVDF_V2)) ? P.sfx_of[e.rep] : 0u;
-                    if (nl > 0) agg_domain_r(R, m, mlen, st, q2, q3, h2, h3, sfx == 0xffu ? 0u : sfx);
+                    const uint32_t sfx = name_sfx(P, e.rep, P.sfx_of);
+                    if (nl > 0) agg_domain_r(R, m, mlen, st, q2, q3, h2, h3, sfx);
                     else { q2 = 0; q3 = -1; }
                     const int st0 = metric == TM_QNAME2 ? q2 : q3;
                     start = st0 < 0 ? nch : (uint32_t)st0;
@@ -3841,7 +4171,7 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
     st.mm.finish(h1, h2);
     if (st.n > 0 && (g & PV_D2G_CARDINALITY)) cpc_min(P, slot, CPC_QNAME2 + xd, cpc_coupon(h1, h2), order);
     sum_add(P, slot, PV_OFF_QTYPE2 + xd * PV_QTYPE_BINS + (d.qtype & 0xffff), 1);
-    const NameSrc ns_{X.trecs, X.toffs};
+    const NameSrc ns_{X.trecs, X.toffs, 0, 0, X.tsfx};
     const NameSrc *nsp = tcp ? &ns_ : nullptr;
     const uint64_t fp = fp56(st.ph, st.n, 0);
     auto add = [&](uint32_t metric, uint64_t f, uint32_t w) { global_add(P, slot, PV_V2_DKEY(metric, xd, f), w, idx, nsp); };
@@ -3860,7 +4190,10 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
     if (g & PV_D2G_TOP_QNAMES) {
         int q2, q3;
         uint64_t h2p, h3p;
-        agg_domain(st, q2, q3, h2p, h3p, 0);
+        // public_suffix_list: the response's own suffix size (_configs, v2 :612-619)
+        const uint32_t sfx = name_sfx(P, idx, tcp ? X.tsfx : P.sfx_of);
+        if (sfx) agg_domain_r(R, m, len, st, q2, q3, h2p, h3p, sfx);
+        else agg_domain(st, q2, q3, h2p, h3p, 0);
         const uint64_t k2 = q2 == 0 ? st.ph : suffix_hash(st, q2, h2p);
         add(TM_QNAME2, fp56(k2, st.n - q2, 0), 1);
         if (q3 >= 0 && (uint32_t)q3 < st.n) {

@@ -492,9 +492,11 @@ struct PvXactParams {
     PV_G PvXEvent *orph;
     PV_G uint32_t *n_orph;
     uint32_t orph_cap;
-    // TCP message records (events whose idx carries PV_TCP_IDX)
+    // TCP message records (events whose idx carries PV_TCP_IDX) and their suffix sizes
+    // (public_suffix_list, DNS v2)
     const PV_G uint8_t *trecs;
     const PV_G uint32_t *toffs;
+    const PV_G uint8_t *tsfx;
     // DNS v2: per period and direction the p90 slow threshold (< 0 = not known yet)
     float thr2[PV_MAX_SHIFTS + 1][3];
     // sharded runs (pv_set_slow_defer): queries with no earlier event of their key whose second

@@ -29,7 +29,10 @@
 // purge (wall clock in PcapPlusPlus) are not modelled; a timed-out flow is closed lazily at its
 // next packet (data it flushes is ordered there); the LRU holds the DNS-port connections only;
 // the puts of data an eviction flushes are not replayed; no flush of open connections at the
-// end of a capture.
+// end of a capture; the time-out test takes the latest TCP second seen before a packet, where
+// the reference tests the LRU tail against each TCP packet's own second after it
+// (PcapInputStream.cpp:449-459): the two agree while capture timestamps are monotonic and may
+// close a connection one packet earlier or later when they are not.
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>

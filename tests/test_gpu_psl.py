@@ -82,3 +82,40 @@ def test_psl_reference_kat():
     w = j["wire_packets"]
     assert (w["udp"], w["noerror"], w["srvfail"], w["refused"], w["nxdomain"], w["filtered"]) == (24, 10, 0, 1, 1, 0)
     assert j["top_qname2"][0]["name"] == ".mwbsys.com" and j["top_qname3"][0]["name"] == "sirius.mwbsys.com"
+
+
+# ---- DNS v2 (dns/v2/DnsStreamHandler.cpp:192-194 config, _configs :612-619, new_dns_transaction
+# :1067-1072): the response's own suffix size aggregates its transaction's top_qname2/3
+V2_ALL = ["cardinality", "counters", "quantiles", "top_ecs", "top_qtypes", "top_rcodes", "top_size", "top_qnames",
+          "top_ports", "xact_times"]
+
+
+def _both_v2(oracle, tmp_path, pcap, cfg, okw, periods=1, host="192.168.0.0/24"):
+    p = tmp_path / "psl2.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec=host, periods=periods, dns2_config={"enable": V2_ALL, **cfg})
+    ref = oracle.run_bytes(pcap, host_spec=host, num_periods=periods, window=periods, dns2_groups=0x3ff, **okw)
+    return gpu, ref
+
+
+@pytest.mark.parametrize("periods", [1, 5])
+def test_psl_v2_synthetic_parity(oracle, tmp_path, periods):
+    gpu, ref = _both_v2(oracle, tmp_path, psl_pcap(), {"public_suffix_list": True}, {"public_suffix_list": 1}, periods)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+    key = "1m" if periods == 1 else f"{periods}m"
+    names = {e["name"] for e in ref[key]["dns"]["out"]["top_qname2_xacts"]}
+    assert ".example.co.uk" in names and ".k12.ak.us" in names  # listed suffixes took effect
+
+
+@pytest.mark.parametrize("fixture", ["dns_udp_tcp_random.pcap", "dns_ipv6_tcp.pcap", "dns_udp_mixed_rcode.pcap"])
+def test_psl_v2_fixture_parity(oracle, tmp_path, fixture):
+    """UDP and DNS-over-TCP transactions (a TCP response's suffix size comes from the TCP pass)"""
+    pcap = open(os.path.join(GOLD, fixture), "rb").read()
+    gpu, ref = _both_v2(oracle, tmp_path, pcap, {"public_suffix_list": True}, {"public_suffix_list": 1})
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_psl_v2_ignored_with_only_qname_suffix(oracle, tmp_path):
+    cfg = {"public_suffix_list": True, "only_qname_suffix": ["co.uk", ".ak.us"]}
+    gpu, ref = _both_v2(oracle, tmp_path, psl_pcap(8), cfg, {"public_suffix_list": 1, "only_qname_suffix": "co.uk,.ak.us"})
+    assert diff(gpu, ref) is None, diff(gpu, ref)
