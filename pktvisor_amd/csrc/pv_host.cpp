@@ -141,6 +141,7 @@ extern "C" __global__ void pv_net_kernel_fast(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_reg_tc(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
 extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
@@ -2070,6 +2071,21 @@ int pv_set_tcp_reassembly_limit(pv_ctx *c, uint64_t limit)
     return 0;
 }
 
+// the public_suffix_list table on the device and the per-record suffix sizes (v1 and v2)
+static int psl_setup(pv_ctx *c)
+{
+    hipError_t e = hipSuccess;
+    if (!c->d_psl) {
+        const std::vector<uint32_t> blob = pvname::psl_blob();
+        if (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_psl, blob.size() * 4)) ||
+            !hip_ok(e = hipMemcpy(c->d_psl, blob.data(), blob.size() * 4, hipMemcpyHostToDevice)))
+            return c->hipfail(e, "public_suffix_list table");
+    }
+    if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
+        return c->hipfail(e, "public_suffix_list record buffer");
+    return 0;
+}
+
 int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
 {
     if (!c) return PV_EINVAL;
@@ -2126,6 +2142,12 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
             if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
                 return c->hipfail(e, "only_qname_suffix record buffer");
         }
+        // public_suffix_list (_configs, dns/v2/DnsStreamHandler.cpp:192-194,612-619): only while
+        // only_qname_suffix is off; a response's own size aggregates its transaction's names
+        if (f->public_suffix_list && !f->n_qname_suffixes) {
+            if (int rc = psl_setup(c)) return rc;
+            fl |= PVDF_PSL;
+        }
         c->f_flags = fl;
         c->f_rcode_mask = mask;
         c->f_ancount = f->answer_count >= 0 ? (uint32_t)f->answer_count : 0;
@@ -2176,15 +2198,7 @@ int pv_set_dns_filters(pv_ctx *c, const pv_dns_filters *f)
     // the size of a response's own first query name to its transaction's top_qname2/3
     // (new_dns_transaction :1067-1072)
     if (f->public_suffix_list && !f->n_qname_suffixes) {
-        hipError_t e = hipSuccess;
-        if (!c->d_psl) {
-            const std::vector<uint32_t> blob = pvname::psl_blob();
-            if (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_psl, blob.size() * 4)) ||
-                !hip_ok(e = hipMemcpy(c->d_psl, blob.data(), blob.size() * 4, hipMemcpyHostToDevice)))
-                return c->hipfail(e, "public_suffix_list table");
-        }
-        if (!c->d_sfx && (!hip_ok(e = hipSetDevice(c->device)) || !hip_ok(e = hipMalloc(&c->d_sfx, c->max_records + 64))))
-            return c->hipfail(e, "public_suffix_list record buffer");
+        if (int rc = psl_setup(c)) return rc;
         fl |= PVDF_PSL;
     }
     if (f->n_qname_suffixes) {
@@ -3514,10 +3528,11 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
     const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
                       !(force && !strcmp(force, "ns"));
-    // lean: the LDS-DMA ring pass (pv_net_kernel_ring, one workgroup per CU); PV_NET_KERNEL=reg
-    // asks for the register-window pass, =fast for the earlier per-grid-workgroup LDS ring
+    // lean: the register-window pass (pv_net_kernel_reg, its top-IPs specialisation _tc);
+    // PV_NET_KERNEL=ring asks for the LDS-DMA ring pass with producer waves, =fast for the
+    // earlier per-grid-workgroup LDS ring
     const bool ring = force && !strcmp(force, "fast");
-    const bool regw = force && !strcmp(force, "reg");
+    const bool regw = !(force && !strcmp(force, "ring"));
     // the ring and register passes write the compact IP log (4 B + a direction bit per record)
     P.ip_compact = lean && !ring ? 1u : 0u;
     P.ip_base = ((uint64_t)P.slot_of[0] << 60) | ((uint64_t)TM_IPV4 << 56) |
@@ -3527,14 +3542,27 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
+    const bool tc = (c->net_groups & PV_NET_TOP_IPS) && c->reg_waves != 8;
     c->net_kernel = general ? "pv_net_kernel"
                             : (lean ? (ring ? "pv_net_kernel_fast"
-                                            : (!regw ? "pv_net_kernel_ring" : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : "pv_net_kernel_reg")))
+                                            : (!regw ? "pv_net_kernel_ring"
+                                                     : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : (tc ? "pv_net_kernel_reg_tc" : "pv_net_kernel_reg"))))
                                     : "pv_net_kernel_ns");
     if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-    else if (lean && !regw) hipLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(256), 0, st, (const PvParams *)c->d_params);
+    else if (lean && !regw) {
+        // its block size is the kernel's own launch bound (parsing + producer waves; tuning
+        // builds change the layout)
+        static int ring_threads = 0;
+        if (!ring_threads) {
+            hipFuncAttributes fa{};
+            ring_threads = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(pv_net_kernel_ring)) == hipSuccess
+                               ? fa.maxThreadsPerBlock : 512;
+        }
+        hipLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(ring_threads), 0, st, (const PvParams *)c->d_params);
+    }
     else if (lean && c->reg_waves == 8) hipLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, (const PvParams *)c->d_params);
+    else if (lean && tc) hipLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     e = hipGetLastError();
@@ -3610,6 +3638,19 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
                 if (!m[0] && !m[1]) continue;
                 nm++;
                 for (int k = 0; k < 8; k++) ms[k] += (double)m[k];
+            }
+            {
+                // the ring Net pass's parsing waves (reg_grid x 4)
+                std::vector<uint64_t> rv((size_t)reg_grid * (getenv("PV_RING_NP") ? atoi(getenv("PV_RING_NP")) : 4) * 8);
+                if (hip_ok(hipMemcpy(rv.data(), c->d_stamps + (1u << 20) + 131072, rv.size() * 8, hipMemcpyDeviceToHost))) {
+                    double a[8] = {0};
+                    for (size_t w = 0; w < rv.size() / 8; w++)
+                        for (int k = 0; k < 8; k++) a[k] += (double)rv[w * 8 + k];
+                    const double nw = (double)(rv.size() / 8);
+                    fprintf(stderr, "pv_tstamps ring parser (%u waves): wait_full=%.0f load_fields=%.0f dns_tcp_slow=%.0f hist=%.0f "
+                                    "stores=%.0f loop=%.0f\n",
+                            (unsigned)(rv.size() / 8), a[0] / nw, a[1] / nw, a[2] / nw, a[3] / nw, a[4] / nw, a[7] / nw);
+                }
             }
             fprintf(stderr, "pv_tstamps combine (%u wg): init=%.0f insert=%.0f count=%.0f scan=%.0f out=%.0f | merge (%lu wg): "
                             "runs=%.0f load=%.0f insert=%.0f wb=%.0f names=%.0f\n",

@@ -66,6 +66,14 @@
 #define TST(k)
 #define TST_FLUSH(base)
 #endif
+// the ring Net pass's parsing waves (-DPV_TSTAMPS): cycles per phase, at stamps[(1 << 20) + 131072 ...]
+#ifdef PV_TSTAMPS
+#define RST_FLUSH                                                                            \
+    if ((threadIdx.x & 63) == 0)                                                             \
+        for (int k_ = 0; k_ < 8; k_++) P.stamps[(1u << 20) + 131072 + ((uint64_t)blockIdx.x * PV_RING_NP + cw) * 8 + k_] = tst_acc[k_];
+#else
+#define RST_FLUSH
+#endif
 #ifndef PV_WIN
 #define PV_WIN 128 // bytes of each record staged into LDS (record header + frame start)
 #endif
@@ -1251,6 +1259,18 @@ __device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds)
                  : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
 #define PV_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
+// A workgroup barrier for LDS data only: the wave's LDS ops complete (lgkmcnt 0), then s_barrier.
+// __syncthreads() also waits for every global store the wave has in flight (its release fence is a
+// vmcnt(0)), and a store takes microseconds to complete under load; after a phase of global stores
+// whose results no other wave of the workgroup reads, this barrier is the one to use.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0); vmcnt / expcnt untouched
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // s_waitcnt vmcnt(0) as the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15), which
 // the compiler's wait insertion sees, unlike inline asm
 #define PV_WAIT_VMCNT0 0x0F70
@@ -2184,8 +2204,13 @@ __device__ __forceinline__ void win_words(const uint4 (&W)[5], uint32_t sh, RecW
 #pragma unroll
     for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
 }
-// NW: waves of the workgroup (one workgroup per CU); wave w takes tiles w, w + NW, ... of each range
-template <uint32_t NW>
+// NW: waves of the workgroup (one workgroup per CU); wave w takes tiles w, w + NW, ... of each range.
+// TC: top IPs on with the compact IP log (the default groups). Its two stores per tile are then
+// unconditional instructions, so the compiler's counted vmcnt for the next tile's windows counts
+// them as younger ops instead of waiting for them: a store takes microseconds to complete under
+// the read stream, and a wait that covers the previous tile's stores (as the branchy form's
+// does) stalls every tile on them (tools/ring_probe.hip: 138 -> 177 us on C2 with a 4-B store).
+template <uint32_t NW, bool TC = false>
 __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
@@ -2316,15 +2341,22 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                 dd[1] = dm.b;
             }
         }
-        if (tops) {
-            if (compact) {
+        if (TC || tops) {
+            if (TC || compact) {
                 // the IPv4 entry as its address and a direction bit; anything else (an IPv6
                 // key of a general-path record) into the range's exception list
                 const bool v4 = ek && ((ek >> 32) & ~1ull) == (P.ip_base >> 32);
                 const uint64_t xm = __ballot(active && ek && !v4);
-                if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
                 const uint64_t dbit = __ballot(v4 && ((ek >> 32) & 1));
-                if (lane == 0) P.ipdir[t] = dbit;
+                if (TC) {
+                    // every lane (the log has 64 words of slack past the batch) and every lane
+                    // the same direction word: two unconditional store instructions
+                    P.iplog32[i] = active && v4 ? (uint32_t)ek : 0u;
+                    P.ipdir[t] = dbit;
+                } else {
+                    if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
+                    if (lane == 0) P.ipdir[t] = dbit;
+                }
                 if (xm) {
                     uint32_t q = 0;
                     if (lane == 0) q = atomicAdd(&S.nx, (uint32_t)__popcll(xm));
@@ -2400,8 +2432,10 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         oB = oN2;
     }
 #endif
-    // this range's DNS list: its count, and the slot counter reset for the next range
-    __syncthreads();
+    // this range's DNS list: its count, and the slot counter reset for the next range (LDS-only
+    // barriers: the range's IP-log and DNS-list stores are other kernels' to read, and waiting
+    // for them here would stall every wave on their completion)
+    lds_barrier();
     if (threadIdx.x == 0) {
         P.mq_cnt[lb] = 0;
         P.dq_cnt[lb] = S.nd;
@@ -2410,7 +2444,7 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         S.nd = 0;
         S.nx = 0;
     }
-    __syncthreads();
+    lds_barrier();
     }
     {
         const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
@@ -2423,55 +2457,98 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     NetK K;
     K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
     if (any) knet_flush(K, slot, c);
-    __syncthreads();
+    lds_barrier();
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
         if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
 }
 
 // ------------------------------------------------------------------ the lean Net pass, LDS-DMA ring
 // The lean pass with its records staged in LDS by LDS-DMA (global_load_lds_dwordx4), one
-// workgroup of four waves per CU. tools/ring_probe.hip measured the staging alone: the register
-// windows at one workgroup per CU 201-211 us on C2 (two tiles, 10 KiB, in flight per wave: ~40 KiB
-// per CU, too few to cover an HBM miss), this ring 138-143 us against 133-137 us for a plain
-// coalesced read of the blob: a wave keeps Q - 1 tiles in flight in LDS while it parses one,
-// which costs no VGPRs (profiles/r4_head/ring_probe.log).
-//   - each wave's tiles: w, w + 4, ... of its workgroup's contiguous run of grid ranges (one
-//     workgroup per CU walks ceil(grid / CUs) consecutive ranges, so the DNS pass, combine and merge
-//     keep the grid's partition; per-range DNS list and exception counters in LDS);
-//   - per tile, two offset rows by LDS-DMA (each lane's record start, the tile's end) issued 2Q
-//     tiles ahead, and NJ 1-KiB pieces: the tile's packed span from its 16-B aligned start when it
-//     fits (C2: 64 x 80 B), else each lane's own 80-B window (C3 / C4: headers only);
-//   - waits are counted vmcnt: the ops a step issues are fixed (rows + NJ pieces, a window-mode
-//     tile's unused pieces re-read one shared 16 B), so "tile k landed" is vmcnt((Q - 1) * OPS);
-//     the pass's own stores only make that wait a little longer (they are never counted);
+// workgroup per CU of four parsing waves and four producer waves. tools/ring_probe.hip measured
+// the staging alone: the register windows at one workgroup per CU 201-211 us on C2 (two tiles, 10
+// KiB, in flight per wave: ~40 KiB per CU, too few to cover an HBM miss), an LDS ring 138-143 us
+// against 133-137 us for a plain coalesced read of the blob (profiles/r4_head/ring_probe.log). A
+// wave's vmcnt counts its loads and stores together, in issue order, and a store's completion
+// takes microseconds under the read stream: a parsing wave that waited on its own ring would wait
+// on its IP-log and DNS-list stores too (the first ring build did, at 370 us on C2). So the ring of
+// parsing wave w is filled by producer wave 4 + w, which issues nothing else:
+//   - the producer issues, per tile, two offset rows (each lane's record start, the tile's end)
+//     Q + 1 tiles ahead and NJ 1-KiB pieces: the tile's packed span from its 16-B aligned start
+//     when it fits a slot (C2: 64 x 80 B), else each lane's own 80-B window (C3 / C4: headers
+//     only; the unused pieces re-read one shared 16 B, so every issue is OPS ops);
+//   - it publishes a tile (LDS word FULL) once a counted vmcnt shows it landed, and reuses a slot
+//     once the parsing wave has released it (LDS word FREE); issuing comes first, so up to Q
+//     tiles are in flight while the parser works;
+//   - each parsing wave's tiles: w, w + 4, ... of its workgroup's contiguous run of grid ranges
+//     (one workgroup per CU walks ceil(grid / CUs) consecutive ranges, so the DNS pass, combine
+//     and merge keep the grid's partition; per-range DNS list and exception counters in LDS);
 //   - the per-record work is net_fast_reg's (fast path from the words, general path out of line).
+#ifndef PV_RING_NP
+#define PV_RING_NP 4 // parsing waves per workgroup
+#endif
+#ifndef PV_RING_SP
+#define PV_RING_SP 1 // parsing waves one producer wave fills
+#endif
 #ifndef PV_RING_Q
-#define PV_RING_Q 4 // tile slots per wave (Q - 1 in flight while one is parsed)
+#define PV_RING_Q 4 // tile slots per parsing wave
 #endif
 #ifndef PV_RING_NJ
 #define PV_RING_NJ 6 // 1-KiB pieces per slot (a packed tile spans at most NJ KiB - 15 B)
 #endif
-#define PV_RING_R (2 * PV_RING_Q + 1)  // offset rows per wave
-#define PV_RING_OPS (PV_RING_NJ + 2)   // vector-memory ops one step issues (rows + pieces)
+#define PV_RING_NW (PV_RING_NP + PV_RING_NP / PV_RING_SP) // waves per workgroup
+#define PV_RING_D (PV_RING_Q + 1)      // rows issued this many tiles ahead of their pieces
+#define PV_RING_R (2 * PV_RING_Q + 1)  // offset rows per parsing wave
+#define PV_RING_OPS (PV_RING_NJ + 2)   // vector-memory ops one issue makes (rows + pieces)
 #define PV_RING_MAXG 8                 // grid ranges one ring workgroup may own
+#define PV_RING_INF (PV_RING_SP * PV_RING_Q) // issues one producer may have in flight
+#define PV_RING_WAITA (PV_RING_NJ + (PV_RING_SP * PV_RING_D - 1) * PV_RING_OPS + 2)
 static_assert(PV_RING_NJ >= 5, "a window-mode tile needs five pieces");
-static_assert(PV_RING_NJ + PV_RING_Q * PV_RING_OPS + 2 <= 63 || PV_RING_Q * PV_RING_OPS < 63, "vmcnt range");
+static_assert(PV_RING_NP % PV_RING_SP == 0 && PV_RING_INF <= 8, "producer layout");
+static_assert(PV_RING_WAITA < 64 && (PV_RING_INF - 1) * PV_RING_OPS < 64, "vmcnt range");
+static_assert(PV_RING_D <= PV_RING_R - PV_RING_Q, "a row is rewritten only after its tile is released");
 struct RingWave {
     uint32_t slot[PV_RING_Q][PV_RING_NJ * 256];
     uint32_t lo[PV_RING_R][PV_WT]; // each lane's record start
     uint32_t hi[PV_RING_R][PV_WT]; // the tile's end (the record after its last; all lanes alike)
 };
 struct NetRingState {
-    RingWave w[4];
+    RingWave w[PV_RING_NP];
     uint32_t hist[PV_HBINS];
     uint32_t nd[PV_RING_MAXG], nx[PV_RING_MAXG];
+    uint32_t full[PV_RING_NP], fre[PV_RING_NP]; // per parsing wave: tiles published / released
     int64_t dthresh[PV_MAX_SHIFTS];
 };
+static_assert(sizeof(NetRingState) <= 160 * 1024, "ring Net pass LDS");
 template <int N>
 __device__ __forceinline__ void ring_vmcnt()
 {
     static_assert(N >= 0 && N < 64, "vmcnt range");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p)
+{
+    const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v)
+{
+    asm volatile("" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait until at most n - 1 issues (of PV_RING_OPS ops each) are younger than the oldest in flight
+__device__ __forceinline__ void ring_wait_oldest(uint32_t n)
+{
+    switch (n) {
+    case 1: ring_vmcnt<0>(); break;
+    case 2: ring_vmcnt<PV_RING_OPS>(); break;
+    case 3: ring_vmcnt<(PV_RING_INF >= 3 ? 2 * PV_RING_OPS : 0)>(); break;
+    case 4: ring_vmcnt<(PV_RING_INF >= 4 ? 3 * PV_RING_OPS : 0)>(); break;
+    case 5: ring_vmcnt<(PV_RING_INF >= 5 ? 4 * PV_RING_OPS : 0)>(); break;
+    case 6: ring_vmcnt<(PV_RING_INF >= 6 ? 5 * PV_RING_OPS : 0)>(); break;
+    case 7: ring_vmcnt<(PV_RING_INF >= 7 ? 6 * PV_RING_OPS : 0)>(); break;
+    default: ring_vmcnt<(PV_RING_INF >= 8 ? 7 * PV_RING_OPS : 0)>(); break;
+    }
 }
 __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
 {
@@ -2480,6 +2557,7 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x < PV_RING_MAXG) { S.nd[threadIdx.x] = 0; S.nx[threadIdx.x] = 0; }
+    if (threadIdx.x < PV_RING_NP) { S.full[threadIdx.x] = 0; S.fre[threadIdx.x] = 0; }
     if (threadIdx.x < PV_MAX_SHIFTS) S.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
     __syncthreads();
     const PV_G uint8_t *const recs = P.recs;
@@ -2492,78 +2570,113 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
     const bool tops = groups & PV_NET_TOP_IPS_BIT, card = groups & PV_NET_CARDINALITY_BIT;
     const uint32_t ts_nano = P.ts_nano;
     const uint32_t wtpb = P.wt_per_block;
+    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
+    // this workgroup's ranges [lb0, lb1) and their tiles [T0, T1); parsing wave q takes tiles
+    // T0 + q, T0 + q + NP, ...
+    const uint32_t G = (P.grid_main + gridDim.x - 1) / gridDim.x;
+    const uint32_t lb0 = min(blockIdx.x * G, P.grid_main), lb1 = min(lb0 + G, P.grid_main);
+    const uint64_t T0 = (uint64_t)lb0 * wtpb, T1 = min<uint64_t>((uint64_t)lb1 * wtpb, nwt);
+    auto ntl_of = [&](uint32_t q) -> uint32_t {
+        return T1 > T0 + q ? (uint32_t)((T1 - T0 - q + PV_RING_NP - 1) / PV_RING_NP) : 0u;
+    };
+    // tile k of parsing wave q (clamped to its last: the producer's tail issues re-read it)
+    auto tile_of = [&](uint32_t q, uint32_t nq, int64_t k) -> uint64_t {
+        return T0 + q + (uint64_t)PV_RING_NP * (uint64_t)min<int64_t>(max<int64_t>(k, 0), (int64_t)nq - 1);
+    };
+    // the span of tile k in HBM: [base, b1), packed when it fits a slot
+    auto span = [&](RingWave &W, uint64_t t, int64_t k, uint32_t &base, uint32_t &nch) {
+        const uint32_t row = (uint32_t)(k % PV_RING_R);
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(W.lo[row][0]);
+        const uint32_t b1 = t * PV_WT + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(W.hi[row][0]);
+        base = b0 & ~15u;
+        nch = (b1 - base + 15) >> 4;
+    };
+    const uint32_t cw = wave < PV_RING_NP ? wave : 0u;
+    const uint32_t ntl = wave < PV_RING_NP ? ntl_of(cw) : 0u;
+    if (wave >= PV_RING_NP) {
+        // ---- producer of parsing waves q0 .. q0 + SP - 1: issue e is tile e / SP of wave q0 + e % SP
+        // (every served wave takes the same count; a wave's surplus issues re-read its last tile)
+        const uint32_t q0 = (wave - PV_RING_NP) * PV_RING_SP;
+        uint32_t nt = 0, nts[PV_RING_SP];
+#pragma unroll
+        for (int u = 0; u < PV_RING_SP; u++) { nts[u] = ntl_of(q0 + u); nt = max(nt, nts[u]); }
+        auto ev_q = [&](uint32_t e) -> uint32_t { return PV_RING_SP == 1 ? 0u : e % PV_RING_SP; };
+        auto ev_k = [&](uint32_t e) -> uint32_t { return PV_RING_SP == 1 ? e : e / PV_RING_SP; };
+        auto nq_of = [&](uint32_t u) -> uint32_t {
+            uint32_t v = nts[0];
+#pragma unroll
+            for (int x = 1; x < PV_RING_SP; x++) v = (uint32_t)x == u ? nts[x] : v;
+            return v;
+        };
+        auto rows = [&](uint32_t u, int64_t k) {
+            RingWave &W = S.w[q0 + u];
+            const uint64_t t = tile_of(q0 + u, nq_of(u), k), r = t * PV_WT + lane;
+            const uint32_t row = (uint32_t)(k % PV_RING_R);
+            dma4(offs + min<uint64_t>(r, last), lds_addr(&W.lo[row][0]));
+            dma4(offs + min<uint64_t>(t * PV_WT + PV_WT, last), lds_addr(&W.hi[row][0]));
+        };
+        auto issue = [&](uint32_t e) {
+            const uint32_t u = ev_q(e), k = ev_k(e);
+            rows(u, (int64_t)k + PV_RING_D);
+            ring_vmcnt<PV_RING_WAITA>(); // rows of this tile (issued SP * D issues ago) landed
+            RingWave &W = S.w[q0 + u];
+            uint32_t base, nch;
+            span(W, tile_of(q0 + u, nq_of(u), k), k, base, nch);
+            const bool packed = nch <= (uint32_t)(PV_RING_NJ * 64);
+            const uint32_t o = W.lo[k % PV_RING_R][lane];
+            const uint32_t dst = lds_addr(&W.slot[k % PV_RING_Q][0]);
+#pragma unroll
+            for (int j = 0; j < PV_RING_NJ; j++) {
+                const uint32_t ch = (uint32_t)(j * 64) + lane;
+                const uint32_t src = packed ? base + min(ch, nch - 1) * 16 : (j < 5 ? (o & ~15u) + 16u * j : base);
+                dma16(recs + src, dst + j * 1024);
+            }
+        };
+        if (nt) {
+            for (uint32_t e = 0; e < PV_RING_SP * PV_RING_D; e++) rows(ev_q(e), ev_k(e));
+            ring_vmcnt<0>();
+            const uint32_t total = PV_RING_SP * nt;
+            uint32_t issued = 0, published = 0;
+            while (published < total) {
+                if (issued < total && ev_k(issued) < lds_ld(&S.fre[q0 + ev_q(issued)]) + PV_RING_Q) {
+                    issue(issued++); // a free slot: keep HBM busy first
+                    continue;
+                }
+                if (published < issued) {
+                    ring_wait_oldest(issued - published); // the oldest issue in flight landed
+                    const uint32_t e = published++;
+                    if (lane == 0) lds_st(&S.full[q0 + ev_q(e)], ev_k(e) + 1);
+                    continue;
+                }
+                __builtin_amdgcn_s_sleep(1); // every slot holds a published tile the parser has not released
+            }
+        }
+    } else {
+    RingWave &W = S.w[cw];
+    // ---- parsing wave cw
+    TST_DECL
     HostNets h;
     {
         const uint32_t n4 = P.nets.n4;
         h.a0 = P.nets.v4_addr[0]; h.m0 = P.nets.v4_mask[0]; h.e0 = n4 > 0 ? ~0u : 0u;
         h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
     }
-    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
-    // this workgroup's ranges [lb0, lb1) and their tiles [T0, T1)
-    const uint32_t G = (P.grid_main + gridDim.x - 1) / gridDim.x;
-    const uint32_t lb0 = min(blockIdx.x * G, P.grid_main), lb1 = min(lb0 + G, P.grid_main);
-    const uint64_t T0 = (uint64_t)lb0 * wtpb, T1 = min<uint64_t>((uint64_t)lb1 * wtpb, nwt);
-    const uint32_t ntl = T1 > T0 + wave ? (uint32_t)((T1 - T0 - wave + 3) / 4) : 0u;
-    RingWave &W = S.w[wave];
-    auto tile_of = [&](int64_t k) -> uint64_t {
-        return T0 + wave + 4ull * (uint64_t)min<int64_t>(max<int64_t>(k, 0), (int64_t)ntl - 1);
-    };
-    auto rows = [&](int64_t k) {
-        const uint64_t t = tile_of(k), r = t * PV_WT + lane;
-        const uint32_t row = (uint32_t)(k % PV_RING_R);
-        dma4(offs + min<uint64_t>(r, last), lds_addr(&W.lo[row][0]));
-        dma4(offs + min<uint64_t>(t * PV_WT + PV_WT, last), lds_addr(&W.hi[row][0]));
-    };
-    // the span of tile k in HBM: [base, b1), packed when it fits a slot
-    auto span = [&](int64_t k, uint32_t &base, uint32_t &nch) {
-        const uint32_t row = (uint32_t)(k % PV_RING_R);
-        const uint64_t t = tile_of(k);
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane(W.lo[row][0]);
-        const uint32_t b1 = t * PV_WT + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(W.hi[row][0]);
-        base = b0 & ~15u;
-        nch = (b1 - base + 15) >> 4;
-    };
-    auto pieces = [&](int64_t k) {
-        uint32_t base, nch;
-        span(k, base, nch);
-        const bool packed = nch <= (uint32_t)(PV_RING_NJ * 64);
-        const uint32_t o = W.lo[k % PV_RING_R][lane];
-        const uint32_t dst = lds_addr(&W.slot[k % PV_RING_Q][0]);
-#pragma unroll
-        for (int j = 0; j < PV_RING_NJ; j++) {
-            const uint32_t ch = (uint32_t)(j * 64) + lane;
-            const uint32_t src = packed ? base + min(ch, nch - 1) * 16 : (j < 5 ? (o & ~15u) + 16u * j : base);
-            dma16(recs + src, dst + j * 1024);
-        }
-    };
     uint64_t cd = 0, cl = 0; // fast lanes' packed counters (net_fast)
     NetCtr c;
     c.zero();
-    if (ntl) {
-        // rows of tiles 0 .. Q, then Q - 1 steps without a tile (rows k + 2Q, pieces k + Q - 1,
-        // k = 1 - Q .. -1), so every step of the loop sees the same ops younger than its tile
-        for (int k = 0; k <= PV_RING_Q; k++) rows(k);
-        ring_vmcnt<0>();
-        for (int k = 1 - PV_RING_Q; k < 0; k++) {
-            rows(k + 2 * PV_RING_Q);
-            pieces(k + PV_RING_Q - 1);
-        }
-    }
     for (uint32_t k = 0; k < ntl; k++) {
-        rows((int64_t)k + 2 * PV_RING_Q);
-        // the rows of tile k + Q - 1 (issued Q + 1 steps ago) landed
-        ring_vmcnt<(PV_RING_NJ + PV_RING_Q * PV_RING_OPS + 2 < 63 ? PV_RING_NJ + PV_RING_Q * PV_RING_OPS + 2 : 63)>();
-        pieces((int64_t)k + PV_RING_Q - 1);
-        ring_vmcnt<(PV_RING_Q - 1) * PV_RING_OPS>(); // tile k landed
+        TST(7)
+        while (lds_ld(&S.full[cw]) <= k) __builtin_amdgcn_s_sleep(1);
+        TST(0)
         const uint32_t row = k % PV_RING_R;
-        const uint64_t t = tile_of(k);
+        const uint64_t t = tile_of(cw, ntl, k);
         const uint32_t lb = (uint32_t)(t / wtpb), lr = lb - lb0; // the tile's grid range
         const uint64_t wbeg = (uint64_t)lb * wtpb;
         const uint64_t r0 = t * PV_WT, i = r0 + lane;
         const bool active = i < n;
         const uint32_t off = W.lo[row][lane];
         uint32_t base, nch;
-        span(k, base, nch);
+        span(W, t, k, base, nch);
         const bool packed = nch <= (uint32_t)(PV_RING_NJ * 64);
         const uint32_t *Ls = W.slot[k % PV_RING_Q];
         const uint32_t gb = packed ? base : (off & ~15u);
@@ -2573,6 +2686,10 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
         if (packed) recw_load_packed(Ls, rel, rw);
         else recw_load_window(Ls, rel >> 2, rel & 3, lane * 4, rw);
         const FastRec f = fast_fields(rw, h);
+#ifdef PV_TSTAMPS
+        asm volatile("" ::"v"(f.ok), "v"(f.dir) : "memory");
+#endif
+        TST(1)
         const bool fast = active & ((rel >> 2) + 17 <= (lim + 4) >> 2) & (f.ok != 0);
         const uint64_t slowm = __ballot(active & !fast);
         cd += fast ? 1ull << (f.dir * 16) : 0ull;
@@ -2631,7 +2748,9 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
         if (__ballot(hv != PV_NOH && hv > 65535)) {
             if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
         }
+        TST(2)
         hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
+        TST(3)
         const uint64_t m = __ballot(isdns);
         if (m) {
             uint32_t q = 0;
@@ -2672,8 +2791,12 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
                 tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, seg, lane);
             }
         }
+        TST(4)
+        // the tile's slot and row are read (LDS reads complete) before the producer may reuse them
+        __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0), vmcnt / expcnt untouched
+        if (lane == 0) lds_st(&S.fre[cw], k + 1);
     }
-    ring_vmcnt<0>();
+    RST_FLUSH
     {
         const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
         const uint32_t nf = fin + fout + funk;
@@ -2685,7 +2808,10 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
     NetK K;
     K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
     if (ntl) knet_flush(K, slot, c);
-    __syncthreads();
+    }
+    lds_barrier();
+    NetK K;
+    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
         if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
     // the ranges' DNS list counts (and the update-log counters the DNS pass starts from)
@@ -2702,7 +2828,8 @@ extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(con
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(const PvParams *__restrict__ Pp) { net_pass<false>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg<4>(Pp); }
-extern "C" __global__ void __launch_bounds__(256) pv_net_kernel_ring(const PvParams *__restrict__ Pp) { net_ring(Pp); }
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_tc(const PvParams *__restrict__ Pp) { net_fast_reg<4, true>(Pp); }
+extern "C" __global__ void __launch_bounds__(64 * PV_RING_NW) pv_net_kernel_ring(const PvParams *__restrict__ Pp) { net_ring(Pp); }
 // eight waves in the one workgroup of a CU: two per SIMD to hide instruction latency, one record stream per CU
 extern "C" __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg8(const PvParams *__restrict__ Pp) { net_fast_reg<8>(Pp); }
 
@@ -2753,6 +2880,13 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ DnsState S;
+    if (*P.n_dns == 0) {
+        // no DNS message in the batch (the Net pass counted them): only the ranges' event counts
+        // (the update-log counters stay as the Net pass reset them)
+        for (uint32_t lb = blockIdx.x * blockDim.x + threadIdx.x; lb < P.grid_main; lb += gridDim.x * blockDim.x)
+            P.blk_events[lb] = 0;
+        return;
+    }
     S.C.clear();
     if (threadIdx.x == 0) S.nresp = 0;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -3059,7 +3193,6 @@ struct CombState {
     uint32_t rep[CN];
     uint32_t h[NR];   // entries per region, then the placement cursors
     uint32_t tb[NR];  // tables (bit per PV_TSLOT) among each region's entries
-    uint32_t st[NR];  // each region's run start in the sorted list
     uint32_t wsum[16];
     uint32_t nsp;
 };
@@ -3097,6 +3230,32 @@ __device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, St &S, PV_G ulongl
         if (cur == ck) {
             atomicAdd(&S.cnt[pos], w);
             if (rep < S.rep[pos]) atomicMin(&S.rep[pos], rep);
+            return;
+        }
+        pos = (pos + 1) & (CN - 1);
+    }
+    const ulonglong2 e = comb_entry(ck, w, rep);
+    sp[atomicAdd(&S.nsp, 1u)] = e;
+    comb_count(P, S, e.x);
+}
+
+// comb_add with the first probe's key and rep words already read (cur0 / rep0, read for a whole
+// batch at once so the LDS round trips overlap)
+template <uint32_t CN, class St>
+__device__ __forceinline__ void comb_add_pre(PV_CREF(PvParams) P, St &S, PV_G ulonglong2 *sp, uint64_t ck, uint32_t w,
+                                             uint32_t rep, uint32_t pos, uint64_t cur0, uint32_t rep0)
+{
+    uint64_t cur = cur0;
+    for (int probe = 0; probe < 16; probe++) {
+        if (probe) { cur = S.key[pos]; rep0 = 0; }
+        if (cur == 0) {
+            const uint64_t prev = atomicCAS((unsigned long long *)&S.key[pos], 0ull, (unsigned long long)ck);
+            cur = prev == 0 ? ck : prev;
+            rep0 = 0xffffffffu;
+        }
+        if (cur == ck) {
+            atomicAdd(&S.cnt[pos], w);
+            if (rep < rep0 || probe) atomicMin(&S.rep[pos], rep);
             return;
         }
         pos = (pos + 1) & (CN - 1);
@@ -3158,14 +3317,35 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
         if (P.ip_compact) {
             // the register-window pass's compact log: address + direction bit, then the
             // range's exception entries
+            // software-pipelined per batch of PV_CB_U entries a thread: the log words and their
+            // direction words in flight together, then every entry's first-probe key and rep
+            // words read from LDS together, then the inserts (most end at that first probe)
             const PV_G uint32_t *ip4 = P.iplog32;
-            batched<PV_CB_U>(z - a, [&](uint64_t j) { return (uint64_t)ip4[a + j]; }, [&](uint64_t j, uint64_t ip) {
-                if (ip) {
-                    const uint64_t r = a + j;
-                    const uint64_t e = P.ip_base | ((P.ipdir[r >> 6] >> (r & 63)) & 1) << 32 | ip;
-                    comb_add<CN>(P, S, sp, e, 1u, (uint32_t)r);
+            const uint64_t nn = z - a, bd = blockDim.x;
+            const uint64_t ipb = P.ip_base;
+            for (uint64_t j0 = threadIdx.x; j0 < nn; j0 += (uint64_t)PV_CB_U * bd) {
+                uint32_t ipv[PV_CB_U];
+                uint64_t dw[PV_CB_U];
+#pragma unroll
+                for (int u = 0; u < PV_CB_U; u++) {
+                    const uint64_t j = j0 + (uint64_t)u * bd;
+                    ipv[u] = j < nn ? ip4[a + j] : 0u;
+                    dw[u] = j < nn ? P.ipdir[(a + j) >> 6] : 0ull;
                 }
-            });
+                uint64_t ck[PV_CB_U], cur[PV_CB_U];
+                uint32_t pos[PV_CB_U], rp[PV_CB_U];
+#pragma unroll
+                for (int u = 0; u < PV_CB_U; u++) {
+                    const uint64_t r = a + j0 + (uint64_t)u * bd;
+                    ck[u] = ipb | ((dw[u] >> (r & 63)) & 1) << 32 | ipv[u];
+                    pos[u] = (uint32_t)(fmix64(ck[u]) >> 20) & (CN - 1);
+                    cur[u] = ipv[u] ? S.key[pos[u]] : 0ull;
+                    rp[u] = ipv[u] ? S.rep[pos[u]] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < PV_CB_U; u++)
+                    if (ipv[u]) comb_add_pre<CN>(P, S, sp, ck[u], 1u, (uint32_t)(a + j0 + (uint64_t)u * bd), pos[u], cur[u], rp[u]);
+            }
             const uint32_t nx = P.ipx_cnt[blockIdx.x];
             for (uint32_t q = threadIdx.x; q < nx; q += blockDim.x) comb_add<CN>(P, S, sp, ipl[q], 1u, P.ipx_rep[a + q]);
         } else {
@@ -3201,12 +3381,11 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     PV_G uint64_t *col = P.cb_run + (blockIdx.x % 8) * ng8 + blockIdx.x / 8;
     for (uint32_t r = r0; r < r1; r++) {
         const uint32_t c = S.h[r];
-        S.st[r] = run;
         col[(uint64_t)r * 8 * ng8] = pv_run_word(run, c, S.tb[r]);
         S.h[r] = run; // the placement cursor
         run += c;
     }
-    __syncthreads();
+    lds_barrier(); // the run-table stores are the merge kernel's to read
     TST(3)
 #ifndef PV_ABL_COMB_NOOUT
 #define PV_ABL_COMB_NOOUT 0 // tuning/ablation only: skip writing the combined list
@@ -3260,7 +3439,9 @@ struct MergeRuns {
     uint32_t tabs;
 };
 
-extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams *__restrict__ Pp)
+#define PV_MG_THREADS 1024
+static_assert(PV_MG_THREADS >= (PV_MAX_GRID + 7) / 8 * 8, "one run per merge thread");
+extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) pv_topn_merge(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     const uint32_t rk = blockIdx.x;                  // run key: handler << reg_log2 | region
@@ -3270,6 +3451,28 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
     __shared__ MergeRuns U;
     TST_DECL
     const uint32_t ng8 = (P.grid_main + 7) / 8, ng = 8 * ng8;
+    // the region of the table this run key almost always holds (the handler's first period slot)
+    // is DMA'd into LDS now, in flight with the run words, not after them
+    const uint32_t rsl = P.tcap_log2 - P.reg_log2;
+    const uint32_t rs = 1u << rsl;
+    constexpr int PF = PV_RS / PV_MG_THREADS; // region entries per thread
+    static_assert(PF * PV_MG_THREADS == PV_RS, "region entries per thread");
+    const uint32_t tbg = hd ? PV_SLOTS + P.dslot_of[0] : P.slot_of[0];
+    const uint64_t rbg = ((uint64_t)tbg << P.tcap_log2) + ((uint64_t)r << rsl);
+    const bool pf = rs == PV_RS;
+    __shared__ MergeState S;
+    if (pf) {
+        // LDS-DMA straight into S.key / S.cnt: 32 1-KiB pieces each, two of each per wave (no
+        // VGPR holds them; the run words' wait below covers them)
+        static_assert(PV_RS * 8 == 32 * 1024 && PV_MG_THREADS == 1024, "two pieces per array and wave");
+        const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const uint32_t pc = wv * 2 + q;
+            dma16(P.tkeys + rbg + pc * 128 + ln * 2, lds_addr(&S.key[pc * 128]));
+            dma16(P.tcnt + rbg + pc * 128 + ln * 2, lds_addr(&S.cnt[pc * 128]));
+        }
+    }
     uint32_t n;
     {
         uint32_t c = 0, tb = 0;
@@ -3285,6 +3488,7 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
             }
         }
         uint32_t total;
+        PV_VMCNT(0); // the region DMA too, before the barriers below
         const uint32_t pre = block_excl_scan(c, U.wsum, total);
         if (threadIdx.x < ng) U.pref[threadIdx.x] = pre;
         if (threadIdx.x == 0) U.pref[ng] = total;
@@ -3322,29 +3526,36 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
         }
         return;
     }
-    __shared__ MergeState S;
-    const uint32_t rsl = P.tcap_log2 - P.reg_log2;
-    const uint32_t rs = 1u << rsl;
     static_assert(PV_TABLES <= 32, "table mask");
+    static_assert(sizeof(MergeState) + sizeof(MergeRuns) <= 160 * 1024, "pv_topn_merge LDS");
     uint32_t tabs = U.tabs << (hd * PV_SLOTS); // the tables among this run key's entries
     const bool one = !(tabs & (tabs - 1));
+    bool fresh = true; // S still holds the DMA'd region (no earlier table of this loop reloaded it)
     while (tabs) {
         const uint32_t tb = __builtin_ctz(tabs);
         const uint32_t s = tb % PV_SLOTS; // the handler slot (Net for tb < PV_SLOTS, else DNS)
         tabs &= tabs - 1;
         const uint64_t rbase = ((uint64_t)tb << P.tcap_log2) + ((uint64_t)r << rsl);
-        batched<4>(rs, [&](uint64_t i) { return make_ulonglong2(P.tkeys[rbase + i], P.tcnt[rbase + i]); },
-                   [&](uint64_t i, ulonglong2 kc) {
-                       S.key[i] = kc.x;
-                       S.cnt[i] = kc.x ? kc.y : 0; // an empty entry's count word is stale
-                       S.dirty[i] = !kc.x && kc.y;  // written back as zero
-                       S.mn[0][i] = 0xffffffffu;
-                       S.mn[1][i] = 0xffffffffu;
-                   });
+        auto put = [&](uint64_t i, ulonglong2 kc) {
+            S.key[i] = kc.x;
+            S.cnt[i] = kc.x ? kc.y : 0; // an empty entry's count word is stale
+            S.dirty[i] = !kc.x && kc.y;  // written back as zero
+            S.mn[0][i] = 0xffffffffu;
+            S.mn[1][i] = 0xffffffffu;
+        };
+        if (pf && tb == tbg && fresh) {
+#pragma unroll
+            for (int u = 0; u < PF; u++) {
+                const uint32_t i = threadIdx.x + u * PV_MG_THREADS;
+                put(i, make_ulonglong2(S.key[i], S.cnt[i]));
+            }
+        } else {
+            batched<4>(rs, [&](uint64_t i) { return make_ulonglong2(P.tkeys[rbase + i], P.tcnt[rbase + i]); }, put);
+        }
         if (threadIdx.x == 0) { S.nnew = 0; S.ncr = 0; }
         __syncthreads();
         TST(1)
-        batched<PV_MG_U>(n, ld, [&](uint64_t, ulonglong2 e) {
+        auto ins = [&](ulonglong2 e) __attribute__((always_inline)) {
             const uint64_t e0 = e.x;
             if (!one && entry_table(e0) != tb) return;
             const uint64_t e1 = e.y;
@@ -3388,22 +3599,15 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
                     table_overflow(P, s, key, w, rep, true);
                 }
             }
-        });
+        };
+        batched<PV_MG_U>(n, ld, [&](uint64_t, ulonglong2 e) { ins(e); });
         __syncthreads();
         TST(2)
 #ifndef PV_ABL_MERGE
 #define PV_ABL_MERGE 0 // tuning/ablation only: 1 no CPC updates, 2 no write-back, 3 neither
 #endif
-        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
-            if ((PV_ABL_MERGE & 2) == 0 && S.dirty[i]) {
-                P.tkeys[rbase + i] = S.key[i];
-                P.tcnt[rbase + i] = S.cnt[i];
-            }
-            // IPv4 cardinality: one first-occurrence update per address and direction
-            for (uint32_t d = 0; d < 2; d++)
-                if ((PV_ABL_MERGE & 1) == 0 && S.mn[d][i] != 0xffffffffu)
-                    cpc_min(P, s, d ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)S.key[i]), (int64_t)(P.gbase + S.mn[d][i]));
-        }
+        // the new names' list slots first, then the names and the write-back: the region's stores
+        // and CPC atomics come last, so nothing of this workgroup waits for them to complete
         const uint32_t nnew = S.nnew;
         if (threadIdx.x == 0 && nnew) S.nbase = atomicAdd(P.nn_cnt, nnew);
         if (threadIdx.x == 0 && S.ncr) atomicAdd(&P.tab_live[tb], S.ncr);
@@ -3415,8 +3619,19 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_merge(const PvParams 
             if (g < P.nn_cap) P.nn[g] = PvNewName{tb, S.nrep[k], pos};
             else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k], nullptr, S.key[S.nidx[k]]);
         }
-        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+            if ((PV_ABL_MERGE & 2) == 0 && S.dirty[i]) {
+                P.tkeys[rbase + i] = S.key[i];
+                P.tcnt[rbase + i] = S.cnt[i];
+            }
+            // IPv4 cardinality: one first-occurrence update per address and direction
+            for (uint32_t d = 0; d < 2; d++)
+                if ((PV_ABL_MERGE & 1) == 0 && S.mn[d][i] != 0xffffffffu)
+                    cpc_min(P, s, d ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)S.key[i]), (int64_t)(P.gbase + S.mn[d][i]));
+        }
+        if (tabs) lds_barrier(); // another table's region reuses S
         TST(4)
+        fresh = false;
     }
     TST_FLUSH(65536)
 }
