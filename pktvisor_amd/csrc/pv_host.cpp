@@ -153,7 +153,7 @@ extern "C" __global__ void pv_dns_suffix(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
 extern "C" __global__ void pv_fill_multi(PvFillList L);
-extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t nblk);
+extern "C" __global__ void pv_xact_compact(const PvParams *P, uint32_t b0, uint32_t kbase);
 extern "C" __global__ void pv_dns_prescan(const PvParams *P);
 extern "C" __global__ void pv_topn_combine(const PvParams *P);
 extern "C" __global__ void pv_topn_combine_r12(const PvParams *P);
@@ -172,10 +172,12 @@ extern "C" __global__ void pv_topn_names(const PvParams *P);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" __global__ void pv_xact_carry(const PvXactParams *X);
+extern "C" __global__ void pv_xact_edge2(const PvXactParams *X, const PvEdgePair *pairs, uint32_t n, uint8_t *sfx, uint8_t *tsfx);
 extern "C" __global__ void pv_xact_defer(const uint64_t *skeys, const uint32_t *svals, const PvXEvent *events, uint32_t n,
-                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at, const uint64_t *eecs, uint64_t *pecs);
-extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, uint32_t n_pend,
-                                           uint32_t at);
+                                         PvXEvent *pend, uint64_t *pkeys, uint32_t *pvals, uint32_t at, uint32_t ehi,
+                                         const uint64_t *eecs, uint64_t *pecs, uint32_t *ctr);
+extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, const uint32_t *pvals,
+                                           uint32_t n_pend, uint32_t at);
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
                                           uint32_t *vout, size_t n, hipStream_t s);
 extern "C" __global__ void pv_dns_tcp(const PvParams *P);
@@ -193,7 +195,7 @@ namespace {
 
 // status words (device): flags, n_events, n_resp, n_vals, DNS messages, new top-N names
 enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNEW = 5, ST_TSEG = 6, ST_TSEG_BYTES = 7,
-       ST_WORDS = 8, ST_HANDS = 8 /* top-N handlers with entries (device only) */ };
+       ST_HANDS = 8 /* top-N handlers with entries (device only) */, ST_NKEYS = 9 /* key-list length */, ST_WORDS = 10 };
 // status allocation (zeroed per batch): the words above, padded
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
 #define PV_TRASH_WAVES 16384 // Net-pass waves with a 2-KiB trash area (grid <= 4096)
@@ -552,8 +554,12 @@ struct pv_ctx {
     // DNS v2 top_ecs: the ECS address of each query event, and of each carried query
     uint64_t *d_eecs = nullptr, *d_pecs[2] = {nullptr, nullptr};
     uint64_t *d_pkeys[2] = {nullptr, nullptr};
+    uint32_t *d_pvals[2] = {nullptr, nullptr}; // each carried query's index in the event store d_pend
     uint32_t pend_cur = 0;
     uint64_t n_pend = 0, pend_cap = 0;
+    // event store: capacity of d_events / d_pend (equal, so a query-only batch's store can be
+    // handed over), extent of d_pend[pend_cur] in use; key list capacity (d_skeys / d_pkeys)
+    uint64_t ev_store_cap = 0, pend_hi = 0, key_cap = 0;
     int64_t pend_base = -1;
     // shard-edge stubs (orphan responses) accumulated since reset, device counter in d_nvals[3]
     PvXEvent *d_orph = nullptr;
@@ -722,8 +728,10 @@ struct pv_ctx {
     struct EdgeStub {
         PvXEvent e;
         uint64_t ord;
-        int64_t cand; // SlowCand template in sorph (responses), -1 for queries
+        int64_t cand;  // SlowCand template in sorph (responses), -1 for queries
+        int64_t order; // DNS v2: first-occurrence order (the response's qname CPC order as an edge pair)
     };
+    int64_t *d_orph_ord = nullptr; // DNS v2 stubs' orders (pv_set_slow_defer)
     std::vector<EdgeStub> stubs;
     int64_t edge_h = 0;                                        // first record second + ttl + 61
     std::vector<std::pair<int64_t, uint64_t>> dns_shift_ord;   // (threshold second, ordinal) of local DNS shifts
@@ -2298,6 +2306,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
     const uint64_t region_max = mr / ((uint64_t)c->wg_per_cu * c->cus) + 64 * 64;
     const uint64_t ev_cap = mr + region_max + 64 * 64 + 16 * 256 + c->tmsg_cap + 2 * region_max;
     c->pend_cap = 2 * mr; // open queries carried between batches
+    c->ev_store_cap = std::max<uint64_t>(ev_cap, c->pend_cap + mr);
+    c->key_cap = mr + c->tmsg_cap + c->pend_cap;
+    const size_t esc = (size_t)c->ev_store_cap, kc = (size_t)c->key_cap;
     c->orph_cap = (uint32_t)std::min<uint64_t>(2 * mr, 1u << 30);
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) ||
         !hip_ok(e = hipMalloc(&c->d_sum, (size_t)PV_SLOTS * PV_SUM_WORDS * 8)) ||
@@ -2309,7 +2320,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_arena_top, PV_TABLES * PV_ARENA_PARTS * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_dbits, (size_t)(mr / 64 + 2) * 8)) ||
         !hip_ok(e = hipHostMalloc((void **)&c->h_dbits, (size_t)(mr / 64 + 2) * 8, hipHostMallocDefault)) ||
-        !hip_ok(e = hipMalloc(&c->d_events, (size_t)ev_cap * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_events, esc * sizeof(PvXEvent))) ||
         !hip_ok(e = hipMalloc(&c->d_ekeys, (size_t)ev_cap * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_mq_cnt, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_dq, (size_t)ev_cap * 32)) ||
@@ -2317,14 +2328,16 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_stamps, 65536 * 4 * 8 * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_blk_events, 65536 * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_orph, (size_t)c->orph_cap * sizeof(PvXEvent))) ||
-        !hip_ok(e = hipMalloc(&c->d_pend[0], (size_t)(c->pend_cap + mr) * sizeof(PvXEvent))) ||
-        !hip_ok(e = hipMalloc(&c->d_pend[1], (size_t)(c->pend_cap + mr) * sizeof(PvXEvent))) ||
-        !hip_ok(e = hipMalloc(&c->d_pkeys[0], (size_t)(c->pend_cap + mr) * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_pkeys[1], (size_t)(c->pend_cap + mr) * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_skeys, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_skeys2, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 8)) ||
-        !hip_ok(e = hipMalloc(&c->d_svals, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_svals2, (size_t)(mr + c->tmsg_cap + c->pend_cap) * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_pend[0], esc * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_pend[1], esc * sizeof(PvXEvent))) ||
+        !hip_ok(e = hipMalloc(&c->d_pkeys[0], kc * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_pkeys[1], kc * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_pvals[0], kc * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_pvals[1], kc * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_skeys, kc * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_skeys2, kc * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_svals, kc * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_svals2, kc * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
@@ -2336,9 +2349,9 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_theta, ((size_t)1 << c->reg_log2) * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_ovf, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
         ((c->dns2_groups & PV_DNS2_TOP_ECS) &&
-         (!hip_ok(e = hipMalloc(&c->d_eecs, (size_t)ev_cap * 8)) ||
-          !hip_ok(e = hipMalloc(&c->d_pecs[0], (size_t)(c->pend_cap + mr) * 8)) ||
-          !hip_ok(e = hipMalloc(&c->d_pecs[1], (size_t)(c->pend_cap + mr) * 8)))) ||
+         (!hip_ok(e = hipMalloc(&c->d_eecs, esc * 8)) ||
+          !hip_ok(e = hipMalloc(&c->d_pecs[0], esc * 8)) ||
+          !hip_ok(e = hipMalloc(&c->d_pecs[1], esc * 8)))) ||
         !hip_ok(e = hipMalloc(&c->d_ovf2, (size_t)c->ovf_cap * sizeof(PvOvf))) ||
 
         !hip_ok(e = hipMalloc(&c->d_nn, (size_t)c->nn_cap * sizeof(PvNewName))) ||
@@ -2367,8 +2380,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         return c->hipfail(e, "device allocation");
     }
     size_t tmp = 0;
-    pv_radix_sort_pairs(nullptr, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
-                        (size_t)(mr + c->tmsg_cap + c->pend_cap), c->stream);
+    pv_radix_sort_pairs(nullptr, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, kc, c->stream);
     c->sort_tmp_bytes = std::max<size_t>(tmp, 256);
     if (!hip_ok(e = hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes))) { *out = c; return c->hipfail(e, "sort scratch"); }
     *out = c;
@@ -2384,7 +2396,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
                     c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_cb_h, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
-                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_orph, c->d_sfx, c->d_psl,
+                    c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_pvals[0], c->d_pvals[1], c->d_orph, c->d_orph_ord, c->d_sfx, c->d_psl,
                     c->d_tseg, c->d_tmask, c->d_tpm, c->d_tcpcnt, c->d_tparams, c->d_tkey[0], c->d_tkey[1], c->d_tval[0],
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
@@ -2456,6 +2468,7 @@ int pv_reset(pv_ctx *c)
     c->p90_2[0] = c->p90_2[1] = c->p90_2[2] = 0.0f;
     c->remote_topn.clear();
     c->n_pend = 0;
+    c->pend_hi = 0;
     c->pend_base = -1;
     c->dns_shifts.clear();
     c->sg_ord.clear();
@@ -3102,7 +3115,7 @@ int defer_slow(pv_ctx *c, const PvParams &P, hipStream_t st)
         if (int rc = gather_records(c, P, reinterpret_cast<const uint32_t *>(c->d_valid), sizeof(PvXValid) / 4, nv[1], offs, st))
             return rc;
         for (uint32_t i = 0; i < nv[1]; i++)
-            if (v[i].dir < 2)
+            if (v[i].dir < 2 || v[i].dir >= 4) // v1 directions, DNS v2's 4 + transaction direction
                 c->scands.push_back(pv_ctx::SlowCand{ord_of(v[i].period), v[i].us, offs[i], v[i].dir, (uint8_t)((v[i].idx & PV_TCP_IDX) != 0)});
         const uint32_t zero = 0;
         if (!hip_ok(e = hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st))) return c->hipfail(e, "deferred candidates");
@@ -3112,7 +3125,9 @@ int defer_slow(pv_ctx *c, const PvParams &P, hipStream_t st)
     if (no > c->orph_done) {
         const uint32_t k = no - c->orph_done;
         std::vector<PvXEvent> o(k);
-        if (!hip_ok(e = hipMemcpy(o.data(), c->d_orph + c->orph_done, (size_t)k * sizeof(PvXEvent), hipMemcpyDeviceToHost)))
+        std::vector<int64_t> oo(k, 0);
+        if (!hip_ok(e = hipMemcpy(o.data(), c->d_orph + c->orph_done, (size_t)k * sizeof(PvXEvent), hipMemcpyDeviceToHost)) ||
+            (c->d_orph_ord && !hip_ok(e = hipMemcpy(oo.data(), c->d_orph_ord + c->orph_done, (size_t)k * 8, hipMemcpyDeviceToHost))))
             return c->hipfail(e, "orphan stubs");
         // the records of the responses (an edge pair's top_slow candidate needs its name)
         std::vector<uint32_t> ridx;
@@ -3130,13 +3145,13 @@ int defer_slow(pv_ctx *c, const PvParams &P, hipStream_t st)
         }
         size_t r = 0;
         for (uint32_t i = 0; i < k; i++) {
-            const uint64_t ord = ord_of(o[i].period);
+            const uint64_t ord = ord_of(o[i].period & 0x3f); // DNS v2 stubs: the kept flag in bit 7
             int64_t cand = -1;
             if (o[i].qr) {
                 cand = (int64_t)c->sorph.size();
                 c->sorph.push_back(pv_ctx::SlowCand{ord, 0, offs[r++], o[i].dir, (uint8_t)((o[i].idx & PV_TCP_IDX) != 0)});
             }
-            c->stubs.push_back(pv_ctx::EdgeStub{o[i], ord, cand});
+            c->stubs.push_back(pv_ctx::EdgeStub{o[i], ord, cand, oo[i]});
         }
         c->orph_done = no;
     }
@@ -3148,31 +3163,48 @@ int defer_slow(pv_ctx *c, const PvParams &P, hipStream_t st)
 // queries carried in; a batch of queries only just appends them to the carried list. Also the
 // heartbeat's DNS shift (nev_b = 0, one shift): the carried queries the shift purges time out
 // in the new live bucket, the rest carry on.
-int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uint64_t n, hipStream_t st)
+int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uint32_t nresp, uint64_t n, hipStream_t st,
+               uint64_t ev_hi)
 {
     hipError_t e;
     const bool dns_here = nev_b > 0;
     bool pair = (dns_here && (nresp > 0 || P.n_dshift > 0)) || (!dns_here && P.n_dshift > 0 && c->n_pend > 0);
-    if (dns_here && !pair && c->n_pend + nev_b > c->pend_cap) pair = true; // compact the carried list
+    if (dns_here && !pair && (c->n_pend + nev_b > c->pend_cap || (c->n_pend && c->pend_hi + nev_b > c->ev_store_cap)))
+        pair = true; // compact the carried list
     if (dns_here && !pair) {
-        hipLaunchKernelGGL(pv_xact_defer, dim3((nev_b + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
-                           c->d_events, nev_b, c->d_pend[c->pend_cur], c->d_pkeys[c->pend_cur], (uint32_t)c->n_pend,
-                           c->d_eecs, c->d_pecs[c->pend_cur]);
-        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_defer");
+        const uint32_t cur = c->pend_cur;
+        if (c->n_pend == 0 && nkeys == nev_b) {
+            // nothing carried: the batch's event store, sorted-key inputs and ECS words become the
+            // carried list as they lie (pointer exchange; the next batch writes the other buffers)
+            std::swap(c->d_events, c->d_pend[cur]);
+            std::swap(c->d_skeys, c->d_pkeys[cur]);
+            std::swap(c->d_svals, c->d_pvals[cur]);
+            if (c->d_eecs) std::swap(c->d_eecs, c->d_pecs[cur]);
+            c->pend_hi = ev_hi;
+        } else {
+            // (the key list's sentinel slots, messages without an event, are left out)
+            if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st))) return c->hipfail(e, "defer counter");
+            hipLaunchKernelGGL(pv_xact_defer, dim3((nkeys + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
+                               c->d_events, nkeys, c->d_pend[cur], c->d_pkeys[cur], c->d_pvals[cur], (uint32_t)c->n_pend,
+                               (uint32_t)c->pend_hi, c->d_eecs, c->d_pecs[cur], c->d_nvals + 2);
+            if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_defer");
+            c->pend_hi += nev_b;
+        }
         c->n_pend += nev_b;
     }
     if (pair) {
         const uint32_t np_in = (uint32_t)c->n_pend;
         if (np_in) {
             hipLaunchKernelGGL(pv_xact_pend_in, dim3((np_in + 255) / 256), dim3(256), 0, st, c->d_skeys, c->d_svals,
-                               c->d_pkeys[c->pend_cur], np_in, nev_b);
+                               c->d_pkeys[c->pend_cur], c->d_pvals[c->pend_cur], np_in, nkeys);
             if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_pend_in");
         }
+        // sorted: this batch's events and the carried queries first, the sentinel slots behind
         const uint32_t nev = nev_b + np_in;
         uint32_t threads = 256, blocks = (nev + threads - 1) / threads;
         size_t tmp = c->sort_tmp_bytes;
         if (!hip_ok(e = pv_radix_sort_pairs(c->d_sort_tmp, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
-                                             (size_t)nev, st)))
+                                             (size_t)nkeys + np_in, st)))
             return c->hipfail(e, "radix sort");
         PvXactParams X;
         memset(&X, 0, sizeof X);
@@ -3188,7 +3220,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
             X.slot_gen[k] = P.dslot_of[k] | (c->gen[P.dslot_of[k]] << 8);
             X.thr_from[k] = k == 0 && !c->slow_defer ? c->from90 : -1.0f;
             X.thr_to[k] = k == 0 && !c->slow_defer ? c->to90 : -1.0f;
-            for (uint32_t d = 0; d < 3; d++) X.thr2[k][d] = k == 0 ? c->p90_2[d] : -1.0f;
+            for (uint32_t d = 0; d < 3; d++) X.thr2[k][d] = k == 0 && !c->slow_defer ? c->p90_2[d] : -1.0f;
         }
         X.vals = c->d_xvals;
         X.n_vals = c->d_nvals;
@@ -3200,6 +3232,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         X.pecs = c->d_pecs[c->pend_cur];
         X.pecs_out = c->d_pecs[c->pend_cur ^ 1];
         X.pkeys_out = c->d_pkeys[c->pend_cur ^ 1];
+        X.pvals_out = c->d_pvals[c->pend_cur ^ 1];
         X.n_pend_out = c->d_nvals + 2;
         X.orph = c->d_orph;
         X.n_orph = c->d_nvals + 3;
@@ -3207,7 +3240,8 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         X.trecs = c->d_marena;
         X.toffs = c->d_moffs;
         X.tsfx = c->d_tsfx;
-        X.edge_h = c->slow_defer && !c->dns2_groups ? c->edge_h : 0;
+        X.edge_h = c->slow_defer ? c->edge_h : 0;
+        X.orph_ord = c->slow_defer && c->dns2_groups ? c->d_orph_ord : nullptr; // DNS v2 stubs
         if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
             !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
             return c->hipfail(e, "parameter upload");
@@ -3268,6 +3302,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nresp, uin
         }
         if (npo > c->pend_cap) return c->fail(PV_ECAPACITY, "%u open DNS queries exceed the carried-list capacity", npo);
         c->n_pend = npo;
+        c->pend_hi = npo;
         c->pend_cur ^= 1;
         c->pend_base = (int64_t)(c->records_seen + n) - 1;
     }
@@ -3439,7 +3474,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.blk_events = c->d_blk_events;
     P.skeys = c->d_skeys;
     P.svals = c->d_svals;
-    P.n_events = c->d_status + ST_NEV; // [0] packed total, [1] responses (ST_NRESP)
+    P.n_events = c->d_status + ST_NEV; // [0] events, [1] responses (ST_NRESP)
+    P.n_keys = c->d_status + ST_NKEYS;
     P.n_dns = c->d_status + ST_NDNS;
     P.want_events = ((c->dns_groups & PV_DNS_TRANSACTIONS) || c->dns2_groups) ? 1 : 0;
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
@@ -3586,8 +3622,6 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);
     // names: as many workgroups as are resident (LDS: two per CU), each pipelining its entries
     hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 2), dim3(256), 0, st, (const PvParams *)c->d_params);
-    if (P.want_events)
-        hipLaunchKernelGGL(pv_xact_compact, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params, grid);
     if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch");
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
@@ -3608,8 +3642,10 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     }
     const uint32_t gt = tcp_pass(c, P, a, a + n, st, c->h_params + 1);
     if (gt) {
+        // the TCP messages' events behind the UDP pass's key list
         if (P.want_events)
-            hipLaunchKernelGGL(pv_xact_compact, dim3(grid + gt), dim3(256), 0, st, (const PvParams *)c->d_params, grid + gt);
+            hipLaunchKernelGGL(pv_xact_compact, dim3(gt), dim3(256), 0, st, (const PvParams *)c->d_params, grid,
+                               status[ST_NKEYS]);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_dns_tcp");
         if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_RB_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
@@ -3672,7 +3708,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             fprintf(stderr, "\n");
         }
     }
-    if (int rc = pair_stage(c, P, status[ST_NEV], status[ST_NRESP], n, st)) return rc;
+    if (int rc = pair_stage(c, P, status[ST_NEV], status[ST_NKEYS], status[ST_NRESP], n, st,
+                            (uint64_t)(grid + gt) * P.wt_per_block * 64u))
+        return rc;
     // top_slow updates of the transaction stage (only when it ran)
     if ((status[ST_NEV] || c->n_pend) && P.want_events)
         if (int rc = drain_overflow(c, st)) return rc;
@@ -4298,6 +4336,7 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
             P.skeys = c->d_skeys;
             P.svals = c->d_svals;
             P.n_events = c->d_status + ST_NEV;
+            P.n_keys = c->d_status + ST_NKEYS;
             P.wt_per_block = 4; // 64-record tiles: 256 events per block
             P.grid_main = blocks;
             if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
@@ -4310,14 +4349,15 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
             return c->hipfail(e, "parameter upload");
         hipLaunchKernelGGL(pv_dnstap_kernel, dim3(blocks), dim3(256), 0, st, (const PvParams *)c->d_params);
-        if (P.want_events) hipLaunchKernelGGL(pv_xact_compact, dim3(blocks), dim3(256), 0, st, (const PvParams *)c->d_params, blocks);
+        if (P.want_events) hipLaunchKernelGGL(pv_xact_compact, dim3(blocks), dim3(256), 0, st, (const PvParams *)c->d_params, 0u, 0u);
         if (!hip_ok(e = hipGetLastError()) ||
             !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_RB_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "pv_dnstap_kernel");
         if (P.want_events) {
             const uint32_t nev = c->h_status[ST_NEV], nresp = c->h_status[ST_NRESP];
-            if (int rc = pair_stage(c, P, nev, nresp, b - a, st)) return rc;
+            if (int rc = pair_stage(c, P, nev, c->h_status[ST_NKEYS], nresp, b - a, st, (uint64_t)blocks * P.wt_per_block * 64u))
+                return rc;
         }
         if (int rc = drain_overflow(c, st)) return rc;
         uint32_t flags = 0;
@@ -4842,7 +4882,7 @@ int dns_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
         P.ekey_base = (uint32_t)((int64_t)c->records_seen - c->pend_base);
         P.flags = c->d_status + ST_FLAGS;
         flush_fills(c);
-        if (int rc = pair_stage(c, P, 0, 0, 0, st)) return rc;
+        if (int rc = pair_stage(c, P, 0, 0, 0, 0, st, 0)) return rc;
     } else if (xacts && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
         // nothing open: only the slow thresholds of the closed bucket (kept when it had none)
         if (int rc = sync_xvals(c)) return rc;
@@ -5469,6 +5509,237 @@ bool in_dns_window(pv_ctx *c, uint32_t slot)
 {
     return std::find(c->dns.slots.begin(), c->dns.slots.end(), slot) != c->dns.slots.end();
 }
+// the carried list on the host: each open query event (gathered from the event store by its
+// index) with its sort key
+int read_carried(pv_ctx *c, std::vector<PvXEvent> &pend, std::vector<uint64_t> &pk, std::vector<uint64_t> *ecs = nullptr)
+{
+    pend.clear();
+    pk.assign(c->n_pend, 0);
+    if (ecs) ecs->assign(c->n_pend, 0);
+    if (!c->n_pend) return 0;
+    std::vector<uint32_t> pv(c->n_pend);
+    std::vector<PvXEvent> store(c->pend_hi);
+    std::vector<uint64_t> estore(ecs && c->d_pecs[c->pend_cur] ? c->pend_hi : 0);
+    hipError_t e;
+    if (!hip_ok(e = hipMemcpy(pk.data(), c->d_pkeys[c->pend_cur], c->n_pend * 8, hipMemcpyDeviceToHost)) ||
+        !hip_ok(e = hipMemcpy(pv.data(), c->d_pvals[c->pend_cur], c->n_pend * 4, hipMemcpyDeviceToHost)) ||
+        !hip_ok(e = hipMemcpy(store.data(), c->d_pend[c->pend_cur], c->pend_hi * sizeof(PvXEvent), hipMemcpyDeviceToHost)) ||
+        (!estore.empty() && !hip_ok(e = hipMemcpy(estore.data(), c->d_pecs[c->pend_cur], c->pend_hi * 8, hipMemcpyDeviceToHost))))
+        return c->hipfail(e, "open queries");
+    pend.resize(c->n_pend);
+    for (size_t i = 0; i < pv.size(); i++) {
+        if (pv[i] >= c->pend_hi) return c->fail(PV_EINVAL, "carried query %zu indexes past the event store", i);
+        pend[i] = store[pv[i]];
+        if (!estore.empty()) (*ecs)[i] = estore[pv[i]];
+    }
+    return 0;
+}
+// one SUM word of a slot += delta (host read-modify-write: the few counters an edge merge moves)
+int add_sum_word(pv_ctx *c, uint32_t slot, uint32_t word, int64_t delta)
+{
+    if (!delta) return 0;
+    c->dns.clean[slot] = false;
+    uint64_t *dp = c->d_sum + (size_t)slot * PV_SUM_WORDS + word;
+    uint64_t v = 0;
+    hipError_t e;
+    if (!hip_ok(e = hipMemcpy(&v, dp, 8, hipMemcpyDeviceToHost))) return c->hipfail(e, "edge counters");
+    v += (uint64_t)delta;
+    if (!hip_ok(e = hipMemcpy(dp, &v, 8, hipMemcpyHostToDevice))) return c->hipfail(e, "edge counters");
+    return 0;
+}
+
+// pv_edge_carry for DNS v2 (one TransactionManager per transaction direction, the direction in
+// the key; dns/v2/DnsStreamHandler.cpp:1100-1145, the manager's purge at its shifts .h:440-453):
+// an open query meets the first event of its key in this shard as resolve_one2 would have met it
+// in one stream. A response there, which this shard counted as an orphan, pairs instead: the
+// orphan count is taken back and the transaction accounted on the response (pv_xact_edge2), or
+// counted filtered / timed out. Purges are time-outs of the purging shift's bucket. The edge
+// pairs' times feed the stream's thresholds (slow_xv) and their slow candidates (scands).
+// Buffers: n x (PvXEvent [+ u64 ECS address with top_ecs]).
+int edge_carry2(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes)
+{
+    const bool ecs = c->d_pecs[0] != nullptr;
+    const size_t esz = sizeof(PvXEvent) + (ecs ? 8 : 0);
+    if (in_bytes % esz) return c->fail(PV_EINVAL, "malformed open-query buffer");
+    std::unordered_map<uint64_t, size_t> first;
+    first.reserve(c->stubs.size() * 2);
+    for (size_t i = 0; i < c->stubs.size(); i++) first.emplace(c->stubs[i].e.key, i);
+    const uint64_t live = c->dns.ordinal;
+    auto in_win = [&](uint64_t ord) { return ord <= live && ord + c->dns.slots.size() > live; };
+    auto slot_of = [&](uint64_t ord) { return c->dns.slots[live - ord]; };
+    const uint32_t g = c->dns2_groups;
+    std::map<std::pair<uint32_t, uint32_t>, int64_t> add; // (slot, SUM word) -> delta
+    std::vector<PvXEvent> keep;
+    std::vector<uint64_t> keep_ecs;
+    std::vector<PvEdgePair> pairs;
+    std::vector<size_t> pair_stub;
+    const size_t nin = in_bytes / esz;
+    for (size_t k = 0; k < nin; k++) {
+        PvXEvent qe;
+        uint64_t qaddr = 0;
+        memcpy(&qe, in + k * esz, sizeof qe);
+        if (ecs) memcpy(&qaddr, in + k * esz + sizeof qe, 8);
+        const uint32_t xd = (uint32_t)((qe.key >> 48) & 3) - 1;
+        if (xd >= 3) return c->fail(PV_EINVAL, "open query %zu has no DNS v2 transaction direction", k);
+        auto d2 = [&](uint32_t slot, uint32_t ctr, int64_t v) { add[{slot, PV_OFF_DNS2 + xd * PV_DNS2_CTRS + ctr}] += v; };
+        int ps = -1;
+        for (size_t i = 0; i < c->dns_shift_ord.size(); i++)
+            if (c->dns_shift_ord[i].first >= (int64_t)c->ttl_s + qe.sec) { ps = (int)i; break; }
+        auto purged = [&]() {
+            const uint64_t o = c->dns_shift_ord[ps].second;
+            if (in_win(o)) { d2(slot_of(o), D2_TIMEOUT, 1); d2(slot_of(o), D2_SEEN, 1); }
+        };
+        auto it = first.find(qe.key);
+        if (it == first.end()) {
+            if (ps >= 0) purged();
+            else { keep.push_back(qe); keep_ecs.push_back(qaddr); }
+            continue;
+        }
+        const pv_ctx::EdgeStub &st = c->stubs[it->second];
+        if (ps >= 0 && st.ord >= c->dns_shift_ord[ps].second) { purged(); continue; } // purged before its key's next event
+        if (!st.e.qr) continue;                                                          // overwritten by a new query
+        const PvXEvent &r = st.e;
+        const bool win = in_win(st.ord), kept = (r.period & 0x80) && win;
+        const uint32_t slot = win ? slot_of(st.ord) : 0;
+        const bool rf = r.pad & 4, qf = qe.pad & 4, rdeep = !(r.pad & 32);
+        int64_t dsec = r.sec > qe.sec ? r.sec - qe.sec : qe.sec - r.sec;
+        int64_t dnsec = (int64_t)r.nsec - (int64_t)qe.nsec;
+        if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
+        const bool timed_out = dsec > (int64_t)c->ttl_s || (dsec == (int64_t)c->ttl_s && ((double)dnsec / 1.0e6) >= (double)c->ttl_ms);
+        if (kept && !rf) d2(slot, D2_ORPHAN, -1); // this shard counted it NotExist; it is Valid / TimedOut
+        auto filtered = [&]() { if (kept && (g & PV_D2G_COUNTERS)) add[{slot, PV_OFF_DNS + DC_FILTERED}] += 1; };
+        if (rf) { if (!timed_out && !qf) filtered(); continue; }
+        if (qf) { filtered(); continue; }
+        if (timed_out) { if (kept) d2(slot, D2_TIMEOUT, 1); continue; }
+        const uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
+        const PvXValue tv{us, 0, (uint32_t)XV2_TIME + xd};
+        if (!(r.period & 0x80)) { // a period outside the window then: its time feeds the next p90 only
+            if (g & PV_D2G_XACT_TIMES) c->slow_xv.push_back({st.ord, tv});
+            continue;
+        }
+        if ((g & PV_D2G_XACT_TIMES) && rdeep) c->slow_xv.push_back({st.ord, tv});
+        if (!win) continue; // its bucket has left the window since
+        if ((g & PV_D2G_XACT_TIMES) && rdeep && st.cand >= 0) {
+            pv_ctx::SlowCand sc = c->sorph[(size_t)st.cand];
+            sc.us = us;
+            sc.dir = (uint8_t)(4 + xd);
+            c->scands.push_back(sc);
+        }
+        if (st.cand < 0) return c->fail(PV_EINVAL, "shard-edge response without its record");
+        pairs.push_back(PvEdgePair{qe, r, qaddr, st.order, us});
+        pair_stub.push_back(it->second);
+    }
+    for (auto &kv : add)
+        if (int rc = add_sum_word(c, kv.first.first, kv.first.second, kv.second)) return rc;
+    // the edge pairs on the device, by groups of at most PV_MAX_SHIFTS + 1 periods (the edge
+    // run's period table)
+    std::vector<uint64_t> ords;
+    for (size_t i : pair_stub) ords.push_back(c->stubs[i].ord);
+    std::sort(ords.begin(), ords.end());
+    ords.erase(std::unique(ords.begin(), ords.end()), ords.end());
+    hipError_t e;
+    for (size_t g0 = 0; g0 < ords.size(); g0 += PV_MAX_SHIFTS + 1) {
+        const size_t g1 = std::min(ords.size(), g0 + PV_MAX_SHIFTS + 1);
+        std::vector<uint8_t> blob[2];
+        std::vector<uint32_t> offs[2];
+        std::vector<PvEdgePair> run;
+        for (size_t i = 0; i < pairs.size(); i++) {
+            const pv_ctx::EdgeStub &st = c->stubs[pair_stub[i]];
+            auto itp = std::find(ords.begin() + g0, ords.begin() + g1, st.ord);
+            if (itp == ords.begin() + g1) continue;
+            const pv_ctx::SlowCand &sc = c->sorph[(size_t)st.cand];
+            const uint8_t *rec = c->sstore.data() + sc.off;
+            uint32_t cap;
+            memcpy(&cap, rec + 8, 4);
+            const uint32_t sz = (16 + cap + 3) & ~3u;
+            offs[sc.tcp].push_back((uint32_t)blob[sc.tcp].size());
+            blob[sc.tcp].insert(blob[sc.tcp].end(), rec, rec + sz);
+            PvEdgePair pp = pairs[i];
+            pp.r.idx = (uint32_t)(offs[sc.tcp].size() - 1) | (sc.tcp ? PV_TCP_IDX : 0u);
+            pp.r.period = (uint8_t)(itp - (ords.begin() + g0));
+            run.push_back(pp);
+        }
+        if (run.empty()) continue;
+        for (int k = 0; k < 2; k++) blob[k].resize(blob[k].size() + PV_RECS_PAD, 0);
+        void *d[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+        struct Free { void **p; ~Free() { for (int i = 0; i < 7; i++) if (p[i]) hipFree(p[i]); } } fr{d};
+        for (int k = 0; k < 2; k++) {
+            if (!hip_ok(e = hipMalloc(&d[2 * k], blob[k].size())) || !hip_ok(e = hipMalloc(&d[2 * k + 1], (offs[k].size() + 1) * 4)) ||
+                !hip_ok(e = hipMalloc(&d[4 + k], offs[k].size() + 1)) ||
+                !hip_ok(e = hipMemcpy(d[2 * k], blob[k].data(), blob[k].size(), hipMemcpyHostToDevice)) ||
+                (!offs[k].empty() && !hip_ok(e = hipMemcpy(d[2 * k + 1], offs[k].data(), offs[k].size() * 4, hipMemcpyHostToDevice))))
+                return c->hipfail(e, "edge pairs");
+        }
+        if (!hip_ok(e = hipMalloc(&d[6], run.size() * sizeof(PvEdgePair))) ||
+            !hip_ok(e = hipMemcpy(d[6], run.data(), run.size() * sizeof(PvEdgePair), hipMemcpyHostToDevice)))
+            return c->hipfail(e, "edge pairs");
+        PvParams P;
+        params_common(c, P, (const uint8_t *)d[0], (const uint32_t *)d[1], offs[0].size());
+        P.sum = c->d_sum;
+        P.cpc = c->d_cpc;
+        P.tkeys = c->d_tkeys;
+        P.tcnt = c->d_tcnt;
+        P.taux = c->d_taux;
+        P.tcap_log2 = c->tcap_log2;
+        P.reg_log2 = c->reg_log2;
+        P.arena = c->d_arena;
+        P.arena_top = c->d_arena_top;
+        P.arena_cap = c->arena_cap;
+        P.tab_live = c->d_tab_live;
+        P.flags = c->d_status + ST_FLAGS;
+        P.sfx_of = (uint8_t *)d[4];
+        P.n_dshift = (uint32_t)(g1 - g0 - 1);
+        PvXactParams X;
+        memset(&X, 0, sizeof X); // thresholds 0: the slow candidates are the host's (scands)
+        for (size_t j = g0; j < g1; j++) {
+            const uint32_t k = (uint32_t)(j - g0), slot = slot_of(ords[j]);
+            P.dslot_of[k] = slot;
+            X.slot_gen[k] = slot | (c->gen[slot] << 8);
+            c->dns.clean[slot] = false;
+        }
+        X.P = P;
+        X.vals = c->d_xvals;
+        X.n_vals = c->d_nvals;
+        X.vals_cap = (uint32_t)(c->max_records * 2);
+        X.valid = c->d_valid;
+        X.n_valid = c->d_nvals + 1;
+        X.trecs = (const uint8_t *)d[2];
+        X.toffs = (const uint32_t *)d[3];
+        X.tsfx = (const uint8_t *)d[5];
+        flush_fills(c);
+        *c->h_xparams = X;
+        if (!hip_ok(e = hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, c->stream)))
+            return c->hipfail(e, "edge pairs");
+        hipLaunchKernelGGL(pv_xact_edge2, dim3((uint32_t)((run.size() + 255) / 256)), dim3(256), 0, c->stream,
+                           (const PvXactParams *)c->d_xparams, (const PvEdgePair *)d[6], (uint32_t)run.size(), (uint8_t *)d[4],
+                           (uint8_t *)d[5]);
+        if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipStreamSynchronize(c->stream))) return c->hipfail(e, "pv_xact_edge2");
+    }
+    uint32_t flags = 0;
+    if (!hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
+    if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "top-N table full: raise table_log2");
+    // this shard's own open queries (the carried list, latest event per key) with their ECS words
+    if (c->n_pend) {
+        std::vector<PvXEvent> pend;
+        std::vector<uint64_t> pk, pe;
+        if (int rc = read_carried(c, pend, pk, &pe)) return rc;
+        std::unordered_map<uint64_t, size_t> last;
+        last.reserve(pend.size() * 2);
+        for (size_t i = 0; i < pend.size(); i++) {
+            auto it = last.find(pend[i].key);
+            if (it == last.end() || (uint32_t)pk[i] >= (uint32_t)pk[it->second]) last[pend[i].key] = i;
+        }
+        for (auto &kv : last) { keep.push_back(pend[kv.second]); keep_ecs.push_back(pe[kv.second]); }
+    }
+    *out_bytes = keep.size() * esz;
+    *out = (uint8_t *)malloc(*out_bytes ? *out_bytes : 1);
+    if (!*out) return c->fail(PV_ECAPACITY, "out of host memory");
+    for (size_t i = 0; i < keep.size(); i++) {
+        memcpy(*out + i * esz, &keep[i], sizeof(PvXEvent));
+        if (ecs) memcpy(*out + i * esz + sizeof(PvXEvent), &keep_ecs[i], 8);
+    }
+    return 0;
+}
 } // namespace
 
 int pv_edge_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
@@ -5481,12 +5752,10 @@ int pv_edge_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
     if (!hip_ok(e = hipMemcpy(nv, c->d_nvals, 16, hipMemcpyDeviceToHost))) return c->hipfail(e, "edge counts");
     if (nv[3] > c->orph_cap) return c->fail(PV_ECAPACITY, "%u shard-edge responses exceed the stub capacity", nv[3]);
     // open queries: the carried list, latest event per key (rank order in the sort keys)
-    std::vector<PvXEvent> pend(c->n_pend), open;
-    std::vector<uint64_t> pk(c->n_pend);
+    std::vector<PvXEvent> pend, open;
+    std::vector<uint64_t> pk;
+    if (int rc = read_carried(c, pend, pk)) return rc;
     if (c->n_pend) {
-        if (!hip_ok(e = hipMemcpy(pend.data(), c->d_pend[c->pend_cur], c->n_pend * sizeof(PvXEvent), hipMemcpyDeviceToHost)) ||
-            !hip_ok(e = hipMemcpy(pk.data(), c->d_pkeys[c->pend_cur], c->n_pend * 8, hipMemcpyDeviceToHost)))
-            return c->hipfail(e, "open queries");
         std::unordered_map<uint64_t, size_t> last;
         last.reserve(pend.size() * 2);
         for (size_t i = 0; i < pend.size(); i++) {
@@ -5521,6 +5790,8 @@ int pv_edge_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
 
 int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks, uint32_t me)
 {
+    if (c->dns2_groups)
+        return c->fail(PV_EUNSUPPORTED, "DNS v2 shard edges go rank by rank: pv_set_slow_defer, then pv_edge_carry");
     if (c->slow_defer) {
         // this rank's own transaction times end here (the edge pairs' follow)
         if (int rc = sync_xvals(c)) return rc;
@@ -5619,13 +5890,14 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
     *out = nullptr;
     *out_bytes = 0;
     if (!c->slow_defer) return c->fail(PV_EINVAL, "pv_edge_carry needs pv_set_slow_defer");
-    if (in_bytes % sizeof(PvXEvent)) return c->fail(PV_EINVAL, "malformed open-query buffer");
+    if (!c->dns2_groups && in_bytes % sizeof(PvXEvent)) return c->fail(PV_EINVAL, "malformed open-query buffer");
     if (int rc = sync_xvals(c)) return rc;
     if (c->xv_local_end == SIZE_MAX) c->xv_local_end = c->xvals_host.size();
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return c->hipfail(e, "synchronize");
+    if (c->dns2_groups) return edge_carry2(c, in, in_bytes, out, out_bytes);
     std::unordered_map<uint64_t, size_t> first;
     first.reserve(c->stubs.size() * 2);
     for (size_t i = 0; i < c->stubs.size(); i++) first.emplace(c->stubs[i].e.key, i);
@@ -5694,11 +5966,9 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
     }
     // this shard's own open queries (the carried list, latest event per key)
     if (c->n_pend) {
-        std::vector<PvXEvent> pend(c->n_pend);
-        std::vector<uint64_t> pk(c->n_pend);
-        if (!hip_ok(e = hipMemcpy(pend.data(), c->d_pend[c->pend_cur], c->n_pend * sizeof(PvXEvent), hipMemcpyDeviceToHost)) ||
-            !hip_ok(e = hipMemcpy(pk.data(), c->d_pkeys[c->pend_cur], c->n_pend * 8, hipMemcpyDeviceToHost)))
-            return c->hipfail(e, "open queries");
+        std::vector<PvXEvent> pend;
+        std::vector<uint64_t> pk;
+        if (int rc = read_carried(c, pend, pk)) return rc;
         std::unordered_map<uint64_t, size_t> last;
         last.reserve(pend.size() * 2);
         for (size_t i = 0; i < pend.size(); i++) {
@@ -5717,15 +5987,20 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
 int pv_set_slow_defer(pv_ctx *c, int defer)
 {
     std::lock_guard<std::mutex> g(c->mu);
-    if (defer && c->dns2_groups) return c->fail(PV_EUNSUPPORTED, "sharded top_slow with the DNS v2 handler is not built");
     if (c->records_seen) return c->fail(PV_EINVAL, "set the slow-transaction mode before the first batch");
+    if (defer && c->dns2_groups && !c->d_orph_ord) {
+        // DNS v2 stubs carry their first-occurrence order (an edge pair's qname CPC order)
+        hipSetDevice(c->device);
+        hipError_t e;
+        if (!hip_ok(e = hipMalloc(&c->d_orph_ord, (size_t)c->orph_cap * 8))) return c->hipfail(e, "stub orders");
+    }
     c->slow_defer = defer != 0;
     return 0;
 }
 
 // This rank's own transaction times per DNS period ordinal: (ordinal u32, kind u32, value u64)
-// records of kinds XV_FROM_US / XV_TO_US. Call before pv_values_merge (which appends the other
-// ranks' values).
+// records of kinds XV_FROM_US / XV_TO_US (DNS v2: XV2_TIME + transaction direction). Call before
+// pv_values_merge (which appends the other ranks' values).
 int pv_slow_values_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
 {
     std::lock_guard<std::mutex> g(c->mu);
@@ -5742,7 +6017,7 @@ int pv_slow_values_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
     const size_t nloc = std::min(c->xv_local_end, c->xvals_host.size());
     for (size_t i = 0; i < nloc; i++) {
         const PvXValue &v = c->xvals_host[i];
-        if (v.kind != XV_FROM_US && v.kind != XV_TO_US) continue;
+        if (v.kind != XV_FROM_US && v.kind != XV_TO_US && (v.kind < XV2_TIME || v.kind >= XV2_TIME + 3)) continue;
         auto it = c->sg_ord.find(v.slot);
         if (it != c->sg_ord.end()) put((uint32_t)it->second, v);
     }
@@ -5764,10 +6039,16 @@ int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, u
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
     if (!c->slow_defer) return c->fail(PV_EINVAL, "pv_slow_finish without pv_set_slow_defer");
-    // thresholds come from the quantile sketches: none without the quantiles group
-    if (!c->started || !(c->dns_groups & PV_DNS_QUANTILES) || !(c->dns_groups & PV_DNS_TRANSACTIONS)) return 0;
-    // merged values per ordinal
-    std::map<uint64_t, std::vector<uint64_t>> vals[2];
+    // thresholds come from the quantile sketches: none without the quantiles group (v1) or the
+    // transaction-times group (DNS v2, per transaction direction)
+    const bool v2 = c->dns2_groups != 0;
+    if (!c->started) return 0;
+    if (v2 ? !(c->dns2_groups & PV_DNS2_XACT_TIMES)
+           : (!(c->dns_groups & PV_DNS_QUANTILES) || !(c->dns_groups & PV_DNS_TRANSACTIONS)))
+        return 0;
+    // merged values per ordinal: [0] from, [1] to (v1); [2 + d] DNS v2 direction d
+    constexpr int NK = 5;
+    std::map<uint64_t, std::vector<uint64_t>> vals[NK];
     for (uint32_t r = 0; r < nranks; r++) {
         if (sizes[r] % 16) return c->fail(PV_EINVAL, "malformed slow-value buffer of rank %u", r);
         for (size_t p = 0; p < sizes[r]; p += 16) {
@@ -5777,12 +6058,13 @@ int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, u
             memcpy(&kind, bufs[r] + p + 4, 4);
             memcpy(&bits, bufs[r] + p + 8, 8);
             if (kind == XV_FROM_US || kind == XV_TO_US) vals[kind == XV_TO_US][ord].push_back(bits);
+            else if (kind >= XV2_TIME && kind < XV2_TIME + 3) vals[2 + kind - XV2_TIME][ord].push_back(bits);
         }
     }
     // thresholds of every ordinal up to the live one
     const uint64_t live = c->dns.ordinal;
-    std::vector<float> thr[2];
-    for (int k = 0; k < 2; k++) {
+    std::vector<float> thr[NK];
+    for (int k = 0; k < NK; k++) {
         thr[k].assign(live + 1, 0.0f);
         float t = 0.0f;
         for (uint64_t o = 1; o <= live; o++) {
@@ -5797,7 +6079,8 @@ int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, u
     std::vector<pv_ctx::SlowCand> sel;
     for (auto &sc : c->scands) {
         if (!win.count(sc.ord) || sc.ord > live) continue;
-        const float t = thr[sc.dir == 1][sc.ord]; // dir 0 (toHost): from; 1 (fromHost): to
+        // v1 dir 0 (toHost): from, 1 (fromHost): to; DNS v2 4 + transaction direction
+        const float t = sc.dir >= 4 ? thr[2 + sc.dir - 4][sc.ord] : thr[sc.dir == 1][sc.ord];
         if (t > 0.0f && (float)sc.us >= t) sel.push_back(sc);
     }
     if (sel.empty()) return 0;
@@ -5867,6 +6150,7 @@ int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, u
             P.dslot_of[k] = win[ords[j]];
             X.thr_from[k] = thr[0][ords[j]];
             X.thr_to[k] = thr[1][ords[j]];
+            for (int d = 0; d < 3; d++) X.thr2[k][d] = thr[2 + d][ords[j]];
             c->dns.clean[P.dslot_of[k]] = false;
         }
         X.P = P;

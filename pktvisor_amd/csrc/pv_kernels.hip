@@ -447,9 +447,12 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
 #define PV_CACHE_PROBES 4 // slots a key may probe before it goes to the update log
 #endif
 #define PV_LKEY(slot, lm, payload) (((uint64_t)(slot) << 60) | ((uint64_t)(lm) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
+#ifndef PV_CACHE_BUCKET
+#define PV_CACHE_BUCKET 0 // 1: a key probes the aligned 4-entry bucket of its hash, read with two 16-B loads
+#endif
 template <int N>
 struct KeyCache {
-    uint64_t key[N];
+    alignas(16) uint64_t key[N];
     uint32_t cnt[N];
     uint32_t rep[N];
     __device__ __forceinline__ void clear()
@@ -460,6 +463,28 @@ struct KeyCache {
     // entry's smallest record index before this call (0xffffffff if new)
     __device__ __forceinline__ bool add(uint64_t k, uint32_t w, uint32_t idx, uint32_t &first)
     {
+#if PV_CACHE_BUCKET
+        // one LDS round trip for the whole probe window (a miss used to cost four dependent reads)
+        const uint32_t b = (uint32_t)(fmix64(k) >> 32) & (N - 4);
+        const uint4 *kp = reinterpret_cast<const uint4 *>(&key[b]);
+        const uint4 lo = kp[0], hi = kp[1];
+        uint64_t cur4[4] = {(uint64_t)lo.x | ((uint64_t)lo.y << 32), (uint64_t)lo.z | ((uint64_t)lo.w << 32),
+                            (uint64_t)hi.x | ((uint64_t)hi.y << 32), (uint64_t)hi.z | ((uint64_t)hi.w << 32)};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            uint64_t cur = cur4[j];
+            if (cur == 0) {
+                const uint64_t prev = atomicCAS((unsigned long long *)&key[b + j], 0ull, (unsigned long long)k);
+                cur = prev == 0 ? k : prev;
+            }
+            if (cur == k) {
+                if (w) atomicAdd(&cnt[b + j], w);
+                first = atomicMin(&rep[b + j], idx);
+                return true;
+            }
+        }
+        return false;
+#endif
         uint32_t h = (uint32_t)(fmix64(k) >> 32) & (N - 1);
         for (int probe = 0; probe < PV_CACHE_PROBES; probe++) {
             uint64_t cur = key[h];
@@ -804,7 +829,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     // the message's transaction event (filtered: a DNS v2 event its filters rejected, which
     // still opens or ends a transaction, DnsMetricsManager::process_filtered, dns/v2 ...cpp:1147-1174)
     auto emit = [&](bool deep, bool filtered, uint32_t efam, uint64_t eaddr) {
-        if (!P.want_events || TAP) return;
+        if (!P.want_events || TAP || (P.dbg & 1024)) return; // 1024: profiling knob, no events
         // the workgroup's event region; LDS counter, order irrelevant (sorted by key, index)
         const uint64_t e = ebase + atomicAdd(nev, 1u);
         if (qr) atomicAdd(nresp, 1u);
@@ -831,7 +856,16 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             if (efam) P.eecs[e] = eaddr;
         }
         P.events[e] = ev;
-        P.ekeys[e] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
+        const uint64_t sk = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
+        if constexpr (!TCP && !TAP) {
+            // the UDP pass: straight into the batch's key list at the range's reserved slots
+            // (nev[1]: one per DNS message of the range; pv_xact_compact's work for these ranges)
+            const uint64_t ks = (uint64_t)nev[1] + (e - ebase);
+            P.skeys[ks] = sk;
+            P.svals[ks] = (uint32_t)e;
+        } else {
+            P.ekeys[e] = sk;
+        }
     };
     if (FILT && (P.f_flags & PVDF_V2) && !TAP) {
         // DnsStreamHandler::_filtering, DNS v2 (dns/v2/DnsStreamHandler.cpp:484-609): the
@@ -924,7 +958,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
     auto top = [&](uint32_t metric, uint64_t payload, uint32_t w) {
         const uint64_t key = PV_KEY(metric, payload);
         if (P.dbg & 32) return; // profiling knob: no table updates
-        if (cache) {
+        if (cache && !(P.dbg & 256)) { // 256: profiling knob, no LDS key cache
             uint32_t first;
             if (cache->add(PV_LKEY(slot, metric, payload), w, i, first)) return;
             if (metric >= TM_DENSE_PORT) sum_add(P, slot, dense_word(metric, payload), w);
@@ -981,7 +1015,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                 if (d.name_len_enc > 0 && !(P.dbg & 16)) name_stats(R, m, dlen, 12, st);
                 uint64_t h1, h2;
                 st.mm.finish(h1, h2);
-                if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT)) {
+                if (st.n > 0 && (P.dns_groups & PV_DNS_CARDINALITY_BIT) && !(P.dbg & 512)) { // 512: knob, no qname CPC
                     const uint32_t coupon = cpc_coupon(h1, h2);
                     uint32_t first = 0xffffffffu;
                     // same name => same coupon: skip when a smaller record index already submitted it
@@ -1071,7 +1105,8 @@ struct DnsState {
     uint32_t stage[PV_DNS_WAVES][PV_WSTAGE / 4];
     KeyCache<PV_NCACHE> C;
     uint32_t mq_n[2]; // the range's update-log count, the range
-    uint32_t nev, nresp;
+    uint32_t nev[2];  // the range's event count, its first slot in the batch's key list
+    uint32_t nresp;
 };
 
 // Adds one to bin v for every lane with v != PV_NOH: bins below PV_HBINS in the LDS
@@ -2895,9 +2930,15 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
     c.zero();
     uint32_t wslot = 0xffffffffu;
     for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
-        if (threadIdx.x == 0) { S.mq_n[0] = P.mq_cnt[lb]; S.mq_n[1] = lb; S.nev = 0; }
-        __syncthreads();
         const uint32_t nd = P.dq_cnt[lb];
+        if (threadIdx.x == 0) {
+            S.mq_n[0] = P.mq_cnt[lb];
+            S.mq_n[1] = lb;
+            S.nev[0] = 0;
+            // the range's slots in the key list: at most one event per message
+            if (P.want_events && nd) S.nev[1] = atomicAdd(P.n_keys, nd);
+        }
+        __syncthreads();
         const uint64_t region = (uint64_t)lb * P.wt_per_block * PV_WT;
         const PV_G DnsMsg *Q = reinterpret_cast<const PV_G DnsMsg *>(P.dq) + region;
         const uint32_t ntl = (nd + PV_WT - 1) / PV_WT;
@@ -2948,7 +2989,7 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
             if (active) {
                 const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
                 const bool own = P.dslot_of[dm.period] == wslot;
-                dns_process<false, false, SFX, FILT>(P, &S.C, S.mq_n, &S.nev, &S.nresp, region, R, dm, own, c);
+                dns_process<false, false, SFX, FILT>(P, &S.C, S.mq_n, S.nev, &S.nresp, region, R, dm, own, c);
             }
         }
         __syncthreads();
@@ -2956,10 +2997,17 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
             cache_flush(P, S.C, PV_NCACHE, S.mq_n);
             __syncthreads();
         }
-        if (threadIdx.x == 0) {
-            P.mq_cnt[lb] = S.mq_n[0];
-            P.blk_events[lb] = S.nev;
+        if (P.want_events) {
+            // messages without an event leave their reserved key slots as sentinels (all ones:
+            // sorted behind every event key, whose top bit is clear)
+            const uint32_t ne = S.nev[0];
+            for (uint32_t j = ne + threadIdx.x; j < nd; j += blockDim.x) {
+                P.skeys[(uint64_t)S.nev[1] + j] = ~0ull;
+                P.svals[(uint64_t)S.nev[1] + j] = 0;
+            }
+            if (threadIdx.x == 0 && ne) atomicAdd(P.n_events, ne);
         }
+        if (threadIdx.x == 0) P.mq_cnt[lb] = S.mq_n[0];
     }
     if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
     if (threadIdx.x == 0 && S.nresp) atomicAdd(P.n_events + 1, S.nresp);
@@ -4201,25 +4249,30 @@ __device__ void dnstap_event(PV_CREF(PvParams) P, uint32_t j, uint32_t *nev, uin
     }
 }
 
-// Packs the per-workgroup event regions into one dense run and writes the total to
-// n_events[0] (region order is irrelevant: events are sorted by (key, index)).
-extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint32_t nblk)
+// Packs the event regions of workgroups b0 .. b0 + gridDim.x - 1 (the TCP pass's, dnstap's; the
+// UDP DNS pass writes its keys in place) into one dense run of the key list from kbase, adding
+// their total to n_events[0] and setting the key list's length n_keys (region order is
+// irrelevant: events are sorted by (key, index)).
+extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint32_t b0, uint32_t kbase)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ uint32_t part[4];
     // this block's base: the events of all earlier blocks, summed by the whole block
     uint32_t b = 0;
-    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += blockDim.x) b += P.blk_events[j];
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += blockDim.x) b += P.blk_events[b0 + j];
     b = wave_sum(b);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = b;
     __syncthreads();
     const uint32_t base = part[0] + part[1] + part[2] + part[3];
-    const uint32_t cnt = P.blk_events[blockIdx.x];
-    if (threadIdx.x == 0 && blockIdx.x == nblk - 1) P.n_events[0] = base + cnt;
-    const uint64_t src = (uint64_t)blockIdx.x * P.wt_per_block * PV_WT;
+    const uint32_t cnt = P.blk_events[b0 + blockIdx.x];
+    if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
+        if (base + cnt) atomicAdd(P.n_events, base + cnt);
+        *P.n_keys = kbase + base + cnt;
+    }
+    const uint64_t src = (uint64_t)(b0 + blockIdx.x) * P.wt_per_block * PV_WT;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-        P.skeys[base + j] = P.ekeys[src + j];
-        P.svals[base + j] = (uint32_t)(src + j);
+        P.skeys[kbase + base + j] = P.ekeys[src + j];
+        P.svals[kbase + base + j] = (uint32_t)(src + j);
     }
 }
 
@@ -4541,6 +4594,19 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
     }
 }
 
+// A DNS v2 shard-edge stub (sharded runs, X.orph_ord set): the first event of its key in this
+// context's stream, kept whole (pad intact: the edge pair's accounting reads it) with the kept
+// flag in period bit 7, and its first-occurrence order
+__device__ __forceinline__ void stub2(PV_CREF(PvXactParams) X, const PvXEvent &e, uint32_t p, bool kept)
+{
+    PV_CREF(PvParams) P = X.P;
+    const uint32_t k = atomicAdd(X.n_orph, 1u);
+    if (k >= X.orph_cap) return;
+    PvXEvent o = e;
+    o.period = (uint8_t)(e.period | (kept ? 0x80u : 0u));
+    X.orph[k] = o;
+    X.orph_ord[k] = (int64_t)((P.gbase << 2) + ((uint32_t)X.skeys[p] - (P.ekey_base << 2)));
+}
 // TransactionManager per direction, DNS v2 (dns/v2/DnsStreamHandler.cpp:1100-1145 and the
 // manager's on_period_shift, .h:440-453): a response of transaction direction xd is
 // Valid, TimedOut or NotExist (orphan) against the latest event of its key (the key holds
@@ -4559,7 +4625,9 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         int q = (int)p - 1;
         for (; q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h; q--)
             if (xev(X, q).key == e.key) break;
-        const bool found = q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h && !xev(X, q).qr;
+        const bool first = q < 0 || (uint32_t)(X.skeys[q] >> 32) != h;
+        if (first && X.orph_ord) stub2(X, e, p, kept); // may answer a query an earlier shard left open
+        const bool found = !first && !xev(X, q).qr;
         const PvXEvent qe = found ? xev(X, q) : e;
         const uint32_t kp = found ? purge_period(P, X.ttl_s, qe.period, qe.sec) : 0u;
         const bool rf = e.pad & 4, qf = found && (qe.pad & 4); // filtered response / query (v2 filters)
@@ -4586,6 +4654,13 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         const int64_t order = (int64_t)((P.gbase << 2) + ((uint32_t)X.skeys[p] - (P.ekey_base << 2)));
         dns2_xact(X, T, e, qe, xd, us, order, ((qe.pad >> 3) & 3) ? xecs(X, q) : 0ull);
     } else {
+        if (X.orph_ord && X.edge_h && e.sec < X.edge_h) {
+            // sharded runs: the first query of its key may overwrite an open query of an earlier shard
+            int q = (int)p - 1;
+            for (; q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h; q--)
+                if (xev(X, q).key == e.key) break;
+            if (q < 0 || (uint32_t)(X.skeys[q] >> 32) != h) stub2(X, e, p, e.period >= P.dskip_before);
+        }
         const uint32_t kp = purge_period(P, X.ttl_s, e.period, e.sec);
         if (!kp) return;
         uint32_t q = p + 1;
@@ -4598,21 +4673,18 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
     }
 }
 
-extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvXactParams *__restrict__ Xp)
+__device__ __forceinline__ void xstate_init(XState &T)
 {
-    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
-    PV_CREF(PvParams) P = X.P;
-    __shared__ XState T;
     for (uint32_t j = threadIdx.x; j < (PV_MAX_SHIFTS + 1) * XC_N; j += blockDim.x) (&T.ctr[0][0])[j] = 0;
     for (uint32_t j = threadIdx.x; j < (PV_MAX_SHIFTS + 1) * 3 * D2_N; j += blockDim.x) (&T.c2[0][0][0])[j] = 0;
     if (threadIdx.x == 0) { T.nval = 0; T.nvalid = 0; }
     __syncthreads();
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < X.n) {
-        if (P.dns2_groups) resolve_one2(X, T, p);
-        else resolve_one(X, T, p);
-    }
-    __syncthreads();
+}
+// the block's transaction counters into the periods' buckets, its values and deferred slow
+// candidates appended to the context's lists (after a __syncthreads)
+__device__ __forceinline__ void xstate_flush(PV_CREF(PvXactParams) X, XState &T)
+{
+    PV_CREF(PvParams) P = X.P;
     if (P.dns2_groups)
         for (uint32_t j = threadIdx.x; j < (P.n_dshift + 1) * 3 * D2_N; j += blockDim.x) {
             const uint32_t per = j / (3 * D2_N), w = j % (3 * D2_N);
@@ -4640,6 +4712,59 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvX
     for (uint32_t j = threadIdx.x; j < T.nvalid; j += blockDim.x) X.valid[T.dbase + j] = T.valid[j];
 }
 
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvXactParams *__restrict__ Xp)
+{
+    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
+    PV_CREF(PvParams) P = X.P;
+    __shared__ XState T;
+    xstate_init(T);
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < X.n) {
+        if (P.dns2_groups) resolve_one2(X, T, p);
+        else resolve_one(X, T, p);
+    }
+    __syncthreads();
+    xstate_flush(X, T);
+}
+
+// DNS v2 transactions across a shard edge (pv_edge_carry): each pair as resolve_one2 accounts a
+// valid, kept transaction (dns2_xact), the response's record in the run's blobs (P.recs / offs,
+// TCP message records X.trecs / toffs), its period r.period of the run's table. With
+// public_suffix_list the response's suffix size is matched here first (pv_dns_suffix's rule).
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_edge2(const PvXactParams *__restrict__ Xp,
+                                                                     const PvEdgePair *__restrict__ pairs, uint32_t n,
+                                                                     uint8_t *sfx, uint8_t *tsfx)
+{
+    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
+    PV_CREF(PvParams) P = X.P;
+    __shared__ XState T;
+    xstate_init(T);
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) {
+        const PvEdgePair e = pairs[p];
+        const uint32_t xd = (uint32_t)((e.r.key >> 48) & 3) - 1;
+        if ((P.f_flags & PVDF_PSL) && !(P.f_flags & PVDF_ONLY_QSUFFIX)) {
+            const bool tcp = e.r.idx & PV_TCP_IDX;
+            const uint32_t idx = e.r.idx & ~PV_TCP_IDX;
+            const GAcc R{tcp ? X.trecs : P.recs};
+            Parsed o;
+            if (tcp) {
+                ParseCfg C = parse_cfg(P);
+                C.linktype = 101;
+                parse_record(R, C, P, X.toffs[idx], o);
+            } else {
+                parse_record(R, P, P.offs[idx], o);
+            }
+            const uint64_t m = o.l4off + 8;
+            (tcp ? tsfx : sfx)[idx] = (uint8_t)dns_suffix_of(P, R, m, e.r.len, be16(R, m + 4), be16(R, m + 6), be16(R, m + 8),
+                                                             be16(R, m + 10));
+        }
+        if (xd < 3) dns2_xact(X, T, e.r, e.q, xd, e.us, e.order, e.qaddr);
+    }
+    __syncthreads();
+    xstate_flush(X, T);
+}
+
 // Queries still open after this batch (the latest event of their (flow, txid) is a query
 // not purged by a period shift here) move to the carried list for the next batch, as
 // period 0 with sort rank 0: TransactionManager's map surviving the batch edge.
@@ -4658,27 +4783,43 @@ extern "C" __global__ void pv_xact_carry(const PvXactParams *__restrict__ Xp)
     X.pend_out[k] = e;
     if (X.pecs_out) X.pecs_out[k] = ((e.pad >> 3) & 3) ? xecs(X, p) : 0ull;
     X.pkeys_out[k] = (uint64_t)h << 32;
+    X.pvals_out[k] = k;
 }
 // A batch with queries only and no period shift pairs nothing: its events join the
-// carried list unresolved, in rank order behind the earlier ones.
+// carried list unresolved. With nothing carried the host hands the batch's event store, keys
+// and values over to the carried list as they lie (no copy); otherwise this kernel appends them
+// (the key list's sentinel slots left out): keys at `at`, events densely at `ehi` of the store,
+// in the order of a wave-aggregated counter (ctr, zero at launch).
 extern "C" __global__ void pv_xact_defer(const uint64_t *skeys, const uint32_t *svals, const PvXEvent *events, uint32_t n,
-                                         PvXEvent *pend, uint64_t *pkeys, uint32_t at, const uint64_t *eecs, uint64_t *pecs)
+                                         PvXEvent *pend, uint64_t *pkeys, uint32_t *pvals, uint32_t at, uint32_t ehi,
+                                         const uint64_t *eecs, uint64_t *pecs, uint32_t *ctr)
 {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+    const uint64_t k = j < n ? skeys[j] : ~0ull;
+    const bool ok = k != ~0ull;
+    const uint64_t m = __ballot(ok);
+    if (!m) return;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader, 64);
+    if (!ok) return;
+    const uint32_t q = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
     const uint32_t v = svals[j];
-    pend[at + j] = events[v];
-    pkeys[at + j] = skeys[j];
-    if (pecs) pecs[at + j] = ((events[v].pad >> 3) & 3) ? eecs[v] : 0ull;
+    const PvXEvent ev = events[v];
+    pend[ehi + q] = ev;
+    pkeys[at + q] = k;
+    pvals[at + q] = ehi + q;
+    if (pecs) pecs[ehi + q] = ((ev.pad >> 3) & 3) ? eecs[v] : 0ull;
 }
 // the carried list's keys behind this batch's compacted keys, values flagged
-extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, uint32_t n_pend,
-                                           uint32_t at)
+extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, const uint64_t *pkeys, const uint32_t *pvals,
+                                           uint32_t n_pend, uint32_t at)
 {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_pend) return;
     skeys[at + j] = pkeys[j];
-    svals[at + j] = PV_PEND_FLAG | j;
+    svals[at + j] = PV_PEND_FLAG | pvals[j];
 }
 
 // top_slow for transactions of periods whose threshold became known after the resolve

@@ -375,7 +375,8 @@ struct PvParams {
     PV_G uint32_t *blk_events; // events appended by each workgroup
     PV_G uint64_t *skeys;      // packed keys (sort input)
     PV_G uint32_t *svals;      // packed event slot positions (sort input)
-    PV_G uint32_t *n_events;   // [0] packed total (pv_xact_compact), [1] responses
+    PV_G uint32_t *n_events;   // [0] events of the batch, [1] responses
+    PV_G uint32_t *n_keys;     // length of the batch's key list skeys / svals (events + sentinel slots)
     uint32_t want_events;
     uint32_t ekey_base;        // sort rank of the batch's first record (open queries carried in have rank 0)
     uint32_t wt_per_block; // 64-record wave tiles per workgroup (contiguous record range)
@@ -478,13 +479,16 @@ struct PvXactParams {
     PV_G PvXValid *valid;
     PV_G uint32_t *n_valid;
     // DNS queries still open from earlier batches (TransactionManager's map carried across
-    // batches): sorted-key values with PV_PEND_FLAG index `pend`; pv_xact_carry writes the
-    // queries still open after this batch to pend_out / pkeys_out, counting n_pend_out
+    // batches): sorted-key values with PV_PEND_FLAG index the event store `pend` (a query-only
+    // batch's own event regions become the store as they lie, so it may be sparse); pv_xact_carry
+    // writes the queries still open after this batch densely to pend_out / pkeys_out /
+    // pvals_out, counting n_pend_out
     const PV_G PvXEvent *pend;
     PV_G PvXEvent *pend_out;
     const PV_G uint64_t *pecs; // DNS v2 top_ecs: ECS addresses of the carried queries (pend), and of pend_out
     PV_G uint64_t *pecs_out;
     PV_G uint64_t *pkeys_out;
+    PV_G uint32_t *pvals_out;
     PV_G uint32_t *n_pend_out;
     // shard-edge stubs: responses that are the first event of their (flow, txid) in this
     // context's whole stream ("orphans"; they may answer a query open at the end of the
@@ -492,6 +496,9 @@ struct PvXactParams {
     PV_G PvXEvent *orph;
     PV_G uint32_t *n_orph;
     uint32_t orph_cap;
+    // DNS v2 stubs: the first-occurrence order of each (a response's qname CPC order when it
+    // becomes an edge pair), next to orph; null in v1 runs
+    PV_G int64_t *orph_ord;
     // TCP message records (events whose idx carries PV_TCP_IDX) and their suffix sizes
     // (public_suffix_list, DNS v2)
     const PV_G uint8_t *trecs;
@@ -505,6 +512,15 @@ struct PvXactParams {
     int64_t edge_h;
 };
 #define PV_PEND_FLAG 0x80000000u
+// A DNS v2 transaction across a shard edge (pv_edge_carry): a query an earlier shard left open
+// and the response that is the first event of its key in this shard, accounted on the response
+// (pv_xact_edge2). r.idx indexes the edge run's record blobs, r.period its period table.
+struct PvEdgePair {
+    PvXEvent q, r;
+    uint64_t qaddr; // the query's ECS address (top_ecs)
+    int64_t order;  // the response's first-occurrence order in the stream
+    uint64_t us;    // transaction time
+};
 
 // TCP stage parameters (pv_tcp_* kernels)
 struct PvTcpParams {

@@ -5,7 +5,8 @@ share cuda:0 under gloo), the ranks merge with pktvisor_amd.dist.merge_window, a
 rank 0 writes the merged window JSON. CPU mode ("cpu"): exercises the collective
 helpers of pktvisor_amd.dist alone and writes what each rank saw.
 
-usage: python -m tests.dist_worker gpu PCAP OUT HOST_SPEC PERIODS [DEEP_SAMPLE_RATE [DNS_FILTERS_JSON]]
+usage: python -m tests.dist_worker gpu PCAP OUT HOST_SPEC PERIODS [DEEP_SAMPLE_RATE [DNS_FILTERS_JSON [DNS2_CONFIG_JSON]]]
+       (DNS_FILTERS_JSON "null": none)
        python -m tests.dist_worker cpu OUT
 (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the environment)"""
 import json
@@ -33,7 +34,7 @@ def cpu_main(out):
     dist.destroy_process_group()
 
 
-def gpu_main(pcap_path, out, host, periods, rate=100, filters=None):
+def gpu_main(pcap_path, out, host, periods, rate=100, filters=None, dns2_config=None):
     import torch
     import torch.distributed as dist
     import pktvisor_amd as pa
@@ -49,7 +50,8 @@ def gpu_main(pcap_path, out, host, periods, rate=100, filters=None):
     lo, hi = cuts[rank], cuts[rank + 1]
     offs = [int(x) for x in idx.offsets] + [len(recs)]
     h = pa.PvHandlers(host_spec=host or None, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
-                      max_records=max(1, hi - lo), device=dev.index, deep_sample_rate=rate, dns_filters=filters)
+                      max_records=max(1, hi - lo), device=dev.index, deep_sample_rate=rate, dns_filters=filters,
+                      dns2_config=dns2_config)
     try:
         h.set_global_base(lo)
         sec, frac = struct.unpack_from("<II", recs, offs[0])
@@ -72,4 +74,4 @@ if __name__ == "__main__":
         cpu_main(sys.argv[2])
     else:
         gpu_main(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), int(sys.argv[6]) if len(sys.argv) > 6 else 100,
-                 json.loads(sys.argv[7]) if len(sys.argv) > 7 else None)
+                 json.loads(sys.argv[7]) if len(sys.argv) > 7 else None, json.loads(sys.argv[8]) if len(sys.argv) > 8 else None)
