@@ -152,7 +152,38 @@ struct TAcc {
     }
 };
 
+// A lane's LDS window alone (TAcc without the HBM path), for messages the window holds whole:
+// decoding them issues no vector-memory load, so it never waits on the loads in flight behind
+// it (a load's vmcnt wait covers every load issued before it: TAcc's HBM path, even when no lane
+// takes it, puts a vmcnt(0) after each access, draining the next tile's prefetch)
+struct LAcc {
+    const uint32_t *L;
+    uint64_t gbase;
+    uint32_t mul, add;
+    PV_FN uint32_t u32(uint64_t off) const
+    {
+        const uint32_t r = (uint32_t)(off - gbase), d = (r >> 2) * mul + add;
+        return __builtin_amdgcn_alignbyte(L[d + mul], L[d], r & 3);
+    }
+    PV_FN uint32_t u32a(uint64_t off) const { return L[((uint32_t)(off - gbase) >> 2) * mul + add]; }
+    PV_FN uint32_t u8(uint64_t off) const
+    {
+        const uint32_t r = (uint32_t)(off - gbase);
+        return (L[(r >> 2) * mul + add] >> ((r & 3) * 8)) & 0xff;
+    }
+};
+
 __device__ __forceinline__ uint64_t *slot_sum(PV_CREF(PvParams) P, uint32_t slot) { return P.sum + (uint64_t)slot * PV_SUM_WORDS; }
+// the DNS slot of a lane's period index as a select over the uniform table (a divergent index
+// into the parameter block is a vector-memory load, whose wait drains the loads in flight)
+__device__ __forceinline__ uint32_t dslot(PV_CREF(PvParams) P, uint32_t period)
+{
+    // readfirstlane keeps the table opaque (the optimiser would fold the chain back into a load)
+    uint32_t s = __builtin_amdgcn_readfirstlane(P.dslot_of[0]);
+#pragma unroll
+    for (uint32_t k = 1; k <= PV_MAX_SHIFTS; k++) s = period == k ? __builtin_amdgcn_readfirstlane(P.dslot_of[k]) : s;
+    return s;
+}
 
 // DnsStreamHandler::_filtering's only_qname_suffix (dns/v1/DnsStreamHandler.cpp:615-630): the
 // length of the first listed suffix the lower-case first-query name ends with (the
@@ -809,7 +840,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
 {
     const bool upd = dm.flags & 8;
     const uint32_t period = dm.period;
-    const uint32_t slot = P.dslot_of[period];
+    const uint32_t slot = dslot(P, period);
     const uint64_t m = dm.moff;
     const uint32_t dlen = dm.mlen;
     const uint32_t i = dm.idx;
@@ -1104,10 +1135,15 @@ static_assert(PV_NCACHE <= PV_CACHE_MAX, "update log sized for PV_CACHE_MAX cach
 struct DnsState {
     uint32_t stage[PV_DNS_WAVES][PV_WSTAGE / 4];
     KeyCache<PV_NCACHE> C;
+    uint4 desc[PV_DNS_WAVES][2][PV_WT]; // each wave's staged tile: its lanes' message descriptors (DnsMsgW words)
     uint32_t mq_n[2]; // the range's update-log count, the range
     uint32_t nev[2];  // the range's event count, its first slot in the batch's key list
     uint32_t nresp;
+    uint32_t nlong;   // the range's messages past the LDS window (decoded after the range's tiles)
 };
+#ifndef PV_DNS_LACC
+#define PV_DNS_LACC 1 // tuning: 0 decodes every message with the HBM-backed window accessor (TAcc)
+#endif
 
 // Adds one to bin v for every lane with v != PV_NOH: bins below PV_HBINS in the LDS
 // histogram H, larger ones straight to the HBM table G (G[v]: the slot's payload-size words).
@@ -2935,6 +2971,7 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
             S.mq_n[0] = P.mq_cnt[lb];
             S.mq_n[1] = lb;
             S.nev[0] = 0;
+            S.nlong = 0;
             // the range's slots in the key list: at most one event per message
             if (P.want_events && nd) S.nev[1] = atomicAdd(P.n_keys, nd);
         }
@@ -2948,22 +2985,39 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
         auto msg = [&](uint32_t t) -> DnsMsg { return Q[min(t * PV_WT + lane, nd - 1)]; };
         constexpr uint32_t NW = PV_DNS_WAVES;
         uint32_t t = wave;
-        DnsMsg m_cur{}, m_n{};
         uint4 pf[8];
         auto issue = [&](const DnsMsg &d, bool) {
             const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + ((uint64_t)d.moff & ~15ull));
 #pragma unroll
             for (int j = 0; j < 8; j++) pf[j] = src[j];
         };
+        // The staged tile's descriptors sit in LDS (desc, as raw words) next to its windows; one
+        // descriptor is in registers, loaded a tile ahead of its windows. So the only loop-carried
+        // loads are the windows (pf) and that descriptor's words (mw), both consumed behind the one
+        // wait at the top of the next iteration, and nothing in the decode waits on them.
+        const PV_G uint4 *Qw = reinterpret_cast<const PV_G uint4 *>(Q);
+        auto msgw = [&](uint32_t t, uint4 &a, uint4 &b) {
+            const uint32_t j = min(t * PV_WT + lane, nd - 1);
+            a = Qw[2 * (uint64_t)j];
+            b = Qw[2 * (uint64_t)j + 1];
+        };
+        auto win = [&](uint32_t moff) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(P.recs + ((uint64_t)moff & ~15ull));
+#pragma unroll
+            for (int j = 0; j < 8; j++) pf[j] = src[j];
+        };
+        uint4 mwa{}, mwb{};
         if (t < ntl) {
-            m_cur = msg(t);
-            issue(m_cur, t * PV_WT + lane < nd);
-            m_n = msg(t + NW);
+            uint4 a, b;
+            msgw(t, a, b);
+            S.desc[wave][0][lane] = a;
+            S.desc[wave][1][lane] = b;
+            win(a.y);
+            msgw(t + NW, mwa, mwb);
         }
         for (; t < ntl; t += NW) {
             t = __builtin_amdgcn_readfirstlane(t);
             const bool active = t * PV_WT + lane < nd;
-            const DnsMsg dm = m_cur;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 L[(4 * j + 0) * PV_WT + lane] = pf[j].x;
@@ -2971,28 +3025,79 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
                 L[(4 * j + 2) * PV_WT + lane] = pf[j].z;
                 L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
             }
+            const uint4 da = S.desc[wave][0][lane], db = S.desc[wave][1][lane];
             if (t + NW < ntl) {
-                // the message after next is loaded before the next windows: loads retire in
-                // issue order, so the register moves of the message rotation then wait for
-                // the message alone, never for the windows still in flight
-                const DnsMsg m_nn = msg(t + 2 * NW);
-                issue(m_n, (t + NW) * PV_WT + lane < nd);
-                m_cur = m_n;
-                m_n = m_nn;
+                // (a wave's LDS operations retire in order: the reads above see the old words)
+                S.desc[wave][0][lane] = mwa;
+                S.desc[wave][1][lane] = mwb;
+                win(mwa.y);
+                msgw(t + 2 * NW, mwa, mwb);
             }
+            DnsMsg dm;
+            dm.idx = da.x;
+            dm.moff = da.y;
+            dm.mlen = (uint16_t)(da.z & 0xffff);
+            dm.mcap = (uint16_t)(da.z >> 16);
+            dm.port = (uint16_t)(da.w & 0xffff);
+            dm.flags = (uint8_t)((da.w >> 16) & 0xff);
+            dm.period = (uint8_t)(da.w >> 24);
+            dm.fkey = db.x;
+            dm.sec = db.y;
+            dm.nsec = db.z;
+            dm.pad = db.w;
             // the wave's register counters follow the slot of its first message
             const uint32_t s0 = P.dslot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
             if (s0 != wslot) {
                 if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
                 wslot = s0;
             }
-            if (active) {
-                const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
-                const bool own = P.dslot_of[dm.period] == wslot;
-                dns_process<false, false, SFX, FILT>(P, &S.C, S.mq_n, S.nev, &S.nresp, region, R, dm, own, c);
+            const uint64_t wbase = (uint64_t)dm.moff & ~15ull;
+            if (PV_DNS_LACC) {
+                // a message the window holds whole (every byte the decoder reads lies in
+                // [moff, moff + max(mlen, mcap))) decodes from LDS alone; the rest wait for the
+                // range's long pass, where no prefetch is in flight
+                const bool fits = (uint64_t)dm.moff + max((uint32_t)dm.mlen, (uint32_t)dm.mcap) - wbase <= (uint64_t)(PV_WIN - 4);
+                if (active && fits) {
+                    const LAcc R{L, wbase, (uint32_t)PV_WT, lane};
+                    dns_process<false, false, SFX, FILT>(P, &S.C, S.mq_n, S.nev, &S.nresp, region, R, dm, dslot(P, dm.period) == wslot, c);
+                } else if (active) {
+                    reinterpret_cast<PV_G uint32_t *>(P.ekeys + region)[atomicAdd(&S.nlong, 1u)] = t * PV_WT + lane;
+                }
+            } else if (active) {
+                const TAcc R{P.recs, L, wbase, PV_WIN - 4, (uint32_t)PV_WT, lane};
+                dns_process<false, false, SFX, FILT>(P, &S.C, S.mq_n, S.nev, &S.nresp, region, R, dm, dslot(P, dm.period) == wslot, c);
             }
         }
         __syncthreads();
+        if (PV_DNS_LACC && S.nlong) {
+            // the long pass: one wave per 64 long messages, their windows staged as above, bytes past
+            // the window from HBM (TAcc)
+            const uint32_t nl = S.nlong;
+            const PV_G uint32_t *lq = reinterpret_cast<const PV_G uint32_t *>(P.ekeys + region);
+            for (uint32_t u = wave; u * PV_WT < nl; u += NW) {
+                u = __builtin_amdgcn_readfirstlane(u);
+                const bool active = u * PV_WT + lane < nl;
+                const DnsMsg dm = Q[lq[min(u * PV_WT + lane, nl - 1)]];
+                issue(dm, active);
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    L[(4 * j + 0) * PV_WT + lane] = pf[j].x;
+                    L[(4 * j + 1) * PV_WT + lane] = pf[j].y;
+                    L[(4 * j + 2) * PV_WT + lane] = pf[j].z;
+                    L[(4 * j + 3) * PV_WT + lane] = pf[j].w;
+                }
+                const uint32_t s0 = P.dslot_of[__builtin_amdgcn_readfirstlane((uint32_t)dm.period)];
+                if (s0 != wslot) {
+                    if (wslot != 0xffffffffu) dns_flush(P, wslot, c);
+                    wslot = s0;
+                }
+                if (active) {
+                    const TAcc R{P.recs, L, (uint64_t)dm.moff & ~15ull, PV_WIN - 4, (uint32_t)PV_WT, lane};
+                    dns_process<false, false, SFX, FILT>(P, &S.C, S.mq_n, S.nev, &S.nresp, region, R, dm, dslot(P, dm.period) == wslot, c);
+                }
+            }
+            __syncthreads();
+        }
         if (lb + gridDim.x >= P.grid_main) {
             cache_flush(P, S.C, PV_NCACHE, S.mq_n);
             __syncthreads();
