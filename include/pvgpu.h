@@ -162,6 +162,28 @@ int pv_set_dns_filters(pv_ctx *ctx, const pv_dns_filters *f);
  * (closeConnection). 0 (the default): the reference's DEFAULT_LRULIST_SIZE behaviour without
  * the capacity check. Call before the first batch. */
 int pv_set_tcp_reassembly_limit(pv_ctx *ctx, uint64_t limit);
+/* A classic-BPF instruction (struct sock_filter, linux/filter.h): what libpcap's pcap_compile
+ * produces and `tcpdump -dd EXPR` prints. */
+typedef struct pv_bpf_insn {
+    uint16_t code;
+    uint8_t jt, jf;
+    uint32_t k;
+} pv_bpf_insn;
+/* The pcap input's "bpf" filter (PcapInputStream::_open_pcap: reader->setFilter(bpf),
+ * src/inputs/pcap/PcapInputStream.cpp:485-488, pcap_offline_filter semantics): records the
+ * program answers 0 for never reach the handlers (no event, no timestamp, no period shift).
+ * Applies to pv_process_host input from the next call; the program comes compiled (libpcap is
+ * not linked). n = 0 removes the filter. PV_EINVAL for a program the classic-BPF checker
+ * refuses (unknown opcode, jump out of range, scratch index >= 16, division by a constant 0,
+ * no final return). Device-resident input (pv_process_device) is the caller's: not filtered. */
+int pv_set_bpf(pv_ctx *ctx, const pv_bpf_insn *prog, uint32_t n);
+/* Pure host functions of the same machine: validate a program (PV_OK / PV_EINVAL); run it on one
+ * frame (wirelen = the record's orig_len, buflen = its incl_len; 0 = drop); copy the records of
+ * a block of classic-pcap records the program keeps to out (out may equal recs). */
+int pv_bpf_validate(const pv_bpf_insn *prog, uint32_t n);
+uint32_t pv_bpf_run(const pv_bpf_insn *prog, const uint8_t *frame, uint32_t wirelen, uint32_t buflen);
+int pv_bpf_filter_records(const pv_bpf_insn *prog, uint32_t n, const uint8_t *recs, size_t bytes, uint8_t *out,
+                          size_t *out_bytes, uint64_t *kept);
 /* Name or decimal -> code for kind 0 = rcode (RCodeNumbers) or 1 = qtype (QTypeNumbers),
  * case-insensitive, libs/visor_dns/dns.h:31-265; PV_EINVAL if unknown. Pure host function. */
 int pv_dns_code(int kind, const char *name, uint32_t *value);

@@ -172,11 +172,39 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name",
            "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_dnstap_only_hosts",
            "pv_afpacket_open", "pv_afpacket_attach", "pv_afpacket_run", "pv_afpacket_start", "pv_afpacket_stop",
-           "pv_afpacket_stats", "pv_afpacket_close", "pv_afpacket_last_error"]
+           "pv_afpacket_stats", "pv_afpacket_close", "pv_afpacket_last_error", "pv_set_bpf", "pv_bpf_validate",
+           "pv_bpf_run", "pv_bpf_filter_records"]
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
 PV_REDUCE_SUM, PV_REDUCE_MIN = 0, 1
+
+
+class pv_bpf_insn(ctypes.Structure):
+    """struct sock_filter (linux/filter.h): one classic-BPF instruction"""
+    _fields_ = [("code", ctypes.c_uint16), ("jt", ctypes.c_uint8), ("jf", ctypes.c_uint8), ("k", ctypes.c_uint32)]
+
+
+def bpf_program(insns):
+    """a ctypes array of pv_bpf_insn from (code, jt, jf, k) tuples (`tcpdump -dd EXPR` output)"""
+    arr = (pv_bpf_insn * max(1, len(insns)))()
+    for i, (c, jt, jf, k) in enumerate(insns):
+        arr[i] = pv_bpf_insn(c, jt, jf, k & 0xFFFFFFFF)
+    return arr
+
+
+def bpf_filter(recs: bytes, insns) -> bytes:
+    """the classic-pcap records of `recs` the program keeps (pv_bpf_filter_records, host only)"""
+    lib = load_library()
+    prog = bpf_program(insns)
+    src = np.frombuffer(recs, dtype=np.uint8)
+    out = np.empty(max(1, len(recs)), dtype=np.uint8)
+    nb = ctypes.c_size_t()
+    rc = lib.pv_bpf_filter_records(prog, len(insns), src.ctypes.data if len(recs) else None, len(recs), out.ctypes.data,
+                                   ctypes.byref(nb), None)
+    if rc:
+        raise PvError(f"pv_bpf_filter_records failed ({rc}): invalid BPF program")
+    return out[:nb.value].tobytes()
 
 
 class pv_afpacket_config(ctypes.Structure):
@@ -273,6 +301,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_window_periods.argtypes = [P, ctypes.c_int, P, P, U32, ctypes.POINTER(U32)]
     lib.pv_set_dns_filters.argtypes = [P, ctypes.POINTER(pv_dns_filters)]
     lib.pv_set_tcp_reassembly_limit.argtypes = [P, ctypes.c_uint64]
+    lib.pv_set_bpf.argtypes = [P, P, U32]
+    lib.pv_bpf_validate.argtypes = [P, U32]
+    lib.pv_bpf_run.argtypes = [P, P, U32, U32]
+    lib.pv_bpf_run.restype = ctypes.c_uint32
+    lib.pv_bpf_filter_records.argtypes = [P, U32, P, ctypes.c_size_t, P, ctypes.POINTER(ctypes.c_size_t), P]
     lib.pv_set_dnstap_only_hosts.argtypes = [P, ctypes.c_char_p]
     lib.pv_dns_code.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(U32)]
     lib.pv_comm_unique_id.argtypes = [P]
@@ -547,7 +580,7 @@ class PvHandlers:
                  dns_filters: Optional[dict] = None, net_config: Optional[dict] = None,
                  dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0,
                  net2_config: Optional[dict] = None, dns2_config: Optional[dict] = None,
-                 deep_sample_rate: int = 100, tcp_packet_reassembly_cache_limit: int = 0):
+                 deep_sample_rate: int = 100, tcp_packet_reassembly_cache_limit: int = 0, bpf=None):
         from pktvisor_amd import config as pvcfg
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
@@ -619,6 +652,14 @@ class PvHandlers:
             # the pcap input's config (PcapInputStream.cpp:97-99)
             self._check(self.lib.pv_set_tcp_reassembly_limit(self.ctx, int(tcp_packet_reassembly_cache_limit)),
                         "pv_set_tcp_reassembly_limit")
+        if bpf:
+            self.set_bpf(bpf)
+
+    def set_bpf(self, insns):
+        """the pcap input's "bpf" filter as its compiled classic-BPF program (pv_set_bpf): records it
+        rejects never reach the handlers; [] removes it"""
+        self._bpf = bpf_program(insns or [])
+        self._check(self.lib.pv_set_bpf(self.ctx, self._bpf, len(insns or [])), "pv_set_bpf")
 
     def _check(self, rc, what):
         if rc:
@@ -943,6 +984,9 @@ def last_record_ts(recs: bytes, index: RecordIndex, ts_nano: int = 0):
 def pktvisor_reader(path: str, host_spec: Optional[str] = None, periods: int = 5, **kw) -> dict:
     """GPU equivalent of `pktvisor-reader [-H host_spec] --periods N FILE` for net + dns."""
     linktype, ts_nano, recs = read_pcap(path)
+    if kw.get("bpf"):
+        # the reader delivers only the records the filter keeps (their last one ends the capture)
+        recs = bpf_filter(recs, kw["bpf"])
     idx = RecordIndex(recs, ts_nano)
     h = PvHandlers(host_spec=host_spec, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
                    max_records=max(1, idx.n), **kw)

@@ -494,6 +494,8 @@ inline bool hip_ok(hipError_t e) { return e == hipSuccess; }
 
 // ---------------------------------------------------------------- context
 struct pv_ctx {
+    std::vector<pv_bpf_insn> bpf; // the pcap input's BPF program (pv_set_bpf), empty = none
+    std::vector<uint8_t> bpf_buf; // the records it keeps of one pv_process_host block
     pv_config cfg{};
     std::string err;
     std::mutex mu;
@@ -4625,7 +4627,39 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
 // chunk k + 1 (parallel copy into pinned memory unless the caller's buffer is already
 // pinned, parallel record index, H2D on the copy stream) while the calling thread runs
 // chunk k's kernels. Results equal one pv_process_device per chunk, in order.
+int pv_set_bpf(pv_ctx *c, const pv_bpf_insn *prog, uint32_t n)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    if (n == 0) { c->bpf.clear(); return 0; }
+    if (pv_bpf_validate(prog, n)) return c->fail(PV_EINVAL, "invalid BPF program (classic-BPF checker)");
+    c->bpf.assign(prog, prog + n);
+    return 0;
+}
+
+namespace {
+int process_host_block(pv_ctx *c, const uint8_t *recs, size_t bytes);
+}
+
 int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
+{
+    std::vector<pv_bpf_insn> prog;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        prog = c->bpf;
+    }
+    if (prog.empty()) return process_host_block(c, recs, bytes);
+    // the pcap input's filter (PcapInputStream.cpp:485-488): the kept records, in order, go on
+    // as the block (libpcap runs the program on the reading thread, as here); bpf_buf is the
+    // input thread's (one producer per context)
+    c->bpf_buf.resize(bytes);
+    size_t kb = 0;
+    if (pv_bpf_filter_records(prog.data(), (uint32_t)prog.size(), recs, bytes, c->bpf_buf.data(), &kb, nullptr))
+        return c->fail(PV_EINVAL, "BPF filter");
+    return kb ? process_host_block(c, c->bpf_buf.data(), kb) : 0;
+}
+
+namespace {
+int process_host_block(pv_ctx *c, const uint8_t *recs, size_t bytes)
 {
     hipSetDevice(c->device);
     if (int rc = ingest_setup(c)) return rc;
@@ -4729,6 +4763,7 @@ int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
     if (prod_rc) return c->fail(prod_rc, "%s", prod_err.c_str());
     return 0;
 }
+} // namespace
 
 // The device record index (pv_index.hip) of one block in host memory, filled as
 // pv_index_records fills its outputs (a block of at most one ingest chunk).

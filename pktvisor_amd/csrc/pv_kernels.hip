@@ -173,6 +173,34 @@ struct LAcc {
     }
 };
 
+// LAcc that records how far its reads went (the end of the highest dword read, in window
+// bytes): a side-effect-free decode runs on it speculatively and is redone on TAcc when it read
+// past the window
+struct LAccT {
+    const uint32_t *L;
+    uint64_t gbase;
+    uint32_t mul, add;
+    uint32_t *hi;
+    PV_FN uint32_t u32(uint64_t off) const
+    {
+        const uint32_t r = (uint32_t)(off - gbase), d = (r >> 2) * mul + add;
+        *hi = max(*hi, ((r >> 2) + 2) * 4);
+        return __builtin_amdgcn_alignbyte(L[d + mul], L[d], r & 3);
+    }
+    PV_FN uint32_t u32a(uint64_t off) const
+    {
+        const uint32_t r = (uint32_t)(off - gbase);
+        *hi = max(*hi, ((r >> 2) + 1) * 4);
+        return L[(r >> 2) * mul + add];
+    }
+    PV_FN uint32_t u8(uint64_t off) const
+    {
+        const uint32_t r = (uint32_t)(off - gbase);
+        *hi = max(*hi, ((r >> 2) + 1) * 4);
+        return (L[(r >> 2) * mul + add] >> ((r & 3) * 8)) & 0xff;
+    }
+};
+
 __device__ __forceinline__ uint64_t *slot_sum(PV_CREF(PvParams) P, uint32_t slot) { return P.sum + (uint64_t)slot * PV_SUM_WORDS; }
 // the DNS slot of a lane's period index as a select over the uniform table (a divergent index
 // into the parameter block is a vector-memory load, whose wait drains the loads in flight)
@@ -3959,34 +3987,44 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
             L[(4 * j + 2) * 64 + lane] = pf[j].z;
             L[(4 * j + 3) * 64 + lane] = pf[j].w;
         }
+        // the next entry's window: in flight through this entry's decode, which reads LDS alone
+        // (LAccT); the reservation's wait below lands it
+        const uint32_t i_n = i + step, i_nn = i + 2 * step;
+        ld_win(roff_n, i_n < n);
         const TAcc R{P.recs, L, wbase, PV_NWIN - 4, 64u, lane};
-        if (act) {
-            parse_record(R, P, roff, o);
+        uint32_t hi = 0;
+        const LAccT RL{L, wbase, 64u, lane, &hi};
+        auto decode = [&](const auto &A) {
+            parse_record(A, P, roff, o);
             m = o.l4off + 8;
             mlen = o.l4len - 8;
-        }
-        if (act) {
             if (metric == TM_IPV6) {
-                a6 = ip6_name_addr(R, o, tkey);
+                a6 = ip6_name_addr(A, o, tkey);
                 size = 18;
             } else {
                 NameStats st;
                 st.init();
-                nl = name_len_l1(R, m, mlen, 12);
-                if (nl > 0) name_stats(R, m, mlen, 12, st);
+                nl = name_len_l1(A, m, mlen, 12);
+                if (nl > 0) name_stats(A, m, mlen, 12, st);
                 const uint32_t nch = nl > 0 ? st.n : 0;
+                start = 0;
                 if (metric == TM_QNAME2 || metric == TM_QNAME3) {
                     int q2, q3;
                     uint64_t h2, h3;
                     const uint32_t sfx = name_sfx(P, e.rep, P.sfx_of);
-                    if (nl > 0) agg_domain_r(R, m, mlen, st, q2, q3, h2, h3, sfx);
+                    if (nl > 0) agg_domain_r(A, m, mlen, st, q2, q3, h2, h3, sfx);
                     else { q2 = 0; q3 = -1; }
                     const int st0 = metric == TM_QNAME2 ? q2 : q3;
                     start = st0 < 0 ? nch : (uint32_t)st0;
                 }
                 size = nch - start + 2;
             }
-        }
+        };
+        if (act) decode(RL);
+        // a record whose decode read past the window (rare: long names, IP options) is decoded
+        // again with the HBM path, whose waits also land the prefetch
+        const bool inwin = hi <= PV_NWIN;
+        if (act && !inwin) decode(R);
         // wave prefix sum of the sizes; one arena reservation per wave when its lanes
         // share a slot (the common case), else one per lane
         uint32_t incl = size;
@@ -4000,9 +4038,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
         const uint32_t s0 = __shfl(e.slot, 0, 64);
         const bool uniform = __all(!act || e.slot == s0);
         const bool packed = uniform && tot4 <= PV_NOUT;
-        // prefetch (see above): issued before the reservation, whose wait covers them
-        const uint32_t i_n = i + step, i_nn = i + 2 * step;
-        ld_win(roff_n, i_n < n);
+        // the key / record offset of the entry after next: landed by the reservation's wait
         const uint64_t tkey_nn = i_nn < n ? P.tkeys[e_nn.pos] : 0, roff_nn = i_nn < n ? P.offs[e_nn.rep] : 0;
         auto emit_to = [&](uint8_t *dst) {
             const uint32_t slen = size - 2;
@@ -4012,7 +4048,8 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 for (int k = 0; k < 16; k++) dst[2 + k] = (uint8_t)G.u8(a6 + k);
             } else if (slen > 0 && nl > 0) {
                 CopyEmit ce{dst + 2, start, 0, (metric == TM_SLOW_IN || metric == TM_SLOW_OUT) ? 1u : 0u};
-                name_emit(R, m, mlen, 12, ce);
+                if (inwin) name_emit(RL, m, mlen, 12, ce);
+                else name_emit(R, m, mlen, 12, ce);
             }
         };
         if (uniform) {

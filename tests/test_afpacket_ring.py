@@ -38,10 +38,12 @@ class FakeKernel:
     def status(self, k):
         return struct.unpack_from("<I", self.mm, k * self.bs + 8)[0]
 
-    def put(self, raw, timeout=20.0):
+    def put(self, raw, timeout=20.0, stopped=lambda: False):
         k = self.next
         t0 = time.time()
         while self.status(k) != 0:  # TP_STATUS_KERNEL: the loop gave it back
+            if stopped():
+                return False  # the loop ended (a failing sink): no one returns blocks any more
             if time.time() - t0 > timeout:
                 raise TimeoutError("ring block never returned")
             time.sleep(0.0005)
@@ -52,6 +54,7 @@ class FakeKernel:
         os.eventfd_write(self.efd, 1)
         self.next = (k + 1) % self.nb
         self.handed += 1
+        return True
 
     def close(self):
         os.close(self.efd)
@@ -94,8 +97,7 @@ def run_capture(blocks, num_blocks=4, batch_bytes=1 << 15, sink_fail_after=None)
     t.start()
     try:
         for part, ts in blocks:
-            fk.put(block(part, ts_last=ts, size=BS))
-            if rc[0] is not None:
+            if not fk.put(block(part, ts_last=ts, size=BS), stopped=lambda: rc[0] is not None) or rc[0] is not None:
                 break
         want = sum(len(p) for p, _ in blocks)
         t0 = time.time()
