@@ -2979,13 +2979,9 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ DnsState S;
-    if (*P.n_dns == 0) {
-        // no DNS message in the batch (the Net pass counted them): only the ranges' event counts
-        // (the update-log counters stay as the Net pass reset them)
-        for (uint32_t lb = blockIdx.x * blockDim.x + threadIdx.x; lb < P.grid_main; lb += gridDim.x * blockDim.x)
-            P.blk_events[lb] = 0;
-        return;
-    }
+    // no DNS message in the batch (the Net pass counted them): nothing to do (the update-log
+    // counters stay as the Net pass reset them, the key list stays empty)
+    if (*P.n_dns == 0) return;
     S.C.clear();
     if (threadIdx.x == 0) S.nresp = 0;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;

@@ -191,3 +191,26 @@ def test_dns2_dnstap_windows_and_filter(periods):
     out = pa.dnstap_reader(FIX, periods=periods, dns2_config={})
     d = out[f"{periods}m"]["dns"]
     assert d["observed_packets"] == 153 and d["in"]["xacts"] == 72
+
+
+def test_dnstap_only_hosts_failed_call_keeps_state():
+    """a spec list that fails to parse leaves the previous only_hosts state as it was
+    (the reference's parse_host_specs throws before any proxy filters with a partial list)"""
+    frames = open(FIX, "rb").read()
+    h = pa.PvHandlers(num_periods=1, net_config={}, dns_config={})
+    try:
+        # no filter, then a failing call: every message still reaches the handlers
+        with pytest.raises(pa.PvError, match="invalid CIDR"):
+            h._check(h.lib.pv_set_dnstap_only_hosts(h.ctx, b"192.168.0.0/24,10.0.0.0/99"), "pv_set_dnstap_only_hosts")
+        h.process_dnstap(frames)
+        assert jget({"w": h.window_json(0)}, "w.dns.wire_packets.events") == 153
+        # a filter, then a failing call: the filter stays (no message matches it, as above)
+        h.reset()
+        h._check(h.lib.pv_set_dnstap_only_hosts(h.ctx, b"192.168.0.0/24"), "pv_set_dnstap_only_hosts")
+        with pytest.raises(pa.PvError, match="invalid IPv4 address"):
+            h._check(h.lib.pv_set_dnstap_only_hosts(h.ctx, b"192.168.AE.0/24"), "pv_set_dnstap_only_hosts")
+        h.process_dnstap(frames)
+        with pytest.raises(pa.PvError, match="no data"):
+            h.window_json(0)
+    finally:
+        h.close()

@@ -71,3 +71,36 @@ def test_flood_one_batch_degrades(table_log2):
         assert t <= e["estimate"] <= t + rounds_bound, (e, t)
     assert dns["top_qname2"][0] == {"name": ".victim.example", "estimate": total}
     assert dns["wire_packets"]["total"] == total
+
+
+def test_dirty_writeback_after_purge():
+    """pv_topn_merge writes back only the entries a batch changed (a dirty byte per
+    entry). After a flood has purged the table, batches that touch only the heavy names must move
+    each heavy estimate by exactly its new count (no purge runs: 24 live keys), so the merge wrote
+    every changed entry back and left the others as the purge left them."""
+    import struct
+    pcap, heavy, total = synth.qname_flood_pcap(7, flood=60000)
+    extra, heavy2, total2 = synth.qname_flood_pcap(8, flood=0, duration_s=5.0)
+    more = bytearray(extra[24:])
+    p = 0
+    while p < len(more):  # 45 s later: the same 60 s period, after the flood
+        s, us, cl, ol = struct.unpack_from("<IIII", more, p)
+        struct.pack_into("<I", more, p, s + 45)
+        p += 16 + cl
+    h = pa.PvHandlers(host_spec="10.0.0.0/8", num_periods=1, table_log2=12, max_records=1 << 17, topn_count=24)
+    try:
+        def feed(recs, batch):
+            idx = pa.RecordIndex(recs)
+            offs = list(idx.offsets) + [len(recs)]
+            for i in range(0, idx.n, batch):
+                h.process_host(recs[offs[i]:offs[min(idx.n, i + batch)]])
+        feed(pcap[24:], 1000)
+        e1 = {e["name"]: e["estimate"] for e in h.window_json(0)["dns"]["top_qname3"]}
+        feed(bytes(more), 300)
+        e2 = {e["name"]: e["estimate"] for e in h.window_json(0)["dns"]["top_qname3"]}
+    finally:
+        h.close()
+    common = [n for n in heavy if n in e1 and n in e2]
+    assert len(common) >= 20
+    for n in common:
+        assert e2[n] - e1[n] == heavy2[n], (n, e1[n], e2[n], heavy2[n])
