@@ -3365,7 +3365,7 @@ __device__ __forceinline__ uint64_t ip_tkey(uint64_t e)
 #endif
 template <uint32_t CN, uint32_t NR>
 struct CombState {
-    uint64_t key[CN];
+    alignas(16) uint64_t key[CN];
     uint32_t cnt[CN];
     uint32_t rep[CN];
     uint32_t h[NR];   // entries per region, then the placement cursors
@@ -3393,11 +3393,48 @@ __device__ __forceinline__ void comb_count(PV_CREF(PvParams) P, St &S, uint64_t 
     const uint32_t bit = 1u << entry_table(e0);
     if (!(S.tb[r] & bit)) atomicOr(&S.tb[r], bit);
 }
+#ifndef PV_CB_BUCKET
+#define PV_CB_BUCKET 0 // tuning: 1 probes aligned 4-entry buckets (two 16-B LDS reads each) instead of single entries
+#endif
+// one aligned 4-entry bucket of the combine table: match or claim; false = the bucket is full of
+// other keys
+template <class St>
+__device__ __forceinline__ bool comb_bucket(St &S, uint32_t b, uint64_t ck, uint32_t w, uint32_t rep)
+{
+    const uint4 *kp = reinterpret_cast<const uint4 *>(&S.key[b]);
+    const uint4 lo = kp[0], hi = kp[1];
+    const uint64_t cur4[4] = {(uint64_t)lo.x | ((uint64_t)lo.y << 32), (uint64_t)lo.z | ((uint64_t)lo.w << 32),
+                              (uint64_t)hi.x | ((uint64_t)hi.y << 32), (uint64_t)hi.z | ((uint64_t)hi.w << 32)};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint64_t cur = cur4[j];
+        if (cur == 0) {
+            const uint64_t prev = atomicCAS((unsigned long long *)&S.key[b + j], 0ull, (unsigned long long)ck);
+            cur = prev == 0 ? ck : prev;
+        }
+        if (cur == ck) {
+            atomicAdd(&S.cnt[b + j], w);
+            if (rep < S.rep[b + j]) atomicMin(&S.rep[b + j], rep);
+            return true;
+        }
+    }
+    return false;
+}
 template <uint32_t CN, class St>
 __device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, St &S, PV_G ulonglong2 *sp, uint64_t ck, uint32_t w,
                                          uint32_t rep)
 {
     uint32_t pos = (uint32_t)(fmix64(ck) >> 20) & (CN - 1);
+#if PV_CB_BUCKET
+    for (int g = 0; g < 4; g++)
+        if (comb_bucket(S, ((pos & ~3u) + 4u * g) & (CN - 1), ck, w, rep)) return;
+    {
+        const ulonglong2 e = comb_entry(ck, w, rep);
+        sp[atomicAdd(&S.nsp, 1u)] = e;
+        comb_count(P, S, e.x);
+        return;
+    }
+#endif
     for (int probe = 0; probe < 16; probe++) {
         uint64_t cur = S.key[pos];
         if (cur == 0) {
@@ -3423,6 +3460,27 @@ __device__ __forceinline__ void comb_add_pre(PV_CREF(PvParams) P, St &S, PV_G ul
                                              uint32_t rep, uint32_t pos, uint64_t cur0, uint32_t rep0)
 {
     uint64_t cur = cur0;
+#if PV_CB_BUCKET
+    // the pre-read first probe, then the aligned buckets after it
+    if (cur == 0) {
+        const uint64_t prev = atomicCAS((unsigned long long *)&S.key[pos], 0ull, (unsigned long long)ck);
+        cur = prev == 0 ? ck : prev;
+        rep0 = 0xffffffffu;
+    }
+    if (cur == ck) {
+        atomicAdd(&S.cnt[pos], w);
+        if (rep < rep0) atomicMin(&S.rep[pos], rep);
+        return;
+    }
+    for (int g = 1; g <= 4; g++)
+        if (comb_bucket(S, ((pos & ~3u) + 4u * g) & (CN - 1), ck, w, rep)) return;
+    {
+        const ulonglong2 e = comb_entry(ck, w, rep);
+        sp[atomicAdd(&S.nsp, 1u)] = e;
+        comb_count(P, S, e.x);
+        return;
+    }
+#endif
     for (int probe = 0; probe < 16; probe++) {
         if (probe) { cur = S.key[pos]; rep0 = 0; }
         if (cur == 0) {
