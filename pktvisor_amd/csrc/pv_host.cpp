@@ -3249,8 +3249,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
             return c->hipfail(e, "parameter upload");
         hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
-        hipLaunchKernelGGL(pv_xact_carry, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
-        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_carry");
+        // (the resolve kernel also moves the queries still open to the carried list: pv_xact_carry's work)
         if (c->slow_defer) {
             if (int rc = defer_slow(c, P, st)) return rc;
         } else if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {

@@ -3006,7 +3006,6 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
         // message and window loads are unconditional (clamped index; an inactive lane's copy is
         // never read), so every iteration issues the same number of loads in the same order and
         // the compiler's vmcnt waits stay exact instead of falling back to vmcnt(0)
-        auto msg = [&](uint32_t t) -> DnsMsg { return Q[min(t * PV_WT + lane, nd - 1)]; };
         constexpr uint32_t NW = PV_DNS_WAVES;
         uint32_t t = wave;
         uint4 pf[8];
@@ -4869,6 +4868,31 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
     }
 }
 
+// Queries still open after this batch (the latest event of their (flow, txid) is a query
+// not purged by a period shift here) move to the carried list for the next batch, as
+// period 0 with sort rank 0: TransactionManager's map surviving the batch edge. Run by the
+// resolve kernel's threads on their own sorted positions (one pass over the events).
+__device__ __forceinline__ void carry_one(PV_CREF(PvXactParams) X, uint32_t p)
+{
+    PvXEvent e = xev(X, p);
+    if (e.qr || purge_period(X.P, X.ttl_s, e.period, e.sec)) return;
+    const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
+    for (uint32_t q = p + 1; q < X.n && (uint32_t)(X.skeys[q] >> 32) == h; q++)
+        if (xev(X, q).key == e.key) return;
+    e.period = 0;
+    const uint32_t k = atomicAdd(X.n_pend_out, 1u);
+    X.pend_out[k] = e;
+    if (X.pecs_out) X.pecs_out[k] = ((e.pad >> 3) & 3) ? xecs(X, p) : 0ull;
+    X.pkeys_out[k] = (uint64_t)h << 32;
+    X.pvals_out[k] = k;
+}
+extern "C" __global__ void pv_xact_carry(const PvXactParams *__restrict__ Xp)
+{
+    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < X.n) carry_one(X, p);
+}
+
 __device__ __forceinline__ void xstate_init(XState &T)
 {
     for (uint32_t j = threadIdx.x; j < (PV_MAX_SHIFTS + 1) * XC_N; j += blockDim.x) (&T.ctr[0][0])[j] = 0;
@@ -4918,6 +4942,7 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvX
     if (p < X.n) {
         if (P.dns2_groups) resolve_one2(X, T, p);
         else resolve_one(X, T, p);
+        if (X.pend_out) carry_one(X, p); // the queries still open go on to the next batch
     }
     __syncthreads();
     xstate_flush(X, T);
@@ -4961,26 +4986,6 @@ extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_edge2(const PvXac
     xstate_flush(X, T);
 }
 
-// Queries still open after this batch (the latest event of their (flow, txid) is a query
-// not purged by a period shift here) move to the carried list for the next batch, as
-// period 0 with sort rank 0: TransactionManager's map surviving the batch edge.
-extern "C" __global__ void pv_xact_carry(const PvXactParams *__restrict__ Xp)
-{
-    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= X.n) return;
-    PvXEvent e = xev(X, p);
-    if (e.qr || purge_period(X.P, X.ttl_s, e.period, e.sec)) return;
-    const uint32_t h = (uint32_t)(X.skeys[p] >> 32);
-    for (uint32_t q = p + 1; q < X.n && (uint32_t)(X.skeys[q] >> 32) == h; q++)
-        if (xev(X, q).key == e.key) return;
-    e.period = 0;
-    const uint32_t k = atomicAdd(X.n_pend_out, 1u);
-    X.pend_out[k] = e;
-    if (X.pecs_out) X.pecs_out[k] = ((e.pad >> 3) & 3) ? xecs(X, p) : 0ull;
-    X.pkeys_out[k] = (uint64_t)h << 32;
-    X.pvals_out[k] = k;
-}
 // A batch with queries only and no period shift pairs nothing: its events join the
 // carried list unresolved. With nothing carried the host hands the batch's event store, keys
 // and values over to the carried list as they lie (no copy); otherwise this kernel appends them
