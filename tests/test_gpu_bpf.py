@@ -14,8 +14,9 @@ from tests.test_gpu_parity import GOLD, diff
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("prog", ["udp53", "short", "arith"])
-@pytest.mark.parametrize("src", ["dns_udp_tcp_random.pcap", "c4"])
+@pytest.mark.parametrize("prog,src", [("udp53", "dns_udp_tcp_random.pcap"), ("short", "dns_udp_tcp_random.pcap"),
+                                      ("arith", "dns_udp_mixed_rcode.pcap"), ("udp53", "c4"), ("short", "c4"),
+                                      ("arith", "c4")])
 def test_bpf_reader_parity(oracle, tmp_path, prog, src):
     pcap = open(os.path.join(GOLD, src), "rb").read() if src.endswith(".pcap") else synth.pcap_bytes(4, 20000)
     p = tmp_path / "in.pcap"
