@@ -507,7 +507,8 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
 #endif
 #define PV_LKEY(slot, lm, payload) (((uint64_t)(slot) << 60) | ((uint64_t)(lm) << 56) | ((uint64_t)(payload) & 0x00ffffffffffffffULL))
 #ifndef PV_CACHE_BUCKET
-#define PV_CACHE_BUCKET 0 // 1: a key probes the aligned 4-entry bucket of its hash, read with two 16-B loads
+#define PV_CACHE_BUCKET 1 // a key probes the aligned 4-entry bucket of its hash, read with two 16-B loads (0: four
+                          // dependent single-entry probes; C3 DNS pass 1024 -> 997 us, C4 498 -> 484, profiles/r4/ab)
 #endif
 template <int N>
 struct KeyCache {
@@ -3393,7 +3394,8 @@ __device__ __forceinline__ void comb_count(PV_CREF(PvParams) P, St &S, uint64_t 
     if (!(S.tb[r] & bit)) atomicOr(&S.tb[r], bit);
 }
 #ifndef PV_CB_BUCKET
-#define PV_CB_BUCKET 0 // tuning: 1 probes aligned 4-entry buckets (two 16-B LDS reads each) instead of single entries
+#define PV_CB_BUCKET 1 // probe aligned 4-entry buckets (two 16-B LDS reads each), at most 4 (0: 16 dependent
+                       // single-entry probes; C3 combine 307 -> 271 us, C4 229 -> 216, profiles/r4/ab)
 #endif
 // one aligned 4-entry bucket of the combine table: match or claim; false = the bucket is full of
 // other keys
