@@ -155,6 +155,13 @@ def main():
                          "step_traffic": prof.get("hbm_bytes_per_step"),
                          "traffic_source": prof.get("source")},
         }
+        tr = prof.get("hbm_bytes_per_launch")
+        if tr:
+            # the Net pass's counter bandwidth next to the algorithmic one: on C4 the pass reads the
+            # headers and skips payloads, so B / t exceeds what HBM delivered (frac > 1 there)
+            ca = tr / (kernel_ms * 1e-3) / 1e9
+            line["roofline"]["counter_achieved"] = round(ca, 1)
+            line["roofline"]["counter_frac"] = round(ca / HBM_PEAK_GBS, 4)
         if args.read_ceiling:
             line["read_ceiling_gbs"] = read_ceiling(d_recs, used)
         if args.e2e and world == 1:
