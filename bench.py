@@ -230,8 +230,9 @@ def bench_stream(args, world: int, rank: int, local: int, device):
         h.synchronize()
         t2 = time.perf_counter()
         kms, launches = h.kernel_timing()
+        ing = h.ingest_timing(reset=True)
         if it >= args.warmup:
-            times.append((t1 - t0, t2 - t1, kms))
+            times.append((t1 - t0, t2 - t1, kms, ing))
         events = h.window_json(5, merged=True)["packets"]["events"] if it == args.warmup + args.steps - 1 else None
         h.close()
     if registered:
@@ -257,6 +258,10 @@ def bench_stream(args, world: int, rank: int, local: int, device):
                        "bytes_per_record": round(per_rec, 2), "window_events_5m": events,
                        "host_memory": "page-locked (pv_host_register)" if registered else "pageable",
                        "parallelism": f"dp{world} (contiguous shards, global period plan, merge_window)"},
+            # pv_process_host's own split, ms (rank 0, last step): waiting for a piece's index (H2D
+            # landed + device index), the batches' device work with their status read-backs
+            "ingest_ms": {"index_wait": round(times[-1][3][1], 1), "device": round(times[-1][3][3], 1),
+                          "staging_copy": round(times[-1][3][0], 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "pv_net_kernel",
                          "kernel_ms_total": round(kernel_ms, 3), "note": "Net-pass time summed over the shard's chunks"},

@@ -3911,7 +3911,7 @@ int device_index(pv_ctx *c, pv_ctx::Stage &st, const uint8_t *d_base, uint32_t f
     if (!hip_ok(e = hipMemcpyAsync(d, st.h_ix, sizeof X, hipMemcpyHostToDevice, s)) ||
         !hip_ok(e = hipMemsetAsync(X.status, 0, 16, s)))
         return c->hipfail(e, "device index");
-    hipLaunchKernelGGL(pv_ix_guess, g, b, 0, s, dX);
+    hipLaunchKernelGGL(pv_ix_guess, dim3((nseg + 3) / 4), dim3(256), 0, s, dX); // a wave per segment
     uint32_t src = 0;
     bool settled = false;
     for (int pass = 0; pass < 64 && !settled; pass++) {

@@ -89,26 +89,119 @@ __device__ __forceinline__ uint64_t seg_hi(const PvIxParams &X, uint32_t s) { re
 
 } // namespace
 
-extern "C" __global__ void pv_ix_guess(const PvIxParams *__restrict__ Xp)
+// pv_ix_guess stages its segment, and the first header past it, in LDS: one wave per segment
+#define PV_IX_WIN (PV_IX_SEG + 64)
+#define PV_IX_WAVES 4
+
+namespace {
+
+// 16 bytes at byte o of a staged segment, as four little-endian words (five aligned LDS
+// reads and byte alignment, not sixteen byte reads)
+__device__ __forceinline__ void win_hdr(const uint32_t *w, uint32_t o, uint32_t &sec, uint32_t &frac, uint32_t &cl,
+                                        uint32_t &len)
+{
+    const uint32_t a = o >> 2, sh = o & 3;
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) d[k] = w[a + k];
+    sec = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+    frac = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+    cl = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+    len = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+}
+__device__ __forceinline__ uint32_t win_caplen(const uint32_t *w, uint32_t o)
+{
+    const uint32_t a = (o + 8) >> 2, sh = (o + 8) & 3;
+    return __builtin_amdgcn_alignbyte(w[a + 1], w[a], sh);
+}
+
+// plausible() with the headers inside the staged window [lo, lo + PV_IX_WIN) read from LDS
+__device__ bool plausible_w(const PvIxParams &X, const uint32_t *w, uint64_t lo, uint64_t p)
+{
+    for (int k = 0; k < 4; k++) {
+        if (p == X.bytes) return true;
+        if (p + 16 > X.bytes) return k > 0;
+        uint32_t sec, frac, cl, len;
+        if (p + 20 <= lo + PV_IX_WIN) win_hdr(w, (uint32_t)(p - lo), sec, frac, cl, len);
+        else hdr(X.recs, p, sec, frac, cl, len);
+        const uint32_t dsec = sec > X.sec0 ? sec - X.sec0 : X.sec0 - sec;
+        if (dsec > 86400 || cl > (256u << 10) || cl > len || frac >= X.frac_lim) return false;
+        if (p + 16 + (uint64_t)cl > X.bytes) return k > 0;
+        p += 16 + (uint64_t)cl;
+    }
+    return true;
+}
+
+// walk() with the caplens inside the staged window read from LDS
+__device__ uint64_t walk_w(const PvIxParams &X, const uint32_t *w, uint64_t lo, uint64_t p, uint64_t hi, uint32_t &n)
+{
+    n = 0;
+    while (p < hi) {
+        if (p + 16 > X.bytes) return p | PV_IX_STOP;
+        const uint32_t cl = p + 16 <= lo + PV_IX_WIN ? win_caplen(w, (uint32_t)(p - lo)) : caplen_at(X.recs, p);
+        if (p + 16 + (uint64_t)cl > X.bytes) return p | PV_IX_STOP;
+        n++;
+        p += 16 + (uint64_t)cl;
+    }
+    return p;
+}
+
+} // namespace
+
+// One wave per segment: the segment is staged in LDS with 16-B loads, the lanes test 64
+// consecutive candidate offsets per round (the first plausible one by ballot, so the guess is
+// the sequential scan's), and lane 0 walks the segment from LDS. A record start lies within
+// the first record length of the segment, so a round or a few settle the guess.
+extern "C" __global__ void __launch_bounds__(64 * PV_IX_WAVES) pv_ix_guess(const PvIxParams *__restrict__ Xp)
 {
     const PvIxParams X = *Xp;
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= X.nseg) return;
-    const uint64_t lo = seg_lo(X, s), hi = seg_hi(X, s);
-    uint64_t p = s ? lo : X.first;
+    __shared__ uint4 win[PV_IX_WAVES][PV_IX_WIN / 16 + 1]; // + 1: win_hdr's fifth word
+    const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const uint32_t s = blockIdx.x * PV_IX_WAVES + wv;
+    const bool live = s < X.nseg;
+    const uint64_t lo = seg_lo(X, s);
+    constexpr uint32_t NQ = PV_IX_WIN / 16, QR = (NQ + 63) / 64;
+    if (live) {
+        // bytes past X.bytes are staged as they lie (the buffer's pad); every test is bounded by X.bytes
+        uint4 v[QR];
+#pragma unroll
+        for (uint32_t u = 0; u < QR; u++) {
+            const uint32_t q = ln + u * 64;
+            if (q < NQ && lo + q * 16 < X.bytes) v[u] = *reinterpret_cast<const uint4 *>(X.recs + lo + q * 16);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < QR; u++) {
+            const uint32_t q = ln + u * 64;
+            if (q < NQ && lo + q * 16 < X.bytes) win[wv][q] = v[u];
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(win[wv]);
+    const uint64_t hi = seg_hi(X, s);
+    uint64_t p = X.first;
     if (s > 0) {
-        while (p < hi && !plausible(X, p)) p++;
-        if (p >= hi) {
-            X.start[s] = PV_IX_NONE;
-            X.cnt[s] = 0;
-            X.exit[0][s] = PV_IX_NONE;
+        p = PV_IX_NONE;
+        for (uint64_t b = lo; b < hi; b += 64) {
+            const uint64_t q = b + ln;
+            const uint64_t m = __ballot(q < hi && plausible_w(X, w, lo, q));
+            if (m) { p = b + __builtin_ctzll(m); break; }
+        }
+        if (p == PV_IX_NONE) {
+            if (ln == 0) {
+                X.start[s] = PV_IX_NONE;
+                X.cnt[s] = 0;
+                X.exit[0][s] = PV_IX_NONE;
+            }
             return;
         }
     }
-    uint32_t n;
-    X.start[s] = p;
-    X.exit[0][s] = walk(X, p, hi, n);
-    X.cnt[s] = n;
+    if (ln == 0) {
+        uint32_t n;
+        X.start[s] = p;
+        X.exit[0][s] = walk_w(X, w, lo, p, hi, n);
+        X.cnt[s] = n;
+    }
 }
 
 // one validation pass: exit[src] -> exit[src ^ 1]
@@ -156,26 +249,58 @@ extern "C" __global__ void pv_ix_fix(const PvIxParams *__restrict__ Xp, uint32_t
     eout[s] = cur;
 }
 
-// exclusive prefix of the segment counts (one workgroup of 1024)
+// exclusive prefix of the segment counts (one workgroup of 1024): tiles of 8192 counts staged
+// in LDS with coalesced loads, each thread summing eight consecutive counts, a wave-shuffle scan
+// of the sums, and coalesced stores of the bases
 extern "C" __global__ void __launch_bounds__(1024) pv_ix_scan(const PvIxParams *__restrict__ Xp)
 {
     const PvIxParams X = *Xp;
-    __shared__ uint32_t part[1024];
-    const uint32_t per = (X.nseg + 1023) / 1024;
-    const uint32_t a = threadIdx.x * per, b = min(X.nseg, a + per);
-    uint32_t sum = 0;
-    for (uint32_t s = a; s < b; s++) sum += X.cnt[s];
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-        const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+    constexpr uint32_t PER = 8, T = PER * 1024;
+    __shared__ uint32_t tile[T + T / 32]; // one pad word per 32: a thread's eight counts are not all in one bank
+    __shared__ uint32_t ws[16];
+    const uint32_t t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    auto at = [](uint32_t i) { return i + i / 32; };
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < X.nseg; t0 += T) {
+        uint32_t v[PER];
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = t0 + u * 1024 + t;
+            v[u] = i < X.nseg ? X.cnt[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) tile[at(u * 1024 + t)] = v[u];
         __syncthreads();
-        part[threadIdx.x] += v;
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) { v[u] = tile[at(t * PER + u)]; sum += v[u]; }
+        uint32_t x = sum;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (ln >= o) x += y;
+        }
+        if (ln == 63) ws[wv] = x;
         __syncthreads();
+        uint32_t run = carry + x - sum, total = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint32_t z = ws[k];
+            if (k < wv) run += z;
+            total += z;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) { tile[at(t * PER + u)] = run; run += v[u]; }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = t0 + u * 1024 + t;
+            if (i < X.nseg) X.base[i] = tile[at(u * 1024 + t)];
+        }
+        carry += total;
+        __syncthreads(); // tile and ws are the next tile's
     }
-    uint32_t run = part[threadIdx.x] - sum;
-    for (uint32_t s = a; s < b; s++) { X.base[s] = run; run += X.cnt[s]; }
-    if (threadIdx.x == 1023) X.base[X.nseg] = part[1023];
+    if (t == 0) X.base[X.nseg] = carry;
 }
 
 extern "C" __global__ void pv_ix_write(const PvIxParams *__restrict__ Xp)
