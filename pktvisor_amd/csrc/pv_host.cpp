@@ -622,7 +622,8 @@ struct pv_ctx {
         uint32_t *d_offs = nullptr;
         uint8_t *h_stage = nullptr;         // pinned staging of a pageable source
         hipEvent_t landed = nullptr;
-    } ring[3];
+    } ring[8];
+    uint32_t ring_n = 4; // slots in use (PV_INGEST_RING, 3..8): the producer runs ring_n - 2 pieces ahead
     hipStream_t copy_stream2 = nullptr;
     std::unique_ptr<pvi::Pool> pool;
     Stage stage[2];
@@ -3846,6 +3847,7 @@ int ingest_setup(pv_ctx *c)
     if (const char *v = getenv("PV_INGEST_CHUNK_MB")) chunk = std::max<size_t>(1, strtoull(v, nullptr, 10)) << 20;
     c->stage_recs = std::min<uint64_t>(c->max_records, chunk / 16 + 1);
     c->stage_bytes = chunk;
+    if (const char *v = getenv("PV_INGEST_RING")) c->ring_n = (uint32_t)std::min<unsigned long>(8, std::max<unsigned long>(3, strtoul(v, nullptr, 10)));
     c->pool.reset(new pvi::Pool(pvi::default_threads()));
     if (!hip_ok(e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking))) return c->hipfail(e, "copy stream");
     for (auto &st : c->stage) {
@@ -4452,7 +4454,7 @@ int pv_dnstap_count(const uint8_t *buf, size_t bytes, uint32_t *frames, uint32_t
 
 // Host-memory path with the record index on the device. The blob is cut into fixed
 // chunk-sized pieces in host order, so their H2D copies stream back to back (a producer
-// thread, two copy streams, a ring of three device buffers of two chunks each) without
+// thread, two copy streams, a ring of ring_n device buffers of two chunks each) without
 // waiting on any index. The calling thread, per piece: moves the previous batch's tail (the
 // records after its last ts_sec cut) in front of the piece on the device, indexes the joined
 // run there (pv_index.hip), cuts it at its last ts_sec boundary and runs the batch. The host
@@ -4462,7 +4464,9 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
 {
     const size_t L = c->stage_bytes; // a multiple of 256: runs start 256-B aligned (+ first)
     hipError_t e;
-    for (auto &r : c->ring) {
+    const uint32_t NR = c->ring_n;
+    for (uint32_t q = 0; q < NR; q++) {
+        pv_ctx::Ring &r = c->ring[q];
         if (r.d_buf) continue;
         if (!hip_ok(e = hipMalloc(&r.d_buf, 2 * L + PV_RECS_PAD)) || !hip_ok(e = hipMalloc(&r.d_offs, c->stage_recs * 4)) ||
             !hip_ok(e = hipEventCreateWithFlags(&r.landed, hipEventDisableTiming)) ||
@@ -4476,13 +4480,13 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
         return c->hipfail(e, "copy stream");
     const bool pinned = host_pinned(recs);
     if (!pinned)
-        for (auto &r : c->ring)
-            if (!r.h_stage && !hip_ok(e = hipHostMalloc((void **)&r.h_stage, L, hipHostMallocDefault)))
+        for (uint32_t q = 0; q < NR; q++)
+            if (!c->ring[q].h_stage && !hip_ok(e = hipHostMalloc((void **)&c->ring[q].h_stage, L, hipHostMallocDefault)))
                 return c->hipfail(e, "ingest staging");
     const uint64_t npieces = (bytes + L - 1) / L;
-    // producer: piece p's copy into ring slot p % 3 at offset L. Slot p % 3 last held run
-    // p - 3, whose batches are done and whose tail run p - 2 has moved out: issued once the
-    // consumer has finished run p - 2 (freed > p - 3). The consumer synchronises its stream
+    // producer: piece p's copy into ring slot p % NR at offset L. Slot p % NR last held run
+    // p - NR, whose batches are done and whose tail run p - NR + 1 has moved out: issued once the
+    // consumer has finished run p - NR + 1 (freed > p - NR), so up to NR - 2 pieces ahead of it. The consumer synchronises its stream
     // after each run, so the host-side order is the device-side order.
     std::mutex mu;
     std::condition_variable cv;
@@ -4494,10 +4498,10 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
         for (uint64_t k = 0; k < npieces; k++) {
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return abort || k < freed + 3; });
+                cv.wait(lk, [&] { return abort || k < freed + NR; });
                 if (abort) return;
             }
-            pv_ctx::Ring &r = c->ring[k % 3];
+            pv_ctx::Ring &r = c->ring[k % NR];
             const size_t len = std::min(L, bytes - k * L);
             const uint8_t *src = recs + k * L;
             if (!pinned) {
@@ -4532,7 +4536,7 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
             cv.wait(lk, [&] { return abort || issued > k; });
             if (abort) break;
         }
-        pv_ctx::Ring &r = c->ring[k % 3];
+        pv_ctx::Ring &r = c->ring[k % NR];
         const size_t len = std::min(L, bytes - k * L);
         const bool last_piece = k + 1 == npieces;
         // the run: the tail at [L - tail, L), the piece at [L, L + len); b is 256-B aligned and
@@ -4604,14 +4608,14 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
         }
         {
             std::lock_guard<std::mutex> g(mu);
-            freed = k; // slot (k - 1) % 3 is free: its tail has moved into this run
+            freed = k; // slot (k - 1) % NR is free: its tail has moved into this run
             cv.notify_all();
         }
     }
     {
         std::lock_guard<std::mutex> g(mu);
         if (rc) abort = true;
-        freed = npieces + 3;
+        freed = npieces + NR;
         cv.notify_all();
     }
     th.join();

@@ -61,11 +61,12 @@ def test_device_index_bench_shapes(handler, cfg, n):
     check(handler, synth.pcap_bytes(cfg, n)[24:])
 
 
-@pytest.mark.parametrize("chunk_mb", ["1", "3"])
-def test_ingest_device_index_parity(oracle, monkeypatch, chunk_mb):
-    """pv_process_host with the device index (small chunks: many cuts at ts_sec boundaries)
-    equals the oracle's single pass"""
+@pytest.mark.parametrize("chunk_mb,ring", [("1", "4"), ("3", "4"), ("1", "3"), ("1", "8")])
+def test_ingest_device_index_parity(oracle, monkeypatch, chunk_mb, ring):
+    """pv_process_host with the device index (small chunks: many cuts at ts_sec boundaries;
+    ring depths 3..8: the producer 1..6 pieces ahead) equals the oracle's single pass"""
     monkeypatch.setenv("PV_INGEST_CHUNK_MB", chunk_mb)
+    monkeypatch.setenv("PV_INGEST_RING", ring)
     pcap = synth.pcap_bytes(4, 300_000, ts_step_us=700)
     recs = pcap[24:]
     idx = pa.RecordIndex(recs)
