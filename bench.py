@@ -210,9 +210,12 @@ def bench_stream(args, world: int, rank: int, local: int, device):
         idx = pa.RecordIndex(recs, max_records=hi - lo, threads=16)
     start_sec = synth.T0_US // 1000000
     times = []
+    # one context for every step, reset between them outside the timed region (as C2-C4 steps are):
+    # its device buffers, ingest ring and index state are allocated once, by the first step
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=min(hi - lo, 16_000_000) or 1,
+                      device=local)
     for it in range(args.warmup + args.steps):
-        h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=min(hi - lo, 16_000_000) or 1,
-                          device=local)
+        h.reset()
         h.set_global_base(lo)
         if world > 1:
             dist.barrier()
@@ -234,7 +237,7 @@ def bench_stream(args, world: int, rank: int, local: int, device):
         if it >= args.warmup:
             times.append((t1 - t0, t2 - t1, kms, ing))
         events = h.window_json(5, merged=True)["packets"]["events"] if it == args.warmup + args.steps - 1 else None
-        h.close()
+    h.close()
     if registered:
         lib.pv_host_unregister(buf.ctypes.data)
     parse = float(np.median([t[0] for t in times]))
@@ -261,7 +264,7 @@ def bench_stream(args, world: int, rank: int, local: int, device):
             # pv_process_host's own split, ms (rank 0, last step): waiting for a piece's index (H2D
             # landed + device index), the batches' device work with their status read-backs
             "ingest_ms": {"index_wait": round(times[-1][3][1], 1), "device": round(times[-1][3][3], 1),
-                          "staging_copy": round(times[-1][3][0], 1)},
+                          "staging_copy": round(times[-1][3][0], 1), "h2d_issue": round(times[-1][3][2], 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "pv_net_kernel",
                          "kernel_ms_total": round(kernel_ms, 3), "note": "Net-pass time summed over the shard's chunks"},

@@ -631,6 +631,10 @@ struct pv_ctx {
     uint64_t stage_recs = 0;  // records per chunk
     hipStream_t copy_stream = nullptr;
     double ingest_ms[4] = {0, 0, 0, 0}; // host copy, index, H2D issue, device processing (pv_ingest_timing)
+    // PV_HOST_PROF: host wall time between marks of the ingest loop and the batch (HP), printed by pv_destroy
+    bool hprof_on = getenv("PV_HOST_PROF") != nullptr;
+    double hprof[10] = {};
+    std::chrono::steady_clock::time_point hp_t = std::chrono::steady_clock::now();
     // window state: the Net and DNS managers shift independently
     Window net, dns;
     bool started = false, ended = false;
@@ -754,6 +758,16 @@ struct pv_ctx {
         return fail(PV_EHIP, "%s: %s", what, hipGetErrorString(e));
     }
 };
+
+// PV_HOST_PROF mark k: host time since the previous mark goes to hprof[k]
+#define HP(k)                                                                                      \
+    do {                                                                                           \
+        if (c->hprof_on) {                                                                         \
+            const auto n_ = std::chrono::steady_clock::now();                                      \
+            c->hprof[k] += std::chrono::duration<double, std::milli>(n_ - c->hp_t).count();        \
+            c->hp_t = n_;                                                                          \
+        }                                                                                          \
+    } while (0)
 
 namespace {
 
@@ -2392,6 +2406,10 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
 
 void pv_destroy(pv_ctx *c)
 {
+    if (c && c->hprof_on)
+        fprintf(stderr, "pv_hostprof ms: wait=%.1f index=%.1f cut=%.1f shifts=%.1f kernels=%.1f tcp=%.1f pairs=%.1f tail=%.1f sync=%.1f loop=%.1f\n",
+                c->hprof[0], c->hprof[1], c->hprof[2], c->hprof[3], c->hprof[4], c->hprof[5], c->hprof[6], c->hprof[7],
+                c->hprof[8], c->hprof[9]);
     if (!c) return;
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
@@ -3632,6 +3650,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "kernel execution");
     memcpy(status, c->h_status, sizeof status);
+    HP(4);
     {
         float ms = 0;
         if (hipEventElapsedTime(&ms, c->ev_start, c->ev_stop) == hipSuccess) { c->kernel_ms += ms; c->kernel_launches++; }
@@ -3710,9 +3729,11 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             fprintf(stderr, "\n");
         }
     }
+    HP(5);
     if (int rc = pair_stage(c, P, status[ST_NEV], status[ST_NKEYS], status[ST_NRESP], n, st,
                             (uint64_t)(grid + gt) * P.wt_per_block * 64u))
         return rc;
+    HP(6);
     // top_slow updates of the transaction stage (only when it ran)
     if ((status[ST_NEV] || c->n_pend) && P.want_events)
         if (int rc = drain_overflow(c, st)) return rc;
@@ -3725,7 +3746,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         c->dns_shift_ord.emplace_back(sh.sec, c->dns.ordinal);
     }
     c->records_seen += n;
-    return purge_tables(c, st);
+    const int prc = purge_tables(c, st);
+    HP(7);
+    return prc;
 }
 
 // Both managers' shifts of a batch (Net from the record seconds, DNS from the prescan bits
@@ -3802,6 +3825,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     ensure_started(c, info->first_sec, info->first_nsec);
     std::vector<Shift> nsh, dsh;
     if (int rc = batch_shifts(c, d_recs, d_offs, info, sc_idx, sc_sec, st, nsh, dsh)) return rc;
+    HP(3);
     // spans of at most PV_MAX_SHIFTS shifts of each manager, cut at the shifting record
     uint64_t a = 0;
     size_t ni = 0, di = 0;
@@ -4012,6 +4036,7 @@ bool host_pinned(const void *p)
     }
     return a.type == hipMemoryTypeHost;
 }
+
 
 double ms_since(std::chrono::steady_clock::time_point t0)
 {
@@ -4511,8 +4536,11 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
                 c->ingest_ms[0] += ms_since(t1);
             }
             hipStream_t cs = (k & 1) ? c->copy_stream2 : c->copy_stream;
-            if (!hip_ok(e = hipMemcpyAsync(r.d_buf + L, src, len, hipMemcpyHostToDevice, cs)) ||
-                !hip_ok(e = hipEventRecord(r.landed, cs))) {
+            const auto ti = std::chrono::steady_clock::now();
+            const bool ok = hip_ok(e = hipMemcpyAsync(r.d_buf + L, src, len, hipMemcpyHostToDevice, cs)) &&
+                            hip_ok(e = hipEventRecord(r.landed, cs));
+            c->ingest_ms[2] += ms_since(ti); // host time the copy's issue takes (a blocking copy shows here)
+            if (!ok) {
                 std::lock_guard<std::mutex> g(mu);
                 prod_rc = PV_EHIP;
                 prod_err = std::string("H2D: ") + hipGetErrorString(e);
@@ -4536,6 +4564,7 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
             cv.wait(lk, [&] { return abort || issued > k; });
             if (abort) break;
         }
+        HP(0);
         pv_ctx::Ring &r = c->ring[k % NR];
         const size_t len = std::min(L, bytes - k * L);
         const bool last_piece = k + 1 == npieces;
@@ -4559,6 +4588,7 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
             if (ix > 0 && (rc = host_index_run(c, st, b, first, hf, end, r.d_offs, &capped))) break;
             pv_index_info info = st.info;
             c->ingest_ms[1] += ms_since(t0);
+            HP(1);
             const bool more = !last_piece || capped; // records follow this batch
             if (info.n_records == 0) {
                 if (!last_piece && end - first >= L) { rc = c->fail(PV_ECAPACITY, "record larger than the ingest chunk"); break; }
@@ -4586,8 +4616,10 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
                 capped = true;
             }
             auto t2 = std::chrono::steady_clock::now();
+            HP(2);
             rc = pv_process_device(c, b, r.d_offs, &info, st.sci.data(), st.scs.data(), nullptr);
             if (!rc) rc = pv_synchronize(c);
+            HP(8);
             c->ingest_ms[3] += ms_since(t2);
             if (rc) break;
             t0 = std::chrono::steady_clock::now();
@@ -4611,6 +4643,7 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
             freed = k; // slot (k - 1) % NR is free: its tail has moved into this run
             cv.notify_all();
         }
+        HP(9);
     }
     {
         std::lock_guard<std::mutex> g(mu);

@@ -79,3 +79,25 @@ def test_ingest_device_index_parity(oracle, monkeypatch, chunk_mb, ring):
         h.close()
     ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5)
     assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_ingest_reset_reuses_ring(oracle, monkeypatch):
+    """One context, pv_reset between two passes of the same stream (bench --config 5's steps): the
+    ingest ring, index state and device tables carry over, the window restarts; both passes equal
+    the oracle's single pass"""
+    monkeypatch.setenv("PV_INGEST_CHUNK_MB", "1")
+    monkeypatch.setenv("PV_INGEST_RING", "6")
+    pcap = synth.pcap_bytes(4, 200_000, ts_step_us=700)
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5)
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=1 << 20)
+    try:
+        for _ in range(2):
+            h.reset()
+            h.process_host(recs)
+            h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+            gpu = {"5m": h.window_json(5, merged=True)}
+            assert diff(gpu, ref) is None, diff(gpu, ref)
+    finally:
+        h.close()
