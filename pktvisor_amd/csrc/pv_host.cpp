@@ -160,6 +160,8 @@ extern "C" __global__ void pv_topn_combine_r12(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
 extern "C" __global__ void pv_net2_kernel(const PvParams *P);
 extern "C" __global__ void pv_ix_guess(const PvIxParams *X);
+extern "C" __global__ void pv_xv_hist(const PvXValue *v, const uint32_t *n_vals, uint32_t sg, uint32_t shift, PvXvSel sel,
+                                      uint32_t *hist);
 extern "C" __global__ void pv_ix_fix(const PvIxParams *X, uint32_t src);
 extern "C" __global__ void pv_ix_scan(const PvIxParams *X);
 extern "C" __global__ void pv_ix_write(const PvIxParams *X);
@@ -548,6 +550,7 @@ struct pv_ctx {
     void *d_sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     PvXValue *d_xvals = nullptr;
+    uint32_t *d_xvh = nullptr, *h_xvh = nullptr; // pv_xv_hist's histograms (device, pinned read-back)
     PvXValid *d_valid = nullptr;
     uint32_t *d_nvals = nullptr;  // [0] values appended since reset, [1] deferred slow candidates, [2] carried queries
     // DNS queries still open at the end of the last batch (double-buffered), in sort-key
@@ -633,7 +636,7 @@ struct pv_ctx {
     double ingest_ms[4] = {0, 0, 0, 0}; // host copy, index, H2D issue, device processing (pv_ingest_timing)
     // PV_HOST_PROF: host wall time between marks of the ingest loop and the batch (HP), printed by pv_destroy
     bool hprof_on = getenv("PV_HOST_PROF") != nullptr;
-    double hprof[10] = {};
+    double hprof[20] = {};
     std::chrono::steady_clock::time_point hp_t = std::chrono::steady_clock::now();
     // window state: the Net and DNS managers shift independently
     Window net, dns;
@@ -2002,10 +2005,12 @@ void dns2_metrics(pv_ctx *c, Sink &p, const HostBucket &b)
 // KLL inclusive rank rule on exact data
 uint64_t quantile_at(std::vector<uint64_t> v, double r)
 {
-    std::sort(v.begin(), v.end());
+    // the element of rank ceil(r n) - 1 of the sorted values: a selection, not a sort (a period
+    // shift's thresholds select over every transaction of the bucket that closed)
     uint64_t w = (uint64_t)std::ceil(r * (double)v.size());
     size_t idx = w == 0 ? 0 : (size_t)(w - 1);
     if (idx >= v.size()) idx = v.size() - 1;
+    std::nth_element(v.begin(), v.begin() + idx, v.end());
     return v[idx];
 }
 
@@ -2407,14 +2412,14 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
 void pv_destroy(pv_ctx *c)
 {
     if (c && c->hprof_on)
-        fprintf(stderr, "pv_hostprof ms: wait=%.1f index=%.1f cut=%.1f shifts=%.1f kernels=%.1f tcp=%.1f pairs=%.1f tail=%.1f sync=%.1f loop=%.1f\n",
+        fprintf(stderr, "pv_hostprof ms: wait=%.1f index=%.1f cut=%.1f shifts=%.1f kernels=%.1f tcp=%.1f pairs=%.1f tail=%.1f sync=%.1f loop=%.1f | launch=%.1f pend_in=%.1f sort=%.1f resolve=%.1f nv_sync=%.1f | X=%.1f memset=%.1f upload=%.1f launch=%.1f xsync=%.1f\n",
                 c->hprof[0], c->hprof[1], c->hprof[2], c->hprof[3], c->hprof[4], c->hprof[5], c->hprof[6], c->hprof[7],
-                c->hprof[8], c->hprof[9]);
+                c->hprof[8], c->hprof[9], c->hprof[14], c->hprof[10], c->hprof[11], c->hprof[12], c->hprof[13], c->hprof[15], c->hprof[16], c->hprof[17], c->hprof[18], c->hprof[19]);
     if (!c) return;
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     if (c->stream) { hipSetDevice(c->device); hipStreamSynchronize(c->stream); }
     void *ptrs[] = {c->d_sum, c->d_cpc, c->d_tkeys, c->d_tcnt, c->d_taux, c->d_arena, c->d_arena_top, c->d_events,
-                    c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
+                    c->d_xvh, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2, c->d_sort_tmp, c->d_xvals, c->d_status,
                     c->d_valid, c->d_nvals, c->d_params, c->d_xparams, c->d_ekeys, c->d_blk_events, c->d_mq, c->d_tpbuf, c->d_cb, c->d_cb_cnt, c->d_cb_h, c->d_nn, c->d_iplog, c->d_trash, c->d_mq_cnt, c->d_stamps, c->d_dq, c->d_dq_cnt,
                     c->stage[0].d_recs, c->stage[0].d_offs, c->stage[1].d_recs, c->stage[1].d_offs,
                     c->d_pend[0], c->d_pend[1], c->d_pkeys[0], c->d_pkeys[1], c->d_pvals[0], c->d_pvals[1], c->d_orph, c->d_orph_ord, c->d_sfx, c->d_psl,
@@ -3184,6 +3189,63 @@ int defer_slow(pv_ctx *c, const PvParams &P, hipStream_t st)
 // queries carried in; a batch of queries only just appends them to the carried list. Also the
 // heartbeat's DNS shift (nev_b = 0, one shift): the carried queries the shift purges time out
 // in the new live bucket, the rest carry on.
+// The rank values quantile_at(values, r) gives for each kind of PvXvSel among the transaction
+// values of slot sg: the device buffer's by radix selection there (pv_xv_hist, eight passes), and
+// those a drain already moved to the host (xvals_host ahead of the current device buffer's copy)
+// counted into the same histograms. have[k] = the kind has values. Synchronises.
+int xv_select(pv_ctx *c, uint32_t sg, double r, bool have[PV_XV_SEL], uint64_t out[PV_XV_SEL])
+{
+    hipError_t e;
+    if (!c->d_xvh && (!hip_ok(e = hipMalloc(&c->d_xvh, PV_XV_SEL * 256 * 4)) ||
+                      !hip_ok(e = hipHostMalloc((void **)&c->h_xvh, PV_XV_SEL * 256 * 4, hipHostMallocDefault))))
+        return c->hipfail(e, "threshold selection");
+    auto kind_of = [](uint32_t kind) {
+        return kind == XV_FROM_US ? 0 : kind == XV_TO_US ? 1 : (kind >= XV2_TIME && kind < XV2_TIME + 3) ? 2 + (int)(kind - XV2_TIME) : -1;
+    };
+    std::vector<uint64_t> hv[PV_XV_SEL];
+    const size_t host_only = c->xvals_host.size() - c->xvals_synced;
+    for (size_t i = 0; i < host_only; i++) {
+        const PvXValue &v = c->xvals_host[i];
+        const int k = v.slot == sg ? kind_of(v.kind) : -1;
+        if (k >= 0) hv[k].push_back(v.bits);
+    }
+    PvXvSel sel;
+    memset(&sel, 0, sizeof sel);
+    uint64_t rank[PV_XV_SEL] = {0};
+    for (int pass = 0; pass < 8; pass++) {
+        const uint32_t shift = 56 - 8 * pass;
+        if (!hip_ok(e = hipMemsetAsync(c->d_xvh, 0, PV_XV_SEL * 256 * 4, c->stream))) return c->hipfail(e, "threshold selection");
+        hipLaunchKernelGGL(pv_xv_hist, dim3(std::max<uint32_t>(1u, (uint32_t)c->cus * 2)), dim3(256), 0, c->stream, c->d_xvals, c->d_nvals, sg, shift, sel,
+                           c->d_xvh);
+        if (!hip_ok(e = hipGetLastError()) ||
+            !hip_ok(e = hipMemcpyAsync(c->h_xvh, c->d_xvh, PV_XV_SEL * 256 * 4, hipMemcpyDeviceToHost, c->stream)) ||
+            !hip_ok(e = hipStreamSynchronize(c->stream)))
+            return c->hipfail(e, "threshold selection");
+        const uint64_t hm = shift >= 56 ? 0ull : ~0ull << (shift + 8);
+        for (int k = 0; k < PV_XV_SEL; k++) {
+            uint64_t h[256];
+            for (int b = 0; b < 256; b++) h[b] = c->h_xvh[k * 256 + b];
+            for (uint64_t x : hv[k])
+                if ((x & hm) == (sel.prefix[k] & hm)) h[(x >> shift) & 255]++;
+            if (pass == 0) {
+                uint64_t total = 0;
+                for (int b = 0; b < 256; b++) total += h[b];
+                have[k] = total > 0;
+                const uint64_t w = (uint64_t)std::ceil(r * (double)total);
+                rank[k] = w == 0 ? 0 : std::min(w - 1, total ? total - 1 : 0);
+            }
+            if (!have[k]) continue;
+            uint64_t cum = 0;
+            int b = 0;
+            while (b < 255 && cum + h[b] <= rank[k]) cum += h[b++];
+            rank[k] -= cum;
+            sel.prefix[k] |= (uint64_t)b << shift;
+        }
+    }
+    for (int k = 0; k < PV_XV_SEL; k++) out[k] = sel.prefix[k];
+    return 0;
+}
+
 int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uint32_t nresp, uint64_t n, hipStream_t st,
                uint64_t ev_hi)
 {
@@ -3220,6 +3282,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
                                c->d_pkeys[c->pend_cur], c->d_pvals[c->pend_cur], np_in, nkeys);
             if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_pend_in");
         }
+        HP(10);
         // sorted: this batch's events and the carried queries first, the sentinel slots behind
         const uint32_t nev = nev_b + np_in;
         uint32_t threads = 256, blocks = (nev + threads - 1) / threads;
@@ -3227,6 +3290,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
         if (!hip_ok(e = pv_radix_sort_pairs(c->d_sort_tmp, &tmp, c->d_skeys, c->d_skeys2, c->d_svals, c->d_svals2,
                                              (size_t)nkeys + np_in, st)))
             return c->hipfail(e, "radix sort");
+        HP(11);
         PvXactParams X;
         memset(&X, 0, sizeof X);
         X.P = P;
@@ -3263,35 +3327,34 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
         X.tsfx = c->d_tsfx;
         X.edge_h = c->slow_defer ? c->edge_h : 0;
         X.orph_ord = c->slow_defer && c->dns2_groups ? c->d_orph_ord : nullptr; // DNS v2 stubs
-        if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st)) ||
-            !hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
+        HP(15);
+        if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st))) return c->hipfail(e, "parameter upload");
+        HP(16);
+        if (!hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
             return c->hipfail(e, "parameter upload");
+        HP(17);
         hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
+        HP(18);
         // (the resolve kernel also moves the queries still open to the carried list: pv_xact_carry's work)
         if (c->slow_defer) {
             if (int rc = defer_slow(c, P, st)) return rc;
         } else if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
             // on_period_shift: slow thresholds = p90 of the bucket that just closed
             // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
-            int rc = sync_xvals(c);
-            if (rc) return rc;
+            HP(19);
             for (uint32_t k = 1; k <= P.n_dshift; k++) {
                 const uint32_t sg = P.dslot_of[k - 1] | (c->gen[P.dslot_of[k - 1]] << 8);
-                std::vector<uint64_t> fr, to, t2[3];
-                for (auto &v : c->xvals_host) {
-                    if (v.slot != sg) continue;
-                    if (v.kind == XV_FROM_US) fr.push_back(v.bits);
-                    else if (v.kind == XV_TO_US) to.push_back(v.bits);
-                    else if (v.kind >= XV2_TIME && v.kind < XV2_TIME + 3) t2[v.kind - XV2_TIME].push_back(v.bits);
-                }
-                if (!fr.empty()) c->from90 = (float)quantile_at(fr, 0.90);
-                if (!to.empty()) c->to90 = (float)quantile_at(to, 0.90);
+                bool have[PV_XV_SEL];
+                uint64_t q[PV_XV_SEL];
+                if (int rc = xv_select(c, sg, 0.90, have, q)) return rc;
+                if (have[0]) c->from90 = (float)q[0];
+                if (have[1]) c->to90 = (float)q[1];
                 X.thr_from[k] = c->from90;
                 X.thr_to[k] = c->to90;
                 // DNS v2: per direction (dns/v2/DnsStreamHandler.h:440-453)
                 for (uint32_t d = 0; d < 3; d++) {
-                    if (!t2[d].empty()) c->p90_2[d] = (float)quantile_at(t2[d], 0.90);
+                    if (have[2 + d]) c->p90_2[d] = (float)q[2 + d];
                     X.thr2[k][d] = c->p90_2[d];
                 }
             }
@@ -3308,6 +3371,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
             hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st);
             hipStreamSynchronize(st);
         }
+        HP(12);
         uint32_t nv3[3] = {0, 0, 0};
         if (!hip_ok(e = hipMemcpyAsync(nv3, c->d_nvals, 12, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
@@ -3325,6 +3389,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
         c->pend_hi = npo;
         c->pend_cur ^= 1;
         c->pend_base = (int64_t)(c->records_seen + n) - 1;
+        HP(13);
     }
 
     return 0;
@@ -3646,6 +3711,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
 
     // ---- transactions: pair responses with queries (sort by key, then record index)
     uint32_t status[ST_WORDS];
+    HP(14);
     if (!hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_RB_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "kernel execution");

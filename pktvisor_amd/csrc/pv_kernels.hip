@@ -5043,6 +5043,37 @@ extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t
     return rocprim::radix_sort_pairs(tmp, *tmp_bytes, kin, kout, vin, vout, n, 0, 64, s);
 }
 
+// ------------------------------------------------------------------ period-shift thresholds
+// A DNS period shift sets the slow-transaction thresholds to the p90 of the transaction times of
+// the bucket that closed (dns/v1/DnsStreamHandler.h:259-266, v2 :440-453). The rank-r value of
+// each selected kind is found by radix selection over the device value buffer: a pass
+// histograms byte `shift` of the values of slot sg (slot | generation << 8) whose higher bytes
+// equal their kind's prefix so far; the host picks the byte holding the rank and the next pass
+// narrows to it. Eight passes over the buffer instead of copying it to the host and sorting.
+__device__ __forceinline__ int xv_sel_kind(uint32_t kind)
+{
+    return kind == XV_FROM_US ? 0 : kind == XV_TO_US ? 1 : (kind >= XV2_TIME && kind < XV2_TIME + 3) ? 2 + (int)(kind - XV2_TIME) : -1;
+}
+extern "C" __global__ void __launch_bounds__(256) pv_xv_hist(const PvXValue *__restrict__ v, const uint32_t *__restrict__ n_vals,
+                                                          uint32_t sg, uint32_t shift, PvXvSel sel, uint32_t *__restrict__ hist)
+{
+    __shared__ uint32_t h[PV_XV_SEL * 256];
+    for (uint32_t i = threadIdx.x; i < PV_XV_SEL * 256; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint32_t n = *n_vals;
+    const uint64_t hm = shift >= 56 ? 0ull : ~0ull << (shift + 8);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const PvXValue x = v[i];
+        if (x.slot != sg) continue;
+        const int k = xv_sel_kind(x.kind);
+        if (k < 0 || (x.bits & hm) != (sel.prefix[k] & hm)) continue;
+        atomicAdd(&h[k * 256 + (uint32_t)((x.bits >> shift) & 255)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < PV_XV_SEL * 256; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
 // ------------------------------------------------------------------ record gather (sharded top_slow)
 // The records of a list of batch record indices (idx[i * stride], PV_TCP_IDX: a TCP message
 // record of the batch's message arena), copied whole (16-B header + capture, 4-B padded) into

@@ -196,6 +196,12 @@ struct PvXValue {
     uint32_t kind;
 };
 
+// radix selection over the device value buffer (pv_xv_hist): the selected kinds' prefixes so far
+#define PV_XV_SEL 5 // XV_FROM_US, XV_TO_US, XV2_TIME + 0..2
+struct PvXvSel {
+    uint64_t prefix[PV_XV_SEL];
+};
+
 // a valid transaction whose period's slow threshold is not known yet
 struct PvXValid {
     uint32_t idx; // response record index within the batch (PV_TCP_IDX: a TCP message record)

@@ -1,0 +1,11 @@
+#!/bin/bash
+# device threshold selection: transaction/window parity tests, then C5 30M
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$(pwd); O=$R/gpurun_out/r4_sel; mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_windows.py tests/test_gpu_dns2.py tests/test_gpu_v2_outputs.py tests/test_gpu_index.py tests/test_gpu_dns2_sharded.py > $O/tests.log 2>&1 || { tail -25 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for cfg in "64 6" "128 4"; do
+  set -- $cfg
+  PV_HOST_PROF=1 PV_INGEST_CHUNK_MB=$1 PV_INGEST_RING=$2 timeout -k 10 300 python3 -u bench.py --config 5 --stream-records 30000000 --steps 2 --warmup 1 > $O/c5_$1_$2.log 2>&1 || { tail -5 $O/c5_$1_$2.log; exit 1; }
+  echo "chunk $1 ring $2"; grep pv_hostprof $O/c5_$1_$2.log; tail -1 $O/c5_$1_$2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['ingest_ms'])"
+done
