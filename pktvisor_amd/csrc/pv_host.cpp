@@ -165,7 +165,8 @@ extern "C" __global__ void pv_xv_hist(const PvXValue *v, const uint32_t *n_vals,
 extern "C" __global__ void pv_ix_fix(const PvIxParams *X, uint32_t src);
 extern "C" __global__ void pv_ix_scan(const PvIxParams *X);
 extern "C" __global__ void pv_ix_write(const PvIxParams *X);
-extern "C" __global__ void pv_ix_secs(const PvIxParams *X, uint32_t n);
+extern "C" __global__ void pv_ix_secs(const PvIxParams *X, uint32_t cap);
+extern "C" __global__ void pv_ix_cut(const PvIxParams *X);
 extern "C" __global__ void pv_topn_retry(const PvParams *P, const PvOvf *src, uint32_t n);
 extern "C" __global__ void pv_dns_tcp_filter(const PvParams *P);
 extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_t *theta_out);
@@ -616,6 +617,7 @@ struct pv_ctx {
         uint8_t *d_ix = nullptr;    // PvIxParams + arrays, one allocation
         PvIxParams *h_ix = nullptr; // pinned: params, then status / small read-backs
         uint32_t ix_nseg = 0;
+        uint32_t cut_o[2] = {0, 0}; // offsets of the records either side of the last ts_sec change
     };
     bool device_index = true; // PV_INGEST_INDEX=host selects the host walk
     // device-index ingest ring: raw chunks land at offset chunk of 2 x chunk buffers, the
@@ -3989,7 +3991,7 @@ int device_index(pv_ctx *c, pv_ctx::Stage &st, const uint8_t *d_base, uint32_t f
     X.exit[1] = (uint64_t *)take((size_t)nseg * 8);
     X.cnt = (uint32_t *)take((size_t)nseg * 4);
     X.base = (uint32_t *)take((size_t)(nseg + 1) * 4);
-    X.status = (uint32_t *)take(16);
+    X.status = (uint32_t *)take(32);
     X.sci = (uint32_t *)take(st.sci.size() * 4);
     X.scs = (uint32_t *)take(st.sci.size() * 4);
     X.offs = d_offs;
@@ -4001,28 +4003,52 @@ int device_index(pv_ctx *c, pv_ctx::Stage &st, const uint8_t *d_base, uint32_t f
     const dim3 g((nseg + 255) / 256), b(256);
     hipError_t e;
     if (!hip_ok(e = hipMemcpyAsync(d, st.h_ix, sizeof X, hipMemcpyHostToDevice, s)) ||
-        !hip_ok(e = hipMemsetAsync(X.status, 0, 16, s)))
+        !hip_ok(e = hipMemsetAsync(X.status, 0, 32, s)))
         return c->hipfail(e, "device index");
     hipLaunchKernelGGL(pv_ix_guess, dim3((nseg + 3) / 4), dim3(256), 0, s, dX); // a wave per segment
+    // one validation pass, then the scan, the offsets, the change points and the last change's
+    // neighbours, read back under one synchronisation: a pass that changed nothing (the guesses
+    // were right) settles the chain. Otherwise the passes run on, one read-back each, until they
+    // settle, and the rest runs again (its first run only wrote offsets of valid walks).
+    const uint32_t pre = 1024; // change points read back with the status; more in a second copy
+    const uint32_t secs_grid = (uint32_t)std::min<uint64_t>((c->stage_recs + 255) / 256, (uint64_t)c->cus * 8);
     uint32_t src = 0;
-    bool settled = false;
-    for (int pass = 0; pass < 64 && !settled; pass++) {
+    auto fix_pass = [&]() {
         hipMemsetAsync(X.status, 0, 4, s);
         hipLaunchKernelGGL(pv_ix_fix, g, b, 0, s, dX, src);
         src ^= 1;
-        if (!hip_ok(e = hipMemcpyAsync(h, X.status, 4, hipMemcpyDeviceToHost, s)) || !hip_ok(e = hipStreamSynchronize(s)))
-            return c->hipfail(e, "device index pass");
-        settled = h[0] == 0;
+    };
+    auto rest = [&]() -> hipError_t {
+        hipLaunchKernelGGL(pv_ix_scan, dim3(1), dim3(1024), 0, s, dX);
+        hipMemsetAsync(X.status + 1, 0, 28, s);
+        hipLaunchKernelGGL(pv_ix_write, g, b, 0, s, dX);
+        hipLaunchKernelGGL(pv_ix_secs, dim3(std::max(1u, secs_grid)), dim3(256), 0, s, dX, (uint32_t)c->stage_recs);
+        hipLaunchKernelGGL(pv_ix_cut, dim3(1), dim3(64), 0, s, dX);
+        hipError_t e2 = hipGetLastError();
+        if (e2 == hipSuccess) e2 = hipMemcpyAsync(h, X.status, 32, hipMemcpyDeviceToHost, s);
+        if (e2 == hipSuccess) e2 = hipMemcpyAsync(h + 8, X.base + nseg, 4, hipMemcpyDeviceToHost, s);
+        if (e2 == hipSuccess) e2 = hipMemcpyAsync(h + 10, X.exit[src] + nseg - 1, 8, hipMemcpyDeviceToHost, s);
+        if (e2 == hipSuccess) e2 = hipMemcpyAsync(h + 16, X.sci, pre * 4, hipMemcpyDeviceToHost, s);
+        if (e2 == hipSuccess) e2 = hipMemcpyAsync(h + 16 + st.sci.size(), X.scs, pre * 4, hipMemcpyDeviceToHost, s);
+        if (e2 == hipSuccess) e2 = hipStreamSynchronize(s);
+        return e2;
+    };
+    fix_pass();
+    if (!hip_ok(e = rest())) return c->hipfail(e, "device index");
+    if (h[0] != 0) {
+        bool settled = false;
+        for (int pass = 1; pass < 64 && !settled; pass++) {
+            fix_pass();
+            if (!hip_ok(e = hipMemcpyAsync(h, X.status, 4, hipMemcpyDeviceToHost, s)) || !hip_ok(e = hipStreamSynchronize(s)))
+                return c->hipfail(e, "device index pass");
+            settled = h[0] == 0;
+        }
+        if (!settled) return 1;
+        if (!hip_ok(e = rest())) return c->hipfail(e, "device index");
     }
-    if (!settled) return 1;
-    hipLaunchKernelGGL(pv_ix_scan, dim3(1), dim3(1024), 0, s, dX);
+    const uint64_t total = h[8];
     uint64_t chain_end = 0;
-    if (!hip_ok(e = hipMemcpyAsync(h, X.base + nseg, 4, hipMemcpyDeviceToHost, s)) ||
-        !hip_ok(e = hipMemcpyAsync(h + 2, X.exit[src] + nseg - 1, 8, hipMemcpyDeviceToHost, s)) ||
-        !hip_ok(e = hipStreamSynchronize(s)))
-        return c->hipfail(e, "device index scan");
-    const uint64_t total = h[0];
-    memcpy(&chain_end, h + 2, 8);
+    memcpy(&chain_end, h + 10, 8);
     const uint64_t n = std::min<uint64_t>(total, c->stage_recs);
     pv_index_info &info = st.info;
     memset(&info, 0, sizeof info);
@@ -4030,18 +4056,10 @@ int device_index(pv_ctx *c, pv_ctx::Stage &st, const uint8_t *d_base, uint32_t f
     info.n_records = n;
     info.bytes_used = chain_end & ~PV_IX_STOP;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(pv_ix_write, g, b, 0, s, dX);
-    hipLaunchKernelGGL(pv_ix_secs, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, dX, (uint32_t)n);
-    const uint32_t pre = 1024; // change points read back with the status; more in a second copy
-    if (!hip_ok(e = hipGetLastError()) ||
-        !hip_ok(e = hipMemcpyAsync(h, X.status, 16, hipMemcpyDeviceToHost, s)) ||
-        !hip_ok(e = hipMemcpyAsync(h + 4, X.offs + n - 1, 4, hipMemcpyDeviceToHost, s)) ||
-        !hip_ok(e = hipMemcpyAsync(h + 16, X.sci, pre * 4, hipMemcpyDeviceToHost, s)) ||
-        !hip_ok(e = hipMemcpyAsync(h + 16 + st.sci.size(), X.scs, pre * 4, hipMemcpyDeviceToHost, s)) ||
-        !hip_ok(e = hipStreamSynchronize(s)))
-        return c->hipfail(e, "device index read-back");
     const uint32_t nc = h[1];
-    const uint32_t last_off = h[4];
+    const uint32_t last_off = h[3];
+    st.cut_o[0] = h[5];
+    st.cut_o[1] = h[6];
     if (nc > st.sci.size()) return c->fail(PV_ECAPACITY, "more than %zu ts_sec changes in one ingest chunk", st.sci.size());
     if (nc > pre &&
         (!hip_ok(e = hipMemcpyAsync(h + 16, X.sci, (size_t)nc * 4, hipMemcpyDeviceToHost, s)) ||
@@ -4086,6 +4104,11 @@ int host_index_run(pv_ctx *c, pv_ctx::Stage &st, const uint8_t *d_base, uint32_t
     }
     for (uint64_t i = 0; i < n; i++) st.h_offs[i] += first;
     info.bytes_used += first;
+    if (info.n_sec_changes > 1 && info.n_sec_changes <= st.sci.size()) {
+        const uint32_t cut = st.sci[info.n_sec_changes - 1];
+        st.cut_o[0] = st.h_offs[cut - 1];
+        st.cut_o[1] = st.h_offs[cut];
+    }
     hipError_t e;
     if (n && (!hip_ok(e = hipMemcpyAsync(d_offs, st.h_offs, n * 4, hipMemcpyHostToDevice, c->stream)) ||
               !hip_ok(e = hipStreamSynchronize(c->stream))))
@@ -4666,12 +4689,7 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
             // reach the device in the same batch
             if (more && info.n_sec_changes > 1 && info.n_sec_changes <= st.sci.size()) {
                 const uint32_t cut = st.sci[info.n_sec_changes - 1];
-                uint32_t o[2];
-                if (!hip_ok(e = hipMemcpyAsync(o, r.d_offs + cut - 1, 8, hipMemcpyDeviceToHost, c->stream)) ||
-                    !hip_ok(e = hipStreamSynchronize(c->stream))) {
-                    rc = c->hipfail(e, "cut read-back");
-                    break;
-                }
+                const uint32_t o[2] = {st.cut_o[0], st.cut_o[1]}; // the offsets either side of the cut
                 info.n_records = cut;
                 info.bytes_used = o[1];
                 info.n_sec_changes -= 1;

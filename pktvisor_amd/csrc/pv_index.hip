@@ -316,28 +316,44 @@ extern "C" __global__ void pv_ix_write(const PvIxParams *__restrict__ Xp)
     }
 }
 
-// ts_sec change points (record i whose ts_sec differs from record i - 1's) and monotonicity
-extern "C" __global__ void pv_ix_secs(const PvIxParams *__restrict__ Xp, uint32_t n)
+// ts_sec change points (record i whose ts_sec differs from record i - 1's) and monotonicity,
+// over n = min(records indexed, cap) records (n read on the device: no read-back between the
+// scan and here). status: [1] change points, [2] out of order, [3] the last record's offset,
+// [4] the last change point
+extern "C" __global__ void pv_ix_secs(const PvIxParams *__restrict__ Xp, uint32_t cap)
 {
     const PvIxParams X = *Xp;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t p = X.offs[i];
-    const uint32_t sec = ((p & 3) == 0) ? *reinterpret_cast<const uint32_t *>(X.recs + p)
-                                         : (uint32_t)X.recs[p] | ((uint32_t)X.recs[p + 1] << 8) |
-                                               ((uint32_t)X.recs[p + 2] << 16) | ((uint32_t)X.recs[p + 3] << 24);
-    int64_t prev = -1;
-    if (i) {
-        const uint64_t q = X.offs[i - 1];
-        prev = ((q & 3) == 0) ? *reinterpret_cast<const uint32_t *>(X.recs + q)
-                              : (uint32_t)X.recs[q] | ((uint32_t)X.recs[q + 1] << 8) | ((uint32_t)X.recs[q + 2] << 16) |
-                                    ((uint32_t)X.recs[q + 3] << 24);
+    const uint32_t n = min(X.base[X.nseg], cap);
+    auto sec_at = [&](uint64_t p) -> uint32_t {
+        return ((p & 3) == 0) ? *reinterpret_cast<const uint32_t *>(X.recs + p)
+                              : (uint32_t)X.recs[p] | ((uint32_t)X.recs[p + 1] << 8) | ((uint32_t)X.recs[p + 2] << 16) |
+                                    ((uint32_t)X.recs[p + 3] << 24);
+    };
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t p = X.offs[i];
+        if (i == n - 1) X.status[3] = (uint32_t)p;
+        const uint32_t sec = sec_at(p);
+        const int64_t prev = i ? (int64_t)sec_at(X.offs[i - 1]) : -1;
+        if ((int64_t)sec == prev) continue;
+        if ((int64_t)sec < prev) atomicOr(&X.status[2], 1u);
+        atomicMax(&X.status[4], i);
+        const uint32_t k = atomicAdd(&X.status[1], 1u);
+        if (k < X.max_changes) {
+            X.sci[k] = i;
+            X.scs[k] = sec;
+        }
     }
-    if ((int64_t)sec == prev) return;
-    if ((int64_t)sec < prev) atomicOr(&X.status[2], 1u);
-    const uint32_t k = atomicAdd(&X.status[1], 1u);
-    if (k < X.max_changes) {
-        X.sci[k] = i;
-        X.scs[k] = sec;
+}
+
+// the offsets either side of the last change point (the ingest's cut at its last ts_sec
+// boundary): status[5] = offs[last - 1], status[6] = offs[last]
+extern "C" __global__ void pv_ix_cut(const PvIxParams *__restrict__ Xp)
+{
+    const PvIxParams X = *Xp;
+    if (threadIdx.x != 0) return;
+    const uint32_t k = X.status[4];
+    if (k > 0) {
+        X.status[5] = X.offs[k - 1];
+        X.status[6] = X.offs[k];
     }
 }
