@@ -495,6 +495,45 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
     if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns, key);
 }
 
+// global_add for pv_topn_merge's direct regions: a created entry's name goes to the new-name list
+// (pv_topn_names decodes it), as the LDS merge's do, instead of being decoded by this lane
+__device__ __noinline__ void global_add_nn(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
+{
+    const uint32_t metric = PV_KEY_METRIC(key);
+    if (metric == TM_DENSE_PORT || metric == TM_DENSE_QTYPE || metric == TM_DENSE_RCODE || metric == TM_IPV4) {
+        global_add(P, slot, key, w, rep);
+        return;
+    }
+    TPos t = tpos(P, slot, key);
+    int64_t created = -1;
+    bool done = false;
+    for (int probe = 0; probe < PV_PROBES && !done; probe++) {
+        uint64_t *kp = &P.tkeys[t.rbase + t.pos];
+        uint64_t k = __atomic_load_n(kp, __ATOMIC_RELAXED);
+        uint64_t add = w;
+        if (k == 0) {
+            const uint64_t stale = __atomic_load_n(&P.tcnt[t.rbase + t.pos], __ATOMIC_RELAXED);
+            asm volatile("" ::"v"((uint32_t)stale), "v"((uint32_t)(stale >> 32)) : "memory");
+            uint64_t prev = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)key);
+            if (prev == 0) { created = (int64_t)(t.rbase + t.pos); add = w - stale; }
+            k = prev == 0 ? key : prev;
+        }
+        if (k == key) {
+            atomicAdd((unsigned long long *)&P.tcnt[t.rbase + t.pos], (unsigned long long)add);
+            done = true;
+        } else {
+            t.pos = (t.pos + 1) & t.rmask;
+        }
+    }
+    if (!done) table_overflow(P, slot, key, w, rep, !P.tcp_pass);
+    if (created < 0) return;
+    const uint32_t tb = PV_TSLOT(slot, metric);
+    atomicAdd(&P.tab_live[tb], 1u);
+    const uint32_t g = atomicAdd(P.nn_cnt, 1u);
+    if (g < P.nn_cap) P.nn[g] = PvNewName{tb, rep, (uint64_t)created};
+    else P.taux[created] = write_name(P, slot, metric, rep, nullptr, key);
+}
+
 // ------------------------------------------------------------------ LDS key cache
 // Open-addressed key -> (count, min record index) cache shared by a workgroup's
 // waves. Keys carry their bucket slot in bits 60..63 (local metric ids are < 16), so
@@ -3312,7 +3351,9 @@ __device__ __forceinline__ void batched(uint64_t n, Ld ld, Body body)
     }
 }
 #define PV_E16(q) reinterpret_cast<const PV_G ulonglong2 *>(q)
-#define PV_MERGE_DIRECT 64 // regions with at most this many updates use global_add
+#ifndef PV_MERGE_DIRECT
+#define PV_MERGE_DIRECT 64 // regions with at most this many updates use global_add_nn
+#endif
 #define PV_W_IP4 (1u << 31)  // weight word of a combined IPv4 entry: flag | dir << 30 | card << 29 | count
 
 // CPC coupon of an IPv4 address (cpc_sketch update of the int32 address)
@@ -3757,7 +3798,7 @@ extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) pv_topn_merge(const 
                 if ((w >> 29) & 1)
                     cpc_min(P, s, ((w >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
             } else {
-                global_add(P, s, key, w, rep);
+                global_add_nn(P, s, key, w, rep);
             }
         }
         return;
