@@ -551,6 +551,7 @@ struct pv_ctx {
     void *d_sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     PvXValue *d_xvals = nullptr;
+    uint64_t xv_cap = 0; // values d_xvals holds (2 x max_records, doubled while it fits PV_XV_BUDGET_MB)
     uint32_t *d_xvh = nullptr, *h_xvh = nullptr; // pv_xv_hist's histograms (device, pinned read-back)
     PvXValid *d_valid = nullptr;
     uint32_t *d_nvals = nullptr;  // [0] values appended since reset, [1] deferred slow candidates, [2] carried queries
@@ -2026,7 +2027,7 @@ int sync_xvals(pv_ctx *c)
     if (!hip_ok(e = hipMemcpy(status, c->d_status, sizeof status, hipMemcpyDeviceToHost)) ||
         !hip_ok(e = hipMemcpy(&nv, c->d_nvals, 4, hipMemcpyDeviceToHost)))
         return c->hipfail(e, "status");
-    if (status[ST_FLAGS] & PVF_VALUES_FULL || nv > c->max_records * 2)
+    if (status[ST_FLAGS] & PVF_VALUES_FULL || nv > c->xv_cap)
         return c->fail(PV_ECAPACITY, "transaction value buffer full");
     if (nv > c->xvals_synced) {
         size_t old = c->xvals_host.size(), add = nv - c->xvals_synced;
@@ -2362,7 +2363,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         !hip_ok(e = hipMalloc(&c->d_skeys2, kc * 8)) ||
         !hip_ok(e = hipMalloc(&c->d_svals, kc * 4)) ||
         !hip_ok(e = hipMalloc(&c->d_svals2, kc * 4)) ||
-        !hip_ok(e = hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue))) ||
+        !hip_ok(e = (c->xv_cap = (uint64_t)mr * 2, hipMalloc(&c->d_xvals, (size_t)mr * 2 * sizeof(PvXValue)))) ||
         !hip_ok(e = hipMalloc(&c->d_valid, (size_t)mr * sizeof(PvXValid))) ||
         !hip_ok(e = hipMalloc(&c->d_nvals, 16)) ||
         // one read-back block: the status words, the tables' live counts, the two overflow
@@ -3311,7 +3312,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
         }
         X.vals = c->d_xvals;
         X.n_vals = c->d_nvals;
-        X.vals_cap = (uint32_t)(c->max_records * 2);
+        X.vals_cap = (uint32_t)c->xv_cap;
         X.valid = c->d_valid;
         X.n_valid = c->d_nvals + 1;
         X.pend = c->d_pend[c->pend_cur];
@@ -3379,12 +3380,27 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "carried queries");
         const uint32_t npo = nv3[2];
-        if (nv3[0] > c->max_records) {
-            // drain the device value buffer to the host copy: every batch then has the
-            // whole 2 x max_records capacity (at most two values per response)
-            if (int rc = sync_xvals(c)) return rc;
-            c->xvals_synced = 0;
-            if (!hip_ok(e = hipMemsetAsync(c->d_nvals, 0, 4, st))) return c->hipfail(e, "value buffer drain");
+        if (c->xv_cap - nv3[0] < c->max_records) {
+            // less than max_records of room: the device value buffer doubles while it stays
+            // within PV_XV_BUDGET_MB (HBM is plentiful; a copy inside HBM instead of a read-back
+            // of every value inside the stream), else it drains to the host copy and every batch
+            // then has the whole capacity (at most two values per response)
+            const uint64_t grow = c->xv_cap * 2;
+            const char *bv = getenv("PV_XV_BUDGET_MB");
+            const uint64_t budget = (bv ? strtoull(bv, nullptr, 10) : 4096ull) << 20;
+            PvXValue *nb = nullptr;
+            if (grow <= 0xffffffffull && grow * sizeof(PvXValue) <= budget && hip_ok(hipMalloc(&nb, grow * sizeof(PvXValue)))) {
+                if (!hip_ok(e = hipMemcpyAsync(nb, c->d_xvals, (size_t)nv3[0] * sizeof(PvXValue), hipMemcpyDeviceToDevice, st)) ||
+                    !hip_ok(e = hipStreamSynchronize(st)))
+                    return c->hipfail(e, "value buffer growth");
+                hipFree(c->d_xvals);
+                c->d_xvals = nb;
+                c->xv_cap = grow;
+            } else {
+                if (int rc = sync_xvals(c)) return rc;
+                c->xvals_synced = 0;
+                if (!hip_ok(e = hipMemsetAsync(c->d_nvals, 0, 4, st))) return c->hipfail(e, "value buffer drain");
+            }
         }
         if (npo > c->pend_cap) return c->fail(PV_ECAPACITY, "%u open DNS queries exceed the carried-list capacity", npo);
         c->n_pend = npo;
@@ -5855,7 +5871,7 @@ int edge_carry2(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, si
         X.P = P;
         X.vals = c->d_xvals;
         X.n_vals = c->d_nvals;
-        X.vals_cap = (uint32_t)(c->max_records * 2);
+        X.vals_cap = (uint32_t)c->xv_cap;
         X.valid = c->d_valid;
         X.n_valid = c->d_nvals + 1;
         X.trecs = (const uint8_t *)d[2];
