@@ -3,7 +3,7 @@
 # 100M, kernel stats C2-C4 and C5 (30M). Every GPU step has its own limit; the chain stops at the
 # first failure.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-R=$(pwd); O=$R/gpurun_out/r4_fin; mkdir -p $O
+R=$(pwd); O=$R/gpurun_out/${FIN_DIR:-r4_fin}; mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
 step tests
