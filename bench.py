@@ -80,12 +80,25 @@ def main():
     h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=n, device=local,
                       net_groups=args.net_groups, dns_groups=args.dns_groups)
     h.set_global_base(rank * n)
+    if world > 1:
+        # the library's own RCCL communicator: the merge runs device to device (pv_comm_*)
+        uid = [pa.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        h.comm_init(uid[0], world, rank)
+    merge_ms = []
 
     def step():
         h.reset()
         h.process_device(d_recs.data_ptr(), d_offs.data_ptr(), idx)
         if world > 1:
-            pvdist.reduce_handlers(h, device)
+            # the whole state merge every step (dist.merge_window): windows checked aligned, DNS
+            # shard edges, SUM / MIN all-reduce of the buckets, top-N entries to their region owners
+            # and merged there; the read view (names of the leading entries, quantiles) is
+            # assembled once after the timed steps (finalize_window, timed separately)
+            h.synchronize()
+            tm = time.perf_counter()
+            pvdist.merge_window(h, device, comm="pv", finalize=False)
+            merge_ms.append((time.perf_counter() - tm) * 1e3)
         else:
             h.synchronize()
 
@@ -116,6 +129,13 @@ def main():
     else:
         kernel_ms = kms / max(launches, 1)
 
+    finalize_ms = None
+    if world > 1:
+        # the merged read view, once (timed apart from the steps)
+        dist.barrier()
+        tf = time.perf_counter()
+        pvdist.finalize_window(h, comm="pv")
+        finalize_ms = (time.perf_counter() - tf) * 1e3
     # parity sanity on the final state (not timed)
     out = h.window_json(0, merged=False)
     events = out["packets"]["events"]
@@ -144,7 +164,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": WORKLOADS[args.config], "records_per_gpu": n,
                        "bytes_per_record": round(algo_bytes / n, 2), "handlers": "net v1 + dns v1 (default groups)",
-                       "parallelism": f"dp{world} (contiguous record shards, RCCL all-reduce of live buckets)"},
+                       "parallelism": f"dp{world} (record shards, per-step RCCL merge: bucket all-reduce + top-N owner exchange)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": prof.get("hbm_bytes_per_launch"),
                          "kernel": h.net_kernel_name(), "kernel_ms": round(kernel_ms, 4),
@@ -168,6 +188,13 @@ def main():
             line["e2e"] = end_to_end(h, buf[:used], n, max(3, args.steps // 4))
         if args.net_groups or args.dns_groups:
             line["groups"] = {"net": args.net_groups, "dns": args.dns_groups}
+        if world > 1:
+            line["merge"] = {"per_step_ms_median": round(float(np.median(merge_ms[-args.steps:])), 4),
+                             "finalize_ms": round(finalize_ms, 3),
+                             "what": "every step: pv_comm_allgather window check, DNS shard edges, pv_comm_allreduce_window "
+                                     "(SUM/MIN), pv_comm_merge_topn (top-N entries to region owners over RCCL, merged on "
+                                     "the device); once after the steps: finalize_window (leading entries + names, exact "
+                                     "distributed quantile selection)"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         print(json.dumps(line), flush=True)
@@ -214,6 +241,10 @@ def bench_stream(args, world: int, rank: int, local: int, device):
     # its device buffers, ingest ring and index state are allocated once, by the first step
     h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=min(hi - lo, 16_000_000) or 1,
                       device=local)
+    if world > 1:
+        uid = [pa.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        h.comm_init(uid[0], world, rank)
     for it in range(args.warmup + args.steps):
         h.reset()
         h.set_global_base(lo)
@@ -229,7 +260,7 @@ def bench_stream(args, world: int, rank: int, local: int, device):
         h.synchronize()
         t1 = time.perf_counter()
         if world > 1:
-            pvdist.merge_window(h, device)
+            pvdist.merge_window(h, device, comm="pv")
         h.synchronize()
         t2 = time.perf_counter()
         kms, launches = h.kernel_timing()

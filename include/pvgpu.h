@@ -104,12 +104,14 @@ typedef struct pv_config {
     uint32_t net2_groups;    /* Net v2 handler ("net", src/handlers/net/v2) attached next to v1: pv_net2_group bits
                                 | PV_GROUPS_SET, or PV_NET2_ATTACH for its default groups; 0 = not attached */
     uint32_t dns2_groups;    /* DNS v2 handler ("dns", src/handlers/dns/v2) in place of v1: pv_dns2_group bits
-                                | PV_GROUPS_SET, or PV_NET2_ATTACH for its default groups; 0 = DNS v1. Its
-                                filters, top_ecs and multi-GPU edge replay are not built */
+                                | PV_GROUPS_SET, or PV_NET2_ATTACH for its default groups; 0 = DNS v1. Filters
+                                (pv_set_dns_filters, v2 keys incl. only_xact_directions), top_ecs and the
+                                multi-GPU edge replay (pv_edge_carry) are built; geo/ASN filters are refused */
     uint32_t deep_sample_rate; /* "deep_sample_rate" 1..100 (0 = 100): each manager draws jsf32() % 100 < rate
                                   per event (AbstractMetricsManager::new_event, src/AbstractMetricsManager.h:318-333);
-                                  a non-deep event counts in the counters only. Below 100 not with DNS filters,
-                                  geo filters, the v2 handlers or DNS over TCP (PV_EUNSUPPORTED) */
+                                  a non-deep event counts in the counters only. Every handler version, DNS
+                                  filters and DNS over TCP sample; refused (PV_EUNSUPPORTED) only with the Net
+                                  geo filters (net_filter_all: no geo database) */
 } pv_config;
 #define PV_NET2_ATTACH 0x40000000u
 
@@ -243,8 +245,8 @@ int pv_index_records_mt(const uint8_t *recs, size_t bytes, uint32_t ts_nano, uin
 
 /* Process records in host memory, pipelined over 64 MiB chunks (PV_INGEST_CHUNK_MB). The
  * blob is copied to the device in fixed chunks (through pinned staging unless recs is
- * pinned, e.g. registered with pv_host_register) on two copy streams into a ring of three
- * device buffers, ahead of the kernels; each chunk, joined to the previous batch's tail on
+ * pinned, e.g. registered with pv_host_register) on two copy streams into a ring of device
+ * buffers (PV_INGEST_RING, 3..8, default 4), ahead of the kernels; each chunk, joined to the previous batch's tail on
  * the device, is indexed there (pv_index_records_device's kernels) and processed as batches
  * that end at a ts_sec boundary. PV_INGEST_INDEX=host selects the host-walk pipeline
  * (parallel host index, H2D of records + offsets). Returns when every record has been
@@ -257,8 +259,9 @@ int pv_process_host(pv_ctx *ctx, const uint8_t *recs, size_t bytes);
  * :832-843 and :1376-1412). msg_type_mask is the DNS handler's "dnstap_msg_type" filter
  * (bit t: dnstap Message.Type t passes; 0 = no filter, :171-184,260-266): a message of
  * another type is a filtered DNS event. Timestamps: the response time of CLIENT / AUTH /
- * RESOLVER responses, the query time of their queries, else the wall clock. Not built: the
- * v2 handlers' dnstap paths (PV_EUNSUPPORTED) and the input's only_hosts filter. */
+ * RESOLVER responses, the query time of their queries, else the wall clock. The v2 handlers'
+ * dnstap paths (Net v2 process_dnstap, DNS v2 transactions per message-type direction) are built,
+ * and the input's only_hosts filter is pv_set_dnstap_only_hosts. */
 int pv_process_dnstap(pv_ctx *ctx, const uint8_t *frames, size_t bytes, uint32_t msg_type_mask);
 /* The dnstap input proxy's "only_hosts" (DnstapInputEventProxy, src/inputs/dnstap/DnstapInputStream.h:
  * 96-146): comma-separated CIDRs, parsed with parse_host_specs' error texts; NULL clears. A message is
@@ -521,6 +524,51 @@ int pv_comm_destroy(pv_ctx *ctx);
  * pv_merge_topn adds such records from another rank into this context's view. */
 int pv_export_topn(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
 int pv_merge_topn(pv_ctx *ctx, const uint8_t *buf, size_t bytes);
+
+/* ---- Multi-GPU top-N merge on the device (the frequent-items merge of
+ * AbstractMetricsBucket::merge, src/AbstractMetricsManager.h:177-195 / src/Metrics.h:534-538,
+ * over shards of one stream). Every table's regions are split over the ranks in contiguous
+ * blocks; each rank ships the live entries (key, count) of the regions others own to their
+ * owners, which merge them into their regions on the device (pv_topn_merge). Names are not
+ * shipped: the read path collects every owner's leading entries per metric and fetches the
+ * names of those from whichever rank holds them. Collective: every rank calls each step with
+ * windows holding the same periods (the global period plan).
+ *   pv_comm_merge_topn: the whole exchange over the context's RCCL communicator (device to
+ *     device, one count round and one point-to-point round);
+ *   pv_topn_x_export / pv_topn_x_import: the same through host blobs (any transport): export
+ *     gives this rank's blob (pv_free), import takes every rank's blob in rank order.
+ * Afterwards the context's top-N view is its own regions until pv_topn_x_view installs the
+ * merged lists:
+ *   pv_topn_x_candidates: this rank's leading entries per metric (topn_count, and every entry
+ *     tied with the last), with the names it holds (blob, pv_free);
+ *   pv_topn_x_names: given every rank's candidate blob, the names this rank holds for the
+ *     candidates that came without one (blob, pv_free);
+ *   pv_topn_x_view: every rank's candidate and name blobs: the merged top-N lists. */
+int pv_comm_merge_topn(pv_ctx *ctx);
+int pv_topn_x_export(pv_ctx *ctx, uint32_t ranks, uint32_t rank, uint8_t **blob, size_t *bytes);
+int pv_topn_x_import(pv_ctx *ctx, uint32_t ranks, uint32_t rank, const uint8_t *const *blobs, const size_t *sizes);
+int pv_topn_x_candidates(pv_ctx *ctx, uint8_t **blob, size_t *bytes);
+int pv_topn_x_names(pv_ctx *ctx, const uint8_t *const *cands, const size_t *sizes, uint32_t n, uint8_t **blob, size_t *bytes);
+int pv_topn_x_view(pv_ctx *ctx, const uint8_t *const *cands, const size_t *csizes, const uint8_t *const *names,
+                   const size_t *nsizes, uint32_t n);
+
+/* Quantile inputs across shards without shipping the values (replaces pv_values_export /
+ * pv_values_merge for merged reads): an exact radix selection, eight passes of 256-bin group
+ * histograms summed over the ranks, gives per live DNS slot and value kind the count, p50, p90,
+ * p95, p99 and maximum of the union of the shards' transaction values (the KLL inclusive rank rule
+ * of Quantile, src/Metrics.h:334-481), and for the time kinds the counts at the histogram points
+ * (Histogram, :189-327); the merged view reads them instead of this rank's values. Collective.
+ * pv_values_x_select sums through the caller's all-reduce (op 0 SUM, 1 MAX; return 0 on success),
+ * pv_comm_values_select through the context's RCCL communicator. */
+typedef int (*pv_allreduce_fn)(uint64_t *buf, size_t n, int op, void *user);
+int pv_values_x_select(pv_ctx *ctx, pv_allreduce_fn allreduce, void *user);
+int pv_comm_values_select(pv_ctx *ctx);
+/* pv_slow_finish without shipping the transaction times: each DNS period's p90 (the bucket
+ * that closed at each shift, DnsMetricsManager::on_period_shift, dns/v1/DnsStreamHandler.h:
+ * 252-267) by the same distributed selection, then this rank's deferred candidates judged.
+ * Collective (every rank, pv_set_slow_defer contexts). */
+int pv_slow_x_finish(pv_ctx *ctx, pv_allreduce_fn allreduce, void *user);
+int pv_comm_slow_finish(pv_ctx *ctx);
 
 /* Device time of the Net-pass kernel (pv_net_kernel), from HIP events
  * recorded on the launch stream around every launch since the last reset:

@@ -173,7 +173,11 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_dnstap_only_hosts",
            "pv_afpacket_open", "pv_afpacket_attach", "pv_afpacket_run", "pv_afpacket_start", "pv_afpacket_stop",
            "pv_afpacket_stats", "pv_afpacket_close", "pv_afpacket_last_error", "pv_set_bpf", "pv_bpf_validate",
-           "pv_bpf_run", "pv_bpf_filter_records"]
+           "pv_bpf_run", "pv_bpf_filter_records", "pv_comm_merge_topn", "pv_topn_x_export", "pv_topn_x_import",
+           "pv_topn_x_candidates", "pv_topn_x_names", "pv_topn_x_view", "pv_values_x_select", "pv_comm_values_select",
+           "pv_slow_x_finish", "pv_comm_slow_finish"]
+# pv_allreduce_fn: (uint64_t *buf, size_t n, int op, void *user) -> int
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p)
 PV_HANDLER_NET, PV_HANDLER_DNS = 1, 2
 PV_PERIOD_AUTO = 0xFFFFFFFF
 PART_NET, PART_DNS = 0, 1
@@ -313,6 +317,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_comm_allreduce_window.argtypes = [P]
     lib.pv_comm_allgather.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), P]
     lib.pv_comm_destroy.argtypes = [P]
+    lib.pv_comm_merge_topn.argtypes = [P]
+    lib.pv_topn_x_export.argtypes = [P, U32, U32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_topn_x_import.argtypes = [P, U32, U32, P, P]
+    lib.pv_topn_x_candidates.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_topn_x_names.argtypes = [P, P, P, U32, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.pv_topn_x_view.argtypes = [P, P, P, P, P, U32]
+    lib.pv_values_x_select.argtypes = [P, ALLREDUCE_FN, P]
+    lib.pv_comm_values_select.argtypes = [P]
+    lib.pv_slow_x_finish.argtypes = [P, ALLREDUCE_FN, P]
+    lib.pv_comm_slow_finish.argtypes = [P]
     lib.pv_process_dnstap.argtypes = [P, P, ctypes.c_size_t, U32]
     lib.pv_tpacket3_block_records.argtypes = [P, ctypes.c_size_t, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                               ctypes.POINTER(U64)]
@@ -896,6 +910,79 @@ class PvHandlers:
         buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, dtype=np.uint8)
         self._check(self.lib.pv_merge_topn(self.ctx, buf.ctypes.data, len(data)), "pv_merge_topn")
 
+    # ---- multi-GPU top-N merge on the device (pv_topn_x_*, pv_comm_merge_topn)
+    @staticmethod
+    def _blob_arrays(blobs):
+        keep = [np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, dtype=np.uint8) for b in blobs]
+        ptrs = (ctypes.c_void_p * max(1, len(blobs)))(*[k.ctypes.data for k in keep])
+        sizes = (ctypes.c_size_t * max(1, len(blobs)))(*[len(b) for b in blobs])
+        return keep, ptrs, sizes
+
+    def comm_merge_topn(self):
+        self._check(self.lib.pv_comm_merge_topn(self.ctx), "pv_comm_merge_topn")
+
+    def topn_x_export(self, ranks: int, rank: int) -> bytes:
+        return self._export(lambda c, p, n: self.lib.pv_topn_x_export(c, ranks, rank, p, n), "pv_topn_x_export")
+
+    def topn_x_import(self, ranks: int, rank: int, blobs):
+        keep, ptrs, sizes = self._blob_arrays(blobs)
+        self._check(self.lib.pv_topn_x_import(self.ctx, ranks, rank, ptrs, sizes), "pv_topn_x_import")
+
+    def topn_x_candidates(self) -> bytes:
+        return self._export(self.lib.pv_topn_x_candidates, "pv_topn_x_candidates")
+
+    def topn_x_names(self, cands) -> bytes:
+        keep, ptrs, sizes = self._blob_arrays(cands)
+        return self._export(lambda c, p, n: self.lib.pv_topn_x_names(c, ptrs, sizes, len(cands), p, n), "pv_topn_x_names")
+
+    def topn_x_view(self, cands, names):
+        kc, pc, sc = self._blob_arrays(cands)
+        kn, pn, sn = self._blob_arrays(names)
+        self._check(self.lib.pv_topn_x_view(self.ctx, pc, sc, pn, sn, len(cands)), "pv_topn_x_view")
+
+    def values_x_select(self, allreduce):
+        """allreduce(np.ndarray uint64, op) sums (op 0) or maxes (op 1) the array over the ranks in place"""
+        err = []
+
+        def cb(buf, n, op, user):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(n,))
+                allreduce(a, op)
+                return 0
+            except Exception as e:  # surfaced after the call
+                err.append(e)
+                return 1
+        fn = ALLREDUCE_FN(cb)
+        rc = self.lib.pv_values_x_select(self.ctx, fn, None)
+        if err:
+            raise err[0]
+        self._check(rc, "pv_values_x_select")
+
+    def _with_allreduce(self, fn, what, allreduce):
+        err = []
+
+        def cb(buf, n, op, user):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(n,)), op)
+                return 0
+            except Exception as e:  # surfaced after the call
+                err.append(e)
+                return 1
+        cfn = ALLREDUCE_FN(cb)
+        rc = fn(self.ctx, cfn, None)
+        if err:
+            raise err[0]
+        self._check(rc, what)
+
+    def slow_x_finish(self, allreduce):
+        self._with_allreduce(self.lib.pv_slow_x_finish, "pv_slow_x_finish", allreduce)
+
+    def comm_slow_finish(self):
+        self._check(self.lib.pv_comm_slow_finish(self.ctx), "pv_comm_slow_finish")
+
+    def comm_values_select(self):
+        self._check(self.lib.pv_comm_values_select(self.ctx), "pv_comm_values_select")
+
     def _export(self, fn, what) -> bytes:
         p, n = ctypes.c_void_p(), ctypes.c_size_t()
         self._check(fn(self.ctx, ctypes.byref(p), ctypes.byref(n)), what)
@@ -984,9 +1071,11 @@ def last_record_ts(recs: bytes, index: RecordIndex, ts_nano: int = 0):
 def pktvisor_reader(path: str, host_spec: Optional[str] = None, periods: int = 5, **kw) -> dict:
     """GPU equivalent of `pktvisor-reader [-H host_spec] --periods N FILE` for net + dns."""
     linktype, ts_nano, recs = read_pcap(path)
-    if kw.get("bpf"):
-        # the reader delivers only the records the filter keeps (their last one ends the capture)
-        recs = bpf_filter(recs, kw["bpf"])
+    bpf = kw.pop("bpf", None)
+    if bpf:
+        # the reader delivers only the records the filter keeps (their last one ends the capture);
+        # the context then gets no program of its own (the records are filtered once)
+        recs = bpf_filter(recs, bpf)
     idx = RecordIndex(recs, ts_nano)
     h = PvHandlers(host_spec=host_spec, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
                    max_records=max(1, idx.n), **kw)

@@ -89,7 +89,7 @@ struct pv_afpacket {
     void *user = nullptr;
     // counters
     std::atomic<uint64_t> blocks{0}, packets{0}, batches{0}, bytes{0};
-    uint64_t drops = 0, kpackets = 0, freezes = 0;
+    std::atomic<uint64_t> drops{0}, kpackets{0}, freezes{0}; // read_stats runs on the capture and caller threads
 
     ~pv_afpacket()
     {
@@ -150,8 +150,10 @@ struct pv_afpacket {
         std::unique_lock<std::mutex> g(m);
         cv.wait(g, [&] { return pending < 0 && !busy; });
     }
+    std::mutex stats_m; // PACKET_STATISTICS resets on read: one reader at a time
     void read_stats()
     {
+        std::lock_guard<std::mutex> g(stats_m);
         if (fd < 0) return;
         tpacket_stats_v3 st{};
         socklen_t len = sizeof st;
@@ -296,6 +298,9 @@ int pv_afpacket_open(const pv_afpacket_config *cfg, pv_afpacket **out)
             return bail(PV_EINVAL, "Failed to enable promisc mode on AF_PACKET socket");
     }
     if (cfg->bpf_insns && cfg->bpf_len) {
+        // the kernel takes a 16-bit length: validate first (at most BPF_MAXINSNS, classic-BPF rules)
+        if (pv_bpf_validate(static_cast<const pv_bpf_insn *>(cfg->bpf_insns), cfg->bpf_len) != 0)
+            return bail(PV_EINVAL, "invalid BPF program for the AF_PACKET socket");
         sock_fprog prog{};
         prog.len = (unsigned short)cfg->bpf_len;
         prog.filter = const_cast<sock_filter *>(static_cast<const sock_filter *>(cfg->bpf_insns));
@@ -404,9 +409,9 @@ int pv_afpacket_stats(pv_afpacket *a, pv_afpacket_counters *out)
     out->packets = a->packets;
     out->batches = a->batches;
     out->bytes = a->bytes;
-    out->kernel_packets = a->kpackets;
-    out->kernel_drops = a->drops;
-    out->kernel_freezes = a->freezes;
+    out->kernel_packets = a->kpackets.load();
+    out->kernel_drops = a->drops.load();
+    out->kernel_freezes = a->freezes.load();
     return 0;
 }
 

@@ -36,6 +36,8 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <set>
+#include <tuple>
 #include <vector>
 
 #include <chrono>
@@ -158,9 +160,25 @@ extern "C" __global__ void pv_dns_prescan(const PvParams *P);
 extern "C" __global__ void pv_topn_combine(const PvParams *P);
 extern "C" __global__ void pv_topn_combine_r12(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
+extern "C" uint32_t pv_topn_merge_threads();
+struct PvBpfIns;
+extern "C" __global__ void pv_bpf_keep(const uint8_t *recs, const uint32_t *offs, uint32_t n, const PvBpfIns *prog, uint32_t ninsn,
+                                       uint32_t *sz, uint32_t *kf);
+extern "C" __global__ void pv_bpf_gather(const uint8_t *recs, const uint32_t *offs, uint32_t n, const uint32_t *sz, const uint32_t *boff,
+                                         const uint32_t *rank, uint8_t *out, uint32_t *ooffs);
+extern "C" __global__ void pv_bpf_secs(const uint8_t *out, const uint32_t *ooffs, uint32_t nk, uint32_t *flag, uint32_t *sec, uint32_t *down);
+extern "C" __global__ void pv_bpf_secs_compact(const uint32_t *flag, const uint32_t *pos, const uint32_t *sec, uint32_t nk, uint32_t cap,
+                                               uint32_t *sci, uint32_t *scs);
+extern "C" hipError_t pv_exclusive_scan_u32(void *tmp, size_t *tmp_bytes, const uint32_t *in, uint32_t *out, size_t n, hipStream_t s);
+extern "C" __global__ void pv_topn_xcount(const PvParams *P, PvXTabs T, uint32_t *cnt);
+extern "C" __global__ void pv_topn_xscan(uint32_t reg_log2, uint32_t W, const uint32_t *cnt, uint32_t *off, uint32_t *hdr);
+extern "C" __global__ void pv_topn_xwrite(const PvParams *P, PvXTabs T, const uint32_t *off, ulonglong2 *out);
+extern "C" __global__ void pv_topn_xruns(uint32_t reg_log2, uint32_t W, uint32_t me, const uint32_t *hdr, uint32_t hdr_stride,
+                                         uint64_t *cb_run);
+extern "C" __global__ void pv_topn_xlookup(const PvParams *P, const uint64_t *keys, const uint32_t *tbs, uint32_t n, uint32_t *aux);
 extern "C" __global__ void pv_net2_kernel(const PvParams *P);
 extern "C" __global__ void pv_ix_guess(const PvIxParams *X);
-extern "C" __global__ void pv_xv_hist(const PvXValue *v, const uint32_t *n_vals, uint32_t sg, uint32_t shift, PvXvSel sel,
+extern "C" __global__ void pv_xv_hist(const PvXValue *v, const uint32_t *n_vals, uint32_t cap, uint32_t sg, uint32_t shift, PvXvSel sel,
                                       uint32_t *hist);
 extern "C" __global__ void pv_ix_fix(const PvIxParams *X, uint32_t src);
 extern "C" __global__ void pv_ix_scan(const PvIxParams *X);
@@ -496,9 +514,24 @@ inline bool hip_ok(hipError_t e) { return e == hipSuccess; }
 } // namespace
 
 // ---------------------------------------------------------------- context
+// a value group's summary over every shard (pv_values_x_select)
+struct XQuant {
+    uint64_t n = 0, max = 0;
+    std::vector<uint64_t> q;   // p50 p90 p95 p99 (value bits)
+    std::vector<uint64_t> cdf; // counts at or below each hist_points() point (time kinds)
+};
+
 struct pv_ctx {
     std::vector<pv_bpf_insn> bpf; // the pcap input's BPF program (pv_set_bpf), empty = none
-    std::vector<uint8_t> bpf_buf; // the records it keeps of one pv_process_host block
+    // the program on the device and the filtered batch (pv_process_device runs the filter there)
+    pv_bpf_insn *d_bpf = nullptr;
+    size_t d_bpf_n = 0;
+    bool bpf_dirty = false;
+    uint32_t *d_fwork = nullptr; // 4 x max_records u32: sizes, keep flags, byte offsets, ranks
+    uint8_t *d_frecs = nullptr;  // the kept records (max_records' bytes + PV_RECS_PAD)
+    uint32_t *d_foffs = nullptr, *d_fsc = nullptr; // their offsets; change points (idx, sec) + counters
+    void *d_fscan = nullptr;
+    size_t fwork_n = 0, frecs_bytes = 0, fscan_bytes = 0;
     pv_config cfg{};
     std::string err;
     std::mutex mu;
@@ -541,6 +574,7 @@ struct pv_ctx {
     int cus = 256;
     int wg_per_cu = 3;     // grid workgroups per CU (the batch's partition)
     int reg_wg_per_cu = 1; // workgroups per CU of the register-window Net pass
+    uint32_t cb_fan = 1;   // grid ranges per top-N combine workgroup
     int reg_waves = 4;     // its waves per workgroup (4 or 8; PV_REG_WAVES)
     int dns_wg_per_cu = 1; // resident workgroups per CU of the DNS pass (its register count)
     const char *net_kernel = "none"; // the Net-pass kernel the last span launched (pv_net_kernel_name)
@@ -650,6 +684,19 @@ struct pv_ctx {
     std::vector<PvXValue> xvals_host;
     // merged top-N records from other ranks: table -> key -> (count, name)
     std::map<uint32_t, std::map<uint64_t, std::pair<uint64_t, std::string>>> remote_topn;
+    // multi-GPU top-N exchange (pv_topn_x_*, pv_comm_merge_topn): device scratch, and the merged
+    // view: this rank's regions of x_ranks (0: not merged), then every owner's leading entries
+    uint32_t *d_xcnt = nullptr, *d_xrhdr = nullptr;
+    uint64_t *d_xtot = nullptr;
+    void *d_xsend = nullptr, *d_xrecv = nullptr;
+    size_t xcnt_bytes = 0, xrhdr_bytes = 0, xtot_bytes = 0, xsend_bytes = 0, xrecv_bytes = 0;
+    PvParams *d_xp = nullptr;
+    uint32_t x_ranks = 0, x_rank = 0;
+    bool x_view_on = false;
+    std::map<uint32_t, std::map<uint64_t, std::pair<uint64_t, std::string>>> x_view; // part << 16 | slot mask -> key -> (estimate, name)
+    // merged quantile inputs (pv_values_x_select): per (DNS slot set as a bit mask, value kind)
+    std::map<std::pair<uint32_t, uint32_t>, XQuant> xq;
+    bool xq_on = false;
     // device fills not launched yet (launch_fill*; one pv_fill_multi per flush_fills)
     PvFillList fills{};
     uint64_t fills_max = 0;
@@ -859,6 +906,7 @@ void clear_part(pv_ctx *c, int part, uint32_t s)
     }
     const uint32_t t = s + (part == PART_DNS ? PV_SLOTS : 0);
     c->remote_topn.erase(t);
+    c->x_view.clear(); // (its slot sets name slots)
     w.meta[s] = SlotMeta();
     if (w.clean[s]) return;
     const uint64_t tcap = 1ull << c->tcap_log2;
@@ -946,7 +994,14 @@ int read_topn(pv_ctx *c, uint32_t s, std::vector<TopRec> &out) // s: table (PV_T
             return c->hipfail(e, "read name arena");
     }
     const std::vector<uint64_t> &roff = c->roff[s];
-    for (uint64_t i = 0; i < tcap; i++) {
+    // after a multi-GPU exchange (before pv_topn_x_view), this rank's regions only
+    uint64_t i0 = 0, i1 = tcap;
+    if (c->x_ranks > 1) {
+        const uint32_t nreg = 1u << c->reg_log2, rsl = c->tcap_log2 - c->reg_log2;
+        i0 = (uint64_t)(((uint64_t)c->x_rank * nreg + c->x_ranks - 1) / c->x_ranks) << rsl;
+        i1 = (uint64_t)(((uint64_t)(c->x_rank + 1) * nreg + c->x_ranks - 1) / c->x_ranks) << rsl;
+    }
+    for (uint64_t i = i0; i < i1; i++) {
         if (!keys[i]) continue;
         // a purged region's survivors report count + the thetas its purges subtracted (the
         // frequent-items estimate, exact for a key no purge dropped)
@@ -1075,6 +1130,46 @@ double cpc_estimate(const int64_t *t, bool merged)
 }
 
 // One handler's bucket over `slots` (merged: window_merged_json's fold, AbstractMetricsManager.h:601-647)
+// The merged view's values of a set of DNS slots (pv_values_x_select; mask: bit per slot): per kind a stand-in list of the
+// group's count whose histogram-point counts and maximum are the merged ones (each value at the
+// point that bounds it, the largest replaced by the maximum), its quantiles set as overrides.
+const std::vector<uint64_t> &hist_points();
+void x_values_standin(pv_ctx *c, uint32_t mask, HostBucket &b)
+{
+    const std::vector<uint64_t> &pts = hist_points();
+    for (auto &kv : c->xq) {
+        if (kv.first.first != mask) continue;
+        const uint32_t kind = kv.first.second;
+        const XQuant &x = kv.second;
+        std::vector<uint64_t> v;
+        v.reserve(x.n);
+        if (!x.cdf.empty()) {
+            uint64_t prev = 0;
+            for (size_t k = 0; k < pts.size(); k++) {
+                for (uint64_t i = prev; i < x.cdf[k]; i++) v.push_back(pts[k]);
+                prev = std::max(prev, x.cdf[k]);
+            }
+        }
+        while (v.size() < x.n) v.push_back(x.max);
+        if (!v.empty()) v.back() = x.max;
+        auto dbl = [](const std::vector<uint64_t> &u) {
+            std::vector<double> d(u.size());
+            for (size_t i = 0; i < u.size(); i++) memcpy(&d[i], &u[i], 8);
+            return d;
+        };
+        if (kind == XV_FROM_US) { b.from_us.insert(b.from_us.end(), v.begin(), v.end()); b.qs_from = x.q; }
+        else if (kind == XV_TO_US) { b.to_us.insert(b.to_us.end(), v.begin(), v.end()); b.qs_to = x.q; }
+        else if (kind == XV_RATIO) { auto d = dbl(v); b.ratio.insert(b.ratio.end(), d.begin(), d.end()); b.qs_ratio = dbl(x.q); }
+        else if (kind >= XV2_TIME && kind < XV2_TIME + 3) { auto &t = b.time2[kind - XV2_TIME]; t.insert(t.end(), v.begin(), v.end()); b.qs_time2[kind - XV2_TIME] = x.q; }
+        else if (kind >= XV2_RATIO && kind < XV2_RATIO + 3) {
+            auto d = dbl(v);
+            auto &t = b.ratio2[kind - XV2_RATIO];
+            t.insert(t.end(), d.begin(), d.end());
+            b.qs_ratio2[kind - XV2_RATIO] = dbl(x.q);
+        }
+    }
+}
+
 int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int part, HostBucket &b)
 {
     flush_fills(c);
@@ -1105,12 +1200,15 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int 
         if (first || m.start_sec < b.start_sec) { b.start_sec = m.start_sec; b.start_nsec = m.start_nsec; }
         if (m.end_sec > b.end_sec) { b.end_sec = m.end_sec; b.end_nsec = m.end_nsec; }
         first = false;
-        std::vector<TopRec> recs;
-        int rc = read_topn(c, s + (part == PART_DNS ? PV_SLOTS : 0), recs);
-        if (rc) return rc;
-        for (auto &r : recs) b.tops[host_metric(c, r.key)][r.name] += r.count;
+        if (!(c->x_ranks > 1 && c->x_view_on)) {
+            std::vector<TopRec> recs;
+            int rc = read_topn(c, s + (part == PART_DNS ? PV_SLOTS : 0), recs);
+            if (rc) return rc;
+            for (auto &r : recs) b.tops[host_metric(c, r.key)][r.name] += r.count;
+        }
         if (part != PART_DNS) continue;
         const uint32_t sg = s | (c->gen[s] << 8);
+        if (c->xq_on) continue; // (the merged view's values: after the loop, for the slot set)
         for (auto &v : c->xvals_host) {
             if (v.slot != sg) continue;
             if (v.kind == XV_FROM_US) b.from_us.push_back(v.bits);
@@ -1124,6 +1222,15 @@ int load_bucket(pv_ctx *c, const std::vector<uint32_t> &slots, bool merged, int 
             }
         }
     }
+    uint32_t mask = 0;
+    for (uint32_t sl : slots) mask |= 1u << sl;
+    if (c->x_ranks > 1 && c->x_view_on) {
+        // a multi-GPU merged view (pv_topn_x_view): every owner's leading entries of this slot set
+        auto it = c->x_view.find(((uint32_t)part << 16) | mask);
+        if (it != c->x_view.end())
+            for (auto &kv : it->second) b.tops[host_metric(c, kv.first)][kv.second.second] += kv.second.first;
+    }
+    if (part == PART_DNS && c->xq_on) x_values_standin(c, mask, b);
     return 0;
 }
 
@@ -2430,7 +2537,9 @@ void pv_destroy(pv_ctx *c)
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
                     c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_iplog32,
-                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose};
+                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose,
+                    c->d_xcnt, c->d_xrhdr, c->d_xtot, c->d_xsend, c->d_xrecv, c->d_xp, c->d_bpf, c->d_fwork, c->d_frecs,
+                    c->d_foffs, c->d_fsc, c->d_fscan};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
     for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
@@ -2496,6 +2605,11 @@ int pv_reset(pv_ctx *c)
     c->from90 = c->to90 = 0.0f;
     c->p90_2[0] = c->p90_2[1] = c->p90_2[2] = 0.0f;
     c->remote_topn.clear();
+    c->x_ranks = c->x_rank = 0;
+    c->x_view_on = false;
+    c->x_view.clear();
+    c->xq_on = false;
+    c->xq.clear();
     c->n_pend = 0;
     c->pend_hi = 0;
     c->pend_base = -1;
@@ -3205,6 +3319,15 @@ int xv_select(pv_ctx *c, uint32_t sg, double r, bool have[PV_XV_SEL], uint64_t o
     auto kind_of = [](uint32_t kind) {
         return kind == XV_FROM_US ? 0 : kind == XV_TO_US ? 1 : (kind >= XV2_TIME && kind < XV2_TIME + 3) ? 2 + (int)(kind - XV2_TIME) : -1;
     };
+    {
+        // a value buffer that overflowed holds a truncated value set: fail as sync_xvals does
+        uint32_t flags = 0, nv = 0;
+        if (!hip_ok(e = hipStreamSynchronize(c->stream)) ||
+            !hip_ok(e = hipMemcpy(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost)) ||
+            !hip_ok(e = hipMemcpy(&nv, c->d_nvals, 4, hipMemcpyDeviceToHost)))
+            return c->hipfail(e, "threshold selection");
+        if ((flags & PVF_VALUES_FULL) || nv > c->xv_cap) return c->fail(PV_ECAPACITY, "transaction value buffer full");
+    }
     std::vector<uint64_t> hv[PV_XV_SEL];
     const size_t host_only = c->xvals_host.size() - c->xvals_synced;
     for (size_t i = 0; i < host_only; i++) {
@@ -3218,8 +3341,8 @@ int xv_select(pv_ctx *c, uint32_t sg, double r, bool have[PV_XV_SEL], uint64_t o
     for (int pass = 0; pass < 8; pass++) {
         const uint32_t shift = 56 - 8 * pass;
         if (!hip_ok(e = hipMemsetAsync(c->d_xvh, 0, PV_XV_SEL * 256 * 4, c->stream))) return c->hipfail(e, "threshold selection");
-        hipLaunchKernelGGL(pv_xv_hist, dim3(std::max<uint32_t>(1u, (uint32_t)c->cus * 2)), dim3(256), 0, c->stream, c->d_xvals, c->d_nvals, sg, shift, sel,
-                           c->d_xvh);
+        hipLaunchKernelGGL(pv_xv_hist, dim3(std::max<uint32_t>(1u, (uint32_t)c->cus * 2)), dim3(256), 0, c->stream, c->d_xvals, c->d_nvals,
+                           (uint32_t)c->xv_cap, sg, shift, sel, c->d_xvh);
         if (!hip_ok(e = hipGetLastError()) ||
             !hip_ok(e = hipMemcpyAsync(c->h_xvh, c->d_xvh, PV_XV_SEL * 256 * 4, hipMemcpyDeviceToHost, c->stream)) ||
             !hip_ok(e = hipStreamSynchronize(c->stream)))
@@ -3380,8 +3503,12 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "carried queries");
         const uint32_t npo = nv3[2];
-        if (c->xv_cap - nv3[0] < c->max_records) {
-            // less than max_records of room: the device value buffer doubles while it stays
+        uint32_t vflags = 0;
+        if (!hip_ok(e = hipMemcpy(&vflags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
+        if ((vflags & PVF_VALUES_FULL) || nv3[0] > c->xv_cap) return c->fail(PV_ECAPACITY, "transaction value buffer full");
+        // a batch pushes at most two values per response (time + ratio), so keep 2 x max_records free
+        if (c->xv_cap - nv3[0] < 2ull * c->max_records) {
+            // less than that room: the device value buffer doubles while it stays
             // within PV_XV_BUDGET_MB (HBM is plentiful; a copy inside HBM instead of a read-back
             // of every value inside the stream), else it drains to the host copy and every batch
             // then has the whole capacity (at most two values per response)
@@ -3653,6 +3780,14 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if ((uint64_t)grid * 4 > PV_TRASH_WAVES) return c->fail(PV_ECAPACITY, "grid of %u workgroups exceeds the trash area", grid);
     P.cb = c->d_cb;
     P.cb_cnt = c->d_cb_cnt;
+    P.cb_hm = c->d_cb_cnt + 32768;
+    {
+        // grid ranges per combine workgroup (PV_CB_FAN, A/B runs): fewer, larger tables
+        static const char *fan = getenv("PV_CB_FAN");
+        P.cb_fan = fan ? std::max(1u, std::min(8u, (uint32_t)atoi(fan))) : c->cb_fan;
+        while (P.cb_fan > 1 && (uint64_t)P.cb_fan * P.mq_cap >= (1u << 24)) P.cb_fan--; // run starts are 24-bit
+        P.cb_grid = (grid + P.cb_fan - 1) / P.cb_fan;
+    }
     P.stamps = c->d_stamps;
     P.dq = c->d_dq;
     P.dq_cnt = c->d_dq_cnt;
@@ -3720,9 +3855,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates into a list sorted by table region, merge
     // each region's runs in LDS, decode the names of new entries
-    hipLaunchKernelGGL(c->reg_log2 <= 10 ? pv_topn_combine : pv_topn_combine_r12, dim3(grid), dim3(PV_CB_THREADS), 0, st,
+    hipLaunchKernelGGL(c->reg_log2 <= 10 ? pv_topn_combine : pv_topn_combine_r12, dim3(P.cb_grid), dim3(PV_CB_THREADS), 0, st,
                        (const PvParams *)c->d_params);
-    hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(1024), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(pv_topn_merge_threads()), 0, st, (const PvParams *)c->d_params);
     // names: as many workgroups as are resident (LDS: two per CU), each pipelining its entries
     hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 2), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch");
@@ -3893,6 +4028,114 @@ int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const
 
 } // namespace
 
+int x_grow_dev(pv_ctx *c, void **p, size_t &have, size_t need, const char *what)
+{
+    if (need <= have) return 0;
+    hipError_t e;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    have = 0;
+    if (!hip_ok(e = hipMalloc(p, std::max<size_t>(need, 256)))) return c->hipfail(e, what);
+    have = std::max<size_t>(need, 256);
+    return 0;
+}
+// The BPF filter on a device batch: keep flags and sizes (pv_bpf_keep), their exclusive scans (byte
+// offsets, ranks), the kept records compacted into d_frecs / d_foffs (pv_bpf_gather), and the
+// kept run's index info and ts_sec change points (pv_bpf_secs). The caller holds c->mu.
+int bpf_filter_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info, hipStream_t st,
+                      pv_index_info &out, std::vector<uint32_t> &sci, std::vector<uint32_t> &scs)
+{
+    hipError_t e;
+    const uint32_t n = (uint32_t)info->n_records;
+    memset(&out, 0, sizeof out);
+    if (c->bpf_dirty || !c->d_bpf) {
+        if (c->d_bpf) hipFree(c->d_bpf);
+        c->d_bpf = nullptr;
+        if (!hip_ok(e = hipMalloc(&c->d_bpf, c->bpf.size() * sizeof(pv_bpf_insn))) ||
+            !hip_ok(e = hipMemcpy(c->d_bpf, c->bpf.data(), c->bpf.size() * sizeof(pv_bpf_insn), hipMemcpyHostToDevice)))
+            return c->hipfail(e, "BPF program");
+        c->d_bpf_n = c->bpf.size();
+        c->bpf_dirty = false;
+    }
+    if (n > c->fwork_n) {
+        for (void *p : {(void *)c->d_fwork, (void *)c->d_foffs, (void *)c->d_fsc}) if (p) hipFree(p);
+        c->d_fwork = c->d_foffs = c->d_fsc = nullptr;
+        c->fwork_n = 0;
+        if (!hip_ok(e = hipMalloc(&c->d_fwork, (size_t)n * 16)) || !hip_ok(e = hipMalloc(&c->d_foffs, (size_t)n * 4)) ||
+            !hip_ok(e = hipMalloc(&c->d_fsc, (size_t)n * 8 + 64)))
+            return c->hipfail(e, "BPF filter buffers");
+        c->fwork_n = n;
+    }
+    if (info->bytes_used + PV_RECS_PAD > c->frecs_bytes) {
+        if (c->d_frecs) hipFree(c->d_frecs);
+        c->d_frecs = nullptr;
+        c->frecs_bytes = 0;
+        if (!hip_ok(e = hipMalloc(&c->d_frecs, info->bytes_used + PV_RECS_PAD)) ||
+            !hip_ok(e = hipMemsetAsync(c->d_frecs, 0, info->bytes_used + PV_RECS_PAD, st)))
+            return c->hipfail(e, "BPF filter buffers");
+        c->frecs_bytes = info->bytes_used + PV_RECS_PAD;
+    }
+    size_t tb = 0;
+    if (!hip_ok(e = pv_exclusive_scan_u32(nullptr, &tb, nullptr, nullptr, n, st))) return c->hipfail(e, "scan size");
+    if (int rc = x_grow_dev(c, &c->d_fscan, c->fscan_bytes, tb, "BPF scan")) return rc;
+    uint32_t *sz = c->d_fwork, *kf = sz + n, *boff = kf + n, *rank = boff + n;
+    const uint32_t grid = (n + 255) / 256;
+    hipLaunchKernelGGL(pv_bpf_keep, dim3(grid), dim3(256), 0, st, d_recs, d_offs, n, (const PvBpfIns *)c->d_bpf,
+                       (uint32_t)c->d_bpf_n, sz, kf);
+    if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_bpf_keep");
+    tb = c->fscan_bytes;
+    if (!hip_ok(e = pv_exclusive_scan_u32(c->d_fscan, &tb, sz, boff, n, st))) return c->hipfail(e, "scan");
+    tb = c->fscan_bytes;
+    if (!hip_ok(e = pv_exclusive_scan_u32(c->d_fscan, &tb, kf, rank, n, st))) return c->hipfail(e, "scan");
+    uint32_t tail[4];
+    if (!hip_ok(e = hipMemcpyAsync(&tail[0], boff + n - 1, 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(&tail[1], sz + n - 1, 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(&tail[2], rank + n - 1, 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(&tail[3], kf + n - 1, 4, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "BPF filter");
+    const uint64_t bytes = (uint64_t)tail[0] + tail[1];
+    const uint32_t nk = tail[2] + tail[3];
+    if (!nk) return 0;
+    hipLaunchKernelGGL(pv_bpf_gather, dim3(grid), dim3(256), 0, st, d_recs, d_offs, n, (const uint32_t *)sz, (const uint32_t *)boff,
+                       (const uint32_t *)rank, c->d_frecs, c->d_foffs);
+    // the kept run's change points (sz / kf / boff reused: flags, seconds, positions)
+    uint32_t *flag = sz, *sec = kf, *pos = boff, *down = c->d_fsc + 2 * (size_t)n;
+    if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipMemsetAsync(down, 0, 4, st))) return c->hipfail(e, "BPF filter");
+    hipLaunchKernelGGL(pv_bpf_secs, dim3((nk + 255) / 256), dim3(256), 0, st, (const uint8_t *)c->d_frecs, (const uint32_t *)c->d_foffs,
+                       nk, flag, sec, down);
+    tb = c->fscan_bytes;
+    if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = pv_exclusive_scan_u32(c->d_fscan, &tb, flag, pos, nk, st)))
+        return c->hipfail(e, "BPF filter");
+    hipLaunchKernelGGL(pv_bpf_secs_compact, dim3((nk + 255) / 256), dim3(256), 0, st, (const uint32_t *)flag, (const uint32_t *)pos,
+                       (const uint32_t *)sec, nk, n, c->d_fsc, c->d_fsc + n);
+    uint32_t w[4], lo = 0, hi_off = 0;
+    uint32_t h0[4], h1[4];
+    if (!hip_ok(e = hipGetLastError()) ||
+        !hip_ok(e = hipMemcpyAsync(&w[0], pos + nk - 1, 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(&w[1], flag + nk - 1, 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(&w[2], down, 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(&hi_off, c->d_foffs + nk - 1, 4, hipMemcpyDeviceToHost, st)) ||
+        !hip_ok(e = hipMemcpyAsync(h0, c->d_frecs, 16, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)) ||
+        !hip_ok(e = hipMemcpy(h1, c->d_frecs + hi_off, 16, hipMemcpyDeviceToHost)))
+        return c->hipfail(e, "BPF filter");
+    (void)lo;
+    const uint32_t nch = w[0] + w[1];
+    sci.resize(nch);
+    scs.resize(nch);
+    if (nch && (!hip_ok(e = hipMemcpy(sci.data(), c->d_fsc, (size_t)nch * 4, hipMemcpyDeviceToHost)) ||
+                !hip_ok(e = hipMemcpy(scs.data(), c->d_fsc + n, (size_t)nch * 4, hipMemcpyDeviceToHost))))
+        return c->hipfail(e, "BPF filter");
+    out.n_records = nk;
+    out.bytes_used = bytes;
+    out.first_sec = h0[0];
+    out.first_nsec = c->cfg.ts_nano ? (int64_t)h0[1] : (int64_t)h0[1] * 1000;
+    out.last_sec = h1[0];
+    out.last_nsec = c->cfg.ts_nano ? (int64_t)h1[1] : (int64_t)h1[1] * 1000;
+    out.monotone = w[2] == 0;
+    out.n_sec_changes = nch;
+    return 0;
+}
+
 int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const pv_index_info *info,
                       const uint32_t *sc_idx, const uint32_t *sc_sec, void *stream)
 {
@@ -3902,10 +4145,23 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     hipStream_t saved = c->stream;
     c->stream = st;
     struct Restore { pv_ctx *c; hipStream_t s; ~Restore() { c->stream = s; } } restore{c, saved};
+    if (info->n_records == 0) return 0;
+    if (info->n_records > c->max_records) return c->fail(PV_ECAPACITY, "batch of %llu records exceeds max_records %llu",
+                                           (unsigned long long)info->n_records, (unsigned long long)c->max_records);
+    pv_index_info finfo;
+    std::vector<uint32_t> fsci, fscs;
+    if (!c->bpf.empty()) {
+        // the pcap input's BPF filter (PcapInputStream.cpp:485-488) over the batch in HBM: the kept
+        // records become the batch
+        if (int rc = bpf_filter_device(c, d_recs, d_offs, info, st, finfo, fsci, fscs)) return rc;
+        if (finfo.n_records == 0) return 0;
+        d_recs = c->d_frecs;
+        d_offs = c->d_foffs;
+        info = &finfo;
+        sc_idx = fsci.data();
+        sc_sec = fscs.data();
+    }
     const uint64_t n = info->n_records;
-    if (n == 0) return 0;
-    if (n > c->max_records) return c->fail(PV_ECAPACITY, "batch of %llu records exceeds max_records %llu",
-                                           (unsigned long long)n, (unsigned long long)c->max_records);
     ensure_started(c, info->first_sec, info->first_nsec);
     std::vector<Shift> nsh, dsh;
     if (int rc = batch_shifts(c, d_recs, d_offs, info, sc_idx, sc_sec, st, nsh, dsh)) return rc;
@@ -4769,6 +5025,7 @@ int pv_set_bpf(pv_ctx *c, const pv_bpf_insn *prog, uint32_t n)
     if (n == 0) { c->bpf.clear(); return 0; }
     if (pv_bpf_validate(prog, n)) return c->fail(PV_EINVAL, "invalid BPF program (classic-BPF checker)");
     c->bpf.assign(prog, prog + n);
+    c->bpf_dirty = true;
     return 0;
 }
 
@@ -4778,20 +5035,9 @@ int process_host_block(pv_ctx *c, const uint8_t *recs, size_t bytes);
 
 int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
 {
-    std::vector<pv_bpf_insn> prog;
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        prog = c->bpf;
-    }
-    if (prog.empty()) return process_host_block(c, recs, bytes);
-    // the pcap input's filter (PcapInputStream.cpp:485-488): the kept records, in order, go on
-    // as the block (libpcap runs the program on the reading thread, as here); bpf_buf is the
-    // input thread's (one producer per context)
-    c->bpf_buf.resize(bytes);
-    size_t kb = 0;
-    if (pv_bpf_filter_records(prog.data(), (uint32_t)prog.size(), recs, bytes, c->bpf_buf.data(), &kb, nullptr))
-        return c->fail(PV_EINVAL, "BPF filter");
-    return kb ? process_host_block(c, c->bpf_buf.data(), kb) : 0;
+    // (the pcap input's BPF filter, PcapInputStream.cpp:485-488, runs on the device on each batch:
+    // pv_process_device)
+    return process_host_block(c, recs, bytes);
 }
 
 namespace {
@@ -5472,6 +5718,784 @@ int pv_merge_topn(pv_ctx *c, const uint8_t *buf, size_t bytes)
     return 0;
 }
 
+int comm_allgather_locked(pv_ctx *c, const void *buf, size_t bytes, std::vector<uint8_t> &out);
+
+// ------------------------------------------------------------------ multi-GPU top-N exchange
+// (pv_topn_x_*, pv_comm_merge_topn; kernels pv_topn_x* in pv_kernels.hip). Every table's
+// regions are split over the ranks in contiguous blocks; a rank ships the live entries of the
+// regions others own to their owners (device lists, RCCL point-to-point or host blobs), and
+// each owner merges them into its regions with pv_topn_merge. Afterwards a rank's top-N view is
+// its own regions; pv_topn_x_candidates / _names / _view then assemble the merged lists from
+// every owner's leading entries, names fetched from whichever rank holds them.
+namespace {
+const uint32_t X_MAGIC = 0x31585650u; // "PVX1"
+// candidates per metric and owner: topn_count and the entries tied with the last; a tied group
+// larger than this is cut by key order (the merged list's order among equal estimates can then
+// differ from one stream's, which orders them by name)
+const size_t PV_X_TIES = 8192;
+struct XPrep {
+    PvXTabs T;
+    uint32_t nreg = 0, E = 0;
+    std::vector<uint32_t> hdr;      // the header stream, (owner, handler, region, slot) order
+    std::vector<uint64_t> dtot, dstart; // entries per owner, where its slice starts
+};
+uint32_t x_lo_h(uint32_t d, uint32_t nreg, uint32_t W) { return (uint32_t)(((uint64_t)d * nreg + W - 1) / W); }
+
+void x_tables(pv_ctx *c, PvXTabs &T, uint32_t W, uint32_t me)
+{
+    memset(&T, 0, sizeof T);
+    T.W = W;
+    T.me = me;
+    for (uint32_t s : c->net.slots) T.tb[T.n++] = s;
+    for (uint32_t s : c->dns.slots) T.tb[T.n++] = PV_SLOTS + s;
+}
+
+// the parameter block the exchange kernels read (tables, geometry), uploaded to d_xp
+int x_params(pv_ctx *c, PvParams &P)
+{
+    params_common(c, P, nullptr, nullptr, 0);
+    P.tcap_log2 = c->tcap_log2;
+    P.reg_log2 = c->reg_log2;
+    P.tkeys = c->d_tkeys;
+    P.tcnt = c->d_tcnt;
+    P.taux = c->d_taux;
+    P.tab_live = c->d_tab_live;
+    P.flags = c->d_status + ST_FLAGS;
+    P.cpc = c->d_cpc;
+    P.sum = c->d_sum;
+    hipError_t e;
+    if (!c->d_xp && !hip_ok(e = hipMalloc(&c->d_xp, sizeof(PvParams)))) return c->hipfail(e, "exchange parameters");
+    if (!hip_ok(e = hipMemcpyAsync(c->d_xp, &P, sizeof P, hipMemcpyHostToDevice, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "exchange parameters");
+    return 0;
+}
+
+int x_grow(pv_ctx *c, void **p, size_t &have, size_t need, const char *what)
+{
+    if (need <= have) return 0;
+    hipError_t e;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    have = 0;
+    if (!hip_ok(e = hipMalloc(p, std::max<size_t>(need, 256)))) return c->hipfail(e, what);
+    have = std::max<size_t>(need, 256);
+    return 0;
+}
+
+// the send list on the device (d_xsend) and its layout on the host
+int x_prepare(pv_ctx *c, uint32_t W, uint32_t me, XPrep &X)
+{
+    hipSetDevice(c->device);
+    flush_fills(c);
+    x_tables(c, X.T, W, me);
+    X.nreg = 1u << c->reg_log2;
+    X.E = 2 * X.nreg * PV_SLOTS;
+    PvParams P;
+    if (int rc = x_params(c, P)) return rc;
+    hipError_t e;
+    size_t need = (size_t)X.E * 4;
+    if (int rc = x_grow(c, (void **)&c->d_xcnt, c->xcnt_bytes, need * 3, "exchange counts")) return rc;
+    uint32_t *d_cnt = c->d_xcnt, *d_off = c->d_xcnt + X.E, *d_hdr = c->d_xcnt + 2 * X.E;
+    if (!hip_ok(e = hipMemsetAsync(d_cnt, 0, need, c->stream))) return c->hipfail(e, "exchange counts");
+    if (X.T.n) {
+        hipLaunchKernelGGL(pv_topn_xcount, dim3(X.T.n * X.nreg), dim3(256), 0, c->stream, (const PvParams *)c->d_xp, X.T, d_cnt);
+        if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_topn_xcount");
+    }
+    hipLaunchKernelGGL(pv_topn_xscan, dim3(1), dim3(1024), 0, c->stream, c->reg_log2, W, (const uint32_t *)d_cnt, d_off, d_hdr);
+    X.hdr.resize(X.E);
+    if (!hip_ok(e = hipGetLastError()) ||
+        !hip_ok(e = hipMemcpyAsync(X.hdr.data(), d_hdr, need, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "exchange scan");
+    X.dtot.assign(W, 0);
+    X.dstart.assign(W + 1, 0);
+    for (uint32_t d = 0; d < W; d++) {
+        const uint32_t lo = x_lo_h(d, X.nreg, W), hi = x_lo_h(d + 1, X.nreg, W);
+        for (uint32_t p = 2 * PV_SLOTS * lo; p < 2 * PV_SLOTS * hi; p++) X.dtot[d] += X.hdr[p];
+        X.dstart[d + 1] = X.dstart[d] + X.dtot[d];
+    }
+    if (int rc = x_grow(c, &c->d_xsend, c->xsend_bytes, (size_t)X.dstart[W] * 16, "exchange send list")) return rc;
+    if (X.T.n && X.dstart[W]) {
+        hipLaunchKernelGGL(pv_topn_xwrite, dim3(X.T.n * X.nreg), dim3(256), 0, c->stream, (const PvParams *)c->d_xp, X.T,
+                           (const uint32_t *)d_off, (ulonglong2 *)c->d_xsend);
+        if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipStreamSynchronize(c->stream))) return c->hipfail(e, "exchange list");
+    }
+    return 0;
+}
+
+// merge the received lists (device: d_xrecv, W slots of `stride` entries; headers d_xrhdr) into
+// this rank's regions
+int x_merge_recv(pv_ctx *c, uint32_t W, uint32_t me, const std::vector<uint64_t> &rtot, uint64_t stride)
+{
+    const uint32_t nreg = 1u << c->reg_log2;
+    const uint32_t lo = x_lo_h(me, nreg, W), hi = x_lo_h(me + 1, nreg, W);
+    if (stride >= (1u << 24)) return c->fail(PV_ECAPACITY, "multi-GPU top-N exchange: %lu entries from one rank exceed 2^24",
+                                             (unsigned long)stride);
+    uint64_t total = 0;
+    for (uint64_t v : rtot) total += v;
+    hipError_t e;
+    // the run table ([run key][column] of W columns, pv_topn_merge's layout)
+    if (W > c->cb_h_grid) {
+        if (c->d_cb_h) hipFree(c->d_cb_h);
+        c->d_cb_h = nullptr;
+        c->cb_h_grid = 0;
+        if (!hip_ok(e = hipMalloc(&c->d_cb_h, (size_t)((W + 7) & ~7u) << (PV_MAX_REGIONS_LOG2 + 4)))) return c->hipfail(e, "region runs");
+        c->cb_h_grid = W;
+    }
+    if (!total) { c->x_ranks = W; c->x_rank = me; return 0; }
+    hipLaunchKernelGGL(pv_topn_xruns, dim3(W), dim3(1024), 0, c->stream, c->reg_log2, W, me, (const uint32_t *)c->d_xrhdr,
+                       2 * PV_SLOTS * (hi - lo), (uint64_t *)c->d_cb_h);
+    if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_topn_xruns");
+    PvParams P;
+    params_common(c, P, nullptr, nullptr, 0);
+    P.tcap_log2 = c->tcap_log2;
+    P.reg_log2 = c->reg_log2;
+    P.tkeys = c->d_tkeys;
+    P.tcnt = c->d_tcnt;
+    P.taux = c->d_taux;
+    P.tab_live = c->d_tab_live;
+    P.flags = c->d_status + ST_FLAGS;
+    P.cpc = c->d_cpc;
+    P.xmerge = 1;
+    P.x_lo = lo;
+    P.x_hi = hi;
+    P.cb = (uint64_t *)c->d_xrecv;
+    P.cb_fan = 1;
+    P.mq_cap = (uint32_t)stride;
+    P.cb_grid = W;
+    P.cb_run = (uint64_t *)c->d_cb_h;
+    P.cb_hm = c->d_cb_cnt + 32768;
+    P.tp_hands = c->d_cb_cnt + 32768 + 1024; // a word holding 3: both handlers
+    P.slot_of[0] = c->net.slots.empty() ? 0 : c->net.slots.front();
+    P.dslot_of[0] = c->dns.slots.empty() ? 0 : c->dns.slots.front();
+    if (W + 1 > 1024 + 1) return c->fail(PV_EINVAL, "%u ranks", W);
+    launch_fill32(c, c->d_cb_cnt + 32768, 1024 + 1, 3u);
+    launch_fill32(c, c->d_status + ST_FLAGS, 1, 0u);
+    flush_fills(c);
+    if (!c->d_xp && !hip_ok(e = hipMalloc(&c->d_xp, sizeof(PvParams)))) return c->hipfail(e, "exchange parameters");
+    if (!hip_ok(e = hipMemcpyAsync(c->d_xp, &P, sizeof P, hipMemcpyHostToDevice, c->stream))) return c->hipfail(e, "exchange parameters");
+    hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(pv_topn_merge_threads()), 0, c->stream, (const PvParams *)c->d_xp);
+    uint32_t flags = 0;
+    if (!hip_ok(e = hipGetLastError()) ||
+        !hip_ok(e = hipMemcpyAsync(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "exchange merge");
+    if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "multi-GPU top-N merge: a region is full (raise table_log2)");
+    for (uint32_t s : c->net.slots) c->net.clean[s] = false;
+    for (uint32_t s : c->dns.slots) c->dns.clean[s] = false;
+    c->x_ranks = W;
+    c->x_rank = me;
+    return 0;
+}
+
+// the purge offsets (frequent-items thetas) of the live tables' regions, nreg u64 per table
+void x_roff_pack(pv_ctx *c, const PvXTabs &T, uint32_t nreg, std::vector<uint64_t> &o)
+{
+    o.assign((size_t)T.n * nreg, 0);
+    for (uint32_t t = 0; t < T.n; t++)
+        if (!c->roff[T.tb[t]].empty())
+            for (uint32_t r = 0; r < nreg; r++) o[(size_t)t * nreg + r] = c->roff[T.tb[t]][r];
+}
+// add another rank's offsets of this rank's regions
+void x_roff_add(pv_ctx *c, const PvXTabs &T, uint32_t nreg, uint32_t lo, uint32_t hi, const uint64_t *o)
+{
+    for (uint32_t t = 0; t < T.n; t++) {
+        bool any = false;
+        for (uint32_t r = lo; r < hi && !any; r++) any = o[(size_t)t * nreg + r] != 0;
+        if (!any) continue;
+        std::vector<uint64_t> &ro = c->roff[T.tb[t]];
+        if (ro.empty()) ro.assign(nreg, 0);
+        for (uint32_t r = lo; r < hi; r++) ro[r] += o[(size_t)t * nreg + r];
+    }
+}
+} // namespace
+
+// blob: magic, W, rank, ntab, nreg | tb[ntab] | roff[ntab][nreg] | dtot[W] | hdr[E] | entries
+int pv_topn_x_export(pv_ctx *c, uint32_t W, uint32_t me, uint8_t **blob, size_t *bytes)
+{
+    *blob = nullptr;
+    *bytes = 0;
+    if (W < 1 || me >= W || W > 1024) return c->fail(PV_EINVAL, "rank %u of %u", me, W);
+    std::lock_guard<std::mutex> g(c->mu);
+    XPrep X;
+    if (int rc = x_prepare(c, W, me, X)) return rc;
+    std::vector<uint64_t> ro;
+    x_roff_pack(c, X.T, X.nreg, ro);
+    const size_t head = 20 + 4 * (size_t)X.T.n;
+    const size_t n = head + ro.size() * 8 + (size_t)W * 8 + (size_t)X.E * 4 + (size_t)X.dstart[W] * 16;
+    uint8_t *o = (uint8_t *)malloc(n);
+    if (!o) return c->fail(PV_ECAPACITY, "exchange blob");
+    const uint32_t h[5] = {X_MAGIC, W, me, X.T.n, X.nreg};
+    memcpy(o, h, 20);
+    memcpy(o + 20, X.T.tb, 4 * (size_t)X.T.n);
+    size_t at = head;
+    memcpy(o + at, ro.data(), ro.size() * 8);
+    at += ro.size() * 8;
+    memcpy(o + at, X.dtot.data(), (size_t)W * 8);
+    at += (size_t)W * 8;
+    memcpy(o + at, X.hdr.data(), (size_t)X.E * 4);
+    at += (size_t)X.E * 4;
+    hipError_t e;
+    if (X.dstart[W] && !hip_ok(e = hipMemcpy(o + at, c->d_xsend, (size_t)X.dstart[W] * 16, hipMemcpyDeviceToHost))) {
+        free(o);
+        return c->hipfail(e, "exchange download");
+    }
+    *blob = o;
+    *bytes = n;
+    return 0;
+}
+
+int pv_topn_x_import(pv_ctx *c, uint32_t W, uint32_t me, const uint8_t *const *blobs, const size_t *sizes)
+{
+    if (W < 1 || me >= W || W > 1024) return c->fail(PV_EINVAL, "rank %u of %u", me, W);
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    PvXTabs T;
+    x_tables(c, T, W, me);
+    const uint32_t nreg = 1u << c->reg_log2, E = 2 * nreg * PV_SLOTS;
+    const uint32_t lo = x_lo_h(me, nreg, W), hi = x_lo_h(me + 1, nreg, W);
+    struct Src { const uint64_t *ro, *dtot; const uint32_t *hdr; const uint8_t *ent; };
+    std::vector<Src> src(W);
+    std::vector<uint64_t> rtot(W, 0);
+    uint64_t stride = 0;
+    for (uint32_t q = 0; q < W; q++) {
+        const uint8_t *b = blobs[q];
+        uint32_t h[5];
+        if (!b || sizes[q] < 20) return c->fail(PV_EINVAL, "exchange blob %u missing", q);
+        memcpy(h, b, 20);
+        if (h[0] != X_MAGIC || h[1] != W || h[2] != q || h[3] != T.n || h[4] != nreg || memcmp(b + 20, T.tb, 4 * (size_t)T.n))
+            return c->fail(PV_EINVAL, "exchange blob %u does not match this rank's windows", q);
+        size_t at = 20 + 4 * (size_t)T.n;
+        src[q].ro = reinterpret_cast<const uint64_t *>(b + at);
+        at += (size_t)T.n * nreg * 8;
+        src[q].dtot = reinterpret_cast<const uint64_t *>(b + at);
+        at += (size_t)W * 8;
+        src[q].hdr = reinterpret_cast<const uint32_t *>(b + at);
+        at += (size_t)E * 4;
+        src[q].ent = b + at;
+        uint64_t all = 0;
+        for (uint32_t d = 0; d < W; d++) all += src[q].dtot[d];
+        if (at + all * 16 > sizes[q]) return c->fail(PV_EINVAL, "exchange blob %u truncated", q);
+        rtot[q] = q == me ? 0 : src[q].dtot[me];
+        stride = std::max(stride, rtot[q]);
+    }
+    hipError_t e;
+    const size_t hlen = (size_t)2 * PV_SLOTS * (hi - lo);
+    if (int rc = x_grow(c, (void **)&c->d_xrhdr, c->xrhdr_bytes, std::max<size_t>(1, W * hlen) * 4, "exchange headers")) return rc;
+    if (int rc = x_grow(c, &c->d_xrecv, c->xrecv_bytes, std::max<size_t>(1, W * stride) * 16, "exchange receive list")) return rc;
+    for (uint32_t q = 0; q < W; q++) {
+        if (q == me) continue;
+        uint64_t before = 0;
+        for (uint32_t d = 0; d < me; d++) before += src[q].dtot[d];
+        if (!hip_ok(e = hipMemcpyAsync(c->d_xrhdr + (size_t)q * hlen, src[q].hdr + (size_t)2 * PV_SLOTS * lo, hlen * 4,
+                                       hipMemcpyHostToDevice, c->stream)) ||
+            (rtot[q] && !hip_ok(e = hipMemcpyAsync((uint8_t *)c->d_xrecv + (size_t)q * stride * 16, src[q].ent + before * 16,
+                                                   rtot[q] * 16, hipMemcpyHostToDevice, c->stream))))
+            return c->hipfail(e, "exchange upload");
+        x_roff_add(c, T, nreg, lo, hi, src[q].ro);
+    }
+    return x_merge_recv(c, W, me, rtot, stride);
+}
+
+int pv_comm_merge_topn(pv_ctx *c)
+{
+    if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
+    const uint32_t W = (uint32_t)c->comm_ranks, me = (uint32_t)c->comm_rank;
+    std::lock_guard<std::mutex> g(c->mu);
+    XPrep X;
+    if (int rc = x_prepare(c, W, me, X)) return rc;
+    const uint32_t nreg = X.nreg, lo = x_lo_h(me, nreg, W), hi = x_lo_h(me + 1, nreg, W);
+    hipError_t e;
+    // entries per (source, this rank), and the purge offsets: one small all-to-all / all-gather
+    if (int rc = x_grow(c, (void **)&c->d_xtot, c->xtot_bytes, (size_t)W * 16, "exchange counts")) return rc;
+    if (!hip_ok(e = hipMemcpyAsync(c->d_xtot, X.dtot.data(), (size_t)W * 8, hipMemcpyHostToDevice, c->stream)))
+        return c->hipfail(e, "exchange counts");
+    ncclResult_t r = ncclGroupStart();
+    for (uint32_t q = 0; q < W && r == ncclSuccess; q++) {
+        if (q == me) continue;
+        r = ncclSend(c->d_xtot + q, 1, ncclUint64, (int)q, c->comm, c->stream);
+        if (r == ncclSuccess) r = ncclRecv(c->d_xtot + W + q, 1, ncclUint64, (int)q, c->comm, c->stream);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess) return c->fail(PV_EHIP, "exchange counts: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+    std::vector<uint64_t> rtot(W, 0);
+    if (!hip_ok(e = hipMemcpyAsync(rtot.data(), c->d_xtot + W, (size_t)W * 8, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "exchange counts");
+    rtot[me] = 0;
+    uint64_t stride = 0;
+    for (uint64_t v : rtot) stride = std::max(stride, v);
+    const size_t hlen = (size_t)2 * PV_SLOTS * (hi - lo);
+    if (int rc = x_grow(c, (void **)&c->d_xrhdr, c->xrhdr_bytes, std::max<size_t>(1, W * hlen) * 4, "exchange headers")) return rc;
+    if (int rc = x_grow(c, &c->d_xrecv, c->xrecv_bytes, std::max<size_t>(1, W * stride) * 16, "exchange receive list")) return rc;
+    const uint32_t *d_hdr = c->d_xcnt + 2 * X.E;
+    r = ncclGroupStart();
+    for (uint32_t q = 0; q < W && r == ncclSuccess; q++) {
+        if (q == me) continue;
+        const uint32_t qlo = x_lo_h(q, nreg, W), qhi = x_lo_h(q + 1, nreg, W);
+        r = ncclSend(d_hdr + (size_t)2 * PV_SLOTS * qlo, (size_t)2 * PV_SLOTS * (qhi - qlo), ncclUint32, (int)q, c->comm, c->stream);
+        if (r == ncclSuccess) r = ncclRecv(c->d_xrhdr + (size_t)q * hlen, hlen, ncclUint32, (int)q, c->comm, c->stream);
+        if (r == ncclSuccess && X.dtot[q])
+            r = ncclSend((const uint8_t *)c->d_xsend + X.dstart[q] * 16, X.dtot[q] * 2, ncclUint64, (int)q, c->comm, c->stream);
+        if (r == ncclSuccess && rtot[q])
+            r = ncclRecv((uint8_t *)c->d_xrecv + (size_t)q * stride * 16, rtot[q] * 2, ncclUint64, (int)q, c->comm, c->stream);
+    }
+    r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess) return c->fail(PV_EHIP, "exchange lists: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+    // purge offsets (host blobs, a few KB)
+    {
+        std::vector<uint64_t> ro;
+        x_roff_pack(c, X.T, nreg, ro);
+        bool any = false;
+        for (uint64_t v : ro) any |= v != 0;
+        uint8_t anyb = any ? 1 : 0;
+        // (skipped when no rank purged: one byte each first)
+        std::vector<uint8_t> flags;
+        if (int rc = comm_allgather_locked(c, &anyb, 1, flags)) return rc;
+        bool someone = false;
+        for (uint8_t f : flags) someone |= f != 0;
+        if (someone) {
+            std::vector<uint8_t> all;
+            if (int rc = comm_allgather_locked(c, ro.data(), ro.size() * 8, all)) return rc;
+            for (uint32_t q = 0; q < W; q++)
+                if (q != me) x_roff_add(c, X.T, nreg, lo, hi, reinterpret_cast<const uint64_t *>(all.data() + (size_t)q * ro.size() * 8));
+        }
+    }
+    return x_merge_recv(c, W, me, rtot, stride);
+}
+
+// ---- the merged view's lists: every owner's leading entries per metric, names from any rank
+namespace {
+// the text of a table entry's name record (read_topn's rules)
+void x_name_text(uint32_t metric, const uint8_t *rec, uint32_t len, std::string &out)
+{
+    char b[64];
+    if (metric == TM_IPV6 && len == 16) out = inet_ntop(AF_INET6, rec, b, sizeof b) ? b : "";
+    else if (metric == TM_ECS && len == 17) out = inet_ntop(rec[0] == 1 ? AF_INET : AF_INET6, rec + 1, b, sizeof b) ? b : "";
+    else out.assign((const char *)rec, len);
+}
+// a name record of table tb at aux (0: none): its text, or false
+bool x_read_name(pv_ctx *c, uint32_t tb, uint64_t key, uint32_t aux, std::string &out)
+{
+    if (!aux) return false;
+    uint8_t l2[2];
+    const uint8_t *base = c->d_arena + (uint64_t)tb * c->arena_cap + (aux - 1);
+    if (!hip_ok(hipMemcpy(l2, base, 2, hipMemcpyDeviceToHost))) return false;
+    const uint32_t len = l2[0] | (l2[1] << 8);
+    std::vector<uint8_t> b(len);
+    if (len && !hip_ok(hipMemcpy(b.data(), base + 2, len, hipMemcpyDeviceToHost))) return false;
+    x_name_text(PV_KEY_METRIC(key), b.data(), len, out);
+    return true;
+}
+void put_u32(std::vector<uint8_t> &o, uint32_t v) { const size_t p = o.size(); o.resize(p + 4); memcpy(&o[p], &v, 4); }
+void put_u64(std::vector<uint8_t> &o, uint64_t v) { const size_t p = o.size(); o.resize(p + 8); memcpy(&o[p], &v, 8); }
+void put_name(std::vector<uint8_t> &o, const std::string *s)
+{
+    const uint16_t l = s ? (uint16_t)std::min<size_t>(s->size(), 65534) : (uint16_t)0xffff;
+    const size_t p = o.size();
+    o.resize(p + 2 + (s ? l : 0));
+    memcpy(&o[p], &l, 2);
+    if (s && l) memcpy(&o[p + 2], s->data(), l);
+}
+} // namespace
+
+// The slot sets a window read asks for, per part: each live slot alone and each run of the most
+// recent slots (merged windows); a set id is part << 16 | slot mask.
+void x_slot_sets(pv_ctx *c, int part, std::vector<uint32_t> &v)
+{
+    const Window &w = part == PART_NET ? c->net : c->dns;
+    v.clear();
+    uint32_t m = 0;
+    for (size_t i = 0; i < w.slots.size(); i++) {
+        v.push_back(((uint32_t)part << 16) | (1u << w.slots[i]));
+        m |= 1u << w.slots[i];
+        if (i) v.push_back(((uint32_t)part << 16) | m);
+    }
+}
+
+// candidates: u32 set id | u64 key | u64 estimate | u16 name length (0xffff: unknown here) | name.
+// Per slot set and metric, this rank's regions' leading entries by the estimate summed over the
+// set's tables (the merged window's counts).
+int pv_topn_x_candidates(pv_ctx *c, uint8_t **blob, size_t *bytes)
+{
+    *blob = nullptr;
+    *bytes = 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->x_ranks < 1) return c->fail(PV_EINVAL, "no multi-GPU top-N merge on this context (pv_topn_x_import / pv_comm_merge_topn)");
+    hipSetDevice(c->device);
+    flush_fills(c);
+    const uint32_t W = c->x_ranks, me = c->x_rank, nreg = 1u << c->reg_log2, rsl = c->tcap_log2 - c->reg_log2;
+    const uint32_t lo = x_lo_h(me, nreg, W), hi = x_lo_h(me + 1, nreg, W);
+    const size_t K = std::max<size_t>(c->cfg.topn_count, 1);
+    const size_t n = (size_t)(hi - lo) << rsl;
+    std::vector<uint8_t> o;
+    hipError_t e;
+    // each live table's regions, read once
+    struct Slice { std::vector<uint64_t> keys, cnt; std::vector<uint32_t> aux; };
+    std::map<uint32_t, Slice> sl;
+    auto slice = [&](uint32_t tb) -> const Slice * {
+        auto it = sl.find(tb);
+        if (it != sl.end()) return &it->second;
+        Slice &x = sl[tb];
+        const size_t base = ((size_t)tb << c->tcap_log2) + ((size_t)lo << rsl);
+        x.keys.resize(n); x.cnt.resize(n); x.aux.resize(n);
+        if (n && (!hip_ok(e = hipMemcpy(x.keys.data(), c->d_tkeys + base, n * 8, hipMemcpyDeviceToHost)) ||
+                  !hip_ok(e = hipMemcpy(x.cnt.data(), c->d_tcnt + base, n * 8, hipMemcpyDeviceToHost)) ||
+                  !hip_ok(e = hipMemcpy(x.aux.data(), c->d_taux + base, n * 4, hipMemcpyDeviceToHost))))
+            return nullptr;
+        return &x;
+    };
+    for (int part = PART_NET; part <= PART_DNS; part++) {
+        std::vector<uint32_t> sets;
+        x_slot_sets(c, part, sets);
+        for (uint32_t set : sets) {
+            // key -> (estimate summed over the set's tables, a table and aux holding its name)
+            std::unordered_map<uint64_t, std::tuple<uint64_t, uint32_t, uint32_t>> sum;
+            for (uint32_t s = 0; s < PV_SLOTS; s++) {
+                if (!((set >> s) & 1)) continue;
+                const uint32_t tb = s + (part == PART_DNS ? PV_SLOTS : 0);
+                const Slice *x = slice(tb);
+                if (!x) return c->hipfail(e, "read top-N regions");
+                const std::vector<uint64_t> &roff = c->roff[tb];
+                for (size_t i = 0; i < n; i++) {
+                    if (!x->keys[i]) continue;
+                    auto &v = sum[x->keys[i]];
+                    std::get<0>(v) += x->cnt[i] + (roff.empty() ? 0 : roff[lo + (i >> rsl)]);
+                    if (!std::get<2>(v) && x->aux[i]) { std::get<1>(v) = tb; std::get<2>(v) = x->aux[i]; }
+                }
+            }
+            std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> by; // host metric -> (estimate, key)
+            for (auto &kv : sum) by[host_metric(c, kv.first)].push_back({std::get<0>(kv.second), kv.first});
+            for (auto &mv : by) {
+                auto &v = mv.second;
+                std::sort(v.begin(), v.end(), [](const auto &a, const auto &b2) { return a.first != b2.first ? a.first > b2.first : a.second < b2.second; });
+                // the topn_count leading entries and every entry tied with the last of them (the lists
+                // order ties by name, which only the whole tied group decides; at most PV_X_TIES)
+                size_t m = std::min(K, v.size());
+                while (m < v.size() && m < PV_X_TIES && v[m].first == v[m - 1].first) m++;
+                for (size_t k = 0; k < m; k++) {
+                    const uint64_t key = v[k].second;
+                    const auto &sv = sum[key];
+                    put_u32(o, set);
+                    put_u64(o, key);
+                    put_u64(o, v[k].first);
+                    std::string nm;
+                    if (PV_KEY_METRIC(key) == TM_IPV4) {
+                        const uint32_t ip = (uint32_t)key;
+                        char bb[20];
+                        snprintf(bb, sizeof bb, "%u.%u.%u.%u", ip & 0xff, (ip >> 8) & 0xff, (ip >> 16) & 0xff, ip >> 24);
+                        nm = bb;
+                        put_name(o, &nm);
+                    } else if (x_read_name(c, std::get<1>(sv), key, std::get<2>(sv), nm)) {
+                        put_name(o, &nm);
+                    } else {
+                        put_name(o, nullptr);
+                    }
+                }
+            }
+        }
+    }
+    *blob = (uint8_t *)malloc(std::max<size_t>(o.size(), 1));
+    if (!*blob) return c->fail(PV_ECAPACITY, "candidates");
+    memcpy(*blob, o.data(), o.size());
+    *bytes = o.size();
+    return 0;
+}
+
+namespace {
+struct XCand {
+    uint32_t tb;
+    uint64_t key, est;
+    bool named;
+    std::string name;
+};
+bool x_parse_cands(const uint8_t *b, size_t n, std::vector<XCand> &out)
+{
+    size_t p = 0;
+    while (p < n) {
+        if (p + 22 > n) return false;
+        XCand x;
+        uint16_t l;
+        memcpy(&x.tb, b + p, 4);
+        memcpy(&x.key, b + p + 4, 8);
+        memcpy(&x.est, b + p + 12, 8);
+        memcpy(&l, b + p + 20, 2);
+        p += 22;
+        x.named = l != 0xffff;
+        if (x.named) {
+            if (p + l > n) return false;
+            x.name.assign((const char *)b + p, l);
+            p += l;
+        }
+        out.push_back(std::move(x));
+    }
+    return true;
+}
+} // namespace
+
+// answers: the names this rank holds for candidates (of every rank) that came without one:
+// u32 tb | u64 key | u16 length | name
+int pv_topn_x_names(pv_ctx *c, const uint8_t *const *cands, const size_t *sizes, uint32_t n, uint8_t **blob, size_t *bytes)
+{
+    *blob = nullptr;
+    *bytes = 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    std::vector<XCand> want;
+    for (uint32_t q = 0; q < n; q++) {
+        std::vector<XCand> v;
+        if (!x_parse_cands(cands[q], sizes[q], v)) return c->fail(PV_EINVAL, "malformed candidate blob %u", q);
+        for (auto &x : v)
+            if (!x.named) want.push_back(x);
+    }
+    std::vector<uint8_t> o;
+    // each wanted key against every live table of its set's part (a rank may hold it in any period)
+    {
+        std::vector<XCand> w2;
+        for (auto &x : want) {
+            const int part = (int)(x.tb >> 16);
+            for (uint32_t s : (part == PART_DNS ? c->dns.slots : c->net.slots)) {
+                XCand y = x;
+                y.tb = s + (part == PART_DNS ? PV_SLOTS : 0);
+                y.name = std::to_string(x.tb); // (the set id, for the answer)
+                w2.push_back(y);
+            }
+        }
+        want.swap(w2);
+    }
+    if (!want.empty()) {
+        std::vector<uint64_t> keys;
+        std::vector<uint32_t> tbs;
+        for (auto &x : want) { keys.push_back(x.key); tbs.push_back(x.tb); }
+        PvParams P;
+        if (int rc = x_params(c, P)) return rc;
+        uint64_t *d_k = nullptr;
+        uint32_t *d_t = nullptr, *d_a = nullptr;
+        hipError_t e;
+        std::vector<uint32_t> aux(want.size());
+        if (!hip_ok(e = hipMalloc(&d_k, keys.size() * 8)) || !hip_ok(e = hipMalloc(&d_t, keys.size() * 4)) ||
+            !hip_ok(e = hipMalloc(&d_a, keys.size() * 4))) {
+            hipFree(d_k); hipFree(d_t); hipFree(d_a);
+            return c->hipfail(e, "name lookup");
+        }
+        bool ok = hip_ok(e = hipMemcpy(d_k, keys.data(), keys.size() * 8, hipMemcpyHostToDevice)) &&
+                  hip_ok(e = hipMemcpy(d_t, tbs.data(), tbs.size() * 4, hipMemcpyHostToDevice));
+        if (ok) {
+            hipLaunchKernelGGL(pv_topn_xlookup, dim3((uint32_t)((keys.size() + 255) / 256)), dim3(256), 0, c->stream,
+                               (const PvParams *)c->d_xp, (const uint64_t *)d_k, (const uint32_t *)d_t, (uint32_t)keys.size(), d_a);
+            ok = hip_ok(e = hipGetLastError()) && hip_ok(e = hipStreamSynchronize(c->stream)) &&
+                 hip_ok(e = hipMemcpy(aux.data(), d_a, aux.size() * 4, hipMemcpyDeviceToHost));
+        }
+        hipFree(d_k); hipFree(d_t); hipFree(d_a);
+        if (!ok) return c->hipfail(e, "name lookup");
+        std::set<std::pair<uint32_t, uint64_t>> done;
+        for (size_t i = 0; i < want.size(); i++) {
+            const uint32_t set = (uint32_t)std::stoul(want[i].name);
+            if (done.count({set, want[i].key})) continue;
+            std::string nm;
+            if (!x_read_name(c, want[i].tb, want[i].key, aux[i], nm)) continue;
+            done.insert({set, want[i].key});
+            put_u32(o, set);
+            put_u64(o, want[i].key);
+            put_name(o, &nm);
+        }
+    }
+    *blob = (uint8_t *)malloc(std::max<size_t>(o.size(), 1));
+    if (!*blob) return c->fail(PV_ECAPACITY, "name answers");
+    memcpy(*blob, o.data(), o.size());
+    *bytes = o.size();
+    return 0;
+}
+
+int pv_topn_x_view(pv_ctx *c, const uint8_t *const *cands, const size_t *csizes, const uint8_t *const *names,
+                   const size_t *nsizes, uint32_t n)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    std::map<std::pair<uint32_t, uint64_t>, std::string> known;
+    for (uint32_t q = 0; q < n; q++) {
+        const uint8_t *b = names[q];
+        size_t p = 0, m = nsizes[q];
+        while (p + 14 <= m) {
+            uint32_t tb; uint64_t key; uint16_t l;
+            memcpy(&tb, b + p, 4); memcpy(&key, b + p + 4, 8); memcpy(&l, b + p + 12, 2);
+            if (l == 0xffff || p + 14 + l > m) return c->fail(PV_EINVAL, "malformed name blob %u", q);
+            known[{tb, key}].assign((const char *)b + p + 14, l);
+            p += 14 + l;
+        }
+    }
+    c->x_view.clear();
+    for (uint32_t q = 0; q < n; q++) {
+        std::vector<XCand> v;
+        if (!x_parse_cands(cands[q], csizes[q], v)) return c->fail(PV_EINVAL, "malformed candidate blob %u", q);
+        for (auto &x : v) {
+            std::string nm = x.name;
+            if (!x.named) {
+                auto it = known.find({x.tb, x.key});
+                if (it != known.end()) nm = it->second;
+            }
+            c->x_view[x.tb][x.key] = {x.est, nm};
+        }
+    }
+    c->x_view_on = true;
+    return 0;
+}
+
+// ---- quantile inputs across shards without shipping the values: exact radix selection whose
+// per-pass group histograms (256 bins, one byte of the value) are summed over the ranks by a
+// caller-supplied all-reduce (pv_values_x_select) or RCCL (pv_comm_values_select). Per live DNS
+// slot and value kind: the count, p50/p90/p95/p99 and the maximum (the KLL inclusive rank rule
+// of Quantile, src/Metrics.h:334-481, on the union of the shards' values: what one stream
+// gives) and, for the time kinds, the count at or below each histogram point (Histogram,
+// src/Metrics.h:189-327). The merged view then holds a stand-in value list per slot and kind
+// with those counts, that maximum and those quantiles.
+namespace {
+int x_allreduce(pv_ctx *c, pv_allreduce_fn ar, void *user, std::vector<uint64_t> &buf, int op)
+{
+    if (buf.empty()) return 0;
+    if (ar) return ar(buf.data(), buf.size(), op, user) ? c->fail(PV_EINVAL, "all-reduce callback failed") : 0;
+    // RCCL on the context's communicator
+    hipError_t e;
+    uint64_t *d = nullptr;
+    if (!hip_ok(e = hipMalloc(&d, buf.size() * 8))) return c->hipfail(e, "selection all-reduce");
+    ncclResult_t r = ncclSuccess;
+    const bool ok = hip_ok(e = hipMemcpyAsync(d, buf.data(), buf.size() * 8, hipMemcpyHostToDevice, c->stream)) &&
+                    (r = ncclAllReduce(d, d, buf.size(), ncclUint64, op ? ncclMax : ncclSum, c->comm, c->stream)) == ncclSuccess &&
+                    hip_ok(e = hipMemcpyAsync(buf.data(), d, buf.size() * 8, hipMemcpyDeviceToHost, c->stream)) &&
+                    hip_ok(e = hipStreamSynchronize(c->stream));
+    hipFree(d);
+    if (r != ncclSuccess) return c->fail(PV_EHIP, "ncclAllReduce: %s", ncclGetErrorString(r));
+    if (!ok) return c->hipfail(e, "selection all-reduce");
+    return 0;
+}
+// rank of fraction p among n values (quantiles(): ceil(p n) - 1, clamped); p > 1: the maximum
+uint64_t x_rank_of(double p, uint64_t n)
+{
+    if (p > 1.0) return n ? n - 1 : 0;
+    const uint64_t w = (uint64_t)std::ceil(p * (double)n);
+    uint64_t idx = w == 0 ? 0 : w - 1;
+    return n && idx >= n ? n - 1 : idx;
+}
+// groups[g]: this rank's values of group g; fr[g]: the fractions wanted. out[g][k]: the value at
+// each fraction's rank over every rank's values (0 when the group is empty everywhere); n[g]: the
+// group's count over every rank
+int x_select(pv_ctx *c, pv_allreduce_fn ar, void *user, const std::vector<std::vector<uint64_t>> &groups,
+             const std::vector<std::vector<double>> &fr, std::vector<uint64_t> &n, std::vector<std::vector<uint64_t>> &out)
+{
+    const size_t G = groups.size();
+    struct Tg { uint32_t g; double p; uint64_t rank, prefix; };
+    std::vector<Tg> T;
+    for (uint32_t g = 0; g < G; g++)
+        for (double p : fr[g]) T.push_back(Tg{g, p, 0, 0});
+    n.assign(G, 0);
+    out.assign(G, {});
+    std::vector<uint64_t> h;
+    for (int pass = 0; pass < 8; pass++) {
+        const uint32_t shift = 56 - 8 * pass;
+        const uint64_t hm = pass == 0 ? 0ull : ~0ull << (shift + 8);
+        if (pass == 0) {
+            // one histogram per group (every target of a group shares it)
+            h.assign(G * 256, 0);
+            for (uint32_t g = 0; g < G; g++)
+                for (uint64_t x : groups[g]) h[(size_t)g * 256 + (x >> 56)]++;
+        } else {
+            h.assign(T.size() * 256, 0);
+            for (size_t t = 0; t < T.size(); t++)
+                for (uint64_t x : groups[T[t].g])
+                    if ((x & hm) == (T[t].prefix & hm)) h[t * 256 + ((x >> shift) & 255)]++;
+        }
+        if (int rc = x_allreduce(c, ar, user, h, 0)) return rc;
+        for (size_t t = 0; t < T.size(); t++) {
+            const uint64_t *hh = &h[(pass == 0 ? (size_t)T[t].g : t) * 256];
+            if (pass == 0) {
+                uint64_t tot = 0;
+                for (int b = 0; b < 256; b++) tot += hh[b];
+                n[T[t].g] = tot;
+                T[t].rank = x_rank_of(T[t].p, tot);
+            }
+            if (!n[T[t].g]) continue;
+            uint64_t cum = 0;
+            int b = 0;
+            while (b < 255 && cum + hh[b] <= T[t].rank) cum += hh[b++];
+            T[t].rank -= cum;
+            T[t].prefix |= (uint64_t)b << shift;
+        }
+    }
+    for (auto &t : T) out[t.g].push_back(n[t.g] ? t.prefix : 0);
+    return 0;
+}
+const uint32_t X_KINDS[9] = {XV_FROM_US, XV_TO_US, XV_RATIO, XV2_TIME, XV2_TIME + 1, XV2_TIME + 2, XV2_RATIO, XV2_RATIO + 1, XV2_RATIO + 2};
+bool x_time_kind(uint32_t k) { return k == XV_FROM_US || k == XV_TO_US || (k >= XV2_TIME && k < XV2_TIME + 3); }
+
+int values_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (int rc = sync_xvals(c)) return rc;
+    // groups: (slot set, kind), the sets a window read can ask for: each live DNS slot alone
+    // (window_json of one period) and each run of the most recent slots (merged windows)
+    std::vector<uint32_t> sets;
+    for (uint32_t s : c->dns.slots) sets.push_back(1u << s);
+    {
+        uint32_t m = 0;
+        for (size_t i = 0; i < c->dns.slots.size(); i++) {
+            m |= 1u << c->dns.slots[i];
+            if (i) sets.push_back(m);
+        }
+    }
+    const size_t G = sets.size() * 9;
+    std::vector<std::vector<uint64_t>> groups(G);
+    std::vector<std::vector<double>> fr(G, std::vector<double>{0.50, 0.90, 0.95, 0.99, 2.0});
+    std::map<uint32_t, uint32_t> sg_bit; // live slot | gen << 8 -> its slot bit
+    for (uint32_t s : c->dns.slots) sg_bit[s | (c->gen[s] << 8)] = 1u << s;
+    for (const PvXValue &v : c->xvals_host) {
+        auto it = sg_bit.find(v.slot);
+        if (it == sg_bit.end()) continue;
+        int k = 0;
+        while (k < 9 && v.kind != X_KINDS[k]) k++;
+        if (k == 9) continue;
+        for (size_t i = 0; i < sets.size(); i++)
+            if (sets[i] & it->second) groups[i * 9 + k].push_back(v.bits);
+    }
+    std::vector<uint64_t> n;
+    std::vector<std::vector<uint64_t>> q;
+    if (int rc = x_select(c, ar, user, groups, fr, n, q)) return rc;
+    // counts at or below each histogram point, time kinds
+    const std::vector<uint64_t> &pts = hist_points();
+    std::vector<uint64_t> cdf(G * pts.size(), 0);
+    for (size_t gi = 0; gi < G; gi++) {
+        if (!x_time_kind(X_KINDS[gi % 9])) continue;
+        std::vector<uint64_t> v = groups[gi];
+        std::sort(v.begin(), v.end());
+        for (size_t k = 0; k < pts.size(); k++) cdf[gi * pts.size() + k] = (uint64_t)(std::upper_bound(v.begin(), v.end(), pts[k]) - v.begin());
+    }
+    if (int rc = x_allreduce(c, ar, user, cdf, 0)) return rc;
+    c->xq.clear();
+    for (size_t gi = 0; gi < G; gi++) {
+        if (!n[gi]) continue;
+        XQuant &x = c->xq[{sets[gi / 9], X_KINDS[gi % 9]}];
+        x.n = n[gi];
+        x.q.assign(q[gi].begin(), q[gi].begin() + 4);
+        x.max = q[gi][4];
+        if (x_time_kind(X_KINDS[gi % 9])) x.cdf.assign(cdf.begin() + gi * pts.size(), cdf.begin() + (gi + 1) * pts.size());
+    }
+    c->xq_on = true;
+    return 0;
+}
+} // namespace
+
+int pv_values_x_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
+{
+    if (!ar) return c->fail(PV_EINVAL, "no all-reduce callback");
+    return values_select(c, ar, user);
+}
+
+int pv_comm_values_select(pv_ctx *c)
+{
+    if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
+    return values_select(c, nullptr, nullptr);
+}
+
 // The device regions of both live windows a multi-GPU reduce combines: each Net slot's
 // net part and each DNS slot's dns part of the SUM (all-reduce SUM) and MIN (all-reduce MIN)
 // words. The caller writes them, so they stop being clean.
@@ -5552,6 +6576,26 @@ int pv_comm_allreduce_window(pv_ctx *c)
     if (r != ncclSuccess || r2 != ncclSuccess) return c->fail(PV_EHIP, "ncclAllReduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
     hipError_t e;
     if (!hip_ok(e = hipStreamSynchronize(c->stream))) return c->hipfail(e, "window all-reduce");
+    return 0;
+}
+
+// all-gather of one equal-sized host block per rank (the caller holds c->mu)
+int comm_allgather_locked(pv_ctx *c, const void *buf, size_t bytes, std::vector<uint8_t> &out)
+{
+    const int R = c->comm_ranks;
+    out.assign((size_t)R * bytes, 0);
+    if (!bytes) return 0;
+    hipError_t e;
+    uint8_t *d = nullptr;
+    if (!hip_ok(e = hipMalloc(&d, bytes * (R + 1)))) return c->hipfail(e, "all-gather buffers");
+    ncclResult_t r = ncclSuccess;
+    bool ok = hip_ok(e = hipMemcpyAsync(d + bytes * R, buf, bytes, hipMemcpyHostToDevice, c->stream)) &&
+              (r = ncclAllGather(d + bytes * R, d, bytes, ncclUint8, c->comm, c->stream)) == ncclSuccess &&
+              hip_ok(e = hipMemcpyAsync(out.data(), d, bytes * R, hipMemcpyDeviceToHost, c->stream)) &&
+              hip_ok(e = hipStreamSynchronize(c->stream));
+    hipFree(d);
+    if (r != ncclSuccess) return c->fail(PV_EHIP, "ncclAllGather: %s", ncclGetErrorString(r));
+    if (!ok) return c->hipfail(e, "all-gather");
     return 0;
 }
 
@@ -6205,6 +7249,7 @@ int pv_slow_values_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
 // rank's deferred candidates of those periods checked against them and counted into the
 // periods' top_slow tables (DnsMetricsBucket::new_dns_transaction, dns/v1/DnsStreamHandler.cpp:
 // 1121-1136). Call before the top-N exchange.
+int slow_apply(pv_ctx *c, const std::vector<float> thr[5]);
 int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks)
 {
     std::lock_guard<std::mutex> g(c->mu);
@@ -6244,6 +7289,73 @@ int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, u
             thr[k][o] = t;
         }
     }
+    return slow_apply(c, thr);
+}
+
+// pv_slow_finish without shipping the values: each ordinal's p90 by the distributed selection
+int slow_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    hipSetDevice(c->device);
+    if (!c->slow_defer) return c->fail(PV_EINVAL, "pv_slow_finish without pv_set_slow_defer");
+    const bool v2 = c->dns2_groups != 0;
+    // (a collective: every rank takes part, even one with nothing to judge)
+    const bool want = c->started && (v2 ? (c->dns2_groups & PV_DNS2_XACT_TIMES) != 0
+                                        : ((c->dns_groups & PV_DNS_QUANTILES) && (c->dns_groups & PV_DNS_TRANSACTIONS)));
+    if (int rc = sync_xvals(c)) return rc;
+    constexpr int NK = 5;
+    // the ordinals: every rank's windows hold the same (global period plan)
+    const uint64_t live = c->dns.ordinal;
+    std::vector<std::vector<uint64_t>> groups((size_t)NK * (live + 1));
+    auto kind_of = [](uint32_t kind) {
+        return kind == XV_FROM_US ? 0 : kind == XV_TO_US ? 1 : (kind >= XV2_TIME && kind < XV2_TIME + 3) ? 2 + (int)(kind - XV2_TIME) : -1;
+    };
+    auto put = [&](uint64_t ord, const PvXValue &v) {
+        const int k = kind_of(v.kind);
+        if (k >= 0 && ord <= live) groups[(size_t)k * (live + 1) + ord].push_back(v.bits);
+    };
+    const size_t nloc = std::min(c->xv_local_end, c->xvals_host.size());
+    for (size_t i = 0; i < nloc; i++) {
+        auto it = c->sg_ord.find(c->xvals_host[i].slot);
+        if (it != c->sg_ord.end()) put(it->second, c->xvals_host[i]);
+    }
+    for (auto &ev : c->slow_xv) put(ev.first, ev.second);
+    std::vector<std::vector<double>> fr(groups.size(), std::vector<double>{0.90});
+    std::vector<uint64_t> n;
+    std::vector<std::vector<uint64_t>> q;
+    if (int rc = x_select(c, ar, user, groups, fr, n, q)) return rc;
+    if (!want) return 0;
+    std::vector<float> thr[NK];
+    for (int k = 0; k < NK; k++) {
+        thr[k].assign(live + 1, 0.0f);
+        float t = 0.0f;
+        for (uint64_t o = 1; o <= live; o++) {
+            const size_t gi = (size_t)k * (live + 1) + (o - 1);
+            if (n[gi]) t = (float)q[gi][0];
+            thr[k][o] = t;
+        }
+    }
+    return slow_apply(c, thr);
+}
+
+int pv_slow_x_finish(pv_ctx *c, pv_allreduce_fn ar, void *user)
+{
+    if (!ar) return c->fail(PV_EINVAL, "no all-reduce callback");
+    return slow_select(c, ar, user);
+}
+
+int pv_comm_slow_finish(pv_ctx *c)
+{
+    if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
+    return slow_select(c, nullptr, nullptr);
+}
+
+// this rank's deferred slow candidates against the thresholds of every ordinal (thr[k][ord]:
+// [0] from, [1] to (v1), [2 + d] DNS v2 direction d), counted into the periods' top_slow tables
+// (the caller holds c->mu)
+int slow_apply(pv_ctx *c, const std::vector<float> thr[5])
+{
+    const uint64_t live = c->dns.ordinal;
     // the window's periods: ordinal -> slot
     std::map<uint64_t, uint32_t> win;
     for (size_t i = 0; i < c->dns.slots.size(); i++) win[live - i] = c->dns.slots[i];

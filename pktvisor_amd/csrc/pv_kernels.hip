@@ -490,9 +490,10 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
         }
     }
     // (a TCP message's record lives in the TCP pass's arena, not the batch the retry reads: fail)
-    if (!done) table_overflow(P, slot, key, w, rep, ns == nullptr && !P.tcp_pass);
+    if (!done) table_overflow(P, slot, key, w, rep, ns == nullptr && !P.tcp_pass && !P.xmerge);
     if (created >= 0) atomicAdd(&P.tab_live[PV_TSLOT(slot, metric)], 1u);
-    if (created >= 0 && metric != TM_IPV4) P.taux[created] = write_name(P, slot, metric, rep, ns, key);
+    // (a multi-GPU owner merge knows no record: the name stays unknown, pv_comm_finalize fetches it)
+    if (created >= 0 && metric != TM_IPV4) P.taux[created] = P.xmerge ? 0u : write_name(P, slot, metric, rep, ns, key);
 }
 
 // global_add for pv_topn_merge's direct regions: a created entry's name goes to the new-name list
@@ -3413,6 +3414,7 @@ struct CombState {
     uint32_t tb[NR];  // tables (bit per PV_TSLOT) among each region's entries
     uint32_t wsum[16];
     uint32_t nsp;
+    uint32_t hm; // handlers among the entries (bit 0 Net, 1 DNS)
 };
 // combined entry (e0 = slot | table key, e1 = weight word | rep << 32) of a cache key;
 // IPv4 cache keys are dense entries (card << 33 | dir << 32 | address)
@@ -3441,7 +3443,7 @@ __device__ __forceinline__ void comb_count(PV_CREF(PvParams) P, St &S, uint64_t 
 // one aligned 4-entry bucket of the combine table: match or claim; false = the bucket is full of
 // other keys
 template <class St>
-__device__ __forceinline__ bool comb_bucket(St &S, uint32_t b, uint64_t ck, uint32_t w, uint32_t rep)
+__device__ __forceinline__ bool comb_bucket(PV_CREF(PvParams) P, St &S, uint32_t b, uint64_t ck, uint32_t w, uint32_t rep)
 {
     const uint4 *kp = reinterpret_cast<const uint4 *>(&S.key[b]);
     const uint4 lo = kp[0], hi = kp[1];
@@ -3462,6 +3464,15 @@ __device__ __forceinline__ bool comb_bucket(St &S, uint32_t b, uint64_t ck, uint
     }
     return false;
 }
+// an entry the LDS table cannot take: to the workgroup's spill list, counted
+template <class St>
+__device__ __forceinline__ void comb_spill(PV_CREF(PvParams) P, St &S, PV_G ulonglong2 *sp, uint64_t ck, uint32_t w,
+                                           uint32_t rep)
+{
+    const ulonglong2 e = comb_entry(ck, w, rep);
+    sp[atomicAdd(&S.nsp, 1u)] = e;
+    comb_count(P, S, e.x);
+}
 template <uint32_t CN, class St>
 __device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, St &S, PV_G ulonglong2 *sp, uint64_t ck, uint32_t w,
                                          uint32_t rep)
@@ -3469,13 +3480,9 @@ __device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, St &S, PV_G ulongl
     uint32_t pos = (uint32_t)(fmix64(ck) >> 20) & (CN - 1);
 #if PV_CB_BUCKET
     for (int g = 0; g < 4; g++)
-        if (comb_bucket(S, ((pos & ~3u) + 4u * g) & (CN - 1), ck, w, rep)) return;
-    {
-        const ulonglong2 e = comb_entry(ck, w, rep);
-        sp[atomicAdd(&S.nsp, 1u)] = e;
-        comb_count(P, S, e.x);
-        return;
-    }
+        if (comb_bucket(P, S, ((pos & ~3u) + 4u * g) & (CN - 1), ck, w, rep)) return;
+    comb_spill(P, S, sp, ck, w, rep);
+    return;
 #endif
     for (int probe = 0; probe < 16; probe++) {
         uint64_t cur = S.key[pos];
@@ -3490,9 +3497,7 @@ __device__ __forceinline__ void comb_add(PV_CREF(PvParams) P, St &S, PV_G ulongl
         }
         pos = (pos + 1) & (CN - 1);
     }
-    const ulonglong2 e = comb_entry(ck, w, rep);
-    sp[atomicAdd(&S.nsp, 1u)] = e;
-    comb_count(P, S, e.x);
+    comb_spill(P, S, sp, ck, w, rep);
 }
 
 // comb_add with the first probe's key and rep words already read (cur0 / rep0, read for a whole
@@ -3515,13 +3520,9 @@ __device__ __forceinline__ void comb_add_pre(PV_CREF(PvParams) P, St &S, PV_G ul
         return;
     }
     for (int g = 1; g <= 4; g++)
-        if (comb_bucket(S, ((pos & ~3u) + 4u * g) & (CN - 1), ck, w, rep)) return;
-    {
-        const ulonglong2 e = comb_entry(ck, w, rep);
-        sp[atomicAdd(&S.nsp, 1u)] = e;
-        comb_count(P, S, e.x);
-        return;
-    }
+        if (comb_bucket(P, S, ((pos & ~3u) + 4u * g) & (CN - 1), ck, w, rep)) return;
+    comb_spill(P, S, sp, ck, w, rep);
+    return;
 #endif
     for (int probe = 0; probe < 16; probe++) {
         if (probe) { cur = S.key[pos]; rep0 = 0; }
@@ -3537,9 +3538,7 @@ __device__ __forceinline__ void comb_add_pre(PV_CREF(PvParams) P, St &S, PV_G ul
         }
         pos = (pos + 1) & (CN - 1);
     }
-    const ulonglong2 e = comb_entry(ck, w, rep);
-    sp[atomicAdd(&S.nsp, 1u)] = e;
-    comb_count(P, S, e.x);
+    comb_spill(P, S, sp, ck, w, rep);
 }
 
 // exclusive prefix of v over the workgroup (all threads call it); *total = the sum
@@ -3577,11 +3576,15 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     if (threadIdx.x == 0) S.nsp = 0;
     __syncthreads();
     TST(0)
-    const uint64_t wbase = (uint64_t)blockIdx.x * P.mq_cap;
+    // this workgroup's grid ranges [g0, g1) (cb_fan of them): their update logs and IP logs into
+    // one table, one list at the first range's place
+    const uint32_t g0 = blockIdx.x * P.cb_fan, g1 = min(g0 + P.cb_fan, P.grid_main);
+    const uint64_t wbase = (uint64_t)g0 * P.mq_cap;
     PV_G ulonglong2 *sp = reinterpret_cast<PV_G ulonglong2 *>(P.tp_buf) + wbase;
     PV_G ulonglong2 *out = reinterpret_cast<PV_G ulonglong2 *>(P.cb) + wbase;
-    const uint32_t cnt = P.mq_cnt[blockIdx.x];
-    const PV_G uint64_t *q = P.mq + wbase * 2;
+    for (uint32_t gr = g0; gr < g1; gr++) {
+    const uint32_t cnt = P.mq_cnt[gr];
+    const PV_G uint64_t *q = P.mq + (uint64_t)gr * P.mq_cap * 2;
     batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; },
                [&](uint64_t, ulonglong2 e) { comb_add<CN>(P, S, sp, e.x, (uint32_t)e.y, (uint32_t)(e.y >> 32)); });
 #ifndef PV_ABL_COMB_NOIP
@@ -3589,7 +3592,7 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
 #endif
     if ((P.net_groups & PV_NET_TOP_IPS_BIT) && !PV_ABL_COMB_NOIP) {
         uint64_t a, z;
-        wg_records(P, blockIdx.x, a, z);
+        wg_records(P, gr, a, z);
         const PV_G uint64_t *ipl = P.iplog + a;
         if (P.ip_compact) {
             // the register-window pass's compact log: address + direction bit, then the
@@ -3623,7 +3626,7 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
                 for (int u = 0; u < PV_CB_U; u++)
                     if (ipv[u]) comb_add_pre<CN>(P, S, sp, ck[u], 1u, (uint32_t)(a + j0 + (uint64_t)u * bd), pos[u], cur[u], rp[u]);
             }
-            const uint32_t nx = P.ipx_cnt[blockIdx.x];
+            const uint32_t nx = P.ipx_cnt[gr];
             for (uint32_t q = threadIdx.x; q < nx; q += blockDim.x) comb_add<CN>(P, S, sp, ipl[q], 1u, P.ipx_rep[a + q]);
         } else {
             batched<PV_CB_U>(z - a, [&](uint64_t j) { return ipl[j]; }, [&](uint64_t j, uint64_t e) {
@@ -3631,6 +3634,8 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
             });
         }
     }
+    }
+    if (threadIdx.x == 0) S.hm = 0;
     __syncthreads();
     TST(1)
     // the table's entries per region (the spilled ones were counted as they spilled)
@@ -3643,22 +3648,26 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     const uint32_t r0 = min(threadIdx.x * per, nreg), r1 = min(r0 + per, nreg);
     uint32_t s = 0;
     for (uint32_t r = r0; r < r1; r++) s += S.h[r];
-    uint32_t total;
-    uint32_t run = block_excl_scan(s, S.wsum, total);
-    // handlers with entries in this batch (pv_topn_merge's workgroups of the other exit early)
-    if (threadIdx.x < 2) {
-        const uint32_t half = 1u << P.reg_log2;
-        uint32_t any = 0;
-        for (uint32_t r = threadIdx.x * half; r < (threadIdx.x + 1) * half && !any; r++) any = S.h[r];
-        if (any) atomicOr(P.tp_hands, 1u << threadIdx.x);
+    // handlers with entries in this workgroup (a share never straddles the two halves: per | half)
+    {
+        const uint32_t hb = s ? 1u << (r0 >> P.reg_log2) : 0u;
+        const uint64_t b0 = __ballot(hb & 1), b1 = __ballot(hb & 2);
+        if ((threadIdx.x & 63) == 0 && (b0 | b1)) atomicOr(&S.hm, (b0 ? 1u : 0u) | (b1 ? 2u : 0u));
     }
+    uint32_t total;
+    uint32_t run = block_excl_scan(s, S.wsum, total); // (its barriers publish S.hm)
+    const uint32_t hm = S.hm;
+    // handlers with entries in this batch (pv_topn_merge's workgroups of the other exit early)
+    if (threadIdx.x < 2 && ((hm >> threadIdx.x) & 1)) atomicOr(P.tp_hands, 1u << threadIdx.x);
+    if (threadIdx.x == 0) P.cb_hm[blockIdx.x] = hm;
     // this workgroup's column of the run table: [run key][XCD][workgroup / 8], so the
-    // workgroups of one XCD (blockIdx % 8) fill whole lines of its L2
-    const uint32_t ng8 = (P.grid_main + 7) / 8;
+    // workgroups of one XCD (blockIdx % 8) fill whole lines of its L2; a handler without entries
+    // here writes no words (the merge reads cb_hm first)
+    const uint32_t ng8 = (P.cb_grid + 7) / 8;
     PV_G uint64_t *col = P.cb_run + (blockIdx.x % 8) * ng8 + blockIdx.x / 8;
     for (uint32_t r = r0; r < r1; r++) {
         const uint32_t c = S.h[r];
-        col[(uint64_t)r * 8 * ng8] = pv_run_word(run, c, S.tb[r]);
+        if ((hm >> (r >> P.reg_log2)) & 1) col[(uint64_t)r * 8 * ng8] = pv_run_word(run, c, S.tb[r]);
         S.h[r] = run; // the placement cursor
         run += c;
     }
@@ -3697,77 +3706,97 @@ extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine_r12(
     topn_combine<2048, 2u << PV_MAX_REGIONS_LOG2>(P);
 }
 
+// Merge, round 5: a region's keys (32 KiB) and this batch's weight per entry (32 KiB) in LDS, so two
+// workgroups share a CU (one's loads overlap the other's inserts); the count words are read at
+// write-back for the existing entries the batch changed, never for the others; the IPv4 CPC
+// minima were applied by the combine. PV_CREATED marks an entry this batch claimed.
+#define PV_MG_THREADS 512
+#ifndef PV_MG_U2
+#define PV_MG_U2 4 // tuning: run entries in flight per merge thread
+#endif
+#define PV_MG_NN 640 // created named entries a workgroup lists in LDS (more go straight to the list)
+#define PV_CREATED (1ull << 63)
+#define PV_MV4 (1ull << 62)              // LDS key word of a v1 IPv4 entry (minima inside)
+#define PV_MN1 (0xffffffull << 32)       // its direction-1 minimum (0xffffff: none)
+#define PV_DL0 (0xffffffffull << 32)     // a weight word's start: direction-0 minimum unset
+// a v1 IPv4 table key (bits 32..55 zero; Net v2 keys set bit 40)
+__device__ __forceinline__ bool mv4_key(uint64_t k) { return PV_KEY_METRIC(k) == TM_IPV4 && !((k >> 40) & 1); }
+// an LDS key word without its batch state (created bit, direction-1 minimum)
+__device__ __forceinline__ uint64_t mv4_norm(uint64_t w) { return w & ~(PV_CREATED | ((w & PV_MV4) ? PV_MN1 : 0ull)); }
 struct MergeState {
-    uint64_t key[PV_RS];
-    uint64_t cnt[PV_RS];
-    uint32_t mn[2][PV_RS]; // smallest record index of an IPv4 key per direction (CPC)
-    uint32_t nidx[PV_RS]; // entries created in this batch: region index, source record
-    uint32_t nrep[PV_RS];
-    uint8_t dirty[PV_RS]; // entries this batch changed (only those are written back)
+    alignas(16) uint64_t key[PV_RS];
+    uint64_t dl[PV_RS];
+    uint32_t nrep[PV_MG_NN]; // created named entries: source record, region index (past the list's
+    uint16_t nidx[PV_MG_NN]; // capacity the source record waits in the entry's aux word)
     uint32_t nnew, nbase, ncr;
+    uint32_t ip4c; // the run key has IPv4 entries with a cardinality update
 };
-// The region's runs in the combine workgroups' region-sorted lists (cb_run): run w holds
-// entries [pref[w], pref[w+1]) of the region, from list w at start[w].
+// The region's runs in the combine workgroups' region-sorted lists (cb_run): run i holds
+// entries [pref[i], pref[i+1]) of the region, from list list[i] at start[i].
 struct MergeRuns {
     uint32_t start[PV_MAX_GRID + 8];
-    uint32_t list[PV_MAX_GRID + 8];
     uint32_t pref[PV_MAX_GRID + 9];
+    uint16_t list[PV_MAX_GRID + 8];
     uint32_t wsum[16];
     uint32_t tabs;
 };
-
-#define PV_MG_THREADS 1024
-static_assert(PV_MG_THREADS >= (PV_MAX_GRID + 7) / 8 * 8, "one run per merge thread");
-extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) pv_topn_merge(const PvParams *__restrict__ Pp)
+static_assert(2 * PV_MG_THREADS >= (PV_MAX_GRID + 7) / 8 * 8, "two runs per merge thread");
+static_assert(sizeof(MergeState) + sizeof(MergeRuns) <= 80 * 1024, "pv_topn_merge: two workgroups per CU");
+extern "C" uint32_t pv_topn_merge_threads() { return PV_MG_THREADS; }
+// (waves_per_eu 4: two 8-wave workgroups per CU need at most 128 VGPRs a lane)
+extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) __attribute__((amdgpu_waves_per_eu(4))) pv_topn_merge(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     const uint32_t rk = blockIdx.x;                  // run key: handler << reg_log2 | region
     const uint32_t r = rk & ((1u << P.reg_log2) - 1);
     const uint32_t hd = rk >> P.reg_log2;            // 0 Net tables, 1 DNS tables
     if (!((*P.tp_hands >> hd) & 1)) return; // no entry of this handler in the batch
+    if (P.xmerge && (r < P.x_lo || r >= P.x_hi)) return; // (multi-GPU owner merge: this rank's regions)
     __shared__ MergeRuns U;
+    __shared__ MergeState S;
     TST_DECL
-    const uint32_t ng8 = (P.grid_main + 7) / 8, ng = 8 * ng8;
-    // the region of the table this run key almost always holds (the handler's first period slot)
-    // is DMA'd into LDS now, in flight with the run words, not after them
+    const uint32_t ng8 = (P.cb_grid + 7) / 8, ng = 8 * ng8;
+    const uint64_t lcap = (uint64_t)P.cb_fan * P.mq_cap; // a combine workgroup's list capacity
     const uint32_t rsl = P.tcap_log2 - P.reg_log2;
     const uint32_t rs = 1u << rsl;
-    constexpr int PF = PV_RS / PV_MG_THREADS; // region entries per thread
-    static_assert(PF * PV_MG_THREADS == PV_RS, "region entries per thread");
     const uint32_t tbg = hd ? PV_SLOTS + P.dslot_of[0] : P.slot_of[0];
     const uint64_t rbg = ((uint64_t)tbg << P.tcap_log2) + ((uint64_t)r << rsl);
     const bool pf = rs == PV_RS;
-    __shared__ MergeState S;
     if (pf) {
-        // LDS-DMA straight into S.key / S.cnt: 32 1-KiB pieces each, two of each per wave (no
-        // VGPR holds them; the run words' wait below covers them)
-        static_assert(PV_RS * 8 == 32 * 1024 && PV_MG_THREADS == 1024, "two pieces per array and wave");
+        // the keys of the region this run key almost always holds (the handler's first period
+        // slot), LDS-DMA'd in flight with the run words: 32 1-KiB pieces, four per wave
+        static_assert(PV_RS * 8 == 32 * 1024 && PV_MG_THREADS == 512, "four pieces per wave");
         const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll
-        for (int q = 0; q < 2; q++) {
-            const uint32_t pc = wv * 2 + q;
+        for (int q = 0; q < 4; q++) {
+            const uint32_t pc = wv * 4 + q;
             dma16(P.tkeys + rbg + pc * 128 + ln * 2, lds_addr(&S.key[pc * 128]));
-            dma16(P.tcnt + rbg + pc * 128 + ln * 2, lds_addr(&S.cnt[pc * 128]));
         }
     }
     uint32_t n;
     {
-        uint32_t c = 0, tb = 0;
+        // runs 2t and 2t + 1 of the column (one 16-B load); a combine workgroup without entries of
+        // this handler wrote no words
+        uint32_t c0 = 0, c1 = 0, tb = 0;
         if (threadIdx.x == 0) U.tabs = 0;
-        if (threadIdx.x < ng) {
-            const uint32_t w = (threadIdx.x % ng8) * 8 + threadIdx.x / ng8; // the combine workgroup
-            if (w < P.grid_main) {
-                const uint64_t v = P.cb_run[(uint64_t)rk * ng + threadIdx.x];
-                U.start[threadIdx.x] = (uint32_t)v & 0xffffffu;
-                U.list[threadIdx.x] = w;
-                c = (uint32_t)(v >> 24) & 0xffffffu;
-                tb = (uint32_t)(v >> 48);
-            }
+        const uint32_t i0 = 2 * threadIdx.x;
+        if (i0 < ng) {
+            const ulonglong2 v = *reinterpret_cast<const PV_G ulonglong2 *>(P.cb_run + (uint64_t)rk * ng + i0);
+            const uint32_t w0 = (i0 % ng8) * 8 + i0 / ng8, w1 = ((i0 + 1) % ng8) * 8 + (i0 + 1) / ng8;
+            const bool h0 = w0 < P.cb_grid && ((P.cb_hm[w0] >> hd) & 1);
+            const bool h1 = w1 < P.cb_grid && ((P.cb_hm[w1] >> hd) & 1);
+            U.start[i0] = (uint32_t)v.x & 0xffffffu;
+            U.start[i0 + 1] = (uint32_t)v.y & 0xffffffu;
+            U.list[i0] = (uint16_t)w0;
+            U.list[i0 + 1] = (uint16_t)w1;
+            c0 = h0 ? (uint32_t)(v.x >> 24) & 0xffffffu : 0u;
+            c1 = h1 ? (uint32_t)(v.y >> 24) & 0xffffffu : 0u;
+            tb = (h0 ? (uint32_t)(v.x >> 48) : 0u) | (h1 ? (uint32_t)(v.y >> 48) : 0u);
         }
         uint32_t total;
         PV_VMCNT(0); // the region DMA too, before the barriers below
-        const uint32_t pre = block_excl_scan(c, U.wsum, total);
-        if (threadIdx.x < ng) U.pref[threadIdx.x] = pre;
+        const uint32_t pre = block_excl_scan(c0 + c1, U.wsum, total);
+        if (i0 < ng) { U.pref[i0] = pre; U.pref[i0 + 1] = pre + c0; }
         if (threadIdx.x == 0) U.pref[ng] = total;
         if (tb) atomicOr(&U.tabs, tb);
         __syncthreads();
@@ -3785,132 +3814,337 @@ extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) pv_topn_merge(const 
             const uint32_t m = lo + st;
             if (m < ng && U.pref[m] <= (uint32_t)j) lo = m;
         }
-        return cb[(uint64_t)U.list[lo] * P.mq_cap + U.start[lo] + ((uint32_t)j - U.pref[lo])];
+        return cb[(uint64_t)U.list[lo] * lcap + U.start[lo] + ((uint32_t)j - U.pref[lo])];
     };
     if (n <= PV_MERGE_DIRECT) {
         for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
             const ulonglong2 e = ld(j);
-            const uint64_t e0 = e.x, e1 = e.y;
-            const uint32_t s = (uint32_t)(e0 >> 60), w = (uint32_t)e1, rep = (uint32_t)(e1 >> 32);
-            const uint64_t key = e0 & ((1ull << 60) - 1);
-            if (w & PV_W_IP4) {
-                global_add(P, s, key, w & PV_W_CNT, rep);
-                if ((w >> 29) & 1)
-                    cpc_min(P, s, ((w >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
-            } else {
-                global_add_nn(P, s, key, w, rep);
-            }
+            const uint32_t s = (uint32_t)(e.x >> 60), w = (uint32_t)e.y, rep = (uint32_t)(e.y >> 32);
+            const uint64_t key = e.x & ((1ull << 60) - 1);
+            if (P.xmerge) { global_add(P, s, key, e.y, 0); continue; } // (64-bit weight, no name)
+            if ((w & PV_W_IP4) && ((w >> 29) & 1))
+                cpc_min(P, s, ((w >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
+            if (w & PV_W_IP4) global_add(P, s, key, w & PV_W_CNT, rep);
+            else global_add_nn(P, s, key, w, rep);
         }
         return;
     }
     static_assert(PV_TABLES <= 32, "table mask");
-    static_assert(sizeof(MergeState) + sizeof(MergeRuns) <= 160 * 1024, "pv_topn_merge LDS");
+    constexpr uint32_t PF = PV_RS / PV_MG_THREADS; // region entries per thread
+    // IPv4 cardinality minima in the insert pass (batches of at most 2^24 records): a v1 IPv4
+    // entry's LDS key word carries PV_MV4 and direction 1's smallest record index in bits
+    // 32..55 (the key's own bits there are zero; the word's atomicMin lowers that field alone,
+    // the other bits being the entry's constants), its weight word the count in the low half and
+    // direction 0's smallest index in the high half. Longer batches take a second pass.
+    const bool narrow = P.n <= (1ull << 24) && !P.xmerge;
+    const bool xm = P.xmerge != 0; // multi-GPU owner merge: 64-bit weights, no names, no CPC
     uint32_t tabs = U.tabs << (hd * PV_SLOTS); // the tables among this run key's entries
     const bool one = !(tabs & (tabs - 1));
-    bool fresh = true; // S still holds the DMA'd region (no earlier table of this loop reloaded it)
+    bool fresh = true; // S.key still holds the DMA'd region
     while (tabs) {
         const uint32_t tb = __builtin_ctz(tabs);
         const uint32_t s = tb % PV_SLOTS; // the handler slot (Net for tb < PV_SLOTS, else DNS)
         tabs &= tabs - 1;
         const uint64_t rbase = ((uint64_t)tb << P.tcap_log2) + ((uint64_t)r << rsl);
-        auto put = [&](uint64_t i, ulonglong2 kc) {
-            S.key[i] = kc.x;
-            S.cnt[i] = kc.x ? kc.y : 0; // an empty entry's count word is stale
-            S.dirty[i] = !kc.x && kc.y;  // written back as zero
-            S.mn[0][i] = 0xffffffffu;
-            S.mn[1][i] = 0xffffffffu;
-        };
-        if (pf && tb == tbg && fresh) {
-#pragma unroll
-            for (int u = 0; u < PF; u++) {
-                const uint32_t i = threadIdx.x + u * PV_MG_THREADS;
-                put(i, make_ulonglong2(S.key[i], S.cnt[i]));
-            }
-        } else {
-            batched<4>(rs, [&](uint64_t i) { return make_ulonglong2(P.tkeys[rbase + i], P.tcnt[rbase + i]); }, put);
+        if (!(pf && tb == tbg && fresh)) batched<4>(rs, [&](uint64_t i) { return P.tkeys[rbase + i]; }, [&](uint64_t i, uint64_t k) { S.key[i] = k; });
+        // the LDS forms of the loaded keys; weights start at PV_DL0 (direction 0's minimum unset)
+        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+            const uint64_t k = S.key[i];
+            if (narrow && mv4_key(k)) S.key[i] = k | PV_MV4 | PV_MN1;
+            S.dl[i] = PV_DL0;
         }
-        if (threadIdx.x == 0) { S.nnew = 0; S.ncr = 0; }
-        __syncthreads();
+        if (threadIdx.x == 0) { S.nnew = 0; S.ncr = 0; S.ip4c = 0; }
+        lds_barrier();
         TST(1)
         auto ins = [&](ulonglong2 e) __attribute__((always_inline)) {
             const uint64_t e0 = e.x;
             if (!one && entry_table(e0) != tb) return;
-            const uint64_t e1 = e.y;
+            const uint32_t w32 = (uint32_t)e.y, rep = (uint32_t)(e.y >> 32);
+            const uint64_t w = xm ? e.y : (w32 & PV_W_IP4) ? (uint64_t)(w32 & PV_W_CNT) : (uint64_t)w32;
             const uint64_t key = e0 & ((1ull << 60) - 1);
+            const bool v4 = narrow && mv4_key(key);
+            const bool card = !xm && (w32 & PV_W_IP4) && ((w32 >> 29) & 1);
+            if (card && !v4) S.ip4c = 1; // (a long batch: the second pass)
+            const uint64_t pk = v4 ? key | PV_MV4 : key;
             uint32_t pos = (uint32_t)tkey_hash(key) & (rs - 1);
-            bool done = false;
-            for (int probe = 0; probe < PV_PROBES && !done; probe++) {
+            for (int probe = 0; probe < PV_PROBES; probe++) {
                 uint64_t cur = S.key[pos];
                 bool created = false;
                 if (cur == 0) {
-                    const uint64_t prev = atomicCAS((unsigned long long *)&S.key[pos], 0ull, (unsigned long long)key);
+                    const uint64_t nw = pk | (v4 ? PV_MN1 : 0ull) | PV_CREATED;
+                    const uint64_t prev = atomicCAS((unsigned long long *)&S.key[pos], 0ull, (unsigned long long)nw);
                     created = prev == 0;
-                    cur = created ? key : prev;
+                    cur = created ? nw : prev;
                 }
-                if (cur == key) {
-                    const uint32_t w = (uint32_t)e1;
-                    S.dirty[pos] = 1;
-                    if (w & PV_W_IP4) {
-                        atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)(w & PV_W_CNT));
-                        if ((w >> 29) & 1) atomicMin(&S.mn[(w >> 30) & 1][pos], (uint32_t)(e1 >> 32));
+                if (mv4_norm(cur) == pk) {
+                    if (v4) {
+                        atomicAdd(reinterpret_cast<uint32_t *>(&S.dl[pos]), (uint32_t)w);
+                        if (card) {
+                            if ((w32 >> 30) & 1) atomicMin((unsigned long long *)&S.key[pos], (unsigned long long)((cur & ~PV_MN1) | ((uint64_t)rep << 32)));
+                            else atomicMin(reinterpret_cast<uint32_t *>(&S.dl[pos]) + 1, rep);
+                        }
                     } else {
-                        atomicAdd((unsigned long long *)&S.cnt[pos], (unsigned long long)w);
+                        atomicAdd((unsigned long long *)&S.dl[pos], (unsigned long long)w);
                     }
-                    if (created) atomicAdd(&S.ncr, 1u);
-                    if (created && PV_KEY_METRIC(key) != TM_IPV4) {
-                        const uint32_t k = atomicAdd(&S.nnew, 1u);
-                        S.nidx[k] = pos;
-                        S.nrep[k] = (uint32_t)(e1 >> 32);
+                    if (created) {
+                        atomicAdd(&S.ncr, 1u);
+                        if (PV_KEY_METRIC(key) != TM_IPV4 && !xm) {
+                            // (past the list's capacity the names phase scans the region instead)
+                            const uint32_t k = atomicAdd(&S.nnew, 1u);
+                            if (k < PV_MG_NN) { S.nidx[k] = (uint16_t)pos; S.nrep[k] = rep; }
+                            else P.taux[rbase + pos] = rep;
+                        }
                     }
-                    done = true;
-                } else {
-                    pos = (pos + 1) & (rs - 1);
+                    return;
                 }
+                pos = (pos + 1) & (rs - 1);
             }
-            if (!done) {
-                const uint32_t w = (uint32_t)e1, rep = (uint32_t)(e1 >> 32);
-                if (w & PV_W_IP4) {
-                    if ((w >> 29) & 1) cpc_min(P, s, ((w >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
-                    table_overflow(P, s, key, w & PV_W_CNT, rep, true);
-                } else {
-                    table_overflow(P, s, key, w, rep, true);
-                }
-            }
+            if (card && v4) cpc_min(P, s, ((w32 >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
+            table_overflow(P, s, key, w, rep, !xm);
         };
-        batched<PV_MG_U>(n, ld, [&](uint64_t, ulonglong2 e) { ins(e); });
+        batched<PV_MG_U2>(n, ld, [&](uint64_t, ulonglong2 e) { ins(e); });
         __syncthreads();
         TST(2)
-#ifndef PV_ABL_MERGE
-#define PV_ABL_MERGE 0 // tuning/ablation only: 1 no CPC updates, 2 no write-back, 3 neither
-#endif
-        // the new names' list slots first, then the names and the write-back: the region's stores
-        // and CPC atomics come last, so nothing of this workgroup waits for them to complete
+        // the created named entries' slots in the new-name list (pv_topn_names decodes them)
         const uint32_t nnew = S.nnew;
-        if (threadIdx.x == 0 && nnew) S.nbase = atomicAdd(P.nn_cnt, nnew);
-        if (threadIdx.x == 0 && S.ncr) atomicAdd(&P.tab_live[tb], S.ncr);
-        __syncthreads();
-        TST(3)
-        for (uint32_t k = threadIdx.x; k < nnew; k += blockDim.x) {
-            const uint32_t g = S.nbase + k;
-            const uint64_t pos = rbase + S.nidx[k];
-            if (g < P.nn_cap) P.nn[g] = PvNewName{tb, S.nrep[k], pos};
-            else P.taux[pos] = write_name(P, s, PV_KEY_METRIC(S.key[S.nidx[k]]), S.nrep[k], nullptr, S.key[S.nidx[k]]);
-        }
-        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
-            if ((PV_ABL_MERGE & 2) == 0 && S.dirty[i]) {
-                P.tkeys[rbase + i] = S.key[i];
-                P.tcnt[rbase + i] = S.cnt[i];
+        auto new_name = [&](uint32_t g, uint32_t i, uint32_t rep) {
+            if (g < P.nn_cap) P.nn[g] = PvNewName{tb, rep, rbase + i};
+            else {
+                const uint64_t key = S.key[i] & ~PV_CREATED;
+                P.taux[rbase + i] = write_name(P, s, PV_KEY_METRIC(key), rep, nullptr, key);
             }
-            // IPv4 cardinality: one first-occurrence update per address and direction
-            for (uint32_t d = 0; d < 2; d++)
-                if ((PV_ABL_MERGE & 1) == 0 && S.mn[d][i] != 0xffffffffu)
-                    cpc_min(P, s, d ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)S.key[i]), (int64_t)(P.gbase + S.mn[d][i]));
+        };
+        if (nnew && nnew <= PV_MG_NN) {
+            if (threadIdx.x == 0) S.nbase = atomicAdd(P.nn_cnt, nnew);
+            lds_barrier();
+            for (uint32_t k = threadIdx.x; k < nnew; k += blockDim.x) new_name(S.nbase + k, S.nidx[k], S.nrep[k]);
+        } else if (nnew) {
+            // more than the list holds: every thread lists its share of the region's created entries
+            uint32_t mine = 0;
+            for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+                const uint64_t k = S.key[i];
+                mine += (k & PV_CREATED) && PV_KEY_METRIC(k & ~PV_CREATED) != TM_IPV4;
+            }
+            uint32_t tot;
+            uint32_t g = block_excl_scan(mine, U.wsum, tot);
+            if (threadIdx.x == 0) S.nbase = atomicAdd(P.nn_cnt, tot);
+            // the listed entries' source records to their aux words too (visible to the
+            // workgroup after the barrier; read past L1)
+            for (uint32_t k = threadIdx.x; k < PV_MG_NN; k += blockDim.x) P.taux[rbase + S.nidx[k]] = S.nrep[k];
+            __syncthreads();
+            g += S.nbase;
+            for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+                const uint64_t k = S.key[i];
+                if ((k & PV_CREATED) && PV_KEY_METRIC(k & ~PV_CREATED) != TM_IPV4)
+                    new_name(g++, i, __hip_atomic_load(&P.taux[rbase + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+        }
+        TST(3)
+        // write-back of the entries this batch changed: a created entry's key and weight; an
+        // existing one's count word read (all of a thread's reads in flight together) and stored
+        // with the weight added. Then the IPv4 cardinality minima of the changed v1 entries.
+        constexpr uint32_t WB = PF < 4 ? PF : 4;
+        for (uint32_t q0 = 0; q0 < PF; q0 += WB) {
+            uint64_t kk[WB], dd[WB], cc[WB];
+#pragma unroll
+            for (uint32_t q = 0; q < WB; q++) {
+                const uint32_t i = threadIdx.x + (q0 + q) * PV_MG_THREADS;
+                kk[q] = i < rs ? S.key[i] : 0;
+                const uint64_t d = i < rs ? S.dl[i] : PV_DL0;
+                dd[q] = (kk[q] & PV_MV4) ? (d & 0xffffffffull) : d - PV_DL0;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < WB; q++) {
+                const uint32_t i = threadIdx.x + (q0 + q) * PV_MG_THREADS;
+                cc[q] = (dd[q] && !(kk[q] & PV_CREATED)) ? P.tcnt[rbase + i] : 0;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < WB; q++) {
+                const uint32_t i = threadIdx.x + (q0 + q) * PV_MG_THREADS;
+                if (kk[q] & PV_CREATED) {
+                    P.tkeys[rbase + i] = mv4_norm(kk[q]) & ~PV_MV4;
+                    if (xm && PV_KEY_METRIC(kk[q] & ~PV_CREATED) != TM_IPV4) P.taux[rbase + i] = 0; // name unknown here
+                }
+                if (dd[q]) P.tcnt[rbase + i] = cc[q] + dd[q];
+                if ((kk[q] & PV_MV4) && dd[q]) {
+                    const uint32_t m0 = (uint32_t)(S.dl[i] >> 32), m1 = (uint32_t)(kk[q] >> 32) & 0xffffffu;
+                    if (m0 != 0xffffffffu || m1 != 0xffffffu) {
+                        const uint32_t cp = ip4_coupon((uint32_t)kk[q]);
+                        if (m0 != 0xffffffffu) cpc_min(P, s, CPC_SRC, cp, (int64_t)(P.gbase + m0));
+                        if (m1 != 0xffffffu) cpc_min(P, s, CPC_DST, cp, (int64_t)(P.gbase + m1));
+                    }
+                }
+            }
+        }
+        if (threadIdx.x == 0 && S.ncr) atomicAdd(&P.tab_live[tb], S.ncr);
+        // batches longer than 2^24 records: the minima by a second pass over the run's entries,
+        // in dl (now free: the low word direction 0, the high word direction 1)
+        if (S.ip4c) {
+            lds_barrier(); // the write-back's reads of dl
+            for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) S.dl[i] = ~0ull;
+            lds_barrier();
+            batched<PV_MG_U2>(n, ld, [&](uint64_t, ulonglong2 e) {
+                const uint32_t w32 = (uint32_t)e.y, rep = (uint32_t)(e.y >> 32), d = (w32 >> 30) & 1;
+                if (!(w32 & PV_W_IP4) || !((w32 >> 29) & 1) || (!one && entry_table(e.x) != tb)) return;
+                const uint64_t key = e.x & ((1ull << 60) - 1);
+                uint32_t pos = (uint32_t)tkey_hash(key) & (rs - 1);
+                for (int probe = 0; probe < PV_PROBES; probe++) {
+                    const uint64_t cur = S.key[pos] & ~PV_CREATED;
+                    if (cur == key) {
+                        atomicMin(reinterpret_cast<uint32_t *>(&S.dl[pos]) + d, rep);
+                        return;
+                    }
+                    if (cur == 0) break;
+                    pos = (pos + 1) & (rs - 1);
+                }
+                // (an update the full region could not take, gone to the overflow list)
+                cpc_min(P, s, d ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
+            });
+            lds_barrier();
+            for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) {
+                const uint64_t m = S.dl[i];
+                if (m == ~0ull) continue;
+                const uint32_t cp = ip4_coupon((uint32_t)S.key[i]);
+                if ((uint32_t)m != 0xffffffffu) cpc_min(P, s, CPC_SRC, cp, (int64_t)(P.gbase + (uint32_t)m));
+                if ((uint32_t)(m >> 32) != 0xffffffffu) cpc_min(P, s, CPC_DST, cp, (int64_t)(P.gbase + (uint32_t)(m >> 32)));
+            }
         }
         if (tabs) lds_barrier(); // another table's region reuses S
         TST(4)
         fresh = false;
     }
     TST_FLUSH(65536)
+}
+
+// ------------------------------------------------------------------ multi-GPU top-N exchange
+// The regions of every table are partitioned over the ranks in contiguous blocks (the owner of
+// region r: r * W / nreg). A rank sends the live entries of the regions it does not own to
+// their owners, ordered (owner, handler, region, slot), with the counts of each (handler,
+// region, slot) as a header; each owner merges what it receives into its own regions with
+// pv_topn_merge (xmerge: 64-bit weights, no names), the analog of the frequent-items merge of
+// AbstractMetricsBucket::merge (src/AbstractMetricsManager.h:177-195, src/Metrics.h:534-538)
+// over shards of one stream.
+__device__ __forceinline__ uint32_t x_owner(uint32_t r, uint32_t reg_log2, uint32_t W) { return (uint32_t)(((uint64_t)r * W) >> reg_log2); }
+__device__ __forceinline__ uint32_t x_lo(uint32_t d, uint32_t reg_log2, uint32_t W) { return (uint32_t)((((uint64_t)d << reg_log2) + W - 1) / W); }
+#define PV_XC(hd, r, slot, reg_log2) ((((uint32_t)(hd) << (reg_log2)) + (r)) * PV_SLOTS + (slot))
+
+// live entries per (table, region) of the regions other ranks own
+extern "C" __global__ void __launch_bounds__(256) pv_topn_xcount(const PvParams *__restrict__ Pp, PvXTabs T, uint32_t *__restrict__ cnt)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t wsum[16];
+    const uint32_t r = blockIdx.x & ((1u << P.reg_log2) - 1), tb = T.tb[blockIdx.x >> P.reg_log2];
+    const uint32_t rs = 1u << (P.tcap_log2 - P.reg_log2);
+    uint32_t c = 0;
+    if (x_owner(r, P.reg_log2, T.W) != T.me) {
+        const PV_G uint64_t *k = P.tkeys + ((uint64_t)tb << P.tcap_log2) + ((uint64_t)r << (P.tcap_log2 - P.reg_log2));
+        for (uint32_t i = threadIdx.x; i < rs; i += blockDim.x) c += k[i] != 0;
+    }
+    uint32_t tot;
+    block_excl_scan(c, wsum, tot);
+    if (threadIdx.x == 0) cnt[PV_XC(tb / PV_SLOTS, r, tb % PV_SLOTS, P.reg_log2)] = tot;
+}
+
+// One workgroup: the counts in (owner, handler, region, slot) order: each cell's offset in the
+// send list and the header stream (the counts in that order; an owner's slice is its header)
+extern "C" __global__ void __launch_bounds__(1024) pv_topn_xscan(uint32_t reg_log2, uint32_t W, const uint32_t *__restrict__ cnt,
+                                                                 uint32_t *__restrict__ off, uint32_t *__restrict__ hdr)
+{
+    __shared__ uint32_t wsum[16];
+    const uint32_t E = (2u << reg_log2) * PV_SLOTS, per = (E + blockDim.x - 1) / blockDim.x;
+    const uint32_t p0 = min(threadIdx.x * per, E), p1 = min(p0 + per, E);
+    auto cell = [&](uint32_t p) {
+        const uint32_t d = x_owner(p / (2 * PV_SLOTS), reg_log2, W);
+        const uint32_t lo = x_lo(d, reg_log2, W), len = x_lo(d + 1, reg_log2, W) - lo;
+        const uint32_t rem = p - 2 * PV_SLOTS * lo, hd = rem / (PV_SLOTS * len);
+        return PV_XC(hd, lo + (rem % (PV_SLOTS * len)) / PV_SLOTS, rem % PV_SLOTS, reg_log2);
+    };
+    uint32_t s = 0;
+    for (uint32_t p = p0; p < p1; p++) s += cnt[cell(p)];
+    uint32_t tot;
+    uint32_t at = block_excl_scan(s, wsum, tot);
+    for (uint32_t p = p0; p < p1; p++) {
+        const uint32_t i = cell(p), c = cnt[i];
+        off[i] = at;
+        hdr[p] = c;
+        at += c;
+    }
+}
+
+// the live entries of the regions other ranks own into the send list: {key | slot << 60, count}
+extern "C" __global__ void __launch_bounds__(256) pv_topn_xwrite(const PvParams *__restrict__ Pp, PvXTabs T, const uint32_t *__restrict__ off,
+                                                                 ulonglong2 *__restrict__ out)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ uint32_t wsum[16];
+    const uint32_t r = blockIdx.x & ((1u << P.reg_log2) - 1), tb = T.tb[blockIdx.x >> P.reg_log2];
+    if (x_owner(r, P.reg_log2, T.W) == T.me) return;
+    const uint32_t rsl = P.tcap_log2 - P.reg_log2, rs = 1u << rsl;
+    const uint64_t rb = ((uint64_t)tb << P.tcap_log2) + ((uint64_t)r << rsl);
+    const uint32_t per = rs / blockDim.x; // contiguous positions per thread
+    const uint32_t i0 = threadIdx.x * per;
+    uint32_t c = 0;
+    for (uint32_t i = i0; i < i0 + per; i++) c += P.tkeys[rb + i] != 0;
+    uint32_t tot;
+    uint32_t at = off[PV_XC(tb / PV_SLOTS, r, tb % PV_SLOTS, P.reg_log2)] + block_excl_scan(c, wsum, tot);
+    for (uint32_t i = i0; i < i0 + per; i++) {
+        const uint64_t k = P.tkeys[rb + i];
+        if (k) out[at++] = make_ulonglong2(k | ((uint64_t)(tb % PV_SLOTS) << 60), P.tcnt[rb + i]);
+    }
+}
+
+// The run table of the received lists for pv_topn_merge: workgroup q scans source q's header
+// (this rank's regions, (handler, region, slot) order) into one run word per (handler, region):
+// start in q's list, count, the slots present. Source me sends nothing: zero words.
+extern "C" __global__ void __launch_bounds__(1024) pv_topn_xruns(uint32_t reg_log2, uint32_t W, uint32_t me, const uint32_t *__restrict__ hdr,
+                                                                 uint32_t hdr_stride, uint64_t *__restrict__ cb_run)
+{
+    __shared__ uint32_t wsum[16];
+    const uint32_t q = blockIdx.x, lo = x_lo(me, reg_log2, W), len = x_lo(me + 1, reg_log2, W) - lo;
+    const uint32_t ng8 = (W + 7) / 8, ng = 8 * ng8, col = (q % 8) * ng8 + q / 8;
+    const uint32_t E = 2 * len; // (handler, region) runs
+    const uint32_t per = (E + blockDim.x - 1) / blockDim.x, e0 = min(threadIdx.x * per, E), e1 = min(e0 + per, E);
+    const uint32_t *h = hdr + (uint64_t)q * hdr_stride;
+    uint32_t s = 0;
+    if (q != me)
+        for (uint32_t e = e0; e < e1; e++)
+            for (uint32_t k = 0; k < PV_SLOTS; k++) s += h[e * PV_SLOTS + k];
+    uint32_t tot;
+    uint32_t at = block_excl_scan(s, wsum, tot);
+    for (uint32_t e = e0; e < e1; e++) {
+        uint32_t c = 0, tabs = 0;
+        if (q != me)
+            for (uint32_t k = 0; k < PV_SLOTS; k++) {
+                const uint32_t v = h[e * PV_SLOTS + k];
+                c += v;
+                if (v) tabs |= 1u << k;
+            }
+        const uint32_t hd = e / len, rk = (hd << reg_log2) | (lo + e % len);
+        cb_run[(uint64_t)rk * ng + col] = pv_run_word(at, c, tabs);
+        at += c;
+    }
+}
+
+// Finalize support: the aux word (name record) of each listed (table, key) in this rank's
+// tables, 0 when absent or unnamed
+extern "C" __global__ void pv_topn_xlookup(const PvParams *__restrict__ Pp, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ tbs,
+                                           uint32_t n, uint32_t *__restrict__ aux)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t key = keys[j];
+    const uint32_t tb = tbs[j], rsl = P.tcap_log2 - P.reg_log2;
+    const uint64_t h = tkey_hash(key);
+    const uint64_t rb = ((uint64_t)tb << P.tcap_log2) + ((uint64_t)tregion(P, h) << rsl);
+    uint32_t pos = (uint32_t)h & ((1u << rsl) - 1), a = 0;
+    for (int probe = 0; probe < PV_PROBES; probe++) {
+        const uint64_t k = P.tkeys[rb + pos];
+        if (k == key) { a = P.taux[rb + pos]; break; }
+        if (k == 0) break;
+        pos = (pos + 1) & ((1u << rsl) - 1);
+    }
+    aux[j] = a;
 }
 
 // The updates full regions could not take in this batch, once the host has purged their tables:
@@ -5096,12 +5330,13 @@ __device__ __forceinline__ int xv_sel_kind(uint32_t kind)
     return kind == XV_FROM_US ? 0 : kind == XV_TO_US ? 1 : (kind >= XV2_TIME && kind < XV2_TIME + 3) ? 2 + (int)(kind - XV2_TIME) : -1;
 }
 extern "C" __global__ void __launch_bounds__(256) pv_xv_hist(const PvXValue *__restrict__ v, const uint32_t *__restrict__ n_vals,
-                                                          uint32_t sg, uint32_t shift, PvXvSel sel, uint32_t *__restrict__ hist)
+                                                          uint32_t cap, uint32_t sg, uint32_t shift, PvXvSel sel,
+                                                          uint32_t *__restrict__ hist)
 {
     __shared__ uint32_t h[PV_XV_SEL * 256];
     for (uint32_t i = threadIdx.x; i < PV_XV_SEL * 256; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    const uint32_t n = *n_vals;
+    const uint32_t n = min(*n_vals, cap); // the buffer's values (a full buffer counts past its end)
     const uint64_t hm = shift >= 56 ? 0ull : ~0ull << (shift + 8);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const PvXValue x = v[i];
@@ -5146,4 +5381,158 @@ extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *of
     for (uint32_t b = lane; b < bytes; b += 64) o[b] = r[b];
     if (lane == 0) *reinterpret_cast<uint32_t *>(o + 8) = cap; // a clamped capture length stays consistent
     for (uint32_t b = bytes + lane; b < ((bytes + 3u) & ~3u); b += 64) o[b] = 0;
+}
+
+// ------------------------------------------------------------------ pcap BPF filter on the device
+// The pcap input's filter (PcapInputStream::_open_pcap: reader->setFilter(bpf),
+// src/inputs/pcap/PcapInputStream.cpp:485-488; libpcap runs the compiled classic-BPF program on
+// every record, bpf_filter with the capture length as the buffer and the wire length for
+// BPF_LEN) over a batch already in HBM: one lane per record runs the machine (pv_bpf.cpp's
+// restatement; the program in LDS), the kept records are compacted into a new blob (sizes and
+// record ranks by exclusive scans, one wave per 64 records copying each record with its 64 lanes)
+// and the kept run's ts_sec change points found, so pv_process_device then takes the kept
+// records as its batch.
+struct PvBpfIns {
+    uint16_t code;
+    uint8_t jt, jf;
+    uint32_t k;
+};
+#define PV_BPF_LDS 1024 // program instructions held in LDS (longer programs read the rest from HBM)
+__device__ __forceinline__ bool bpf_ld(const uint8_t *p, uint32_t buflen, uint64_t k, uint32_t n, uint32_t &v)
+{
+    if (k + n > buflen) return false;
+    v = 0;
+    for (uint32_t i = 0; i < n; i++) v = (v << 8) | p[k + i];
+    return true;
+}
+__device__ uint32_t bpf_run_dev(const PvBpfIns *lds, const PvBpfIns *prog, const uint8_t *p, uint32_t wirelen,
+                                uint32_t buflen)
+{
+    uint32_t a = 0, x = 0, mem[16];
+    for (int i = 0; i < 16; i++) mem[i] = 0;
+    for (uint32_t pc = 0;; pc++) {
+        const PvBpfIns f = pc < PV_BPF_LDS ? lds[pc] : prog[pc];
+        const uint16_t c = f.code;
+        uint32_t v;
+        switch (c & 7) {
+        case 0: { // LD
+            const uint16_t mode = c & 0xe0;
+            const uint32_t n = (c & 0x18) == 0 ? 4 : (c & 0x18) == 8 ? 2 : 1;
+            if (mode == 0x00) a = f.k;
+            else if (mode == 0x80) a = wirelen;
+            else if (mode == 0x60) a = mem[f.k & 15];
+            else {
+                if (!bpf_ld(p, buflen, (mode == 0x40 ? (uint64_t)x : 0) + f.k, n, v)) return 0;
+                a = v;
+            }
+            break;
+        }
+        case 1: { // LDX
+            const uint16_t mode = c & 0xe0;
+            if (mode == 0x00) x = f.k;
+            else if (mode == 0x80) x = wirelen;
+            else if (mode == 0x60) x = mem[f.k & 15];
+            else {
+                if (!bpf_ld(p, buflen, f.k, 1, v)) return 0;
+                x = (v & 0xf) << 2;
+            }
+            break;
+        }
+        case 2: mem[f.k & 15] = a; break;
+        case 3: mem[f.k & 15] = x; break;
+        case 4: { // ALU
+            const uint32_t s = (c & 8) ? x : f.k;
+            switch (c & 0xf0) {
+            case 0x00: a += s; break;
+            case 0x10: a -= s; break;
+            case 0x20: a *= s; break;
+            case 0x30: if (!s) return 0; a /= s; break;
+            case 0x90: if (!s) return 0; a %= s; break;
+            case 0x40: a |= s; break;
+            case 0x50: a &= s; break;
+            case 0xa0: a ^= s; break;
+            case 0x60: a <<= (s & 31); break;
+            case 0x70: a >>= (s & 31); break;
+            case 0x80: a = 0u - a; break;
+            }
+            break;
+        }
+        case 5: { // JMP
+            const uint16_t op = c & 0xf0;
+            if (op == 0x00) { pc += f.k; break; }
+            const uint32_t s = (c & 8) ? x : f.k;
+            const bool t = op == 0x10 ? a == s : op == 0x20 ? a > s : op == 0x30 ? a >= s : (a & s) != 0;
+            pc += t ? f.jt : f.jf;
+            break;
+        }
+        case 6: return (c & 0x18) == 0x10 ? a : f.k; // RET
+        default: if ((c & 0xf8) == 0x80) a = x; else x = a; break; // MISC: TXA / TAX
+        }
+    }
+}
+__device__ __forceinline__ uint32_t rec_u32(const uint8_t *r, uint64_t p)
+{
+    return (uint32_t)r[p] | ((uint32_t)r[p + 1] << 8) | ((uint32_t)r[p + 2] << 16) | ((uint32_t)r[p + 3] << 24);
+}
+// sz[i]: 16 + caplen of a kept record, else 0; kf[i]: 1 if kept
+extern "C" __global__ void __launch_bounds__(256) pv_bpf_keep(const uint8_t *__restrict__ recs, const uint32_t *__restrict__ offs, uint32_t n,
+                                                              const PvBpfIns *__restrict__ prog, uint32_t ninsn, uint32_t *__restrict__ sz,
+                                                              uint32_t *__restrict__ kf)
+{
+    __shared__ PvBpfIns lp[PV_BPF_LDS];
+    for (uint32_t j = threadIdx.x; j < min(ninsn, (uint32_t)PV_BPF_LDS); j += blockDim.x) lp[j] = prog[j];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o = offs[i];
+    const uint32_t cap = rec_u32(recs, o + 8), len = rec_u32(recs, o + 12);
+    const bool keep = bpf_run_dev(lp, prog, recs + o + 16, len, cap) != 0;
+    sz[i] = keep ? 16 + cap : 0;
+    kf[i] = keep ? 1u : 0u;
+}
+// kept record i to out at boff[i], its offset to ooffs[rank[i]]: one wave per 64 records
+extern "C" __global__ void __launch_bounds__(256) pv_bpf_gather(const uint8_t *__restrict__ recs, const uint32_t *__restrict__ offs, uint32_t n,
+                                                                const uint32_t *__restrict__ sz, const uint32_t *__restrict__ boff,
+                                                                const uint32_t *__restrict__ rank, uint8_t *__restrict__ out,
+                                                                uint32_t *__restrict__ ooffs)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
+    const uint32_t mi = w0 + lane;
+    const uint32_t my_sz = mi < n ? sz[mi] : 0u, my_off = mi < n ? offs[mi] : 0u, my_b = mi < n ? boff[mi] : 0u;
+    if (my_sz) ooffs[rank[mi]] = my_b;
+    for (uint32_t r = 0; r < 64 && w0 + r < n; r++) {
+        const uint32_t s = __shfl(my_sz, r, 64);
+        if (!s) continue;
+        const uint32_t so = __shfl(my_off, r, 64), d = __shfl(my_b, r, 64);
+        for (uint32_t b = lane; b < s; b += 64) out[(uint64_t)d + b] = recs[(uint64_t)so + b];
+    }
+}
+// ts_sec change points of the kept run: flag[j] = 1 where record j's second differs from j - 1's
+// (record 0 always); sec[j] its second; down[0] counts decreases (non-monotone)
+extern "C" __global__ void __launch_bounds__(256) pv_bpf_secs(const uint8_t *__restrict__ out, const uint32_t *__restrict__ ooffs, uint32_t nk,
+                                                              uint32_t *__restrict__ flag, uint32_t *__restrict__ sec, uint32_t *__restrict__ down)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nk) return;
+    const uint32_t s = rec_u32(out, ooffs[j]);
+    const uint32_t p = j ? rec_u32(out, ooffs[j - 1]) : 0u;
+    flag[j] = (j == 0 || s != p) ? 1u : 0u;
+    sec[j] = s;
+    if (j && s < p) atomicAdd(down, 1u);
+}
+// the change points, compacted by the flags' exclusive scan
+extern "C" __global__ void __launch_bounds__(256) pv_bpf_secs_compact(const uint32_t *__restrict__ flag, const uint32_t *__restrict__ pos,
+                                                                      const uint32_t *__restrict__ sec, uint32_t nk, uint32_t cap,
+                                                                      uint32_t *__restrict__ sci, uint32_t *__restrict__ scs)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nk || !flag[j] || pos[j] >= cap) return;
+    sci[pos[j]] = j;
+    scs[pos[j]] = sec[j];
+}
+// Exclusive prefix sum of n u32 (rocPRIM), tmp sized by a first call with tmp == nullptr.
+extern "C" hipError_t pv_exclusive_scan_u32(void *tmp, size_t *tmp_bytes, const uint32_t *in, uint32_t *out, size_t n, hipStream_t s)
+{
+    return rocprim::exclusive_scan(tmp, *tmp_bytes, in, out, 0u, n, rocprim::plus<uint32_t>(), s);
 }

@@ -334,6 +334,12 @@ static_assert(sizeof(PvDtEv) == 80, "PvDtEv is five 16-B words");
 
 // an update a full top-N region could not take inside a batch: kept for the retry after the
 // table's purge (pv_topn_retry), so a burst of distinct keys degrades like the sketch's purge
+// multi-GPU top-N exchange: the live tables and this rank's place (pv_topn_x*)
+struct PvXTabs {
+    uint32_t n, W, me, pad;
+    uint32_t tb[PV_TABLES];
+};
+
 struct PvOvf {
     uint64_t key;
     uint32_t w, rep, slot, pad;
@@ -423,6 +429,11 @@ struct PvParams {
     PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
     PV_G uint64_t *cb;    // combined update lists sorted by table region, mq_cap entries per workgroup
     PV_G uint32_t *cb_cnt;
+    PV_G uint32_t *cb_hm; // per combine workgroup: handlers with entries (bit 0 Net, 1 DNS); run words of the others unwritten
+    uint32_t cb_fan;      // grid ranges per combine workgroup (its list: cb_fan x mq_cap entries)
+    uint32_t cb_grid;     // combine workgroups: ceil(grid_main / cb_fan)
+    uint32_t xmerge;      // pv_topn_merge over received multi-GPU entries (64-bit weights, no names)
+    uint32_t x_lo, x_hi;  // its regions [x_lo, x_hi)
     uint32_t dbg; // profiling knob (PV_DEBUG_STAGES env): 1 stop after staging, 2 after parse, 4 no DNS lane,
                   // 16 no DNS name decode, 32 no DNS table updates
     PV_G uint32_t *flags;

@@ -204,37 +204,88 @@ def merge_edges(handlers, group=None, comm=None):
 
 
 def merge_slow(handlers, group=None, comm=None):
-    """top_slow over the whole stream: every rank's transaction times per DNS period ordinal,
-    then each rank's deferred candidates (after the edge merge, before the value merge)"""
+    """top_slow over the whole stream: each DNS period's p90 over every rank's transaction times
+    by distributed selection (no values shipped), then each rank's deferred candidates (after the
+    edge merge, before the top-N exchange)"""
     if getattr(handlers, "slow_defer", False):
-        handlers.slow_finish(_allgather(handlers, handlers.slow_values_export(), group, comm))
+        if comm == "pv":
+            handlers.comm_slow_finish()
+        else:
+            handlers.slow_x_finish(_torch_allreduce(group))
+
+
+def _torch_allreduce(group=None):
+    """an all-reduce of a host uint64 array through torch.distributed (int64: two's-complement
+    sums are identical; the values summed and maxed here are below 2^63)"""
+    def ar(a, op):
+        t = torch.from_numpy(a.view(np.int64))
+        if dist.get_backend(group) != "gloo":
+            d = t.cuda()
+            dist.all_reduce(d, op=dist.ReduceOp.MAX if op else dist.ReduceOp.SUM, group=group)
+            t.copy_(d.cpu())
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op else dist.ReduceOp.SUM, group=group)
+    return ar
 
 
 def merge_values(handlers, group=None, comm=None):
-    me = _rank(handlers, group, comm)
-    for r, data in enumerate(_allgather(handlers, handlers.values_export(), group, comm)):
-        if r != me and data:
-            handlers.values_merge(data)
+    """quantile inputs across shards: exact distributed selection (pv_values_x_select), eight
+    rounds of group histograms summed over the ranks instead of every rank's values"""
+    if (handlers.comm_ranks if comm == "pv" else dist.get_world_size(group)) == 1:
+        return
+    if comm == "pv":
+        handlers.comm_values_select()
+    else:
+        handlers.values_x_select(_torch_allreduce(group))
 
 
-def merge_window(handlers, device, group=None, comm=None):
+def merge_window(handlers, device, group=None, comm=None, finalize=True):
     """Full merge of every rank's shard into every rank's handlers (read path). comm="pv"
-    runs every collective on the library's own RCCL communicator (pv_comm_init first)."""
+    runs every collective on the library's own RCCL communicator (pv_comm_init first).
+    The state merge (edges, slow tops, bucket all-reduce, top-N to the region owners) is the
+    device part; finalize=True then assembles the read view (the top-N lists with names, the
+    quantiles by distributed selection), which finalize_window also does on its own."""
     handlers.synchronize()
     check_aligned(handlers, group, comm)
     merge_edges(handlers, group, comm)
     merge_slow(handlers, group, comm)
-    merge_values(handlers, group, comm)
     if comm == "pv":
         handlers.comm_allreduce_window()
     else:
         reduce_handlers(handlers, device, group)
     merge_topn(handlers, group, comm)
+    if finalize:
+        finalize_window(handlers, group, comm)
+
+
+def finalize_window(handlers, group=None, comm=None):
+    """the merged read view: top-N lists (every owner's leading entries, names from any rank) and
+    the quantile inputs (exact distributed selection)"""
+    finalize_topn(handlers, group, comm)
+    merge_values(handlers, group, comm)
 
 
 def merge_topn(handlers, group=None, comm=None):
-    """Exchange exact per-rank top-N counts (host records) and add the other ranks' into this view."""
+    """Top-N across shards on the device: every table's regions are split over the ranks, each
+    rank ships the live entries of the regions others own to their owners (RCCL point-to-point
+    with comm="pv", else host blobs over torch.distributed), and the owners merge them into their
+    regions (pv_topn_merge). Names stay where they are until finalize_topn."""
+    world = handlers.comm_ranks if comm == "pv" else dist.get_world_size(group)
+    if world == 1:
+        return
     me = _rank(handlers, group, comm)
-    for r, data in enumerate(_allgather(handlers, handlers.export_topn(), group, comm)):
-        if r != me and data:
-            handlers.merge_topn(data)
+    if comm == "pv":
+        handlers.comm_merge_topn()
+    else:
+        handlers.topn_x_import(world, me, _allgather(handlers, handlers.topn_x_export(world, me), group, comm))
+
+
+def finalize_topn(handlers, group=None, comm=None):
+    """the merged top-N lists: every owner's leading entries per metric (topn_count and the ties
+    of the last), the names of those that lack one from the rank that holds it"""
+    world = handlers.comm_ranks if comm == "pv" else dist.get_world_size(group)
+    if world == 1:
+        return
+    cands = _allgather(handlers, handlers.topn_x_candidates(), group, comm)
+    names = _allgather(handlers, handlers.topn_x_names(cands), group, comm)
+    handlers.topn_x_view(cands, names)

@@ -50,3 +50,30 @@ def test_bpf_context_filter(oracle):
         h.close()
     ref = oracle.run_bytes(pcap[:24] + kept, host_spec=synth.HOST_SPEC, num_periods=1, window=1)
     assert diff(got, ref) is None, diff(got, ref)
+
+
+@pytest.mark.parametrize("prog", ["udp53", "short", "arith"])
+def test_bpf_device_resident(oracle, prog):
+    """pv_process_device with a program set: the filter runs on the batch in HBM (pv_bpf_keep /
+    pv_bpf_gather), so device-resident input is filtered as the pcap input filters its reader"""
+    import numpy as np
+    import torch
+    pcap = synth.pcap_bytes(4, 30000)
+    recs = pcap[24:]
+    insns = bpf_progs.PROGRAMS[prog]
+    idx = pa.RecordIndex(recs)
+    d_recs = torch.from_numpy(np.frombuffer(recs + bytes(256), dtype=np.uint8).copy()).cuda()
+    d_offs = torch.from_numpy(np.ascontiguousarray(idx.offsets[: idx.n])).cuda()
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=1, max_records=idx.n, bpf=insns)
+    try:
+        h.process_device(d_recs.data_ptr(), d_offs.data_ptr(), idx)
+        h.synchronize()
+        kept = bpf_progs.filter_records(recs, insns)
+        assert 0 < len(kept) < len(recs)
+        kidx = pa.RecordIndex(kept)
+        h.set_end_tstamp(*pa.last_record_ts(kept, kidx))
+        got = {"1m": h.window_json(0)}
+    finally:
+        h.close()
+    ref = oracle.run_bytes(pcap[:24] + kept, host_spec=synth.HOST_SPEC, num_periods=1, window=1)
+    assert diff(got, ref) is None, diff(got, ref)

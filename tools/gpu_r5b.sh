@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 5: merge v2 / combine check: top-N parity tests, C2-C4 bench lines, phase stamps, C2 kernel stats.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/${R5_DIR:-r5b}; mkdir -p $O
+export TMPDIR=/tmp
+step() { echo "[$(date +%T)] $*"; }
+step tests
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_kat.py tests/test_gpu_topn_bound.py tests/test_gpu_fullsize.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for c in 2 3 4; do
+  step bench c$c
+  timeout -k 10 300 python3 -u bench.py --config $c --no-cpu-baseline --no-e2e > $O/bench_c$c.log 2>&1 || { tail -20 $O/bench_c$c.log; exit 1; }
+  tail -1 $O/bench_c$c.log | cut -c1-200
+done
+for c in 2 3 4; do
+  PVGPU_LIB=$PWD/pktvisor_amd/variants/libpvgpu_tst.so PV_TSTAMPS=1 timeout -k 10 300 python3 -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $O/tst_c$c.log 2>&1 || { tail -20 $O/tst_c$c.log; exit 1; }
+  grep "pv_tstamps combine" $O/tst_c$c.log | tail -1
+done
+step prof c2
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_c2 -o k -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-e2e --steps 10 --config 2 > $GRAFT_REPO_ROOT/$O/prof_c2.log 2>&1) || { tail -20 $O/prof_c2.log; exit 1; }
+python3 tools/kstats.py $O/prof_c2 2>/dev/null | cut -c1-200
+step done
