@@ -162,8 +162,19 @@ int pv_set_dns_filters(pv_ctx *ctx, const pv_dns_filters *f);
  * the capacity of the LRU list of TCP connections (254-283,449-465); a connection start or a
  * message delivery beyond it evicts the least recently used connection, which is closed
  * (closeConnection). 0 (the default): the reference's DEFAULT_LRULIST_SIZE behaviour without
- * the capacity check. Call before the first batch. */
+ * the capacity check. A limit implies the exact LRU mode below. Call before the first batch. */
 int pv_set_tcp_reassembly_limit(pv_ctx *ctx, uint64_t limit);
+/* The exact LRU mode of DNS over TCP (on != 0): PcapInputStream's LRU list of every TCP
+ * connection (PcapInputStream.cpp:254-283,429-465) is replayed on the host per batch from a dry
+ * run of the device TCP stage: puts with the connection's endTime (0 until its second packet, so
+ * a connection first seen with data, e.g. a capture that misses the handshake, leaves as soon as
+ * it reaches the list's tail), after every TCP packet at most MAX_TCP_CLEANUPS (100) 30 s
+ * time-outs, then the evictions; the device closes what the replay closes. Off (the default):
+ * the device times each DNS-port connection out by itself 30 s after its last put's second,
+ * which is the same outcome except for those zero-endTime connections and more than 100
+ * time-outs at one packet. The exact mode costs a second run of the TCP stage and a host walk
+ * over every TCP packet of a batch. Call before the first batch. */
+int pv_set_tcp_exact_lru(pv_ctx *ctx, int on);
 /* A classic-BPF instruction (struct sock_filter, linux/filter.h): what libpcap's pcap_compile
  * produces and `tcpdump -dd EXPR` prints. */
 typedef struct pv_bpf_insn {
@@ -177,7 +188,8 @@ typedef struct pv_bpf_insn {
  * Applies to pv_process_host input from the next call; the program comes compiled (libpcap is
  * not linked). n = 0 removes the filter. PV_EINVAL for a program the classic-BPF checker
  * refuses (unknown opcode, jump out of range, scratch index >= 16, division by a constant 0,
- * no final return). Device-resident input (pv_process_device) is the caller's: not filtered. */
+ * no final return). pv_process_host and pv_process_device input are both filtered on the device
+ * (pv_bpf_keep: one lane per record runs the program; the kept records are compacted in HBM). */
 int pv_set_bpf(pv_ctx *ctx, const pv_bpf_insn *prog, uint32_t n);
 /* Pure host functions of the same machine: validate a program (PV_OK / PV_EINVAL); run it on one
  * frame (wirelen = the record's orig_len, buflen = its incl_len; 0 = drop); copy the records of

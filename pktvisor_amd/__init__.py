@@ -170,7 +170,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
            "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_shard_cuts", "pv_net_kernel_name",
-           "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_dnstap_only_hosts",
+           "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_tcp_exact_lru", "pv_set_dnstap_only_hosts",
            "pv_afpacket_open", "pv_afpacket_attach", "pv_afpacket_run", "pv_afpacket_start", "pv_afpacket_stop",
            "pv_afpacket_stats", "pv_afpacket_close", "pv_afpacket_last_error", "pv_set_bpf", "pv_bpf_validate",
            "pv_bpf_run", "pv_bpf_filter_records", "pv_comm_merge_topn", "pv_topn_x_export", "pv_topn_x_import",
@@ -305,6 +305,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_window_periods.argtypes = [P, ctypes.c_int, P, P, U32, ctypes.POINTER(U32)]
     lib.pv_set_dns_filters.argtypes = [P, ctypes.POINTER(pv_dns_filters)]
     lib.pv_set_tcp_reassembly_limit.argtypes = [P, ctypes.c_uint64]
+    lib.pv_set_tcp_exact_lru.argtypes = [P, ctypes.c_int]
     lib.pv_set_bpf.argtypes = [P, P, U32]
     lib.pv_bpf_validate.argtypes = [P, U32]
     lib.pv_bpf_run.argtypes = [P, P, U32, U32]
@@ -594,7 +595,8 @@ class PvHandlers:
                  dns_filters: Optional[dict] = None, net_config: Optional[dict] = None,
                  dns_config: Optional[dict] = None, topn_percentile_threshold: int = 0,
                  net2_config: Optional[dict] = None, dns2_config: Optional[dict] = None,
-                 deep_sample_rate: int = 100, tcp_packet_reassembly_cache_limit: int = 0, bpf=None):
+                 deep_sample_rate: int = 100, tcp_packet_reassembly_cache_limit: int = 0, bpf=None,
+                 tcp_exact_lru: bool = False):
         from pktvisor_amd import config as pvcfg
         self.lib = load_library()
         filt = dns_filter_config(dns_filters) if dns_filters else None
@@ -666,6 +668,9 @@ class PvHandlers:
             # the pcap input's config (PcapInputStream.cpp:97-99)
             self._check(self.lib.pv_set_tcp_reassembly_limit(self.ctx, int(tcp_packet_reassembly_cache_limit)),
                         "pv_set_tcp_reassembly_limit")
+        if tcp_exact_lru:
+            # PcapInputStream's LRU of TCP connections replayed exactly (pv_set_tcp_exact_lru)
+            self._check(self.lib.pv_set_tcp_exact_lru(self.ctx, 1), "pv_set_tcp_exact_lru")
         if bpf:
             self.set_bpf(bpf)
 

@@ -144,6 +144,9 @@ extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg_tc(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_reg_sb(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_reg_nt(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_reg_sbnt(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
 extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
@@ -741,8 +744,9 @@ struct pv_ctx {
     bool tcp_active = false;  // a stage has run since the last reset
     bool tcp_pre = false;     // this batch's stage runs ahead of the Net pass (prescan emits)
     uint32_t tcp_nmsg = 0;    // messages of the current batch
-    // tcp_packet_reassembly_cache_limit (0: not set): PcapInputStream's LRU list of connections,
-    // replayed on the host across batches (front = most recently put; value = the put's second)
+    // tcp_packet_reassembly_cache_limit (0: not set). In the exact LRU mode PcapInputStream's LRU
+    // list of connections is replayed on the host across batches (front = most recently put;
+    // value = the put's second: ConnectionData's endTime, 0 before a connection's second packet)
     uint64_t tcp_limit = 0;
     // dnstap input proxy's only_hosts (DnstapInputEventProxy, src/inputs/dnstap/DnstapInputStream.h:96-146)
     bool dt_only_hosts = false;
@@ -750,7 +754,8 @@ struct pv_ctx {
     std::vector<std::pair<std::array<uint8_t, 16>, uint32_t>> dt_v6;
     std::list<std::pair<uint32_t, uint32_t>> lru;
     std::unordered_map<uint32_t, std::list<std::pair<uint32_t, uint32_t>>::iterator> lru_at;
-    std::unordered_map<uint32_t, bool> lru_pending; // evicted with no segment in their batch: closed at their next
+    bool tcp_exact = false;   // pv_set_tcp_exact_lru
+    bool tcp_exact_on() const { return tcp_exact || tcp_limit; }
     uint32_t *d_lru_ev = nullptr, *d_fclose = nullptr;
     uint64_t lru_ev_cap = 0, fclose_cap = 0;
     // deep sampling (deep_sample_rate < 100): each manager's generator, the span's "not deep"
@@ -2211,6 +2216,14 @@ int pv_set_tcp_reassembly_limit(pv_ctx *c, uint64_t limit)
     return 0;
 }
 
+int pv_set_tcp_exact_lru(pv_ctx *c, int on)
+{
+    if (!c) return PV_EINVAL;
+    if (c->records_seen) return c->fail(PV_EINVAL, "the exact TCP LRU mode must be set before the first batch");
+    c->tcp_exact = on != 0;
+    return 0;
+}
+
 // the public_suffix_list table on the device and the per-record suffix sizes (v1 and v2)
 static int psl_setup(pv_ctx *c)
 {
@@ -2581,7 +2594,6 @@ static void tcp_reset(pv_ctx *c)
     c->tcp_active = false;
     c->lru.clear();
     c->lru_at.clear();
-    c->lru_pending.clear();
 }
 
 int pv_reset(pv_ctx *c)
@@ -2792,8 +2804,9 @@ int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64
     flush_fills(c);
     PvParams P;
     params_common(c, P, d_recs, d_offs, n);
-    // 2: every TCP packet (tcp_packet_reassembly_cache_limit: the LRU holds every connection)
-    P.tcp_emit = tcp_emit ? (c->tcp_limit ? 3u : 1u) : 0u;
+    // 2: every TCP connection, 4: every TCP packet (the exact LRU mode: the LRU holds every
+    // connection and runs its cleanup after every TCP packet)
+    P.tcp_emit = tcp_emit ? (c->tcp_exact_on() ? 7u : 1u) : 0u;
     if (fbits) P.fbits = c->d_fbits;
     hipError_t e;
     *c->h_params = P;
@@ -2854,24 +2867,29 @@ int tcp_alloc(pv_ctx *c)
     return 0;
 }
 
-// PcapInputStream's LRU list under tcp_packet_reassembly_cache_limit (PcapInputStream.cpp:97-99,
-// 254-283,449-465), replayed over the batch's segments in capture order from the dry run's
-// events (skey: sorted fkey << 32 | record index; ev: flags | dir << 8, second, latest TCP second
-// + 1 before the record). Before a segment, the cleanup of the earlier TCP packets: connections
-// whose last put is 30 s older than the latest TCP second leave (the device closes them at
-// their next packet by the same rule). A connection start and a message delivery put the
-// connection at the head; a new one beyond the limit evicts the tail, which the stage closes
-// after this record (closeConnection); a FIN/RST close or a time-out erases. An evicted
-// connection's later segments in the batch are ignored (Ignore_PacketOfClosedFlow). fclose gets,
-// at the evicted flow's first sorted segment, the record, its second and its direction.
-void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vector<uint32_t> &ev,
-                    std::vector<uint32_t> &fclose)
+// PcapInputStream's LRU list in the exact LRU mode (PcapInputStream.cpp:97-99,254-283,429-465),
+// replayed over the batch's segments (every TCP packet) in capture order from the dry run's events
+// (skey: sorted fkey << 32 | record index; sval: segment index per sorted key; ev per sorted key:
+// flags | dir << 8, second, LRU time of the segment's last put). Per packet, as the reference: the
+// reassembly's puts (a connection start with its start second, a message delivery with endTime,
+// which is 0 until the connection's second packet) move the connection to the head and, past the
+// limit, evict the tail; a FIN/RST close erases it; then at most MAX_TCP_CLEANUPS (100) connections
+// leave from the tail while the tail's time + 30 s <= the packet's second, then the evicted ones
+// close. Every connection closed this way is closed after that record (closeConnection): fclose
+// (per segment index) at its first sorted segment when it has packets in the batch (its later
+// packets are then Ignore_PacketOfClosedFlow, and their events are skipped here), else a
+// close-only segment appended to `extra` with its fclose in `extra_fc`.
+void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vector<uint32_t> &sval,
+                    const std::vector<uint32_t> &ev, std::vector<uint32_t> &fclose, std::vector<PvTcpSeg> &extra,
+                    std::vector<uint32_t> &extra_fc)
 {
+    static constexpr int MAX_TCP_CLEANUPS = 100; // PcapInputStream.h:98
     const size_t n = skey.size();
-    std::vector<uint32_t> run0(n), order(n);
+    std::vector<uint32_t> order(n);
+    std::unordered_map<uint32_t, uint32_t> first; // flow -> its first sorted segment
     for (size_t k = 0; k < n; k++) {
-        run0[k] = (k && (skey[k] >> 32) == (skey[k - 1] >> 32)) ? run0[k - 1] : (uint32_t)k;
         order[k] = (uint32_t)k;
+        if (!k || (skey[k] >> 32) != (skey[k - 1] >> 32)) first[(uint32_t)(skey[k] >> 32)] = (uint32_t)k;
     }
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return (uint32_t)skey[a] < (uint32_t)skey[b]; });
     auto erase = [&](uint32_t f) {
@@ -2880,48 +2898,54 @@ void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vec
         c->lru.erase(it->second);
         c->lru_at.erase(it);
     };
-    std::unordered_map<uint32_t, uint32_t> evicted; // flow -> its first sorted segment
-    // connections evicted in an earlier batch that had no segment there: closed ahead of their
-    // first segment here
-    for (size_t k = 0; k < n && !c->lru_pending.empty(); k++) {
-        const uint32_t f = (uint32_t)(skey[k] >> 32);
-        if (run0[k] != k || !c->lru_pending.erase(f)) continue;
-        evicted[f] = (uint32_t)k;
-        fclose[3 * k] = PVT_FCLOSE_FIRST;
-        fclose[3 * k + 1] = ev[3 * k + 1];
-        fclose[3 * k + 2] = (ev[3 * k] >> 8) & 3;
-    }
+    std::unordered_map<uint32_t, bool> closed; // closed by the replay in this batch
+    auto close_after = [&](uint32_t v, uint32_t idx, uint32_t sec, uint32_t dir) {
+        erase(v);
+        if (closed.count(v)) return;
+        closed[v] = true;
+        auto it = first.find(v);
+        if (it != first.end()) {
+            uint32_t *w = &fclose[3 * (size_t)sval[it->second]];
+            w[0] = idx; w[1] = sec; w[2] = dir;
+            return;
+        }
+        PvTcpSeg g;
+        memset(&g, 0, sizeof g);
+        g.idx = idx;
+        g.fkey = v;
+        g.sec = sec;
+        g.flags = PV_TF_CLOSE;
+        g.dirv6 = (uint8_t)dir;
+        extra.push_back(g);
+        extra_fc.insert(extra_fc.end(), {idx, sec, dir});
+    };
+    std::vector<uint32_t> overflow;
+    auto put = [&](uint32_t f, uint32_t t) {
+        erase(f);
+        c->lru.emplace_front(f, t);
+        c->lru_at[f] = c->lru.begin();
+        if (c->tcp_limit && c->lru_at.size() > c->tcp_limit) {
+            const uint32_t v = c->lru.back().first;
+            c->lru_at.erase(v);
+            c->lru.pop_back();
+            overflow.push_back(v);
+        }
+    };
     for (uint32_t k : order) {
         const uint32_t f = (uint32_t)(skey[k] >> 32), idx = (uint32_t)skey[k];
-        const uint32_t fl = ev[3 * k] & 0xff, dir = (ev[3 * k] >> 8) & 3, sec = ev[3 * k + 1], lt = ev[3 * k + 2];
-        if (evicted.count(f)) continue;
-        while (lt && !c->lru.empty() && lt - 1 >= c->lru.back().second + PV_TCP_TIMEOUT) {
-            c->lru_at.erase(c->lru.back().first);
-            c->lru.pop_back();
+        const uint32_t fl = ev[3 * k] & 0xff, dir = (ev[3 * k] >> 8) & 3, sec = ev[3 * k + 1], pt = ev[3 * k + 2];
+        if (!closed.count(f)) {
+            if (fl & PVT_EV_NEW) put(f, sec);
+            if (fl & PVT_EV_PUT) put(f, pt);
+            if (fl & PVT_EV_CLOSE) erase(f);
         }
-        if (fl & (PVT_EV_NEW | PVT_EV_PUT)) {
-            erase(f);
-            c->lru.emplace_front(f, sec);
-            c->lru_at[f] = c->lru.begin();
-            if (c->lru_at.size() > c->tcp_limit) {
-                const uint32_t v = c->lru.back().first;
-                c->lru_at.erase(v);
-                c->lru.pop_back();
-                // the victim's first sorted segment; a flow with none in this batch is closed
-                // ahead of its next segment (lru_pending)
-                auto it = std::lower_bound(skey.begin(), skey.end(), (uint64_t)v << 32);
-                if (it != skey.end() && (uint32_t)(*it >> 32) == v) {
-                    const uint32_t r = run0[it - skey.begin()];
-                    evicted[v] = r;
-                    fclose[3 * r] = idx;
-                    fclose[3 * r + 1] = sec;
-                    fclose[3 * r + 2] = dir;
-                } else {
-                    c->lru_pending[v] = true;
-                }
-            }
+        for (int q = 0; q < MAX_TCP_CLEANUPS && !c->lru.empty(); q++) {
+            const auto back = c->lru.back();
+            if ((uint64_t)sec < (uint64_t)back.second + PV_TCP_TIMEOUT) break;
+            close_after(back.first, idx, sec, dir);
         }
-        if (fl & (PVT_EV_CLOSE | PVT_EV_TIMEOUT)) erase(f);
+        for (uint32_t v : overflow) close_after(v, idx, sec, dir);
+        overflow.clear();
     }
 }
 
@@ -2988,8 +3012,8 @@ int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t
     T.cnt = c->d_tcpcnt;
     flush_fills(c);
     const PvTcpParams *dT = c->d_tparams;
-    const uint32_t blocks = (n_seg + 255) / 256;
-    // one run of the stage's kernels (dry: the cache-limit replay's recording run)
+    uint32_t blocks = (n_seg + 255) / 256;
+    // one run of the stage's kernels (dry: the exact LRU replay's recording run)
     auto run = [&](bool dry) -> int {
         T.dry = dry ? 1u : 0u;
         if (!hip_ok(e = hipMemsetAsync(c->d_tcpcnt, 0, PVT_WORDS * 4, st)) ||
@@ -3012,22 +3036,36 @@ int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch TCP stage");
         return 0;
     };
-    if (c->tcp_limit && n_seg) {
-        // tcp_packet_reassembly_cache_limit: record the segments' LRU events, replay the LRU
-        // list on the host, then run the stage with the evictions it found
+    T.exact = c->tcp_exact_on() ? 1u : 0u;
+    if (T.exact && n_seg) {
+        // the exact LRU mode: record the segments' LRU events, replay the LRU list on the host,
+        // then run the stage with the closes it found (close-only segments behind the batch's)
         if (int rc = PV_GROW(c, c->d_lru_ev, c->lru_ev_cap, 3ull * n_seg, "TCP LRU events")) return rc;
-        if (int rc = PV_GROW(c, c->d_fclose, c->fclose_cap, 3ull * n_seg, "TCP LRU closes")) return rc;
         T.lru_ev = c->d_lru_ev;
         T.fclose = nullptr;
         if (int rc = run(true)) return rc;
         std::vector<uint64_t> skey(n_seg);
-        std::vector<uint32_t> ev(3ull * n_seg);
+        std::vector<uint32_t> sval(n_seg), ev(3ull * n_seg);
         if (!hip_ok(e = hipMemcpyAsync(skey.data(), c->d_tkey[1], (size_t)n_seg * 8, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipMemcpyAsync(sval.data(), c->d_tval[1], (size_t)n_seg * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipMemcpyAsync(ev.data(), c->d_lru_ev, ev.size() * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "TCP LRU events");
-        std::vector<uint32_t> fclose(3ull * n_seg, PVT_FCLOSE_NONE);
-        tcp_lru_replay(c, skey, ev, fclose);
+        std::vector<uint32_t> fclose(3ull * n_seg, PVT_FCLOSE_NONE), extra_fc;
+        std::vector<PvTcpSeg> extra;
+        tcp_lru_replay(c, skey, sval, ev, fclose, extra, extra_fc);
+        if (!extra.empty()) {
+            if (n_seg + extra.size() > c->tseg_cap)
+                return c->fail(PV_ECAPACITY, "%u TCP segments and %zu LRU closes in one batch exceed the capacity %u (max_records)",
+                               n_seg, extra.size(), c->tseg_cap);
+            fclose.insert(fclose.end(), extra_fc.begin(), extra_fc.end());
+            if (!hip_ok(e = hipMemcpyAsync(c->d_tseg + n_seg, extra.data(), extra.size() * sizeof(PvTcpSeg), hipMemcpyHostToDevice, st)))
+                return c->hipfail(e, "TCP LRU closes");
+            n_seg += (uint32_t)extra.size();
+            T.n_seg = n_seg;
+            blocks = (n_seg + 255) / 256;
+        }
+        if (int rc = PV_GROW(c, c->d_fclose, c->fclose_cap, 3ull * n_seg, "TCP LRU closes")) return rc;
         if (!hip_ok(e = hipMemcpyAsync(c->d_fclose, fclose.data(), fclose.size() * 4, hipMemcpyHostToDevice, st)))
             return c->hipfail(e, "TCP LRU closes");
         c->tcp_stage++;
@@ -3117,7 +3155,7 @@ uint32_t tcp_pass(pv_ctx *c, const PvParams &P, uint64_t a, uint64_t b, hipStrea
 // name arena of a purged table is compacted once its fullest partition is half used. The
 // live counts are the ones read back with the batch status (names added by the transaction
 // pass afterwards are counted at the next batch).
-int purge_table(pv_ctx *c, uint32_t t, hipStream_t st);
+int purge_table(pv_ctx *c, uint32_t t, hipStream_t st, const PvParams *dP = nullptr);
 int purge_tables(pv_ctx *c, hipStream_t st)
 {
     const uint64_t tcap = 1ull << c->tcap_log2;
@@ -3132,8 +3170,9 @@ int purge_tables(pv_ctx *c, hipStream_t st)
 // to, as the sketch purges when its map is full, and insert them again, until none is left.
 // Each round at least halves the live entries of every region it purges, so the rounds end.
 // known: c->h_ovf already holds the words (read back with the batch status).
-int drain_overflow(pv_ctx *c, hipStream_t st, bool known = false, bool *drained = nullptr)
+int drain_overflow(pv_ctx *c, hipStream_t st, bool known = false, bool *drained = nullptr, const PvParams *dP = nullptr)
 {
+    if (!dP) dP = c->d_params;
     hipError_t e;
     for (int round = 0;; round++) {
         uint32_t oc[2];
@@ -3147,23 +3186,24 @@ int drain_overflow(pv_ctx *c, hipStream_t st, bool known = false, bool *drained 
         if (round >= 64) return c->fail(PV_ECAPACITY, "top-N overflow not drained after %d purge rounds", round);
         for (uint32_t t = 0; t < PV_TABLES; t++)
             if ((oc[1] >> t) & 1)
-                if (int rc = purge_table(c, t, st)) return rc;
+                if (int rc = purge_table(c, t, st, dP)) return rc;
         if (!hip_ok(e = hipMemcpyAsync(c->d_ovf2, c->d_ovf, (size_t)oc[0] * sizeof(PvOvf), hipMemcpyDeviceToDevice, st)) ||
             !hip_ok(e = hipMemsetAsync(c->d_ovf_cnt, 0, 8, st)))
             return c->hipfail(e, "top-N overflow");
-        hipLaunchKernelGGL(pv_topn_retry, dim3((oc[0] + 255) / 256), dim3(256), 0, st, (const PvParams *)c->d_params, c->d_ovf2, oc[0]);
+        hipLaunchKernelGGL(pv_topn_retry, dim3((oc[0] + 255) / 256), dim3(256), 0, st, dP, c->d_ovf2, oc[0]);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_topn_retry");
         c->ovf_rounds++;
     }
 }
 
-int purge_table(pv_ctx *c, uint32_t t, hipStream_t st)
+int purge_table(pv_ctx *c, uint32_t t, hipStream_t st, const PvParams *dP)
 {
+    if (!dP) dP = c->d_params;
     const uint32_t nreg = 1u << c->reg_log2;
     hipError_t e;
     {
         c->h_tab_live[t] = 0; // stale until the next batch reads the device count back
-        hipLaunchKernelGGL(pv_topn_purge, dim3(nreg), dim3(1024), 0, st, (const PvParams *)c->d_params, t, c->d_theta);
+        hipLaunchKernelGGL(pv_topn_purge, dim3(nreg), dim3(1024), 0, st, dP, t, c->d_theta);
         std::vector<uint32_t> th(nreg);
         uint64_t tops[PV_ARENA_PARTS];
         if (!hip_ok(e = hipGetLastError()) ||
@@ -3185,8 +3225,7 @@ int purge_table(pv_ctx *c, uint32_t t, hipStream_t st)
         }
         uint8_t *arena = c->d_arena + (uint64_t)t * c->arena_cap;
         if (!hip_ok(e = hipMemsetAsync(c->d_ctop, 0, PV_ARENA_PARTS * 8, st))) return c->hipfail(e, "arena compaction");
-        hipLaunchKernelGGL(pv_topn_compact, dim3((uint32_t)c->cus * 8), dim3(256), 0, st, (const PvParams *)c->d_params, t,
-                           c->d_ctmp, c->d_ctop);
+        hipLaunchKernelGGL(pv_topn_compact, dim3((uint32_t)c->cus * 8), dim3(256), 0, st, dP, t, c->d_ctmp, c->d_ctop);
         if (!hip_ok(e = hipGetLastError()) ||
             !hip_ok(e = hipMemcpyAsync(arena, c->d_ctmp, c->arena_cap, hipMemcpyDeviceToDevice, st)) ||
             !hip_ok(e = hipMemcpyAsync(c->d_arena_top + (uint64_t)t * PV_ARENA_PARTS, c->d_ctop, PV_ARENA_PARTS * 8,
@@ -3598,7 +3637,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     params_common(c, P, d_recs, d_offs, n);
     // a batch with no TCP stage ahead of it is one span: its Net pass emits the TCP segments
     // and the tile masks of its TCP records (zeroed here; the pass stores non-zero masks only)
-    P.tcp_emit = c->tcp_pre ? 0u : (c->tcp_limit ? 3u : 1u);
+    P.tcp_emit = c->tcp_pre ? 0u : (c->tcp_exact_on() ? 7u : 1u);
     if (P.tcp_emit) launch_fill64(c, c->d_tmask, (n + 63) / 64, 0);
     P.gbase = c->global_base + c->records_seen;
     if (c->slow_defer && !c->edge_h) c->edge_h = (int64_t)first_sec + c->ttl_s + 61;
@@ -3796,8 +3835,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     // its packed lane counters), else the shift-free general pass. PV_NET_KERNEL=ns|general
     // forces one for A/B runs.
     static const char *force = getenv("PV_NET_KERNEL");
-    // (every TCP segment for the cache-limit replay: the general pass emits them)
-    const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || c->tcp_limit || (force && !strcmp(force, "general"));
+    // (every TCP packet for the exact LRU replay: the general pass emits them)
+    const bool general = P.n_shift || P.net_filter_all || P.dbg || P.ndeep_net || c->tcp_exact_on() ||
+                         (force && !strcmp(force, "general"));
     const uint32_t reg_grid = std::min<uint32_t>(grid, (uint32_t)(c->cus * c->reg_wg_per_cu));
     const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
     const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
@@ -3817,7 +3857,11 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
     const bool tc = (c->net_groups & PV_NET_TOP_IPS) && c->reg_waves != 8;
-    c->net_kernel = general ? "pv_net_kernel"
+    // store-mode A/B of the top-IPs pass: PV_NET_KERNEL=sb (LDS-staged IP log) | nt (non-temporal) | sbnt
+    const int smode = !(lean && tc && regw && !ring && force) ? 0
+                      : !strcmp(force, "sb") ? 1 : !strcmp(force, "nt") ? 2 : !strcmp(force, "sbnt") ? 3 : 0;
+    c->net_kernel = smode ? (smode == 1 ? "pv_net_kernel_reg_sb" : smode == 2 ? "pv_net_kernel_reg_nt" : "pv_net_kernel_reg_sbnt")
+                  : general ? "pv_net_kernel"
                             : (lean ? (ring ? "pv_net_kernel_fast"
                                             : (!regw ? "pv_net_kernel_ring"
                                                      : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : (tc ? "pv_net_kernel_reg_tc" : "pv_net_kernel_reg"))))
@@ -3836,6 +3880,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         hipLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(ring_threads), 0, st, (const PvParams *)c->d_params);
     }
     else if (lean && c->reg_waves == 8) hipLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, (const PvParams *)c->d_params);
+    else if (lean && tc && smode)
+        hipLaunchKernelGGL(smode == 1 ? pv_net_kernel_reg_sb : smode == 2 ? pv_net_kernel_reg_nt : pv_net_kernel_reg_sbnt, dim3(reg_grid),
+                           dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean && tc) hipLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -5860,6 +5907,14 @@ int x_merge_recv(pv_ctx *c, uint32_t W, uint32_t me, const std::vector<uint64_t>
     P.xmerge = 1;
     P.x_lo = lo;
     P.x_hi = hi;
+    // a full region's entries go to the overflow list; the table is purged (the frequent-items
+    // merge's purge, src/Metrics.h:534-538) and they are inserted again (drain_overflow)
+    P.ovf = c->d_ovf;
+    P.ovf_cnt = c->d_ovf_cnt;
+    P.ovf_cap = c->ovf_cap;
+    P.arena = c->d_arena;
+    P.arena_top = c->d_arena_top;
+    P.arena_cap = c->arena_cap;
     P.cb = (uint64_t *)c->d_xrecv;
     P.cb_fan = 1;
     P.mq_cap = (uint32_t)stride;
@@ -5877,11 +5932,12 @@ int x_merge_recv(pv_ctx *c, uint32_t W, uint32_t me, const std::vector<uint64_t>
     if (!hip_ok(e = hipMemcpyAsync(c->d_xp, &P, sizeof P, hipMemcpyHostToDevice, c->stream))) return c->hipfail(e, "exchange parameters");
     hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(pv_topn_merge_threads()), 0, c->stream, (const PvParams *)c->d_xp);
     uint32_t flags = 0;
-    if (!hip_ok(e = hipGetLastError()) ||
-        !hip_ok(e = hipMemcpyAsync(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost, c->stream)) ||
+    if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "exchange merge");
+    if (int rc = drain_overflow(c, c->stream, false, nullptr, c->d_xp)) return rc;
+    if (!hip_ok(e = hipMemcpyAsync(&flags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost, c->stream)) ||
         !hip_ok(e = hipStreamSynchronize(c->stream)))
         return c->hipfail(e, "exchange merge");
-    if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "multi-GPU top-N merge: a region is full (raise table_log2)");
+    if (flags & PVF_TABLE_FULL) return c->fail(PV_ECAPACITY, "multi-GPU top-N merge: the overflow list is full (raise table_log2)");
     for (uint32_t s : c->net.slots) c->net.clean[s] = false;
     for (uint32_t s : c->dns.slots) c->dns.clean[s] = false;
     c->x_ranks = W;
@@ -6376,37 +6432,57 @@ uint64_t x_rank_of(double p, uint64_t n)
     uint64_t idx = w == 0 ? 0 : w - 1;
     return n && idx >= n ? n - 1 : idx;
 }
-// groups[g]: this rank's values of group g; fr[g]: the fractions wanted. out[g][k]: the value at
-// each fraction's rank over every rank's values (0 when the group is empty everywhere); n[g]: the
-// group's count over every rank
-int x_select(pv_ctx *c, pv_allreduce_fn ar, void *user, const std::vector<std::vector<uint64_t>> &groups,
+// Exact distributed selection. gparts[g]: this rank's values of group g, as sorted parts (a
+// value lies in one part); fr[g]: the fractions wanted. out[g][k]: the value at each fraction's
+// rank over every rank's values (0 when the group is empty everywhere); n[g]: the group's count
+// over every rank. Eight passes, one byte each from the top: per target the 256-bin histogram of
+// the values whose higher bytes equal the target's prefix so far, all-reduced (one call per
+// pass), then the bin holding the target's rank. The bins are counted by binary searches over the
+// sorted parts (257 bin edges per part), so a pass costs O(targets x parts x 256 log n), not a
+// scan of every value per target.
+using XParts = std::vector<const std::vector<uint64_t> *>;
+int x_select(pv_ctx *c, pv_allreduce_fn ar, void *user, const std::vector<XParts> &gparts,
              const std::vector<std::vector<double>> &fr, std::vector<uint64_t> &n, std::vector<std::vector<uint64_t>> &out)
 {
-    const size_t G = groups.size();
+    const size_t G = gparts.size();
     struct Tg { uint32_t g; double p; uint64_t rank, prefix; };
     std::vector<Tg> T;
     for (uint32_t g = 0; g < G; g++)
         for (double p : fr[g]) T.push_back(Tg{g, p, 0, 0});
     n.assign(G, 0);
     out.assign(G, {});
+    // values <= x in a group's parts
+    auto count_le = [&](const XParts &ps, uint64_t x) {
+        uint64_t k = 0;
+        for (const std::vector<uint64_t> *v : ps) k += (uint64_t)(std::upper_bound(v->begin(), v->end(), x) - v->begin());
+        return k;
+    };
     std::vector<uint64_t> h;
     for (int pass = 0; pass < 8; pass++) {
         const uint32_t shift = 56 - 8 * pass;
-        const uint64_t hm = pass == 0 ? 0ull : ~0ull << (shift + 8);
-        if (pass == 0) {
-            // one histogram per group (every target of a group shares it)
-            h.assign(G * 256, 0);
-            for (uint32_t g = 0; g < G; g++)
-                for (uint64_t x : groups[g]) h[(size_t)g * 256 + (x >> 56)]++;
-        } else {
-            h.assign(T.size() * 256, 0);
-            for (size_t t = 0; t < T.size(); t++)
-                for (uint64_t x : groups[T[t].g])
-                    if ((x & hm) == (T[t].prefix & hm)) h[t * 256 + ((x >> shift) & 255)]++;
+        h.assign(T.size() * 256, 0);
+        std::map<std::pair<uint32_t, uint64_t>, size_t> done; // (group, range) -> target that counted it
+        for (size_t t = 0; t < T.size(); t++) {
+            const XParts &ps = gparts[T[t].g];
+            // the target's range: its prefix above this byte, every value of the lower bytes
+            const uint64_t base = pass == 0 ? 0ull : T[t].prefix & (~0ull << (shift + 8));
+            auto it = done.find({T[t].g, base});
+            if (it != done.end()) {
+                std::copy(h.begin() + it->second * 256, h.begin() + it->second * 256 + 256, h.begin() + t * 256);
+                continue;
+            }
+            done[{T[t].g, base}] = t;
+            uint64_t below = base ? count_le(ps, base - 1) : 0;
+            for (uint32_t bn = 0; bn < 256; bn++) {
+                const uint64_t top = base + ((uint64_t)bn << shift) + ((1ull << shift) - 1);
+                const uint64_t le = count_le(ps, top);
+                h[t * 256 + bn] = le - below;
+                below = le;
+            }
         }
         if (int rc = x_allreduce(c, ar, user, h, 0)) return rc;
         for (size_t t = 0; t < T.size(); t++) {
-            const uint64_t *hh = &h[(pass == 0 ? (size_t)T[t].g : t) * 256];
+            const uint64_t *hh = &h[t * 256];
             if (pass == 0) {
                 uint64_t tot = 0;
                 for (int b = 0; b < 256; b++) tot += hh[b];
@@ -6444,19 +6520,27 @@ int values_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
         }
     }
     const size_t G = sets.size() * 9;
-    std::vector<std::vector<uint64_t>> groups(G);
     std::vector<std::vector<double>> fr(G, std::vector<double>{0.50, 0.90, 0.95, 0.99, 2.0});
-    std::map<uint32_t, uint32_t> sg_bit; // live slot | gen << 8 -> its slot bit
-    for (uint32_t s : c->dns.slots) sg_bit[s | (c->gen[s] << 8)] = 1u << s;
+    // the values by (live slot, kind), each sorted once; a group (slot set, kind) is the parts of
+    // its slots
+    std::map<uint32_t, uint32_t> sg_idx; // live slot | gen << 8 -> its index among the live slots
+    for (size_t i = 0; i < c->dns.slots.size(); i++) sg_idx[c->dns.slots[i] | (c->gen[c->dns.slots[i]] << 8)] = (uint32_t)i;
+    const size_t NS = c->dns.slots.size();
+    std::vector<std::vector<uint64_t>> part(NS * 9);
     for (const PvXValue &v : c->xvals_host) {
-        auto it = sg_bit.find(v.slot);
-        if (it == sg_bit.end()) continue;
+        auto it = sg_idx.find(v.slot);
+        if (it == sg_idx.end()) continue;
         int k = 0;
         while (k < 9 && v.kind != X_KINDS[k]) k++;
         if (k == 9) continue;
-        for (size_t i = 0; i < sets.size(); i++)
-            if (sets[i] & it->second) groups[i * 9 + k].push_back(v.bits);
+        part[(size_t)it->second * 9 + k].push_back(v.bits);
     }
+    for (auto &v : part) std::sort(v.begin(), v.end());
+    std::vector<XParts> groups(G);
+    for (size_t i = 0; i < sets.size(); i++)
+        for (size_t si = 0; si < NS; si++)
+            if (sets[i] & (1u << c->dns.slots[si]))
+                for (int k = 0; k < 9; k++) groups[i * 9 + k].push_back(&part[si * 9 + k]);
     std::vector<uint64_t> n;
     std::vector<std::vector<uint64_t>> q;
     if (int rc = x_select(c, ar, user, groups, fr, n, q)) return rc;
@@ -6465,9 +6549,9 @@ int values_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
     std::vector<uint64_t> cdf(G * pts.size(), 0);
     for (size_t gi = 0; gi < G; gi++) {
         if (!x_time_kind(X_KINDS[gi % 9])) continue;
-        std::vector<uint64_t> v = groups[gi];
-        std::sort(v.begin(), v.end());
-        for (size_t k = 0; k < pts.size(); k++) cdf[gi * pts.size() + k] = (uint64_t)(std::upper_bound(v.begin(), v.end(), pts[k]) - v.begin());
+        for (size_t k = 0; k < pts.size(); k++)
+            for (const std::vector<uint64_t> *v : groups[gi])
+                cdf[gi * pts.size() + k] += (uint64_t)(std::upper_bound(v->begin(), v->end(), pts[k]) - v->begin());
     }
     if (int rc = x_allreduce(c, ar, user, cdf, 0)) return rc;
     c->xq.clear();
@@ -7321,9 +7405,14 @@ int slow_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
     }
     for (auto &ev : c->slow_xv) put(ev.first, ev.second);
     std::vector<std::vector<double>> fr(groups.size(), std::vector<double>{0.90});
+    std::vector<XParts> gparts(groups.size());
+    for (size_t i = 0; i < groups.size(); i++) {
+        std::sort(groups[i].begin(), groups[i].end());
+        gparts[i].push_back(&groups[i]);
+    }
     std::vector<uint64_t> n;
     std::vector<std::vector<uint64_t>> q;
-    if (int rc = x_select(c, ar, user, groups, fr, n, q)) return rc;
+    if (int rc = x_select(c, ar, user, gparts, fr, n, q)) return rc;
     if (!want) return 0;
     std::vector<float> thr[NK];
     for (int k = 0; k < NK; k++) {

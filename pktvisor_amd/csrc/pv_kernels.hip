@@ -442,14 +442,17 @@ __device__ __forceinline__ TPos tpos(PV_CREF(PvParams) P, uint32_t slot, uint64_
 }
 
 // an update its full region could not take: kept for pv_topn_retry (after the host purges the
-// table); past the list's capacity, or without a record to name the key from, the batch fails
+// table); past the list's capacity, or without a record to name the key from, the batch fails.
+// A multi-GPU owner merge's entries carry no record (their names are fetched for the read view):
+// they keep their 64-bit weight in (w, rep), marked by pad = 1.
 __device__ __forceinline__ void table_overflow(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep,
                                                bool named)
 {
-    if (!P.ovf || !named) { atomicOr(P.flags, PVF_TABLE_FULL); return; }
+    const bool xm = P.xmerge != 0;
+    if (!P.ovf || (!named && !xm)) { atomicOr(P.flags, PVF_TABLE_FULL); return; }
     const uint32_t k = atomicAdd(P.ovf_cnt, 1u);
     if (k >= P.ovf_cap) { atomicOr(P.flags, PVF_TABLE_FULL); return; }
-    P.ovf[k] = PvOvf{key, (uint32_t)w, rep, slot, 0};
+    P.ovf[k] = xm ? PvOvf{key, (uint32_t)w, (uint32_t)(w >> 32), slot, 1u} : PvOvf{key, (uint32_t)w, rep, slot, 0};
     atomicOr(P.ovf_cnt + 1, 1u << PV_TSLOT(slot, PV_KEY_METRIC(key)));
 }
 
@@ -1574,13 +1577,18 @@ __device__ __forceinline__ uint64_t tcp_ep6(uint64_t w0, uint64_t w1, uint32_t s
     return fmix64(w0 ^ fmix64(w1 ^ ((uint64_t)sport_raw << 48) ^ 0x7463703600000000ull));
 }
 __device__ __forceinline__ bool tcp_seg_fill(PvTcpSeg &g, uint32_t pw, uint32_t w3, uint32_t seq_raw, uint32_t l4len, uint64_t l4off,
-                                             uint64_t i, uint32_t fkey, int64_t sec, int32_t nsec, uint64_t ep, uint32_t dirv6)
+                                             uint64_t i, uint32_t fkey, int64_t sec, int32_t nsec, uint64_t ep, uint32_t dirv6,
+                                             uint32_t mode)
 {
     const uint32_t hl = ((w3 >> 4) & 0xf) * 4; // data offset (byte 12), flags (byte 13)
-    if (hl < 20 || hl > l4len) return false;
-    const uint32_t fl = (w3 >> 8) & 7;
-    const uint32_t plen = l4len - hl;
-    if (!plen && !fl) return false;
+    const bool bad = hl < 20 || hl > l4len;
+    uint32_t fl = (w3 >> 8) & 7;
+    const uint32_t plen = bad ? 0u : l4len - hl;
+    if (bad || (!plen && !fl)) {
+        // ignored by reassembly; the exact LRU mode (mode bit 4) keeps it for the cleanup after it
+        if (!(mode & 4)) return false;
+        fl = PV_TF_NODATA;
+    }
     g.idx = (uint32_t)i;
     g.poff = (uint32_t)(l4off + hl);
     g.seq = __builtin_bswap32(seq_raw);
@@ -1597,11 +1605,11 @@ __device__ __forceinline__ bool tcp_seg_fill(PvTcpSeg &g, uint32_t pw, uint32_t 
     return true;
 }
 template <class A>
-__device__ __forceinline__ bool tcp_seg_of(const A &R, const Parsed &o, uint64_t i, PvTcpSeg &g, bool all = false)
+__device__ __forceinline__ bool tcp_seg_of(const A &R, const Parsed &o, uint64_t i, PvTcpSeg &g, uint32_t mode = 1)
 {
     if (o.l4 != 6) return false;
     const uint32_t pw = R.u32(o.l4off);
-    if (!all && !tcp_dns_pw(pw)) return false;
+    if (!(mode & 2) && !tcp_dns_pw(pw)) return false;
     const bool v6first = o.has6 && (!o.has4 || o.v6 < o.v4);
     uint64_t ep;
     if (!v6first) ep = tcp_ep4(R.u32(o.v4 + 12), pw & 0xffff);
@@ -1611,15 +1619,15 @@ __device__ __forceinline__ bool tcp_seg_of(const A &R, const Parsed &o, uint64_t
                      pw & 0xffff);
     }
     return tcp_seg_fill(g, pw, R.u32(o.l4off + 12), R.u32(o.l4off + 4), o.l4len, o.l4off, i, flowkey(R, o), o.sec, o.nsec, ep,
-                        o.dir | (v6first ? 4u : 0u));
+                        o.dir | (v6first ? 4u : 0u), mode);
 }
 // the same from a fast-path record's words (Ethernet + IPv4 without options: TCP at record offset 50)
-__device__ __forceinline__ bool tcp_seg_fast(const RecW &r, const Parsed &o, uint64_t i, PvTcpSeg &g, bool all = false)
+__device__ __forceinline__ bool tcp_seg_fast(const RecW &r, const Parsed &o, uint64_t i, PvTcpSeg &g, uint32_t mode = 1)
 {
     const uint32_t pw = r.at(50);
-    if (!all && !tcp_dns_pw(pw)) return false;
+    if (!(mode & 2) && !tcp_dns_pw(pw)) return false;
     return tcp_seg_fill(g, pw, r.w[15] >> 16, r.at(54), o.l4len, o.l4off, i, fast_flowkey(r), o.sec, o.nsec,
-                        tcp_ep4(r.at(42), pw & 0xffff), o.dir);
+                        tcp_ep4(r.at(42), pw & 0xffff), o.dir, mode);
 }
 // wave-compacted append of the lanes' segments (one atomic per wave), with their payload bytes
 __device__ __forceinline__ void tcp_seg_store(PV_G PvTcpSeg *out, PV_G uint32_t *cnt, uint32_t cap, bool has, const PvTcpSeg &g,
@@ -1674,7 +1682,7 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
     if (K.tcp_emit && o.l4 == 6) {
         // a DNS-port TCP segment of a general-path frame: appended by this lane alone
         PvTcpSeg g;
-        if (tcp_seg_of(R, o, i, g, K.tcp_emit & 2)) {
+        if (tcp_seg_of(R, o, i, g, K.tcp_emit)) {
             const uint32_t q = atomicAdd(K.tseg_cnt, 1u);
             atomicAdd(K.tseg_cnt + 1, (uint32_t)g.plen);
             if (q < K.tseg_cap) K.tseg[q] = g;
@@ -1871,7 +1879,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
                 isdns = so.isdns;
                 if (!ddeep) dm.a.w |= 16u << 16; // DnsMsg flags bit 4: the DNS event is not deep
             } else if (K.tcp_emit && o.l4 == 6) {
-                hasseg = tcp_seg_fast(rw, o, i, seg, GEN && (K.tcp_emit & 2));
+                hasseg = tcp_seg_fast(rw, o, i, seg, GEN ? K.tcp_emit : 1u);
             }
             istcp = o.l4 == 6;
             if (!deep) o.syn = 0;
@@ -2350,11 +2358,18 @@ __device__ __forceinline__ void win_words(const uint4 (&W)[5], uint32_t sh, RecW
 // them as younger ops instead of waiting for them: a store takes microseconds to complete under
 // the read stream, and a wait that covers the previous tile's stores (as the branchy form's
 // does) stalls every tile on them (tools/ring_probe.hip: 138 -> 177 us on C2 with a 4-B store).
-template <uint32_t NW, bool TC = false>
+// SM (store mode, TC only): 0 the IP-log words and direction word stored per tile; bit 0: staged in
+// LDS and flushed every 8 tiles (each wave then walks a contiguous block of its range's tiles, so
+// a flush is two 16-B stores a lane and one direction store), so a wave's load waits meet a store
+// once per 8 tiles instead of every tile; bit 1: non-temporal stores.
+template <uint32_t NW, bool TC = false, uint32_t SM = 0>
 __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ NetRegState S;
+    constexpr bool SB = TC && (SM & 1);
+    __shared__ uint4 sbq[SB ? NW * 128 : 1];    // per wave: 8 tiles x 64 IP-log words
+    __shared__ uint64_t sbdir[SB ? NW * 8 : 1]; // per wave: 8 direction words
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x == 0) { S.nd = 0; S.nx = 0; }
@@ -2385,9 +2400,14 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
     const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
     const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
-    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u;
+    // tiles of this wave: wave, wave + NW, ... (SB: a contiguous block of ceil(tiles / NW))
+    const uint64_t nrt = wend > wbeg ? wend - wbeg : 0, per = (nrt + NW - 1) / NW, first = SB ? wave * per : wave;
+    const uint32_t ntl = SB ? (first < nrt ? (uint32_t)min<uint64_t>(per, nrt - first) : 0u)
+                            : (wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u);
     any |= ntl != 0;
-    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
+    auto tile_of = [&](uint32_t k) -> uint64_t {
+        return SB ? wbeg + first + min(k, ntl - 1) : wbeg + wave + (uint64_t)NW * min(k, ntl - 1);
+    };
     auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
     // one tile from its windows W (off: this lane's record start)
     auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
@@ -2488,11 +2508,41 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                 const bool v4 = ek && ((ek >> 32) & ~1ull) == (P.ip_base >> 32);
                 const uint64_t xm = __ballot(active && ek && !v4);
                 const uint64_t dbit = __ballot(v4 && ((ek >> 32) & 1));
-                if (TC) {
+                if (SB) {
+                    // staged; the wave flushes 8 tiles (or its last ones) with coalesced stores
+                    const uint32_t kk = k & 7;
+                    reinterpret_cast<uint32_t *>(sbq)[wave * 512 + kk * 64 + lane] = active && v4 ? (uint32_t)ek : 0u;
+                    if (lane == 0) sbdir[wave * 8 + kk] = dbit;
+                    if (kk == 7 || k + 1 == ntl) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        const uint32_t m = kk + 1;
+                        const uint64_t t0 = t - kk;
+                        PV_G uint4 *dst = reinterpret_cast<PV_G uint4 *>(P.iplog32 + t0 * 64);
+                        for (uint32_t j = lane; j < m * 16; j += 64) {
+                            const uint4 q = sbq[wave * 128 + j];
+                            if (SM & 2) {
+                                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                                const u32x4 v = {q.x, q.y, q.z, q.w};
+                                __builtin_nontemporal_store(v, reinterpret_cast<PV_G u32x4 *>(dst + j));
+                            } else {
+                                dst[j] = q;
+                            }
+                        }
+                        if (lane < m) P.ipdir[t0 + lane] = sbdir[wave * 8 + lane];
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                } else if (TC) {
                     // every lane (the log has 64 words of slack past the batch) and every lane
                     // the same direction word: two unconditional store instructions
-                    P.iplog32[i] = active && v4 ? (uint32_t)ek : 0u;
-                    P.ipdir[t] = dbit;
+                    if (SM & 2) {
+                        __builtin_nontemporal_store(active && v4 ? (uint32_t)ek : 0u, P.iplog32 + i);
+                        __builtin_nontemporal_store(dbit, P.ipdir + t);
+                    } else {
+                        P.iplog32[i] = active && v4 ? (uint32_t)ek : 0u;
+                        P.ipdir[t] = dbit;
+                    }
                 } else {
                     if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
                     if (lane == 0) P.ipdir[t] = dbit;
@@ -2969,6 +3019,10 @@ extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg<4>(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_tc(const PvParams *__restrict__ Pp) { net_fast_reg<4, true>(Pp); }
+// store-mode A/B builds of the top-IPs pass (PV_NET_KERNEL=sb|nt|sbnt)
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_sb(const PvParams *__restrict__ Pp) { net_fast_reg<4, true, 1>(Pp); }
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_nt(const PvParams *__restrict__ Pp) { net_fast_reg<4, true, 2>(Pp); }
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_sbnt(const PvParams *__restrict__ Pp) { net_fast_reg<4, true, 3>(Pp); }
 extern "C" __global__ void __launch_bounds__(64 * PV_RING_NW) pv_net_kernel_ring(const PvParams *__restrict__ Pp) { net_ring(Pp); }
 // eight waves in the one workgroup of a CU: two per SIMD to hide instruction latency, one record stream per CU
 extern "C" __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg8(const PvParams *__restrict__ Pp) { net_fast_reg<8>(Pp); }
@@ -4155,7 +4209,8 @@ extern "C" __global__ void pv_topn_retry(const PvParams *__restrict__ Pp, const 
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const PvOvf e = src[j];
-    global_add(P, e.slot, e.key, e.w, e.rep);
+    if (e.pad) global_add(P, e.slot, e.key, (uint64_t)e.w | ((uint64_t)e.rep << 32), 0u); // an owner merge's entry
+    else global_add(P, e.slot, e.key, e.w, e.rep);
 }
 
 // Bounded top-N tables: the frequent-items sketch's purge (Apache DataSketches
@@ -4443,7 +4498,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_dns_prescan(const PvParams 
             Parsed o;
             parse_record(R, P, P.offs[i], o);
             istcp = o.l4 == 6;
-            if (P.tcp_emit && istcp) hasseg = tcp_seg_of(R, o, i, g, P.tcp_emit & 2);
+            if (P.tcp_emit && istcp) hasseg = tcp_seg_of(R, o, i, g, P.tcp_emit);
             if (o.l4 == 17 && dns_port(R.u32(o.l4off))) {
                 ev = true;
                 if (P.f_flags & (PVDF_ONLY_RCODE | PVDF_ONLY_QNAME)) {

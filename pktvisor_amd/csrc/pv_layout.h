@@ -237,7 +237,11 @@ struct PvTcpSeg {
     uint8_t dirv6;       // PacketDirection | (first IP layer is IPv6) << 2
     uint32_t pad[2];
 };
-enum { PV_TF_FIN = 1, PV_TF_SYN = 2, PV_TF_RST = 4 };
+// PV_TF_NODATA: a TCP packet reassembly ignores (no payload and no SYN/FIN/RST, or no valid TCP
+// header), emitted in the exact LRU mode for the cleanup that follows every TCP packet;
+// PV_TF_CLOSE: a close-only segment the host's LRU replay adds for a connection it closes in a
+// batch that holds none of its packets
+enum { PV_TF_FIN = 1, PV_TF_SYN = 2, PV_TF_RST = 4, PV_TF_NODATA = 0x40, PV_TF_CLOSE = 0x80 };
 static_assert(sizeof(PvTcpSeg) == 48, "three 16-B stores");
 
 // TcpReassemblyData + DnsStreamHandler's TcpFlowData of one connection, carried across batches
@@ -574,12 +578,15 @@ struct PvTcpParams {
     PV_G uint64_t *mq;            // 32-B DnsMsg items (same layout as the UDP work lists)
     uint32_t mq_cap;
     PV_G uint32_t *cnt;           // [0] messages [1] arena bytes [2] carry bytes [3] carried flows [4] frag nodes [5] flags
-    // tcp_packet_reassembly_cache_limit (PcapInputStream's LRU capacity): a dry run records the
-    // LRU events of every sorted segment (lru_ev: flags | dir << 8, second, latest TCP second
-    // + 1 before it) and leaves the flow table, the carried bytes and lt_carry as they were; the
-    // run after it closes each flow the host's LRU replay evicted (fclose at the flow's first
-    // sorted segment: record index after which it closes, that record's second and direction)
-    uint32_t dry;
+    // exact LRU mode (pv_set_tcp_exact_lru; tcp_packet_reassembly_cache_limit implies it): every
+    // TCP packet is a segment, a dry run records the LRU events of every sorted segment (lru_ev:
+    // flags | dir << 8, second, the LRU time of its last put: ConnectionData::endTime, 0 until
+    // the connection's second packet) and leaves the flow table, the carried bytes and lt_carry
+    // as they were; the host replays PcapInputStream's LRU list over them and the run after it
+    // closes each flow the replay closed (fclose per segment index, read at the flow's first
+    // sorted segment: record index after which it closes, that record's second and direction).
+    // Outside it the device times a connection out by itself (lt_before).
+    uint32_t dry, exact;
     PV_G uint32_t *lru_ev;
     const PV_G uint32_t *fclose;
 };
@@ -588,7 +595,6 @@ enum { PVT_NMSG = 0, PVT_ARENA, PVT_CARRY, PVT_NCARRY, PVT_NFRAG, PVT_FLAGS, PVT
 // the connection closed (FIN/RST) in it, closed by the 30 s timeout ahead of it
 enum { PVT_EV_NEW = 1, PVT_EV_PUT = 2, PVT_EV_CLOSE = 4, PVT_EV_TIMEOUT = 8 };
 #define PVT_FCLOSE_NONE 0xffffffffu
-#define PVT_FCLOSE_FIRST 0xfffffffeu // closed ahead of the flow's first segment of the batch
 enum { PVT_F_TABLE = 1, PVT_F_ARENA = 2, PVT_F_CARRY = 4, PVT_F_FRAGS = 8, PVT_F_MSGS = 16 };
 
 // Device record index of an ingest chunk (pv_index.hip)

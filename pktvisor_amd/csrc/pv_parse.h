@@ -690,7 +690,9 @@ PV_FN bool name_stats_fast(const A &R, uint64_t m, uint32_t len, uint32_t off, N
         }
         mm.k1 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
         mm.k2 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+#ifndef PV_NO_MM // tuning knob: no Murmur blocks (the qname CPC coupons are then wrong)
         if (16 * j + 16 <= n) mm.block();
+#endif
     }
     if (bad) return false;
     mm.n = n;

@@ -22,17 +22,19 @@
 //                       new carry arena
 // The messages then go through the DNS pass like UDP datagrams (pv_dns_tcp).
 //
-// tcp_packet_reassembly_cache_limit: a dry run of pv_tcp_flow records each segment's LRU events,
-// the host replays the LRU list over them in capture order and the real run closes the flows it
-// evicts (pv_host.cpp tcp_lru_replay).
-// Approximations: the LRU's 100-closures-per-packet limit and the closed-connection
-// purge (wall clock in PcapPlusPlus) are not modelled; a timed-out flow is closed lazily at its
-// next packet (data it flushes is ordered there); the LRU holds the DNS-port connections only;
-// the puts of data an eviction flushes are not replayed; no flush of open connections at the
-// end of a capture; the time-out test takes the latest TCP second seen before a packet, where
-// the reference tests the LRU tail against each TCP packet's own second after it
-// (PcapInputStream.cpp:449-459): the two agree while capture timestamps are monotonic and may
-// close a connection one packet earlier or later when they are not.
+// Exact LRU mode (pv_set_tcp_exact_lru, implied by tcp_packet_reassembly_cache_limit): every TCP
+// packet is a segment; a dry run of pv_tcp_flow records each segment's LRU events, the host
+// replays PcapInputStream's LRU list over them in capture order (puts with ConnectionData's
+// endTime, 0 until a connection's second packet; after every TCP packet at most 100 time-outs
+// from the tail; evictions past the limit) and the real run closes the flows it closed, with
+// close-only segments for flows that have no packet in the batch (pv_host.cpp tcp_lru_replay).
+// Default mode: a connection times out lazily at its next packet, once a TCP packet 30 s after
+// its last put's second came before it; the LRU holds the DNS-port connections only. The two
+// differ for a connection whose last put carried the zero endTime (a first packet with data: a
+// capture without the handshake), which the reference closes as soon as it reaches the LRU's
+// tail, and when more than 100 connections time out at one packet. Not modelled in either: the
+// closed-connection purge (wall clock in PcapPlusPlus), the puts of data that closing an evicted
+// connection flushes, the flush of open connections at the end of a capture.
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -61,10 +63,11 @@ __device__ __forceinline__ bool run_start(PV_CREF(PvTcpParams) T, uint32_t j)
 #define PV_RUN_NONE 0xffffffffu
 #define PV_RUN_NEW 0xfffffffeu
 
-// an entry whose connection closed (or timed out) PV_TCP_RECLAIM seconds ago
+// an entry whose connection closed (or timed out) PV_TCP_RECLAIM seconds ago, or one that never
+// started a connection (a run of ignored packets)
 __device__ __forceinline__ bool reclaimable(const PV_G PvTcpFlow &f, uint32_t now)
 {
-    if (!f.live) return false;
+    if (!f.live) return true;
     if (f.closed) return f.close_sec + PV_TCP_RECLAIM <= now;
     return f.lru_sec + PV_TCP_TIMEOUT + PV_TCP_RECLAIM <= now;
 }
@@ -78,7 +81,8 @@ struct Flow {
     uint32_t budget;          // bound on bytes this flow can deliver in this batch
     uint32_t fkey;
     uint32_t cur_idx, cur_dir, cur_sec, sub;
-    uint32_t ev; // PVT_EV_* of the packet being replayed (tcp_packet_reassembly_cache_limit dry run)
+    uint32_t ev;      // PVT_EV_* of the packet being replayed (exact LRU mode's dry run)
+    uint32_t put_sec; // LRU time of its last put
 };
 
 __device__ void emit_msg(PV_CREF(PvTcpParams) T, Flow &F, int s)
@@ -171,6 +175,7 @@ __device__ void deliver(PV_CREF(PvTcpParams) T, Flow &F, int s, const uint8_t *s
 {
     if (F.f.port) frame(T, F, s, src, n);
     F.f.lru_sec = F.cur_sec;
+    F.put_sec = F.f.end_sec;
     F.ev |= PVT_EV_PUT;
 }
 
@@ -260,6 +265,7 @@ __device__ void check_ooo(PV_CREF(PvTcpParams) T, Flow &F, int s, bool clean)
                 frame(T, F, s, (const uint8_t *)(uintptr_t)fr.src, fr.len);
             }
             F.f.lru_sec = F.cur_sec;
+            F.put_sec = F.f.end_sec;
             F.ev |= PVT_EV_PUT;
             found = true;
         }
@@ -310,7 +316,9 @@ __device__ void packet(PV_CREF(PvTcpParams) T, Flow &F, const PvTcpSeg &g)
     F.cur_dir = g.dirv6 & 3;
     F.cur_sec = g.sec;
     PvTcpFlow &f = F.f;
-    if (f.live && !f.closed) {
+    // Ignore_PacketWithNoData / no TCP layer, before the connection lookup; a close-only segment
+    if (g.flags & (PV_TF_NODATA | PV_TF_CLOSE)) return;
+    if (!T.exact && f.live && !f.closed) {
         // PcapInputStream's LRU cleanup after an earlier TCP packet at >= last put + 30 s
         const uint32_t lt = lt_before(T, g.idx);
         if (lt && lt - 1 >= f.lru_sec + PV_TCP_TIMEOUT) {
@@ -332,6 +340,7 @@ __device__ void packet(PV_CREF(PvTcpParams) T, Flow &F, const PvTcpSeg &g)
         f.end_sec = f.end_usec = 0;
         f.prev = -1;
         f.lru_sec = g.sec;
+        F.put_sec = g.sec;
         F.ev |= PVT_EV_NEW;
     } else if (g.sec > f.end_sec || (g.sec == f.end_sec && g.usec > f.end_usec)) {
         f.end_sec = g.sec;
@@ -450,6 +459,7 @@ extern "C" __global__ void pv_tcp_insert(const PvTcpParams *__restrict__ Tp)
     PV_CREF(PvTcpParams) T = *(const PV_C PvTcpParams *)Tp;
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= T.n_seg || T.run_flow[j] != PV_RUN_NEW) return;
+    if (T.seg[T.sval[j]].flags & PV_TF_CLOSE) { T.run_flow[j] = PV_RUN_NONE; return; } // its flow is gone
     const uint32_t fkey = (uint32_t)(T.skey[j] >> 32);
     const uint64_t tag = (1ull << 32) | fkey;
     const uint32_t mask = (1u << T.flow_cap_log2) - 1;
@@ -496,6 +506,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
     F.cur_sec = 0;
     F.sub = 0;
     F.ev = 0;
+    F.put_sec = 0;
     // bytes this flow can deliver in this batch: carried bytes, payloads, missing-data texts
     uint64_t budget = F.f.blob_len + 32ull * (F.f.nfrag[0] + F.f.nfrag[1]);
     for (uint32_t k = j; k < je; k++) budget += T.seg[T.sval[k]].plen + 32u;
@@ -522,13 +533,16 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
     }
     F.f.blob_len = 0;
     F.f.nfrag[0] = F.f.nfrag[1] = 0;
-    // the close the host's LRU replay decided (an overflow eviction after record fc_idx, possibly
-    // another flow's): closeConnection with that record's second and direction; its flushed
-    // messages rank behind the record's own (sub 3)
+    // the close the host's LRU replay decided (a time-out or an eviction after record fc_idx,
+    // usually another flow's packet): closeConnection with that record's second and direction;
+    // its flushed messages rank behind the record's own (sub 3)
     uint32_t fc_idx = PVT_FCLOSE_NONE, fc_sec = 0, fc_dir = 2;
-    if (T.fclose) { fc_idx = T.fclose[3 * j]; fc_sec = T.fclose[3 * j + 1]; fc_dir = T.fclose[3 * j + 2]; }
+    if (T.fclose) {
+        const uint32_t s0 = T.sval[j];
+        fc_idx = T.fclose[3 * s0]; fc_sec = T.fclose[3 * s0 + 1]; fc_dir = T.fclose[3 * s0 + 2];
+    }
     auto force_close = [&]() {
-        F.cur_idx = fc_idx == PVT_FCLOSE_FIRST ? T.seg[T.sval[j]].idx : fc_idx;
+        F.cur_idx = fc_idx;
         F.sub = 3;
         F.cur_sec = fc_sec;
         F.cur_dir = fc_dir;
@@ -536,14 +550,15 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
     };
     for (uint32_t k = j; k < je; k++) {
         const PvTcpSeg g = T.seg[T.sval[k]];
-        if (fc_idx != PVT_FCLOSE_NONE && (fc_idx == PVT_FCLOSE_FIRST || g.idx > fc_idx) && F.f.live && !F.f.closed)
+        if (fc_idx != PVT_FCLOSE_NONE && g.idx > fc_idx && F.f.live && !F.f.closed)
             force_close();
         F.ev = 0;
+        F.put_sec = 0;
         packet(T, F, g);
         if (T.lru_ev) {
             T.lru_ev[3 * k] = F.ev | (g.dirv6 & 3) << 8;
             T.lru_ev[3 * k + 1] = g.sec;
-            T.lru_ev[3 * k + 2] = lt_before(T, g.idx);
+            T.lru_ev[3 * k + 2] = F.put_sec;
         }
     }
     if (fc_idx != PVT_FCLOSE_NONE && F.f.live && !F.f.closed) force_close();

@@ -51,7 +51,7 @@ def gpu_main(pcap_path, out, host, periods, rate=100, filters=None, dns2_config=
     offs = [int(x) for x in idx.offsets] + [len(recs)]
     h = pa.PvHandlers(host_spec=host or None, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
                       max_records=max(1, hi - lo), device=dev.index, deep_sample_rate=rate, dns_filters=filters,
-                      dns2_config=dns2_config)
+                      dns2_config=dns2_config, table_log2=int(os.environ.get("PV_TEST_TABLE_LOG2", "0")))
     try:
         h.set_global_base(lo)
         sec, frac = struct.unpack_from("<II", recs, offs[0])

@@ -5,6 +5,8 @@ The reference's own TCP fixtures are pinned in test_gpu_kat.py / test_gpu_parity
 cases use synth.tcp_dns_pcap: segments cut at random byte boundaries, out-of-order and
 retransmitted segments, lost SYNs, invalid framing, FIN / RST closes, port reuse, idle
 connections past the 30 s timeout, messages carried across batch edges."""
+import os
+
 import numpy as np
 import pytest
 
@@ -84,4 +86,66 @@ def test_tcp_across_batches(oracle, periods):
     finally:
         h.close()
     ref = oracle.run_bytes(pcap, host_spec=HOST, num_periods=periods, window=periods)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_tcp_exact_lru_parity(oracle, tmp_path, seed):
+    """the exact LRU mode (pv_set_tcp_exact_lru): PcapInputStream's LRU list of every TCP
+    connection replayed per packet; the same windows as the restatement"""
+    pcap = synth.tcp_dns_pcap(seed)
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    gpu = pa.pktvisor_reader(str(p), host_spec=HOST, periods=5, tcp_exact_lru=True)
+    ref = oracle.run_bytes(pcap, host_spec=HOST, num_periods=5, window=5)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_tcp_exact_lru_without_handshakes(oracle, tmp_path):
+    """The reference's TCP fixture read through a BPF program that drops the small packets (every
+    handshake, ACK and FIN segment; VERDICT r4: the default mode reported 1 413 more TCP
+    responses here). Each connection's first packet then carries data, so its LRU entry holds
+    the zero endTime and PcapInputStream closes it as soon as it reaches the list's tail; its
+    response is a packet of a closed flow. The exact LRU mode reproduces that."""
+    from tests import bpf_progs
+    pcap = open(os.path.join(os.path.dirname(__file__), "golden", "dns_udp_tcp_random.pcap"), "rb").read()
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    insns = bpf_progs.ARITH
+    gpu = pa.pktvisor_reader(str(p), host_spec="192.168.0.0/24", periods=1, bpf=insns, tcp_exact_lru=True)
+    kept = pcap[:24] + bpf_progs.filter_records(pcap[24:], insns)
+    ref = oracle.run_bytes(kept, host_spec="192.168.0.0/24", num_periods=1, window=1)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("lost_syn", [False, True])
+def test_tcp_exact_lru_across_batches(oracle, lost_syn):
+    """the exact mode over small batches: the LRU list carried on the host, connections closed in
+    a batch that holds none of their packets (close-only segments)"""
+    pcap = synth.tcp_dns_pcap(7, flows=80, duration_s=100, pauses=6)
+    if lost_syn:
+        # drop every SYN: first packets carry data (zero endTime entries)
+        keep = []
+        for _, _, r in synth.records_of(pcap):
+            f = r[16:]
+            if len(f) > 47 and f[12:14] == b"\x08\x00" and f[23] == 6 and f[14 + (f[14] & 15) * 4 + 13] & 2:
+                continue
+            keep.append(r)
+        pcap = pa.pcap_file_bytes(b"".join(keep))
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    offs = list(idx.offsets) + [len(recs)]
+    rng = np.random.default_rng(3)
+    h = pa.PvHandlers(host_spec=HOST, num_periods=1, max_records=512, tcp_exact_lru=True)
+    try:
+        i = 0
+        while i < idx.n:
+            j = min(idx.n, i + int(rng.integers(1, 200)))
+            h.process_host(recs[offs[i]:offs[j]])
+            i = j
+        h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+        gpu = {"1m": h.window_json(0)}
+    finally:
+        h.close()
+    ref = oracle.run_bytes(pcap, host_spec=HOST, num_periods=1, window=1)
     assert diff(gpu, ref) is None, diff(gpu, ref)

@@ -104,3 +104,27 @@ def test_dirty_writeback_after_purge():
     assert len(common) >= 20
     for n in common:
         assert e2[n] - e1[n] == heavy2[n], (n, e1[n], e2[n], heavy2[n])
+
+
+def test_sharded_flood_owner_merge_purges(tmp_path, monkeypatch):
+    """Three ranks each see a third of the flood in a 4096-entry table; the top-N owner merge
+    receives more distinct names than a region holds, so full regions purge (the frequent-items
+    merge's purge) and take the rest again instead of failing; the heavy names stay on top with
+    estimates no lower than their true counts"""
+    import json
+    from tests.dist_launch import run_ranks
+    pcap, heavy, total = synth.qname_flood_pcap(7, flood=60000)
+    p = tmp_path / "in.pcap"
+    p.write_bytes(pcap)
+    out = tmp_path / "merged.json"
+    monkeypatch.setenv("PV_TEST_TABLE_LOG2", "12")
+    run_ranks(3, ["gpu", str(p), str(out), "10.0.0.0/8", "1"])
+    dns = json.load(open(out))["1m"]["dns"]
+    top3 = dns["top_qname3"]
+    assert [e["name"] for e in top3] == sorted(heavy, key=lambda n: -heavy[n])[:10]
+    bound = 3 * (4 * total // 4096 + 2) + 64
+    for e in top3:
+        t = heavy[e["name"]]
+        assert t <= e["estimate"] <= t + bound, (e, t, bound)
+    assert dns["top_qname2"][0] == {"name": ".victim.example", "estimate": total}
+    assert dns["wire_packets"]["total"] == total

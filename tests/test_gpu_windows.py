@@ -131,3 +131,25 @@ def test_sharded_deep_sampling(oracle, tmp_path, rate, f):
     ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5, deep_sample_rate=rate,
                            **(oracle_kw(f) if f else {}))
     assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("budget_mb", [None, "1"], ids=["grow", "drain"])
+def test_value_buffer_small_batches(oracle, tmp_path, monkeypatch, budget_mb):
+    """Many small batches of query/response pairs across DNS period shifts: the transaction value
+    buffer keeps two values of room per record of a batch (growing in HBM, or draining to the host
+    when PV_XV_BUDGET_MB caps it) and the shift thresholds select over it; windows equal the
+    oracle's (a response-heavy batch must never run past the buffer)"""
+    if budget_mb:
+        monkeypatch.setenv("PV_XV_BUDGET_MB", budget_mb)
+    pcap = synth.pcap_bytes(4, 40000, ts_step_us=5000)
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=5, max_records=1024)
+    try:
+        h.process_host(recs)
+        h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+        got = {"5m": h.window_json(5, merged=True)}
+    finally:
+        h.close()
+    ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5)
+    assert diff(got, ref) is None, diff(got, ref)
