@@ -36,6 +36,7 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <queue>
 #include <set>
 #include <tuple>
 #include <vector>
@@ -144,9 +145,6 @@ extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg_tc(const PvParams *P);
-extern "C" __global__ void pv_net_kernel_reg_sb(const PvParams *P);
-extern "C" __global__ void pv_net_kernel_reg_nt(const PvParams *P);
-extern "C" __global__ void pv_net_kernel_reg_sbnt(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
 extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
@@ -189,6 +187,10 @@ extern "C" __global__ void pv_ix_write(const PvIxParams *X);
 extern "C" __global__ void pv_ix_secs(const PvIxParams *X, uint32_t cap);
 extern "C" __global__ void pv_ix_cut(const PvIxParams *X);
 extern "C" __global__ void pv_topn_retry(const PvParams *P, const PvOvf *src, uint32_t n);
+extern "C" __global__ void pv_xname_len(const uint8_t *arena, uint64_t arena_cap, const uint32_t *tb, const uint32_t *aux, uint32_t n,
+                                        uint32_t *len);
+extern "C" __global__ void pv_xname_copy(const uint8_t *arena, uint64_t arena_cap, const uint32_t *tb, const uint32_t *aux,
+                                         const uint32_t *len, const uint64_t *off, uint32_t n, uint8_t *out);
 extern "C" __global__ void pv_dns_tcp_filter(const PvParams *P);
 extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_t *theta_out);
 extern "C" __global__ void pv_topn_compact(const PvParams *P, uint32_t tb, uint8_t *tmp, unsigned long long *tmp_top);
@@ -3857,11 +3859,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
     const bool tc = (c->net_groups & PV_NET_TOP_IPS) && c->reg_waves != 8;
-    // store-mode A/B of the top-IPs pass: PV_NET_KERNEL=sb (LDS-staged IP log) | nt (non-temporal) | sbnt
-    const int smode = !(lean && tc && regw && !ring && force) ? 0
-                      : !strcmp(force, "sb") ? 1 : !strcmp(force, "nt") ? 2 : !strcmp(force, "sbnt") ? 3 : 0;
-    c->net_kernel = smode ? (smode == 1 ? "pv_net_kernel_reg_sb" : smode == 2 ? "pv_net_kernel_reg_nt" : "pv_net_kernel_reg_sbnt")
-                  : general ? "pv_net_kernel"
+    c->net_kernel = general ? "pv_net_kernel"
                             : (lean ? (ring ? "pv_net_kernel_fast"
                                             : (!regw ? "pv_net_kernel_ring"
                                                      : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : (tc ? "pv_net_kernel_reg_tc" : "pv_net_kernel_reg"))))
@@ -3880,9 +3878,6 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         hipLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(ring_threads), 0, st, (const PvParams *)c->d_params);
     }
     else if (lean && c->reg_waves == 8) hipLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, (const PvParams *)c->d_params);
-    else if (lean && tc && smode)
-        hipLaunchKernelGGL(smode == 1 ? pv_net_kernel_reg_sb : smode == 2 ? pv_net_kernel_reg_nt : pv_net_kernel_reg_sbnt, dim3(reg_grid),
-                           dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean && tc) hipLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
     else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -6131,18 +6126,53 @@ void x_name_text(uint32_t metric, const uint8_t *rec, uint32_t len, std::string 
     else if (metric == TM_ECS && len == 17) out = inet_ntop(rec[0] == 1 ? AF_INET : AF_INET6, rec + 1, b, sizeof b) ? b : "";
     else out.assign((const char *)rec, len);
 }
-// a name record of table tb at aux (0: none): its text, or false
-bool x_read_name(pv_ctx *c, uint32_t tb, uint64_t key, uint32_t aux, std::string &out)
+// the texts of many name records at once (pv_xname_len / pv_xname_copy): ok[i] false where aux[i]
+// is 0 (no record)
+int x_read_names(pv_ctx *c, const std::vector<uint32_t> &tb, const std::vector<uint32_t> &aux, const std::vector<uint64_t> &key,
+                 std::vector<std::string> &out, std::vector<bool> &ok)
 {
-    if (!aux) return false;
-    uint8_t l2[2];
-    const uint8_t *base = c->d_arena + (uint64_t)tb * c->arena_cap + (aux - 1);
-    if (!hip_ok(hipMemcpy(l2, base, 2, hipMemcpyDeviceToHost))) return false;
-    const uint32_t len = l2[0] | (l2[1] << 8);
-    std::vector<uint8_t> b(len);
-    if (len && !hip_ok(hipMemcpy(b.data(), base + 2, len, hipMemcpyDeviceToHost))) return false;
-    x_name_text(PV_KEY_METRIC(key), b.data(), len, out);
-    return true;
+    const size_t n = tb.size();
+    out.assign(n, std::string());
+    ok.assign(n, false);
+    if (!n) return 0;
+    hipError_t e;
+    uint32_t *d_tb = nullptr, *d_aux = nullptr, *d_len = nullptr;
+    uint64_t *d_off = nullptr;
+    uint8_t *d_out = nullptr;
+    struct Free { void *p[5]; ~Free() { for (void *q : p) if (q) hipFree(q); } } fr{{nullptr, nullptr, nullptr, nullptr, nullptr}};
+    if (!hip_ok(e = hipMalloc(&d_tb, n * 4)) || !hip_ok(e = hipMalloc(&d_aux, n * 4)) || !hip_ok(e = hipMalloc(&d_len, n * 4)) ||
+        !hip_ok(e = hipMalloc(&d_off, n * 8)))
+        return c->hipfail(e, "name gather");
+    fr.p[0] = d_tb; fr.p[1] = d_aux; fr.p[2] = d_len; fr.p[3] = d_off;
+    std::vector<uint32_t> len(n);
+    const uint32_t g = (uint32_t)((n + 255) / 256);
+    if (!hip_ok(e = hipMemcpyAsync(d_tb, tb.data(), n * 4, hipMemcpyHostToDevice, c->stream)) ||
+        !hip_ok(e = hipMemcpyAsync(d_aux, aux.data(), n * 4, hipMemcpyHostToDevice, c->stream)))
+        return c->hipfail(e, "name gather");
+    hipLaunchKernelGGL(pv_xname_len, dim3(g), dim3(256), 0, c->stream, c->d_arena, c->arena_cap, d_tb, d_aux, (uint32_t)n, d_len);
+    if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipMemcpyAsync(len.data(), d_len, n * 4, hipMemcpyDeviceToHost, c->stream)) ||
+        !hip_ok(e = hipStreamSynchronize(c->stream)))
+        return c->hipfail(e, "name gather");
+    std::vector<uint64_t> off(n);
+    uint64_t tot = 0;
+    for (size_t i = 0; i < n; i++) { off[i] = tot; tot += len[i] == 0xffffffffu ? 0 : len[i]; }
+    std::vector<uint8_t> bytes(tot);
+    if (tot) {
+        if (!hip_ok(e = hipMalloc(&d_out, tot))) return c->hipfail(e, "name gather");
+        fr.p[4] = d_out;
+        if (!hip_ok(e = hipMemcpyAsync(d_off, off.data(), n * 8, hipMemcpyHostToDevice, c->stream))) return c->hipfail(e, "name gather");
+        hipLaunchKernelGGL(pv_xname_copy, dim3(g), dim3(256), 0, c->stream, c->d_arena, c->arena_cap, d_tb, d_aux, d_len, d_off,
+                           (uint32_t)n, d_out);
+        if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipMemcpyAsync(bytes.data(), d_out, tot, hipMemcpyDeviceToHost, c->stream)) ||
+            !hip_ok(e = hipStreamSynchronize(c->stream)))
+            return c->hipfail(e, "name gather");
+    }
+    for (size_t i = 0; i < n; i++) {
+        if (len[i] == 0xffffffffu) continue;
+        x_name_text(PV_KEY_METRIC(key[i]), bytes.data() + off[i], len[i], out[i]);
+        ok[i] = true;
+    }
+    return 0;
 }
 void put_u32(std::vector<uint8_t> &o, uint32_t v) { const size_t p = o.size(); o.resize(p + 4); memcpy(&o[p], &v, 4); }
 void put_u64(std::vector<uint8_t> &o, uint64_t v) { const size_t p = o.size(); o.resize(p + 8); memcpy(&o[p], &v, 8); }
@@ -6202,53 +6232,120 @@ int pv_topn_x_candidates(pv_ctx *c, uint8_t **blob, size_t *bytes)
             return nullptr;
         return &x;
     };
+    // Per part: every live slot's entries of this rank's regions, sorted by key once; then per key
+    // its estimate in each slot set (single slots and the merged runs) and, per (set, metric), the
+    // topn_count leading entries with the ties of the last: a first walk finds each list's
+    // threshold (a bounded heap of estimates), a second collects the entries at or above it.
+    struct XE { uint64_t key, est; uint32_t tb, aux; uint32_t slot; };
+    struct XOut { uint32_t set; uint64_t key, est; uint32_t tb, aux; };
+    std::vector<XOut> out;
     for (int part = PART_NET; part <= PART_DNS; part++) {
         std::vector<uint32_t> sets;
         x_slot_sets(c, part, sets);
-        for (uint32_t set : sets) {
-            // key -> (estimate summed over the set's tables, a table and aux holding its name)
-            std::unordered_map<uint64_t, std::tuple<uint64_t, uint32_t, uint32_t>> sum;
-            for (uint32_t s = 0; s < PV_SLOTS; s++) {
-                if (!((set >> s) & 1)) continue;
-                const uint32_t tb = s + (part == PART_DNS ? PV_SLOTS : 0);
-                const Slice *x = slice(tb);
-                if (!x) return c->hipfail(e, "read top-N regions");
-                const std::vector<uint64_t> &roff = c->roff[tb];
-                for (size_t i = 0; i < n; i++) {
-                    if (!x->keys[i]) continue;
-                    auto &v = sum[x->keys[i]];
-                    std::get<0>(v) += x->cnt[i] + (roff.empty() ? 0 : roff[lo + (i >> rsl)]);
-                    if (!std::get<2>(v) && x->aux[i]) { std::get<1>(v) = tb; std::get<2>(v) = x->aux[i]; }
+        if (sets.empty()) continue;
+        const Window &w = part == PART_NET ? c->net : c->dns;
+        std::vector<XE> ents;
+        for (uint32_t s : w.slots) {
+            const uint32_t tb = s + (part == PART_DNS ? PV_SLOTS : 0);
+            const Slice *x = slice(tb);
+            if (!x) return c->hipfail(e, "read top-N regions");
+            const std::vector<uint64_t> &roff = c->roff[tb];
+            for (size_t i = 0; i < n; i++)
+                if (x->keys[i])
+                    ents.push_back(XE{x->keys[i], x->cnt[i] + (roff.empty() ? 0 : roff[lo + (i >> rsl)]), tb, x->aux[i], s});
+        }
+        std::sort(ents.begin(), ents.end(), [](const XE &p1, const XE &p2) { return p1.key < p2.key; });
+        const size_t NZ = sets.size();
+        // per key group [g0, g1): the estimate in set z, and whether the set holds the key
+        auto group_est = [&](size_t g0, size_t g1, size_t z, uint64_t &est) {
+            bool in = false;
+            est = 0;
+            for (size_t j = g0; j < g1; j++)
+                if ((sets[z] >> ents[j].slot) & 1) { est += ents[j].est; in = true; }
+            return in;
+        };
+        // walk 1: thresholds (a min-heap of the K largest estimates per (set, metric))
+        std::map<std::pair<uint32_t, uint32_t>, std::priority_queue<uint64_t, std::vector<uint64_t>, std::greater<uint64_t>>> heaps;
+        for (size_t g0 = 0, g1; g0 < ents.size(); g0 = g1) {
+            g1 = g0 + 1;
+            while (g1 < ents.size() && ents[g1].key == ents[g0].key) g1++;
+            const uint32_t hm = host_metric(c, ents[g0].key);
+            for (size_t z = 0; z < NZ; z++) {
+                uint64_t est;
+                if (!group_est(g0, g1, z, est)) continue;
+                auto &h = heaps[{(uint32_t)z, hm}];
+                if (h.size() < K) h.push(est);
+                else if (est > h.top()) { h.pop(); h.push(est); }
+            }
+        }
+        std::map<std::pair<uint32_t, uint32_t>, uint64_t> thr;
+        for (auto &kv : heaps) thr[kv.first] = kv.second.size() < K ? 0 : kv.second.top();
+        // walk 2: entries at or above the threshold (est, key, name table, name aux)
+        std::map<std::pair<uint32_t, uint32_t>, std::vector<std::tuple<uint64_t, uint64_t, uint32_t, uint32_t>>> got;
+        for (size_t g0 = 0, g1; g0 < ents.size(); g0 = g1) {
+            g1 = g0 + 1;
+            while (g1 < ents.size() && ents[g1].key == ents[g0].key) g1++;
+            const uint32_t hm = host_metric(c, ents[g0].key);
+            for (size_t z = 0; z < NZ; z++) {
+                uint64_t est;
+                if (!group_est(g0, g1, z, est)) continue;
+                if (est < thr[{(uint32_t)z, hm}]) continue;
+                uint32_t ntb = 0, naux = 0;
+                for (size_t j = g0; j < g1 && !naux; j++)
+                    if (((sets[z] >> ents[j].slot) & 1) && ents[j].aux) { ntb = ents[j].tb; naux = ents[j].aux; }
+                auto &v = got[{(uint32_t)z, hm}];
+                v.emplace_back(est, ents[g0].key, ntb, naux);
+                if (v.size() > 4 * (PV_X_TIES + K)) {
+                    // a flat list: keep the leading ones by (estimate desc, key asc)
+                    auto cmp = [](const auto &a1, const auto &b1) {
+                        return std::get<0>(a1) != std::get<0>(b1) ? std::get<0>(a1) > std::get<0>(b1) : std::get<1>(a1) < std::get<1>(b1);
+                    };
+                    std::nth_element(v.begin(), v.begin() + (PV_X_TIES + K), v.end(), cmp);
+                    v.resize(PV_X_TIES + K);
                 }
             }
-            std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> by; // host metric -> (estimate, key)
-            for (auto &kv : sum) by[host_metric(c, kv.first)].push_back({std::get<0>(kv.second), kv.first});
-            for (auto &mv : by) {
-                auto &v = mv.second;
-                std::sort(v.begin(), v.end(), [](const auto &a, const auto &b2) { return a.first != b2.first ? a.first > b2.first : a.second < b2.second; });
+        }
+        for (size_t z = 0; z < NZ; z++) {
+            for (auto it = got.lower_bound({(uint32_t)z, 0u}); it != got.end() && it->first.first == z; ++it) {
+                auto &v = it->second;
+                std::sort(v.begin(), v.end(), [](const auto &a1, const auto &b1) {
+                    return std::get<0>(a1) != std::get<0>(b1) ? std::get<0>(a1) > std::get<0>(b1) : std::get<1>(a1) < std::get<1>(b1);
+                });
                 // the topn_count leading entries and every entry tied with the last of them (the lists
                 // order ties by name, which only the whole tied group decides; at most PV_X_TIES)
                 size_t m = std::min(K, v.size());
-                while (m < v.size() && m < PV_X_TIES && v[m].first == v[m - 1].first) m++;
-                for (size_t k = 0; k < m; k++) {
-                    const uint64_t key = v[k].second;
-                    const auto &sv = sum[key];
-                    put_u32(o, set);
-                    put_u64(o, key);
-                    put_u64(o, v[k].first);
-                    std::string nm;
-                    if (PV_KEY_METRIC(key) == TM_IPV4) {
-                        const uint32_t ip = (uint32_t)key;
-                        char bb[20];
-                        snprintf(bb, sizeof bb, "%u.%u.%u.%u", ip & 0xff, (ip >> 8) & 0xff, (ip >> 16) & 0xff, ip >> 24);
-                        nm = bb;
-                        put_name(o, &nm);
-                    } else if (x_read_name(c, std::get<1>(sv), key, std::get<2>(sv), nm)) {
-                        put_name(o, &nm);
-                    } else {
-                        put_name(o, nullptr);
-                    }
-                }
+                while (m < v.size() && m < PV_X_TIES && std::get<0>(v[m]) == std::get<0>(v[m - 1])) m++;
+                for (size_t k = 0; k < m; k++) out.push_back(XOut{sets[z], std::get<1>(v[k]), std::get<0>(v[k]), std::get<2>(v[k]), std::get<3>(v[k])});
+            }
+        }
+    }
+    // the names: IPv4 from the key, the others gathered from the arena in one pass
+    {
+        std::vector<uint32_t> gtb, gaux;
+        std::vector<uint64_t> gkey;
+        std::vector<size_t> at;
+        for (size_t i = 0; i < out.size(); i++)
+            if (PV_KEY_METRIC(out[i].key) != TM_IPV4 && out[i].aux) {
+                gtb.push_back(out[i].tb); gaux.push_back(out[i].aux); gkey.push_back(out[i].key); at.push_back(i);
+            }
+        std::vector<std::string> txt;
+        std::vector<bool> okv;
+        if (int rc = x_read_names(c, gtb, gaux, gkey, txt, okv)) return rc;
+        std::vector<const std::string *> nmp(out.size(), nullptr);
+        for (size_t j = 0; j < at.size(); j++) if (okv[j]) nmp[at[j]] = &txt[j];
+        for (size_t i = 0; i < out.size(); i++) {
+            const uint64_t key = out[i].key;
+            put_u32(o, out[i].set);
+            put_u64(o, key);
+            put_u64(o, out[i].est);
+            if (PV_KEY_METRIC(key) == TM_IPV4) {
+                const uint32_t ip = (uint32_t)key;
+                char bb[20];
+                snprintf(bb, sizeof bb, "%u.%u.%u.%u", ip & 0xff, (ip >> 8) & 0xff, (ip >> 16) & 0xff, ip >> 24);
+                const std::string nm = bb;
+                put_name(o, &nm);
+            } else {
+                put_name(o, nmp[i]);
             }
         }
     }
@@ -6345,16 +6442,20 @@ int pv_topn_x_names(pv_ctx *c, const uint8_t *const *cands, const size_t *sizes,
         }
         hipFree(d_k); hipFree(d_t); hipFree(d_a);
         if (!ok) return c->hipfail(e, "name lookup");
+        std::vector<uint32_t> gtb, gaux;
+        std::vector<uint64_t> gkey;
+        for (size_t i = 0; i < want.size(); i++) { gtb.push_back(want[i].tb); gaux.push_back(aux[i]); gkey.push_back(want[i].key); }
+        std::vector<std::string> txt;
+        std::vector<bool> okv;
+        if (int rc = x_read_names(c, gtb, gaux, gkey, txt, okv)) return rc;
         std::set<std::pair<uint32_t, uint64_t>> done;
         for (size_t i = 0; i < want.size(); i++) {
             const uint32_t set = (uint32_t)std::stoul(want[i].name);
-            if (done.count({set, want[i].key})) continue;
-            std::string nm;
-            if (!x_read_name(c, want[i].tb, want[i].key, aux[i], nm)) continue;
+            if (done.count({set, want[i].key}) || !okv[i]) continue;
             done.insert({set, want[i].key});
             put_u32(o, set);
             put_u64(o, want[i].key);
-            put_name(o, &nm);
+            put_name(o, &txt[i]);
         }
     }
     *blob = (uint8_t *)malloc(std::max<size_t>(o.size(), 1));

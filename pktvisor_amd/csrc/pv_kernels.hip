@@ -2358,18 +2358,11 @@ __device__ __forceinline__ void win_words(const uint4 (&W)[5], uint32_t sh, RecW
 // them as younger ops instead of waiting for them: a store takes microseconds to complete under
 // the read stream, and a wait that covers the previous tile's stores (as the branchy form's
 // does) stalls every tile on them (tools/ring_probe.hip: 138 -> 177 us on C2 with a 4-B store).
-// SM (store mode, TC only): 0 the IP-log words and direction word stored per tile; bit 0: staged in
-// LDS and flushed every 8 tiles (each wave then walks a contiguous block of its range's tiles, so
-// a flush is two 16-B stores a lane and one direction store), so a wave's load waits meet a store
-// once per 8 tiles instead of every tile; bit 1: non-temporal stores.
-template <uint32_t NW, bool TC = false, uint32_t SM = 0>
+template <uint32_t NW, bool TC = false>
 __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     __shared__ NetRegState S;
-    constexpr bool SB = TC && (SM & 1);
-    __shared__ uint4 sbq[SB ? NW * 128 : 1];    // per wave: 8 tiles x 64 IP-log words
-    __shared__ uint64_t sbdir[SB ? NW * 8 : 1]; // per wave: 8 direction words
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x == 0) { S.nd = 0; S.nx = 0; }
@@ -2400,14 +2393,9 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
     const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
     const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
-    // tiles of this wave: wave, wave + NW, ... (SB: a contiguous block of ceil(tiles / NW))
-    const uint64_t nrt = wend > wbeg ? wend - wbeg : 0, per = (nrt + NW - 1) / NW, first = SB ? wave * per : wave;
-    const uint32_t ntl = SB ? (first < nrt ? (uint32_t)min<uint64_t>(per, nrt - first) : 0u)
-                            : (wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u);
+    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u;
     any |= ntl != 0;
-    auto tile_of = [&](uint32_t k) -> uint64_t {
-        return SB ? wbeg + first + min(k, ntl - 1) : wbeg + wave + (uint64_t)NW * min(k, ntl - 1);
-    };
+    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
     auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
     // one tile from its windows W (off: this lane's record start)
     auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
@@ -2508,41 +2496,11 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                 const bool v4 = ek && ((ek >> 32) & ~1ull) == (P.ip_base >> 32);
                 const uint64_t xm = __ballot(active && ek && !v4);
                 const uint64_t dbit = __ballot(v4 && ((ek >> 32) & 1));
-                if (SB) {
-                    // staged; the wave flushes 8 tiles (or its last ones) with coalesced stores
-                    const uint32_t kk = k & 7;
-                    reinterpret_cast<uint32_t *>(sbq)[wave * 512 + kk * 64 + lane] = active && v4 ? (uint32_t)ek : 0u;
-                    if (lane == 0) sbdir[wave * 8 + kk] = dbit;
-                    if (kk == 7 || k + 1 == ntl) {
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        const uint32_t m = kk + 1;
-                        const uint64_t t0 = t - kk;
-                        PV_G uint4 *dst = reinterpret_cast<PV_G uint4 *>(P.iplog32 + t0 * 64);
-                        for (uint32_t j = lane; j < m * 16; j += 64) {
-                            const uint4 q = sbq[wave * 128 + j];
-                            if (SM & 2) {
-                                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                                const u32x4 v = {q.x, q.y, q.z, q.w};
-                                __builtin_nontemporal_store(v, reinterpret_cast<PV_G u32x4 *>(dst + j));
-                            } else {
-                                dst[j] = q;
-                            }
-                        }
-                        if (lane < m) P.ipdir[t0 + lane] = sbdir[wave * 8 + lane];
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                } else if (TC) {
+                if (TC) {
                     // every lane (the log has 64 words of slack past the batch) and every lane
                     // the same direction word: two unconditional store instructions
-                    if (SM & 2) {
-                        __builtin_nontemporal_store(active && v4 ? (uint32_t)ek : 0u, P.iplog32 + i);
-                        __builtin_nontemporal_store(dbit, P.ipdir + t);
-                    } else {
-                        P.iplog32[i] = active && v4 ? (uint32_t)ek : 0u;
-                        P.ipdir[t] = dbit;
-                    }
+                    P.iplog32[i] = active && v4 ? (uint32_t)ek : 0u;
+                    P.ipdir[t] = dbit;
                 } else {
                     if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
                     if (lane == 0) P.ipdir[t] = dbit;
@@ -3019,10 +2977,6 @@ extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg<4>(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_tc(const PvParams *__restrict__ Pp) { net_fast_reg<4, true>(Pp); }
-// store-mode A/B builds of the top-IPs pass (PV_NET_KERNEL=sb|nt|sbnt)
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_sb(const PvParams *__restrict__ Pp) { net_fast_reg<4, true, 1>(Pp); }
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_nt(const PvParams *__restrict__ Pp) { net_fast_reg<4, true, 2>(Pp); }
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_sbnt(const PvParams *__restrict__ Pp) { net_fast_reg<4, true, 3>(Pp); }
 extern "C" __global__ void __launch_bounds__(64 * PV_RING_NW) pv_net_kernel_ring(const PvParams *__restrict__ Pp) { net_ring(Pp); }
 // eight waves in the one workgroup of a CU: two per SIMD to hide instruction latency, one record stream per CU
 extern "C" __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg8(const PvParams *__restrict__ Pp) { net_fast_reg<8>(Pp); }
@@ -4181,6 +4135,28 @@ extern "C" __global__ void __launch_bounds__(1024) pv_topn_xruns(uint32_t reg_lo
 
 // Finalize support: the aux word (name record) of each listed (table, key) in this rank's
 // tables, 0 when absent or unnamed
+// Name records of table entries for the multi-GPU read view (pv_topn_x_candidates / _names), in
+// two launches: each record's length (its 2-byte header; ~0 for none), then, at the host's prefix
+// offsets, its bytes, so the host reads every name with two copies instead of two per name.
+extern "C" __global__ void pv_xname_len(const uint8_t *__restrict__ arena, uint64_t arena_cap, const uint32_t *__restrict__ tb,
+                                        const uint32_t *__restrict__ aux, uint32_t n, uint32_t *__restrict__ len)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    if (!aux[j]) { len[j] = 0xffffffffu; return; }
+    const uint8_t *b = arena + (uint64_t)tb[j] * arena_cap + (aux[j] - 1);
+    len[j] = (uint32_t)b[0] | ((uint32_t)b[1] << 8);
+}
+extern "C" __global__ void pv_xname_copy(const uint8_t *__restrict__ arena, uint64_t arena_cap, const uint32_t *__restrict__ tb,
+                                         const uint32_t *__restrict__ aux, const uint32_t *__restrict__ len,
+                                         const uint64_t *__restrict__ off, uint32_t n, uint8_t *__restrict__ out)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n || len[j] == 0xffffffffu) return;
+    const uint8_t *b = arena + (uint64_t)tb[j] * arena_cap + (aux[j] - 1) + 2;
+    for (uint32_t k = 0; k < len[j]; k++) out[off[j] + k] = b[k];
+}
+
 extern "C" __global__ void pv_topn_xlookup(const PvParams *__restrict__ Pp, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ tbs,
                                            uint32_t n, uint32_t *__restrict__ aux)
 {

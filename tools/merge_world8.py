@@ -85,13 +85,26 @@ def rank_main(args):
         region_bytes = sum(x.numel() * x.element_size() for x in sums + mins)
         dist.barrier()
         t2 = time.perf_counter()
-        pvdist.merge_window(h, dev, finalize=False)
+        # merge_window(finalize=False), step by step
+        part = {}
+
+        def step(name, f):
+            a = time.perf_counter()
+            f()
+            h.synchronize()
+            part[name] = round((time.perf_counter() - a) * 1e3, 1)
         h.synchronize()
+        step("check_aligned", lambda: pvdist.check_aligned(h))
+        step("edges", lambda: pvdist.merge_edges(h))
+        step("slow", lambda: pvdist.merge_slow(h))
+        step("buckets", lambda: pvdist.reduce_handlers(h, dev))
+        step("topn_owner", lambda: pvdist.merge_topn(h))
         t3 = time.perf_counter()
         state = dict(sent)
         dist.barrier()
         t4 = time.perf_counter()
-        pvdist.finalize_window(h)
+        step("finalize_topn", lambda: pvdist.finalize_topn(h))
+        step("finalize_values", lambda: pvdist.merge_values(h))
         t5 = time.perf_counter()
         fin = {k: sent[k] - state[k] for k in sent}
         events = h.window_json(5, merged=True)["packets"]["events"]
@@ -107,7 +120,7 @@ def rank_main(args):
                 "state_merge_bytes_per_rank_max": {"gathered": int(v[3]), "allreduced": int(v[4]),
                                                    "bucket_regions": int(region_bytes)},
                 "finalize_bytes_per_rank_max": {"gathered": int(v[5]), "allreduced": int(v[6])},
-                "window_events_5m": events}), flush=True)
+                "rank0_steps_ms": part, "window_events_5m": events}), flush=True)
     finally:
         h.close()
         dist.destroy_process_group()
