@@ -7203,13 +7203,31 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
     std::vector<EdgeView> v(nranks);
     for (uint32_t j = 0; j <= me; j++)
         if (!edge_parse(bufs[j], sizes[j], v[j])) return c->fail(PV_EINVAL, "malformed shard-edge buffer of rank %u", j);
-    // queries open at the start of shard me, as the ranks before it leave them
-    std::unordered_map<uint64_t, PvXEvent> M;
+    // queries open at the start of shard me, as the ranks before it leave them. A shift of shard j
+    // purges every query with sec + ttl <= its second, so shard j purges the queries at or below
+    // (its last shift - ttl): taken from a min-heap by second (entries a later query of the key or an
+    // answer replaced are skipped by their sequence number), not by a walk over all of them per shard.
+    std::unordered_map<uint64_t, std::pair<PvXEvent, uint64_t>> M; // key -> (query, sequence)
+    using HE = std::tuple<int64_t, uint64_t, uint64_t>;              // second, sequence, key
+    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> H;
+    uint64_t seqn = 0;
     for (uint32_t j = 0; j < me; j++) {
         for (auto &o : v[j].orph) M.erase(o.key); // answered (or found purged) in shard j
-        for (auto it = M.begin(); it != M.end();)
-            it = purge_shift(v[j].shifts, c->ttl_s, it->second.sec) >= 0 ? M.erase(it) : std::next(it);
-        for (auto &q : v[j].open) M[q.key] = q;
+        if (!v[j].shifts.empty()) {
+            int64_t last = v[j].shifts[0].first;
+            for (auto &sh : v[j].shifts) last = std::max(last, sh.first);
+            const int64_t lim = last - (int64_t)c->ttl_s;
+            while (!H.empty() && std::get<0>(H.top()) <= lim) {
+                const HE t = H.top();
+                H.pop();
+                auto it = M.find(std::get<2>(t));
+                if (it != M.end() && it->second.second == std::get<1>(t)) M.erase(it);
+            }
+        }
+        for (auto &q : v[j].open) {
+            M[q.key] = {q, ++seqn};
+            H.push(HE{(int64_t)q.sec, seqn, q.key});
+        }
     }
     if (M.empty()) return 0;
     // the earliest orphan of each key (stubs are appended in stream order, one per key and batch)
@@ -7218,7 +7236,7 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
     std::map<uint32_t, std::array<uint64_t, 4>> add; // slot -> total, out, in, timeout
     const bool quant = c->dns_groups & PV_DNS_QUANTILES;
     for (auto &kv : M) {
-        const PvXEvent &qe = kv.second;
+        const PvXEvent &qe = kv.second.first;
         const int ps = purge_shift(c->dns_shifts, c->ttl_s, qe.sec);
         auto it = orph.find(kv.first);
         if (it != orph.end() && (ps < 0 || it->second->sec < c->dns_shifts[ps].first)) {

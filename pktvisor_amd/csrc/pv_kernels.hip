@@ -4832,10 +4832,37 @@ struct XState {
     PvXValid valid[PV_BLOCK];
     uint32_t nval, nvalid, vbase, dbase;
 };
-__device__ __forceinline__ void xctr(XState &T, uint32_t period, uint32_t c) { atomicAdd(&T.ctr[period][c], 1u); }
+// Lanes of a wave adding to one LDS word serialise there (most transactions of a batch bump the
+// same few counters): one add per distinct word instead, each by the lowest lane that holds it.
+// Callable in divergent code: the loop runs over the active lanes' words, uniformly.
+__device__ __forceinline__ void lds_inc(uint32_t *a)
+{
+    const uint32_t lane = __lane_id();
+    const uint64_t ad = (uint64_t)(uintptr_t)a;
+    uint64_t pend = __ballot(1);
+    while (pend) {
+        const uint32_t ld = (uint32_t)__builtin_ctzll(pend);
+        const uint64_t la = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ad >> 32), ld) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)ad, ld);
+        const uint64_t eq = __ballot(ad == la);
+        if (lane == ld) atomicAdd(a, (uint32_t)__popcll(eq));
+        pend &= ~eq;
+    }
+}
+// one slot of an LDS-counted list per active lane: one add per wave
+__device__ __forceinline__ uint32_t lds_reserve(uint32_t *ctr)
+{
+    const uint64_t m = __ballot(1);
+    const uint32_t ld = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (__lane_id() == ld) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __builtin_amdgcn_readlane(base, ld);
+    return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ void xctr(XState &T, uint32_t period, uint32_t c) { lds_inc(&T.ctr[period][c]); }
 __device__ __forceinline__ void xval(PV_CREF(PvXactParams) X, XState &T, uint32_t period, uint32_t kind, uint64_t bits)
 {
-    T.val[atomicAdd(&T.nval, 1u)] = PvXValue{bits, X.slot_gen[period], kind};
+    T.val[lds_reserve(&T.nval)] = PvXValue{bits, X.slot_gen[period], kind};
 }
 // DnsMetricsBucket::new_dns_transaction slow branch (dns/v1 ...cpp:1126-1136): the
 // response's first query name (getName(), case kept) into top_slow
@@ -4894,26 +4921,26 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
     const uint32_t qd = be16(R, m + 4), an = be16(R, m + 6), ns = be16(R, m + 8), ar = be16(R, m + 10);
     uint32_t *c = T.c2[period][xd];
     if (g & PV_D2G_COUNTERS) {
-        atomicAdd(&c[D2_XACTS], 1u);
+        lds_inc(&c[D2_XACTS]);
         if (e.dir & 0x80) {
             // a dnstap event: l3 from socket_family, l4 the socket protocol (new_dns_transaction :936-970)
             const uint32_t l3 = (e.dir >> 4) & 3, pr = e.dir & 7;
-            if (l3) atomicAdd(&c[l3 == 2 ? D2_V6 : D2_V4], 1u);
+            if (l3) lds_inc(&c[l3 == 2 ? D2_V6 : D2_V4]);
             if (pr) {
                 const uint32_t w[8] = {0, D2_UDP, D2_TCP, D2_DOT, D2_DOH, D2_CRYPT_UDP, D2_CRYPT_TCP, D2_DOQ};
-                atomicAdd(&c[w[pr]], 1u);
+                lds_inc(&c[w[pr]]);
             }
         } else {
-            atomicAdd(&c[(e.pad & 2) ? D2_V6 : D2_V4], 1u);
-            atomicAdd(&c[tcp ? D2_TCP : D2_UDP], 1u);
+            lds_inc(&c[(e.pad & 2) ? D2_V6 : D2_V4]);
+            lds_inc(&c[tcp ? D2_TCP : D2_UDP]);
         }
-        if (qe.pad & 1) atomicAdd(&c[D2_CD], 1u);
-        if (rcode == 0) { atomicAdd(&c[D2_NOERROR], 1u); if (!an) atomicAdd(&c[D2_NODATA], 1u); }
-        else if (rcode == 2) atomicAdd(&c[D2_SRVFAIL], 1u);
-        else if (rcode == 3) atomicAdd(&c[D2_NX], 1u);
-        else if (rcode == 5) atomicAdd(&c[D2_REFUSED], 1u);
-        if (b23 & 0x04) atomicAdd(&c[D2_AA], 1u);
-        if (b23 & 0x2000) atomicAdd(&c[D2_AD], 1u);
+        if (qe.pad & 1) lds_inc(&c[D2_CD]);
+        if (rcode == 0) { lds_inc(&c[D2_NOERROR]); if (!an) lds_inc(&c[D2_NODATA]); }
+        else if (rcode == 2) lds_inc(&c[D2_SRVFAIL]);
+        else if (rcode == 3) lds_inc(&c[D2_NX]);
+        else if (rcode == 5) lds_inc(&c[D2_REFUSED]);
+        if (b23 & 0x04) lds_inc(&c[D2_AA]);
+        if (b23 & 0x2000) lds_inc(&c[D2_AD]);
     }
     // deep sampling: a response that drew "not deep" stops after the counters (:1006-1008)
     if (e.pad & 32) return;
@@ -4930,7 +4957,7 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
     // question; its name record straight from the carried address
     const uint32_t qfam = (qe.pad >> 3) & 3;
     if ((g & PV_D2G_TOP_ECS) && qfam) {
-        if (g & PV_D2G_COUNTERS) atomicAdd(&c[D2_ECS], 1u);
+        if (g & PV_D2G_COUNTERS) lds_inc(&c[D2_ECS]);
         const NameSrc es{nullptr, nullptr, qaddr, qfam};
         global_add(P, slot, PV_V2_DKEY(TM_ECS, xd, fmix64(qaddr ^ ((uint64_t)qfam << 62) ^ 0xec5ull)), 1, idx, &es);
     }
@@ -4955,7 +4982,7 @@ __device__ void dns2_xact(PV_CREF(PvXactParams) X, XState &T, const PvXEvent &e,
     if (g & PV_D2G_TOP_SIZE) add(TM_SIZED, fp, len);
     if (g & PV_D2G_XACT_TIMES) {
         const float thr = X.thr2[period][xd];
-        if (thr < 0.0f) T.valid[atomicAdd(&T.nvalid, 1u)] = PvXValid{e.idx, (uint8_t)period, (uint8_t)(4 + xd), 0, 0, us};
+        if (thr < 0.0f) T.valid[lds_reserve(&T.nvalid)] = PvXValid{e.idx, (uint8_t)period, (uint8_t)(4 + xd), 0, 0, us};
         else if (thr > 0.0f && (float)us >= thr) add(TM_SLOW_OUT, fp, 1);
     }
     if (g & PV_D2G_TOP_QNAMES) {
@@ -5065,7 +5092,7 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
             xval(X, T, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
         if (!kept || e.dir == 2 || !rdeep) return;
         if (X.thr_from[e.period] < 0.0f) {
-            T.valid[atomicAdd(&T.nvalid, 1u)] = PvXValid{e.idx, (uint8_t)e.period, (uint8_t)e.dir, 0, 0, us};
+            T.valid[lds_reserve(&T.nvalid)] = PvXValid{e.idx, (uint8_t)e.period, (uint8_t)e.dir, 0, 0, us};
         } else {
             slow_check(X, e.idx, e.period, e.dir, us);
         }
@@ -5124,7 +5151,7 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
     if (e.qr) {
         const bool kept = e.period >= P.dskip_before;
         uint32_t *c = T.c2[e.period][xd];
-        if (kept) atomicAdd(&c[D2_SEEN], 1u);
+        if (kept) lds_inc(&c[D2_SEEN]);
         int q = (int)p - 1;
         for (; q >= 0 && (uint32_t)(X.skeys[q] >> 32) == h; q--)
             if (xev(X, q).key == e.key) break;
@@ -5139,14 +5166,14 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         auto filtered = [&]() {
             if (kept && (P.dns2_groups & PV_D2G_COUNTERS)) sum_add(P, P.dslot_of[e.period], PV_OFF_DNS + DC_FILTERED, 1);
         };
-        if (!found || (kp && kp <= e.period)) { if (kept && !rf) atomicAdd(&c[D2_ORPHAN], 1u); return; }
+        if (!found || (kp && kp <= e.period)) { if (kept && !rf) lds_inc(&c[D2_ORPHAN]); return; }
         int64_t dsec = e.sec > qe.sec ? e.sec - qe.sec : qe.sec - e.sec;
         int64_t dnsec = (int64_t)e.nsec - (int64_t)qe.nsec;
         if (dnsec < 0) { dsec--; dnsec += 1000000000LL; }
         const bool timed_out = dsec > (int64_t)X.ttl_s || (dsec == (int64_t)X.ttl_s && ((double)dnsec / 1.0e6) >= (double)X.ttl_ms);
         if (rf) { if (!timed_out && !qf) filtered(); return; }
         if (qf) { filtered(); return; }
-        if (timed_out) { if (kept) atomicAdd(&c[D2_TIMEOUT], 1u); return; }
+        if (timed_out) { if (kept) lds_inc(&c[D2_TIMEOUT]); return; }
         const uint64_t us = (uint64_t)((dsec * 1000000000LL) + dnsec) / 1000;
         if (!kept) {
             // a period outside the window still feeds the next period's p90
@@ -5171,8 +5198,8 @@ __device__ void resolve_one2(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
             if (xev(X, q).key == e.key) break;
         if (q < X.n && (uint32_t)(X.skeys[q] >> 32) == h && xev(X, q).period < kp) return;
         if (kp < P.dskip_before) return;
-        atomicAdd(&T.c2[kp][xd][D2_TIMEOUT], 1u);
-        atomicAdd(&T.c2[kp][xd][D2_SEEN], 1u);
+        lds_inc(&T.c2[kp][xd][D2_TIMEOUT]);
+        lds_inc(&T.c2[kp][xd][D2_SEEN]);
     }
 }
 

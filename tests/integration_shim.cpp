@@ -25,6 +25,7 @@ int integration_shim_calls(Staging &g, const char *qtype, uint64_t cache_limit, 
     g.ctx = ctx;
     // section 1: the handler shim
     rc |= pv_set_tcp_reassembly_limit(ctx, cache_limit);
+    rc |= pv_set_tcp_exact_lru(ctx, 1);
     pv_dns_filters f{};
     f.answer_count = -1;
     uint32_t v = 0;

@@ -89,10 +89,10 @@ def rank_main(args):
         part = {}
 
         def step(name, f):
-            a = time.perf_counter()
+            a, g0 = time.perf_counter(), sent["gather"]
             f()
             h.synchronize()
-            part[name] = round((time.perf_counter() - a) * 1e3, 1)
+            part[name] = {"ms": round((time.perf_counter() - a) * 1e3, 1), "gathered_bytes": sent["gather"] - g0}
         h.synchronize()
         step("check_aligned", lambda: pvdist.check_aligned(h))
         step("edges", lambda: pvdist.merge_edges(h))
