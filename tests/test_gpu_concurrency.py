@@ -127,3 +127,35 @@ def test_reads_during_process_host(oracle, name):
         assert hits, "a concurrent bucket merge matches no batch boundary"
         assert max(hits) >= last
         last = min(j for j in hits if j >= last)
+
+
+def test_read_latency_inside_one_host_block(monkeypatch):
+    """a read issued while ONE pv_process_host call works through a large block
+    waits for the batch in flight, not for the block: the ingest loop takes the context mutex per
+    batch (pv_process_device), so a reader thread sees several intermediate batch boundaries
+    inside the call, each read returning within a few batch times"""
+    import time
+    from pktvisor_amd import synth
+    monkeypatch.setenv("PV_INGEST_CHUNK_MB", "4")
+    pcap = synth.pcap_bytes(4, 400000)
+    recs = pcap[24:]
+    h = pa.PvHandlers(host_spec=synth.HOST_SPEC, num_periods=1, max_records=1 << 20)
+    try:
+        h.window_json(0)  # (first-read setup outside the measurement)
+        t = threading.Thread(target=lambda: h.process_host(recs))
+        lat, seen = [], []
+        t.start()
+        while t.is_alive():
+            a = time.perf_counter()
+            w = h.window_json(0)
+            lat.append(time.perf_counter() - a)
+            seen.append(w["packets"]["events"])
+        t.join()
+        final = h.window_json(0)["packets"]["events"]
+    finally:
+        h.close()
+    assert final == 400000
+    inside = sorted(set(e for e in seen if 0 < e < final))
+    assert len(inside) >= 3, f"reads saw {inside}: no batch boundaries inside the block"
+    assert seen == sorted(seen), "reads must move forward through the batches"
+    assert max(lat) < 1.0, f"a read waited {max(lat):.3f} s"
