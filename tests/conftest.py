@@ -11,6 +11,17 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs under gpurun)")
+    if getattr(config.option, "markexpr", "") == "gpu":
+        # torch ships its own HIP runtime next to the library's (/opt/rocm). On the GPU boxes
+        # torch's cannot open the device once the library's runtime has (a test module's
+        # pv_device_count at collection is enough: 'No HIP GPUs are available'), while the other
+        # order works. So torch's comes up first, before collection imports any test module.
+        import torch
+        try:
+            if torch.cuda.device_count() > 0:
+                torch.cuda.init()
+        except RuntimeError as e:
+            print(f"conftest: torch HIP runtime unavailable: {e}")
 
 
 @pytest.fixture(scope="session")
@@ -19,15 +30,3 @@ def oracle():
     from tests import oracle_ctypes
     return oracle_ctypes.load()
 
-
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_first(request):
-    """torch ships its own HIP runtime next to the library's (/opt/rocm): on the GPU box torch's
-    is brought up first in a GPU session, before any test's context, so a test that moves data
-    with torch never meets a device the other runtime already configured (a run of the TCP / KAT
-    files followed by a torch-using test saw 'No HIP GPUs are available' otherwise)"""
-    if request.config.getoption("-m", default="") == "gpu":
-        import torch
-        if torch.cuda.device_count() > 0:
-            torch.cuda.init()
-    yield

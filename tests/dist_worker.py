@@ -40,9 +40,11 @@ def gpu_main(pcap_path, out, host, periods, rate=100, filters=None, dns2_config=
     import pktvisor_amd as pa
     from pktvisor_amd import dist as pvdist
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    ndev = pa.device_count()
+    # torch's HIP runtime before the library's (the other order leaves torch without a device)
+    ndev = torch.cuda.device_count()
     dev = torch.device("cuda", rank % ndev)
     torch.cuda.set_device(dev)
+    torch.cuda.init()
     dist.init_process_group("gloo", rank=rank, world_size=world)
     linktype, ts_nano, recs = pa.read_pcap(pcap_path)
     idx = pa.RecordIndex(recs, ts_nano)
