@@ -7,8 +7,13 @@ R=$(pwd); O=$R/gpurun_out/${FIN_DIR:-r5_fin}; mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
 step tests
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
+# (no -x: every failure at once; a failing test does not stop the evidence below, a hang or a
+# crash of the suite does)
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1
+trc=$?
 tail -1 $O/gpu_tests.log
+grep -E "^(FAILED|ERROR)" $O/gpu_tests.log | head -20
+[ $trc -le 1 ] || exit 1
 step smoke
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
@@ -30,3 +35,4 @@ step prof c5
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o k -- python3 $R/bench.py --config 5 --stream-records 30000000 --steps 1 --warmup 1 > $O/prof_c5.log 2>&1) || { tail -20 $O/prof_c5.log; exit 1; }
 python3 tools/kstats.py $O/prof_c5 2>/dev/null | cut -c1-300
 step done
+[ $trc -eq 0 ] || exit 1
