@@ -2720,29 +2720,35 @@ uint64_t next_bit(const uint64_t *bits, uint64_t from, uint64_t n)
     return n;
 }
 
-// The DNS manager's shifts: the first DNS event with ts_sec >= next_shift, then next_shift =
-// its second + 60, repeatedly (monotone batch). DNS events: the UDP datagrams of
-// pv_dns_prescan's bits, and the TCP messages (ord, stamp second) of the batch's TCP stage,
-// whose stamps (a connection's end time) may lag their position.
+// The DNS manager's shifts: the first DNS event (in stream order) with ts_sec >= next_shift, then
+// next_shift = its second + 60, repeatedly (AbstractMetricsManager::new_event, per event: the
+// batch's timestamps need not be monotone). DNS events: the UDP datagrams of pv_dns_prescan's
+// bits, and the TCP messages (ord, stamp second) of the batch's TCP stage, whose stamps (a
+// connection's end time) may lag their position.
 void dns_shifts_of(int64_t T, const uint64_t *bits, uint64_t n, const pv_index_info *info, const uint32_t *sc_idx,
                    const uint32_t *sc_sec, const std::vector<std::pair<uint64_t, int64_t>> &tcp, std::vector<Shift> &out)
 {
     const uint32_t nsc = info->n_sec_changes;
-    uint32_t k = 0;
+    uint32_t k = 0;     // the second-run holding record `after / 4`
     size_t t = 0;
     uint64_t after = 0; // events at ord >= after are still candidates
     for (;;) {
-        // UDP: the first event in a second >= T (later than the last shift: times are monotone)
-        while (k < nsc && (int64_t)sc_sec[k] < T) k++;
+        // UDP: the first event at or past `after` whose record's second is >= T, run by run of
+        // equal seconds (sc_idx / sc_sec: the batch's change points, in record order)
+        const uint64_t from = (after + 3) / 4;
+        while (k + 1 < nsc && sc_idx[k + 1] <= from) k++;
         uint64_t ui = n, uord = ~0ull;
         int64_t usec = 0;
-        if (k < nsc) {
-            ui = next_bit(bits, sc_idx[k], n);
-            if (ui < n) {
-                uint32_t kk = k;
-                while (kk + 1 < nsc && sc_idx[kk + 1] <= ui) kk++;
+        for (uint32_t kk = k; kk < nsc; kk++) {
+            if ((int64_t)sc_sec[kk] < T) continue;
+            const uint64_t lo = std::max<uint64_t>(sc_idx[kk], from), hi = kk + 1 < nsc ? sc_idx[kk + 1] : n;
+            if (lo >= hi) continue;
+            const uint64_t i = next_bit(bits, lo, hi);
+            if (i < hi) {
+                ui = i;
                 usec = (int64_t)sc_sec[kk];
                 uord = ui * 4;
+                break;
             }
         }
         // TCP: the first message after the last shift whose stamp second is >= T
@@ -4024,38 +4030,29 @@ int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const
     c->tcp_nmsg = 0;
     c->tcp_ords.clear();
     c->tcp_items.clear();
+    // the batch's latest second (its last record's, unless the timestamps go back somewhere)
+    int64_t top = info->last_sec;
+    if (!info->monotone)
+        for (uint32_t k = 0; k < info->n_sec_changes; k++) top = std::max<int64_t>(top, (int64_t)sc_sec[k]);
     if (c->sample_rate < 100) {
         // deep sampling draws per DNS event in stream order, DNS-over-TCP messages among them:
         // the TCP stage runs ahead of the spans so their order is known first
         c->tcp_pre = true;
         uint32_t tseg[2] = {0, 0};
         if (int rc = dns_prescan(c, d_recs, d_offs, info->n_records, st, true, tseg)) return rc;
-        const bool dns_may = c->cfg.num_periods > 1 && info->last_sec >= c->dns.next_shift_sec;
+        const bool dns_may = c->cfg.num_periods > 1 && top >= c->dns.next_shift_sec;
         if (int rc = tcp_stage(c, d_recs, d_offs, info->n_records, tseg[0], tseg[1], (uint32_t)info->first_sec, true, st))
             return rc;
         if (c->cfg.num_periods <= 1) return 0;
-        const bool net_may = info->last_sec >= c->net.next_shift_sec;
+        const bool net_may = top >= c->net.next_shift_sec;
         if (!net_may && !dns_may) return 0;
-        if (!info->monotone) {
-            for (uint32_t k = 0; k < info->n_sec_changes; k++)
-                if ((int64_t)sc_sec[k] >= std::min(c->net.next_shift_sec, c->dns.next_shift_sec))
-                    return c->fail(PV_EUNSUPPORTED, "period shift inside a batch with non-monotone timestamps");
-            return 0;
-        }
         if (net_may) net_shifts_of(c->net.next_shift_sec, info, sc_idx, sc_sec, nsh);
         if (dns_may) dns_shifts_of(c->dns.next_shift_sec, c->h_dbits, info->n_records, info, sc_idx, sc_sec, c->tcp_ords, dsh);
         return 0;
     }
     if (c->cfg.num_periods <= 1) return 0;
-    const bool net_may = info->last_sec >= c->net.next_shift_sec, dns_may = info->last_sec >= c->dns.next_shift_sec;
+    const bool net_may = top >= c->net.next_shift_sec, dns_may = top >= c->dns.next_shift_sec;
     if (!net_may && !dns_may) return 0;
-    if (!info->monotone) {
-        // a shift decided per event needs event order = time order
-        for (uint32_t k = 0; k < info->n_sec_changes; k++)
-            if ((int64_t)sc_sec[k] >= std::min(c->net.next_shift_sec, c->dns.next_shift_sec))
-                return c->fail(PV_EUNSUPPORTED, "period shift inside a batch with non-monotone timestamps");
-        return 0;
-    }
     if (net_may) net_shifts_of(c->net.next_shift_sec, info, sc_idx, sc_sec, nsh);
     c->tcp_pre = dns_may || nsh.size() > PV_MAX_SHIFTS;
     if (c->tcp_pre) {

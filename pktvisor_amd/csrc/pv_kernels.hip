@@ -701,12 +701,13 @@ __device__ __forceinline__ uint32_t period_of(PV_CREF(PvParams) P, uint64_t i)
     while (p < P.n_shift && i >= P.pstart[p]) p++;
     return p;
 }
-// DNS period of a DNS event at second `sec` (the DNS manager's own shifts; timestamps of a
-// batch with DNS shifts are monotone, so the second decides)
-__device__ __forceinline__ uint32_t dperiod_of(PV_CREF(PvParams) P, int64_t sec)
+// DNS period of the DNS event of span record i (the DNS manager's own shifts, in stream order:
+// the event that shifts and every event after it belong to the new period, whatever their
+// timestamps, as AbstractMetricsManager::new_event decides per event)
+__device__ __forceinline__ uint32_t dperiod_of(PV_CREF(PvParams) P, uint64_t i)
 {
     uint32_t p = 0;
-    while (p < P.n_dshift && sec >= P.dthresh[p]) p++;
+    while (p < P.n_dshift && 4 * i >= (uint64_t)P.dpos[p]) p++;
     return p;
 }
 __device__ __forceinline__ uint64_t uni64(uint64_t v)
@@ -1372,7 +1373,7 @@ struct alignas(16) NetWave {
 // the parameter block would be a vector load whose wait also drains the tiles in flight
 struct PeriodTab {
     uint64_t pstart[PV_MAX_SHIFTS];
-    int64_t dthresh[PV_MAX_SHIFTS];
+    int64_t dord[PV_MAX_SHIFTS]; // span ord of each DNS shift's event (P.dpos)
     uint32_t slot[PV_MAX_SHIFTS + 1];
 };
 struct NetState {
@@ -1692,7 +1693,7 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
     if (o.l4 == 17 && !(K.dbg & 4)) {
         const uint32_t port = dns_port(R.u32(o.l4off));
         if (port) {
-            const uint32_t dp = P.n_dshift ? dperiod_of(P, o.sec) : 0u;
+            const uint32_t dp = P.n_dshift ? dperiod_of(P, i) : 0u;
             so.dm = msg_words(dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, true));
             so.isdns = 1;
         }
@@ -1724,7 +1725,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
     if (threadIdx.x == 0) S.nd = 0;
     if (threadIdx.x < PV_MAX_SHIFTS) {
         S.pt.pstart[threadIdx.x] = P.pstart[threadIdx.x];
-        S.pt.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+        S.pt.dord[threadIdx.x] = P.dpos[threadIdx.x];
     }
     if (threadIdx.x <= PV_MAX_SHIFTS) S.pt.slot[threadIdx.x] = P.slot_of[threadIdx.x];
     __syncthreads();
@@ -1941,7 +1942,7 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
                 const uint32_t port = dns_port(rw.at(50));
                 if (port) {
                     uint32_t dp = 0;
-                    for (uint32_t q = 0; q < K.n_dshift; q++) dp += (int64_t)o.sec >= S.pt.dthresh[q];
+                    for (uint32_t q = 0; q < K.n_dshift; q++) dp += (int64_t)(4 * i) >= S.pt.dord[q];
                     DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= K.dskip_before, false);
                     d.fkey = fast_flowkey(rw);
                     dm = msg_words(d);
@@ -2104,7 +2105,7 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x == 0) S.nd = 0;
-    if (threadIdx.x < PV_MAX_SHIFTS) S.pt.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+    if (threadIdx.x < PV_MAX_SHIFTS) S.pt.dord[threadIdx.x] = P.dpos[threadIdx.x];
     __syncthreads();
     const PV_G uint8_t *const recs = P.recs;
     const PV_G uint32_t *const offs = P.offs;
@@ -2227,7 +2228,7 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
             if (isdns) {
                 const Parsed o = fast_parsed(f, rw, ts_nano, off);
                 uint32_t dp = 0;
-                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)o.sec >= S.pt.dthresh[q];
+                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)(4 * i) >= S.pt.dord[q];
                 const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
                 DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
                 d.fkey = fast_flowkey(rw);
@@ -2335,7 +2336,7 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
 struct NetRegState {
     uint32_t hist[PV_HBINS];
     uint32_t nd, nx;
-    int64_t dthresh[PV_MAX_SHIFTS];
+    int64_t dord[PV_MAX_SHIFTS];
 };
 __device__ __forceinline__ void win_load(const PV_G uint8_t *recs, uint32_t off, uint4 (&W)[5])
 {
@@ -2366,7 +2367,7 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x == 0) { S.nd = 0; S.nx = 0; }
-    if (threadIdx.x < PV_MAX_SHIFTS) S.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+    if (threadIdx.x < PV_MAX_SHIFTS) S.dord[threadIdx.x] = P.dpos[threadIdx.x];
     __syncthreads();
     const PV_G uint8_t *const recs = P.recs;
     const bool compact = P.ip_compact;
@@ -2445,7 +2446,7 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
             if (isdns) {
                 const Parsed o = fast_parsed(f, rw, ts_nano, off);
                 uint32_t dp = 0;
-                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)o.sec >= S.dthresh[q];
+                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)(4 * i) >= S.dord[q];
                 const SAcc R{recs, nullptr, 0, 0, 0, 1};
                 DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
                 d.fkey = fast_flowkey(rw);
@@ -2664,7 +2665,7 @@ struct NetRingState {
     uint32_t hist[PV_HBINS];
     uint32_t nd[PV_RING_MAXG], nx[PV_RING_MAXG];
     uint32_t full[PV_RING_NP], fre[PV_RING_NP]; // per parsing wave: tiles published / released
-    int64_t dthresh[PV_MAX_SHIFTS];
+    int64_t dord[PV_MAX_SHIFTS];
 };
 static_assert(sizeof(NetRingState) <= 160 * 1024, "ring Net pass LDS");
 template <int N>
@@ -2706,7 +2707,7 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
     if (threadIdx.x < PV_RING_MAXG) { S.nd[threadIdx.x] = 0; S.nx[threadIdx.x] = 0; }
     if (threadIdx.x < PV_RING_NP) { S.full[threadIdx.x] = 0; S.fre[threadIdx.x] = 0; }
-    if (threadIdx.x < PV_MAX_SHIFTS) S.dthresh[threadIdx.x] = P.dthresh[threadIdx.x];
+    if (threadIdx.x < PV_MAX_SHIFTS) S.dord[threadIdx.x] = P.dpos[threadIdx.x];
     __syncthreads();
     const PV_G uint8_t *const recs = P.recs;
     const bool compact = P.ip_compact;
@@ -2864,7 +2865,7 @@ __device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
             if (isdns) {
                 const Parsed o = fast_parsed(f, rw, ts_nano, off);
                 uint32_t dp = 0;
-                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)o.sec >= S.dthresh[q];
+                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)(4 * i) >= S.dord[q];
                 const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
                 DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
                 d.fkey = fast_flowkey(rw);

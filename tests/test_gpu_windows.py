@@ -153,3 +153,35 @@ def test_value_buffer_small_batches(oracle, tmp_path, monkeypatch, budget_mb):
         h.close()
     ref = oracle.run_bytes(pcap, host_spec=synth.HOST_SPEC, num_periods=5, window=5)
     assert diff(got, ref) is None, diff(got, ref)
+
+
+def _jittered(pcap, frac=0.1, back=3, seed=5):
+    """the capture with a fraction of its records stamped up to `back` seconds earlier (timestamps
+    out of order around every minute mark, as real captures have them)"""
+    import struct
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = []
+    for s, u, r in synth.records_of(pcap):
+        if rng.random() < frac:
+            r = struct.pack("<I", s - int(rng.integers(1, back + 1))) + r[4:]
+        out.append(r)
+    return pa.pcap_file_bytes(b"".join(out))
+
+
+@pytest.mark.parametrize("periods", [2, 5])
+def test_non_monotone_timestamps_across_shifts(oracle, tmp_path, periods):
+    """period shifts inside batches whose timestamps go back: each manager shifts on the first event
+    (in stream order) at or past its next shift second, and every later event belongs to the new
+    period whatever its stamp (AbstractMetricsManager::new_event); was refused before round 5"""
+    pcap = _jittered(synth.pcap_bytes(4, 60000, ts_step_us=5000))
+    gpu, ref = run_both(oracle, pcap, periods, tmp_path)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def test_non_monotone_small_chunks(oracle, tmp_path, monkeypatch):
+    """the same over 1 MiB ingest batches, with DNS over TCP in the stream"""
+    monkeypatch.setenv("PV_INGEST_CHUNK_MB", "1")
+    pcap = _jittered(synth.c4_tcp_pcap(n=60000, ts_step_us=5000, flows=100), frac=0.05)
+    gpu, ref = run_both(oracle, pcap, 5, tmp_path)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
