@@ -331,7 +331,7 @@ def end_to_end(h, blob, n: int, steps: int) -> dict:
     import pktvisor_amd as pa
     lib = pa.load_library()
     buf = np.frombuffer(blob, dtype=np.uint8).copy()
-    out = {"unit": "Mpkt/s", "steps": steps, "chunk_mb": int(os.environ.get("PV_INGEST_CHUNK_MB", "64")),
+    out = {"unit": "Mpkt/s", "steps": steps, "chunk_mb": int(os.environ.get("PV_INGEST_CHUNK_MB", "128")),
            "path": ("record blob in host RAM -> (pageable only) parallel copy to pinned staging -> H2D of fixed "
                     "chunks on two copy streams into a device ring (PV_INGEST_RING slots, default 4) -> record index on the device "
                     "(pv_index.hip) -> kernels")}
