@@ -145,6 +145,8 @@ extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg_tc(const PvParams *P);
+extern "C" __global__ void pv_net_kernel_span(const PvParams *P);
+extern "C" __global__ void pv_net_slow_list(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
 extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
@@ -570,6 +572,8 @@ struct pv_ctx {
     uint64_t *d_iplog = nullptr; // dense IP log, one u64 per record (max_records + one tile)
     uint32_t *d_iplog32 = nullptr, *d_ipx_cnt = nullptr, *d_ipx_rep = nullptr; // compact IP log (register pass)
     uint64_t *d_ipdir = nullptr;
+    uint32_t *d_slow = nullptr; // span Net pass: deferred record indices (max_records), their count
+    uint64_t slow_cap = 0;
     uint64_t *d_trash = nullptr; // 64 B per Net-pass wave
     uint32_t nn_cap = 0;
     uint32_t reg_log2 = 0;
@@ -2552,7 +2556,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
                     c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_iplog32,
-                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose,
+                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_slow, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose,
                     c->d_xcnt, c->d_xrhdr, c->d_xtot, c->d_xsend, c->d_xrecv, c->d_xp, c->d_bpf, c->d_fwork, c->d_frecs,
                     c->d_foffs, c->d_fsc, c->d_fscan};
     for (void *p : ptrs) if (p) hipFree(p);
@@ -3865,8 +3869,24 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         return c->hipfail(e, "parameter upload");
     hipEventRecord(c->ev_start, st);
     const bool tc = (c->net_groups & PV_NET_TOP_IPS) && c->reg_waves != 8;
+    // PV_NET_KERNEL=span: the span-load pass with the general path deferred (top-IPs groups)
+    const bool span = lean && tc && !ring && regw && force && !strcmp(force, "span");
+    if (span) {
+        if (c->slow_cap < P.n) {
+            if (c->d_slow) hipFree(c->d_slow);
+            c->d_slow = nullptr;
+            c->slow_cap = 0;
+            if (!hip_ok(e = hipMalloc(&c->d_slow, (size_t)(P.n + PV_MAX_GRID) * 4))) return c->hipfail(e, "deferred record list");
+            c->slow_cap = P.n;
+        }
+        P.slow_list = c->d_slow;
+        P.slow_cnt = c->d_slow + c->slow_cap; // written for every range by the span pass
+        *c->h_params = P;
+        if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
+            return c->hipfail(e, "parameter upload");
+    }
     c->net_kernel = general ? "pv_net_kernel"
-                            : (lean ? (ring ? "pv_net_kernel_fast"
+                            : (lean ? (span ? "pv_net_kernel_span" : ring ? "pv_net_kernel_fast"
                                             : (!regw ? "pv_net_kernel_ring"
                                                      : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : (tc ? "pv_net_kernel_reg_tc" : "pv_net_kernel_reg"))))
                                     : "pv_net_kernel_ns");
@@ -3882,6 +3902,10 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
                                ? fa.maxThreadsPerBlock : 512;
         }
         hipLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(ring_threads), 0, st, (const PvParams *)c->d_params);
+    }
+    else if (span) {
+        hipLaunchKernelGGL(pv_net_kernel_span, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+        hipLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (const PvParams *)c->d_params);
     }
     else if (lean && c->reg_waves == 8) hipLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, (const PvParams *)c->d_params);
     else if (lean && tc) hipLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
@@ -3903,7 +3927,13 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates into a list sorted by table region, merge
     // each region's runs in LDS, decode the names of new entries
-    hipLaunchKernelGGL(c->reg_log2 <= 10 ? pv_topn_combine : pv_topn_combine_r12, dim3(P.cb_grid), dim3(PV_CB_THREADS), 0, st,
+    static int cb_threads = 0; // the kernel's own launch bound (tuning builds change it)
+    if (!cb_threads) {
+        hipFuncAttributes fa{};
+        cb_threads = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(pv_topn_combine)) == hipSuccess ? fa.maxThreadsPerBlock
+                                                                                                             : PV_CB_THREADS;
+    }
+    hipLaunchKernelGGL(c->reg_log2 <= 10 ? pv_topn_combine : pv_topn_combine_r12, dim3(P.cb_grid), dim3(cb_threads), 0, st,
                        (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(pv_topn_merge_threads()), 0, st, (const PvParams *)c->d_params);
     // names: as many workgroups as are resident (LDS: two per CU), each pipelining its entries

@@ -2611,6 +2611,292 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
 }
 
+// ------------------------------------------------------------------ the lean Net pass, span loads
+// The register-window pass's loads touch ~40 lines per instruction at an 80-B record stride, and the
+// second to fifth window instruction of a tile hit lines the first one is still fetching: the L1
+// spends 57 % of the C2 pass in pending-miss stalls (profiles/r5/tcp_ta). This pass loads a tile
+// whose 64 records lie in at most PV_SPAN_MAX bytes (C2: 64 x 80 B) as its span: six 16-B loads a
+// lane, each instruction 1 KiB contiguous, one tile ahead; the wave writes the span into its LDS
+// buffer and each lane reads its record's 96 bytes back with aligned 16-B reads (an 80-B stride
+// puts 16 lanes on 16 distinct bank groups). Tiles spread wider load their windows per lane from
+// HBM. Records the fast path does not take are not parsed here (the general path is an out-of-line
+// call, and every value live across a call would be spilled with a wait on the whole load queue at
+// each reload): their indices go to a list that pv_net_slow_list parses after this pass.
+#ifndef PV_SPAN_MAX
+#define PV_SPAN_MAX 6144
+#endif
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+struct NetSpanState {
+    uint32_t hist[PV_HBINS];
+    uint32_t nd, ns;
+    int64_t dord[PV_MAX_SHIFTS];
+    v4u32 buf[4][PV_SPAN_MAX / 16 + 8];
+};
+// (six named registers of a native vector type: HIP's uint4 copies are byte copies, and the
+// buffers they copy from stay in scratch)
+struct SpanX {
+    v4u32 v0, v1, v2, v3, v4, v5;
+};
+__device__ __forceinline__ void span_load(const PV_G uint8_t *recs, uint32_t o, uint32_t lane, SpanX &X, uint32_t &b)
+{
+    const uint32_t o0 = __builtin_amdgcn_readfirstlane(o), o63 = __builtin_amdgcn_readlane(o, 63);
+    const uint32_t b16 = o0 & ~15u;
+    const uint32_t len = o63 + 80u - b16;
+    const PV_G v4u32 *ps = reinterpret_cast<const PV_G v4u32 *>(recs + b16);
+    // a span: lane 0's and lane 63's records bound every lane's, within PV_SPAN_MAX bytes
+    const bool sp = o63 >= o0 && len <= PV_SPAN_MAX && !__ballot(o < o0 || o > o63);
+    b = sp ? b16 : 0xffffffffu;
+    // (always six loads, so the compiler's vmcnt waits stay counted; past the span: chunk 0 again)
+    const uint32_t lim = sp ? len : 0u;
+#define PV_SPAN_LD(j) X.v##j = ps[16u * (lane + 64u * j) < lim ? lane + 64u * j : 0u]
+    PV_SPAN_LD(0); PV_SPAN_LD(1); PV_SPAN_LD(2); PV_SPAN_LD(3); PV_SPAN_LD(4); PV_SPAN_LD(5);
+#undef PV_SPAN_LD
+}
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_span(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    __shared__ NetSpanState S;
+    constexpr uint32_t NW = 4;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
+    if (threadIdx.x == 0) { S.nd = 0; S.ns = 0; }
+    if (threadIdx.x < PV_MAX_SHIFTS) S.dord[threadIdx.x] = P.dpos[threadIdx.x];
+    __syncthreads();
+    const PV_G uint8_t *const recs = P.recs;
+    const PV_G uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint32_t slot = P.slot_of[0];
+    const uint32_t groups = P.net_groups;
+    const bool card = groups & PV_NET_CARDINALITY_BIT;
+    const uint32_t ts_nano = P.ts_nano;
+    HostNets h;
+    {
+        const uint32_t n4 = P.nets.n4;
+        h.a0 = P.nets.v4_addr[0]; h.m0 = P.nets.v4_mask[0]; h.e0 = n4 > 0 ? ~0u : 0u;
+        h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
+    }
+    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
+    uint64_t cd = 0, cl = 0; // fast lanes' packed counters (net_fast_reg's)
+    v4u32 *Lq = S.buf[wave];
+    for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
+    const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
+    const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u;
+    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
+    auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
+    auto tile = [&](uint32_t k, uint32_t off, const SpanX &X, uint32_t b) {
+        const uint64_t t = tile_of(k);
+        const uint64_t i = t * PV_WT + lane;
+        const bool active = i < n;
+        RecW rw;
+        if (b != 0xffffffffu) {
+            Lq[lane] = X.v0; Lq[lane + 64] = X.v1; Lq[lane + 128] = X.v2;
+            Lq[lane + 192] = X.v3; Lq[lane + 256] = X.v4; Lq[lane + 320] = X.v5;
+            // (a wave's LDS operations execute in issue order: only the compiler's order matters)
+            asm volatile("" ::: "memory");
+            const uint32_t rel = off - b;
+            const v4u32 *q = Lq + (rel >> 4);
+            uint32_t x[24];
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const v4u32 v = q[j];
+                x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+            }
+            // the record's dwords from its dword-aligned start: x[d + m], d = (rel >> 2) & 3
+            // (bit selects on opaque masks: written as selects, the compiler indexes the array
+            // with d and puts it in scratch)
+            uint32_t m1 = 0u - ((rel >> 2) & 1), m2 = 0u - ((rel >> 3) & 1);
+            asm volatile("" : "+v"(m1), "+v"(m2));
+            uint32_t y[19], z[17];
+#pragma unroll
+            for (int m = 0; m < 19; m++) y[m] = (x[m + 1] & m1) | (x[m] & ~m1);
+#pragma unroll
+            for (int m = 0; m < 17; m++) z[m] = (y[m + 2] & m2) | (y[m] & ~m2);
+#pragma unroll
+            for (int j = 0; j < 16; j++) rw.w[j] = __builtin_amdgcn_alignbyte(z[j + 1], z[j], rel & 3);
+            asm volatile("" ::: "memory");
+        } else {
+            uint4 W[5];
+            win_load(recs, off, W);
+            win_words(W, off & 3, rw);
+        }
+        if (PV_LEAN_LEVEL == 1) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int j = 0; j < 16; j++) x ^= rw.w[j];
+            cd += active ? x : 0u;
+            return;
+        }
+        const FastRec f = fast_fields(rw, h);
+        const bool fast = active & (f.ok != 0);
+        cd += fast ? 1ull << (f.dir * 16) : 0ull;
+        cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
+        if (PV_LEAN_LEVEL == 2) return;
+        // the records the fast path does not take: the range's list for pv_net_slow_list (an LDS
+        // reservation: a returning global atomic would wait on every load in flight)
+        {
+            const uint64_t sm = __ballot(active & !fast);
+            if (sm) {
+                uint32_t q = 0;
+                if (lane == 0) q = atomicAdd(&S.ns, (uint32_t)__popcll(sm));
+                q = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+                if (active && !fast) P.slow_list[wbeg * PV_WT + q] = (uint32_t)i;
+            }
+        }
+        uint32_t hv = fast ? f.caplen : PV_NOH;
+        const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
+        const bool ipok = fast & (f.dir != 2) & (ip != 0);
+        const uint32_t port = (fast & (f.l4 == 17)) ? dns_port_bf(rw.at(50)) : 0u;
+        DnsMsgW dm{};
+        const bool isdns = port != 0;
+        if (__ballot(isdns)) {
+            if (isdns) {
+                const Parsed o = fast_parsed(f, rw, ts_nano, off);
+                uint32_t dp = 0;
+                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)(4 * i) >= S.dord[q];
+                const SAcc R{recs, nullptr, 0, 0, 0, 1};
+                DnsMsg dmsg = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
+                dmsg.fkey = fast_flowkey(rw);
+                dm = msg_words(dmsg);
+            }
+        }
+        const bool istcp = fast & (f.l4 == 6);
+        bool hasseg = false;
+        PvTcpSeg seg;
+        const uint32_t temit = P.tcp_emit;
+        if (temit && __ballot(istcp)) {
+            if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
+        }
+        if (__ballot(hv != PV_NOH && hv > 65535)) {
+            if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
+        }
+        hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
+        const uint64_t m = __ballot(isdns);
+        if (m) {
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(&S.nd, (uint32_t)__popcll(m));
+            q = __builtin_amdgcn_readlane(q, 0);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (isdns) {
+                PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(P.dq) + 2 * (wbeg * PV_WT + q + below);
+                dd[0] = dm.a;
+                dd[1] = dm.b;
+            }
+        }
+        // the compact IP log: every lane's word (the log has 64 words of slack past the batch;
+        // a deferred record's word is pv_net_slow_list's), the tile's direction word
+        const uint64_t ek = ipok ? ((uint64_t)card << 33) | ((uint64_t)f.dir << 32) | ip : 0ull;
+        P.iplog32[i] = (uint32_t)ek;
+        P.ipdir[t] = __ballot(ipok && f.dir == 1);
+        if (temit) {
+            const uint64_t tm = __ballot(istcp);
+            if (tm) {
+                if (lane == 0) P.tmask[t] = tm;
+                tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, seg, lane);
+            }
+        }
+    };
+    SpanX XA, XB;
+    uint32_t oA = 0, oB = 0, bA = 0xffffffffu, bB = 0xffffffffu;
+    if (ntl) {
+        oA = off_of(0);
+        oB = off_of(1);
+        span_load(recs, oA, lane, XA, bA);
+    }
+    for (uint32_t k = 0; k < ntl; k += 2) {
+        const uint32_t oN = off_of(k + 2);
+        span_load(recs, oB, lane, XB, bB);   // tile k + 1 (a clamped copy past the range's end)
+        tile(k, oA, XA, bA);
+        if (k + 1 >= ntl) break;
+        const uint32_t oN2 = off_of(k + 3);
+        span_load(recs, oN, lane, XA, bA);   // tile k + 2
+        oA = oN;
+        tile(k + 1, oB, XB, bB);
+        oB = oN2;
+    }
+    // this range's DNS list count; the exception list is pv_net_slow_list's (0 here)
+    lds_barrier();
+    if (threadIdx.x == 0) {
+        P.mq_cnt[lb] = 0;
+        P.dq_cnt[lb] = S.nd;
+        P.ipx_cnt[lb] = 0;
+        P.slow_cnt[lb] = S.ns;
+        if (S.nd) atomicAdd(P.n_dns, S.nd);
+        S.nd = 0;
+        S.ns = 0;
+    }
+    lds_barrier();
+    }
+    NetCtr c;
+    c.zero();
+    {
+        const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
+        const uint32_t nf = fin + fout + funk;
+        c.nev += nf; c.n4 += nf;
+        c.nin += fin; c.nout += fout; c.nunk += funk;
+        c.nudp += (uint32_t)(cl & 0xffff); c.ntcp += (uint32_t)((cl >> 16) & 0xffff);
+        c.noth += (uint32_t)((cl >> 32) & 0xffff); c.nsyn += (uint32_t)(cl >> 48);
+    }
+    NetK K;
+    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
+    knet_flush(K, slot, c);
+    lds_barrier();
+    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
+        if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
+}
+
+// The span pass's deferred records (VLAN, IPv6, options, tunnels, other link types), one lane
+// each: the general path (net_slow_p: counters' fields, IP entry, DNS message, TCP segment), then
+// what the span pass does for a fast record, through atomics (the records' ranges have closed):
+// payload histogram, compact IP log word or exception entry, direction bit, DNS list entry, TCP
+// tile mask. A persistent grid walks the list.
+extern "C" __global__ void __launch_bounds__(256) pv_net_slow_list(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t slot = P.slot_of[0];
+    const uint64_t per_range = (uint64_t)P.wt_per_block * PV_WT;
+    NetCtr c;
+    c.zero();
+    for (uint32_t r = blockIdx.x; r < P.grid_main; r += gridDim.x)
+    for (uint32_t j = threadIdx.x; j < P.slow_cnt[r]; j += blockDim.x) {
+        const uint64_t i = P.slow_list[r * per_range + j];
+        const SAcc R{P.recs, nullptr, 0, 0, 0, 1};
+        const SlowOut so = net_slow_p(Pp, R, P.offs[i], i);
+        Parsed o;
+        o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
+        c.add(o);
+        uint32_t hv = so.caplen;
+        if (hv != PV_NOH) {
+            if (hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
+            __hip_atomic_fetch_add(P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD + hv, 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint64_t lb = r, t = i / PV_WT;
+        if (so.isdns) {
+            const uint32_t q = atomicAdd(P.dq_cnt + lb, 1u);
+            PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(P.dq) + 2 * (lb * per_range + q);
+            dd[0] = so.dm.a;
+            dd[1] = so.dm.b;
+            atomicAdd(P.n_dns, 1u);
+        }
+        const uint64_t ek = so.ek;
+        if (ek) {
+            if (((ek >> 32) & ~1ull) == (P.ip_base >> 32)) {
+                P.iplog32[i] = (uint32_t)ek;
+                if ((ek >> 32) & 1) atomicOr(reinterpret_cast<unsigned long long *>(P.ipdir + t), 1ull << (i & 63));
+            } else {
+                const uint32_t q = atomicAdd(P.ipx_cnt + lb, 1u);
+                P.iplog[lb * per_range + q] = ek;
+                P.ipx_rep[lb * per_range + q] = (uint32_t)i;
+            }
+        }
+        if (P.tcp_emit && so.l4 == 6) atomicOr(reinterpret_cast<unsigned long long *>(P.tmask + t), 1ull << (i & 63));
+    }
+    NetK K;
+    K.sum = P.sum; K.net_groups = P.net_groups; K.net_filter_all = 0;
+    knet_flush(K, slot, c);
+}
+
 // ------------------------------------------------------------------ the lean Net pass, LDS-DMA ring
 // The lean pass with its records staged in LDS by LDS-DMA (global_load_lds_dwordx4), one
 // workgroup per CU of four parsing waves and four producer waves. tools/ring_probe.hip measured
@@ -3420,8 +3706,9 @@ struct CombState {
     uint32_t cnt[CN];
     uint32_t rep[CN];
     uint32_t h[NR];   // entries per region, then the placement cursors
-    uint32_t tb[NR];  // tables (bit per PV_TSLOT) among each region's entries
-    uint32_t wsum[16];
+    uint32_t tb[NR / 2]; // tables among each region's entries (16 bits a region: the run word's
+                         // folded PV_TSLOT bit), two regions a word
+    uint32_t wsum[PV_CB_THREADS / 64];
     uint32_t nsp;
     uint32_t hm; // handlers among the entries (bit 0 Net, 1 DNS)
 };
@@ -3442,8 +3729,8 @@ __device__ __forceinline__ void comb_count(PV_CREF(PvParams) P, St &S, uint64_t 
 {
     const uint32_t r = run_key(P, e0);
     atomicAdd(&S.h[r], 1u);
-    const uint32_t bit = 1u << entry_table(e0);
-    if (!(S.tb[r] & bit)) atomicOr(&S.tb[r], bit);
+    const uint32_t bit = 1u << ((entry_table(e0) & 15u) + 16u * (r & 1u));
+    if (!(S.tb[r >> 1] & bit)) atomicOr(&S.tb[r >> 1], bit);
 }
 #ifndef PV_CB_BUCKET
 #define PV_CB_BUCKET 1 // probe aligned 4-entry buckets (two 16-B LDS reads each), at most 4 (0: 16 dependent
@@ -3581,7 +3868,10 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     TST_DECL
     const uint32_t nreg = 2u << P.reg_log2; // run keys
     for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x) { S.key[j] = 0; S.cnt[j] = 0; S.rep[j] = 0xffffffffu; }
-    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) { S.h[r] = 0; S.tb[r] = 0; }
+    for (uint32_t r = threadIdx.x; r < nreg; r += blockDim.x) {
+        S.h[r] = 0;
+        if (!(r & 1)) S.tb[r >> 1] = 0;
+    }
     if (threadIdx.x == 0) S.nsp = 0;
     __syncthreads();
     TST(0)
@@ -3676,7 +3966,7 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     PV_G uint64_t *col = P.cb_run + (blockIdx.x % 8) * ng8 + blockIdx.x / 8;
     for (uint32_t r = r0; r < r1; r++) {
         const uint32_t c = S.h[r];
-        if ((hm >> (r >> P.reg_log2)) & 1) col[(uint64_t)r * 8 * ng8] = pv_run_word(run, c, S.tb[r]);
+        if ((hm >> (r >> P.reg_log2)) & 1) col[(uint64_t)r * 8 * ng8] = pv_run_word(run, c, (S.tb[r >> 1] >> (16u * (r & 1u))) & 0xffffu);
         S.h[r] = run; // the placement cursor
         run += c;
     }
@@ -3704,10 +3994,14 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
 }
 // LDS: an 8192-entry table with up to 2^10 regions per table (152 KiB), 2048 entries with
 // more (128 KiB); two run keys per region
+#ifndef PV_CB_CN
+#define PV_CB_CN 8192
+#endif
+static_assert(PV_SLOTS == 16, "pv_topn_combine folds a table bit to 16 bits a region");
 extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    topn_combine<8192, 2048>(P);
+    topn_combine<PV_CB_CN, 2048>(P);
 }
 extern "C" __global__ void __launch_bounds__(PV_CB_THREADS) pv_topn_combine_r12(const PvParams *__restrict__ Pp)
 {

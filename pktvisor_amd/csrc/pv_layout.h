@@ -152,7 +152,9 @@ enum {
 // plus linear probing that wraps inside the region, so one workgroup of pv_topn_merge
 // can own a region outright and merge a batch's updates into it in LDS.
 #define PV_REGION_LOG2 12
-#define PV_CB_THREADS 1024 // pv_topn_combine workgroup size
+#ifndef PV_CB_THREADS
+#define PV_CB_THREADS 1024 // pv_topn_combine workgroup size (the host launches the kernel's own bound)
+#endif
 #define PV_MAX_GRID 1024   // Net/DNS-pass workgroups per batch (pv_topn_merge's run table)
 #define PV_MAX_REGIONS_LOG2 12 // table_log2 <= PV_REGION_LOG2 + PV_MAX_REGIONS_LOG2
 #define PV_PROBES 256
@@ -430,6 +432,10 @@ struct PvParams {
     PV_G uint32_t *ipx_rep; // the exception entries' record indices (names of IPv6 keys)
     uint64_t ip_base;     // slot << 60 | TM_IPV4 << 56 | cardinality << 33: the entries' common bits
     uint32_t ip_compact;
+    // span Net pass (pv_net_kernel_span): the records the fast path does not take, deferred to
+    // pv_net_slow_list (record indices at each range's base, each range's count)
+    PV_G uint32_t *slow_list;
+    PV_G uint32_t *slow_cnt;
     PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
     PV_G uint64_t *cb;    // combined update lists sorted by table region, mq_cap entries per workgroup
     PV_G uint32_t *cb_cnt;
