@@ -17,6 +17,7 @@
 // reference estimator replayed exactly from per-coupon first-occurrence indices
 // (HIP for a single bucket, ICON after a union), bit-identical to datasketches.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -146,6 +147,7 @@ extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg_tc(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_span(const PvParams *P);
+extern "C" __global__ void pv_store_blob(PvBlob b, uint4 *dst, uint32_t n16);
 extern "C" __global__ void pv_net_slow_list(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
@@ -2775,6 +2777,18 @@ void dns_shifts_of(int64_t T, const uint64_t *bits, uint64_t n, const pv_index_i
 }
 
 // parameter fields every kernel reads: record access, parse configuration, DNS filters
+// A parameter block to device memory through pv_store_blob's kernel arguments (blocks up to
+// 2 KiB; larger ones by copy)
+static hipError_t upload_params(void *dst, const void *src, size_t bytes, hipStream_t st)
+{
+    if (bytes > sizeof(PvBlob) || ((uintptr_t)dst & 15)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    PvBlob b;
+    memcpy(b.w, src, bytes);
+    const uint32_t n16 = (uint32_t)((bytes + 15) / 16);
+    hipLaunchKernelGGL(pv_store_blob, dim3(1), dim3(PV_BLOB_WORDS), 0, st, b, (uint4 *)dst, n16);
+    return hipGetLastError();
+}
+
 void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n)
 {
     memset(&P, 0, sizeof P);
@@ -2822,7 +2836,7 @@ int dns_prescan(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64
     if (fbits) P.fbits = c->d_fbits;
     hipError_t e;
     *c->h_params = P;
-    if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
+    if (!hip_ok(e = upload_params(c->d_params, c->h_params, sizeof P, st)))
         return c->hipfail(e, "parameter upload");
     const uint64_t tiles = (n + 63) / 64;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + 3) / 4, (uint64_t)c->cus * 8);
@@ -3029,7 +3043,7 @@ int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t
     auto run = [&](bool dry) -> int {
         T.dry = dry ? 1u : 0u;
         if (!hip_ok(e = hipMemsetAsync(c->d_tcpcnt, 0, PVT_WORDS * 4, st)) ||
-            !hip_ok(e = hipMemcpyAsync(c->d_tparams, c->h_tparams, sizeof T, hipMemcpyHostToDevice, st)))
+            !hip_ok(e = upload_params(c->d_tparams, c->h_tparams, sizeof T, st)))
             return c->hipfail(e, "TCP stage upload");
         hipLaunchKernelGGL(pv_tcp_scan, dim3(1), dim3(1024), 0, st, dT);
         if (n_seg) {
@@ -3507,7 +3521,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
         HP(15);
         if (!hip_ok(e = hipMemsetAsync(c->d_nvals + 2, 0, 4, st))) return c->hipfail(e, "parameter upload");
         HP(16);
-        if (!hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
+        if (!hip_ok(e = (*c->h_xparams = X, upload_params(c->d_xparams, c->h_xparams, sizeof X, st))))
             return c->hipfail(e, "parameter upload");
         HP(17);
         hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
@@ -3538,7 +3552,7 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
             uint32_t nvalid = 0;
             if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
             if (nvalid) {
-                if (!hip_ok(e = (*c->h_xparams = X, hipMemcpyAsync(c->d_xparams, c->h_xparams, sizeof X, hipMemcpyHostToDevice, st))))
+                if (!hip_ok(e = (*c->h_xparams = X, upload_params(c->d_xparams, c->h_xparams, sizeof X, st))))
                     return c->hipfail(e, "parameter upload");
                 hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st,
                                    (const PvXactParams *)c->d_xparams, nvalid);
@@ -3628,7 +3642,7 @@ int tcp_filter_bits(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, ui
     Q.fbits = c->d_tfbits;
     c->h_params[1] = Q;
     hipError_t e;
-    if (!hip_ok(e = hipMemcpyAsync(c->d_params + 1, c->h_params + 1, sizeof Q, hipMemcpyHostToDevice, st)))
+    if (!hip_ok(e = upload_params(c->d_params + 1, c->h_params + 1, sizeof Q, st)))
         return c->hipfail(e, "parameter upload");
     const uint32_t tiles = (nmsg + 63) / 64;
     hipLaunchKernelGGL(pv_dns_tcp_filter, dim3(std::min<uint32_t>((tiles + 3) / 4, (uint32_t)c->cus * 8)), dim3(256), 0, st,
@@ -3863,11 +3877,6 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.ip_compact = lean && !ring ? 1u : 0u;
     P.ip_base = ((uint64_t)P.slot_of[0] << 60) | ((uint64_t)TM_IPV4 << 56) |
                 ((uint64_t)((c->net_groups & PV_NET_CARDINALITY) ? 1 : 0) << 33);
-    flush_fills(c);
-    *c->h_params = P;
-    if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
-        return c->hipfail(e, "parameter upload");
-    hipEventRecord(c->ev_start, st);
     const bool tc = (c->net_groups & PV_NET_TOP_IPS) && c->reg_waves != 8;
     // PV_NET_KERNEL=span: the span-load pass with the general path deferred (top-IPs groups)
     const bool span = lean && tc && !ring && regw && force && !strcmp(force, "span");
@@ -3881,17 +3890,23 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         }
         P.slow_list = c->d_slow;
         P.slow_cnt = c->d_slow + c->slow_cap; // written for every range by the span pass
-        *c->h_params = P;
-        if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
-            return c->hipfail(e, "parameter upload");
     }
+    flush_fills(c);
+    *c->h_params = P;
+    if (!hip_ok(e = upload_params(c->d_params, c->h_params, sizeof P, st)))
+        return c->hipfail(e, "parameter upload");
     c->net_kernel = general ? "pv_net_kernel"
                             : (lean ? (span ? "pv_net_kernel_span" : ring ? "pv_net_kernel_fast"
                                             : (!regw ? "pv_net_kernel_ring"
                                                      : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : (tc ? "pv_net_kernel_reg_tc" : "pv_net_kernel_reg"))))
                                     : "pv_net_kernel_ns");
-    if (general) hipLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-    else if (lean && ring) hipLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    // pv_kernel_timing (bench roofline): the record-parse kernel alone, timed by the start and
+    // end stamps of its own dispatch packet (hipExtLaunchKernelGGL), so no event marker packets
+    // sit in the stream between the step's kernels
+    const PvParams *dp = (const PvParams *)c->d_params;
+    hipEvent_t e0 = c->ev_start, e1 = c->ev_stop;
+    if (general) hipExtLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
+    else if (lean && ring) hipExtLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     else if (lean && !regw) {
         // its block size is the kernel's own launch bound (parsing + producer waves; tuning
         // builds change the layout)
@@ -3901,19 +3916,18 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             ring_threads = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(pv_net_kernel_ring)) == hipSuccess
                                ? fa.maxThreadsPerBlock : 512;
         }
-        hipLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(ring_threads), 0, st, (const PvParams *)c->d_params);
+        hipExtLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(ring_threads), 0, st, e0, e1, 0, dp);
     }
     else if (span) {
-        hipLaunchKernelGGL(pv_net_kernel_span, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-        hipLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (const PvParams *)c->d_params);
+        hipExtLaunchKernelGGL(pv_net_kernel_span, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
+        hipExtLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (hipEvent_t) nullptr, e1, 0, dp);
     }
-    else if (lean && c->reg_waves == 8) hipLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, (const PvParams *)c->d_params);
-    else if (lean && tc) hipLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-    else if (lean) hipLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
-    else hipLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, (const PvParams *)c->d_params);
+    else if (lean && c->reg_waves == 8) hipExtLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, e0, e1, 0, dp);
+    else if (lean && tc) hipExtLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
+    else if (lean) hipExtLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
+    else hipExtLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
-    hipEventRecord(c->ev_stop, st); // pv_kernel_timing: the record-parse kernel alone (bench roofline)
     if (P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL))
         hipLaunchKernelGGL(pv_dns_suffix, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // the DNS pass walks the logical grid's ranges with its resident grid
@@ -4807,7 +4821,7 @@ int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_
         launch_fill32(c, c->d_status + ST_FLAGS, 1, 0);
         flush_fills(c);
         *c->h_params = P;
-        if (!hip_ok(e = hipMemcpyAsync(c->d_params, c->h_params, sizeof P, hipMemcpyHostToDevice, st)))
+        if (!hip_ok(e = upload_params(c->d_params, c->h_params, sizeof P, st)))
             return c->hipfail(e, "parameter upload");
         hipLaunchKernelGGL(pv_dnstap_kernel, dim3(blocks), dim3(256), 0, st, (const PvParams *)c->d_params);
         if (P.want_events) hipLaunchKernelGGL(pv_xact_compact, dim3(blocks), dim3(256), 0, st, (const PvParams *)c->d_params, 0u, 0u);

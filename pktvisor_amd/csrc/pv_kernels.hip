@@ -5091,6 +5091,13 @@ extern "C" __global__ void pv_fill_multi(PvFillList L)
     }
 }
 
+// Stores a by-value parameter block (n16 16-B words) to device memory: one workgroup.
+extern "C" __global__ void __launch_bounds__(PV_BLOB_WORDS) pv_store_blob(PvBlob b, uint4 *dst, uint32_t n16)
+{
+    const uint32_t t = threadIdx.x;
+    if (t < n16) dst[t] = make_uint4(b.w[4 * t], b.w[4 * t + 1], b.w[4 * t + 2], b.w[4 * t + 3]);
+}
+
 // Zero a device region of 64-bit words (grid-stride).
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v)
 {

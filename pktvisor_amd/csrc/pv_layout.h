@@ -489,6 +489,14 @@ struct PvFillList {
     uint32_t n;
 };
 
+// A parameter block passed by value to pv_store_blob (kernel arguments): the per-batch upload
+// without a copy command (a small host-to-device copy is a blit dispatch plus the stream's
+// dependency on it)
+#define PV_BLOB_WORDS 128 // 16-B words (2 KiB)
+struct PvBlob {
+    uint32_t w[4 * PV_BLOB_WORDS];
+};
+
 struct PvXactParams {
     PvParams P;            // record access + top-N tables (slow transaction names)
     const PV_G PvXEvent *events;
