@@ -148,6 +148,7 @@ extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg_tc(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_span(const PvParams *P);
 extern "C" __global__ void pv_store_blob(PvBlob b, uint4 *dst, uint32_t n16);
+extern "C" __global__ void pv_fill_store(PvFillList L, PvBlob b, uint4 *dst, uint32_t n16);
 extern "C" __global__ void pv_net_slow_list(const PvParams *P);
 extern "C" __global__ void pv_rec_sizes(const uint8_t *recs, const uint32_t *offs, const uint8_t *trecs, const uint32_t *toffs,
                                         const uint32_t *idx, uint32_t stride, uint32_t n, uint32_t *sizes);
@@ -2789,6 +2790,27 @@ static hipError_t upload_params(void *dst, const void *src, size_t bytes, hipStr
     return hipGetLastError();
 }
 
+// The queued fills and a parameter block in one launch (pv_fill_store) when both fit; else the
+// fills, then upload_params
+static hipError_t fill_and_upload(pv_ctx *c, void *dst, const void *src, size_t bytes, hipStream_t st)
+{
+    static const char *nofuse = getenv("PV_FILL_FUSE"); // (=0: separate launches, A/B runs)
+    if (!c->fills.n || st != c->stream || bytes > sizeof(PvBlob) || ((uintptr_t)dst & 15) || (nofuse && !strcmp(nofuse, "0"))) {
+        flush_fills(c);
+        return upload_params(dst, src, bytes, st);
+    }
+    PvBlob b;
+    memcpy(b.w, src, bytes);
+    const uint32_t n16 = (uint32_t)((bytes + 15) / 16);
+    hipSetDevice(c->device);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((c->fills_max + 255) / 256, 4096);
+    static_assert(PV_BLOB_WORDS <= 256, "the blob's words in the first workgroup");
+    hipLaunchKernelGGL(pv_fill_store, dim3(blocks), dim3(256), 0, c->stream, c->fills, b, (uint4 *)dst, n16);
+    c->fills.n = 0;
+    c->fills_max = 0;
+    return hipGetLastError();
+}
+
 void params_common(pv_ctx *c, PvParams &P, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t n)
 {
     memset(&P, 0, sizeof P);
@@ -3891,9 +3913,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         P.slow_list = c->d_slow;
         P.slow_cnt = c->d_slow + c->slow_cap; // written for every range by the span pass
     }
-    flush_fills(c);
     *c->h_params = P;
-    if (!hip_ok(e = upload_params(c->d_params, c->h_params, sizeof P, st)))
+    if (!hip_ok(e = fill_and_upload(c, c->d_params, c->h_params, sizeof P, st)))
         return c->hipfail(e, "parameter upload");
     c->net_kernel = general ? "pv_net_kernel"
                             : (lean ? (span ? "pv_net_kernel_span" : ring ? "pv_net_kernel_fast"

@@ -5076,7 +5076,16 @@ extern "C" __global__ void pv_xact_compact(const PvParams *__restrict__ Pp, uint
 
 // Fills a list of device regions in one launch (bucket-slot clears and the per-batch
 // status reset), grid-stride over every segment.
-extern "C" __global__ void pv_fill_multi(PvFillList L)
+__device__ __forceinline__ void fill_segs(const PvFillList &L);
+extern "C" __global__ void pv_fill_multi(PvFillList L) { fill_segs(L); }
+// the fills and a parameter block (pv_store_blob's store) in one launch: the batch's first
+extern "C" __global__ void pv_fill_store(PvFillList L, PvBlob b, uint4 *dst, uint32_t n16)
+{
+    const uint32_t t = threadIdx.x;
+    if (blockIdx.x == 0 && t < n16) dst[t] = make_uint4(b.w[4 * t], b.w[4 * t + 1], b.w[4 * t + 2], b.w[4 * t + 3]);
+    fill_segs(L);
+}
+__device__ __forceinline__ void fill_segs(const PvFillList &L)
 {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint32_t k = 0; k < L.n; k++) {
