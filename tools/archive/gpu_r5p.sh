@@ -14,5 +14,5 @@ for mb in 64 128 256; do
   PV_INGEST_CHUNK_MB=$mb timeout -k 10 600 python3 -u bench.py --config 5 --steps 2 --warmup 1 > $O/c5_chunk$mb.log 2>&1 || { tail -5 $O/c5_chunk$mb.log; continue; }
   echo "chunk $mb: $(tail -1 $O/c5_chunk$mb.log | cut -c1-260)"
 done
-R5_DIR=r5n bash tools/gpu_r5n.sh
+R5_DIR=r5n bash tools/archive/gpu_r5n.sh
 echo done
