@@ -582,9 +582,12 @@ int pv_comm_values_select(pv_ctx *ctx);
 int pv_slow_x_finish(pv_ctx *ctx, pv_allreduce_fn allreduce, void *user);
 int pv_comm_slow_finish(pv_ctx *ctx);
 
-/* Device time of the Net-pass kernel (pv_net_kernel), from HIP events
- * recorded on the launch stream around every launch since the last reset:
- * total milliseconds and number of launches. */
+/* Device time of the Net-pass kernel (pv_net_kernel): the start and end stamps of its dispatch
+ * packet (HIP events of hipExtLaunchKernelGGL), summed over the stamped launches since the last
+ * reset: total milliseconds and number of stamped launches. Which launches are stamped is
+ * pv_set_kernel_timing's: every `every`-th batch, 0 (the default) none. A stamped dispatch
+ * leaves the device idle for ~14 us around it, so a measurement samples. */
+int pv_set_kernel_timing(pv_ctx *ctx, uint32_t every);
 /* The Net-pass kernel the last span launched ("pv_net_kernel_reg", "pv_net_kernel", ...): the
  * name rocprofv3 reports for the launches pv_kernel_timing times. */
 const char *pv_net_kernel_name(pv_ctx *ctx);

@@ -712,10 +712,12 @@ struct pv_ctx {
     // device fills not launched yet (launch_fill*; one pv_fill_multi per flush_fills)
     PvFillList fills{};
     uint64_t fills_max = 0;
-    // kernel timing (pv_kernel_timing)
+    // kernel timing (pv_kernel_timing): the Net pass of every timing_every-th batch (0: none)
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     double kernel_ms = 0;
     uint64_t kernel_launches = 0;
+    uint32_t timing_every = 0;
+    uint64_t timing_ctr = 0;
     // RCCL communicator (pv_comm_*)
     ncclComm_t comm = nullptr;
     int comm_ranks = 0, comm_rank = 0;
@@ -3925,7 +3927,10 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     // end stamps of its own dispatch packet (hipExtLaunchKernelGGL), so no event marker packets
     // sit in the stream between the step's kernels
     const PvParams *dp = (const PvParams *)c->d_params;
-    hipEvent_t e0 = c->ev_start, e1 = c->ev_stop;
+    // (stamping a dispatch costs ~14 us of idle around it: only the batches pv_set_kernel_timing
+    // asks for are stamped)
+    const bool timed = c->timing_every && (c->timing_ctr++ % c->timing_every) == 0;
+    hipEvent_t e0 = timed ? c->ev_start : nullptr, e1 = timed ? c->ev_stop : nullptr;
     if (general) hipExtLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     else if (lean && ring) hipExtLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     else if (lean && !regw) {
@@ -3985,7 +3990,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     HP(4);
     {
         float ms = 0;
-        if (hipEventElapsedTime(&ms, c->ev_start, c->ev_stop) == hipSuccess) { c->kernel_ms += ms; c->kernel_launches++; }
+        if (timed && hipEventElapsedTime(&ms, c->ev_start, c->ev_stop) == hipSuccess) { c->kernel_ms += ms; c->kernel_launches++; }
     }
     // the parts this batch wrote are no longer clean
     // ---- DNS over TCP: the stage of a one-span batch (its segments came from the Net pass),
@@ -6898,6 +6903,13 @@ int pv_comm_destroy(pv_ctx *c)
     if (!c->comm) return 0;
     ncclCommDestroy(c->comm);
     c->comm = nullptr;
+    return 0;
+}
+
+int pv_set_kernel_timing(pv_ctx *c, uint32_t every)
+{
+    c->timing_every = every;
+    c->timing_ctr = 0;
     return 0;
 }
 
