@@ -585,6 +585,8 @@ struct pv_ctx {
     uint64_t *d_stamps = nullptr; // diagnostic phase stamps (PV_STAMPS env + -DPV_STAMPS build)
     int cus = 256;
     int wg_per_cu = 3;     // grid workgroups per CU (the batch's partition)
+    bool wg_forced = false; // PV_NET_WGCU set: no per-batch choice
+    bool dns_heavy = false; // the last batch was mostly DNS messages: four ranges per CU
     int reg_wg_per_cu = 1; // workgroups per CU of the register-window Net pass
     uint32_t cb_fan = 1;   // grid ranges per top-N combine workgroup
     int reg_waves = 4;     // its waves per workgroup (4 or 8; PV_REG_WAVES)
@@ -2441,7 +2443,7 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         // three workgroups per CU; the register-window Net pass walks it with one workgroup per
         // CU (reg_wg_per_cu). PV_NET_WGCU / PV_REG_WGCU override them for A/B runs
         c->wg_per_cu = 3;
-        if (const char *w = getenv("PV_NET_WGCU")) c->wg_per_cu = std::max(1, atoi(w));
+        if (const char *w = getenv("PV_NET_WGCU")) { c->wg_per_cu = std::max(1, atoi(w)); c->wg_forced = true; }
         if (const char *w = getenv("PV_REG_WGCU")) c->reg_wg_per_cu = std::max(1, atoi(w));
         if (const char *w = getenv("PV_REG_WAVES")) c->reg_waves = atoi(w) == 8 ? 8 : 4;
         {
@@ -3808,7 +3810,11 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     const uint64_t tiles = (n + 63) / 64; // 64-record wave tiles
     // persistent grid: exactly the workgroups that are resident at once (LDS/VGPR
     // occupancy), each owning a contiguous run of wave tiles
-    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->cus * c->wg_per_cu);
+    // (a batch after one that was mostly DNS messages takes four ranges per CU: the DNS pass,
+    // combine and merge of such batches gain from the finer partition, C3 2.16 -> 2.11 ms, while
+    // Net-heavy batches lose, C2 0.450 -> 0.465; profiles/r5/experiments/r5oo)
+    const int wgcu = !c->wg_forced && c->dns_heavy ? std::max(c->wg_per_cu, 4) : c->wg_per_cu;
+    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->cus * wgcu);
     P.wt_per_block = (uint32_t)((tiles + grid - 1) / grid);
     P.rec_bytes = rec_bytes;
     {
@@ -3987,6 +3993,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         !hip_ok(e = hipStreamSynchronize(st)))
         return c->hipfail(e, "kernel execution");
     memcpy(status, c->h_status, sizeof status);
+    c->dns_heavy = (uint64_t)status[ST_NDNS] * 2 > n;
     HP(4);
     {
         float ms = 0;
