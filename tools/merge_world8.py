@@ -3,7 +3,8 @@
 Without RANK in the environment this starts WORLD (default 8) rank processes of itself on
 127.0.0.1 (gloo: RCCL needs one GPU per rank, so the exchange here is host blobs and gloo
 all-reduces; on an 8-GPU node the same steps run on the library's RCCL communicator). Each rank
-generates its contiguous shard of a C5-shape stream (--records in total, C4 records at 1 us),
+generates its contiguous shard of a C5-shape stream (--records in total, C4 records at 1 us; --config 2:
+C2 records, the bench's N > 1 shape),
 processes it under the global period plan (dist.process_shard), and then times, separately:
   state merge    dist.merge_window(finalize=False): edges, slow tops, bucket all-reduce, top-N
                  entries to their region owners (what bench.py --gpus N runs every step);
@@ -50,7 +51,7 @@ def rank_main(args):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = pvdist.shard_range(args.records, world, rank)
     t = time.time()
-    buf, used = synth.stream_shard(4, lo, hi, synth.SEEDS[5] + rank)
+    buf, used = synth.stream_shard(args.config, lo, hi, synth.SEEDS[5] + rank)
     recs = buf[:used]
     idx = pa.RecordIndex(recs, max_records=hi - lo, threads=2)
     if rank == 0:
@@ -113,7 +114,7 @@ def rank_main(args):
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         if rank == 0:
             print(json.dumps({
-                "tool": "merge_world8", "world": world, "records": args.records, "records_per_rank": hi - lo,
+                "tool": "merge_world8", "world": world, "config": args.config, "records": args.records, "records_per_rank": hi - lo,
                 "transport": "gloo, ranks sharing one GPU (host blobs + gloo all-reduce)",
                 "process_shard_s_max": round(float(v[0]), 3),
                 "state_merge_ms_max": round(float(v[1]) * 1e3, 1), "finalize_ms_max": round(float(v[2]) * 1e3, 1),
@@ -130,6 +131,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--records", type=int, default=100_000_000)
+    ap.add_argument("--config", type=int, default=4, help="record shape: 4 = C4 / C5 stream (default), 2 = C2 (the bench's N > 1 step)")
     a = ap.parse_args()
     if "RANK" in os.environ:
         rank_main(a)
