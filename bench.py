@@ -4,11 +4,15 @@
 python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--records R]
 
 One step = one pass of the fused Net v1 + DNS v1 hot path over one batch of
-synthetic pcap records already resident in HBM: bucket reset, the parse kernel
-(pv_net_kernel, pv_dns_kernel, the top-N merge kernels), DNS transaction pairing when the batch has DNS, the status
-read-back, and - for N > 1 - the RCCL all-reduce of the live buckets over xGMI.
-Each rank processes its own shard of R records (weak scaling). Rank 0 prints
-one JSON line. The default workload is BASELINE.json configs[1] (C2: 10M x 64 B
+synthetic pcap records already resident in HBM, added to the live window: the parse
+kernels (pv_net_kernel, pv_dns_kernel, the top-N merge kernels), DNS transaction pairing
+when the batch has DNS, the status read-back. Each rank processes its own shard of R
+records per step (weak scaling). For N > 1 the window is read once after the K steps,
+inside the timed region, as pktvisord merges its handlers at read time
+(src/Policies.cpp:420-446, src/AbstractMetricsManager.h:177-195): merge_window (windows
+checked aligned, DNS shard edges, RCCL SUM / MIN all-reduce of the buckets over xGMI,
+top-N entries to their region owners) and finalize_window (leading entries + names, exact
+distributed quantile selection), reported as `merge`. Rank 0 prints one JSON line. The default workload is BASELINE.json configs[1] (C2: 10M x 64 B
 UDP, host_spec 10.0.0.0/8) with both handlers attached, the config the
 north-star roofline target is quoted on.
 """
@@ -48,12 +52,16 @@ def main():
     ap.add_argument("--net-groups", type=int, default=0, help="pv_net_group bits (0 = reference defaults)")
     ap.add_argument("--dns-groups", type=int, default=0, help="pv_dns_group bits (0 = reference defaults)")
     ap.add_argument("--read-ceiling", action="store_true", help="also time a plain read of the blob (HBM ceiling)")
+    ap.add_argument("--reset-each-step", action="store_true",
+                    help="reset the window before every step (rounds 1-5's step; N = 1 only)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip timing the host-memory path (record blob in host RAM -> index -> H2D -> kernels)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.reset_each_step and world > 1:
+        raise SystemExit("bench: --reset-each-step is a single-GPU step (the read merges the accumulated window)")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
@@ -92,25 +100,32 @@ def main():
         uid = [pa.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         h.comm_init(uid[0], world, rank)
-    merge_ms = []
 
     def step():
-        h.reset()
+        # one batch into the live window (no reset: the window accumulates the steps' batches,
+        # as a capture's stream does)
+        if args.reset_each_step:
+            h.reset()
         h.process_device(d_recs.data_ptr(), d_offs.data_ptr(), idx)
-        if world > 1:
-            # the whole state merge every step (dist.merge_window): windows checked aligned, DNS
-            # shard edges, SUM / MIN all-reduce of the buckets, top-N entries to their region owners
-            # and merged there; the read view (names of the leading entries, quantiles) is
-            # assembled once after the timed steps (finalize_window, timed separately)
-            h.synchronize()
-            tm = time.perf_counter()
-            pvdist.merge_window(h, device, comm="pv", finalize=False)
-            merge_ms.append((time.perf_counter() - tm) * 1e3)
-        else:
-            h.synchronize()
+        h.synchronize()
+
+    def read():
+        # the merged read view of every rank's window, once per read (dist.merge_window with
+        # finalize): state merge, then the read view
+        tm = time.perf_counter()
+        pvdist.merge_window(h, device, comm="pv", finalize=False)
+        h.synchronize()
+        tf = time.perf_counter()
+        pvdist.finalize_window(h, comm="pv")
+        h.synchronize()
+        return (tf - tm) * 1e3, (time.perf_counter() - tf) * 1e3
 
     for _ in range(args.warmup):
+        h.reset()
         step()
+    if world > 1 and args.warmup:
+        read()  # the merge's own buffers and RCCL channels come up outside the timed region
+    h.reset()
     # the Net pass's dispatch stamps on every TIMING_EVERY-th timed step (a stamped dispatch
     # leaves the device idle ~14 us around it; the others run as a deployment would)
     h.set_kernel_timing(TIMING_EVERY)
@@ -125,6 +140,9 @@ def main():
         step()  # ends with a device synchronisation
         step_ms.append((time.perf_counter() - ts) * 1e3)
     h.synchronize()
+    tr = time.perf_counter()
+    merge_ms = read() if world > 1 else (0.0, 0.0)
+    steps_s = tr - t0
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -133,27 +151,28 @@ def main():
     kms, launches = h.kernel_timing(reset=True)
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed, kms / max(launches, 1)], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kms / max(launches, 1), steps_s, merge_ms[0], merge_ms[1]], dtype=torch.float64,
+                         device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        elapsed, kernel_ms, steps_s = float(t[0]), float(t[1]), float(t[2])
+        merge_ms = (float(t[3]), float(t[4]))
     else:
         kernel_ms = kms / max(launches, 1)
 
-    finalize_ms = None
-    if world > 1:
-        # the merged read view, once (timed apart from the steps)
-        dist.barrier()
-        tf = time.perf_counter()
-        pvdist.finalize_window(h, comm="pv")
-        finalize_ms = (time.perf_counter() - tf) * 1e3
-    # parity sanity on the final state (not timed)
+    # sanity on the final state (not timed): every step's batch of every rank is in the window
+    # (for N > 1 the merged window every rank now holds)
     out = h.window_json(0, merged=False)
     events = out["packets"]["events"]
-    if events != n * world:
+    if args.reset_each_step:
+        expect = n
+    else:
+        expect = n * world * args.steps
+    if events != expect:
         if not os.environ.get("PVGPU_LIB"):
-            raise SystemExit(f"bench: bucket holds {events} events, expected {n * world}")
+            raise SystemExit(f"bench: bucket holds {events} events, expected {expect}")
         # a tuning variant (lean levels) skips work on purpose
-        print(f"bench: tuning variant: bucket holds {events} events, expected {n * world}", file=sys.stderr)
+        print(f"bench: tuning variant: bucket holds {events} events, expected {expect}",
+              file=sys.stderr)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -177,7 +196,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": WORKLOADS[args.config], "records_per_gpu": n,
                        "bytes_per_record": round(algo_bytes / n, 2), "handlers": "net v1 + dns v1 (default groups)",
-                       "parallelism": f"dp{world} (record shards, per-step RCCL merge: bucket all-reduce + top-N owner exchange)"},
+                       "parallelism": f"dp{world} (record shards; one read-time merge of the window after the "
+                                      "steps: RCCL bucket all-reduce + top-N owner exchange)" if world > 1 else "dp1"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": prof.get("hbm_bytes_per_launch"),
                          "kernel": h.net_kernel_name(), "kernel_ms": round(kernel_ms, 4),
@@ -206,12 +226,13 @@ def main():
         if args.net_groups or args.dns_groups:
             line["groups"] = {"net": args.net_groups, "dns": args.dns_groups}
         if world > 1:
-            line["merge"] = {"per_step_ms_median": round(float(np.median(merge_ms[-args.steps:])), 4),
-                             "finalize_ms": round(finalize_ms, 3),
-                             "what": "every step: pv_comm_allgather window check, DNS shard edges, pv_comm_allreduce_window "
-                                     "(SUM/MIN), pv_comm_merge_topn (top-N entries to region owners over RCCL, merged on "
-                                     "the device); once after the steps: finalize_window (leading entries + names, exact "
-                                     "distributed quantile selection)"}
+            line["merge"] = {"state_merge_ms": round(merge_ms[0], 3), "finalize_ms": round(merge_ms[1], 3),
+                             "steps_ms": round(steps_s * 1e3, 3),
+                             "what": "once per read, inside the timed region after the K steps (max over ranks): "
+                                     "merge_window = pv_comm_allgather window check, DNS shard edges, "
+                                     "pv_comm_allreduce_window (SUM/MIN), pv_comm_merge_topn (top-N entries to region "
+                                     "owners over RCCL, merged on the device); finalize_window = leading entries + "
+                                     "names, exact distributed quantile selection"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         print(json.dumps(line), flush=True)
@@ -401,10 +422,10 @@ def cpu_model() -> str:
 def cpu_baseline(cfg: int, seconds: float):
     """The oracle (CPU restatement of the reference handlers, oracle/pv_oracle.cpp) on a
     bounded sample of the same workload, timed on this host: one thread, then one
-    independent oracle instance per thread on up to 16 threads (the box's CPU share),
-    each over the same in-memory pcap, as the reference's per-input handler threads
-    would run on separate captures. The multi-thread rate is reported; the one-thread
-    rate is in `sample`."""
+    independent oracle instance per host core (`nproc`, as SURVEY.md §8(d) and BASELINE.md
+    ask), each over the same in-memory pcap, as the reference's per-input handler threads
+    would run on separate captures (ctypes releases the GIL for the call). The all-core rate
+    is `value`; the one-thread rate is `single_thread`."""
     import threading
     from pktvisor_amd import synth
     from tests.oracle_ctypes import load
@@ -423,8 +444,20 @@ def cpu_baseline(cfg: int, seconds: float):
         orc.run_bytes(pcap, **cfgs)
     dt1 = time.perf_counter() - t0
     rate1 = n * reps / dt1
-    threads = max(1, min(16, os.cpu_count() or 1))
-    reps_t = max(1, int(round(seconds / 2 / (n / rate1))))
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = nproc
+    quota = cgroup_cpus()
+    threads = max(1, nproc)
+    reps_t = 1
+    # each thread's sample sized so the all-core leg takes about seconds / 2 of wall time on the
+    # cores this process may actually run on (affinity, cgroup quota)
+    eff = max(1.0, min(float(avail), quota or float(nproc)))
+    n_t = int(max(10_000, min(n, rate1 * seconds / 2 * eff / threads)))
+    if n_t != n:
+        pcap = synth.pcap_bytes(cfg, n_t)
 
     def work():
         for _ in range(reps_t):
@@ -436,11 +469,22 @@ def cpu_baseline(cfg: int, seconds: float):
     for t in ts:
         t.join()
     dtn = time.perf_counter() - t0
-    raten = n * reps_t * threads / dtn
+    raten = n_t * reps_t * threads / dtn
     return {"value": round(raten / 1e6, 4), "unit": "Mpkt/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-            "sample": (f"{n} records of the same synthetic workload (in-memory pcap), oracle/pv_oracle.cpp: "
-                       f"{threads} threads x {reps_t} passes in {dtn:.1f} s; one thread {rate1 / 1e6:.3f} Mpkt/s "
-                       f"({reps} passes, {dt1:.1f} s)")}
+            "single_thread": round(rate1 / 1e6, 4), "nproc": nproc, "affinity_cpus": avail,
+            "cgroup_cpu_quota": quota,
+            "sample": (f"the same synthetic workload as in-memory pcaps, oracle/pv_oracle.cpp: {threads} threads "
+                       f"(nproc) x {n_t} records in {dtn:.1f} s; one thread {n} records x {reps} passes in {dt1:.1f} s "
+                       f"({rate1 / 1e6:.3f} Mpkt/s)")}
+
+
+def cgroup_cpus():
+    """the CPU quota of this process's cgroup in cores (cpu.max), or None when unlimited"""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
 
 
 if __name__ == "__main__":

@@ -638,6 +638,7 @@ class PvHandlers:
                         device, table_log2, max_records, topn_percentile_threshold, net_filter_all, net2_groups,
                         dns2_groups, deep_sample_rate)
         self.num_periods = num_periods
+        self.device = device  # HIP device ordinal (-1: the caller's current device at pv_create)
         self.ctx = ctypes.c_void_p()
         rc = self.lib.pv_create(ctypes.byref(cfg), ctypes.byref(self.ctx))
         if rc:

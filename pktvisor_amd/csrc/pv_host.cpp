@@ -707,6 +707,11 @@ struct pv_ctx {
     PvParams *d_xp = nullptr;
     uint32_t x_ranks = 0, x_rank = 0;
     bool x_view_on = false;
+    // a merge across ranks (bucket all-reduce, top-N owner exchange, shard edges, merged values)
+    // rewrote this context's window with other shards' data: the merged window is terminal, and
+    // batches are refused until pv_reset (merged_refuse)
+    bool merged = false;
+    const char *merged_by = nullptr;
     std::map<uint32_t, std::map<uint64_t, std::pair<uint64_t, std::string>>> x_view; // part << 16 | slot mask -> key -> (estimate, name)
     // merged quantile inputs (pv_values_x_select): per (DNS slot set as a bit mask, value kind)
     std::map<std::pair<uint32_t, uint32_t>, XQuant> xq;
@@ -2185,6 +2190,20 @@ int window_slots(pv_ctx *c, const Window &w, uint32_t period, bool merged, std::
 
 } // namespace
 
+// the merge entry points rewrite the window with other shards' data (note at pv_ctx::merged)
+static void mark_merged(pv_ctx *c, const char *by)
+{
+    if (!c) return;
+    c->merged = true;
+    if (!c->merged_by) c->merged_by = by;
+}
+static int merged_refuse(pv_ctx *c)
+{
+    if (!c->merged) return 0;
+    return c->fail(PV_EINVAL, "the window was merged across ranks (%s): a merged window is read-only until pv_reset",
+                   c->merged_by ? c->merged_by : "merge");
+}
+
 // ====================================================================== C ABI
 extern "C" {
 
@@ -2632,6 +2651,8 @@ int pv_reset(pv_ctx *c)
     c->remote_topn.clear();
     c->x_ranks = c->x_rank = 0;
     c->x_view_on = false;
+    c->merged = false;
+    c->merged_by = nullptr;
     c->x_view.clear();
     c->xq_on = false;
     c->xq.clear();
@@ -3814,7 +3835,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     // combine and merge of such batches gain from the finer partition, C3 2.16 -> 2.11 ms, while
     // Net-heavy batches lose, C2 0.450 -> 0.465; profiles/r5/experiments/r5oo)
     const int wgcu = !c->wg_forced && c->dns_heavy ? std::max(c->wg_per_cu, 4) : c->wg_per_cu;
-    uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)c->cus * wgcu);
+    uint32_t grid = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(tiles, (uint64_t)c->cus * wgcu), PV_MAX_GRID);
     P.wt_per_block = (uint32_t)((tiles + grid - 1) / grid);
     P.rec_bytes = rec_bytes;
     {
@@ -4256,6 +4277,7 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
                       const uint32_t *sc_idx, const uint32_t *sc_sec, void *stream)
 {
     std::lock_guard<std::mutex> g(c->mu);
+    if (int rc = merged_refuse(c)) return rc;
     hipSetDevice(c->device);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     hipStream_t saved = c->stream;
@@ -4657,6 +4679,7 @@ int pv_set_dnstap_only_hosts(pv_ctx *c, const char *hosts)
 int pv_process_dnstap(pv_ctx *c, const uint8_t *buf, size_t bytes, uint32_t msg_type_mask)
 {
     std::lock_guard<std::mutex> g(c->mu);
+    if (int rc = merged_refuse(c)) return rc;
     hipSetDevice(c->device);
     std::vector<pvi::DtMessage> msgs;
     uint32_t frames = 0;
@@ -5154,6 +5177,10 @@ int process_host_block(pv_ctx *c, const uint8_t *recs, size_t bytes);
 
 int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
 {
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (int rc = merged_refuse(c)) return rc;
+    }
     // (the pcap input's BPF filter, PcapInputStream.cpp:485-488, runs on the device on each batch:
     // pv_process_device)
     return process_host_block(c, recs, bytes);
@@ -5369,6 +5396,7 @@ int pv_set_end_tstamp(pv_ctx *c, int64_t sec, int64_t nsec)
 int pv_check_period_shift(pv_ctx *c, int64_t sec, int64_t nsec)
 {
     std::lock_guard<std::mutex> g(c->mu);
+    if (int rc = merged_refuse(c)) return rc;
     hipSetDevice(c->device);
     if (!c->started || c->cfg.num_periods <= 1) return 0;
     if (sec >= c->net.next_shift_sec) {
@@ -5824,6 +5852,7 @@ int pv_export_topn(pv_ctx *c, uint8_t **buf, size_t *bytes)
 
 int pv_merge_topn(pv_ctx *c, const uint8_t *buf, size_t bytes)
 {
+    mark_merged(c, "pv_merge_topn");
     size_t p = 0;
     while (p + 22 <= bytes) {
         uint32_t s; uint64_t key, cnt; uint16_t l;
@@ -6076,6 +6105,7 @@ int pv_topn_x_export(pv_ctx *c, uint32_t W, uint32_t me, uint8_t **blob, size_t 
 
 int pv_topn_x_import(pv_ctx *c, uint32_t W, uint32_t me, const uint8_t *const *blobs, const size_t *sizes)
 {
+    mark_merged(c, "pv_topn_x_import");
     if (W < 1 || me >= W || W > 1024) return c->fail(PV_EINVAL, "rank %u of %u", me, W);
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
@@ -6095,6 +6125,10 @@ int pv_topn_x_import(pv_ctx *c, uint32_t W, uint32_t me, const uint8_t *const *b
         if (h[0] != X_MAGIC || h[1] != W || h[2] != q || h[3] != T.n || h[4] != nreg || memcmp(b + 20, T.tb, 4 * (size_t)T.n))
             return c->fail(PV_EINVAL, "exchange blob %u does not match this rank's windows", q);
         size_t at = 20 + 4 * (size_t)T.n;
+        // the fixed sections (region offsets, per-owner totals, counts) must lie in the blob
+        // before any of them is read
+        if (at + (size_t)T.n * nreg * 8 + (size_t)W * 8 + (size_t)E * 4 > sizes[q])
+            return c->fail(PV_EINVAL, "exchange blob %u truncated", q);
         src[q].ro = reinterpret_cast<const uint64_t *>(b + at);
         at += (size_t)T.n * nreg * 8;
         src[q].dtot = reinterpret_cast<const uint64_t *>(b + at);
@@ -6103,8 +6137,17 @@ int pv_topn_x_import(pv_ctx *c, uint32_t W, uint32_t me, const uint8_t *const *b
         at += (size_t)E * 4;
         src[q].ent = b + at;
         uint64_t all = 0;
-        for (uint32_t d = 0; d < W; d++) all += src[q].dtot[d];
+        for (uint32_t d = 0; d < W; d++) {
+            if (src[q].dtot[d] > (uint64_t)1 << 40) return c->fail(PV_EINVAL, "exchange blob %u: bad entry total", q);
+            all += src[q].dtot[d];
+        }
         if (at + all * 16 > sizes[q]) return c->fail(PV_EINVAL, "exchange blob %u truncated", q);
+        // the counts of this rank's slice (owner me: cells [2 * PV_SLOTS * lo, 2 * PV_SLOTS * hi))
+        // index the receive list on the device (pv_topn_xruns / pv_topn_merge): they must add up to
+        // what the source sends this rank
+        uint64_t mine = 0;
+        for (size_t k = (size_t)2 * PV_SLOTS * lo; k < (size_t)2 * PV_SLOTS * hi; k++) mine += src[q].hdr[k];
+        if (mine != src[q].dtot[me]) return c->fail(PV_EINVAL, "exchange blob %u: counts do not match its total", q);
         rtot[q] = q == me ? 0 : src[q].dtot[me];
         stride = std::max(stride, rtot[q]);
     }
@@ -6128,6 +6171,7 @@ int pv_topn_x_import(pv_ctx *c, uint32_t W, uint32_t me, const uint8_t *const *b
 
 int pv_comm_merge_topn(pv_ctx *c)
 {
+    mark_merged(c, "pv_comm_merge_topn");
     if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
     const uint32_t W = (uint32_t)c->comm_ranks, me = (uint32_t)c->comm_rank;
     std::lock_guard<std::mutex> g(c->mu);
@@ -6545,6 +6589,7 @@ int pv_topn_x_names(pv_ctx *c, const uint8_t *const *cands, const size_t *sizes,
 int pv_topn_x_view(pv_ctx *c, const uint8_t *const *cands, const size_t *csizes, const uint8_t *const *names,
                    const size_t *nsizes, uint32_t n)
 {
+    mark_merged(c, "pv_topn_x_view");
     std::lock_guard<std::mutex> g(c->mu);
     std::map<std::pair<uint32_t, uint64_t>, std::string> known;
     for (uint32_t q = 0; q < n; q++) {
@@ -6748,12 +6793,14 @@ int values_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
 
 int pv_values_x_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
 {
+    mark_merged(c, "pv_values_x_select");
     if (!ar) return c->fail(PV_EINVAL, "no all-reduce callback");
     return values_select(c, ar, user);
 }
 
 int pv_comm_values_select(pv_ctx *c)
 {
+    mark_merged(c, "pv_comm_values_select");
     if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
     return values_select(c, nullptr, nullptr);
 }
@@ -6763,6 +6810,7 @@ int pv_comm_values_select(pv_ctx *c)
 // words. The caller writes them, so they stop being clean.
 int pv_window_regions(pv_ctx *c, pv_region *r, uint32_t max, uint32_t *n)
 {
+    mark_merged(c, "pv_window_regions");
     std::lock_guard<std::mutex> g(c->mu);
     flush_fills(c);
     std::vector<pv_region> v;
@@ -6823,6 +6871,7 @@ int pv_comm_init(pv_ctx *c, const uint8_t id[PV_COMM_ID_BYTES], int nranks, int 
 
 int pv_comm_allreduce_window(pv_ctx *c)
 {
+    mark_merged(c, "pv_comm_allreduce_window");
     if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
     std::vector<pv_region> v(8 * PV_SLOTS);
     uint32_t n = 0;
@@ -7274,6 +7323,7 @@ int pv_edge_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
 
 int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks, uint32_t me)
 {
+    mark_merged(c, "pv_edge_merge");
     if (c->dns2_groups)
         return c->fail(PV_EUNSUPPORTED, "DNS v2 shard edges go rank by rank: pv_set_slow_defer, then pv_edge_carry");
     if (c->slow_defer) {
@@ -7389,6 +7439,7 @@ int pv_edge_merge(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, ui
 // the rest stay open. *out: those, and this shard's own queries open at its end (pv_free).
 int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes)
 {
+    mark_merged(c, "pv_edge_carry");
     *out = nullptr;
     *out_bytes = 0;
     if (!c->slow_defer) return c->fail(PV_EINVAL, "pv_edge_carry needs pv_set_slow_defer");
@@ -7539,6 +7590,7 @@ int pv_slow_values_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
 int slow_apply(pv_ctx *c, const std::vector<float> thr[5]);
 int pv_slow_finish(pv_ctx *c, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks)
 {
+    mark_merged(c, "pv_slow_finish");
     std::lock_guard<std::mutex> g(c->mu);
     hipSetDevice(c->device);
     if (!c->slow_defer) return c->fail(PV_EINVAL, "pv_slow_finish without pv_set_slow_defer");
@@ -7632,12 +7684,14 @@ int slow_select(pv_ctx *c, pv_allreduce_fn ar, void *user)
 
 int pv_slow_x_finish(pv_ctx *c, pv_allreduce_fn ar, void *user)
 {
+    mark_merged(c, "pv_slow_x_finish");
     if (!ar) return c->fail(PV_EINVAL, "no all-reduce callback");
     return slow_select(c, ar, user);
 }
 
 int pv_comm_slow_finish(pv_ctx *c)
 {
+    mark_merged(c, "pv_comm_slow_finish");
     if (!c->comm) return c->fail(PV_EINVAL, "no communicator (pv_comm_init)");
     return slow_select(c, nullptr, nullptr);
 }
@@ -7772,6 +7826,7 @@ int pv_values_export(pv_ctx *c, uint8_t **buf, size_t *bytes)
 
 int pv_values_merge(pv_ctx *c, const uint8_t *buf, size_t bytes)
 {
+    mark_merged(c, "pv_values_merge");
     std::lock_guard<std::mutex> g(c->mu);
     if (bytes % 16) return c->fail(PV_EINVAL, "malformed value buffer");
     if (int rc = sync_xvals(c)) return rc;

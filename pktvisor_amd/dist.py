@@ -211,21 +211,29 @@ def merge_slow(handlers, group=None, comm=None):
         if comm == "pv":
             handlers.comm_slow_finish()
         else:
-            handlers.slow_x_finish(_torch_allreduce(group))
+            handlers.slow_x_finish(_torch_allreduce(group, _handlers_device(handlers)))
 
 
-def _torch_allreduce(group=None):
+def _torch_allreduce(group=None, device=None):
     """an all-reduce of a host uint64 array through torch.distributed (int64: two's-complement
-    sums are identical; the values summed and maxed here are below 2^63)"""
+    sums are identical; the values summed and maxed here are below 2^63). On RCCL the array
+    travels through `device` (the handlers' GPU), not torch's current device, so ranks that
+    never called torch.cuda.set_device still reduce on their own GPU."""
     def ar(a, op):
         t = torch.from_numpy(a.view(np.int64))
         if dist.get_backend(group) != "gloo":
-            d = t.cuda()
+            d = t.to(device if device is not None else torch.device("cuda", torch.cuda.current_device()))
             dist.all_reduce(d, op=dist.ReduceOp.MAX if op else dist.ReduceOp.SUM, group=group)
             t.copy_(d.cpu())
         else:
             dist.all_reduce(t, op=dist.ReduceOp.MAX if op else dist.ReduceOp.SUM, group=group)
     return ar
+
+
+def _handlers_device(handlers):
+    """the torch device of the handlers' GPU (None: torch's current device)"""
+    d = getattr(handlers, "device", -1)
+    return torch.device("cuda", d) if isinstance(d, int) and d >= 0 else None
 
 
 def merge_values(handlers, group=None, comm=None):
@@ -236,7 +244,7 @@ def merge_values(handlers, group=None, comm=None):
     if comm == "pv":
         handlers.comm_values_select()
     else:
-        handlers.values_x_select(_torch_allreduce(group))
+        handlers.values_x_select(_torch_allreduce(group, _handlers_device(handlers)))
 
 
 def merge_window(handlers, device, group=None, comm=None, finalize=True):

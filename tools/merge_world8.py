@@ -65,8 +65,8 @@ def rank_main(args):
     pvdist._allgather = counting_gather
     orig_ar = pvdist._torch_allreduce
 
-    def counting_ar(group=None):
-        f = orig_ar(group)
+    def counting_ar(group=None, device=None):
+        f = orig_ar(group, device)
 
         def ar(a, op):
             sent["allreduce"] += a.nbytes
