@@ -3976,7 +3976,14 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         hipExtLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (hipEvent_t) nullptr, e1, 0, dp);
     }
     else if (lean && c->reg_waves == 8) hipExtLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, e0, e1, 0, dp);
-    else if (lean && tc) hipExtLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
+    else if (lean && tc) {
+        hipExtLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
+        // tuning only (PV_NET_REPEAT=k): k more launches back to back, so a kernel trace shows the
+        // pass right after itself next to the pass after the previous batch's kernels (counters are
+        // then counted k + 1 times)
+        static const int rep = getenv("PV_NET_REPEAT") ? atoi(getenv("PV_NET_REPEAT")) : 0;
+        for (int r = 0; r < rep; r++) hipLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, dp);
+    }
     else if (lean) hipExtLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     else hipExtLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     e = hipGetLastError();
@@ -7089,14 +7096,35 @@ int add_sum_word(pv_ctx *c, uint32_t slot, uint32_t word, int64_t delta)
 // counted filtered / timed out. Purges are time-outs of the purging shift's bucket. The edge
 // pairs' times feed the stream's thresholds (slow_xv) and their slow candidates (scands).
 // Buffers: n x (PvXEvent [+ u64 ECS address with top_ecs]).
+// The first stub (this shard's first event) of each incoming open query's key: a map over the
+// incoming keys (usually few) and one scan of the stubs in first-occurrence order, instead of a map
+// over every stub of the shard (millions in a shard the edge horizon covers whole: the map's build
+// was most of each rank's turn in the edge chain).
+std::unordered_map<uint64_t, size_t> edge_first_stubs(const pv_ctx *c, const uint8_t *in, size_t n, size_t esz)
+{
+    std::unordered_map<uint64_t, size_t> first;
+    first.reserve(n * 2);
+    for (size_t k = 0; k < n; k++) {
+        uint64_t key;
+        memcpy(&key, in + k * esz + offsetof(PvXEvent, key), 8);
+        first.emplace(key, SIZE_MAX);
+    }
+    if (first.empty()) return first;
+    size_t left = first.size();
+    for (size_t i = 0; i < c->stubs.size() && left; i++) {
+        auto it = first.find(c->stubs[i].e.key);
+        if (it != first.end() && it->second == SIZE_MAX) { it->second = i; left--; }
+    }
+    for (auto it = first.begin(); it != first.end();) it = it->second == SIZE_MAX ? first.erase(it) : std::next(it);
+    return first;
+}
+
 int edge_carry2(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes)
 {
     const bool ecs = c->d_pecs[0] != nullptr;
     const size_t esz = sizeof(PvXEvent) + (ecs ? 8 : 0);
     if (in_bytes % esz) return c->fail(PV_EINVAL, "malformed open-query buffer");
-    std::unordered_map<uint64_t, size_t> first;
-    first.reserve(c->stubs.size() * 2);
-    for (size_t i = 0; i < c->stubs.size(); i++) first.emplace(c->stubs[i].e.key, i);
+    const std::unordered_map<uint64_t, size_t> first = edge_first_stubs(c, in, in_bytes / esz, esz);
     const uint64_t live = c->dns.ordinal;
     auto in_win = [&](uint64_t ord) { return ord <= live && ord + c->dns.slots.size() > live; };
     auto slot_of = [&](uint64_t ord) { return c->dns.slots[live - ord]; };
@@ -7451,9 +7479,7 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return c->hipfail(e, "synchronize");
     if (c->dns2_groups) return edge_carry2(c, in, in_bytes, out, out_bytes);
-    std::unordered_map<uint64_t, size_t> first;
-    first.reserve(c->stubs.size() * 2);
-    for (size_t i = 0; i < c->stubs.size(); i++) first.emplace(c->stubs[i].e.key, i);
+    const std::unordered_map<uint64_t, size_t> first = edge_first_stubs(c, in, in_bytes / sizeof(PvXEvent), sizeof(PvXEvent));
     const uint64_t live = c->dns.ordinal;
     auto in_win = [&](uint64_t ord) { return ord <= live && ord + c->dns.slots.size() > live; };
     const bool quant = c->dns_groups & PV_DNS_QUANTILES;
@@ -7534,6 +7560,13 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
     *out = (uint8_t *)malloc(*out_bytes ? *out_bytes : 1);
     if (!*out) return c->fail(PV_ECAPACITY, "out of host memory");
     if (!keep.empty()) memcpy(*out, keep.data(), *out_bytes);
+    return 0;
+}
+
+int pv_edge_open_count(pv_ctx *c, uint64_t *n)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    *n = c->n_pend;
     return 0;
 }
 

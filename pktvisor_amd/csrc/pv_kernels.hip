@@ -1403,6 +1403,36 @@ __device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds)
                  : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
 #define PV_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
+// Store flavours of the step's large writers. A plain store leaves its line dirty in the
+// Infinity Cache until the read stream of a later kernel evicts it, and that kernel then pays for
+// the write-back (tools/net_probe.hip, round 6: a pass over the C2 blob right after 160 MB of plain
+// stores runs 158 us against 134 after the same bytes stored non-temporally, whose writer took
+// 37 instead of 32 us). PV_NT_* pick non-temporal stores for the writers whose bytes no kernel of
+// the same step reads back.
+#ifndef PV_NT_MERGE
+#define PV_NT_MERGE 1 // pv_topn_merge's write-back of the table regions (read by the next batch's merge)
+#endif
+#ifndef PV_NT_IPLOG
+#define PV_NT_IPLOG 0 // tuning: the Net pass's IP log (read by pv_topn_combine right after)
+#endif
+#ifndef PV_NT_COMB
+#define PV_NT_COMB 0 // tuning: pv_topn_combine's list (read by pv_topn_merge right after)
+#endif
+template <bool NT, class T>
+__device__ __forceinline__ void st_nt(PV_G T *p, T v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ void st_nt16(PV_G ulonglong2 *p, ulonglong2 v)
+{
+    if constexpr (NT) {
+        PV_G uint64_t *q = reinterpret_cast<PV_G uint64_t *>(p);
+        __builtin_nontemporal_store((unsigned long long)v.x, q);
+        __builtin_nontemporal_store((unsigned long long)v.y, q + 1);
+    } else *p = v;
+}
 // A workgroup barrier for LDS data only: the wave's LDS ops complete (lgkmcnt 0), then s_barrier.
 // __syncthreads() also waits for every global store the wave has in flight (its release fence is a
 // vmcnt(0)), and a store takes microseconds to complete under load; after a phase of global stores
@@ -2331,7 +2361,13 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
 #define PV_REG_MINW 2 // waves per SIMD the register allocation must allow
 #endif
 #ifndef PV_REG_DEPTH
-#define PV_REG_DEPTH 2 // tiles whose windows are in registers (the parsed one + those in flight)
+#define PV_REG_DEPTH 3 // tiles whose windows are in registers (the parsed one + those in flight)
+#endif
+#ifndef PV_REG_UNCOND
+#define PV_REG_UNCOND 1 // the pipeline with unconditional (clamped) loads
+#endif
+#ifndef PV_ABL_NOSLOW
+#define PV_ABL_NOSLOW 0 // tuning/ablation only: the register pass without its general-path call
 #endif
 struct NetRegState {
     uint32_t hist[PV_HBINS];
@@ -2399,10 +2435,14 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
     auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * PV_WT + lane, last)]; };
     // one tile from its windows W (off: this lane's record start)
+    // (a tile past the wave's last, live false, is a clamped copy: it parses nothing and its
+    // unconditional stores go to the wave's trash line)
+    PV_G uint64_t *const trash = P.trash + ((uint64_t)blockIdx.x * NW + wave) * 256;
     auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
+        const bool live = k < ntl;
         const uint64_t t = tile_of(k);
         const uint64_t r0 = t * PV_WT, i = r0 + lane;
-        const bool active = i < n;
+        const bool active = live && i < n;
         RecW rw;
         win_words(W, off & 3, rw);
         if (PV_LEAN_LEVEL == 1) {
@@ -2459,8 +2499,7 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         if (temit && __ballot(istcp)) {
             if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
         }
-        if (slowm) {
-            // general-path records (VLAN, IPv6, options, tunnels, other link types): every byte from HBM
+        if (slowm && !PV_ABL_NOSLOW) {
             if (active && !fast) {
                 const SAcc R{recs, nullptr, 0, 0, 0, 1};
                 const SlowOut so = net_slow_p(Pp, R, off, i);
@@ -2500,9 +2539,11 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                 if (TC) {
                     // every lane (the log has 64 words of slack past the batch) and every lane
                     // the same direction word: two unconditional store instructions
-                    P.iplog32[i] = active && v4 ? (uint32_t)ek : 0u;
-                    P.ipdir[t] = dbit;
-                } else {
+                    PV_G uint32_t *const l32 = live ? P.iplog32 + i : reinterpret_cast<PV_G uint32_t *>(trash) + lane;
+                    PV_G uint64_t *const ldw = live ? P.ipdir + t : trash + 32;
+                    st_nt<PV_NT_IPLOG, uint32_t>(l32, active && v4 ? (uint32_t)ek : 0u);
+                    st_nt<PV_NT_IPLOG, uint64_t>(ldw, dbit);
+                } else if (live) {
                     if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
                     if (lane == 0) P.ipdir[t] = dbit;
                 }
@@ -2528,7 +2569,47 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
             }
         }
     };
+#if PV_REG_UNCOND
+    // software pipeline of depth PV_REG_DEPTH with unconditional loads: every load is issued on
+    // every path (tile_of clamps past the wave's last tile; tile() skips a clamped copy), so no load
+    // can be sunk behind the parse it should overlap into a loop exit's branch
+    if (ntl) {
 #if PV_REG_DEPTH == 3
+        uint4 W0[5], W1[5], W2[5];
+        uint32_t o0 = off_of(0), o1 = off_of(1), o2 = off_of(2);
+        win_load(recs, o0, W0);
+        win_load(recs, o1, W1);
+        for (uint32_t k = 0; k < ntl; k += 3) {
+            const uint32_t oN = off_of(k + 3);
+            win_load(recs, o2, W2);
+            tile(k, o0, W0);
+            const uint32_t oN1 = off_of(k + 4);
+            win_load(recs, oN, W0);
+            o0 = oN;
+            tile(k + 1, o1, W1);
+            const uint32_t oN2 = off_of(k + 5);
+            win_load(recs, oN1, W1);
+            o1 = oN1;
+            tile(k + 2, o2, W2);
+            o2 = oN2;
+        }
+#else
+        uint4 WA[5], WB[5];
+        uint32_t oA = off_of(0), oB = off_of(1);
+        win_load(recs, oA, WA);
+        for (uint32_t k = 0; k < ntl; k += 2) {
+            const uint32_t oN = off_of(k + 2);
+            win_load(recs, oB, WB);
+            tile(k, oA, WA);
+            const uint32_t oN2 = off_of(k + 3);
+            win_load(recs, oN, WA);
+            oA = oN;
+            tile(k + 1, oB, WB);
+            oB = oN2;
+        }
+#endif
+    }
+#elif PV_REG_DEPTH == 3
     // three buffers: the windows of tiles k + 1 and k + 2 in flight while tile k is parsed
     uint4 W0[5], W1[5], W2[5];
     uint32_t o0 = 0, o1 = 0, o2 = 0;
@@ -3979,12 +4060,12 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x)
         if (S.key[j]) {
             const ulonglong2 e = comb_entry(S.key[j], S.cnt[j], S.rep[j]);
-            out[atomicAdd(&S.h[run_key(P, e.x)], 1u)] = e;
+            st_nt16<PV_NT_COMB>(out + atomicAdd(&S.h[run_key(P, e.x)], 1u), e);
         }
     // spilled entries (this workgroup's own writes: same CU, coherent after the barrier)
     const uint32_t nsp = S.nsp;
     batched<8>(nsp, [&](uint64_t j) { return sp[j]; },
-               [&](uint64_t, ulonglong2 e) { out[atomicAdd(&S.h[run_key(P, e.x)], 1u)] = e; });
+               [&](uint64_t, ulonglong2 e) { st_nt16<PV_NT_COMB>(out + atomicAdd(&S.h[run_key(P, e.x)], 1u), e); });
     if (threadIdx.x == 0) P.cb_cnt[blockIdx.x] = total;
 #ifdef PV_TSTAMPS
     __syncthreads();
@@ -4265,10 +4346,10 @@ extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) __attribute__((amdgp
             for (uint32_t q = 0; q < WB; q++) {
                 const uint32_t i = threadIdx.x + (q0 + q) * PV_MG_THREADS;
                 if (kk[q] & PV_CREATED) {
-                    P.tkeys[rbase + i] = mv4_norm(kk[q]) & ~PV_MV4;
+                    st_nt<PV_NT_MERGE, uint64_t>(P.tkeys + rbase + i, mv4_norm(kk[q]) & ~PV_MV4);
                     if (xm && PV_KEY_METRIC(kk[q] & ~PV_CREATED) != TM_IPV4) P.taux[rbase + i] = 0; // name unknown here
                 }
-                if (dd[q]) P.tcnt[rbase + i] = cc[q] + dd[q];
+                if (dd[q]) st_nt<PV_NT_MERGE, uint64_t>(P.tcnt + rbase + i, cc[q] + dd[q]);
                 if ((kk[q] & PV_MV4) && dd[q]) {
                     const uint32_t m0 = (uint32_t)(S.dl[i] >> 32), m1 = (uint32_t)(kk[q] >> 32) & 0xffffffu;
                     if (m0 != 0xffffffffu || m1 != 0xffffffu) {

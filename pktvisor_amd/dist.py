@@ -177,30 +177,49 @@ def _rank(handlers, group=None, comm=None):
 
 def check_aligned(handlers, group=None, comm=None):
     """The bucket merge pairs slots by id: every rank's windows must hold the same periods
-    (slot, start second) — what the global plan guarantees; checked before the merge."""
+    (slot, start second) — what the global plan guarantees; checked before the merge. The same
+    gather carries each rank's count of DNS queries open at its shard's end
+    (pv_edge_open_count), which merge_edges uses; returns those counts in rank order."""
     import json
     from pktvisor_amd import PART_DNS, PART_NET
-    mine = json.dumps([handlers.window_periods(PART_NET), handlers.window_periods(PART_DNS)]).encode()
-    allv = _allgather(handlers, mine, group, comm)
-    if any(v != allv[0] for v in allv):
-        raise RuntimeError(f"shard windows differ across ranks: {allv}")
+    wins = [handlers.window_periods(PART_NET), handlers.window_periods(PART_DNS)]
+    mine = json.dumps([wins, handlers.edge_open_count()]).encode()
+    allv = [json.loads(v) for v in _allgather(handlers, mine, group, comm)]
+    if any(v[0] != allv[0][0] for v in allv):
+        raise RuntimeError(f"shard windows differ across ranks: {[v[0] for v in allv]}")
+    return [int(v[1]) for v in allv]
 
 
-def merge_edges(handlers, group=None, comm=None):
+def merge_edges(handlers, group=None, comm=None, open_counts=None):
     """DNS transactions across shard edges. Deferred runs carry the open queries rank by rank
-    (pv_edge_carry: W gather rounds, rank r computes its carry in round r from rank r-1's), so a
-    query meets the first event of its key in ANY later shard, after that shard's purges;
-    otherwise every rank's stubs are gathered once and paired with the previous shards'."""
+    (pv_edge_carry: rank r computes its carry in round r from rank r-1's), so a query meets the
+    first event of its key in ANY later shard, after that shard's purges; otherwise every rank's
+    stubs are gathered once and paired with the previous shards'. open_counts (every rank's
+    pv_edge_open_count, from check_aligned): a rank before the first that leaves a query open
+    receives nothing, so the chain starts there, and with no open query anywhere nothing crosses
+    an edge and no round runs (a stream without DNS transactions). The last rank's carry is
+    nobody's input: it is computed, not gathered."""
+    if open_counts is None:
+        open_counts = [int(x) for x in _allgather_ints(handlers, handlers.edge_open_count(), group, comm)]
+    if not any(open_counts):
+        return
+    first = next(r for r, k in enumerate(open_counts) if k)
+    me = _rank(handlers, group, comm)
+    world = len(open_counts)
     if getattr(handlers, "slow_defer", False):
-        me = _rank(handlers, group, comm)
-        world = handlers.comm_ranks if comm == "pv" else dist.get_world_size(group)
         carried = b""
-        for r in range(world):
+        for r in range(first, world):
             mine = handlers.edge_carry(carried) if r == me else b""
+            if r == world - 1:
+                break
             got = _allgather(handlers, mine, group, comm)
             carried = got[r]
         return
-    handlers.edge_merge(_allgather(handlers, handlers.edge_export(), group, comm), _rank(handlers, group, comm))
+    handlers.edge_merge(_allgather(handlers, handlers.edge_export(), group, comm), me)
+
+
+def _allgather_ints(handlers, v: int, group=None, comm=None):
+    return [int.from_bytes(b, "little") for b in _allgather(handlers, int(v).to_bytes(8, "little"), group, comm)]
 
 
 def merge_slow(handlers, group=None, comm=None):
@@ -254,8 +273,8 @@ def merge_window(handlers, device, group=None, comm=None, finalize=True):
     device part; finalize=True then assembles the read view (the top-N lists with names, the
     quantiles by distributed selection), which finalize_window also does on its own."""
     handlers.synchronize()
-    check_aligned(handlers, group, comm)
-    merge_edges(handlers, group, comm)
+    open_counts = check_aligned(handlers, group, comm)
+    merge_edges(handlers, group, comm, open_counts)
     merge_slow(handlers, group, comm)
     if comm == "pv":
         handlers.comm_allreduce_window()

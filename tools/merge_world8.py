@@ -95,8 +95,9 @@ def rank_main(args):
             h.synchronize()
             part[name] = {"ms": round((time.perf_counter() - a) * 1e3, 1), "gathered_bytes": sent["gather"] - g0}
         h.synchronize()
-        step("check_aligned", lambda: pvdist.check_aligned(h))
-        step("edges", lambda: pvdist.merge_edges(h))
+        counts = []
+        step("check_aligned", lambda: counts.append(pvdist.check_aligned(h)))
+        step("edges", lambda: pvdist.merge_edges(h, open_counts=counts[0]))
         step("slow", lambda: pvdist.merge_slow(h))
         step("buckets", lambda: pvdist.reduce_handlers(h, dev))
         step("topn_owner", lambda: pvdist.merge_topn(h))

@@ -342,6 +342,336 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     if (acc == 0x12345678u) P.out[0] = acc;
 }
 
+
+// plain coalesced read of the blob (ring_probe's ceiling); WR: plus one 4-B store per lane every
+// 20 loaded 16-B chunks (the IP log's 1:20 byte ratio at C2's 80-B records), to a log laid out as
+// the IP log is (contiguous per lane group), so the write's own HBM cost shows next to the reads
+template <bool WR>
+__global__ void __launch_bounds__(256) plainw(const uint4 *__restrict__ p, uint64_t n16, uint32_t *out, uint32_t *log)
+{
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t k = 0;
+    for (; i + 7 * stride < n16; i += 8 * stride) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = p[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        if (WR && (k++ % 5) == 4) log[i / 20 + (k & 1)] = acc; // 8 chunks x 5 = 40 loads : 2 stores
+    }
+    for (; i < n16; i += stride) acc ^= p[i].x;
+    if (acc == 0x12345678u) out[0] = acc;
+}
+// rung 4 with the record windows loaded non-temporally (nt: streamed, so the log's writes may stay
+// in the Infinity Cache), and with the log stored non-temporally too
+template <uint32_t NW, bool NTST>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) rk4nt(const Prm *__restrict__ Pp)
+{
+    const PC Prm &P = *(const PC Prm *)Pp;
+    __shared__ uint32_t hist[2048];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const uint8_t *const recs = P.recs;
+    const uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint64_t nwt = (n + WT - 1) / WT;
+    uint32_t acc = 0;
+    for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
+        const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
+        const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+        const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u;
+        auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
+        auto off_of = [&](uint32_t k) -> uint32_t { return __builtin_nontemporal_load(&offs[min<uint64_t>(tile_of(k) * WT + lane, last)]); };
+        auto wl = [&](uint32_t off, uint4 (&W)[5]) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(recs + (off & ~3u));
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                W[j].x = __builtin_nontemporal_load(&p[j].x);
+                W[j].y = __builtin_nontemporal_load(&p[j].y);
+                W[j].z = __builtin_nontemporal_load(&p[j].z);
+                W[j].w = __builtin_nontemporal_load(&p[j].w);
+            }
+        };
+        auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
+            const uint64_t t = tile_of(k), i = t * WT + lane;
+            const uint32_t a = fold(W, off & 3);
+            acc += a;
+            const uint32_t cap = W[0].z & 2047;
+            if (i < n) __hip_atomic_fetch_add(&hist[cap], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint64_t dbit = __ballot(i < n && (a & 1));
+            if (NTST) {
+                __builtin_nontemporal_store(i < n ? a : 0u, &P.log[i]);
+                __builtin_nontemporal_store(dbit, &P.dirw[t]);
+            } else {
+                P.log[i] = i < n ? a : 0u;
+                P.dirw[t] = dbit;
+            }
+        };
+        uint4 WA[5], WB[5];
+        uint32_t oA = 0, oB = 0;
+        if (ntl) {
+            oA = off_of(0);
+            oB = off_of(1);
+            wl(oA, WA);
+        }
+        for (uint32_t k = 0; k < ntl; k += 2) {
+            const uint32_t oN = off_of(k + 2);
+            wl(oB, WB);
+            tile(k, oA, WA);
+            if (k + 1 >= ntl) break;
+            const uint32_t oN2 = off_of(k + 3);
+            wl(oN, WA);
+            oA = oN;
+            tile(k + 1, oB, WB);
+            oB = oN2;
+        }
+    }
+    if (acc == 0x12345678u) P.out[0] = acc;
+}
+// rung 4 storing into a 1 MiB L2-resident target (is it the HBM write or the store instruction?)
+template <uint32_t NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) rk4l2(const Prm *__restrict__ Pp)
+{
+    const PC Prm &P = *(const PC Prm *)Pp;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint8_t *const recs = P.recs;
+    const uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint64_t nwt = (n + WT - 1) / WT;
+    uint32_t acc = 0;
+    for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
+        const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
+        const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+        const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u;
+        auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
+        auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * WT + lane, last)]; };
+        auto wl = [&](uint32_t off, uint4 (&W)[5]) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(recs + (off & ~3u));
+#pragma unroll
+            for (int j = 0; j < 5; j++) W[j] = p[j];
+        };
+        auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
+            const uint64_t t = tile_of(k), i = t * WT + lane;
+            const uint32_t a = fold(W, off & 3);
+            acc += a;
+            P.log[i & 0x3ffff] = i < n ? a : 0u;
+        };
+        uint4 WA[5], WB[5];
+        uint32_t oA = 0, oB = 0;
+        if (ntl) {
+            oA = off_of(0);
+            oB = off_of(1);
+            wl(oA, WA);
+        }
+        for (uint32_t k = 0; k < ntl; k += 2) {
+            const uint32_t oN = off_of(k + 2);
+            wl(oB, WB);
+            tile(k, oA, WA);
+            if (k + 1 >= ntl) break;
+            const uint32_t oN2 = off_of(k + 3);
+            wl(oN, WA);
+            oA = oN;
+            tile(k + 1, oB, WB);
+            oB = oN2;
+        }
+    }
+    if (acc == 0x12345678u) P.out[0] = acc;
+}
+
+
+// rung 4 with super-tiles: wave w takes groups of G contiguous tiles (group w, w + NW, ...), stages
+// the group's IP-log words in LDS and writes them as one 16-B store per lane per 4 tiles (G * 256 B
+// contiguous), the group's direction words by G lanes; ST = false: the same mapping without stores
+template <uint32_t NW, int G, bool ST>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) rk4g(const Prm *__restrict__ Pp)
+{
+    const PC Prm &P = *(const PC Prm *)Pp;
+    __shared__ uint32_t hist[2048];
+    __shared__ uint32_t stg[NW][G * 64];
+    __shared__ uint64_t sdir[NW][G];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const uint8_t *const recs = P.recs;
+    const uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint64_t nwt = (n + WT - 1) / WT;
+    uint32_t acc = 0;
+    for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
+        const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
+        const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+        // this wave's tiles: groups w, w + NW, ... of G tiles (the range holds whole groups but its last)
+        const uint64_t ng = wend > wbeg ? (wend - wbeg + G - 1) / G : 0;
+        const uint32_t ngw = ng > wave ? (uint32_t)((ng - wave + NW - 1) / NW) : 0u;
+        const uint32_t ntl = ngw * G;
+        auto tile_of = [&](uint32_t k) -> uint64_t {
+            const uint32_t kk = min(k, ntl - 1);
+            return min<uint64_t>(wbeg + (uint64_t)G * (wave + (uint64_t)NW * (kk / G)) + kk % G, wend - 1);
+        };
+        auto real_tile = [&](uint32_t k) -> bool { return wbeg + (uint64_t)G * (wave + (uint64_t)NW * (k / G)) + k % G < wend; };
+        auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * WT + lane, last)]; };
+        auto wl = [&](uint32_t off, uint4 (&W)[5]) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(recs + (off & ~3u));
+#pragma unroll
+            for (int j = 0; j < 5; j++) W[j] = p[j];
+        };
+        auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
+            const uint64_t t = tile_of(k), i = t * WT + lane;
+            const bool rt = real_tile(k);
+            const uint32_t a = fold(W, off & 3);
+            acc += a;
+            const uint32_t cap = W[0].z & 2047;
+            if (rt && i < n) __hip_atomic_fetch_add(&hist[cap], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (ST) {
+                const uint64_t dbit = __ballot(rt && i < n && (a & 1));
+                stg[wave][(k % G) * 64 + lane] = rt && i < n ? a : 0u;
+                if (lane == 0) sdir[wave][k % G] = dbit;
+                if (k % G == G - 1) {
+                    // the group's G * 64 words: lane l writes words 4l .. 4l + 3 of each 256-word block
+                    const uint64_t t0 = wbeg + (uint64_t)G * (wave + (uint64_t)NW * (k / G));
+#pragma unroll
+                    for (int b = 0; b < G / 4; b++) {
+                        const uint4 v = reinterpret_cast<const uint4 *>(&stg[wave][b * 256])[lane];
+                        *reinterpret_cast<uint4 *>(&P.log[(t0 + 4 * b) * WT + 4 * lane]) = v;
+                    }
+                    if (lane < G) P.dirw[t0 + lane] = sdir[wave][lane];
+                }
+            }
+        };
+        uint4 WA[5], WB[5];
+        uint32_t oA = 0, oB = 0;
+        if (ntl) {
+            oA = off_of(0);
+            oB = off_of(1);
+            wl(oA, WA);
+        }
+        for (uint32_t k = 0; k < ntl; k += 2) {
+            const uint32_t oN = off_of(k + 2);
+            wl(oB, WB);
+            tile(k, oA, WA);
+            if (k + 1 >= ntl) break;
+            const uint32_t oN2 = off_of(k + 3);
+            wl(oN, WA);
+            oA = oN;
+            tile(k + 1, oB, WB);
+            oB = oN2;
+        }
+    }
+    if (acc == 0x12345678u) P.out[0] = acc;
+}
+
+
+// rung 4 plus a synthetic per-tile compute the size of the product's (the C2 PMC pass: ~159 VALU and
+// ~137 SALU instructions per tile per wave), at pipeline depth D (D tiles' windows in flight: D - 1
+// ahead of the parsed one); loads are unconditional (clamped tiles), only the compute and the
+// stores are guarded, so no load can be sunk behind a loop exit
+template <uint32_t NW, int D, int CV>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) rk4c(const Prm *__restrict__ Pp)
+{
+    const PC Prm &P = *(const PC Prm *)Pp;
+    __shared__ uint32_t hist[2048];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    const uint8_t *const recs = P.recs;
+    const uint32_t *const offs = P.offs;
+    const uint64_t n = P.n, last = n - 1;
+    const uint64_t nwt = (n + WT - 1) / WT;
+    uint32_t acc = 0, sacc = 0;
+    for (uint32_t lb = blockIdx.x; lb < P.grid_main; lb += gridDim.x) {
+        const uint64_t wbeg = (uint64_t)lb * P.wt_per_block;
+        const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
+        const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + NW - 1) / NW) : 0u;
+        if (!ntl) continue;
+        auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + (uint64_t)NW * min(k, ntl - 1); };
+        auto off_of = [&](uint32_t k) -> uint32_t { return offs[min<uint64_t>(tile_of(k) * WT + lane, last)]; };
+        auto wl = [&](uint32_t off, uint4 (&W)[5]) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(recs + (off & ~3u));
+#pragma unroll
+            for (int j = 0; j < 5; j++) W[j] = p[j];
+        };
+        auto tile = [&](uint32_t k, uint32_t off, const uint4 (&W)[5]) {
+            const bool live = k < ntl;
+            const uint64_t t = tile_of(k), i = t * WT + lane;
+            const bool act = live && i < n;
+            uint32_t a = fold(W, off & 3);
+            // synthetic parse work
+#pragma unroll
+            for (int r = 0; r < CV; r++) a = (a * 0x9E3779B1u + (a >> 7)) ^ (r & 1 ? W[r & 3].x : W[r & 3].y);
+            uint32_t sv = __builtin_amdgcn_readfirstlane(a);
+#pragma unroll
+            for (int r = 0; r < CV; r++) sv = sv * 31u + (sv >> 3) + (uint32_t)r;
+            sacc += sv;
+            acc += a;
+            const uint32_t cap = W[0].z & 2047;
+            if (act) __hip_atomic_fetch_add(&hist[cap], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint64_t dbit = __ballot(act && (a & 1));
+            if (live) {
+                P.log[i] = act ? a : 0u;
+                P.dirw[t] = dbit;
+            }
+        };
+        if constexpr (D == 2) {
+            uint4 WA[5], WB[5];
+            uint32_t oA = off_of(0), oB = off_of(1);
+            wl(oA, WA);
+            for (uint32_t k = 0; k < ntl; k += 2) {
+                const uint32_t oN = off_of(k + 2);
+                wl(oB, WB);
+                asm volatile("" ::: "memory");
+                tile(k, oA, WA);
+                const uint32_t oN2 = off_of(k + 3);
+                wl(oN, WA);
+                asm volatile("" ::: "memory");
+                oA = oN;
+                tile(k + 1, oB, WB);
+                oB = oN2;
+            }
+        } else {
+            uint4 W0[5], W1[5], W2[5];
+            uint32_t o0 = off_of(0), o1 = off_of(1), o2 = off_of(2);
+            wl(o0, W0);
+            wl(o1, W1);
+            for (uint32_t k = 0; k < ntl; k += 3) {
+                const uint32_t oN = off_of(k + 3);
+                wl(o2, W2);
+                asm volatile("" ::: "memory");
+                tile(k, o0, W0);
+                const uint32_t oN1 = off_of(k + 4);
+                wl(oN, W0);
+                asm volatile("" ::: "memory");
+                o0 = oN;
+                tile(k + 1, o1, W1);
+                const uint32_t oN2 = off_of(k + 5);
+                wl(oN1, W1);
+                asm volatile("" ::: "memory");
+                o1 = oN1;
+                tile(k + 2, o2, W2);
+                o2 = oN2;
+            }
+        }
+    }
+    if (acc == 0x12345678u || sacc == 0x12345678u) P.out[0] = acc;
+}
+
+// MODE 1: non-temporal stores, 2: sc1 (agent-scope relaxed atomic) 8-B stores
+template <int MODE>
+__global__ void dirtym(uint4 *p, uint64_t n16, uint32_t v)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 x = make_uint4(v, v + 1, v + 2, v + 3);
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        if (MODE == 1) __builtin_nontemporal_store((v4u){x.x, x.y, x.z, x.w}, reinterpret_cast<v4u *>(p + i));
+        else {
+            uint64_t *q = reinterpret_cast<uint64_t *>(p + i);
+            __hip_atomic_store(q, (uint64_t)x.x | (uint64_t)x.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(q + 1, (uint64_t)x.z | (uint64_t)x.w << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
 __global__ void dirty(uint4 *p, uint64_t n16, uint32_t v)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x)
@@ -382,11 +712,14 @@ int main(int argc, char **argv)
     hipEventCreate(&a);
     hipEventCreate(&b);
     const uint64_t nwt = (n + WT - 1) / WT;
-    bool dirt = false;
+    int dirt = 0;
     auto timeit = [&](const char *name, const char *data, int wgcu, auto launch) {
         float best = 1e9f, sum = 0;
         for (int it = 0; it < 12; it++) {
-            if (dirt) hipLaunchKernelGGL(dirty, dim3(cus * 4), dim3(256), 0, 0, junk, junk16, (uint32_t)it);
+            if (dirt == 1) hipLaunchKernelGGL(dirty, dim3(cus * 4), dim3(256), 0, 0, junk, junk16, (uint32_t)it);
+            if (dirt == 2) hipLaunchKernelGGL(dirtym<1>, dim3(cus * 4), dim3(256), 0, 0, junk, junk16, (uint32_t)it);
+            if (dirt == 3) hipLaunchKernelGGL(dirtym<2>, dim3(cus * 4), dim3(256), 0, 0, junk, junk16, (uint32_t)it);
+            if (dirt) { hipEvent_t x0, x1; (void)x0; (void)x1; }
             hipEventRecord(a);
             launch();
             hipEventRecord(b);
@@ -396,49 +729,35 @@ int main(int argc, char **argv)
             if (it >= 2) { sum += ms; if (ms < best) best = ms; }
         }
         hipError_t e = hipGetLastError();
-        printf("%-10s %-5s %-5s wg/cu=%d  best %.1f us  mean %.1f us  %.0f GB/s  %s\n", name, data, dirt ? "dirty" : "clean", wgcu,
+        static const char *dn[4] = {"clean", "dirty", "dirnt", "dirsc1"};
+        printf("%-10s %-5s %-6s wg/cu=%d  best %.1f us  mean %.1f us  %.0f GB/s  %s\n", name, data, dn[dirt], wgcu,
                best * 1e3, sum / 10 * 1e3, n * 80.0 / (best * 1e-3) / 1e9, e == hipSuccess ? "" : hipGetErrorString(e));
         fflush(stdout);
     };
-    for (int real = 1; real >= 0; real--) {
-        if (real) hipMemcpy(d, hrec.data(), bytes, hipMemcpyHostToDevice);
-        else hipMemset(d, 1, bytes);
-        const char *dn = real ? "real" : "ones";
-        for (int dd = 0; dd < 2; dd++) {
-            dirt = dd;
-            if (!real && dd) continue;
-            for (int wgcu : {1, 2}) {
-                const uint32_t grid = cus * wgcu;
-                const uint64_t wtpb = (nwt + grid - 1) / grid;
-                timeit("r0", dn, wgcu, [&] { hipLaunchKernelGGL((r0<4, false>), dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); });
-                timeit("r0+st", dn, wgcu, [&] { hipLaunchKernelGGL((r0<4, true>), dim3(grid), dim3(256), 0, 0, d, offs, n, wtpb, o, log); });
-                for (int gm : {wgcu, 3 * wgcu}) {
-                    Prm h{d, offs, n, 0, 0, o, log, dq, dirw};
-                    uint32_t gmain = (uint32_t)cus * gm;
-                    h.wt_per_block = (uint32_t)((nwt + gmain - 1) / gmain);
-                    h.grid_main = (uint32_t)((nwt + h.wt_per_block - 1) / h.wt_per_block);
-                    hipMemcpy(dp, &h, sizeof h, hipMemcpyHostToDevice);
-                    char nm[32];
-                    const uint32_t g = (uint32_t)cus * wgcu;
-                    if (gm == wgcu) {
-                        snprintf(nm, sizeof nm, "r1 g%d", gm);
-                        timeit(nm, dn, wgcu, [&] { hipLaunchKernelGGL((rk<4, 1>), dim3(h.grid_main), dim3(256), 0, 0, dp); });
-                        snprintf(nm, sizeof nm, "r5w8 g%d", gm);
-                        timeit(nm, dn, wgcu, [&] { hipLaunchKernelGGL((rkwriter<4, 8>), dim3(h.grid_main), dim3(320), 0, 0, dp); });
-                        snprintf(nm, sizeof nm, "r5w16 g%d", gm);
-                        timeit(nm, dn, wgcu, [&] { hipLaunchKernelGGL((rkwriter<4, 16>), dim3(h.grid_main), dim3(320), 0, 0, dp); });
-                    }
-                    snprintf(nm, sizeof nm, "r2 g%d", gm);
-                    timeit(nm, dn, wgcu, [&] { hipLaunchKernelGGL((rk<4, 2>), dim3(g), dim3(256), 0, 0, dp); });
-                    snprintf(nm, sizeof nm, "r3 g%d", gm);
-                    timeit(nm, dn, wgcu, [&] { hipLaunchKernelGGL((rkw<4, 3>), dim3(g), dim3(256), 0, 0, dp); });
-                    snprintf(nm, sizeof nm, "r4 g%d", gm);
-                    timeit(nm, dn, wgcu, [&] { hipLaunchKernelGGL((rkw<4, 4>), dim3(g), dim3(256), 0, 0, dp); });
-                    snprintf(nm, sizeof nm, "r4b g%d", gm);
-                    timeit(nm, dn, wgcu, [&] { hipLaunchKernelGGL((rk4b<4>), dim3(g), dim3(256), 0, 0, dp); });
-                }
-            }
+    hipMemcpy(d, hrec.data(), bytes, hipMemcpyHostToDevice);
+    for (int dd = 0; dd < 4; dd++) {
+        dirt = dd;
+        for (int wgcu : {1}) {
+            const int gm = 3;
+            Prm h{d, offs, n, 0, 0, o, log, dq, dirw};
+            uint32_t gmain = (uint32_t)cus * gm;
+            h.wt_per_block = (uint32_t)((nwt + gmain - 1) / gmain);
+            h.grid_main = (uint32_t)((nwt + h.wt_per_block - 1) / h.wt_per_block);
+            hipMemcpy(dp, &h, sizeof h, hipMemcpyHostToDevice);
+            const uint32_t g = (uint32_t)cus * wgcu;
+            timeit("r3", "real", wgcu, [&] { hipLaunchKernelGGL((rkw<4, 3>), dim3(g), dim3(256), 0, 0, dp); });
+            timeit("r4", "real", wgcu, [&] { hipLaunchKernelGGL((rkw<4, 4>), dim3(g), dim3(256), 0, 0, dp); });
+            timeit("r4c40 d3", "real", wgcu, [&] { hipLaunchKernelGGL((rk4c<4, 3, 40>), dim3(g), dim3(256), 0, 0, dp); });
         }
+    }
+    // the dirtying kernels' own time
+    for (int m = 1; m < 4; m++) {
+        dirt = 0;
+        timeit(m == 1 ? "dirty" : m == 2 ? "dirtynt" : "dirtysc1", "-", 4, [&] {
+            if (m == 1) hipLaunchKernelGGL(dirty, dim3(cus * 4), dim3(256), 0, 0, junk, junk16, 7u);
+            if (m == 2) hipLaunchKernelGGL(dirtym<1>, dim3(cus * 4), dim3(256), 0, 0, junk, junk16, 7u);
+            if (m == 3) hipLaunchKernelGGL(dirtym<2>, dim3(cus * 4), dim3(256), 0, 0, junk, junk16, 7u);
+        });
     }
     return 0;
 }
