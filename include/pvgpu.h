@@ -385,12 +385,14 @@ int pv_set_slow_defer(pv_ctx *ctx, int defer);
  * dns/v1/DnsStreamHandler.h:252-267). *out: the queries still open at this shard's end, the
  * earlier shards' survivors and this shard's own (pv_free). */
 int pv_edge_carry(pv_ctx *ctx, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes);
-/* Sharded runs: the number of DNS queries this shard leaves open at its end, before any edge
- * carry (an upper bound: the carried list, one entry per event). A merge in which every rank
- * reports 0 has no transaction across a shard edge, so the edge exchange is skipped; otherwise it
- * starts at the first rank that reports one (TransactionManager.h:51-106: a query is the only event
- * a later shard can complete). */
-int pv_edge_open_count(pv_ctx *ctx, uint64_t *n);
+/* Sharded runs, before the merge: what this shard holds that a merge step exchanges.
+ * open_queries: the DNS queries it leaves open at its end, before any edge carry (an upper bound:
+ * the carried list, one entry per event); a merge in which every rank reports 0 has no transaction
+ * across a shard edge, so the edge exchange is skipped, else it starts at the first rank that
+ * reports one (TransactionManager.h:51-106: a query is the only event a later shard can complete).
+ * xact_values: its DNS transaction values (quantile and top_slow inputs); with 0 on every rank the
+ * distributed selections (pv_comm_slow_finish, pv_comm_values_select) have nothing to select. */
+int pv_merge_hints(pv_ctx *ctx, uint64_t *open_queries, uint64_t *xact_values);
 int pv_slow_values_export(pv_ctx *ctx, uint8_t **buf, size_t *bytes);
 int pv_slow_finish(pv_ctx *ctx, const uint8_t *const *bufs, const size_t *sizes, uint32_t nranks);
 /* Quantile inputs of the live window, (slot, kind, value) records, for the merge of the

@@ -169,7 +169,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label",
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
-           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_edge_open_count", "pv_shard_cuts", "pv_net_kernel_name",
+           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_merge_hints", "pv_shard_cuts", "pv_net_kernel_name",
            "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_tcp_exact_lru", "pv_set_dnstap_only_hosts",
            "pv_afpacket_open", "pv_afpacket_attach", "pv_afpacket_run", "pv_afpacket_start", "pv_afpacket_stop",
            "pv_afpacket_stats", "pv_afpacket_close", "pv_afpacket_last_error", "pv_set_bpf", "pv_bpf_validate",
@@ -299,7 +299,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_net_kernel_name.restype = ctypes.c_char_p
     lib.pv_shard_cuts.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, U32, U32, U32, P]
     lib.pv_edge_carry.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
-    lib.pv_edge_open_count.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
+    lib.pv_merge_hints.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     lib.pv_slow_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_slow_finish.argtypes = [P, P, P, U32]
     lib.pv_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
@@ -795,6 +795,7 @@ class PvHandlers:
         self._check(self.lib.pv_synchronize(self.ctx), "pv_synchronize")
 
     def reset(self):
+        self._merge_hints = None  # (dist.check_aligned's, for this window only)
         self._check(self.lib.pv_reset(self.ctx), "pv_reset")
 
     def window_json(self, period: int = 0, merged: bool = False) -> dict:
@@ -1039,11 +1040,12 @@ class PvHandlers:
         self.lib.pv_free(p)
         return data
 
-    def edge_open_count(self) -> int:
-        """DNS queries this shard leaves open at its end, an upper bound (pv_edge_open_count)"""
-        v = ctypes.c_uint64()
-        self._check(self.lib.pv_edge_open_count(self.ctx, ctypes.byref(v)), "pv_edge_open_count")
-        return int(v.value)
+    def merge_hints(self):
+        """(DNS queries this shard leaves open at its end (an upper bound), its DNS transaction
+        values) before a merge (pv_merge_hints)"""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.pv_merge_hints(self.ctx, ctypes.byref(a), ctypes.byref(b)), "pv_merge_hints")
+        return int(a.value), int(b.value)
 
     def values_export(self) -> bytes:
         return self._export(self.lib.pv_values_export, "pv_values_export")

@@ -226,7 +226,8 @@ namespace {
 
 // status words (device): flags, n_events, n_resp, n_vals, DNS messages, new top-N names
 enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNEW = 5, ST_TSEG = 6, ST_TSEG_BYTES = 7,
-       ST_HANDS = 8 /* top-N handlers with entries (device only) */, ST_NKEYS = 9 /* key-list length */, ST_WORDS = 10 };
+       ST_HANDS = 8 /* top-N handlers with entries (device only) */, ST_NKEYS = 9 /* key-list length */,
+       ST_NSLOW = 10 /* general-path records the Net pass deferred (device only) */, ST_WORDS = 11 };
 // status allocation (zeroed per batch): the words above, padded
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
 #define PV_TRASH_WAVES 16384 // Net-pass waves with a 2-KiB trash area (grid <= 4096)
@@ -3819,6 +3820,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.n_events = c->d_status + ST_NEV; // [0] events, [1] responses (ST_NRESP)
     P.n_keys = c->d_status + ST_NKEYS;
     P.n_dns = c->d_status + ST_NDNS;
+    P.n_slow = c->d_status + ST_NSLOW;
     P.want_events = ((c->dns_groups & PV_DNS_TRANSACTIONS) || c->dns2_groups) ? 1 : 0;
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
@@ -3931,7 +3933,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     const bool tc = (c->net_groups & PV_NET_TOP_IPS) && c->reg_waves != 8;
     // PV_NET_KERNEL=span: the span-load pass with the general path deferred (top-IPs groups)
     const bool span = lean && tc && !ring && regw && force && !strcmp(force, "span");
-    if (span) {
+    // the span and register passes defer general-path records to pv_net_slow_list
+    const bool defer = lean && !ring && regw;
+    if (defer) {
         if (c->slow_cap < P.n) {
             if (c->d_slow) hipFree(c->d_slow);
             c->d_slow = nullptr;
@@ -3975,16 +3979,13 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         hipExtLaunchKernelGGL(pv_net_kernel_span, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
         hipExtLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (hipEvent_t) nullptr, e1, 0, dp);
     }
-    else if (lean && c->reg_waves == 8) hipExtLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, e0, e1, 0, dp);
-    else if (lean && tc) {
-        hipExtLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
-        // tuning only (PV_NET_REPEAT=k): k more launches back to back, so a kernel trace shows the
-        // pass right after itself next to the pass after the previous batch's kernels (counters are
-        // then counted k + 1 times)
-        static const int rep = getenv("PV_NET_REPEAT") ? atoi(getenv("PV_NET_REPEAT")) : 0;
-        for (int r = 0; r < rep; r++) hipLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, dp);
+    else if (lean) {
+        // the register pass, then its deferred general-path records (the dispatch stamps span both)
+        if (c->reg_waves == 8) hipExtLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
+        else if (tc) hipExtLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
+        else hipExtLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
+        hipExtLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (hipEvent_t) nullptr, e1, 0, dp);
     }
-    else if (lean) hipExtLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     else hipExtLaunchKernelGGL(pv_net_kernel_ns, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
     e = hipGetLastError();
     if (e != hipSuccess) return c->hipfail(e, "launch pv_net_kernel");
@@ -7563,10 +7564,12 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
     return 0;
 }
 
-int pv_edge_open_count(pv_ctx *c, uint64_t *n)
+int pv_merge_hints(pv_ctx *c, uint64_t *open_queries, uint64_t *xact_values)
 {
+    if (int rc = sync_xvals(c)) return rc;
     std::lock_guard<std::mutex> g(c->mu);
-    *n = c->n_pend;
+    *open_queries = c->n_pend;
+    *xact_values = c->xvals_host.size() + c->slow_xv.size() + c->scands.size();
     return 0;
 }
 

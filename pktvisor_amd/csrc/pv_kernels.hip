@@ -2366,12 +2366,12 @@ __device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
 #ifndef PV_REG_UNCOND
 #define PV_REG_UNCOND 1 // the pipeline with unconditional (clamped) loads
 #endif
-#ifndef PV_ABL_NOSLOW
-#define PV_ABL_NOSLOW 0 // tuning/ablation only: the register pass without its general-path call
+#ifndef PV_REG_SLOW_INLINE
+#define PV_REG_SLOW_INLINE 0 // tuning: the general path as an out-of-line call in the loop (rounds 3-5)
 #endif
 struct NetRegState {
     uint32_t hist[PV_HBINS];
-    uint32_t nd, nx;
+    uint32_t nd, nx, ns;
     int64_t dord[PV_MAX_SHIFTS];
 };
 __device__ __forceinline__ void win_load(const PV_G uint8_t *recs, uint32_t off, uint4 (&W)[5])
@@ -2402,7 +2402,7 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
     __shared__ NetRegState S;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
-    if (threadIdx.x == 0) { S.nd = 0; S.nx = 0; }
+    if (threadIdx.x == 0) { S.nd = 0; S.nx = 0; S.ns = 0; }
     if (threadIdx.x < PV_MAX_SHIFTS) S.dord[threadIdx.x] = P.dpos[threadIdx.x];
     __syncthreads();
     const PV_G uint8_t *const recs = P.recs;
@@ -2499,7 +2499,8 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         if (temit && __ballot(istcp)) {
             if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
         }
-        if (slowm && !PV_ABL_NOSLOW) {
+#if PV_REG_SLOW_INLINE
+        if (slowm) {
             if (active && !fast) {
                 const SAcc R{recs, nullptr, 0, 0, 0, 1};
                 const SlowOut so = net_slow_p(Pp, R, off, i);
@@ -2513,6 +2514,19 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                 istcp = so.l4 == 6;
             }
         }
+#else
+        if (slowm) {
+            // general-path records (VLAN, IPv6, options, tunnels, other link types): their indices
+            // to the range's list, which pv_net_slow_list parses after this pass (an out-of-line
+            // call in the loop made the compiler give every wave a stack: 176 B of scratch a lane and
+            // 167 VGPRs, against 101 without it, and C2 222 -> 208 us, profiles/r6/noslow); an LDS
+            // reservation, since a returning global atomic would wait on every load in flight
+            uint32_t q = 0;
+            if (lane == 0) q = atomicAdd(&S.ns, (uint32_t)__popcll(slowm));
+            q = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_mbcnt_hi((uint32_t)(slowm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)slowm, 0u));
+            if (active && !fast) P.slow_list[wbeg * PV_WT + q] = (uint32_t)i;
+        }
+#endif
         if (__ballot(hv != PV_NOH && hv > 65535)) {
             if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
         }
@@ -2670,9 +2684,12 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         P.mq_cnt[lb] = 0;
         P.dq_cnt[lb] = S.nd;
         if (compact) P.ipx_cnt[lb] = S.nx;
+        P.slow_cnt[lb] = S.ns;
         if (S.nd) atomicAdd(P.n_dns, S.nd);
+        if (S.ns) atomicAdd(P.n_slow, S.ns);
         S.nd = 0;
         S.nx = 0;
+        S.ns = 0;
     }
     lds_barrier();
     }
@@ -2903,6 +2920,7 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
         P.ipx_cnt[lb] = 0;
         P.slow_cnt[lb] = S.ns;
         if (S.nd) atomicAdd(P.n_dns, S.nd);
+        if (S.ns) atomicAdd(P.n_slow, S.ns);
         S.nd = 0;
         S.ns = 0;
     }
@@ -2934,6 +2952,7 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 extern "C" __global__ void __launch_bounds__(256) pv_net_slow_list(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    if (!*P.n_slow) return; // (the common batch: Ethernet + IPv4 only, nothing deferred)
     const uint32_t slot = P.slot_of[0];
     const uint64_t per_range = (uint64_t)P.wt_per_block * PV_WT;
     NetCtr c;

@@ -436,6 +436,7 @@ struct PvParams {
     // pv_net_slow_list (record indices at each range's base, each range's count)
     PV_G uint32_t *slow_list;
     PV_G uint32_t *slow_cnt;
+    PV_G uint32_t *n_slow; // deferred records of the batch (status word; pv_net_slow_list exits at 0)
     PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
     PV_G uint64_t *cb;    // combined update lists sorted by table region, mq_cap entries per workgroup
     PV_G uint32_t *cb_cnt;

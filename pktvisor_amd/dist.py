@@ -178,29 +178,33 @@ def _rank(handlers, group=None, comm=None):
 def check_aligned(handlers, group=None, comm=None):
     """The bucket merge pairs slots by id: every rank's windows must hold the same periods
     (slot, start second) — what the global plan guarantees; checked before the merge. The same
-    gather carries each rank's count of DNS queries open at its shard's end
-    (pv_edge_open_count), which merge_edges uses; returns those counts in rank order."""
+    gather carries each rank's merge hints (pv_merge_hints: DNS queries open at its shard's end,
+    DNS transaction values), which merge_edges and the selections use; returns them in rank
+    order."""
     import json
     from pktvisor_amd import PART_DNS, PART_NET
     wins = [handlers.window_periods(PART_NET), handlers.window_periods(PART_DNS)]
-    mine = json.dumps([wins, handlers.edge_open_count()]).encode()
+    mine = json.dumps([wins, list(handlers.merge_hints())]).encode()
     allv = [json.loads(v) for v in _allgather(handlers, mine, group, comm)]
     if any(v[0] != allv[0][0] for v in allv):
         raise RuntimeError(f"shard windows differ across ranks: {[v[0] for v in allv]}")
-    return [int(v[1]) for v in allv]
+    hints = [tuple(int(x) for x in v[1]) for v in allv]
+    handlers._merge_hints = hints  # (merge_values, in finalize_window, reads the value counts)
+    return hints
 
 
-def merge_edges(handlers, group=None, comm=None, open_counts=None):
+def merge_edges(handlers, group=None, comm=None, hints=None):
     """DNS transactions across shard edges. Deferred runs carry the open queries rank by rank
     (pv_edge_carry: rank r computes its carry in round r from rank r-1's), so a query meets the
     first event of its key in ANY later shard, after that shard's purges; otherwise every rank's
-    stubs are gathered once and paired with the previous shards'. open_counts (every rank's
-    pv_edge_open_count, from check_aligned): a rank before the first that leaves a query open
+    stubs are gathered once and paired with the previous shards'. hints (every rank's
+    pv_merge_hints, from check_aligned): a rank before the first that leaves a query open
     receives nothing, so the chain starts there, and with no open query anywhere nothing crosses
     an edge and no round runs (a stream without DNS transactions). The last rank's carry is
     nobody's input: it is computed, not gathered."""
-    if open_counts is None:
-        open_counts = [int(x) for x in _allgather_ints(handlers, handlers.edge_open_count(), group, comm)]
+    if hints is None:
+        hints = check_aligned(handlers, group, comm)
+    open_counts = [h[0] for h in hints]
     if not any(open_counts):
         return
     first = next(r for r, k in enumerate(open_counts) if k)
@@ -218,15 +222,17 @@ def merge_edges(handlers, group=None, comm=None, open_counts=None):
     handlers.edge_merge(_allgather(handlers, handlers.edge_export(), group, comm), me)
 
 
-def _allgather_ints(handlers, v: int, group=None, comm=None):
-    return [int.from_bytes(b, "little") for b in _allgather(handlers, int(v).to_bytes(8, "little"), group, comm)]
+def _no_values(handlers):
+    """every rank reported no DNS transaction value at check_aligned (nothing to select)"""
+    hints = getattr(handlers, "_merge_hints", None)
+    return hints is not None and not any(h[1] for h in hints)
 
 
 def merge_slow(handlers, group=None, comm=None):
     """top_slow over the whole stream: each DNS period's p90 over every rank's transaction times
     by distributed selection (no values shipped), then each rank's deferred candidates (after the
-    edge merge, before the top-N exchange)"""
-    if getattr(handlers, "slow_defer", False):
+    edge merge, before the top-N exchange); skipped when no rank holds a transaction value"""
+    if getattr(handlers, "slow_defer", False) and not _no_values(handlers):
         if comm == "pv":
             handlers.comm_slow_finish()
         else:
@@ -258,7 +264,7 @@ def _handlers_device(handlers):
 def merge_values(handlers, group=None, comm=None):
     """quantile inputs across shards: exact distributed selection (pv_values_x_select), eight
     rounds of group histograms summed over the ranks instead of every rank's values"""
-    if (handlers.comm_ranks if comm == "pv" else dist.get_world_size(group)) == 1:
+    if (handlers.comm_ranks if comm == "pv" else dist.get_world_size(group)) == 1 or _no_values(handlers):
         return
     if comm == "pv":
         handlers.comm_values_select()
@@ -273,8 +279,8 @@ def merge_window(handlers, device, group=None, comm=None, finalize=True):
     device part; finalize=True then assembles the read view (the top-N lists with names, the
     quantiles by distributed selection), which finalize_window also does on its own."""
     handlers.synchronize()
-    open_counts = check_aligned(handlers, group, comm)
-    merge_edges(handlers, group, comm, open_counts)
+    hints = check_aligned(handlers, group, comm)
+    merge_edges(handlers, group, comm, hints)
     merge_slow(handlers, group, comm)
     if comm == "pv":
         handlers.comm_allreduce_window()

@@ -97,7 +97,7 @@ def rank_main(args):
         h.synchronize()
         counts = []
         step("check_aligned", lambda: counts.append(pvdist.check_aligned(h)))
-        step("edges", lambda: pvdist.merge_edges(h, open_counts=counts[0]))
+        step("edges", lambda: pvdist.merge_edges(h, hints=counts[0]))
         step("slow", lambda: pvdist.merge_slow(h))
         step("buckets", lambda: pvdist.reduce_handlers(h, dev))
         step("topn_owner", lambda: pvdist.merge_topn(h))
