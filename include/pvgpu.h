@@ -385,6 +385,15 @@ int pv_set_slow_defer(pv_ctx *ctx, int defer);
  * dns/v1/DnsStreamHandler.h:252-267). *out: the queries still open at this shard's end, the
  * earlier shards' survivors and this shard's own (pv_free). */
 int pv_edge_carry(pv_ctx *ctx, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes);
+/* The end of the capture: the next pv_process_host / pv_process_device call holds the capture's
+ * last records, and after them every TCP connection still open is closed, as
+ * TcpReassembly::closeAllConnections does when a pcap file ends and when the input stops
+ * (src/inputs/pcap/PcapInputStream.cpp:522, :244): a connection's held out-of-order fragments are
+ * delivered behind their missing-data markers and the DNS messages that completes are counted at
+ * the connection's end time, with the direction the input cached for its last packet
+ * (_packet_dir_cache, :399-416). on = 0 disarms it. The flag applies to that call's final batch
+ * (pv_process_host cuts its data into batches) and is cleared by the call. */
+int pv_set_end_of_capture(pv_ctx *ctx, int on);
 /* Sharded runs, before the merge: what this shard holds that a merge step exchanges.
  * open_queries: the DNS queries it leaves open at its end, before any edge carry (an upper bound:
  * the carried list, one entry per event); a merge in which every rank reports 0 has no transaction

@@ -169,7 +169,7 @@ EXPORTS = ["pv_version", "pv_device_count", "pv_create", "pv_destroy", "pv_last_
            "pv_pcapng_records", "pv_tpacket3_block_records", "pv_window_prometheus", "pv_add_static_label",
            "pv_window_opentelemetry", "pv_check_period_shift", "pv_bucket_merge", "pv_bucket_json",
            "pv_bucket_prometheus", "pv_bucket_opentelemetry", "pv_bucket_free", "pv_set_slow_defer",
-           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_merge_hints", "pv_shard_cuts", "pv_net_kernel_name",
+           "pv_slow_values_export", "pv_slow_finish", "pv_edge_carry", "pv_merge_hints", "pv_set_end_of_capture", "pv_shard_cuts", "pv_net_kernel_name",
            "pv_plan_dns_draws", "pv_sample_skip", "pv_set_tcp_reassembly_limit", "pv_set_tcp_exact_lru", "pv_set_dnstap_only_hosts",
            "pv_afpacket_open", "pv_afpacket_attach", "pv_afpacket_run", "pv_afpacket_start", "pv_afpacket_stop",
            "pv_afpacket_stats", "pv_afpacket_close", "pv_afpacket_last_error", "pv_set_bpf", "pv_bpf_validate",
@@ -300,6 +300,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.pv_shard_cuts.argtypes = [P, ctypes.c_size_t, P, ctypes.c_uint64, U32, U32, U32, P]
     lib.pv_edge_carry.argtypes = [P, P, ctypes.c_size_t, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_merge_hints.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.pv_set_end_of_capture.argtypes = [P, ctypes.c_int]
     lib.pv_slow_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.pv_slow_finish.argtypes = [P, P, P, U32]
     lib.pv_values_export.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
@@ -702,6 +703,11 @@ class PvHandlers:
         buf = recs if isinstance(recs, np.ndarray) else np.frombuffer(recs, dtype=np.uint8)
         self._check(self.lib.pv_process_host(self.ctx, buf.ctypes.data, buf.nbytes), "pv_process_host")
 
+    def set_end_of_capture(self, on: bool = True):
+        """the next process_host / process_device call ends the capture: TCP connections still open
+        after its last record are closed (pv_set_end_of_capture, TcpReassembly::closeAllConnections)"""
+        self._check(self.lib.pv_set_end_of_capture(self.ctx, int(on)), "pv_set_end_of_capture")
+
     def process_dnstap(self, frames):
         """pv_process_dnstap: a dnstap Frame Streams file's events through both handlers (the
         DNS handler's dnstap_msg_type from dns_config)."""
@@ -1101,6 +1107,8 @@ def pktvisor_reader(path: str, host_spec: Optional[str] = None, periods: int = 5
     h = PvHandlers(host_spec=host_spec, num_periods=periods, linktype=linktype, ts_nano=ts_nano,
                    max_records=max(1, idx.n), **kw)
     try:
+        # the file's end closes the connections still open (PcapInputStream.cpp:522)
+        h.set_end_of_capture()
         h.process_host(recs)
         if idx.n:
             h.set_end_tstamp(*last_record_ts(recs, idx, ts_nano))

@@ -219,6 +219,8 @@ extern "C" __global__ void pv_tcp_lookup(const PvTcpParams *T);
 extern "C" __global__ void pv_tcp_insert(const PvTcpParams *T);
 extern "C" __global__ void pv_tcp_flow(const PvTcpParams *T);
 extern "C" __global__ void pv_tcp_migrate(const PvTcpParams *T);
+extern "C" __global__ void pv_tcp_eoc(const PvTcpParams *T, const PvTcpSeg *seg, uint32_t n_seg, uint64_t *set, uint32_t set_mask,
+                                      PvTcpSeg *out, uint32_t *cnt, uint32_t idx, uint32_t sec, uint32_t usec, uint32_t dir);
 extern "C" hipError_t pv_tcp_sort(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin, uint32_t *vout,
                                   size_t n, hipStream_t s);
 
@@ -668,6 +670,7 @@ struct pv_ctx {
         PvIxParams *h_ix = nullptr; // pinned: params, then status / small read-backs
         uint32_t ix_nseg = 0;
         uint32_t cut_o[2] = {0, 0}; // offsets of the records either side of the last ts_sec change
+        bool last = false;          // host-index ingest: the data's final batch
     };
     bool device_index = true; // PV_INGEST_INDEX=host selects the host walk
     // device-index ingest ring: raw chunks land at offset chunk of 2 x chunk buffers, the
@@ -761,6 +764,13 @@ struct pv_ctx {
     uint32_t tmsg_cap = 0;
     uint32_t tcp_stage = 0;   // stage ordinal (flow entries remember the last one that touched them)
     bool tcp_active = false;  // a stage has run since the last reset
+    // the end of the capture (pv_set_end_of_capture): armed for the next processing call, which
+    // marks its final batch (eoc_batch) and that batch's last TCP stage (eoc_stage); in_host: inside
+    // pv_process_host, whose ingest loops mark the final batch themselves
+    bool eoc_armed = false, eoc_batch = false, eoc_stage = false, in_host = false;
+    PvTcpSeg *d_eoc = nullptr; // close segments of the open connections (eoc_cap: flow table + batch segments)
+    uint64_t eoc_cap = 0;
+    uint32_t *d_eoc_cnt = nullptr;
     bool tcp_pre = false;     // this batch's stage runs ahead of the Net pass (prescan emits)
     uint32_t tcp_nmsg = 0;    // messages of the current batch
     // tcp_packet_reassembly_cache_limit (0: not set). In the exact LRU mode PcapInputStream's LRU
@@ -2585,7 +2595,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_iplog32,
                     c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_slow, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose,
                     c->d_xcnt, c->d_xrhdr, c->d_xtot, c->d_xsend, c->d_xrecv, c->d_xp, c->d_bpf, c->d_fwork, c->d_frecs,
-                    c->d_foffs, c->d_fsc, c->d_fscan};
+                    c->d_foffs, c->d_fsc, c->d_fscan, c->d_eoc, c->d_eoc_cnt};
     for (void *p : ptrs) if (p) hipFree(p);
     if (c->d_dbits) hipFree(c->d_dbits);
     for (void *hp : {(void *)c->h_params, (void *)c->h_xparams, (void *)c->h_status, (void *)c->h_dbits, (void *)c->h_tcpcnt,
@@ -3023,6 +3033,42 @@ void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vec
     }
 }
 
+// The segment arrays of the TCP stage for `need` segments (the end of a capture adds one per open
+// connection to a batch's own), the first `keep` segments kept
+int tcp_grow_segs(pv_ctx *c, uint64_t need, uint32_t keep, hipStream_t st)
+{
+    if (need <= c->tseg_cap) return 0;
+    if (need > 0xffffffffull) return c->fail(PV_ECAPACITY, "TCP segments");
+    hipError_t e;
+    PvTcpSeg *seg = nullptr;
+    if (!hip_ok(e = hipMalloc(&seg, need * sizeof(PvTcpSeg))) ||
+        (keep && !hip_ok(e = hipMemcpyAsync(seg, c->d_tseg, (size_t)keep * sizeof(PvTcpSeg), hipMemcpyDeviceToDevice, st))) ||
+        !hip_ok(e = hipStreamSynchronize(st)))
+        return c->hipfail(e, "TCP segments");
+    hipFree(c->d_tseg);
+    c->d_tseg = seg;
+    for (int k = 0; k < 2; k++) {
+        hipFree(c->d_tkey[k]);
+        hipFree(c->d_tval[k]);
+        c->d_tkey[k] = nullptr;
+        c->d_tval[k] = nullptr;
+    }
+    hipFree(c->d_run_flow);
+    hipFree(c->d_tsort_tmp);
+    c->d_run_flow = nullptr;
+    c->d_tsort_tmp = nullptr;
+    if (!hip_ok(e = hipMalloc(&c->d_tkey[0], need * 8)) || !hip_ok(e = hipMalloc(&c->d_tkey[1], need * 8)) ||
+        !hip_ok(e = hipMalloc(&c->d_tval[0], need * 4)) || !hip_ok(e = hipMalloc(&c->d_tval[1], need * 4)) ||
+        !hip_ok(e = hipMalloc(&c->d_run_flow, need * 4)))
+        return c->hipfail(e, "TCP segments");
+    size_t tmp = 0;
+    pv_tcp_sort(nullptr, &tmp, c->d_tkey[0], c->d_tkey[1], c->d_tval[0], c->d_tval[1], need, st);
+    c->tsort_tmp_bytes = std::max<size_t>(tmp, 256);
+    if (!hip_ok(e = hipMalloc(&c->d_tsort_tmp, c->tsort_tmp_bytes))) return c->hipfail(e, "TCP sort scratch");
+    c->tseg_cap = (uint32_t)need;
+    return 0;
+}
+
 // The TCP stage of a batch: its segments (n_seg, seg_bytes payload) through reassembly and
 // framing into message records. d_offs / n: the whole batch. With want_ords the messages'
 // (ord, second) pairs come back for the DNS shift plan.
@@ -3034,6 +3080,8 @@ int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t
     if (n_seg > c->tseg_cap)
         return c->fail(PV_ECAPACITY, "%u DNS-over-TCP segments in one batch exceed the capacity %u (max_records)", n_seg,
                        c->tseg_cap);
+    const bool eoc = c->eoc_stage && n > 0;
+    c->eoc_stage = false;
     if (n_seg == 0 && !c->tcp_active) return 0;
     if (int rc = tcp_alloc(c)) return rc;
     hipError_t e;
@@ -3147,6 +3195,78 @@ int tcp_stage(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, uint64_t
         T.lru_ev = nullptr;
         T.fclose = c->d_fclose;
         if (!hip_ok(e = hipStreamSynchronize(st))) return c->hipfail(e, "TCP LRU closes");
+    }
+    if (eoc) {
+        // TcpReassembly::closeAllConnections after the capture's last record (PcapInputStream.cpp:522,
+        // :244 on stop): a close segment for every open connection, with the last record's time and
+        // the direction the input cached for it (_packet_dir_cache, :399-416)
+        const uint32_t ncap = 1u << c->flow_cap_log2;
+        const uint64_t ncand = (uint64_t)ncap + n_seg;
+        uint32_t set_log2 = 4;
+        while ((1ull << set_log2) < 2 * ncand) set_log2++;
+        if (ncand > c->eoc_cap) {
+            if (c->d_eoc) (void)hipFree(c->d_eoc);
+            c->d_eoc = nullptr;
+            c->eoc_cap = 0;
+            if (!hip_ok(e = hipMalloc(&c->d_eoc, (size_t)ncand * sizeof(PvTcpSeg)))) return c->hipfail(e, "TCP end-of-capture segments");
+            c->eoc_cap = ncand;
+        }
+        if (!c->d_eoc_cnt && !hip_ok(e = hipMalloc(&c->d_eoc_cnt, 4))) return c->hipfail(e, "TCP end-of-capture segments");
+        uint64_t *d_set = nullptr;
+        struct SetFree {
+            uint64_t *&p;
+            ~SetFree() { if (p) (void)hipFree(p); }
+        } set_free{d_set};
+        if (!hip_ok(e = hipMalloc((void **)&d_set, (size_t)8 << set_log2)) ||
+            !hip_ok(e = hipMemsetAsync(d_set, 0, (size_t)8 << set_log2, st)))
+            return c->hipfail(e, "TCP end-of-capture key set");
+        uint32_t lo = 0;
+        uint8_t rec[16 + 512];
+        memset(rec, 0, sizeof rec);
+        if (!hip_ok(e = hipMemcpyAsync(&lo, d_offs + (n - 1), 4, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)) ||
+            !hip_ok(e = hipMemcpyAsync(rec, d_recs + lo, 16, hipMemcpyDeviceToHost, st)) || !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "last record");
+        uint32_t hdr[4];
+        memcpy(hdr, rec, 16);
+        const uint32_t cap = std::min<uint32_t>(hdr[2], 512);
+        if (cap && (!hip_ok(e = hipMemcpyAsync(rec + 16, d_recs + lo + 16, cap, hipMemcpyDeviceToHost, st)) ||
+                    !hip_ok(e = hipStreamSynchronize(st))))
+            return c->hipfail(e, "last record");
+        PvParams P;
+        params_common(c, P, d_recs, d_offs, n);
+        pvname::Parsed o;
+        pvname::parse_record(pvname::HostRecs{rec, 16 + (size_t)cap}, pvname::parse_cfg(P), P, 0, o);
+        const uint32_t usec = c->cfg.ts_nano ? hdr[1] / 1000u : hdr[1];
+        if (!hip_ok(e = hipMemsetAsync(c->d_eoc_cnt, 0, 4, st)) || !hip_ok(e = upload_params(c->d_tparams, c->h_tparams, sizeof T, st)))
+            return c->hipfail(e, "TCP end of capture");
+        hipLaunchKernelGGL(pv_tcp_eoc, dim3((uint32_t)((ncand + 255) / 256)), dim3(256), 0, st, dT, (const PvTcpSeg *)c->d_tseg, n_seg,
+                           d_set, (uint32_t)((1ull << set_log2) - 1), c->d_eoc, c->d_eoc_cnt, (uint32_t)(n - 1), hdr[0], usec,
+                           (uint32_t)o.dir);
+        uint32_t ne = 0;
+        if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipMemcpyAsync(&ne, c->d_eoc_cnt, 4, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipStreamSynchronize(st)))
+            return c->hipfail(e, "TCP end of capture");
+        if (ne) {
+            if (int rc = tcp_grow_segs(c, (uint64_t)n_seg + ne, n_seg, st)) return rc;
+            if (!hip_ok(e = hipMemcpyAsync(c->d_tseg + n_seg, c->d_eoc, (size_t)ne * sizeof(PvTcpSeg), hipMemcpyDeviceToDevice, st)))
+                return c->hipfail(e, "TCP end of capture");
+            if (T.fclose) {
+                // (the exact LRU mode's closes are per segment: none for these)
+                std::vector<uint32_t> none(3ull * ne, PVT_FCLOSE_NONE);
+                if (int rc = PV_GROW(c, c->d_fclose, c->fclose_cap, 3ull * (n_seg + ne), "TCP LRU closes")) return rc;
+                if (!hip_ok(e = hipMemcpyAsync(c->d_fclose + 3ull * n_seg, none.data(), none.size() * 4, hipMemcpyHostToDevice, st)) ||
+                    !hip_ok(e = hipStreamSynchronize(st)))
+                    return c->hipfail(e, "TCP end of capture");
+                T.fclose = c->d_fclose;
+            }
+            n_seg += ne;
+            T.n_seg = n_seg;
+            T.seg = c->d_tseg;
+            T.skey = c->d_tkey[1];
+            T.sval = c->d_tval[1];
+            T.run_flow = c->d_run_flow;
+            blocks = (n_seg + 255) / 256;
+        }
     }
     if (int rc = run(false)) return rc;
     if (!hip_ok(e = hipMemcpyAsync(c->h_tcpcnt, c->d_tcpcnt, PVT_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
@@ -4147,6 +4267,7 @@ int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const
         uint32_t tseg[2] = {0, 0};
         if (int rc = dns_prescan(c, d_recs, d_offs, info->n_records, st, true, tseg)) return rc;
         const bool dns_may = c->cfg.num_periods > 1 && top >= c->dns.next_shift_sec;
+        c->eoc_stage = c->eoc_batch;
         if (int rc = tcp_stage(c, d_recs, d_offs, info->n_records, tseg[0], tseg[1], (uint32_t)info->first_sec, true, st))
             return rc;
         if (c->cfg.num_periods <= 1) return 0;
@@ -4164,6 +4285,7 @@ int batch_shifts(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, const
     if (c->tcp_pre) {
         uint32_t tseg[2] = {0, 0};
         if (int rc = dns_prescan(c, d_recs, d_offs, info->n_records, st, true, tseg)) return rc;
+        c->eoc_stage = c->eoc_batch;
         if (int rc = tcp_stage(c, d_recs, d_offs, info->n_records, tseg[0], tseg[1], (uint32_t)info->first_sec, dns_may, st))
             return rc;
     }
@@ -4291,6 +4413,17 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
     hipStream_t saved = c->stream;
     c->stream = st;
     struct Restore { pv_ctx *c; hipStream_t s; ~Restore() { c->stream = s; } } restore{c, saved};
+    // the end of the capture (pv_set_end_of_capture): a direct call is the capture's final batch;
+    // pv_process_host's ingest loops mark their final batch themselves
+    if (!c->in_host) c->eoc_batch = c->eoc_armed;
+    struct EocDone {
+        pv_ctx *c;
+        ~EocDone()
+        {
+            c->eoc_stage = false;
+            if (!c->in_host) c->eoc_armed = c->eoc_batch = false;
+        }
+    } eoc_done{c};
     if (info->n_records == 0) return 0;
     if (info->n_records > c->max_records) return c->fail(PV_ECAPACITY, "batch of %llu records exceeds max_records %llu",
                                            (unsigned long long)info->n_records, (unsigned long long)c->max_records);
@@ -4330,6 +4463,8 @@ int pv_process_device(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_offs, 
                 return c->hipfail(e, "span end");
             rec_bytes = ob;
         }
+        // (a batch with a TCP stage ahead of its spans ran it in batch_shifts)
+        c->eoc_stage = c->eoc_batch && b == n && !c->tcp_pre;
         if (int rc = process_span(c, d_recs, d_offs, a, b - a, rec_bytes, ns, ds, (uint32_t)info->first_sec, st)) return rc;
         a = b;
     }
@@ -5123,6 +5258,7 @@ int process_host_ring(pv_ctx *c, const uint8_t *recs, size_t bytes)
             }
             auto t2 = std::chrono::steady_clock::now();
             HP(2);
+            c->eoc_batch = c->eoc_armed && !capped && last_piece; // the data ends with this batch
             rc = pv_process_device(c, b, r.d_offs, &info, st.sci.data(), st.scs.data(), nullptr);
             if (!rc) rc = pv_synchronize(c);
             HP(8);
@@ -5188,10 +5324,15 @@ int pv_process_host(pv_ctx *c, const uint8_t *recs, size_t bytes)
     {
         std::lock_guard<std::mutex> g(c->mu);
         if (int rc = merged_refuse(c)) return rc;
+        c->in_host = true;
     }
     // (the pcap input's BPF filter, PcapInputStream.cpp:485-488, runs on the device on each batch:
     // pv_process_device)
-    return process_host_block(c, recs, bytes);
+    const int rc = process_host_block(c, recs, bytes);
+    std::lock_guard<std::mutex> g(c->mu);
+    c->in_host = false;
+    c->eoc_armed = c->eoc_batch = c->eoc_stage = false;
+    return rc;
 }
 
 namespace {
@@ -5261,6 +5402,13 @@ int process_host_block(pv_ctx *c, const uint8_t *recs, size_t bytes)
             }
             c->ingest_ms[2] += ms_since(t2);
             pos += used;
+            // the final batch: no complete record follows (at most a partial one)
+            {
+                const size_t rest = bytes - pos;
+                uint32_t cl = 0;
+                if (rest >= 16) memcpy(&cl, recs + pos + 8, 4);
+                st.last = rest < 16 || 16 + (size_t)cl > rest;
+            }
             std::lock_guard<std::mutex> g(mu);
             state[k & 1] = 1;
             k++;
@@ -5284,6 +5432,7 @@ int process_host_block(pv_ctx *c, const uint8_t *recs, size_t bytes)
         auto t0 = std::chrono::steady_clock::now();
         hipError_t e = hipStreamWaitEvent(c->stream, st.copied, 0);
         if (!hip_ok(e)) rc = c->hipfail(e, "stream wait");
+        c->eoc_batch = c->eoc_armed && st.last;
         if (!rc) rc = pv_process_device(c, st.d_recs, st.d_offs, &st.info, st.sci.data(), st.scs.data(), nullptr);
         if (!rc) rc = pv_synchronize(c);
         c->ingest_ms[3] += ms_since(t0);
@@ -7561,6 +7710,13 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
     *out = (uint8_t *)malloc(*out_bytes ? *out_bytes : 1);
     if (!*out) return c->fail(PV_ECAPACITY, "out of host memory");
     if (!keep.empty()) memcpy(*out, keep.data(), *out_bytes);
+    return 0;
+}
+
+int pv_set_end_of_capture(pv_ctx *c, int on)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    c->eoc_armed = on != 0;
     return 0;
 }
 

@@ -242,8 +242,10 @@ struct PvTcpSeg {
 // PV_TF_NODATA: a TCP packet reassembly ignores (no payload and no SYN/FIN/RST, or no valid TCP
 // header), emitted in the exact LRU mode for the cleanup that follows every TCP packet;
 // PV_TF_CLOSE: a close-only segment the host's LRU replay adds for a connection it closes in a
-// batch that holds none of its packets
-enum { PV_TF_FIN = 1, PV_TF_SYN = 2, PV_TF_RST = 4, PV_TF_NODATA = 0x40, PV_TF_CLOSE = 0x80 };
+// batch that holds none of its packets;
+// PV_TF_EOC (with PV_TF_CLOSE): the end of the capture for an open connection, after the batch's
+// last record (TcpReassembly::closeAllConnections, PcapInputStream.cpp:244,522; pv_tcp_eoc)
+enum { PV_TF_FIN = 1, PV_TF_SYN = 2, PV_TF_RST = 4, PV_TF_EOC = 0x20, PV_TF_NODATA = 0x40, PV_TF_CLOSE = 0x80 };
 static_assert(sizeof(PvTcpSeg) == 48, "three 16-B stores");
 
 // TcpReassemblyData + DnsStreamHandler's TcpFlowData of one connection, carried across batches

@@ -34,7 +34,8 @@
 // capture without the handshake), which the reference closes as soon as it reaches the LRU's
 // tail, and when more than 100 connections time out at one packet. Not modelled in either: the
 // closed-connection purge (wall clock in PcapPlusPlus), the puts of data that closing an evicted
-// connection flushes, the flush of open connections at the end of a capture.
+// connection flushes. The flush of open connections at the end of a capture is pv_tcp_eoc's
+// segments in the final batch (pv_set_end_of_capture).
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -552,6 +553,26 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
         const PvTcpSeg g = T.seg[T.sval[k]];
         if (fc_idx != PVT_FCLOSE_NONE && g.idx > fc_idx && F.f.live && !F.f.closed)
             force_close();
+        if (g.flags & PV_TF_EOC) {
+            // closeAllConnections after the capture's last record: the connection's held fragments
+            // go out behind their missing-data markers, its messages at its endTime, with the
+            // direction of the capture's last packet (_packet_dir_cache). A connection the default
+            // mode would have timed out at a later TCP packet of another flow closes at its
+            // time-out second, as it would have there.
+            if (F.f.live && !F.f.closed) {
+                F.cur_idx = g.idx;
+                F.sub = 3;
+                F.cur_sec = g.sec;
+                F.cur_dir = g.dirv6 & 3;
+                uint32_t when = g.sec;
+                if (!T.exact) {
+                    const uint32_t lt = *T.lt_carry;
+                    if (lt && lt - 1 >= F.f.lru_sec + PV_TCP_TIMEOUT) when = F.f.lru_sec + PV_TCP_TIMEOUT;
+                }
+                close_conn(T, F, when);
+            }
+            continue;
+        }
         F.ev = 0;
         F.put_sec = 0;
         packet(T, F, g);
@@ -602,6 +623,47 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
     }
     F.f.stage = T.stage;
     T.flows[fi] = F.f;
+}
+
+// TcpReassembly::closeAllConnections at the end of a capture: a close segment (PV_TF_EOC) for
+// every connection that may be open after the batch, at the batch's last record (idx), the
+// record's time and the direction of the capture's last packet; the TCP stage then runs them as
+// its last segments. Candidates: the open entries of the flow table (threads [0, 2^flow_cap_log2))
+// and the flow keys of the batch's segments (the threads after), once each (a hash set of the
+// keys, at least twice the candidates in size); a close of a connection the batch closes is a
+// no-op in pv_tcp_flow.
+extern "C" __global__ void pv_tcp_eoc(const PvTcpParams *__restrict__ Tp, const PvTcpSeg *__restrict__ seg, uint32_t n_seg,
+                                      uint64_t *__restrict__ set, uint32_t set_mask, PvTcpSeg *__restrict__ out,
+                                      uint32_t *__restrict__ cnt, uint32_t idx, uint32_t sec, uint32_t usec, uint32_t dir)
+{
+    PV_CREF(PvTcpParams) T = *(const PV_C PvTcpParams *)Tp;
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t ncap = 1u << T.flow_cap_log2;
+    uint32_t fkey;
+    if (h < ncap) {
+        const PV_G PvTcpFlow &f = T.flows[h];
+        if (!(f.tag >> 32) || !f.live || f.closed) return;
+        fkey = (uint32_t)f.tag;
+    } else if (h - ncap < n_seg) {
+        fkey = seg[h - ncap].fkey;
+    } else {
+        return;
+    }
+    const uint64_t mine = (1ull << 32) | fkey;
+    for (uint32_t slot = fmix32(fkey) & set_mask;; slot = (slot + 1) & set_mask) {
+        const uint64_t prev = atomicCAS((unsigned long long *)&set[slot], 0ull, (unsigned long long)mine);
+        if (prev == mine) return; // another candidate of this connection emits it
+        if (prev == 0) break;
+    }
+    PvTcpSeg g;
+    memset(&g, 0, sizeof g);
+    g.idx = idx;
+    g.fkey = fkey;
+    g.sec = sec;
+    g.usec = usec;
+    g.flags = PV_TF_CLOSE | PV_TF_EOC;
+    g.dirv6 = (uint8_t)dir;
+    out[atomicAdd(cnt, 1u)] = g;
 }
 
 // flows that carried bytes into this batch but had no packet in it keep them: copied to

@@ -159,7 +159,7 @@ def _frame(src, dst, sport, dport, seq, flags, payload, v6):
 
 
 def tcp_dns_pcap(seed: int = 1, flows: int = 60, duration_s: float = 20.0, udp_share: float = 0.3,
-                 noise_share: float = 0.3, pauses: int = 0) -> bytes:
+                 noise_share: float = 0.3, pauses: int = 0, open_tails: int = 0) -> bytes:
     """DNS over TCP traffic for the reassembly parity tests: connections to port 53 (IPv4 and
     IPv6) carrying pipelined queries and responses that are cut into segments at random byte
     boundaries, with out-of-order segments, duplicate and overlapping retransmissions, a
@@ -167,8 +167,12 @@ def tcp_dns_pcap(seed: int = 1, flows: int = 60, duration_s: float = 20.0, udp_s
     FIN and RST closes, a reused client port after a close; interleaved with UDP DNS and
     non-DNS TCP noise (port 443). With pauses > 0 that many connections fall silent for 35 s
     while the noise goes on (PcapInputStream's 30 s TCP timeout). Timestamps are monotone.
-    Every connection with a gap left in its stream ends with FIN or RST, so no data is left
-    for the end-of-capture flush (which the device path does not model)."""
+    Every connection with a gap left in its stream ends with FIN or RST, except with
+    open_tails > 0: that many connections lose one data segment for good and send no FIN or
+    RST, so the segments after the hole are still held when the capture ends and only the
+    end-of-capture flush delivers them (PcapInputStream closes every connection when the
+    file is read, TcpReassembly::closeAllConnections; the device path emits those closes
+    with pv_set_end_of_capture, pv_tcp.hip)."""
     import struct
     from pktvisor_amd import pcap_file_bytes
     rng = np.random.default_rng(seed)
@@ -187,6 +191,10 @@ def tcp_dns_pcap(seed: int = 1, flows: int = 60, duration_s: float = 20.0, udp_s
     # connections that fall silent for 35 s keep their segments in order (a timeout that
     # flushes buffered data is ordered differently on the device, see pv_tcp.hip)
     pause_flows = set(rng.choice(flows, size=min(pauses, flows), replace=False).tolist()) if pauses else set()
+    tail_rng = np.random.default_rng(seed + 7919)  # keeps the other flows as without open_tails
+    open_flows = set(tail_rng.choice([f for f in range(flows) if f not in pause_flows],
+                                     size=min(open_tails, flows - len(pause_flows)), replace=False).tolist()) \
+        if open_tails else set()
     for f in range(flows):
         v6 = bool(rng.random() < 0.3)
         cli, srv = addr(v6, False), addr(v6, True)
@@ -245,9 +253,18 @@ def tcp_dns_pcap(seed: int = 1, flows: int = 60, duration_s: float = 20.0, udp_s
                         segs.insert(k + 1, (s[0], s[1], s[2], s[3], s[4], 0x18, s[6] + nxt[6][:max(1, len(nxt[6]) // 2)]))
                     k += 1
                 k += 1
+        if f in open_flows:
+            # one data segment never arrives: what follows it waits for the end of the capture
+            sides = [x for x in (csegs, ssegs) if len(x) >= 2]
+            if sides:
+                segs = sides[int(tail_rng.integers(0, len(sides)))]
+                del segs[int(tail_rng.integers(0, len(segs) - 1))]
         pkts += csegs + ssegs if rng.random() < 0.5 else [p for pair in zip(csegs, ssegs) for p in pair] + \
             csegs[len(ssegs):] + ssegs[len(csegs):]
         end = rng.random()
+        if f in open_flows:
+            streams.append(list(pkts))
+            continue
         if end < 0.6 or gaps:
             pkts.append((cli, srv, cport, 53, cseq + len(cbytes), 0x11, b""))
             pkts.append((srv, cli, 53, cport, sseq + len(sbytes), 0x11, b""))

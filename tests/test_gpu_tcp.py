@@ -149,3 +149,75 @@ def test_tcp_exact_lru_across_batches(oracle, lost_syn):
         h.close()
     ref = oracle.run_bytes(pcap, host_spec=HOST, num_periods=1, window=1)
     assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+def _batches(h, recs, idx, rng, eoc=True):
+    offs = list(idx.offsets) + [len(recs)]
+    i = 0
+    while i < idx.n:
+        j = min(idx.n, i + int(rng.integers(1, 200)))
+        if j == idx.n and eoc:
+            h.set_end_of_capture()
+        h.process_host(recs[offs[i]:offs[j]])
+        i = j
+
+
+@pytest.mark.parametrize("exact", [False, True])
+@pytest.mark.parametrize("periods", [1, 5])
+@pytest.mark.parametrize("seed", range(3))
+def test_tcp_end_of_capture_flush(oracle, tmp_path, seed, periods, exact):
+    """connections that lost a segment for good and never close: the segments after the hole are
+    held until the file ends, when PcapInputStream closes every connection
+    (PcapInputStream.cpp:522, TcpReassembly::closeAllConnections) and their out-of-order data is
+    delivered (pv_set_end_of_capture, pv_tcp_eoc)"""
+    pcap = synth.tcp_dns_pcap(seed, flows=80, open_tails=16)
+    gpu, ref = run_both(oracle, pcap, HOST, periods, tmp_path, tcp_exact_lru=exact)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_tcp_end_of_capture_across_batches(oracle, exact):
+    """the flush armed before the last of many small batches; without it the held data is lost,
+    (the control run must differ, so the capture really leaves data for the flush: most held data
+    follows a "[N bytes missing]" text and frames nothing, but in this capture one connection's
+    flushed bytes complete a message whose question parses)"""
+    pcap = synth.tcp_dns_pcap(0, flows=80, open_tails=16)
+    recs = pcap[24:]
+    idx = pa.RecordIndex(recs)
+    ref = oracle.run_bytes(pcap, host_spec=HOST, num_periods=1, window=1)
+    got = []
+    for eoc in (True, False):
+        h = pa.PvHandlers(host_spec=HOST, num_periods=1, max_records=512, tcp_exact_lru=exact)
+        try:
+            _batches(h, recs, idx, np.random.default_rng(9), eoc)
+            h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+            got.append({"1m": h.window_json(0)})
+        finally:
+            h.close()
+    assert diff(got[0], ref) is None, diff(got[0], ref)
+    if not exact:  # (the exact LRU list closes that connection before the end: a lost SYN)
+        assert diff(got[1], ref) is not None
+
+
+def test_tcp_end_of_capture_device_batch(oracle):
+    """the flush after a batch resident in HBM (pv_process_device, the bench's entry point)"""
+    import torch
+    pcap = synth.tcp_dns_pcap(6, flows=120, duration_s=40, open_tails=24)
+    recs = pcap[24:]
+    buf = np.zeros(len(recs) + 256, dtype=np.uint8)
+    buf[:len(recs)] = np.frombuffer(recs, dtype=np.uint8)
+    idx = pa.RecordIndex(recs)
+    d_recs = torch.from_numpy(buf).cuda()
+    d_offs = torch.from_numpy(idx.offsets).cuda()
+    torch.cuda.synchronize()
+    h = pa.PvHandlers(host_spec=HOST, num_periods=5, max_records=idx.n)
+    try:
+        h.set_end_of_capture()
+        h.process_device(d_recs.data_ptr(), d_offs.data_ptr(), idx)
+        h.synchronize()
+        h.set_end_tstamp(*pa.last_record_ts(recs, idx))
+        gpu = {"5m": h.window_json(5, merged=True)}
+    finally:
+        h.close()
+    ref = oracle.run_bytes(pcap, host_spec=HOST, num_periods=5, window=5)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
