@@ -141,10 +141,7 @@ inline uint64_t name_fp(const char *s, size_t n)
 
 extern "C" __global__ void pv_net_kernel(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_ns(const PvParams *P);
-extern "C" __global__ void pv_net_kernel_fast(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg(const PvParams *P);
-extern "C" __global__ void pv_net_kernel_reg8(const PvParams *P);
-extern "C" __global__ void pv_net_kernel_ring(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_reg_tc(const PvParams *P);
 extern "C" __global__ void pv_net_kernel_span(const PvParams *P);
 extern "C" __global__ void pv_store_blob(PvBlob b, uint4 *dst, uint32_t n16);
@@ -592,7 +589,6 @@ struct pv_ctx {
     bool dns_heavy = false; // the last batch was mostly DNS messages: four ranges per CU
     int reg_wg_per_cu = 1; // workgroups per CU of the register-window Net pass
     uint32_t cb_fan = 1;   // grid ranges per top-N combine workgroup
-    int reg_waves = 4;     // its waves per workgroup (4 or 8; PV_REG_WAVES)
     int dns_wg_per_cu = 1; // resident workgroups per CU of the DNS pass (its register count)
     const char *net_kernel = "none"; // the Net-pass kernel the last span launched (pv_net_kernel_name)
     uint64_t *d_dq = nullptr; // DNS work lists (32-B messages)
@@ -2475,7 +2471,6 @@ int pv_create(const pv_config *cfg, pv_ctx **out)
         c->wg_per_cu = 3;
         if (const char *w = getenv("PV_NET_WGCU")) { c->wg_per_cu = std::max(1, atoi(w)); c->wg_forced = true; }
         if (const char *w = getenv("PV_REG_WGCU")) c->reg_wg_per_cu = std::max(1, atoi(w));
-        if (const char *w = getenv("PV_REG_WAVES")) c->reg_waves = atoi(w) == 8 ? 8 : 4;
         {
             int nb = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(pv_dns_kernel), 64 * PV_DNS_WAVES, 0) == hipSuccess &&
@@ -4041,21 +4036,16 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     const uint64_t per_wave = ((uint64_t)P.wt_per_block / 4 + 1) * ((grid + reg_grid - 1) / reg_grid); // packed lane counters
     const bool lean = !general && P.linktype == 1 && P.nets.n4 <= 2 && P.skip_before == 0 && per_wave < 65535 &&
                       !(force && !strcmp(force, "ns"));
-    // lean: the register-window pass (pv_net_kernel_reg, its top-IPs specialisation _tc);
-    // PV_NET_KERNEL=ring asks for the LDS-DMA ring pass with producer waves, =fast for the
-    // earlier per-grid-workgroup LDS ring
-    const bool ring = force && !strcmp(force, "fast");
-    const bool regw = !(force && !strcmp(force, "ring"));
-    // the ring and register passes write the compact IP log (4 B + a direction bit per record)
-    P.ip_compact = lean && !ring ? 1u : 0u;
+    // lean: the register-window pass (pv_net_kernel_reg, its top-IPs specialisation _tc), which
+    // writes the compact IP log (4 B + a direction bit per record)
+    P.ip_compact = lean ? 1u : 0u;
     P.ip_base = ((uint64_t)P.slot_of[0] << 60) | ((uint64_t)TM_IPV4 << 56) |
                 ((uint64_t)((c->net_groups & PV_NET_CARDINALITY) ? 1 : 0) << 33);
-    const bool tc = (c->net_groups & PV_NET_TOP_IPS) && c->reg_waves != 8;
-    // PV_NET_KERNEL=span: the span-load pass with the general path deferred (top-IPs groups)
-    const bool span = lean && tc && !ring && regw && force && !strcmp(force, "span");
-    // the span and register passes defer general-path records to pv_net_slow_list
-    const bool defer = lean && !ring && regw;
-    if (defer) {
+    const bool tc = (c->net_groups & PV_NET_TOP_IPS) != 0;
+    // PV_NET_KERNEL=span: the span-load pass (top-IPs groups), kept for A/B runs
+    const bool span = lean && tc && force && !strcmp(force, "span");
+    // both lean passes defer general-path records to pv_net_slow_list
+    if (lean) {
         if (c->slow_cap < P.n) {
             if (c->d_slow) hipFree(c->d_slow);
             c->d_slow = nullptr;
@@ -4064,15 +4054,13 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
             c->slow_cap = P.n;
         }
         P.slow_list = c->d_slow;
-        P.slow_cnt = c->d_slow + c->slow_cap; // written for every range by the span pass
+        P.slow_cnt = c->d_slow + c->slow_cap; // written for every range by the lean passes
     }
     *c->h_params = P;
     if (!hip_ok(e = fill_and_upload(c, c->d_params, c->h_params, sizeof P, st)))
         return c->hipfail(e, "parameter upload");
     c->net_kernel = general ? "pv_net_kernel"
-                            : (lean ? (span ? "pv_net_kernel_span" : ring ? "pv_net_kernel_fast"
-                                            : (!regw ? "pv_net_kernel_ring"
-                                                     : (c->reg_waves == 8 ? "pv_net_kernel_reg8" : (tc ? "pv_net_kernel_reg_tc" : "pv_net_kernel_reg"))))
+                            : (lean ? (span ? "pv_net_kernel_span" : (tc ? "pv_net_kernel_reg_tc" : "pv_net_kernel_reg"))
                                     : "pv_net_kernel_ns");
     // pv_kernel_timing (bench roofline): the record-parse kernel alone, timed by the start and
     // end stamps of its own dispatch packet (hipExtLaunchKernelGGL), so no event marker packets
@@ -4083,25 +4071,9 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     const bool timed = c->timing_every && (c->timing_ctr++ % c->timing_every) == 0;
     hipEvent_t e0 = timed ? c->ev_start : nullptr, e1 = timed ? c->ev_stop : nullptr;
     if (general) hipExtLaunchKernelGGL(pv_net_kernel, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
-    else if (lean && ring) hipExtLaunchKernelGGL(pv_net_kernel_fast, dim3(grid), dim3(PV_NET_THREADS), 0, st, e0, e1, 0, dp);
-    else if (lean && !regw) {
-        // its block size is the kernel's own launch bound (parsing + producer waves; tuning
-        // builds change the layout)
-        static int ring_threads = 0;
-        if (!ring_threads) {
-            hipFuncAttributes fa{};
-            ring_threads = hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(pv_net_kernel_ring)) == hipSuccess
-                               ? fa.maxThreadsPerBlock : 512;
-        }
-        hipExtLaunchKernelGGL(pv_net_kernel_ring, dim3(reg_grid), dim3(ring_threads), 0, st, e0, e1, 0, dp);
-    }
-    else if (span) {
-        hipExtLaunchKernelGGL(pv_net_kernel_span, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
-        hipExtLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (hipEvent_t) nullptr, e1, 0, dp);
-    }
     else if (lean) {
-        // the register pass, then its deferred general-path records (the dispatch stamps span both)
-        if (c->reg_waves == 8) hipExtLaunchKernelGGL(pv_net_kernel_reg8, dim3(reg_grid), dim3(512), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
+        // the lean pass, then its deferred general-path records (the dispatch stamps span both)
+        if (span) hipExtLaunchKernelGGL(pv_net_kernel_span, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
         else if (tc) hipExtLaunchKernelGGL(pv_net_kernel_reg_tc, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
         else hipExtLaunchKernelGGL(pv_net_kernel_reg, dim3(reg_grid), dim3(PV_NET_THREADS), 0, st, e0, (hipEvent_t) nullptr, 0, dp);
         hipExtLaunchKernelGGL(pv_net_slow_list, dim3(c->cus * 2), dim3(256), 0, st, (hipEvent_t) nullptr, e1, 0, dp);
@@ -7250,23 +7222,21 @@ int add_sum_word(pv_ctx *c, uint32_t slot, uint32_t word, int64_t delta)
 // incoming keys (usually few) and one scan of the stubs in first-occurrence order, instead of a map
 // over every stub of the shard (millions in a shard the edge horizon covers whole: the map's build
 // was most of each rank's turn in the edge chain).
-std::unordered_map<uint64_t, size_t> edge_first_stubs(const pv_ctx *c, const uint8_t *in, size_t n, size_t esz)
+static void edge_first_stubs(const pv_ctx *c, const uint8_t *in, size_t n, size_t esz, std::unordered_map<uint64_t, size_t> &first)
 {
-    std::unordered_map<uint64_t, size_t> first;
     first.reserve(n * 2);
     for (size_t k = 0; k < n; k++) {
         uint64_t key;
         memcpy(&key, in + k * esz + offsetof(PvXEvent, key), 8);
         first.emplace(key, SIZE_MAX);
     }
-    if (first.empty()) return first;
+    if (first.empty()) return;
     size_t left = first.size();
     for (size_t i = 0; i < c->stubs.size() && left; i++) {
         auto it = first.find(c->stubs[i].e.key);
         if (it != first.end() && it->second == SIZE_MAX) { it->second = i; left--; }
     }
     for (auto it = first.begin(); it != first.end();) it = it->second == SIZE_MAX ? first.erase(it) : std::next(it);
-    return first;
 }
 
 int edge_carry2(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, size_t *out_bytes)
@@ -7274,7 +7244,8 @@ int edge_carry2(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, si
     const bool ecs = c->d_pecs[0] != nullptr;
     const size_t esz = sizeof(PvXEvent) + (ecs ? 8 : 0);
     if (in_bytes % esz) return c->fail(PV_EINVAL, "malformed open-query buffer");
-    const std::unordered_map<uint64_t, size_t> first = edge_first_stubs(c, in, in_bytes / esz, esz);
+    std::unordered_map<uint64_t, size_t> first;
+    edge_first_stubs(c, in, in_bytes / esz, esz, first);
     const uint64_t live = c->dns.ordinal;
     auto in_win = [&](uint64_t ord) { return ord <= live && ord + c->dns.slots.size() > live; };
     auto slot_of = [&](uint64_t ord) { return c->dns.slots[live - ord]; };
@@ -7629,7 +7600,8 @@ int pv_edge_carry(pv_ctx *c, const uint8_t *in, size_t in_bytes, uint8_t **out, 
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return c->hipfail(e, "synchronize");
     if (c->dns2_groups) return edge_carry2(c, in, in_bytes, out, out_bytes);
-    const std::unordered_map<uint64_t, size_t> first = edge_first_stubs(c, in, in_bytes / sizeof(PvXEvent), sizeof(PvXEvent));
+    std::unordered_map<uint64_t, size_t> first;
+    edge_first_stubs(c, in, in_bytes / sizeof(PvXEvent), sizeof(PvXEvent), first);
     const uint64_t live = c->dns.ordinal;
     auto in_win = [&](uint64_t ord) { return ord <= live && ord + c->dns.slots.size() > live; };
     const bool quant = c->dns_groups & PV_DNS_QUANTILES;

@@ -66,14 +66,6 @@
 #define TST(k)
 #define TST_FLUSH(base)
 #endif
-// the ring Net pass's parsing waves (-DPV_TSTAMPS): cycles per phase, at stamps[(1 << 20) + 131072 ...]
-#ifdef PV_TSTAMPS
-#define RST_FLUSH                                                                            \
-    if ((threadIdx.x & 63) == 0)                                                             \
-        for (int k_ = 0; k_ < 8; k_++) P.stamps[(1u << 20) + 131072 + ((uint64_t)blockIdx.x * PV_RING_NP + cw) * 8 + k_] = tst_acc[k_];
-#else
-#define RST_FLUSH
-#endif
 #ifndef PV_WIN
 #define PV_WIN 128 // bytes of each record staged into LDS (record header + frame start)
 #endif
@@ -1407,31 +1399,17 @@ __device__ __forceinline__ void dma4(const void *gsrc, uint32_t lds)
 // Infinity Cache until the read stream of a later kernel evicts it, and that kernel then pays for
 // the write-back (tools/net_probe.hip, round 6: a pass over the C2 blob right after 160 MB of plain
 // stores runs 158 us against 134 after the same bytes stored non-temporally, whose writer took
-// 37 instead of 32 us). PV_NT_* pick non-temporal stores for the writers whose bytes no kernel of
-// the same step reads back.
+// 37 instead of 32 us). Non-temporal stores for the writers whose bytes no kernel of the same step
+// reads back: the top-N merge's write-back. (The IP log and the combine list are read right after
+// by the next kernel: non-temporal there measured slower, 87 -> 159 us for the combine list.)
 #ifndef PV_NT_MERGE
 #define PV_NT_MERGE 1 // pv_topn_merge's write-back of the table regions (read by the next batch's merge)
-#endif
-#ifndef PV_NT_IPLOG
-#define PV_NT_IPLOG 0 // tuning: the Net pass's IP log (read by pv_topn_combine right after)
-#endif
-#ifndef PV_NT_COMB
-#define PV_NT_COMB 0 // tuning: pv_topn_combine's list (read by pv_topn_merge right after)
 #endif
 template <bool NT, class T>
 __device__ __forceinline__ void st_nt(PV_G T *p, T v)
 {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
-}
-template <bool NT>
-__device__ __forceinline__ void st_nt16(PV_G ulonglong2 *p, ulonglong2 v)
-{
-    if constexpr (NT) {
-        PV_G uint64_t *q = reinterpret_cast<PV_G uint64_t *>(p);
-        __builtin_nontemporal_store((unsigned long long)v.x, q);
-        __builtin_nontemporal_store((unsigned long long)v.y, q + 1);
-    } else *p = v;
 }
 // A workgroup barrier for LDS data only: the wave's LDS ops complete (lgkmcnt 0), then s_barrier.
 // __syncthreads() also waits for every global store the wave has in flight (its release fence is a
@@ -2041,16 +2019,18 @@ __device__ __forceinline__ void net_pass(const PvParams *__restrict__ Pp)
 
 // ------------------------------------------------------------------ the lean Net pass
 // The common batch: one Net period (no shift inside the batch), no filter-all, no deep
-// sampling, no profiling knobs, Ethernet link type, at most two IPv4 host subnets. Same ring
-// and the same results as net_pass, with a tile's work written for the instruction budget:
-// the general pass is issue-bound (rocprofv3 on C2: ~300 VALU and ~320 SALU
-// wave-instructions per 64-record tile, each wave issuing 40 % of its cycles), most of it exec
-// masking of nested per-lane branches and spilled scalars. Here the fast path (Ethernet II +
-// IPv4 without options) is straight-line selects, the fast lanes' nine counters are three
-// packed lane registers, every rarely taken piece (DNS messages, TCP segments, caplen > 65535,
-// cardinality without top IPs) sits behind a uniform ballot branch, and general-path records
-// go to an out-of-line call that reads its parameters itself (so nothing it needs is live
-// across the loop).
+// sampling, no profiling knobs, Ethernet link type, at most two IPv4 host subnets. The same
+// results as net_pass, with a tile's work written for the instruction budget: the general pass
+// is issue-bound (rocprofv3 on C2: ~300 VALU and ~320 SALU wave-instructions per 64-record tile,
+// each wave issuing 40 % of its cycles), most of it exec masking of nested per-lane branches and
+// spilled scalars. Here the fast path (Ethernet II + IPv4 without options) is straight-line
+// selects, the fast lanes' nine counters are three packed lane registers, every rarely taken
+// piece (DNS messages, TCP segments, caplen > 65535, cardinality without top IPs) sits behind a
+// uniform ballot branch, and general-path records (VLAN, IPv6, options, tunnels, other link
+// types) are deferred to pv_net_slow_list, which parses every byte of them from HBM.
+// (Measured and dropped, in the history of round 6: an LDS-DMA ring with producer waves, a
+// per-grid-workgroup LDS ring, eight waves per workgroup, depth-2 and conditional-load
+// pipelines, the general path as an out-of-line call in the loop)
 
 // fast-path fields of one record (parse_record's fast path, branch-free)
 struct FastRec {
@@ -2125,249 +2105,14 @@ __device__ __noinline__ SlowOut net_slow_p(const PvParams *__restrict__ Pp, cons
     return net_slow(R, parse_cfg(P), P, K, off, i, K.slot0, true);
 }
 
-#ifndef PV_LEAN_LEVEL
-#define PV_LEAN_LEVEL 0 // tuning: 1 ring only, 2 + parse and counters, 3 + histogram, 4 + IP log, 0 everything
-#endif
-__device__ __forceinline__ void net_fast(const PvParams *__restrict__ Pp)
-{
-    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ NetState S;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
-    if (threadIdx.x == 0) S.nd = 0;
-    if (threadIdx.x < PV_MAX_SHIFTS) S.pt.dord[threadIdx.x] = P.dpos[threadIdx.x];
-    __syncthreads();
-    const PV_G uint8_t *const recs = P.recs;
-    const PV_G uint32_t *const offs = P.offs;
-    const uint64_t n = P.n, last = n - 1;
-    const uint32_t rec_bytes = (uint32_t)P.rec_bytes;
-    const uint32_t slot = P.slot_of[0];
-    const uint32_t groups = P.net_groups;
-    const bool tops = groups & PV_NET_TOP_IPS_BIT, card = groups & PV_NET_CARDINALITY_BIT;
-    const uint32_t ts_nano = P.ts_nano;
-    HostNets h;
-    {
-        const uint32_t n4 = P.nets.n4;
-        h.a0 = P.nets.v4_addr[0]; h.m0 = P.nets.v4_mask[0]; h.e0 = n4 > 0 ? ~0u : 0u;
-        h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
-    }
-    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
-    const uint64_t wbeg = (uint64_t)blockIdx.x * P.wt_per_block;
-    const uint64_t wend = min<uint64_t>(wbeg + P.wt_per_block, nwt);
-    const uint32_t ntl = wend > wbeg + wave ? (uint32_t)((wend - wbeg - wave + 3) / 4) : 0u;
-    NetWave &NW = S.w[wave];
-    auto tile_of = [&](uint32_t k) -> uint64_t { return wbeg + wave + 4ull * min(k, ntl - 1); };
-    auto issue_rows = [&](uint32_t k) {
-        const uint64_t r = tile_of(k) * PV_WT + lane;
-        const uint32_t row = k % PV_NL_OROWS;
-        dma4(offs + min<uint64_t>(r, last), lds_addr(&NW.lo[row][0]));
-        const uint32_t ha = lds_addr(&NW.hi[row]) - 4 * 63;
-        if (lane == 63) dma4(offs + min<uint64_t>(r + 1, last), ha);
-    };
-    auto issue_tile = [&](uint32_t k) {
-        const uint32_t row = k % PV_NL_OROWS;
-        const uint64_t t = tile_of(k);
-        const uint32_t o = NW.lo[row][lane];
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
-        const uint32_t b1 = t * PV_WT + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row]);
-        const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
-        const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
-        const uint32_t dst = lds_addr(&NW.slot[k % PV_NL_Q][0]);
-#pragma unroll
-        for (int j = 0; j < PV_NL_NJ; j++) {
-            const uint32_t ch = (uint32_t)(j * 64) + lane;
-            const uint32_t src = packed ? base + min(ch, nch - 1) * 16 : (o & ~15u) + 16u * j;
-            dma16(recs + src, dst + j * 1024);
-        }
-    };
-    auto refill = [&](uint32_t k) {
-        issue_rows(k + PV_NL_Q + 2);
-        PV_VMCNT(2 * PV_NL_OPS);
-        issue_tile(k + PV_NL_Q);
-    };
-    if (ntl) {
-        issue_rows(0);
-        issue_rows(1);
-        PV_VMCNT(0);
-        for (uint32_t j = 0; j < PV_NL_Q; j++) {
-            issue_rows(j + 2);
-            if (j >= 2) PV_VMCNT(2 * PV_NL_OPS);
-            issue_tile(j);
-        }
-    }
-    // fast lanes' counters, 16-bit fields (a lane counts at most one record per tile of its
-    // wave, and the host keeps a wave's tiles below 2^16): in | out << 16 | unknown << 32,
-    // udp | tcp << 16 | other << 32 | syn << 48
-    uint64_t cd = 0, cl = 0;
-    NetCtr c; // general-path records
-    c.zero();
-    for (uint32_t k = 0; k < ntl; k++) {
-        PV_VMCNT((PV_NL_Q - 1) * PV_NL_OPS); // tile k landed
-        const uint32_t sl = k % PV_NL_Q, row = k % PV_NL_OROWS;
-        const uint64_t t = tile_of(k);
-        const uint64_t r0 = t * PV_WT, i = r0 + lane;
-        const bool active = i < n;
-        const uint32_t off = NW.lo[row][lane];
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane(NW.lo[row][0]);
-        const uint32_t b1 = r0 + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(NW.hi[row]);
-        const uint32_t base = b0 & ~15u, nch = (b1 - base + 15) >> 4;
-        const bool packed = nch <= (uint32_t)(PV_NL_SLOT / 16);
-        const uint32_t *Ls = NW.slot[sl];
-        const uint32_t gb = packed ? base : (off & ~15u);
-        const uint32_t lim = packed ? nch * 16 - 4 : PV_NL_SLOT / PV_WT - 4;
-        const uint32_t rel = off - gb;
-        if (PV_LEAN_LEVEL == 1) {
-            cd += active ? 1ull : 0ull;
-            asm volatile("" ::: "memory");
-            refill(k);
-            continue;
-        }
-        RecW rw;
-        if (packed) recw_load_packed(Ls, rel, rw);
-        else recw_load_window(Ls, rel >> 2, rel & 3, lane * 4, rw);
-        FastRec f = fast_fields(rw, h);
-        const bool fast = active & ((rel >> 2) + 17 <= (lim + 4) >> 2) & (f.ok != 0);
-        const uint64_t slowm = __ballot(active & !fast);
-        if (!slowm) {
-            asm volatile("" ::: "memory");
-            refill(k);
-        }
-        cd += fast ? 1ull << (f.dir * 16) : 0ull;
-        cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
-        uint32_t hv = fast ? f.caplen : PV_NOH;
-        const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
-        const bool ipok = fast & (f.dir != 2) & (ip != 0);
-        uint64_t ek = tops && ipok ? ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
-                                         ((uint64_t)f.dir << 32) | ip
-                                   : 0ull;
-        if (card && !tops) {
-            // cardinality without top IPs: first-occurrence coupons straight to the table
-            if (ipok) {
-                uint64_t h1, h2;
-                murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
-                __hip_atomic_fetch_min(P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)(f.dir == 0 ? CPC_SRC : CPC_DST) * PV_CPC_COUPONS +
-                                           cpc_coupon(h1, h2),
-                                       (int64_t)(P.gbase + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        // DNS over UDP (the DNS handler takes the pcap input's UDP signal itself)
-        const uint32_t port = (fast & (f.l4 == 17)) ? dns_port_bf(rw.at(50)) : 0u;
-        DnsMsgW dm{};
-        bool isdns = port != 0;
-        if (__ballot(isdns)) {
-            if (isdns) {
-                const Parsed o = fast_parsed(f, rw, ts_nano, off);
-                uint32_t dp = 0;
-                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)(4 * i) >= S.pt.dord[q];
-                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
-                DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
-                d.fkey = fast_flowkey(rw);
-                dm = msg_words(d);
-            }
-        }
-        bool istcp = fast & (f.l4 == 6), hasseg = false;
-        PvTcpSeg seg;
-        const uint32_t temit = P.tcp_emit;
-        if (temit && __ballot(istcp)) {
-            if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
-        }
-        // general-path records of the tile (VLAN, IPv6, options, tunnels, short windows)
-        if (slowm) {
-            if (active && !fast) {
-                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
-                const SlowOut so = net_slow_p(Pp, R, off, i);
-                Parsed o;
-                o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
-                c.add(o);
-                hv = so.caplen;
-                ek = so.ek;
-                dm = so.dm;
-                isdns = so.isdns;
-                istcp = so.l4 == 6;
-            }
-            asm volatile("" ::: "memory");
-        }
-        if (PV_LEAN_LEVEL == 2) {
-            if (slowm) refill(k);
-            asm volatile("" ::: "memory");
-            continue;
-        }
-        if (__ballot(hv != PV_NOH && hv > 65535)) {
-            if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
-        }
-        hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
-        if (PV_LEAN_LEVEL == 3) {
-            if (slowm) refill(k);
-            continue;
-        }
-        const uint64_t m = __ballot(isdns);
-        if (m) {
-            uint32_t q = 0;
-            if (lane == 0) q = atomicAdd(&S.nd, (uint32_t)__popcll(m));
-            q = __builtin_amdgcn_readlane(q, 0);
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (isdns) {
-                PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(P.dq) + 2 * (wbeg * PV_WT + q + below);
-                dd[0] = dm.a;
-                dd[1] = dm.b;
-            }
-        }
-        if (tops && active) P.iplog[i] = ek;
-        if (PV_LEAN_LEVEL == 4) {
-            if (slowm) refill(k);
-            continue;
-        }
-        if (temit) {
-            const uint64_t tm = __ballot(istcp);
-            if (tm) {
-                if (lane == 0) P.tmask[t] = tm;
-                tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, seg, lane);
-            }
-        }
-        if (slowm) refill(k);
-    }
-    PV_VMCNT(0);
-    // fast lanes' fields into the counters (every fast record is Ethernet + IPv4: an event,
-    // a deep sample, total and IPv4)
-    {
-        const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
-        const uint32_t nf = fin + fout + funk;
-        c.nev += nf; c.n4 += nf;
-        c.nin += fin; c.nout += fout; c.nunk += funk;
-        c.nudp += (uint32_t)(cl & 0xffff); c.ntcp += (uint32_t)((cl >> 16) & 0xffff);
-        c.noth += (uint32_t)((cl >> 32) & 0xffff); c.nsyn += (uint32_t)(cl >> 48);
-    }
-    NetK K;
-    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
-    if (ntl) knet_flush(K, slot, c);
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
-        if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
-    if (threadIdx.x == 0) {
-        P.mq_cnt[blockIdx.x] = 0;
-        P.dq_cnt[blockIdx.x] = S.nd;
-        if (S.nd) atomicAdd(P.n_dns, S.nd);
-    }
-}
-
 // ------------------------------------------------------------------ the lean Net pass, register windows
-// The lean pass without the LDS ring: each lane loads its own record's first 80 bytes straight
-// into registers (five 16-B loads from the record's dword-aligned start, so the record's
-// dwords are one alignbyte away: no selects), the next tile's windows in flight while the wave
-// parses this one (two register buffers, the loop unrolled by two so no copy waits on them).
-// tools/stream_probe.hip measured the pattern alone at 5.8 TB/s (modes 7/8) against 4.2 TB/s
-// for the LDS-DMA ring's staging; the LDS keeps only the histogram and the DNS list counter.
+// Each lane loads its own record's first 80 bytes straight into registers (five 16-B loads from
+// the record's dword-aligned start, so the record's dwords are one alignbyte away: no selects),
+// the windows of the next two tiles in flight while the wave parses this one. tools/stream_probe.hip
+// measured the pattern alone at 5.8 TB/s (modes 7/8) against 4.2 TB/s for LDS-DMA staging; the
+// LDS keeps only the histogram and the DNS / exception / deferred-record list counters.
 #ifndef PV_REG_MINW
 #define PV_REG_MINW 2 // waves per SIMD the register allocation must allow
-#endif
-#ifndef PV_REG_DEPTH
-#define PV_REG_DEPTH 3 // tiles whose windows are in registers (the parsed one + those in flight)
-#endif
-#ifndef PV_REG_UNCOND
-#define PV_REG_UNCOND 1 // the pipeline with unconditional (clamped) loads
-#endif
-#ifndef PV_REG_SLOW_INLINE
-#define PV_REG_SLOW_INLINE 0 // tuning: the general path as an out-of-line call in the loop (rounds 3-5)
 #endif
 struct NetRegState {
     uint32_t hist[PV_HBINS];
@@ -2389,7 +2134,7 @@ __device__ __forceinline__ void win_words(const uint4 (&W)[5], uint32_t sh, RecW
 #pragma unroll
     for (int j = 0; j < 16; j++) r.w[j] = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
 }
-// NW: waves of the workgroup (one workgroup per CU); wave w takes tiles w, w + NW, ... of each range.
+// NW: waves of the workgroup; wave w takes tiles w, w + NW, ... of each range.
 // TC: top IPs on with the compact IP log (the default groups). Its two stores per tile are then
 // unconditional instructions, so the compiler's counted vmcnt for the next tile's windows counts
 // them as younger ops instead of waiting for them: a store takes microseconds to complete under
@@ -2445,31 +2190,17 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         const bool active = live && i < n;
         RecW rw;
         win_words(W, off & 3, rw);
-        if (PV_LEAN_LEVEL == 1) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int j = 0; j < 16; j++) x ^= rw.w[j];
-            cd += active ? x : 0u;
-            return;
-        }
         const FastRec f = fast_fields(rw, h);
         const bool fast = active & (f.ok != 0);
         const uint64_t slowm = __ballot(active & !fast);
         cd += fast ? 1ull << (f.dir * 16) : 0ull;
         cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
         uint32_t hv = fast ? f.caplen : PV_NOH;
-        if (PV_LEAN_LEVEL == 2) return;
-        if (PV_LEAN_LEVEL == 3) { hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane); return; }
         const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
         const bool ipok = fast & (f.dir != 2) & (ip != 0);
         uint64_t ek = tops && ipok ? ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
                                          ((uint64_t)f.dir << 32) | ip
                                    : 0ull;
-        if (PV_LEAN_LEVEL == 4) {
-            hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
-            if (tops && active) P.iplog[i] = ek;
-            return;
-        }
         if (card && !tops) {
             if (ipok) {
                 uint64_t h1, h2;
@@ -2499,22 +2230,6 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
         if (temit && __ballot(istcp)) {
             if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
         }
-#if PV_REG_SLOW_INLINE
-        if (slowm) {
-            if (active && !fast) {
-                const SAcc R{recs, nullptr, 0, 0, 0, 1};
-                const SlowOut so = net_slow_p(Pp, R, off, i);
-                Parsed o;
-                o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
-                c.add(o);
-                hv = so.caplen;
-                ek = so.ek;
-                dm = so.dm;
-                isdns = so.isdns;
-                istcp = so.l4 == 6;
-            }
-        }
-#else
         if (slowm) {
             // general-path records (VLAN, IPv6, options, tunnels, other link types): their indices
             // to the range's list, which pv_net_slow_list parses after this pass (an out-of-line
@@ -2526,7 +2241,6 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
             q = __builtin_amdgcn_readlane(q, 0) + __builtin_amdgcn_mbcnt_hi((uint32_t)(slowm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)slowm, 0u));
             if (active && !fast) P.slow_list[wbeg * PV_WT + q] = (uint32_t)i;
         }
-#endif
         if (__ballot(hv != PV_NOH && hv > 65535)) {
             if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
         }
@@ -2555,8 +2269,8 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
                     // the same direction word: two unconditional store instructions
                     PV_G uint32_t *const l32 = live ? P.iplog32 + i : reinterpret_cast<PV_G uint32_t *>(trash) + lane;
                     PV_G uint64_t *const ldw = live ? P.ipdir + t : trash + 32;
-                    st_nt<PV_NT_IPLOG, uint32_t>(l32, active && v4 ? (uint32_t)ek : 0u);
-                    st_nt<PV_NT_IPLOG, uint64_t>(ldw, dbit);
+                    *l32 = active && v4 ? (uint32_t)ek : 0u;
+                    *ldw = dbit;
                 } else if (live) {
                     if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
                     if (lane == 0) P.ipdir[t] = dbit;
@@ -2583,99 +2297,32 @@ __device__ __forceinline__ void net_fast_reg(const PvParams *__restrict__ Pp)
             }
         }
     };
-#if PV_REG_UNCOND
-    // software pipeline of depth PV_REG_DEPTH with unconditional loads: every load is issued on
-    // every path (tile_of clamps past the wave's last tile; tile() skips a clamped copy), so no load
-    // can be sunk behind the parse it should overlap into a loop exit's branch
+    // software pipeline of depth 3 with unconditional loads: the windows of tiles k + 1 and k + 2
+    // in flight while tile k is parsed, every load issued on every path (tile_of clamps past the
+    // wave's last tile; tile() skips a clamped copy), so the compiler cannot sink a load behind the
+    // parse it should overlap into a loop exit's branch (the conditional form: 237 -> 229 us on C2,
+    // profiles/r6). Loads retire in order, so each counted wait the compiler places for a tile's
+    // windows leaves the younger loads and the previous tiles' stores in flight.
     if (ntl) {
-#if PV_REG_DEPTH == 3
         uint4 W0[5], W1[5], W2[5];
         uint32_t o0 = off_of(0), o1 = off_of(1), o2 = off_of(2);
         win_load(recs, o0, W0);
         win_load(recs, o1, W1);
         for (uint32_t k = 0; k < ntl; k += 3) {
             const uint32_t oN = off_of(k + 3);
-            win_load(recs, o2, W2);
+            win_load(recs, o2, W2);  // tile k + 2
             tile(k, o0, W0);
             const uint32_t oN1 = off_of(k + 4);
-            win_load(recs, oN, W0);
+            win_load(recs, oN, W0);  // tile k + 3
             o0 = oN;
             tile(k + 1, o1, W1);
             const uint32_t oN2 = off_of(k + 5);
-            win_load(recs, oN1, W1);
+            win_load(recs, oN1, W1); // tile k + 4
             o1 = oN1;
             tile(k + 2, o2, W2);
             o2 = oN2;
         }
-#else
-        uint4 WA[5], WB[5];
-        uint32_t oA = off_of(0), oB = off_of(1);
-        win_load(recs, oA, WA);
-        for (uint32_t k = 0; k < ntl; k += 2) {
-            const uint32_t oN = off_of(k + 2);
-            win_load(recs, oB, WB);
-            tile(k, oA, WA);
-            const uint32_t oN2 = off_of(k + 3);
-            win_load(recs, oN, WA);
-            oA = oN;
-            tile(k + 1, oB, WB);
-            oB = oN2;
-        }
-#endif
     }
-#elif PV_REG_DEPTH == 3
-    // three buffers: the windows of tiles k + 1 and k + 2 in flight while tile k is parsed
-    uint4 W0[5], W1[5], W2[5];
-    uint32_t o0 = 0, o1 = 0, o2 = 0;
-    if (ntl) {
-        o0 = off_of(0);
-        o1 = off_of(1);
-        o2 = off_of(2);
-        win_load(recs, o0, W0);
-        win_load(recs, o1, W1);
-    }
-    for (uint32_t k = 0; k < ntl; k += 3) {
-        const uint32_t oN = off_of(k + 3);
-        win_load(recs, o2, W2);              // tile k + 2
-        tile(k, o0, W0);
-        if (k + 1 >= ntl) break;
-        const uint32_t oN1 = off_of(k + 4);
-        win_load(recs, oN, W0);              // tile k + 3
-        o0 = oN;
-        tile(k + 1, o1, W1);
-        if (k + 2 >= ntl) break;
-        const uint32_t oN2 = off_of(k + 5);
-        win_load(recs, oN1, W1);             // tile k + 4
-        o1 = oN1;
-        tile(k + 2, o2, W2);
-        o2 = oN2;
-    }
-#else
-    // software pipeline, unrolled by two: while tile k is parsed from one buffer the windows of
-    // tile k + 1 land in the other; tile k + 2's offsets are loaded ahead of tile k + 1's windows
-    uint4 WA[5], WB[5];
-    uint32_t oA = 0, oB = 0;
-    if (ntl) {
-        oA = off_of(0);
-        oB = off_of(1);
-        win_load(recs, oA, WA);
-    }
-    // Issue order per tile j: offsets of tile j + 2, windows of tile j + 1, then tile j's work.
-    // Loads retire in order, so the offsets a window load needs were issued before the windows
-    // still in flight, and each wait the compiler places (for offsets, then for windows) leaves
-    // the younger loads and the previous tile's stores in flight.
-    for (uint32_t k = 0; k < ntl; k += 2) {
-        const uint32_t oN = off_of(k + 2);
-        win_load(recs, oB, WB);              // tile k + 1 (a clamped copy past the range's end)
-        tile(k, oA, WA);
-        if (k + 1 >= ntl) break;
-        const uint32_t oN2 = off_of(k + 3);
-        win_load(recs, oN, WA);              // tile k + 2
-        oA = oN;
-        tile(k + 1, oB, WB);
-        oB = oN2;
-    }
-#endif
     // this range's DNS list: its count, and the slot counter reset for the next range (LDS-only
     // barriers: the range's IP-log and DNS-list stores are other kernels' to read, and waiting
     // for them here would stall every wave on their completion)
@@ -2818,18 +2465,10 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
             win_load(recs, off, W);
             win_words(W, off & 3, rw);
         }
-        if (PV_LEAN_LEVEL == 1) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int j = 0; j < 16; j++) x ^= rw.w[j];
-            cd += active ? x : 0u;
-            return;
-        }
         const FastRec f = fast_fields(rw, h);
         const bool fast = active & (f.ok != 0);
         cd += fast ? 1ull << (f.dir * 16) : 0ull;
         cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
-        if (PV_LEAN_LEVEL == 2) return;
         // the records the fast path does not take: the range's list for pv_net_slow_list (an LDS
         // reservation: a returning global atomic would wait on every load in flight)
         {
@@ -2997,376 +2636,10 @@ extern "C" __global__ void __launch_bounds__(256) pv_net_slow_list(const PvParam
     knet_flush(K, slot, c);
 }
 
-// ------------------------------------------------------------------ the lean Net pass, LDS-DMA ring
-// The lean pass with its records staged in LDS by LDS-DMA (global_load_lds_dwordx4), one
-// workgroup per CU of four parsing waves and four producer waves. tools/ring_probe.hip measured
-// the staging alone: the register windows at one workgroup per CU 201-211 us on C2 (two tiles, 10
-// KiB, in flight per wave: ~40 KiB per CU, too few to cover an HBM miss), an LDS ring 138-143 us
-// against 133-137 us for a plain coalesced read of the blob (profiles/r4_head/ring_probe.log). A
-// wave's vmcnt counts its loads and stores together, in issue order, and a store's completion
-// takes microseconds under the read stream: a parsing wave that waited on its own ring would wait
-// on its IP-log and DNS-list stores too (the first ring build did, at 370 us on C2). So the ring of
-// parsing wave w is filled by producer wave 4 + w, which issues nothing else:
-//   - the producer issues, per tile, two offset rows (each lane's record start, the tile's end)
-//     Q + 1 tiles ahead and NJ 1-KiB pieces: the tile's packed span from its 16-B aligned start
-//     when it fits a slot (C2: 64 x 80 B), else each lane's own 80-B window (C3 / C4: headers
-//     only; the unused pieces re-read one shared 16 B, so every issue is OPS ops);
-//   - it publishes a tile (LDS word FULL) once a counted vmcnt shows it landed, and reuses a slot
-//     once the parsing wave has released it (LDS word FREE); issuing comes first, so up to Q
-//     tiles are in flight while the parser works;
-//   - each parsing wave's tiles: w, w + 4, ... of its workgroup's contiguous run of grid ranges
-//     (one workgroup per CU walks ceil(grid / CUs) consecutive ranges, so the DNS pass, combine
-//     and merge keep the grid's partition; per-range DNS list and exception counters in LDS);
-//   - the per-record work is net_fast_reg's (fast path from the words, general path out of line).
-#ifndef PV_RING_NP
-#define PV_RING_NP 4 // parsing waves per workgroup
-#endif
-#ifndef PV_RING_SP
-#define PV_RING_SP 1 // parsing waves one producer wave fills
-#endif
-#ifndef PV_RING_Q
-#define PV_RING_Q 4 // tile slots per parsing wave
-#endif
-#ifndef PV_RING_NJ
-#define PV_RING_NJ 6 // 1-KiB pieces per slot (a packed tile spans at most NJ KiB - 15 B)
-#endif
-#define PV_RING_NW (PV_RING_NP + PV_RING_NP / PV_RING_SP) // waves per workgroup
-#define PV_RING_D (PV_RING_Q + 1)      // rows issued this many tiles ahead of their pieces
-#define PV_RING_R (2 * PV_RING_Q + 1)  // offset rows per parsing wave
-#define PV_RING_OPS (PV_RING_NJ + 2)   // vector-memory ops one issue makes (rows + pieces)
-#define PV_RING_MAXG 8                 // grid ranges one ring workgroup may own
-#define PV_RING_INF (PV_RING_SP * PV_RING_Q) // issues one producer may have in flight
-#define PV_RING_WAITA (PV_RING_NJ + (PV_RING_SP * PV_RING_D - 1) * PV_RING_OPS + 2)
-static_assert(PV_RING_NJ >= 5, "a window-mode tile needs five pieces");
-static_assert(PV_RING_NP % PV_RING_SP == 0 && PV_RING_INF <= 8, "producer layout");
-static_assert(PV_RING_WAITA < 64 && (PV_RING_INF - 1) * PV_RING_OPS < 64, "vmcnt range");
-static_assert(PV_RING_D <= PV_RING_R - PV_RING_Q, "a row is rewritten only after its tile is released");
-struct RingWave {
-    uint32_t slot[PV_RING_Q][PV_RING_NJ * 256];
-    uint32_t lo[PV_RING_R][PV_WT]; // each lane's record start
-    uint32_t hi[PV_RING_R][PV_WT]; // the tile's end (the record after its last; all lanes alike)
-};
-struct NetRingState {
-    RingWave w[PV_RING_NP];
-    uint32_t hist[PV_HBINS];
-    uint32_t nd[PV_RING_MAXG], nx[PV_RING_MAXG];
-    uint32_t full[PV_RING_NP], fre[PV_RING_NP]; // per parsing wave: tiles published / released
-    int64_t dord[PV_MAX_SHIFTS];
-};
-static_assert(sizeof(NetRingState) <= 160 * 1024, "ring Net pass LDS");
-template <int N>
-__device__ __forceinline__ void ring_vmcnt()
-{
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p)
-{
-    const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
-    return v;
-}
-__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v)
-{
-    asm volatile("" ::: "memory");
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// wait until at most n - 1 issues (of PV_RING_OPS ops each) are younger than the oldest in flight
-__device__ __forceinline__ void ring_wait_oldest(uint32_t n)
-{
-    switch (n) {
-    case 1: ring_vmcnt<0>(); break;
-    case 2: ring_vmcnt<PV_RING_OPS>(); break;
-    case 3: ring_vmcnt<(PV_RING_INF >= 3 ? 2 * PV_RING_OPS : 0)>(); break;
-    case 4: ring_vmcnt<(PV_RING_INF >= 4 ? 3 * PV_RING_OPS : 0)>(); break;
-    case 5: ring_vmcnt<(PV_RING_INF >= 5 ? 4 * PV_RING_OPS : 0)>(); break;
-    case 6: ring_vmcnt<(PV_RING_INF >= 6 ? 5 * PV_RING_OPS : 0)>(); break;
-    case 7: ring_vmcnt<(PV_RING_INF >= 7 ? 6 * PV_RING_OPS : 0)>(); break;
-    default: ring_vmcnt<(PV_RING_INF >= 8 ? 7 * PV_RING_OPS : 0)>(); break;
-    }
-}
-__device__ __forceinline__ void net_ring(const PvParams *__restrict__ Pp)
-{
-    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
-    __shared__ NetRingState S;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x) S.hist[b] = 0;
-    if (threadIdx.x < PV_RING_MAXG) { S.nd[threadIdx.x] = 0; S.nx[threadIdx.x] = 0; }
-    if (threadIdx.x < PV_RING_NP) { S.full[threadIdx.x] = 0; S.fre[threadIdx.x] = 0; }
-    if (threadIdx.x < PV_MAX_SHIFTS) S.dord[threadIdx.x] = P.dpos[threadIdx.x];
-    __syncthreads();
-    const PV_G uint8_t *const recs = P.recs;
-    const bool compact = P.ip_compact;
-    const PV_G uint32_t *const offs = P.offs;
-    const uint64_t n = P.n, last = n - 1;
-    const uint32_t rec_bytes = (uint32_t)P.rec_bytes;
-    const uint32_t slot = P.slot_of[0];
-    const uint32_t groups = P.net_groups;
-    const bool tops = groups & PV_NET_TOP_IPS_BIT, card = groups & PV_NET_CARDINALITY_BIT;
-    const uint32_t ts_nano = P.ts_nano;
-    const uint32_t wtpb = P.wt_per_block;
-    const uint64_t nwt = (n + PV_WT - 1) / PV_WT;
-    // this workgroup's ranges [lb0, lb1) and their tiles [T0, T1); parsing wave q takes tiles
-    // T0 + q, T0 + q + NP, ...
-    const uint32_t G = (P.grid_main + gridDim.x - 1) / gridDim.x;
-    const uint32_t lb0 = min(blockIdx.x * G, P.grid_main), lb1 = min(lb0 + G, P.grid_main);
-    const uint64_t T0 = (uint64_t)lb0 * wtpb, T1 = min<uint64_t>((uint64_t)lb1 * wtpb, nwt);
-    auto ntl_of = [&](uint32_t q) -> uint32_t {
-        return T1 > T0 + q ? (uint32_t)((T1 - T0 - q + PV_RING_NP - 1) / PV_RING_NP) : 0u;
-    };
-    // tile k of parsing wave q (clamped to its last: the producer's tail issues re-read it)
-    auto tile_of = [&](uint32_t q, uint32_t nq, int64_t k) -> uint64_t {
-        return T0 + q + (uint64_t)PV_RING_NP * (uint64_t)min<int64_t>(max<int64_t>(k, 0), (int64_t)nq - 1);
-    };
-    // the span of tile k in HBM: [base, b1), packed when it fits a slot
-    auto span = [&](RingWave &W, uint64_t t, int64_t k, uint32_t &base, uint32_t &nch) {
-        const uint32_t row = (uint32_t)(k % PV_RING_R);
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane(W.lo[row][0]);
-        const uint32_t b1 = t * PV_WT + PV_WT >= n ? rec_bytes : __builtin_amdgcn_readfirstlane(W.hi[row][0]);
-        base = b0 & ~15u;
-        nch = (b1 - base + 15) >> 4;
-    };
-    const uint32_t cw = wave < PV_RING_NP ? wave : 0u;
-    const uint32_t ntl = wave < PV_RING_NP ? ntl_of(cw) : 0u;
-    if (wave >= PV_RING_NP) {
-        // ---- producer of parsing waves q0 .. q0 + SP - 1: issue e is tile e / SP of wave q0 + e % SP
-        // (every served wave takes the same count; a wave's surplus issues re-read its last tile)
-        const uint32_t q0 = (wave - PV_RING_NP) * PV_RING_SP;
-        uint32_t nt = 0, nts[PV_RING_SP];
-#pragma unroll
-        for (int u = 0; u < PV_RING_SP; u++) { nts[u] = ntl_of(q0 + u); nt = max(nt, nts[u]); }
-        auto ev_q = [&](uint32_t e) -> uint32_t { return PV_RING_SP == 1 ? 0u : e % PV_RING_SP; };
-        auto ev_k = [&](uint32_t e) -> uint32_t { return PV_RING_SP == 1 ? e : e / PV_RING_SP; };
-        auto nq_of = [&](uint32_t u) -> uint32_t {
-            uint32_t v = nts[0];
-#pragma unroll
-            for (int x = 1; x < PV_RING_SP; x++) v = (uint32_t)x == u ? nts[x] : v;
-            return v;
-        };
-        auto rows = [&](uint32_t u, int64_t k) {
-            RingWave &W = S.w[q0 + u];
-            const uint64_t t = tile_of(q0 + u, nq_of(u), k), r = t * PV_WT + lane;
-            const uint32_t row = (uint32_t)(k % PV_RING_R);
-            dma4(offs + min<uint64_t>(r, last), lds_addr(&W.lo[row][0]));
-            dma4(offs + min<uint64_t>(t * PV_WT + PV_WT, last), lds_addr(&W.hi[row][0]));
-        };
-        auto issue = [&](uint32_t e) {
-            const uint32_t u = ev_q(e), k = ev_k(e);
-            rows(u, (int64_t)k + PV_RING_D);
-            ring_vmcnt<PV_RING_WAITA>(); // rows of this tile (issued SP * D issues ago) landed
-            RingWave &W = S.w[q0 + u];
-            uint32_t base, nch;
-            span(W, tile_of(q0 + u, nq_of(u), k), k, base, nch);
-            const bool packed = nch <= (uint32_t)(PV_RING_NJ * 64);
-            const uint32_t o = W.lo[k % PV_RING_R][lane];
-            const uint32_t dst = lds_addr(&W.slot[k % PV_RING_Q][0]);
-#pragma unroll
-            for (int j = 0; j < PV_RING_NJ; j++) {
-                const uint32_t ch = (uint32_t)(j * 64) + lane;
-                const uint32_t src = packed ? base + min(ch, nch - 1) * 16 : (j < 5 ? (o & ~15u) + 16u * j : base);
-                dma16(recs + src, dst + j * 1024);
-            }
-        };
-        if (nt) {
-            for (uint32_t e = 0; e < PV_RING_SP * PV_RING_D; e++) rows(ev_q(e), ev_k(e));
-            ring_vmcnt<0>();
-            const uint32_t total = PV_RING_SP * nt;
-            uint32_t issued = 0, published = 0;
-            while (published < total) {
-                if (issued < total && ev_k(issued) < lds_ld(&S.fre[q0 + ev_q(issued)]) + PV_RING_Q) {
-                    issue(issued++); // a free slot: keep HBM busy first
-                    continue;
-                }
-                if (published < issued) {
-                    ring_wait_oldest(issued - published); // the oldest issue in flight landed
-                    const uint32_t e = published++;
-                    if (lane == 0) lds_st(&S.full[q0 + ev_q(e)], ev_k(e) + 1);
-                    continue;
-                }
-                __builtin_amdgcn_s_sleep(1); // every slot holds a published tile the parser has not released
-            }
-        }
-    } else {
-    RingWave &W = S.w[cw];
-    // ---- parsing wave cw
-    TST_DECL
-    HostNets h;
-    {
-        const uint32_t n4 = P.nets.n4;
-        h.a0 = P.nets.v4_addr[0]; h.m0 = P.nets.v4_mask[0]; h.e0 = n4 > 0 ? ~0u : 0u;
-        h.a1 = P.nets.v4_addr[1]; h.m1 = P.nets.v4_mask[1]; h.e1 = n4 > 1 ? ~0u : 0u;
-    }
-    uint64_t cd = 0, cl = 0; // fast lanes' packed counters (net_fast)
-    NetCtr c;
-    c.zero();
-    for (uint32_t k = 0; k < ntl; k++) {
-        TST(7)
-        while (lds_ld(&S.full[cw]) <= k) __builtin_amdgcn_s_sleep(1);
-        TST(0)
-        const uint32_t row = k % PV_RING_R;
-        const uint64_t t = tile_of(cw, ntl, k);
-        const uint32_t lb = (uint32_t)(t / wtpb), lr = lb - lb0; // the tile's grid range
-        const uint64_t wbeg = (uint64_t)lb * wtpb;
-        const uint64_t r0 = t * PV_WT, i = r0 + lane;
-        const bool active = i < n;
-        const uint32_t off = W.lo[row][lane];
-        uint32_t base, nch;
-        span(W, t, k, base, nch);
-        const bool packed = nch <= (uint32_t)(PV_RING_NJ * 64);
-        const uint32_t *Ls = W.slot[k % PV_RING_Q];
-        const uint32_t gb = packed ? base : (off & ~15u);
-        const uint32_t lim = packed ? nch * 16 - 4 : 76;
-        const uint32_t rel = off - gb;
-        RecW rw;
-        if (packed) recw_load_packed(Ls, rel, rw);
-        else recw_load_window(Ls, rel >> 2, rel & 3, lane * 4, rw);
-        const FastRec f = fast_fields(rw, h);
-#ifdef PV_TSTAMPS
-        asm volatile("" ::"v"(f.ok), "v"(f.dir) : "memory");
-#endif
-        TST(1)
-        const bool fast = active & ((rel >> 2) + 17 <= (lim + 4) >> 2) & (f.ok != 0);
-        const uint64_t slowm = __ballot(active & !fast);
-        cd += fast ? 1ull << (f.dir * 16) : 0ull;
-        cl += fast ? (1ull << (f.l4 == 17 ? 0u : (f.l4 == 6 ? 16u : 32u))) + ((uint64_t)f.syn << 48) : 0ull;
-        uint32_t hv = fast ? f.caplen : PV_NOH;
-        const uint32_t ip = f.dir == 0 ? rw.at(42) : rw.at(46);
-        const bool ipok = fast & (f.dir != 2) & (ip != 0);
-        uint64_t ek = tops && ipok ? ((uint64_t)slot << 60) | ((uint64_t)TM_IPV4 << 56) | ((uint64_t)card << 33) |
-                                         ((uint64_t)f.dir << 32) | ip
-                                   : 0ull;
-        if (card && !tops) {
-            if (ipok) {
-                uint64_t h1, h2;
-                murmur_8((uint64_t)(int64_t)(int32_t)ip, h1, h2);
-                __hip_atomic_fetch_min(P.cpc + (uint64_t)slot * PV_MIN_WORDS + (uint64_t)(f.dir == 0 ? CPC_SRC : CPC_DST) * PV_CPC_COUPONS +
-                                           cpc_coupon(h1, h2),
-                                       (int64_t)(P.gbase + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        const uint32_t port = (fast & (f.l4 == 17)) ? dns_port_bf(rw.at(50)) : 0u;
-        DnsMsgW dm{};
-        bool isdns = port != 0;
-        if (__ballot(isdns)) {
-            if (isdns) {
-                const Parsed o = fast_parsed(f, rw, ts_nano, off);
-                uint32_t dp = 0;
-                for (uint32_t q = 0; q < P.n_dshift; q++) dp += (int64_t)(4 * i) >= S.dord[q];
-                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
-                DnsMsg d = dns_msg_of(P, R, o, i, port, dp, dp >= P.dskip_before, false);
-                d.fkey = fast_flowkey(rw);
-                dm = msg_words(d);
-            }
-        }
-        bool istcp = fast & (f.l4 == 6), hasseg = false;
-        PvTcpSeg seg;
-        const uint32_t temit = P.tcp_emit;
-        if (temit && __ballot(istcp)) {
-            if (istcp) hasseg = tcp_seg_fast(rw, fast_parsed(f, rw, ts_nano, off), i, seg);
-        }
-        if (slowm) {
-            // general-path records (VLAN, IPv6, options, tunnels, other link types): the staged
-            // window where it reaches, else HBM
-            if (active && !fast) {
-                const SAcc R{recs, Ls, gb, lim, lane * 4, packed};
-                const SlowOut so = net_slow_p(Pp, R, off, i);
-                Parsed o;
-                o.dir = so.dir; o.l3 = so.l3; o.l4 = so.l4; o.syn = so.syn;
-                c.add(o);
-                hv = so.caplen;
-                ek = so.ek;
-                dm = so.dm;
-                isdns = so.isdns;
-                istcp = so.l4 == 6;
-            }
-        }
-        if (__ballot(hv != PV_NOH && hv > 65535)) {
-            if (hv != PV_NOH && hv > 65535) { atomicOr(P.flags, PVF_BIG_CAPLEN); hv = 65535; }
-        }
-        TST(2)
-        hist_add(S.hist, P.sum + (uint64_t)slot * PV_SUM_WORDS + PV_OFF_PAYLOAD, hv, lane);
-        TST(3)
-        const uint64_t m = __ballot(isdns);
-        if (m) {
-            uint32_t q = 0;
-            if (lane == 0) q = atomicAdd(&S.nd[lr], (uint32_t)__popcll(m));
-            q = __builtin_amdgcn_readlane(q, 0);
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (isdns) {
-                PV_G uint4 *dd = reinterpret_cast<PV_G uint4 *>(P.dq) + 2 * (wbeg * PV_WT + q + below);
-                dd[0] = dm.a;
-                dd[1] = dm.b;
-            }
-        }
-        if (tops) {
-            if (compact) {
-                const bool v4 = ek && ((ek >> 32) & ~1ull) == (P.ip_base >> 32);
-                const uint64_t xm = __ballot(active && ek && !v4);
-                if (active) P.iplog32[i] = v4 ? (uint32_t)ek : 0u;
-                const uint64_t dbit = __ballot(v4 && ((ek >> 32) & 1));
-                if (lane == 0) P.ipdir[t] = dbit;
-                if (xm) {
-                    uint32_t q = 0;
-                    if (lane == 0) q = atomicAdd(&S.nx[lr], (uint32_t)__popcll(xm));
-                    q = __builtin_amdgcn_readlane(q, 0);
-                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(xm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xm, 0u));
-                    if (active && ek && !v4) {
-                        P.iplog[wbeg * PV_WT + q + below] = ek;
-                        P.ipx_rep[wbeg * PV_WT + q + below] = (uint32_t)i;
-                    }
-                }
-            } else if (active) {
-                P.iplog[i] = ek;
-            }
-        }
-        if (temit) {
-            const uint64_t tm = __ballot(istcp);
-            if (tm) {
-                if (lane == 0) P.tmask[t] = tm;
-                tcp_seg_store(P.tseg, P.tseg_cnt, P.tseg_cap, hasseg, seg, lane);
-            }
-        }
-        TST(4)
-        // the tile's slot and row are read (LDS reads complete) before the producer may reuse them
-        __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0), vmcnt / expcnt untouched
-        if (lane == 0) lds_st(&S.fre[cw], k + 1);
-    }
-    RST_FLUSH
-    {
-        const uint32_t fin = (uint32_t)(cd & 0xffff), fout = (uint32_t)((cd >> 16) & 0xffff), funk = (uint32_t)((cd >> 32) & 0xffff);
-        const uint32_t nf = fin + fout + funk;
-        c.nev += nf; c.n4 += nf;
-        c.nin += fin; c.nout += fout; c.nunk += funk;
-        c.nudp += (uint32_t)(cl & 0xffff); c.ntcp += (uint32_t)((cl >> 16) & 0xffff);
-        c.noth += (uint32_t)((cl >> 32) & 0xffff); c.nsyn += (uint32_t)(cl >> 48);
-    }
-    NetK K;
-    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
-    if (ntl) knet_flush(K, slot, c);
-    }
-    lds_barrier();
-    NetK K;
-    K.sum = P.sum; K.net_groups = groups; K.net_filter_all = 0;
-    for (uint32_t b = threadIdx.x; b < PV_HBINS; b += blockDim.x)
-        if (S.hist[b]) ksum_add(K, slot, PV_OFF_PAYLOAD + b, S.hist[b]);
-    // the ranges' DNS list counts (and the update-log counters the DNS pass starts from)
-    for (uint32_t lb = lb0 + threadIdx.x; lb < lb1; lb += blockDim.x) {
-        const uint32_t nd = S.nd[lb - lb0];
-        P.mq_cnt[lb] = 0;
-        P.dq_cnt[lb] = nd;
-        if (compact) P.ipx_cnt[lb] = S.nx[lb - lb0];
-        if (nd) atomicAdd(P.n_dns, nd);
-    }
-}
-
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel(const PvParams *__restrict__ Pp) { net_pass<true>(Pp); }
 extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_ns(const PvParams *__restrict__ Pp) { net_pass<false>(Pp); }
-extern "C" __global__ void __launch_bounds__(256, PV_NET_MINB) pv_net_kernel_fast(const PvParams *__restrict__ Pp) { net_fast(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg(const PvParams *__restrict__ Pp) { net_fast_reg<4>(Pp); }
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg_tc(const PvParams *__restrict__ Pp) { net_fast_reg<4, true>(Pp); }
-extern "C" __global__ void __launch_bounds__(64 * PV_RING_NW) pv_net_kernel_ring(const PvParams *__restrict__ Pp) { net_ring(Pp); }
-// eight waves in the one workgroup of a CU: two per SIMD to hide instruction latency, one record stream per CU
-extern "C" __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PV_REG_MINW))) pv_net_kernel_reg8(const PvParams *__restrict__ Pp) { net_fast_reg<8>(Pp); }
 
 // ------------------------------------------------------------------ the DNS pass
 // One lane per DNS message of the Net pass's work list (same workgroup mapping).
@@ -3986,10 +3259,7 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     const PV_G uint64_t *q = P.mq + (uint64_t)gr * P.mq_cap * 2;
     batched<8>(cnt, [&](uint64_t j) { return PV_E16(q)[j]; },
                [&](uint64_t, ulonglong2 e) { comb_add<CN>(P, S, sp, e.x, (uint32_t)e.y, (uint32_t)(e.y >> 32)); });
-#ifndef PV_ABL_COMB_NOIP
-#define PV_ABL_COMB_NOIP 0 // tuning/ablation only: skip the dense IP log
-#endif
-    if ((P.net_groups & PV_NET_TOP_IPS_BIT) && !PV_ABL_COMB_NOIP) {
+    if (P.net_groups & PV_NET_TOP_IPS_BIT) {
         uint64_t a, z;
         wg_records(P, gr, a, z);
         const PV_G uint64_t *ipl = P.iplog + a;
@@ -4072,19 +3342,15 @@ __device__ __forceinline__ void topn_combine(PV_CREF(PvParams) P)
     }
     lds_barrier(); // the run-table stores are the merge kernel's to read
     TST(3)
-#ifndef PV_ABL_COMB_NOOUT
-#define PV_ABL_COMB_NOOUT 0 // tuning/ablation only: skip writing the combined list
-#endif
-    if (!PV_ABL_COMB_NOOUT)
     for (uint32_t j = threadIdx.x; j < CN; j += blockDim.x)
         if (S.key[j]) {
             const ulonglong2 e = comb_entry(S.key[j], S.cnt[j], S.rep[j]);
-            st_nt16<PV_NT_COMB>(out + atomicAdd(&S.h[run_key(P, e.x)], 1u), e);
+            out[atomicAdd(&S.h[run_key(P, e.x)], 1u)] = e;
         }
     // spilled entries (this workgroup's own writes: same CU, coherent after the barrier)
     const uint32_t nsp = S.nsp;
     batched<8>(nsp, [&](uint64_t j) { return sp[j]; },
-               [&](uint64_t, ulonglong2 e) { st_nt16<PV_NT_COMB>(out + atomicAdd(&S.h[run_key(P, e.x)], 1u), e); });
+               [&](uint64_t, ulonglong2 e) { out[atomicAdd(&S.h[run_key(P, e.x)], 1u)] = e; });
     if (threadIdx.x == 0) P.cb_cnt[blockIdx.x] = total;
 #ifdef PV_TSTAMPS
     __syncthreads();

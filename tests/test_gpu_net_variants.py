@@ -1,7 +1,6 @@
 """The Net pass's A/B variants (PV_NET_KERNEL), each in a process of its own
 (tests/net_variant_worker.py), against the oracle: the span-load pass with deferred general-path
-records, the LDS-DMA ring passes, the shift-free and the general pass must stay parity-green
-while they are kept."""
+records, the shift-free and the general pass must stay parity-green while they are kept."""
 import os
 import subprocess
 import sys
@@ -12,8 +11,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("variant,kernel", [("span", "pv_net_kernel_span"), ("ring", "pv_net_kernel_ring"),
-                                            ("fast", "pv_net_kernel_fast"), ("ns", "pv_net_kernel_ns"),
+@pytest.mark.parametrize("variant,kernel", [("span", "pv_net_kernel_span"), ("ns", "pv_net_kernel_ns"),
                                             ("general", "pv_net_kernel")])
 def test_net_variant_parity(variant, kernel):
     env = dict(os.environ, PV_NET_KERNEL=variant)

@@ -7,28 +7,26 @@ WRITE_SIZE, KB x 1024. The step's bytes sum every pv_* kernel
 of the summary, each counted once per step (pmc_summary.py reports per-dispatch means; the bench
 steps launch each pv_* kernel once, except where --launches says otherwise).
 
-  python tools/pmc_bench.py profiles/r4/pmc_c2.json 2 10000000 pv_net_kernel_ring "C2 10M x 64 B" > profiles/pmc_c2_10000000.json
+  python tools/pmc_bench.py profiles/r4/pmc_c2.json 2 10000000 pv_net_kernel_reg_tc "C2 10M x 64 B" > profiles/pmc_c2_10000000.json
 """
 import json
 import sys
 
 
-# Kernels whose reads are wide coalesced streaming reads (16 B per lane, global_load_dwordx4 or
-# LDS-DMA dwordx4 over consecutive records): FETCH_SIZE counts half their bytes on gfx950
+# Kernels whose reads are wide streaming reads (16 B per lane, global_load_dwordx4 or LDS-DMA
+# dwordx4 over consecutive records or messages): FETCH_SIZE counts half their bytes on gfx950
 # (MI355X_MICROARCH.md HBM section), so x2. Every other kernel's reads are gathers or 4/8-B loads,
 # for which the guide gives no calibration: FETCH_SIZE is taken as it reads (x1), the lower figure
 # (the merge's raw fetch matches its expected region + list bytes; VERDICT r4 #6).
 STREAMING = {
     "pv_net_kernel_reg_tc": "record windows, 5 x 16 B per lane, lanes on consecutive records",
     "pv_net_kernel_reg": "record windows, 5 x 16 B per lane, lanes on consecutive records",
-    "pv_net_kernel_reg8": "record windows, 5 x 16 B per lane, lanes on consecutive records",
-    "pv_net_kernel_ring": "LDS-DMA dwordx4 of packed tiles",
-    "pv_net_kernel_fast": "LDS-DMA dwordx4 of packed tiles",
     "pv_net_kernel": "LDS-DMA dwordx4 of packed tiles",
     "pv_net_kernel_ns": "LDS-DMA dwordx4 of packed tiles",
-    "pv_dns_kernel": "LDS-DMA dwordx4 message windows of consecutive work items",
-    "pv_dns_kernel_f": "LDS-DMA dwordx4 message windows of consecutive work items",
-    "pv_dns_kernel_sfx": "LDS-DMA dwordx4 message windows of consecutive work items",
+    "pv_dns_kernel": "128-B message windows, 8 x 16 B per lane into registers, lanes on consecutive messages",
+    "pv_dns_kernel_f": "128-B message windows, 8 x 16 B per lane into registers, lanes on consecutive messages",
+    "pv_dns_kernel_sfx": "128-B message windows, 8 x 16 B per lane into registers, lanes on consecutive messages",
+    "pv_net_kernel_span": "each tile's packed span, 16 B per lane, consecutive",
 }
 
 
