@@ -952,7 +952,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
             if (efam) P.eecs[e] = eaddr;
         }
         P.events[e] = ev;
-        const uint64_t sk = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + ordr);
+        const uint64_t sk = xact_sort_key(ev.key, (P.ekey_base << 2) + ordr);
         if constexpr (!TCP && !TAP) {
             // the UDP pass: straight into the batch's key list at the range's reserved slots
             // (nev[1]: one per DNS message of the range; pv_xact_compact's work for these ranges)
@@ -4370,7 +4370,7 @@ __device__ void dnstap_event(PV_CREF(PvParams) P, uint32_t j, uint32_t *nev, uin
         const uint64_t eidx = (uint64_t)blockIdx.x * P.wt_per_block * PV_WT + atomicAdd(nev, 1u);
         if (ev.qr) atomicAdd(nresp, 1u);
         P.events[eidx] = ev;
-        P.ekeys[eidx] = ((uint64_t)(hash32(ev.key) >> 1) << 32) | (uint32_t)((P.ekey_base << 2) + (j << 2));
+        P.ekeys[eidx] = xact_sort_key(ev.key, (P.ekey_base << 2) + (j << 2));
         return;
     }
     // ---- DNS v1
@@ -4485,7 +4485,7 @@ extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v)
 
 // ------------------------------------------------------------------ DNS transactions
 // TransactionManager semantics (libs/visor_transaction/TransactionManager.h:51-106) over
-// a whole batch at once: events sorted by (hash32(flow,txid), record index); a
+// a whole batch at once: events sorted by (24-bit hash of (flow,txid), stream rank); a
 // response pairs with the immediately preceding event of the same key iff that
 // event is a query (start_transaction overwrites, maybe_end_transaction erases).
 // Period shifts purge queries older than the TTL (DnsStreamHandler.h:252-267).
@@ -5046,11 +5046,12 @@ extern "C" __global__ void pv_xact_slow(const PvXactParams *__restrict__ Xp, uin
     else slow_check(X, v.idx, v.period, v.dir, v.us);
 }
 
-// Stable LSD radix sort of (key, value) pairs over all 64 key bits (rocPRIM onesweep).
+// Stable LSD radix sort of (key, value) pairs over the transaction keys' bits [0, 32 + 24)
+// (rocPRIM onesweep; the all-ones sentinel is all ones there too, so it still sorts last)
 extern "C" hipError_t pv_radix_sort_pairs(void *tmp, size_t *tmp_bytes, uint64_t *kin, uint64_t *kout, uint32_t *vin,
                                           uint32_t *vout, size_t n, hipStream_t s)
 {
-    return rocprim::radix_sort_pairs(tmp, *tmp_bytes, kin, kout, vin, vout, n, 0, 64, s);
+    return rocprim::radix_sort_pairs(tmp, *tmp_bytes, kin, kout, vin, vout, n, 0, 32 + PV_XHASH_BITS, s);
 }
 
 // ------------------------------------------------------------------ period-shift thresholds

@@ -391,7 +391,7 @@ struct PvParams {
                                // TCP message (pv_dns_tcp_filter), set for an event _filtering rejects
     PV_G PvXEvent *events;     // per-workgroup regions, indexed by workgroup tile range
     PV_G uint64_t *eecs;       // DNS v2 top_ecs: the ECS address of a query event (pad bits 3-4: family)
-    PV_G uint64_t *ekeys;      // sort key per event slot: (hash32(flow,txid) >> 1) << 32 | record index
+    PV_G uint64_t *ekeys;      // sort key per event slot: xact_sort_key (24-bit hash of (flow,txid) << 32 | rank)
     PV_G uint32_t *blk_events; // events appended by each workgroup
     PV_G uint64_t *skeys;      // packed keys (sort input)
     PV_G uint32_t *svals;      // packed event slot positions (sort input)
@@ -503,7 +503,7 @@ struct PvBlob {
 struct PvXactParams {
     PvParams P;            // record access + top-N tables (slow transaction names)
     const PV_G PvXEvent *events;
-    const PV_G uint64_t *skeys; // sorted (hash32(key) << 32 | idx)
+    const PV_G uint64_t *skeys; // sorted xact_sort_key (hash24(key) << 32 | rank)
     const PV_G uint32_t *svals; // event position for each sorted key
     uint32_t n;
     uint32_t ttl_s, ttl_ms;

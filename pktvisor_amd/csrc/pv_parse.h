@@ -107,10 +107,15 @@ PV_FN uint32_t cpc_coupon(uint64_t h1, uint64_t h2)
 
 // Name fingerprint state: two polynomial string hashes over Z/2^32 with odd bases, packed
 // as lo | hi << 32. Prefix hashes give suffix hashes by H(s[i:n]) = H(s[:n]) - H(s[:i]) *
-// B^(n-i) in each lane. Two 32-bit lanes cost a GPU two quarter-rate multiplies per
-// character where one 64-bit lane costs four. Names are <= 255 chars.
-#define PB1 0x9e3779b1u
-#define PB2 0x85ebca77u
+// B^(n-i) in each lane. Names are <= 255 chars. The bases are primes below 2^8, so B, B^2 and
+// B^3 fit 24 bits: a dword of four characters costs one quarter-rate multiply per lane (h * B^4)
+// and three full-rate 24-bit multiply-adds (v_mad_u32_u24) for its characters, where 32-bit
+// bases cost four quarter-rate multiplies per lane (C3 DNS pass). Distinct
+// strings of up to four characters never collide in both lanes (the difference polynomial
+// would need both bases as roots with coefficients below 2^8); longer ones wrap mod 2^32 in
+// each lane, and fp56 mixes the 64 bits with the length.
+#define PB1 251u
+#define PB2 239u
 PV_FN uint64_t ph_step(uint64_t h, uint32_t c)
 {
     const uint32_t lo = (uint32_t)h * PB1 + (c + 1), hi = (uint32_t)(h >> 32) * PB2 + (c + 1);
@@ -124,11 +129,13 @@ PV_FN uint64_t ph_step(uint64_t h, uint32_t c)
 #define PB2_2 (PB2 * PB2)
 #define PB2_3 (PB2_2 * PB2)
 #define PB2_4 (PB2_2 * PB2_2)
+static_assert(PB1_3 < (1u << 24) && PB2_3 < (1u << 24), "24-bit multiply-adds");
 PV_FN uint64_t ph_step4(uint64_t h, uint32_t x)
 {
-    const uint32_t c0 = (x & 0xff) + 1, c1 = ((x >> 8) & 0xff) + 1, c2 = ((x >> 16) & 0xff) + 1, c3 = (x >> 24) + 1;
-    const uint32_t lo = (uint32_t)h * PB1_4 + c0 * PB1_3 + c1 * PB1_2 + c2 * PB1 + c3;
-    const uint32_t hi = (uint32_t)(h >> 32) * PB2_4 + c0 * PB2_3 + c1 * PB2_2 + c2 * PB2 + c3;
+    // (c + 1) B^k = c B^k + B^k: the ones folded into one constant per lane
+    const uint32_t c0 = x & 0xff, c1 = (x >> 8) & 0xff, c2 = (x >> 16) & 0xff, c3 = x >> 24;
+    const uint32_t lo = (uint32_t)h * PB1_4 + c0 * PB1_3 + c1 * PB1_2 + c2 * PB1 + c3 + (PB1_3 + PB1_2 + PB1 + 1u);
+    const uint32_t hi = (uint32_t)(h >> 32) * PB2_4 + c0 * PB2_3 + c1 * PB2_2 + c2 * PB2 + c3 + (PB2_3 + PB2_2 + PB2 + 1u);
     return ((uint64_t)hi << 32) | lo;
 }
 PV_FN uint64_t powb(uint32_t e) // (PB1^e, PB2^e)
@@ -154,6 +161,11 @@ PV_FN uint64_t fp56(uint64_t poly, uint32_t len, uint32_t salt)
     return fmix64(poly ^ ((uint64_t)len << 48) ^ ((uint64_t)salt << 40) ^ 0x9e3779b97f4a7c15ULL) & 0x00ffffffffffffffULL;
 }
 PV_FN uint32_t hash32(uint64_t k) { return (uint32_t)(fmix64(k) >> 17); }
+// transaction sort key: a 24-bit hash of the (flow, txid) key above the 32-bit stream rank, so
+// the radix sort covers bits [0, 56): seven 8-bit passes instead of eight (the pairing compares
+// the keys themselves inside a hash group, so a narrower hash only lengthens a few groups)
+#define PV_XHASH_BITS 24
+PV_FN uint64_t xact_sort_key(uint64_t key, uint32_t rank) { return ((fmix64(key) >> (64 - PV_XHASH_BITS)) << 32) | rank; }
 
 // ------------------------------------------------------------------ packet parse
 struct Parsed {
