@@ -668,6 +668,8 @@ class PvHandlers:
                 f.n_qname_suffixes = len(sx)
                 f.qname_suffixes = ctypes.cast(self._qsfx, ctypes.POINTER(ctypes.c_char_p))
             self._check(self.lib.pv_set_dns_filters(self.ctx, ctypes.byref(f)), "pv_set_dns_filters")
+        # PcapInputStream's LRU of TCP connections replayed per packet (a cache limit implies it)
+        self.tcp_exact = bool(tcp_exact_lru or tcp_packet_reassembly_cache_limit)
         if tcp_packet_reassembly_cache_limit:
             # the pcap input's config (PcapInputStream.cpp:97-99)
             self._check(self.lib.pv_set_tcp_reassembly_limit(self.ctx, int(tcp_packet_reassembly_cache_limit)),

@@ -143,6 +143,13 @@ def process_shard(handlers, recs, index, start_sec: int, start_nsec: int = 0, gr
     """A rank's whole shard of a capture held in host memory: the capture's start_tstamp,
     the global period plan, the shard's batches, the later ranks' shifts. Afterwards every
     rank's windows hold the same periods in the same slots."""
+    if getattr(handlers, "tcp_exact", False) and _world(group) > 1:
+        # the exact LRU mode replays PcapInputStream's one list of TCP connections over the whole
+        # capture (PcapInputStream.cpp:449-459: time-outs of connections of earlier records, at
+        # most MAX_TCP_CLEANUPS per packet, evictions past the cache limit); a shard's list starts
+        # empty, so a sharded run could close connections differently: refused, not approximated
+        raise ValueError("sharded runs do not carry the exact TCP LRU list across shards "
+                         "(tcp_exact_lru / tcp_packet_reassembly_cache_limit): process the capture on one rank")
     handlers.set_start_tstamp(start_sec, start_nsec)
     if not getattr(handlers, "slow_defer", False):
         try:
@@ -159,6 +166,10 @@ def process_shard(handlers, recs, index, start_sec: int, start_nsec: int = 0, gr
         handlers.process_host(recs)
     apply_plan(handlers, plan, 1)
     return plan
+
+
+def _world(group=None) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
 def _allgather(handlers, blob, group=None, comm=None):

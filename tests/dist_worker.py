@@ -29,8 +29,17 @@ def cpu_main(out):
     ranges = [pvdist.shard_range(10, world, r) for r in range(world)]
     got = [None] * world
     dist.all_gather_object(got, {"rank": rank, "blob": bytes([rank]) * (rank + 1)})
+    # a sharded run in the exact TCP LRU mode is refused before it touches the handlers
+    class ExactLru:
+        tcp_exact = True
+    try:
+        pvdist.process_shard(ExactLru(), b"", None, 0)
+        refused = ""
+    except ValueError as e:
+        refused = str(e)
     json.dump({"sum": [int(x) for x in s], "min": [int(x) for x in m], "ranges": ranges,
-               "gathered": [(g["rank"], g["blob"].hex()) for g in got]}, open(f"{out}.{rank}", "w"))
+               "gathered": [(g["rank"], g["blob"].hex()) for g in got], "exact_lru_refused": refused},
+              open(f"{out}.{rank}", "w"))
     dist.destroy_process_group()
 
 
