@@ -2212,19 +2212,6 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
                 nm++;
                 for (int k = 0; k < 8; k++) ms[k] += (double)m[k];
             }
-            {
-                // the ring Net pass's parsing waves (reg_grid x 4)
-                std::vector<uint64_t> rv((size_t)reg_grid * (getenv("PV_RING_NP") ? atoi(getenv("PV_RING_NP")) : 4) * 8);
-                if (hip_ok(hipMemcpy(rv.data(), c->d_stamps + (1u << 20) + 131072, rv.size() * 8, hipMemcpyDeviceToHost))) {
-                    double a[8] = {0};
-                    for (size_t w = 0; w < rv.size() / 8; w++)
-                        for (int k = 0; k < 8; k++) a[k] += (double)rv[w * 8 + k];
-                    const double nw = (double)(rv.size() / 8);
-                    fprintf(stderr, "pv_tstamps ring parser (%u waves): wait_full=%.0f load_fields=%.0f dns_tcp_slow=%.0f hist=%.0f "
-                                    "stores=%.0f loop=%.0f\n",
-                            (unsigned)(rv.size() / 8), a[0] / nw, a[1] / nw, a[2] / nw, a[3] / nw, a[4] / nw, a[7] / nw);
-                }
-            }
             fprintf(stderr, "pv_tstamps combine (%u wg): init=%.0f insert=%.0f count=%.0f scan=%.0f out=%.0f | merge (%lu wg): "
                             "runs=%.0f load=%.0f insert=%.0f wb=%.0f names=%.0f\n",
                     grid, cs[0] / grid, cs[1] / grid, cs[2] / grid, cs[3] / grid, cs[4] / grid, (unsigned long)nm,
