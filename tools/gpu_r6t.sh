@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 6: names kernel decoding name geometry without hashing: the tests that check names
+# (fixtures, KATs, PSL, filters, DNS v2, TCP, full-size C3/C4), then C3 / C4 kernel stats.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$(pwd); O=$R/gpurun_out/${R6_DIR:-r6t}; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_kat.py tests/test_gpu_psl.py tests/test_gpu_filters.py tests/test_gpu_dns2.py tests/test_gpu_tcp.py "tests/test_gpu_bench_shape.py::test_bench_step_full_size[3]" "tests/test_gpu_bench_shape.py::test_bench_step_full_size[4]" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for c in 3 4; do
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c$c -o k -- python3 $R/bench.py --no-cpu-baseline --no-e2e --steps 10 --config $c --reset-each-step > $O/prof_c$c.log 2>&1) || { tail -20 $O/prof_c$c.log; exit 1; }
+  echo "c$c $(python3 tools/kstats.py $O/prof_c$c 2>/dev/null | cut -c1-400)"
+done
