@@ -422,10 +422,13 @@ def cpu_model() -> str:
 def cpu_baseline(cfg: int, seconds: float):
     """The oracle (CPU restatement of the reference handlers, oracle/pv_oracle.cpp) on a
     bounded sample of the same workload, timed on this host: one thread, then one
-    independent oracle instance per host core (`nproc`, as SURVEY.md §8(d) and BASELINE.md
-    ask), each over the same in-memory pcap, as the reference's per-input handler threads
-    would run on separate captures (ctypes releases the GIL for the call). The all-core rate
-    is `value`; the one-thread rate is `single_thread`."""
+    independent oracle instance per core this process may run on (`nproc`, as SURVEY.md §8(d)
+    and BASELINE.md ask, bounded by the affinity mask and the cgroup's CPU quota: the GPU box
+    shows 256 CPUs to a job with a 16-CPU quota, where 256 threads measured 49 against ~100
+    Mpkt/s on C2 for 16, the quota throttling them), each over the same in-memory pcap, as the
+    reference's per-input handler threads would run on separate captures (ctypes releases the
+    GIL for the call). The all-core rate is `value`; the one-thread rate is `single_thread`,
+    and `nproc_estimate` scales it to every CPU the host has (linear, an upper bound)."""
     import threading
     from pktvisor_amd import synth
     from tests.oracle_ctypes import load
@@ -450,7 +453,7 @@ def cpu_baseline(cfg: int, seconds: float):
     except (AttributeError, OSError):
         avail = nproc
     quota = cgroup_cpus()
-    threads = max(1, nproc)
+    threads = max(1, min(nproc, avail, int(quota) if quota else nproc))
     reps_t = 1
     # each thread's sample sized so the all-core leg takes about seconds / 2 of wall time on the
     # cores this process may actually run on (affinity, cgroup quota)
@@ -472,10 +475,10 @@ def cpu_baseline(cfg: int, seconds: float):
     raten = n_t * reps_t * threads / dtn
     return {"value": round(raten / 1e6, 4), "unit": "Mpkt/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "single_thread": round(rate1 / 1e6, 4), "nproc": nproc, "affinity_cpus": avail,
-            "cgroup_cpu_quota": quota,
+            "cgroup_cpu_quota": quota, "nproc_estimate": round(rate1 * nproc / 1e6, 2),
             "sample": (f"the same synthetic workload as in-memory pcaps, oracle/pv_oracle.cpp: {threads} threads "
-                       f"(nproc) x {n_t} records in {dtn:.1f} s; one thread {n} records x {reps} passes in {dt1:.1f} s "
-                       f"({rate1 / 1e6:.3f} Mpkt/s)")}
+                       f"(the CPUs this job may use of nproc {nproc}) x {n_t} records in {dtn:.1f} s; one thread {n} "
+                       f"records x {reps} passes in {dt1:.1f} s ({rate1 / 1e6:.3f} Mpkt/s)")}
 
 
 def cgroup_cpus():
