@@ -454,13 +454,13 @@ def cpu_baseline(cfg: int, seconds: float):
         avail = nproc
     quota = cgroup_cpus()
     threads = max(1, min(nproc, avail, int(quota) if quota else nproc))
-    reps_t = 1
-    # each thread's sample sized so the all-core leg takes about seconds / 2 of wall time on the
-    # cores this process may actually run on (affinity, cgroup quota)
-    eff = max(1.0, min(float(avail), quota or float(nproc)))
-    n_t = int(max(10_000, min(n, rate1 * seconds / 2 * eff / threads)))
+    # the all-core leg: about 2 x seconds of CPU work over the threads (one independent pass of
+    # the sample per repetition), so it stays a bounded sample on any core count
+    per_thread_s = 2.0 * seconds / threads
+    n_t = int(max(10_000, min(n, rate1 * per_thread_s)))
     if n_t != n:
         pcap = synth.pcap_bytes(cfg, n_t)
+    reps_t = max(1, int(round(per_thread_s * rate1 / n_t)))
 
     def work():
         for _ in range(reps_t):
@@ -477,7 +477,7 @@ def cpu_baseline(cfg: int, seconds: float):
             "single_thread": round(rate1 / 1e6, 4), "nproc": nproc, "affinity_cpus": avail,
             "cgroup_cpu_quota": quota, "nproc_estimate": round(rate1 * nproc / 1e6, 2),
             "sample": (f"the same synthetic workload as in-memory pcaps, oracle/pv_oracle.cpp: {threads} threads "
-                       f"(the CPUs this job may use of nproc {nproc}) x {n_t} records in {dtn:.1f} s; one thread {n} "
+                       f"(the CPUs this job may use of nproc {nproc}) x {n_t} records x {reps_t} passes in {dtn:.1f} s; one thread {n} "
                        f"records x {reps} passes in {dt1:.1f} s ({rate1 / 1e6:.3f} Mpkt/s)")}
 
 
