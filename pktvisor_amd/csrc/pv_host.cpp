@@ -1655,8 +1655,9 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
                uint64_t ev_hi)
 {
     hipError_t e;
+    c->ovf_known = false;
     const bool dns_here = nev_b > 0;
-    bool pair = (dns_here && (nresp > 0 || P.n_dshift > 0)) || (!dns_here && P.n_dshift > 0 && c->n_pend > 0);
+    bool pair =(dns_here && (nresp > 0 || P.n_dshift > 0)) || (!dns_here && P.n_dshift > 0 && c->n_pend > 0);
     if (dns_here && !pair && (c->n_pend + nev_b > c->pend_cap || (c->n_pend && c->pend_hi + nev_b > c->ev_store_cap)))
         pair = true; // compact the carried list
     if (dns_here && !pair) {
@@ -1777,13 +1778,16 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
             hipStreamSynchronize(st);
         }
         HP(12);
+        // one read-back: the value / carried counts, the flags and the overflow words (the
+        // caller's top_slow drain then needs no read of its own)
         uint32_t nv3[3] = {0, 0, 0};
         if (!hip_ok(e = hipMemcpyAsync(nv3, c->d_nvals, 12, hipMemcpyDeviceToHost, st)) ||
+            !hip_ok(e = hipMemcpyAsync(c->h_status, c->d_status, ST_RB_WORDS * 4, hipMemcpyDeviceToHost, st)) ||
             !hip_ok(e = hipStreamSynchronize(st)))
             return c->hipfail(e, "carried queries");
+        c->ovf_known = true;
         const uint32_t npo = nv3[2];
-        uint32_t vflags = 0;
-        if (!hip_ok(e = hipMemcpy(&vflags, c->d_status + ST_FLAGS, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "status");
+        const uint32_t vflags = c->h_status[ST_FLAGS];
         if ((vflags & PVF_VALUES_FULL) || nv3[0] > c->xv_cap) return c->fail(PV_ECAPACITY, "transaction value buffer full");
         // a batch pushes at most two values per response (time + ratio), so keep 2 x max_records free
         if (c->xv_cap - nv3[0] < 2ull * c->max_records) {
@@ -2237,9 +2241,12 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
                             (uint64_t)(grid + gt) * P.wt_per_block * 64u))
         return rc;
     HP(6);
-    // top_slow updates of the transaction stage (only when it ran)
+    // top_slow updates of the transaction stage (only when it ran; its read-back after the
+    // resolve holds the overflow words)
+    const bool ovf_known = c->ovf_known;
+    c->ovf_known = false;
     if ((status[ST_NEV] || c->n_pend) && P.want_events)
-        if (int rc = drain_overflow(c, st)) return rc;
+        if (int rc = drain_overflow(c, st, ovf_known)) return rc;
 
     // ---- window bookkeeping (host mirror of each manager's _period_shift)
     for (const Shift &sh : nsh) win_shift(c, c->net, sh.sec);

@@ -620,6 +620,7 @@ struct pv_ctx {
     PvOvf *d_ovf = nullptr, *d_ovf2 = nullptr; // top-N overflow list and its retry copy
     uint32_t *d_ovf_cnt = nullptr, ovf_cap = 0;
     uint32_t *h_ovf = nullptr;                  // pinned copy of the two overflow words (read with the status)
+    bool ovf_known = false;                     // h_ovf read back after the transaction stage's resolve
     uint64_t ovf_rounds = 0;                    // purge-and-retry rounds so far
     uint8_t *d_ctmp = nullptr;          // arena compaction scratch (one table's arena)
     unsigned long long *d_ctop = nullptr;
