@@ -675,6 +675,7 @@ static void tcp_reset(pv_ctx *c)
     c->tcp_active = false;
     c->lru.clear();
     c->lru_at.clear();
+    c->lru_hold.clear();
 }
 
 int pv_reset(pv_ctx *c)
@@ -1004,7 +1005,10 @@ int tcp_alloc(pv_ctx *c)
 // close. Every connection closed this way is closed after that record (closeConnection): fclose
 // (per segment index) at its first sorted segment when it has packets in the batch (its later
 // packets are then Ignore_PacketOfClosedFlow, and their events are skipped here), else a
-// close-only segment appended to `extra` with its fclose in `extra_fc`.
+// close-only segment appended to `extra` with its fclose in `extra_fc`. A connection whose close
+// flushes held fragments is put into the list once more by that delivery before its end erases
+// it (PcapInputStream.cpp:254-263,276-283): an evicted one can evict the next tail that way,
+// which the same overflow loop then closes.
 void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vector<uint32_t> &sval,
                     const std::vector<uint32_t> &ev, std::vector<uint32_t> &fclose, std::vector<PvTcpSeg> &extra,
                     std::vector<uint32_t> &extra_fc)
@@ -1025,10 +1029,24 @@ void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vec
         c->lru_at.erase(it);
     };
     std::unordered_map<uint32_t, bool> closed; // closed by the replay in this batch
+    std::vector<uint32_t> overflow;
+    auto put = [&](uint32_t f, uint32_t t) {
+        erase(f);
+        c->lru.emplace_front(f, t);
+        c->lru_at[f] = c->lru.begin();
+        if (c->tcp_limit && c->lru_at.size() > c->tcp_limit) {
+            const uint32_t v = c->lru.back().first;
+            c->lru_at.erase(v);
+            c->lru.pop_back();
+            overflow.push_back(v);
+        }
+    };
     auto close_after = [&](uint32_t v, uint32_t idx, uint32_t sec, uint32_t dir) {
-        erase(v);
-        if (closed.count(v)) return;
+        if (closed.count(v)) { erase(v); return; }
         closed[v] = true;
+        // the flush's put (its time is moot: the connection's end erases it next)
+        if (c->lru_hold.erase(v)) put(v, 0);
+        erase(v);
         auto it = first.find(v);
         if (it != first.end()) {
             uint32_t *w = &fclose[3 * (size_t)sval[it->second]];
@@ -1045,18 +1063,6 @@ void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vec
         extra.push_back(g);
         extra_fc.insert(extra_fc.end(), {idx, sec, dir});
     };
-    std::vector<uint32_t> overflow;
-    auto put = [&](uint32_t f, uint32_t t) {
-        erase(f);
-        c->lru.emplace_front(f, t);
-        c->lru_at[f] = c->lru.begin();
-        if (c->tcp_limit && c->lru_at.size() > c->tcp_limit) {
-            const uint32_t v = c->lru.back().first;
-            c->lru_at.erase(v);
-            c->lru.pop_back();
-            overflow.push_back(v);
-        }
-    };
     for (uint32_t k : order) {
         const uint32_t f = (uint32_t)(skey[k] >> 32), idx = (uint32_t)skey[k];
         const uint32_t fl = ev[3 * k] & 0xff, dir = (ev[3 * k] >> 8) & 3, sec = ev[3 * k + 1], pt = ev[3 * k + 2];
@@ -1064,13 +1070,16 @@ void tcp_lru_replay(pv_ctx *c, const std::vector<uint64_t> &skey, const std::vec
             if (fl & PVT_EV_NEW) put(f, sec);
             if (fl & PVT_EV_PUT) put(f, pt);
             if (fl & PVT_EV_CLOSE) erase(f);
+            if (fl & PVT_EV_HOLD) c->lru_hold.insert(f);
+            else c->lru_hold.erase(f);
         }
         for (int q = 0; q < MAX_TCP_CLEANUPS && !c->lru.empty(); q++) {
             const auto back = c->lru.back();
             if ((uint64_t)sec < (uint64_t)back.second + PV_TCP_TIMEOUT) break;
             close_after(back.first, idx, sec, dir);
         }
-        for (uint32_t v : overflow) close_after(v, idx, sec, dir);
+        // indexed: a close's put may append the next eviction
+        for (size_t q = 0; q < overflow.size(); q++) close_after(overflow[q], idx, sec, dir);
         overflow.clear();
     }
 }

@@ -769,6 +769,8 @@ struct pv_ctx {
     std::vector<std::pair<std::array<uint8_t, 16>, uint32_t>> dt_v6;
     std::list<std::pair<uint32_t, uint32_t>> lru;
     std::unordered_map<uint32_t, std::list<std::pair<uint32_t, uint32_t>>::iterator> lru_at;
+    // connections whose close would deliver held fragments (PVT_EV_HOLD after their last segment)
+    std::set<uint32_t> lru_hold;
     bool tcp_exact = false;   // pv_set_tcp_exact_lru
     bool tcp_exact_on() const { return tcp_exact || tcp_limit; }
     uint32_t *d_lru_ev = nullptr, *d_fclose = nullptr;

@@ -609,8 +609,9 @@ struct PvTcpParams {
 };
 enum { PVT_NMSG = 0, PVT_ARENA, PVT_CARRY, PVT_NCARRY, PVT_NFRAG, PVT_FLAGS, PVT_WORDS };
 // LRU events of one segment (lru_ev flags): a connection start's put, a message delivery's put,
-// the connection closed (FIN/RST) in it, closed by the 30 s timeout ahead of it
-enum { PVT_EV_NEW = 1, PVT_EV_PUT = 2, PVT_EV_CLOSE = 4, PVT_EV_TIMEOUT = 8 };
+// the connection closed (FIN/RST) in it, closed by the 30 s timeout ahead of it; HOLD: after it
+// the connection holds a fragment that closing it would deliver (the close's own put)
+enum { PVT_EV_NEW = 1, PVT_EV_PUT = 2, PVT_EV_CLOSE = 4, PVT_EV_TIMEOUT = 8, PVT_EV_HOLD = 16 };
 #define PVT_FCLOSE_NONE 0xffffffffu
 enum { PVT_F_TABLE = 1, PVT_F_ARENA = 2, PVT_F_CARRY = 4, PVT_F_FRAGS = 8, PVT_F_MSGS = 16 };
 

@@ -273,6 +273,17 @@ __device__ void check_ooo(PV_CREF(PvTcpParams) T, Flow &F, int s, bool clean)
     } while (found);
 }
 
+// closing the connection now would deliver data (checkOutOfOrderFragments with cleanup: a held
+// fragment that ends past the side's next sequence), so the close puts it into the LRU list
+// once more (PcapInputStream::tcp_message_ready) before its end erases it
+__device__ bool held_delivery(PV_CREF(PvTcpParams) T, const Flow &F)
+{
+    for (int s = 0; s < 2; s++)
+        for (uint32_t q = F.head[s]; q != PV_TCP_FRAG_NIL; q = T.frags[q].next)
+            if (seq_gt(T.frags[q].seq + T.frags[q].len, F.f.seq[s])) return true;
+    return false;
+}
+
 // TcpReassembly::closeConnectionInternal (+ DnsStreamHandler::tcp_connection_end_cb)
 __device__ void close_conn(PV_CREF(PvTcpParams) T, Flow &F, uint32_t when)
 {
@@ -577,6 +588,7 @@ extern "C" __global__ void __launch_bounds__(256) pv_tcp_flow(const PvTcpParams 
         F.put_sec = 0;
         packet(T, F, g);
         if (T.lru_ev) {
+            if (!F.f.closed && held_delivery(T, F)) F.ev |= PVT_EV_HOLD;
             T.lru_ev[3 * k] = F.ev | (g.dirv6 & 3) << 8;
             T.lru_ev[3 * k + 1] = g.sec;
             T.lru_ev[3 * k + 2] = F.put_sec;

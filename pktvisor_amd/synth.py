@@ -322,6 +322,89 @@ def tcp_dns_pcap(seed: int = 1, flows: int = 60, duration_s: float = 20.0, udp_s
     return pcap_file_bytes(bytes(out))
 
 
+def _pcap_of(events) -> bytes:
+    """(seconds, frame) pairs, sorted by time, as a classic pcap file"""
+    import struct
+    from pktvisor_amd import pcap_file_bytes
+    out = bytearray()
+    for t, fr in sorted(events, key=lambda e: e[0]):
+        us = int(round((1700000000.0 + t) * 1e6))
+        out += struct.pack("<IIII", us // 1000000, us % 1000000, len(fr), len(fr)) + fr
+    return pcap_file_bytes(bytes(out))
+
+
+def tcp_reput_pcap() -> bytes:
+    """Three DNS-over-TCP connections under tcp_packet_reassembly_cache_limit = 2, one second
+    apart (PcapInputStream.cpp:254-283,429-465):
+      A: SYN, then a segment 10 bytes past the next sequence (held out of order);
+      B: SYN, then the first 10 bytes of a framed 24-byte query (length + 8 bytes);
+      C: SYN: its put overflows the list [C, B, A] and evicts A. Closing A flushes the held
+         fragment behind "[10 bytes missing]", whose delivery puts A into the list again
+         ([A, C, B]): that put evicts B, which the same overflow loop closes;
+      B: the remaining 16 bytes of the query: a packet of a closed flow, ignored.
+    So no TCP query is counted; a replay without the flush's put keeps B open and counts one."""
+    import struct
+    srv = bytes([8, 8, 8, 8])
+    q = _dns_msg(np.random.default_rng(0), 0x1234, False, "ab.com", 1)
+    assert len(q) == 24
+    framed = struct.pack(">H", len(q)) + q
+    a, b, c = bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2]), bytes([10, 0, 0, 3])
+    sa, sb, sc = 1000, 5000, 9000
+    ev = [(0.0, _frame(a, srv, 1001, 53, sa, 0x02, b"", False)),
+          (1.0, _frame(a, srv, 1001, 53, sa + 1 + 10, 0x18, bytes(range(1, 21)), False)),
+          (2.0, _frame(b, srv, 1002, 53, sb, 0x02, b"", False)),
+          (3.0, _frame(b, srv, 1002, 53, sb + 1, 0x18, framed[:10], False)),
+          (4.0, _frame(c, srv, 1003, 53, sc, 0x02, b"", False)),
+          (5.0, _frame(b, srv, 1002, 53, sb + 11, 0x18, framed[10:], False))]
+    return _pcap_of(ev)
+
+
+def tcp_held_evict_pcap(seed: int = 1, flows: int = 48, duration_s: float = 12.0) -> bytes:
+    """DNS-over-TCP connections that hold out-of-order fragments for a long time while many
+    others start: each client sends its framed queries cut into 3-6 segments, the second one
+    delayed by 0.3-3 s behind the later ones, then FIN; the server answers in order. Under a
+    small tcp_packet_reassembly_cache_limit the list evicts connections that hold fragments,
+    whose closes put them into the list again (tcp_reput_pcap)."""
+    import struct
+    rng = np.random.default_rng(seed)
+    srv = bytes([8, 8, 8, 8])
+    names = [f"h{k}.example.{tld}" for k in range(6) for tld in ("com", "net")]
+    ev = []
+    for f in range(flows):
+        cli = bytes([10, 1, int(rng.integers(0, 256)), int(rng.integers(1, 255))])
+        cp = 2000 + f
+        cs, ss = int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32))
+        cb, sb = b"", b""
+        for _ in range(int(rng.integers(1, 4))):
+            name = names[int(rng.integers(0, len(names)))]
+            txid = int(rng.integers(0, 65536))
+            qm = _dns_msg(rng, txid, False, name, 1)
+            rm = _dns_msg(rng, txid, True, name, 1, 0, int(rng.integers(0, 3)))
+            cb += struct.pack(">H", len(qm)) + qm
+            sb += struct.pack(">H", len(rm)) + rm
+        cuts = sorted(set(int(x) for x in rng.integers(1, len(cb), int(rng.integers(2, 6)))))
+        bounds = [0] + cuts + [len(cb)]
+        segs = [(cs + 1 + bounds[k], cb[bounds[k]:bounds[k + 1]]) for k in range(len(bounds) - 1)]
+        t = float(rng.random() * duration_s)
+        ev.append((t, _frame(cli, srv, cp, 53, cs, 0x02, b"", False)))
+        t += float(rng.exponential(0.05))
+        ev.append((t, _frame(srv, cli, 53, cp, ss, 0x12, b"", False)))
+        late = 1 if len(segs) > 2 else len(segs) - 1
+        for k, (sq, pl) in enumerate(segs):
+            if k == late:
+                continue
+            t += float(rng.exponential(0.05))
+            ev.append((t, _frame(cli, srv, cp, 53, sq, 0x18, pl, False)))
+        t += 0.3 + float(rng.random()) * 2.7
+        ev.append((t, _frame(cli, srv, cp, 53, segs[late][0], 0x18, segs[late][1], False)))
+        t += float(rng.exponential(0.05))
+        ev.append((t, _frame(srv, cli, 53, cp, ss + 1, 0x18, sb, False)))
+        t += float(rng.exponential(0.05))
+        ev.append((t, _frame(cli, srv, cp, 53, cs + 1 + len(cb), 0x11, b"", False)))
+        ev.append((t + 0.01, _frame(srv, cli, 53, cp, ss + 1 + len(sb), 0x11, b"", False)))
+    return _pcap_of(ev)
+
+
 # ---------------------------------------------------------------- random-subdomain flood
 def qname_flood_pcap(seed: int = 1, heavy: int = 24, flood: int = 40000, duration_s: float = 40.0):
     """UDP DNS queries for a random-subdomain flood: `flood` distinct one-off names

@@ -56,11 +56,31 @@ def test_limit_synthetic(oracle, tmp_path, limit, periods):
     assert diff(gpu, ref) is None, diff(gpu, ref)
 
 
-@pytest.mark.parametrize("limit", [3, 12])
-def test_limit_across_batches(oracle, limit):
+@pytest.mark.parametrize("limit", [2, 3])
+def test_limit_reput_crafted(oracle, tmp_path, limit):
+    """closing an evicted connection flushes its held fragment, whose put evicts the next tail
+    (synth.tcp_reput_pcap: at 2 no TCP query survives, at 3 one does; the oracle's counts are
+    pinned by test_synth_oracle.py::test_tcp_reput_crafted)"""
+    gpu, ref = both(oracle, synth.tcp_reput_pcap(), tmp_path, "", 1, limit)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+    assert gpu["1m"]["dns"]["wire_packets"]["tcp"] == (0 if limit == 2 else 1)
+
+
+@pytest.mark.parametrize("limit", [2, 3, 5, 8])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_limit_held_evict(oracle, tmp_path, seed, limit):
+    """connections evicted while they hold out-of-order fragments (synth.tcp_held_evict_pcap:
+    seed 1 at limit 3 has 17 such closes whose flush evicts another connection)"""
+    gpu, ref = both(oracle, synth.tcp_held_evict_pcap(seed), tmp_path, HOST, 1, limit)
+    assert diff(gpu, ref) is None, diff(gpu, ref)
+
+
+@pytest.mark.parametrize("limit,kind", [(3, "dns"), (12, "dns"), (3, "held")])
+def test_limit_across_batches(oracle, limit, kind):
     """many small batches: the LRU list, and evictions of connections with no segment in their
-    batch (closed ahead of their next segment), carried from batch to batch"""
-    pcap = synth.tcp_dns_pcap(5, flows=80, duration_s=100, pauses=6)
+    batch (closed ahead of their next segment), carried from batch to batch; "held": the
+    connections holding fragments, carried too"""
+    pcap = synth.tcp_dns_pcap(5, flows=80, duration_s=100, pauses=6) if kind == "dns" else synth.tcp_held_evict_pcap(3)
     recs = pcap[24:]
     idx = pa.RecordIndex(recs)
     offs = list(idx.offsets) + [len(recs)]

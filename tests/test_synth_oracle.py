@@ -35,3 +35,14 @@ def test_paired_configs(oracle, cfg):
 def test_edge_mix_runs(oracle):
     out = oracle.run_bytes(synth.pcap_bytes(9, 20000), host_spec="10.0.0.0/8,2000::/3", num_periods=1, window=1)
     assert out["1m"]["packets"]["events"] == 20000
+
+
+@pytest.mark.parametrize("limit,tcp", [(2, 0), (3, 1), (None, 1)])
+def test_tcp_reput_crafted(oracle, limit, tcp):
+    """The oracle against the reference's LRU order derived by hand (synth.tcp_reput_pcap): with
+    the list capped at 2, closing the evicted A flushes its held fragment, that delivery's put
+    evicts B, and B's last segment then belongs to a closed flow (PcapInputStream.cpp:254-263,
+    449-465; TcpReassembly::closeConnection). Without the cap, or at 3, B's query counts."""
+    out = oracle.run_bytes(synth.tcp_reput_pcap(), num_periods=1, window=1, tcp_packet_reassembly_cache_limit=limit)
+    d = out["1m"]["dns"]["wire_packets"]
+    assert (d["tcp"], d["queries"]) == (tcp, tcp)
