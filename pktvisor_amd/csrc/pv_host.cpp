@@ -631,7 +631,7 @@ void pv_destroy(pv_ctx *c)
                     c->d_tval[1], c->d_run_flow, c->d_tsort_tmp, c->d_flows, c->d_carry[0], c->d_carry[1], c->d_clist[0],
                     c->d_clist[1], c->d_frags, c->d_marena, c->d_moffs, c->d_tmq, c->d_tsfx,
                     c->d_theta, c->d_ctmp, c->d_ctop, c->d_ovf, c->d_ovf2, c->d_iplog32,
-                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_slow, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose,
+                    c->d_ipx_rep, c->d_ipdir, c->d_ipx_cnt, c->d_slow, c->d_ecs, c->d_eecs, c->d_pecs[0], c->d_pecs[1], c->d_lru_ev, c->d_fclose,
                     c->d_xcnt, c->d_xrhdr, c->d_xtot, c->d_xsend, c->d_xrecv, c->d_xp, c->d_bpf, c->d_fwork, c->d_frecs,
                     c->d_foffs, c->d_fsc, c->d_fscan, c->d_eoc, c->d_eoc_cnt};
     for (void *p : ptrs) if (p) hipFree(p);
@@ -2000,6 +2000,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
     P.n_keys = c->d_status + ST_NKEYS;
     P.n_dns = c->d_status + ST_NDNS;
     P.n_slow = c->d_status + ST_NSLOW;
+    P.n_ecs = c->d_status + ST_NECS;
     P.want_events = ((c->dns_groups & PV_DNS_TRANSACTIONS) || c->dns2_groups) ? 1 : 0;
     // sort ranks: carried queries 0, this batch's records from records_seen - pend_base on
     if (c->n_pend == 0) c->pend_base = (int64_t)c->records_seen - 1;
@@ -2120,6 +2121,18 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         P.slow_list = c->d_slow;
         P.slow_cnt = c->d_slow + c->slow_cap; // written for every range by the lean passes
     }
+    // top_ecs: the UDP DNS pass lists its updates (at most one per record) for pv_dns_ecs
+    if (c->dns_groups & PV_DNS_TOP_ECS) {
+        if (c->ecs_cap < P.n) {
+            if (c->d_ecs) hipFree(c->d_ecs);
+            c->d_ecs = nullptr;
+            c->ecs_cap = 0;
+            if (!hip_ok(e = hipMalloc(&c->d_ecs, (size_t)P.n * sizeof(uint4)))) return c->hipfail(e, "top_ecs list");
+            c->ecs_cap = P.n;
+        }
+        P.ecs_list = reinterpret_cast<uint32_t *>(c->d_ecs);
+        P.ecs_cap = (uint32_t)c->ecs_cap;
+    }
     *c->h_params = P;
     if (!hip_ok(e = fill_and_upload(c, c->d_params, c->h_params, sizeof P, st)))
         return c->hipfail(e, "parameter upload");
@@ -2155,6 +2168,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         hipLaunchKernelGGL(pv_dns_kernel_f, dim3(dns_grid), dim3(64 * PV_DNS_WAVES), 0, st, (const PvParams *)c->d_params);
     else
         hipLaunchKernelGGL(pv_dns_kernel, dim3(dns_grid), dim3(64 * PV_DNS_WAVES), 0, st, (const PvParams *)c->d_params);
+    if (c->dns_groups & PV_DNS_TOP_ECS)
+        hipLaunchKernelGGL(pv_dns_ecs, dim3((uint32_t)c->cus * 2), dim3(256), 0, st, (const PvParams *)c->d_params);
     if (c->net2_groups) hipLaunchKernelGGL(pv_net2_kernel, dim3(grid), dim3(256), 0, st, (const PvParams *)c->d_params);
     // top-N: combine each workgroup's updates into a list sorted by table region, merge
     // each region's runs in LDS, decode the names of new entries

@@ -142,6 +142,7 @@ extern "C" __global__ void pv_rec_gather(const uint8_t *recs, const uint32_t *of
 extern "C" __global__ void pv_dns_kernel(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel_sfx(const PvParams *P);
 extern "C" __global__ void pv_dns_kernel_f(const PvParams *P);
+extern "C" __global__ void pv_dns_ecs(const PvParams *P);
 extern "C" __global__ void pv_dns_suffix(const PvParams *P);
 extern "C" __global__ void pv_fill_u64(uint64_t *p, uint64_t n, uint64_t v);
 extern "C" __global__ void pv_fill_u32(uint32_t *p, uint64_t n, uint32_t v);
@@ -214,7 +215,8 @@ namespace pvh {
 // status words (device): flags, n_events, n_resp, n_vals, DNS messages, new top-N names
 enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNEW = 5, ST_TSEG = 6, ST_TSEG_BYTES = 7,
        ST_HANDS = 8 /* top-N handlers with entries (device only) */, ST_NKEYS = 9 /* key-list length */,
-       ST_NSLOW = 10 /* general-path records the Net pass deferred (device only) */, ST_WORDS = 11 };
+       ST_NSLOW = 10 /* general-path records the Net pass deferred (device only) */,
+       ST_NECS = 11 /* top_ecs updates the DNS pass listed (device only) */, ST_WORDS = 12 };
 // status allocation (zeroed per batch): the words above, padded
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
 #define PV_TRASH_WAVES 16384 // Net-pass waves with a 2-KiB trash area (grid <= 4096)
@@ -566,6 +568,8 @@ struct pv_ctx {
     uint64_t *d_ipdir = nullptr;
     uint32_t *d_slow = nullptr; // span Net pass: deferred record indices (max_records), their count
     uint64_t slow_cap = 0;
+    uint4 *d_ecs = nullptr; // top_ecs updates of the UDP DNS pass (one per record at most)
+    uint64_t ecs_cap = 0;
     uint64_t *d_trash = nullptr; // 64 B per Net-pass wave
     uint32_t nn_cap = 0;
     uint32_t reg_log2 = 0;

@@ -1051,10 +1051,12 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
         }
     }
     // top-N / dense update: cache, else log (hashed) or HBM atomic (dense); boundary: global table
+    // (the UDP pass always has the cache: no call to global_add is compiled into it, so its
+    // registers and scratch follow no call convention)
     auto top = [&](uint32_t metric, uint64_t payload, uint32_t w) {
         const uint64_t key = PV_KEY(metric, payload);
         if (P.dbg & 32) return; // profiling knob: no table updates
-        if (cache && !(P.dbg & 256)) { // 256: profiling knob, no LDS key cache
+        if constexpr (!TCP && !TAP) {
             uint32_t first;
             if (cache->add(PV_LKEY(slot, metric, payload), w, i, first)) return;
             if (metric >= TM_DENSE_PORT) sum_add(P, slot, dense_word(metric, payload), w);
@@ -1152,7 +1154,14 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
                 if (fam) {
                     if (own) c.dqecs++;
                     else if (P.dns_groups & PV_DNS_COUNTERS_BIT) sum_add(P, slot, PV_OFF_DNS + DC_QECS, 1);
-                    global_add(P, slot, PV_KEY(TM_ECS, fmix64(addr ^ ((uint64_t)fam << 62) ^ 0xec5ull)), 1, i);
+                    const uint64_t ek = PV_KEY(TM_ECS, fmix64(addr ^ ((uint64_t)fam << 62) ^ 0xec5ull));
+                    if constexpr (TCP || TAP) global_add(P, slot, ek, 1, i);
+                    else {
+                        // listed for pv_dns_ecs (one per record at most: the list holds the batch)
+                        const uint32_t q = atomicAdd(P.n_ecs, 1u);
+                        if (q < P.ecs_cap) reinterpret_cast<PV_G uint4 *>(P.ecs_list)[q] = make_uint4((uint32_t)ek, (uint32_t)(ek >> 32), slot, (uint32_t)i);
+                        else atomicOr(P.flags, PVF_TABLE_FULL);
+                    }
                 }
             }
         }
@@ -1171,7 +1180,7 @@ __device__ __forceinline__ void dns_process(PV_CREF(PvParams) P, Cache *cache, u
 
 // Flush a workgroup's key cache: hashed keys to the update log, dense keys to HBM.
 template <class Cache>
-__device__ void cache_flush(PV_CREF(PvParams) P, Cache &C, uint32_t n, uint32_t *mq_n)
+__device__ __forceinline__ void cache_flush(PV_CREF(PvParams) P, Cache &C, uint32_t n, uint32_t *mq_n)
 {
     for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
         const uint64_t k = C.key[j];
@@ -2852,6 +2861,17 @@ __device__ __forceinline__ void dns_pass(const PvParams *__restrict__ Pp)
 extern "C" __global__ void __launch_bounds__(64 * PV_DNS_WAVES, PV_DNS_MINW) pv_dns_kernel(const PvParams *__restrict__ Pp)
 {
     dns_pass<false, false>(Pp);
+}
+// the UDP DNS pass's top_ecs updates into the global table (global_add, as the TCP pass inserts
+// its own): kept out of the pass, whose registers then follow no device-call convention
+extern "C" __global__ void __launch_bounds__(256) pv_dns_ecs(const PvParams *__restrict__ Pp)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint32_t n = min(*P.n_ecs, P.ecs_cap);
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const uint4 e = reinterpret_cast<const PV_G uint4 *>(P.ecs_list)[j];
+        global_add(P, e.z, (uint64_t)e.x | (uint64_t)e.y << 32, 1, e.w);
+    }
 }
 // a context with DNS filters (v1 or v2), no suffix
 extern "C" __global__ void __launch_bounds__(64 * PV_DNS_WAVES, PV_DNS_MINW) pv_dns_kernel_f(const PvParams *__restrict__ Pp)

@@ -439,6 +439,11 @@ struct PvParams {
     PV_G uint32_t *slow_list;
     PV_G uint32_t *slow_cnt;
     PV_G uint32_t *n_slow; // deferred records of the batch (status word; pv_net_slow_list exits at 0)
+    // top_ecs of the UDP DNS pass: {key lo, key hi, slot, record} per query with an ECS option,
+    // inserted into the global table by pv_dns_ecs after the pass (no device call in the pass)
+    PV_G uint32_t *ecs_list; // four words an entry
+    PV_G uint32_t *n_ecs; // status word
+    uint32_t ecs_cap;
     PV_G uint64_t *trash; // 64-B line per Net-pass wave for stores that have nothing to store
     PV_G uint64_t *cb;    // combined update lists sorted by table region, mq_cap entries per workgroup
     PV_G uint32_t *cb_cnt;
