@@ -1748,17 +1748,26 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
         if (!hip_ok(e = (*c->h_xparams = X, upload_params(c->d_xparams, c->h_xparams, sizeof X, st))))
             return c->hipfail(e, "parameter upload");
         HP(17);
-        hipLaunchKernelGGL(pv_xact_resolve, dim3(blocks), dim3(threads), 0, st, (const PvXactParams *)c->d_xparams);
+        // the v1 resolve (36 VGPRs) would hold eight workgroups a CU; its scattered event reads
+        // run best at three (C4: 190 us at eight, 162 at four, 157 at three, 162 at two, 233 at
+        // one; profiles/r6/resolve/), which 30 KiB of dynamic LDS beside its 18 KiB XState sets
+        const uint32_t rpad = P.dns2_groups ? 0u : PV_RESOLVE_PAD;
+        hipLaunchKernelGGL(P.dns2_groups ? pv_xact_resolve2 : pv_xact_resolve, dim3(blocks), dim3(threads), rpad, st,
+                           (const PvXactParams *)c->d_xparams);
         if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_resolve");
         HP(18);
         // (the resolve kernel also moves the queries still open to the carried list: pv_xact_carry's work)
+        // the DNS v1 resolve lists the slow transactions of periods with a threshold for
+        // pv_xact_slow_dev instead of naming them itself
+        const bool listed_slow = !P.dns2_groups && (X.thr_from[0] > 0.0f || X.thr_to[0] > 0.0f);
+        const bool shift_thr = P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES));
         if (c->slow_defer) {
             if (int rc = defer_slow(c, P, st)) return rc;
-        } else if (P.n_dshift > 0 && ((c->dns_groups & PV_DNS_QUANTILES) || (c->dns2_groups & PV_DNS2_XACT_TIMES))) {
+        } else if (shift_thr || listed_slow) {
             // on_period_shift: slow thresholds = p90 of the bucket that just closed
             // (dns/v1/DnsStreamHandler.h:259-266); kept when that bucket had none
             HP(19);
-            for (uint32_t k = 1; k <= P.n_dshift; k++) {
+            for (uint32_t k = 1; shift_thr && k <= P.n_dshift; k++) {
                 const uint32_t sg = P.dslot_of[k - 1] | (c->gen[P.dslot_of[k - 1]] << 8);
                 bool have[PV_XV_SEL];
                 uint64_t q[PV_XV_SEL];
@@ -1773,18 +1782,13 @@ int pair_stage(pv_ctx *c, const PvParams &P, uint32_t nev_b, uint32_t nkeys, uin
                     X.thr2[k][d] = c->p90_2[d];
                 }
             }
-            uint32_t nvalid = 0;
-            if (!hip_ok(e = hipMemcpy(&nvalid, c->d_nvals + 1, 4, hipMemcpyDeviceToHost))) return c->hipfail(e, "valid count");
-            if (nvalid) {
-                if (!hip_ok(e = (*c->h_xparams = X, upload_params(c->d_xparams, c->h_xparams, sizeof X, st))))
-                    return c->hipfail(e, "parameter upload");
-                hipLaunchKernelGGL(pv_xact_slow, dim3((nvalid + 255) / 256), dim3(256), 0, st,
-                                   (const PvXactParams *)c->d_xparams, nvalid);
-                if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch pv_xact_slow");
-            }
-            uint32_t zero = 0;
-            hipMemcpyAsync(c->d_nvals + 1, &zero, 4, hipMemcpyHostToDevice, st);
-            hipStreamSynchronize(st);
+            // (xv_select synchronised the stream: the parameter block is free to rewrite)
+            if (shift_thr && !hip_ok(e = (*c->h_xparams = X, upload_params(c->d_xparams, c->h_xparams, sizeof X, st))))
+                return c->hipfail(e, "parameter upload");
+            // the listed transactions, their count read on the device
+            hipLaunchKernelGGL(pv_xact_slow_dev, dim3((uint32_t)c->cus), dim3(256), 0, st, (const PvXactParams *)c->d_xparams);
+            if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipMemsetAsync(c->d_nvals + 1, 0, 4, st)))
+                return c->hipfail(e, "launch pv_xact_slow_dev");
         }
         HP(12);
         // one read-back: the value / carried counts, the flags and the overflow words (the

@@ -187,6 +187,8 @@ extern "C" __global__ void pv_topn_purge(const PvParams *P, uint32_t tb, uint32_
 extern "C" __global__ void pv_topn_compact(const PvParams *P, uint32_t tb, uint8_t *tmp, unsigned long long *tmp_top);
 extern "C" __global__ void pv_topn_names(const PvParams *P);
 extern "C" __global__ void pv_xact_resolve(const PvXactParams *X);
+extern "C" __global__ void pv_xact_resolve2(const PvXactParams *X);
+extern "C" __global__ void pv_xact_slow_dev(const PvXactParams *X);
 extern "C" __global__ void pv_xact_slow(const PvXactParams *X, uint32_t n_valid);
 extern "C" __global__ void pv_xact_carry(const PvXactParams *X);
 extern "C" __global__ void pv_xact_edge2(const PvXactParams *X, const PvEdgePair *pairs, uint32_t n, uint8_t *sfx, uint8_t *tsfx);
@@ -221,6 +223,7 @@ enum { ST_FLAGS = 0, ST_NEV = 1, ST_NRESP = 2, ST_NVALS = 3, ST_NDNS = 4, ST_NNE
 #define PV_NET_THREADS 256    // pv_net_kernel: four waves
 #define PV_TRASH_WAVES 16384 // Net-pass waves with a 2-KiB trash area (grid <= 4096)
 #define ST_ALLOC 32
+#define PV_RESOLVE_PAD (30u << 10) // dynamic LDS of a v1 resolve workgroup: three workgroups a CU
 #define ST_RB_WORDS (ST_ALLOC + PV_TABLES + 2) // status | tables' live counts | overflow words
 
 struct SlotMeta {

@@ -4788,11 +4788,12 @@ __device__ void resolve_one(PV_CREF(PvXactParams) X, XState &T, uint32_t p)
         if ((X.quantiles & 1) && qe.len && kept && rdeep)
             xval(X, T, e.period, XV_RATIO, (uint64_t)__double_as_longlong((double)e.len / (double)qe.len));
         if (!kept || e.dir == 2 || !rdeep) return;
-        if (X.thr_from[e.period] < 0.0f) {
+        // top_slow: a period without a threshold yet defers every candidate; with one, only the
+        // slow transactions are listed. pv_xact_slow_dev names them after the resolve (the record
+        // parse and the table insert stay out of this kernel, which then makes no device call)
+        const float thr = e.dir == 0 ? X.thr_from[e.period] : X.thr_to[e.period];
+        if (X.thr_from[e.period] < 0.0f || (thr > 0.0f && (float)us >= thr))
             T.valid[lds_reserve(&T.nvalid)] = PvXValid{e.idx, (uint8_t)e.period, (uint8_t)e.dir, 0, 0, us};
-        } else {
-            slow_check(X, e.idx, e.period, e.dir, us);
-        }
     } else {
         if (X.edge_h && e.sec < X.edge_h) {
             // sharded runs: the first query of its key may overwrite an open query of an earlier
@@ -4964,20 +4965,30 @@ __device__ __forceinline__ void xstate_flush(PV_CREF(PvXactParams) X, XState &T)
     for (uint32_t j = threadIdx.x; j < T.nvalid; j += blockDim.x) X.valid[T.dbase + j] = T.valid[j];
 }
 
-extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvXactParams *__restrict__ Xp)
+template <bool V2>
+__device__ __forceinline__ void xact_resolve(const PvXactParams *__restrict__ Xp)
 {
     PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
-    PV_CREF(PvParams) P = X.P;
     __shared__ XState T;
     xstate_init(T);
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p < X.n) {
-        if (P.dns2_groups) resolve_one2(X, T, p);
+        if constexpr (V2) resolve_one2(X, T, p);
         else resolve_one(X, T, p);
         if (X.pend_out) carry_one(X, p); // the queries still open go on to the next batch
     }
     __syncthreads();
     xstate_flush(X, T);
+}
+// DNS v1 (a context without the v2 handler) and DNS v2: one kernel each, so the v1 one carries
+// none of the v2 accounting's table inserts
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve(const PvXactParams *__restrict__ Xp)
+{
+    xact_resolve<false>(Xp);
+}
+extern "C" __global__ void __launch_bounds__(PV_BLOCK) pv_xact_resolve2(const PvXactParams *__restrict__ Xp)
+{
+    xact_resolve<true>(Xp);
 }
 
 // DNS v2 transactions across a shard edge (pv_edge_carry): each pair as resolve_one2 accounts a
@@ -5055,6 +5066,18 @@ extern "C" __global__ void pv_xact_pend_in(uint64_t *skeys, uint32_t *svals, con
     svals[at + j] = PV_PEND_FLAG | pvals[j];
 }
 
+// top_slow of the resolve's listed transactions (its count read on the device): the slow ones of
+// periods with a threshold, and the candidates of periods whose threshold the host set after it
+extern "C" __global__ void __launch_bounds__(256) pv_xact_slow_dev(const PvXactParams *__restrict__ Xp)
+{
+    PV_CREF(PvXactParams) X = *(const PV_C PvXactParams *)Xp;
+    const uint32_t n = *X.n_valid;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const PvXValid v = X.valid[i];
+        if (v.dir >= 4) dns2_slow(X, v.idx, v.period, v.dir - 4, v.us);
+        else slow_check(X, v.idx, v.period, v.dir, v.us);
+    }
+}
 // top_slow for transactions of periods whose threshold became known after the resolve
 extern "C" __global__ void pv_xact_slow(const PvXactParams *__restrict__ Xp, uint32_t n_valid)
 {
