@@ -2187,7 +2187,8 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
                        (const PvParams *)c->d_params);
     hipLaunchKernelGGL(pv_topn_merge, dim3(2u << c->reg_log2), dim3(pv_topn_merge_threads()), 0, st, (const PvParams *)c->d_params);
     // names: as many workgroups as are resident (LDS: two per CU), each pipelining its entries
-    hipLaunchKernelGGL(pv_topn_names, dim3((uint32_t)c->cus * 2), dim3(256), 0, st, (const PvParams *)c->d_params);
+    hipLaunchKernelGGL((P.f_flags & (PVDF_ONLY_QSUFFIX | PVDF_PSL)) ? pv_topn_names_sfx : pv_topn_names, dim3((uint32_t)c->cus * 2),
+                       dim3(256), 0, st, (const PvParams *)c->d_params);
     if (!hip_ok(e = hipGetLastError())) return c->hipfail(e, "launch");
 
     // ---- transactions: pair responses with queries (sort by key, then record index)

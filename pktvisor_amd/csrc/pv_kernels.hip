@@ -3980,7 +3980,11 @@ extern "C" __global__ void pv_topn_compact(const PvParams *__restrict__ Pp, uint
 // is parsed again, the first PV_WIN bytes of its DNS message are staged into the lane's
 // LDS window with independent 16-B loads, and the name is decoded from there (bytes past
 // the window come from HBM). Each wave reserves its lanes' arena bytes with one atomic.
-extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *__restrict__ Pp)
+// SFX: suffix sizes in play (only_qname_suffix / public_suffix_list): qname2/3 may need the
+// name walked again (agg_domain_r's out-of-line dots_up_to); without them the kernel makes
+// no device call
+template <bool SFX>
+__device__ __forceinline__ void topn_names(const PvParams *__restrict__ Pp)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     // each lane stages PV_NWIN bytes from its record's 16-B aligned start: the frame
@@ -4053,9 +4057,9 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
                 if (metric == TM_QNAME2 || metric == TM_QNAME3) {
                     int q2, q3;
                     uint64_t h2, h3;
-                    const uint32_t sfx = name_sfx(P, e.rep, P.sfx_of);
-                    if (nl > 0) agg_domain_r(A, m, mlen, st, q2, q3, h2, h3, sfx);
-                    else { q2 = 0; q3 = -1; }
+                    if (nl == 0) { q2 = 0; q3 = -1; }
+                    else if constexpr (SFX) agg_domain_r(A, m, mlen, st, q2, q3, h2, h3, name_sfx(P, e.rep, P.sfx_of));
+                    else agg_domain(st, q2, q3, h2, h3, 0);
                     const int st0 = metric == TM_QNAME2 ? q2 : q3;
                     start = st0 < 0 ? nch : (uint32_t)st0;
                 }
@@ -4134,6 +4138,14 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *
         e_n = e_nn; tkey_n = tkey_nn; roff_n = roff_nn;
         e_nn = ld_e(i + 3 * step);
     }
+}
+extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *__restrict__ Pp)
+{
+    topn_names<false>(Pp);
+}
+extern "C" __global__ void __launch_bounds__(256) pv_topn_names_sfx(const PvParams *__restrict__ Pp)
+{
+    topn_names<true>(Pp);
 }
 
 // DNS events of a batch for the DNS manager's own window (AbstractMetricsManager::new_event,
