@@ -1686,8 +1686,8 @@ struct SlowOut {
     uint32_t caplen, isdns;
     uint8_t dir, l3, l4, syn;
 };
-__device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF(PvParams) P, const NetK K, uint64_t off,
-                                         uint64_t i, uint32_t slot, bool upd)
+__device__ __forceinline__ SlowOut net_slow_body(const SAcc R, const ParseCfg C, PV_CREF(PvParams) P, const NetK K, uint64_t off,
+                                                 uint64_t i, uint32_t slot, bool upd)
 {
     SlowOut so;
     so.ek = 0;
@@ -1716,6 +1716,12 @@ __device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF
         }
     }
     return so;
+}
+// out of line for the general Net pass's rare records (its fast path keeps no frame for it)
+__device__ __noinline__ SlowOut net_slow(const SAcc R, const ParseCfg C, PV_CREF(PvParams) P, const NetK K, uint64_t off,
+                                         uint64_t i, uint32_t slot, bool upd)
+{
+    return net_slow_body(R, C, P, K, off, i, slot, upd);
 }
 
 // ------------------------------------------------------------------ the Net pass
@@ -2098,9 +2104,9 @@ PV_FN Parsed fast_parsed(const FastRec &f, const RecW &r, uint32_t ts_nano, uint
     o.l4len = f.l4 ? f.l4len : 0;
     return o;
 }
-// a general-path record of the lean pass: net_slow with the parameters read here, not held
-// live across the caller's loop
-__device__ __noinline__ SlowOut net_slow_p(const PvParams *__restrict__ Pp, const SAcc R, uint64_t off, uint64_t i)
+// a general-path record of the lean pass: net_slow with the parameters read here (inlined into
+// pv_net_slow_list, which then makes no device call)
+__device__ __forceinline__ SlowOut net_slow_p(const PvParams *__restrict__ Pp, const SAcc R, uint64_t off, uint64_t i)
 {
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     NetK K;
@@ -2111,7 +2117,7 @@ __device__ __noinline__ SlowOut net_slow_p(const PvParams *__restrict__ Pp, cons
     K.n_dshift = P.n_dshift; K.dskip_before = P.dskip_before;
     K.tcp_emit = P.tcp_emit; K.tseg_cap = P.tseg_cap; K.tseg = P.tseg; K.tseg_cnt = P.tseg_cnt; K.tmask = P.tmask;
     K.ndeep_net = nullptr; K.ndeep_dns = nullptr;
-    return net_slow(R, parse_cfg(P), P, K, off, i, K.slot0, true);
+    return net_slow_body(R, parse_cfg(P), P, K, off, i, K.slot0, true);
 }
 
 // ------------------------------------------------------------------ the lean Net pass, register windows
