@@ -2199,6 +2199,13 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         return c->hipfail(e, "kernel execution");
     memcpy(status, c->h_status, sizeof status);
     c->dns_heavy = (uint64_t)status[ST_NDNS] * 2 > n;
+    if (status[ST_FLAGS] & PVF_NAMES_PENDING) {
+        // more created entries than the new-name list holds: their names, before anything reads
+        // or purges the tables
+        for (uint32_t t = 0; t < PV_TABLES; t++)
+            hipLaunchKernelGGL(pv_topn_name_fix, dim3((uint32_t)c->cus * 4), dim3(256), 0, st, (const PvParams *)c->d_params, t);
+        if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipStreamSynchronize(st))) return c->hipfail(e, "pending names");
+    }
     HP(4);
     {
         float ms = 0;

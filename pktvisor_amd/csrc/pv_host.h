@@ -153,6 +153,7 @@ extern "C" __global__ void pv_topn_combine(const PvParams *P);
 extern "C" __global__ void pv_topn_combine_r12(const PvParams *P);
 extern "C" __global__ void pv_topn_merge(const PvParams *P);
 extern "C" __global__ void pv_topn_names_sfx(const PvParams *P);
+extern "C" __global__ void pv_topn_name_fix(const PvParams *P, uint32_t tb);
 extern "C" uint32_t pv_topn_merge_threads();
 struct PvBpfIns;
 extern "C" __global__ void pv_bpf_keep(const uint8_t *recs, const uint32_t *offs, uint32_t n, const PvBpfIns *prog, uint32_t ninsn,

@@ -491,44 +491,6 @@ __device__ __noinline__ void global_add(PV_CREF(PvParams) P, uint32_t slot, uint
     if (created >= 0 && metric != TM_IPV4) P.taux[created] = P.xmerge ? 0u : write_name(P, slot, metric, rep, ns, key);
 }
 
-// global_add for pv_topn_merge's direct regions: a created entry's name goes to the new-name list
-// (pv_topn_names decodes it), as the LDS merge's do, instead of being decoded by this lane
-__device__ __noinline__ void global_add_nn(PV_CREF(PvParams) P, uint32_t slot, uint64_t key, uint64_t w, uint32_t rep)
-{
-    const uint32_t metric = PV_KEY_METRIC(key);
-    if (metric == TM_DENSE_PORT || metric == TM_DENSE_QTYPE || metric == TM_DENSE_RCODE || metric == TM_IPV4) {
-        global_add(P, slot, key, w, rep);
-        return;
-    }
-    TPos t = tpos(P, slot, key);
-    int64_t created = -1;
-    bool done = false;
-    for (int probe = 0; probe < PV_PROBES && !done; probe++) {
-        uint64_t *kp = &P.tkeys[t.rbase + t.pos];
-        uint64_t k = __atomic_load_n(kp, __ATOMIC_RELAXED);
-        uint64_t add = w;
-        if (k == 0) {
-            const uint64_t stale = __atomic_load_n(&P.tcnt[t.rbase + t.pos], __ATOMIC_RELAXED);
-            asm volatile("" ::"v"((uint32_t)stale), "v"((uint32_t)(stale >> 32)) : "memory");
-            uint64_t prev = atomicCAS((unsigned long long *)kp, 0ull, (unsigned long long)key);
-            if (prev == 0) { created = (int64_t)(t.rbase + t.pos); add = w - stale; }
-            k = prev == 0 ? key : prev;
-        }
-        if (k == key) {
-            atomicAdd((unsigned long long *)&P.tcnt[t.rbase + t.pos], (unsigned long long)add);
-            done = true;
-        } else {
-            t.pos = (t.pos + 1) & t.rmask;
-        }
-    }
-    if (!done) table_overflow(P, slot, key, w, rep, !P.tcp_pass);
-    if (created < 0) return;
-    const uint32_t tb = PV_TSLOT(slot, metric);
-    atomicAdd(&P.tab_live[tb], 1u);
-    const uint32_t g = atomicAdd(P.nn_cnt, 1u);
-    if (g < P.nn_cap) P.nn[g] = PvNewName{tb, rep, (uint64_t)created};
-    else P.taux[created] = write_name(P, slot, metric, rep, nullptr, key);
-}
 
 // ------------------------------------------------------------------ LDS key cache
 // Open-addressed key -> (count, min record index) cache shared by a workgroup's
@@ -3046,9 +3008,6 @@ __device__ __forceinline__ void batched(uint64_t n, Ld ld, Body body)
     }
 }
 #define PV_E16(q) reinterpret_cast<const PV_G ulonglong2 *>(q)
-#ifndef PV_MERGE_DIRECT
-#define PV_MERGE_DIRECT 64 // regions with at most this many updates use global_add_nn
-#endif
 #define PV_W_IP4 (1u << 31)  // weight word of a combined IPv4 entry: flag | dir << 30 | card << 29 | count
 
 // CPC coupon of an IPv4 address (cpc_sketch update of the int32 address)
@@ -3511,19 +3470,8 @@ extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) __attribute__((amdgp
         }
         return cb[(uint64_t)U.list[lo] * lcap + U.start[lo] + ((uint32_t)j - U.pref[lo])];
     };
-    if (n <= PV_MERGE_DIRECT) {
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            const ulonglong2 e = ld(j);
-            const uint32_t s = (uint32_t)(e.x >> 60), w = (uint32_t)e.y, rep = (uint32_t)(e.y >> 32);
-            const uint64_t key = e.x & ((1ull << 60) - 1);
-            if (P.xmerge) { global_add(P, s, key, e.y, 0); continue; } // (64-bit weight, no name)
-            if ((w & PV_W_IP4) && ((w >> 29) & 1))
-                cpc_min(P, s, ((w >> 30) & 1) ? CPC_DST : CPC_SRC, ip4_coupon((uint32_t)key), (int64_t)(P.gbase + rep));
-            if (w & PV_W_IP4) global_add(P, s, key, w & PV_W_CNT, rep);
-            else global_add_nn(P, s, key, w, rep);
-        }
-        return;
-    }
+    // (every run key takes the LDS path, however few its entries: a direct global insert here
+    // would bind the kernel to the device-call convention)
     static_assert(PV_TABLES <= 32, "table mask");
     constexpr uint32_t PF = PV_RS / PV_MG_THREADS; // region entries per thread
     // IPv4 cardinality minima in the insert pass (batches of at most 2^24 records): a v1 IPv4
@@ -3605,8 +3553,9 @@ extern "C" __global__ void __launch_bounds__(PV_MG_THREADS) __attribute__((amdgp
         auto new_name = [&](uint32_t g, uint32_t i, uint32_t rep) {
             if (g < P.nn_cap) P.nn[g] = PvNewName{tb, rep, rbase + i};
             else {
-                const uint64_t key = S.key[i] & ~PV_CREATED;
-                P.taux[rbase + i] = write_name(P, s, PV_KEY_METRIC(key), rep, nullptr, key);
+                // past the list: the record waits in the aux word for pv_topn_name_fix
+                P.taux[rbase + i] = PV_AUX_PENDING | rep;
+                atomicOr(P.flags, (uint32_t)PVF_NAMES_PENDING);
             }
         };
         if (nnew && nnew <= PV_MG_NN) {
@@ -4148,6 +4097,19 @@ __device__ __forceinline__ void topn_names(const PvParams *__restrict__ Pp)
 extern "C" __global__ void __launch_bounds__(256) pv_topn_names(const PvParams *__restrict__ Pp)
 {
     topn_names<false>(Pp);
+}
+// Names of the entries the merge created past the new-name list (PVF_NAMES_PENDING, rare): every
+// aux word of table tb holding PV_AUX_PENDING | record gets its name record (write_name)
+extern "C" __global__ void __launch_bounds__(256) pv_topn_name_fix(const PvParams *__restrict__ Pp, uint32_t tb)
+{
+    PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
+    const uint64_t tcap = 1ull << P.tcap_log2, base = (uint64_t)tb * tcap;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < tcap; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t a = P.taux[base + i];
+        if (!(a & PV_AUX_PENDING)) continue;
+        const uint64_t key = P.tkeys[base + i];
+        P.taux[base + i] = key ? write_name(P, tb % PV_SLOTS, PV_KEY_METRIC(key), a & ~PV_AUX_PENDING, nullptr, key) : 0u;
+    }
 }
 extern "C" __global__ void __launch_bounds__(256) pv_topn_names_sfx(const PvParams *__restrict__ Pp)
 {

@@ -174,8 +174,10 @@ enum {
     PVF_ARENA_FULL = 1u << 1,
     PVF_EVENTS_FULL = 1u << 2,
     PVF_VALUES_FULL = 1u << 3,
-    PVF_BIG_CAPLEN = 1u << 4
+    PVF_BIG_CAPLEN = 1u << 4,
+    PVF_NAMES_PENDING = 1u << 5 // created entries past the new-name list: aux = PV_AUX_PENDING | record
 };
+#define PV_AUX_PENDING 0x80000000u // (arena offsets stay below 2^31: arena_cap per table)
 
 // DNS transaction event, one per DNS wire packet (for the pairing pass)
 struct PvXEvent {
