@@ -2205,6 +2205,7 @@ int process_span(pv_ctx *c, const uint8_t *d_recs, const uint32_t *d_boffs, uint
         for (uint32_t t = 0; t < PV_TABLES; t++)
             hipLaunchKernelGGL(pv_topn_name_fix, dim3((uint32_t)c->cus * 4), dim3(256), 0, st, (const PvParams *)c->d_params, t);
         if (!hip_ok(e = hipGetLastError()) || !hip_ok(e = hipStreamSynchronize(st))) return c->hipfail(e, "pending names");
+        if (getenv("PV_NAMEFIX_TRACE")) fprintf(stderr, "pv: pending top-N names written (pv_topn_name_fix)\n");
     }
     HP(4);
     {

@@ -128,3 +128,46 @@ def test_sharded_flood_owner_merge_purges(tmp_path, monkeypatch):
         assert t <= e["estimate"] <= t + bound, (e, t, bound)
     assert dns["top_qname2"][0] == {"name": ".victim.example", "estimate": total}
     assert dns["wire_packets"]["total"] == total
+
+
+def _v6_query_pcap(n, seed):
+    """UDP DNS queries from n random IPv6 clients (2001:db8::/32) to one server, each asking
+    h<k>.n<k % 997>.example.com"""
+    import ipaddress
+    import struct
+    rng = np.random.default_rng(seed)
+    dst = bytes.fromhex("20014860000000000000000000008888")
+    out, srcs = bytearray(), set()
+    for k in range(n):
+        src = bytes.fromhex("20010db8") + rng.integers(0, 256, 12, dtype=np.uint8).tobytes()
+        srcs.add(str(ipaddress.IPv6Address(src)))
+        q = synth._dns_msg(rng, k & 0xffff, False, f"h{k}.n{k % 997}.example.com", 1)
+        udp = struct.pack(">HHHH", 1024 + k % 50000, 53, 8 + len(q), 0) + q
+        fr = b"\x00\x11\x22\x33\x44\x55\x66\x77\x88\x99\xaa\xbb\x86\xdd" + struct.pack(">IHBB", 0x60000000, len(udp), 17, 64) + src + dst + udp
+        us = 1700000000 * 10**6 + 10 * k
+        out += struct.pack("<IIII", us // 10**6, us % 10**6, len(fr), len(fr)) + fr
+    return pa.pcap_file_bytes(bytes(out)), srcs | {str(ipaddress.IPv6Address(dst))}
+
+
+def test_new_name_list_overflow(monkeypatch, capfd):
+    """one batch creating more named entries than the new-name list holds (table_log2 8: 256
+    entries a table and in the list; the Net table's IPv6 keys and the DNS table's names fill
+    512): the merge leaves the rest pending in their aux words and pv_topn_name_fix names them,
+    so every listed entry carries its own name"""
+    n = 6000
+    pcap, addrs = _v6_query_pcap(n, 5)
+    monkeypatch.setenv("PV_NAMEFIX_TRACE", "1")
+    h = pa.PvHandlers(host_spec="2001:db8::/32", num_periods=1, table_log2=8, max_records=1 << 14, topn_count=10)
+    try:
+        h.process_host(pcap[24:])
+        w = h.window_json(0)
+    finally:
+        h.close()
+    assert "pending top-N names written" in capfd.readouterr().err  # the path under test ran
+    v6 = w["packets"]["top_ipv6"]
+    assert v6 and v6[0]["name"] == "2001:4860::8888" and v6[0]["estimate"] >= n
+    assert all(e["name"] in addrs for e in v6), v6
+    q3 = w["dns"]["top_qname3"]
+    assert q3 and all(e["name"] in {f".n{j}.example.com" for j in range(997)} for e in q3), q3
+    assert w["dns"]["top_qname2"][0] == {"name": ".example.com", "estimate": n}
+    assert w["dns"]["wire_packets"]["total"] == n
