@@ -4105,10 +4105,14 @@ extern "C" __global__ void __launch_bounds__(256) pv_topn_name_fix(const PvParam
     PV_CREF(PvParams) P = *(const PV_C PvParams *)Pp;
     const uint64_t tcap = 1ull << P.tcap_log2, base = (uint64_t)tb * tcap;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < tcap; i += (uint64_t)gridDim.x * blockDim.x) {
+        // (only named entries: an IPv4 entry's aux word is never written, and an empty slot's is
+        // whatever its last occupant left)
+        const uint64_t key = P.tkeys[base + i];
+        if (!key || PV_KEY_METRIC(key) == TM_IPV4) continue;
         const uint32_t a = P.taux[base + i];
         if (!(a & PV_AUX_PENDING)) continue;
-        const uint64_t key = P.tkeys[base + i];
-        P.taux[base + i] = key ? write_name(P, tb % PV_SLOTS, PV_KEY_METRIC(key), a & ~PV_AUX_PENDING, nullptr, key) : 0u;
+        const uint32_t rep = a & ~PV_AUX_PENDING;
+        P.taux[base + i] = rep < P.n ? write_name(P, tb % PV_SLOTS, PV_KEY_METRIC(key), rep, nullptr, key) : 0u;
     }
 }
 extern "C" __global__ void __launch_bounds__(256) pv_topn_names_sfx(const PvParams *__restrict__ Pp)
